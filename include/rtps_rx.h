@@ -1,0 +1,242 @@
+/*
+ * rtps_rx.h — C ABI of the MI355X-native RTPS receive-path parser.
+ *
+ * Drop-in boundary for the rx parse of RustDDS (w-utter/rustdds-io_uring).
+ * The functions below replace, for a *batch* of datagrams at once:
+ *
+ *   Message::read_from_buffer(&Bytes) -> io::Result<Message>
+ *       src/rtps/message.rs:64-81
+ *   MessageReceiver::handle_received_packet_2(&mut self, &Bytes)
+ *       -> Option<SubmessageIter2>          src/io_uring/rtps/message_receiver.rs:232-287
+ *   SubmessageIter2::next -> PassedSubmessage  (interpreter state, dest filter)
+ *       src/io_uring/rtps/message_receiver.rs:56-119, 618-665, 289-295
+ *   builtin-pair / matched-writer classification feeding Reader::handle_data_msg
+ *       src/io_uring/discovery/discovery.rs:2795-2816, 3075-3095
+ *       src/io_uring/rtps/dp_event_loop.rs:266-327, src/io_uring/rtps/reader.rs:474-484
+ *   payload-kind decision of Reader::data_to_dds_data + SerializedPayload::from_bytes
+ *       src/io_uring/rtps/reader.rs:760-833, src/messages/submessages/elements/serialized_payload.rs:86-110
+ *
+ * Plain C types only (no torch, no HIP types): a Rust caller binds this with
+ * bindgen / a hand-written `extern "C"` block.
+ *
+ * Output model
+ * ------------
+ * For every input datagram i the library writes status[i] (RTPS_DGRAM_*).
+ * For every submessage the reference *materialises* in Message.submessages
+ * (everything except PAD and unknown / vendor / security kinds) of a datagram
+ * whose status is RTPS_DGRAM_OK, one 64-byte rtps_record is written.
+ * Records are in the reference's order: ascending (dgram_idx, sub_off).
+ * A datagram whose status is not OK has zero records (the reference drops
+ * the whole datagram on any submessage error: message.rs:75,
+ * message_receiver.rs:275-282).
+ *
+ * All multi-byte record fields are host (little-endian) integers already
+ * converted from the submessage's own byte order (flags bit 0).
+ * GUID prefixes / entity ids are raw wire bytes.
+ * Offsets (sub_off, pl_off, ...) are relative to the start of the datagram.
+ */
+#ifndef RTPS_RX_H
+#define RTPS_RX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RTPS_RX_ABI_VERSION 1u
+
+/* Largest datagram the record layout can address (u16 offsets).  The
+ * reference's io_uring provided buffers are 64 KiB each
+ * (src/io_uring/network/udp_listener.rs:7,27), so no datagram it can
+ * receive is longer. */
+#define RTPS_MAX_DATAGRAM 65536u
+
+/* ---- per-datagram status (handle_received_packet_2 outcome) ------------ */
+enum rtps_dgram_status {
+  RTPS_DGRAM_OK = 0,         /* parsed; records emitted                          */
+  RTPS_DGRAM_SHORT = 1,      /* len < 20, not a ping   (message_receiver.rs:238-251) */
+  RTPS_DGRAM_PING = 2,       /* len < 20, "RTPS"...."DDSPING"                     */
+  RTPS_DGRAM_RTPX = 3,       /* magic "RTPX"           (:254-266)                 */
+  RTPS_DGRAM_BAD_MAGIC = 4,  /* other magic            (:267-271)                 */
+  RTPS_DGRAM_BAD_HEADER = 5, /* version major > 2      (messages/header.rs:30-39)  */
+  RTPS_DGRAM_SUBMSG_ERR = 6, /* any submessage read error -> whole datagram dropped */
+  RTPS_DGRAM_TOO_LONG = 7    /* len > RTPS_MAX_DATAGRAM (cannot come from a UDP socket) */
+};
+
+/* ---- submessage kinds (messages/submessages/submessage_kind.rs:17-34) --- */
+enum rtps_kind {
+  RTPS_PAD = 0x01,
+  RTPS_ACKNACK = 0x06,
+  RTPS_HEARTBEAT = 0x07,
+  RTPS_GAP = 0x08,
+  RTPS_INFO_TS = 0x09,
+  RTPS_INFO_SRC = 0x0c,
+  RTPS_INFO_REPLY_IP4 = 0x0d,
+  RTPS_INFO_DST = 0x0e,
+  RTPS_INFO_REPLY = 0x0f,
+  RTPS_NACK_FRAG = 0x12,
+  RTPS_HEARTBEAT_FRAG = 0x13,
+  RTPS_DATA = 0x15,
+  RTPS_DATA_FRAG = 0x16
+};
+
+/* ---- rtps_record.route bits -------------------------------------------- */
+/* PASS: SubmessageIter2::next would yield this submessage
+ *   writer kinds: dest == own || dest == UNKNOWN   (message_receiver.rs:75-84)
+ *   reader kinds: always                            (message_receiver.rs:88-113)
+ *   interpreter kinds: never (state change only)    (message_receiver.rs:70-73) */
+#define RTPS_ROUTE_PASS 0x01u
+#define RTPS_ROUTE_TS_VALID 0x02u    /* a source timestamp is in effect (ts_sec/ts_frac) */
+#define RTPS_ROUTE_HAS_QOS 0x04u     /* DATA / DATA_FRAG: inline QoS present (Q flag)    */
+#define RTPS_ROUTE_HAS_PAYLOAD 0x08u /* DATA with D|K, DATA_FRAG: serialized payload    */
+#define RTPS_ROUTE_BUILTIN 0x10u     /* (reader_id, writer_id) is a builtin discovery pair */
+#define RTPS_ROUTE_MATCHED 0x20u     /* writer GUID found in the match table             */
+
+/* ---- rtps_record.payload_kind (Reader::data_to_dds_data, reader.rs:760-833) */
+enum rtps_payload_kind {
+  RTPS_PK_NONE = 0,           /* not a DATA submessage                            */
+  RTPS_PK_DATA = 1,           /* (payload, D=1, K=0) -> DDSData::Data              */
+  RTPS_PK_KEY = 2,            /* (payload, D=0, K=1) -> DDSData::DisposeByKey      */
+  RTPS_PK_KEY_HASH = 3,       /* (none, 0, 0) + 16-byte PID_KEY_HASH -> DisposeByKeyHash */
+  RTPS_PK_ERR_NO_CONTENT = 0x81, /* (none, 0, 0) without a usable KEY_HASH           */
+  RTPS_PK_ERR_AMBIGUOUS = 0x82,  /* D=1 and K=1                                       */
+  RTPS_PK_ERR_SHORT = 0x83       /* payload shorter than the 4-byte encapsulation header */
+};
+
+/* ---- one parsed submessage (64 bytes) ----------------------------------- */
+typedef struct rtps_record {
+  uint32_t dgram_idx;   /*  0 index of the datagram in the batch                   */
+  uint16_t sub_off;     /*  4 offset of the submessage header in the datagram      */
+  uint8_t kind;         /*  6 SubmessageKind                                       */
+  uint8_t flags;        /*  7 raw submessage flags byte                            */
+  uint8_t prefix[12];   /*  8 writer/reader kinds: source GuidPrefix in effect
+                              (writer GUID = prefix||writer_id, reader_submsg source);
+                              INFO_DST / INFO_SRC: the prefix the submessage carries;
+                              INFO_TS / INFO_REPLY: source prefix in effect            */
+  uint8_t writer_id[4]; /* 20 EntityId (raw)                                       */
+  uint8_t reader_id[4]; /* 24 EntityId (raw)                                       */
+  uint16_t aux16;       /* 28 DATA/DATA_FRAG: inline-QoS length incl. sentinel
+                              (qos_off = pl_off - aux16); other kinds: body length   */
+  uint8_t route;        /* 30 RTPS_ROUTE_* bits                                    */
+  uint8_t payload_kind; /* 31 rtps_payload_kind (DATA only)                        */
+  int64_t sn;           /* 32 DATA/DATA_FRAG/HB_FRAG/NACK_FRAG: writerSN;
+                              HEARTBEAT: firstSN; GAP: gapStart; ACKNACK: readerSNState.base */
+  union {               /* 40 kind-specific (16 bytes)                             */
+    struct { uint16_t pl_off, pl_len; uint8_t rep_id[2], rep_opts[2];
+             uint16_t key_hash_off, status_info_off, rsi_off, _r; } data;
+    struct { uint16_t pl_off, pl_len; uint32_t frag_start;
+             uint16_t frags_in_sub, frag_size; uint32_t data_size; } frag;
+    struct { int64_t last_sn; int32_t count; uint32_t _r; } hb;
+    struct { uint32_t last_frag_num; int32_t count; uint32_t _r[2]; } hbfrag;
+    struct { int64_t list_base; uint32_t num_bits; uint16_t bitmap_off, _r; } gap;
+    struct { int32_t count; uint32_t _r; uint32_t num_bits; uint16_t bitmap_off, _r2; } acknack;
+    struct { uint32_t fns_base; int32_t count; uint32_t num_bits; uint16_t bitmap_off, _r; } nackfrag;
+    struct { uint8_t version[2], vendor[2]; uint32_t _r[3]; } infosrc;
+    struct { uint32_t n_unicast, n_multicast; uint32_t _r[2]; } inforeply; /* n_multicast = 0xFFFFFFFF: None */
+    uint8_t raw[16];
+  } u;
+  uint32_t ts_sec;      /* 56 source timestamp in effect (iff route & TS_VALID)    */
+  uint32_t ts_frac;     /* 60                                                     */
+} rtps_record;
+
+#ifdef __cplusplus
+#define RTPS_RX_STATIC_ASSERT(c, m) static_assert(c, m)
+#else
+#define RTPS_RX_STATIC_ASSERT(c, m) _Static_assert(c, m)
+#endif
+RTPS_RX_STATIC_ASSERT(sizeof(rtps_record) == 64, "rtps_record must be 64 bytes");
+RTPS_RX_STATIC_ASSERT(offsetof(rtps_record, sn) == 32, "rtps_record.sn at 32");
+RTPS_RX_STATIC_ASSERT(offsetof(rtps_record, u) == 40, "rtps_record.u at 40");
+RTPS_RX_STATIC_ASSERT(offsetof(rtps_record, ts_sec) == 56, "rtps_record.ts_sec at 56");
+
+/* ---- writer GUID -> local reader slot (Reader::matched_writers) --------- */
+typedef struct rtps_match {
+  uint8_t writer_guid[16]; /* prefix[12] || entity_id[4] */
+  uint16_t reader_slot;    /* caller-defined local reader index (< 0xFFFF) */
+  uint16_t _pad;
+} rtps_match;
+
+#define RTPS_NO_MATCH 0xFFFFu
+
+/* ---- context ------------------------------------------------------------ */
+typedef struct rtps_rx_config {
+  uint32_t abi_version;    /* RTPS_RX_ABI_VERSION */
+  int32_t device;          /* HIP device ordinal */
+  uint8_t own_prefix[12];  /* participant GuidPrefix (MessageReceiver::new) */
+  uint32_t max_datagrams;  /* largest batch this context will parse */
+  uint32_t flags;          /* reserved, 0 */
+} rtps_rx_config;
+
+/* Output buffers of one batch.  All pointers are DEVICE pointers (the
+ * caller owns them).  records/match have room for max_records entries;
+ * records past max_records are counted but not written. */
+typedef struct rtps_rx_out {
+  uint8_t* status;          /* [n]            required */
+  rtps_record* records;     /* [max_records]  required */
+  uint64_t max_records;
+  uint16_t* match;          /* [max_records]  optional: reader slot or RTPS_NO_MATCH */
+  uint32_t* rec_begin;      /* [n]            optional: index of datagram i's first record */
+  uint64_t* n_records;      /* [1]            required: total records of the batch */
+} rtps_rx_out;
+
+typedef struct rtps_rx_ctx rtps_rx_ctx;
+
+/* error codes (negative) */
+#define RTPS_RX_OK 0
+#define RTPS_RX_EINVAL (-1)
+#define RTPS_RX_EHIP (-2)
+#define RTPS_RX_ENOMEM (-3)
+#define RTPS_RX_ETOOBIG (-4)
+#define RTPS_RX_EABI (-5)
+
+/* MessageReceiver::new(participant_guid_prefix, None)  (message_receiver.rs:158-182) */
+int rtps_rx_create(const rtps_rx_config* cfg, rtps_rx_ctx** out_ctx);
+int rtps_rx_destroy(rtps_rx_ctx* ctx);
+/* Launch on the caller's hipStream_t (NULL = the context's own stream). */
+int rtps_rx_set_stream(rtps_rx_ctx* ctx, void* hip_stream);
+/* Replace the writer-GUID -> reader-slot table (first entry wins on duplicates). */
+int rtps_rx_set_match_table(rtps_rx_ctx* ctx, const rtps_match* table, uint32_t n);
+/* Parse n datagrams: datagram i = arena[dgram_off[i] .. dgram_off[i]+dgram_len[i]).
+ * arena, dgram_off, dgram_len are DEVICE pointers.  Asynchronous on the
+ * context's stream; call rtps_rx_sync (or synchronise the stream) before
+ * reading the outputs. */
+int rtps_rx_parse_batch(rtps_rx_ctx* ctx, const uint8_t* arena, uint64_t arena_len,
+                        const uint64_t* dgram_off, const uint32_t* dgram_len, uint32_t n,
+                        const rtps_rx_out* out);
+int rtps_rx_sync(rtps_rx_ctx* ctx);
+const char* rtps_rx_strerror(int code);
+
+/* Multi-GPU sharding (>= 2 GPUs): stable partition of the writer/reader-kind
+ * records (interpreter records are not exchanged) by owner GPU =
+ * fnv1a32(prefix || writer_id) % n_dest (the same hash as the match table).
+ * recs/n_records are a parse_batch output (device); out has room for
+ * max_records records; dest_counts[n_dest] (device u64) receives the bucket
+ * sizes; bucket d starts at sum(dest_counts[0..d)).  Input order is kept
+ * inside each bucket.  New: the reference has one process and no exchange. */
+int rtps_rx_bucket_by_writer(rtps_rx_ctx* ctx, const rtps_record* recs, const uint64_t* n_records,
+                             uint64_t max_records, uint32_t n_dest, rtps_record* out, uint64_t* dest_counts);
+
+/* Upper bound on records for datagram lengths (host arrays): sum((len-20)/4). */
+uint64_t rtps_rx_max_records_host(const uint32_t* dgram_len, uint32_t n);
+
+/* ---- synthetic workload generator (device) ------------------------------
+ * Deterministic f(seed, idx) datagrams shaped like MessageBuilder output
+ * (src/rtps/message.rs:146-562, io_uring/rtps/writer.rs:681-893).
+ * workload: RTPS_WL_* ; dgram_off/dgram_len are DEVICE arrays already filled
+ * (rtps_gen_layout_host computes them). */
+enum rtps_workload {
+  RTPS_WL_C2 = 2,   /* 1M x 300 B, one DATA each, 256 B CDR payload             */
+  RTPS_WL_T = 1,    /* 1M x 1024 B, one DATA each (north-star target)            */
+  RTPS_WL_C3 = 3,   /* mixed DATA/HB/ACKNACK/GAP/INFO_*, 128..1500 B, 16 writers  */
+  RTPS_WL_C4 = 4    /* DATA_FRAG: 64 KiB samples in 1400 B datagrams, 16 writers */
+};
+int rtps_rx_generate(rtps_rx_ctx* ctx, int workload, uint64_t seed, uint64_t first_idx,
+                     uint32_t n_writers, uint8_t* arena, const uint64_t* dgram_off,
+                     const uint32_t* dgram_len, uint32_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RTPS_RX_H */

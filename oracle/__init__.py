@@ -1,0 +1,98 @@
+"""ctypes binding of the CPU oracle (oracle/rtps_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, as the parity checker / CPU baseline.  The
+product path (rustdds-io_uring_amd/) never imports this module.
+"""
+import ctypes
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_REPO = os.path.dirname(_HERE)
+sys.path.insert(0, os.path.join(_REPO, "rustdds-io_uring_amd"))
+from rtps_rx.records import RECORD_DTYPE, MATCH_DTYPE, max_records  # noqa: E402
+
+LIB_PATH = os.path.join(_HERE, "librtps_oracle.so")
+_lib = None
+
+OWN_PREFIX = bytes([0x01, 0x03, 0x00, 0x0c, 0x29, 0x2d, 0x31, 0xa2, 0x28, 0x20, 0x02, 0x08])
+SEED = 0x52545053
+WL_T, WL_C2, WL_C3, WL_C4 = 1, 2, 3, 4
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        P = ctypes.c_void_p
+        L.rtps_oracle_parse.restype = ctypes.c_uint64
+        L.rtps_oracle_parse.argtypes = [P, P, P, ctypes.c_uint32, P, P, ctypes.c_uint32,
+                                        P, P, ctypes.c_uint64, P, P, ctypes.c_int]
+        L.rtps_oracle_gen_layout.restype = ctypes.c_uint64
+        L.rtps_oracle_gen_layout.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                                             ctypes.c_uint32, P, P]
+        L.rtps_oracle_gen_fill.restype = None
+        L.rtps_oracle_gen_fill.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                                           ctypes.c_uint32, P, P]
+        L.rtps_oracle_record_size.restype = ctypes.c_uint32
+        assert L.rtps_oracle_record_size() == RECORD_DTYPE.itemsize
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+def pack(datagrams, align=16):
+    """list of bytes -> (arena u8, off u64, len u32) with `align`-byte aligned starts."""
+    lens = np.array([len(d) for d in datagrams], dtype=np.uint32)
+    offs = np.zeros(len(datagrams), dtype=np.uint64)
+    pos = 0
+    for i, d in enumerate(datagrams):
+        offs[i] = pos
+        pos += (len(d) + align - 1) // align * align if align > 1 else len(d)
+    arena = np.zeros(max(pos, 1), dtype=np.uint8)
+    for i, d in enumerate(datagrams):
+        arena[int(offs[i]):int(offs[i]) + len(d)] = np.frombuffer(bytes(d), dtype=np.uint8)
+    return arena, offs, lens
+
+
+def parse(arena, offs, lens, own=OWN_PREFIX, match_table=None, threads=1, want_match=True):
+    """Returns (status u8[n], records RECORD_DTYPE[m], match u16[m], rec_begin u32[n])."""
+    arena = np.ascontiguousarray(arena, dtype=np.uint8)
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint32)
+    n = len(lens)
+    cap = max(max_records(lens), 1)
+    status = np.zeros(n, dtype=np.uint8)
+    recs = np.zeros(cap, dtype=RECORD_DTYPE)
+    match = np.zeros(cap, dtype=np.uint16) if want_match else None
+    rec_begin = np.zeros(max(n, 1), dtype=np.uint32)
+    own_a = np.frombuffer(bytes(own), dtype=np.uint8).copy()
+    tbl = match_table if match_table is not None else np.zeros(0, dtype=MATCH_DTYPE)
+    tbl = np.ascontiguousarray(tbl, dtype=MATCH_DTYPE)
+    total = lib().rtps_oracle_parse(_ptr(arena), _ptr(offs), _ptr(lens), n, _ptr(own_a),
+                                    _ptr(tbl) if len(tbl) else None, len(tbl), _ptr(status), _ptr(recs),
+                                    cap, _ptr(match), _ptr(rec_begin), threads)
+    return status, recs[:total], (match[:total] if want_match else None), rec_begin[:n]
+
+
+def gen(workload, n, seed=SEED, first_idx=0, n_writers=16):
+    """Host build of the synthetic generator: (arena, off, len)."""
+    offs = np.zeros(n, dtype=np.uint64)
+    lens = np.zeros(n, dtype=np.uint32)
+    size = lib().rtps_oracle_gen_layout(workload, seed, first_idx, n_writers, n, _ptr(offs), _ptr(lens))
+    arena = np.zeros(max(int(size), 16), dtype=np.uint8)
+    lib().rtps_oracle_gen_fill(workload, seed, first_idx, n_writers, n, _ptr(offs), _ptr(arena))
+    return arena, offs, lens

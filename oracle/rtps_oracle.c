@@ -1,0 +1,635 @@
+/*
+ * rtps_oracle.c — CPU restatement of the RustDDS receive-path parse.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the parity checker for the HIP
+ * product path and the "port" CPU baseline of bench.py.  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it.  The
+ * product library (rustdds-io_uring_amd/csrc) never links it.
+ *
+ * Parity pinning: the reference is Rust and cannot be built in this image
+ * (no cargo/rustc, crates not vendored: SURVEY.md §0, §8c).  This
+ * restatement is pinned by the reference's own wire vectors and
+ * assertions, extracted into tests/golden/ by tests/golden/make_golden.py
+ * (see tests/test_oracle_golden.py).  Behaviour of the third-party `speedy`
+ * 0.8 reader that no vector covers (INFO_REPLY Option tag, trailing bytes
+ * after fixed-size bodies) is "parity unpinned" and documented in DESIGN.md.
+ *
+ * Structure mirrors the reference:
+ *   rtps_message_read_from_buffer   <- Message::read_from_buffer   rtps/message.rs:64-81
+ *   submessage_read_from_buffer     <- Submessage::read_from_buffer rtps/submessage.rs:56-295
+ *   data_deserialize                <- Data::deserialize_data      messages/submessages/data.rs:57-144
+ *   datafrag_deserialize            <- DataFrag::deserialize       messages/submessages/data_frag.rs:121-257
+ *   parameter_list_read             <- ParameterList::read_from    elements/parameter_list.rs:79-102
+ *   number_set_read                 <- NumberSet::read_from        structure/sequence_number.rs:464-498
+ *   handle_received_packet_2        <- io_uring/rtps/message_receiver.rs:232-287
+ *   interpreter (iter_next)         <- io_uring/rtps/message_receiver.rs:56-119, 618-665, 289-295
+ *   data_to_dds_data_kind           <- io_uring/rtps/reader.rs:760-833
+ *   builtin pairs                   <- io_uring/discovery/discovery.rs:2795-2816, 3075-3095
+ */
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/rtps_rx.h"
+#include "../rustdds-io_uring_amd/csrc/rtps_gen.h"
+
+/* ------------------------------------------------------------------------ */
+/* speedy-style reader over a byte slice (io::Cursor + Endianness)          */
+/* ------------------------------------------------------------------------ */
+typedef struct cursor {
+  const uint8_t* buf; /* slice start */
+  size_t len;         /* slice length */
+  size_t pos;         /* cursor position */
+  int le;             /* endianness_flag(flags): submessage_flag.rs:36-42 */
+} cursor;
+
+static int rd_u8(cursor* c, uint8_t* v) {
+  if (c->pos + 1 > c->len) return -1;
+  *v = c->buf[c->pos++];
+  return 0;
+}
+static int rd_u16(cursor* c, uint16_t* v) {
+  if (c->pos + 2 > c->len) return -1;
+  const uint8_t* p = c->buf + c->pos;
+  *v = c->le ? (uint16_t)(p[0] | (p[1] << 8)) : (uint16_t)((p[0] << 8) | p[1]);
+  c->pos += 2;
+  return 0;
+}
+static int rd_u32(cursor* c, uint32_t* v) {
+  if (c->pos + 4 > c->len) return -1;
+  const uint8_t* p = c->buf + c->pos;
+  *v = c->le ? ((uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24))
+             : (((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | (uint32_t)p[3]);
+  c->pos += 4;
+  return 0;
+}
+static int rd_bytes(cursor* c, uint8_t* out, size_t n) {
+  if (c->pos + n > c->len) return -1;
+  memcpy(out, c->buf + c->pos, n);
+  c->pos += n;
+  return 0;
+}
+/* EntityId::read_from: 3 key bytes + kind byte (structure/guid.rs:495-505) */
+static int rd_entity_id(cursor* c, uint8_t e[4]) { return rd_bytes(c, e, 4); }
+/* SequenceNumber::read_from: i32 high then u32 low (sequence_number.rs:169-182) */
+static int rd_sn(cursor* c, int64_t* sn) {
+  uint32_t hi, lo;
+  if (rd_u32(c, &hi) || rd_u32(c, &lo)) return -1;
+  *sn = (int64_t)(((int64_t)(int32_t)hi) * 4294967296LL) + (int64_t)lo;
+  return 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* parsed submessage (one element of Message.submessages)                    */
+/* ------------------------------------------------------------------------ */
+enum body_class { BODY_WRITER = 1, BODY_READER = 2, BODY_INTERP = 3 };
+
+typedef struct submsg {
+  uint32_t off;   /* submessage header offset within the datagram */
+  uint8_t kind, flags;
+  uint32_t content_len;
+  int cls;
+  uint8_t reader_id[4], writer_id[4];
+  int64_t sn, sn2;
+  int32_t count;
+  uint32_t num_bits, bitmap_off, u32a;
+  /* DATA / DATA_FRAG */
+  int has_qos, has_payload;
+  uint32_t qos_len, pl_off, pl_len;
+  uint32_t key_hash_off, status_info_off, rsi_off;
+  uint32_t frag_start, frags_in_sub, frag_size, data_size;
+  /* interpreter */
+  uint8_t prefix[12];
+  int ts_valid;
+  uint32_t ts_sec, ts_frac;
+  uint8_t version[2], vendor[2];
+  uint32_t n_uni, n_multi;
+} submsg;
+
+/* ParameterList::read_from (parameter_list.rs:79-102): loop { pid u16, length u16;
+ * pid == PID_SENTINEL -> stop (value not read); else read exactly `length`
+ * bytes }.  Also records the first KEY_HASH (value must be 16 bytes,
+ * key.rs:64-68 / inline_qos.rs:44-53), STATUS_INFO (inline_qos.rs:28-42) and
+ * RELATED_SAMPLE_IDENTITY(_CUSTOM) (inline_qos.rs:56-85) values.
+ * `dgram_base` converts cursor positions to datagram offsets. */
+static int parameter_list_read(cursor* c, uint32_t dgram_base, submsg* s) {
+  int seen_kh = 0, seen_si = 0, seen_rsi = 0;
+  for (;;) {
+    uint16_t pid, plen;
+    if (rd_u16(c, &pid) || rd_u16(c, &plen)) return -1;
+    if (pid == 0x0001) return 0; /* PID_SENTINEL */
+    if (c->pos + plen > c->len) return -1; /* reader.read_vec(length) */
+    uint32_t value_off = dgram_base + (uint32_t)c->pos;
+    if (pid == 0x0070 && !seen_kh) { seen_kh = 1; if (plen == 16) s->key_hash_off = value_off; }
+    if (pid == 0x0071 && !seen_si) { seen_si = 1; s->status_info_off = value_off; }
+    if ((pid == 0x0083 || pid == 0x800f) && !seen_rsi) { seen_rsi = 1; s->rsi_off = value_off; }
+    c->pos += plen;
+  }
+}
+
+/* Data::deserialize_data (data.rs:57-144).  body = submessage content. */
+static int data_deserialize(cursor* c, uint32_t dgram_base, uint8_t flags, submsg* s) {
+  uint16_t extra_flags, otq;
+  if (rd_u16(c, &extra_flags) || rd_u16(c, &otq)) return -1;
+  if (rd_entity_id(c, s->reader_id) || rd_entity_id(c, s->writer_id)) return -1;
+  if (rd_sn(c, &s->sn)) return -1;
+  int expect_qos = (flags & 0x02) != 0;                    /* DATA_Flags::InlineQos */
+  int expect_data = (flags & 0x04) != 0 || (flags & 0x08) != 0; /* Data || Key */
+  if (otq < 16) return -1;                                  /* :86-91 */
+  if (otq > 16) {                                           /* :95-116 */
+    c->pos += (size_t)(otq - 16);
+    if (c->pos > c->len) return -1;
+  }
+  uint32_t qos_start = (uint32_t)c->pos;
+  if (expect_qos) {
+    s->has_qos = 1;
+    if (parameter_list_read(c, dgram_base, s)) return -1;
+  }
+  s->qos_len = (uint32_t)c->pos - qos_start;
+  s->pl_off = dgram_base + (uint32_t)c->pos;
+  s->pl_len = (uint32_t)(c->len - c->pos);
+  s->has_payload = expect_data;                             /* :131-135 split_off(cursor) */
+  return 0;
+}
+
+/* DataFrag::deserialize (data_frag.rs:121-257) and total_number_of_fragments (:97-119). */
+static int datafrag_deserialize(cursor* c, uint32_t dgram_base, uint8_t flags, submsg* s) {
+  uint16_t extra_flags, otq, frags_in_sub, frag_size;
+  uint32_t frag_start, data_size;
+  if (rd_u16(c, &extra_flags) || rd_u16(c, &otq)) return -1;
+  if (rd_entity_id(c, s->reader_id) || rd_entity_id(c, s->writer_id)) return -1;
+  if (rd_sn(c, &s->sn)) return -1;
+  if (rd_u32(c, &frag_start) || rd_u16(c, &frags_in_sub) || rd_u16(c, &frag_size) || rd_u32(c, &data_size))
+    return -1;
+  int expect_qos = (flags & 0x02) != 0; /* DATAFRAG_Flags::InlineQos */
+  if (otq < 28) return -1;
+  if (otq > 28) {
+    c->pos += (size_t)(otq - 28);
+    if (c->pos > c->len) return -1;
+  }
+  uint32_t qos_start = (uint32_t)c->pos;
+  if (expect_qos) {
+    s->has_qos = 1;
+    if (parameter_list_read(c, dgram_base, s)) return -1;
+  }
+  s->qos_len = (uint32_t)c->pos - qos_start;
+  if (s->sn < 1) return -1;                                         /* :202-207 */
+  if (frag_size < 1 || (uint32_t)frag_size > data_size) return -1;  /* :215-224 */
+  s->pl_off = dgram_base + (uint32_t)c->pos;
+  s->pl_len = (uint32_t)(c->len - c->pos);
+  s->has_payload = 1;
+  uint32_t total = data_size / frag_size + ((data_size % frag_size) > 0 ? 1u : 0u);
+  if (frag_start < 1 || frag_start > total) return -1;              /* :244-254 */
+  s->frag_start = frag_start;
+  s->frags_in_sub = frags_in_sub;
+  s->frag_size = frag_size;
+  s->data_size = data_size;
+  return 0;
+}
+
+/* NumberSet<N>::read_from (sequence_number.rs:464-498); base already read by caller. */
+static int number_set_tail(cursor* c, uint32_t dgram_base, submsg* s) {
+  uint32_t num_bits;
+  if (rd_u32(c, &num_bits)) return -1;
+  if (num_bits > 256) return -1;
+  uint32_t words = (num_bits + 31u) / 32u;
+  s->num_bits = num_bits;
+  s->bitmap_off = dgram_base + (uint32_t)c->pos;
+  for (uint32_t i = 0; i < words; ++i) {
+    uint32_t wv;
+    if (rd_u32(c, &wv)) return -1;
+  }
+  return 0;
+}
+
+/* Submessage::read_from_buffer (rtps/submessage.rs:56-295).
+ * Returns 1 = materialised submessage, 0 = skipped (PAD / unknown), -1 = error.
+ * `rem` = remaining bytes of the message starting at `m + off`. */
+static int submessage_read_from_buffer(const uint8_t* m, uint32_t off, uint32_t rem,
+                                       submsg* s, uint32_t* consumed) {
+  /* SubmessageHeader::read_from (submessage_header.rs:14-35), minimum 4 bytes */
+  if (rem < 4) return -1;
+  uint8_t kind = m[off], flags = m[off + 1];
+  int le = (flags & 0x01) != 0;
+  uint16_t content_length = le ? (uint16_t)(m[off + 2] | (m[off + 3] << 8))
+                               : (uint16_t)((m[off + 2] << 8) | m[off + 3]);
+  uint32_t proposed;
+  if (content_length == 0) {
+    proposed = (kind == RTPS_PAD || kind == RTPS_INFO_TS) ? 0u : rem - 4u; /* :61-78 */
+  } else {
+    proposed = content_length;
+  }
+  if (4u + proposed > rem) return -1; /* :80-91 */
+  *consumed = 4u + proposed;
+
+  memset(s, 0, sizeof *s);
+  s->off = off;
+  s->kind = kind;
+  s->flags = flags;
+  s->content_len = proposed;
+  cursor c = {m + off + 4, proposed, 0, le};
+  uint32_t base = off + 4; /* datagram offset of body[0] */
+
+  switch (kind) {
+    case RTPS_DATA:
+      s->cls = BODY_WRITER;
+      return data_deserialize(&c, base, (uint8_t)(flags & 0x1f), s) ? -1 : 1;
+    case RTPS_DATA_FRAG:
+      s->cls = BODY_WRITER;
+      return datafrag_deserialize(&c, base, (uint8_t)(flags & 0x0f), s) ? -1 : 1;
+    case RTPS_GAP: /* Gap (gap.rs:23-46) */
+      s->cls = BODY_WRITER;
+      if (rd_entity_id(&c, s->reader_id) || rd_entity_id(&c, s->writer_id) || rd_sn(&c, &s->sn) ||
+          rd_sn(&c, &s->sn2) || number_set_tail(&c, base, s))
+        return -1;
+      return 1;
+    case RTPS_ACKNACK: /* AckNack (ack_nack.rs:27-50) */
+      s->cls = BODY_READER;
+      if (rd_entity_id(&c, s->reader_id) || rd_entity_id(&c, s->writer_id) || rd_sn(&c, &s->sn) ||
+          number_set_tail(&c, base, s))
+        return -1;
+      if (rd_u32(&c, (uint32_t*)&s->count)) return -1;
+      return 1;
+    case RTPS_NACK_FRAG: /* NackFrag (nack_frag.rs:31-53): FragmentNumberSet base is u32 */
+      s->cls = BODY_READER;
+      if (rd_entity_id(&c, s->reader_id) || rd_entity_id(&c, s->writer_id) || rd_sn(&c, &s->sn) ||
+          rd_u32(&c, &s->u32a) || number_set_tail(&c, base, s))
+        return -1;
+      if (rd_u32(&c, (uint32_t*)&s->count)) return -1;
+      return 1;
+    case RTPS_HEARTBEAT: /* Heartbeat (heartbeat.rs:21-49) */
+      s->cls = BODY_WRITER;
+      if (rd_entity_id(&c, s->reader_id) || rd_entity_id(&c, s->writer_id) || rd_sn(&c, &s->sn) ||
+          rd_sn(&c, &s->sn2) || rd_u32(&c, (uint32_t*)&s->count))
+        return -1;
+      return 1;
+    case RTPS_HEARTBEAT_FRAG: /* HeartbeatFrag (heartbeat_frag.rs:16-37) */
+      s->cls = BODY_WRITER;
+      if (rd_entity_id(&c, s->reader_id) || rd_entity_id(&c, s->writer_id) || rd_sn(&c, &s->sn) ||
+          rd_u32(&c, &s->u32a) || rd_u32(&c, (uint32_t*)&s->count))
+        return -1;
+      return 1;
+    case RTPS_INFO_DST: /* InfoDestination (info_destination.rs:20-25) */
+      s->cls = BODY_INTERP;
+      return rd_bytes(&c, s->prefix, 12) ? -1 : 1;
+    case RTPS_INFO_SRC: { /* InfoSource (info_source.rs:22-36) */
+      uint32_t unused;
+      s->cls = BODY_INTERP;
+      if (rd_u32(&c, &unused) || rd_bytes(&c, s->version, 2) || rd_bytes(&c, s->vendor, 2) ||
+          rd_bytes(&c, s->prefix, 12))
+        return -1;
+      return 1;
+    }
+    case RTPS_INFO_TS: /* rtps/submessage.rs:211-225; Timestamp (structure/time.rs:37-56) */
+      s->cls = BODY_INTERP;
+      if (flags & 0x02) { s->ts_valid = 0; return 1; } /* Invalidate */
+      if (rd_u32(&c, &s->ts_sec) || rd_u32(&c, &s->ts_frac)) return -1;
+      s->ts_valid = 1;
+      return 1;
+    case RTPS_INFO_REPLY: { /* InfoReply (info_reply.rs:9-21): speedy Vec<Locator> + Option<Vec<Locator>> */
+      uint32_t n1, n2 = 0xffffffffu;
+      uint8_t tag;
+      s->cls = BODY_INTERP;
+      if (rd_u32(&c, &n1)) return -1;
+      if ((uint64_t)n1 * 24u > (uint64_t)(c.len - c.pos)) return -1; /* Locator = i32 + u32 + 16 B */
+      c.pos += (size_t)n1 * 24u;
+      if (rd_u8(&c, &tag)) return -1;
+      if (tag != 0) { /* parity unpinned: speedy Option tag (non-zero -> Some) */
+        if (rd_u32(&c, &n2)) return -1;
+        if ((uint64_t)n2 * 24u > (uint64_t)(c.len - c.pos)) return -1;
+        c.pos += (size_t)n2 * 24u;
+      }
+      s->n_uni = n1;
+      s->n_multi = n2;
+      return 1;
+    }
+    case RTPS_PAD:
+    default:
+      /* PAD (:233-235); INFO_REPLY_IP4, SEC_* without `security`, vendor kinds (:278-293) */
+      return 0;
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* classification                                                            */
+/* ------------------------------------------------------------------------ */
+static const uint8_t E_UNKNOWN[4] = {0, 0, 0, 0};
+static const uint8_t E_SEDP_PUB_W[4] = {0, 0, 3, 0xc2}, E_SEDP_PUB_R[4] = {0, 0, 3, 0xc7};
+static const uint8_t E_SEDP_TOP_W[4] = {0, 0, 2, 0xc2}, E_SEDP_TOP_R[4] = {0, 0, 2, 0xc7};
+static const uint8_t E_SEDP_SUB_W[4] = {0, 0, 4, 0xc2}, E_SEDP_SUB_R[4] = {0, 0, 4, 0xc7};
+static const uint8_t E_SPDP_W[4] = {0, 1, 0, 0xc2}, E_SPDP_R[4] = {0, 1, 0, 0xc7};
+static const uint8_t E_P2P_W[4] = {0, 2, 0, 0xc2}, E_P2P_R[4] = {0, 2, 0, 0xc7};
+
+static int eid_eq(const uint8_t a[4], const uint8_t b[4]) { return memcmp(a, b, 4) == 0; }
+
+/* Discovery2::handle_writer_msg pair test (io_uring/discovery/discovery.rs:2795-2816),
+ * (receiver, sender) = (reader_id, writer_id) for writer submessages. */
+static int builtin_writer_pair(const uint8_t rid[4], const uint8_t wid[4]) {
+  if (eid_eq(rid, E_UNKNOWN))
+    return eid_eq(wid, E_SEDP_PUB_W) || eid_eq(wid, E_SEDP_TOP_W) || eid_eq(wid, E_SPDP_W) ||
+           eid_eq(wid, E_SEDP_SUB_W) || eid_eq(wid, E_P2P_W);
+  return (eid_eq(rid, E_SEDP_PUB_R) && eid_eq(wid, E_SEDP_PUB_W)) ||
+         (eid_eq(rid, E_SEDP_TOP_R) && eid_eq(wid, E_SEDP_TOP_W)) ||
+         (eid_eq(rid, E_SEDP_SUB_R) && eid_eq(wid, E_SEDP_SUB_W));
+}
+/* Discovery2::handle_reader_submsg pair test (discovery.rs:3075-3095),
+ * (receiver, sender) = (writer_id, reader_id) for ACKNACK / NACK_FRAG. */
+static int builtin_reader_pair(const uint8_t rid[4], const uint8_t wid[4]) {
+  return (eid_eq(wid, E_SEDP_PUB_W) && eid_eq(rid, E_SEDP_PUB_R)) ||
+         (eid_eq(wid, E_SEDP_TOP_W) && eid_eq(rid, E_SEDP_TOP_R)) ||
+         (eid_eq(wid, E_SEDP_SUB_W) && eid_eq(rid, E_SEDP_SUB_R)) ||
+         (eid_eq(wid, E_SPDP_W) && eid_eq(rid, E_SPDP_R)) ||
+         (eid_eq(wid, E_P2P_W) && eid_eq(rid, E_P2P_R));
+}
+
+/* matched_writers lookup by full GUID (reader.rs:474-484, 712-738): first entry wins */
+static uint16_t match_lookup(const rtps_match* table, uint32_t n, const uint8_t prefix[12],
+                             const uint8_t wid[4]) {
+  for (uint32_t i = 0; i < n; ++i)
+    if (memcmp(table[i].writer_guid, prefix, 12) == 0 && memcmp(table[i].writer_guid + 12, wid, 4) == 0)
+      return table[i].reader_slot;
+  return RTPS_NO_MATCH;
+}
+
+/* Reader::data_to_dds_data (io_uring/rtps/reader.rs:760-833) +
+ * SerializedPayload::from_bytes (serialized_payload.rs:86-110). */
+static uint8_t data_to_dds_data_kind(const submsg* s) {
+  int d = (s->flags & 0x04) != 0, k = (s->flags & 0x08) != 0;
+  if (s->has_payload) {
+    if (d && k) return RTPS_PK_ERR_AMBIGUOUS;
+    if (s->pl_len < 4) return RTPS_PK_ERR_SHORT;
+    return d ? RTPS_PK_DATA : RTPS_PK_KEY;
+  }
+  /* (None, false, false): needs a 16-byte KEY_HASH in the inline QoS */
+  return s->key_hash_off ? RTPS_PK_KEY_HASH : RTPS_PK_ERR_NO_CONTENT;
+}
+
+/* ------------------------------------------------------------------------ */
+/* one datagram: handle_received_packet_2 + Message::read_from_buffer +      */
+/* the SubmessageIter2 interpreter                                            */
+/* ------------------------------------------------------------------------ */
+typedef struct oracle_cfg {
+  uint8_t own[12];
+  const rtps_match* table;
+  uint32_t n_match;
+} oracle_cfg;
+
+#define MAX_SUBMSGS (RTPS_MAX_DATAGRAM / 4)
+
+/* returns status; writes up to cap records into recs (count in *n_out) */
+static uint8_t oracle_datagram(const oracle_cfg* cfg, const uint8_t* m, uint32_t L, uint32_t dgram_idx,
+                               submsg* subs /* scratch [MAX_SUBMSGS] */, rtps_record* recs,
+                               uint16_t* match_out, uint32_t* n_out) {
+  *n_out = 0;
+  if (L > RTPS_MAX_DATAGRAM) return RTPS_DGRAM_TOO_LONG;
+  /* message_receiver.rs:238-251 */
+  if (L < 20) {
+    if (L >= 16 && memcmp(m, "RTPS", 4) == 0 && memcmp(m + 9, "DDSPING", 7) == 0) return RTPS_DGRAM_PING;
+    return RTPS_DGRAM_SHORT;
+  }
+  /* :254-271 */
+  if (memcmp(m, "RTPS", 4) != 0) return memcmp(m, "RTPX", 4) == 0 ? RTPS_DGRAM_RTPX : RTPS_DGRAM_BAD_MAGIC;
+  /* Header::valid (messages/header.rs:30-39): protocol id checked above, major <= 2 */
+  if (m[4] > 2) return RTPS_DGRAM_BAD_HEADER;
+  /* Message::read_from_buffer submessage loop (rtps/message.rs:74-78) */
+  uint32_t nsub = 0, off = 20;
+  while (off < L) {
+    uint32_t used = 0;
+    int r = submessage_read_from_buffer(m, off, L - off, &subs[nsub], &used);
+    if (r < 0) return RTPS_DGRAM_SUBMSG_ERR;
+    if (r > 0) nsub++;
+    off += used;
+  }
+  /* handle_parsed_message_2 (:289-295): reset(), dest := own, src := header prefix */
+  uint8_t src[12], dest[12];
+  static const uint8_t zero12[12] = {0};
+  memcpy(src, m + 8, 12);
+  memcpy(dest, cfg->own, 12);
+  int ts_valid = 0;
+  uint32_t ts_sec = 0, ts_frac = 0;
+  for (uint32_t i = 0; i < nsub; ++i) {
+    const submsg* s = &subs[i];
+    rtps_record* rec = &recs[i];
+    memset(rec, 0, sizeof *rec);
+    rec->dgram_idx = dgram_idx;
+    rec->sub_off = (uint16_t)s->off;
+    rec->kind = s->kind;
+    rec->flags = s->flags;
+    uint16_t mslot = RTPS_NO_MATCH;
+    if (s->cls == BODY_INTERP) {
+      /* handle_interpreter_submessage (message_receiver.rs:618-665) */
+      switch (s->kind) {
+        case RTPS_INFO_TS:
+          ts_valid = s->ts_valid; ts_sec = s->ts_valid ? s->ts_sec : 0; ts_frac = s->ts_valid ? s->ts_frac : 0;
+          memcpy(rec->prefix, src, 12);
+          break;
+        case RTPS_INFO_SRC:
+          memcpy(src, s->prefix, 12);
+          ts_valid = 0; ts_sec = 0; ts_frac = 0;
+          memcpy(rec->prefix, s->prefix, 12);
+          memcpy(rec->u.infosrc.version, s->version, 2);
+          memcpy(rec->u.infosrc.vendor, s->vendor, 2);
+          break;
+        case RTPS_INFO_DST:
+          if (memcmp(s->prefix, zero12, 12) == 0) memcpy(dest, cfg->own, 12);
+          else memcpy(dest, s->prefix, 12);
+          memcpy(rec->prefix, s->prefix, 12);
+          break;
+        case RTPS_INFO_REPLY:
+          memcpy(rec->prefix, src, 12);
+          rec->u.inforeply.n_unicast = s->n_uni;
+          rec->u.inforeply.n_multicast = s->n_multi;
+          break;
+      }
+      rec->aux16 = (uint16_t)s->content_len;
+    } else {
+      memcpy(rec->prefix, src, 12);
+      memcpy(rec->writer_id, s->writer_id, 4);
+      memcpy(rec->reader_id, s->reader_id, 4);
+      rec->sn = s->sn;
+      if (s->cls == BODY_WRITER) {
+        /* SubmessageIter2::next writer filter (message_receiver.rs:75-84) */
+        int pass = memcmp(dest, cfg->own, 12) == 0 || memcmp(dest, zero12, 12) == 0;
+        if (pass) rec->route |= RTPS_ROUTE_PASS;
+        if (builtin_writer_pair(s->reader_id, s->writer_id)) rec->route |= RTPS_ROUTE_BUILTIN;
+        else {
+          mslot = match_lookup(cfg->table, cfg->n_match, src, s->writer_id);
+          if (mslot != RTPS_NO_MATCH) rec->route |= RTPS_ROUTE_MATCHED;
+        }
+      } else {
+        rec->route |= RTPS_ROUTE_PASS; /* reader submessages always pass (:88-113) */
+        if (builtin_reader_pair(s->reader_id, s->writer_id)) rec->route |= RTPS_ROUTE_BUILTIN;
+      }
+      switch (s->kind) {
+        case RTPS_DATA:
+          rec->aux16 = (uint16_t)s->qos_len;
+          if (s->has_qos) rec->route |= RTPS_ROUTE_HAS_QOS;
+          if (s->has_payload) rec->route |= RTPS_ROUTE_HAS_PAYLOAD;
+          rec->u.data.pl_off = (uint16_t)s->pl_off;
+          rec->u.data.pl_len = (uint16_t)s->pl_len;
+          rec->payload_kind = data_to_dds_data_kind(s);
+          if (rec->payload_kind == RTPS_PK_DATA || rec->payload_kind == RTPS_PK_KEY) {
+            memcpy(rec->u.data.rep_id, m + s->pl_off, 2);
+            memcpy(rec->u.data.rep_opts, m + s->pl_off + 2, 2);
+          }
+          rec->u.data.key_hash_off = (uint16_t)s->key_hash_off;
+          rec->u.data.status_info_off = (uint16_t)s->status_info_off;
+          rec->u.data.rsi_off = (uint16_t)s->rsi_off;
+          break;
+        case RTPS_DATA_FRAG:
+          rec->aux16 = (uint16_t)s->qos_len;
+          if (s->has_qos) rec->route |= RTPS_ROUTE_HAS_QOS;
+          rec->route |= RTPS_ROUTE_HAS_PAYLOAD;
+          rec->u.frag.pl_off = (uint16_t)s->pl_off;
+          rec->u.frag.pl_len = (uint16_t)s->pl_len;
+          rec->u.frag.frag_start = s->frag_start;
+          rec->u.frag.frags_in_sub = (uint16_t)s->frags_in_sub;
+          rec->u.frag.frag_size = (uint16_t)s->frag_size;
+          rec->u.frag.data_size = s->data_size;
+          break;
+        case RTPS_HEARTBEAT:
+          rec->aux16 = (uint16_t)s->content_len;
+          rec->u.hb.last_sn = s->sn2;
+          rec->u.hb.count = s->count;
+          break;
+        case RTPS_HEARTBEAT_FRAG:
+          rec->aux16 = (uint16_t)s->content_len;
+          rec->u.hbfrag.last_frag_num = s->u32a;
+          rec->u.hbfrag.count = s->count;
+          break;
+        case RTPS_GAP:
+          rec->aux16 = (uint16_t)s->content_len;
+          rec->u.gap.list_base = s->sn2;
+          rec->u.gap.num_bits = s->num_bits;
+          rec->u.gap.bitmap_off = (uint16_t)s->bitmap_off;
+          break;
+        case RTPS_ACKNACK:
+          rec->aux16 = (uint16_t)s->content_len;
+          rec->u.acknack.count = s->count;
+          rec->u.acknack.num_bits = s->num_bits;
+          rec->u.acknack.bitmap_off = (uint16_t)s->bitmap_off;
+          break;
+        case RTPS_NACK_FRAG:
+          rec->aux16 = (uint16_t)s->content_len;
+          rec->u.nackfrag.fns_base = s->u32a;
+          rec->u.nackfrag.count = s->count;
+          rec->u.nackfrag.num_bits = s->num_bits;
+          rec->u.nackfrag.bitmap_off = (uint16_t)s->bitmap_off;
+          break;
+      }
+    }
+    if (ts_valid) {
+      rec->route |= RTPS_ROUTE_TS_VALID;
+      rec->ts_sec = ts_sec;
+      rec->ts_frac = ts_frac;
+    }
+    if (match_out) match_out[i] = mslot;
+  }
+  *n_out = nsub;
+  return RTPS_DGRAM_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+/* batch entry points (ctypes)                                               */
+/* ------------------------------------------------------------------------ */
+typedef struct slice_job {
+  const oracle_cfg* cfg;
+  const uint8_t* arena;
+  const uint64_t* off;
+  const uint32_t* len;
+  uint32_t lo, hi;
+  uint8_t* status;
+  rtps_record* recs; /* thread-local */
+  uint16_t* match;   /* thread-local */
+  uint32_t* counts;  /* per datagram */
+  uint64_t n_recs, cap;
+  submsg* scratch;
+} slice_job;
+
+static void* run_slice(void* arg) {
+  slice_job* j = (slice_job*)arg;
+  j->n_recs = 0;
+  for (uint32_t i = j->lo; i < j->hi; ++i) {
+    uint32_t L = j->len[i];
+    uint32_t nr = 0;
+    uint64_t need = (L >= 20 && L <= RTPS_MAX_DATAGRAM) ? (uint64_t)(L - 20) / 4u : 0u;
+    if (j->n_recs + need > j->cap) { /* grow thread-local buffers */
+      uint64_t ncap = (j->cap + need) * 2 + 64;
+      j->recs = (rtps_record*)realloc(j->recs, ncap * sizeof(rtps_record));
+      j->match = (uint16_t*)realloc(j->match, ncap * sizeof(uint16_t));
+      j->cap = ncap;
+    }
+    j->status[i] = oracle_datagram(j->cfg, j->arena + j->off[i], L, i, j->scratch, j->recs + j->n_recs,
+                                   j->match + j->n_recs, &nr);
+    j->counts[i] = nr;
+    j->n_recs += nr;
+  }
+  return 0;
+}
+
+/* Parse a batch on `threads` host threads (contiguous slices).  Outputs are
+ * identical to the device library's: status[n], records (ascending
+ * (dgram_idx, sub_off)), match[], rec_begin[n] (optional), total count.
+ * Returns the total number of records (records beyond max_records are not
+ * written). */
+uint64_t rtps_oracle_parse(const uint8_t* arena, const uint64_t* off, const uint32_t* len, uint32_t n,
+                           const uint8_t own[12], const rtps_match* table, uint32_t n_match,
+                           uint8_t* status, rtps_record* records, uint64_t max_records,
+                           uint16_t* match, uint32_t* rec_begin, int threads) {
+  oracle_cfg cfg;
+  memcpy(cfg.own, own, 12);
+  cfg.table = table;
+  cfg.n_match = n_match;
+  if (threads < 1) threads = 1;
+  if ((uint32_t)threads > n && n > 0) threads = (int)n;
+  uint32_t* counts = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
+  slice_job* jobs = (slice_job*)calloc((size_t)threads, sizeof(slice_job));
+  pthread_t* tids = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+  for (int t = 0; t < threads; ++t) {
+    jobs[t].cfg = &cfg;
+    jobs[t].arena = arena;
+    jobs[t].off = off;
+    jobs[t].len = len;
+    jobs[t].lo = (uint32_t)((uint64_t)n * t / threads);
+    jobs[t].hi = (uint32_t)((uint64_t)n * (t + 1) / threads);
+    jobs[t].status = status;
+    jobs[t].counts = counts;
+    jobs[t].scratch = (submsg*)malloc(sizeof(submsg) * MAX_SUBMSGS);
+    if (threads > 1) pthread_create(&tids[t], 0, run_slice, &jobs[t]);
+  }
+  if (threads == 1) run_slice(&jobs[0]);
+  else for (int t = 0; t < threads; ++t) pthread_join(tids[t], 0);
+  uint64_t total = 0;
+  for (int t = 0; t < threads; ++t) {
+    uint64_t k = jobs[t].n_recs;
+    if (records && total < max_records) {
+      uint64_t w = (total + k <= max_records) ? k : max_records - total;
+      memcpy(records + total, jobs[t].recs, w * sizeof(rtps_record));
+      if (match) memcpy(match + total, jobs[t].match, w * sizeof(uint16_t));
+    }
+    total += k;
+    free(jobs[t].recs);
+    free(jobs[t].match);
+    free(jobs[t].scratch);
+  }
+  if (rec_begin) {
+    uint64_t acc = 0;
+    for (uint32_t i = 0; i < n; ++i) { rec_begin[i] = (uint32_t)acc; acc += counts[i]; }
+  }
+  free(counts);
+  free(jobs);
+  free(tids);
+  return total;
+}
+
+/* Host-side synthetic generator (same f(seed, idx) as the device kernel). */
+uint64_t rtps_oracle_gen_layout(int wl, uint64_t seed, uint64_t first_idx, uint32_t n_writers, uint32_t n,
+                                uint64_t* off, uint32_t* len) {
+  return rtps_gen_layout_host(wl, seed, first_idx, n_writers, n, off, len);
+}
+void rtps_oracle_gen_fill(int wl, uint64_t seed, uint64_t first_idx, uint32_t n_writers, uint32_t n,
+                          const uint64_t* off, uint8_t* arena) {
+  for (uint32_t i = 0; i < n; ++i) rtps_gen_datagram(wl, seed, first_idx + i, n_writers, arena + off[i]);
+}
+uint32_t rtps_oracle_record_size(void) { return (uint32_t)sizeof(rtps_record); }

@@ -1,0 +1,921 @@
+// rtps_rx.hip — MI355X (gfx950) RTPS receive-path parser + C ABI (include/rtps_rx.h).
+//
+// One kernel, rtps_parse_kernel, replaces for a whole batch of datagrams:
+//   MessageReceiver::handle_received_packet_2      io_uring/rtps/message_receiver.rs:232-287
+//   Message::read_from_buffer + Submessage::read_from_buffer
+//                                                  rtps/message.rs:64-81, rtps/submessage.rs:56-295
+//   the per-kind readers in src/messages/**        (data.rs:57-144, data_frag.rs:121-257, ...)
+//   SubmessageIter2 interpreter + dest filter      io_uring/rtps/message_receiver.rs:56-119, 618-665
+//   builtin-pair / matched-writer classification   io_uring/discovery/discovery.rs:2795-2816,3075-3095
+//   Reader::data_to_dds_data payload decision      io_uring/rtps/reader.rs:760-833
+//
+// Layout / mapping:
+//   * one LANE per datagram, 256 datagrams (4 wave64s) per workgroup "tile";
+//     the submessage chain of a datagram is a serial pointer chase, so the
+//     parallelism is across datagrams;
+//   * the datagram bytes are never copied: each submessage is read through a
+//     48-byte register window (3 x 16-B buffer loads at the submessage start,
+//     every fixed field at a compile-time offset), variable-offset fields
+//     (inline-QoS parameters, AckNack count, ...) by 4-byte loads; payload
+//     bytes stay in HBM (zero-copy spans, like the reference's Bytes slices);
+//   * records are placed in the reference's order (ascending dgram, sub_off)
+//     by a single-pass decoupled look-back scan over tiles: walk 1 counts,
+//     the tile publishes its aggregate, looks back for its prefix, walk 2
+//     writes the 64-B records at their final index;
+//   * all arena reads go through a bounds-checked buffer resource (reads past
+//     the arena return 0 and never fault).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "../../include/rtps_rx.h"
+#include "rtps_gen.h"
+
+namespace {
+
+constexpr uint32_t TILE = 256;  // datagrams per workgroup
+constexpr uint32_t WAVES = TILE / 64;
+constexpr uint64_t FLAG_AGG = 1ull << 62, FLAG_INC = 2ull << 62, VAL_MASK = (1ull << 62) - 1;
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+struct KParams {
+  const uint8_t* arena;
+  uint64_t arena_len;
+  const uint64_t* dgram_off;
+  const uint32_t* dgram_len;
+  uint32_t n;
+  uint32_t own0, own1, own2;  // own GuidPrefix as 3 little-endian words
+  uint8_t* status;
+  rtps_record* records;
+  uint64_t max_records;
+  uint16_t* match_out;
+  uint32_t* rec_begin;
+  uint64_t* n_records;
+  const u32x4* mt_keys;       // match table (open addressing), may be null
+  const uint16_t* mt_slots;
+  uint32_t mt_mask;           // capacity - 1
+  uint64_t* scratch;          // [0] = tile ticket, [1] = look-back timeouts, [2..] tile states
+};
+
+// ---------------------------------------------------------------------------
+// arena access: byte offsets are relative to the lane's datagram start
+// ---------------------------------------------------------------------------
+struct Src {
+  __amdgpu_buffer_rsrc_t rsrc;  // wave-uniform, base = arena + tile_base
+  uint32_t base;                // datagram start relative to the descriptor base
+  uint32_t avail;               // bytes addressable through the descriptor
+};
+
+__device__ __forceinline__ uint32_t ld_u8_raw(const Src& s, uint32_t a) {
+  return (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(s.rsrc, a, 0, 0);
+}
+// 16 bytes at datagram offset o (unaligned). Bytes past the arena read as 0.
+__device__ __forceinline__ u32x4 ld16(const Src& s, uint32_t o) {
+  uint32_t a = s.base + o;
+  if ((uint64_t)a + 16u <= s.avail) return __builtin_amdgcn_raw_buffer_load_b128(s.rsrc, a, 0, 0);
+  u32x4 r = {0u, 0u, 0u, 0u};
+  for (uint32_t k = 0; k < 16; ++k) {
+    uint32_t b = ((uint64_t)a + k < s.avail) ? ld_u8_raw(s, a + k) : 0u;
+    r[k >> 2] |= b << (8u * (k & 3u));
+  }
+  return r;
+}
+// 4 bytes at datagram offset o (unaligned), raw wire order packed little-endian.
+__device__ __forceinline__ uint32_t ld4(const Src& s, uint32_t o) {
+  uint32_t a = s.base + o;
+  if ((uint64_t)a + 4u <= s.avail) return __builtin_amdgcn_raw_buffer_load_b32(s.rsrc, a, 0, 0);
+  uint32_t r = 0;
+  for (uint32_t k = 0; k < 4; ++k)
+    if ((uint64_t)a + k < s.avail) r |= ld_u8_raw(s, a + k) << (8u * k);
+  return r;
+}
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+// wire dword -> value in the submessage byte order
+__device__ __forceinline__ uint32_t e32(uint32_t raw, bool le) { return le ? raw : bswap32(raw); }
+// wire u16 stored in the low (sel=0) or high (sel=1) half of a raw dword
+__device__ __forceinline__ uint32_t e16(uint32_t raw, uint32_t sel, bool le) {
+  uint32_t v = (raw >> (16u * sel)) & 0xffffu;
+  return le ? v : (((v & 0xffu) << 8) | (v >> 8));
+}
+__device__ __forceinline__ int64_t sn_of(uint32_t hi_raw, uint32_t lo_raw, bool le) {
+  // SequenceNumber::read_from: i32 high, u32 low (sequence_number.rs:169-182)
+  return (int64_t)(((uint64_t)(int64_t)(int32_t)e32(hi_raw, le)) << 32) + (int64_t)e32(lo_raw, le);
+}
+
+// 48-byte window at a submessage start: w[0] = header, w[1..] = body dwords
+struct Win {
+  uint32_t w[12];
+};
+__device__ __forceinline__ void load_win(const Src& s, uint32_t o, Win& W) {
+  u32x4 a = ld16(s, o), b = ld16(s, o + 16), c = ld16(s, o + 32);
+  W.w[0] = a[0]; W.w[1] = a[1]; W.w[2] = a[2]; W.w[3] = a[3];
+  W.w[4] = b[0]; W.w[5] = b[1]; W.w[6] = b[2]; W.w[7] = b[3];
+  W.w[8] = c[0]; W.w[9] = c[1]; W.w[10] = c[2]; W.w[11] = c[3];
+}
+
+// builtin (reader_id, writer_id) pairs; entity ids as raw little-endian-packed words
+// (bytes k0 k1 k2 kind -> k0 | k1<<8 | k2<<16 | kind<<24)
+__device__ __forceinline__ uint32_t eid(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t kind) {
+  return k0 | (k1 << 8) | (k2 << 16) | (kind << 24);
+}
+// Discovery2::handle_writer_msg (io_uring/discovery/discovery.rs:2795-2816)
+__device__ __forceinline__ bool builtin_writer_pair(uint32_t rid, uint32_t wid) {
+  const uint32_t SEDP_PUB_W = eid(0, 0, 3, 0xc2), SEDP_PUB_R = eid(0, 0, 3, 0xc7);
+  const uint32_t SEDP_TOP_W = eid(0, 0, 2, 0xc2), SEDP_TOP_R = eid(0, 0, 2, 0xc7);
+  const uint32_t SEDP_SUB_W = eid(0, 0, 4, 0xc2), SEDP_SUB_R = eid(0, 0, 4, 0xc7);
+  const uint32_t SPDP_W = eid(0, 1, 0, 0xc2), P2P_W = eid(0, 2, 0, 0xc2);
+  if (rid == 0u)
+    return wid == SEDP_PUB_W || wid == SEDP_TOP_W || wid == SPDP_W || wid == SEDP_SUB_W || wid == P2P_W;
+  return (rid == SEDP_PUB_R && wid == SEDP_PUB_W) || (rid == SEDP_TOP_R && wid == SEDP_TOP_W) ||
+         (rid == SEDP_SUB_R && wid == SEDP_SUB_W);
+}
+// Discovery2::handle_reader_submsg (discovery.rs:3075-3095): (writer_id, reader_id)
+__device__ __forceinline__ bool builtin_reader_pair(uint32_t rid, uint32_t wid) {
+  return (wid == eid(0, 0, 3, 0xc2) && rid == eid(0, 0, 3, 0xc7)) ||
+         (wid == eid(0, 0, 2, 0xc2) && rid == eid(0, 0, 2, 0xc7)) ||
+         (wid == eid(0, 0, 4, 0xc2) && rid == eid(0, 0, 4, 0xc7)) ||
+         (wid == eid(0, 1, 0, 0xc2) && rid == eid(0, 1, 0, 0xc7)) ||
+         (wid == eid(0, 2, 0, 0xc2) && rid == eid(0, 2, 0, 0xc7));
+}
+
+__device__ __forceinline__ uint32_t guid_hash(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  uint32_t h = 0x811c9dc5u;
+  h = (h ^ a) * 0x01000193u; h = (h ^ b) * 0x01000193u;
+  h = (h ^ c) * 0x01000193u; h = (h ^ d) * 0x01000193u;
+  return h ^ (h >> 15);
+}
+__device__ __forceinline__ uint16_t match_lookup(const KParams& p, uint32_t a, uint32_t b, uint32_t c,
+                                                 uint32_t d) {
+  if (p.mt_keys == nullptr) return RTPS_NO_MATCH;
+  uint32_t i = guid_hash(a, b, c, d) & p.mt_mask;
+  for (uint32_t probe = 0; probe <= p.mt_mask; ++probe) {
+    uint16_t slot = p.mt_slots[i];
+    if (slot == RTPS_NO_MATCH) return RTPS_NO_MATCH;
+    u32x4 k = p.mt_keys[i];
+    if (k[0] == a && k[1] == b && k[2] == c && k[3] == d) return slot;
+    i = (i + 1u) & p.mt_mask;
+  }
+  return RTPS_NO_MATCH;
+}
+
+// One record being assembled in registers (16 dwords = 64 bytes).
+struct Rec {
+  uint32_t d[16];
+};
+__device__ __forceinline__ void rec_clear(Rec& r) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) r.d[i] = 0u;
+}
+__device__ __forceinline__ void rec_store(rtps_record* dst, const Rec& r) {
+  u32x4* p = reinterpret_cast<u32x4*>(dst);
+  p[0] = u32x4{r.d[0], r.d[1], r.d[2], r.d[3]};
+  p[1] = u32x4{r.d[4], r.d[5], r.d[6], r.d[7]};
+  p[2] = u32x4{r.d[8], r.d[9], r.d[10], r.d[11]};
+  p[3] = u32x4{r.d[12], r.d[13], r.d[14], r.d[15]};
+}
+
+// ParameterList::read_from (elements/parameter_list.rs:79-102) over the body
+// starting at body position pos; records the first KEY_HASH (16-byte value
+// required, dds/key.rs:64-68), STATUS_INFO and RELATED_SAMPLE_IDENTITY values.
+// Returns false on a read error.
+__device__ __forceinline__ bool param_list(const Src& s, uint32_t body_off, uint32_t blen, bool le,
+                                           uint32_t& pos, uint32_t& kh, uint32_t& si, uint32_t& rsi) {
+  bool seen_kh = false, seen_si = false, seen_rsi = false;
+  for (;;) {
+    if (pos + 4u > blen) return false;
+    uint32_t raw = ld4(s, body_off + pos);
+    uint32_t pid = e16(raw, 0, le), plen = e16(raw, 1, le);
+    pos += 4u;
+    if (pid == 0x0001u) return true;  // PID_SENTINEL: value not read
+    if (pos + plen > blen) return false;
+    uint32_t voff = body_off + pos;
+    if (pid == 0x0070u && !seen_kh) { seen_kh = true; if (plen == 16u) kh = voff; }
+    if (pid == 0x0071u && !seen_si) { seen_si = true; si = voff; }
+    if ((pid == 0x0083u || pid == 0x800fu) && !seen_rsi) { seen_rsi = true; rsi = voff; }
+    pos += plen;
+  }
+}
+
+// Walk one datagram.  WRITE=false: validate + count materialised submessages.
+// WRITE=true: (datagram known OK) write its records starting at record index `ridx`.
+template <bool WRITE>
+__device__ uint32_t walk(const KParams& p, const Src& s, uint32_t L, uint32_t dgram_idx, uint64_t ridx,
+                         uint32_t& nrec) {
+  nrec = 0;
+  if (L > RTPS_MAX_DATAGRAM) return RTPS_DGRAM_TOO_LONG;
+  const uint32_t MAGIC_RTPS = 0x53505452u, MAGIC_RTPX = 0x58505452u;  // "RTPS" / "RTPX"
+  u32x4 h0 = ld16(s, 0);
+  if (L < 20u) {  // message_receiver.rs:238-251
+    if (L >= 16u && h0[0] == MAGIC_RTPS && (h0[2] >> 8) == 0x534444u /* "DDS" */ &&
+        h0[3] == 0x474e4950u /* "PING" */)
+      return RTPS_DGRAM_PING;
+    return RTPS_DGRAM_SHORT;
+  }
+  if (h0[0] != MAGIC_RTPS) return h0[0] == MAGIC_RTPX ? RTPS_DGRAM_RTPX : RTPS_DGRAM_BAD_MAGIC;
+  if ((h0[1] & 0xffu) > 2u) return RTPS_DGRAM_BAD_HEADER;  // ProtocolVersion major
+  // handle_parsed_message_2 (:289-295): src := header prefix, dest := own, ts := None
+  uint32_t src0 = h0[2], src1 = h0[3], src2 = ld4(s, 16);
+  uint32_t dst0 = p.own0, dst1 = p.own1, dst2 = p.own2;
+  bool ts_valid = false;
+  uint32_t ts_sec = 0, ts_frac = 0;
+
+  uint32_t o = 20;
+  while (o < L) {
+    uint32_t rem = L - o;
+    if (rem < 4u) return RTPS_DGRAM_SUBMSG_ERR;  // SubmessageHeader needs 4 bytes
+    Win W;
+    load_win(s, o, W);
+    uint32_t kind = W.w[0] & 0xffu, flags = (W.w[0] >> 8) & 0xffu;
+    bool le = (flags & 1u) != 0u;
+    uint32_t clen = e16(W.w[0], 1, le);
+    uint32_t eff = clen != 0u ? clen : ((kind == RTPS_PAD || kind == RTPS_INFO_TS) ? 0u : rem - 4u);
+    if (4u + eff > rem) return RTPS_DGRAM_SUBMSG_ERR;
+    const uint32_t blen = eff, body = o + 4u;
+    const uint32_t next = o + 4u + eff;
+
+    Rec R;
+    if (WRITE) {
+      rec_clear(R);
+      R.d[0] = dgram_idx;
+      R.d[1] = o | (kind << 16) | (flags << 24);
+    }
+    bool emit = true;
+    uint32_t route = 0, pk = 0, aux16 = blen;
+    uint16_t mslot = RTPS_NO_MATCH;
+    int cls = 0;  // 1 writer, 2 reader, 3 interpreter
+    uint32_t rid = 0, wid = 0;
+
+    switch (kind) {
+      case RTPS_DATA: {  // Data::deserialize_data (data.rs:57-144)
+        if (blen < 20u) return RTPS_DGRAM_SUBMSG_ERR;
+        uint32_t otq = e16(W.w[1], 1, le);
+        if (otq < 16u) return RTPS_DGRAM_SUBMSG_ERR;
+        uint32_t pos = 20u;
+        if (otq > 16u) { pos = 4u + otq; if (pos > blen) return RTPS_DGRAM_SUBMSG_ERR; }
+        uint32_t fl = flags & 0x1fu;
+        bool q = (fl & 0x02u) != 0u, dk = (fl & 0x0cu) != 0u;
+        uint32_t qstart = pos, kh = 0, si = 0, rsi = 0;
+        if (q && !param_list(s, body, blen, le, pos, kh, si, rsi)) return RTPS_DGRAM_SUBMSG_ERR;
+        cls = 1;
+        if (WRITE) {
+          rid = W.w[2]; wid = W.w[3];
+          int64_t sn = sn_of(W.w[4], W.w[5], le);
+          uint32_t pl_off = body + pos, pl_len = blen - pos;
+          aux16 = pos - qstart;
+          if (q) route |= RTPS_ROUTE_HAS_QOS;
+          if (dk) route |= RTPS_ROUTE_HAS_PAYLOAD;
+          // Reader::data_to_dds_data (reader.rs:760-833)
+          uint32_t enc = 0;
+          if (dk) {
+            bool d = (fl & 0x04u) != 0u, k = (fl & 0x08u) != 0u;
+            if (d && k) pk = RTPS_PK_ERR_AMBIGUOUS;
+            else if (pl_len < 4u) pk = RTPS_PK_ERR_SHORT;
+            else {
+              pk = d ? RTPS_PK_DATA : RTPS_PK_KEY;
+              enc = (pos == 20u) ? W.w[6] : ld4(s, pl_off);  // rep_id[2] + options[2]
+            }
+          } else {
+            pk = kh ? RTPS_PK_KEY_HASH : RTPS_PK_ERR_NO_CONTENT;
+          }
+          R.d[8] = (uint32_t)sn; R.d[9] = (uint32_t)((uint64_t)sn >> 32);
+          R.d[10] = pl_off | (pl_len << 16);
+          R.d[11] = enc;
+          R.d[12] = kh | (si << 16);
+          R.d[13] = rsi;
+        }
+        break;
+      }
+      case RTPS_DATA_FRAG: {  // DataFrag::deserialize (data_frag.rs:121-257)
+        if (blen < 32u) return RTPS_DGRAM_SUBMSG_ERR;
+        uint32_t otq = e16(W.w[1], 1, le);
+        if (otq < 28u) return RTPS_DGRAM_SUBMSG_ERR;
+        uint32_t pos = 32u;
+        if (otq > 28u) { pos = 4u + otq; if (pos > blen) return RTPS_DGRAM_SUBMSG_ERR; }
+        bool q = (flags & 0x02u) != 0u;
+        uint32_t qstart = pos, kh = 0, si = 0, rsi = 0;
+        if (q && !param_list(s, body, blen, le, pos, kh, si, rsi)) return RTPS_DGRAM_SUBMSG_ERR;
+        int64_t sn = sn_of(W.w[4], W.w[5], le);
+        if (sn < 1) return RTPS_DGRAM_SUBMSG_ERR;
+        uint32_t frag_start = e32(W.w[6], le);
+        uint32_t frags_in_sub = e16(W.w[7], 0, le), frag_size = e16(W.w[7], 1, le);
+        uint32_t data_size = e32(W.w[8], le);
+        if (frag_size < 1u || frag_size > data_size) return RTPS_DGRAM_SUBMSG_ERR;
+        uint32_t total = data_size / frag_size + ((data_size % frag_size) ? 1u : 0u);
+        if (frag_start < 1u || frag_start > total) return RTPS_DGRAM_SUBMSG_ERR;
+        cls = 1;
+        if (WRITE) {
+          rid = W.w[2]; wid = W.w[3];
+          aux16 = pos - qstart;
+          if (q) route |= RTPS_ROUTE_HAS_QOS;
+          route |= RTPS_ROUTE_HAS_PAYLOAD;
+          uint32_t pl_off = body + pos, pl_len = blen - pos;
+          R.d[8] = (uint32_t)sn; R.d[9] = (uint32_t)((uint64_t)sn >> 32);
+          R.d[10] = pl_off | (pl_len << 16);
+          R.d[11] = frag_start;
+          R.d[12] = frags_in_sub | (frag_size << 16);
+          R.d[13] = data_size;
+        }
+        break;
+      }
+      case RTPS_HEARTBEAT: {  // Heartbeat (heartbeat.rs:21-49): 28 bytes
+        if (blen < 28u) return RTPS_DGRAM_SUBMSG_ERR;
+        cls = 1;
+        if (WRITE) {
+          rid = W.w[1]; wid = W.w[2];
+          int64_t first = sn_of(W.w[3], W.w[4], le), last = sn_of(W.w[5], W.w[6], le);
+          R.d[8] = (uint32_t)first; R.d[9] = (uint32_t)((uint64_t)first >> 32);
+          R.d[10] = (uint32_t)last; R.d[11] = (uint32_t)((uint64_t)last >> 32);
+          R.d[12] = e32(W.w[7], le);
+        }
+        break;
+      }
+      case RTPS_HEARTBEAT_FRAG: {  // HeartbeatFrag (heartbeat_frag.rs:16-37): 24 bytes
+        if (blen < 24u) return RTPS_DGRAM_SUBMSG_ERR;
+        cls = 1;
+        if (WRITE) {
+          rid = W.w[1]; wid = W.w[2];
+          int64_t sn = sn_of(W.w[3], W.w[4], le);
+          R.d[8] = (uint32_t)sn; R.d[9] = (uint32_t)((uint64_t)sn >> 32);
+          R.d[10] = e32(W.w[5], le);
+          R.d[11] = e32(W.w[6], le);
+        }
+        break;
+      }
+      case RTPS_GAP: {  // Gap (gap.rs:23-46): rid wid gapStart SNSet
+        if (blen < 28u) return RTPS_DGRAM_SUBMSG_ERR;
+        uint32_t nb = e32(W.w[7], le);
+        if (nb > 256u) return RTPS_DGRAM_SUBMSG_ERR;
+        uint32_t words = (nb + 31u) >> 5;
+        if (28u + 4u * words > blen) return RTPS_DGRAM_SUBMSG_ERR;
+        cls = 1;
+        if (WRITE) {
+          rid = W.w[1]; wid = W.w[2];
+          int64_t gs = sn_of(W.w[3], W.w[4], le), lb = sn_of(W.w[5], W.w[6], le);
+          R.d[8] = (uint32_t)gs; R.d[9] = (uint32_t)((uint64_t)gs >> 32);
+          R.d[10] = (uint32_t)lb; R.d[11] = (uint32_t)((uint64_t)lb >> 32);
+          R.d[12] = nb;
+          R.d[13] = body + 28u;
+        }
+        break;
+      }
+      case RTPS_ACKNACK: {  // AckNack (ack_nack.rs:27-50): rid wid SNSet count
+        if (blen < 20u) return RTPS_DGRAM_SUBMSG_ERR;
+        uint32_t nb = e32(W.w[5], le);
+        if (nb > 256u) return RTPS_DGRAM_SUBMSG_ERR;
+        uint32_t words = (nb + 31u) >> 5;
+        if (24u + 4u * words > blen) return RTPS_DGRAM_SUBMSG_ERR;
+        cls = 2;
+        if (WRITE) {
+          rid = W.w[1]; wid = W.w[2];
+          int64_t base = sn_of(W.w[3], W.w[4], le);
+          R.d[8] = (uint32_t)base; R.d[9] = (uint32_t)((uint64_t)base >> 32);
+          R.d[10] = e32(ld4(s, body + 20u + 4u * words), le);
+          R.d[12] = nb;
+          R.d[13] = body + 20u;
+        }
+        break;
+      }
+      case RTPS_NACK_FRAG: {  // NackFrag (nack_frag.rs:31-53): rid wid sn FNSet count
+        if (blen < 24u) return RTPS_DGRAM_SUBMSG_ERR;
+        uint32_t nb = e32(W.w[6], le);
+        if (nb > 256u) return RTPS_DGRAM_SUBMSG_ERR;
+        uint32_t words = (nb + 31u) >> 5;
+        if (28u + 4u * words > blen) return RTPS_DGRAM_SUBMSG_ERR;
+        cls = 2;
+        if (WRITE) {
+          rid = W.w[1]; wid = W.w[2];
+          int64_t sn = sn_of(W.w[3], W.w[4], le);
+          R.d[8] = (uint32_t)sn; R.d[9] = (uint32_t)((uint64_t)sn >> 32);
+          R.d[10] = e32(W.w[5], le);
+          R.d[11] = e32(ld4(s, body + 24u + 4u * words), le);
+          R.d[12] = nb;
+          R.d[13] = body + 24u;
+        }
+        break;
+      }
+      case RTPS_INFO_TS: {  // rtps/submessage.rs:211-225
+        cls = 3;
+        if (flags & 0x02u) { ts_valid = false; ts_sec = 0; ts_frac = 0; }
+        else {
+          if (blen < 8u) return RTPS_DGRAM_SUBMSG_ERR;
+          ts_valid = true; ts_sec = e32(W.w[1], le); ts_frac = e32(W.w[2], le);
+        }
+        if (WRITE) { R.d[2] = src0; R.d[3] = src1; R.d[4] = src2; }
+        break;
+      }
+      case RTPS_INFO_SRC: {  // InfoSource (info_source.rs:22-36); interpreter :626-636
+        if (blen < 20u) return RTPS_DGRAM_SUBMSG_ERR;
+        cls = 3;
+        src0 = W.w[3]; src1 = W.w[4]; src2 = W.w[5];
+        ts_valid = false; ts_sec = 0; ts_frac = 0;
+        if (WRITE) { R.d[2] = src0; R.d[3] = src1; R.d[4] = src2; R.d[10] = W.w[2]; }
+        break;
+      }
+      case RTPS_INFO_DST: {  // InfoDestination; interpreter :656-662
+        if (blen < 12u) return RTPS_DGRAM_SUBMSG_ERR;
+        cls = 3;
+        uint32_t a = W.w[1], b = W.w[2], c = W.w[3];
+        if ((a | b | c) == 0u) { dst0 = p.own0; dst1 = p.own1; dst2 = p.own2; }
+        else { dst0 = a; dst1 = b; dst2 = c; }
+        if (WRITE) { R.d[2] = a; R.d[3] = b; R.d[4] = c; }
+        break;
+      }
+      case RTPS_INFO_REPLY: {  // InfoReply (info_reply.rs:9-21): Vec<Locator> + Option<Vec<Locator>>
+        if (blen < 4u) return RTPS_DGRAM_SUBMSG_ERR;
+        uint32_t n1 = e32(W.w[1], le), n2 = 0xffffffffu;
+        uint64_t pos = 4u + 24ull * n1;
+        if (pos > blen) return RTPS_DGRAM_SUBMSG_ERR;
+        if (pos + 1u > blen) return RTPS_DGRAM_SUBMSG_ERR;
+        uint32_t tag = ld4(s, body + (uint32_t)pos) & 0xffu;
+        pos += 1u;
+        if (tag != 0u) {
+          if (pos + 4u > blen) return RTPS_DGRAM_SUBMSG_ERR;
+          n2 = e32(ld4(s, body + (uint32_t)pos), le);
+          pos += 4u;
+          if (pos + 24ull * n2 > blen) return RTPS_DGRAM_SUBMSG_ERR;
+        }
+        cls = 3;
+        if (WRITE) { R.d[2] = src0; R.d[3] = src1; R.d[4] = src2; R.d[10] = n1; R.d[11] = n2; }
+        break;
+      }
+      default:  // PAD, INFO_REPLY_IP4, SEC_*, vendor and unknown kinds: skipped (:233-235, :278-293)
+        emit = false;
+        break;
+    }
+
+    if (emit) {
+      if (WRITE) {
+        if (cls != 3) {
+          R.d[2] = src0; R.d[3] = src1; R.d[4] = src2;
+          R.d[5] = wid; R.d[6] = rid;
+          if (cls == 1) {  // SubmessageIter2::next writer filter (message_receiver.rs:75-84)
+            bool own = dst0 == p.own0 && dst1 == p.own1 && dst2 == p.own2;
+            bool unk = (dst0 | dst1 | dst2) == 0u;
+            if (own || unk) route |= RTPS_ROUTE_PASS;
+            if (builtin_writer_pair(rid, wid)) route |= RTPS_ROUTE_BUILTIN;
+            else {
+              mslot = match_lookup(p, src0, src1, src2, wid);
+              if (mslot != RTPS_NO_MATCH) route |= RTPS_ROUTE_MATCHED;
+            }
+          } else {
+            route |= RTPS_ROUTE_PASS;
+            if (builtin_reader_pair(rid, wid)) route |= RTPS_ROUTE_BUILTIN;
+          }
+        }
+        if (ts_valid) { route |= RTPS_ROUTE_TS_VALID; R.d[14] = ts_sec; R.d[15] = ts_frac; }
+        R.d[7] = (aux16 & 0xffffu) | (route << 16) | (pk << 24);
+        uint64_t r = ridx + nrec;
+        if (r < p.max_records) {
+          rec_store(p.records + r, R);
+          if (p.match_out) p.match_out[r] = mslot;
+        }
+      }
+      nrec++;
+    }
+    o = next;
+  }
+  return RTPS_DGRAM_OK;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, uint32_t lane) {
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  return x;
+}
+
+// Decoupled look-back over tiles (single pass, ordered output).  Tile states
+// are 8-byte {flag:2, value:62} granules written by single agent-scope
+// atomic stores and polled by relaxed agent-scope loads (an untorn granule
+// needs no fence: MI355X_MICROARCH.md, visibility R2).  Tickets come from an
+// atomic counter, so every tile a tile waits on is already resident.
+__device__ uint64_t lookback(uint64_t* states, uint32_t tile, uint64_t agg, uint64_t* timeouts) {
+  if (tile == 0) {
+    __hip_atomic_store(&states[0], FLAG_INC | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return 0;
+  }
+  __hip_atomic_store(&states[tile], FLAG_AGG | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint64_t excl = 0;
+  int64_t t = (int64_t)tile - 1;
+  uint32_t spins = 0;
+  while (t >= 0) {
+    uint64_t v = __hip_atomic_load(&states[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t f = v & ~VAL_MASK;
+    if (f == 0) {
+      if (++spins > (1u << 24)) {  // never expected; bounded so the grid always drains
+        atomicAdd(reinterpret_cast<unsigned long long*>(timeouts), 1ull);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    excl += v & VAL_MASK;
+    if (f == FLAG_INC) break;
+    --t;
+  }
+  __hip_atomic_store(&states[tile], FLAG_INC | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return excl;
+}
+
+__global__ __launch_bounds__(TILE) void rtps_parse_kernel(KParams p) {
+  __shared__ uint32_t s_tile;
+  __shared__ uint64_t s_min_off, s_base_rec;
+  __shared__ uint32_t s_wave_sum[WAVES];
+
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  uint64_t* states = p.scratch + 2;
+  if (tid == 0) {
+    s_tile = atomicAdd(reinterpret_cast<unsigned int*>(p.scratch), 1u);
+    s_min_off = ~0ull;
+  }
+  __syncthreads();
+  const uint32_t tile = s_tile;
+  const uint32_t i = tile * TILE + tid;
+  const bool valid = i < p.n;
+  uint64_t off = valid ? p.dgram_off[i] : ~0ull;
+  uint32_t L = valid ? p.dgram_len[i] : 0u;
+
+  // tile base for the buffer descriptor: min offset over the tile
+  uint64_t m = off;
+#pragma unroll
+  for (uint32_t d = 32; d >= 1; d >>= 1) {
+    uint64_t y = __shfl_xor(m, d, 64);
+    m = y < m ? y : m;
+  }
+  if (lane == 0) atomicMin(reinterpret_cast<unsigned long long*>(&s_min_off), (unsigned long long)m);
+  __syncthreads();
+  uint64_t tb = s_min_off;
+  if (tb > p.arena_len) tb = p.arena_len;
+  uint64_t avail64 = p.arena_len - tb;
+  uint32_t avail = avail64 > 0xffffffffull ? 0xffffffffu : (uint32_t)avail64;
+  uint32_t tb_lo = __builtin_amdgcn_readfirstlane((uint32_t)tb);
+  uint32_t tb_hi = __builtin_amdgcn_readfirstlane((uint32_t)(tb >> 32));
+  avail = __builtin_amdgcn_readfirstlane(avail);
+  const uint8_t* tbase = p.arena + (((uint64_t)tb_hi << 32) | tb_lo);
+  Src s;
+  s.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(tbase), (short)0, (int)avail, 0x00020000);
+  s.avail = avail;
+  uint64_t rel = valid ? off - tb : 0;
+  bool addressable = valid && off <= p.arena_len && (uint64_t)L <= p.arena_len - off && rel + L <= avail;
+  s.base = (uint32_t)rel;
+
+  // walk 1: status + count
+  uint32_t cnt = 0, st = RTPS_DGRAM_OK;
+  if (valid) {
+    if (!addressable) st = RTPS_DGRAM_TOO_LONG;
+    else st = walk<false>(p, s, L, i, 0, cnt);
+    if (st != RTPS_DGRAM_OK) cnt = 0;
+  }
+
+  // tile scan
+  uint32_t incl = wave_incl_scan(cnt, lane);
+  if (lane == 63) s_wave_sum[wave] = incl;
+  __syncthreads();
+  uint32_t wave_off = 0, agg = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < WAVES; ++w) {
+    uint32_t v = s_wave_sum[w];
+    if (w < wave) wave_off += v;
+    agg += v;
+  }
+  if (tid == 0) {
+    uint64_t excl = lookback(states, tile, agg, p.scratch + 1);
+    s_base_rec = excl;
+    if (tile == gridDim.x - 1) *p.n_records = excl + agg;
+  }
+  __syncthreads();
+  const uint64_t my_first = s_base_rec + wave_off + (incl - cnt);
+
+  if (valid) {
+    p.status[i] = (uint8_t)st;
+    if (p.rec_begin) p.rec_begin[i] = (uint32_t)my_first;
+    if (st == RTPS_DGRAM_OK && cnt) {
+      uint32_t n2 = 0;
+      walk<true>(p, s, L, i, my_first, n2);
+    }
+  }
+}
+
+// device-side synthetic generator: one lane per datagram
+__global__ void rtps_gen_kernel(int wl, uint64_t seed, uint64_t first_idx, uint32_t n_writers,
+                                uint8_t* arena, const uint64_t* off, uint32_t n) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) rtps_gen_datagram(wl, seed, first_idx + i, n_writers, arena + off[i]);
+}
+
+
+// ---------------------------------------------------------------------------
+// writer-GUID sharding for >= 2 GPUs: stable partition of
+// the writer/reader-kind records by owner = guid_hash(prefix || writer_id) %
+// n_dest.  Three launches: per-tile histogram, per-destination scan over
+// tiles, stable scatter (wave ballots keep input order inside a bucket).
+// ---------------------------------------------------------------------------
+constexpr uint32_t MAX_DEST = 64;
+
+__device__ __forceinline__ uint32_t owner_of(const rtps_record* r, uint32_t n_dest) {
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(r);
+  uint32_t kind = (d[1] >> 16) & 0xffu;
+  bool exch = kind == RTPS_DATA || kind == RTPS_DATA_FRAG || kind == RTPS_HEARTBEAT || kind == RTPS_GAP ||
+              kind == RTPS_HEARTBEAT_FRAG || kind == RTPS_ACKNACK || kind == RTPS_NACK_FRAG;
+  if (!exch) return 0xffffffffu;
+  return guid_hash(d[2], d[3], d[4], d[5]) % n_dest;
+}
+
+__global__ __launch_bounds__(TILE) void bucket_hist_kernel(const rtps_record* recs, const uint64_t* n_rec,
+                                                            uint32_t n_dest, uint32_t* hist) {
+  __shared__ uint32_t h[MAX_DEST];
+  if (threadIdx.x < n_dest) h[threadIdx.x] = 0;
+  __syncthreads();
+  uint64_t i = (uint64_t)blockIdx.x * TILE + threadIdx.x;
+  if (i < *n_rec) {
+    uint32_t o = owner_of(recs + i, n_dest);
+    if (o != 0xffffffffu) atomicAdd(&h[o], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < n_dest) hist[(uint64_t)blockIdx.x * n_dest + threadIdx.x] = h[threadIdx.x];
+}
+
+// one workgroup: exclusive scan of hist[t][d] over t for every d, then add the
+// bucket bases (exclusive scan of the per-destination totals)
+__global__ __launch_bounds__(TILE) void bucket_scan_kernel(uint32_t* hist, uint32_t tiles, uint32_t n_dest,
+                                                            uint64_t* dest_counts) {
+  __shared__ uint32_t part[TILE];
+  __shared__ uint32_t totals[MAX_DEST];
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t d = 0; d < n_dest; ++d) {
+    uint32_t carry = 0;
+    for (uint32_t t0 = 0; t0 < tiles; t0 += TILE) {
+      uint32_t t = t0 + tid;
+      uint32_t v = t < tiles ? hist[(uint64_t)t * n_dest + d] : 0u;
+      part[tid] = v;
+      __syncthreads();
+      for (uint32_t k = 1; k < TILE; k <<= 1) {  // Hillis-Steele inclusive scan
+        uint32_t y = tid >= k ? part[tid - k] : 0u;
+        __syncthreads();
+        part[tid] += y;
+        __syncthreads();
+      }
+      if (t < tiles) hist[(uint64_t)t * n_dest + d] = carry + part[tid] - v;
+      carry += part[TILE - 1];
+      __syncthreads();
+    }
+    if (tid == 0) totals[d] = carry;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    uint32_t acc = 0;
+    for (uint32_t d = 0; d < n_dest; ++d) { dest_counts[d] = totals[d]; uint32_t t = totals[d]; totals[d] = acc; acc += t; }
+  }
+  __syncthreads();
+  for (uint64_t k = tid; k < (uint64_t)tiles * n_dest; k += TILE) hist[k] += totals[k % n_dest];
+}
+
+__global__ __launch_bounds__(TILE) void bucket_scatter_kernel(const rtps_record* recs, const uint64_t* n_rec,
+                                                               uint32_t n_dest, const uint32_t* offs,
+                                                               rtps_record* out) {
+  __shared__ uint32_t wcnt[WAVES][MAX_DEST];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  uint64_t i = (uint64_t)blockIdx.x * TILE + tid;
+  uint32_t o = (i < *n_rec) ? owner_of(recs + i, n_dest) : 0xffffffffu;
+  uint32_t rank = 0;
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64u - lane));
+  for (uint32_t d = 0; d < n_dest; ++d) {
+    uint64_t m = __ballot(o == d);
+    if (o == d) rank = (uint32_t)__popcll(m & lt);
+    if (lane == 0) wcnt[wave][d] = (uint32_t)__popcll(m);
+  }
+  __syncthreads();
+  if (o != 0xffffffffu) {
+    uint32_t before = 0;
+    for (uint32_t w = 0; w < wave; ++w) before += wcnt[w][o];
+    uint64_t dst = (uint64_t)offs[(uint64_t)blockIdx.x * n_dest + o] + before + rank;
+    const u32x4* src = reinterpret_cast<const u32x4*>(recs + i);
+    u32x4* dp = reinterpret_cast<u32x4*>(out + dst);
+    u32x4 a = src[0], b = src[1], c = src[2], e = src[3];
+    dp[0] = a; dp[1] = b; dp[2] = c; dp[3] = e;
+  }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+struct rtps_rx_ctx {
+  int device = 0;
+  uint8_t own[12] = {0};
+  uint32_t max_datagrams = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  uint64_t* scratch = nullptr;  // ticket, timeouts, tile states
+  size_t scratch_words = 0;
+  u32x4* mt_keys = nullptr;
+  uint16_t* mt_slots = nullptr;
+  uint32_t mt_cap = 0;
+  bool mt_active = false;
+  uint32_t* bucket_hist = nullptr;
+  size_t bucket_bytes = 0;
+};
+
+static int hip_fail(hipError_t e) { return e == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP; }
+
+extern "C" {
+
+int rtps_rx_create(const rtps_rx_config* cfg, rtps_rx_ctx** out_ctx) {
+  if (!cfg || !out_ctx) return RTPS_RX_EINVAL;
+  if (cfg->abi_version != RTPS_RX_ABI_VERSION) return RTPS_RX_EABI;
+  rtps_rx_ctx* c = new (std::nothrow) rtps_rx_ctx();
+  if (!c) return RTPS_RX_ENOMEM;
+  c->device = cfg->device;
+  memcpy(c->own, cfg->own_prefix, 12);
+  c->max_datagrams = cfg->max_datagrams;
+  if (hipSetDevice(c->device) != hipSuccess) { delete c; return RTPS_RX_EHIP; }
+  if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) { delete c; return RTPS_RX_EHIP; }
+  c->stream = c->own_stream;
+  size_t tiles = ((size_t)cfg->max_datagrams + TILE - 1) / TILE;
+  c->scratch_words = 2 + (tiles ? tiles : 1);
+  c->scratch_words = (c->scratch_words + 1) & ~(size_t)1;  // 16-B multiple for the memset
+  if (hipMalloc(&c->scratch, c->scratch_words * sizeof(uint64_t)) != hipSuccess) {
+    (void)hipStreamDestroy(c->own_stream);
+    delete c;
+    return RTPS_RX_ENOMEM;
+  }
+  *out_ctx = c;
+  return RTPS_RX_OK;
+}
+
+int rtps_rx_destroy(rtps_rx_ctx* c) {
+  if (!c) return RTPS_RX_EINVAL;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  (void)hipFree(c->scratch);
+  (void)hipFree(c->mt_keys);
+  (void)hipFree(c->mt_slots);
+  (void)hipFree(c->bucket_hist);
+  (void)hipStreamDestroy(c->own_stream);
+  delete c;
+  return RTPS_RX_OK;
+}
+
+int rtps_rx_set_stream(rtps_rx_ctx* c, void* s) {
+  if (!c) return RTPS_RX_EINVAL;
+  c->stream = s ? (hipStream_t)s : c->own_stream;
+  return RTPS_RX_OK;
+}
+
+static uint32_t host_guid_hash(const uint8_t g[16]) {
+  uint32_t w[4];
+  memcpy(w, g, 16);
+  uint32_t h = 0x811c9dc5u;
+  for (int k = 0; k < 4; ++k) h = (h ^ w[k]) * 0x01000193u;
+  return h ^ (h >> 15);
+}
+
+int rtps_rx_set_match_table(rtps_rx_ctx* c, const rtps_match* t, uint32_t n) {
+  if (!c || (n && !t)) return RTPS_RX_EINVAL;
+  (void)hipSetDevice(c->device);
+  if (n == 0) { c->mt_active = false; return RTPS_RX_OK; }
+  uint32_t cap = 16;
+  while (cap < 2u * n) cap <<= 1;
+  std::vector<u32x4> keys(cap, u32x4{0u, 0u, 0u, 0u});
+  std::vector<uint16_t> slots(cap, (uint16_t)RTPS_NO_MATCH);
+  for (uint32_t k = 0; k < n; ++k) {  // first entry wins on duplicates (oracle: linear scan)
+    if (t[k].reader_slot == RTPS_NO_MATCH) return RTPS_RX_EINVAL;
+    uint32_t w[4];
+    memcpy(w, t[k].writer_guid, 16);
+    uint32_t i = host_guid_hash(t[k].writer_guid) & (cap - 1);
+    for (;;) {
+      if (slots[i] == RTPS_NO_MATCH) { keys[i] = u32x4{w[0], w[1], w[2], w[3]}; slots[i] = t[k].reader_slot; break; }
+      if (keys[i][0] == w[0] && keys[i][1] == w[1] && keys[i][2] == w[2] && keys[i][3] == w[3]) break;
+      i = (i + 1) & (cap - 1);
+    }
+  }
+  if (hipStreamSynchronize(c->stream) != hipSuccess) return RTPS_RX_EHIP;
+  if (cap > c->mt_cap) {
+    (void)hipFree(c->mt_keys);
+    (void)hipFree(c->mt_slots);
+    c->mt_keys = nullptr; c->mt_slots = nullptr; c->mt_cap = 0;
+    if (hipMalloc(&c->mt_keys, cap * sizeof(u32x4)) != hipSuccess) return RTPS_RX_ENOMEM;
+    if (hipMalloc(&c->mt_slots, cap * sizeof(uint16_t)) != hipSuccess) return RTPS_RX_ENOMEM;
+    c->mt_cap = cap;
+  }
+  // keep the device table's capacity == cap (mask) by writing a full-size image
+  if (hipMemcpy(c->mt_keys, keys.data(), cap * sizeof(u32x4), hipMemcpyHostToDevice) != hipSuccess) return RTPS_RX_EHIP;
+  if (hipMemcpy(c->mt_slots, slots.data(), cap * sizeof(uint16_t), hipMemcpyHostToDevice) != hipSuccess) return RTPS_RX_EHIP;
+  c->mt_active = true;
+  c->mt_cap = cap;
+  return RTPS_RX_OK;
+}
+
+int rtps_rx_parse_batch(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len, const uint64_t* dgram_off,
+                        const uint32_t* dgram_len, uint32_t n, const rtps_rx_out* out) {
+  if (!c || !out || !out->status || !out->records || !out->n_records) return RTPS_RX_EINVAL;
+  if (n && (!arena || !dgram_off || !dgram_len)) return RTPS_RX_EINVAL;
+  if (n > c->max_datagrams) return RTPS_RX_ETOOBIG;
+  (void)hipSetDevice(c->device);
+  if (n == 0) return hip_fail(hipMemsetAsync(out->n_records, 0, sizeof(uint64_t), c->stream));
+  uint32_t tiles = (n + TILE - 1) / TILE;
+  // zero ticket + timeout + tile states (one contiguous block, 16-B multiple)
+  size_t words = (2 + (size_t)tiles + 1) & ~(size_t)1;
+  hipError_t e = hipMemsetAsync(c->scratch, 0, words * sizeof(uint64_t), c->stream);
+  if (e != hipSuccess) return RTPS_RX_EHIP;
+  KParams p;
+  p.arena = arena;
+  p.arena_len = arena_len;
+  p.dgram_off = dgram_off;
+  p.dgram_len = dgram_len;
+  p.n = n;
+  memcpy(&p.own0, c->own + 0, 4);
+  memcpy(&p.own1, c->own + 4, 4);
+  memcpy(&p.own2, c->own + 8, 4);
+  p.status = out->status;
+  p.records = out->records;
+  p.max_records = out->max_records;
+  p.match_out = out->match;
+  p.rec_begin = out->rec_begin;
+  p.n_records = out->n_records;
+  p.mt_keys = c->mt_active ? c->mt_keys : nullptr;
+  p.mt_slots = c->mt_slots;
+  p.mt_mask = c->mt_active ? c->mt_cap - 1 : 0;
+  p.scratch = c->scratch;
+  hipLaunchKernelGGL(rtps_parse_kernel, dim3(tiles), dim3(TILE), 0, c->stream, p);
+  return hip_fail(hipGetLastError());
+}
+
+int rtps_rx_sync(rtps_rx_ctx* c) {
+  if (!c) return RTPS_RX_EINVAL;
+  return hip_fail(hipStreamSynchronize(c->stream));
+}
+
+const char* rtps_rx_strerror(int code) {
+  switch (code) {
+    case RTPS_RX_OK: return "ok";
+    case RTPS_RX_EINVAL: return "invalid argument";
+    case RTPS_RX_EHIP: return "HIP runtime error";
+    case RTPS_RX_ENOMEM: return "out of device memory";
+    case RTPS_RX_ETOOBIG: return "batch larger than the context's max_datagrams";
+    case RTPS_RX_EABI: return "ABI version mismatch";
+    default: return "unknown error";
+  }
+}
+
+uint64_t rtps_rx_max_records_host(const uint32_t* len, uint32_t n) {
+  uint64_t t = 0;
+  for (uint32_t i = 0; i < n; ++i)
+    if (len[i] >= 20 && len[i] <= RTPS_MAX_DATAGRAM) t += (len[i] - 20) / 4;
+  return t;
+}
+
+int rtps_rx_generate(rtps_rx_ctx* c, int wl, uint64_t seed, uint64_t first_idx, uint32_t n_writers,
+                     uint8_t* arena, const uint64_t* off, const uint32_t* len, uint32_t n) {
+  (void)len;
+  if (!c || (n && (!arena || !off))) return RTPS_RX_EINVAL;
+  if (wl < 1 || wl > 4) return RTPS_RX_EINVAL;
+  if (n == 0) return RTPS_RX_OK;
+  (void)hipSetDevice(c->device);
+  hipLaunchKernelGGL(rtps_gen_kernel, dim3((n + 255) / 256), dim3(256), 0, c->stream, wl, seed, first_idx,
+                     n_writers, arena, off, n);
+  return hip_fail(hipGetLastError());
+}
+
+/* host copy of the generator's layout (same f(seed, idx) as the device kernel) */
+uint64_t rtps_rx_gen_layout_host(int wl, uint64_t seed, uint64_t first_idx, uint32_t n_writers, uint32_t n,
+                                 uint64_t* off, uint32_t* len) {
+  return rtps_gen_layout_host(wl, seed, first_idx, n_writers, n, off, len);
+}
+
+
+int rtps_rx_bucket_by_writer(rtps_rx_ctx* c, const rtps_record* recs, const uint64_t* n_records,
+                             uint64_t max_records, uint32_t n_dest, rtps_record* out, uint64_t* dest_counts) {
+  if (!c || !recs || !n_records || !out || !dest_counts || n_dest < 1 || n_dest > MAX_DEST) return RTPS_RX_EINVAL;
+  (void)hipSetDevice(c->device);
+  uint64_t tiles64 = (max_records + TILE - 1) / TILE;
+  if (tiles64 == 0) return hip_fail(hipMemsetAsync(dest_counts, 0, n_dest * sizeof(uint64_t), c->stream));
+  if (tiles64 > 0xffffffffull) return RTPS_RX_ETOOBIG;
+  uint32_t tiles = (uint32_t)tiles64;
+  size_t need = (size_t)tiles * n_dest * sizeof(uint32_t);
+  if (need > c->bucket_bytes) {
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipFree(c->bucket_hist);
+    c->bucket_hist = nullptr; c->bucket_bytes = 0;
+    if (hipMalloc(&c->bucket_hist, need) != hipSuccess) return RTPS_RX_ENOMEM;
+    c->bucket_bytes = need;
+  }
+  hipLaunchKernelGGL(bucket_hist_kernel, dim3(tiles), dim3(TILE), 0, c->stream, recs, n_records, n_dest, c->bucket_hist);
+  hipLaunchKernelGGL(bucket_scan_kernel, dim3(1), dim3(TILE), 0, c->stream, c->bucket_hist, tiles, n_dest, dest_counts);
+  hipLaunchKernelGGL(bucket_scatter_kernel, dim3(tiles), dim3(TILE), 0, c->stream, recs, n_records, n_dest,
+                     c->bucket_hist, out);
+  return hip_fail(hipGetLastError());
+}
+
+uint32_t rtps_rx_record_size(void) { return (uint32_t)sizeof(rtps_record); }
+
+}  // extern "C"

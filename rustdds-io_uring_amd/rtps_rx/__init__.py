@@ -1,0 +1,224 @@
+"""Python host side of the MI355X RTPS receive-path parser.
+
+Binds the C ABI of include/rtps_rx.h (librtps_rx.so, built from csrc/) with
+ctypes; torch provides device memory and streams (plumbing only).  The
+object model mirrors the reference's receive path:
+
+  MessageReceiver(own_guid_prefix)         io_uring/rtps/message_receiver.rs:158-182
+  .handle_received_batch(...)              batch form of handle_received_packet_2 (:232-287)
+  BatchResult.passed_submessages(i)        SubmessageIter2::next -> PassedSubmessage (:56-119)
+
+There is no CPU fallback: if the shared library (or a GPU) is missing the
+constructor raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from .records import (RECORD_DTYPE, MATCH_DTYPE, STATUS_NAMES, KIND_NAMES, WRITER_KINDS, READER_KINDS,
+                      ROUTE_PASS, NO_MATCH, max_records, record_to_dict, pack_match_table)
+
+_PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_PKG_DIR), "librtps_rx.so")
+ABI_VERSION = 1
+
+WL_T, WL_C2, WL_C3, WL_C4 = 1, 2, 3, 4
+WORKLOADS = {"T": WL_T, "C2": WL_C2, "C3": WL_C3, "C4": WL_C4}
+SEED = 0x52545053
+
+_lib = None
+
+
+class RtpsRxError(RuntimeError):
+    pass
+
+
+class _Config(ctypes.Structure):
+    _fields_ = [("abi_version", ctypes.c_uint32), ("device", ctypes.c_int32),
+                ("own_prefix", ctypes.c_uint8 * 12), ("max_datagrams", ctypes.c_uint32),
+                ("flags", ctypes.c_uint32)]
+
+
+class _Out(ctypes.Structure):
+    _fields_ = [("status", ctypes.c_void_p), ("records", ctypes.c_void_p), ("max_records", ctypes.c_uint64),
+                ("match", ctypes.c_void_p), ("rec_begin", ctypes.c_void_p), ("n_records", ctypes.c_void_p)]
+
+
+EXPORTS = ["rtps_rx_create", "rtps_rx_destroy", "rtps_rx_set_stream", "rtps_rx_set_match_table",
+           "rtps_rx_parse_batch", "rtps_rx_sync", "rtps_rx_strerror", "rtps_rx_max_records_host",
+           "rtps_rx_generate", "rtps_rx_bucket_by_writer"]
+
+
+def lib():
+    """Load librtps_rx.so (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RtpsRxError(f"{LIB_PATH} missing: run __graft_entry__.build() (make -C csrc)")
+        L = ctypes.CDLL(LIB_PATH)
+        P, U32, U64, I = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+        L.rtps_rx_create.argtypes = [ctypes.POINTER(_Config), ctypes.POINTER(P)]
+        L.rtps_rx_destroy.argtypes = [P]
+        L.rtps_rx_set_stream.argtypes = [P, P]
+        L.rtps_rx_set_match_table.argtypes = [P, P, U32]
+        L.rtps_rx_parse_batch.argtypes = [P, P, U64, P, P, U32, ctypes.POINTER(_Out)]
+        L.rtps_rx_sync.argtypes = [P]
+        L.rtps_rx_strerror.argtypes = [I]
+        L.rtps_rx_strerror.restype = ctypes.c_char_p
+        L.rtps_rx_max_records_host.argtypes = [P, U32]
+        L.rtps_rx_max_records_host.restype = U64
+        L.rtps_rx_generate.argtypes = [P, I, U64, U64, U32, P, P, P, U32]
+        L.rtps_rx_gen_layout_host.argtypes = [I, U64, U64, U32, U32, P, P]
+        L.rtps_rx_gen_layout_host.restype = U64
+        L.rtps_rx_record_size.restype = U32
+        L.rtps_rx_bucket_by_writer.argtypes = [P, P, P, U64, U32, P, P]
+        L.rtps_rx_bucket_by_writer.restype = I
+        for fn in ("rtps_rx_create", "rtps_rx_destroy", "rtps_rx_set_stream", "rtps_rx_set_match_table",
+                   "rtps_rx_parse_batch", "rtps_rx_sync", "rtps_rx_generate"):
+            getattr(L, fn).restype = I
+        assert L.rtps_rx_record_size() == RECORD_DTYPE.itemsize
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise RtpsRxError(lib().rtps_rx_strerror(rc).decode())
+
+
+def gen_layout(workload, n, seed=SEED, first_idx=0, n_writers=16):
+    """Host layout of the synthetic generator: (off u64[n], len u32[n], arena_bytes)."""
+    off = np.zeros(n, dtype=np.uint64)
+    ln = np.zeros(n, dtype=np.uint32)
+    size = lib().rtps_rx_gen_layout_host(workload, seed, first_idx, n_writers, n, off.ctypes.data, ln.ctypes.data)
+    return off, ln, int(size)
+
+
+class BatchResult:
+    """Host copies of one batch's outputs (status, records, match, rec_begin)."""
+
+    def __init__(self, status, records, match, rec_begin, n_records):
+        self.status = status
+        self.records = records
+        self.match = match
+        self.rec_begin = rec_begin
+        self.n_records = n_records
+
+    def submessages(self, i):
+        """All materialised submessages of datagram i (Message.submessages order)."""
+        if self.status[i] != 0:
+            return self.records[0:0]
+        lo = int(self.rec_begin[i])
+        hi = int(self.rec_begin[i + 1]) if i + 1 < len(self.rec_begin) else self.n_records
+        return self.records[lo:hi]
+
+    def passed_submessages(self, i):
+        """What SubmessageIter2::next yields for datagram i: writer/reader submessages with PASS."""
+        r = self.submessages(i)
+        return r[(r["route"] & ROUTE_PASS) != 0]
+
+
+class MessageReceiver:
+    """Batch receive-path parser bound to one GPU (one context = one stream)."""
+
+    def __init__(self, own_guid_prefix, device=0, max_datagrams=1 << 20):
+        import torch  # noqa: F401  (device memory / streams)
+        if not torch.cuda.is_available():
+            raise RtpsRxError("no GPU visible: the RTPS parser has no CPU fallback")
+        cfg = _Config()
+        cfg.abi_version = ABI_VERSION
+        cfg.device = device
+        own = bytes(own_guid_prefix)
+        assert len(own) == 12
+        for k in range(12):
+            cfg.own_prefix[k] = own[k]
+        cfg.max_datagrams = max_datagrams
+        cfg.flags = 0
+        h = ctypes.c_void_p()
+        _check(lib().rtps_rx_create(ctypes.byref(cfg), ctypes.byref(h)))
+        self._h = h
+        self.device = device
+        self.max_datagrams = max_datagrams
+        self.own_guid_prefix = own
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().rtps_rx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream):
+        """Launch on a torch.cuda.Stream (None = the context's own stream)."""
+        _check(lib().rtps_rx_set_stream(self._h, None if stream is None else ctypes.c_void_p(stream.cuda_stream)))
+
+    def set_match_table(self, entries):
+        """entries: MATCH_DTYPE array or iterable of (writer_guid bytes[16], reader_slot)."""
+        t = entries if isinstance(entries, np.ndarray) else pack_match_table(entries)
+        t = np.ascontiguousarray(t, dtype=MATCH_DTYPE)
+        _check(lib().rtps_rx_set_match_table(self._h, t.ctypes.data if len(t) else None, len(t)))
+
+    def sync(self):
+        _check(lib().rtps_rx_sync(self._h))
+
+    # ---- device-resident batch API (hot path) ----
+    def alloc_outputs(self, n, max_recs):
+        import torch
+        dev = torch.device("cuda", self.device)
+        return {
+            "status": torch.empty(max(n, 1), dtype=torch.uint8, device=dev),
+            "records": torch.empty((max(max_recs, 1), RECORD_DTYPE.itemsize), dtype=torch.uint8, device=dev),
+            "match": torch.empty(max(max_recs, 1), dtype=torch.int16, device=dev),
+            "rec_begin": torch.empty(max(n, 1), dtype=torch.int32, device=dev),
+            "n_records": torch.zeros(1, dtype=torch.int64, device=dev),
+            "max_records": max_recs,
+        }
+
+    def parse_batch_device(self, arena, off, lens, n, outs, want_match=True, want_rec_begin=True):
+        """arena u8 / off i64 / lens i32 torch CUDA tensors; asynchronous."""
+        o = _Out()
+        o.status = outs["status"].data_ptr()
+        o.records = outs["records"].data_ptr()
+        o.max_records = outs["max_records"]
+        o.match = outs["match"].data_ptr() if want_match else None
+        o.rec_begin = outs["rec_begin"].data_ptr() if want_rec_begin else None
+        o.n_records = outs["n_records"].data_ptr()
+        _check(lib().rtps_rx_parse_batch(self._h, arena.data_ptr(), arena.numel(), off.data_ptr(),
+                                         lens.data_ptr(), n, ctypes.byref(o)))
+
+    def generate(self, workload, arena, off, lens, n, seed=SEED, first_idx=0, n_writers=16):
+        """Fill device arena with datagrams [first_idx, first_idx+n) of a synthetic workload."""
+        _check(lib().rtps_rx_generate(self._h, workload, seed, first_idx, n_writers, arena.data_ptr(),
+                                      off.data_ptr(), lens.data_ptr(), n))
+
+    def bucket_by_writer(self, outs, n_dest, out_records, dest_counts):
+        """Stable partition of outs["records"] by owner GPU (writer-GUID hash % n_dest); asynchronous."""
+        _check(lib().rtps_rx_bucket_by_writer(self._h, outs["records"].data_ptr(), outs["n_records"].data_ptr(),
+                                              outs["max_records"], n_dest, out_records.data_ptr(),
+                                              dest_counts.data_ptr()))
+
+    # ---- convenience: host datagrams in, host results out ----
+    def handle_received_batch(self, arena_np, off_np, len_np):
+        """Parse host arrays on the GPU (H2D copy, parse, D2H copy) -> BatchResult."""
+        import torch
+        n = len(len_np)
+        dev = torch.device("cuda", self.device)
+        arena = torch.from_numpy(np.ascontiguousarray(arena_np, dtype=np.uint8)).to(dev)
+        off = torch.from_numpy(np.ascontiguousarray(off_np, dtype=np.uint64).view(np.int64)).to(dev)
+        lens = torch.from_numpy(np.ascontiguousarray(len_np, dtype=np.uint32).view(np.int32)).to(dev)
+        cap = max_records(len_np)
+        outs = self.alloc_outputs(n, cap)
+        torch.cuda.synchronize(dev)
+        self.parse_batch_device(arena, off, lens, n, outs)
+        self.sync()
+        total = int(outs["n_records"].item())
+        kept = min(total, cap)
+        recs = outs["records"][:kept].cpu().numpy().reshape(-1).view(RECORD_DTYPE)
+        match = outs["match"][:kept].cpu().numpy().view(np.uint16)
+        return BatchResult(outs["status"][:n].cpu().numpy(), recs, match,
+                           outs["rec_begin"][:n].cpu().numpy().view(np.uint32), total)

@@ -1,0 +1,232 @@
+"""GPU parity: the HIP parser (through the C ABI) vs the CPU oracle, bit-exact.
+
+Every record byte, every status byte, the match slots, rec_begin and the
+record count must be identical.  Inputs: the reference's golden vectors,
+the four synthetic BASELINE workloads (generated on the device and copied
+back for the oracle), misaligned packing, byte-flip fuzz, edge cases
+(empty batch, 64 KiB datagrams, max-records datagrams, arena tail), and the
+full 1M-datagram configs.
+"""
+import struct
+
+import numpy as np
+import pytest
+
+import oracle
+from golden_cases import cases, check_case, shape_type_from_payload
+from rtps_rx.records import record_to_dict, RECORD_DTYPE, DGRAM_OK, DATA, max_records
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def rx():
+    import rtps_rx
+    r = rtps_rx.MessageReceiver(oracle.OWN_PREFIX, max_datagrams=1 << 21)
+    yield r
+    r.close()
+
+
+def _assert_same(gpu, ora, label):
+    st, recs, match, rb = ora
+    assert np.array_equal(gpu.status, st), f"{label}: status differs at {np.nonzero(gpu.status != st)[0][:10]}"
+    assert gpu.n_records == len(recs), f"{label}: {gpu.n_records} records vs oracle {len(recs)}"
+    g = gpu.records.view(np.uint8).reshape(-1, 64)
+    o = recs.view(np.uint8).reshape(-1, 64)
+    if not np.array_equal(g, o):
+        bad = np.nonzero((g != o).any(axis=1))[0]
+        i = int(bad[0])
+        raise AssertionError(f"{label}: {len(bad)} records differ; first #{i}: gpu {record_to_dict(gpu.records[i])}"
+                             f" oracle {record_to_dict(recs[i])}")
+    assert np.array_equal(gpu.match, match), f"{label}: match slots differ"
+    assert np.array_equal(gpu.rec_begin, rb), f"{label}: rec_begin differs"
+
+
+def _parity(rx, arena, off, ln, label, own=None, table=None):
+    if table is not None:
+        rx.set_match_table(table)
+    try:
+        gpu = rx.handle_received_batch(arena, off, ln)
+        ora = oracle.parse(arena, off, ln, own=own or oracle.OWN_PREFIX, match_table=table, threads=8)
+    finally:
+        if table is not None:
+            rx.set_match_table([])
+    _assert_same(gpu, ora, label)
+    return gpu
+
+
+def test_golden_vectors(rx):
+    cs = [c for c in cases() if c[2] == oracle.OWN_PREFIX]
+    arena, off, ln = oracle.pack([c[1] for c in cs])
+    gpu = _parity(rx, arena, off, ln, "golden")
+    for i, c in enumerate(cs):
+        check_case(c, int(gpu.status[i]), gpu.submessages(i), record_to_dict)
+
+
+def test_golden_shape_type_red(rx):
+    c = next(c for c in cases() if c[0] == "mr_shapes_red")
+    arena, off, ln = oracle.pack([c[1]])
+    gpu = rx.handle_received_batch(arena, off, ln)
+    d = [record_to_dict(r) for r in gpu.records if r["kind"] == DATA][0]
+    assert shape_type_from_payload(c[1][d["pl_off"]:d["pl_off"] + d["pl_len"]]) == ("RED", 105, 23, 30)
+    assert len(gpu.submessages(0)) == 4  # message_receiver.rs:1223
+
+
+def test_golden_zero_own_prefix():
+    """mr_test_submsg_count uses GUID::default() as own prefix (message_receiver.rs:1280)."""
+    import rtps_rx
+    r = rtps_rx.MessageReceiver(bytes(12), max_datagrams=64)
+    cs = [c for c in cases() if c[2] == bytes(12)]
+    arena, off, ln = oracle.pack([c[1] for c in cs])
+    gpu = r.handle_received_batch(arena, off, ln)
+    _assert_same(gpu, oracle.parse(arena, off, ln, own=bytes(12)), "zero-own")
+    assert [len(gpu.submessages(i)) for i in range(len(cs))] == [4, 2]
+    r.close()
+
+
+def _device_gen(rx, wl, n, first_idx=0, n_writers=16):
+    import rtps_rx
+    off, ln, size = rtps_rx.gen_layout(wl, n, first_idx=first_idx, n_writers=n_writers)
+    dev = torch.device("cuda", 0)
+    arena_t = torch.zeros(max(size, 16), dtype=torch.uint8, device=dev)
+    off_t = torch.from_numpy(off.view(np.int64)).to(dev)
+    ln_t = torch.from_numpy(ln.view(np.int32)).to(dev)
+    rx.generate(wl, arena_t, off_t, ln_t, n, first_idx=first_idx, n_writers=n_writers)
+    rx.sync()
+    return arena_t.cpu().numpy(), off, ln
+
+
+@pytest.mark.parametrize("wl,name", [(1, "T"), (2, "C2"), (3, "C3"), (4, "C4")])
+def test_workload_parity(rx, wl, name):
+    n = 20000
+    arena, off, ln = _device_gen(rx, wl, n, first_idx=12345)
+    h_arena, h_off, h_ln = oracle.gen(wl, n, first_idx=12345)
+    assert np.array_equal(h_off, off) and np.array_equal(h_ln, ln)
+    assert np.array_equal(h_arena[:len(arena)], arena[:len(h_arena)]), "device generator != host generator"
+    _parity(rx, arena, off, ln, name)
+
+
+def test_match_table(rx):
+    import rtps_rx
+    arena, off, ln = oracle.gen(oracle.WL_C3, 20000)
+    # matched writers: 10 of the 16 generated writers, slot = writer index; plus duplicates (first wins)
+    st, recs, _, _ = oracle.parse(arena, off, ln)
+    guids = sorted({bytes(r["prefix"]) + bytes(r["writer_id"]) for r in recs if r["kind"] == DATA})
+    entries = [(g, i % 7) for i, g in enumerate(guids[:40])] + [(guids[0], 99)]
+    table = rtps_rx.pack_match_table(entries)
+    gpu = _parity(rx, arena, off, ln, "match", table=table)
+    assert (gpu.match != 0xFFFF).sum() > 0
+
+
+def test_misaligned_packing(rx):
+    arena, off, ln = oracle.gen(oracle.WL_C3, 5000)
+    dg = [arena[int(o):int(o) + int(l)].tobytes() for o, l in zip(off, ln)]
+    for align in (1, 2, 3):
+        a2, o2, l2 = oracle.pack(dg, align=align) if align > 1 else oracle.pack(dg, align=1)
+        if align == 3:  # odd start
+            a2 = np.concatenate([np.zeros(3, np.uint8), a2])
+            o2 = o2 + 3
+        _parity(rx, a2, o2, l2, f"align{align}")
+
+
+def test_fuzz_byte_flips(rx):
+    rng = np.random.default_rng(7)
+    arena, off, ln = oracle.gen(oracle.WL_C3, 20000)
+    arena = arena.copy()
+    for _ in range(4):
+        a = arena.copy()
+        k = len(a) // 40
+        pos = rng.integers(0, len(a), k)
+        a[pos] = rng.integers(0, 256, k).astype(np.uint8)
+        _parity(rx, a, off, ln, "fuzz")
+    # header-region flips hit the walk hardest
+    a = arena.copy()
+    for o, l in zip(off[::3], ln[::3]):
+        p = int(o) + int(rng.integers(0, min(int(l), 64)))
+        a[p] = rng.integers(0, 256)
+    _parity(rx, a, off, ln, "fuzz-headers")
+
+
+def test_random_submessage_soup(rx):
+    """Random kinds/lengths/flags: exercises every error path of every reader."""
+    rng = np.random.default_rng(11)
+    kinds = [0x01, 0x06, 0x07, 0x08, 0x09, 0x0c, 0x0d, 0x0e, 0x0f, 0x12, 0x13, 0x15, 0x16, 0x30, 0x80, 0x02]
+    dgrams = []
+    for i in range(20000):
+        d = bytearray(b"RTPS\x02\x04\x01\x12") + bytearray(rng.integers(0, 256, 12, dtype=np.uint8))
+        for _ in range(int(rng.integers(1, 6))):
+            kind = int(rng.choice(kinds))
+            le = int(rng.integers(0, 2))
+            flags = int(rng.integers(0, 256)) & ~1 | le
+            blen = int(rng.choice([0, 4, 8, 12, 16, 20, 24, 28, 32, 36, 40, 44, 48, 60, 64, int(rng.integers(0, 90))]))
+            body = bytearray(rng.integers(0, 256, blen, dtype=np.uint8))
+            if blen >= 4 and rng.random() < 0.7:  # plausible otq / numBits
+                struct.pack_into("<H" if le else ">H", body, 2, int(rng.choice([16, 28, 17, 30, 8, 0])))
+            if kind in (0x06, 0x08, 0x12) and blen >= 28 and rng.random() < 0.7:
+                struct.pack_into("<I" if le else ">I", body, {0x06: 16, 0x08: 24, 0x12: 20}[kind],
+                                 int(rng.choice([0, 1, 31, 32, 33, 64, 256, 257])))
+            if kind in (0x15, 0x16) and blen >= 36 and rng.random() < 0.5:  # inline QoS params
+                flags |= 2
+            declared = blen if rng.random() < 0.9 else int(rng.integers(0, 120))
+            d += bytes([kind, flags]) + struct.pack("<H" if le else ">H", declared) + body
+        if rng.random() < 0.05:
+            d += bytes(rng.integers(0, 256, int(rng.integers(1, 4)), dtype=np.uint8))
+        dgrams.append(bytes(d))
+    arena, off, ln = oracle.pack(dgrams)
+    _parity(rx, arena, off, ln, "soup")
+
+
+def test_edge_cases(rx):
+    dg = []
+    dg.append(b"")                                              # empty datagram
+    dg.append(b"RTPS")                                          # short
+    dg.append(b"RTPS\x02\x04\x01\x12\x00DDSPING")               # 16-B ping
+    dg.append(b"RTPX" + bytes(16))                              # RTPX
+    dg.append(b"RTPS\x03\x00" + bytes(14))                      # version 3
+    dg.append(b"RTPS\x02\x04" + bytes(14))                      # header only: OK, 0 records
+    dg.append(b"RTPS\x02\x04" + bytes(14) + b"\x09\x01")         # trailing 2 bytes
+    hdr = b"RTPS\x02\x04\x01\x12" + bytes(range(1, 13))
+    # max records: INFO_TS with Invalidate and length 0, repeated to 64 KiB
+    dg.append(hdr + b"\x09\x03\x00\x00" * ((65536 - 20) // 4))
+    # 64 KiB datagram: one DATA with octetsToNextHeader = 0 (extends to the end)
+    body = b"\x00\x00\x10\x00" + bytes(4) + b"\x00\x00\x01\x02" + struct.pack("<iI", 0, 5) + b"\x00\x01\x00\x00"
+    big = hdr + b"\x15\x05\x00\x00" + body
+    dg.append(big + bytes(65536 - len(big)))
+    dg.append(big + bytes(65537 - len(big)))                    # too long for the record layout
+    # PAD / INFO_TS with length 0 in the middle
+    dg.append(hdr + b"\x01\x01\x00\x00" + b"\x09\x03\x00\x00" + b"\x07\x01\x1c\x00" + bytes(28))
+    arena, off, ln = oracle.pack(dg)
+    gpu = _parity(rx, arena, off, ln, "edge")
+    assert gpu.status.tolist()[:7] == [1, 1, 2, 3, 5, 0, 6]
+    assert len(gpu.submessages(7)) == (65536 - 20) // 4
+    assert gpu.status[9] == 7
+
+
+def test_arena_tail_exact(rx):
+    """Last datagram ends exactly at the arena end: the window loads must not lose bytes."""
+    arena, off, ln = oracle.gen(oracle.WL_C3, 300)
+    dg = [arena[int(o):int(o) + int(l)].tobytes() for o, l in zip(off, ln)]
+    a2, o2, l2 = oracle.pack(dg, align=1)
+    a2 = a2[:int(o2[-1]) + int(l2[-1])]
+    _parity(rx, a2, o2, l2, "tail")
+
+
+def test_empty_batch(rx):
+    gpu = rx.handle_received_batch(np.zeros(16, np.uint8), np.zeros(0, np.uint64), np.zeros(0, np.uint32))
+    assert gpu.n_records == 0 and len(gpu.status) == 0
+
+
+@pytest.mark.parametrize("wl,name", [(1, "T"), (2, "C2"), (3, "C3"), (4, "C4")])
+def test_full_size_parity(rx, wl, name):
+    """BASELINE full sizes (1M datagrams): bit-exact vs the oracle on all datagrams."""
+    n = 1 << 20
+    arena, off, ln = _device_gen(rx, wl, n)
+    gpu = _parity(rx, arena, off, ln, f"{name}-1M")
+    if wl in (1, 2):  # size-independent properties of the one-DATA-per-datagram configs
+        assert (gpu.status == DGRAM_OK).all() and gpu.n_records == n
+        assert np.array_equal(gpu.records["dgram_idx"], np.arange(n, dtype=np.uint32))
+        assert np.array_equal(gpu.records["sn"], np.arange(n) // 16 + 1)
+        u = gpu.records["u"].view(np.uint16).reshape(-1, 8)
+        assert (u[:, 1] == (980 if wl == 1 else 256)).all()
