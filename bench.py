@@ -120,7 +120,8 @@ def main():
     # ---- input: this rank's chunk of the synthetic stream, generated in HBM ----
     off, ln, size = rtps_rx.gen_layout(wl, n, first_idx=rank * n, n_writers=args.writers)
     rx = rtps_rx.MessageReceiver(OWN_PREFIX, device=local_rank, max_datagrams=n)
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     rx.set_stream(stream)
     arena = torch.empty(size, dtype=torch.uint8, device=dev)
     off_t = torch.from_numpy(off.view(np.int64)).to(dev)

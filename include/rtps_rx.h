@@ -194,7 +194,10 @@ typedef struct rtps_rx_ctx rtps_rx_ctx;
 /* MessageReceiver::new(participant_guid_prefix, None)  (message_receiver.rs:158-182) */
 int rtps_rx_create(const rtps_rx_config* cfg, rtps_rx_ctx** out_ctx);
 int rtps_rx_destroy(rtps_rx_ctx* ctx);
-/* Launch on the caller's hipStream_t (NULL = the context's own stream). */
+/* Launch on the caller's hipStream_t.  NULL = the HIP null (default)
+ * stream; RTPS_RX_OWN_STREAM = the context's own non-blocking stream
+ * (the default after rtps_rx_create). */
+#define RTPS_RX_OWN_STREAM ((void*)(intptr_t)-1)
 int rtps_rx_set_stream(rtps_rx_ctx* ctx, void* hip_stream);
 /* Replace the writer-GUID -> reader-slot table (first entry wins on duplicates). */
 int rtps_rx_set_match_table(rtps_rx_ctx* ctx, const rtps_match* table, uint32_t n);
@@ -206,6 +209,11 @@ int rtps_rx_parse_batch(rtps_rx_ctx* ctx, const uint8_t* arena, uint64_t arena_l
                         const uint64_t* dgram_off, const uint32_t* dgram_len, uint32_t n,
                         const rtps_rx_out* out);
 int rtps_rx_sync(rtps_rx_ctx* ctx);
+/* Performance hint: the number of records most datagrams of the coming
+ * batches produce (default 1: one DATA per datagram; 2 for INFO_TS+DATA).
+ * Tiles of 256 datagrams that all match it are written in a single pass;
+ * any other tile costs a second walk.  Results never depend on the hint. */
+int rtps_rx_set_spec_hint(rtps_rx_ctx* ctx, uint32_t records_per_datagram);
 const char* rtps_rx_strerror(int code);
 
 /* Multi-GPU sharding (>= 2 GPUs): stable partition of the writer/reader-kind

@@ -39,7 +39,9 @@ namespace {
 
 constexpr uint32_t TILE = 256;  // datagrams per workgroup
 constexpr uint32_t WAVES = TILE / 64;
-constexpr uint64_t FLAG_AGG = 1ull << 62, FLAG_INC = 2ull << 62, VAL_MASK = (1ull << 62) - 1;
+#ifndef RTPS_WAVES_PER_SIMD
+#define RTPS_WAVES_PER_SIMD 6  // 80 VGPRs, no spill; SGPR use caps a CU at 6 such workgroups anyway
+#endif
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -59,7 +61,7 @@ struct KParams {
   const u32x4* mt_keys;       // match table (open addressing), may be null
   const uint16_t* mt_slots;
   uint32_t mt_mask;           // capacity - 1
-  uint64_t* scratch;          // [0] = tile ticket, [1] = look-back timeouts, [2..] tile states
+  uint64_t* scratch;          // per-tile counts / prefixes (Scratch)
 };
 
 // ---------------------------------------------------------------------------
@@ -108,15 +110,23 @@ __device__ __forceinline__ int64_t sn_of(uint32_t hi_raw, uint32_t lo_raw, bool 
   return (int64_t)(((uint64_t)(int64_t)(int32_t)e32(hi_raw, le)) << 32) + (int64_t)e32(lo_raw, le);
 }
 
-// 48-byte window at a submessage start: w[0] = header, w[1..] = body dwords
+// 36-byte window at a submessage start: w[0] = header, w[1..8] = body dwords
+// (the largest fixed field, DATA_FRAG sampleSize, ends at body byte 32).
 struct Win {
   uint32_t w[12];
 };
 __device__ __forceinline__ void load_win(const Src& s, uint32_t o, Win& W) {
-  u32x4 a = ld16(s, o), b = ld16(s, o + 16), c = ld16(s, o + 32);
+  u32x4 a = ld16(s, o), b = ld16(s, o + 16);
   W.w[0] = a[0]; W.w[1] = a[1]; W.w[2] = a[2]; W.w[3] = a[3];
   W.w[4] = b[0]; W.w[5] = b[1]; W.w[6] = b[2]; W.w[7] = b[3];
-  W.w[8] = c[0]; W.w[9] = c[1]; W.w[10] = c[2]; W.w[11] = c[3];
+  W.w[8] = ld4(s, o + 32); W.w[9] = 0; W.w[10] = 0; W.w[11] = 0;
+}
+// the first submessage always starts at byte 20: its window comes from the
+// 64-byte head (bytes 0..64) already in registers
+__device__ __forceinline__ void head_win(const uint32_t* H, Win& W) {
+#pragma unroll
+  for (int k = 0; k < 11; ++k) W.w[k] = H[5 + k];
+  W.w[11] = 0;
 }
 
 // builtin (reader_id, writer_id) pairs; entity ids as raw little-endian-packed words
@@ -205,22 +215,21 @@ __device__ __forceinline__ bool param_list(const Src& s, uint32_t body_off, uint
 // Walk one datagram.  WRITE=false: validate + count materialised submessages.
 // WRITE=true: (datagram known OK) write its records starting at record index `ridx`.
 template <bool WRITE>
-__device__ uint32_t walk(const KParams& p, const Src& s, uint32_t L, uint32_t dgram_idx, uint64_t ridx,
-                         uint32_t& nrec) {
+__device__ uint32_t walk(const KParams& p, const Src& s, const uint32_t* H, uint32_t L, uint32_t dgram_idx,
+                         uint64_t ridx, uint32_t& nrec) {
   nrec = 0;
   if (L > RTPS_MAX_DATAGRAM) return RTPS_DGRAM_TOO_LONG;
   const uint32_t MAGIC_RTPS = 0x53505452u, MAGIC_RTPX = 0x58505452u;  // "RTPS" / "RTPX"
-  u32x4 h0 = ld16(s, 0);
   if (L < 20u) {  // message_receiver.rs:238-251
-    if (L >= 16u && h0[0] == MAGIC_RTPS && (h0[2] >> 8) == 0x534444u /* "DDS" */ &&
-        h0[3] == 0x474e4950u /* "PING" */)
+    if (L >= 16u && H[0] == MAGIC_RTPS && (H[2] >> 8) == 0x534444u /* "DDS" */ &&
+        H[3] == 0x474e4950u /* "PING" */)
       return RTPS_DGRAM_PING;
     return RTPS_DGRAM_SHORT;
   }
-  if (h0[0] != MAGIC_RTPS) return h0[0] == MAGIC_RTPX ? RTPS_DGRAM_RTPX : RTPS_DGRAM_BAD_MAGIC;
-  if ((h0[1] & 0xffu) > 2u) return RTPS_DGRAM_BAD_HEADER;  // ProtocolVersion major
+  if (H[0] != MAGIC_RTPS) return H[0] == MAGIC_RTPX ? RTPS_DGRAM_RTPX : RTPS_DGRAM_BAD_MAGIC;
+  if ((H[1] & 0xffu) > 2u) return RTPS_DGRAM_BAD_HEADER;  // ProtocolVersion major
   // handle_parsed_message_2 (:289-295): src := header prefix, dest := own, ts := None
-  uint32_t src0 = h0[2], src1 = h0[3], src2 = ld4(s, 16);
+  uint32_t src0 = H[2], src1 = H[3], src2 = H[4];
   uint32_t dst0 = p.own0, dst1 = p.own1, dst2 = p.own2;
   bool ts_valid = false;
   uint32_t ts_sec = 0, ts_frac = 0;
@@ -230,7 +239,8 @@ __device__ uint32_t walk(const KParams& p, const Src& s, uint32_t L, uint32_t dg
     uint32_t rem = L - o;
     if (rem < 4u) return RTPS_DGRAM_SUBMSG_ERR;  // SubmessageHeader needs 4 bytes
     Win W;
-    load_win(s, o, W);
+    if (o == 20u) head_win(H, W);
+    else load_win(s, o, W);
     uint32_t kind = W.w[0] & 0xffu, flags = (W.w[0] >> 8) & 0xffu;
     bool le = (flags & 1u) != 0u;
     uint32_t clen = e16(W.w[0], 1, le);
@@ -492,115 +502,196 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, uint32_t lane) {
   return x;
 }
 
-// Decoupled look-back over tiles (single pass, ordered output).  Tile states
-// are 8-byte {flag:2, value:62} granules written by single agent-scope
-// atomic stores and polled by relaxed agent-scope loads (an untorn granule
-// needs no fence: MI355X_MICROARCH.md, visibility R2).  Tickets come from an
-// atomic counter, so every tile a tile waits on is already resident.
-__device__ uint64_t lookback(uint64_t* states, uint32_t tile, uint64_t agg, uint64_t* timeouts) {
-  if (tile == 0) {
-    __hip_atomic_store(&states[0], FLAG_INC | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return 0;
-  }
-  __hip_atomic_store(&states[tile], FLAG_AGG | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  uint64_t excl = 0;
-  int64_t t = (int64_t)tile - 1;
-  uint32_t spins = 0;
-  while (t >= 0) {
-    uint64_t v = __hip_atomic_load(&states[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uint64_t f = v & ~VAL_MASK;
-    if (f == 0) {
-      if (++spins > (1u << 24)) {  // never expected; bounded so the grid always drains
-        atomicAdd(reinterpret_cast<unsigned long long*>(timeouts), 1ull);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-      continue;
-    }
-    excl += v & VAL_MASK;
-    if (f == FLAG_INC) break;
-    --t;
-  }
-  __hip_atomic_store(&states[tile], FLAG_INC | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return excl;
-}
+// ---------------------------------------------------------------------------
+// Ordered output without inter-workgroup waiting:
+//   A  rtps_parse_spec_kernel  one workgroup per tile of 256 datagrams (blockIdx
+//      order): walk 1 counts each datagram's records; a tile in which every
+//      datagram has exactly k_spec records ("speculative" tile) walks again and
+//      writes its records at tile*256*k_spec + local prefix, which is the final
+//      position whenever every earlier tile is speculative too.  Every tile
+//      publishes count | nonspec<<31.
+//   S  rtps_tile_scan_kernel   one workgroup: exclusive scan of the tile counts,
+//      first non-speculative tile f, total -> n_records.
+//   B  rtps_parse_fix_kernel   persistent: re-walks tiles f.. and writes them at
+//      their scanned positions (overwriting any speculative writes there).
+// One-DATA-per-datagram traffic (T, C2, C4) finishes in A; mixed traffic (C3)
+// becomes an exact two-pass parse.  No spin-waits, tickets or grid barriers.
+// ---------------------------------------------------------------------------
+struct TileCtx {
+  uint32_t i;      // datagram index of this lane
+  bool valid, addressable;
+  uint32_t L;
+  Src s;
+  uint32_t H[16];  // datagram bytes 0..64
+};
 
-__global__ __launch_bounds__(TILE) void rtps_parse_kernel(KParams p) {
-  __shared__ uint32_t s_tile;
-  __shared__ uint64_t s_min_off, s_base_rec;
-  __shared__ uint32_t s_wave_sum[WAVES];
-
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  uint64_t* states = p.scratch + 2;
-  if (tid == 0) {
-    s_tile = atomicAdd(reinterpret_cast<unsigned int*>(p.scratch), 1u);
-    s_min_off = ~0ull;
-  }
-  __syncthreads();
-  const uint32_t tile = s_tile;
-  const uint32_t i = tile * TILE + tid;
-  const bool valid = i < p.n;
-  uint64_t off = valid ? p.dgram_off[i] : ~0ull;
-  uint32_t L = valid ? p.dgram_len[i] : 0u;
-
-  // tile base for the buffer descriptor: min offset over the tile
+// load this lane's (offset, length), build the workgroup's buffer descriptor
+// (base = min offset of the tile) and the 64-byte head
+__device__ __forceinline__ void load_tile(const KParams& p, uint32_t tile, uint64_t* s_min_off, TileCtx& t) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  t.i = tile * TILE + tid;
+  t.valid = t.i < p.n;
+  const uint64_t off = t.valid ? p.dgram_off[t.i] : ~0ull;
+  t.L = t.valid ? p.dgram_len[t.i] : 0u;
   uint64_t m = off;
 #pragma unroll
   for (uint32_t d = 32; d >= 1; d >>= 1) {
     uint64_t y = __shfl_xor(m, d, 64);
     m = y < m ? y : m;
   }
-  if (lane == 0) atomicMin(reinterpret_cast<unsigned long long*>(&s_min_off), (unsigned long long)m);
+  if (lane == 0) atomicMin(reinterpret_cast<unsigned long long*>(s_min_off), (unsigned long long)m);
   __syncthreads();
-  uint64_t tb = s_min_off;
+  uint64_t tb = *s_min_off;
   if (tb > p.arena_len) tb = p.arena_len;
-  uint64_t avail64 = p.arena_len - tb;
-  uint32_t avail = avail64 > 0xffffffffull ? 0xffffffffu : (uint32_t)avail64;
   uint32_t tb_lo = __builtin_amdgcn_readfirstlane((uint32_t)tb);
   uint32_t tb_hi = __builtin_amdgcn_readfirstlane((uint32_t)(tb >> 32));
-  avail = __builtin_amdgcn_readfirstlane(avail);
-  const uint8_t* tbase = p.arena + (((uint64_t)tb_hi << 32) | tb_lo);
-  Src s;
-  s.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(tbase), (short)0, (int)avail, 0x00020000);
-  s.avail = avail;
-  uint64_t rel = valid ? off - tb : 0;
-  bool addressable = valid && off <= p.arena_len && (uint64_t)L <= p.arena_len - off && rel + L <= avail;
-  s.base = (uint32_t)rel;
+  tb = ((uint64_t)tb_hi << 32) | tb_lo;
+  uint64_t avail64 = p.arena_len - tb;
+  uint32_t avail = __builtin_amdgcn_readfirstlane(avail64 > 0xffffffffull ? 0xffffffffu : (uint32_t)avail64);
+  t.s.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p.arena + tb), (short)0, (int)avail,
+                                               0x00020000);
+  t.s.avail = avail;
+  const uint64_t rel = t.valid ? off - tb : 0;
+  t.addressable = t.valid && off <= p.arena_len && (uint64_t)t.L <= p.arena_len - off && rel + t.L <= avail;
+  t.s.base = (uint32_t)rel;
+  u32x4 a = {0u, 0u, 0u, 0u}, b = a, c = a, d = a;
+  if (t.addressable) { a = ld16(t.s, 0); b = ld16(t.s, 16); c = ld16(t.s, 32); d = ld16(t.s, 48); }
+  t.H[0] = a[0]; t.H[1] = a[1]; t.H[2] = a[2]; t.H[3] = a[3];
+  t.H[4] = b[0]; t.H[5] = b[1]; t.H[6] = b[2]; t.H[7] = b[3];
+  t.H[8] = c[0]; t.H[9] = c[1]; t.H[10] = c[2]; t.H[11] = c[3];
+  t.H[12] = d[0]; t.H[13] = d[1]; t.H[14] = d[2]; t.H[15] = d[3];
+}
 
-  // walk 1: status + count
-  uint32_t cnt = 0, st = RTPS_DGRAM_OK;
-  if (valid) {
-    if (!addressable) st = RTPS_DGRAM_TOO_LONG;
-    else st = walk<false>(p, s, L, i, 0, cnt);
+__device__ __forceinline__ uint32_t count_lane(const KParams& p, TileCtx& t, uint32_t& cnt) {
+  cnt = 0;
+  uint32_t st = RTPS_DGRAM_OK;
+  if (t.valid) {
+    if (!t.addressable) st = RTPS_DGRAM_TOO_LONG;
+    else st = walk<false>(p, t.s, t.H, t.L, t.i, 0, cnt);
     if (st != RTPS_DGRAM_OK) cnt = 0;
   }
+  return st;
+}
 
-  // tile scan
-  uint32_t incl = wave_incl_scan(cnt, lane);
-  if (lane == 63) s_wave_sum[wave] = incl;
+// scratch layout (bytes): u32 info[n_tiles] | u64 prefix[n_tiles] | u32 ctl[4]
+struct Scratch {
+  uint32_t* info;    // count | nonspec << 31
+  uint64_t* prefix;  // exclusive record prefix per tile
+  uint32_t* ctl;     // [0] first non-speculative tile
+};
+__device__ __forceinline__ Scratch scratch_of(uint64_t* base, uint32_t n_tiles) {
+  Scratch x;
+  x.info = reinterpret_cast<uint32_t*>(base);
+  x.prefix = base + ((n_tiles + 1u) / 2u);
+  x.ctl = reinterpret_cast<uint32_t*>(x.prefix + n_tiles);
+  return x;
+}
+
+__global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_spec_kernel(KParams p, uint32_t n_tiles,
+                                                                                     uint32_t k_spec) {
+  __shared__ uint64_t s_min_off;
+  __shared__ uint32_t s_wave_sum[WAVES], s_wave_bad[WAVES];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t tile = blockIdx.x;
+  if (tid == 0) s_min_off = ~0ull;
   __syncthreads();
-  uint32_t wave_off = 0, agg = 0;
+  TileCtx t;
+  load_tile(p, tile, &s_min_off, t);
+  uint32_t cnt;
+  const uint32_t st = count_lane(p, t, cnt);
+  const uint32_t incl = wave_incl_scan(cnt, lane);
+  const uint64_t bad = __ballot(t.valid && cnt != k_spec);
+  if (lane == 63) { s_wave_sum[wave] = incl; s_wave_bad[wave] = bad != 0ull; }
+  __syncthreads();
+  uint32_t wave_off = 0, agg = 0, nonspec = 0;
 #pragma unroll
   for (uint32_t w = 0; w < WAVES; ++w) {
     uint32_t v = s_wave_sum[w];
     if (w < wave) wave_off += v;
     agg += v;
+    nonspec |= s_wave_bad[w];
+  }
+  Scratch x = scratch_of(p.scratch, n_tiles);
+  if (tid == 0) x.info[tile] = agg | (nonspec << 31);
+  if (t.valid) p.status[t.i] = (uint8_t)st;
+  if (!nonspec) {
+    const uint64_t my_first = (uint64_t)tile * TILE * k_spec + wave_off + (incl - cnt);
+    if (t.valid) {
+      if (p.rec_begin) p.rec_begin[t.i] = (uint32_t)my_first;
+      if (cnt) {
+        uint32_t n2;
+        walk<true>(p, t.s, t.H, t.L, t.i, my_first, n2);
+      }
+    }
+  }
+}
+
+constexpr uint32_t SCAN_THREADS = 1024;
+__global__ __launch_bounds__(SCAN_THREADS) void rtps_tile_scan_kernel(uint64_t* scratch, uint32_t n_tiles,
+                                                                      uint64_t* n_records) {
+  __shared__ uint64_t s_part[SCAN_THREADS / 64];
+  __shared__ uint32_t s_first;
+  Scratch x = scratch_of(scratch, n_tiles);
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  if (tid == 0) s_first = n_tiles;
+  __syncthreads();
+  uint64_t carry = 0;
+  for (uint32_t t0 = 0; t0 < n_tiles; t0 += SCAN_THREADS) {
+    const uint32_t t = t0 + tid;
+    const uint32_t info = t < n_tiles ? x.info[t] : 0u;
+    if (t < n_tiles && (info >> 31)) atomicMin(&s_first, t);
+    uint64_t v = info & 0x7fffffffu, incl = v;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      uint64_t y = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += y;
+    }
+    if (lane == 63) s_part[wave] = incl;
+    __syncthreads();
+    uint64_t before = carry, total = carry;
+    for (uint32_t w = 0; w < SCAN_THREADS / 64; ++w) {
+      if (w < wave) before += s_part[w];
+      total += s_part[w];
+    }
+    if (t < n_tiles) x.prefix[t] = before + incl - v;
+    carry = total;
+    __syncthreads();
   }
   if (tid == 0) {
-    uint64_t excl = lookback(states, tile, agg, p.scratch + 1);
-    s_base_rec = excl;
-    if (tile == gridDim.x - 1) *p.n_records = excl + agg;
+    x.ctl[0] = s_first;
+    *n_records = carry;
   }
-  __syncthreads();
-  const uint64_t my_first = s_base_rec + wave_off + (incl - cnt);
+}
 
-  if (valid) {
-    p.status[i] = (uint8_t)st;
-    if (p.rec_begin) p.rec_begin[i] = (uint32_t)my_first;
-    if (st == RTPS_DGRAM_OK && cnt) {
-      uint32_t n2 = 0;
-      walk<true>(p, s, L, i, my_first, n2);
+__global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_fix_kernel(KParams p, uint32_t n_tiles) {
+  __shared__ uint64_t s_min_off;
+  __shared__ uint32_t s_wave_sum[WAVES];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  Scratch x = scratch_of(p.scratch, n_tiles);
+  const uint32_t first = __builtin_amdgcn_readfirstlane(x.ctl[0]);
+  for (uint32_t tile = first + blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    if (tid == 0) s_min_off = ~0ull;
+    __syncthreads();
+    TileCtx t;
+    load_tile(p, tile, &s_min_off, t);
+    uint32_t cnt;
+    const uint32_t st = count_lane(p, t, cnt);
+    const uint32_t incl = wave_incl_scan(cnt, lane);
+    if (lane == 63) s_wave_sum[wave] = incl;
+    __syncthreads();
+    uint32_t wave_off = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < WAVES; ++w)
+      if (w < wave) wave_off += s_wave_sum[w];
+    const uint64_t my_first = x.prefix[tile] + wave_off + (incl - cnt);
+    if (t.valid) {
+      if (p.rec_begin) p.rec_begin[t.i] = (uint32_t)my_first;
+      if (st == RTPS_DGRAM_OK && cnt) {
+        uint32_t n2;
+        walk<true>(p, t.s, t.H, t.L, t.i, my_first, n2);
+      }
     }
+    __syncthreads();  // s_min_off / s_wave_sum reuse
   }
 }
 
@@ -715,7 +806,7 @@ struct rtps_rx_ctx {
   uint32_t max_datagrams = 0;
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
-  uint64_t* scratch = nullptr;  // ticket, timeouts, tile states
+  uint64_t* scratch = nullptr;  // per-tile counts / prefixes (Scratch)
   size_t scratch_words = 0;
   u32x4* mt_keys = nullptr;
   uint16_t* mt_slots = nullptr;
@@ -723,6 +814,8 @@ struct rtps_rx_ctx {
   bool mt_active = false;
   uint32_t* bucket_hist = nullptr;
   size_t bucket_bytes = 0;
+  uint32_t resident_blocks = 1024;
+  uint32_t k_spec = 1;  // speculated records per datagram (0 disables nothing: see set_spec_hint)
 };
 
 static int hip_fail(hipError_t e) { return e == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP; }
@@ -740,9 +833,15 @@ int rtps_rx_create(const rtps_rx_config* cfg, rtps_rx_ctx** out_ctx) {
   if (hipSetDevice(c->device) != hipSuccess) { delete c; return RTPS_RX_EHIP; }
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) { delete c; return RTPS_RX_EHIP; }
   c->stream = c->own_stream;
+  {
+    int cus = 0, per_cu = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess && cus > 0 &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rtps_parse_fix_kernel, TILE, 0) == hipSuccess && per_cu > 0)
+      c->resident_blocks = (uint32_t)cus * (uint32_t)per_cu;
+  }
   size_t tiles = ((size_t)cfg->max_datagrams + TILE - 1) / TILE;
-  c->scratch_words = 2 + (tiles ? tiles : 1);
-  c->scratch_words = (c->scratch_words + 1) & ~(size_t)1;  // 16-B multiple for the memset
+  if (tiles == 0) tiles = 1;
+  c->scratch_words = (tiles + 1) / 2 + tiles + 2;  // u32 info[tiles] | u64 prefix[tiles] | u32 ctl[4]
   if (hipMalloc(&c->scratch, c->scratch_words * sizeof(uint64_t)) != hipSuccess) {
     (void)hipStreamDestroy(c->own_stream);
     delete c;
@@ -767,7 +866,7 @@ int rtps_rx_destroy(rtps_rx_ctx* c) {
 
 int rtps_rx_set_stream(rtps_rx_ctx* c, void* s) {
   if (!c) return RTPS_RX_EINVAL;
-  c->stream = s ? (hipStream_t)s : c->own_stream;
+  c->stream = (s == RTPS_RX_OWN_STREAM) ? c->own_stream : (hipStream_t)s;
   return RTPS_RX_OK;
 }
 
@@ -822,11 +921,7 @@ int rtps_rx_parse_batch(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len
   if (n > c->max_datagrams) return RTPS_RX_ETOOBIG;
   (void)hipSetDevice(c->device);
   if (n == 0) return hip_fail(hipMemsetAsync(out->n_records, 0, sizeof(uint64_t), c->stream));
-  uint32_t tiles = (n + TILE - 1) / TILE;
-  // zero ticket + timeout + tile states (one contiguous block, 16-B multiple)
-  size_t words = (2 + (size_t)tiles + 1) & ~(size_t)1;
-  hipError_t e = hipMemsetAsync(c->scratch, 0, words * sizeof(uint64_t), c->stream);
-  if (e != hipSuccess) return RTPS_RX_EHIP;
+  uint32_t tiles = (n + TILE - 1) / TILE;  // one tile = one workgroup = 256 datagrams
   KParams p;
   p.arena = arena;
   p.arena_len = arena_len;
@@ -846,8 +941,18 @@ int rtps_rx_parse_batch(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len
   p.mt_slots = c->mt_slots;
   p.mt_mask = c->mt_active ? c->mt_cap - 1 : 0;
   p.scratch = c->scratch;
-  hipLaunchKernelGGL(rtps_parse_kernel, dim3(tiles), dim3(TILE), 0, c->stream, p);
+  hipLaunchKernelGGL(rtps_parse_spec_kernel, dim3(tiles), dim3(TILE), 0, c->stream, p, tiles, c->k_spec);
+  hipLaunchKernelGGL(rtps_tile_scan_kernel, dim3(1), dim3(SCAN_THREADS), 0, c->stream, c->scratch, tiles,
+                     out->n_records);
+  uint32_t grid = tiles < c->resident_blocks ? tiles : c->resident_blocks;
+  hipLaunchKernelGGL(rtps_parse_fix_kernel, dim3(grid), dim3(TILE), 0, c->stream, p, tiles);
   return hip_fail(hipGetLastError());
+}
+
+int rtps_rx_set_spec_hint(rtps_rx_ctx* c, uint32_t records_per_datagram) {
+  if (!c || records_per_datagram > 0xffffu) return RTPS_RX_EINVAL;
+  c->k_spec = records_per_datagram;
+  return RTPS_RX_OK;
 }
 
 int rtps_rx_sync(rtps_rx_ctx* c) {
@@ -917,5 +1022,12 @@ int rtps_rx_bucket_by_writer(rtps_rx_ctx* c, const rtps_record* recs, const uint
 }
 
 uint32_t rtps_rx_record_size(void) { return (uint32_t)sizeof(rtps_record); }
+
+/* diagnostics (not part of the public header): copy the first k scratch words */
+int rtps_rx_debug_scratch(rtps_rx_ctx* c, uint64_t* host, uint32_t k) {
+  if (!c || !host || k > c->scratch_words) return RTPS_RX_EINVAL;
+  (void)hipStreamSynchronize(c->stream);
+  return hip_fail(hipMemcpy(host, c->scratch, k * sizeof(uint64_t), hipMemcpyDeviceToHost));
+}
 
 }  // extern "C"

@@ -20,7 +20,7 @@ from .records import (RECORD_DTYPE, MATCH_DTYPE, STATUS_NAMES, KIND_NAMES, WRITE
                       ROUTE_PASS, NO_MATCH, max_records, record_to_dict, pack_match_table)
 
 _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_PKG_DIR), "librtps_rx.so")
+LIB_PATH = os.environ.get("RTPS_RX_LIB") or os.path.join(os.path.dirname(_PKG_DIR), "librtps_rx.so")
 ABI_VERSION = 1
 
 WL_T, WL_C2, WL_C3, WL_C4 = 1, 2, 3, 4
@@ -47,7 +47,7 @@ class _Out(ctypes.Structure):
 
 EXPORTS = ["rtps_rx_create", "rtps_rx_destroy", "rtps_rx_set_stream", "rtps_rx_set_match_table",
            "rtps_rx_parse_batch", "rtps_rx_sync", "rtps_rx_strerror", "rtps_rx_max_records_host",
-           "rtps_rx_generate", "rtps_rx_bucket_by_writer"]
+           "rtps_rx_generate", "rtps_rx_bucket_by_writer", "rtps_rx_set_spec_hint"]
 
 
 def lib():
@@ -74,6 +74,8 @@ def lib():
         L.rtps_rx_record_size.restype = U32
         L.rtps_rx_bucket_by_writer.argtypes = [P, P, P, U64, U32, P, P]
         L.rtps_rx_bucket_by_writer.restype = I
+        L.rtps_rx_set_spec_hint.argtypes = [P, U32]
+        L.rtps_rx_set_spec_hint.restype = I
         for fn in ("rtps_rx_create", "rtps_rx_destroy", "rtps_rx_set_stream", "rtps_rx_set_match_table",
                    "rtps_rx_parse_batch", "rtps_rx_sync", "rtps_rx_generate"):
             getattr(L, fn).restype = I
@@ -154,14 +156,20 @@ class MessageReceiver:
             pass
 
     def set_stream(self, stream):
-        """Launch on a torch.cuda.Stream (None = the context's own stream)."""
-        _check(lib().rtps_rx_set_stream(self._h, None if stream is None else ctypes.c_void_p(stream.cuda_stream)))
+        """Launch on a torch.cuda.Stream (its handle 0 = the HIP null stream);
+        None = the context's own stream."""
+        h = ctypes.c_void_p(-1) if stream is None else ctypes.c_void_p(stream.cuda_stream)
+        _check(lib().rtps_rx_set_stream(self._h, h))
 
     def set_match_table(self, entries):
         """entries: MATCH_DTYPE array or iterable of (writer_guid bytes[16], reader_slot)."""
         t = entries if isinstance(entries, np.ndarray) else pack_match_table(entries)
         t = np.ascontiguousarray(t, dtype=MATCH_DTYPE)
         _check(lib().rtps_rx_set_match_table(self._h, t.ctypes.data if len(t) else None, len(t)))
+
+    def set_spec_hint(self, records_per_datagram):
+        """Performance hint only (results never depend on it): expected records per datagram."""
+        _check(lib().rtps_rx_set_spec_hint(self._h, records_per_datagram))
 
     def sync(self):
         _check(lib().rtps_rx_sync(self._h))

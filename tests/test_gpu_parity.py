@@ -108,6 +108,23 @@ def test_workload_parity(rx, wl, name):
     _parity(rx, arena, off, ln, name)
 
 
+@pytest.mark.parametrize("hint", [0, 1, 2, 4, 7])
+def test_spec_hint_never_changes_results(rx, hint):
+    """The speculative single-pass tiles and the two-pass fix-up give identical output."""
+    arena, off, ln = oracle.gen(oracle.WL_C3, 30000)
+    # splice one-DATA datagrams (T) in front so some tiles are speculative for hint 1
+    a2, o2, l2 = oracle.gen(oracle.WL_C2, 3000)
+    dg = [a2[int(o):int(o) + int(l)].tobytes() for o, l in zip(o2, l2)] + \
+         [arena[int(o):int(o) + int(l)].tobytes() for o, l in zip(off, ln)] + \
+         [a2[int(o):int(o) + int(l)].tobytes() for o, l in zip(o2, l2)]
+    A, O, L = oracle.pack(dg)
+    rx.set_spec_hint(hint)
+    try:
+        _parity(rx, A, O, L, f"hint{hint}")
+    finally:
+        rx.set_spec_hint(1)
+
+
 def test_match_table(rx):
     import rtps_rx
     arena, off, ln = oracle.gen(oracle.WL_C3, 20000)
