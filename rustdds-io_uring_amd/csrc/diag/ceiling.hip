@@ -1,0 +1,52 @@
+// Diagnostic ceiling kernels for the parse's memory-traffic shape (not product code).
+// mode 0: read 12 B (off,len) + 64-B head per datagram, write 64-B record + 1 B + 4 B (per-lane stores)
+// mode 1: reads only (off,len + head), 1 B status write
+// mode 2: writes only (records + status + rec_begin)
+// mode 3: as 0 but the record is transposed through LDS and stored as contiguous 16-B pieces
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+template <int MODE>
+__global__ __launch_bounds__(256) void ceil_kernel(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
+                                                   uint32_t n, u32x4* rec, uint8_t* status, uint32_t* rb) {
+  __shared__ u32x4 lds[256 * 4];
+  uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  u32x4 a = {0, 0, 0, 0}, b = a, c = a, d = a;
+  uint32_t L = 0;
+  if (MODE != 2) {
+    uint64_t o = off[i];
+    L = len[i];
+    const u32x4* h = reinterpret_cast<const u32x4*>(arena + o);
+    a = h[0]; b = h[1]; c = h[2]; d = h[3];
+  } else {
+    a[0] = i; b[1] = i; c[2] = i; d[3] = i;
+  }
+  a[1] ^= L;
+  status[i] = (uint8_t)(a[0] ^ b[0] ^ c[0] ^ d[0]);
+  if (MODE == 1) return;
+  rb[i] = i;
+  if (MODE == 3) {
+    uint32_t t = threadIdx.x;
+    lds[t * 4 + 0] = a; lds[t * 4 + 1] = b; lds[t * 4 + 2] = c; lds[t * 4 + 3] = d;
+    __syncthreads();
+    u32x4* base = rec + (uint64_t)blockIdx.x * 256 * 4;
+    for (int k = 0; k < 4; ++k) base[k * 256 + t] = lds[k * 256 + t];
+  } else {
+    u32x4* r = rec + (uint64_t)i * 4;
+    r[0] = a; r[1] = b; r[2] = c; r[3] = d;
+  }
+}
+extern "C" int diag_ceiling(int mode, const uint8_t* arena, const uint64_t* off, const uint32_t* len, uint32_t n,
+                            void* rec, uint8_t* status, uint32_t* rb, void* stream) {
+  dim3 g((n + 255) / 256), b(256);
+  hipStream_t s = (hipStream_t)stream;
+  switch (mode) {
+    case 0: hipLaunchKernelGGL(ceil_kernel<0>, g, b, 0, s, arena, off, len, n, (u32x4*)rec, status, rb); break;
+    case 1: hipLaunchKernelGGL(ceil_kernel<1>, g, b, 0, s, arena, off, len, n, (u32x4*)rec, status, rb); break;
+    case 2: hipLaunchKernelGGL(ceil_kernel<2>, g, b, 0, s, arena, off, len, n, (u32x4*)rec, status, rb); break;
+    case 3: hipLaunchKernelGGL(ceil_kernel<3>, g, b, 0, s, arena, off, len, n, (u32x4*)rec, status, rb); break;
+    default: return -1;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}

@@ -214,9 +214,12 @@ __device__ __forceinline__ bool param_list(const Src& s, uint32_t body_off, uint
 
 // Walk one datagram.  WRITE=false: validate + count materialised submessages.
 // WRITE=true: (datagram known OK) write its records starting at record index `ridx`.
+// Records go to p.records[ridx + k], or, when stage != nullptr, to the LDS
+// staging buffer stage[ridx + k - stage_first] (the caller copies it out).
 template <bool WRITE>
 __device__ uint32_t walk(const KParams& p, const Src& s, const uint32_t* H, uint32_t L, uint32_t dgram_idx,
-                         uint64_t ridx, uint32_t& nrec) {
+                         uint64_t ridx, uint32_t& nrec, u32x4* stage = nullptr, uint16_t* stage_match = nullptr,
+                         uint64_t stage_first = 0) {
   nrec = 0;
   if (L > RTPS_MAX_DATAGRAM) return RTPS_DGRAM_TOO_LONG;
   const uint32_t MAGIC_RTPS = 0x53505452u, MAGIC_RTPX = 0x58505452u;  // "RTPS" / "RTPX"
@@ -481,7 +484,14 @@ __device__ uint32_t walk(const KParams& p, const Src& s, const uint32_t* H, uint
         if (ts_valid) { route |= RTPS_ROUTE_TS_VALID; R.d[14] = ts_sec; R.d[15] = ts_frac; }
         R.d[7] = (aux16 & 0xffffu) | (route << 16) | (pk << 24);
         uint64_t r = ridx + nrec;
-        if (r < p.max_records) {
+        if (stage) {
+          u32x4* q = stage + (r - stage_first) * 4u;
+          q[0] = u32x4{R.d[0], R.d[1], R.d[2], R.d[3]};
+          q[1] = u32x4{R.d[4], R.d[5], R.d[6], R.d[7]};
+          q[2] = u32x4{R.d[8], R.d[9], R.d[10], R.d[11]};
+          q[3] = u32x4{R.d[12], R.d[13], R.d[14], R.d[15]};
+          stage_match[r - stage_first] = mslot;
+        } else if (r < p.max_records) {
           rec_store(p.records + r, R);
           if (p.match_out) p.match_out[r] = mslot;
         }
@@ -525,10 +535,10 @@ struct TileCtx {
   uint32_t H[16];  // datagram bytes 0..64
 };
 
-// load this lane's (offset, length), build the workgroup's buffer descriptor
-// (base = min offset of the tile) and the 64-byte head
-__device__ __forceinline__ void load_tile(const KParams& p, uint32_t tile, uint64_t* s_min_off, TileCtx& t) {
-  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+// load this lane's (offset, length), build the wave's buffer descriptor
+// (base = min offset over the wave: no workgroup barrier) and the 64-byte head
+__device__ __forceinline__ void load_tile(const KParams& p, uint32_t tile, TileCtx& t) {
+  const uint32_t tid = threadIdx.x;
   t.i = tile * TILE + tid;
   t.valid = t.i < p.n;
   const uint64_t off = t.valid ? p.dgram_off[t.i] : ~0ull;
@@ -539,10 +549,7 @@ __device__ __forceinline__ void load_tile(const KParams& p, uint32_t tile, uint6
     uint64_t y = __shfl_xor(m, d, 64);
     m = y < m ? y : m;
   }
-  if (lane == 0) atomicMin(reinterpret_cast<unsigned long long*>(s_min_off), (unsigned long long)m);
-  __syncthreads();
-  uint64_t tb = *s_min_off;
-  if (tb > p.arena_len) tb = p.arena_len;
+  uint64_t tb = m > p.arena_len ? p.arena_len : m;
   uint32_t tb_lo = __builtin_amdgcn_readfirstlane((uint32_t)tb);
   uint32_t tb_hi = __builtin_amdgcn_readfirstlane((uint32_t)(tb >> 32));
   tb = ((uint64_t)tb_hi << 32) | tb_lo;
@@ -573,30 +580,26 @@ __device__ __forceinline__ uint32_t count_lane(const KParams& p, TileCtx& t, uin
   return st;
 }
 
-// scratch layout (bytes): u32 info[n_tiles] | u64 prefix[n_tiles] | u32 ctl[4]
+// scratch layout: u32 info[n_tiles] = records of the tile | nonspec << 31
 struct Scratch {
-  uint32_t* info;    // count | nonspec << 31
-  uint64_t* prefix;  // exclusive record prefix per tile
-  uint32_t* ctl;     // [0] first non-speculative tile
+  uint32_t* info;
 };
-__device__ __forceinline__ Scratch scratch_of(uint64_t* base, uint32_t n_tiles) {
+__device__ __forceinline__ Scratch scratch_of(uint64_t* base, uint32_t) {
   Scratch x;
   x.info = reinterpret_cast<uint32_t*>(base);
-  x.prefix = base + ((n_tiles + 1u) / 2u);
-  x.ctl = reinterpret_cast<uint32_t*>(x.prefix + n_tiles);
   return x;
 }
 
+constexpr uint32_t STAGE_RECS = TILE;  // LDS staging for speculative tiles with k_spec == 1
 __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_spec_kernel(KParams p, uint32_t n_tiles,
                                                                                      uint32_t k_spec) {
-  __shared__ uint64_t s_min_off;
   __shared__ uint32_t s_wave_sum[WAVES], s_wave_bad[WAVES];
+  __shared__ u32x4 s_stage[STAGE_RECS * 4];
+  __shared__ uint16_t s_stage_match[STAGE_RECS];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const uint32_t tile = blockIdx.x;
-  if (tid == 0) s_min_off = ~0ull;
-  __syncthreads();
   TileCtx t;
-  load_tile(p, tile, &s_min_off, t);
+  load_tile(p, tile, t);
   uint32_t cnt;
   const uint32_t st = count_lane(p, t, cnt);
   const uint32_t incl = wave_incl_scan(cnt, lane);
@@ -612,68 +615,84 @@ __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_spec_ker
     nonspec |= s_wave_bad[w];
   }
   Scratch x = scratch_of(p.scratch, n_tiles);
-  if (tid == 0) x.info[tile] = agg | (nonspec << 31);
+  if (tid == 0) x.info[tile] = agg | (nonspec << 31);  // read by kernel B (next launch)
   if (t.valid) p.status[t.i] = (uint8_t)st;
   if (!nonspec) {
-    const uint64_t my_first = (uint64_t)tile * TILE * k_spec + wave_off + (incl - cnt);
+    const uint64_t tile_first = (uint64_t)tile * TILE * k_spec;
+    const uint64_t my_first = tile_first + wave_off + (incl - cnt);
+    const bool stage = k_spec == 1u;  // agg == valid datagrams <= STAGE_RECS
     if (t.valid) {
       if (p.rec_begin) p.rec_begin[t.i] = (uint32_t)my_first;
       if (cnt) {
         uint32_t n2;
-        walk<true>(p, t.s, t.H, t.L, t.i, my_first, n2);
+        if (stage) walk<true>(p, t.s, t.H, t.L, t.i, my_first, n2, s_stage, s_stage_match, tile_first);
+        else walk<true>(p, t.s, t.H, t.L, t.i, my_first, n2);
       }
     }
+    if (stage) {  // coalesced copy-out: 16 B per lane, contiguous per wave instruction
+      __syncthreads();
+      const uint64_t lim = p.max_records > tile_first ? p.max_records - tile_first : 0;
+      const uint32_t nrec = agg < lim ? agg : (uint32_t)lim;
+      u32x4* dst = reinterpret_cast<u32x4*>(p.records + tile_first);
+      for (uint32_t k = tid; k < nrec * 4u; k += TILE) dst[k] = s_stage[k];
+      if (p.match_out)
+        for (uint32_t k = tid; k < nrec; k += TILE) p.match_out[tile_first + k] = s_stage_match[k];
+    }
   }
 }
 
-constexpr uint32_t SCAN_THREADS = 1024;
-__global__ __launch_bounds__(SCAN_THREADS) void rtps_tile_scan_kernel(uint64_t* scratch, uint32_t n_tiles,
-                                                                      uint64_t* n_records) {
-  __shared__ uint64_t s_part[SCAN_THREADS / 64];
-  __shared__ uint32_t s_first;
-  Scratch x = scratch_of(scratch, n_tiles);
+// sum of info[lo, hi) counts and min non-speculative index, over the workgroup
+__device__ __forceinline__ void reduce_info(const uint32_t* info, uint32_t lo, uint32_t hi, uint64_t* s_sum,
+                                            uint32_t* s_min, uint64_t& sum, uint32_t& first_bad) {
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  if (tid == 0) s_first = n_tiles;
-  __syncthreads();
-  uint64_t carry = 0;
-  for (uint32_t t0 = 0; t0 < n_tiles; t0 += SCAN_THREADS) {
-    const uint32_t t = t0 + tid;
-    const uint32_t info = t < n_tiles ? x.info[t] : 0u;
-    if (t < n_tiles && (info >> 31)) atomicMin(&s_first, t);
-    uint64_t v = info & 0x7fffffffu, incl = v;
+  uint64_t acc = 0;
+  uint32_t fb = 0xffffffffu;
+  for (uint32_t t = lo + tid; t < hi; t += TILE) {
+    uint32_t v = info[t];
+    acc += v & 0x7fffffffu;
+    if ((v >> 31) && t < fb) fb = t;
+  }
 #pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-      uint64_t y = __shfl_up(incl, d, 64);
-      if (lane >= d) incl += y;
-    }
-    if (lane == 63) s_part[wave] = incl;
-    __syncthreads();
-    uint64_t before = carry, total = carry;
-    for (uint32_t w = 0; w < SCAN_THREADS / 64; ++w) {
-      if (w < wave) before += s_part[w];
-      total += s_part[w];
-    }
-    if (t < n_tiles) x.prefix[t] = before + incl - v;
-    carry = total;
-    __syncthreads();
+  for (uint32_t d = 32; d >= 1; d >>= 1) {
+    acc += __shfl_xor(acc, d, 64);
+    uint32_t y = __shfl_xor(fb, d, 64);
+    fb = y < fb ? y : fb;
   }
-  if (tid == 0) {
-    x.ctl[0] = s_first;
-    *n_records = carry;
+  if (lane == 0) { s_sum[wave] = acc; s_min[wave] = fb; }
+  __syncthreads();
+  sum = 0;
+  first_bad = 0xffffffffu;
+#pragma unroll
+  for (uint32_t w = 0; w < WAVES; ++w) {
+    sum += s_sum[w];
+    first_bad = s_min[w] < first_bad ? s_min[w] : first_bad;
   }
+  __syncthreads();
 }
 
+// Kernel B: every workgroup first reduces the tile counts of kernel A (16 KB
+// per 1M datagrams, L2-resident) to find the first non-speculative tile f and
+// the total; workgroup 0 publishes the total.  Tiles f.. are then re-walked in
+// a grid-stride loop, each at its exact prefix.
 __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_fix_kernel(KParams p, uint32_t n_tiles) {
-  __shared__ uint64_t s_min_off;
   __shared__ uint32_t s_wave_sum[WAVES];
+  __shared__ uint64_t s_rsum[WAVES];
+  __shared__ uint32_t s_rmin[WAVES];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   Scratch x = scratch_of(p.scratch, n_tiles);
-  const uint32_t first = __builtin_amdgcn_readfirstlane(x.ctl[0]);
-  for (uint32_t tile = first + blockIdx.x; tile < n_tiles; tile += gridDim.x) {
-    if (tid == 0) s_min_off = ~0ull;
-    __syncthreads();
+  uint64_t total;
+  uint32_t first;
+  reduce_info(x.info, 0, n_tiles, s_rsum, s_rmin, total, first);
+  if (blockIdx.x == 0 && tid == 0) *p.n_records = total;
+  if (first > n_tiles) first = n_tiles;
+  uint32_t tile = first + blockIdx.x;
+  if (tile >= n_tiles) return;
+  uint64_t prefix, dummy_sum;
+  uint32_t dummy_min;
+  reduce_info(x.info, 0, tile, s_rsum, s_rmin, prefix, dummy_min);
+  for (;;) {
     TileCtx t;
-    load_tile(p, tile, &s_min_off, t);
+    load_tile(p, tile, t);
     uint32_t cnt;
     const uint32_t st = count_lane(p, t, cnt);
     const uint32_t incl = wave_incl_scan(cnt, lane);
@@ -683,7 +702,7 @@ __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_fix_kern
 #pragma unroll
     for (uint32_t w = 0; w < WAVES; ++w)
       if (w < wave) wave_off += s_wave_sum[w];
-    const uint64_t my_first = x.prefix[tile] + wave_off + (incl - cnt);
+    const uint64_t my_first = prefix + wave_off + (incl - cnt);
     if (t.valid) {
       if (p.rec_begin) p.rec_begin[t.i] = (uint32_t)my_first;
       if (st == RTPS_DGRAM_OK && cnt) {
@@ -691,7 +710,12 @@ __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_fix_kern
         walk<true>(p, t.s, t.H, t.L, t.i, my_first, n2);
       }
     }
-    __syncthreads();  // s_min_off / s_wave_sum reuse
+    __syncthreads();  // s_wave_sum reuse
+    const uint32_t next = tile + gridDim.x;
+    if (next >= n_tiles) break;
+    reduce_info(x.info, tile, next, s_rsum, s_rmin, dummy_sum, dummy_min);
+    prefix += dummy_sum;
+    tile = next;
   }
 }
 
@@ -841,8 +865,9 @@ int rtps_rx_create(const rtps_rx_config* cfg, rtps_rx_ctx** out_ctx) {
   }
   size_t tiles = ((size_t)cfg->max_datagrams + TILE - 1) / TILE;
   if (tiles == 0) tiles = 1;
-  c->scratch_words = (tiles + 1) / 2 + tiles + 2;  // u32 info[tiles] | u64 prefix[tiles] | u32 ctl[4]
-  if (hipMalloc(&c->scratch, c->scratch_words * sizeof(uint64_t)) != hipSuccess) {
+  c->scratch_words = (tiles + 1) / 2 + 2;  // u32 info[tiles]
+  if (hipMalloc(&c->scratch, c->scratch_words * sizeof(uint64_t)) != hipSuccess ||
+      hipMemset(c->scratch, 0, c->scratch_words * sizeof(uint64_t)) != hipSuccess) {
     (void)hipStreamDestroy(c->own_stream);
     delete c;
     return RTPS_RX_ENOMEM;
@@ -942,8 +967,6 @@ int rtps_rx_parse_batch(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len
   p.mt_mask = c->mt_active ? c->mt_cap - 1 : 0;
   p.scratch = c->scratch;
   hipLaunchKernelGGL(rtps_parse_spec_kernel, dim3(tiles), dim3(TILE), 0, c->stream, p, tiles, c->k_spec);
-  hipLaunchKernelGGL(rtps_tile_scan_kernel, dim3(1), dim3(SCAN_THREADS), 0, c->stream, c->scratch, tiles,
-                     out->n_records);
   uint32_t grid = tiles < c->resident_blocks ? tiles : c->resident_blocks;
   hipLaunchKernelGGL(rtps_parse_fix_kernel, dim3(grid), dim3(TILE), 0, c->stream, p, tiles);
   return hip_fail(hipGetLastError());
