@@ -71,6 +71,45 @@ def algorithmic_bytes(status, recs, n, record_bytes=64):
     return reads + writes, reads, writes
 
 
+def pmc_traffic(workload):
+    """Calibrated HBM bytes per launch from the committed rocprofv3 PMC profile (profiles/)."""
+    path = os.path.join(REPO, "profiles", f"r1_pmc_{workload}.json")
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        d = json.load(f)
+    return d.get("parse_traffic_bytes"), os.path.relpath(path, REPO)
+
+
+def end_to_end(rx, arena, off_t, ln_t, n, outs, n_rec, stream, reps=5):
+    """Host-memory-in / host-memory-out rate: pinned H2D of the arena + parse +
+    D2H of status and records (the path starts in io_uring receive buffers and
+    ends in the history cache).  Returned separately: never the headline value."""
+    host_arena = torch.empty(arena.numel(), dtype=torch.uint8, pin_memory=True)
+    host_arena.copy_(arena)
+    host_status = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    host_recs = torch.empty((max(n_rec, 1), 64), dtype=torch.uint8, pin_memory=True)
+    torch.cuda.synchronize()
+    times = []
+    for _ in range(reps):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        arena.copy_(host_arena, non_blocking=True)
+        rx.parse_batch_device(arena, off_t, ln_t, n, outs)
+        host_status.copy_(outs["status"][:n], non_blocking=True)
+        host_recs[:n_rec].copy_(outs["records"][:n_rec], non_blocking=True)
+        e1.record(stream)
+        e1.synchronize()
+        times.append(e0.elapsed_time(e1) * 1e-3)
+    t = min(times)
+    h2d = arena.numel()
+    d2h = n + n_rec * 64
+    return {"datagrams_per_s": n / t, "ms": t * 1e3, "h2d_bytes": h2d, "d2h_bytes": d2h,
+            "pcie_gb_per_s": (h2d + d2h) / t / 1e9,
+            "note": "pinned H2D of the whole arena + parse + D2H of status and records, one stream, min of reps"}
+
+
 def cpu_baseline(workload, n, target_cpu_s=10.0):
     """The oracle (C restatement of the reference parse) on this host's cores."""
     import oracle
@@ -102,6 +141,7 @@ def main():
     ap.add_argument("--writers", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-e2e", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -137,22 +177,16 @@ def main():
     outs = rx.alloc_outputs(n, n_rec)
     del probe
     exch = None
+    received = {}
     if world > 1:
-        exch = {"bucketed": torch.empty((max(n_rec, 1), 64), dtype=torch.uint8, device=dev),
-                "counts": torch.zeros(world, dtype=torch.int64, device=dev),
-                "recv_counts": torch.zeros(world, dtype=torch.int64, device=dev)}
+        from rtps_rx.shard import Exchange
+        exch = Exchange(rx, n_rec, world, dist, dev)
 
     def step():
         rx.parse_batch_device(arena, off_t, ln_t, n, outs)
         if world > 1:
-            rx.bucket_by_writer(outs, world, exch["bucketed"], exch["counts"])
-            dist.all_to_all_single(exch["recv_counts"], exch["counts"])
-            send = exch["counts"].tolist()
-            recv = exch["recv_counts"].tolist()
-            nsend = sum(send)
-            out = torch.empty((sum(recv), 64), dtype=torch.uint8, device=dev)
-            dist.all_to_all_single(out, exch["bucketed"][:nsend], recv, send)
-            exch["received"] = out
+            exch.bucket(outs)
+            received["records"], received["split"] = exch.exchange()
 
     for _ in range(args.warmup):
         step()
@@ -183,6 +217,7 @@ def main():
     status = outs["status"][:n].cpu().numpy()
     recs = outs["records"][:n_rec].cpu().numpy().reshape(-1).view(RECORD_DTYPE)
     alg_total, alg_reads, alg_writes = algorithmic_bytes(status, recs, n)
+    traffic, traffic_src = pmc_traffic(args.workload) if world == 1 else (None, None)
     total_bytes = float(ln.astype(np.int64).sum())
     ms_per_step = wall / args.steps * 1e3
     value = world * n / (wall / args.steps)
@@ -206,15 +241,18 @@ def main():
                    "parallelism": f"{world} ranks, datagram-sharded" + (
                        ", writer-GUID all-to-all (RCCL)" if world > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": alg_total / (ev_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": alg_total / (ev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "rtps_parse_kernel", "kernel_ms": ev_ms,
+                     "unit": "GB/s", "frac": alg_total / (ev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "kernel": "rtps_parse_spec_kernel + rtps_parse_fix_kernel (one launch pair)", "kernel_ms": ev_ms,
                      "alg_bytes_per_launch": alg_total, "alg_read_bytes": alg_reads, "alg_write_bytes": alg_writes,
                      "note": "zero-copy parse: payload bytes are not read (the reference's Bytes::split_off is "
                              "zero-copy too); alg bytes = header/fixed-field reads + record writes"},
     }
     if world > 1:
         result["roofline"]["note"] += "; kernel_ms here is the whole step (parse + bucket + all-to-all)"
-        result["config"]["received_records_rank0"] = int(exch["received"].shape[0])
+        result["config"]["received_records_rank0"] = int(received["records"].shape[0])
+    if world == 1 and not args.no_e2e:
+        result["end_to_end"] = end_to_end(rx, arena, off_t, ln_t, n, outs, n_rec, stream)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.workload, n, args.cpu_seconds)
     if rank == 0:

@@ -7,7 +7,7 @@ import torch, rtps_rx
 D = ctypes.CDLL(os.path.join(REPO, "build", "libdiag_ceiling.so"))
 D.diag_ceiling.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 3 + [ctypes.c_uint32] + [ctypes.c_void_p] * 4
 dev = torch.device("cuda", 0)
-for wlname in ("T", "C2"):
+for wlname in (sys.argv[1:] or ["T", "C2"]):
     wl = rtps_rx.WORKLOADS[wlname]
     n = 1 << 20
     off, ln, size = rtps_rx.gen_layout(wl, n)

@@ -1,0 +1,58 @@
+"""World-size-N check of the full sharded path on GPU(s): each rank generates
+its chunk on the device, parses it, buckets by writer GUID on the device and
+exchanges records (gloo on a 1-GPU box, nccl=RCCL across GPUs); every rank
+verifies what it received against the CPU oracle.  Launch with
+python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 scripts/shard_check.py [backend]"""
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "rustdds-io_uring_amd"), os.path.join(REPO, "tests")]
+import torch
+import torch.distributed as dist
+
+import oracle
+import rtps_rx
+from rtps_rx.records import RECORD_DTYPE
+from rtps_rx.shard import Exchange
+from shard_ref import owner_np
+
+backend = sys.argv[1] if len(sys.argv) > 1 else "gloo"
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+ngpu = torch.cuda.device_count()
+dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")) % ngpu)
+torch.cuda.set_device(dev)
+dist.init_process_group(backend)
+n = 20000
+off, ln, size = rtps_rx.gen_layout(rtps_rx.WL_C3, n, first_idx=rank * n)
+rx = rtps_rx.MessageReceiver(oracle.OWN_PREFIX, device=dev.index, max_datagrams=n)
+st = torch.cuda.Stream(dev)
+torch.cuda.set_stream(st)
+rx.set_stream(st)
+arena = torch.zeros(size, dtype=torch.uint8, device=dev)
+off_t = torch.from_numpy(off.view(np.int64)).to(dev)
+ln_t = torch.from_numpy(ln.view(np.int32)).to(dev)
+rx.generate(rtps_rx.WL_C3, arena, off_t, ln_t, n, first_idx=rank * n)
+cap = rtps_rx.max_records(ln)
+outs = rx.alloc_outputs(n, cap)
+rx.parse_batch_device(arena, off_t, ln_t, n, outs)
+ex = Exchange(rx, cap, world, dist, dev)
+ex.bucket(outs)
+torch.cuda.synchronize(dev)
+got, split = ex.exchange()
+torch.cuda.synchronize(dev)
+got = got.cpu().numpy().reshape(-1).view(RECORD_DTYPE)
+exp = []
+for r in range(world):
+    a, o, l = oracle.gen(oracle.WL_C3, n, first_idx=r * n)
+    _, recs, _, _ = oracle.parse(a, o, l)
+    exp.append(recs[owner_np(recs, world) == rank])
+exp = np.concatenate(exp)
+ok = got.tobytes() == exp.tobytes()
+print(f"rank {rank}/{world} ({backend}): received {len(got)} records, expected {len(exp)}, "
+      f"{'OK' if ok else 'MISMATCH'}", flush=True)
+dist.barrier()
+dist.destroy_process_group()
+sys.exit(0 if ok else 1)

@@ -1,0 +1,25 @@
+"""numpy reference of the writer-GUID owner hash and stable bucketing (test helper)."""
+import numpy as np
+
+from rtps_rx.records import WRITER_KINDS, READER_KINDS
+
+
+def owner_np(recs, world):
+    w = recs.view(np.uint32).reshape(-1, 16)[:, 2:6].astype(np.uint64)
+    h = np.full(len(recs), 0x811C9DC5, dtype=np.uint64)
+    for k in range(4):
+        h = ((h ^ w[:, k]) * np.uint64(0x01000193)) & np.uint64(0xFFFFFFFF)
+    h ^= h >> np.uint64(15)
+    owner = (h % np.uint64(world)).astype(np.int64)
+    exch = np.isin(recs["kind"], WRITER_KINDS + READER_KINDS)
+    return np.where(exch, owner, -1)
+
+
+def bucket_np(recs, world):
+    """(bucketed records, counts per destination): stable partition by owner."""
+    o = owner_np(recs, world)
+    keep = o >= 0
+    idx = np.nonzero(keep)[0]
+    order = idx[np.argsort(o[keep], kind="stable")]
+    counts = np.bincount(o[keep], minlength=world).astype(np.int64)
+    return recs[order], counts
