@@ -580,19 +580,27 @@ __device__ __forceinline__ uint32_t count_lane(const KParams& p, TileCtx& t, uin
   return st;
 }
 
-// scratch layout: u32 info[n_tiles] = records of the tile | nonspec << 31
+// scratch layout (all written before being read in every launch, except flag[]):
+//   u32 flag[4]          flag[parity] = 1 if any tile of the launch is non-speculative
+//                        (plain stores of the same value); kernel B clears flag[parity ^ 1]
+//   u32 info[n_tiles]    records of the tile | nonspec << 31
+//   u16 dcount[n]        records per datagram, written for non-speculative tiles only
 struct Scratch {
+  uint32_t* flag;
   uint32_t* info;
+  uint16_t* dcount;
 };
-__device__ __forceinline__ Scratch scratch_of(uint64_t* base, uint32_t) {
+__device__ __forceinline__ Scratch scratch_of(uint64_t* base, uint32_t n_tiles) {
   Scratch x;
-  x.info = reinterpret_cast<uint32_t*>(base);
+  x.flag = reinterpret_cast<uint32_t*>(base);
+  x.info = x.flag + 4;
+  x.dcount = reinterpret_cast<uint16_t*>(x.info + ((n_tiles + 3u) & ~3u));
   return x;
 }
 
 constexpr uint32_t STAGE_RECS = TILE;  // LDS staging for speculative tiles with k_spec == 1
 __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_spec_kernel(KParams p, uint32_t n_tiles,
-                                                                                     uint32_t k_spec) {
+                                                                                     uint32_t k_spec, uint32_t parity) {
   __shared__ uint32_t s_wave_sum[WAVES], s_wave_bad[WAVES];
   __shared__ u32x4 s_stage[STAGE_RECS * 4];
   __shared__ uint16_t s_stage_match[STAGE_RECS];
@@ -615,8 +623,14 @@ __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_spec_ker
     nonspec |= s_wave_bad[w];
   }
   Scratch x = scratch_of(p.scratch, n_tiles);
-  if (tid == 0) x.info[tile] = agg | (nonspec << 31);  // read by kernel B (next launch)
-  if (t.valid) p.status[t.i] = (uint8_t)st;
+  if (tid == 0) {
+    x.info[tile] = agg | (nonspec << 31);  // read by kernel B (next launch)
+    if (nonspec) x.flag[parity] = 1u;
+  }
+  if (t.valid) {
+    p.status[t.i] = (uint8_t)st;
+    if (nonspec) x.dcount[t.i] = (uint16_t)cnt;
+  }
   if (!nonspec) {
     const uint64_t tile_first = (uint64_t)tile * TILE * k_spec;
     const uint64_t my_first = tile_first + wave_off + (incl - cnt);
@@ -674,12 +688,19 @@ __device__ __forceinline__ void reduce_info(const uint32_t* info, uint32_t lo, u
 // per 1M datagrams, L2-resident) to find the first non-speculative tile f and
 // the total; workgroup 0 publishes the total.  Tiles f.. are then re-walked in
 // a grid-stride loop, each at its exact prefix.
-__global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_fix_kernel(KParams p, uint32_t n_tiles) {
+__global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_fix_kernel(KParams p, uint32_t n_tiles,
+                                                                                    uint32_t k_spec, uint32_t parity) {
   __shared__ uint32_t s_wave_sum[WAVES];
   __shared__ uint64_t s_rsum[WAVES];
   __shared__ uint32_t s_rmin[WAVES];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   Scratch x = scratch_of(p.scratch, n_tiles);
+  if (blockIdx.x == 0 && tid == 0) x.flag[parity ^ 1u] = 0u;  // for the next launch
+  if (__builtin_amdgcn_readfirstlane(x.flag[parity]) == 0u) {
+    // every tile was speculative: every datagram has exactly k_spec records
+    if (blockIdx.x == 0 && tid == 0) *p.n_records = (uint64_t)p.n * k_spec;
+    return;
+  }
   uint64_t total;
   uint32_t first;
   reduce_info(x.info, 0, n_tiles, s_rsum, s_rmin, total, first);
@@ -691,10 +712,12 @@ __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_fix_kern
   uint32_t dummy_min;
   reduce_info(x.info, 0, tile, s_rsum, s_rmin, prefix, dummy_min);
   for (;;) {
-    TileCtx t;
-    load_tile(p, tile, t);
-    uint32_t cnt;
-    const uint32_t st = count_lane(p, t, cnt);
+    const uint32_t info = x.info[tile];
+    const uint32_t i = tile * TILE + tid;
+    // non-speculative tiles stored their per-datagram counts; speculative tiles
+    // (after the first non-speculative one) have exactly k_spec per datagram
+    uint32_t cnt = 0;
+    if (i < p.n) cnt = (info >> 31) ? (uint32_t)x.dcount[i] : k_spec;
     const uint32_t incl = wave_incl_scan(cnt, lane);
     if (lane == 63) s_wave_sum[wave] = incl;
     __syncthreads();
@@ -703,9 +726,11 @@ __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_fix_kern
     for (uint32_t w = 0; w < WAVES; ++w)
       if (w < wave) wave_off += s_wave_sum[w];
     const uint64_t my_first = prefix + wave_off + (incl - cnt);
+    TileCtx t;
+    load_tile(p, tile, t);
     if (t.valid) {
       if (p.rec_begin) p.rec_begin[t.i] = (uint32_t)my_first;
-      if (st == RTPS_DGRAM_OK && cnt) {
+      if (cnt) {  // cnt > 0 implies status OK
         uint32_t n2;
         walk<true>(p, t.s, t.H, t.L, t.i, my_first, n2);
       }
@@ -839,6 +864,7 @@ struct rtps_rx_ctx {
   uint32_t* bucket_hist = nullptr;
   size_t bucket_bytes = 0;
   uint32_t resident_blocks = 1024;
+  uint32_t launch_parity = 0;
   uint32_t k_spec = 1;  // speculated records per datagram (0 disables nothing: see set_spec_hint)
 };
 
@@ -865,7 +891,8 @@ int rtps_rx_create(const rtps_rx_config* cfg, rtps_rx_ctx** out_ctx) {
   }
   size_t tiles = ((size_t)cfg->max_datagrams + TILE - 1) / TILE;
   if (tiles == 0) tiles = 1;
-  c->scratch_words = (tiles + 1) / 2 + 2;  // u32 info[tiles]
+  // u32 flag[4] | u32 info[tiles rounded to 4] | u16 dcount[max_datagrams]
+  c->scratch_words = 2 + ((tiles + 3) & ~(size_t)3) / 2 + ((size_t)cfg->max_datagrams + 3) / 4 + 2;
   if (hipMalloc(&c->scratch, c->scratch_words * sizeof(uint64_t)) != hipSuccess ||
       hipMemset(c->scratch, 0, c->scratch_words * sizeof(uint64_t)) != hipSuccess) {
     (void)hipStreamDestroy(c->own_stream);
@@ -966,9 +993,11 @@ int rtps_rx_parse_batch(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len
   p.mt_slots = c->mt_slots;
   p.mt_mask = c->mt_active ? c->mt_cap - 1 : 0;
   p.scratch = c->scratch;
-  hipLaunchKernelGGL(rtps_parse_spec_kernel, dim3(tiles), dim3(TILE), 0, c->stream, p, tiles, c->k_spec);
+  const uint32_t parity = c->launch_parity;
+  c->launch_parity ^= 1u;
+  hipLaunchKernelGGL(rtps_parse_spec_kernel, dim3(tiles), dim3(TILE), 0, c->stream, p, tiles, c->k_spec, parity);
   uint32_t grid = tiles < c->resident_blocks ? tiles : c->resident_blocks;
-  hipLaunchKernelGGL(rtps_parse_fix_kernel, dim3(grid), dim3(TILE), 0, c->stream, p, tiles);
+  hipLaunchKernelGGL(rtps_parse_fix_kernel, dim3(grid), dim3(TILE), 0, c->stream, p, tiles, c->k_spec, parity);
   return hip_fail(hipGetLastError());
 }
 

@@ -188,14 +188,19 @@ class MessageReceiver:
         }
 
     def parse_batch_device(self, arena, off, lens, n, outs, want_match=True, want_rec_begin=True):
-        """arena u8 / off i64 / lens i32 torch CUDA tensors; asynchronous."""
-        o = _Out()
-        o.status = outs["status"].data_ptr()
-        o.records = outs["records"].data_ptr()
-        o.max_records = outs["max_records"]
-        o.match = outs["match"].data_ptr() if want_match else None
-        o.rec_begin = outs["rec_begin"].data_ptr() if want_rec_begin else None
-        o.n_records = outs["n_records"].data_ptr()
+        """arena u8 / off i64 / lens i32 tensors (HBM, or pinned host memory for a
+        zero-copy parse); outputs likewise.  Asynchronous on the context's stream."""
+        key = (want_match, want_rec_begin)
+        o = outs.get("_c_out", {}).get(key)
+        if o is None:
+            o = _Out()
+            o.status = outs["status"].data_ptr()
+            o.records = outs["records"].data_ptr()
+            o.max_records = outs["max_records"]
+            o.match = outs["match"].data_ptr() if want_match else None
+            o.rec_begin = outs["rec_begin"].data_ptr() if want_rec_begin else None
+            o.n_records = outs["n_records"].data_ptr()
+            outs.setdefault("_c_out", {})[key] = o
         _check(lib().rtps_rx_parse_batch(self._h, arena.data_ptr(), arena.numel(), off.data_ptr(),
                                          lens.data_ptr(), n, ctypes.byref(o)))
 

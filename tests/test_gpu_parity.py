@@ -285,3 +285,26 @@ def test_sharded_path_two_ranks_gloo():
                        capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert r.stdout.count(" OK") == 2
+
+
+@pytest.mark.parametrize("wl", [1, 3])
+def test_zero_copy_host_memory(rx, wl):
+    """Arena, offsets, lengths and all outputs in pinned host memory (zero-copy over PCIe)."""
+    arena, off, ln = oracle.gen(wl, 20000)
+    A = torch.from_numpy(arena).pin_memory()
+    O = torch.from_numpy(off.view(np.int64)).pin_memory()
+    L = torch.from_numpy(ln.view(np.int32)).pin_memory()
+    cap = max_records(ln)
+    outs = {"status": torch.empty(len(ln), dtype=torch.uint8).pin_memory(),
+            "records": torch.empty((cap, 64), dtype=torch.uint8).pin_memory(),
+            "match": torch.empty(cap, dtype=torch.int16).pin_memory(),
+            "rec_begin": torch.empty(len(ln), dtype=torch.int32).pin_memory(),
+            "n_records": torch.zeros(1, dtype=torch.int64).pin_memory(), "max_records": cap}
+    rx.parse_batch_device(A, O, L, len(ln), outs)
+    rx.sync()
+    st, recs, match, rb = oracle.parse(arena, off, ln)
+    n = int(outs["n_records"][0])
+    assert n == len(recs)
+    assert np.array_equal(outs["status"].numpy(), st)
+    assert outs["records"][:n].numpy().tobytes() == recs.view(np.uint8).tobytes()
+    assert np.array_equal(outs["rec_begin"].numpy().view(np.uint32), rb)
