@@ -131,6 +131,36 @@ def end_to_end(rx, arena, off_t, ln_t, n, outs, n_rec, stream, reps=5):
     return res
 
 
+CDR_TYPES = {"T": "TSample", "C2": "C2Sample", "C3": "ShapeType", "C4": "C2Sample"}
+
+
+def cdr_decode_leg(rx, workload, arena, off_t, outs, n_rec, stream, steps):
+    """a18: batch CDR decode of this batch's DATA payloads into fixed-layout rows,
+    timed separately from the parse step (HIP events on the launch stream)."""
+    from rtps_rx import cdr
+    t = getattr(cdr, CDR_TYPES[workload])
+    rows, row_status = rx.alloc_rows(t, n_rec)
+    for _ in range(3):
+        rx.cdr_decode(t, arena, off_t, outs, rows, row_status)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    torch.cuda.synchronize()
+    for a, b in ev:
+        a.record(stream)
+        rx.cdr_decode(t, arena, off_t, outs, rows, row_status)
+        b.record(stream)
+    torch.cuda.synchronize()
+    ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    st = row_status[:n_rec].cpu().numpy()
+    ok = int((st == cdr.CDR_OK).sum())
+    # algorithmic bytes: 40 B of each record read, 1 status byte + one row written per record,
+    # and for decoded rows the value bytes consumed (= row_bytes for these all-primitive types)
+    alg = n_rec * (40 + 1 + t.row_bytes) + ok * t.row_bytes
+    return {"sample_type": CDR_TYPES[workload], "row_bytes": t.row_bytes, "records": n_rec, "decoded_ok": ok,
+            "status_hist": np.bincount(st, minlength=7).tolist(), "kernel": "cdr_decode_kernel", "kernel_ms": ms,
+            "rows_per_s": ok / (ms * 1e-3), "alg_bytes_per_launch": alg,
+            "achieved_gbs": alg / (ms * 1e-3) / 1e9, "frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+
+
 def cpu_baseline(workload, n, target_cpu_s=10.0):
     """The oracle (C restatement of the reference parse) on this host's cores."""
     import oracle
@@ -163,6 +193,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-cdr", action="store_true", help="skip the CDR decode (a18) measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -272,6 +303,8 @@ def main():
     if world > 1:
         result["roofline"]["note"] += "; kernel_ms here is the whole step (parse + bucket + all-to-all)"
         result["config"]["received_records_rank0"] = int(received["records"].shape[0])
+    if world == 1 and not args.no_cdr:
+        result["cdr_decode"] = cdr_decode_leg(rx, args.workload, arena, off_t, outs, n_rec, stream, args.steps)
     if world == 1 and not args.no_e2e:
         result["end_to_end"] = end_to_end(rx, arena, off_t, ln_t, n, outs, n_rec, stream)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -226,6 +226,48 @@ const char* rtps_rx_strerror(int code);
 int rtps_rx_bucket_by_writer(rtps_rx_ctx* ctx, const rtps_record* recs, const uint64_t* n_records,
                              uint64_t max_records, uint32_t n_dest, rtps_record* out, uint64_t* dest_counts);
 
+/* ---- batch CDR primitive decode (a18) ------------------------------------
+ * Replaces, for fixed-layout sample types, the per-sample decode
+ *   SimpleDataReader::deserialize_with -> DA::from_bytes_with(&payload.value, rep_id, ..)
+ *       io_uring/dds/with_key/simpledatareader.rs:137-160, dds/adapters.rs:128-139
+ *   -> deserialize_from_cdr_with_decoder_and_rep_id   serialization/cdr_adapters.rs:246-275
+ *   -> cdr_encoding::CdrDeserializer (external crate cdr-encoding 0.10)
+ * The type is a flat "program" of ops (a struct's fields in order; nested
+ * structs flatten because classic CDR aligns each primitive to its own size
+ * relative to the first byte after the 4-byte encapsulation header).  Every
+ * DATA record with payload_kind == RTPS_PK_DATA is decoded into a row of
+ * row_bytes at rows + record_index * row_bytes (host byte order). */
+enum rtps_cdr_op_kind {
+  RTPS_CDR_PRIM = 1,   /* size 1/2/4/8 (ints, f32, f64, char, enum=u32): out `size` bytes        */
+  RTPS_CDR_BOOL = 2,   /* 1 byte, must be 0 or 1: out 1 byte                                    */
+  RTPS_CDR_STRING = 3, /* u32 length incl. NUL + bytes, UTF-8 checked: out u32 len + char[count] */
+  RTPS_CDR_SEQ = 4,    /* u32 n + n primitives of `size` (n <= count): out u32 n + size*count     */
+  RTPS_CDR_ARRAY = 5   /* count primitives of `size`, no length: out size*count                  */
+};
+typedef struct rtps_cdr_op {
+  uint8_t kind;      /* rtps_cdr_op_kind */
+  uint8_t size;      /* primitive size for PRIM / SEQ / ARRAY */
+  uint16_t _r;
+  uint32_t count;    /* STRING: char slot capacity; SEQ: max elements; ARRAY: elements */
+  uint32_t out_off;  /* byte offset of the field in the output row */
+} rtps_cdr_op;
+enum rtps_cdr_status {
+  RTPS_CDR_OK = 0,
+  RTPS_CDR_NOT_DATA = 1,        /* record is not a DATA with payload_kind == RTPS_PK_DATA   */
+  RTPS_CDR_BAD_ENCODING = 2,    /* rep id not in {CDR_BE, CDR_LE, PL_CDR_LE} (cdr_adapters.rs:96-100) */
+  RTPS_CDR_EOF = 3,             /* payload ends before the type does                        */
+  RTPS_CDR_BAD_BOOL = 4,        /* bool byte not 0/1                                        */
+  RTPS_CDR_BAD_UTF8 = 5,        /* string bytes are not UTF-8                               */
+  RTPS_CDR_TOO_LONG = 6         /* string/sequence longer than the row slot (not a reference error) */
+};
+#define RTPS_CDR_MAX_OPS 64u
+/* arena / dgram_off: the batch given to rtps_rx_parse_batch; records / n_records:
+ * its outputs.  rows: [max_records * row_bytes], row_status: [max_records]. */
+int rtps_rx_cdr_decode(rtps_rx_ctx* ctx, const rtps_cdr_op* prog, uint32_t n_ops, uint32_t row_bytes,
+                       const uint8_t* arena, uint64_t arena_len, const uint64_t* dgram_off,
+                       const rtps_record* records, const uint64_t* n_records, uint64_t max_records,
+                       uint8_t* rows, uint8_t* row_status);
+
 /* Upper bound on records for datagram lengths (host arrays): sum((len-20)/4). */
 uint64_t rtps_rx_max_records_host(const uint32_t* dgram_len, uint32_t n);
 

@@ -45,6 +45,8 @@ def lib():
         L.rtps_oracle_gen_fill.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
                                            ctypes.c_uint32, P, P]
         L.rtps_oracle_record_size.restype = ctypes.c_uint32
+        L.rtps_oracle_cdr_decode.restype = None
+        L.rtps_oracle_cdr_decode.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32, P, P, P, ctypes.c_uint64, P, P]
         assert L.rtps_oracle_record_size() == RECORD_DTYPE.itemsize
         _lib = L
     return _lib
@@ -96,3 +98,17 @@ def gen(workload, n, seed=SEED, first_idx=0, n_writers=16):
     arena = np.zeros(max(int(size), 16), dtype=np.uint8)
     lib().rtps_oracle_gen_fill(workload, seed, first_idx, n_writers, n, _ptr(offs), _ptr(arena))
     return arena, offs, lens
+
+
+def cdr_decode(sample_type, arena, offs, recs):
+    """CDR-decode every record's DATA payload (rtps_oracle_cdr_decode) -> (rows u8[m, row_bytes], status u8[m])."""
+    arena = np.ascontiguousarray(arena, dtype=np.uint8)
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    recs = np.ascontiguousarray(recs, dtype=RECORD_DTYPE)
+    m = len(recs)
+    rows = np.zeros((max(m, 1), sample_type.row_bytes), dtype=np.uint8)
+    status = np.zeros(max(m, 1), dtype=np.uint8)
+    ops = np.ascontiguousarray(sample_type.ops)
+    lib().rtps_oracle_cdr_decode(_ptr(ops), len(ops), sample_type.row_bytes, _ptr(arena), _ptr(offs),
+                                 _ptr(recs) if m else None, m, _ptr(rows), _ptr(status))
+    return rows[:m], status[:m]

@@ -633,3 +633,141 @@ void rtps_oracle_gen_fill(int wl, uint64_t seed, uint64_t first_idx, uint32_t n_
   for (uint32_t i = 0; i < n; ++i) rtps_gen_datagram(wl, seed, first_idx + i, n_writers, arena + off[i]);
 }
 uint32_t rtps_oracle_record_size(void) { return (uint32_t)sizeof(rtps_record); }
+
+/* ------------------------------------------------------------------------ */
+/* CDR primitive decode (a18)                                                */
+/*   deserialize_from_cdr_with_decoder_and_rep_id  serialization/cdr_adapters.rs:246-275 */
+/*   CDRDeserializerAdapter::supported_encodings    cdr_adapters.rs:96-100     */
+/*   -> external crate cdr-encoding 0.10 (not vendored): its published         */
+/*      CdrDeserializer rules are restated here: classic CDR, every primitive  */
+/*      aligned to its size relative to the first byte of the value (after the */
+/*      4-byte encapsulation), padding skipped only when an element is read,   */
+/*      string = u32 length incl. NUL + bytes (last byte dropped, contents     */
+/*      must be UTF-8: str::from_utf8), bool byte must be 0 or 1, sequence =   */
+/*      u32 count + elements, arrays have no length.  Parity pinned by the     */
+/*      ShapeType "RED" vector (rtps/message_receiver.rs:1250-1254); the rest  */
+/*      is "parity unpinned".                                                   */
+/* ------------------------------------------------------------------------ */
+typedef struct cdr_cur { const uint8_t* v; uint32_t len, pos; int le; } cdr_cur;
+
+static uint32_t cdr_pad(uint32_t pos, uint32_t a) { return (a - (pos % a)) % a; }
+static uint64_t cdr_get(const cdr_cur* c, uint32_t at, uint32_t size) {
+  uint64_t x = 0;
+  for (uint32_t k = 0; k < size; ++k) {
+    uint64_t b = c->v[at + k];
+    x |= c->le ? (b << (8 * k)) : (b << (8 * (size - 1 - k)));
+  }
+  return x;
+}
+/* std::str::from_utf8 acceptance */
+static int utf8_ok(const uint8_t* s, uint32_t m) {
+  uint32_t i = 0;
+  while (i < m) {
+    uint8_t c = s[i];
+    if (c < 0x80) { i++; continue; }
+    uint32_t need;
+    uint8_t lo = 0x80, hi = 0xBF;
+    if (c >= 0xC2 && c <= 0xDF) need = 1;
+    else if (c >= 0xE0 && c <= 0xEF) { need = 2; if (c == 0xE0) lo = 0xA0; if (c == 0xED) hi = 0x9F; }
+    else if (c >= 0xF0 && c <= 0xF4) { need = 3; if (c == 0xF0) lo = 0x90; if (c == 0xF4) hi = 0x8F; }
+    else return 0;
+    if (i + need >= m) return 0; /* needs bytes i+1 .. i+need < m */
+    if (s[i + 1] < lo || s[i + 1] > hi) return 0;
+    for (uint32_t k = 2; k <= need; ++k) if (s[i + k] < 0x80 || s[i + k] > 0xBF) return 0;
+    i += need + 1;
+  }
+  return 1;
+}
+
+static void cdr_store(uint8_t* row, uint32_t off, uint64_t x, uint32_t size) {
+  for (uint32_t k = 0; k < size; ++k) row[off + k] = (uint8_t)(x >> (8 * k)); /* host = little-endian */
+}
+
+static uint8_t cdr_decode_one(const rtps_cdr_op* prog, uint32_t n_ops, const uint8_t* value, uint32_t len, int le,
+                              uint8_t* row) {
+  cdr_cur c = {value, len, 0, le};
+  for (uint32_t k = 0; k < n_ops; ++k) {
+    const rtps_cdr_op* op = &prog[k];
+    uint32_t size = op->size;
+    switch (op->kind) {
+      case RTPS_CDR_PRIM:
+      case RTPS_CDR_ARRAY: {
+        uint32_t cnt = op->kind == RTPS_CDR_PRIM ? 1u : op->count;
+        if (cnt == 0) break;
+        uint32_t pad = cdr_pad(c.pos, size);
+        if ((uint64_t)c.pos + pad + (uint64_t)cnt * size > c.len) return RTPS_CDR_EOF;
+        c.pos += pad;
+        for (uint32_t e = 0; e < cnt; ++e) cdr_store(row, op->out_off + e * size, cdr_get(&c, c.pos + e * size, size), size);
+        c.pos += cnt * size;
+        break;
+      }
+      case RTPS_CDR_BOOL: {
+        if (c.pos + 1 > c.len) return RTPS_CDR_EOF;
+        uint8_t b = c.v[c.pos];
+        if (b > 1) return RTPS_CDR_BAD_BOOL;
+        row[op->out_off] = b;
+        c.pos += 1;
+        break;
+      }
+      case RTPS_CDR_STRING: {
+        uint32_t pad = cdr_pad(c.pos, 4);
+        if ((uint64_t)c.pos + pad + 4 > c.len) return RTPS_CDR_EOF;
+        c.pos += pad;
+        uint32_t l = (uint32_t)cdr_get(&c, c.pos, 4);
+        c.pos += 4;
+        if ((uint64_t)c.pos + l > c.len) return RTPS_CDR_EOF;
+        uint32_t m = l ? l - 1 : 0;
+        if (!utf8_ok(c.v + c.pos, m)) return RTPS_CDR_BAD_UTF8;
+        if (m > op->count) return RTPS_CDR_TOO_LONG;
+        cdr_store(row, op->out_off, m, 4);
+        memcpy(row + op->out_off + 4, c.v + c.pos, m);
+        c.pos += l;
+        break;
+      }
+      case RTPS_CDR_SEQ: {
+        uint32_t pad = cdr_pad(c.pos, 4);
+        if ((uint64_t)c.pos + pad + 4 > c.len) return RTPS_CDR_EOF;
+        c.pos += pad;
+        uint32_t n = (uint32_t)cdr_get(&c, c.pos, 4);
+        c.pos += 4;
+        if (n) {
+          uint32_t pe = cdr_pad(c.pos, size);
+          if ((uint64_t)c.pos + pe + (uint64_t)n * size > c.len) return RTPS_CDR_EOF;
+          if (n > op->count) return RTPS_CDR_TOO_LONG;
+          c.pos += pe;
+          for (uint32_t e = 0; e < n; ++e)
+            cdr_store(row, op->out_off + 4 + e * size, cdr_get(&c, c.pos + e * size, size), size);
+          c.pos += n * size;
+        }
+        cdr_store(row, op->out_off, n, 4);
+        break;
+      }
+      default:
+        return RTPS_CDR_TOO_LONG;
+    }
+  }
+  return RTPS_CDR_OK;
+}
+
+/* Decode every record (see rtps_rx_cdr_decode in rtps_rx.h); rows are zeroed
+ * unless the decode succeeds. */
+void rtps_oracle_cdr_decode(const rtps_cdr_op* prog, uint32_t n_ops, uint32_t row_bytes, const uint8_t* arena,
+                            const uint64_t* off, const rtps_record* recs, uint64_t n_recs, uint8_t* rows,
+                            uint8_t* status) {
+  for (uint64_t r = 0; r < n_recs; ++r) {
+    const rtps_record* rec = &recs[r];
+    uint8_t* row = rows + r * row_bytes;
+    memset(row, 0, row_bytes);
+    if (rec->kind != RTPS_DATA || rec->payload_kind != RTPS_PK_DATA) { status[r] = RTPS_CDR_NOT_DATA; continue; }
+    /* SimpleDataReader::deserialize_with: rep id must be a supported encoding */
+    const uint8_t* id = rec->u.data.rep_id;
+    int le;
+    if (id[0] == 0 && id[1] == 0) le = 0;                        /* CDR_BE    */
+    else if (id[0] == 0 && (id[1] == 1 || id[1] == 3)) le = 1;   /* CDR_LE, PL_CDR_LE */
+    else { status[r] = RTPS_CDR_BAD_ENCODING; continue; }
+    const uint8_t* value = arena + off[rec->dgram_idx] + rec->u.data.pl_off + 4;
+    uint8_t st = cdr_decode_one(prog, n_ops, value, (uint32_t)rec->u.data.pl_len - 4, le, row);
+    if (st != RTPS_CDR_OK) memset(row, 0, row_bytes);
+    status[r] = st;
+  }
+}

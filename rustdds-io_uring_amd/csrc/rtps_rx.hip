@@ -34,6 +34,7 @@
 
 #include "../../include/rtps_rx.h"
 #include "rtps_gen.h"
+#include "rtps_cdr.h"
 
 namespace {
 
@@ -1071,6 +1072,41 @@ int rtps_rx_bucket_by_writer(rtps_rx_ctx* c, const rtps_record* recs, const uint
   hipLaunchKernelGGL(bucket_scatter_kernel, dim3(tiles), dim3(TILE), 0, c->stream, recs, n_records, n_dest,
                      c->bucket_hist, out);
   return hip_fail(hipGetLastError());
+}
+
+/* a18: batch CDR decode (rtps_cdr.hip).  The program is validated here so
+ * the kernel can trust every op (sizes, slot bounds inside the row). */
+int rtps_rx_cdr_decode(rtps_rx_ctx* c, const rtps_cdr_op* prog, uint32_t n_ops, uint32_t row_bytes,
+                       const uint8_t* arena, uint64_t arena_len, const uint64_t* dgram_off,
+                       const rtps_record* records, const uint64_t* n_records, uint64_t max_records,
+                       uint8_t* rows, uint8_t* row_status) {
+  if (!c || !prog || n_ops > RTPS_CDR_MAX_OPS || row_bytes == 0 || (row_bytes & 3u) || row_bytes > (1u << 20))
+    return RTPS_RX_EINVAL;
+  if (!records || !n_records || (max_records && (!arena || !dgram_off || !rows || !row_status))) return RTPS_RX_EINVAL;
+  CdrProg P;
+  memset(&P, 0, sizeof(P));
+  for (uint32_t k = 0; k < n_ops; ++k) {
+    const rtps_cdr_op& op = prog[k];
+    const uint64_t sz = op.size;
+    const bool pow2 = sz == 1 || sz == 2 || sz == 4 || sz == 8;
+    uint64_t field;
+    switch (op.kind) {
+      case RTPS_CDR_PRIM: if (!pow2) return RTPS_RX_EINVAL; field = sz; break;
+      case RTPS_CDR_BOOL: field = 1; break;
+      case RTPS_CDR_STRING: field = 4ull + op.count; break;
+      case RTPS_CDR_SEQ: if (!pow2) return RTPS_RX_EINVAL; field = 4ull + sz * op.count; break;
+      case RTPS_CDR_ARRAY: if (!pow2) return RTPS_RX_EINVAL; field = sz * op.count; break;
+      default: return RTPS_RX_EINVAL;
+    }
+    if ((uint64_t)op.out_off + field > row_bytes) return RTPS_RX_EINVAL;
+    P.ops[k] = op;
+  }
+  P.n_ops = n_ops;
+  P.row_bytes = row_bytes;
+  if (max_records == 0) return RTPS_RX_OK;
+  (void)hipSetDevice(c->device);
+  CdrArgs a{arena, arena_len, dgram_off, records, n_records, max_records, rows, row_status};
+  return rtps_cdr_launch(c->stream, P, a, c->resident_blocks) == 0 ? RTPS_RX_OK : RTPS_RX_EHIP;
 }
 
 uint32_t rtps_rx_record_size(void) { return (uint32_t)sizeof(rtps_record); }

@@ -47,7 +47,7 @@ class _Out(ctypes.Structure):
 
 EXPORTS = ["rtps_rx_create", "rtps_rx_destroy", "rtps_rx_set_stream", "rtps_rx_set_match_table",
            "rtps_rx_parse_batch", "rtps_rx_sync", "rtps_rx_strerror", "rtps_rx_max_records_host",
-           "rtps_rx_generate", "rtps_rx_bucket_by_writer", "rtps_rx_set_spec_hint"]
+           "rtps_rx_generate", "rtps_rx_bucket_by_writer", "rtps_rx_set_spec_hint", "rtps_rx_cdr_decode"]
 
 
 def lib():
@@ -76,6 +76,8 @@ def lib():
         L.rtps_rx_bucket_by_writer.restype = I
         L.rtps_rx_set_spec_hint.argtypes = [P, U32]
         L.rtps_rx_set_spec_hint.restype = I
+        L.rtps_rx_cdr_decode.argtypes = [P, P, U32, U32, P, U64, P, P, P, U64, P, P]
+        L.rtps_rx_cdr_decode.restype = I
         for fn in ("rtps_rx_create", "rtps_rx_destroy", "rtps_rx_set_stream", "rtps_rx_set_match_table",
                    "rtps_rx_parse_batch", "rtps_rx_sync", "rtps_rx_generate"):
             getattr(L, fn).restype = I
@@ -215,6 +217,23 @@ class MessageReceiver:
                                               outs["max_records"], n_dest, out_records.data_ptr(),
                                               dest_counts.data_ptr()))
 
+    def alloc_rows(self, sample_type, max_recs):
+        """Row buffers for cdr_decode: ([max_recs, row_bytes] u8, [max_recs] u8 status)."""
+        import torch
+        dev = torch.device("cuda", self.device)
+        return (torch.empty((max(max_recs, 1), sample_type.row_bytes), dtype=torch.uint8, device=dev),
+                torch.empty(max(max_recs, 1), dtype=torch.uint8, device=dev))
+
+    def cdr_decode(self, sample_type, arena, off, outs, rows, row_status):
+        """Decode every DATA payload of a parsed batch into fixed-layout rows of
+        `sample_type` (a cdr.CdrType) on the device; asynchronous.  Row r belongs
+        to record r; row_status[r] is a cdr.CDR_* code (OK rows only are filled)."""
+        ops = sample_type.ops
+        _check(lib().rtps_rx_cdr_decode(self._h, ops.ctypes.data, len(ops), sample_type.row_bytes,
+                                        arena.data_ptr(), arena.numel(), off.data_ptr(), outs["records"].data_ptr(),
+                                        outs["n_records"].data_ptr(), outs["max_records"], rows.data_ptr(),
+                                        row_status.data_ptr()))
+
     # ---- convenience: host datagrams in, host results out ----
     def handle_received_batch(self, arena_np, off_np, len_np):
         """Parse host arrays on the GPU (H2D copy, parse, D2H copy) -> BatchResult."""
@@ -235,3 +254,27 @@ class MessageReceiver:
         match = outs["match"][:kept].cpu().numpy().view(np.uint16)
         return BatchResult(outs["status"][:n].cpu().numpy(), recs, match,
                            outs["rec_begin"][:n].cpu().numpy().view(np.uint32), total)
+
+    def take_batch(self, sample_type, arena_np, off_np, len_np):
+        """Parse + CDR-decode host arrays on the GPU -> (BatchResult, rows, row_status):
+        the batch form of DataReader::take's deserialize step (simpledatareader.rs:137-160)."""
+        import torch
+        n = len(len_np)
+        dev = torch.device("cuda", self.device)
+        arena = torch.from_numpy(np.ascontiguousarray(arena_np, dtype=np.uint8)).to(dev)
+        off = torch.from_numpy(np.ascontiguousarray(off_np, dtype=np.uint64).view(np.int64)).to(dev)
+        lens = torch.from_numpy(np.ascontiguousarray(len_np, dtype=np.uint32).view(np.int32)).to(dev)
+        cap = max_records(len_np)
+        outs = self.alloc_outputs(n, cap)
+        rows, row_status = self.alloc_rows(sample_type, cap)
+        torch.cuda.synchronize(dev)
+        self.parse_batch_device(arena, off, lens, n, outs)
+        self.cdr_decode(sample_type, arena, off, outs, rows, row_status)
+        self.sync()
+        total = int(outs["n_records"].item())
+        kept = min(total, cap)
+        recs = outs["records"][:kept].cpu().numpy().reshape(-1).view(RECORD_DTYPE)
+        match = outs["match"][:kept].cpu().numpy().view(np.uint16)
+        res = BatchResult(outs["status"][:n].cpu().numpy(), recs, match,
+                          outs["rec_begin"][:n].cpu().numpy().view(np.uint32), total)
+        return res, sample_type.rows(rows[:kept].cpu().numpy()), row_status[:kept].cpu().numpy()

@@ -1,0 +1,141 @@
+"""Sample types for the batch CDR decode.
+
+The reference decodes one sample at a time through serde:
+  SimpleDataReader::deserialize_with        io_uring/dds/with_key/simpledatareader.rs:137-160
+  -> CDRDeserializerAdapter::from_bytes_with dds/adapters.rs:128-139, serialization/cdr_adapters.rs:96-100
+  -> deserialize_from_cdr_with_decoder_and_rep_id  cdr_adapters.rs:246-275 (cdr-encoding 0.10)
+Here a `#[derive(Deserialize)]` struct becomes a `CdrType`: the flat list of
+rtps_cdr_op (include/rtps_rx.h) that the GPU decodes for every DATA record of
+a parsed batch, plus the numpy dtype of the fixed-layout output row.
+
+    ShapeType = CdrType([("color", String(128)), ("x", "i32"), ("y", "i32"), ("shapesize", "i32")])
+
+Field specs: a primitive name (PRIMS), "bool", String(cap), Seq(prim, cap),
+Array(prim, n) or a nested CdrType (flattened: classic CDR aligns each
+primitive to its own size from the start of the value, so nesting adds no
+padding of its own).
+"""
+import numpy as np
+
+OP_PRIM, OP_BOOL, OP_STRING, OP_SEQ, OP_ARRAY = 1, 2, 3, 4, 5
+CDR_OK, CDR_NOT_DATA, CDR_BAD_ENCODING, CDR_EOF, CDR_BAD_BOOL, CDR_BAD_UTF8, CDR_TOO_LONG = range(7)
+CDR_STATUS_NAMES = {0: "OK", 1: "NOT_DATA", 2: "BAD_ENCODING", 3: "EOF", 4: "BAD_BOOL", 5: "BAD_UTF8",
+                    6: "TOO_LONG"}
+MAX_OPS = 64
+
+OP_DTYPE = np.dtype([("kind", "u1"), ("size", "u1"), ("_r", "<u2"), ("count", "<u4"), ("out_off", "<u4")])
+assert OP_DTYPE.itemsize == 12
+
+# serde primitive -> numpy type.  (Rust `char` is a 4-byte code point in
+# cdr-encoding and is not offered; unit enums are their u32 discriminant.)
+PRIMS = {"u8": "u1", "i8": "i1", "u16": "<u2", "i16": "<i2", "u32": "<u4", "i32": "<i4",
+         "f32": "<f4", "u64": "<u8", "i64": "<i8", "f64": "<f8"}
+
+
+class String:
+    def __init__(self, cap):
+        self.cap = int(cap)
+
+
+class Seq:
+    def __init__(self, prim, cap):
+        assert prim in PRIMS
+        self.prim, self.cap = prim, int(cap)
+
+
+class Array:
+    def __init__(self, prim, n):
+        assert prim in PRIMS
+        self.prim, self.n = prim, int(n)
+
+
+def _align(x, a):
+    return (x + a - 1) // a * a
+
+
+class CdrType:
+    """Flat decode program + row layout of one sample type."""
+
+    def __init__(self, fields):
+        self.fields = list(fields)
+        ops, names, formats, offsets = [], [], [], []
+        self._layout = []  # (name, kind, spec) in program order, for encoders/decoders
+        pos = 0
+        max_align = 4
+
+        def add(name, spec):
+            nonlocal pos, max_align
+            if isinstance(spec, CdrType):
+                for sub_name, sub_spec in spec.fields:
+                    add(f"{name}.{sub_name}", sub_spec)
+                return
+            if isinstance(spec, str) and spec in PRIMS:
+                dt = np.dtype(PRIMS[spec])
+                a, kind, size, count, fmt = dt.itemsize, OP_PRIM, dt.itemsize, 1, dt
+            elif spec == "bool":
+                a, kind, size, count, fmt = 1, OP_BOOL, 1, 1, np.dtype("u1")
+            elif isinstance(spec, String):
+                a, kind, size, count = 4, OP_STRING, 1, spec.cap
+                fmt = np.dtype([("len", "<u4"), ("data", f"S{max(spec.cap, 1)}")])
+            elif isinstance(spec, Seq):
+                dt = np.dtype(PRIMS[spec.prim])
+                a, kind, size, count = 4, OP_SEQ, dt.itemsize, spec.cap
+                fmt = np.dtype([("n", "<u4"), ("data", dt, (max(spec.cap, 1),))])
+            elif isinstance(spec, Array):
+                dt = np.dtype(PRIMS[spec.prim])
+                a, kind, size, count = dt.itemsize, OP_ARRAY, dt.itemsize, spec.n
+                fmt = np.dtype((dt, (max(spec.n, 1),)))
+            else:
+                raise TypeError(f"unsupported field spec {spec!r} for {name}")
+            pos = _align(pos, a)
+            max_align = max(max_align, a)
+            ops.append((kind, size, 0, count, pos))
+            names.append(name)
+            formats.append(fmt)
+            offsets.append(pos)
+            self._layout.append((name, kind, spec))
+            pos += fmt.itemsize
+
+        for name, spec in self.fields:
+            add(name, spec)
+        if len(ops) > MAX_OPS:
+            raise ValueError(f"{len(ops)} ops > {MAX_OPS}")
+        self.row_bytes = max(_align(pos, max_align), 4)
+        self.ops = np.array(ops, dtype=OP_DTYPE)
+        self.row_dtype = np.dtype({"names": names, "formats": formats, "offsets": offsets,
+                                   "itemsize": self.row_bytes})
+
+    @property
+    def n_ops(self):
+        return len(self.ops)
+
+    def rows(self, raw):
+        """[m, row_bytes] u8 -> structured rows."""
+        return np.ascontiguousarray(raw, dtype=np.uint8).reshape(-1).view(self.row_dtype)
+
+    def to_python(self, row):
+        """One structured row -> {field: value} with str / list values."""
+        out = {}
+        for name, kind, spec in self._layout:
+            v = row[name]
+            if kind == OP_STRING:
+                out[name] = v.tobytes()[4:4 + int(v["len"])].decode()
+            elif kind == OP_SEQ:
+                out[name] = v["data"][: int(v["n"])].tolist()
+            elif kind == OP_ARRAY:
+                out[name] = v.tolist()
+            elif kind == OP_BOOL:
+                out[name] = bool(v)
+            else:
+                out[name] = v.item()
+        return out
+
+
+# The shapes-demo sample type (rtps/message_receiver.rs:1240-1248: color, x, y, size)
+ShapeType = CdrType([("color", String(128)), ("x", "i32"), ("y", "i32"), ("shapesize", "i32")])
+
+# Sample type of the C2 / T synthetic workloads' payloads (252 / 976 value bytes
+# of primitives after the CDR_LE header; the trailing bytes are ignored, as
+# cdr-encoding only reports bytes_consumed).
+C2Sample = CdrType([("seq", "u64"), ("stamp", "f64"), ("vals", Array("f32", 58))])
+TSample = CdrType([("seq", "u64"), ("stamp", "f64"), ("vals", Array("f32", 240))])

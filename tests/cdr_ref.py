@@ -1,0 +1,293 @@
+"""Test-side CDR helpers for the batch decode (a18).
+
+serialize(): classic CDR encoder with the rules of the reference's serializer
+(cdr-encoding 0.10 CdrSerializer, used by CDRSerializerAdapter
+serialization/cdr_adapters.rs:120-180): each primitive aligned to its size
+from the start of the value, string = u32 (len+1) + bytes + NUL, sequence =
+u32 count + elements, arrays without length, bool = one byte.
+
+decode(): an independent pure-Python restatement of the decoder, used to
+cross-check the C oracle (oracle/rtps_oracle.c rtps_oracle_cdr_decode) on
+small corpora.  Its rules (alignment, padding only when an element is read,
+str::from_utf8, bool 0/1) are cdr-encoding's published behaviour; the only
+reference vector is the shapes-demo ShapeType "RED" payload
+(rtps/message_receiver.rs:1250-1254), everything else is parity unpinned.
+"""
+import struct
+
+import numpy as np
+
+from rtps_rx import cdr
+
+_FMT = {"u8": "B", "i8": "b", "u16": "H", "i16": "h", "u32": "I", "i32": "i", "f32": "f",
+        "u64": "Q", "i64": "q", "f64": "d"}
+REP_CDR_BE, REP_CDR_LE, REP_PL_CDR_BE, REP_PL_CDR_LE = b"\x00\x00", b"\x00\x01", b"\x00\x02", b"\x00\x03"
+
+
+def _pad(buf, a):
+    while len(buf) % a:
+        buf.append(0)
+
+
+def serialize(t, values, le=True):
+    """values: {flat field name: value} for CdrType t -> CDR value bytes (no encapsulation header)."""
+    e = "<" if le else ">"
+    buf = bytearray()
+    for name, kind, spec in t._layout:
+        v = values[name]
+        if kind == cdr.OP_PRIM:
+            f = _FMT[spec]
+            _pad(buf, struct.calcsize(f))
+            buf += struct.pack(e + f, v)
+        elif kind == cdr.OP_BOOL:
+            buf.append(v if type(v) is int else (1 if v else 0))  # ints > 1 make invalid bools
+        elif kind == cdr.OP_STRING:
+            raw = v.encode() if isinstance(v, str) else bytes(v)
+            _pad(buf, 4)
+            buf += struct.pack(e + "I", len(raw) + 1) + raw + b"\x00"
+        elif kind == cdr.OP_SEQ:
+            f = _FMT[spec.prim]
+            _pad(buf, 4)
+            buf += struct.pack(e + "I", len(v))
+            if len(v):
+                _pad(buf, struct.calcsize(f))
+                buf += struct.pack(e + f * len(v), *v)
+        elif kind == cdr.OP_ARRAY:
+            f = _FMT[spec.prim]
+            if spec.n:
+                _pad(buf, struct.calcsize(f))
+                buf += struct.pack(e + f * spec.n, *v)
+    return bytes(buf)
+
+
+def payload(t, values, le=True, rep=None):
+    """SerializedPayload bytes: rep id + options + value, padded to 4 (serialized_payload.rs:60-84)."""
+    body = serialize(t, values, le)
+    rep = rep if rep is not None else (REP_CDR_LE if le else REP_CDR_BE)
+    padding = (-len(body)) % 4
+    return rep + bytes([0, padding]) + body + bytes(padding)
+
+
+def _utf8_ok(b):
+    try:
+        b.decode("utf-8", errors="strict")
+    except UnicodeDecodeError:
+        return False
+    return True
+
+
+def decode(t, value, le):
+    """(status, {name: value}, expected row bytes) for value bytes (after the 4-byte header).
+    The row is built from raw (byte-swapped) element bytes, so floats compare bit-exactly."""
+    e = "<" if le else ">"
+    pos = 0
+    out = {}
+    row = bytearray(t.row_bytes)
+    n = len(value)
+
+    def put(off, raw, sz):  # raw element bytes in wire order -> host (LE) order in the row
+        for k in range(0, len(raw), sz):
+            el = raw[k:k + sz]
+            row[off + k:off + k + sz] = el if le else el[::-1]
+
+    err = lambda st: (st, None, bytes(t.row_bytes))  # noqa: E731
+    for (name, kind, spec), op in zip(t._layout, t.ops):
+        o = int(op["out_off"])
+        if kind in (cdr.OP_PRIM, cdr.OP_ARRAY):
+            prim = spec if kind == cdr.OP_PRIM else spec.prim
+            f = _FMT[prim]
+            sz = struct.calcsize(f)
+            cnt = 1 if kind == cdr.OP_PRIM else spec.n
+            if cnt == 0:
+                out[name] = []
+                continue
+            pad = (-pos) % sz
+            if pos + pad + cnt * sz > n:
+                return err(cdr.CDR_EOF)
+            pos += pad
+            vals = list(struct.unpack_from(e + f * cnt, value, pos))
+            put(o, bytes(value[pos:pos + cnt * sz]), sz)
+            out[name] = vals[0] if kind == cdr.OP_PRIM else vals
+            pos += cnt * sz
+        elif kind == cdr.OP_BOOL:
+            if pos + 1 > n:
+                return err(cdr.CDR_EOF)
+            if value[pos] > 1:
+                return err(cdr.CDR_BAD_BOOL)
+            out[name] = value[pos] == 1
+            row[o] = value[pos]
+            pos += 1
+        elif kind == cdr.OP_STRING:
+            pos += (-pos) % 4
+            if pos + 4 > n:
+                return err(cdr.CDR_EOF)
+            ln = struct.unpack_from(e + "I", value, pos)[0]
+            pos += 4
+            if pos + ln > n:
+                return err(cdr.CDR_EOF)
+            sb = bytes(value[pos:pos + max(ln - 1, 0)])
+            if not _utf8_ok(sb):
+                return err(cdr.CDR_BAD_UTF8)
+            if len(sb) > spec.cap:
+                return err(cdr.CDR_TOO_LONG)
+            out[name] = sb.decode()
+            row[o:o + 4] = struct.pack("<I", len(sb))
+            row[o + 4:o + 4 + len(sb)] = sb
+            pos += ln
+        elif kind == cdr.OP_SEQ:
+            f = _FMT[spec.prim]
+            sz = struct.calcsize(f)
+            pos += (-pos) % 4
+            if pos + 4 > n:
+                return err(cdr.CDR_EOF)
+            cnt = struct.unpack_from(e + "I", value, pos)[0]
+            pos += 4
+            vals = []
+            if cnt:
+                pad = (-pos) % sz
+                if pos + pad + cnt * sz > n:
+                    return err(cdr.CDR_EOF)
+                if cnt > spec.cap:
+                    return err(cdr.CDR_TOO_LONG)
+                pos += pad
+                vals = list(struct.unpack_from(e + f * cnt, value, pos))
+                put(o + 4, bytes(value[pos:pos + cnt * sz]), sz)
+                pos += cnt * sz
+            row[o:o + 4] = struct.pack("<I", cnt)
+            out[name] = vals
+    return cdr.CDR_OK, out, bytes(row)
+
+
+def expected_rows(t, arena, offs, recs):
+    """(rows u8[m, row_bytes], status u8[m]) computed record by record with decode()."""
+    from rtps_rx.records import DATA, PK_DATA
+    m = len(recs)
+    rows = np.zeros((m, t.row_bytes), dtype=np.uint8)
+    status = np.zeros(m, dtype=np.uint8)
+    for r in range(m):
+        rec = recs[r]
+        if int(rec["kind"]) != DATA or int(rec["payload_kind"]) != PK_DATA:
+            status[r] = cdr.CDR_NOT_DATA
+            continue
+        u = rec["u"].tobytes()
+        pl_off, pl_len = struct.unpack_from("<HH", u, 0)
+        rep = u[4:6]
+        if rep not in (REP_CDR_BE, REP_CDR_LE, REP_PL_CDR_LE):
+            status[r] = cdr.CDR_BAD_ENCODING
+            continue
+        base = int(offs[int(rec["dgram_idx"])]) + pl_off
+        value = bytes(arena[base + 4:base + pl_len])
+        st, _, row = decode(t, value, rep != REP_CDR_BE)
+        status[r] = st
+        rows[r] = np.frombuffer(row, dtype=np.uint8)
+    return rows, status
+
+
+def data_datagram(payload_bytes, sn=1, le=True, writer_key=b"\x00\x00\x01", prefix=bytes(range(1, 13)),
+                  flags_extra=0x04):
+    """RTPS message with one DATA (reader UNKNOWN, writer user-defined with key) carrying payload_bytes."""
+    e = "<" if le else ">"
+    body = struct.pack(e + "HH", 0, 16) + b"\x00\x00\x00\x00" + writer_key + b"\x02" + \
+        struct.pack(e + "iI", sn >> 32, sn & 0xFFFFFFFF) + payload_bytes
+    hdr = b"RTPS" + b"\x02\x04" + b"\x01\x0f" + prefix
+    return hdr + bytes([0x15, (1 if le else 0) | flags_extra]) + struct.pack(e + "H", len(body)) + body
+
+
+def random_values(t, rng, str_alphabet=("a", "Z", "0", " ", "é", "ß", "€", "😀", "\x00")):
+    """Random field values that fit t's slots."""
+    vals = {}
+    for name, kind, spec in t._layout:
+        if kind == cdr.OP_PRIM:
+            vals[name] = _rand_prim(spec, rng)
+        elif kind == cdr.OP_BOOL:
+            vals[name] = bool(rng.integers(0, 2))
+        elif kind == cdr.OP_STRING:
+            s = ""
+            while True:
+                c = str_alphabet[rng.integers(0, len(str_alphabet))]
+                if len((s + c).encode()) > spec.cap or rng.random() < 0.08:
+                    break
+                s += c
+            vals[name] = s
+        elif kind == cdr.OP_SEQ:
+            vals[name] = [_rand_prim(spec.prim, rng) for _ in range(int(rng.integers(0, spec.cap + 1)))]
+        elif kind == cdr.OP_ARRAY:
+            vals[name] = [_rand_prim(spec.prim, rng) for _ in range(spec.n)]
+    return vals
+
+
+def _rand_prim(p, rng):
+    f = _FMT[p]
+    if f in "fd":
+        x = float(rng.standard_normal() * 1e3)
+        return float(np.float32(x)) if f == "f" else x
+    bits = struct.calcsize(f) * 8
+    if f.isupper():
+        return int(rng.integers(0, 1 << bits, dtype=np.uint64)) if bits == 64 else int(rng.integers(0, 1 << bits))
+    lo = -(1 << (bits - 1))
+    return int(rng.integers(lo, -lo, dtype=np.int64))
+
+
+BAD_UTF8 = [b"\xc0\x80", b"\xed\xa0\x80", b"\x80", b"\xf0\x80\x80\x80", b"\xf4\x90\x80\x80", b"abc\xe2\x82",
+            b"\xff", b"\xe0\x9f\xbf", b"\xc2", b"ok\xf5\x80\x80\x80"]
+HB = bytes.fromhex("07010000" "00000000" "00000102" "0000000001000000" "0000000005000000" "01000000")
+
+
+def corpus(t, n, seed, prefix=bytes(range(1, 13))):
+    """n datagrams carrying t-typed payloads: clean LE/BE samples plus every error class
+    (truncation, byte corruption, bad UTF-8, over-long strings/sequences, bad bool,
+    unsupported rep ids, KEY payloads and non-DATA submessages)."""
+    rng = np.random.default_rng(seed)
+    has = {k for _, k, _ in t._layout}
+    out = []
+    for i in range(n):
+        le = bool(rng.integers(0, 2))
+        vals = random_values(t, rng)
+        mode = int(rng.integers(0, 12))
+        rep = None
+        flags = 0x04
+        if mode == 4 and cdr.OP_STRING in has:    # invalid UTF-8 inside a string
+            name = next(nm for nm, k, _ in t._layout if k == cdr.OP_STRING)
+            vals[name] = BAD_UTF8[int(rng.integers(0, len(BAD_UTF8)))]
+        elif mode == 5 and cdr.OP_STRING in has:  # longer than the slot
+            name, _, spec = next(x for x in t._layout if x[1] == cdr.OP_STRING)
+            vals[name] = "x" * (spec.cap + 1 + int(rng.integers(0, 3)))
+        elif mode == 6 and cdr.OP_SEQ in has:     # more elements than the slot
+            name, _, spec = next(x for x in t._layout if x[1] == cdr.OP_SEQ)
+            vals[name] = [0] * (spec.cap + 1)
+        elif mode == 7:
+            rep = [REP_PL_CDR_BE, b"\x00\x06", b"\x01\x00", b"\x00\x0a"][int(rng.integers(0, 4))]
+        elif mode == 8:
+            flags = 0x08  # KEY payload -> not a DATA sample
+        elif mode == 3 and cdr.OP_BOOL in has:    # invalid bool byte
+            names = [nm for nm, k, _ in t._layout if k == cdr.OP_BOOL]
+            vals[names[int(rng.integers(0, len(names)))]] = int(rng.integers(2, 256))
+        body = serialize(t, vals, le)
+        if mode == 2 and body:                    # truncation
+            body = body[:int(rng.integers(0, len(body)))]
+        elif mode == 3 and cdr.OP_BOOL not in has and body:  # corrupt one byte
+            b = bytearray(body)
+            b[int(rng.integers(0, len(b)))] = int(rng.integers(2, 256))
+            body = bytes(b)
+        elif mode == 9 and body:                  # several random bytes
+            b = bytearray(body)
+            for _ in range(int(rng.integers(1, 5))):
+                b[int(rng.integers(0, len(b)))] = int(rng.integers(0, 256))
+            body = bytes(b)
+        rep = rep if rep is not None else (REP_CDR_LE if le else REP_CDR_BE)
+        if mode == 10 and le:
+            rep = REP_PL_CDR_LE                   # accepted, little-endian
+        pad = (-len(body)) % 4
+        pl = rep + bytes([0, pad]) + body + bytes(pad)
+        dg = data_datagram(pl, sn=i + 1, le=bool(rng.integers(0, 2)), prefix=prefix, flags_extra=flags)
+        if mode == 11:                            # a HEARTBEAT after the DATA: NOT_DATA record
+            dg = dg + HB
+        out.append(dg)
+    return out
+
+
+# A type exercising every op kind, alignment step and slot tail
+MIXED = cdr.CdrType([("id", "u8"), ("temp", "f64"), ("flag", "bool"), ("name", cdr.String(24)),
+                     ("hist", cdr.Seq("u16", 6)), ("big", cdr.Seq("i64", 3)), ("pos", cdr.Array("f32", 3)),
+                     ("c", "i8"), ("t", "i16"), ("ok", "bool"), ("inner", cdr.ShapeType),
+                     ("tail", cdr.Array("u64", 2))])

@@ -1,0 +1,107 @@
+"""GPU parity of the batch CDR decode (a18) through the C ABI
+(rtps_rx_cdr_decode) vs the CPU oracle (rtps_oracle_cdr_decode): every row
+byte and every row status identical."""
+import numpy as np
+import pytest
+
+import cdr_ref
+import oracle
+from golden_cases import cases
+from rtps_rx import cdr
+from rtps_rx.records import DATA
+from test_cdr_oracle import TYPES
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def rx():
+    import rtps_rx
+    r = rtps_rx.MessageReceiver(oracle.OWN_PREFIX, max_datagrams=1 << 21)
+    yield r
+    r.close()
+
+
+def _check(rx, t, arena, off, ln, label):
+    res, rows, status = rx.take_batch(t, arena, off, ln)
+    st, recs, _, _ = oracle.parse(arena, off, ln, threads=8)
+    assert res.n_records == len(recs)
+    o_rows, o_status = oracle.cdr_decode(t, arena, off, recs)
+    bad = np.nonzero(status != o_status)[0]
+    assert len(bad) == 0, f"{label}: row status differs at {bad[:8]}: gpu {status[bad[:8]]} oracle {o_status[bad[:8]]}"
+    g = rows.view(np.uint8).reshape(len(recs), t.row_bytes) if len(recs) else rows
+    if len(recs):
+        diff = np.nonzero((g != o_rows).any(axis=1))[0]
+        assert len(diff) == 0, f"{label}: {len(diff)} rows differ, first {diff[:8]}"
+    return rows, status
+
+
+def test_shape_type_red(rx):
+    dgram = next(c[1] for c in cases() if c[0] == "mr_shapes_red")
+    arena, off, ln = oracle.pack([dgram])
+    res, rows, status = rx.take_batch(cdr.ShapeType, arena, off, ln)
+    i = [k for k, r in enumerate(res.records) if r["kind"] == DATA][0]
+    assert status[i] == cdr.CDR_OK
+    assert cdr.ShapeType.to_python(rows[i]) == {"color": "RED", "x": 105, "y": 23, "shapesize": 30}
+
+
+@pytest.mark.parametrize("name", sorted(TYPES))
+def test_corpus_parity(rx, name):
+    t = TYPES[name]
+    dgrams = cdr_ref.corpus(t, 3000, seed=100 + len(name))
+    arena, off, ln = oracle.pack(dgrams, align=1)  # unaligned payloads
+    _, status = _check(rx, t, arena, off, ln, name)
+    if name != "empty":
+        assert np.bincount(status, minlength=7)[[0, 1, 2, 3]].all()
+
+
+def test_bad_program_rejected(rx):
+    import rtps_rx
+    dev = torch.device("cuda", 0)
+    outs = rx.alloc_outputs(1, 4)
+    rows, st = rx.alloc_rows(cdr.ShapeType, 4)
+    arena = torch.zeros(64, dtype=torch.uint8, device=dev)
+    off = torch.zeros(1, dtype=torch.int64, device=dev)
+    bad = cdr.CdrType([("x", "u32")])
+    bad.ops = bad.ops.copy()
+    bad.ops["size"] = 3
+    with pytest.raises(rtps_rx.RtpsRxError):
+        rx.cdr_decode(bad, arena, off, outs, rows, st)
+    bad.ops["size"] = 4
+    bad.ops["out_off"] = bad.row_bytes  # field past the row
+    with pytest.raises(rtps_rx.RtpsRxError):
+        rx.cdr_decode(bad, arena, off, outs, rows, st)
+
+
+def _device_gen(rx, wl, n):
+    import rtps_rx
+    off, ln, size = rtps_rx.gen_layout(wl, n)
+    dev = torch.device("cuda", 0)
+    arena_t = torch.zeros(max(size, 16), dtype=torch.uint8, device=dev)
+    off_t = torch.from_numpy(off.view(np.int64)).to(dev)
+    ln_t = torch.from_numpy(ln.view(np.int32)).to(dev)
+    rx.generate(wl, arena_t, off_t, ln_t, n)
+    rx.sync()
+    return arena_t.cpu().numpy(), off, ln
+
+
+@pytest.mark.parametrize("wl,t", [(2, "C2Sample"), (1, "TSample"), (3, "ShapeType"), (3, "MIXED"), (4, "C2Sample")])
+def test_workload_decode_parity(rx, wl, t):
+    typ = cdr_ref.MIXED if t == "MIXED" else getattr(cdr, t)
+    arena, off, ln = _device_gen(rx, wl, 20000)
+    _check(rx, typ, arena, off, ln, f"wl{wl}-{t}")
+
+
+def test_c2_full_size(rx):
+    """1M C2 datagrams: every record decodes (payload of primitives), bit-exact vs the oracle,
+    and the rows are the payload bytes themselves (LE wire = host order)."""
+    n = 1 << 20
+    arena, off, ln = _device_gen(rx, 2, n)
+    rows, status = _check(rx, cdr.C2Sample, arena, off, ln, "C2-1M")
+    assert (status == cdr.CDR_OK).all()
+    raw = rows.view(np.uint8).reshape(n, -1)
+    k = np.arange(0, n, 4099)
+    for i in k[:64]:
+        base = int(off[i]) + 44 + 4
+        assert np.array_equal(raw[i], arena[base:base + cdr.C2Sample.row_bytes])

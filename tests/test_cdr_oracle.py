@@ -1,0 +1,126 @@
+"""CPU checks of the CDR decode oracle (a18): the reference's ShapeType vector,
+an independent Python restatement on mixed corpora (every error class, LE/BE),
+round trips through the encoder and edge cases of the classic-CDR rules."""
+import struct
+
+import numpy as np
+import pytest
+
+import cdr_ref
+import oracle
+from golden_cases import cases
+from rtps_rx import cdr
+from rtps_rx.records import DATA
+
+TYPES = {
+    "shape": cdr.ShapeType,
+    "mixed": cdr_ref.MIXED,
+    "prims": cdr.CdrType([("a", "u8"), ("b", "u64"), ("c", "i16"), ("d", "f32"), ("e", "i8"), ("f", "f64")]),
+    "seqs": cdr.CdrType([("s", cdr.Seq("f64", 4)), ("t", cdr.Seq("u8", 9)), ("n", cdr.String(3)),
+                         ("v", cdr.Seq("i32", 0))]),
+    "empty": cdr.CdrType([]),
+}
+
+
+def _decode_corpus(t, n, seed):
+    dgrams = cdr_ref.corpus(t, n, seed)
+    arena, off, ln = oracle.pack(dgrams)
+    st, recs, _, _ = oracle.parse(arena, off, ln)
+    assert (st == 0).all()
+    return arena, off, recs
+
+
+def test_shape_type_red_known_answer():
+    """rtps/message_receiver.rs:1250-1254 decodes the DATA payload as ShapeType with color "RED"."""
+    dgram = next(c[1] for c in cases() if c[0] == "mr_shapes_red")
+    arena, off, ln = oracle.pack([dgram])
+    st, recs, _, _ = oracle.parse(arena, off, ln)
+    rows, status = oracle.cdr_decode(cdr.ShapeType, arena, off, recs)
+    data = [i for i, r in enumerate(recs) if r["kind"] == DATA]
+    assert len(data) == 1 and status[data[0]] == cdr.CDR_OK
+    assert all(status[i] == cdr.CDR_NOT_DATA for i in range(len(recs)) if i not in data)
+    v = cdr.ShapeType.to_python(cdr.ShapeType.rows(rows)[data[0]])
+    assert v == {"color": "RED", "x": 105, "y": 23, "shapesize": 30}
+    assert not rows[[i for i in range(len(recs)) if i not in data]].any()
+
+
+@pytest.mark.parametrize("name", sorted(TYPES))
+def test_oracle_matches_python_restatement(name):
+    t = TYPES[name]
+    arena, off, recs = _decode_corpus(t, 600, seed=len(name))
+    rows, status = oracle.cdr_decode(t, arena, off, recs)
+    exp_rows, exp_status = cdr_ref.expected_rows(t, arena, off, recs)
+    bad = np.nonzero(status != exp_status)[0]
+    assert len(bad) == 0, f"{name}: status differs at {bad[:8]}: {status[bad[:8]]} vs {exp_status[bad[:8]]}"
+    assert np.array_equal(rows, exp_rows), f"{name}: rows differ at {np.nonzero((rows != exp_rows).any(1))[0][:8]}"
+    if name != "empty":
+        hist = np.bincount(status, minlength=7)
+        assert hist[cdr.CDR_OK] > 0 and hist[cdr.CDR_NOT_DATA] > 0 and hist[cdr.CDR_BAD_ENCODING] > 0
+
+
+@pytest.mark.parametrize("le", [True, False])
+def test_round_trip(le):
+    t = cdr_ref.MIXED
+    rng = np.random.default_rng(7 + le)
+    vals = [cdr_ref.random_values(t, rng) for _ in range(64)]
+    dgrams = [cdr_ref.data_datagram(cdr_ref.payload(t, v, le), sn=i + 1) for i, v in enumerate(vals)]
+    arena, off, ln = oracle.pack(dgrams)
+    st, recs, _, _ = oracle.parse(arena, off, ln)
+    rows, status = oracle.cdr_decode(t, arena, off, recs)
+    assert (status == cdr.CDR_OK).all()
+    for v, row in zip(vals, t.rows(rows)):
+        got = t.to_python(row)
+        for k in v:
+            want = v[k]
+            if isinstance(want, float):
+                assert struct.pack("<d", got[k]) == struct.pack("<d", want) or got[k] == want, k
+            else:
+                assert got[k] == (list(want) if isinstance(want, list) else want), (k, got[k], want)
+
+
+def _one(t, value, rep=cdr_ref.REP_CDR_LE):
+    dg = cdr_ref.data_datagram(rep + b"\x00\x00" + value)
+    arena, off, ln = oracle.pack([dg])
+    st, recs, _, _ = oracle.parse(arena, off, ln)
+    rows, status = oracle.cdr_decode(t, arena, off, recs)
+    return int(status[0]), rows[0]
+
+
+def test_edge_rules():
+    S = cdr.CdrType([("s", cdr.String(8))])
+    assert _one(S, struct.pack("<I", 0))[0] == cdr.CDR_OK              # length 0: empty string
+    assert _one(S, struct.pack("<I", 1) + b"\x00")[0] == cdr.CDR_OK    # "" with NUL
+    st, row = _one(S, struct.pack("<I", 3) + b"hiX")                  # last byte dropped, NUL not checked
+    assert st == cdr.CDR_OK and bytes(row[4:6]) == b"hi" and row[0] == 2
+    assert _one(S, struct.pack("<I", 10) + b"12345678\x00")[0] == cdr.CDR_EOF
+    assert _one(S, struct.pack("<I", 10) + b"123456789\x00")[0] == cdr.CDR_TOO_LONG
+    assert _one(S, struct.pack("<I", 3) + b"\xc3\xa9\x00")[0] == cdr.CDR_OK  # é
+    assert _one(S, struct.pack("<I", 2) + b"\xc3\x00")[0] == cdr.CDR_BAD_UTF8
+    # empty sequence of 8-byte elements: no alignment padding is consumed
+    Q = cdr.CdrType([("q", cdr.Seq("u64", 2)), ("x", "u32")])
+    st, row = _one(Q, struct.pack("<II", 0, 77))
+    assert st == cdr.CDR_OK and struct.unpack_from("<I", row, Q.ops[1]["out_off"])[0] == 77
+    st, row = _one(Q, struct.pack("<IIQI", 1, 0, 5, 9))                # pad 4 before the u64
+    assert st == cdr.CDR_OK and struct.unpack_from("<IQ", row, 0)[0] == 1
+    # trailing bytes after the type are ignored (bytes_consumed is only reported)
+    P = cdr.CdrType([("a", "u16")])
+    assert _one(P, b"\x01\x02\xff\xff\xff\xff")[0] == cdr.CDR_OK
+    assert _one(P, b"\x01")[0] == cdr.CDR_EOF
+    B = cdr.CdrType([("b", "bool")])
+    assert [_one(B, bytes([x]))[0] for x in (0, 1, 2, 255)] == [0, 0, cdr.CDR_BAD_BOOL, cdr.CDR_BAD_BOOL]
+    # rep ids: CDR_BE / CDR_LE / PL_CDR_LE accepted (cdr_adapters.rs:96-100), PL_CDR_BE refused
+    U = cdr.CdrType([("u", "u32")])
+    st, row = _one(U, b"\x00\x00\x01\x02", rep=cdr_ref.REP_CDR_BE)
+    assert st == 0 and bytes(row[:4]) == b"\x02\x01\x00\x00"
+    assert _one(U, b"\x00\x00\x01\x02", rep=cdr_ref.REP_PL_CDR_LE)[0] == 0
+    assert _one(U, b"\x00\x00\x01\x02", rep=cdr_ref.REP_PL_CDR_BE)[0] == cdr.CDR_BAD_ENCODING
+
+
+def test_type_layout():
+    t = cdr_ref.MIXED
+    assert t.row_bytes % 4 == 0 and t.row_dtype.itemsize == t.row_bytes
+    for op in t.ops:
+        assert op["out_off"] % (4 if op["kind"] in (cdr.OP_STRING, cdr.OP_SEQ) else op["size"]) == 0
+    assert cdr.ShapeType.row_bytes == 144
+    with pytest.raises(ValueError):
+        cdr.CdrType([(f"f{i}", "u8") for i in range(cdr.MAX_OPS + 1)])
