@@ -238,18 +238,26 @@ int rtps_rx_bucket_by_writer(rtps_rx_ctx* ctx, const rtps_record* recs, const ui
  * DATA record with payload_kind == RTPS_PK_DATA is decoded into a row of
  * row_bytes at rows + record_index * row_bytes (host byte order). */
 enum rtps_cdr_op_kind {
-  RTPS_CDR_PRIM = 1,   /* size 1/2/4/8 (ints, f32, f64, char, enum=u32): out `size` bytes        */
-  RTPS_CDR_BOOL = 2,   /* 1 byte, must be 0 or 1: out 1 byte                                    */
-  RTPS_CDR_STRING = 3, /* u32 length incl. NUL + bytes, UTF-8 checked: out u32 len + char[count] */
-  RTPS_CDR_SEQ = 4,    /* u32 n + n primitives of `size` (n <= count): out u32 n + size*count     */
-  RTPS_CDR_ARRAY = 5   /* count primitives of `size`, no length: out size*count                  */
+  RTPS_CDR_PRIM = 1,   /* size 1/2/4/8 (ints, f32, f64, unit enum = u32)                          */
+  RTPS_CDR_BOOL = 2,   /* 1 byte, must be 0 or 1                                                   */
+  RTPS_CDR_STRING = 3, /* u32 length incl. NUL + bytes, UTF-8 checked; count = max chars (no NUL) */
+  RTPS_CDR_SEQ = 4,    /* u32 n + n primitives of `size`; count = max elements                     */
+  RTPS_CDR_ARRAY = 5   /* count primitives of `size`, no length                                    */
 };
+/* Row layout: each op owns a slot that starts at out_off (4-aligned) and spans
+ * a multiple of 4 bytes; slots must not overlap and must lie inside the row:
+ *   PRIM  align4(size)           value (host order), zero-extended
+ *   BOOL  4                      byte 0 = 0/1, rest 0
+ *   STRING 4 + align4(count)     u32 chars, then the chars, zero tail (no NUL)
+ *   SEQ   4 + align4(size*count) u32 n, then n elements, zero tail
+ *   ARRAY align4(size*count)     count elements
+ * Bytes not covered by a slot are zero.  A row whose decode fails is all zero. */
 typedef struct rtps_cdr_op {
   uint8_t kind;      /* rtps_cdr_op_kind */
   uint8_t size;      /* primitive size for PRIM / SEQ / ARRAY */
   uint16_t _r;
-  uint32_t count;    /* STRING: char slot capacity; SEQ: max elements; ARRAY: elements */
-  uint32_t out_off;  /* byte offset of the field in the output row */
+  uint32_t count;    /* STRING: max chars; SEQ: max elements; ARRAY: elements */
+  uint32_t out_off;  /* byte offset of the slot in the output row (multiple of 4) */
 } rtps_cdr_op;
 enum rtps_cdr_status {
   RTPS_CDR_OK = 0,
@@ -261,8 +269,11 @@ enum rtps_cdr_status {
   RTPS_CDR_TOO_LONG = 6         /* string/sequence longer than the row slot (not a reference error) */
 };
 #define RTPS_CDR_MAX_OPS 64u
-/* arena / dgram_off: the batch given to rtps_rx_parse_batch; records / n_records:
- * its outputs.  rows: [max_records * row_bytes], row_status: [max_records]. */
+/* prog: host array of n_ops ops (copied at the call).  arena / dgram_off: the
+ * batch given to rtps_rx_parse_batch; records / n_records: its outputs.
+ * rows: [max_records * row_bytes] (row_bytes a multiple of 4), row_status:
+ * [max_records]; rows/statuses [0, min(*n_records, max_records)) are written.
+ * Asynchronous on the context's stream.  RTPS_RX_EINVAL for a malformed program. */
 int rtps_rx_cdr_decode(rtps_rx_ctx* ctx, const rtps_cdr_op* prog, uint32_t n_ops, uint32_t row_bytes,
                        const uint8_t* arena, uint64_t arena_len, const uint64_t* dgram_off,
                        const rtps_record* records, const uint64_t* n_records, uint64_t max_records,

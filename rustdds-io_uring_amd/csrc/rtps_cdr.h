@@ -6,10 +6,27 @@
 
 #include "../../include/rtps_rx.h"
 
+constexpr uint32_t CDR_MAX_SLOTS = 2 * RTPS_CDR_MAX_OPS + 1;  // op slots + zero gaps
+constexpr uint8_t CDR_SLOT_ZERO = 0;                          // gap between op slots
+
+// One write-phase slot of the row: `dwords` 4-byte words at out_off.
+struct CdrSlot {
+  uint8_t kind;   // rtps_cdr_op_kind or CDR_SLOT_ZERO
+  uint8_t size;   // primitive size
+  uint16_t op;    // decode op index (position / length table row)
+  uint32_t out_off;
+  uint32_t dwords;
+  uint32_t count;  // PRIM 1, ARRAY count, others unused
+  float inv_dwords;  // 1/dwords for the item -> (record, word) split
+};
+
 struct CdrProg {  // passed by value as a kernel argument (wave-uniform)
   rtps_cdr_op ops[RTPS_CDR_MAX_OPS];
+  CdrSlot slots[CDR_MAX_SLOTS];
   uint32_t n_ops;
+  uint32_t n_slots;
   uint32_t row_bytes;
+  uint32_t lds_per_wave;  // bytes of the per-wave LDS table
 };
 struct CdrArgs {
   const uint8_t* arena;
@@ -22,5 +39,8 @@ struct CdrArgs {
   uint8_t* row_status;
 };
 
-// Validates nothing (the caller does); returns 0 or -1 on a launch error.
-int rtps_cdr_launch(hipStream_t s, const CdrProg& P, const CdrArgs& a, uint32_t max_blocks);
+// Builds the slot list from validated ops (host).  Returns false if slots overlap
+// or leave the row.
+bool rtps_cdr_build_slots(CdrProg& P);
+// Launches the decode; returns 0 or -1 on a launch error.
+int rtps_cdr_launch(hipStream_t s, const CdrProg& P, const CdrArgs& a, uint32_t cus);

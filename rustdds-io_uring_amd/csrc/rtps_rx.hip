@@ -1103,6 +1103,7 @@ int rtps_rx_cdr_decode(rtps_rx_ctx* c, const rtps_cdr_op* prog, uint32_t n_ops, 
   }
   P.n_ops = n_ops;
   P.row_bytes = row_bytes;
+  if (!rtps_cdr_build_slots(P)) return RTPS_RX_EINVAL;
   if (max_records == 0) return RTPS_RX_OK;
   (void)hipSetDevice(c->device);
   CdrArgs a{arena, arena_len, dgram_off, records, n_records, max_records, rows, row_status};

@@ -61,46 +61,44 @@ class CdrType:
         ops, names, formats, offsets = [], [], [], []
         self._layout = []  # (name, kind, spec) in program order, for encoders/decoders
         pos = 0
-        max_align = 4
 
         def add(name, spec):
-            nonlocal pos, max_align
+            nonlocal pos
             if isinstance(spec, CdrType):
                 for sub_name, sub_spec in spec.fields:
                     add(f"{name}.{sub_name}", sub_spec)
                 return
+            # every slot is 4-aligned and a multiple of 4 bytes (include/rtps_rx.h)
             if isinstance(spec, str) and spec in PRIMS:
                 dt = np.dtype(PRIMS[spec])
-                a, kind, size, count, fmt = dt.itemsize, OP_PRIM, dt.itemsize, 1, dt
+                kind, size, count, fmt, slot = OP_PRIM, dt.itemsize, 1, dt, _align(dt.itemsize, 4)
             elif spec == "bool":
-                a, kind, size, count, fmt = 1, OP_BOOL, 1, 1, np.dtype("u1")
+                kind, size, count, fmt, slot = OP_BOOL, 1, 1, np.dtype("u1"), 4
             elif isinstance(spec, String):
-                a, kind, size, count = 4, OP_STRING, 1, spec.cap
-                fmt = np.dtype([("len", "<u4"), ("data", f"S{max(spec.cap, 1)}")])
+                kind, size, count, slot = OP_STRING, 1, spec.cap, 4 + _align(spec.cap, 4)
+                fmt = np.dtype([("len", "<u4")] + ([("data", f"S{_align(spec.cap, 4)}")] if spec.cap else []))
             elif isinstance(spec, Seq):
                 dt = np.dtype(PRIMS[spec.prim])
-                a, kind, size, count = 4, OP_SEQ, dt.itemsize, spec.cap
-                fmt = np.dtype([("n", "<u4"), ("data", dt, (max(spec.cap, 1),))])
+                kind, size, count, slot = OP_SEQ, dt.itemsize, spec.cap, 4 + _align(dt.itemsize * spec.cap, 4)
+                fmt = np.dtype([("n", "<u4")] + ([("data", dt, (spec.cap,))] if spec.cap else []))
             elif isinstance(spec, Array):
                 dt = np.dtype(PRIMS[spec.prim])
-                a, kind, size, count = dt.itemsize, OP_ARRAY, dt.itemsize, spec.n
-                fmt = np.dtype((dt, (max(spec.n, 1),)))
+                kind, size, count, slot = OP_ARRAY, dt.itemsize, spec.n, _align(dt.itemsize * spec.n, 4)
+                fmt = np.dtype((dt, (spec.n,)))
             else:
                 raise TypeError(f"unsupported field spec {spec!r} for {name}")
-            pos = _align(pos, a)
-            max_align = max(max_align, a)
             ops.append((kind, size, 0, count, pos))
             names.append(name)
             formats.append(fmt)
             offsets.append(pos)
             self._layout.append((name, kind, spec))
-            pos += fmt.itemsize
+            pos += slot
 
         for name, spec in self.fields:
             add(name, spec)
         if len(ops) > MAX_OPS:
             raise ValueError(f"{len(ops)} ops > {MAX_OPS}")
-        self.row_bytes = max(_align(pos, max_align), 4)
+        self.row_bytes = max(pos, 4)
         self.ops = np.array(ops, dtype=OP_DTYPE)
         self.row_dtype = np.dtype({"names": names, "formats": formats, "offsets": offsets,
                                    "itemsize": self.row_bytes})
@@ -121,7 +119,7 @@ class CdrType:
             if kind == OP_STRING:
                 out[name] = v.tobytes()[4:4 + int(v["len"])].decode()
             elif kind == OP_SEQ:
-                out[name] = v["data"][: int(v["n"])].tolist()
+                out[name] = v["data"][: int(v["n"])].tolist() if spec.cap else []
             elif kind == OP_ARRAY:
                 out[name] = v.tolist()
             elif kind == OP_BOOL:
