@@ -50,3 +50,34 @@ extern "C" int diag_ceiling(int mode, const uint8_t* arena, const uint64_t* off,
   }
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+
+// ---- copy ceilings for the CDR decode (T: 976 value bytes per datagram -> 976-B rows) ----
+// mode 0: one wave per record, 16 B per lane (the decode's wide-slot shape)
+// mode 1: flat grid, one 16-B quad per thread (pure streaming gather)
+typedef uint4 u128u __attribute__((aligned(1)));
+__global__ __launch_bounds__(256) void copy_wave_kernel(const uint8_t* arena, const uint64_t* off, uint32_t n,
+                                                        uint8_t* rows, uint32_t row_bytes, uint32_t skip) {
+  const uint32_t lane = threadIdx.x & 63, nq = row_bytes / 16;
+  for (uint64_t r = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < n; r += (uint64_t)gridDim.x * 4) {
+    const uint8_t* src = arena + off[r] + skip;
+    for (uint32_t q = lane; q < nq; q += 64)
+      *(u128u*)(rows + r * row_bytes + 16 * q) = *(const u128u*)(src + 16 * q);
+  }
+}
+__global__ __launch_bounds__(256) void copy_flat_kernel(const uint8_t* arena, const uint64_t* off, uint32_t n,
+                                                        uint8_t* rows, uint32_t row_bytes, uint32_t skip) {
+  const uint32_t nq = row_bytes / 16;
+  const uint64_t total = (uint64_t)n * nq;
+  for (uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (uint64_t)gridDim.x * 256) {
+    const uint64_t r = t / nq, q = t - r * nq;
+    *(u128u*)(rows + r * row_bytes + 16 * q) = *(const u128u*)(arena + off[r] + skip + 16 * q);
+  }
+}
+extern "C" int diag_copy(int mode, const uint8_t* arena, const uint64_t* off, uint32_t n, uint8_t* rows,
+                         uint32_t row_bytes, uint32_t skip, uint32_t blocks, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (mode == 0) hipLaunchKernelGGL(copy_wave_kernel, dim3(blocks), dim3(256), 0, s, arena, off, n, rows, row_bytes, skip);
+  else if (mode == 1) hipLaunchKernelGGL(copy_flat_kernel, dim3(blocks), dim3(256), 0, s, arena, off, n, rows, row_bytes, skip);
+  else return -1;
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}

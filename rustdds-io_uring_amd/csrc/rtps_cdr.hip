@@ -140,23 +140,113 @@ __device__ uint8_t cdr_validate(const CdrProg& P, const uint8_t* v, uint32_t len
   return RTPS_CDR_OK;
 }
 
-// Word j of a run of nb bytes of `size`-byte elements at src, in host order;
-// bytes at or past nb are zero and never read.
-__device__ __forceinline__ uint32_t data_word(const uint8_t* src, uint32_t j, uint32_t nb, uint32_t size, bool le) {
-  const uint32_t b = 4u * j;
-  if (b >= nb) return 0u;
-  uint32_t x;
-  if (b + 4 <= nb) {
-    x = *(const u32u*)(src + ((!le && size == 8) ? (b ^ 4u) : b));
-  } else {  // 1..3 trailing bytes (size 1 or 2 only)
-    x = 0;
-    for (uint32_t t = 0; t < nb - b; ++t) x |= (uint32_t)src[b + t] << (8 * t);
-  }
+#ifndef CDR_UNROLL_N
+#define CDR_UNROLL_N 8
+#endif
+#ifndef CDR_RUN_N
+#define CDR_RUN_N 4
+#endif
+#ifndef CDR_ABLATE
+#define CDR_ABLATE 0  // timing ablations (wrong output): 1 phase A only, 2 no narrow slots, 3 no wide slots
+#endif
+#ifndef CDR_WAVES_PER_EU
+#define CDR_WAVES_PER_EU 1
+#endif
+constexpr uint32_t CDR_UNROLL = CDR_UNROLL_N;
+constexpr uint32_t CDR_WIDE_DWORDS = 8;   // slots at least this long take the 16-B-per-lane path
+constexpr uint32_t CDR_RUN = CDR_RUN_N;   // record groups per round of the wide path
+
+typedef uint4 u128u __attribute__((aligned(1)));
+
+// Host-order fix of one loaded word (mask the bytes at or past nb, swap big-endian elements)
+__device__ __forceinline__ uint32_t fix_word(uint32_t x, uint32_t bb, uint32_t nb, uint32_t size, bool le) {
+  if (bb >= nb) return 0u;
+  const uint32_t rem = nb - bb;
+  if (rem < 4) x &= (1u << (8u * rem)) - 1u;
   if (!le) {
     if (size == 2) x = ((x & 0xff00ff00u) >> 8) | ((x & 0x00ff00ffu) << 8);
     else if (size >= 4) x = __builtin_bswap32(x);
   }
   return x;
+}
+
+// Wide slot: lane (lr, lq) handles data quad lq (16 bytes, aligned to the data
+// start) of record lr of each group of rpi = 64 / nq records (nq = quads per
+// slot; rpi = 1 and a quad loop when nq > 64), CDR_RUN groups per round so
+// several 16-B loads per lane are in flight.  A 976-byte array is one load +
+// one store per lane and record.  The header word of STRING / SEQ slots is
+// stored by the lane with lq == 0.
+__device__ __forceinline__ void wide_slot(const CdrProg& P, const CdrSlot& S, const CdrArgs& a, uint32_t hdr,
+                                          uint32_t nv, uint32_t lane, const uint32_t* meta, const uint64_t* vbase,
+                                          const uint32_t* posT, const uint32_t* lenT, uint8_t* rowc) {
+  const uint32_t dwd = S.dwords - hdr;  // data words of the slot
+  const uint32_t nq = (dwd + 3) >> 2;
+  const uint32_t rpi = nq >= 64 ? 1u : 64u / nq;
+  const uint32_t lr = nq >= 64 ? 0u : lane / nq;
+  const uint32_t lq = nq >= 64 ? lane : lane - lr * nq;
+  if (lr >= rpi) return;  // idle lanes (64 not a multiple of nq)
+  for (uint32_t q0 = 0; q0 < nq; q0 += 64) {
+    const uint32_t q = q0 + lq;
+    const uint32_t bq = 16u * q;
+    for (uint32_t r = 0; r < nv; r += rpi * CDR_RUN) {
+      uint4 x[CDR_RUN];
+      uint32_t nbv[CDR_RUN];
+#pragma unroll
+      for (uint32_t u = 0; u < CDR_RUN; ++u) {
+        const uint32_t rr = r + u * rpi + lr;
+        const uint32_t rec = min(rr, nv - 1);
+        const uint32_t m = meta[rec];
+        const bool ok = rr < nv && (m & 0xffu) == RTPS_CDR_OK && S.kind != CDR_SLOT_ZERO;
+        const uint32_t ln = hdr ? lenT[S.op * 64u + rec] : 0u;
+        const uint32_t nb = S.kind == RTPS_CDR_STRING ? ln : (S.kind == RTPS_CDR_SEQ ? ln * S.size : S.count * S.size);
+        nbv[u] = ok ? nb : 0u;
+        const uint64_t abs = vbase[rec] + posT[S.op * 64u + rec] + bq;
+        const bool fast = q < nq && bq < nbv[u] && abs + 16 <= a.arena_len;
+        x[u] = *(const u128u*)(fast ? a.arena + abs : (const uint8_t*)a.records);
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < CDR_RUN; ++u) {
+        const uint32_t rr = r + u * rpi + lr;
+        if (rr >= nv) break;
+        const uint32_t m = meta[rr];
+        const bool le = (m >> 8) != 0;
+        const uint32_t nb = nbv[u];
+        uint8_t* rowp = rowc + (uint64_t)rr * P.row_bytes + S.out_off;
+        if (hdr && q == 0) *(uint32_t*)rowp = nb ? lenT[S.op * 64u + rr] : 0u;  // nb == 0 <=> length 0 or failed row
+        if (q >= nq) continue;
+        uint32_t w[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
+        if (bq < nb) {
+          const uint64_t abs = vbase[rr] + posT[S.op * 64u + rr] + bq;
+          if (abs + 16 > a.arena_len) {  // quad runs past the arena end (rare)
+#pragma unroll
+            for (uint32_t t = 0; t < 4; ++t) {
+              w[t] = 0;
+              for (uint32_t c = 0; c < 4; ++c)
+                if (abs + 4 * t + c < a.arena_len) w[t] |= (uint32_t)a.arena[abs + 4 * t + c] << (8 * c);
+            }
+          }
+        }
+        if (!le && S.size == 8) {
+          uint32_t t0 = w[0], t2 = w[2];
+          w[0] = w[1]; w[1] = t0; w[2] = w[3]; w[3] = t2;
+        }
+        uint4 o;
+        o.x = fix_word(w[0], bq, nb, S.size, le);
+        o.y = fix_word(w[1], bq + 4, nb, S.size, le);
+        o.z = fix_word(w[2], bq + 8, nb, S.size, le);
+        o.w = fix_word(w[3], bq + 12, nb, S.size, le);
+        uint8_t* d = rowp + 4u * hdr + bq;
+        if (4 * q + 4 <= dwd) {
+          *(u128u*)d = o;
+        } else {
+          const uint32_t nw = dwd - 4 * q;
+          *(uint32_t*)d = o.x;
+          if (nw > 1) *(uint32_t*)(d + 4) = o.y;
+          if (nw > 2) *(uint32_t*)(d + 8) = o.z;
+        }
+      }
+    }
+  }
 }
 
 __device__ __forceinline__ void wave_sync() {
@@ -171,7 +261,8 @@ extern __shared__ uint8_t cdr_lds[];
 // table).  Phase B: the wave writes the chunk's rows slot by slot, one 4-byte
 // word per lane and item (item = record x word of the slot), so consecutive
 // lanes store consecutive words and every row byte is written exactly once.
-__global__ __launch_bounds__(256) void cdr_decode_kernel(CdrProg P, CdrArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CDR_WAVES_PER_EU)))
+void cdr_decode_kernel(CdrProg P, CdrArgs a) {
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, wpb = blockDim.x >> 6;
   uint8_t* T = cdr_lds + wave * P.lds_per_wave;
   uint32_t* meta = (uint32_t*)T;             // [64] status | le << 8
@@ -215,34 +306,68 @@ __global__ __launch_bounds__(256) void cdr_decode_kernel(CdrProg P, CdrArgs a) {
     uint8_t* rowc = a.rows + r0 * P.row_bytes;
     for (uint32_t si = 0; si < P.n_slots; ++si) {
       const CdrSlot S = P.slots[si];
+      const uint32_t hdr = (S.kind == RTPS_CDR_STRING || S.kind == RTPS_CDR_SEQ) ? 1u : 0u;
+#if CDR_ABLATE == 1
+      continue;  // timing ablation: phase A only
+#endif
+      if (S.dwords >= CDR_WIDE_DWORDS) {
+#if CDR_ABLATE != 3
+        wide_slot(P, S, a, hdr, nv, lane, meta, vbase, posT, lenT, rowc);
+#endif
+        continue;
+      }
+#if CDR_ABLATE == 2
+      continue;  // timing ablation: no narrow slots
+#endif
       const uint32_t total = nv * S.dwords;
-      for (uint32_t item = lane; item < total; item += 64) {
-        uint32_t rec = (uint32_t)((float)item * S.inv_dwords);
-        if (rec * S.dwords > item) rec--;
-        else if ((rec + 1) * S.dwords <= item) rec++;
-        const uint32_t k = item - rec * S.dwords;
-        const uint32_t m = meta[rec];
-        uint32_t val = 0;
-        if ((m & 0xffu) == RTPS_CDR_OK && S.kind != CDR_SLOT_ZERO) {
-          const bool lle = (m >> 8) != 0;
-          const uint8_t* src = a.arena + vbase[rec] + posT[S.op * 64u + rec];
-          switch (S.kind) {
-            case RTPS_CDR_PRIM:
-            case RTPS_CDR_ARRAY: val = data_word(src, k, S.count * S.size, S.size, lle); break;
-            case RTPS_CDR_BOOL: val = src[0]; break;
-            case RTPS_CDR_STRING: {
-              const uint32_t ln = lenT[S.op * 64u + rec];
-              val = k == 0 ? ln : data_word(src, k - 1, ln, 1, lle);
-              break;
-            }
-            default: {  // SEQ
-              const uint32_t ln = lenT[S.op * 64u + rec];
-              val = k == 0 ? ln : data_word(src, k - 1, ln * S.size, S.size, lle);
-              break;
+      const bool swap8 = S.size == 8;
+      // CDR_UNROLL independent words per lane per round, branch-free: every
+      // load of the round is in flight before the first store waits
+      for (uint32_t it0 = 0; it0 < total; it0 += 64u * CDR_UNROLL) {
+        uint32_t val[CDR_UNROLL], dst[CDR_UNROLL], keep[CDR_UNROLL], shift[CDR_UNROLL], flags[CDR_UNROLL];
+#pragma unroll
+        for (uint32_t u = 0; u < CDR_UNROLL; ++u) {
+          const uint32_t item = it0 + u * 64u + lane;
+          const bool in = item < total;
+          uint32_t rec = (uint32_t)((float)item * S.inv_dwords);
+          rec = (rec * S.dwords > item) ? rec - 1 : rec;
+          rec = ((rec + 1) * S.dwords <= item) ? rec + 1 : rec;
+          rec = in ? rec : 0u;
+          const uint32_t k = item - rec * S.dwords;
+          dst[u] = in ? rec * P.row_bytes + S.out_off + 4u * k : ~0u;
+          const uint32_t m = meta[rec];
+          const bool le = (m >> 8) != 0;
+          const bool ok = in && (m & 0xffu) == RTPS_CDR_OK && S.kind != CDR_SLOT_ZERO;
+          const uint32_t ln = hdr ? lenT[S.op * 64u + rec] : 0u;
+          const uint32_t nb = S.kind == RTPS_CDR_STRING ? ln : (S.kind == RTPS_CDR_SEQ ? ln * S.size : S.count * S.size);
+          const uint32_t j = k - hdr;  // data word index (wraps for the header word)
+          const uint32_t bb = 4u * j;
+          const bool data = ok && k >= hdr && bb < nb;
+          // absolute arena offset of the word; 8-byte big-endian elements take the other half
+          uint64_t abs = vbase[rec] + posT[S.op * 64u + rec] + ((!le && swap8) ? (bb ^ 4u) : bb);
+          abs = data ? abs : 0ull;
+          // clamp a word that would run past the arena end; its valid bytes shift down
+          const uint64_t over = (abs + 4 > a.arena_len) ? abs + 4 - a.arena_len : 0ull;
+          shift[u] = (uint32_t)over * 8u;
+          const uint32_t rem = nb - bb;
+          keep[u] = !data ? 0u : (rem >= 4 ? 0xffffffffu : ((1u << (8u * rem)) - 1u));
+          flags[u] = (ok && k < hdr ? 1u : 0u) | (le ? 2u : 0u);
+          // lanes without data read a record word instead (always in bounds, cached)
+          const uint8_t* pa = data ? a.arena + (abs - over) : (const uint8_t*)a.records;
+          val[u] = ok && k < hdr ? ln : *(const u32u*)pa;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < CDR_UNROLL; ++u) {
+          uint32_t x = val[u];
+          if (!(flags[u] & 1u)) {
+            x = (x >> shift[u]) & keep[u];
+            if (!(flags[u] & 2u)) {
+              if (S.size == 2) x = ((x & 0xff00ff00u) >> 8) | ((x & 0x00ff00ffu) << 8);
+              else if (S.size >= 4) x = __builtin_bswap32(x);
             }
           }
+          if (dst[u] != ~0u) *(uint32_t*)(rowc + dst[u]) = x;
         }
-        *(uint32_t*)(rowc + (uint64_t)rec * P.row_bytes + S.out_off + 4u * k) = val;
       }
     }
     wave_sync();  // the LDS table is reused by the wave's next chunk
