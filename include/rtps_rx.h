@@ -225,6 +225,13 @@ const char* rtps_rx_strerror(int code);
  * inside each bucket.  New: the reference has one process and no exchange. */
 int rtps_rx_bucket_by_writer(rtps_rx_ctx* ctx, const rtps_record* recs, const uint64_t* n_records,
                              uint64_t max_records, uint32_t n_dest, rtps_record* out, uint64_t* dest_counts);
+/* Same partition into fixed-capacity buckets: bucket d occupies
+ * out[d*cap, (d+1)*cap); records past position cap of their bucket are not
+ * written (dest_counts[d] > cap tells the caller).  Lets the exchange use an
+ * equal-split all-to-all whose sizes need no device-to-host round trip. */
+int rtps_rx_bucket_by_writer_padded(rtps_rx_ctx* ctx, const rtps_record* recs, const uint64_t* n_records,
+                                    uint64_t max_records, uint32_t n_dest, uint64_t cap, rtps_record* out,
+                                    uint64_t* dest_counts);
 
 /* ---- batch CDR primitive decode (a18) ------------------------------------
  * Replaces, for fixed-layout sample types, the per-sample decode

@@ -156,7 +156,14 @@ constexpr uint32_t CDR_UNROLL = CDR_UNROLL_N;
 constexpr uint32_t CDR_WIDE_DWORDS = 8;   // slots at least this long take the 16-B-per-lane path
 constexpr uint32_t CDR_RUN = CDR_RUN_N;   // record groups per round of the wide path
 
-typedef uint4 u128u __attribute__((aligned(1)));
+// 16-byte loads / stores at any byte alignment (gfx950 runs them as single
+// unaligned dwordx4 accesses)
+__device__ __forceinline__ uint4 ld16u(const uint8_t* p) {
+  uint4 v;
+  __builtin_memcpy(&v, p, 16);
+  return v;
+}
+__device__ __forceinline__ void st16u(uint8_t* p, uint4 v) { __builtin_memcpy(p, &v, 16); }
 
 // Host-order fix of one loaded word (mask the bytes at or past nb, swap big-endian elements)
 __device__ __forceinline__ uint32_t fix_word(uint32_t x, uint32_t bb, uint32_t nb, uint32_t size, bool le) {
@@ -202,7 +209,7 @@ __device__ __forceinline__ void wide_slot(const CdrProg& P, const CdrSlot& S, co
         nbv[u] = ok ? nb : 0u;
         const uint64_t abs = vbase[rec] + posT[S.op * 64u + rec] + bq;
         const bool fast = q < nq && bq < nbv[u] && abs + 16 <= a.arena_len;
-        x[u] = *(const u128u*)(fast ? a.arena + abs : (const uint8_t*)a.records);
+        x[u] = ld16u(fast ? a.arena + abs : (const uint8_t*)a.records);
       }
 #pragma unroll
       for (uint32_t u = 0; u < CDR_RUN; ++u) {
@@ -237,7 +244,7 @@ __device__ __forceinline__ void wide_slot(const CdrProg& P, const CdrSlot& S, co
         o.w = fix_word(w[3], bq + 12, nb, S.size, le);
         uint8_t* d = rowp + 4u * hdr + bq;
         if (4 * q + 4 <= dwd) {
-          *(u128u*)d = o;
+          st16u(d, o);
         } else {
           const uint32_t nw = dwd - 4 * q;
           *(uint32_t*)d = o.x;

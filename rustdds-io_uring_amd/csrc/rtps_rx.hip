@@ -784,46 +784,44 @@ __global__ __launch_bounds__(TILE) void bucket_hist_kernel(const rtps_record* re
   if (threadIdx.x < n_dest) hist[(uint64_t)blockIdx.x * n_dest + threadIdx.x] = h[threadIdx.x];
 }
 
-// one workgroup: exclusive scan of hist[t][d] over t for every d, then add the
-// bucket bases (exclusive scan of the per-destination totals)
+// one workgroup per destination d: exclusive scan of hist[t][d] over the tiles
+// t (offsets inside bucket d), and the bucket size dest_counts[d]
 __global__ __launch_bounds__(TILE) void bucket_scan_kernel(uint32_t* hist, uint32_t tiles, uint32_t n_dest,
                                                             uint64_t* dest_counts) {
-  __shared__ uint32_t part[TILE];
-  __shared__ uint32_t totals[MAX_DEST];
-  const uint32_t tid = threadIdx.x;
-  for (uint32_t d = 0; d < n_dest; ++d) {
-    uint32_t carry = 0;
-    for (uint32_t t0 = 0; t0 < tiles; t0 += TILE) {
-      uint32_t t = t0 + tid;
-      uint32_t v = t < tiles ? hist[(uint64_t)t * n_dest + d] : 0u;
-      part[tid] = v;
-      __syncthreads();
-      for (uint32_t k = 1; k < TILE; k <<= 1) {  // Hillis-Steele inclusive scan
-        uint32_t y = tid >= k ? part[tid - k] : 0u;
-        __syncthreads();
-        part[tid] += y;
-        __syncthreads();
-      }
-      if (t < tiles) hist[(uint64_t)t * n_dest + d] = carry + part[tid] - v;
-      carry += part[TILE - 1];
-      __syncthreads();
+  __shared__ uint32_t wsum[WAVES];
+  const uint32_t d = blockIdx.x, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  uint32_t carry = 0;
+  for (uint32_t t0 = 0; t0 < tiles; t0 += TILE) {
+    const uint32_t t = t0 + tid;
+    const uint32_t v = t < tiles ? hist[(uint64_t)t * n_dest + d] : 0u;
+    const uint32_t incl = wave_incl_scan(v, lane);
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t before = carry, total = carry;
+    for (uint32_t w = 0; w < WAVES; ++w) {
+      if (w < wave) before += wsum[w];
+      total += wsum[w];
     }
-    if (tid == 0) totals[d] = carry;
+    if (t < tiles) hist[(uint64_t)t * n_dest + d] = before + incl - v;
+    carry = total;
     __syncthreads();
   }
-  if (tid == 0) {
-    uint32_t acc = 0;
-    for (uint32_t d = 0; d < n_dest; ++d) { dest_counts[d] = totals[d]; uint32_t t = totals[d]; totals[d] = acc; acc += t; }
-  }
-  __syncthreads();
-  for (uint64_t k = tid; k < (uint64_t)tiles * n_dest; k += TILE) hist[k] += totals[k % n_dest];
+  if (tid == 0) dest_counts[d] = carry;
 }
 
+// cap == 0: bucket d starts at sum(dest_counts[0..d)); cap > 0: at d * cap, and
+// records at positions >= cap inside their bucket are dropped
 __global__ __launch_bounds__(TILE) void bucket_scatter_kernel(const rtps_record* recs, const uint64_t* n_rec,
                                                                uint32_t n_dest, const uint32_t* offs,
+                                                               const uint64_t* dest_counts, uint64_t cap,
                                                                rtps_record* out) {
   __shared__ uint32_t wcnt[WAVES][MAX_DEST];
+  __shared__ uint64_t base[MAX_DEST];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  if (tid == 0) {
+    uint64_t acc = 0;
+    for (uint32_t d = 0; d < n_dest; ++d) { base[d] = cap ? d * cap : acc; acc += dest_counts[d]; }
+  }
   uint64_t i = (uint64_t)blockIdx.x * TILE + tid;
   uint32_t o = (i < *n_rec) ? owner_of(recs + i, n_dest) : 0xffffffffu;
   uint32_t rank = 0;
@@ -837,11 +835,13 @@ __global__ __launch_bounds__(TILE) void bucket_scatter_kernel(const rtps_record*
   if (o != 0xffffffffu) {
     uint32_t before = 0;
     for (uint32_t w = 0; w < wave; ++w) before += wcnt[w][o];
-    uint64_t dst = (uint64_t)offs[(uint64_t)blockIdx.x * n_dest + o] + before + rank;
-    const u32x4* src = reinterpret_cast<const u32x4*>(recs + i);
-    u32x4* dp = reinterpret_cast<u32x4*>(out + dst);
-    u32x4 a = src[0], b = src[1], c = src[2], e = src[3];
-    dp[0] = a; dp[1] = b; dp[2] = c; dp[3] = e;
+    const uint64_t pos = (uint64_t)offs[(uint64_t)blockIdx.x * n_dest + o] + before + rank;
+    if (cap == 0 || pos < cap) {
+      const u32x4* src = reinterpret_cast<const u32x4*>(recs + i);
+      u32x4* dp = reinterpret_cast<u32x4*>(out + base[o] + pos);
+      u32x4 a = src[0], b = src[1], c = src[2], e = src[3];
+      dp[0] = a; dp[1] = b; dp[2] = c; dp[3] = e;
+    }
   }
 }
 
@@ -1051,8 +1051,8 @@ uint64_t rtps_rx_gen_layout_host(int wl, uint64_t seed, uint64_t first_idx, uint
 }
 
 
-int rtps_rx_bucket_by_writer(rtps_rx_ctx* c, const rtps_record* recs, const uint64_t* n_records,
-                             uint64_t max_records, uint32_t n_dest, rtps_record* out, uint64_t* dest_counts) {
+static int bucket_impl(rtps_rx_ctx* c, const rtps_record* recs, const uint64_t* n_records, uint64_t max_records,
+                       uint32_t n_dest, uint64_t cap, rtps_record* out, uint64_t* dest_counts) {
   if (!c || !recs || !n_records || !out || !dest_counts || n_dest < 1 || n_dest > MAX_DEST) return RTPS_RX_EINVAL;
   (void)hipSetDevice(c->device);
   uint64_t tiles64 = (max_records + TILE - 1) / TILE;
@@ -1068,10 +1068,23 @@ int rtps_rx_bucket_by_writer(rtps_rx_ctx* c, const rtps_record* recs, const uint
     c->bucket_bytes = need;
   }
   hipLaunchKernelGGL(bucket_hist_kernel, dim3(tiles), dim3(TILE), 0, c->stream, recs, n_records, n_dest, c->bucket_hist);
-  hipLaunchKernelGGL(bucket_scan_kernel, dim3(1), dim3(TILE), 0, c->stream, c->bucket_hist, tiles, n_dest, dest_counts);
+  hipLaunchKernelGGL(bucket_scan_kernel, dim3(n_dest), dim3(TILE), 0, c->stream, c->bucket_hist, tiles, n_dest,
+                     dest_counts);
   hipLaunchKernelGGL(bucket_scatter_kernel, dim3(tiles), dim3(TILE), 0, c->stream, recs, n_records, n_dest,
-                     c->bucket_hist, out);
+                     c->bucket_hist, dest_counts, cap, out);
   return hip_fail(hipGetLastError());
+}
+
+int rtps_rx_bucket_by_writer(rtps_rx_ctx* c, const rtps_record* recs, const uint64_t* n_records,
+                             uint64_t max_records, uint32_t n_dest, rtps_record* out, uint64_t* dest_counts) {
+  return bucket_impl(c, recs, n_records, max_records, n_dest, 0, out, dest_counts);
+}
+
+int rtps_rx_bucket_by_writer_padded(rtps_rx_ctx* c, const rtps_record* recs, const uint64_t* n_records,
+                                    uint64_t max_records, uint32_t n_dest, uint64_t cap, rtps_record* out,
+                                    uint64_t* dest_counts) {
+  if (cap == 0) return RTPS_RX_EINVAL;
+  return bucket_impl(c, recs, n_records, max_records, n_dest, cap, out, dest_counts);
 }
 
 /* a18: batch CDR decode (rtps_cdr.hip).  The program is validated here so

@@ -47,7 +47,8 @@ class _Out(ctypes.Structure):
 
 EXPORTS = ["rtps_rx_create", "rtps_rx_destroy", "rtps_rx_set_stream", "rtps_rx_set_match_table",
            "rtps_rx_parse_batch", "rtps_rx_sync", "rtps_rx_strerror", "rtps_rx_max_records_host",
-           "rtps_rx_generate", "rtps_rx_bucket_by_writer", "rtps_rx_set_spec_hint", "rtps_rx_cdr_decode"]
+           "rtps_rx_generate", "rtps_rx_bucket_by_writer", "rtps_rx_set_spec_hint", "rtps_rx_cdr_decode",
+           "rtps_rx_bucket_by_writer_padded"]
 
 
 def lib():
@@ -74,6 +75,8 @@ def lib():
         L.rtps_rx_record_size.restype = U32
         L.rtps_rx_bucket_by_writer.argtypes = [P, P, P, U64, U32, P, P]
         L.rtps_rx_bucket_by_writer.restype = I
+        L.rtps_rx_bucket_by_writer_padded.argtypes = [P, P, P, U64, U32, U64, P, P]
+        L.rtps_rx_bucket_by_writer_padded.restype = I
         L.rtps_rx_set_spec_hint.argtypes = [P, U32]
         L.rtps_rx_set_spec_hint.restype = I
         L.rtps_rx_cdr_decode.argtypes = [P, P, U32, U32, P, U64, P, P, P, U64, P, P]
@@ -233,6 +236,13 @@ class MessageReceiver:
                                         arena.data_ptr(), arena.numel(), off.data_ptr(), outs["records"].data_ptr(),
                                         outs["n_records"].data_ptr(), outs["max_records"], rows.data_ptr(),
                                         row_status.data_ptr()))
+
+    def bucket_by_writer_padded(self, outs, n_dest, cap, out_records, dest_counts):
+        """Same partition into n_dest fixed buckets of cap records (out_records[d*cap:(d+1)*cap]);
+        dest_counts gets the true sizes (> cap = overflow, records past cap dropped)."""
+        _check(lib().rtps_rx_bucket_by_writer_padded(self._h, outs["records"].data_ptr(),
+                                                     outs["n_records"].data_ptr(), outs["max_records"], n_dest, cap,
+                                                     out_records.data_ptr(), dest_counts.data_ptr()))
 
     # ---- convenience: host datagrams in, host results out ----
     def handle_received_batch(self, arena_np, off_np, len_np):

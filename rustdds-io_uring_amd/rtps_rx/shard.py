@@ -7,6 +7,16 @@ rtps_rx_bucket_by_writer) and exchanged with ONE all-to-all.  The owner then
 holds every record of its writers (ready for per-writer ordering, dedup and
 fragment assembly).  The reference has a single process and no exchange;
 this is the only collective of the path.
+
+Two modes:
+  * contiguous (cap=None): buckets back to back, split sizes read back to the
+    host (one device->host round trip per exchange); exact-size messages.
+  * padded (cap=C): every bucket is a fixed slot of C records
+    (rtps_rx_bucket_by_writer_padded), so the all-to-all has equal splits and
+    the true counts travel in a second tiny all-to-all: no host round trip,
+    fully asynchronous (exchange_async), so the exchange of batch k overlaps
+    the parse of batch k+1.  Overflow (a bucket > C) is reported by
+    overflowed(); C is sized from the previous batch's counts.
 """
 import torch
 
@@ -24,23 +34,33 @@ def owner_hash_words(words):
 class Exchange:
     """Buffers + the exchange step for one rank."""
 
-    def __init__(self, rx, max_records, world, dist, device):
+    def __init__(self, rx, max_records, world, dist, device, cap=None):
         self.rx = rx
         self.world = world
         self.dist = dist
         self.device = device
-        self.bucketed = torch.empty((max(max_records, 1), RECORD_BYTES), dtype=torch.uint8, device=device)
+        self.cap = cap
+        slots = world * cap if cap else max(max_records, 1)
+        self.bucketed = torch.empty((max(slots, 1), RECORD_BYTES), dtype=torch.uint8, device=device)
         self.counts = torch.zeros(world, dtype=torch.int64, device=device)
         self.recv_counts = torch.zeros(world, dtype=torch.int64, device=device)
+        self.received = torch.empty((max(slots, 1), RECORD_BYTES), dtype=torch.uint8, device=device) if cap else None
         backend = dist.get_backend() if dist is not None else None
         self.host_collectives = backend == "gloo"  # gloo moves CPU tensors only
 
     def bucket(self, outs):
         """Stable partition of this rank's records by owner rank (asynchronous)."""
-        self.rx.bucket_by_writer(outs, self.world, self.bucketed, self.counts)
+        if self.cap:
+            self.rx.bucket_by_writer_padded(outs, self.world, self.cap, self.bucketed, self.counts)
+        else:
+            self.rx.bucket_by_writer(outs, self.world, self.bucketed, self.counts)
 
     def exchange(self):
-        """All-to-all of the bucketed records; returns this rank's received records [m, 64] u8."""
+        """All-to-all of the bucketed records; returns (records [m, 64] u8, per-source counts list)."""
+        if self.cap:
+            for w in self.exchange_async():
+                w.wait()
+            return self.gather_received()
         dist = self.dist
         if self.host_collectives:
             counts = self.counts.cpu()
@@ -59,3 +79,32 @@ class Exchange:
         out = torch.empty((sum(recv), RECORD_BYTES), dtype=torch.uint8, device=self.device)
         dist.all_to_all_single(out, self.bucketed[:nsend], recv, send)
         return out, recv
+
+    # ---- padded mode ----
+    def exchange_async(self):
+        """Equal-split all-to-all of the padded buckets + their counts; returns the work handles
+        (wait() on them orders the caller's stream after the exchange)."""
+        assert self.cap, "exchange_async needs the padded mode"
+        dist = self.dist
+        if self.host_collectives:
+            rc = torch.zeros(self.world, dtype=torch.int64)
+            dist.all_to_all_single(rc, self.counts.cpu())
+            rv = torch.empty_like(self.received, device="cpu")
+            dist.all_to_all_single(rv, self.bucketed.cpu())
+            self.recv_counts.copy_(rc)
+            self.received.copy_(rv)
+            return []
+        w1 = dist.all_to_all_single(self.recv_counts, self.counts, async_op=True)
+        w2 = dist.all_to_all_single(self.received, self.bucketed, async_op=True)
+        return [w1, w2]
+
+    def gather_received(self):
+        """Host view after exchange_async completed: the valid records from every source in
+        rank order ([m, 64] u8 on the device) and the per-source counts."""
+        rc = self.recv_counts.cpu().tolist()
+        parts = [self.received[s * self.cap:s * self.cap + min(c, self.cap)] for s, c in enumerate(rc)]
+        return torch.cat(parts) if parts else self.received[:0], [min(c, self.cap) for c in rc]
+
+    def overflowed(self):
+        """True if a bucket of the last bucket() call had more than cap records (host sync)."""
+        return bool(self.cap) and int(self.counts.max().item()) > self.cap

@@ -2,7 +2,7 @@
 its chunk on the device, parses it, buckets by writer GUID on the device and
 exchanges records (gloo on a 1-GPU box, nccl=RCCL across GPUs); every rank
 verifies what it received against the CPU oracle.  Launch with
-python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 scripts/shard_check.py [backend]"""
+python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 scripts/shard_check.py [backend] [padded]"""
 import os
 import sys
 
@@ -20,6 +20,7 @@ from rtps_rx.shard import Exchange
 from shard_ref import owner_np
 
 backend = sys.argv[1] if len(sys.argv) > 1 else "gloo"
+padded = len(sys.argv) > 2 and sys.argv[2] == "padded"
 rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
 ngpu = torch.cuda.device_count()
 dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")) % ngpu)
@@ -38,9 +39,18 @@ rx.generate(rtps_rx.WL_C3, arena, off_t, ln_t, n, first_idx=rank * n)
 cap = rtps_rx.max_records(ln)
 outs = rx.alloc_outputs(n, cap)
 rx.parse_batch_device(arena, off_t, ln_t, n, outs)
-ex = Exchange(rx, cap, world, dist, dev)
+if padded:  # fixed bucket capacity agreed over ranks from a first contiguous bucketing
+    probe = Exchange(rx, cap, world, dist, dev)
+    probe.bucket(outs)
+    t = probe.counts.max().reshape(1)
+    t = t.cpu() if backend == "gloo" else t
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    ex = Exchange(rx, cap, world, dist, dev, cap=int(t.item()))
+else:
+    ex = Exchange(rx, cap, world, dist, dev)
 ex.bucket(outs)
 torch.cuda.synchronize(dev)
+assert not (padded and ex.overflowed())
 got, split = ex.exchange()
 torch.cuda.synchronize(dev)
 got = got.cpu().numpy().reshape(-1).view(RECORD_DTYPE)
@@ -51,7 +61,7 @@ for r in range(world):
     exp.append(recs[owner_np(recs, world) == rank])
 exp = np.concatenate(exp)
 ok = got.tobytes() == exp.tobytes()
-print(f"rank {rank}/{world} ({backend}): received {len(got)} records, expected {len(exp)}, "
+print(f"rank {rank}/{world} ({backend}{', padded' if padded else ''}): received {len(got)} records, expected {len(exp)}, "
       f"{'OK' if ok else 'MISMATCH'}", flush=True)
 dist.barrier()
 dist.destroy_process_group()

@@ -270,10 +270,26 @@ def test_bucket_by_writer_matches_reference(rx, world):
     assert counts.cpu().numpy().tolist() == exp_counts.tolist()
     got = bucketed[:int(exp_counts.sum())].cpu().numpy()
     assert got.tobytes() == exp.view(np.uint8).tobytes()
+    # padded buckets: a roomy capacity keeps everything, a tight one keeps each bucket's prefix
+    start = np.concatenate([[0], np.cumsum(exp_counts)[:-1]])
+    raw = exp.view(np.uint8).reshape(-1, 64)
+    for pcap in (int(exp_counts.max()) + 5, max(int(exp_counts.min()) // 2, 1)):
+        padded = torch.zeros((world * pcap, 64), dtype=torch.uint8, device=dev)
+        pc = torch.zeros(world, dtype=torch.int64, device=dev)
+        rx.bucket_by_writer_padded(outs, world, pcap, padded, pc)
+        rx.sync()
+        assert pc.cpu().numpy().tolist() == exp_counts.tolist()
+        pn = padded.cpu().numpy()
+        for d in range(world):
+            k = min(int(exp_counts[d]), pcap)
+            assert pn[d * pcap:d * pcap + k].tobytes() == raw[start[d]:start[d] + k].tobytes(), (pcap, d)
+            assert not pn[d * pcap + k:(d + 1) * pcap].any()
 
 
-def test_sharded_path_two_ranks_gloo():
-    """Full N=2 path (device parse + device bucket + all-to-all) on one GPU with gloo."""
+@pytest.mark.parametrize("mode", ["", "padded"])
+def test_sharded_path_two_ranks_gloo(mode):
+    """Full N=2 path (device parse + device bucket + all-to-all) on one GPU with gloo;
+    "padded" = fixed-capacity buckets with the equal-split exchange."""
     import os
     import subprocess
     import sys
@@ -281,7 +297,7 @@ def test_sharded_path_two_ranks_gloo():
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
                         "--master-addr=127.0.0.1", "--master-port=29517",
-                        os.path.join(repo, "scripts", "shard_check.py"), "gloo"],
+                        os.path.join(repo, "scripts", "shard_check.py"), "gloo"] + ([mode] if mode else []),
                        capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert r.stdout.count(" OK") == 2

@@ -29,28 +29,42 @@ def _rank_records(rank, n):
     return recs
 
 
-def _worker(rank, world, port, n, q):
+def _worker(rank, world, port, n, q, padded):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         recs = _rank_records(rank, n)
         bucketed, counts = bucket_np(recs, world)
-        ex = Exchange(rx=None, max_records=len(bucketed), world=world, dist=dist, device=torch.device("cpu"))
-        ex.bucketed[:len(bucketed)] = torch.from_numpy(bucketed.view(np.uint8).reshape(-1, 64))
-        ex.counts.copy_(torch.from_numpy(counts))
+        raw = bucketed.view(np.uint8).reshape(-1, 64)
+        if padded:  # fixed slots of cap records (what rtps_rx_bucket_by_writer_padded writes)
+            cap = int(padded)
+            ex = Exchange(rx=None, max_records=len(bucketed), world=world, dist=dist, device=torch.device("cpu"),
+                          cap=cap)
+            ex.bucketed.zero_()
+            start = np.concatenate([[0], np.cumsum(counts)[:-1]])
+            for d in range(world):
+                k = min(int(counts[d]), cap)
+                ex.bucketed[d * cap:d * cap + k] = torch.from_numpy(raw[start[d]:start[d] + k])
+            ex.counts.copy_(torch.from_numpy(counts))
+            assert ex.overflowed() == (counts.max() > cap)
+        else:
+            ex = Exchange(rx=None, max_records=len(bucketed), world=world, dist=dist, device=torch.device("cpu"))
+            ex.bucketed[:len(bucketed)] = torch.from_numpy(raw)
+            ex.counts.copy_(torch.from_numpy(counts))
         got, split = ex.exchange()
         q.put((rank, got.numpy().tobytes(), split))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_exchange_gloo(world):
+@pytest.mark.parametrize("world,padded", [(2, 0), (3, 0), (2, 8000), (3, 6000)])
+def test_exchange_gloo(world, padded):
+    """padded = fixed bucket capacity (equal-split all-to-all, counts sent alongside)."""
     n = 3000
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, q, padded)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
