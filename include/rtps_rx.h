@@ -286,6 +286,60 @@ int rtps_rx_cdr_decode(rtps_rx_ctx* ctx, const rtps_cdr_op* prog, uint32_t n_ops
                        const rtps_record* records, const uint64_t* n_records, uint64_t max_records,
                        uint8_t* rows, uint8_t* row_status);
 
+/* ---- DataFrag reassembly ---------------------------
+ * Replaces the per-reader FragmentAssembler / AssemblyBuffer
+ * (rtps/fragment_assembler.rs:23-214) driven by Reader::handle_datafrag_msg
+ * (io_uring/rtps/reader.rs:563-636), for every DATA_FRAG record with
+ * RTPS_ROUTE_PASS of a parse_batch output, in record order:
+ *   - per writer GUID the fragment size is the one of its first DATA_FRAG ever
+ *     (FragmentAssembler::new :163-169, reader.rs:638-647);
+ *   - per (writer GUID, SN) an assembly buffer of data_size bytes and
+ *     ceil(data_size / fragment_size) fragment bits is created from the first
+ *     DATA_FRAG of that SN (AssemblyBuffer::new :35-63);
+ *   - each DATA_FRAG copies min(frags_in_submessage * F, payload length) bytes
+ *     to (fragment_starting_num - 1) * F, clamped to the buffer, and sets its
+ *     fragment bits (insert_frags :65-140);
+ *   - when every bit is set the sample is emitted and the buffer dropped
+ *     (new_datafrag :172-214, is_complete :142-144).
+ * State (writer fragment sizes, incomplete buffers) persists in the context
+ * across batches.  Completed samples are emitted in completing-record order;
+ * their SerializedPayload bytes (incl. the 4-byte encapsulation) are written
+ * back to back (16-byte aligned) into `heap`.  Inputs the reference rejects
+ * by panicking (fragment bits past the buffer's count, byte ranges past its
+ * end) are clamped here. */
+typedef struct rtps_frag_sample {
+  uint8_t writer_guid[16]; /* source prefix || writer_id */
+  int64_t sn;
+  uint64_t heap_off;       /* offset of the sample bytes in the heap */
+  uint32_t data_size;      /* bytes of the SerializedPayload (incl. encapsulation) */
+  uint32_t rec_idx;        /* record (of this batch) that completed the sample */
+  uint8_t flags;           /* DATA_FRAG flags of the completing record (0x04 Key: dispose by key) */
+  uint8_t status;          /* rtps_frag_status */
+  uint16_t _r;
+  uint32_t _r2;
+} rtps_frag_sample;
+enum rtps_frag_status {
+  RTPS_FRAG_OK = 0,
+  RTPS_FRAG_SHORT = 1,     /* data_size < 4: SerializedPayload::from_bytes fails, no DDSData (:189-198) */
+  RTPS_FRAG_NO_ROOM = 2    /* heap too small: descriptor only, bytes not written */
+};
+typedef struct rtps_frag_out {
+  rtps_frag_sample* samples; /* [max_samples] */
+  uint64_t max_samples;
+  uint8_t* heap;             /* [heap_bytes] */
+  uint64_t heap_bytes;
+  uint64_t* n_samples;       /* device u64: completed samples (may exceed max_samples) */
+  uint64_t* heap_used;       /* device u64: bytes the samples need */
+  uint64_t* n_pending;       /* device u64: incomplete buffers carried to the next batch */
+} rtps_frag_out;
+/* Assemble one parsed batch (asynchronous).  arena / dgram_off / records /
+ * n_records / max_records: the batch and its parse_batch output. */
+int rtps_rx_frag_assemble(rtps_rx_ctx* ctx, const uint8_t* arena, uint64_t arena_len, const uint64_t* dgram_off,
+                          const rtps_record* records, const uint64_t* n_records, uint64_t max_records,
+                          const rtps_frag_out* out);
+/* Drop every incomplete buffer and the writer fragment sizes (a new reader). */
+int rtps_rx_frag_reset(rtps_rx_ctx* ctx);
+
 /* Upper bound on records for datagram lengths (host arrays): sum((len-20)/4). */
 uint64_t rtps_rx_max_records_host(const uint32_t* dgram_len, uint32_t n);
 

@@ -14,7 +14,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _REPO = os.path.dirname(_HERE)
 sys.path.insert(0, os.path.join(_REPO, "rustdds-io_uring_amd"))
-from rtps_rx.records import RECORD_DTYPE, MATCH_DTYPE, max_records  # noqa: E402
+from rtps_rx.records import RECORD_DTYPE, MATCH_DTYPE, FRAG_SAMPLE_DTYPE, max_records  # noqa: E402
 
 LIB_PATH = os.path.join(_HERE, "librtps_oracle.so")
 _lib = None
@@ -45,6 +45,12 @@ def lib():
         L.rtps_oracle_gen_fill.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
                                            ctypes.c_uint32, P, P]
         L.rtps_oracle_record_size.restype = ctypes.c_uint32
+        L.rtps_oracle_frag_new.restype = P
+        L.rtps_oracle_frag_free.argtypes = [P]
+        L.rtps_oracle_frag_pending.restype = ctypes.c_uint64
+        L.rtps_oracle_frag_pending.argtypes = [P]
+        L.rtps_oracle_frag_batch.restype = ctypes.c_uint64
+        L.rtps_oracle_frag_batch.argtypes = [P, P, P, P, ctypes.c_uint64, P, ctypes.c_uint64, P, ctypes.c_uint64, P]
         L.rtps_oracle_cdr_decode.restype = None
         L.rtps_oracle_cdr_decode.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32, P, P, P, ctypes.c_uint64, P, P]
         assert L.rtps_oracle_record_size() == RECORD_DTYPE.itemsize
@@ -112,3 +118,32 @@ def cdr_decode(sample_type, arena, offs, recs):
     lib().rtps_oracle_cdr_decode(_ptr(ops), len(ops), sample_type.row_bytes, _ptr(arena), _ptr(offs),
                                  _ptr(recs) if m else None, m, _ptr(rows), _ptr(status))
     return rows[:m], status[:m]
+
+
+class FragAssembler:
+    """Sequential DataFrag reassembly with state across batches (rtps_oracle_frag_*)."""
+
+    def __init__(self):
+        self.h = ctypes.c_void_p(lib().rtps_oracle_frag_new())
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().rtps_oracle_frag_free(self.h)
+            self.h = None
+
+    def pending(self):
+        return int(lib().rtps_oracle_frag_pending(self.h))
+
+    def batch(self, arena, offs, recs, max_samples=None, heap_bytes=None):
+        """-> (samples FRAG_SAMPLE_DTYPE[n], heap u8[heap_used], n_completed, heap_used)."""
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        recs = np.ascontiguousarray(recs, dtype=RECORD_DTYPE)
+        ms = len(recs) if max_samples is None else max_samples
+        hb = (int(arena.nbytes) + 16 * len(recs) + (1 << 22)) if heap_bytes is None else heap_bytes
+        samples = np.zeros(max(ms, 1), dtype=FRAG_SAMPLE_DTYPE)
+        heap = np.zeros(max(hb, 1), dtype=np.uint8)
+        used = ctypes.c_uint64()
+        n = lib().rtps_oracle_frag_batch(self.h, _ptr(arena), _ptr(offs), _ptr(recs) if len(recs) else None,
+                                         len(recs), _ptr(samples), ms, _ptr(heap), hb, ctypes.byref(used))
+        return samples[:min(n, ms)], heap[:min(used.value, hb)], int(n), int(used.value)

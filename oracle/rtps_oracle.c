@@ -771,3 +771,164 @@ void rtps_oracle_cdr_decode(const rtps_cdr_op* prog, uint32_t n_ops, uint32_t ro
     status[r] = st;
   }
 }
+
+/* ------------------------------------------------------------------------ */
+/* DataFrag reassembly                                */
+/*   FragmentAssembler / AssemblyBuffer   rtps/fragment_assembler.rs:23-214  */
+/*   driven by Reader::handle_datafrag_msg io_uring/rtps/reader.rs:563-647    */
+/* Sequential restatement with state kept across batches.                    */
+/* ------------------------------------------------------------------------ */
+typedef struct fa_writer { uint8_t guid[16]; uint16_t frag_size; int used; } fa_writer;
+typedef struct fa_buf {      /* AssemblyBuffer (:23-33) */
+  uint8_t guid[16];
+  int64_t sn;
+  uint32_t data_size, count, nset;
+  uint8_t* bytes;            /* buffer_bytes, zero-initialised (:49-50) */
+  uint8_t* bits;             /* received_bitmap */
+  int used;
+} fa_buf;
+typedef struct rtps_oracle_frag {
+  fa_writer* w; size_t wcap, wn;
+  fa_buf* b; size_t bcap, bn;
+} rtps_oracle_frag;
+
+static uint64_t fa_hash(const uint8_t* k, size_t n) {
+  uint64_t h = 1469598103934665603ull;
+  for (size_t i = 0; i < n; ++i) { h ^= k[i]; h *= 1099511628211ull; }
+  return h ^ (h >> 29);
+}
+static fa_writer* fa_writer_get(rtps_oracle_frag* f, const uint8_t guid[16], int create) {
+  if (create && (f->wn + 1) * 2 > f->wcap) {
+    size_t ncap = f->wcap ? f->wcap * 2 : 64;
+    fa_writer* nw = (fa_writer*)calloc(ncap, sizeof(fa_writer));
+    for (size_t i = 0; i < f->wcap; ++i)
+      if (f->w[i].used) {
+        size_t j = fa_hash(f->w[i].guid, 16) & (ncap - 1);
+        while (nw[j].used) j = (j + 1) & (ncap - 1);
+        nw[j] = f->w[i];
+      }
+    free(f->w); f->w = nw; f->wcap = ncap;
+  }
+  if (!f->wcap) return NULL;
+  size_t j = fa_hash(guid, 16) & (f->wcap - 1);
+  while (f->w[j].used) {
+    if (!memcmp(f->w[j].guid, guid, 16)) return &f->w[j];
+    j = (j + 1) & (f->wcap - 1);
+  }
+  if (!create) return NULL;
+  f->w[j].used = 1; memcpy(f->w[j].guid, guid, 16); f->wn++;
+  return &f->w[j];
+}
+static void fa_key(uint8_t k[24], const uint8_t guid[16], int64_t sn) { memcpy(k, guid, 16); memcpy(k + 16, &sn, 8); }
+static fa_buf* fa_buf_find(rtps_oracle_frag* f, const uint8_t guid[16], int64_t sn, size_t* slot) {
+  if (!f->bcap) return NULL;
+  uint8_t k[24];
+  fa_key(k, guid, sn);
+  size_t j = fa_hash(k, 24) & (f->bcap - 1);
+  while (f->b[j].used) {
+    if (f->b[j].used == 1 && f->b[j].sn == sn && !memcmp(f->b[j].guid, guid, 16)) { if (slot) *slot = j; return &f->b[j]; }
+    j = (j + 1) & (f->bcap - 1);
+  }
+  return NULL;
+}
+static void fa_buf_rehash(rtps_oracle_frag* f, size_t ncap) {
+  fa_buf* nb = (fa_buf*)calloc(ncap, sizeof(fa_buf));
+  for (size_t i = 0; i < f->bcap; ++i)
+    if (f->b[i].used == 1) {
+      uint8_t k[24];
+      fa_key(k, f->b[i].guid, f->b[i].sn);
+      size_t j = fa_hash(k, 24) & (ncap - 1);
+      while (nb[j].used) j = (j + 1) & (ncap - 1);
+      nb[j] = f->b[i];
+    }
+  free(f->b); f->b = nb; f->bcap = ncap;
+}
+static fa_buf* fa_buf_new(rtps_oracle_frag* f, const uint8_t guid[16], int64_t sn) {
+  if ((f->bn + 1) * 2 > f->bcap) fa_buf_rehash(f, f->bcap ? f->bcap * 2 : 64);
+  uint8_t k[24];
+  fa_key(k, guid, sn);
+  size_t j = fa_hash(k, 24) & (f->bcap - 1);
+  while (f->b[j].used == 1) j = (j + 1) & (f->bcap - 1);
+  memset(&f->b[j], 0, sizeof(fa_buf));
+  f->b[j].used = 1; memcpy(f->b[j].guid, guid, 16); f->b[j].sn = sn; f->bn++;
+  return &f->b[j];
+}
+static void fa_buf_drop(rtps_oracle_frag* f, fa_buf* b) {
+  free(b->bytes); free(b->bits);
+  b->bytes = NULL; b->bits = NULL;
+  b->used = 2;  /* tombstone */
+  f->bn--;
+  fa_buf_rehash(f, f->bcap);  /* clears tombstones (test sizes: fine) */
+}
+
+rtps_oracle_frag* rtps_oracle_frag_new(void) { return (rtps_oracle_frag*)calloc(1, sizeof(rtps_oracle_frag)); }
+void rtps_oracle_frag_free(rtps_oracle_frag* f) {
+  if (!f) return;
+  for (size_t i = 0; i < f->bcap; ++i) if (f->b[i].used == 1) { free(f->b[i].bytes); free(f->b[i].bits); }
+  free(f->b); free(f->w); free(f);
+}
+uint64_t rtps_oracle_frag_pending(const rtps_oracle_frag* f) { return f->bn; }
+
+/* One batch: every RTPS_DATA_FRAG record with ROUTE_PASS, in record order.
+ * Returns the number of completed samples (descriptors beyond max_samples and
+ * bytes beyond heap_bytes are not written, as in rtps_rx_frag_assemble). */
+uint64_t rtps_oracle_frag_batch(rtps_oracle_frag* f, const uint8_t* arena, const uint64_t* off,
+                                const rtps_record* recs, uint64_t n_recs, rtps_frag_sample* samples,
+                                uint64_t max_samples, uint8_t* heap, uint64_t heap_bytes, uint64_t* heap_used) {
+  uint64_t ns = 0, used = 0;
+  for (uint64_t r = 0; r < n_recs; ++r) {
+    const rtps_record* rec = &recs[r];
+    if (rec->kind != RTPS_DATA_FRAG || !(rec->route & RTPS_ROUTE_PASS)) continue;
+    uint8_t guid[16];
+    memcpy(guid, rec->prefix, 12);
+    memcpy(guid + 12, rec->writer_id, 4);
+    /* Reader::fragment_assembler_mutable: or_insert_with(FragmentAssembler::new(datafrag.fragment_size)) */
+    fa_writer* w = fa_writer_get(f, guid, 0);
+    if (!w) { w = fa_writer_get(f, guid, 1); w->frag_size = rec->u.frag.frag_size; }
+    const uint32_t F = w->frag_size;
+    /* assembly_buffers.entry(writer_sn).or_insert_with(|| AssemblyBuffer::new(datafrag)) */
+    fa_buf* b = fa_buf_find(f, guid, rec->sn, NULL);
+    if (!b) {
+      b = fa_buf_new(f, guid, rec->sn);
+      const uint32_t ds = rec->u.frag.data_size, fs = rec->u.frag.frag_size;  /* 1 <= fs <= ds (parse) */
+      b->data_size = ds;
+      b->count = ds / fs + (ds % fs > 0);  /* total_number_of_fragments, data_frag.rs:97-119 */
+      b->bytes = (uint8_t*)calloc(ds ? ds : 1, 1);
+      b->bits = (uint8_t*)calloc(b->count ? b->count : 1, 1);
+    }
+    /* insert_frags (:65-140) with frag_size = the assembler's F */
+    const uint64_t start0 = (uint64_t)rec->u.frag.frag_start - 1;
+    const uint64_t fis = rec->u.frag.frags_in_sub;
+    const uint64_t pl_len = rec->u.frag.pl_len;
+    const uint64_t from = start0 * F;
+    uint64_t to = from + (fis * F < pl_len ? fis * F : pl_len);
+    if (to > b->data_size) to = b->data_size;
+    if (to > from)  /* reference: to < from panics (usize underflow); clamped to nothing here */
+      memcpy(b->bytes + from, arena + off[rec->dgram_idx] + rec->u.frag.pl_off, (size_t)(to - from));
+    for (uint64_t k = 0; k < fis; ++k) {
+      const uint64_t bit = start0 + k;
+      if (bit >= b->count) break;  /* reference: BitVec::set panics; ignored here */
+      if (!b->bits[bit]) { b->bits[bit] = 1; b->nset++; }
+    }
+    if (b->nset == b->count) {  /* is_complete -> remove, SerializedPayload::from_bytes */
+      if (ns < max_samples) {
+        rtps_frag_sample* s = &samples[ns];
+        memset(s, 0, sizeof(*s));
+        memcpy(s->writer_guid, guid, 16);
+        s->sn = rec->sn;
+        s->data_size = b->data_size;
+        s->rec_idx = (uint32_t)r;
+        s->flags = rec->flags;
+        s->heap_off = used;
+        s->status = b->data_size < 4 ? RTPS_FRAG_SHORT : RTPS_FRAG_OK;
+        if (used + b->data_size <= heap_bytes) memcpy(heap + used, b->bytes, b->data_size);
+        else s->status = RTPS_FRAG_NO_ROOM;
+      }
+      used += ((uint64_t)b->data_size + 15) & ~15ull;
+      ns++;
+      fa_buf_drop(f, b);
+    }
+  }
+  if (heap_used) *heap_used = used;
+  return ns;
+}

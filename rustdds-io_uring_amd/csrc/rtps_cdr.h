@@ -6,18 +6,28 @@
 
 #include "../../include/rtps_rx.h"
 
-constexpr uint32_t CDR_MAX_SLOTS = 2 * RTPS_CDR_MAX_OPS + 1;  // op slots + zero gaps
-constexpr uint8_t CDR_SLOT_ZERO = 0;                          // gap between op slots
+constexpr uint32_t CDR_MAX_SLOTS = 144;  // op slots + zero gaps + segments (kernel-argument budget)
+constexpr uint8_t CDR_SLOT_ZERO = 0;     // gap between op slots
+constexpr uint8_t CDR_SLOT_SEG = 0x10;   // merged run of op slots, copied as one block for LE records
+constexpr uint8_t CDR_IN_SEG = 1;        // flag: op slot covered by a segment (written here only for
+                                         // records that are not decoded little-endian)
 
 // One write-phase slot of the row: `dwords` 4-byte words at out_off.
+//
+// Segment: a run of >= 2 consecutive ops, all PRIM/ARRAY of 4/8-byte elements
+// at wire offsets known on the host (no STRING/SEQ before them), whose row
+// slots and wire bytes are both contiguous.  For a little-endian record the run
+// is one memcpy of dwords*4 bytes from value + wire_off.
 struct CdrSlot {
-  uint8_t kind;   // rtps_cdr_op_kind or CDR_SLOT_ZERO
-  uint8_t size;   // primitive size
+  uint8_t kind;   // rtps_cdr_op_kind, CDR_SLOT_ZERO or CDR_SLOT_SEG
+  uint8_t size;   // primitive size (SEG: 4)
+  uint8_t flags;  // CDR_IN_SEG
+  uint8_t _r;
   uint16_t op;    // decode op index (position / length table row)
+  uint16_t _r2;
   uint32_t out_off;
   uint32_t dwords;
-  uint32_t count;  // PRIM 1, ARRAY count, others unused
-  float inv_dwords;  // 1/dwords for the item -> (record, word) split
+  uint32_t count;  // PRIM 1, ARRAY count; SEG: wire offset of the run in the value
 };
 
 struct CdrProg {  // passed by value as a kernel argument (wave-uniform)

@@ -144,10 +144,13 @@ __device__ uint8_t cdr_validate(const CdrProg& P, const uint8_t* v, uint32_t len
 #define CDR_UNROLL_N 8
 #endif
 #ifndef CDR_RUN_N
-#define CDR_RUN_N 4
+#define CDR_RUN_N 2
 #endif
 #ifndef CDR_ABLATE
 #define CDR_ABLATE 0  // timing ablations (wrong output): 1 phase A only, 2 no narrow slots, 3 no wide slots
+#endif
+#ifndef CDR_GRID_MULT
+#define CDR_GRID_MULT 1  // grid cap = resident blocks x this
 #endif
 #ifndef CDR_WAVES_PER_EU
 #define CDR_WAVES_PER_EU 1
@@ -198,23 +201,29 @@ __device__ __forceinline__ void wide_slot(const CdrProg& P, const CdrSlot& S, co
     for (uint32_t r = 0; r < nv; r += rpi * CDR_RUN) {
       uint4 x[CDR_RUN];
       uint32_t nbv[CDR_RUN];
+      bool own[CDR_RUN];  // this slot writes record rr (segments vs their member slots)
 #pragma unroll
       for (uint32_t u = 0; u < CDR_RUN; ++u) {
         const uint32_t rr = r + u * rpi + lr;
         const uint32_t rec = min(rr, nv - 1);
         const uint32_t m = meta[rec];
-        const bool ok = rr < nv && (m & 0xffu) == RTPS_CDR_OK && S.kind != CDR_SLOT_ZERO;
+        const bool okrec = (m & 0xffu) == RTPS_CDR_OK, le = (m >> 8) != 0;
+        const bool ok = rr < nv && okrec && S.kind != CDR_SLOT_ZERO;
         const uint32_t ln = hdr ? lenT[S.op * 64u + rec] : 0u;
-        const uint32_t nb = S.kind == RTPS_CDR_STRING ? ln : (S.kind == RTPS_CDR_SEQ ? ln * S.size : S.count * S.size);
+        const uint32_t nb = S.kind == CDR_SLOT_SEG ? 4u * S.dwords
+                          : S.kind == RTPS_CDR_STRING ? ln : (S.kind == RTPS_CDR_SEQ ? ln * S.size : S.count * S.size);
         nbv[u] = ok ? nb : 0u;
-        const uint64_t abs = vbase[rec] + posT[S.op * 64u + rec] + bq;
-        const bool fast = q < nq && bq < nbv[u] && abs + 16 <= a.arena_len;
+        own[u] = S.kind == CDR_SLOT_SEG ? (okrec && le) : (S.flags & CDR_IN_SEG) ? !(okrec && le) : true;
+        const uint32_t dpos = S.kind == CDR_SLOT_SEG ? S.count : posT[S.op * 64u + rec];
+        const uint64_t abs = vbase[rec] + dpos + bq;
+        const bool fast = own[u] && q < nq && bq < nbv[u] && abs + 16 <= a.arena_len;
         x[u] = ld16u(fast ? a.arena + abs : (const uint8_t*)a.records);
       }
 #pragma unroll
       for (uint32_t u = 0; u < CDR_RUN; ++u) {
         const uint32_t rr = r + u * rpi + lr;
         if (rr >= nv) break;
+        if (!own[u]) continue;
         const uint32_t m = meta[rr];
         const bool le = (m >> 8) != 0;
         const uint32_t nb = nbv[u];
@@ -223,7 +232,7 @@ __device__ __forceinline__ void wide_slot(const CdrProg& P, const CdrSlot& S, co
         if (q >= nq) continue;
         uint32_t w[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
         if (bq < nb) {
-          const uint64_t abs = vbase[rr] + posT[S.op * 64u + rr] + bq;
+          const uint64_t abs = vbase[rr] + (S.kind == CDR_SLOT_SEG ? S.count : posT[S.op * 64u + rr]) + bq;
           if (abs + 16 > a.arena_len) {  // quad runs past the arena end (rare)
 #pragma unroll
             for (uint32_t t = 0; t < 4; ++t) {
@@ -250,6 +259,39 @@ __device__ __forceinline__ void wide_slot(const CdrProg& P, const CdrSlot& S, co
           *(uint32_t*)d = o.x;
           if (nw > 1) *(uint32_t*)(d + 4) = o.y;
           if (nw > 2) *(uint32_t*)(d + 8) = o.z;
+        }
+      }
+    }
+  }
+}
+
+// Segment of an all-little-endian chunk: a plain block copy of dwords*4 bytes
+// per record from value + wire_off, 16 B per lane, rpi records per pass.
+__device__ __forceinline__ void seg_copy(const CdrProg& P, const CdrSlot& S, const CdrArgs& a, uint32_t nv,
+                                         uint32_t lane, const uint64_t* vbase, uint8_t* rowc) {
+  const uint32_t nb = 4u * S.dwords;
+  const uint32_t nq = (S.dwords + 3) >> 2;
+  const uint32_t rpi = nq >= 64 ? 1u : 64u / nq;
+  const uint32_t lr = nq >= 64 ? 0u : lane / nq;
+  const uint32_t lq = nq >= 64 ? lane : lane - lr * nq;
+  if (lr >= rpi) return;
+  for (uint32_t q0 = 0; q0 < nq; q0 += 64) {
+    const uint32_t q = q0 + lq;
+    if (q >= nq) break;
+    const uint32_t bq = 16u * q;
+    const bool full = bq + 16 <= nb;
+    for (uint32_t rr = lr; rr < nv; rr += rpi) {
+      const uint64_t abs = vbase[rr] + S.count + bq;
+      uint8_t* d = rowc + (uint64_t)rr * P.row_bytes + S.out_off + bq;
+      if (full && abs + 16 <= a.arena_len) {
+        st16u(d, ld16u(a.arena + abs));
+      } else {  // last partial quad (whole words) or the arena tail
+        for (uint32_t b = bq; b < nb && b < bq + 16; b += 4) {
+          uint32_t w = 0;
+          const uint64_t o = abs + (b - bq);
+          if (o + 4 <= a.arena_len) w = *(const u32u*)(a.arena + o);
+          else for (uint32_t c = 0; c < 4; ++c) if (o + c < a.arena_len) w |= (uint32_t)a.arena[o + c] << (8 * c);
+          *(uint32_t*)(d + (b - bq)) = w;
         }
       }
     }
@@ -308,12 +350,30 @@ void cdr_decode_kernel(CdrProg P, CdrArgs a) {
     }
     meta[lane] = st | (le << 8);
     vbase[lane] = vb;
+    // every record of the chunk decoded little-endian: segments are plain copies
+    // and their member slots have nothing to write
+    const bool all_okle = __all(lane >= nv || (st == RTPS_CDR_OK && le));
+    const bool all_fail = __all(lane >= nv || st != RTPS_CDR_OK);
     wave_sync();
     // ---- phase B ----
     uint8_t* rowc = a.rows + r0 * P.row_bytes;
+    if (all_fail) {  // every row of the chunk is zero: one contiguous fill
+      const uint32_t bytes = nv * P.row_bytes;
+      for (uint32_t b = 16u * lane; b < bytes; b += 1024u) {
+        if (b + 16 <= bytes) st16u(rowc + b, make_uint4(0, 0, 0, 0));
+        else for (uint32_t t = b; t < bytes; t += 4) *(uint32_t*)(rowc + t) = 0u;
+      }
+      wave_sync();
+      continue;
+    }
     for (uint32_t si = 0; si < P.n_slots; ++si) {
       const CdrSlot S = P.slots[si];
       const uint32_t hdr = (S.kind == RTPS_CDR_STRING || S.kind == RTPS_CDR_SEQ) ? 1u : 0u;
+      if (all_okle && (S.flags & CDR_IN_SEG)) continue;
+      if (all_okle && S.kind == CDR_SLOT_SEG) {
+        seg_copy(P, S, a, nv, lane, vbase, rowc);
+        continue;
+      }
 #if CDR_ABLATE == 1
       continue;  // timing ablation: phase A only
 #endif
@@ -328,6 +388,7 @@ void cdr_decode_kernel(CdrProg P, CdrArgs a) {
 #endif
       const uint32_t total = nv * S.dwords;
       const bool swap8 = S.size == 8;
+      const float inv_dwords = 1.0f / (float)S.dwords;
       // CDR_UNROLL independent words per lane per round, branch-free: every
       // load of the round is in flight before the first store waits
       for (uint32_t it0 = 0; it0 < total; it0 += 64u * CDR_UNROLL) {
@@ -336,27 +397,31 @@ void cdr_decode_kernel(CdrProg P, CdrArgs a) {
         for (uint32_t u = 0; u < CDR_UNROLL; ++u) {
           const uint32_t item = it0 + u * 64u + lane;
           const bool in = item < total;
-          uint32_t rec = (uint32_t)((float)item * S.inv_dwords);
+          uint32_t rec = (uint32_t)((float)item * inv_dwords);
           rec = (rec * S.dwords > item) ? rec - 1 : rec;
           rec = ((rec + 1) * S.dwords <= item) ? rec + 1 : rec;
           rec = in ? rec : 0u;
           const uint32_t k = item - rec * S.dwords;
-          dst[u] = in ? rec * P.row_bytes + S.out_off + 4u * k : ~0u;
           const uint32_t m = meta[rec];
           const bool le = (m >> 8) != 0;
-          const bool ok = in && (m & 0xffu) == RTPS_CDR_OK && S.kind != CDR_SLOT_ZERO;
+          const bool okrec = (m & 0xffu) == RTPS_CDR_OK;
+          const bool mine = S.kind == CDR_SLOT_SEG ? (okrec && le) : (S.flags & CDR_IN_SEG) ? !(okrec && le) : true;
+          dst[u] = (in && mine) ? rec * P.row_bytes + S.out_off + 4u * k : ~0u;
+          const bool ok = in && mine && okrec && S.kind != CDR_SLOT_ZERO;
           const uint32_t ln = hdr ? lenT[S.op * 64u + rec] : 0u;
           const uint32_t nb = S.kind == RTPS_CDR_STRING ? ln : (S.kind == RTPS_CDR_SEQ ? ln * S.size : S.count * S.size);
+          const uint32_t nbs = S.kind == CDR_SLOT_SEG ? 4u * S.dwords : nb;
           const uint32_t j = k - hdr;  // data word index (wraps for the header word)
           const uint32_t bb = 4u * j;
-          const bool data = ok && k >= hdr && bb < nb;
+          const bool data = ok && k >= hdr && bb < nbs;
           // absolute arena offset of the word; 8-byte big-endian elements take the other half
-          uint64_t abs = vbase[rec] + posT[S.op * 64u + rec] + ((!le && swap8) ? (bb ^ 4u) : bb);
+          const uint32_t dpos = S.kind == CDR_SLOT_SEG ? S.count : posT[S.op * 64u + rec];
+          uint64_t abs = vbase[rec] + dpos + ((!le && swap8) ? (bb ^ 4u) : bb);
           abs = data ? abs : 0ull;
           // clamp a word that would run past the arena end; its valid bytes shift down
           const uint64_t over = (abs + 4 > a.arena_len) ? abs + 4 - a.arena_len : 0ull;
           shift[u] = (uint32_t)over * 8u;
-          const uint32_t rem = nb - bb;
+          const uint32_t rem = nbs - bb;
           keep[u] = !data ? 0u : (rem >= 4 ? 0xffffffffu : ((1u << (8u * rem)) - 1u));
           flags[u] = (ok && k < hdr ? 1u : 0u) | (le ? 2u : 0u);
           // lanes without data read a record word instead (always in bounds, cached)
@@ -404,22 +469,66 @@ bool rtps_cdr_build_slots(CdrProg& P) {
     }
   uint32_t ns = 0;
   uint64_t at = 0;
-  auto push = [&](uint8_t kind, uint8_t size, uint32_t op, uint64_t off, uint64_t dw, uint32_t count) {
+  bool full = false;
+  auto push = [&](uint8_t kind, uint8_t size, uint32_t op, uint64_t off, uint64_t dw, uint32_t count) -> CdrSlot* {
+    if (ns >= CDR_MAX_SLOTS) { full = true; return nullptr; }
     CdrSlot& S = P.slots[ns++];
+    S = CdrSlot{};
     S.kind = kind; S.size = size; S.op = (uint16_t)op; S.out_off = (uint32_t)off; S.dwords = (uint32_t)dw;
-    S.count = count; S.inv_dwords = 1.0f / (float)dw;
+    S.count = count;
+    return &S;
   };
+  uint32_t slot_of[RTPS_CDR_MAX_OPS];
   for (uint32_t i = 0; i < P.n_ops; ++i) {
     const rtps_cdr_op& op = P.ops[order[i]];
+    slot_of[order[i]] = 0xffffffffu;
     if (op.out_off & 3u) return false;
     if (op.out_off < at) return false;  // overlap
     const uint64_t dw = slot_dwords(op);
     if (op.out_off + 4 * dw > P.row_bytes) return false;
     if (op.out_off > at) push(CDR_SLOT_ZERO, 0, 0, at, (op.out_off - at) / 4, 0);
-    if (dw) push(op.kind, op.size, order[i], op.out_off, dw, op.kind == RTPS_CDR_PRIM ? 1u : op.count);
+    if (dw) {
+      slot_of[order[i]] = ns;
+      push(op.kind, op.size, order[i], op.out_off, dw, op.kind == RTPS_CDR_PRIM ? 1u : op.count);
+    }
     at = op.out_off + 4 * dw;
   }
   if (at < P.row_bytes) push(CDR_SLOT_ZERO, 0, 0, at, (P.row_bytes - at) / 4, 0);
+  // segments over the static prefix of the program (wire offsets known here)
+  uint64_t w = 0;
+  uint32_t k = 0, run0 = 0, run_n = 0;
+  uint64_t run_wire = 0, run_out = 0, run_bytes = 0;
+  auto close_run = [&]() {
+    if (run_n >= 2) {
+      CdrSlot* S = push(CDR_SLOT_SEG, 4, run0, run_out, run_bytes / 4, (uint32_t)run_wire);
+      if (S)
+        for (uint32_t t = run0; t < run0 + run_n; ++t) P.slots[slot_of[t]].flags |= CDR_IN_SEG;
+    }
+    run_n = 0;
+  };
+  for (; k < P.n_ops; ++k) {
+    const rtps_cdr_op& op = P.ops[k];
+    if (op.kind == RTPS_CDR_STRING || op.kind == RTPS_CDR_SEQ) break;  // wire offsets turn dynamic
+    const uint64_t cnt = op.kind == RTPS_CDR_ARRAY ? op.count : 1u;
+    const uint64_t sz = op.kind == RTPS_CDR_BOOL ? 1u : op.size;
+    if (cnt == 0) {  // no bytes, no slot: ends a run (runs are consecutive op indices)
+      close_run();
+      continue;
+    }
+    w = (w + sz - 1) / sz * sz;
+    const uint64_t bytes = sz * cnt;
+    const bool cand = (op.kind == RTPS_CDR_PRIM || op.kind == RTPS_CDR_ARRAY) && sz >= 4 && w < (1ull << 32);
+    if (cand && run_n && run_out + run_bytes == op.out_off && run_wire + run_bytes == w) {
+      run_n++;
+      run_bytes += bytes;
+    } else {
+      close_run();
+      if (cand) { run0 = k; run_n = 1; run_wire = w; run_out = op.out_off; run_bytes = bytes; }
+    }
+    w += bytes;
+  }
+  close_run();
+  if (full) return false;
   P.n_slots = ns;
   P.lds_per_wave = 768u + 512u * P.n_ops;
   return true;
@@ -431,7 +540,7 @@ int rtps_cdr_launch(hipStream_t s, const CdrProg& P, const CdrArgs& a, uint32_t 
   wpb = wpb < 1 ? 1 : (wpb > 4 ? 4 : wpb);
   const uint64_t chunks = (a.max_records + 63) / 64;
   uint64_t blocks = (chunks + wpb - 1) / wpb;
-  if (blocks > max_blocks) blocks = max_blocks;
+  if (blocks > (uint64_t)max_blocks * CDR_GRID_MULT) blocks = (uint64_t)max_blocks * CDR_GRID_MULT;
   if (blocks == 0) return 0;
   hipLaunchKernelGGL(cdr_decode_kernel, dim3((uint32_t)blocks), dim3(64 * wpb), wpb * P.lds_per_wave, s, P, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -1,0 +1,20 @@
+// rtps_frag.h — internal interface of the DataFrag reassembly (rtps_frag.hip)
+// used by the C ABI in rtps_rx.hip.  Not installed; see include/rtps_rx.h.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/rtps_rx.h"
+
+struct FragState;  // persistent device state of one context (writers, pending buffers)
+
+// Creates the state lazily on first use (device `device`); returns nullptr on
+// allocation failure.
+FragState* rtps_frag_state_new(int device);
+void rtps_frag_state_free(FragState* s);
+// Drops writers and pending buffers (asynchronous on `stream`).
+int rtps_frag_state_reset(FragState* s, hipStream_t stream);
+// One batch (asynchronous on `stream`); returns an rtps_rx_status code.
+int rtps_frag_assemble(FragState* s, hipStream_t stream, const uint8_t* arena, uint64_t arena_len,
+                       const uint64_t* dgram_off, const rtps_record* records, const uint64_t* n_records,
+                       uint64_t max_records, const rtps_frag_out* out);

@@ -1,0 +1,656 @@
+// rtps_frag.hip — DataFrag reassembly on the device.
+//
+// Replaces the per-reader FragmentAssembler / AssemblyBuffer
+// (rtps/fragment_assembler.rs:23-214) driven by Reader::handle_datafrag_msg
+// (io_uring/rtps/reader.rs:563-647).  The reference walks DATA_FRAG
+// submessages one at a time; here a whole parsed batch is assembled at once,
+// with the same result as the sequential walk in record order
+// (the CPU restatement that tests/ check it against):
+//
+//  1 sort   every DATA_FRAG record with ROUTE_PASS is keyed by a 32-bit hash of
+//           (writer GUID, SN); a stable radix sort (hipCUB) groups each
+//           assembly buffer's fragments in record order (hash collisions are
+//           resolved by the walk, which compares full keys).
+//  2 writers the fragment size of a writer is the one of its first DATA_FRAG
+//           ever (FragmentAssembler::new): persistent open-addressing table,
+//           atomicMin over the batch's first records of new writers.
+//  3 walk   one thread per key run replays AssemblyBuffer::new / insert_frags /
+//           is_complete on a bitmap (starting from the buffer carried over from
+//           the previous batch, if any) and cuts the run into epochs: each
+//           completed buffer, and at most one still incomplete.
+//  4 place  completed samples are ranked by completing record (exclusive scans)
+//           and get 16-byte-aligned heap offsets; incomplete buffers get room in
+//           the next pending store.
+//  5 copy   a regular epoch (no repeated fragment, fragment size equal to the
+//           writer's, no clamping) tiles its buffer with its fragments' spans,
+//           so every record copies its span (payload, then zeros for a short
+//           payload) in parallel, one wave per record, after the carried-over
+//           bytes were copied.  Irregular epochs replay the copies in record
+//           order in one workgroup each (rare).
+//
+// Roofline: HBM-bound.  Algorithmic bytes per DATA_FRAG record = its payload
+// bytes read + the same bytes written + 64 B of the record read.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <string.h>
+
+#include <new>
+
+#include "rtps_frag.h"
+
+namespace {
+
+constexpr uint32_t FT = 256;             // threads per block
+constexpr uint32_t NONE = 0xffffffffu;
+constexpr uint32_t SENT = 0xffffffffu;   // sort key of records that are not assembled
+constexpr uint32_t FIXED = 0x80000000u;  // writer table: fragment size resolved
+
+constexpr uint32_t WCAP = 1u << 16;      // writers
+constexpr uint32_t PCAP = 1u << 16;      // pending buffers
+constexpr uint32_t PTCAP = 2 * PCAP;     // pending hash table slots
+constexpr uint64_t PBYTES = 1ull << 28;  // pending byte store (per side)
+constexpr uint64_t PWORDS = 1ull << 22;  // pending bitmap words (per side)
+
+// counters (device u64)
+enum { C_OLD_N = 0, C_NEW_N, C_NEW_BYTES, C_NEW_WORDS, C_EPOCHS, C_POOL, C_OVERFLOW, C_COUNT };
+
+enum EpochState : uint32_t { E_PENDING = 0, E_DONE = 1, E_DEAD = 2 };  // DEAD: bitmap allocation failed
+enum EpochFlags : uint32_t { EF_IRREGULAR = 1, EF_SKIP = 2 };  // SKIP: no bytes to write (no room)
+
+struct Epoch {
+  uint32_t guid[4];
+  int64_t sn;
+  uint32_t data_size, count, nset, F;
+  uint32_t state, eflags;
+  uint32_t done_rec;   // completing record
+  uint32_t rec_flags;  // DATA_FRAG flags of the completing record
+  uint32_t old_pend;   // previous batch's pending entry it continues, or NONE
+  uint32_t p0, p1;     // sorted-position range of its key run
+  uint32_t new_pend;   // new pending entry (state PENDING)
+  uint64_t bits;       // word offset of its bitmap in the walk pool
+  uint64_t dst;        // heap offset (DONE) or new pending byte offset (PENDING)
+};
+
+struct Pend {
+  uint32_t guid[4];
+  int64_t sn;
+  uint32_t data_size, count, nset, consumed;
+  uint64_t bytes;  // offset in the pending byte store
+  uint64_t bits;   // word offset in the pending bitmap store
+};
+
+__device__ __forceinline__ void guid_of(const rtps_record* r, uint32_t g[4]) {
+  const uint4 v = *(const uint4*)((const uint8_t*)r + 8);  // prefix[12] @8, writer_id @20
+  g[0] = v.x; g[1] = v.y; g[2] = v.z; g[3] = v.w;
+}
+__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+  return h;
+}
+__device__ __forceinline__ uint32_t key_hash(const uint32_t g[4], int64_t sn) {
+  uint32_t h = 0x811c9dc5u;
+  h = (h ^ g[0]) * 0x01000193u; h = (h ^ g[1]) * 0x01000193u; h = (h ^ g[2]) * 0x01000193u;
+  h = (h ^ g[3]) * 0x01000193u; h = (h ^ (uint32_t)sn) * 0x01000193u; h = (h ^ (uint32_t)(sn >> 32)) * 0x01000193u;
+  h = fmix32(h);
+  return h == SENT ? SENT - 1 : h;
+}
+__device__ __forceinline__ uint64_t writer_hash(const uint32_t g[4]) {
+  uint32_t a = 0x811c9dc5u, b = 0x9e3779b9u;
+  for (int k = 0; k < 4; ++k) { a = (a ^ g[k]) * 0x01000193u; b = fmix32(b ^ g[k]) + 0x7f4a7c15u; }
+  return (((uint64_t)fmix32(a) << 32) | fmix32(b)) | 1ull;
+}
+__device__ __forceinline__ bool same_key(const uint32_t a[4], int64_t asn, const uint32_t b[4], int64_t bsn) {
+  return a[0] == b[0] && a[1] == b[1] && a[2] == b[2] && a[3] == b[3] && asn == bsn;
+}
+__device__ __forceinline__ bool is_frag(const rtps_record* r) { return r->kind == RTPS_DATA_FRAG && (r->route & RTPS_ROUTE_PASS); }
+
+__device__ __forceinline__ uint32_t wslot_find(const uint64_t* wkey, uint64_t h) {
+  uint32_t s = (uint32_t)(h >> 7) & (WCAP - 1);
+  for (uint32_t i = 0; i < WCAP; ++i, s = (s + 1) & (WCAP - 1)) {
+    const uint64_t k = wkey[s];
+    if (k == h) return s;
+    if (k == 0) return NONE;
+  }
+  return NONE;
+}
+
+// ---- 1: sort keys ----
+__global__ __launch_bounds__(FT) void k_keys(const rtps_record* recs, const uint64_t* n_rec, uint64_t max,
+                                             uint32_t* keys, uint32_t* vals) {
+  const uint64_t n = min(*n_rec, max);
+  for (uint64_t i = (uint64_t)blockIdx.x * FT + threadIdx.x; i < max; i += (uint64_t)gridDim.x * FT) {
+    uint32_t k = SENT;
+    if (i < n && is_frag(recs + i)) {
+      uint32_t g[4];
+      guid_of(recs + i, g);
+      k = key_hash(g, recs[i].sn);
+    }
+    keys[i] = k;
+    vals[i] = (uint32_t)i;
+  }
+}
+
+// ---- 2: writers (first DATA_FRAG of each new writer) ----
+__global__ __launch_bounds__(FT) void k_writers(const rtps_record* recs, const uint32_t* skeys, const uint32_t* svals,
+                                                uint64_t max, uint64_t* wkey, uint32_t* wfirst, const uint32_t* wF,
+                                                uint64_t* ctr) {
+  for (uint64_t p = (uint64_t)blockIdx.x * FT + threadIdx.x; p < max; p += (uint64_t)gridDim.x * FT) {
+    const uint32_t k = skeys[p];
+    if (k == SENT) continue;
+    const uint32_t r = svals[p];
+    uint32_t g[4];
+    guid_of(recs + r, g);
+    if (p > 0 && skeys[p - 1] == k) {  // inside a run: only where the full key changes (collisions)
+      uint32_t h[4];
+      const uint32_t q = svals[p - 1];
+      guid_of(recs + q, h);
+      if (same_key(g, recs[r].sn, h, recs[q].sn)) continue;
+    }
+    const uint64_t wh = writer_hash(g);
+    uint32_t s = (uint32_t)(wh >> 7) & (WCAP - 1);
+    uint32_t i = 0;
+    for (; i < WCAP; ++i, s = (s + 1) & (WCAP - 1)) {
+      const uint64_t old = atomicCAS((unsigned long long*)&wkey[s], 0ull, (unsigned long long)wh);
+      if (old == 0 || old == wh) break;
+    }
+    if (i == WCAP) { atomicOr((unsigned long long*)&ctr[C_OVERFLOW], 1ull); continue; }
+    if (!(wF[s] & FIXED)) atomicMin(&wfirst[s], r);
+  }
+}
+__global__ __launch_bounds__(FT) void k_writers_fix(const rtps_record* recs, const uint64_t* wkey, uint32_t* wfirst,
+                                                    uint32_t* wF) {
+  const uint32_t s = blockIdx.x * FT + threadIdx.x;
+  if (s >= WCAP || wkey[s] == 0 || (wF[s] & FIXED) || wfirst[s] == NONE) return;
+  wF[s] = (uint32_t)recs[wfirst[s]].u.frag.frag_size | FIXED;
+  wfirst[s] = NONE;
+}
+
+// ---- 3: walk ----
+__device__ uint32_t pend_lookup(const uint32_t* ptable, const Pend* pend, uint32_t kh, const uint32_t g[4],
+                                int64_t sn) {
+  uint32_t s = kh & (PTCAP - 1);
+  for (uint32_t i = 0; i < PTCAP; ++i, s = (s + 1) & (PTCAP - 1)) {
+    const uint32_t j = ptable[s];
+    if (j == NONE) return NONE;
+    if (same_key(pend[j].guid, pend[j].sn, g, sn)) return j;
+  }
+  return NONE;
+}
+
+struct WalkArgs {
+  const rtps_record* recs;
+  const uint32_t* skeys;
+  const uint32_t* svals;
+  uint64_t max;
+  const uint64_t* wkey;
+  const uint32_t* wF;
+  Pend* old_pend;
+  const uint32_t* old_ptable;
+  const uint32_t* old_bits;
+  Epoch* epochs;
+  uint64_t max_epochs;
+  uint32_t* pool;
+  uint64_t pool_words;
+  uint32_t* pos_epoch;
+  uint32_t* dmark;
+  uint8_t* seen;  // per position: consumed by a walk pass (collision runs)
+  uint64_t* ctr;
+};
+
+__device__ uint32_t new_epoch(const WalkArgs& A, const uint32_t g[4], int64_t sn, uint32_t p0, uint32_t p1) {
+  const uint64_t e = atomicAdd((unsigned long long*)&A.ctr[C_EPOCHS], 1ull);
+  if (e >= A.max_epochs) { atomicOr((unsigned long long*)&A.ctr[C_OVERFLOW], 2ull); return NONE; }
+  Epoch& E = A.epochs[e];
+  for (int k = 0; k < 4; ++k) E.guid[k] = g[k];
+  E.sn = sn; E.state = E_PENDING; E.eflags = 0; E.done_rec = NONE; E.old_pend = NONE; E.new_pend = NONE;
+  E.p0 = p0; E.p1 = p1; E.nset = 0; E.rec_flags = 0; E.dst = 0; E.bits = 0;
+  return (uint32_t)e;
+}
+__device__ bool alloc_bits(const WalkArgs& A, Epoch& E) {
+  const uint64_t words = ((uint64_t)E.count + 31) / 32;
+  const uint64_t at = atomicAdd((unsigned long long*)&A.ctr[C_POOL], (unsigned long long)words);
+  if (at + words > A.pool_words) {
+    atomicOr((unsigned long long*)&A.ctr[C_OVERFLOW], 4ull);
+    E.state = E_DEAD;
+    E.eflags |= EF_SKIP;
+    return false;
+  }
+  E.bits = at;
+  return true;
+}
+
+__global__ __launch_bounds__(FT) void k_walk(WalkArgs A) {
+  for (uint64_t p = (uint64_t)blockIdx.x * FT + threadIdx.x; p < A.max; p += (uint64_t)gridDim.x * FT) {
+    const uint32_t key = A.skeys[p];
+    if (key == SENT || (p > 0 && A.skeys[p - 1] == key)) continue;  // not a run head
+    uint64_t p1 = p + 1;
+    while (p1 < A.max && A.skeys[p1] == key) ++p1;
+    // one pass per distinct full key of the run (more than one only on a hash collision)
+    for (uint64_t q0 = p; q0 < p1; ++q0) {
+      if (A.seen[q0]) continue;
+      uint32_t g[4];
+      const rtps_record* r0 = A.recs + A.svals[q0];
+      guid_of(r0, g);
+      const int64_t sn = r0->sn;
+      const uint64_t wh = writer_hash(g);
+      const uint32_t ws = wslot_find(A.wkey, wh);
+      const uint32_t F = ws == NONE ? 0u : (A.wF[ws] & 0xffffu);
+      // continue the buffer carried over from the previous batch
+      uint32_t e = NONE;
+      bool started = false;
+      const uint32_t j = pend_lookup(A.old_ptable, A.old_pend, key, g, sn);
+      if (j != NONE) {
+        e = new_epoch(A, g, sn, (uint32_t)p, (uint32_t)p1);
+        if (e != NONE) {
+          Epoch& E = A.epochs[e];
+          const Pend& P = A.old_pend[j];
+          A.old_pend[j].consumed = 1;
+          E.data_size = P.data_size; E.count = P.count; E.nset = P.nset; E.F = F; E.old_pend = j;
+          if (alloc_bits(A, E)) {
+            const uint64_t words = ((uint64_t)E.count + 31) / 32;
+            for (uint64_t w = 0; w < words; ++w) A.pool[E.bits + w] = A.old_bits[P.bits + w];
+            started = true;
+          }
+        }
+      }
+      for (uint64_t q = q0; q < p1; ++q) {
+        if (A.seen[q]) continue;
+        const uint32_t ri = A.svals[q];
+        const rtps_record* r = A.recs + ri;
+        uint32_t h[4];
+        guid_of(r, h);
+        if (!same_key(g, sn, h, r->sn)) continue;
+        A.seen[q] = 1;
+        const uint32_t ds = r->u.frag.data_size, fsz = r->u.frag.frag_size;
+        if (!started) {  // AssemblyBuffer::new (fragment_assembler.rs:35-63)
+          e = new_epoch(A, g, sn, (uint32_t)p, (uint32_t)p1);
+          if (e == NONE) { A.pos_epoch[q] = NONE; continue; }
+          Epoch& E = A.epochs[e];
+          E.data_size = ds;
+          E.count = ds / fsz + (ds % fsz > 0);
+          E.F = F;
+          if (!alloc_bits(A, E)) { A.pos_epoch[q] = NONE; continue; }
+          for (uint64_t w = 0; w < ((uint64_t)E.count + 31) / 32; ++w) A.pool[E.bits + w] = 0u;
+          if (F != fsz) E.eflags |= EF_IRREGULAR;  // spans do not tile the buffer
+          started = true;
+        }
+        Epoch& E = A.epochs[e];
+        A.pos_epoch[q] = e;
+        // insert_frags (:65-140): byte range and fragment bits
+        const uint64_t start0 = (uint64_t)r->u.frag.frag_start - 1, fis = r->u.frag.frags_in_sub;
+        const uint64_t from = start0 * E.F;
+        if (from > E.data_size) E.eflags |= EF_IRREGULAR;  // reference panics; clamped
+        for (uint64_t k = 0; k < fis; ++k) {
+          const uint64_t bit = start0 + k;
+          if (bit >= E.count) { E.eflags |= EF_IRREGULAR; break; }  // reference panics; ignored
+          uint32_t& word = A.pool[E.bits + bit / 32];
+          const uint32_t m = 1u << (bit & 31);
+          if (word & m) E.eflags |= EF_IRREGULAR;  // repeated fragment: copy order matters
+          else { word |= m; E.nset++; }
+        }
+        if (E.nset == E.count) {  // is_complete -> emit, drop the buffer
+          E.state = E_DONE;
+          E.done_rec = ri;
+          E.rec_flags = r->flags;
+          A.dmark[ri] = e;
+          started = false;
+        }
+      }
+    }
+  }
+}
+
+// ---- 4: place ----
+__global__ __launch_bounds__(FT) void k_place_in(const uint32_t* dmark, const Epoch* ep, uint64_t max,
+                                                 uint32_t* cnt, uint64_t* dsz) {
+  for (uint64_t r = (uint64_t)blockIdx.x * FT + threadIdx.x; r < max; r += (uint64_t)gridDim.x * FT) {
+    const uint32_t e = dmark[r];
+    cnt[r] = e != NONE;
+    dsz[r] = e != NONE ? ((uint64_t)ep[e].data_size + 15) & ~15ull : 0ull;
+  }
+}
+__global__ __launch_bounds__(FT) void k_samples(const uint32_t* dmark, Epoch* ep, const uint32_t* cnt,
+                                                const uint32_t* rank, const uint64_t* dsz, const uint64_t* hoff,
+                                                uint64_t max, rtps_frag_out out) {
+  for (uint64_t r = (uint64_t)blockIdx.x * FT + threadIdx.x; r < max; r += (uint64_t)gridDim.x * FT) {
+    if (r == max - 1) {
+      *out.n_samples = (uint64_t)rank[r] + cnt[r];
+      *out.heap_used = hoff[r] + dsz[r];
+    }
+    const uint32_t e = dmark[r];
+    if (e == NONE) continue;
+    Epoch& E = ep[e];
+    E.dst = hoff[r];
+    const uint64_t k = rank[r];
+    if (k >= out.max_samples) { E.eflags |= EF_SKIP; continue; }
+    rtps_frag_sample s;
+    memset(&s, 0, sizeof(s));
+    memcpy(s.writer_guid, E.guid, 16);
+    s.sn = E.sn;
+    s.heap_off = E.dst;
+    s.data_size = E.data_size;
+    s.rec_idx = (uint32_t)r;
+    s.flags = (uint8_t)E.rec_flags;
+    s.status = E.data_size < 4 ? RTPS_FRAG_SHORT : RTPS_FRAG_OK;
+    if (E.dst + E.data_size > out.heap_bytes) { s.status = RTPS_FRAG_NO_ROOM; E.eflags |= EF_SKIP; }
+    out.samples[k] = s;
+  }
+}
+
+// pending epochs: room in the new pending store + carry their bitmaps
+__global__ __launch_bounds__(FT) void k_pend_alloc(Epoch* ep, const uint64_t* ctr_ro, uint64_t max_epochs,
+                                                   Pend* np, uint32_t* nbits, const uint32_t* pool, uint64_t* ctr) {
+  const uint64_t ne = min(ctr_ro[C_EPOCHS], max_epochs);
+  for (uint64_t e = (uint64_t)blockIdx.x * FT + threadIdx.x; e < ne; e += (uint64_t)gridDim.x * FT) {
+    Epoch& E = ep[e];
+    if (E.state != E_PENDING) continue;
+    const uint64_t words = ((uint64_t)E.count + 31) / 32;
+    const uint64_t j = atomicAdd((unsigned long long*)&ctr[C_NEW_N], 1ull);
+    const uint64_t b = atomicAdd((unsigned long long*)&ctr[C_NEW_BYTES], ((unsigned long long)E.data_size + 15) & ~15ull);
+    const uint64_t w = atomicAdd((unsigned long long*)&ctr[C_NEW_WORDS], (unsigned long long)words);
+    if (j >= PCAP || b + E.data_size > PBYTES || w + words > PWORDS) {
+      atomicOr((unsigned long long*)&ctr[C_OVERFLOW], 8ull);
+      E.eflags |= EF_SKIP;
+      continue;
+    }
+    Pend& P = np[j];
+    for (int k = 0; k < 4; ++k) P.guid[k] = E.guid[k];
+    P.sn = E.sn; P.data_size = E.data_size; P.count = E.count; P.nset = E.nset; P.consumed = 0;
+    P.bytes = b; P.bits = w;
+    for (uint64_t t = 0; t < words; ++t) nbits[w + t] = pool[E.bits + t];
+    E.new_pend = (uint32_t)j;
+    E.dst = b;
+  }
+}
+
+// old pending entries no record of this batch continued: move to the new store
+__global__ __launch_bounds__(FT) void k_carry(const Pend* op, const uint8_t* obytes, const uint32_t* obits,
+                                              Pend* np, uint8_t* nbytes, uint32_t* nbits, uint64_t* ctr) {
+  const uint64_t n_old = ctr[C_OLD_N];
+  __shared__ uint64_t sj, sb, sw;
+  __shared__ int ok;
+  for (uint64_t i = blockIdx.x; i < n_old; i += gridDim.x) {
+    const Pend& P = op[i];
+    if (P.consumed) continue;
+    const uint64_t words = ((uint64_t)P.count + 31) / 32;
+    if (threadIdx.x == 0) {
+      sj = atomicAdd((unsigned long long*)&ctr[C_NEW_N], 1ull);
+      sb = atomicAdd((unsigned long long*)&ctr[C_NEW_BYTES], ((unsigned long long)P.data_size + 15) & ~15ull);
+      sw = atomicAdd((unsigned long long*)&ctr[C_NEW_WORDS], (unsigned long long)words);
+      ok = !(sj >= PCAP || sb + P.data_size > PBYTES || sw + words > PWORDS);
+      if (!ok) atomicOr((unsigned long long*)&ctr[C_OVERFLOW], 8ull);
+      else { Pend Q = P; Q.bytes = sb; Q.bits = sw; Q.consumed = 0; np[sj] = Q; }
+    }
+    __syncthreads();
+    if (ok) {
+      for (uint64_t b = threadIdx.x; b < P.data_size; b += FT) nbytes[sb + b] = obytes[P.bytes + b];
+      for (uint64_t t = threadIdx.x; t < words; t += FT) nbits[sw + t] = obits[P.bits + t];
+    }
+    __syncthreads();
+  }
+}
+
+// ---- 5: copy ----
+__device__ __forceinline__ uint8_t* epoch_dst(const Epoch& E, const rtps_frag_out& out, uint8_t* nbytes) {
+  return E.state == E_DONE ? out.heap + E.dst : nbytes + E.dst;
+}
+// regular epochs: carried-over bytes (or zeros for a new pending buffer) first
+__global__ __launch_bounds__(FT) void k_init(const Epoch* ep, const uint64_t* ctr, uint64_t max_epochs,
+                                             const Pend* op, const uint8_t* obytes, uint8_t* nbytes,
+                                             rtps_frag_out out) {
+  const uint64_t ne = min(ctr[C_EPOCHS], max_epochs);
+  for (uint64_t e = blockIdx.x; e < ne; e += gridDim.x) {
+    const Epoch& E = ep[e];
+    if (E.eflags & (EF_IRREGULAR | EF_SKIP)) continue;
+    if (E.state == E_DONE && E.old_pend == NONE) continue;  // its spans cover every byte
+    uint8_t* d = epoch_dst(E, out, nbytes);
+    if (E.old_pend != NONE) {
+      const uint8_t* s = obytes + op[E.old_pend].bytes;
+      for (uint64_t b = threadIdx.x; b < E.data_size; b += FT) d[b] = s[b];
+    } else {
+      for (uint64_t b = threadIdx.x; b < E.data_size; b += FT) d[b] = 0;
+    }
+  }
+}
+
+__device__ __forceinline__ uint4 ld16(const uint8_t* p) { uint4 v; __builtin_memcpy(&v, p, 16); return v; }
+__device__ __forceinline__ void st16(uint8_t* p, uint4 v) { __builtin_memcpy(p, &v, 16); }
+
+// regular epochs: every record writes its fragments' span, one wave per record
+__global__ __launch_bounds__(FT) void k_span(const rtps_record* recs, const uint8_t* arena, uint64_t arena_len,
+                                             const uint64_t* dgram_off, const uint32_t* svals,
+                                             const uint32_t* pos_epoch, const uint32_t* skeys, uint64_t max,
+                                             const Epoch* ep, uint8_t* nbytes, rtps_frag_out out) {
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  for (uint64_t p = (uint64_t)blockIdx.x * (FT / 64) + wave; p < max; p += (uint64_t)gridDim.x * (FT / 64)) {
+    if (skeys[p] == SENT) break;  // sorted: the rest are not assembled
+    const uint32_t e = pos_epoch[p];
+    if (e == NONE) continue;
+    const Epoch& E = ep[e];
+    if (E.eflags & (EF_IRREGULAR | EF_SKIP)) continue;
+    const rtps_record* r = recs + svals[p];
+    const uint64_t from = (uint64_t)(r->u.frag.frag_start - 1) * E.F;
+    const uint64_t span_end = min<uint64_t>(from + (uint64_t)r->u.frag.frags_in_sub * E.F, E.data_size);
+    const uint64_t to = min<uint64_t>(from + min<uint64_t>((uint64_t)r->u.frag.frags_in_sub * E.F, r->u.frag.pl_len),
+                                      E.data_size);
+    const uint8_t* src = arena + dgram_off[r->dgram_idx] + r->u.frag.pl_off;
+    uint8_t* d = epoch_dst(E, out, nbytes) + from;
+    const uint64_t n = span_end - from, nv = to - from;  // span bytes, payload bytes
+    const bool src16 = dgram_off[r->dgram_idx] + r->u.frag.pl_off + nv <= arena_len;  // always (parse output)
+    for (uint64_t b = 16u * lane; b < n; b += 1024u) {
+      if (b + 16 <= nv && src16) {
+        st16(d + b, ld16(src + b));
+      } else if (b + 16 <= n && b >= nv) {
+        st16(d + b, make_uint4(0, 0, 0, 0));
+      } else {
+        for (uint64_t t = b; t < b + 16 && t < n; ++t) d[t] = t < nv ? src[t] : (uint8_t)0;
+      }
+    }
+  }
+}
+
+// irregular epochs: the sequential replay (zero buffer, carried bytes, then every
+// record's clamped copy in record order), one workgroup each
+__global__ __launch_bounds__(FT) void k_serial(const rtps_record* recs, const uint8_t* arena,
+                                               const uint64_t* dgram_off, const uint32_t* svals,
+                                               const uint32_t* pos_epoch, const Epoch* ep, const uint64_t* ctr,
+                                               uint64_t max_epochs, const Pend* op, const uint8_t* obytes,
+                                               uint8_t* nbytes, rtps_frag_out out) {
+  const uint64_t ne = min(ctr[C_EPOCHS], max_epochs);
+  for (uint64_t e = blockIdx.x; e < ne; e += gridDim.x) {
+    const Epoch& E = ep[e];
+    if (!(E.eflags & EF_IRREGULAR) || (E.eflags & EF_SKIP)) continue;
+    uint8_t* d = epoch_dst(E, out, nbytes);
+    if (E.old_pend != NONE) {
+      const uint8_t* s = obytes + op[E.old_pend].bytes;
+      for (uint64_t b = threadIdx.x; b < E.data_size; b += FT) d[b] = s[b];
+    } else {
+      for (uint64_t b = threadIdx.x; b < E.data_size; b += FT) d[b] = 0;
+    }
+    __threadfence();
+    __syncthreads();
+    for (uint64_t p = E.p0; p < E.p1; ++p) {
+      if (pos_epoch[p] != e) continue;
+      const rtps_record* r = recs + svals[p];
+      const uint64_t from = (uint64_t)(r->u.frag.frag_start - 1) * E.F;
+      const uint64_t to = min<uint64_t>(from + min<uint64_t>((uint64_t)r->u.frag.frags_in_sub * E.F, r->u.frag.pl_len),
+                                        E.data_size);
+      if (to > from) {
+        const uint8_t* src = arena + dgram_off[r->dgram_idx] + r->u.frag.pl_off;
+        for (uint64_t b = threadIdx.x; b < to - from; b += FT) d[from + b] = src[b];
+      }
+      __threadfence();
+      __syncthreads();
+    }
+  }
+}
+
+// new pending hash table (for the next batch's walk)
+__global__ __launch_bounds__(FT) void k_ptable(const Pend* np, const uint64_t* ctr, uint32_t* ptable) {
+  const uint64_t n = min<uint64_t>(ctr[C_NEW_N], PCAP);
+  for (uint64_t j = (uint64_t)blockIdx.x * FT + threadIdx.x; j < n; j += (uint64_t)gridDim.x * FT) {
+    uint32_t g[4] = {np[j].guid[0], np[j].guid[1], np[j].guid[2], np[j].guid[3]};
+    uint32_t s = key_hash(g, np[j].sn) & (PTCAP - 1);
+    while (atomicCAS(&ptable[s], NONE, (uint32_t)j) != NONE) s = (s + 1) & (PTCAP - 1);
+  }
+}
+__global__ void k_finish(uint64_t* ctr, uint64_t* n_pending) {
+  const uint64_t n = min<uint64_t>(ctr[C_NEW_N], PCAP);
+  *n_pending = n | (ctr[C_OVERFLOW] ? (1ull << 63) : 0ull);
+  ctr[C_OLD_N] = n;
+}
+
+}  // namespace
+
+static inline uint64_t hmin(uint64_t a, uint64_t b) { return a < b ? a : b; }
+
+struct FragState {
+  int device = 0;
+  int cur = 0;  // pending side holding the previous batch's buffers
+  uint64_t* wkey = nullptr;
+  uint32_t* wfirst = nullptr;
+  uint32_t* wF = nullptr;
+  Pend* pend[2] = {nullptr, nullptr};
+  uint8_t* pbytes[2] = {nullptr, nullptr};
+  uint32_t* pbits[2] = {nullptr, nullptr};
+  uint32_t* ptable[2] = {nullptr, nullptr};
+  uint64_t* ctr = nullptr;
+  // per-batch scratch (grown on demand)
+  uint64_t cap = 0;
+  uint32_t *keys = nullptr, *vals = nullptr, *skeys = nullptr, *svals = nullptr;
+  uint32_t *pos_epoch = nullptr, *dmark = nullptr, *cnt = nullptr, *rank = nullptr;
+  uint8_t* seen = nullptr;
+  uint64_t *dsz = nullptr, *hoff = nullptr;
+  Epoch* epochs = nullptr;
+  uint64_t max_epochs = 0;
+  uint32_t* pool = nullptr;
+  uint64_t pool_words = 0;
+  void* tmp = nullptr;
+  size_t tmp_bytes = 0;
+};
+
+static void free_scratch(FragState* s) {
+  void* ptrs[] = {s->keys, s->vals, s->skeys, s->svals, s->pos_epoch, s->dmark, s->cnt, s->rank,
+                  s->seen, s->dsz, s->hoff, s->epochs, s->pool, s->tmp};
+  for (void* p : ptrs) if (p) (void)hipFree(p);
+  s->keys = s->vals = s->skeys = s->svals = s->pos_epoch = s->dmark = s->cnt = s->rank = nullptr;
+  s->seen = nullptr; s->dsz = s->hoff = nullptr; s->epochs = nullptr; s->pool = nullptr; s->tmp = nullptr;
+  s->cap = 0; s->tmp_bytes = 0;
+}
+
+static bool grow(FragState* s, uint64_t max, hipStream_t st) {
+  if (max <= s->cap) return true;
+  (void)hipStreamSynchronize(st);
+  free_scratch(s);
+  const uint64_t n = max;
+  bool ok = hipMalloc(&s->keys, n * 4) == hipSuccess && hipMalloc(&s->vals, n * 4) == hipSuccess &&
+            hipMalloc(&s->skeys, n * 4) == hipSuccess && hipMalloc(&s->svals, n * 4) == hipSuccess &&
+            hipMalloc(&s->pos_epoch, n * 4) == hipSuccess && hipMalloc(&s->dmark, n * 4) == hipSuccess &&
+            hipMalloc(&s->cnt, n * 4) == hipSuccess && hipMalloc(&s->rank, n * 4) == hipSuccess &&
+            hipMalloc(&s->seen, n) == hipSuccess && hipMalloc(&s->dsz, n * 8) == hipSuccess &&
+            hipMalloc(&s->hoff, n * 8) == hipSuccess;
+  s->max_epochs = n + PCAP;
+  s->pool_words = 4 * n + PWORDS;
+  ok = ok && hipMalloc(&s->epochs, s->max_epochs * sizeof(Epoch)) == hipSuccess &&
+       hipMalloc(&s->pool, s->pool_words * 4) == hipSuccess;
+  size_t b1 = 0, b2 = 0, b3 = 0;
+  ok = ok && hipcub::DeviceRadixSort::SortPairs(nullptr, b1, s->keys, s->skeys, s->vals, s->svals, (int)n, 0, 32, st) == hipSuccess;
+  ok = ok && hipcub::DeviceScan::ExclusiveSum(nullptr, b2, s->cnt, s->rank, (int)n, st) == hipSuccess;
+  ok = ok && hipcub::DeviceScan::ExclusiveSum(nullptr, b3, s->dsz, s->hoff, (int)n, st) == hipSuccess;
+  s->tmp_bytes = b1 > b2 ? (b1 > b3 ? b1 : b3) : (b2 > b3 ? b2 : b3);
+  ok = ok && hipMalloc(&s->tmp, s->tmp_bytes) == hipSuccess;
+  if (!ok) { free_scratch(s); return false; }
+  s->cap = n;
+  return true;
+}
+
+FragState* rtps_frag_state_new(int device) {
+  FragState* s = new (std::nothrow) FragState();
+  if (!s) return nullptr;
+  s->device = device;
+  bool ok = hipMalloc(&s->wkey, WCAP * 8) == hipSuccess && hipMalloc(&s->wfirst, WCAP * 4) == hipSuccess &&
+            hipMalloc(&s->wF, WCAP * 4) == hipSuccess && hipMalloc(&s->ctr, C_COUNT * 8) == hipSuccess;
+  for (int k = 0; k < 2 && ok; ++k)
+    ok = hipMalloc(&s->pend[k], PCAP * sizeof(Pend)) == hipSuccess && hipMalloc(&s->pbytes[k], PBYTES) == hipSuccess &&
+         hipMalloc(&s->pbits[k], PWORDS * 4) == hipSuccess && hipMalloc(&s->ptable[k], PTCAP * 4) == hipSuccess;
+  if (!ok) { rtps_frag_state_free(s); return nullptr; }
+  if (rtps_frag_state_reset(s, nullptr) != RTPS_RX_OK || hipDeviceSynchronize() != hipSuccess) {
+    rtps_frag_state_free(s);
+    return nullptr;
+  }
+  return s;
+}
+
+void rtps_frag_state_free(FragState* s) {
+  if (!s) return;
+  free_scratch(s);
+  void* ptrs[] = {s->wkey, s->wfirst, s->wF, s->ctr, s->pend[0], s->pend[1], s->pbytes[0], s->pbytes[1],
+                  s->pbits[0], s->pbits[1], s->ptable[0], s->ptable[1]};
+  for (void* p : ptrs) if (p) (void)hipFree(p);
+  delete s;
+}
+
+int rtps_frag_state_reset(FragState* s, hipStream_t st) {
+  bool ok = hipMemsetAsync(s->wkey, 0, WCAP * 8, st) == hipSuccess &&
+            hipMemsetAsync(s->wfirst, 0xff, WCAP * 4, st) == hipSuccess &&
+            hipMemsetAsync(s->wF, 0, WCAP * 4, st) == hipSuccess &&
+            hipMemsetAsync(s->ctr, 0, C_COUNT * 8, st) == hipSuccess &&
+            hipMemsetAsync(s->ptable[0], 0xff, PTCAP * 4, st) == hipSuccess &&
+            hipMemsetAsync(s->ptable[1], 0xff, PTCAP * 4, st) == hipSuccess;
+  s->cur = 0;
+  return ok ? RTPS_RX_OK : RTPS_RX_EHIP;
+}
+
+int rtps_frag_assemble(FragState* s, hipStream_t st, const uint8_t* arena, uint64_t arena_len,
+                       const uint64_t* dgram_off, const rtps_record* records, const uint64_t* n_records,
+                       uint64_t max_records, const rtps_frag_out* out) {
+  if (max_records > 0x7fffffffull) return RTPS_RX_ETOOBIG;
+  const uint64_t max = max_records ? max_records : 1;
+  if (!grow(s, max, st)) return RTPS_RX_ENOMEM;
+  const int o = s->cur, nw = s->cur ^ 1;
+  const uint32_t gb = (uint32_t)hmin((max + FT - 1) / FT, 8192);
+  bool ok = hipMemsetAsync(s->ctr + C_NEW_N, 0, (C_COUNT - C_NEW_N) * 8, st) == hipSuccess &&
+            hipMemsetAsync(s->pos_epoch, 0xff, max * 4, st) == hipSuccess &&
+            hipMemsetAsync(s->dmark, 0xff, max * 4, st) == hipSuccess &&
+            hipMemsetAsync(s->seen, 0, max, st) == hipSuccess &&
+            hipMemsetAsync(s->ptable[nw], 0xff, PTCAP * 4, st) == hipSuccess;
+  if (!ok) return RTPS_RX_EHIP;
+  if (max_records == 0) {
+    (void)hipMemsetAsync(out->n_samples, 0, 8, st);
+    (void)hipMemsetAsync(out->heap_used, 0, 8, st);
+  }
+  hipLaunchKernelGGL(k_keys, dim3(gb), dim3(FT), 0, st, records, n_records, max, s->keys, s->vals);
+  size_t tb = s->tmp_bytes;
+  if (hipcub::DeviceRadixSort::SortPairs(s->tmp, tb, s->keys, s->skeys, s->vals, s->svals, (int)max, 0, 32, st) !=
+      hipSuccess)
+    return RTPS_RX_EHIP;
+  hipLaunchKernelGGL(k_writers, dim3(gb), dim3(FT), 0, st, records, s->skeys, s->svals, max, s->wkey, s->wfirst,
+                     s->wF, s->ctr);
+  hipLaunchKernelGGL(k_writers_fix, dim3(WCAP / FT), dim3(FT), 0, st, records, s->wkey, s->wfirst, s->wF);
+  WalkArgs A{records, s->skeys, s->svals, max, s->wkey, s->wF, s->pend[o], s->ptable[o], s->pbits[o], s->epochs,
+             s->max_epochs, s->pool, s->pool_words, s->pos_epoch, s->dmark, s->seen, s->ctr};
+  hipLaunchKernelGGL(k_walk, dim3(gb), dim3(FT), 0, st, A);
+  hipLaunchKernelGGL(k_place_in, dim3(gb), dim3(FT), 0, st, s->dmark, s->epochs, max, s->cnt, s->dsz);
+  tb = s->tmp_bytes;
+  if (hipcub::DeviceScan::ExclusiveSum(s->tmp, tb, s->cnt, s->rank, (int)max, st) != hipSuccess) return RTPS_RX_EHIP;
+  tb = s->tmp_bytes;
+  if (hipcub::DeviceScan::ExclusiveSum(s->tmp, tb, s->dsz, s->hoff, (int)max, st) != hipSuccess) return RTPS_RX_EHIP;
+  hipLaunchKernelGGL(k_samples, dim3(gb), dim3(FT), 0, st, s->dmark, s->epochs, s->cnt, s->rank, s->dsz, s->hoff,
+                     max, *out);
+  const uint32_t ge = (uint32_t)hmin((s->max_epochs + FT - 1) / FT, 8192);
+  hipLaunchKernelGGL(k_pend_alloc, dim3(ge), dim3(FT), 0, st, s->epochs, s->ctr, s->max_epochs, s->pend[nw],
+                     s->pbits[nw], s->pool, s->ctr);
+  hipLaunchKernelGGL(k_carry, dim3(1024), dim3(FT), 0, st, s->pend[o], s->pbytes[o], s->pbits[o], s->pend[nw],
+                     s->pbytes[nw], s->pbits[nw], s->ctr);
+  hipLaunchKernelGGL(k_init, dim3(4096), dim3(FT), 0, st, s->epochs, s->ctr, s->max_epochs, s->pend[o], s->pbytes[o],
+                     s->pbytes[nw], *out);
+  hipLaunchKernelGGL(k_span, dim3((uint32_t)hmin((max + 3) / 4, 16384)), dim3(FT), 0, st, records, arena,
+                     arena_len, dgram_off, s->svals, s->pos_epoch, s->skeys, max, s->epochs, s->pbytes[nw], *out);
+  hipLaunchKernelGGL(k_serial, dim3(1024), dim3(FT), 0, st, records, arena, dgram_off, s->svals, s->pos_epoch,
+                     s->epochs, s->ctr, s->max_epochs, s->pend[o], s->pbytes[o], s->pbytes[nw], *out);
+  hipLaunchKernelGGL(k_ptable, dim3(PCAP / FT), dim3(FT), 0, st, s->pend[nw], s->ctr, s->ptable[nw]);
+  hipLaunchKernelGGL(k_finish, dim3(1), dim3(1), 0, st, s->ctr, out->n_pending);
+  if (hipGetLastError() != hipSuccess) return RTPS_RX_EHIP;
+  s->cur = nw;
+  return RTPS_RX_OK;
+}

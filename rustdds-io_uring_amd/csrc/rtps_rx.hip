@@ -35,6 +35,7 @@
 #include "../../include/rtps_rx.h"
 #include "rtps_gen.h"
 #include "rtps_cdr.h"
+#include "rtps_frag.h"
 
 namespace {
 
@@ -867,6 +868,7 @@ struct rtps_rx_ctx {
   uint32_t resident_blocks = 1024;
   uint32_t launch_parity = 0;
   uint32_t k_spec = 1;  // speculated records per datagram (0 disables nothing: see set_spec_hint)
+  FragState* frag = nullptr;  // DataFrag reassembly state (created on first use)
 };
 
 static int hip_fail(hipError_t e) { return e == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP; }
@@ -912,6 +914,7 @@ int rtps_rx_destroy(rtps_rx_ctx* c) {
   (void)hipFree(c->mt_keys);
   (void)hipFree(c->mt_slots);
   (void)hipFree(c->bucket_hist);
+  rtps_frag_state_free(c->frag);
   (void)hipStreamDestroy(c->own_stream);
   delete c;
   return RTPS_RX_OK;
@@ -1121,6 +1124,28 @@ int rtps_rx_cdr_decode(rtps_rx_ctx* c, const rtps_cdr_op* prog, uint32_t n_ops, 
   (void)hipSetDevice(c->device);
   CdrArgs a{arena, arena_len, dgram_off, records, n_records, max_records, rows, row_status};
   return rtps_cdr_launch(c->stream, P, a, c->resident_blocks) == 0 ? RTPS_RX_OK : RTPS_RX_EHIP;
+}
+
+/* DataFrag reassembly (rtps_frag.hip) */
+int rtps_rx_frag_assemble(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len, const uint64_t* dgram_off,
+                          const rtps_record* records, const uint64_t* n_records, uint64_t max_records,
+                          const rtps_frag_out* out) {
+  if (!c || !records || !n_records || !out || !out->n_samples || !out->heap_used || !out->n_pending) return RTPS_RX_EINVAL;
+  if ((out->max_samples && !out->samples) || (out->heap_bytes && !out->heap)) return RTPS_RX_EINVAL;
+  if (max_records && (!arena || !dgram_off)) return RTPS_RX_EINVAL;
+  (void)hipSetDevice(c->device);
+  if (!c->frag) {
+    c->frag = rtps_frag_state_new(c->device);
+    if (!c->frag) return RTPS_RX_ENOMEM;
+  }
+  return rtps_frag_assemble(c->frag, c->stream, arena, arena_len, dgram_off, records, n_records, max_records, out);
+}
+
+int rtps_rx_frag_reset(rtps_rx_ctx* c) {
+  if (!c) return RTPS_RX_EINVAL;
+  if (!c->frag) return RTPS_RX_OK;
+  (void)hipSetDevice(c->device);
+  return rtps_frag_state_reset(c->frag, c->stream);
 }
 
 uint32_t rtps_rx_record_size(void) { return (uint32_t)sizeof(rtps_record); }

@@ -16,7 +16,7 @@ import os
 
 import numpy as np
 
-from .records import (RECORD_DTYPE, MATCH_DTYPE, STATUS_NAMES, KIND_NAMES, WRITER_KINDS, READER_KINDS,
+from .records import (RECORD_DTYPE, MATCH_DTYPE, FRAG_SAMPLE_DTYPE, STATUS_NAMES, KIND_NAMES, WRITER_KINDS, READER_KINDS,
                       ROUTE_PASS, NO_MATCH, max_records, record_to_dict, pack_match_table)
 
 _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
@@ -40,6 +40,12 @@ class _Config(ctypes.Structure):
                 ("flags", ctypes.c_uint32)]
 
 
+class _FragOut(ctypes.Structure):
+    _fields_ = [("samples", ctypes.c_void_p), ("max_samples", ctypes.c_uint64), ("heap", ctypes.c_void_p),
+                ("heap_bytes", ctypes.c_uint64), ("n_samples", ctypes.c_void_p), ("heap_used", ctypes.c_void_p),
+                ("n_pending", ctypes.c_void_p)]
+
+
 class _Out(ctypes.Structure):
     _fields_ = [("status", ctypes.c_void_p), ("records", ctypes.c_void_p), ("max_records", ctypes.c_uint64),
                 ("match", ctypes.c_void_p), ("rec_begin", ctypes.c_void_p), ("n_records", ctypes.c_void_p)]
@@ -48,7 +54,7 @@ class _Out(ctypes.Structure):
 EXPORTS = ["rtps_rx_create", "rtps_rx_destroy", "rtps_rx_set_stream", "rtps_rx_set_match_table",
            "rtps_rx_parse_batch", "rtps_rx_sync", "rtps_rx_strerror", "rtps_rx_max_records_host",
            "rtps_rx_generate", "rtps_rx_bucket_by_writer", "rtps_rx_set_spec_hint", "rtps_rx_cdr_decode",
-           "rtps_rx_bucket_by_writer_padded"]
+           "rtps_rx_bucket_by_writer_padded", "rtps_rx_frag_assemble", "rtps_rx_frag_reset"]
 
 
 def lib():
@@ -77,6 +83,10 @@ def lib():
         L.rtps_rx_bucket_by_writer.restype = I
         L.rtps_rx_bucket_by_writer_padded.argtypes = [P, P, P, U64, U32, U64, P, P]
         L.rtps_rx_bucket_by_writer_padded.restype = I
+        L.rtps_rx_frag_assemble.argtypes = [P, P, U64, P, P, P, U64, ctypes.POINTER(_FragOut)]
+        L.rtps_rx_frag_assemble.restype = I
+        L.rtps_rx_frag_reset.argtypes = [P]
+        L.rtps_rx_frag_reset.restype = I
         L.rtps_rx_set_spec_hint.argtypes = [P, U32]
         L.rtps_rx_set_spec_hint.restype = I
         L.rtps_rx_cdr_decode.argtypes = [P, P, U32, U32, P, U64, P, P, P, U64, P, P]
@@ -243,6 +253,68 @@ class MessageReceiver:
         _check(lib().rtps_rx_bucket_by_writer_padded(self._h, outs["records"].data_ptr(),
                                                      outs["n_records"].data_ptr(), outs["max_records"], n_dest, cap,
                                                      out_records.data_ptr(), dest_counts.data_ptr()))
+
+    # ---- DataFrag reassembly (state persists in the context across batches) ----
+    def alloc_frag_outputs(self, max_samples, heap_bytes):
+        import torch
+        dev = torch.device("cuda", self.device)
+        return {"samples": torch.empty((max(max_samples, 1), FRAG_SAMPLE_DTYPE.itemsize), dtype=torch.uint8,
+                                       device=dev),
+                "max_samples": max_samples,
+                "heap": torch.empty(max(heap_bytes, 1), dtype=torch.uint8, device=dev), "heap_bytes": heap_bytes,
+                "n_samples": torch.zeros(1, dtype=torch.int64, device=dev),
+                "heap_used": torch.zeros(1, dtype=torch.int64, device=dev),
+                "n_pending": torch.zeros(1, dtype=torch.int64, device=dev)}
+
+    def frag_assemble(self, arena, off, outs, fouts):
+        """Reassemble the DATA_FRAG records of a parsed batch (asynchronous)."""
+        o = fouts.get("_c")
+        if o is None:
+            o = _FragOut()
+            o.samples = fouts["samples"].data_ptr()
+            o.max_samples = fouts["max_samples"]
+            o.heap = fouts["heap"].data_ptr()
+            o.heap_bytes = fouts["heap_bytes"]
+            o.n_samples = fouts["n_samples"].data_ptr()
+            o.heap_used = fouts["heap_used"].data_ptr()
+            o.n_pending = fouts["n_pending"].data_ptr()
+            fouts["_c"] = o
+        _check(lib().rtps_rx_frag_assemble(self._h, arena.data_ptr(), arena.numel(), off.data_ptr(),
+                                           outs["records"].data_ptr(), outs["n_records"].data_ptr(),
+                                           outs["max_records"], ctypes.byref(o)))
+
+    def frag_reset(self):
+        _check(lib().rtps_rx_frag_reset(self._h))
+
+    def assemble_batch(self, arena_np, off_np, len_np, max_samples=None, heap_bytes=None):
+        """Parse + reassemble host arrays -> (BatchResult, samples FRAG_SAMPLE_DTYPE, heap u8, n_samples,
+        heap_used, n_pending)."""
+        import torch
+        n = len(len_np)
+        dev = torch.device("cuda", self.device)
+        arena = torch.from_numpy(np.ascontiguousarray(arena_np, dtype=np.uint8)).to(dev)
+        off = torch.from_numpy(np.ascontiguousarray(off_np, dtype=np.uint64).view(np.int64)).to(dev)
+        lens = torch.from_numpy(np.ascontiguousarray(len_np, dtype=np.uint32).view(np.int32)).to(dev)
+        cap = max_records(len_np)
+        outs = self.alloc_outputs(n, cap)
+        ms = cap if max_samples is None else max_samples
+        hb = (int(arena.numel()) + 16 * cap + (1 << 22)) if heap_bytes is None else heap_bytes
+        fouts = self.alloc_frag_outputs(ms, hb)
+        torch.cuda.synchronize(dev)
+        self.parse_batch_device(arena, off, lens, n, outs)
+        self.frag_assemble(arena, off, outs, fouts)
+        self.sync()
+        total = int(outs["n_records"].item())
+        kept = min(total, cap)
+        recs = outs["records"][:kept].cpu().numpy().reshape(-1).view(RECORD_DTYPE)
+        match = outs["match"][:kept].cpu().numpy().view(np.uint16)
+        res = BatchResult(outs["status"][:n].cpu().numpy(), recs, match,
+                          outs["rec_begin"][:n].cpu().numpy().view(np.uint32), total)
+        ns = int(fouts["n_samples"].item())
+        used = int(fouts["heap_used"].item())
+        samples = fouts["samples"][:min(ns, ms)].cpu().numpy().reshape(-1).view(FRAG_SAMPLE_DTYPE)
+        heap = fouts["heap"][:min(used, hb)].cpu().numpy()
+        return res, samples, heap, ns, used, int(fouts["n_pending"].item())
 
     # ---- convenience: host datagrams in, host results out ----
     def handle_received_batch(self, arena_np, off_np, len_np):

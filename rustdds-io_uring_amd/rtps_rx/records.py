@@ -58,6 +58,13 @@ UNION_BY_KIND = {DATA: U_DATA, DATA_FRAG: U_FRAG, HEARTBEAT: U_HB, HEARTBEAT_FRA
                  ACKNACK: U_ACKNACK, NACK_FRAG: U_NACKFRAG, INFO_SRC: U_INFOSRC, INFO_REPLY: U_INFOREPLY}
 
 MATCH_DTYPE = np.dtype([("writer_guid", "u1", (16,)), ("reader_slot", "<u2"), ("_pad", "<u2")])
+
+# DataFrag reassembly output (rtps_frag_sample, include/rtps_rx.h)
+FRAG_OK, FRAG_SHORT, FRAG_NO_ROOM = 0, 1, 2
+FRAG_SAMPLE_DTYPE = np.dtype([("writer_guid", "u1", (16,)), ("sn", "<i8"), ("heap_off", "<u8"),
+                              ("data_size", "<u4"), ("rec_idx", "<u4"), ("flags", "u1"), ("status", "u1"),
+                              ("_r", "<u2"), ("_r2", "<u4")])
+assert FRAG_SAMPLE_DTYPE.itemsize == 48
 assert MATCH_DTYPE.itemsize == 20
 
 

@@ -23,7 +23,7 @@ for wl in C2 C3 C4; do
 done
 echo "== rocprof"
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run \
-  --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline \
+  --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-e2e \
   > "$GRAFT_REPO_ROOT/gpurun_out/rocprof.log" 2>&1; rc=$?
 tail -5 "$GRAFT_REPO_ROOT/gpurun_out/rocprof.log"; ok_or_stop $rc rocprof
 find "$GRAFT_REPO_ROOT/gpurun_out/prof" -name "*stats*" | head

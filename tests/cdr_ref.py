@@ -233,7 +233,7 @@ BAD_UTF8 = [b"\xc0\x80", b"\xed\xa0\x80", b"\x80", b"\xf0\x80\x80\x80", b"\xf4\x
 HB = bytes.fromhex("07010000" "00000000" "00000102" "0000000001000000" "0000000005000000" "01000000")
 
 
-def corpus(t, n, seed, prefix=bytes(range(1, 13))):
+def corpus(t, n, seed, prefix=bytes(range(1, 13)), le_only=False, clean=False):
     """n datagrams carrying t-typed payloads: clean LE/BE samples plus every error class
     (truncation, byte corruption, bad UTF-8, over-long strings/sequences, bad bool,
     unsupported rep ids, KEY payloads and non-DATA submessages)."""
@@ -241,9 +241,9 @@ def corpus(t, n, seed, prefix=bytes(range(1, 13))):
     has = {k for _, k, _ in t._layout}
     out = []
     for i in range(n):
-        le = bool(rng.integers(0, 2))
+        le = True if le_only else bool(rng.integers(0, 2))
         vals = random_values(t, rng)
-        mode = int(rng.integers(0, 12))
+        mode = 0 if clean else int(rng.integers(0, 12))
         rep = None
         flags = 0x04
         if mode == 4 and cdr.OP_STRING in has:    # invalid UTF-8 inside a string
@@ -275,7 +275,9 @@ def corpus(t, n, seed, prefix=bytes(range(1, 13))):
                 b[int(rng.integers(0, len(b)))] = int(rng.integers(0, 256))
             body = bytes(b)
         rep = rep if rep is not None else (REP_CDR_LE if le else REP_CDR_BE)
-        if mode == 10 and le:
+        if mode in (1, 10) and le and le_only:
+            rep = REP_PL_CDR_LE if mode == 10 else rep
+        elif mode == 10 and le:
             rep = REP_PL_CDR_LE                   # accepted, little-endian
         pad = (-len(body)) % 4
         pl = rep + bytes([0, pad]) + body + bytes(pad)
@@ -291,3 +293,9 @@ MIXED = cdr.CdrType([("id", "u8"), ("temp", "f64"), ("flag", "bool"), ("name", c
                      ("hist", cdr.Seq("u16", 6)), ("big", cdr.Seq("i64", 3)), ("pos", cdr.Array("f32", 3)),
                      ("c", "i8"), ("t", "i16"), ("ok", "bool"), ("inner", cdr.ShapeType),
                      ("tail", cdr.Array("u64", 2))])
+
+
+# Leading run of 4/8-byte fields contiguous on the wire and in the row: decoded
+# little-endian chunks copy it as one block (a "segment"), others field by field
+SEGS = cdr.CdrType([("a", "u64"), ("b", "f64"), ("c", cdr.Array("i32", 5)), ("d", "u32"), ("s", cdr.String(8)),
+                    ("e", "u64"), ("f", cdr.Array("u16", 3))])

@@ -56,6 +56,18 @@ def test_corpus_parity(rx, name):
         assert np.bincount(status, minlength=7)[[0, 1, 2, 3]].all()
 
 
+@pytest.mark.parametrize("name,clean", [("segs", True), ("segs", False), ("mixed", True), ("shape", True)])
+def test_little_endian_chunks(rx, name, clean):
+    """All-little-endian batches take the block-copy path for segments (and clean ones the
+    all-OK path); mixed-status LE batches mix it with the per-slot path."""
+    t = TYPES[name]
+    dgrams = cdr_ref.corpus(t, 5000, seed=7, le_only=True, clean=clean)
+    arena, off, ln = oracle.pack(dgrams, align=1)
+    _, status = _check(rx, t, arena, off, ln, f"{name}-le{'-clean' if clean else ''}")
+    if clean:
+        assert (status[status != cdr.CDR_NOT_DATA] == cdr.CDR_OK).all()
+
+
 def test_bad_program_rejected(rx):
     import rtps_rx
     dev = torch.device("cuda", 0)

@@ -19,6 +19,7 @@ TYPES = {
     "seqs": cdr.CdrType([("s", cdr.Seq("f64", 4)), ("t", cdr.Seq("u8", 9)), ("n", cdr.String(3)),
                          ("v", cdr.Seq("i32", 0))]),
     "empty": cdr.CdrType([]),
+    "segs": cdr_ref.SEGS,
 }
 
 

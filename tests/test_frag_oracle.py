@@ -1,0 +1,113 @@
+"""CPU checks of the DataFrag reassembly oracle:
+against an independent Python model of the reference's FragmentAssembler on
+an anomaly-rich corpus (single batch and split into batches), and on the C4
+workload against the generator's own fragment layout (size-independent:
+every 64 KiB sample is the concatenation of its 49 fragments)."""
+import struct
+
+import numpy as np
+import pytest
+
+import frag_ref
+import oracle
+from rtps_rx.records import DATA_FRAG, FRAG_OK, FRAG_SHORT, FRAG_NO_ROOM
+
+
+def _parse(dgrams):
+    arena, off, ln = oracle.pack(dgrams)
+    st, recs, _, _ = oracle.parse(arena, off, ln)
+    return arena, off, recs, st
+
+
+def _check_against_model(samples, heap, model_out, label):
+    assert len(samples) == len(model_out), f"{label}: {len(samples)} samples vs model {len(model_out)}"
+    for s, (guid, sn, data, ri, flags) in zip(samples, model_out):
+        assert bytes(s["writer_guid"]) == guid and int(s["sn"]) == sn, label
+        assert int(s["rec_idx"]) == ri and int(s["flags"]) == flags, label
+        assert int(s["data_size"]) == len(data), label
+        assert int(s["status"]) == (FRAG_SHORT if len(data) < 4 else FRAG_OK), label
+        o = int(s["heap_off"])
+        assert heap[o:o + len(data)].tobytes() == data, f"{label}: bytes of sn {sn} differ"
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_oracle_matches_model_single_batch(seed):
+    arena, off, recs, st = _parse(frag_ref.soup(1500, seed))
+    assert (st == 0).all()
+    f = oracle.FragAssembler()
+    samples, heap, n, used = f.batch(arena, off, recs)
+    model = frag_ref.FragRef()
+    exp = model.batch(arena, off, recs)
+    _check_against_model(samples, heap, exp, f"seed {seed}")
+    assert f.pending() == model.pending()
+    assert n > 50
+
+
+def test_soup_covers_the_anomalies():
+    short = key = irregular = 0
+    for seed in (1, 2, 3):
+        arena, off, recs, st = _parse(frag_ref.soup(1500, seed))
+        exp = frag_ref.FragRef().batch(arena, off, recs)
+        short += sum(len(e[2]) < 4 for e in exp)
+        key += sum(bool(e[4] & 0x04) for e in exp)
+        u = recs["u"].view(np.uint8).reshape(-1, 16)
+        irregular += int((u[:, 8:10].copy().view("<u2")[:, 0] > 1).sum())  # several fragments per submessage
+    assert short and key and irregular
+
+
+@pytest.mark.parametrize("cuts", [[700], [1, 2, 3, 500, 1000], list(range(100, 1500, 100))])
+def test_oracle_state_across_batches(cuts):
+    dgrams = frag_ref.soup(1500, 9)
+    f = oracle.FragAssembler()
+    model = frag_ref.FragRef()
+    bounds = [0] + cuts + [len(dgrams)]
+    total = 0
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        arena, off, recs, st = _parse(dgrams[a:b])
+        samples, heap, n, used = f.batch(arena, off, recs)
+        _check_against_model(samples, heap, model.batch(arena, off, recs), f"batch {a}:{b}")
+        assert f.pending() == model.pending()
+        total += n
+    assert total > 50
+
+
+def test_capacity_limits():
+    arena, off, recs, st = _parse(frag_ref.soup(800, 4))
+    full, fheap, n, used = oracle.FragAssembler().batch(arena, off, recs)
+    # max_samples truncation: the count still reports every completed sample
+    s2, _, n2, used2 = oracle.FragAssembler().batch(arena, off, recs, max_samples=10)
+    assert n2 == n and len(s2) == 10 and used2 == used
+    assert s2.tobytes() == full[:10].tobytes()
+    # heap too small: descriptors kept, later samples NO_ROOM
+    cap = int(full["heap_off"][n // 2])
+    s3, h3, n3, used3 = oracle.FragAssembler().batch(arena, off, recs, heap_bytes=cap)
+    assert n3 == n and used3 == used
+    ok = full["heap_off"] + full["data_size"] <= cap
+    assert (s3["status"][~ok] == FRAG_NO_ROOM).all() and (s3["status"][ok] == full["status"][ok]).all()
+
+
+def test_c4_samples_are_their_fragments():
+    n = 20000
+    arena, off, ln = oracle.gen(oracle.WL_C4, n)
+    st, recs, _, _ = oracle.parse(arena, off, ln)
+    f = oracle.FragAssembler()
+    samples, heap, ns, used = f.batch(arena, off, recs)
+    assert ns >= n // 49 - 16 and (samples["status"] == FRAG_OK).all()
+    assert (samples["data_size"] == 65536).all()
+    u = recs["u"].view(np.uint8).reshape(-1, 16)
+    pl_off = u[:, 0:2].copy().view("<u2")[:, 0]
+    pl_len = u[:, 2:4].copy().view("<u2")[:, 0]
+    fstart = u[:, 4:8].copy().view("<u4")[:, 0]
+    guid = np.concatenate([recs["prefix"], recs["writer_id"]], axis=1)
+    key = {}
+    for i in range(len(recs)):
+        key.setdefault((guid[i].tobytes(), int(recs["sn"][i])), []).append(i)
+    for s in samples[::7]:
+        idx = sorted(key[(s["writer_guid"].tobytes(), int(s["sn"]))], key=lambda i: fstart[i])
+        assert [int(fstart[i]) for i in idx] == list(range(1, 50))
+        data = b"".join(arena[int(off[recs["dgram_idx"][i]]) + int(pl_off[i]):
+                              int(off[recs["dgram_idx"][i]]) + int(pl_off[i]) + int(pl_len[i])].tobytes()
+                        for i in idx)
+        o = int(s["heap_off"])
+        assert heap[o:o + 65536].tobytes() == data
+        assert int(s["rec_idx"]) == max(idx)  # the last fragment to arrive completes it
