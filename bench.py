@@ -161,6 +161,37 @@ def cdr_decode_leg(rx, workload, arena, off_t, outs, n_rec, stream, steps):
             "achieved_gbs": alg / (ms * 1e-3) / 1e9, "frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
 
+def frag_leg(rx, arena, off_t, outs, n_rec, recs, stream, steps):
+    """DataFrag reassembly of this batch's DATA_FRAG records (§8f rank 1), timed
+    separately (HIP events on the launch stream).  Each step re-assembles the same
+    batch from a reset state, so every step does the same work."""
+    u = recs["u"].view(np.uint8).reshape(-1, 16)
+    frag = recs["kind"] == DATA_FRAG
+    payload = int(u[frag][:, 2:4].copy().view("<u2").astype(np.int64).sum())
+    heap_bytes = int(arena.numel()) + 16 * n_rec + (1 << 24)
+    fouts = rx.alloc_frag_outputs(n_rec, heap_bytes)
+    for _ in range(2):
+        rx.frag_reset()
+        rx.frag_assemble(arena, off_t, outs, fouts)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    torch.cuda.synchronize()
+    for a, b in ev:
+        rx.frag_reset()
+        a.record(stream)
+        rx.frag_assemble(arena, off_t, outs, fouts)
+        b.record(stream)
+    torch.cuda.synchronize()
+    ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    ns = int(fouts["n_samples"].item())
+    # algorithmic bytes: each fragment's payload read once and written once + its 64-B record read
+    alg = 2 * payload + 64 * int(frag.sum())
+    return {"kernel": "rtps_frag_assemble (sort + walk + place + copy launches)", "ms": ms,
+            "samples": ns, "pending": int(fouts["n_pending"].item()), "fragments": int(frag.sum()),
+            "samples_per_s": ns / (ms * 1e-3), "gib_per_s_assembled": int(fouts["heap_used"].item()) / (ms * 1e-3) / 2**30,
+            "alg_bytes_per_launch": alg, "achieved_gbs": alg / (ms * 1e-3) / 1e9,
+            "frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+
+
 def cpu_baseline(workload, n, target_cpu_s=10.0):
     """The oracle (C restatement of the reference parse) on this host's cores."""
     import oracle
@@ -194,6 +225,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-cdr", action="store_true", help="skip the CDR decode (a18) measurement")
+    ap.add_argument("--no-frag", action="store_true", help="skip the DataFrag reassembly measurement (C4)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N>1 (gloo only to rehearse several ranks on one GPU)")
     args = ap.parse_args()
@@ -341,6 +373,8 @@ def main():
                                         "overflow": any(e.overflowed() for e in exch)}
     if world == 1 and not args.no_cdr:
         result["cdr_decode"] = cdr_decode_leg(rx, args.workload, arena, off_t, outs, n_rec, stream, args.steps)
+    if world == 1 and not args.no_frag and args.workload == "C4":
+        result["frag_assemble"] = frag_leg(rx, arena, off_t, outs, n_rec, recs, stream, args.steps)
     if world == 1 and not args.no_e2e:
         result["end_to_end"] = end_to_end(rx, arena, off_t, ln_t, n, outs, n_rec, stream)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

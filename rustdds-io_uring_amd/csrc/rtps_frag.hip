@@ -52,7 +52,7 @@ constexpr uint64_t PBYTES = 1ull << 28;  // pending byte store (per side)
 constexpr uint64_t PWORDS = 1ull << 22;  // pending bitmap words (per side)
 
 // counters (device u64)
-enum { C_OLD_N = 0, C_NEW_N, C_NEW_BYTES, C_NEW_WORDS, C_EPOCHS, C_POOL, C_OVERFLOW, C_COUNT };
+enum { C_OLD_N = 0, C_NEW_N, C_NEW_BYTES, C_NEW_WORDS, C_SPECIAL, C_POOL, C_OVERFLOW, C_COUNT };
 
 enum EpochState : uint32_t { E_PENDING = 0, E_DONE = 1, E_DEAD = 2 };  // DEAD: bitmap allocation failed
 enum EpochFlags : uint32_t { EF_IRREGULAR = 1, EF_SKIP = 2 };  // SKIP: no bytes to write (no room)
@@ -116,7 +116,8 @@ __device__ __forceinline__ uint32_t wslot_find(const uint64_t* wkey, uint64_t h)
 
 // ---- 1: sort keys ----
 __global__ __launch_bounds__(FT) void k_keys(const rtps_record* recs, const uint64_t* n_rec, uint64_t max,
-                                             uint32_t* keys, uint32_t* vals) {
+                                             uint32_t* keys, uint32_t* vals, uint32_t* pos_epoch, uint32_t* dmark,
+                                             uint8_t* seen) {
   const uint64_t n = min(*n_rec, max);
   for (uint64_t i = (uint64_t)blockIdx.x * FT + threadIdx.x; i < max; i += (uint64_t)gridDim.x * FT) {
     uint32_t k = SENT;
@@ -127,6 +128,9 @@ __global__ __launch_bounds__(FT) void k_keys(const rtps_record* recs, const uint
     }
     keys[i] = k;
     vals[i] = (uint32_t)i;
+    pos_epoch[i] = NONE;  // per-batch state, reset here instead of three memsets
+    dmark[i] = NONE;
+    seen[i] = 0;
   }
 }
 
@@ -187,8 +191,8 @@ struct WalkArgs {
   Pend* old_pend;
   const uint32_t* old_ptable;
   const uint32_t* old_bits;
-  Epoch* epochs;
-  uint64_t max_epochs;
+  Epoch* epochs;    // indexed by the sorted position of the epoch's first record
+  uint32_t* special; // epochs needing more than their records' spans: continued, pending or irregular
   uint32_t* pool;
   uint64_t pool_words;
   uint32_t* pos_epoch;
@@ -197,14 +201,23 @@ struct WalkArgs {
   uint64_t* ctr;
 };
 
-__device__ uint32_t new_epoch(const WalkArgs& A, const uint32_t g[4], int64_t sn, uint32_t p0, uint32_t p1) {
-  const uint64_t e = atomicAdd((unsigned long long*)&A.ctr[C_EPOCHS], 1ull);
-  if (e >= A.max_epochs) { atomicOr((unsigned long long*)&A.ctr[C_OVERFLOW], 2ull); return NONE; }
+// Epoch ids are the sorted position where the epoch starts (its first record,
+// or the run's first position for a buffer carried over): distinct, no counter.
+__device__ uint32_t new_epoch(const WalkArgs& A, const uint32_t g[4], int64_t sn, uint32_t start, uint32_t p0,
+                              uint32_t p1) {
+  const uint32_t e = start;
   Epoch& E = A.epochs[e];
   for (int k = 0; k < 4; ++k) E.guid[k] = g[k];
   E.sn = sn; E.state = E_PENDING; E.eflags = 0; E.done_rec = NONE; E.old_pend = NONE; E.new_pend = NONE;
   E.p0 = p0; E.p1 = p1; E.nset = 0; E.rec_flags = 0; E.dst = 0; E.bits = 0;
-  return (uint32_t)e;
+  return e;
+}
+// after an epoch's last record: list it if the copy phase needs more than spans
+__device__ void epoch_done(const WalkArgs& A, uint32_t e) {
+  const Epoch& E = A.epochs[e];
+  if (E.state == E_DEAD) return;
+  if (E.old_pend != NONE || E.state == E_PENDING || (E.eflags & EF_IRREGULAR))
+    A.special[atomicAdd((unsigned long long*)&A.ctr[C_SPECIAL], 1ull)] = e;
 }
 __device__ bool alloc_bits(const WalkArgs& A, Epoch& E) {
   const uint64_t words = ((uint64_t)E.count + 31) / 32;
@@ -219,83 +232,235 @@ __device__ bool alloc_bits(const WalkArgs& A, Epoch& E) {
   return true;
 }
 
-__global__ __launch_bounds__(FT) void k_walk(WalkArgs A) {
-  for (uint64_t p = (uint64_t)blockIdx.x * FT + threadIdx.x; p < A.max; p += (uint64_t)gridDim.x * FT) {
-    const uint32_t key = A.skeys[p];
-    if (key == SENT || (p > 0 && A.skeys[p - 1] == key)) continue;  // not a run head
-    uint64_t p1 = p + 1;
-    while (p1 < A.max && A.skeys[p1] == key) ++p1;
-    // one pass per distinct full key of the run (more than one only on a hash collision)
-    for (uint64_t q0 = p; q0 < p1; ++q0) {
-      if (A.seen[q0]) continue;
-      uint32_t g[4];
-      const rtps_record* r0 = A.recs + A.svals[q0];
-      guid_of(r0, g);
-      const int64_t sn = r0->sn;
-      const uint64_t wh = writer_hash(g);
-      const uint32_t ws = wslot_find(A.wkey, wh);
-      const uint32_t F = ws == NONE ? 0u : (A.wF[ws] & 0xffffu);
-      // continue the buffer carried over from the previous batch
-      uint32_t e = NONE;
-      bool started = false;
-      const uint32_t j = pend_lookup(A.old_ptable, A.old_pend, key, g, sn);
-      if (j != NONE) {
-        e = new_epoch(A, g, sn, (uint32_t)p, (uint32_t)p1);
-        if (e != NONE) {
-          Epoch& E = A.epochs[e];
-          const Pend& P = A.old_pend[j];
-          A.old_pend[j].consumed = 1;
-          E.data_size = P.data_size; E.count = P.count; E.nset = P.nset; E.F = F; E.old_pend = j;
-          if (alloc_bits(A, E)) {
-            const uint64_t words = ((uint64_t)E.count + 31) / 32;
-            for (uint64_t w = 0; w < words; ++w) A.pool[E.bits + w] = A.old_bits[P.bits + w];
-            started = true;
-          }
-        }
-      }
-      for (uint64_t q = q0; q < p1; ++q) {
-        if (A.seen[q]) continue;
-        const uint32_t ri = A.svals[q];
-        const rtps_record* r = A.recs + ri;
-        uint32_t h[4];
-        guid_of(r, h);
-        if (!same_key(g, sn, h, r->sn)) continue;
-        A.seen[q] = 1;
-        const uint32_t ds = r->u.frag.data_size, fsz = r->u.frag.frag_size;
-        if (!started) {  // AssemblyBuffer::new (fragment_assembler.rs:35-63)
-          e = new_epoch(A, g, sn, (uint32_t)p, (uint32_t)p1);
-          if (e == NONE) { A.pos_epoch[q] = NONE; continue; }
-          Epoch& E = A.epochs[e];
-          E.data_size = ds;
-          E.count = ds / fsz + (ds % fsz > 0);
-          E.F = F;
-          if (!alloc_bits(A, E)) { A.pos_epoch[q] = NONE; continue; }
-          for (uint64_t w = 0; w < ((uint64_t)E.count + 31) / 32; ++w) A.pool[E.bits + w] = 0u;
-          if (F != fsz) E.eflags |= EF_IRREGULAR;  // spans do not tile the buffer
+// Sequential replay of one key run [p, p1) by one thread: the general case
+// (hash collisions mixing several keys in one run, bitmaps larger than LDS).
+__device__ void walk_run_serial(const WalkArgs& A, uint64_t p, uint64_t p1) {
+  const uint32_t key = A.skeys[p];
+  // one pass per distinct full key of the run (more than one only on a hash collision)
+  for (uint64_t q0 = p; q0 < p1; ++q0) {
+    if (A.seen[q0]) continue;
+    uint32_t g[4];
+    const rtps_record* r0 = A.recs + A.svals[q0];
+    guid_of(r0, g);
+    const int64_t sn = r0->sn;
+    const uint64_t wh = writer_hash(g);
+    const uint32_t ws = wslot_find(A.wkey, wh);
+    const uint32_t F = ws == NONE ? 0u : (A.wF[ws] & 0xffffu);
+    // continue the buffer carried over from the previous batch
+    uint32_t e = NONE;
+    bool started = false;
+    const uint32_t j = pend_lookup(A.old_ptable, A.old_pend, key, g, sn);
+    if (j != NONE) {
+      e = new_epoch(A, g, sn, (uint32_t)q0, (uint32_t)p, (uint32_t)p1);
+      if (e != NONE) {
+        Epoch& E = A.epochs[e];
+        const Pend& P = A.old_pend[j];
+        A.old_pend[j].consumed = 1;
+        E.data_size = P.data_size; E.count = P.count; E.nset = P.nset; E.F = F; E.old_pend = j;
+        if (alloc_bits(A, E)) {
+          const uint64_t words = ((uint64_t)E.count + 31) / 32;
+          for (uint64_t w = 0; w < words; ++w) A.pool[E.bits + w] = A.old_bits[P.bits + w];
           started = true;
         }
+      }
+    }
+    for (uint64_t q = q0; q < p1; ++q) {
+      if (A.seen[q]) continue;
+      const uint32_t ri = A.svals[q];
+      const rtps_record* r = A.recs + ri;
+      uint32_t h[4];
+      guid_of(r, h);
+      if (!same_key(g, sn, h, r->sn)) continue;
+      A.seen[q] = 1;
+      const uint32_t ds = r->u.frag.data_size, fsz = r->u.frag.frag_size;
+      if (!started) {  // AssemblyBuffer::new (fragment_assembler.rs:35-63)
+        e = new_epoch(A, g, sn, (uint32_t)q, (uint32_t)p, (uint32_t)p1);
         Epoch& E = A.epochs[e];
-        A.pos_epoch[q] = e;
-        // insert_frags (:65-140): byte range and fragment bits
-        const uint64_t start0 = (uint64_t)r->u.frag.frag_start - 1, fis = r->u.frag.frags_in_sub;
-        const uint64_t from = start0 * E.F;
-        if (from > E.data_size) E.eflags |= EF_IRREGULAR;  // reference panics; clamped
-        for (uint64_t k = 0; k < fis; ++k) {
-          const uint64_t bit = start0 + k;
-          if (bit >= E.count) { E.eflags |= EF_IRREGULAR; break; }  // reference panics; ignored
-          uint32_t& word = A.pool[E.bits + bit / 32];
-          const uint32_t m = 1u << (bit & 31);
-          if (word & m) E.eflags |= EF_IRREGULAR;  // repeated fragment: copy order matters
-          else { word |= m; E.nset++; }
-        }
-        if (E.nset == E.count) {  // is_complete -> emit, drop the buffer
-          E.state = E_DONE;
-          E.done_rec = ri;
-          E.rec_flags = r->flags;
-          A.dmark[ri] = e;
-          started = false;
+        E.data_size = ds;
+        E.count = ds / fsz + (ds % fsz > 0);
+        E.F = F;
+        if (!alloc_bits(A, E)) { A.pos_epoch[q] = NONE; continue; }
+        for (uint64_t w = 0; w < ((uint64_t)E.count + 31) / 32; ++w) A.pool[E.bits + w] = 0u;
+        if (F != fsz) E.eflags |= EF_IRREGULAR;  // spans do not tile the buffer
+        started = true;
+      }
+      Epoch& E = A.epochs[e];
+      A.pos_epoch[q] = e;
+      // insert_frags (:65-140): byte range and fragment bits
+      const uint64_t start0 = (uint64_t)r->u.frag.frag_start - 1, fis = r->u.frag.frags_in_sub;
+      const uint64_t from = start0 * E.F;
+      if (from > E.data_size) E.eflags |= EF_IRREGULAR;  // reference panics; clamped
+      for (uint64_t k = 0; k < fis; ++k) {
+        const uint64_t bit = start0 + k;
+        if (bit >= E.count) { E.eflags |= EF_IRREGULAR; break; }  // reference panics; ignored
+        uint32_t& word = A.pool[E.bits + bit / 32];
+        const uint32_t m = 1u << (bit & 31);
+        if (word & m) E.eflags |= EF_IRREGULAR;  // repeated fragment: copy order matters
+        else { word |= m; E.nset++; }
+      }
+      if (E.nset == E.count) {  // is_complete -> emit, drop the buffer
+        E.state = E_DONE;
+        E.done_rec = ri;
+        E.rec_flags = r->flags;
+        A.dmark[ri] = e;
+        started = false;
+        epoch_done(A, e);
+      }
+    }
+    if (started) epoch_done(A, e);  // still incomplete (bitmap already in the pool)
+  }
+}
+
+constexpr uint32_t BMW = 1024;  // LDS bitmap words per wave: buffers of up to 32768 fragments
+
+__device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); }
+
+// One key run replayed by a wave: each lane loads one record's fields, the
+// wave steps through them in order with the fragment bitmap in LDS.  Runs that
+// mix keys or need a bigger bitmap fall back to walk_run_serial on lane 0.
+__device__ void walk_run_wave(const WalkArgs& A, uint64_t p0, uint64_t p1, uint32_t lane, uint32_t* bm) {
+  const rtps_record* r0 = A.recs + A.svals[p0];
+  uint32_t g[4];
+  guid_of(r0, g);
+  const int64_t sn = r0->sn;
+  bool ok = true;
+  for (uint64_t c = p0; c < p1 && ok; c += 64) {
+    const uint64_t p = c + lane;
+    bool bad = false;
+    if (p < p1) {
+      const rtps_record* r = A.recs + A.svals[p];
+      uint32_t h[4];
+      guid_of(r, h);
+      const uint32_t ds = r->u.frag.data_size, fsz = r->u.frag.frag_size;
+      bad = !same_key(g, sn, h, r->sn) || (uint64_t)(ds / fsz + (ds % fsz > 0)) > (uint64_t)BMW * 32;
+    }
+    ok = !__any(bad);
+  }
+  const uint32_t key = A.skeys[p0];
+  const uint32_t j = pend_lookup(A.old_ptable, A.old_pend, key, g, sn);
+  if (ok && j != NONE && (uint64_t)A.old_pend[j].count > (uint64_t)BMW * 32) ok = false;
+  if (!ok) {
+    if (lane == 0) walk_run_serial(A, p0, p1);
+    return;
+  }
+  const uint32_t ws = wslot_find(A.wkey, writer_hash(g));
+  const uint32_t F = ws == NONE ? 0u : (A.wF[ws] & 0xffffu);
+  uint32_t e = NONE, nset = 0, count = 0, ds = 0, eflags = 0, old_pend = NONE;
+  bool started = false;
+  if (j != NONE) {  // continue the buffer carried over from the previous batch
+    uint32_t e0 = NONE;
+    if (lane == 0) {
+      e0 = new_epoch(A, g, sn, (uint32_t)p0, (uint32_t)p0, (uint32_t)p1);
+      A.old_pend[j].consumed = 1;
+    }
+    e = rl(e0, 0);
+    if (e != NONE) {
+      const Pend& P = A.old_pend[j];
+      ds = P.data_size; count = P.count; nset = P.nset; old_pend = j;
+      for (uint32_t w = lane; w < (count + 31) / 32; w += 64) bm[w] = A.old_bits[P.bits + w];
+      started = true;
+    }
+  }
+  auto finish = [&](uint32_t state, uint32_t done_rec, uint32_t rec_flags) {
+    if (lane == 0) {
+      Epoch& E = A.epochs[e];
+      E.data_size = ds; E.count = count; E.nset = nset; E.F = F; E.eflags = eflags; E.state = state;
+      E.done_rec = done_rec; E.rec_flags = rec_flags; E.old_pend = old_pend;
+      if (state == E_DONE) A.dmark[done_rec] = e;
+      epoch_done(A, e);
+    }
+  };
+  for (uint64_t c = p0; c < p1; c += 64) {
+    const uint64_t p = c + lane;
+    uint32_t ri = 0, fs = 0, fisz = 0, dsz = 0, fl = 0;
+    if (p < p1) {
+      ri = A.svals[p];
+      const rtps_record* r = A.recs + ri;
+      fs = r->u.frag.frag_start;
+      fisz = (uint32_t)r->u.frag.frags_in_sub | ((uint32_t)r->u.frag.frag_size << 16);
+      dsz = r->u.frag.data_size;
+      fl = r->flags;
+    }
+    uint32_t my_e = NONE;
+    const uint32_t m = (uint32_t)min<uint64_t>(64, p1 - c);
+    for (uint32_t jj = 0; jj < m; ++jj) {
+      const uint32_t rj = rl(ri, jj), fsj = rl(fs, jj), fz = rl(fisz, jj), dj = rl(dsz, jj);
+      const uint32_t fis = fz & 0xffffu, fsz = fz >> 16;
+      if (!started) {  // AssemblyBuffer::new (fragment_assembler.rs:35-63)
+        uint32_t e0 = NONE;
+        if (lane == 0) e0 = new_epoch(A, g, sn, (uint32_t)(c + jj), (uint32_t)p0, (uint32_t)p1);
+        e = rl(e0, 0);
+        ds = dj;
+        count = dj / fsz + (dj % fsz > 0);
+        nset = 0;
+        eflags = (F != fsz) ? EF_IRREGULAR : 0u;  // spans do not tile the buffer
+        old_pend = NONE;
+        for (uint32_t w = lane; w < (count + 31) / 32; w += 64) bm[w] = 0u;
+        started = true;
+      }
+      if (lane == jj) my_e = e;
+      // insert_frags (:65-140)
+      const uint64_t start0 = (uint64_t)fsj - 1;
+      if (start0 * F > ds) eflags |= EF_IRREGULAR;  // reference panics; clamped
+      for (uint32_t k = 0; k < fis; ++k) {
+        const uint64_t bit = start0 + k;
+        if (bit >= count) { eflags |= EF_IRREGULAR; break; }  // reference panics; ignored
+        const uint32_t w = bm[bit / 32], msk = 1u << (bit & 31);
+        if (w & msk) {
+          eflags |= EF_IRREGULAR;  // repeated fragment: copy order matters
+        } else {
+          if (lane == 0) bm[bit / 32] = w | msk;
+          nset++;
         }
       }
+      if (nset == count) {  // is_complete -> emit, drop the buffer
+        finish(E_DONE, rj, rl(fl, jj));
+        started = false;
+      }
+    }
+    if (p < p1) A.pos_epoch[p] = my_e;
+  }
+  if (started) {  // still incomplete: its bitmap goes to the pool for the pending store
+    uint64_t bits = 0;
+    bool got = true;
+    if (lane == 0) {
+      Epoch& E = A.epochs[e];
+      E.count = count;
+      got = alloc_bits(A, E);
+      bits = E.bits;
+    }
+    got = rl(got ? 1u : 0u, 0) != 0;
+    const uint64_t b = ((uint64_t)rl((uint32_t)(bits >> 32), 0) << 32) | rl((uint32_t)bits, 0);
+    if (got) {
+      for (uint32_t w = lane; w < (count + 31) / 32; w += 64) A.pool[b + w] = bm[w];
+      finish(E_PENDING, NONE, 0);
+    }
+  }
+}
+
+// a wave takes 64 sorted positions and walks every run that starts there
+__global__ __launch_bounds__(FT) void k_walk(WalkArgs A) {
+  __shared__ uint32_t bms[FT / 64][BMW];
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  for (uint64_t c = ((uint64_t)blockIdx.x * (FT / 64) + wave) * 64; c < A.max; c += (uint64_t)gridDim.x * FT) {
+    const uint64_t p = c + lane;
+    const uint32_t key = p < A.max ? A.skeys[p] : SENT;
+    const bool head = key != SENT && (p == 0 || A.skeys[p - 1] != key);
+    uint64_t heads = __ballot(head);
+    while (heads) {
+      const uint32_t h = (uint32_t)__builtin_ctzll(heads);
+      heads &= heads - 1;
+      const uint64_t p0 = c + h;
+      const uint32_t k0 = rl(key, h);
+      uint64_t p1 = p0 + 1;
+      for (;;) {  // run end: first position with another key
+        const uint64_t q = p1 + lane;
+        const bool other = q >= A.max || A.skeys[q] != k0;
+        const uint64_t b = __ballot(other);
+        if (b) { p1 += __builtin_ctzll(b); break; }
+        p1 += 64;
+      }
+      walk_run_wave(A, p0, p1, lane, bms[wave]);
     }
   }
 }
@@ -338,11 +503,11 @@ __global__ __launch_bounds__(FT) void k_samples(const uint32_t* dmark, Epoch* ep
 }
 
 // pending epochs: room in the new pending store + carry their bitmaps
-__global__ __launch_bounds__(FT) void k_pend_alloc(Epoch* ep, const uint64_t* ctr_ro, uint64_t max_epochs,
-                                                   Pend* np, uint32_t* nbits, const uint32_t* pool, uint64_t* ctr) {
-  const uint64_t ne = min(ctr_ro[C_EPOCHS], max_epochs);
-  for (uint64_t e = (uint64_t)blockIdx.x * FT + threadIdx.x; e < ne; e += (uint64_t)gridDim.x * FT) {
-    Epoch& E = ep[e];
+__global__ __launch_bounds__(FT) void k_pend_alloc(Epoch* ep, const uint32_t* special, Pend* np, uint32_t* nbits,
+                                                   const uint32_t* pool, uint64_t* ctr) {
+  const uint64_t ns = ctr[C_SPECIAL];
+  for (uint64_t i = (uint64_t)blockIdx.x * FT + threadIdx.x; i < ns; i += (uint64_t)gridDim.x * FT) {
+    Epoch& E = ep[special[i]];
     if (E.state != E_PENDING) continue;
     const uint64_t words = ((uint64_t)E.count + 31) / 32;
     const uint64_t j = atomicAdd((unsigned long long*)&ctr[C_NEW_N], 1ull);
@@ -395,12 +560,12 @@ __device__ __forceinline__ uint8_t* epoch_dst(const Epoch& E, const rtps_frag_ou
   return E.state == E_DONE ? out.heap + E.dst : nbytes + E.dst;
 }
 // regular epochs: carried-over bytes (or zeros for a new pending buffer) first
-__global__ __launch_bounds__(FT) void k_init(const Epoch* ep, const uint64_t* ctr, uint64_t max_epochs,
+__global__ __launch_bounds__(FT) void k_init(const Epoch* ep, const uint32_t* special, const uint64_t* ctr,
                                              const Pend* op, const uint8_t* obytes, uint8_t* nbytes,
                                              rtps_frag_out out) {
-  const uint64_t ne = min(ctr[C_EPOCHS], max_epochs);
-  for (uint64_t e = blockIdx.x; e < ne; e += gridDim.x) {
-    const Epoch& E = ep[e];
+  const uint64_t ns = ctr[C_SPECIAL];
+  for (uint64_t i = blockIdx.x; i < ns; i += gridDim.x) {
+    const Epoch& E = ep[special[i]];
     if (E.eflags & (EF_IRREGULAR | EF_SKIP)) continue;
     if (E.state == E_DONE && E.old_pend == NONE) continue;  // its spans cover every byte
     uint8_t* d = epoch_dst(E, out, nbytes);
@@ -416,34 +581,54 @@ __global__ __launch_bounds__(FT) void k_init(const Epoch* ep, const uint64_t* ct
 __device__ __forceinline__ uint4 ld16(const uint8_t* p) { uint4 v; __builtin_memcpy(&v, p, 16); return v; }
 __device__ __forceinline__ void st16(uint8_t* p, uint4 v) { __builtin_memcpy(p, &v, 16); }
 
-// regular epochs: every record writes its fragments' span, one wave per record
+// regular epochs: every record writes its fragments' span.  A wave takes 64
+// sorted positions: each lane resolves one record (epoch, source, destination,
+// lengths), then the wave copies the 64 spans one after the other, 16 B per
+// lane (spans of one sample are adjacent in the heap).
 __global__ __launch_bounds__(FT) void k_span(const rtps_record* recs, const uint8_t* arena, uint64_t arena_len,
                                              const uint64_t* dgram_off, const uint32_t* svals,
                                              const uint32_t* pos_epoch, const uint32_t* skeys, uint64_t max,
                                              const Epoch* ep, uint8_t* nbytes, rtps_frag_out out) {
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-  for (uint64_t p = (uint64_t)blockIdx.x * (FT / 64) + wave; p < max; p += (uint64_t)gridDim.x * (FT / 64)) {
-    if (skeys[p] == SENT) break;  // sorted: the rest are not assembled
-    const uint32_t e = pos_epoch[p];
-    if (e == NONE) continue;
-    const Epoch& E = ep[e];
-    if (E.eflags & (EF_IRREGULAR | EF_SKIP)) continue;
-    const rtps_record* r = recs + svals[p];
-    const uint64_t from = (uint64_t)(r->u.frag.frag_start - 1) * E.F;
-    const uint64_t span_end = min<uint64_t>(from + (uint64_t)r->u.frag.frags_in_sub * E.F, E.data_size);
-    const uint64_t to = min<uint64_t>(from + min<uint64_t>((uint64_t)r->u.frag.frags_in_sub * E.F, r->u.frag.pl_len),
-                                      E.data_size);
-    const uint8_t* src = arena + dgram_off[r->dgram_idx] + r->u.frag.pl_off;
-    uint8_t* d = epoch_dst(E, out, nbytes) + from;
-    const uint64_t n = span_end - from, nv = to - from;  // span bytes, payload bytes
-    const bool src16 = dgram_off[r->dgram_idx] + r->u.frag.pl_off + nv <= arena_len;  // always (parse output)
-    for (uint64_t b = 16u * lane; b < n; b += 1024u) {
-      if (b + 16 <= nv && src16) {
-        st16(d + b, ld16(src + b));
-      } else if (b + 16 <= n && b >= nv) {
-        st16(d + b, make_uint4(0, 0, 0, 0));
-      } else {
-        for (uint64_t t = b; t < b + 16 && t < n; ++t) d[t] = t < nv ? src[t] : (uint8_t)0;
+  for (uint64_t c = ((uint64_t)blockIdx.x * (FT / 64) + wave) * 64; c < max; c += (uint64_t)gridDim.x * FT) {
+    const uint64_t p = c + lane;
+    uint64_t src = 0, dst = 0;
+    uint32_t nv = 0, n = 0;
+    bool live = false;
+    if (p < max && skeys[p] != SENT) {
+      const uint32_t e = pos_epoch[p];
+      if (e != NONE) {
+        const Epoch& E = ep[e];
+        if (!(E.eflags & (EF_IRREGULAR | EF_SKIP)) && E.state != E_DEAD) {
+          const rtps_record* r = recs + svals[p];
+          const uint64_t from = (uint64_t)(r->u.frag.frag_start - 1) * E.F;
+          const uint64_t fisF = (uint64_t)r->u.frag.frags_in_sub * E.F;
+          const uint64_t span_end = min<uint64_t>(from + fisF, E.data_size);
+          const uint64_t to = min<uint64_t>(from + min<uint64_t>(fisF, r->u.frag.pl_len), E.data_size);
+          src = dgram_off[r->dgram_idx] + r->u.frag.pl_off;
+          dst = (uint64_t)(epoch_dst(E, out, nbytes) + from);
+          nv = (uint32_t)(to - from);
+          n = (uint32_t)(span_end - from);
+          live = n > 0;
+        }
+      }
+    }
+    uint64_t todo = __ballot(live);
+    while (todo) {
+      const uint32_t j = (uint32_t)__builtin_ctzll(todo);
+      todo &= todo - 1;
+      const uint64_t sj = ((uint64_t)rl((uint32_t)(src >> 32), j) << 32) | rl((uint32_t)src, j);
+      uint8_t* d = (uint8_t*)(((uint64_t)rl((uint32_t)(dst >> 32), j) << 32) | rl((uint32_t)dst, j));
+      const uint32_t nvj = rl(nv, j), nj = rl(n, j);
+      const uint8_t* sp = arena + sj;
+      for (uint32_t b = 16u * lane; b < nj; b += 1024u) {
+        if (b + 16 <= nvj) {
+          st16(d + b, ld16(sp + b));
+        } else if (b + 16 <= nj && b >= nvj) {
+          st16(d + b, make_uint4(0, 0, 0, 0));
+        } else {
+          for (uint32_t t = b; t < b + 16 && t < nj; ++t) d[t] = t < nvj ? sp[t] : (uint8_t)0;
+        }
       }
     }
   }
@@ -453,11 +638,12 @@ __global__ __launch_bounds__(FT) void k_span(const rtps_record* recs, const uint
 // record's clamped copy in record order), one workgroup each
 __global__ __launch_bounds__(FT) void k_serial(const rtps_record* recs, const uint8_t* arena,
                                                const uint64_t* dgram_off, const uint32_t* svals,
-                                               const uint32_t* pos_epoch, const Epoch* ep, const uint64_t* ctr,
-                                               uint64_t max_epochs, const Pend* op, const uint8_t* obytes,
+                                               const uint32_t* pos_epoch, const Epoch* ep, const uint32_t* special,
+                                               const uint64_t* ctr, const Pend* op, const uint8_t* obytes,
                                                uint8_t* nbytes, rtps_frag_out out) {
-  const uint64_t ne = min(ctr[C_EPOCHS], max_epochs);
-  for (uint64_t e = blockIdx.x; e < ne; e += gridDim.x) {
+  const uint64_t ns = ctr[C_SPECIAL];
+  for (uint64_t i = blockIdx.x; i < ns; i += gridDim.x) {
+    const uint32_t e = special[i];
     const Epoch& E = ep[e];
     if (!(E.eflags & EF_IRREGULAR) || (E.eflags & EF_SKIP)) continue;
     uint8_t* d = epoch_dst(E, out, nbytes);
@@ -518,11 +704,10 @@ struct FragState {
   // per-batch scratch (grown on demand)
   uint64_t cap = 0;
   uint32_t *keys = nullptr, *vals = nullptr, *skeys = nullptr, *svals = nullptr;
-  uint32_t *pos_epoch = nullptr, *dmark = nullptr, *cnt = nullptr, *rank = nullptr;
+  uint32_t *pos_epoch = nullptr, *dmark = nullptr, *cnt = nullptr, *rank = nullptr, *special = nullptr;
   uint8_t* seen = nullptr;
   uint64_t *dsz = nullptr, *hoff = nullptr;
   Epoch* epochs = nullptr;
-  uint64_t max_epochs = 0;
   uint32_t* pool = nullptr;
   uint64_t pool_words = 0;
   void* tmp = nullptr;
@@ -530,10 +715,10 @@ struct FragState {
 };
 
 static void free_scratch(FragState* s) {
-  void* ptrs[] = {s->keys, s->vals, s->skeys, s->svals, s->pos_epoch, s->dmark, s->cnt, s->rank,
+  void* ptrs[] = {s->keys, s->vals, s->skeys, s->svals, s->pos_epoch, s->dmark, s->cnt, s->rank, s->special,
                   s->seen, s->dsz, s->hoff, s->epochs, s->pool, s->tmp};
   for (void* p : ptrs) if (p) (void)hipFree(p);
-  s->keys = s->vals = s->skeys = s->svals = s->pos_epoch = s->dmark = s->cnt = s->rank = nullptr;
+  s->keys = s->vals = s->skeys = s->svals = s->pos_epoch = s->dmark = s->cnt = s->rank = s->special = nullptr;
   s->seen = nullptr; s->dsz = s->hoff = nullptr; s->epochs = nullptr; s->pool = nullptr; s->tmp = nullptr;
   s->cap = 0; s->tmp_bytes = 0;
 }
@@ -547,11 +732,11 @@ static bool grow(FragState* s, uint64_t max, hipStream_t st) {
             hipMalloc(&s->skeys, n * 4) == hipSuccess && hipMalloc(&s->svals, n * 4) == hipSuccess &&
             hipMalloc(&s->pos_epoch, n * 4) == hipSuccess && hipMalloc(&s->dmark, n * 4) == hipSuccess &&
             hipMalloc(&s->cnt, n * 4) == hipSuccess && hipMalloc(&s->rank, n * 4) == hipSuccess &&
+            hipMalloc(&s->special, n * 4) == hipSuccess &&
             hipMalloc(&s->seen, n) == hipSuccess && hipMalloc(&s->dsz, n * 8) == hipSuccess &&
             hipMalloc(&s->hoff, n * 8) == hipSuccess;
-  s->max_epochs = n + PCAP;
   s->pool_words = 4 * n + PWORDS;
-  ok = ok && hipMalloc(&s->epochs, s->max_epochs * sizeof(Epoch)) == hipSuccess &&
+  ok = ok && hipMalloc(&s->epochs, n * sizeof(Epoch)) == hipSuccess &&
        hipMalloc(&s->pool, s->pool_words * 4) == hipSuccess;
   size_t b1 = 0, b2 = 0, b3 = 0;
   ok = ok && hipcub::DeviceRadixSort::SortPairs(nullptr, b1, s->keys, s->skeys, s->vals, s->svals, (int)n, 0, 32, st) == hipSuccess;
@@ -610,16 +795,14 @@ int rtps_frag_assemble(FragState* s, hipStream_t st, const uint8_t* arena, uint6
   const int o = s->cur, nw = s->cur ^ 1;
   const uint32_t gb = (uint32_t)hmin((max + FT - 1) / FT, 8192);
   bool ok = hipMemsetAsync(s->ctr + C_NEW_N, 0, (C_COUNT - C_NEW_N) * 8, st) == hipSuccess &&
-            hipMemsetAsync(s->pos_epoch, 0xff, max * 4, st) == hipSuccess &&
-            hipMemsetAsync(s->dmark, 0xff, max * 4, st) == hipSuccess &&
-            hipMemsetAsync(s->seen, 0, max, st) == hipSuccess &&
             hipMemsetAsync(s->ptable[nw], 0xff, PTCAP * 4, st) == hipSuccess;
   if (!ok) return RTPS_RX_EHIP;
   if (max_records == 0) {
     (void)hipMemsetAsync(out->n_samples, 0, 8, st);
     (void)hipMemsetAsync(out->heap_used, 0, 8, st);
   }
-  hipLaunchKernelGGL(k_keys, dim3(gb), dim3(FT), 0, st, records, n_records, max, s->keys, s->vals);
+  hipLaunchKernelGGL(k_keys, dim3(gb), dim3(FT), 0, st, records, n_records, max, s->keys, s->vals, s->pos_epoch,
+                     s->dmark, s->seen);
   size_t tb = s->tmp_bytes;
   if (hipcub::DeviceRadixSort::SortPairs(s->tmp, tb, s->keys, s->skeys, s->vals, s->svals, (int)max, 0, 32, st) !=
       hipSuccess)
@@ -628,8 +811,8 @@ int rtps_frag_assemble(FragState* s, hipStream_t st, const uint8_t* arena, uint6
                      s->wF, s->ctr);
   hipLaunchKernelGGL(k_writers_fix, dim3(WCAP / FT), dim3(FT), 0, st, records, s->wkey, s->wfirst, s->wF);
   WalkArgs A{records, s->skeys, s->svals, max, s->wkey, s->wF, s->pend[o], s->ptable[o], s->pbits[o], s->epochs,
-             s->max_epochs, s->pool, s->pool_words, s->pos_epoch, s->dmark, s->seen, s->ctr};
-  hipLaunchKernelGGL(k_walk, dim3(gb), dim3(FT), 0, st, A);
+             s->special, s->pool, s->pool_words, s->pos_epoch, s->dmark, s->seen, s->ctr};
+  hipLaunchKernelGGL(k_walk, dim3((uint32_t)hmin((max + FT - 1) / FT, 8192)), dim3(FT), 0, st, A);
   hipLaunchKernelGGL(k_place_in, dim3(gb), dim3(FT), 0, st, s->dmark, s->epochs, max, s->cnt, s->dsz);
   tb = s->tmp_bytes;
   if (hipcub::DeviceScan::ExclusiveSum(s->tmp, tb, s->cnt, s->rank, (int)max, st) != hipSuccess) return RTPS_RX_EHIP;
@@ -637,17 +820,16 @@ int rtps_frag_assemble(FragState* s, hipStream_t st, const uint8_t* arena, uint6
   if (hipcub::DeviceScan::ExclusiveSum(s->tmp, tb, s->dsz, s->hoff, (int)max, st) != hipSuccess) return RTPS_RX_EHIP;
   hipLaunchKernelGGL(k_samples, dim3(gb), dim3(FT), 0, st, s->dmark, s->epochs, s->cnt, s->rank, s->dsz, s->hoff,
                      max, *out);
-  const uint32_t ge = (uint32_t)hmin((s->max_epochs + FT - 1) / FT, 8192);
-  hipLaunchKernelGGL(k_pend_alloc, dim3(ge), dim3(FT), 0, st, s->epochs, s->ctr, s->max_epochs, s->pend[nw],
-                     s->pbits[nw], s->pool, s->ctr);
+  hipLaunchKernelGGL(k_pend_alloc, dim3(64), dim3(FT), 0, st, s->epochs, s->special, s->pend[nw], s->pbits[nw],
+                     s->pool, s->ctr);
   hipLaunchKernelGGL(k_carry, dim3(1024), dim3(FT), 0, st, s->pend[o], s->pbytes[o], s->pbits[o], s->pend[nw],
                      s->pbytes[nw], s->pbits[nw], s->ctr);
-  hipLaunchKernelGGL(k_init, dim3(4096), dim3(FT), 0, st, s->epochs, s->ctr, s->max_epochs, s->pend[o], s->pbytes[o],
+  hipLaunchKernelGGL(k_init, dim3(1024), dim3(FT), 0, st, s->epochs, s->special, s->ctr, s->pend[o], s->pbytes[o],
                      s->pbytes[nw], *out);
-  hipLaunchKernelGGL(k_span, dim3((uint32_t)hmin((max + 3) / 4, 16384)), dim3(FT), 0, st, records, arena,
+  hipLaunchKernelGGL(k_span, dim3((uint32_t)hmin((max + FT - 1) / FT, 8192)), dim3(FT), 0, st, records, arena,
                      arena_len, dgram_off, s->svals, s->pos_epoch, s->skeys, max, s->epochs, s->pbytes[nw], *out);
   hipLaunchKernelGGL(k_serial, dim3(1024), dim3(FT), 0, st, records, arena, dgram_off, s->svals, s->pos_epoch,
-                     s->epochs, s->ctr, s->max_epochs, s->pend[o], s->pbytes[o], s->pbytes[nw], *out);
+                     s->epochs, s->special, s->ctr, s->pend[o], s->pbytes[o], s->pbytes[nw], *out);
   hipLaunchKernelGGL(k_ptable, dim3(PCAP / FT), dim3(FT), 0, st, s->pend[nw], s->ctr, s->ptable[nw]);
   hipLaunchKernelGGL(k_finish, dim3(1), dim3(1), 0, st, s->ctr, out->n_pending);
   if (hipGetLastError() != hipSuccess) return RTPS_RX_EHIP;
