@@ -29,7 +29,7 @@ import torch  # noqa: E402
 
 import rtps_rx  # noqa: E402
 from rtps_rx.records import (RECORD_DTYPE, DATA, DATA_FRAG, HEARTBEAT, HEARTBEAT_FRAG, GAP, ACKNACK,  # noqa: E402
-                             NACK_FRAG, INFO_TS, INFO_SRC, INFO_DST, INFO_REPLY, PK_DATA, PK_KEY)
+                             NACK_FRAG, INFO_TS, INFO_SRC, INFO_DST, INFO_REPLY, PK_DATA, PK_KEY, MATCH_DTYPE)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 OWN_PREFIX = bytes.fromhex("0103000c292d31a228200208")
@@ -192,17 +192,18 @@ def frag_leg(rx, arena, off_t, outs, n_rec, recs, stream, steps):
             "frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
 
-def cpu_baseline(workload, n, target_cpu_s=10.0):
-    """The oracle (C restatement of the reference parse) on this host's cores."""
+def cpu_baseline(workload, n, target_cpu_s=10.0, match_table=None):
+    """The oracle (C restatement of the reference parse) on this host's cores, with the
+    same match table as the device run."""
     import oracle
     threads = max(1, min(16, os.cpu_count() or 1))
     arena, off, ln = oracle.gen(rtps_rx.WORKLOADS[workload], n)
-    oracle.parse(arena, off, ln, threads=threads)  # warm
+    oracle.parse(arena, off, ln, threads=threads, match_table=match_table)  # warm
     t0 = time.perf_counter()
     c0 = time.process_time()
     reps = 0
     while True:
-        oracle.parse(arena, off, ln, threads=threads, want_match=True)
+        oracle.parse(arena, off, ln, threads=threads, want_match=True, match_table=match_table)
         reps += 1
         if time.process_time() - c0 >= target_cpu_s or time.perf_counter() - t0 > 60:
             break
@@ -226,6 +227,10 @@ def main():
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-cdr", action="store_true", help="skip the CDR decode (a18) measurement")
     ap.add_argument("--no-frag", action="store_true", help="skip the DataFrag reassembly measurement (C4)")
+    ap.add_argument("--match", default="writers", choices=["writers", "none"],
+                    help="match table: every writer of the workload (a reader subscribed to all of them) or none")
+    ap.add_argument("--exchange", default="descriptors", choices=["descriptors", "records"],
+                    help="N>1: what crosses xGMI (16-B descriptors of matched records, or 64-B records)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N>1 (gloo only to rehearse several ranks on one GPU)")
     args = ap.parse_args()
@@ -276,6 +281,21 @@ def main():
     n_rec = int(probe["n_records"].item())
     outs = rx.alloc_outputs(n, n_rec)
     del probe
+    n_matched_writers = 0
+    tbl = None
+    if args.match == "writers" or (world > 1 and args.exchange == "descriptors"):
+        # the reader is subscribed to every writer of the stream: match table = the writer
+        # GUIDs found in this batch, sorted (the same table, in the same order, on every rank)
+        rx.parse_batch_device(arena, off_t, ln_t, n, outs)
+        torch.cuda.synchronize(dev)
+        r = outs["records"][:n_rec].cpu().numpy().reshape(-1).view(RECORD_DTYPE)
+        wk = np.isin(r["kind"], [DATA, DATA_FRAG, HEARTBEAT, HEARTBEAT_FRAG, GAP])
+        g = np.concatenate([r["prefix"][wk], r["writer_id"][wk]], axis=1)
+        guids = np.unique(g.view(np.dtype((np.void, 16))).reshape(-1))
+        tbl = np.zeros(len(guids), dtype=MATCH_DTYPE)
+        tbl["writer_guid"] = np.frombuffer(guids.tobytes(), dtype=np.uint8).reshape(-1, 16)
+        rx.set_match_table(tbl)
+        n_matched_writers = len(guids)
     exch = None
     works = [[], []]
     bcap = 0
@@ -286,12 +306,14 @@ def main():
         # this batch over all ranks (the batch repeats every step, so it never overflows;
         # overflow is checked after the timed region).
         from rtps_rx.shard import Exchange
-        probe_ex = Exchange(rx, n_rec, world, dist, dev)
+        item = args.exchange
+        probe_ex = Exchange(rx, n_rec, world, dist, dev, cap=max(n_rec, 1) if item == "descriptors" else None,
+                            item=item)
         rx.parse_batch_device(arena, off_t, ln_t, n, outs)
         probe_ex.bucket(outs)
         bcap = max(int(allreduce_max(probe_ex.counts.max().reshape(1)).item()), 1)
         del probe_ex
-        exch = [Exchange(rx, n_rec, world, dist, dev, cap=bcap) for _ in range(2)]
+        exch = [Exchange(rx, n_rec, world, dist, dev, cap=bcap, item=item) for _ in range(2)]
         outs_pp = [outs, rx.alloc_outputs(n, n_rec)]
 
     def step(k):
@@ -352,7 +374,7 @@ def main():
         "data": "synthetic (deterministic generator f(seed=0x52545053, idx), generated in HBM)",
         "config": {"workload": f"{args.workload}: {WORKLOAD_DESC[args.workload]}",
                    "datagrams_per_gpu": n, "bytes_per_gpu": int(total_bytes), "records_per_gpu": n_rec,
-                   "ok_datagrams": int((status == 0).sum()),
+                   "ok_datagrams": int((status == 0).sum()), "matched_writers": n_matched_writers,
                    "parallelism": f"{world} ranks, datagram-sharded" + (
                        ", writer-GUID all-to-all (RCCL)" if world > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": alg_total / (ev_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
@@ -368,9 +390,13 @@ def main():
                                        "bucket, waiting for the exchange two steps back)")
         got, split = exch[(args.warmup + args.steps - 1) & 1].gather_received()
         result["config"]["received_records_rank0"] = int(got.shape[0])
-        result["config"]["exchange"] = {"mode": "padded equal-split all-to-all, pipelined with the next parse",
-                                        "bucket_capacity": bcap, "bytes_sent_per_rank_per_step": world * bcap * 64,
-                                        "overflow": any(e.overflowed() for e in exch)}
+        ib = 16 if args.exchange == "descriptors" else 64
+        result["config"]["exchange"] = {
+            "mode": "padded equal-split all-to-all, pipelined with the next parse",
+            "item": (f"{ib}-B rtps_xdesc of matched records, owner = match-table entry % world"
+                     if ib == 16 else "64-B records, owner = writer-GUID hash % world"),
+            "bucket_capacity": bcap, "bytes_sent_per_rank_per_step": world * bcap * ib,
+            "overflow": any(e.overflowed() for e in exch)}
     if world == 1 and not args.no_cdr:
         result["cdr_decode"] = cdr_decode_leg(rx, args.workload, arena, off_t, outs, n_rec, stream, args.steps)
     if world == 1 and not args.no_frag and args.workload == "C4":
@@ -378,7 +404,7 @@ def main():
     if world == 1 and not args.no_e2e:
         result["end_to_end"] = end_to_end(rx, arena, off_t, ln_t, n, outs, n_rec, stream)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args.workload, n, args.cpu_seconds)
+        result["cpu_baseline"] = cpu_baseline(args.workload, n, args.cpu_seconds, match_table=tbl)
     if rank == 0:
         print(json.dumps(result), flush=True)
     rx.close()

@@ -102,6 +102,22 @@ __device__ __forceinline__ uint64_t writer_hash(const uint32_t g[4]) {
 __device__ __forceinline__ bool same_key(const uint32_t a[4], int64_t asn, const uint32_t b[4], int64_t bsn) {
   return a[0] == b[0] && a[1] == b[1] && a[2] == b[2] && a[3] == b[3] && asn == bsn;
 }
+// workgroup-wide copy / zero fill of n bytes, 16 B per thread where possible
+__device__ __forceinline__ void blk_copy(uint8_t* d, const uint8_t* s, uint64_t n) {
+  uint64_t b = 16ull * threadIdx.x;
+  for (; b + 16 <= n; b += 16ull * FT) {
+    uint4 v;
+    __builtin_memcpy(&v, s + b, 16);
+    __builtin_memcpy(d + b, &v, 16);
+  }
+  for (uint64_t t = (n & ~15ull) + threadIdx.x; t < n; t += FT) d[t] = s[t];
+}
+__device__ __forceinline__ void blk_zero(uint8_t* d, uint64_t n) {
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  uint64_t b = 16ull * threadIdx.x;
+  for (; b + 16 <= n; b += 16ull * FT) __builtin_memcpy(d + b, &z, 16);
+  for (uint64_t t = (n & ~15ull) + threadIdx.x; t < n; t += FT) d[t] = 0;
+}
 __device__ __forceinline__ bool is_frag(const rtps_record* r) { return r->kind == RTPS_DATA_FRAG && (r->route & RTPS_ROUTE_PASS); }
 
 __device__ __forceinline__ uint32_t wslot_find(const uint64_t* wkey, uint64_t h) {
@@ -548,7 +564,7 @@ __global__ __launch_bounds__(FT) void k_carry(const Pend* op, const uint8_t* oby
     }
     __syncthreads();
     if (ok) {
-      for (uint64_t b = threadIdx.x; b < P.data_size; b += FT) nbytes[sb + b] = obytes[P.bytes + b];
+      blk_copy(nbytes + sb, obytes + P.bytes, P.data_size);
       for (uint64_t t = threadIdx.x; t < words; t += FT) nbits[sw + t] = obits[P.bits + t];
     }
     __syncthreads();
@@ -571,9 +587,9 @@ __global__ __launch_bounds__(FT) void k_init(const Epoch* ep, const uint32_t* sp
     uint8_t* d = epoch_dst(E, out, nbytes);
     if (E.old_pend != NONE) {
       const uint8_t* s = obytes + op[E.old_pend].bytes;
-      for (uint64_t b = threadIdx.x; b < E.data_size; b += FT) d[b] = s[b];
+      blk_copy(d, s, E.data_size);
     } else {
-      for (uint64_t b = threadIdx.x; b < E.data_size; b += FT) d[b] = 0;
+      blk_zero(d, E.data_size);
     }
   }
 }
@@ -649,9 +665,9 @@ __global__ __launch_bounds__(FT) void k_serial(const rtps_record* recs, const ui
     uint8_t* d = epoch_dst(E, out, nbytes);
     if (E.old_pend != NONE) {
       const uint8_t* s = obytes + op[E.old_pend].bytes;
-      for (uint64_t b = threadIdx.x; b < E.data_size; b += FT) d[b] = s[b];
+      blk_copy(d, s, E.data_size);
     } else {
-      for (uint64_t b = threadIdx.x; b < E.data_size; b += FT) d[b] = 0;
+      blk_zero(d, E.data_size);
     }
     __threadfence();
     __syncthreads();

@@ -771,14 +771,43 @@ __device__ __forceinline__ uint32_t owner_of(const rtps_record* r, uint32_t n_de
   return guid_hash(d[2], d[3], d[4], d[5]) % n_dest;
 }
 
+// descriptor mode: matched-writer records only, owner = match-table entry index % n_dest
+struct DescOwner {
+  const u32x4* keys;
+  const uint16_t* slots;
+  const uint32_t* index;
+  uint32_t mask;
+};
+__device__ __forceinline__ uint32_t desc_entry(const rtps_record* r, const DescOwner& m) {
+  if (!(r->route & RTPS_ROUTE_MATCHED)) return 0xffffffffu;
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(r);
+  uint32_t i = guid_hash(d[2], d[3], d[4], d[5]) & m.mask;
+  for (uint32_t probe = 0; probe <= m.mask; ++probe) {
+    if (m.slots[i] == RTPS_NO_MATCH) return 0xffffffffu;
+    const u32x4 k = m.keys[i];
+    if (k[0] == d[2] && k[1] == d[3] && k[2] == d[4] && k[3] == d[5]) return m.index[i];
+    i = (i + 1u) & m.mask;
+  }
+  return 0xffffffffu;
+}
+template <bool DESC>
+__device__ __forceinline__ uint32_t owner_sel(const rtps_record* r, uint32_t n_dest, const DescOwner& m) {
+  if (DESC) {
+    const uint32_t e = desc_entry(r, m);
+    return e == 0xffffffffu ? e : e % n_dest;
+  }
+  return owner_of(r, n_dest);
+}
+
+template <bool DESC>
 __global__ __launch_bounds__(TILE) void bucket_hist_kernel(const rtps_record* recs, const uint64_t* n_rec,
-                                                            uint32_t n_dest, uint32_t* hist) {
+                                                            uint32_t n_dest, uint32_t* hist, DescOwner m) {
   __shared__ uint32_t h[MAX_DEST];
   if (threadIdx.x < n_dest) h[threadIdx.x] = 0;
   __syncthreads();
   uint64_t i = (uint64_t)blockIdx.x * TILE + threadIdx.x;
   if (i < *n_rec) {
-    uint32_t o = owner_of(recs + i, n_dest);
+    uint32_t o = owner_sel<DESC>(recs + i, n_dest, m);
     if (o != 0xffffffffu) atomicAdd(&h[o], 1u);
   }
   __syncthreads();
@@ -812,10 +841,11 @@ __global__ __launch_bounds__(TILE) void bucket_scan_kernel(uint32_t* hist, uint3
 
 // cap == 0: bucket d starts at sum(dest_counts[0..d)); cap > 0: at d * cap, and
 // records at positions >= cap inside their bucket are dropped
+template <bool DESC>
 __global__ __launch_bounds__(TILE) void bucket_scatter_kernel(const rtps_record* recs, const uint64_t* n_rec,
                                                                uint32_t n_dest, const uint32_t* offs,
                                                                const uint64_t* dest_counts, uint64_t cap,
-                                                               rtps_record* out) {
+                                                               void* out_v, DescOwner m) {
   __shared__ uint32_t wcnt[WAVES][MAX_DEST];
   __shared__ uint64_t base[MAX_DEST];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
@@ -824,7 +854,9 @@ __global__ __launch_bounds__(TILE) void bucket_scatter_kernel(const rtps_record*
     for (uint32_t d = 0; d < n_dest; ++d) { base[d] = cap ? d * cap : acc; acc += dest_counts[d]; }
   }
   uint64_t i = (uint64_t)blockIdx.x * TILE + tid;
-  uint32_t o = (i < *n_rec) ? owner_of(recs + i, n_dest) : 0xffffffffu;
+  const uint32_t ent = (DESC && i < *n_rec) ? desc_entry(recs + i, m) : 0xffffffffu;
+  uint32_t o = (i < *n_rec) ? (DESC ? (ent == 0xffffffffu ? ent : ent % n_dest) : owner_of(recs + i, n_dest))
+                            : 0xffffffffu;
   uint32_t rank = 0;
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64u - lane));
   for (uint32_t d = 0; d < n_dest; ++d) {
@@ -838,10 +870,19 @@ __global__ __launch_bounds__(TILE) void bucket_scatter_kernel(const rtps_record*
     for (uint32_t w = 0; w < wave; ++w) before += wcnt[w][o];
     const uint64_t pos = (uint64_t)offs[(uint64_t)blockIdx.x * n_dest + o] + before + rank;
     if (cap == 0 || pos < cap) {
-      const u32x4* src = reinterpret_cast<const u32x4*>(recs + i);
-      u32x4* dp = reinterpret_cast<u32x4*>(out + base[o] + pos);
-      u32x4 a = src[0], b = src[1], c = src[2], e = src[3];
-      dp[0] = a; dp[1] = b; dp[2] = c; dp[3] = e;
+      if (DESC) {
+        const rtps_record* r = recs + i;
+        rtps_xdesc x;
+        x.sn = r->sn;
+        x.rec_idx = (uint32_t)i;
+        x.writer_kind = (ent << 8) | r->kind;
+        reinterpret_cast<rtps_xdesc*>(out_v)[base[o] + pos] = x;
+      } else {
+        const u32x4* src = reinterpret_cast<const u32x4*>(recs + i);
+        u32x4* dp = reinterpret_cast<u32x4*>(reinterpret_cast<rtps_record*>(out_v) + base[o] + pos);
+        u32x4 a = src[0], b = src[1], c = src[2], e = src[3];
+        dp[0] = a; dp[1] = b; dp[2] = c; dp[3] = e;
+      }
     }
   }
 }
@@ -861,6 +902,7 @@ struct rtps_rx_ctx {
   size_t scratch_words = 0;
   u32x4* mt_keys = nullptr;
   uint16_t* mt_slots = nullptr;
+  uint32_t* mt_index = nullptr;  // entry index of each slot (descriptor owners)
   uint32_t mt_cap = 0;
   bool mt_active = false;
   uint32_t* bucket_hist = nullptr;
@@ -913,6 +955,7 @@ int rtps_rx_destroy(rtps_rx_ctx* c) {
   (void)hipFree(c->scratch);
   (void)hipFree(c->mt_keys);
   (void)hipFree(c->mt_slots);
+  (void)hipFree(c->mt_index);
   (void)hipFree(c->bucket_hist);
   rtps_frag_state_free(c->frag);
   (void)hipStreamDestroy(c->own_stream);
@@ -942,13 +985,19 @@ int rtps_rx_set_match_table(rtps_rx_ctx* c, const rtps_match* t, uint32_t n) {
   while (cap < 2u * n) cap <<= 1;
   std::vector<u32x4> keys(cap, u32x4{0u, 0u, 0u, 0u});
   std::vector<uint16_t> slots(cap, (uint16_t)RTPS_NO_MATCH);
+  std::vector<uint32_t> index(cap, 0u);
   for (uint32_t k = 0; k < n; ++k) {  // first entry wins on duplicates (oracle: linear scan)
     if (t[k].reader_slot == RTPS_NO_MATCH) return RTPS_RX_EINVAL;
     uint32_t w[4];
     memcpy(w, t[k].writer_guid, 16);
     uint32_t i = host_guid_hash(t[k].writer_guid) & (cap - 1);
     for (;;) {
-      if (slots[i] == RTPS_NO_MATCH) { keys[i] = u32x4{w[0], w[1], w[2], w[3]}; slots[i] = t[k].reader_slot; break; }
+      if (slots[i] == RTPS_NO_MATCH) {
+        keys[i] = u32x4{w[0], w[1], w[2], w[3]};
+        slots[i] = t[k].reader_slot;
+        index[i] = k;
+        break;
+      }
       if (keys[i][0] == w[0] && keys[i][1] == w[1] && keys[i][2] == w[2] && keys[i][3] == w[3]) break;
       i = (i + 1) & (cap - 1);
     }
@@ -957,14 +1006,17 @@ int rtps_rx_set_match_table(rtps_rx_ctx* c, const rtps_match* t, uint32_t n) {
   if (cap > c->mt_cap) {
     (void)hipFree(c->mt_keys);
     (void)hipFree(c->mt_slots);
-    c->mt_keys = nullptr; c->mt_slots = nullptr; c->mt_cap = 0;
+    (void)hipFree(c->mt_index);
+    c->mt_keys = nullptr; c->mt_slots = nullptr; c->mt_index = nullptr; c->mt_cap = 0;
     if (hipMalloc(&c->mt_keys, cap * sizeof(u32x4)) != hipSuccess) return RTPS_RX_ENOMEM;
     if (hipMalloc(&c->mt_slots, cap * sizeof(uint16_t)) != hipSuccess) return RTPS_RX_ENOMEM;
+    if (hipMalloc(&c->mt_index, cap * sizeof(uint32_t)) != hipSuccess) return RTPS_RX_ENOMEM;
     c->mt_cap = cap;
   }
   // keep the device table's capacity == cap (mask) by writing a full-size image
   if (hipMemcpy(c->mt_keys, keys.data(), cap * sizeof(u32x4), hipMemcpyHostToDevice) != hipSuccess) return RTPS_RX_EHIP;
   if (hipMemcpy(c->mt_slots, slots.data(), cap * sizeof(uint16_t), hipMemcpyHostToDevice) != hipSuccess) return RTPS_RX_EHIP;
+  if (hipMemcpy(c->mt_index, index.data(), cap * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) return RTPS_RX_EHIP;
   c->mt_active = true;
   c->mt_cap = cap;
   return RTPS_RX_OK;
@@ -1055,7 +1107,7 @@ uint64_t rtps_rx_gen_layout_host(int wl, uint64_t seed, uint64_t first_idx, uint
 
 
 static int bucket_impl(rtps_rx_ctx* c, const rtps_record* recs, const uint64_t* n_records, uint64_t max_records,
-                       uint32_t n_dest, uint64_t cap, rtps_record* out, uint64_t* dest_counts) {
+                       uint32_t n_dest, uint64_t cap, void* out, uint64_t* dest_counts, bool desc) {
   if (!c || !recs || !n_records || !out || !dest_counts || n_dest < 1 || n_dest > MAX_DEST) return RTPS_RX_EINVAL;
   (void)hipSetDevice(c->device);
   uint64_t tiles64 = (max_records + TILE - 1) / TILE;
@@ -1070,24 +1122,43 @@ static int bucket_impl(rtps_rx_ctx* c, const rtps_record* recs, const uint64_t* 
     if (hipMalloc(&c->bucket_hist, need) != hipSuccess) return RTPS_RX_ENOMEM;
     c->bucket_bytes = need;
   }
-  hipLaunchKernelGGL(bucket_hist_kernel, dim3(tiles), dim3(TILE), 0, c->stream, recs, n_records, n_dest, c->bucket_hist);
+  DescOwner m{c->mt_keys, c->mt_slots, c->mt_index, c->mt_cap ? c->mt_cap - 1 : 0};
+  if (desc) {
+    hipLaunchKernelGGL(bucket_hist_kernel<true>, dim3(tiles), dim3(TILE), 0, c->stream, recs, n_records, n_dest,
+                       c->bucket_hist, m);
+  } else {
+    hipLaunchKernelGGL(bucket_hist_kernel<false>, dim3(tiles), dim3(TILE), 0, c->stream, recs, n_records, n_dest,
+                       c->bucket_hist, m);
+  }
   hipLaunchKernelGGL(bucket_scan_kernel, dim3(n_dest), dim3(TILE), 0, c->stream, c->bucket_hist, tiles, n_dest,
                      dest_counts);
-  hipLaunchKernelGGL(bucket_scatter_kernel, dim3(tiles), dim3(TILE), 0, c->stream, recs, n_records, n_dest,
-                     c->bucket_hist, dest_counts, cap, out);
+  if (desc) {
+    hipLaunchKernelGGL(bucket_scatter_kernel<true>, dim3(tiles), dim3(TILE), 0, c->stream, recs, n_records, n_dest,
+                       c->bucket_hist, dest_counts, cap, out, m);
+  } else {
+    hipLaunchKernelGGL(bucket_scatter_kernel<false>, dim3(tiles), dim3(TILE), 0, c->stream, recs, n_records, n_dest,
+                       c->bucket_hist, dest_counts, cap, out, m);
+  }
   return hip_fail(hipGetLastError());
 }
 
 int rtps_rx_bucket_by_writer(rtps_rx_ctx* c, const rtps_record* recs, const uint64_t* n_records,
                              uint64_t max_records, uint32_t n_dest, rtps_record* out, uint64_t* dest_counts) {
-  return bucket_impl(c, recs, n_records, max_records, n_dest, 0, out, dest_counts);
+  return bucket_impl(c, recs, n_records, max_records, n_dest, 0, out, dest_counts, false);
 }
 
 int rtps_rx_bucket_by_writer_padded(rtps_rx_ctx* c, const rtps_record* recs, const uint64_t* n_records,
                                     uint64_t max_records, uint32_t n_dest, uint64_t cap, rtps_record* out,
                                     uint64_t* dest_counts) {
   if (cap == 0) return RTPS_RX_EINVAL;
-  return bucket_impl(c, recs, n_records, max_records, n_dest, cap, out, dest_counts);
+  return bucket_impl(c, recs, n_records, max_records, n_dest, cap, out, dest_counts, false);
+}
+
+int rtps_rx_bucket_descriptors(rtps_rx_ctx* c, const rtps_record* recs, const uint64_t* n_records,
+                               uint64_t max_records, uint32_t n_dest, uint64_t cap, rtps_xdesc* out,
+                               uint64_t* dest_counts) {
+  if (!c || cap == 0 || !c->mt_active) return RTPS_RX_EINVAL;
+  return bucket_impl(c, recs, n_records, max_records, n_dest, cap, out, dest_counts, true);
 }
 
 /* a18: batch CDR decode (rtps_cdr.hip).  The program is validated here so

@@ -54,7 +54,8 @@ class _Out(ctypes.Structure):
 EXPORTS = ["rtps_rx_create", "rtps_rx_destroy", "rtps_rx_set_stream", "rtps_rx_set_match_table",
            "rtps_rx_parse_batch", "rtps_rx_sync", "rtps_rx_strerror", "rtps_rx_max_records_host",
            "rtps_rx_generate", "rtps_rx_bucket_by_writer", "rtps_rx_set_spec_hint", "rtps_rx_cdr_decode",
-           "rtps_rx_bucket_by_writer_padded", "rtps_rx_frag_assemble", "rtps_rx_frag_reset"]
+           "rtps_rx_bucket_by_writer_padded", "rtps_rx_frag_assemble", "rtps_rx_frag_reset",
+           "rtps_rx_bucket_descriptors"]
 
 
 def lib():
@@ -83,6 +84,8 @@ def lib():
         L.rtps_rx_bucket_by_writer.restype = I
         L.rtps_rx_bucket_by_writer_padded.argtypes = [P, P, P, U64, U32, U64, P, P]
         L.rtps_rx_bucket_by_writer_padded.restype = I
+        L.rtps_rx_bucket_descriptors.argtypes = [P, P, P, U64, U32, U64, P, P]
+        L.rtps_rx_bucket_descriptors.restype = I
         L.rtps_rx_frag_assemble.argtypes = [P, P, U64, P, P, P, U64, ctypes.POINTER(_FragOut)]
         L.rtps_rx_frag_assemble.restype = I
         L.rtps_rx_frag_reset.argtypes = [P]
@@ -253,6 +256,13 @@ class MessageReceiver:
         _check(lib().rtps_rx_bucket_by_writer_padded(self._h, outs["records"].data_ptr(),
                                                      outs["n_records"].data_ptr(), outs["max_records"], n_dest, cap,
                                                      out_records.data_ptr(), dest_counts.data_ptr()))
+
+    def bucket_descriptors(self, outs, n_dest, cap, out_desc, dest_counts):
+        """16-byte exchange descriptors of the MATCHED records in n_dest fixed buckets of cap
+        (owner = match-table entry index % n_dest); needs a match table."""
+        _check(lib().rtps_rx_bucket_descriptors(self._h, outs["records"].data_ptr(), outs["n_records"].data_ptr(),
+                                                outs["max_records"], n_dest, cap, out_desc.data_ptr(),
+                                                dest_counts.data_ptr()))
 
     # ---- DataFrag reassembly (state persists in the context across batches) ----
     def alloc_frag_outputs(self, max_samples, heap_bytes):

@@ -59,6 +59,10 @@ UNION_BY_KIND = {DATA: U_DATA, DATA_FRAG: U_FRAG, HEARTBEAT: U_HB, HEARTBEAT_FRA
 
 MATCH_DTYPE = np.dtype([("writer_guid", "u1", (16,)), ("reader_slot", "<u2"), ("_pad", "<u2")])
 
+# exchange descriptor (rtps_xdesc): the compact cross-GPU form of a matched writer's record
+XDESC_DTYPE = np.dtype([("sn", "<i8"), ("rec_idx", "<u4"), ("writer_kind", "<u4")])
+assert XDESC_DTYPE.itemsize == 16
+
 # DataFrag reassembly output (rtps_frag_sample, include/rtps_rx.h)
 FRAG_OK, FRAG_SHORT, FRAG_NO_ROOM = 0, 1, 2
 FRAG_SAMPLE_DTYPE = np.dtype([("writer_guid", "u1", (16,)), ("sn", "<i8"), ("heap_off", "<u8"),

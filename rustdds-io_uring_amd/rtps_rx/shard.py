@@ -8,6 +8,14 @@ holds every record of its writers (ready for per-writer ordering, dedup and
 fragment assembly).  The reference has a single process and no exchange;
 this is the only collective of the path.
 
+What crosses xGMI (item):
+  * "records": the 64-byte records of every writer/reader submessage, owner =
+    GUID hash % world (rtps_rx_bucket_by_writer[_padded]);
+  * "descriptors": 16-byte rtps_xdesc of the MATCHED records only, owner =
+    match-table entry index % world (rtps_rx_bucket_descriptors): 4x fewer
+    bytes, and owners balanced by the table order instead of a hash of a few
+    writer GUIDs.  Full records and payloads stay on the source GPU.
+
 Two modes:
   * contiguous (cap=None): buckets back to back, split sizes read back to the
     host (one device->host round trip per exchange); exact-size messages.
@@ -21,6 +29,7 @@ Two modes:
 import torch
 
 RECORD_BYTES = 64
+ITEM_BYTES = {"records": 64, "descriptors": 16}
 
 
 def owner_hash_words(words):
@@ -34,23 +43,28 @@ def owner_hash_words(words):
 class Exchange:
     """Buffers + the exchange step for one rank."""
 
-    def __init__(self, rx, max_records, world, dist, device, cap=None):
+    def __init__(self, rx, max_records, world, dist, device, cap=None, item="records"):
         self.rx = rx
         self.world = world
         self.dist = dist
         self.device = device
         self.cap = cap
+        self.item = item
+        ib = ITEM_BYTES[item]
+        assert item == "records" or cap, "descriptors are exchanged in padded buckets"
         slots = world * cap if cap else max(max_records, 1)
-        self.bucketed = torch.empty((max(slots, 1), RECORD_BYTES), dtype=torch.uint8, device=device)
+        self.bucketed = torch.empty((max(slots, 1), ib), dtype=torch.uint8, device=device)
         self.counts = torch.zeros(world, dtype=torch.int64, device=device)
         self.recv_counts = torch.zeros(world, dtype=torch.int64, device=device)
-        self.received = torch.empty((max(slots, 1), RECORD_BYTES), dtype=torch.uint8, device=device) if cap else None
+        self.received = torch.empty((max(slots, 1), ib), dtype=torch.uint8, device=device) if cap else None
         backend = dist.get_backend() if dist is not None else None
         self.host_collectives = backend == "gloo"  # gloo moves CPU tensors only
 
     def bucket(self, outs):
         """Stable partition of this rank's records by owner rank (asynchronous)."""
-        if self.cap:
+        if self.item == "descriptors":
+            self.rx.bucket_descriptors(outs, self.world, self.cap, self.bucketed, self.counts)
+        elif self.cap:
             self.rx.bucket_by_writer_padded(outs, self.world, self.cap, self.bucketed, self.counts)
         else:
             self.rx.bucket_by_writer(outs, self.world, self.bucketed, self.counts)
@@ -99,8 +113,8 @@ class Exchange:
         return [w1, w2]
 
     def gather_received(self):
-        """Host view after exchange_async completed: the valid records from every source in
-        rank order ([m, 64] u8 on the device) and the per-source counts."""
+        """Host view after exchange_async completed: the valid items from every source in
+        rank order ([m, item bytes] u8 on the device) and the per-source counts."""
         rc = self.recv_counts.cpu().tolist()
         parts = [self.received[s * self.cap:s * self.cap + min(c, self.cap)] for s, c in enumerate(rc)]
         return torch.cat(parts) if parts else self.received[:0], [min(c, self.cap) for c in rc]

@@ -20,7 +20,8 @@ from rtps_rx.shard import Exchange
 from shard_ref import owner_np
 
 backend = sys.argv[1] if len(sys.argv) > 1 else "gloo"
-padded = len(sys.argv) > 2 and sys.argv[2] == "padded"
+padded = len(sys.argv) > 2 and sys.argv[2] in ("padded", "desc")
+desc = len(sys.argv) > 2 and sys.argv[2] == "desc"
 rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
 ngpu = torch.cuda.device_count()
 dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")) % ngpu)
@@ -38,14 +39,24 @@ ln_t = torch.from_numpy(ln.view(np.int32)).to(dev)
 rx.generate(rtps_rx.WL_C3, arena, off_t, ln_t, n, first_idx=rank * n)
 cap = rtps_rx.max_records(ln)
 outs = rx.alloc_outputs(n, cap)
+table = None
+if desc:  # every rank matches the same writers, listed in the same (sorted) order
+    from rtps_rx.records import MATCH_DTYPE
+    a0, o0, l0 = oracle.gen(oracle.WL_C3, 4000)
+    _, r0, _, _ = oracle.parse(a0, o0, l0)
+    guids = sorted({bytes(r["prefix"]) + bytes(r["writer_id"]) for r in r0 if r["kind"] in (0x15, 0x07, 0x08)})
+    table = np.zeros(len(guids), dtype=MATCH_DTYPE)
+    for k, g in enumerate(guids):
+        table[k]["writer_guid"] = np.frombuffer(g, dtype=np.uint8)
+    rx.set_match_table(table)
 rx.parse_batch_device(arena, off_t, ln_t, n, outs)
-if padded:  # fixed bucket capacity agreed over ranks from a first contiguous bucketing
-    probe = Exchange(rx, cap, world, dist, dev)
+if padded:  # fixed bucket capacity agreed over ranks from a first bucketing
+    probe = Exchange(rx, cap, world, dist, dev, cap=cap, item="descriptors") if desc else Exchange(rx, cap, world, dist, dev)
     probe.bucket(outs)
     t = probe.counts.max().reshape(1)
     t = t.cpu() if backend == "gloo" else t
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    ex = Exchange(rx, cap, world, dist, dev, cap=int(t.item()))
+    ex = Exchange(rx, cap, world, dist, dev, cap=int(t.item()), item="descriptors" if desc else "records")
 else:
     ex = Exchange(rx, cap, world, dist, dev)
 ex.bucket(outs)
@@ -53,15 +64,26 @@ torch.cuda.synchronize(dev)
 assert not (padded and ex.overflowed())
 got, split = ex.exchange()
 torch.cuda.synchronize(dev)
-got = got.cpu().numpy().reshape(-1).view(RECORD_DTYPE)
-exp = []
-for r in range(world):
-    a, o, l = oracle.gen(oracle.WL_C3, n, first_idx=r * n)
-    _, recs, _, _ = oracle.parse(a, o, l)
-    exp.append(recs[owner_np(recs, world) == rank])
-exp = np.concatenate(exp)
+if desc:
+    from rtps_rx.records import XDESC_DTYPE
+    from shard_ref import desc_bucket_np
+    got = got.cpu().numpy().reshape(-1).view(XDESC_DTYPE)
+    exp = []
+    for r in range(world):
+        a, o, l = oracle.gen(oracle.WL_C3, n, first_idx=r * n)
+        _, recs, _, _ = oracle.parse(a, o, l, match_table=table)
+        exp.append(desc_bucket_np(recs, [bytes(t["writer_guid"]) for t in table], world)[rank])
+    exp = np.concatenate(exp)
+else:
+    got = got.cpu().numpy().reshape(-1).view(RECORD_DTYPE)
+    exp = []
+    for r in range(world):
+        a, o, l = oracle.gen(oracle.WL_C3, n, first_idx=r * n)
+        _, recs, _, _ = oracle.parse(a, o, l)
+        exp.append(recs[owner_np(recs, world) == rank])
+    exp = np.concatenate(exp)
 ok = got.tobytes() == exp.tobytes()
-print(f"rank {rank}/{world} ({backend}{', padded' if padded else ''}): received {len(got)} records, expected {len(exp)}, "
+print(f"rank {rank}/{world} ({backend}{', desc' if desc else ', padded' if padded else ''}): received {len(got)} records, expected {len(exp)}, "
       f"{'OK' if ok else 'MISMATCH'}", flush=True)
 dist.barrier()
 dist.destroy_process_group()

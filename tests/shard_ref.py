@@ -23,3 +23,21 @@ def bucket_np(recs, world):
     order = idx[np.argsort(o[keep], kind="stable")]
     counts = np.bincount(o[keep], minlength=world).astype(np.int64)
     return recs[order], counts
+
+
+def desc_bucket_np(recs, table_guids, world):
+    """numpy reference of rtps_rx_bucket_descriptors: MATCHED records of table writers,
+    owner = first table index % world, stable; returns (list per owner of XDESC rows)."""
+    from rtps_rx.records import XDESC_DTYPE, ROUTE_MATCHED
+    index = {}
+    for k, g in enumerate(table_guids):
+        index.setdefault(bytes(g), k)
+    out = [[] for _ in range(world)]
+    for i, r in enumerate(recs):
+        if not (int(r["route"]) & ROUTE_MATCHED):
+            continue
+        k = index.get(bytes(r["prefix"]) + bytes(r["writer_id"]))
+        if k is None:
+            continue
+        out[k % world].append((int(r["sn"]), i, (k << 8) | int(r["kind"])))
+    return [np.array(o, dtype=XDESC_DTYPE) for o in out]

@@ -286,7 +286,47 @@ def test_bucket_by_writer_matches_reference(rx, world):
             assert not pn[d * pcap + k:(d + 1) * pcap].any()
 
 
-@pytest.mark.parametrize("mode", ["", "padded"])
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_bucket_descriptors_matches_reference(rx, world):
+    from shard_ref import desc_bucket_np
+    from rtps_rx.records import MATCH_DTYPE, XDESC_DTYPE
+    arena, off, ln = oracle.gen(oracle.WL_C3, 20000)
+    _, recs0, _, _ = oracle.parse(arena, off, ln)
+    guids = sorted({(bytes(r["prefix"]) + bytes(r["writer_id"])) for r in recs0[:4000]})
+    table_guids = guids[:max(3, len(guids) * 2 // 3)]  # some writers matched, some not
+    tbl = np.zeros(len(table_guids), dtype=MATCH_DTYPE)
+    for k, g in enumerate(table_guids):
+        tbl[k]["writer_guid"] = np.frombuffer(g, dtype=np.uint8)
+        tbl[k]["reader_slot"] = k % 5
+    rx.set_match_table(tbl)
+    try:
+        dev = torch.device("cuda", 0)
+        A = torch.from_numpy(arena).to(dev)
+        O = torch.from_numpy(off.view(np.int64)).to(dev)
+        L = torch.from_numpy(ln.view(np.int32)).to(dev)
+        cap = max_records(ln)
+        outs = rx.alloc_outputs(len(ln), cap)
+        torch.cuda.synchronize()
+        rx.parse_batch_device(A, O, L, len(ln), outs)
+        _, recs, _, _ = oracle.parse(arena, off, ln, match_table=tbl)
+        exp = desc_bucket_np(recs, table_guids, world)
+        sizes = [len(e) for e in exp]
+        assert sum(sizes) > 1000
+        for pcap in (max(sizes) + 3, max(min(sizes) // 2, 1)):
+            out = torch.zeros((world * pcap, 16), dtype=torch.uint8, device=dev)
+            cnt = torch.zeros(world, dtype=torch.int64, device=dev)
+            rx.bucket_descriptors(outs, world, pcap, out, cnt)
+            rx.sync()
+            assert cnt.cpu().numpy().tolist() == sizes
+            got = out.cpu().numpy().reshape(-1).view(XDESC_DTYPE)
+            for d in range(world):
+                k = min(sizes[d], pcap)
+                assert got[d * pcap:d * pcap + k].tobytes() == exp[d][:k].tobytes(), (pcap, d)
+    finally:
+        rx.set_match_table([])
+
+
+@pytest.mark.parametrize("mode", ["", "padded", "desc"])
 def test_sharded_path_two_ranks_gloo(mode):
     """Full N=2 path (device parse + device bucket + all-to-all) on one GPU with gloo;
     "padded" = fixed-capacity buckets with the equal-split exchange."""

@@ -90,3 +90,49 @@ def test_owner_hash_scalar_matches_vectorized():
     for i in range(0, len(recs), 37):
         if o[i] >= 0:
             assert owner_hash_words(w[i]) % 5 == o[i]
+
+
+def _desc_worker(rank, world, port, n, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from shard_ref import desc_bucket_np
+        recs = _rank_records(rank, n)
+        guids = sorted({bytes(r["prefix"]) + bytes(r["writer_id"]) for r in recs})
+        # MATCHED needs a match table in the parse: mark every writer record as matched here
+        recs = recs.copy()
+        wk = np.isin(recs["kind"], [0x15, 0x16, 0x07, 0x08, 0x13])
+        recs["route"][wk] |= 0x20
+        buckets = desc_bucket_np(recs, guids, world)
+        cap = 4 * n  # the same on every rank (equal-split all-to-all)
+        ex = Exchange(rx=None, max_records=len(recs), world=world, dist=dist, device=torch.device("cpu"), cap=cap,
+                      item="descriptors")
+        ex.bucketed.zero_()
+        for d in range(world):
+            raw = buckets[d].view(np.uint8).reshape(-1, 16)
+            ex.bucketed[d * cap:d * cap + len(raw)] = torch.from_numpy(raw)
+        ex.counts.copy_(torch.tensor([len(b) for b in buckets]))
+        got, split = ex.exchange()
+        q.put((rank, got.numpy().tobytes(), split, [b.tobytes() for b in buckets]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_descriptor_exchange_gloo():
+    world, n = 3, 2000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_desc_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        rank, buf, split, sent = q.get(timeout=300)
+        res[rank] = (buf, split, sent)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for owner in range(world):
+        exp = b"".join(res[src][2][owner] for src in range(world))
+        assert res[owner][0] == exp and sum(res[owner][1]) * 16 == len(exp)
