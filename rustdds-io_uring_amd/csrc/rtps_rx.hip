@@ -162,14 +162,27 @@ __device__ __forceinline__ uint32_t guid_hash(uint32_t a, uint32_t b, uint32_t c
   h = (h ^ c) * 0x01000193u; h = (h ^ d) * 0x01000193u;
   return h ^ (h >> 15);
 }
+// Match tables of up to MT_LDS slots (128 writers) are staged in LDS by every
+// parse workgroup (mt_stage); larger ones are probed in global memory (L2).
+constexpr uint32_t MT_LDS = 256;
+__shared__ u32x4 s_mt_keys[MT_LDS];
+__shared__ uint16_t s_mt_slots[MT_LDS];
+__device__ __forceinline__ void mt_stage(const KParams& p) {
+  if (p.mt_keys != nullptr && p.mt_mask < MT_LDS)
+    for (uint32_t i = threadIdx.x; i <= p.mt_mask; i += blockDim.x) {
+      s_mt_keys[i] = p.mt_keys[i];
+      s_mt_slots[i] = p.mt_slots[i];
+    }
+}
 __device__ __forceinline__ uint16_t match_lookup(const KParams& p, uint32_t a, uint32_t b, uint32_t c,
                                                  uint32_t d) {
   if (p.mt_keys == nullptr) return RTPS_NO_MATCH;
+  const bool lds = p.mt_mask < MT_LDS;
   uint32_t i = guid_hash(a, b, c, d) & p.mt_mask;
   for (uint32_t probe = 0; probe <= p.mt_mask; ++probe) {
-    uint16_t slot = p.mt_slots[i];
+    uint16_t slot = lds ? s_mt_slots[i] : p.mt_slots[i];
     if (slot == RTPS_NO_MATCH) return RTPS_NO_MATCH;
-    u32x4 k = p.mt_keys[i];
+    u32x4 k = lds ? s_mt_keys[i] : p.mt_keys[i];
     if (k[0] == a && k[1] == b && k[2] == c && k[3] == d) return slot;
     i = (i + 1u) & p.mt_mask;
   }
@@ -608,6 +621,7 @@ __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_spec_ker
   __shared__ uint16_t s_stage_match[STAGE_RECS];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const uint32_t tile = blockIdx.x;
+  mt_stage(p);  // visible after the __syncthreads below, before the writing walk
   TileCtx t;
   load_tile(p, tile, t);
   uint32_t cnt;
@@ -710,6 +724,8 @@ __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_fix_kern
   if (first > n_tiles) first = n_tiles;
   uint32_t tile = first + blockIdx.x;
   if (tile >= n_tiles) return;
+  mt_stage(p);
+  __syncthreads();
   uint64_t prefix, dummy_sum;
   uint32_t dummy_min;
   reduce_info(x.info, 0, tile, s_rsum, s_rmin, prefix, dummy_min);
