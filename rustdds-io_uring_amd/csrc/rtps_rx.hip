@@ -123,6 +123,30 @@ __device__ __forceinline__ void load_win(const Src& s, uint32_t o, Win& W) {
   W.w[4] = b[0]; W.w[5] = b[1]; W.w[6] = b[2]; W.w[7] = b[3];
   W.w[8] = ld4(s, o + 32); W.w[9] = 0; W.w[10] = 0; W.w[11] = 0;
 }
+// Kinds whose reader needs body bytes past 12 (window dwords 4..7): every
+// per-lane gather instruction costs the texture unit about one cycle per
+// active lane, so the second 16 bytes (and the DATA_FRAG sampleSize dword) are
+// fetched only by the lanes that use them.  Counting (WRITE=false) needs only
+// the NumberSet sizes and the DATA_FRAG fields; writing needs every fixed field.
+template <bool WRITE>
+__device__ __forceinline__ bool win_needs_tail(uint32_t kind) {
+  const uint32_t count_mask = (1u << RTPS_GAP) | (1u << RTPS_ACKNACK) | (1u << RTPS_NACK_FRAG);
+  const uint32_t write_mask = count_mask | (1u << RTPS_DATA) | (1u << RTPS_HEARTBEAT) |
+                              (1u << RTPS_HEARTBEAT_FRAG) | (1u << RTPS_INFO_SRC);
+  if (kind == RTPS_DATA_FRAG) return true;
+  return kind < 32u && (((WRITE ? write_mask : count_mask) >> kind) & 1u);
+}
+template <bool WRITE>
+__device__ __forceinline__ void load_win_lazy(const Src& s, uint32_t o, Win& W) {
+  const u32x4 a = ld16(s, o);
+  W.w[0] = a[0]; W.w[1] = a[1]; W.w[2] = a[2]; W.w[3] = a[3];
+  const uint32_t kind = a[0] & 0xffu;
+  u32x4 b = {0u, 0u, 0u, 0u};
+  if (win_needs_tail<WRITE>(kind)) b = ld16(s, o + 16);
+  W.w[4] = b[0]; W.w[5] = b[1]; W.w[6] = b[2]; W.w[7] = b[3];
+  W.w[8] = (kind == RTPS_DATA_FRAG) ? ld4(s, o + 32) : 0u;
+  W.w[9] = 0; W.w[10] = 0; W.w[11] = 0;
+}
 // the first submessage always starts at byte 20: its window comes from the
 // 64-byte head (bytes 0..64) already in registers
 __device__ __forceinline__ void head_win(const uint32_t* H, Win& W) {
@@ -162,27 +186,33 @@ __device__ __forceinline__ uint32_t guid_hash(uint32_t a, uint32_t b, uint32_t c
   h = (h ^ c) * 0x01000193u; h = (h ^ d) * 0x01000193u;
   return h ^ (h >> 15);
 }
-// Match tables of up to MT_LDS slots (128 writers) are staged in LDS by every
-// parse workgroup (mt_stage); larger ones are probed in global memory (L2).
-constexpr uint32_t MT_LDS = 256;
-__shared__ u32x4 s_mt_keys[MT_LDS];
-__shared__ uint16_t s_mt_slots[MT_LDS];
+// Match tables of up to MT_LDS slots (1024 writers) are staged in LDS by every
+// parse workgroup (mt_stage) in dynamic shared memory sized by the launch
+// (keys then slots; 18 B per slot), so small tables cost no occupancy; larger
+// ones are probed in global memory (L2).
+constexpr uint32_t MT_LDS = 2048;
+extern __shared__ u32x4 s_mt_dyn[];
+__host__ __device__ constexpr uint32_t mt_lds_bytes(uint32_t cap) { return cap * 18u; }
+__device__ __forceinline__ bool mt_in_lds(const KParams& p) { return p.mt_keys != nullptr && p.mt_mask < MT_LDS; }
 __device__ __forceinline__ void mt_stage(const KParams& p) {
-  if (p.mt_keys != nullptr && p.mt_mask < MT_LDS)
+  if (mt_in_lds(p)) {
+    uint16_t* slots = reinterpret_cast<uint16_t*>(s_mt_dyn + p.mt_mask + 1u);
     for (uint32_t i = threadIdx.x; i <= p.mt_mask; i += blockDim.x) {
-      s_mt_keys[i] = p.mt_keys[i];
-      s_mt_slots[i] = p.mt_slots[i];
+      s_mt_dyn[i] = p.mt_keys[i];
+      slots[i] = p.mt_slots[i];
     }
+  }
 }
 __device__ __forceinline__ uint16_t match_lookup(const KParams& p, uint32_t a, uint32_t b, uint32_t c,
                                                  uint32_t d) {
   if (p.mt_keys == nullptr) return RTPS_NO_MATCH;
   const bool lds = p.mt_mask < MT_LDS;
+  const uint16_t* s_slots = reinterpret_cast<const uint16_t*>(s_mt_dyn + p.mt_mask + 1u);
   uint32_t i = guid_hash(a, b, c, d) & p.mt_mask;
   for (uint32_t probe = 0; probe <= p.mt_mask; ++probe) {
-    uint16_t slot = lds ? s_mt_slots[i] : p.mt_slots[i];
+    uint16_t slot = lds ? s_slots[i] : p.mt_slots[i];
     if (slot == RTPS_NO_MATCH) return RTPS_NO_MATCH;
-    u32x4 k = lds ? s_mt_keys[i] : p.mt_keys[i];
+    u32x4 k = lds ? s_mt_dyn[i] : p.mt_keys[i];
     if (k[0] == a && k[1] == b && k[2] == c && k[3] == d) return slot;
     i = (i + 1u) & p.mt_mask;
   }
@@ -227,10 +257,276 @@ __device__ __forceinline__ bool param_list(const Src& s, uint32_t body_off, uint
   }
 }
 
-// Walk one datagram.  WRITE=false: validate + count materialised submessages.
-// WRITE=true: (datagram known OK) write its records starting at record index `ridx`.
-// Records go to p.records[ridx + k], or, when stage != nullptr, to the LDS
-// staging buffer stage[ridx + k - stage_first] (the caller copies it out).
+// submessage kinds the reference materialises in Message.submessages (every
+// kind except PAD and unknown / vendor / security ones, rtps/submessage.rs:233-235, 278-293)
+constexpr uint32_t EMIT_MASK = (1u << RTPS_ACKNACK) | (1u << RTPS_HEARTBEAT) | (1u << RTPS_GAP) |
+                               (1u << RTPS_INFO_TS) | (1u << RTPS_INFO_SRC) | (1u << RTPS_INFO_DST) |
+                               (1u << RTPS_INFO_REPLY) | (1u << RTPS_NACK_FRAG) | (1u << RTPS_HEARTBEAT_FRAG) |
+                               (1u << RTPS_DATA) | (1u << RTPS_DATA_FRAG);
+__device__ __forceinline__ bool emits(uint32_t kind) { return kind < 32u && ((EMIT_MASK >> kind) & 1u); }
+
+// Submessage::read_from_buffer length rule (rtps/submessage.rs:61-78): a zero
+// octetsToNextHeader means "to the end of the message" except for PAD / INFO_TS
+__device__ __forceinline__ uint32_t eff_len(uint32_t kind, uint32_t clen, uint32_t rem) {
+  return clen != 0u ? clen : ((kind == RTPS_PAD || kind == RTPS_INFO_TS) ? 0u : rem - 4u);
+}
+
+// What the body reader of one submessage produced.
+struct SubOut {
+  uint32_t cls;  // 0 not materialised, 1 writer kind, 2 reader kind, 3 interpreter kind
+  uint32_t route, pk, aux16, rid, wid;
+};
+
+// The per-kind body readers of src/messages/submessages/** for one submessage
+// whose window W starts at its header (W.w[0]).  Validates exactly what the
+// reference reader rejects; WRITE additionally fills the kind-specific record
+// words R.d[8..13] (and R.d[2..4] / R.d[10..11] for INFO_DST / INFO_SRC /
+// INFO_REPLY).  Returns false on a read error (the datagram is dropped).
+template <bool WRITE>
+__device__ __forceinline__ bool sub_body(const Src& s, const Win& W, uint32_t kind, uint32_t flags, bool le,
+                                         uint32_t body, uint32_t blen, Rec& R, SubOut& so) {
+  so.cls = 0; so.route = 0; so.pk = 0; so.aux16 = blen; so.rid = 0; so.wid = 0;
+  switch (kind) {
+    case RTPS_DATA: {  // Data::deserialize_data (data.rs:57-144)
+      if (blen < 20u) return false;
+      uint32_t otq = e16(W.w[1], 1, le);
+      if (otq < 16u) return false;
+      uint32_t pos = 20u;
+      if (otq > 16u) { pos = 4u + otq; if (pos > blen) return false; }
+      uint32_t fl = flags & 0x1fu;
+      bool q = (fl & 0x02u) != 0u, dk = (fl & 0x0cu) != 0u;
+      uint32_t qstart = pos, kh = 0, si = 0, rsi = 0;
+      if (q && !param_list(s, body, blen, le, pos, kh, si, rsi)) return false;
+      so.cls = 1;
+      if (WRITE) {
+        so.rid = W.w[2]; so.wid = W.w[3];
+        int64_t sn = sn_of(W.w[4], W.w[5], le);
+        uint32_t pl_off = body + pos, pl_len = blen - pos;
+        so.aux16 = pos - qstart;
+        if (q) so.route |= RTPS_ROUTE_HAS_QOS;
+        if (dk) so.route |= RTPS_ROUTE_HAS_PAYLOAD;
+        // Reader::data_to_dds_data (reader.rs:760-833)
+        uint32_t enc = 0;
+        if (dk) {
+          bool d = (fl & 0x04u) != 0u, k = (fl & 0x08u) != 0u;
+          if (d && k) so.pk = RTPS_PK_ERR_AMBIGUOUS;
+          else if (pl_len < 4u) so.pk = RTPS_PK_ERR_SHORT;
+          else {
+            so.pk = d ? RTPS_PK_DATA : RTPS_PK_KEY;
+            enc = (pos == 20u) ? W.w[6] : ld4(s, pl_off);  // rep_id[2] + options[2]
+          }
+        } else {
+          so.pk = kh ? RTPS_PK_KEY_HASH : RTPS_PK_ERR_NO_CONTENT;
+        }
+        R.d[8] = (uint32_t)sn; R.d[9] = (uint32_t)((uint64_t)sn >> 32);
+        R.d[10] = pl_off | (pl_len << 16);
+        R.d[11] = enc;
+        R.d[12] = kh | (si << 16);
+        R.d[13] = rsi;
+      }
+      return true;
+    }
+    case RTPS_DATA_FRAG: {  // DataFrag::deserialize (data_frag.rs:121-257)
+      if (blen < 32u) return false;
+      uint32_t otq = e16(W.w[1], 1, le);
+      if (otq < 28u) return false;
+      uint32_t pos = 32u;
+      if (otq > 28u) { pos = 4u + otq; if (pos > blen) return false; }
+      bool q = (flags & 0x02u) != 0u;
+      uint32_t qstart = pos, kh = 0, si = 0, rsi = 0;
+      if (q && !param_list(s, body, blen, le, pos, kh, si, rsi)) return false;
+      int64_t sn = sn_of(W.w[4], W.w[5], le);
+      if (sn < 1) return false;
+      uint32_t frag_start = e32(W.w[6], le);
+      uint32_t frags_in_sub = e16(W.w[7], 0, le), frag_size = e16(W.w[7], 1, le);
+      uint32_t data_size = e32(W.w[8], le);
+      if (frag_size < 1u || frag_size > data_size) return false;
+      uint32_t total = data_size / frag_size + ((data_size % frag_size) ? 1u : 0u);
+      if (frag_start < 1u || frag_start > total) return false;
+      so.cls = 1;
+      if (WRITE) {
+        so.rid = W.w[2]; so.wid = W.w[3];
+        so.aux16 = pos - qstart;
+        if (q) so.route |= RTPS_ROUTE_HAS_QOS;
+        so.route |= RTPS_ROUTE_HAS_PAYLOAD;
+        uint32_t pl_off = body + pos, pl_len = blen - pos;
+        R.d[8] = (uint32_t)sn; R.d[9] = (uint32_t)((uint64_t)sn >> 32);
+        R.d[10] = pl_off | (pl_len << 16);
+        R.d[11] = frag_start;
+        R.d[12] = frags_in_sub | (frag_size << 16);
+        R.d[13] = data_size;
+      }
+      return true;
+    }
+    case RTPS_HEARTBEAT: {  // Heartbeat (heartbeat.rs:21-49): 28 bytes
+      if (blen < 28u) return false;
+      so.cls = 1;
+      if (WRITE) {
+        so.rid = W.w[1]; so.wid = W.w[2];
+        int64_t first = sn_of(W.w[3], W.w[4], le), last = sn_of(W.w[5], W.w[6], le);
+        R.d[8] = (uint32_t)first; R.d[9] = (uint32_t)((uint64_t)first >> 32);
+        R.d[10] = (uint32_t)last; R.d[11] = (uint32_t)((uint64_t)last >> 32);
+        R.d[12] = e32(W.w[7], le);
+      }
+      return true;
+    }
+    case RTPS_HEARTBEAT_FRAG: {  // HeartbeatFrag (heartbeat_frag.rs:16-37): 24 bytes
+      if (blen < 24u) return false;
+      so.cls = 1;
+      if (WRITE) {
+        so.rid = W.w[1]; so.wid = W.w[2];
+        int64_t sn = sn_of(W.w[3], W.w[4], le);
+        R.d[8] = (uint32_t)sn; R.d[9] = (uint32_t)((uint64_t)sn >> 32);
+        R.d[10] = e32(W.w[5], le);
+        R.d[11] = e32(W.w[6], le);
+      }
+      return true;
+    }
+    case RTPS_GAP: {  // Gap (gap.rs:23-46): rid wid gapStart SNSet
+      if (blen < 28u) return false;
+      uint32_t nb = e32(W.w[7], le);
+      if (nb > 256u) return false;
+      uint32_t words = (nb + 31u) >> 5;
+      if (28u + 4u * words > blen) return false;
+      so.cls = 1;
+      if (WRITE) {
+        so.rid = W.w[1]; so.wid = W.w[2];
+        int64_t gs = sn_of(W.w[3], W.w[4], le), lb = sn_of(W.w[5], W.w[6], le);
+        R.d[8] = (uint32_t)gs; R.d[9] = (uint32_t)((uint64_t)gs >> 32);
+        R.d[10] = (uint32_t)lb; R.d[11] = (uint32_t)((uint64_t)lb >> 32);
+        R.d[12] = nb;
+        R.d[13] = body + 28u;
+      }
+      return true;
+    }
+    case RTPS_ACKNACK: {  // AckNack (ack_nack.rs:27-50): rid wid SNSet count
+      if (blen < 20u) return false;
+      uint32_t nb = e32(W.w[5], le);
+      if (nb > 256u) return false;
+      uint32_t words = (nb + 31u) >> 5;
+      if (24u + 4u * words > blen) return false;
+      so.cls = 2;
+      if (WRITE) {
+        so.rid = W.w[1]; so.wid = W.w[2];
+        int64_t base = sn_of(W.w[3], W.w[4], le);
+        R.d[8] = (uint32_t)base; R.d[9] = (uint32_t)((uint64_t)base >> 32);
+        R.d[10] = e32(ld4(s, body + 20u + 4u * words), le);
+        R.d[12] = nb;
+        R.d[13] = body + 20u;
+      }
+      return true;
+    }
+    case RTPS_NACK_FRAG: {  // NackFrag (nack_frag.rs:31-53): rid wid sn FNSet count
+      if (blen < 24u) return false;
+      uint32_t nb = e32(W.w[6], le);
+      if (nb > 256u) return false;
+      uint32_t words = (nb + 31u) >> 5;
+      if (28u + 4u * words > blen) return false;
+      so.cls = 2;
+      if (WRITE) {
+        so.rid = W.w[1]; so.wid = W.w[2];
+        int64_t sn = sn_of(W.w[3], W.w[4], le);
+        R.d[8] = (uint32_t)sn; R.d[9] = (uint32_t)((uint64_t)sn >> 32);
+        R.d[10] = e32(W.w[5], le);
+        R.d[11] = e32(ld4(s, body + 24u + 4u * words), le);
+        R.d[12] = nb;
+        R.d[13] = body + 24u;
+      }
+      return true;
+    }
+    case RTPS_INFO_TS:  // rtps/submessage.rs:211-225 (Invalidate flag: no body read)
+      if (!(flags & 0x02u) && blen < 8u) return false;
+      so.cls = 3;
+      return true;
+    case RTPS_INFO_SRC:  // InfoSource (info_source.rs:22-36)
+      if (blen < 20u) return false;
+      so.cls = 3;
+      if (WRITE) R.d[10] = W.w[2];
+      return true;
+    case RTPS_INFO_DST:  // InfoDestination (info_destination.rs:20-25)
+      if (blen < 12u) return false;
+      so.cls = 3;
+      if (WRITE) { R.d[2] = W.w[1]; R.d[3] = W.w[2]; R.d[4] = W.w[3]; }
+      return true;
+    case RTPS_INFO_REPLY: {  // InfoReply (info_reply.rs:9-21): Vec<Locator> + Option<Vec<Locator>>
+      if (blen < 4u) return false;
+      uint32_t n1 = e32(W.w[1], le), n2 = 0xffffffffu;
+      uint64_t pos = 4u + 24ull * n1;
+      if (pos > blen) return false;
+      if (pos + 1u > blen) return false;
+      uint32_t tag = ld4(s, body + (uint32_t)pos) & 0xffu;
+      pos += 1u;
+      if (tag != 0u) {
+        if (pos + 4u > blen) return false;
+        n2 = e32(ld4(s, body + (uint32_t)pos), le);
+        pos += 4u;
+        if (pos + 24ull * n2 > blen) return false;
+      }
+      so.cls = 3;
+      if (WRITE) { R.d[10] = n1; R.d[11] = n2; }
+      return true;
+    }
+    default:  // PAD, INFO_REPLY_IP4, SEC_*, vendor and unknown kinds: skipped (:233-235, :278-293)
+      return true;
+  }
+}
+
+// Interpreter state in effect *after* a submessage (SubmessageIter2,
+// io_uring/rtps/message_receiver.rs:56-119, 618-665).
+struct Interp {
+  uint32_t src0, src1, src2;  // source GuidPrefix
+  bool dst_ok;                // dest == own || dest == UNKNOWN
+  bool ts_valid;
+  uint32_t ts_sec, ts_frac;
+};
+
+// Common tail of a record: ids, source prefix, the SubmessageIter2 writer
+// filter (:75-84), builtin / matched classification, timestamp, word 7.
+// Returns the match slot.
+__device__ __forceinline__ uint16_t rec_finish(const KParams& p, Rec& R, const SubOut& so, uint32_t kind,
+                                               const Interp& st) {
+  uint32_t route = so.route;
+  uint16_t mslot = RTPS_NO_MATCH;
+  if (kind != RTPS_INFO_DST) { R.d[2] = st.src0; R.d[3] = st.src1; R.d[4] = st.src2; }
+  if (so.cls != 3) {
+    R.d[5] = so.wid; R.d[6] = so.rid;
+    if (so.cls == 1) {
+      if (st.dst_ok) route |= RTPS_ROUTE_PASS;
+      if (builtin_writer_pair(so.rid, so.wid)) route |= RTPS_ROUTE_BUILTIN;
+      else {
+        mslot = match_lookup(p, st.src0, st.src1, st.src2, so.wid);
+        if (mslot != RTPS_NO_MATCH) route |= RTPS_ROUTE_MATCHED;
+      }
+    } else {
+      route |= RTPS_ROUTE_PASS;
+      if (builtin_reader_pair(so.rid, so.wid)) route |= RTPS_ROUTE_BUILTIN;
+    }
+  }
+  if (st.ts_valid) { route |= RTPS_ROUTE_TS_VALID; R.d[14] = st.ts_sec; R.d[15] = st.ts_frac; }
+  R.d[7] = (so.aux16 & 0xffffu) | (route << 16) | (so.pk << 24);
+  return mslot;
+}
+
+// SubmessageIter2 interpreter transitions (message_receiver.rs:618-665)
+__device__ __forceinline__ void interp_update(const KParams& p, Interp& st, const Win& W, uint32_t kind,
+                                              uint32_t flags, bool le) {
+  if (kind == RTPS_INFO_TS) {  // Invalidate flag -> None
+    st.ts_valid = !(flags & 0x02u);
+    st.ts_sec = st.ts_valid ? e32(W.w[1], le) : 0u;
+    st.ts_frac = st.ts_valid ? e32(W.w[2], le) : 0u;
+  } else if (kind == RTPS_INFO_SRC) {  // new source, timestamp cleared (:626-636)
+    st.src0 = W.w[3]; st.src1 = W.w[4]; st.src2 = W.w[5];
+    st.ts_valid = false; st.ts_sec = 0u; st.ts_frac = 0u;
+  } else if (kind == RTPS_INFO_DST) {  // UNKNOWN -> own (:656-662)
+    const uint32_t a = W.w[1], b = W.w[2], c = W.w[3];
+    st.dst_ok = ((a | b | c) == 0u) || (a == p.own0 && b == p.own1 && c == p.own2);
+  }
+}
+
+// Walk one datagram on one lane.  WRITE=false: validate + count materialised
+// submessages.  WRITE=true (datagram known OK): write its records starting at
+// record index `ridx`, to p.records[ridx + k], or, when stage != nullptr, to
+// the LDS staging buffer stage[ridx + k - stage_first] (the caller copies it out).
 template <bool WRITE>
 __device__ uint32_t walk(const KParams& p, const Src& s, const uint32_t* H, uint32_t L, uint32_t dgram_idx,
                          uint64_t ridx, uint32_t& nrec, u32x4* stage = nullptr, uint16_t* stage_match = nullptr,
@@ -247,258 +543,29 @@ __device__ uint32_t walk(const KParams& p, const Src& s, const uint32_t* H, uint
   if (H[0] != MAGIC_RTPS) return H[0] == MAGIC_RTPX ? RTPS_DGRAM_RTPX : RTPS_DGRAM_BAD_MAGIC;
   if ((H[1] & 0xffu) > 2u) return RTPS_DGRAM_BAD_HEADER;  // ProtocolVersion major
   // handle_parsed_message_2 (:289-295): src := header prefix, dest := own, ts := None
-  uint32_t src0 = H[2], src1 = H[3], src2 = H[4];
-  uint32_t dst0 = p.own0, dst1 = p.own1, dst2 = p.own2;
-  bool ts_valid = false;
-  uint32_t ts_sec = 0, ts_frac = 0;
-
+  Interp st{H[2], H[3], H[4], true, false, 0u, 0u};
   uint32_t o = 20;
   while (o < L) {
     uint32_t rem = L - o;
     if (rem < 4u) return RTPS_DGRAM_SUBMSG_ERR;  // SubmessageHeader needs 4 bytes
     Win W;
     if (o == 20u) head_win(H, W);
-    else load_win(s, o, W);
+    else load_win_lazy<WRITE>(s, o, W);
     uint32_t kind = W.w[0] & 0xffu, flags = (W.w[0] >> 8) & 0xffu;
     bool le = (flags & 1u) != 0u;
-    uint32_t clen = e16(W.w[0], 1, le);
-    uint32_t eff = clen != 0u ? clen : ((kind == RTPS_PAD || kind == RTPS_INFO_TS) ? 0u : rem - 4u);
+    uint32_t eff = eff_len(kind, e16(W.w[0], 1, le), rem);
     if (4u + eff > rem) return RTPS_DGRAM_SUBMSG_ERR;
-    const uint32_t blen = eff, body = o + 4u;
-    const uint32_t next = o + 4u + eff;
-
     Rec R;
-    if (WRITE) {
-      rec_clear(R);
-      R.d[0] = dgram_idx;
-      R.d[1] = o | (kind << 16) | (flags << 24);
-    }
-    bool emit = true;
-    uint32_t route = 0, pk = 0, aux16 = blen;
-    uint16_t mslot = RTPS_NO_MATCH;
-    int cls = 0;  // 1 writer, 2 reader, 3 interpreter
-    uint32_t rid = 0, wid = 0;
-
-    switch (kind) {
-      case RTPS_DATA: {  // Data::deserialize_data (data.rs:57-144)
-        if (blen < 20u) return RTPS_DGRAM_SUBMSG_ERR;
-        uint32_t otq = e16(W.w[1], 1, le);
-        if (otq < 16u) return RTPS_DGRAM_SUBMSG_ERR;
-        uint32_t pos = 20u;
-        if (otq > 16u) { pos = 4u + otq; if (pos > blen) return RTPS_DGRAM_SUBMSG_ERR; }
-        uint32_t fl = flags & 0x1fu;
-        bool q = (fl & 0x02u) != 0u, dk = (fl & 0x0cu) != 0u;
-        uint32_t qstart = pos, kh = 0, si = 0, rsi = 0;
-        if (q && !param_list(s, body, blen, le, pos, kh, si, rsi)) return RTPS_DGRAM_SUBMSG_ERR;
-        cls = 1;
-        if (WRITE) {
-          rid = W.w[2]; wid = W.w[3];
-          int64_t sn = sn_of(W.w[4], W.w[5], le);
-          uint32_t pl_off = body + pos, pl_len = blen - pos;
-          aux16 = pos - qstart;
-          if (q) route |= RTPS_ROUTE_HAS_QOS;
-          if (dk) route |= RTPS_ROUTE_HAS_PAYLOAD;
-          // Reader::data_to_dds_data (reader.rs:760-833)
-          uint32_t enc = 0;
-          if (dk) {
-            bool d = (fl & 0x04u) != 0u, k = (fl & 0x08u) != 0u;
-            if (d && k) pk = RTPS_PK_ERR_AMBIGUOUS;
-            else if (pl_len < 4u) pk = RTPS_PK_ERR_SHORT;
-            else {
-              pk = d ? RTPS_PK_DATA : RTPS_PK_KEY;
-              enc = (pos == 20u) ? W.w[6] : ld4(s, pl_off);  // rep_id[2] + options[2]
-            }
-          } else {
-            pk = kh ? RTPS_PK_KEY_HASH : RTPS_PK_ERR_NO_CONTENT;
-          }
-          R.d[8] = (uint32_t)sn; R.d[9] = (uint32_t)((uint64_t)sn >> 32);
-          R.d[10] = pl_off | (pl_len << 16);
-          R.d[11] = enc;
-          R.d[12] = kh | (si << 16);
-          R.d[13] = rsi;
-        }
-        break;
-      }
-      case RTPS_DATA_FRAG: {  // DataFrag::deserialize (data_frag.rs:121-257)
-        if (blen < 32u) return RTPS_DGRAM_SUBMSG_ERR;
-        uint32_t otq = e16(W.w[1], 1, le);
-        if (otq < 28u) return RTPS_DGRAM_SUBMSG_ERR;
-        uint32_t pos = 32u;
-        if (otq > 28u) { pos = 4u + otq; if (pos > blen) return RTPS_DGRAM_SUBMSG_ERR; }
-        bool q = (flags & 0x02u) != 0u;
-        uint32_t qstart = pos, kh = 0, si = 0, rsi = 0;
-        if (q && !param_list(s, body, blen, le, pos, kh, si, rsi)) return RTPS_DGRAM_SUBMSG_ERR;
-        int64_t sn = sn_of(W.w[4], W.w[5], le);
-        if (sn < 1) return RTPS_DGRAM_SUBMSG_ERR;
-        uint32_t frag_start = e32(W.w[6], le);
-        uint32_t frags_in_sub = e16(W.w[7], 0, le), frag_size = e16(W.w[7], 1, le);
-        uint32_t data_size = e32(W.w[8], le);
-        if (frag_size < 1u || frag_size > data_size) return RTPS_DGRAM_SUBMSG_ERR;
-        uint32_t total = data_size / frag_size + ((data_size % frag_size) ? 1u : 0u);
-        if (frag_start < 1u || frag_start > total) return RTPS_DGRAM_SUBMSG_ERR;
-        cls = 1;
-        if (WRITE) {
-          rid = W.w[2]; wid = W.w[3];
-          aux16 = pos - qstart;
-          if (q) route |= RTPS_ROUTE_HAS_QOS;
-          route |= RTPS_ROUTE_HAS_PAYLOAD;
-          uint32_t pl_off = body + pos, pl_len = blen - pos;
-          R.d[8] = (uint32_t)sn; R.d[9] = (uint32_t)((uint64_t)sn >> 32);
-          R.d[10] = pl_off | (pl_len << 16);
-          R.d[11] = frag_start;
-          R.d[12] = frags_in_sub | (frag_size << 16);
-          R.d[13] = data_size;
-        }
-        break;
-      }
-      case RTPS_HEARTBEAT: {  // Heartbeat (heartbeat.rs:21-49): 28 bytes
-        if (blen < 28u) return RTPS_DGRAM_SUBMSG_ERR;
-        cls = 1;
-        if (WRITE) {
-          rid = W.w[1]; wid = W.w[2];
-          int64_t first = sn_of(W.w[3], W.w[4], le), last = sn_of(W.w[5], W.w[6], le);
-          R.d[8] = (uint32_t)first; R.d[9] = (uint32_t)((uint64_t)first >> 32);
-          R.d[10] = (uint32_t)last; R.d[11] = (uint32_t)((uint64_t)last >> 32);
-          R.d[12] = e32(W.w[7], le);
-        }
-        break;
-      }
-      case RTPS_HEARTBEAT_FRAG: {  // HeartbeatFrag (heartbeat_frag.rs:16-37): 24 bytes
-        if (blen < 24u) return RTPS_DGRAM_SUBMSG_ERR;
-        cls = 1;
-        if (WRITE) {
-          rid = W.w[1]; wid = W.w[2];
-          int64_t sn = sn_of(W.w[3], W.w[4], le);
-          R.d[8] = (uint32_t)sn; R.d[9] = (uint32_t)((uint64_t)sn >> 32);
-          R.d[10] = e32(W.w[5], le);
-          R.d[11] = e32(W.w[6], le);
-        }
-        break;
-      }
-      case RTPS_GAP: {  // Gap (gap.rs:23-46): rid wid gapStart SNSet
-        if (blen < 28u) return RTPS_DGRAM_SUBMSG_ERR;
-        uint32_t nb = e32(W.w[7], le);
-        if (nb > 256u) return RTPS_DGRAM_SUBMSG_ERR;
-        uint32_t words = (nb + 31u) >> 5;
-        if (28u + 4u * words > blen) return RTPS_DGRAM_SUBMSG_ERR;
-        cls = 1;
-        if (WRITE) {
-          rid = W.w[1]; wid = W.w[2];
-          int64_t gs = sn_of(W.w[3], W.w[4], le), lb = sn_of(W.w[5], W.w[6], le);
-          R.d[8] = (uint32_t)gs; R.d[9] = (uint32_t)((uint64_t)gs >> 32);
-          R.d[10] = (uint32_t)lb; R.d[11] = (uint32_t)((uint64_t)lb >> 32);
-          R.d[12] = nb;
-          R.d[13] = body + 28u;
-        }
-        break;
-      }
-      case RTPS_ACKNACK: {  // AckNack (ack_nack.rs:27-50): rid wid SNSet count
-        if (blen < 20u) return RTPS_DGRAM_SUBMSG_ERR;
-        uint32_t nb = e32(W.w[5], le);
-        if (nb > 256u) return RTPS_DGRAM_SUBMSG_ERR;
-        uint32_t words = (nb + 31u) >> 5;
-        if (24u + 4u * words > blen) return RTPS_DGRAM_SUBMSG_ERR;
-        cls = 2;
-        if (WRITE) {
-          rid = W.w[1]; wid = W.w[2];
-          int64_t base = sn_of(W.w[3], W.w[4], le);
-          R.d[8] = (uint32_t)base; R.d[9] = (uint32_t)((uint64_t)base >> 32);
-          R.d[10] = e32(ld4(s, body + 20u + 4u * words), le);
-          R.d[12] = nb;
-          R.d[13] = body + 20u;
-        }
-        break;
-      }
-      case RTPS_NACK_FRAG: {  // NackFrag (nack_frag.rs:31-53): rid wid sn FNSet count
-        if (blen < 24u) return RTPS_DGRAM_SUBMSG_ERR;
-        uint32_t nb = e32(W.w[6], le);
-        if (nb > 256u) return RTPS_DGRAM_SUBMSG_ERR;
-        uint32_t words = (nb + 31u) >> 5;
-        if (28u + 4u * words > blen) return RTPS_DGRAM_SUBMSG_ERR;
-        cls = 2;
-        if (WRITE) {
-          rid = W.w[1]; wid = W.w[2];
-          int64_t sn = sn_of(W.w[3], W.w[4], le);
-          R.d[8] = (uint32_t)sn; R.d[9] = (uint32_t)((uint64_t)sn >> 32);
-          R.d[10] = e32(W.w[5], le);
-          R.d[11] = e32(ld4(s, body + 24u + 4u * words), le);
-          R.d[12] = nb;
-          R.d[13] = body + 24u;
-        }
-        break;
-      }
-      case RTPS_INFO_TS: {  // rtps/submessage.rs:211-225
-        cls = 3;
-        if (flags & 0x02u) { ts_valid = false; ts_sec = 0; ts_frac = 0; }
-        else {
-          if (blen < 8u) return RTPS_DGRAM_SUBMSG_ERR;
-          ts_valid = true; ts_sec = e32(W.w[1], le); ts_frac = e32(W.w[2], le);
-        }
-        if (WRITE) { R.d[2] = src0; R.d[3] = src1; R.d[4] = src2; }
-        break;
-      }
-      case RTPS_INFO_SRC: {  // InfoSource (info_source.rs:22-36); interpreter :626-636
-        if (blen < 20u) return RTPS_DGRAM_SUBMSG_ERR;
-        cls = 3;
-        src0 = W.w[3]; src1 = W.w[4]; src2 = W.w[5];
-        ts_valid = false; ts_sec = 0; ts_frac = 0;
-        if (WRITE) { R.d[2] = src0; R.d[3] = src1; R.d[4] = src2; R.d[10] = W.w[2]; }
-        break;
-      }
-      case RTPS_INFO_DST: {  // InfoDestination; interpreter :656-662
-        if (blen < 12u) return RTPS_DGRAM_SUBMSG_ERR;
-        cls = 3;
-        uint32_t a = W.w[1], b = W.w[2], c = W.w[3];
-        if ((a | b | c) == 0u) { dst0 = p.own0; dst1 = p.own1; dst2 = p.own2; }
-        else { dst0 = a; dst1 = b; dst2 = c; }
-        if (WRITE) { R.d[2] = a; R.d[3] = b; R.d[4] = c; }
-        break;
-      }
-      case RTPS_INFO_REPLY: {  // InfoReply (info_reply.rs:9-21): Vec<Locator> + Option<Vec<Locator>>
-        if (blen < 4u) return RTPS_DGRAM_SUBMSG_ERR;
-        uint32_t n1 = e32(W.w[1], le), n2 = 0xffffffffu;
-        uint64_t pos = 4u + 24ull * n1;
-        if (pos > blen) return RTPS_DGRAM_SUBMSG_ERR;
-        if (pos + 1u > blen) return RTPS_DGRAM_SUBMSG_ERR;
-        uint32_t tag = ld4(s, body + (uint32_t)pos) & 0xffu;
-        pos += 1u;
-        if (tag != 0u) {
-          if (pos + 4u > blen) return RTPS_DGRAM_SUBMSG_ERR;
-          n2 = e32(ld4(s, body + (uint32_t)pos), le);
-          pos += 4u;
-          if (pos + 24ull * n2 > blen) return RTPS_DGRAM_SUBMSG_ERR;
-        }
-        cls = 3;
-        if (WRITE) { R.d[2] = src0; R.d[3] = src1; R.d[4] = src2; R.d[10] = n1; R.d[11] = n2; }
-        break;
-      }
-      default:  // PAD, INFO_REPLY_IP4, SEC_*, vendor and unknown kinds: skipped (:233-235, :278-293)
-        emit = false;
-        break;
-    }
-
-    if (emit) {
+    if (WRITE) rec_clear(R);
+    SubOut so;
+    if (!sub_body<WRITE>(s, W, kind, flags, le, o + 4u, eff, R, so)) return RTPS_DGRAM_SUBMSG_ERR;
+    interp_update(p, st, W, kind, flags, le);
+    if (so.cls != 0u) {
       if (WRITE) {
-        if (cls != 3) {
-          R.d[2] = src0; R.d[3] = src1; R.d[4] = src2;
-          R.d[5] = wid; R.d[6] = rid;
-          if (cls == 1) {  // SubmessageIter2::next writer filter (message_receiver.rs:75-84)
-            bool own = dst0 == p.own0 && dst1 == p.own1 && dst2 == p.own2;
-            bool unk = (dst0 | dst1 | dst2) == 0u;
-            if (own || unk) route |= RTPS_ROUTE_PASS;
-            if (builtin_writer_pair(rid, wid)) route |= RTPS_ROUTE_BUILTIN;
-            else {
-              mslot = match_lookup(p, src0, src1, src2, wid);
-              if (mslot != RTPS_NO_MATCH) route |= RTPS_ROUTE_MATCHED;
-            }
-          } else {
-            route |= RTPS_ROUTE_PASS;
-            if (builtin_reader_pair(rid, wid)) route |= RTPS_ROUTE_BUILTIN;
-          }
-        }
-        if (ts_valid) { route |= RTPS_ROUTE_TS_VALID; R.d[14] = ts_sec; R.d[15] = ts_frac; }
-        R.d[7] = (aux16 & 0xffffu) | (route << 16) | (pk << 24);
-        uint64_t r = ridx + nrec;
+        R.d[0] = dgram_idx;
+        R.d[1] = o | (kind << 16) | (flags << 24);
+        const uint16_t mslot = rec_finish(p, R, so, kind, st);
+        const uint64_t r = ridx + nrec;
         if (stage) {
           u32x4* q = stage + (r - stage_first) * 4u;
           q[0] = u32x4{R.d[0], R.d[1], R.d[2], R.d[3]};
@@ -513,7 +580,7 @@ __device__ uint32_t walk(const KParams& p, const Src& s, const uint32_t* H, uint
       }
       nrec++;
     }
-    o = next;
+    o += 4u + eff;
   }
   return RTPS_DGRAM_OK;
 }
@@ -1066,10 +1133,11 @@ int rtps_rx_parse_batch(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len
   p.mt_mask = c->mt_active ? c->mt_cap - 1 : 0;
   p.scratch = c->scratch;
   const uint32_t parity = c->launch_parity;
+  const uint32_t mt_lds = (c->mt_active && c->mt_cap <= MT_LDS) ? mt_lds_bytes(c->mt_cap) : 0u;
   c->launch_parity ^= 1u;
-  hipLaunchKernelGGL(rtps_parse_spec_kernel, dim3(tiles), dim3(TILE), 0, c->stream, p, tiles, c->k_spec, parity);
+  hipLaunchKernelGGL(rtps_parse_spec_kernel, dim3(tiles), dim3(TILE), mt_lds, c->stream, p, tiles, c->k_spec, parity);
   uint32_t grid = tiles < c->resident_blocks ? tiles : c->resident_blocks;
-  hipLaunchKernelGGL(rtps_parse_fix_kernel, dim3(grid), dim3(TILE), 0, c->stream, p, tiles, c->k_spec, parity);
+  hipLaunchKernelGGL(rtps_parse_fix_kernel, dim3(grid), dim3(TILE), mt_lds, c->stream, p, tiles, c->k_spec, parity);
   return hip_fail(hipGetLastError());
 }
 
