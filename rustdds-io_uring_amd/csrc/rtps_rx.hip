@@ -147,6 +147,14 @@ __device__ __forceinline__ void load_win_lazy(const Src& s, uint32_t o, Win& W) 
   W.w[8] = (kind == RTPS_DATA_FRAG) ? ld4(s, o + 32) : 0u;
   W.w[9] = 0; W.w[10] = 0; W.w[11] = 0;
 }
+// prefetch form: header + body 0..28 (DATA_FRAG's sampleSize dword is fetched
+// when the kind is known)
+__device__ __forceinline__ void load_win_pf(const Src& s, uint32_t o, Win& W) {
+  const u32x4 a = ld16(s, o), b = ld16(s, o + 16);
+  W.w[0] = a[0]; W.w[1] = a[1]; W.w[2] = a[2]; W.w[3] = a[3];
+  W.w[4] = b[0]; W.w[5] = b[1]; W.w[6] = b[2]; W.w[7] = b[3];
+  W.w[8] = 0; W.w[9] = 0; W.w[10] = 0; W.w[11] = 0;
+}
 // the first submessage always starts at byte 20: its window comes from the
 // 64-byte head (bytes 0..64) already in registers
 __device__ __forceinline__ void head_win(const uint32_t* H, Win& W) {
@@ -545,16 +553,28 @@ __device__ uint32_t walk(const KParams& p, const Src& s, const uint32_t* H, uint
   // handle_parsed_message_2 (:289-295): src := header prefix, dest := own, ts := None
   Interp st{H[2], H[3], H[4], true, false, 0u, 0u};
   uint32_t o = 20;
+  // WRITE: the window of the next submessage is loaded before this record's
+  // stores are issued.  vmcnt counts stores too, so a load issued after them
+  // would make the next iteration wait for their write acknowledgements.
+  Win Wn;
+  if (WRITE) head_win(H, Wn);
   while (o < L) {
     uint32_t rem = L - o;
     if (rem < 4u) return RTPS_DGRAM_SUBMSG_ERR;  // SubmessageHeader needs 4 bytes
     Win W;
-    if (o == 20u) head_win(H, W);
-    else load_win_lazy<WRITE>(s, o, W);
+    if (WRITE) {
+      W = Wn;
+      if (o != 20u && (W.w[0] & 0xffu) == RTPS_DATA_FRAG) W.w[8] = ld4(s, o + 32u);
+    } else if (o == 20u) {
+      head_win(H, W);
+    } else {
+      load_win_lazy<WRITE>(s, o, W);
+    }
     uint32_t kind = W.w[0] & 0xffu, flags = (W.w[0] >> 8) & 0xffu;
     bool le = (flags & 1u) != 0u;
     uint32_t eff = eff_len(kind, e16(W.w[0], 1, le), rem);
     if (4u + eff > rem) return RTPS_DGRAM_SUBMSG_ERR;
+    if (WRITE && o + 4u + eff < L) load_win_pf(s, o + 4u + eff, Wn);
     Rec R;
     if (WRITE) rec_clear(R);
     SubOut so;
@@ -574,6 +594,9 @@ __device__ uint32_t walk(const KParams& p, const Src& s, const uint32_t* H, uint
           q[3] = u32x4{R.d[12], R.d[13], R.d[14], R.d[15]};
           stage_match[r - stage_first] = mslot;
         } else if (r < p.max_records) {
+#ifdef ABL_NO_REC_STORE
+          if (R.d[0] == 0xdeadbeefu)
+#endif
           rec_store(p.records + r, R);
           if (p.match_out) p.match_out[r] = mslot;
         }
@@ -817,7 +840,12 @@ __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_fix_kern
       if (p.rec_begin) p.rec_begin[t.i] = (uint32_t)my_first;
       if (cnt) {  // cnt > 0 implies status OK
         uint32_t n2;
+#ifdef ABL_COUNT_IN_FIX
+        walk<false>(p, t.s, t.H, t.L, t.i, my_first, n2);
+        if (n2 == 12345u) p.status[0] = 9;
+#else
         walk<true>(p, t.s, t.H, t.L, t.i, my_first, n2);
+#endif
       }
     }
     __syncthreads();  // s_wave_sum reuse
