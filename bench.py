@@ -192,6 +192,38 @@ def frag_leg(rx, arena, off_t, outs, n_rec, recs, stream, steps):
             "frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
 
+def ingest_leg(rx, arena, off_t, outs, n_rec, recs, n_entries, stream, steps):
+    """History-cache ingest (§8f rank 2) of this batch's samples / HEARTBEATs / GAPs,
+    timed separately (HIP events on the launch stream).  Every step starts from
+    fresh writer proxies (the reset is outside the timed region), so every step
+    does the same work: all first copies accepted."""
+    iouts = rx.alloc_ingest_outputs(n_rec, n_entries)
+    for _ in range(2):
+        rx.ingest_reset()
+        rx.ingest(arena, off_t, outs, iouts)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    torch.cuda.synchronize()
+    for a, b in ev:
+        rx.ingest_reset()
+        a.record(stream)
+        rx.ingest(arena, off_t, outs, iouts)
+        b.record(stream)
+    torch.cuda.synchronize()
+    ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    na = int(iouts["n_accepted"].item())
+    k = recs["kind"]
+    events = int((((recs["route"] & 0x21) == 0x21) & np.isin(k, (DATA, HEARTBEAT, GAP))).sum())
+    # algorithmic bytes: every record read once (64 B), 1 accept byte written per record, 4 B per
+    # accepted index, per event 8 B of writer state read and 4 B of change-set bits touched
+    alg = n_rec * (64 + 1) + 4 * na + 12 * events
+    return {"kernel": "rtps_ingest (classify + heartbeat sort/scans + marks + decide + select + merge + state)",
+            "ms": ms, "records": n_rec, "events": events, "accepted": na,
+            "samples_per_s": na / (ms * 1e-3), "records_per_s": n_rec / (ms * 1e-3),
+            "window_overflow": int(iouts["n_window_overflow"].item()),
+            "alg_bytes_per_launch": alg, "achieved_gbs": alg / (ms * 1e-3) / 1e9,
+            "frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+
+
 def cpu_baseline(workload, n, target_cpu_s=10.0, match_table=None):
     """The oracle (C restatement of the reference parse) on this host's cores, with the
     same match table as the device run."""
@@ -227,6 +259,7 @@ def main():
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-cdr", action="store_true", help="skip the CDR decode (a18) measurement")
     ap.add_argument("--no-frag", action="store_true", help="skip the DataFrag reassembly measurement (C4)")
+    ap.add_argument("--no-ingest", action="store_true", help="skip the history-cache ingest measurement")
     ap.add_argument("--match", default="writers", choices=["writers", "none"],
                     help="match table: every writer of the workload (a reader subscribed to all of them) or none")
     ap.add_argument("--exchange", default="descriptors", choices=["descriptors", "records"],
@@ -401,6 +434,8 @@ def main():
         result["cdr_decode"] = cdr_decode_leg(rx, args.workload, arena, off_t, outs, n_rec, stream, args.steps)
     if world == 1 and not args.no_frag and args.workload == "C4":
         result["frag_assemble"] = frag_leg(rx, arena, off_t, outs, n_rec, recs, stream, args.steps)
+    if world == 1 and not args.no_ingest and n_matched_writers:
+        result["ingest"] = ingest_leg(rx, arena, off_t, outs, n_rec, recs, n_matched_writers, stream, args.steps)
     if world == 1 and not args.no_e2e:
         result["end_to_end"] = end_to_end(rx, arena, off_t, ln_t, n, outs, n_rec, stream)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -360,6 +360,56 @@ int rtps_rx_frag_assemble(rtps_rx_ctx* ctx, const uint8_t* arena, uint64_t arena
 /* Drop every incomplete buffer and the writer fragment sizes (a new reader). */
 int rtps_rx_frag_reset(rtps_rx_ctx* ctx);
 
+/* ---- history-cache ingest ---------------------------
+ * Replaces, for every matched writer (match-table entry) of a stateful reader,
+ * the writer-proxy bookkeeping that decides which samples enter the history
+ * cache:
+ *   Reader::handle_data_msg -> process_received_data      io_uring/rtps/reader.rs:514-561, 693-758
+ *     RtpsWriterProxy::should_ignore_change, received_changes_add, advance_ack_base
+ *                                                         rtps/rtps_writer_proxy.rs:202-224, 338-355
+ *   Reader::handle_datafrag_msg, completed samples        reader.rs:563-636
+ *   Reader::handle_heartbeat_msg (Reliable readers only): count check, then
+ *     irrelevant_changes_up_to(first_sn)                  reader.rs:859-917, rtps_writer_proxy.rs:241-292
+ *   Reader::handle_gap_msg: gapStart > 0 and gapList.base > 0, then
+ *     irrelevant_changes_range(gapStart, gapList.base) and set_irrelevant_change
+ *     for every listed SN                                 reader.rs:1060-1116, rtps_writer_proxy.rs:226-239
+ *   TopicCache::add_change duplicate check, mark_reliably_received_before
+ *                                                         structure/dds_cache.rs:200-262
+ * Events are the records of a parse_batch output with RTPS_ROUTE_PASS and
+ * RTPS_ROUTE_MATCHED, in record order: DATA with payload_kind DATA / KEY /
+ * KEY_HASH and completed DataFrag samples (status != RTPS_FRAG_SHORT, placed
+ * at their completing record) are samples; HEARTBEAT and GAP update the
+ * writer's state.  A sample enters the cache (accept = 1) iff its writer proxy
+ * does not ignore it: sn >= all_ackable_before and sn not in the writer's
+ * change set (received or irrelevant).  Other records get accept = 0
+ * (unmatched writers: the reference drops user-defined ones; discovery traffic
+ * has its own path).  State per match-table entry (all_ackable_before, the
+ * change set above it, received_heartbeat_count) persists in the context across
+ * batches; it is indexed by entry position, so keep entries in place (append
+ * new writers) or call rtps_rx_ingest_reset after reordering the table.
+ * Limit: the change set is kept for RTPS_INGEST_WINDOW sequence numbers from
+ * all_ackable_before; a sample further ahead is accepted without the duplicate
+ * check and counted in *n_window_overflow (the reference's BTreeMap has no bound). */
+#define RTPS_INGEST_WINDOW (1u << 17)
+#define RTPS_INGEST_BEST_EFFORT 0x1u /* flags: BestEffort reader, HEARTBEATs ignored (reader.rs:870-881) */
+typedef struct rtps_ingest_out {
+  uint8_t* accept;              /* [max_records] device: 1 = this record's sample enters the cache */
+  uint32_t* accepted;           /* [max_records] device: indices of the accepting records, ascending */
+  uint64_t* n_accepted;         /* device u64 */
+  int64_t* ack_base;            /* device, optional: all_ackable_before() of every entry after the batch */
+  uint64_t* n_window_overflow;  /* device u64, optional */
+} rtps_ingest_out;
+/* arena / dgram_off / records / n_records / max_records: the batch and its
+ * parse_batch output (GAP bitmaps are read from the arena).  frag / n_frag /
+ * max_frag: optional rtps_rx_frag_assemble output of the same batch (device;
+ * NULL = none).  Asynchronous on the context's stream; needs a match table. */
+int rtps_rx_ingest(rtps_rx_ctx* ctx, const uint8_t* arena, uint64_t arena_len, const uint64_t* dgram_off,
+                   const rtps_record* records, const uint64_t* n_records, uint64_t max_records,
+                   const rtps_frag_sample* frag, const uint64_t* n_frag, uint64_t max_frag, uint32_t flags,
+                   const rtps_ingest_out* out);
+/* Forget every writer proxy's state (all_ackable_before = 1, empty change set, count 0). */
+int rtps_rx_ingest_reset(rtps_rx_ctx* ctx);
+
 /* Upper bound on records for datagram lengths (host arrays): sum((len-20)/4). */
 uint64_t rtps_rx_max_records_host(const uint32_t* dgram_len, uint32_t n);
 

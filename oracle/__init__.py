@@ -51,6 +51,12 @@ def lib():
         L.rtps_oracle_frag_pending.argtypes = [P]
         L.rtps_oracle_frag_batch.restype = ctypes.c_uint64
         L.rtps_oracle_frag_batch.argtypes = [P, P, P, P, ctypes.c_uint64, P, ctypes.c_uint64, P, ctypes.c_uint64, P]
+        L.rtps_oracle_ingest_new.restype = P
+        L.rtps_oracle_ingest_new.argtypes = [P, ctypes.c_uint32]
+        L.rtps_oracle_ingest_free.argtypes = [P]
+        L.rtps_oracle_ingest_batch.restype = ctypes.c_uint64
+        L.rtps_oracle_ingest_batch.argtypes = [P, P, P, P, ctypes.c_uint64, P, ctypes.c_uint64, ctypes.c_uint32,
+                                               P, P, P]
         L.rtps_oracle_cdr_decode.restype = None
         L.rtps_oracle_cdr_decode.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32, P, P, P, ctypes.c_uint64, P, P]
         assert L.rtps_oracle_record_size() == RECORD_DTYPE.itemsize
@@ -147,3 +153,33 @@ class FragAssembler:
         n = lib().rtps_oracle_frag_batch(self.h, _ptr(arena), _ptr(offs), _ptr(recs) if len(recs) else None,
                                          len(recs), _ptr(samples), ms, _ptr(heap), hb, ctypes.byref(used))
         return samples[:min(n, ms)], heap[:min(used.value, hb)], int(n), int(used.value)
+
+
+class HistoryIngest:
+    """Sequential writer-proxy restatement with state across batches (rtps_oracle_ingest_*)."""
+
+    def __init__(self, match_table):
+        t = np.ascontiguousarray(match_table, dtype=MATCH_DTYPE)
+        self.n = len(t)
+        self.h = ctypes.c_void_p(lib().rtps_oracle_ingest_new(_ptr(t) if len(t) else None, len(t)))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().rtps_oracle_ingest_free(self.h)
+            self.h = None
+
+    def batch(self, arena, offs, recs, frag_samples=None, best_effort=False):
+        """-> (accept u8[m], accepted u32[k], ack_base i64[n_entries])."""
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        recs = np.ascontiguousarray(recs, dtype=RECORD_DTYPE)
+        m = len(recs)
+        fs = None if frag_samples is None else np.ascontiguousarray(frag_samples, dtype=FRAG_SAMPLE_DTYPE)
+        accept = np.zeros(max(m, 1), dtype=np.uint8)
+        accepted = np.zeros(max(m, 1), dtype=np.uint32)
+        ack = np.zeros(max(self.n, 1), dtype=np.int64)
+        k = lib().rtps_oracle_ingest_batch(self.h, _ptr(arena), _ptr(offs), _ptr(recs) if m else None, m,
+                                           _ptr(fs) if fs is not None and len(fs) else None,
+                                           0 if fs is None else len(fs), 1 if best_effort else 0,
+                                           _ptr(accept), _ptr(accepted), _ptr(ack))
+        return accept[:m], accepted[:int(k)], ack[:self.n]

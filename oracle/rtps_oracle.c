@@ -932,3 +932,167 @@ uint64_t rtps_oracle_frag_batch(rtps_oracle_frag* f, const uint8_t* arena, const
   if (heap_used) *heap_used = used;
   return ns;
 }
+
+/* ------------------------------------------------------------------------ */
+/* History-cache ingest: the stateful reader's        */
+/* writer-proxy bookkeeping, restated sequentially in record order.          */
+/*   RtpsWriterProxy  rtps/rtps_writer_proxy.rs:17-355                        */
+/*   Reader::handle_data_msg / process_received_data                          */
+/*                    io_uring/rtps/reader.rs:514-561, 693-758                */
+/*   Reader::handle_heartbeat_msg  reader.rs:859-917                          */
+/*   Reader::handle_gap_msg        reader.rs:1060-1116                        */
+/* The proxy's `changes` BTreeMap is a hash set of sequence numbers: only    */
+/* membership is ever observed (should_ignore_change, advance_ack_base); the */
+/* entries irrelevant_changes_range removes all lie below the new ack_base.   */
+/* ------------------------------------------------------------------------ */
+typedef struct ig_proxy {
+  int64_t ack_base;   /* SequenceNumber::new(1) (rtps_writer_proxy.rs:96) */
+  int32_t hb_count;   /* received_heartbeat_count, 0 */
+  int64_t* set; uint8_t* used; size_t cap, n;
+} ig_proxy;
+typedef struct rtps_oracle_ingest {
+  uint32_t n;           /* match-table entries */
+  rtps_match* table;
+  ig_proxy* p;          /* one writer proxy per entry */
+  uint32_t* hslot;      /* GUID hash -> entry index + 1 (first entry wins) */
+  size_t hcap;
+} rtps_oracle_ingest;
+
+static size_t ig_h(int64_t s) { uint64_t x = (uint64_t)s * 0x9e3779b97f4a7c15ull; return (size_t)(x ^ (x >> 31)); }
+static int ig_has(const ig_proxy* p, int64_t s) {
+  if (!p->cap) return 0;
+  for (size_t j = ig_h(s) & (p->cap - 1); p->used[j]; j = (j + 1) & (p->cap - 1))
+    if (p->set[j] == s) return 1;
+  return 0;
+}
+static void ig_add(ig_proxy* p, int64_t s) {
+  if (ig_has(p, s)) return;
+  if ((p->n + 1) * 2 > p->cap) {
+    size_t ncap = p->cap ? p->cap * 2 : 64;
+    int64_t* ns = (int64_t*)calloc(ncap, sizeof(int64_t));
+    uint8_t* nu = (uint8_t*)calloc(ncap, 1);
+    for (size_t i = 0; i < p->cap; ++i)
+      if (p->used[i]) {
+        size_t j = ig_h(p->set[i]) & (ncap - 1);
+        while (nu[j]) j = (j + 1) & (ncap - 1);
+        nu[j] = 1; ns[j] = p->set[i];
+      }
+    free(p->set); free(p->used); p->set = ns; p->used = nu; p->cap = ncap;
+  }
+  size_t j = ig_h(s) & (p->cap - 1);
+  while (p->used[j]) j = (j + 1) & (p->cap - 1);
+  p->used[j] = 1; p->set[j] = s; p->n++;
+}
+/* advance_ack_base (:338-355): move past a run of consecutive known changes */
+static void ig_advance(ig_proxy* p) { while (ig_has(p, p->ack_base)) p->ack_base++; }
+/* should_ignore_change (:202-204) */
+static int ig_should_ignore(const ig_proxy* p, int64_t s) { return s < p->ack_base || ig_has(p, s); }
+/* received_changes_add (:207-224) */
+static void ig_received(ig_proxy* p, int64_t s) { ig_add(p, s); if (s == p->ack_base) ig_advance(p); }
+/* set_irrelevant_change (:226-239) */
+static void ig_irrelevant(ig_proxy* p, int64_t s) {
+  if (s >= p->ack_base) ig_add(p, s);
+  if (s == p->ack_base) ig_advance(p);
+}
+/* irrelevant_changes_range (:241-288) */
+static void ig_irrelevant_range(ig_proxy* p, int64_t from, int64_t until) {
+  if (from > until) return;  /* "negative range": error, nothing changes */
+  if (from <= p->ack_base) {
+    if (until > p->ack_base) { p->ack_base = until; ig_advance(p); }
+  } else {
+    for (int64_t s = from; s < until; ++s) ig_add(p, s);
+  }
+}
+
+static size_t ig_guid_h(const uint8_t g[16]) { return (size_t)fa_hash(g, 16); }
+rtps_oracle_ingest* rtps_oracle_ingest_new(const rtps_match* table, uint32_t n) {
+  rtps_oracle_ingest* h = (rtps_oracle_ingest*)calloc(1, sizeof(rtps_oracle_ingest));
+  h->n = n;
+  h->table = (rtps_match*)calloc(n ? n : 1, sizeof(rtps_match));
+  if (n) memcpy(h->table, table, n * sizeof(rtps_match));
+  h->p = (ig_proxy*)calloc(n ? n : 1, sizeof(ig_proxy));
+  for (uint32_t e = 0; e < n; ++e) h->p[e].ack_base = 1;
+  h->hcap = 16;
+  while (h->hcap < 2 * (size_t)n) h->hcap <<= 1;
+  h->hslot = (uint32_t*)calloc(h->hcap, sizeof(uint32_t));
+  for (uint32_t e = 0; e < n; ++e) {
+    size_t j = ig_guid_h(table[e].writer_guid) & (h->hcap - 1);
+    int dup = 0;
+    while (h->hslot[j]) {
+      if (!memcmp(h->table[h->hslot[j] - 1].writer_guid, table[e].writer_guid, 16)) { dup = 1; break; }
+      j = (j + 1) & (h->hcap - 1);
+    }
+    if (!dup) h->hslot[j] = e + 1;
+  }
+  return h;
+}
+void rtps_oracle_ingest_free(rtps_oracle_ingest* h) {
+  if (!h) return;
+  for (uint32_t e = 0; e < h->n; ++e) { free(h->p[e].set); free(h->p[e].used); }
+  free(h->p); free(h->table); free(h->hslot); free(h);
+}
+/* writer GUID -> entry index (first entry wins), or -1 */
+static int64_t ig_entry(const rtps_oracle_ingest* h, const uint8_t g[16]) {
+  for (size_t j = ig_guid_h(g) & (h->hcap - 1); h->hslot[j]; j = (j + 1) & (h->hcap - 1))
+    if (!memcmp(h->table[h->hslot[j] - 1].writer_guid, g, 16)) return (int64_t)h->hslot[j] - 1;
+  return -1;
+}
+
+/* One batch in record order (see rtps_rx_ingest in rtps_rx.h).  accept[m],
+ * accepted[m] (returns their count), ack_base[n] (optional). */
+uint64_t rtps_oracle_ingest_batch(rtps_oracle_ingest* h, const uint8_t* arena, const uint64_t* offs,
+                                  const rtps_record* recs, uint64_t m, const rtps_frag_sample* frag, uint64_t nf,
+                                  uint32_t flags, uint8_t* accept, uint32_t* accepted, int64_t* ack_base) {
+  uint32_t* fidx = (uint32_t*)malloc((m ? m : 1) * sizeof(uint32_t));
+  for (uint64_t i = 0; i < m; ++i) fidx[i] = 0xffffffffu;
+  for (uint64_t s = 0; s < nf; ++s)
+    if (frag[s].rec_idx < m) fidx[frag[s].rec_idx] = (uint32_t)s;
+  uint64_t na = 0;
+  for (uint64_t i = 0; i < m; ++i) {
+    const rtps_record* r = &recs[i];
+    accept[i] = 0;
+    const int routed = (r->route & RTPS_ROUTE_PASS) && (r->route & RTPS_ROUTE_MATCHED);
+    uint8_t g[16];
+    memcpy(g, r->prefix, 12);
+    memcpy(g + 12, r->writer_id, 4);
+    if (fidx[i] != 0xffffffffu) {  /* completed DataFrag sample (handle_datafrag_msg :614-626) */
+      const rtps_frag_sample* fs = &frag[fidx[i]];
+      int64_t e = ig_entry(h, fs->writer_guid);
+      if (fs->status != RTPS_FRAG_SHORT && e >= 0) {
+        ig_proxy* p = &h->p[e];
+        if (!ig_should_ignore(p, fs->sn)) { ig_received(p, fs->sn); accept[i] = 1; accepted[na++] = (uint32_t)i; }
+      }
+      continue;
+    }
+    if (!routed) continue;
+    int64_t e = ig_entry(h, g);
+    if (e < 0) continue;
+    ig_proxy* p = &h->p[e];
+    if (r->kind == RTPS_DATA) {
+      if (r->payload_kind != RTPS_PK_DATA && r->payload_kind != RTPS_PK_KEY && r->payload_kind != RTPS_PK_KEY_HASH)
+        continue;  /* data_to_dds_data failed: no process_received_data (reader.rs:552-558) */
+      if (!ig_should_ignore(p, r->sn)) { ig_received(p, r->sn); accept[i] = 1; accepted[na++] = (uint32_t)i; }
+    } else if (r->kind == RTPS_HEARTBEAT) {
+      if (flags & RTPS_INGEST_BEST_EFFORT) continue;
+      if (r->u.hb.count <= p->hb_count) continue;  /* already seen (reader.rs:902-905) */
+      p->hb_count = r->u.hb.count;
+      ig_irrelevant_range(p, 0, r->sn);            /* irrelevant_changes_up_to(first_sn) */
+    } else if (r->kind == RTPS_GAP) {
+      const int64_t start = r->sn, base = r->u.gap.list_base;
+      if (start <= 0 || base <= 0) continue;       /* validity (reader.rs:1087-1102) */
+      ig_irrelevant_range(p, start, base);
+      const uint8_t* bm = arena + offs[r->dgram_idx] + r->u.gap.bitmap_off;
+      const int le = r->flags & 1;
+      for (uint32_t b = 0; b < r->u.gap.num_bits; ++b) {  /* NumberSetIter (sequence_number.rs:543-557) */
+        const uint8_t* w = bm + 4 * (b / 32);
+        uint32_t word = le ? (uint32_t)w[0] | ((uint32_t)w[1] << 8) | ((uint32_t)w[2] << 16) | ((uint32_t)w[3] << 24)
+                           : ((uint32_t)w[0] << 24) | ((uint32_t)w[1] << 16) | ((uint32_t)w[2] << 8) | (uint32_t)w[3];
+        if (word & (1u << (31 - b % 32))) ig_irrelevant(p, base + (int64_t)b);
+      }
+    }
+  }
+  if (ack_base)
+    for (uint32_t e = 0; e < h->n; ++e) ack_base[e] = h->p[e].ack_base;
+  free(fidx);
+  return na;
+}

@@ -1,0 +1,595 @@
+// rtps_ingest.hip — history-cache ingest on the device.
+//
+// Replaces the stateful reader's per-writer bookkeeping that decides which
+// samples enter the history cache (RtpsWriterProxy, rtps/rtps_writer_proxy.rs;
+// Reader::handle_data_msg / handle_datafrag_msg / handle_heartbeat_msg /
+// handle_gap_msg, io_uring/rtps/reader.rs:514-1116; TopicCache::add_change's
+// duplicate check, structure/dds_cache.rs:210-262).  The reference applies the
+// submessages one by one; a whole parsed batch is decided at once here.
+//
+// Why the batch can be decided in parallel.  Call a sequence number s of a
+// writer "covered" once a DATA / completed DATA_FRAG with sn s has been
+// processed, a valid GAP listed s or had s in [gapStart, gapList.base), or an
+// accepted HEARTBEAT had firstSN > s.  The proxy's all_ackable_before
+// (ack_base) is then always the smallest s >= 1 that is not covered (every
+// transition of rtps_writer_proxy.rs:202-355 keeps that invariant), so
+// should_ignore_change(s) = s < ack_base || changes.contains(s) is exactly
+// "s < 1 or s covered by an earlier event".  Only HEARTBEAT acceptance is
+// order-dependent (count > every earlier accepted count, reader.rs:902-905,
+// i.e. a strict prefix maximum), and it needs per-writer order only among the
+// HEARTBEATs.  So:
+//   1 classify  lane per record: event kind, writer entry (match table), sn;
+//   2 heartbeats stable radix sort of the HEARTBEAT events by entry, scans by
+//               key: accepted = count > max(state count, earlier counts);
+//               running max of accepted firstSN (the coverage threshold);
+//   3 marks     lane per DATA / GAP: atomicMin(first covering record) over a
+//               per-writer window of RTPS_INGEST_WINDOW sequence numbers;
+//   4 decide    lane per sample: s >= 1, s >= ack_base, s >= threshold of the
+//               HEARTBEATs before it, not in the carried change set, and it is
+//               its sn's first covering event;
+//   5 select    accepted record indices (ascending);
+//   6 merge     the batch's coverage into the persistent change-set bitmap;
+//   7 state     workgroup per writer: new ack_base = first uncovered s from
+//               max(ack_base, threshold), window re-anchored there, count.
+// The CPU restatement the tests hold this to (oracle/, test-only) is the
+// reference's sequential algorithm, so tests/ check this derivation too.
+//
+// Roofline: HBM / L2-bound integer work (64-B record read + a few bytes of
+// state per event); no MFMA.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <string.h>
+
+#include <new>
+
+#include "rtps_ingest.h"
+
+namespace {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr uint32_t IT = 256;
+constexpr uint32_t NONE = 0xffffffffu;
+constexpr uint32_t W = RTPS_INGEST_WINDOW;  // sequence numbers tracked per writer
+constexpr uint32_t WW = W / 32;             // bitmap words per writer
+constexpr uint32_t ECAP_MAX = 1u << 14;     // writers (match-table entries)
+enum : uint8_t { EV_NONE = 0, EV_SAMPLE = 1, EV_HB = 2, EV_GAP = 3 };
+enum { C_OVF = 0, C_COUNT = 1 };
+
+__device__ __forceinline__ uint32_t guid_hash(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  uint32_t h = 0x811c9dc5u;  // the match table's hash (rtps_rx.hip)
+  h = (h ^ a) * 0x01000193u; h = (h ^ b) * 0x01000193u;
+  h = (h ^ c) * 0x01000193u; h = (h ^ d) * 0x01000193u;
+  return h ^ (h >> 15);
+}
+// writer GUID -> match-table entry (first entry wins), or NONE
+__device__ __forceinline__ uint32_t entry_of(const IngestTable& t, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  const u32x4* keys = reinterpret_cast<const u32x4*>(t.keys);
+  uint32_t i = guid_hash(a, b, c, d) & t.mask;
+  for (uint32_t probe = 0; probe <= t.mask; ++probe) {
+    if (t.slots[i] == RTPS_NO_MATCH) return NONE;
+    const u32x4 k = keys[i];
+    if (k[0] == a && k[1] == b && k[2] == c && k[3] == d) return t.index[i];
+    i = (i + 1u) & t.mask;
+  }
+  return NONE;
+}
+// atomicOr(addr, m) for the active lanes, lanes that hit the same word first
+// combined (sequential SNs of a writer share bitmap words: without this, 32
+// same-address atomics per word).  Every lane of the wave must call it.
+__device__ __forceinline__ void wave_or(uint32_t* addr, uint32_t m, bool active) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t a = (uint64_t)addr;
+  uint64_t todo = __ballot(active);
+  while (todo) {
+    const int leader = __builtin_ctzll(todo);
+    const uint64_t la = ((uint64_t)(uint32_t)__shfl((int)(a >> 32), leader, 64) << 32) |
+                        (uint32_t)__shfl((int)(uint32_t)a, leader, 64);
+    const bool mine = active && a == la;
+    uint32_t v = mine ? m : 0u;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v |= (uint32_t)__shfl_xor((int)v, d, 64);
+    if (lane == (uint32_t)leader) atomicOr(addr, v);
+    todo &= ~__ballot(mine);
+  }
+}
+// first-cover key of record i in batch `epoch`: no reset between batches is needed
+__device__ __forceinline__ unsigned long long ekey(uint32_t epoch, uint32_t i) {
+  return ((unsigned long long)(0xffffffffu - epoch) << 32) | i;
+}
+__device__ __forceinline__ uint32_t rd32(const uint8_t* p, bool le) {
+  const uint32_t x = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+  return le ? x : __builtin_bswap32(x);
+}
+
+struct Scratch {
+  uint8_t* evt;     // event kind per record
+  uint32_t* ent;    // writer entry per record
+  int64_t* esn;     // sample sn (DATA / completed DATA_FRAG)
+  uint32_t* fidx;   // completed DataFrag sample of a record, or NONE
+  uint32_t *hkey, *hval, *skey, *sval;  // HEARTBEAT sort
+  int32_t *hcnt, *hexcl;
+  int64_t *hf, *hpre;
+};
+struct State {
+  int64_t* base;    // all_ackable_before
+  int64_t* lo;      // first sequence number of the window (multiple of 32, <= base)
+  int32_t* hbc;     // received_heartbeat_count
+  uint32_t* bits;   // change set: bit (s - lo) of writer e at bits[e * WW + ...]
+  uint64_t* fc;     // first covering record of (e, s - lo): (~epoch << 32 | record); older epochs compare larger
+  uint32_t* dbits;  // this batch's samples, same layout as bits (cleared by k_merge)
+  uint32_t* seg_b;  // HEARTBEAT segment of each entry in sorted order
+  uint32_t* seg_e;
+  uint64_t* ctr;
+};
+
+// ---- 1 classify ----
+__global__ __launch_bounds__(IT) void k_fidx(const rtps_frag_sample* frag, const uint64_t* n_frag, uint64_t max_frag,
+                                             uint64_t max, uint32_t* fidx) {
+  const uint64_t nf = n_frag ? (*n_frag < max_frag ? *n_frag : max_frag) : 0;
+  for (uint64_t s = (uint64_t)blockIdx.x * IT + threadIdx.x; s < nf; s += (uint64_t)gridDim.x * IT)
+    if (frag[s].status != RTPS_FRAG_SHORT && frag[s].rec_idx < max) fidx[frag[s].rec_idx] = (uint32_t)s;
+}
+
+__global__ __launch_bounds__(IT) void k_classify(IngestTable t, const rtps_record* recs, const uint64_t* n_rec,
+                                                 uint64_t max, const rtps_frag_sample* frag, uint32_t flags,
+                                                 Scratch x, uint32_t sent) {
+  const uint64_t n = *n_rec < max ? *n_rec : max;
+  for (uint64_t i = (uint64_t)blockIdx.x * IT + threadIdx.x; i < max; i += (uint64_t)gridDim.x * IT) {
+    uint8_t ev = EV_NONE;
+    uint32_t e = NONE;
+    int64_t sn = 0;
+    if (i < n) {
+      const uint32_t f = x.fidx[i];
+      if (f != NONE) {  // completed DataFrag sample, processed at its completing record (reader.rs:614-626)
+        const uint32_t* g = reinterpret_cast<const uint32_t*>(frag[f].writer_guid);
+        e = entry_of(t, g[0], g[1], g[2], g[3]);
+        if (e != NONE) { ev = EV_SAMPLE; sn = frag[f].sn; }
+      } else {
+        const rtps_record r = recs[i];
+        if ((r.route & RTPS_ROUTE_PASS) && (r.route & RTPS_ROUTE_MATCHED)) {
+          const uint32_t* d = reinterpret_cast<const uint32_t*>(&r);
+          if (r.kind == RTPS_DATA) {
+            // data_to_dds_data must succeed (reader.rs:552-558)
+            if (r.payload_kind == RTPS_PK_DATA || r.payload_kind == RTPS_PK_KEY || r.payload_kind == RTPS_PK_KEY_HASH)
+              ev = EV_SAMPLE;
+          } else if (r.kind == RTPS_HEARTBEAT) {
+            if (!(flags & RTPS_INGEST_BEST_EFFORT)) ev = EV_HB;  // BestEffort: ignored (reader.rs:870-881)
+          } else if (r.kind == RTPS_GAP) {
+            if (r.sn > 0 && r.u.gap.list_base > 0) ev = EV_GAP;   // validity (reader.rs:1087-1102)
+          }
+          if (ev != EV_NONE) {
+            e = entry_of(t, d[2], d[3], d[4], d[5]);
+            if (e == NONE) ev = EV_NONE;
+            sn = r.sn;
+          }
+        }
+      }
+    }
+    x.evt[i] = ev;
+    x.ent[i] = e;
+    x.esn[i] = sn;
+    x.hkey[i] = ev == EV_HB ? e : sent;
+    x.hval[i] = (uint32_t)i;
+  }
+}
+
+// ---- 2 heartbeats ----
+__global__ __launch_bounds__(IT) void k_hvals(const rtps_record* recs, uint64_t max, Scratch x, State s, uint32_t sent) {
+  for (uint64_t q = (uint64_t)blockIdx.x * IT + threadIdx.x; q < max; q += (uint64_t)gridDim.x * IT) {
+    const uint32_t k = x.skey[q];
+    int32_t c = INT32_MIN;
+    if (k != sent) {
+      c = recs[x.sval[q]].u.hb.count;
+      if (q == 0 || x.skey[q - 1] != k) s.seg_b[k] = (uint32_t)q;
+      if (q + 1 == max || x.skey[q + 1] != k) s.seg_e[k] = (uint32_t)q + 1u;
+    }
+    x.hcnt[q] = c;
+  }
+}
+// accepted iff count > max(state count, every earlier count of the writer) (reader.rs:902-905);
+// an accepted HEARTBEAT covers [0, firstSN) (irrelevant_changes_up_to)
+__global__ __launch_bounds__(IT) void k_hacc(const rtps_record* recs, uint64_t max, Scratch x, State s, uint32_t sent) {
+  for (uint64_t q = (uint64_t)blockIdx.x * IT + threadIdx.x; q < max; q += (uint64_t)gridDim.x * IT) {
+    const uint32_t k = x.skey[q];
+    int64_t f = INT64_MIN;
+    if (k != sent) {
+      const int32_t before = x.hexcl[q] > s.hbc[k] ? x.hexcl[q] : s.hbc[k];
+      if (x.hcnt[q] > before) f = recs[x.sval[q]].sn;
+    }
+    x.hf[q] = f;
+  }
+}
+
+// ---- 3 marks ----
+// The sequence numbers a valid GAP covers, as (window word, bit mask) pairs:
+// irrelevant_changes_range(gapStart, gapList.base) (a negative range changes
+// nothing) and set_irrelevant_change per listed SN (NumberSetIter,
+// sequence_number.rs:543-557), clipped to the writer's window [lo, lo + W).
+template <typename F>
+__device__ __forceinline__ void gap_words(const rtps_record& r, const uint8_t* arena, const uint64_t* dgram_off,
+                                          int64_t lo, F&& f) {
+  const int64_t start = r.sn, base = r.u.gap.list_base;
+  if (start <= base) {
+    const int64_t a = (start > lo ? start : lo) - lo, b = (base < lo + (int64_t)W ? base : lo + (int64_t)W) - lo;
+    for (int64_t w = a >> 5; a < b && (w << 5) < b; ++w) {
+      const int64_t lb = a > (w << 5) ? a - (w << 5) : 0, hb = b < ((w + 1) << 5) ? b - (w << 5) : 32;
+      const uint32_t m = (uint32_t)((hb == 32 ? 0xffffffffull : ((1ull << hb) - 1ull)) & ~((1ull << lb) - 1ull));
+      if (m) f((uint64_t)w, m);
+    }
+  }
+  const uint8_t* bm = arena + dgram_off[r.dgram_idx] + r.u.gap.bitmap_off;
+  const bool le = (r.flags & 1u) != 0u;
+  for (uint32_t w = 0; w * 32u < r.u.gap.num_bits; ++w) {
+    uint32_t word = rd32(bm + 4u * w, le);
+    const uint32_t valid = r.u.gap.num_bits - w * 32u;
+    if (valid < 32u) word &= ~(0xffffffffu >> valid);
+    uint64_t src = __builtin_bitreverse32(word);  // bit j = SN base + 32 w + j
+    int64_t off = base + (int64_t)(w * 32u) - lo;
+    if (off < 0) { if (off <= -32) continue; src >>= (uint32_t)(-off); off = 0; }
+    if (!src || off >= (int64_t)W) continue;
+    const uint64_t sh = (uint64_t)off & 31u, dw = (uint64_t)off >> 5;
+    const uint64_t v2 = src << sh;
+    if ((uint32_t)v2) f(dw, (uint32_t)v2);
+    if ((uint32_t)(v2 >> 32) && dw + 1u < WW) f(dw + 1u, (uint32_t)(v2 >> 32));
+  }
+}
+
+// samples first: their sequence numbers (dbits) and first-cover keys
+__global__ __launch_bounds__(IT) void k_marks_d(const uint64_t* n_rec, uint64_t max, Scratch x, State s, uint32_t epoch) {
+  const uint64_t n = *n_rec < max ? *n_rec : max;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * IT; i0 < n; i0 += (uint64_t)gridDim.x * IT) {  // wave-uniform trip count
+    const uint64_t i = i0 + threadIdx.x;
+    bool act = i < n && x.evt[i] == EV_SAMPLE;
+    uint32_t* word = s.dbits;
+    uint32_t bit = 0;
+    if (act) {
+      const uint32_t e = x.ent[i];
+      const int64_t v = x.esn[i], lo = s.lo[e];
+      act = v >= lo && v < lo + (int64_t)W;
+      if (act) {
+        const uint64_t off = (uint64_t)(v - lo);
+        word = s.dbits + (uint64_t)e * WW + (off >> 5);
+        bit = 1u << (off & 31u);
+        atomicMin(reinterpret_cast<unsigned long long*>(s.fc + (uint64_t)e * W) + off, ekey(epoch, (uint32_t)i));
+      }
+    }
+    wave_or(word, bit, act);
+  }
+}
+// then GAPs: a GAP's first-cover key matters only where a sample of the batch
+// has the same sequence number, so only those are marked (32 at a time)
+__global__ __launch_bounds__(IT) void k_marks_g(const rtps_record* recs, const uint8_t* arena, const uint64_t* dgram_off,
+                                                const uint64_t* n_rec, uint64_t max, Scratch x, State s, uint32_t epoch) {
+  const uint64_t n = *n_rec < max ? *n_rec : max;
+  for (uint64_t i = (uint64_t)blockIdx.x * IT + threadIdx.x; i < n; i += (uint64_t)gridDim.x * IT) {
+    if (x.evt[i] != EV_GAP) continue;
+    const uint32_t e = x.ent[i];
+    const int64_t lo = s.lo[e];
+    const uint32_t* db = s.dbits + (uint64_t)e * WW;
+    unsigned long long* fc = reinterpret_cast<unsigned long long*>(s.fc + (uint64_t)e * W);
+    const unsigned long long key = ekey(epoch, (uint32_t)i);
+    auto mark_word = [&](uint64_t w, uint32_t m) {  // window word w, covered bits m
+      m &= db[w];
+      while (m) {
+        const uint32_t b = (uint32_t)__builtin_ctz(m);
+        m &= m - 1u;
+        atomicMin(fc + (w << 5) + b, key);
+      }
+    };
+    gap_words(recs[i], arena, dgram_off, lo, mark_word);
+  }
+}
+
+// ---- 4 decide ----
+__global__ __launch_bounds__(IT) void k_decide(const uint64_t* n_rec, uint64_t max, Scratch x, State s, uint8_t* accept,
+                                               bool reliable, uint32_t epoch) {
+  const uint64_t n = *n_rec < max ? *n_rec : max;
+  for (uint64_t i = (uint64_t)blockIdx.x * IT + threadIdx.x; i < max; i += (uint64_t)gridDim.x * IT) {
+    uint8_t acc = 0;
+    if (i < n && x.evt[i] == EV_SAMPLE) {
+      const uint32_t e = x.ent[i];
+      const int64_t v = x.esn[i], lo = s.lo[e];
+      int64_t thr = s.base[e];
+      const uint32_t sb = s.seg_b[e], se = s.seg_e[e];
+      // accepted HEARTBEATs of this writer before record i (only needed when the
+      // writer's final threshold is above v)
+      if (reliable && se > sb && x.hpre[se - 1u] > v && v >= thr) {
+        uint32_t a = sb, b = se;
+        while (a < b) {  // first sorted position whose record is >= i
+          const uint32_t m = (a + b) >> 1;
+          if (x.sval[m] < (uint32_t)i) a = m + 1u; else b = m;
+        }
+        if (a > sb && x.hpre[a - 1u] > thr) thr = x.hpre[a - 1u];
+      }
+      if (v >= 1 && v >= thr) {
+        if (v >= lo + (int64_t)W) {  // beyond the tracked window: accepted unchecked
+          acc = 1;
+          atomicAdd(reinterpret_cast<unsigned long long*>(s.ctr + C_OVF), 1ull);
+        } else {
+          const uint64_t off = (uint64_t)(v - lo);
+          const bool known = (s.bits[(uint64_t)e * WW + (off >> 5)] >> (off & 31u)) & 1u;
+          acc = (!known && s.fc[(uint64_t)e * W + off] == ekey(epoch, (uint32_t)i)) ? 1 : 0;
+        }
+      }
+    }
+    accept[i] = acc;
+  }
+}
+
+// ---- 6 merge ----
+__global__ __launch_bounds__(IT) void k_merge(const rtps_record* recs, const uint8_t* arena, const uint64_t* dgram_off,
+                                              const uint64_t* n_rec, uint64_t max, Scratch x, State s) {
+  const uint64_t n = *n_rec < max ? *n_rec : max;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * IT; i0 < n; i0 += (uint64_t)gridDim.x * IT) {  // wave-uniform trip count
+    const uint64_t i = i0 + threadIdx.x;
+    const uint8_t ev = i < n ? x.evt[i] : EV_NONE;
+    const uint32_t e = (ev == EV_SAMPLE || ev == EV_GAP) ? x.ent[i] : 0u;
+    const int64_t lo = (ev == EV_SAMPLE || ev == EV_GAP) ? s.lo[e] : 0;
+    uint32_t* bits = s.bits + (uint64_t)e * WW;
+    bool act = false;
+    uint32_t* word = s.bits;
+    uint32_t bit = 0;
+    if (ev == EV_SAMPLE) {
+      const int64_t v = x.esn[i];
+      if (v >= lo && v < lo + (int64_t)W) {
+        const uint64_t w = (uint64_t)(v - lo) >> 5;
+        act = true;
+        word = bits + w;
+        bit = 1u << ((v - lo) & 31);
+        s.dbits[(uint64_t)e * WW + w] = 0u;  // every mark of the batch is done (k_marks_g read them)
+      }
+    } else if (ev == EV_GAP) {
+      gap_words(recs[i], arena, dgram_off, lo, [&](uint64_t w, uint32_t m) { atomicOr(bits + w, m); });
+    }
+    wave_or(word, bit, act);
+  }
+}
+
+// ---- 7 state: one workgroup per writer ----
+__global__ __launch_bounds__(IT) void k_state(uint32_t n_entries, Scratch x, State s, bool reliable, int64_t* ack_out) {
+  __shared__ uint32_t sh[WW];
+  __shared__ uint32_t s_first;
+  const uint32_t e = blockIdx.x, tid = threadIdx.x;
+  if (e >= n_entries) return;
+  const int64_t lo = s.lo[e];
+  int64_t thr = s.base[e];
+  int32_t hbc = s.hbc[e];
+  const uint32_t b0 = s.seg_b[e], b1 = s.seg_e[e];
+  if (reliable && b1 > b0) {
+    const int64_t f = x.hpre[b1 - 1u];
+    if (f > thr) thr = f;
+    const int32_t c = x.hexcl[b1 - 1u] > x.hcnt[b1 - 1u] ? x.hexcl[b1 - 1u] : x.hcnt[b1 - 1u];
+    if (c > hbc) hbc = c;
+  }
+  uint32_t* bits = s.bits + (uint64_t)e * WW;
+  // advance_ack_base: the first sequence number >= thr outside the change set
+  int64_t nb = thr;
+  if (thr < lo + (int64_t)W) {
+    const uint32_t off0 = (uint32_t)(thr - lo);
+    if (tid == 0) s_first = NONE;
+    __syncthreads();
+    for (uint32_t w0 = off0 >> 5; w0 < WW; w0 += IT) {
+      const uint32_t w = w0 + tid;
+      if (w < WW) {
+        uint32_t word = bits[w];
+        if (w == (off0 >> 5)) word |= (1u << (off0 & 31u)) - 1u;  // below thr: covered
+        if (word != 0xffffffffu) atomicMin(&s_first, w * 32u + (uint32_t)__builtin_ctz(~word));
+      }
+      __syncthreads();
+      if (s_first != NONE) break;
+      __syncthreads();
+    }
+    nb = lo + (int64_t)(s_first != NONE ? s_first : W);
+  }
+  // re-anchor the window at the new ack_base (bits below it are no longer needed)
+  const int64_t nlo = nb & ~(int64_t)31;
+  if (nlo != lo) {
+    const uint64_t shift = (uint64_t)(nlo - lo) >> 5;
+    for (uint32_t w = tid; w < WW; w += IT) sh[w] = (w + shift < WW) ? bits[w + shift] : 0u;
+    __syncthreads();
+    for (uint32_t w = tid; w < WW; w += IT) bits[w] = sh[w];
+  }
+  if (tid == 0) {
+    s.base[e] = nb;
+    s.lo[e] = nlo;
+    s.hbc[e] = hbc;
+    if (ack_out) ack_out[e] = nb;
+  }
+}
+
+__global__ void k_init_state(uint32_t n, State s) {
+  for (uint32_t e = blockIdx.x * IT + threadIdx.x; e < n; e += gridDim.x * IT) {
+    s.base[e] = 1;  // RtpsWriterProxy::new: ack_base = SequenceNumber::new(1)
+    s.lo[e] = 0;
+    s.hbc[e] = 0;
+  }
+}
+__global__ void k_finish(const uint64_t* ctr, uint64_t* ovf) { if (ovf) *ovf = ctr[C_OVF]; }
+
+static inline uint64_t hmin(uint64_t a, uint64_t b) { return a < b ? a : b; }
+
+}  // namespace
+
+struct IngestState {
+  int device = 0;
+  uint32_t ecap = 0;  // entries with state
+  State st{};
+  uint64_t cap = 0;   // records of the scratch
+  Scratch x{};
+  void* tmp = nullptr;
+  size_t tmp_bytes = 0;
+  uint32_t epoch = 0;  // batches since the first-cover table was last cleared
+};
+
+static uint64_t* S_fc(IngestState* s) { return s->st.fc; }
+static void free_state(IngestState* s) {
+  void* p[] = {s->st.base, s->st.lo, s->st.hbc, s->st.bits, s->st.fc, s->st.dbits, s->st.seg_b, s->st.seg_e};
+  for (void* q : p) if (q) (void)hipFree(q);
+  uint64_t* ctr = s->st.ctr;
+  s->st = State{};
+  s->st.ctr = ctr;
+  s->ecap = 0;
+}
+static void free_scratch(IngestState* s) {
+  void* p[] = {s->x.evt, s->x.ent, s->x.esn, s->x.fidx, s->x.hkey, s->x.hval, s->x.skey, s->x.sval, s->x.hcnt,
+               s->x.hexcl, s->x.hf, s->x.hpre, s->tmp};
+  for (void* q : p) if (q) (void)hipFree(q);
+  s->x = Scratch{};
+  s->tmp = nullptr;
+  s->tmp_bytes = 0;
+  s->cap = 0;
+}
+
+// per-entry state for n entries; existing entries keep theirs
+static bool grow_state(IngestState* s, uint32_t n, hipStream_t st) {
+  if (n <= s->ecap) return true;
+  uint32_t ncap = s->ecap ? s->ecap : 16;
+  while (ncap < n) ncap <<= 1;
+  (void)hipStreamSynchronize(st);
+  State o = s->st;
+  State m{};
+  m.ctr = o.ctr;
+  bool ok = hipMalloc(&m.base, ncap * 8ull) == hipSuccess && hipMalloc(&m.lo, ncap * 8ull) == hipSuccess &&
+            hipMalloc(&m.hbc, ncap * 4ull) == hipSuccess && hipMalloc(&m.bits, (uint64_t)ncap * WW * 4) == hipSuccess &&
+            hipMalloc(&m.fc, (uint64_t)ncap * W * 8) == hipSuccess && hipMalloc(&m.seg_b, ncap * 4ull) == hipSuccess &&
+            hipMalloc(&m.dbits, (uint64_t)ncap * WW * 4) == hipSuccess &&
+            hipMalloc(&m.seg_e, ncap * 4ull) == hipSuccess;
+  ok = ok && hipMemsetAsync(m.bits, 0, (uint64_t)ncap * WW * 4, st) == hipSuccess &&
+       hipMemsetAsync(m.dbits, 0, (uint64_t)ncap * WW * 4, st) == hipSuccess &&
+       hipMemsetAsync(m.fc, 0xff, (uint64_t)ncap * W * 8, st) == hipSuccess;
+  if (ok) hipLaunchKernelGGL(k_init_state, dim3((ncap + IT - 1) / IT), dim3(IT), 0, st, ncap, m);
+  if (ok && s->ecap) {  // carry the existing writers' state
+    const uint64_t e = s->ecap;
+    ok = hipMemcpyAsync(m.base, o.base, e * 8, hipMemcpyDeviceToDevice, st) == hipSuccess &&
+         hipMemcpyAsync(m.lo, o.lo, e * 8, hipMemcpyDeviceToDevice, st) == hipSuccess &&
+         hipMemcpyAsync(m.hbc, o.hbc, e * 4, hipMemcpyDeviceToDevice, st) == hipSuccess &&
+         hipMemcpyAsync(m.bits, o.bits, e * WW * 4, hipMemcpyDeviceToDevice, st) == hipSuccess;
+  }
+  ok = ok && hipStreamSynchronize(st) == hipSuccess;
+  s->st = m;
+  const uint32_t old_cap = s->ecap;
+  s->ecap = ncap;
+  State dead = o;
+  dead.ctr = nullptr;
+  void* p[] = {dead.base, dead.lo, dead.hbc, dead.bits, dead.fc, dead.dbits, dead.seg_b, dead.seg_e};
+  for (void* q : p) if (q) (void)hipFree(q);
+  (void)old_cap;
+  if (!ok) { free_state(s); return false; }
+  return true;
+}
+
+static bool grow_scratch(IngestState* s, uint64_t max, hipStream_t st) {
+  if (max <= s->cap) return true;
+  (void)hipStreamSynchronize(st);
+  free_scratch(s);
+  const uint64_t n = max;
+  Scratch& x = s->x;
+  bool ok = hipMalloc(&x.evt, n) == hipSuccess && hipMalloc(&x.ent, n * 4) == hipSuccess &&
+            hipMalloc(&x.esn, n * 8) == hipSuccess && hipMalloc(&x.fidx, n * 4) == hipSuccess &&
+            hipMalloc(&x.hkey, n * 4) == hipSuccess && hipMalloc(&x.hval, n * 4) == hipSuccess &&
+            hipMalloc(&x.skey, n * 4) == hipSuccess && hipMalloc(&x.sval, n * 4) == hipSuccess &&
+            hipMalloc(&x.hcnt, n * 4) == hipSuccess && hipMalloc(&x.hexcl, n * 4) == hipSuccess &&
+            hipMalloc(&x.hf, n * 8) == hipSuccess && hipMalloc(&x.hpre, n * 8) == hipSuccess;
+  size_t b1 = 0, b2 = 0, b3 = 0, b4 = 0;
+  ok = ok && hipcub::DeviceRadixSort::SortPairs(nullptr, b1, x.hkey, x.skey, x.hval, x.sval, (int)n, 0, 32, st) == hipSuccess;
+  ok = ok && hipcub::DeviceScan::ExclusiveScanByKey(nullptr, b2, x.skey, x.hcnt, x.hexcl, hipcub::Max(), INT32_MIN,
+                                                    (uint32_t)n, hipcub::Equality(), st) == hipSuccess;
+  ok = ok && hipcub::DeviceScan::InclusiveScanByKey(nullptr, b3, x.skey, x.hf, x.hpre, hipcub::Max(), (uint32_t)n,
+                                                    hipcub::Equality(), st) == hipSuccess;
+  ok = ok && hipcub::DeviceSelect::Flagged(nullptr, b4, hipcub::CountingInputIterator<uint32_t>(0), (uint8_t*)nullptr,
+                                           (uint32_t*)nullptr, (uint64_t*)nullptr, (int64_t)n, st) == hipSuccess;
+  size_t tb = b1;
+  if (b2 > tb) tb = b2;
+  if (b3 > tb) tb = b3;
+  if (b4 > tb) tb = b4;
+  s->tmp_bytes = tb;
+  ok = ok && hipMalloc(&s->tmp, tb) == hipSuccess;
+  if (!ok) { free_scratch(s); return false; }
+  s->cap = n;
+  return true;
+}
+
+IngestState* rtps_ingest_state_new(int device) {
+  IngestState* s = new (std::nothrow) IngestState();
+  if (!s) return nullptr;
+  s->device = device;
+  if (hipMalloc(&s->st.ctr, C_COUNT * 8) != hipSuccess) { delete s; return nullptr; }
+  return s;
+}
+
+void rtps_ingest_state_free(IngestState* s) {
+  if (!s) return;
+  free_scratch(s);
+  free_state(s);
+  if (s->st.ctr) (void)hipFree(s->st.ctr);
+  delete s;
+}
+
+int rtps_ingest_state_reset(IngestState* s, hipStream_t st) {
+  if (!s->ecap) return RTPS_RX_OK;
+  bool ok = hipMemsetAsync(s->st.bits, 0, (uint64_t)s->ecap * WW * 4, st) == hipSuccess &&  // fc: epoch-tagged
+            hipMemsetAsync(s->st.dbits, 0, (uint64_t)s->ecap * WW * 4, st) == hipSuccess;
+  if (ok) hipLaunchKernelGGL(k_init_state, dim3((s->ecap + IT - 1) / IT), dim3(IT), 0, st, s->ecap, s->st);
+  return ok && hipGetLastError() == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP;
+}
+
+int rtps_ingest_batch(IngestState* s, hipStream_t st, const IngestTable& t, const uint8_t* arena, uint64_t arena_len,
+                      const uint64_t* dgram_off, const rtps_record* records, const uint64_t* n_records,
+                      uint64_t max_records, const rtps_frag_sample* frag, const uint64_t* n_frag, uint64_t max_frag,
+                      uint32_t flags, const rtps_ingest_out* out) {
+  (void)arena_len;
+  if (t.n_entries > ECAP_MAX) return RTPS_RX_ETOOBIG;
+  if (max_records > 0x7fffffffull) return RTPS_RX_ETOOBIG;
+  if (!grow_state(s, t.n_entries ? t.n_entries : 1, st)) return RTPS_RX_ENOMEM;
+  const uint64_t max = max_records ? max_records : 1;
+  if (!grow_scratch(s, max, st)) return RTPS_RX_ENOMEM;
+  const bool reliable = !(flags & RTPS_INGEST_BEST_EFFORT);
+  if (++s->epoch == 0xffffffffu) {  // keys would wrap: clear the first-cover table
+    if (hipMemsetAsync(S_fc(s), 0xff, (uint64_t)s->ecap * W * 8, st) != hipSuccess) return RTPS_RX_EHIP;
+    s->epoch = 1;
+  }
+  uint32_t ebits = 1;
+  while ((1u << ebits) <= t.n_entries) ++ebits;  // entries < sent = 2^ebits - 1
+  const uint32_t sent = (1u << ebits) - 1u;
+  const uint32_t gb = (uint32_t)hmin((max + IT - 1) / IT, 8192);
+  Scratch& x = s->x;
+  State& S = s->st;
+  bool ok = hipMemsetAsync(S.ctr, 0, C_COUNT * 8, st) == hipSuccess &&
+            hipMemsetAsync(x.fidx, 0xff, max * 4, st) == hipSuccess &&
+            hipMemsetAsync(S.seg_b, 0, (uint64_t)s->ecap * 4, st) == hipSuccess &&
+            hipMemsetAsync(S.seg_e, 0, (uint64_t)s->ecap * 4, st) == hipSuccess;
+  if (!ok) return RTPS_RX_EHIP;
+  if (frag && n_frag && max_frag)
+    hipLaunchKernelGGL(k_fidx, dim3((uint32_t)hmin((max_frag + IT - 1) / IT, 4096)), dim3(IT), 0, st, frag, n_frag,
+                       max_frag, max, x.fidx);
+  hipLaunchKernelGGL(k_classify, dim3(gb), dim3(IT), 0, st, t, records, n_records, max, frag, flags, x, sent);
+  if (reliable) {
+    size_t tb = s->tmp_bytes;
+    if (hipcub::DeviceRadixSort::SortPairs(s->tmp, tb, x.hkey, x.skey, x.hval, x.sval, (int)max, 0, (int)ebits, st) !=
+        hipSuccess)
+      return RTPS_RX_EHIP;
+    hipLaunchKernelGGL(k_hvals, dim3(gb), dim3(IT), 0, st, records, max, x, S, sent);
+    tb = s->tmp_bytes;
+    if (hipcub::DeviceScan::ExclusiveScanByKey(s->tmp, tb, x.skey, x.hcnt, x.hexcl, hipcub::Max(), INT32_MIN,
+                                               (uint32_t)max, hipcub::Equality(), st) != hipSuccess)
+      return RTPS_RX_EHIP;
+    hipLaunchKernelGGL(k_hacc, dim3(gb), dim3(IT), 0, st, records, max, x, S, sent);
+    tb = s->tmp_bytes;
+    if (hipcub::DeviceScan::InclusiveScanByKey(s->tmp, tb, x.skey, x.hf, x.hpre, hipcub::Max(), (uint32_t)max,
+                                               hipcub::Equality(), st) != hipSuccess)
+      return RTPS_RX_EHIP;
+  }
+  hipLaunchKernelGGL(k_marks_d, dim3(gb), dim3(IT), 0, st, n_records, max, x, S, s->epoch);
+  hipLaunchKernelGGL(k_marks_g, dim3(gb), dim3(IT), 0, st, records, arena, dgram_off, n_records, max, x, S, s->epoch);
+  hipLaunchKernelGGL(k_decide, dim3(gb), dim3(IT), 0, st, n_records, max, x, S, out->accept, reliable, s->epoch);
+  size_t tb = s->tmp_bytes;
+  if (hipcub::DeviceSelect::Flagged(s->tmp, tb, hipcub::CountingInputIterator<uint32_t>(0), out->accept,
+                                    out->accepted, out->n_accepted, (int64_t)max, st) != hipSuccess)
+    return RTPS_RX_EHIP;
+  hipLaunchKernelGGL(k_merge, dim3(gb), dim3(IT), 0, st, records, arena, dgram_off, n_records, max, x, S);
+  if (t.n_entries)
+    hipLaunchKernelGGL(k_state, dim3(t.n_entries), dim3(IT), 0, st, t.n_entries, x, S, reliable, out->ack_base);
+  hipLaunchKernelGGL(k_finish, dim3(1), dim3(1), 0, st, S.ctr, out->n_window_overflow);
+  return hipGetLastError() == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP;
+}

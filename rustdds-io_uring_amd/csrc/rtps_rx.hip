@@ -36,6 +36,7 @@
 #include "rtps_gen.h"
 #include "rtps_cdr.h"
 #include "rtps_frag.h"
+#include "rtps_ingest.h"
 
 namespace {
 
@@ -1022,6 +1023,8 @@ struct rtps_rx_ctx {
   uint32_t launch_parity = 0;
   uint32_t k_spec = 1;  // speculated records per datagram (0 disables nothing: see set_spec_hint)
   FragState* frag = nullptr;  // DataFrag reassembly state (created on first use)
+  IngestState* ingest = nullptr;  // history-cache ingest state (created on first use)
+  uint32_t mt_n = 0;              // match-table entries
 };
 
 static int hip_fail(hipError_t e) { return e == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP; }
@@ -1069,6 +1072,7 @@ int rtps_rx_destroy(rtps_rx_ctx* c) {
   (void)hipFree(c->mt_index);
   (void)hipFree(c->bucket_hist);
   rtps_frag_state_free(c->frag);
+  rtps_ingest_state_free(c->ingest);
   (void)hipStreamDestroy(c->own_stream);
   delete c;
   return RTPS_RX_OK;
@@ -1091,7 +1095,7 @@ static uint32_t host_guid_hash(const uint8_t g[16]) {
 int rtps_rx_set_match_table(rtps_rx_ctx* c, const rtps_match* t, uint32_t n) {
   if (!c || (n && !t)) return RTPS_RX_EINVAL;
   (void)hipSetDevice(c->device);
-  if (n == 0) { c->mt_active = false; return RTPS_RX_OK; }
+  if (n == 0) { c->mt_active = false; c->mt_n = 0; return RTPS_RX_OK; }
   uint32_t cap = 16;
   while (cap < 2u * n) cap <<= 1;
   std::vector<u32x4> keys(cap, u32x4{0u, 0u, 0u, 0u});
@@ -1130,6 +1134,7 @@ int rtps_rx_set_match_table(rtps_rx_ctx* c, const rtps_match* t, uint32_t n) {
   if (hipMemcpy(c->mt_index, index.data(), cap * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) return RTPS_RX_EHIP;
   c->mt_active = true;
   c->mt_cap = cap;
+  c->mt_n = n;
   return RTPS_RX_OK;
 }
 
@@ -1329,6 +1334,33 @@ int rtps_rx_frag_reset(rtps_rx_ctx* c) {
   if (!c->frag) return RTPS_RX_OK;
   (void)hipSetDevice(c->device);
   return rtps_frag_state_reset(c->frag, c->stream);
+}
+
+/* history-cache ingest (rtps_ingest.hip) */
+int rtps_rx_ingest(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len, const uint64_t* dgram_off,
+                   const rtps_record* records, const uint64_t* n_records, uint64_t max_records,
+                   const rtps_frag_sample* frag, const uint64_t* n_frag, uint64_t max_frag, uint32_t flags,
+                   const rtps_ingest_out* out) {
+  if (!c || !records || !n_records || !out || !out->accept || !out->accepted || !out->n_accepted) return RTPS_RX_EINVAL;
+  if (!c->mt_active || c->mt_n == 0) return RTPS_RX_EINVAL;
+  if (max_records && (!arena || !dgram_off)) return RTPS_RX_EINVAL;
+  if (flags & ~RTPS_INGEST_BEST_EFFORT) return RTPS_RX_EINVAL;
+  if (frag && (!n_frag || !max_frag)) return RTPS_RX_EINVAL;
+  (void)hipSetDevice(c->device);
+  if (!c->ingest) {
+    c->ingest = rtps_ingest_state_new(c->device);
+    if (!c->ingest) return RTPS_RX_ENOMEM;
+  }
+  IngestTable t{c->mt_keys, c->mt_slots, c->mt_index, c->mt_cap - 1, c->mt_n};
+  return rtps_ingest_batch(c->ingest, c->stream, t, arena, arena_len, dgram_off, records, n_records, max_records,
+                           frag, n_frag, max_frag, flags, out);
+}
+
+int rtps_rx_ingest_reset(rtps_rx_ctx* c) {
+  if (!c) return RTPS_RX_EINVAL;
+  if (!c->ingest) return RTPS_RX_OK;
+  (void)hipSetDevice(c->device);
+  return rtps_ingest_state_reset(c->ingest, c->stream);
 }
 
 uint32_t rtps_rx_record_size(void) { return (uint32_t)sizeof(rtps_record); }

@@ -46,6 +46,15 @@ class _FragOut(ctypes.Structure):
                 ("n_pending", ctypes.c_void_p)]
 
 
+class _IngestOut(ctypes.Structure):
+    _fields_ = [("accept", ctypes.c_void_p), ("accepted", ctypes.c_void_p), ("n_accepted", ctypes.c_void_p),
+                ("ack_base", ctypes.c_void_p), ("n_window_overflow", ctypes.c_void_p)]
+
+
+INGEST_BEST_EFFORT = 0x1
+INGEST_WINDOW = 1 << 17
+
+
 class _Out(ctypes.Structure):
     _fields_ = [("status", ctypes.c_void_p), ("records", ctypes.c_void_p), ("max_records", ctypes.c_uint64),
                 ("match", ctypes.c_void_p), ("rec_begin", ctypes.c_void_p), ("n_records", ctypes.c_void_p)]
@@ -55,7 +64,7 @@ EXPORTS = ["rtps_rx_create", "rtps_rx_destroy", "rtps_rx_set_stream", "rtps_rx_s
            "rtps_rx_parse_batch", "rtps_rx_sync", "rtps_rx_strerror", "rtps_rx_max_records_host",
            "rtps_rx_generate", "rtps_rx_bucket_by_writer", "rtps_rx_set_spec_hint", "rtps_rx_cdr_decode",
            "rtps_rx_bucket_by_writer_padded", "rtps_rx_frag_assemble", "rtps_rx_frag_reset",
-           "rtps_rx_bucket_descriptors"]
+           "rtps_rx_bucket_descriptors", "rtps_rx_ingest", "rtps_rx_ingest_reset"]
 
 
 def lib():
@@ -90,6 +99,10 @@ def lib():
         L.rtps_rx_frag_assemble.restype = I
         L.rtps_rx_frag_reset.argtypes = [P]
         L.rtps_rx_frag_reset.restype = I
+        L.rtps_rx_ingest.argtypes = [P, P, U64, P, P, P, U64, P, P, U64, U32, ctypes.POINTER(_IngestOut)]
+        L.rtps_rx_ingest.restype = I
+        L.rtps_rx_ingest_reset.argtypes = [P]
+        L.rtps_rx_ingest_reset.restype = I
         L.rtps_rx_set_spec_hint.argtypes = [P, U32]
         L.rtps_rx_set_spec_hint.restype = I
         L.rtps_rx_cdr_decode.argtypes = [P, P, U32, U32, P, U64, P, P, P, U64, P, P]
@@ -325,6 +338,72 @@ class MessageReceiver:
         samples = fouts["samples"][:min(ns, ms)].cpu().numpy().reshape(-1).view(FRAG_SAMPLE_DTYPE)
         heap = fouts["heap"][:min(used, hb)].cpu().numpy()
         return res, samples, heap, ns, used, int(fouts["n_pending"].item())
+
+    # ---- history-cache ingest (writer-proxy state persists in the context) ----
+    def alloc_ingest_outputs(self, max_recs, n_entries):
+        import torch
+        dev = torch.device("cuda", self.device)
+        return {"accept": torch.empty(max(max_recs, 1), dtype=torch.uint8, device=dev),
+                "accepted": torch.empty(max(max_recs, 1), dtype=torch.int32, device=dev),
+                "n_accepted": torch.zeros(1, dtype=torch.int64, device=dev),
+                "ack_base": torch.zeros(max(n_entries, 1), dtype=torch.int64, device=dev),
+                "n_window_overflow": torch.zeros(1, dtype=torch.int64, device=dev)}
+
+    def ingest(self, arena, off, outs, iouts, fouts=None, best_effort=False):
+        """Decide which samples of a parsed batch enter the history cache (the
+        stateful reader's writer proxies, Reader::handle_data_msg / _heartbeat_ /
+        _gap_); fouts: frag_assemble outputs of the same batch.  Asynchronous."""
+        o = iouts.get("_c")
+        if o is None:
+            o = _IngestOut()
+            o.accept = iouts["accept"].data_ptr()
+            o.accepted = iouts["accepted"].data_ptr()
+            o.n_accepted = iouts["n_accepted"].data_ptr()
+            o.ack_base = iouts["ack_base"].data_ptr()
+            o.n_window_overflow = iouts["n_window_overflow"].data_ptr()
+            iouts["_c"] = o
+        frag = fouts["samples"].data_ptr() if fouts is not None else None
+        nfrag = fouts["n_samples"].data_ptr() if fouts is not None else None
+        mfrag = fouts["max_samples"] if fouts is not None else 0
+        _check(lib().rtps_rx_ingest(self._h, arena.data_ptr(), arena.numel(), off.data_ptr(),
+                                    outs["records"].data_ptr(), outs["n_records"].data_ptr(), outs["max_records"],
+                                    frag, nfrag, mfrag, INGEST_BEST_EFFORT if best_effort else 0, ctypes.byref(o)))
+
+    def ingest_reset(self):
+        _check(lib().rtps_rx_ingest_reset(self._h))
+
+    def ingest_batch(self, arena_np, off_np, len_np, n_entries, frag=False, best_effort=False):
+        """Parse (+ reassemble) + ingest host arrays -> (BatchResult, accept u8[m], accepted u32[k],
+        ack_base i64[n_entries], n_window_overflow, frag samples or None)."""
+        import torch
+        n = len(len_np)
+        dev = torch.device("cuda", self.device)
+        arena = torch.from_numpy(np.ascontiguousarray(arena_np, dtype=np.uint8)).to(dev)
+        off = torch.from_numpy(np.ascontiguousarray(off_np, dtype=np.uint64).view(np.int64)).to(dev)
+        lens = torch.from_numpy(np.ascontiguousarray(len_np, dtype=np.uint32).view(np.int32)).to(dev)
+        cap = max_records(len_np)
+        outs = self.alloc_outputs(n, cap)
+        iouts = self.alloc_ingest_outputs(cap, n_entries)
+        fouts = self.alloc_frag_outputs(cap, int(arena.numel()) + 16 * cap + (1 << 20)) if frag else None
+        torch.cuda.synchronize(dev)
+        self.parse_batch_device(arena, off, lens, n, outs)
+        if frag:
+            self.frag_assemble(arena, off, outs, fouts)
+        self.ingest(arena, off, outs, iouts, fouts, best_effort=best_effort)
+        self.sync()
+        total = int(outs["n_records"].item())
+        kept = min(total, cap)
+        recs = outs["records"][:kept].cpu().numpy().reshape(-1).view(RECORD_DTYPE)
+        match = outs["match"][:kept].cpu().numpy().view(np.uint16)
+        res = BatchResult(outs["status"][:n].cpu().numpy(), recs, match,
+                          outs["rec_begin"][:n].cpu().numpy().view(np.uint32), total)
+        na = int(iouts["n_accepted"].item())
+        samples = None
+        if frag:
+            ns = min(int(fouts["n_samples"].item()), cap)
+            samples = fouts["samples"][:ns].cpu().numpy().reshape(-1).view(FRAG_SAMPLE_DTYPE)
+        return (res, iouts["accept"][:kept].cpu().numpy(), iouts["accepted"][:na].cpu().numpy().view(np.uint32),
+                iouts["ack_base"][:n_entries].cpu().numpy(), int(iouts["n_window_overflow"].item()), samples)
 
     # ---- convenience: host datagrams in, host results out ----
     def handle_received_batch(self, arena_np, off_np, len_np):

@@ -1,0 +1,231 @@
+"""Test-side history-cache ingest helpers: datagram builders for DATA /
+HEARTBEAT / GAP traffic and an independent pure-Python model of the
+reference's stateful-reader bookkeeping, used to check the C oracle
+(oracle/rtps_oracle.c rtps_oracle_ingest_batch).
+
+The model transcribes RtpsWriterProxy (rtps/rtps_writer_proxy.rs:17-355) with
+its `changes` BTreeMap kept as a dict that is pruned exactly like the
+reference prunes it (split_off / append in irrelevant_changes_range), driven as
+Reader::handle_data_msg / handle_datafrag_msg / handle_heartbeat_msg /
+handle_gap_msg drive it (io_uring/rtps/reader.rs:514-1116) for the records the
+receiver passes (ROUTE_PASS) from matched writers (ROUTE_MATCHED).
+"""
+import struct
+
+import numpy as np
+
+from rtps_rx.records import DATA, HEARTBEAT, GAP, ROUTE_PASS, ROUTE_MATCHED, PK_DATA, PK_KEY, PK_KEY_HASH
+
+RTPS_HDR = b"RTPS\x02\x04\x01\x0f"
+ZERO_EID = b"\x00\x00\x00\x00"
+
+
+def _sn(e, sn):
+    return struct.pack(e + "iI", sn >> 32, sn & 0xFFFFFFFF)
+
+
+def data_sub(writer_key, sn, le=True, payload=b"\x00\x01\x00\x00abcd", key=False, both=False, key_hash=None):
+    """DATA (data.rs:57-144): D (or K) payload, or a KEY_HASH-only DATA (no payload)."""
+    e = "<" if le else ">"
+    flags = 1 if le else 0
+    qos = b""
+    if key_hash is not None:
+        flags |= 0x02
+        qos = struct.pack(e + "HH", 0x70, 16) + bytes(key_hash) + struct.pack(e + "HH", 1, 0)
+        payload = b""
+    elif both:
+        flags |= 0x0C
+    else:
+        flags |= 0x08 if key else 0x04
+    body = struct.pack(e + "HH", 0, 16) + ZERO_EID + writer_key + _sn(e, sn) + qos + bytes(payload)
+    return bytes([0x15, flags]) + struct.pack(e + "H", len(body)) + body
+
+
+def hb_sub(writer_key, first, last, count, le=True):
+    e = "<" if le else ">"
+    body = ZERO_EID + writer_key + _sn(e, first) + _sn(e, last) + struct.pack(e + "i", count)
+    return bytes([0x07, (1 if le else 0) | 2]) + struct.pack(e + "H", len(body)) + body
+
+
+def gap_sub(writer_key, start, base, bits, le=True):
+    """GAP (gap.rs:23-46): gapStart, gapList = (base, numBits, bitmap MSB-first)."""
+    e = "<" if le else ">"
+    nb = len(bits)
+    words = [0] * ((nb + 31) // 32)
+    for i, b in enumerate(bits):
+        if b:
+            words[i // 32] |= 1 << (31 - i % 32)
+    body = ZERO_EID + writer_key + _sn(e, start) + _sn(e, base) + struct.pack(e + "I", nb)
+    body += b"".join(struct.pack(e + "I", w) for w in words)
+    return bytes([0x08, 1 if le else 0]) + struct.pack(e + "H", len(body)) + body
+
+
+def info_dst_sub(prefix, le=True):
+    e = "<" if le else ">"
+    return bytes([0x0E, 1 if le else 0]) + struct.pack(e + "H", 12) + bytes(prefix)
+
+
+def datagram(prefix, subs):
+    return RTPS_HDR + bytes(prefix) + b"".join(subs)
+
+
+class Proxy:
+    """RtpsWriterProxy: ack_base, changes {sn: received?}, received_heartbeat_count."""
+
+    def __init__(self):
+        self.ack_base = 1
+        self.changes = {}
+        self.hb_count = 0
+
+    def should_ignore(self, s):  # :202-204
+        return s < self.ack_base or s in self.changes
+
+    def advance(self):  # :338-355
+        test = self.ack_base
+        for sn in sorted(k for k in self.changes if k >= self.ack_base):
+            if sn != test:
+                break
+            test += 1
+            self.ack_base = test
+
+    def received_add(self, s):  # :207-224
+        self.changes[s] = True
+        if s == self.ack_base:
+            self.advance()
+
+    def set_irrelevant(self, s):  # :226-239
+        if s >= self.ack_base:
+            self.changes[s] = None
+        if s == self.ack_base:
+            self.advance()
+
+    def irrelevant_range(self, frm, until):  # :241-288
+        if frm > until:
+            return
+        if frm <= self.ack_base:
+            for k in [k for k in self.changes if frm <= k < until]:
+                del self.changes[k]
+            if until > self.ack_base:
+                self.ack_base = until
+                self.advance()
+        else:
+            for s in range(frm, until):
+                self.changes[s] = None
+
+
+class IngestRef:
+    """Sequential model over the records of successive batches."""
+
+    def __init__(self, table_guids):
+        self.entry = {}
+        for i, g in enumerate(table_guids):
+            self.entry.setdefault(bytes(g), i)
+        self.proxies = [Proxy() for _ in table_guids]
+
+    def batch(self, arena, offs, recs, frag_samples=(), best_effort=False):
+        at = {int(s["rec_idx"]): s for s in frag_samples}
+        accepted = []
+        for i, r in enumerate(recs):
+            if i in at:
+                s = at[i]
+                e = self.entry.get(bytes(s["writer_guid"]))
+                if int(s["status"]) != 1 and e is not None:
+                    p = self.proxies[e]
+                    if not p.should_ignore(int(s["sn"])):
+                        p.received_add(int(s["sn"]))
+                        accepted.append(i)
+                continue
+            route = int(r["route"])
+            if not (route & ROUTE_PASS and route & ROUTE_MATCHED):
+                continue
+            e = self.entry.get(bytes(r["prefix"]) + bytes(r["writer_id"]))
+            if e is None:
+                continue
+            p = self.proxies[e]
+            kind, sn = int(r["kind"]), int(r["sn"])
+            u = r["u"].tobytes()
+            if kind == DATA:
+                if int(r["payload_kind"]) not in (PK_DATA, PK_KEY, PK_KEY_HASH):
+                    continue
+                if not p.should_ignore(sn):
+                    p.received_add(sn)
+                    accepted.append(i)
+            elif kind == HEARTBEAT and not best_effort:
+                count = struct.unpack_from("<i", u, 8)[0]
+                if count <= p.hb_count:
+                    continue
+                p.hb_count = count
+                p.irrelevant_range(0, sn)
+            elif kind == GAP:
+                base, nb, boff = struct.unpack_from("<qIH", u, 0)
+                if sn <= 0 or base <= 0:
+                    continue
+                p.irrelevant_range(sn, base)
+                bm = int(offs[int(r["dgram_idx"])]) + boff
+                le = int(r["flags"]) & 1
+                for b in range(nb):
+                    w = bytes(arena[bm + 4 * (b // 32):bm + 4 * (b // 32) + 4])
+                    word = struct.unpack("<I" if le else ">I", w)[0]
+                    if word & (1 << (31 - b % 32)):
+                        p.set_irrelevant(base + b)
+        return accepted, [p.ack_base for p in self.proxies]
+
+
+PREFIXES = [bytes([0xA0 + k] * 12) for k in range(4)]
+OWN = bytes([0x01, 0x03, 0x00, 0x0c, 0x29, 0x2d, 0x31, 0xa2, 0x28, 0x20, 0x02, 0x08])
+
+
+def writer_key(k):
+    return bytes([0, 0, 1 + k, 0x02])
+
+
+def table(n_prefix=3, n_writer=3):
+    """Match table: writers (prefix p, key k) for p < n_prefix, k < n_writer, reader slot = p*n_writer+k.
+    One duplicate entry (first wins) and one unmatched writer (prefix 3) stay out of the table."""
+    from rtps_rx.records import pack_match_table
+    ents = [(PREFIXES[p] + writer_key(k), p * n_writer + k) for p in range(n_prefix) for k in range(n_writer)]
+    ents.append((PREFIXES[0] + writer_key(0), 77))
+    return pack_match_table(ents), [g for g, _ in ents]
+
+
+def stream(n, seed, sn_hi=60, n_prefix=4, n_writer=3):
+    """n datagrams of reliable-reader traffic with every case the proxies have to
+    replay in order: duplicate and out-of-order DATA, KEY and KEY_HASH samples,
+    DATA whose payload decision fails, HEARTBEATs with stale counts and any
+    firstSN (<= 0 too), valid and invalid GAPs with ranges and bitmaps, big- and
+    little-endian submessages, writers outside the match table, and writer
+    submessages after an INFO_DST to another participant (not passed)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        p = int(rng.integers(n_prefix))
+        subs = []
+        if rng.random() < 0.05:
+            subs.append(info_dst_sub(bytes([7] * 12)))
+        for _ in range(int(rng.integers(1, 4))):
+            k = int(rng.integers(n_writer))
+            le = bool(rng.random() < 0.8)
+            x = rng.random()
+            wk = writer_key(k)
+            if x < 0.55:
+                sn = int(rng.integers(-1, sn_hi))
+                y = rng.random()
+                if y < 0.08:
+                    subs.append(data_sub(wk, sn, le, key=True))
+                elif y < 0.12:
+                    subs.append(data_sub(wk, sn, le, both=True))
+                elif y < 0.16:
+                    subs.append(data_sub(wk, sn, le, key_hash=bytes(range(16))))
+                else:
+                    subs.append(data_sub(wk, sn, le))
+            elif x < 0.75:
+                first = int(rng.integers(-2, sn_hi))
+                subs.append(hb_sub(wk, first, first + int(rng.integers(0, 20)), int(rng.integers(-1, 12)), le))
+            else:
+                start = int(rng.integers(-1, sn_hi))
+                base = start + int(rng.integers(-3, 8))
+                nb = int(rng.integers(0, 70))
+                bits = [bool(b) for b in rng.random(nb) < 0.4]
+                subs.append(gap_sub(wk, start, base, bits, le))
+        out.append(datagram(PREFIXES[p], subs))
+    return out

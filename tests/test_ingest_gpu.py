@@ -1,0 +1,173 @@
+"""GPU parity of the history-cache ingest (rtps_rx_ingest) with the CPU
+oracle's sequential writer-proxy restatement: every accept flag, the accepted
+record list and every writer's all_ackable_before, batch after batch (state
+carried in the context), on random reliable / best-effort corpora, completed
+DataFrag samples, the C3 and T workloads at full size, and the edges (window
+overflow, empty batches, reset, a growing match table)."""
+import numpy as np
+import pytest
+
+import frag_ref
+import ingest_ref as R
+import oracle
+from rtps_rx.records import pack_match_table, DATA_FRAG
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture()
+def rx():
+    import rtps_rx
+    r = rtps_rx.MessageReceiver(oracle.OWN_PREFIX, max_datagrams=1 << 21)
+    yield r
+    r.close()
+
+
+def _batch(rx, ing, tbl, dgrams, label, frag=False, fa=None, best_effort=False, align=4):
+    arena, off, ln = oracle.pack(dgrams, align=align)
+    res, acc, accepted, ack, ovf, samples = rx.ingest_batch(arena, off, ln, len(tbl), frag=frag,
+                                                            best_effort=best_effort)
+    st, recs, _, _ = oracle.parse(arena, off, ln, match_table=tbl, threads=8)
+    assert res.records.tobytes() == recs.tobytes(), f"{label}: parse differs"
+    o_samples = fa.batch(arena, off, recs)[0] if frag else None
+    o_acc, o_accepted, o_ack = ing.batch(arena, off, recs, o_samples, best_effort=best_effort)
+    assert np.array_equal(acc, o_acc), f"{label}: accept flags differ at {np.nonzero(acc != o_acc)[0][:10]}"
+    assert np.array_equal(accepted, o_accepted), f"{label}: accepted list"
+    assert np.array_equal(ack, o_ack), f"{label}: ack_base {ack[ack != o_ack][:5]} vs {o_ack[ack != o_ack][:5]}"
+    assert ovf == 0
+    return acc, accepted, ack
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+@pytest.mark.parametrize("best_effort", [False, True])
+def test_stream_across_batches(rx, seed, best_effort):
+    tbl, _ = R.table()
+    rx.set_match_table(tbl)
+    ing = oracle.HistoryIngest(tbl)
+    dgrams = R.stream(6000, seed)
+    total = 0
+    for a, b in [(0, 1), (1, 2000), (2000, 2001), (2001, 6000)]:
+        _, accepted, _ = _batch(rx, ing, tbl, dgrams[a:b], f"seed {seed} {a}:{b}", best_effort=best_effort)
+        total += len(accepted)
+    assert total > 20
+
+
+def test_dense_duplicates_wide_sn(rx):
+    tbl, _ = R.table()
+    rx.set_match_table(tbl)
+    ing = oracle.HistoryIngest(tbl)
+    for k, hi in enumerate([5, 300, 5000]):
+        _batch(rx, ing, tbl, R.stream(4000, 40 + k, sn_hi=hi), f"sn_hi {hi}", align=1)
+
+
+def test_completed_datafrag_samples(rx):
+    dgrams = frag_ref.soup(3000, 7)
+    arena, off, ln = oracle.pack(dgrams, align=4)
+    _, recs0, _, _ = oracle.parse(arena, off, ln)
+    guids = sorted({bytes(r["prefix"]) + bytes(r["writer_id"]) for r in recs0[recs0["kind"] == DATA_FRAG]})
+    tbl = pack_match_table([(g, i) for i, g in enumerate(guids[:-1])])
+    rx.set_match_table(tbl)
+    ing = oracle.HistoryIngest(tbl)
+    fa = oracle.FragAssembler()
+    n = 0
+    for a, b in [(0, 1000), (1000, 3000)]:
+        _, accepted, _ = _batch(rx, ing, tbl, dgrams[a:b], f"frag {a}:{b}", frag=True, fa=fa)
+        n += len(accepted)
+    assert n > 10
+
+
+def test_window_overflow_counted(rx):
+    tbl = pack_match_table([(R.PREFIXES[0] + R.writer_key(0), 0)])
+    rx.set_match_table(tbl)
+    import rtps_rx
+    w = R.writer_key(0)
+    far = 1 + rtps_rx.INGEST_WINDOW + 5
+    d = [R.datagram(R.PREFIXES[0], [R.data_sub(w, 1), R.data_sub(w, far), R.data_sub(w, 2)])]
+    arena, off, ln = oracle.pack(d)
+    _, acc, accepted, ack, ovf, _ = rx.ingest_batch(arena, off, ln, 1)
+    assert accepted.tolist() == [0, 1, 2] and ovf == 1 and ack.tolist() == [3]
+
+
+def test_empty_and_eventless_batches(rx):
+    tbl, _ = R.table()
+    rx.set_match_table(tbl)
+    ing = oracle.HistoryIngest(tbl)
+    _batch(rx, ing, tbl, [], "empty")
+    _batch(rx, ing, tbl, [R.datagram(R.PREFIXES[3], [R.data_sub(R.writer_key(0), 1)])], "unmatched only")
+    _batch(rx, ing, tbl, R.stream(500, 9), "after empty")
+
+
+def test_reset_and_growing_table(rx):
+    tbl, guids = R.table(n_prefix=2, n_writer=2)
+    rx.set_match_table(tbl)
+    ing = oracle.HistoryIngest(tbl)
+    dgrams = R.stream(3000, 21)
+    _batch(rx, ing, tbl, dgrams[:1000], "small table")
+    # append writers: existing entries keep their proxies (oracle: same, by entry position)
+    big, _ = R.table(n_prefix=4, n_writer=3)
+    order = [bytes(g) for g in tbl["writer_guid"]]
+    extra = [e for e in big if bytes(e["writer_guid"]) not in order]
+    tbl2 = np.concatenate([tbl, np.array(extra, dtype=tbl.dtype)])
+    rx.set_match_table(tbl2)
+    ing2 = oracle.HistoryIngest(tbl2)
+    ing2_warm = _replay(ing2, tbl2, dgrams[:1000])
+    _batch(rx, ing2_warm, tbl2, dgrams[1000:3000], "grown table")
+    rx.ingest_reset()
+    _batch(rx, oracle.HistoryIngest(tbl2), tbl2, dgrams[:1000], "after reset")
+
+
+def _replay(ing, tbl, dgrams):
+    """oracle state equivalent to the device's after `dgrams` were ingested with the first table:
+    the entries present then got the same events (later entries were unmatched: no events)."""
+    arena, off, ln = oracle.pack(dgrams, align=4)
+    first = tbl[:len(R.table(n_prefix=2, n_writer=2)[0])]
+    _, recs, _, _ = oracle.parse(arena, off, ln, match_table=first)
+    ing.batch(arena, off, recs)
+    return ing
+
+
+def _device_batch(rx, wl, n):
+    import rtps_rx
+    off, ln, size = rtps_rx.gen_layout(wl, n)
+    dev = torch.device("cuda", 0)
+    arena = torch.zeros(size, dtype=torch.uint8, device=dev)
+    off_t = torch.from_numpy(off.view(np.int64)).to(dev)
+    ln_t = torch.from_numpy(ln.view(np.int32)).to(dev)
+    rx.generate(wl, arena, off_t, ln_t, n)
+    rx.sync()
+    return arena, off_t, ln_t, off, ln
+
+
+@pytest.mark.parametrize("wl,n", [(3, 20000), (3, 1 << 20), (1, 1 << 20)])
+def test_workload_parity(rx, wl, n):
+    import rtps_rx
+    arena, off_t, ln_t, off, ln = _device_batch(rx, wl, n)
+    host = arena.cpu().numpy()
+    st, recs0, _, _ = oracle.parse(host, off, ln, threads=16)
+    wk = np.isin(recs0["kind"], (0x15, 0x07, 0x08))
+    guids = sorted({bytes(r["prefix"]) + bytes(r["writer_id"]) for r in recs0[wk]})
+    tbl = pack_match_table([(g, i) for i, g in enumerate(guids)])
+    rx.set_match_table(tbl)
+    cap = rtps_rx.max_records(ln)
+    outs = rx.alloc_outputs(n, cap)
+    iouts = rx.alloc_ingest_outputs(cap, len(tbl))
+    ing = oracle.HistoryIngest(tbl)
+    _, recs, _, _ = oracle.parse(host, off, ln, match_table=tbl, threads=16)
+    for rep in range(2):  # the second pass sees every sample again: all duplicates
+        rx.parse_batch_device(arena, off_t, ln_t, n, outs)
+        rx.ingest(arena, off_t, outs, iouts)
+        rx.sync()
+        m = int(outs["n_records"].item())
+        assert m == len(recs)
+        o_acc, o_accepted, o_ack = ing.batch(host, off, recs)
+        acc = iouts["accept"][:m].cpu().numpy()
+        na = int(iouts["n_accepted"].item())
+        assert np.array_equal(acc, o_acc), f"wl {wl} rep {rep}: accept"
+        assert np.array_equal(iouts["accepted"][:na].cpu().numpy().view(np.uint32), o_accepted)
+        assert np.array_equal(iouts["ack_base"][:len(tbl)].cpu().numpy(), o_ack)
+        assert int(iouts["n_window_overflow"].item()) == 0
+        if rep == 1:
+            assert na == 0
+        elif wl == 1:
+            assert na == n
