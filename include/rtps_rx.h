@@ -410,6 +410,55 @@ int rtps_rx_ingest(rtps_rx_ctx* ctx, const uint8_t* arena, uint64_t arena_len, c
 /* Forget every writer proxy's state (all_ackable_before = 1, empty change set, count 0). */
 int rtps_rx_ingest_reset(rtps_rx_ctx* ctx);
 
+/* ---- UDP batch receive into a datagram arena -----
+ * Replaces the receive side of the reference: a UDPListener per locator with
+ * an io_uring RecvMulti (multishot recv) on a provided-buffer ring of
+ * 128 x 64 KiB (io_uring/network/udp_listener.rs:7-27, 101-209), whose
+ * completions Domain::handle_event copies out one at a time
+ * (io_uring/rtps/dp_event_loop.rs:190-211: Bytes::copy_from_slice, then
+ * handle_received_packet_2).  Here the provided buffers are the slots of a
+ * caller-owned arena (pinned host memory that the GPU parses zero-copy, or
+ * copies to HBM): the kernel writes each datagram straight into its slot and
+ * a batch is a list of (arena offset, length) pairs ready for
+ * rtps_rx_parse_batch, with no per-datagram copy.  A batch's slots stay out
+ * of the receive pool until released.  Backend: io_uring multishot recv on a
+ * registered buffer ring (IORING_REGISTER_PBUF_RING); where io_uring is not
+ * available (seccomp, old kernel) the same slots are filled with recvmmsg.
+ * Host-side code: no GPU is involved. */
+#define RTPS_UDP_REUSE 0x1u          /* SO_REUSEADDR + SO_REUSEPORT (udp_listener.rs:41-51)      */
+#define RTPS_UDP_FORCE_RECVMMSG 0x2u /* do not try io_uring                                      */
+enum rtps_udp_backend { RTPS_UDP_IO_URING = 1, RTPS_UDP_RECVMMSG = 2 };
+typedef struct rtps_udp_config {
+  uint32_t abi_version;      /* RTPS_RX_ABI_VERSION */
+  uint32_t ipv4_addr;        /* bind address, host byte order (0 = INADDR_ANY) */
+  uint16_t port;             /* 0 = ephemeral (rtps_udp_port) */
+  uint16_t flags;            /* RTPS_UDP_* */
+  uint32_t multicast_group;  /* host byte order, 0 = none (joined on INADDR_ANY) */
+  uint8_t* arena;            /* caller memory of slot_bytes * n_slots bytes */
+  uint32_t slot_bytes;       /* bytes per datagram slot: multiple of 16, 32..65536 */
+  uint32_t n_slots;          /* power of two, 2..32768 */
+  uint32_t rcvbuf_bytes;     /* SO_RCVBUF request, 0 = system default */
+} rtps_udp_config;
+typedef struct rtps_udp_rx rtps_udp_rx;
+int rtps_udp_open(const rtps_udp_config* cfg, rtps_udp_rx** out);
+int rtps_udp_close(rtps_udp_rx* rx);
+int rtps_udp_port(const rtps_udp_rx* rx);     /* bound UDP port */
+int rtps_udp_backend(const rtps_udp_rx* rx);  /* rtps_udp_backend */
+/* Take up to max_n received datagrams, waiting up to timeout_ms for the first
+ * (-1: forever, 0: poll).  off / len: host arrays of max_n, filled in arrival
+ * order with arena offsets (slot * slot_bytes) and lengths.  Returns the count
+ * (>= 0) or a negative RTPS_RX_* code.  *truncated (optional) += datagrams
+ * longer than slot_bytes, which are dropped. */
+int rtps_udp_recv_batch(rtps_udp_rx* rx, uint64_t* off, uint32_t* len, uint32_t max_n, int timeout_ms,
+                        uint64_t* truncated);
+/* Give the slots of n datagrams of a batch (their offsets) back to the receive pool. */
+int rtps_udp_release(rtps_udp_rx* rx, const uint64_t* off, uint32_t n);
+/* Loopback publisher side for tests and the C1 plumbing bench: sendmmsg of n
+ * datagrams arena[off[i] .. off[i]+len[i]) to ipv4_addr:port (host order).
+ * Returns datagrams sent or a negative RTPS_RX_* code. */
+int rtps_udp_send_batch(uint32_t ipv4_addr, uint16_t port, const uint8_t* arena, const uint64_t* off,
+                        const uint32_t* len, uint32_t n);
+
 /* Upper bound on records for datagram lengths (host arrays): sum((len-20)/4). */
 uint64_t rtps_rx_max_records_host(const uint32_t* dgram_len, uint32_t n);
 

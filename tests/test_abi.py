@@ -13,7 +13,7 @@ LIB = os.path.join(REPO, "rustdds-io_uring_amd", "librtps_rx.so")
 
 def declared_functions():
     text = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|uint64_t|const char\*)\s+(rtps_rx_\w+)\s*\(", text, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|uint64_t|const char\*)\s+(rtps_(?:rx|udp)_\w+)\s*\(", text, re.M)))
 
 
 def test_header_declares_api():
