@@ -224,6 +224,160 @@ def ingest_leg(rx, arena, off_t, outs, n_rec, recs, n_entries, stream, steps):
             "frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
 
+HELLO_PREFIX = bytes([0x01, 0x0f, 0x99, 0x06, 0x78, 0x34, 0x00, 0x00, 0x01, 0x00, 0x00, 0x00])
+HELLO_WRITER = bytes([0x00, 0x00, 0x01, 0x02])
+
+
+def hello_world_datagrams(n):
+    """C1 traffic: what examples/io_uring_hello_world_publisher.rs writes (HelloWorldData
+    {user_id: i32, message: String}, :13-16, written at :162), as 64-byte serialized samples:
+    RTPS header + INFO_TS + one DATA per datagram (120 B), one writer, SN 1..n."""
+    L = 120
+    t = bytearray(L)
+    t[0:20] = b"RTPS\x02\x04\x01\x0f" + HELLO_PREFIX
+    t[20:24] = bytes([0x09, 0x01, 8, 0])                       # INFO_TS, LE, 8 bytes
+    t[32:36] = bytes([0x15, 0x05, 84, 0])                      # DATA, LE + D, 20 + 64 bytes
+    t[36:40] = bytes([0, 0, 16, 0])                            # extraFlags, octetsToInlineQos
+    t[44:48] = HELLO_WRITER                                    # readerId UNKNOWN (40:44), writerId
+    t[56:60] = bytes([0x00, 0x01, 0x00, 0x00])                 # CDR_LE encapsulation
+    t[64:68] = (52).to_bytes(4, "little")                      # string length incl. NUL
+    t[68:119] = b"Hello World! ".ljust(51, b".")
+    a = np.tile(np.frombuffer(bytes(t), dtype=np.uint8), (n, 1))
+    i = np.arange(n, dtype=np.int64)
+    a[:, 24:28] = (1_700_000_000 + i // 1000).astype("<u4").view(np.uint8).reshape(n, 4)
+    a[:, 28:32] = ((i % 1000) * 4294967).astype("<u4").view(np.uint8).reshape(n, 4)
+    sn = i + 1
+    a[:, 48:52] = (sn >> 32).astype("<i4").view(np.uint8).reshape(n, 4)
+    a[:, 52:56] = (sn & 0xFFFFFFFF).astype("<u4").view(np.uint8).reshape(n, 4)
+    a[:, 60:64] = (i % 1000).astype("<i4").view(np.uint8).reshape(n, 4)   # user_id
+    digits = np.char.zfill((i % 10**8).astype(str), 8).astype("S8")
+    a[:, 81:89] = np.frombuffer(digits.tobytes(), dtype=np.uint8).reshape(n, 8)
+    return a.reshape(-1), (np.arange(n, dtype=np.uint64) * L), np.full(n, L, dtype=np.uint32)
+
+
+def c1_loopback(dev, stream, n=200_000, batch=16384):
+    """Config C1 (BASELINE.json configs[0]): hello-world publisher -> subscriber over UDP
+    loopback, 64-B samples.  Publisher: sendmmsg on a thread, flow-controlled to two batches
+    in flight (an unthrottled loopback sender outruns any receiver: what gets through is then
+    set by the socket buffer, not by the pipeline).  Subscriber: the io_uring
+    receive (rtps_udp_*) lands datagrams in slots of a pinned arena (a receive thread keeps
+    draining), and each batch is parsed in place by the GPU (zero-copy), ingested into the
+    history cache and CDR-decoded.  Loopback and the kernel bound the rate; dropped
+    datagrams (socket buffer overruns) are reported, never hidden."""
+    import queue
+    import threading
+    from rtps_rx import udp, cdr
+    hello_t = cdr.CdrType([("user_id", "i32"), ("message", cdr.String(60))])
+    data, off, ln = hello_world_datagrams(n)
+    slot, nslot = 256, 32768
+    arena = torch.zeros(slot * nslot, dtype=torch.uint8, pin_memory=True)
+    rxu = udp.UdpReceiver(arena, slot_bytes=slot, rcvbuf_bytes=64 << 20)
+    rx = rtps_rx.MessageReceiver(OWN_PREFIX, device=dev.index, max_datagrams=batch)
+    rx.set_stream(stream)
+    tbl = np.zeros(1, dtype=MATCH_DTYPE)
+    tbl["writer_guid"][0] = np.frombuffer(HELLO_PREFIX + HELLO_WRITER, dtype=np.uint8)
+    rx.set_match_table(tbl)
+    cap = batch * 2
+    outs = rx.alloc_outputs(batch, cap)
+    iouts = rx.alloc_ingest_outputs(cap, 1)
+    rows, row_status = rx.alloc_rows(hello_t, cap)
+    h_off = torch.empty(batch, dtype=torch.int64, pin_memory=True)
+    h_ln = torch.empty(batch, dtype=torch.int32, pin_memory=True)
+    got_q, rel_q = queue.Queue(), queue.Queue()
+    done = threading.Event()
+
+    def receiver():
+        while True:
+            while not rel_q.empty():
+                rxu.release(rel_q.get())
+            o, m = rxu.recv_batch(batch, timeout_ms=5)
+            if len(o):
+                got_q.put((o.copy(), m.copy()))
+            elif done.is_set():
+                got_q.put(None)
+                return
+
+    sent = [0]
+    processed = [0]
+    window = 2 * batch  # flow control: at most two batches in flight (slots and socket buffer hold them)
+
+    def sender():
+        chunk = 4096
+        for a in range(0, n, chunk):
+            while sent[0] - processed[0] > window:
+                time.sleep(0.0002)
+            b = min(n, a + chunk)
+            sent[0] += udp.send_batch("127.0.0.1", rxu.port, data, off[a:b], ln[a:b])
+
+    tr = threading.Thread(target=receiver)
+    ts = threading.Thread(target=sender)
+    t0 = time.perf_counter()
+    tr.start()
+    ts.start()
+    received = accepted = decoded = 0
+    gpu_s = 0.0
+    pend_o, pend_l = [], []
+    finished = False
+    idle_since = None
+    t_last = t0
+    while not finished:
+        try:
+            item = got_q.get(timeout=0.05)
+        except queue.Empty:
+            item = "idle"
+        if item is None:
+            finished = True
+        elif item != "idle":
+            pend_o.append(item[0])
+            pend_l.append(item[1])
+            idle_since = None
+            t_last = time.perf_counter()
+        elif not ts.is_alive():
+            idle_since = idle_since or time.perf_counter()
+            if time.perf_counter() - idle_since > 0.3:
+                done.set()
+        k = sum(len(x) for x in pend_o)
+        while k and (k >= batch // 2 or item == "idle" or finished):
+            allo, alll = np.concatenate(pend_o), np.concatenate(pend_l)
+            o, m = allo[:batch], alll[:batch]  # the rest stays pending for the next GPU batch
+            pend_o, pend_l = ([allo[batch:]], [alll[batch:]]) if len(allo) > batch else ([], [])
+            k -= len(o)
+            c = len(o)
+            h_off[:c].copy_(torch.from_numpy(o.view(np.int64)))
+            h_ln[:c].copy_(torch.from_numpy(m.view(np.int32)))
+            g0 = time.perf_counter()
+            rx.parse_batch_device(arena, h_off, h_ln, c, outs)
+            rx.ingest(arena, h_off, outs, iouts)
+            rx.cdr_decode(hello_t, arena, h_off, outs, rows, row_status)
+            rx.sync()
+            gpu_s += time.perf_counter() - g0
+            nr = int(outs["n_records"].item())
+            accepted += int(iouts["n_accepted"].item())
+            decoded += int((row_status[:nr] == cdr.CDR_OK).sum().item())
+            received += c
+            processed[0] = received
+            rel_q.put(o)
+    wall = time.perf_counter() - t0
+    busy = t_last - t0  # first send .. last datagram handed over (excludes the end-of-stream wait)
+    tr.join()
+    ts.join()
+    rxu.close()
+    rx.close()
+    # the CPU reference parse of the same datagrams (oracle, one thread), for scale
+    import oracle
+    c0 = time.perf_counter()
+    oracle.parse(data, off, ln, threads=1)
+    cpu_s = time.perf_counter() - c0
+    return {"config": "C1: hello-world publisher -> subscriber over UDP loopback, 64-B HelloWorldData samples",
+            "receive_backend": {udp.IO_URING: "io_uring", udp.IO_URING_SQPOLL: "io_uring+sqpoll",
+                                udp.RECVMMSG: "recvmmsg"}[rxu.backend],
+            "datagrams_built": n, "datagrams_sent": sent[0], "datagrams_received": received,
+            "dropped": sent[0] - received,
+            "samples_accepted": accepted, "samples_decoded": decoded, "wall_s": wall, "stream_s": busy,
+            "datagrams_per_s": received / busy, "gpu_busy_s": gpu_s,
+            "cpu_reference_parse_per_s_1_thread": n / cpu_s}
+
+
 def cpu_baseline(workload, n, target_cpu_s=10.0, match_table=None):
     """The oracle (C restatement of the reference parse) on this host's cores, with the
     same match table as the device run."""
@@ -260,6 +414,7 @@ def main():
     ap.add_argument("--no-cdr", action="store_true", help="skip the CDR decode (a18) measurement")
     ap.add_argument("--no-frag", action="store_true", help="skip the DataFrag reassembly measurement (C4)")
     ap.add_argument("--no-ingest", action="store_true", help="skip the history-cache ingest measurement")
+    ap.add_argument("--no-c1", action="store_true", help="skip the C1 UDP-loopback pipeline measurement")
     ap.add_argument("--match", default="writers", choices=["writers", "none"],
                     help="match table: every writer of the workload (a reader subscribed to all of them) or none")
     ap.add_argument("--exchange", default="descriptors", choices=["descriptors", "records"],
@@ -436,6 +591,8 @@ def main():
         result["frag_assemble"] = frag_leg(rx, arena, off_t, outs, n_rec, recs, stream, args.steps)
     if world == 1 and not args.no_ingest and n_matched_writers:
         result["ingest"] = ingest_leg(rx, arena, off_t, outs, n_rec, recs, n_matched_writers, stream, args.steps)
+    if world == 1 and not args.no_c1:
+        result["c1_loopback"] = c1_loopback(dev, stream)
     if world == 1 and not args.no_e2e:
         result["end_to_end"] = end_to_end(rx, arena, off_t, ln_t, n, outs, n_rec, stream)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

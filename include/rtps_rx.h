@@ -427,7 +427,10 @@ int rtps_rx_ingest_reset(rtps_rx_ctx* ctx);
  * Host-side code: no GPU is involved. */
 #define RTPS_UDP_REUSE 0x1u          /* SO_REUSEADDR + SO_REUSEPORT (udp_listener.rs:41-51)      */
 #define RTPS_UDP_FORCE_RECVMMSG 0x2u /* do not try io_uring                                      */
-enum rtps_udp_backend { RTPS_UDP_IO_URING = 1, RTPS_UDP_RECVMMSG = 2 };
+#define RTPS_UDP_SQPOLL 0x4u         /* io_uring with a kernel poll thread (IORING_SETUP_SQPOLL): the
+                                       kernel keeps landing datagrams in slots while the host is busy;
+                                       falls back to a plain ring where it is refused              */
+enum rtps_udp_backend { RTPS_UDP_IO_URING = 1, RTPS_UDP_RECVMMSG = 2, RTPS_UDP_IO_URING_SQPOLL = 3 };
 typedef struct rtps_udp_config {
   uint32_t abi_version;      /* RTPS_RX_ABI_VERSION */
   uint32_t ipv4_addr;        /* bind address, host byte order (0 = INADDR_ANY) */

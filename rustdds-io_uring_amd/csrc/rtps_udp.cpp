@@ -91,6 +91,8 @@ struct rtps_udp_rx {
   size_t br_len = 0;
   uint16_t br_tail = 0;
   bool armed = false;
+  bool sqpoll = false;              // a kernel thread issues the recv and runs its completions
+  unsigned* sq_flags = nullptr;
   uint32_t provided = 0;            // slots currently owned by the kernel
   // recvmmsg
   std::vector<uint32_t> free_slots;
@@ -133,18 +135,31 @@ static int ring_arm(rtps_udp_rx* r) {
   e->user_data = UD_RECV;
   r->sq_array[idx] = idx;
   __atomic_store_n(r->sq_tail, tail + 1u, __ATOMIC_RELEASE);
-  if (sys_enter(r->ring, 1, 0, 0) != 1) return RTPS_RX_EINVAL;
+  if (r->sqpoll) {  // the poll thread takes the entry; wake it if it went idle
+    if (__atomic_load_n(r->sq_flags, __ATOMIC_ACQUIRE) & IORING_SQ_NEED_WAKEUP)
+      (void)sys_enter(r->ring, 0, 0, IORING_ENTER_SQ_WAKEUP);
+    for (int spin = 0; __atomic_load_n(r->sq_head, __ATOMIC_ACQUIRE) != tail + 1u; ++spin) {
+      if (spin > 100000) return RTPS_RX_EINVAL;
+      if (__atomic_load_n(r->sq_flags, __ATOMIC_ACQUIRE) & IORING_SQ_NEED_WAKEUP)
+        (void)sys_enter(r->ring, 0, 0, IORING_ENTER_SQ_WAKEUP);
+      usleep(10);
+    }
+  } else if (sys_enter(r->ring, 1, 0, 0) != 1) {
+    return RTPS_RX_EINVAL;
+  }
   r->armed = true;
   return RTPS_RX_OK;
 }
 
-static bool ring_setup(rtps_udp_rx* r) {
+static bool ring_setup(rtps_udp_rx* r, bool sqpoll) {
   io_uring_params p;
   memset(&p, 0, sizeof(p));
-  p.flags = IORING_SETUP_CQSIZE;
+  p.flags = IORING_SETUP_CQSIZE | (sqpoll ? IORING_SETUP_SQPOLL : 0u);
   p.cq_entries = 2u * r->n_slots;  // every provided slot can hold one completion, plus errors
+  p.sq_thread_idle = 100;          // ms the poll thread spins before it sleeps
   r->ring = sys_setup(8, &p);
   if (r->ring < 0) return false;
+  r->sqpoll = sqpoll;
   r->sq_map_len = p.sq_off.array + p.sq_entries * sizeof(unsigned);
   r->cq_map_len = p.cq_off.cqes + p.cq_entries * sizeof(io_uring_cqe);
   const bool single = (p.features & IORING_FEAT_SINGLE_MMAP) != 0;
@@ -163,6 +178,7 @@ static bool ring_setup(rtps_udp_rx* r) {
   r->sq_tail = at<unsigned>(r->sq_map, p.sq_off.tail);
   r->sq_mask = at<unsigned>(r->sq_map, p.sq_off.ring_mask);
   r->sq_array = at<unsigned>(r->sq_map, p.sq_off.array);
+  r->sq_flags = at<unsigned>(r->sq_map, p.sq_off.flags);
   r->cq_head = at<unsigned>(r->cq_map, p.cq_off.head);
   r->cq_tail = at<unsigned>(r->cq_map, p.cq_off.tail);
   r->cq_mask = at<unsigned>(r->cq_map, p.cq_off.ring_mask);
@@ -329,7 +345,8 @@ int rtps_udp_open(const rtps_udp_config* cfg, rtps_udp_rx** out) {
   socklen_t al = sizeof(a);
   (void)getsockname(r->sock, reinterpret_cast<sockaddr*>(&a), &al);
   r->port = ntohs(a.sin_port);
-  if (!(cfg->flags & RTPS_UDP_FORCE_RECVMMSG) && ring_setup(r)) {
+  const bool try_ring = !(cfg->flags & RTPS_UDP_FORCE_RECVMMSG);
+  if (try_ring && (((cfg->flags & RTPS_UDP_SQPOLL) && ring_setup(r, true)) || ring_setup(r, false))) {
     r->backend = RTPS_UDP_IO_URING;
   } else {
     r->backend = RTPS_UDP_RECVMMSG;
@@ -351,7 +368,10 @@ int rtps_udp_close(rtps_udp_rx* r) {
 }
 
 int rtps_udp_port(const rtps_udp_rx* r) { return r ? (int)r->port : RTPS_RX_EINVAL; }
-int rtps_udp_backend(const rtps_udp_rx* r) { return r ? r->backend : RTPS_RX_EINVAL; }
+int rtps_udp_backend(const rtps_udp_rx* r) {
+  if (!r) return RTPS_RX_EINVAL;
+  return r->backend == RTPS_UDP_IO_URING && r->sqpoll ? RTPS_UDP_IO_URING_SQPOLL : r->backend;
+}
 
 int rtps_udp_recv_batch(rtps_udp_rx* r, uint64_t* off, uint32_t* len, uint32_t max_n, int timeout_ms,
                         uint64_t* truncated) {
@@ -390,7 +410,7 @@ int rtps_udp_send_batch(uint32_t ipv4_addr, uint16_t port, const uint8_t* arena,
   constexpr uint32_t K = 256;
   mmsghdr msgs[K];
   iovec iov[K];
-  uint32_t sent = 0;
+  uint32_t sent = 0, stalls = 0;
   while (sent < n) {
     const uint32_t k = (n - sent) < K ? (n - sent) : K;
     for (uint32_t j = 0; j < k; ++j) {
@@ -403,7 +423,15 @@ int rtps_udp_send_batch(uint32_t ipv4_addr, uint16_t port, const uint8_t* arena,
       msgs[j].msg_hdr.msg_iovlen = 1;
     }
     const int got = sendmmsg(s, msgs, k, 0);
-    if (got <= 0) break;
+    if (got <= 0) {
+      // a full device/socket queue is transient (ENOBUFS, EAGAIN): wait for room and retry
+      if (got < 0 && (errno == ENOBUFS || errno == EAGAIN || errno == EINTR) && ++stalls < 100000) {
+        pollfd pf{s, POLLOUT, 0};
+        (void)poll(&pf, 1, 1);
+        continue;
+      }
+      break;
+    }
     sent += (uint32_t)got;
   }
   close(s);

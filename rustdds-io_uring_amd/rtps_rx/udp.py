@@ -16,7 +16,8 @@ from . import lib, _check, ABI_VERSION
 
 UDP_REUSE = 0x1
 UDP_FORCE_RECVMMSG = 0x2
-IO_URING, RECVMMSG = 1, 2
+UDP_SQPOLL = 0x4
+IO_URING, RECVMMSG, IO_URING_SQPOLL = 1, 2, 3
 
 
 class _UdpConfig(ctypes.Structure):
@@ -59,7 +60,7 @@ class UdpReceiver:
     uint8 tensor on the host; it must outlive the receiver."""
 
     def __init__(self, arena, slot_bytes=2048, addr="127.0.0.1", port=0, multicast=None, reuse=False,
-                 force_recvmmsg=False, rcvbuf_bytes=0):
+                 force_recvmmsg=False, sqpoll=True, rcvbuf_bytes=0):
         L = _bind()
         nbytes = arena.nbytes if isinstance(arena, np.ndarray) else arena.numel()
         self.arena = arena
@@ -70,7 +71,8 @@ class UdpReceiver:
         cfg.abi_version = ABI_VERSION
         cfg.ipv4_addr = ipv4(addr)
         cfg.port = port
-        cfg.flags = (UDP_REUSE if reuse else 0) | (UDP_FORCE_RECVMMSG if force_recvmmsg else 0)
+        cfg.flags = ((UDP_REUSE if reuse else 0) | (UDP_FORCE_RECVMMSG if force_recvmmsg else 0) |
+                     (UDP_SQPOLL if sqpoll else 0))
         cfg.multicast_group = ipv4(multicast) if multicast else 0
         cfg.arena = self.arena_np.ctypes.data
         cfg.slot_bytes = slot_bytes

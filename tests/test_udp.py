@@ -17,7 +17,16 @@ GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "vectors.json")
 
 
 def _backends():
-    return [False, True]  # force_recvmmsg
+    return ["io_uring", "io_uring_sqpoll", "recvmmsg"]
+
+
+def _open(arena, backend, **kw):
+    rx = udp.UdpReceiver(arena, force_recvmmsg=backend == "recvmmsg", sqpoll=backend == "io_uring_sqpoll", **kw)
+    want = {"io_uring": udp.IO_URING, "io_uring_sqpoll": udp.IO_URING_SQPOLL, "recvmmsg": udp.RECVMMSG}[backend]
+    if rx.backend != want:
+        rx.close()
+        pytest.skip(f"{backend} not available here (got backend {rx.backend})")
+    return rx
 
 
 def _drain(rx, want, batch=512, release=True, timeout_ms=2000):
@@ -42,13 +51,10 @@ def _golden_datagrams():
     return [bytes.fromhex(x["hex"]) for x in v["messages"]]
 
 
-@pytest.mark.parametrize("force_recvmmsg", _backends())
-def test_loopback_bytes_and_parse(force_recvmmsg):
+@pytest.mark.parametrize("backend", _backends())
+def test_loopback_bytes_and_parse(backend):
     arena = np.zeros(2048 * 1024, dtype=np.uint8)
-    rx = udp.UdpReceiver(arena, slot_bytes=2048, force_recvmmsg=force_recvmmsg, rcvbuf_bytes=8 << 20)
-    if not force_recvmmsg and rx.backend != udp.IO_URING:
-        pytest.skip("io_uring not available here")
-    assert rx.backend == (udp.RECVMMSG if force_recvmmsg else udp.IO_URING)
+    rx = _open(arena, backend, slot_bytes=2048, rcvbuf_bytes=8 << 20)
     sent = _golden_datagrams()
     a, off, ln = oracle.gen(oracle.WL_C2, 120)
     sent += [a[int(o):int(o) + int(n)].tobytes() for o, n in zip(off, ln)]
@@ -74,10 +80,10 @@ def test_loopback_bytes_and_parse(force_recvmmsg):
     rx.close()
 
 
-@pytest.mark.parametrize("force_recvmmsg", _backends())
-def test_truncated_datagrams_dropped(force_recvmmsg):
+@pytest.mark.parametrize("backend", _backends())
+def test_truncated_datagrams_dropped(backend):
     arena = np.zeros(256 * 64, dtype=np.uint8)
-    rx = udp.UdpReceiver(arena, slot_bytes=256, force_recvmmsg=force_recvmmsg)
+    rx = _open(arena, backend, slot_bytes=256)
     sizes = [100, 300, 256, 257, 40, 1000, 16]
     sent = [bytes([i]) * s for i, s in enumerate(sizes)]
     packed, poff, plen = oracle.pack(sent)
@@ -88,10 +94,10 @@ def test_truncated_datagrams_dropped(force_recvmmsg):
     rx.close()
 
 
-@pytest.mark.parametrize("force_recvmmsg", _backends())
-def test_all_slots_in_use_then_release(force_recvmmsg):
+@pytest.mark.parametrize("backend", _backends())
+def test_all_slots_in_use_then_release(backend):
     arena = np.zeros(128 * 16, dtype=np.uint8)
-    rx = udp.UdpReceiver(arena, slot_bytes=128, force_recvmmsg=force_recvmmsg, rcvbuf_bytes=1 << 20)
+    rx = _open(arena, backend, slot_bytes=128, rcvbuf_bytes=1 << 20)
     sent = [i.to_bytes(4, "little") * 20 for i in range(60)]
     packed, poff, plen = oracle.pack(sent)
     udp.send_batch("127.0.0.1", rx.port, packed, poff, plen)
