@@ -25,6 +25,9 @@
  *   interpreter (iter_next)         <- io_uring/rtps/message_receiver.rs:56-119, 618-665, 289-295
  *   data_to_dds_data_kind           <- io_uring/rtps/reader.rs:760-833
  *   builtin pairs                   <- io_uring/discovery/discovery.rs:2795-2816, 3075-3095
+ *   rtps_oracle_cdr_decode          <- cdr_adapters.rs:246-275 + cdr-encoding 0.10 rules
+ *   rtps_oracle_frag_batch          <- rtps/fragment_assembler.rs:23-214, reader.rs:563-647
+ *   rtps_oracle_ingest_batch        <- rtps/rtps_writer_proxy.rs:202-355, reader.rs:514-1116
  */
 #include <pthread.h>
 #include <stdint.h>
