@@ -54,7 +54,8 @@ constexpr uint32_t W = RTPS_INGEST_WINDOW;  // sequence numbers tracked per writ
 constexpr uint32_t WW = W / 32;             // bitmap words per writer
 constexpr uint32_t ECAP_MAX = 1u << 14;     // writers (match-table entries)
 enum : uint8_t { EV_NONE = 0, EV_SAMPLE = 1, EV_HB = 2, EV_GAP = 3 };
-enum { C_OVF = 0, C_COUNT = 1 };
+enum { C_OVF = 0, C_NSEL, C_SPREAD, C_COUNT = C_SPREAD + 2 * 64 };  // overflow, selected HEARTBEATs, then the
+// HEARTBEAT / GAP event counts in 64 slot pairs (one atomic per block, spread: no single hot address)
 
 __device__ __forceinline__ uint32_t guid_hash(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
   uint32_t h = 0x811c9dc5u;  // the match table's hash (rtps_rx.hip)
@@ -107,7 +108,7 @@ struct Scratch {
   uint32_t* ent;    // writer entry per record
   int64_t* esn;     // sample sn (DATA / completed DATA_FRAG)
   uint32_t* fidx;   // completed DataFrag sample of a record, or NONE
-  uint32_t *hkey, *hval, *skey, *sval;  // HEARTBEAT sort
+  uint32_t *hkey, *hval, *skey, *sval;  // HEARTBEAT sort (hkey: HB flag per record, then the keys)
   int32_t *hcnt, *hexcl;
   int64_t *hf, *hpre;
 };
@@ -133,14 +134,15 @@ __global__ __launch_bounds__(IT) void k_fidx(const rtps_frag_sample* frag, const
 
 __global__ __launch_bounds__(IT) void k_classify(IngestTable t, const rtps_record* recs, const uint64_t* n_rec,
                                                  uint64_t max, const rtps_frag_sample* frag, uint32_t flags,
-                                                 Scratch x, uint32_t sent) {
+                                                 Scratch x, uint64_t* ctr) {
   const uint64_t n = *n_rec < max ? *n_rec : max;
+  uint32_t nh = 0, ng = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * IT + threadIdx.x; i < max; i += (uint64_t)gridDim.x * IT) {
     uint8_t ev = EV_NONE;
     uint32_t e = NONE;
     int64_t sn = 0;
     if (i < n) {
-      const uint32_t f = x.fidx[i];
+      const uint32_t f = frag ? x.fidx[i] : NONE;
       if (f != NONE) {  // completed DataFrag sample, processed at its completing record (reader.rs:614-626)
         const uint32_t* g = reinterpret_cast<const uint32_t*>(frag[f].writer_guid);
         e = entry_of(t, g[0], g[1], g[2], g[3]);
@@ -169,35 +171,46 @@ __global__ __launch_bounds__(IT) void k_classify(IngestTable t, const rtps_recor
     x.evt[i] = ev;
     x.ent[i] = e;
     x.esn[i] = sn;
-    x.hkey[i] = ev == EV_HB ? e : sent;
-    x.hval[i] = (uint32_t)i;
+    x.hkey[i] = ev == EV_HB ? 1u : 0u;  // selection flag of the HEARTBEAT compaction
+    nh += ev == EV_HB;
+    ng += ev == EV_GAP;
+  }
+  __shared__ uint32_t s_n[2];
+  if (threadIdx.x == 0) { s_n[0] = 0; s_n[1] = 0; }
+  __syncthreads();
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) { nh += __shfl_xor(nh, d, 64); ng += __shfl_xor(ng, d, 64); }
+  if ((threadIdx.x & 63u) == 0) { atomicAdd(&s_n[0], nh); atomicAdd(&s_n[1], ng); }
+  __syncthreads();
+  if (threadIdx.x == 0 && (s_n[0] | s_n[1])) {
+    unsigned long long* c = reinterpret_cast<unsigned long long*>(ctr + C_SPREAD + 2u * (blockIdx.x & 63u));
+    if (s_n[0]) atomicAdd(c, (unsigned long long)s_n[0]);
+    if (s_n[1]) atomicAdd(c + 1, (unsigned long long)s_n[1]);
   }
 }
 
+// the compacted HEARTBEAT record indices (hval, record order) -> their writer entries (hkey)
+__global__ __launch_bounds__(IT) void k_hkeys(uint64_t n_hb, Scratch x) {
+  for (uint64_t q = (uint64_t)blockIdx.x * IT + threadIdx.x; q < n_hb; q += (uint64_t)gridDim.x * IT)
+    x.hkey[q] = x.ent[x.hval[q]];
+}
+
 // ---- 2 heartbeats ----
-__global__ __launch_bounds__(IT) void k_hvals(const rtps_record* recs, uint64_t max, Scratch x, State s, uint32_t sent) {
-  for (uint64_t q = (uint64_t)blockIdx.x * IT + threadIdx.x; q < max; q += (uint64_t)gridDim.x * IT) {
+__global__ __launch_bounds__(IT) void k_hvals(const rtps_record* recs, uint64_t n_hb, Scratch x, State s) {
+  for (uint64_t q = (uint64_t)blockIdx.x * IT + threadIdx.x; q < n_hb; q += (uint64_t)gridDim.x * IT) {
     const uint32_t k = x.skey[q];
-    int32_t c = INT32_MIN;
-    if (k != sent) {
-      c = recs[x.sval[q]].u.hb.count;
-      if (q == 0 || x.skey[q - 1] != k) s.seg_b[k] = (uint32_t)q;
-      if (q + 1 == max || x.skey[q + 1] != k) s.seg_e[k] = (uint32_t)q + 1u;
-    }
-    x.hcnt[q] = c;
+    x.hcnt[q] = recs[x.sval[q]].u.hb.count;
+    if (q == 0 || x.skey[q - 1] != k) s.seg_b[k] = (uint32_t)q;
+    if (q + 1 == n_hb || x.skey[q + 1] != k) s.seg_e[k] = (uint32_t)q + 1u;
   }
 }
 // accepted iff count > max(state count, every earlier count of the writer) (reader.rs:902-905);
 // an accepted HEARTBEAT covers [0, firstSN) (irrelevant_changes_up_to)
-__global__ __launch_bounds__(IT) void k_hacc(const rtps_record* recs, uint64_t max, Scratch x, State s, uint32_t sent) {
-  for (uint64_t q = (uint64_t)blockIdx.x * IT + threadIdx.x; q < max; q += (uint64_t)gridDim.x * IT) {
+__global__ __launch_bounds__(IT) void k_hacc(const rtps_record* recs, uint64_t n_hb, Scratch x, State s) {
+  for (uint64_t q = (uint64_t)blockIdx.x * IT + threadIdx.x; q < n_hb; q += (uint64_t)gridDim.x * IT) {
     const uint32_t k = x.skey[q];
-    int64_t f = INT64_MIN;
-    if (k != sent) {
-      const int32_t before = x.hexcl[q] > s.hbc[k] ? x.hexcl[q] : s.hbc[k];
-      if (x.hcnt[q] > before) f = recs[x.sval[q]].sn;
-    }
-    x.hf[q] = f;
+    const int32_t before = x.hexcl[q] > s.hbc[k] ? x.hexcl[q] : s.hbc[k];
+    x.hf[q] = x.hcnt[q] > before ? recs[x.sval[q]].sn : INT64_MIN;
   }
 }
 
@@ -236,7 +249,8 @@ __device__ __forceinline__ void gap_words(const rtps_record& r, const uint8_t* a
 }
 
 // samples first: their sequence numbers (dbits) and first-cover keys
-__global__ __launch_bounds__(IT) void k_marks_d(const uint64_t* n_rec, uint64_t max, Scratch x, State s, uint32_t epoch) {
+__global__ __launch_bounds__(IT) void k_marks_d(const uint64_t* n_rec, uint64_t max, Scratch x, State s, uint32_t epoch,
+                                                bool gaps) {
   const uint64_t n = *n_rec < max ? *n_rec : max;
   for (uint64_t i0 = (uint64_t)blockIdx.x * IT; i0 < n; i0 += (uint64_t)gridDim.x * IT) {  // wave-uniform trip count
     const uint64_t i = i0 + threadIdx.x;
@@ -254,7 +268,7 @@ __global__ __launch_bounds__(IT) void k_marks_d(const uint64_t* n_rec, uint64_t 
         atomicMin(reinterpret_cast<unsigned long long*>(s.fc + (uint64_t)e * W) + off, ekey(epoch, (uint32_t)i));
       }
     }
-    wave_or(word, bit, act);
+    if (gaps) wave_or(word, bit, act);  // the sample bitmap only serves k_marks_g
   }
 }
 // then GAPs: a GAP's first-cover key matters only where a sample of the batch
@@ -319,7 +333,7 @@ __global__ __launch_bounds__(IT) void k_decide(const uint64_t* n_rec, uint64_t m
 
 // ---- 6 merge ----
 __global__ __launch_bounds__(IT) void k_merge(const rtps_record* recs, const uint8_t* arena, const uint64_t* dgram_off,
-                                              const uint64_t* n_rec, uint64_t max, Scratch x, State s) {
+                                              const uint64_t* n_rec, uint64_t max, Scratch x, State s, bool gaps) {
   const uint64_t n = *n_rec < max ? *n_rec : max;
   for (uint64_t i0 = (uint64_t)blockIdx.x * IT; i0 < n; i0 += (uint64_t)gridDim.x * IT) {  // wave-uniform trip count
     const uint64_t i = i0 + threadIdx.x;
@@ -337,7 +351,7 @@ __global__ __launch_bounds__(IT) void k_merge(const rtps_record* recs, const uin
         act = true;
         word = bits + w;
         bit = 1u << ((v - lo) & 31);
-        s.dbits[(uint64_t)e * WW + w] = 0u;  // every mark of the batch is done (k_marks_g read them)
+        if (gaps) s.dbits[(uint64_t)e * WW + w] = 0u;  // every mark of the batch is done (k_marks_g read them)
       }
     } else if (ev == EV_GAP) {
       gap_words(recs[i], arena, dgram_off, lo, [&](uint64_t w, uint32_t m) { atomicOr(bits + w, m); });
@@ -420,6 +434,7 @@ struct IngestState {
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
   uint32_t epoch = 0;  // batches since the first-cover table was last cleared
+  uint64_t* hctr = nullptr;  // pinned host copy of the event counters
 };
 
 static uint64_t* S_fc(IngestState* s) { return s->st.fc; }
@@ -499,6 +514,10 @@ static bool grow_scratch(IngestState* s, uint64_t max, hipStream_t st) {
                                                     hipcub::Equality(), st) == hipSuccess;
   ok = ok && hipcub::DeviceSelect::Flagged(nullptr, b4, hipcub::CountingInputIterator<uint32_t>(0), (uint8_t*)nullptr,
                                            (uint32_t*)nullptr, (uint64_t*)nullptr, (int64_t)n, st) == hipSuccess;
+  size_t b5 = 0;
+  ok = ok && hipcub::DeviceSelect::Flagged(nullptr, b5, hipcub::CountingInputIterator<uint32_t>(0), x.hkey, x.hval,
+                                           (uint64_t*)nullptr, (int64_t)n, st) == hipSuccess;
+  if (b5 > b4) b4 = b5;
   size_t tb = b1;
   if (b2 > tb) tb = b2;
   if (b3 > tb) tb = b3;
@@ -515,6 +534,11 @@ IngestState* rtps_ingest_state_new(int device) {
   if (!s) return nullptr;
   s->device = device;
   if (hipMalloc(&s->st.ctr, C_COUNT * 8) != hipSuccess) { delete s; return nullptr; }
+  if (hipHostMalloc(&s->hctr, C_COUNT * 8, hipHostMallocDefault) != hipSuccess) {
+    (void)hipFree(s->st.ctr);
+    delete s;
+    return nullptr;
+  }
   return s;
 }
 
@@ -523,6 +547,7 @@ void rtps_ingest_state_free(IngestState* s) {
   free_scratch(s);
   free_state(s);
   if (s->st.ctr) (void)hipFree(s->st.ctr);
+  if (s->hctr) (void)hipHostFree(s->hctr);
   delete s;
 }
 
@@ -550,46 +575,63 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const IngestTable& t, cons
     s->epoch = 1;
   }
   uint32_t ebits = 1;
-  while ((1u << ebits) <= t.n_entries) ++ebits;  // entries < sent = 2^ebits - 1
-  const uint32_t sent = (1u << ebits) - 1u;
+  while ((1u << ebits) < t.n_entries) ++ebits;  // sort key width: entries < 2^ebits
   const uint32_t gb = (uint32_t)hmin((max + IT - 1) / IT, 8192);
   Scratch& x = s->x;
   State& S = s->st;
-  bool ok = hipMemsetAsync(S.ctr, 0, C_COUNT * 8, st) == hipSuccess &&
-            hipMemsetAsync(x.fidx, 0xff, max * 4, st) == hipSuccess &&
-            hipMemsetAsync(S.seg_b, 0, (uint64_t)s->ecap * 4, st) == hipSuccess &&
-            hipMemsetAsync(S.seg_e, 0, (uint64_t)s->ecap * 4, st) == hipSuccess;
+  bool ok = hipMemsetAsync(S.ctr, 0, C_COUNT * 8, st) == hipSuccess;
+  const bool with_frag = frag && n_frag && max_frag;
+  if (with_frag) ok = ok && hipMemsetAsync(x.fidx, 0xff, max * 4, st) == hipSuccess;
   if (!ok) return RTPS_RX_EHIP;
-  if (frag && n_frag && max_frag)
+  if (with_frag)
     hipLaunchKernelGGL(k_fidx, dim3((uint32_t)hmin((max_frag + IT - 1) / IT, 4096)), dim3(IT), 0, st, frag, n_frag,
                        max_frag, max, x.fidx);
-  hipLaunchKernelGGL(k_classify, dim3(gb), dim3(IT), 0, st, t, records, n_records, max, frag, flags, x, sent);
-  if (reliable) {
+  hipLaunchKernelGGL(k_classify, dim3(gb), dim3(IT), 0, st, t, records, n_records, max, with_frag ? frag : nullptr,
+                     flags, x, S.ctr);
+  // the batch's HEARTBEAT / GAP counts decide which stages run: one small read-back
+  if (hipMemcpyAsync(s->hctr, S.ctr, C_COUNT * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return RTPS_RX_EHIP;
+  uint64_t n_hb = 0, n_gap = 0;
+  for (uint32_t k = 0; k < 64; ++k) { n_hb += s->hctr[C_SPREAD + 2 * k]; n_gap += s->hctr[C_SPREAD + 2 * k + 1]; }
+  if (!reliable) n_hb = 0;
+  const bool have_hb = n_hb > 0;
+  if (have_hb) {  // stable compaction of the HEARTBEAT events, sort by writer entry, scans by key
+    const uint32_t hb_blocks = (uint32_t)hmin((n_hb + IT - 1) / IT, 8192);
+    ok = hipMemsetAsync(S.seg_b, 0, (uint64_t)s->ecap * 4, st) == hipSuccess &&
+         hipMemsetAsync(S.seg_e, 0, (uint64_t)s->ecap * 4, st) == hipSuccess;
+    if (!ok) return RTPS_RX_EHIP;
     size_t tb = s->tmp_bytes;
-    if (hipcub::DeviceRadixSort::SortPairs(s->tmp, tb, x.hkey, x.skey, x.hval, x.sval, (int)max, 0, (int)ebits, st) !=
+    if (hipcub::DeviceSelect::Flagged(s->tmp, tb, hipcub::CountingInputIterator<uint32_t>(0), x.hkey, x.hval,
+                                      S.ctr + C_NSEL, (int64_t)max, st) != hipSuccess)
+      return RTPS_RX_EHIP;
+    hipLaunchKernelGGL(k_hkeys, dim3(hb_blocks), dim3(IT), 0, st, n_hb, x);
+    tb = s->tmp_bytes;
+    if (hipcub::DeviceRadixSort::SortPairs(s->tmp, tb, x.hkey, x.skey, x.hval, x.sval, (int)n_hb, 0, (int)ebits, st) !=
         hipSuccess)
       return RTPS_RX_EHIP;
-    hipLaunchKernelGGL(k_hvals, dim3(gb), dim3(IT), 0, st, records, max, x, S, sent);
+    hipLaunchKernelGGL(k_hvals, dim3(hb_blocks), dim3(IT), 0, st, records, n_hb, x, S);
     tb = s->tmp_bytes;
     if (hipcub::DeviceScan::ExclusiveScanByKey(s->tmp, tb, x.skey, x.hcnt, x.hexcl, hipcub::Max(), INT32_MIN,
-                                               (uint32_t)max, hipcub::Equality(), st) != hipSuccess)
+                                               (uint32_t)n_hb, hipcub::Equality(), st) != hipSuccess)
       return RTPS_RX_EHIP;
-    hipLaunchKernelGGL(k_hacc, dim3(gb), dim3(IT), 0, st, records, max, x, S, sent);
+    hipLaunchKernelGGL(k_hacc, dim3(hb_blocks), dim3(IT), 0, st, records, n_hb, x, S);
     tb = s->tmp_bytes;
-    if (hipcub::DeviceScan::InclusiveScanByKey(s->tmp, tb, x.skey, x.hf, x.hpre, hipcub::Max(), (uint32_t)max,
+    if (hipcub::DeviceScan::InclusiveScanByKey(s->tmp, tb, x.skey, x.hf, x.hpre, hipcub::Max(), (uint32_t)n_hb,
                                                hipcub::Equality(), st) != hipSuccess)
       return RTPS_RX_EHIP;
   }
-  hipLaunchKernelGGL(k_marks_d, dim3(gb), dim3(IT), 0, st, n_records, max, x, S, s->epoch);
-  hipLaunchKernelGGL(k_marks_g, dim3(gb), dim3(IT), 0, st, records, arena, dgram_off, n_records, max, x, S, s->epoch);
-  hipLaunchKernelGGL(k_decide, dim3(gb), dim3(IT), 0, st, n_records, max, x, S, out->accept, reliable, s->epoch);
+  hipLaunchKernelGGL(k_marks_d, dim3(gb), dim3(IT), 0, st, n_records, max, x, S, s->epoch, n_gap > 0);
+  if (n_gap)
+    hipLaunchKernelGGL(k_marks_g, dim3(gb), dim3(IT), 0, st, records, arena, dgram_off, n_records, max, x, S, s->epoch);
+  hipLaunchKernelGGL(k_decide, dim3(gb), dim3(IT), 0, st, n_records, max, x, S, out->accept, have_hb, s->epoch);
   size_t tb = s->tmp_bytes;
   if (hipcub::DeviceSelect::Flagged(s->tmp, tb, hipcub::CountingInputIterator<uint32_t>(0), out->accept,
                                     out->accepted, out->n_accepted, (int64_t)max, st) != hipSuccess)
     return RTPS_RX_EHIP;
-  hipLaunchKernelGGL(k_merge, dim3(gb), dim3(IT), 0, st, records, arena, dgram_off, n_records, max, x, S);
+  hipLaunchKernelGGL(k_merge, dim3(gb), dim3(IT), 0, st, records, arena, dgram_off, n_records, max, x, S, n_gap > 0);
   if (t.n_entries)
-    hipLaunchKernelGGL(k_state, dim3(t.n_entries), dim3(IT), 0, st, t.n_entries, x, S, reliable, out->ack_base);
+    hipLaunchKernelGGL(k_state, dim3(t.n_entries), dim3(IT), 0, st, t.n_entries, x, S, have_hb, out->ack_base);
   hipLaunchKernelGGL(k_finish, dim3(1), dim3(1), 0, st, S.ctr, out->n_window_overflow);
   return hipGetLastError() == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP;
 }
