@@ -258,13 +258,12 @@ def hello_world_datagrams(n):
 def c1_loopback(dev, stream, n=200_000, batch=16384):
     """Config C1 (BASELINE.json configs[0]): hello-world publisher -> subscriber over UDP
     loopback, 64-B samples.  Publisher: sendmmsg on a thread, flow-controlled to two batches
-    in flight (an unthrottled loopback sender outruns any receiver: what gets through is then
-    set by the socket buffer, not by the pipeline).  Subscriber: the io_uring
-    receive (rtps_udp_*) lands datagrams in slots of a pinned arena (a receive thread keeps
-    draining), and each batch is parsed in place by the GPU (zero-copy), ingested into the
-    history cache and CDR-decoded.  Loopback and the kernel bound the rate; dropped
+    ahead of the subscriber (an unthrottled loopback sender outruns any receiver: what gets
+    through is then set by the socket buffer, not by the pipeline).  Subscriber: the native
+    receive loop (rtps_rx_pump): io_uring lands datagrams in slots of a pinned arena, and each
+    batch is parsed in place by the GPU (zero-copy), ingested into the history cache and
+    CDR-decoded, two batches in flight.  Loopback and the kernel bound the rate; dropped
     datagrams (socket buffer overruns) are reported, never hidden."""
-    import queue
     import threading
     from rtps_rx import udp, cdr
     hello_t = cdr.CdrType([("user_id", "i32"), ("message", cdr.String(60))])
@@ -277,90 +276,40 @@ def c1_loopback(dev, stream, n=200_000, batch=16384):
     tbl = np.zeros(1, dtype=MATCH_DTYPE)
     tbl["writer_guid"][0] = np.frombuffer(HELLO_PREFIX + HELLO_WRITER, dtype=np.uint8)
     rx.set_match_table(tbl)
-    cap = batch * 2
-    outs = rx.alloc_outputs(batch, cap)
-    iouts = rx.alloc_ingest_outputs(cap, 1)
-    rows, row_status = rx.alloc_rows(hello_t, cap)
-    h_off = torch.empty(batch, dtype=torch.int64, pin_memory=True)
-    h_ln = torch.empty(batch, dtype=torch.int32, pin_memory=True)
-    got_q, rel_q = queue.Queue(), queue.Queue()
-    done = threading.Event()
-
-    def receiver():
-        while True:
-            while not rel_q.empty():
-                rxu.release(rel_q.get())
-            o, m = rxu.recv_batch(batch, timeout_ms=5)
-            if len(o):
-                got_q.put((o.copy(), m.copy()))
-            elif done.is_set():
-                got_q.put(None)
-                return
-
+    pump = udp.Pump(rx, rxu, max_batch=batch, ingest=True, sample_type=hello_t, max_recs=2 * batch, n_entries=1)
+    live = pump.stats
     sent = [0]
-    processed = [0]
-    window = 2 * batch  # flow control: at most two batches in flight (slots and socket buffer hold them)
+    window = 2 * batch
+
+    send_s = [0.0, 0.0]  # time inside sendmmsg, time waiting on flow control
 
     def sender():
         chunk = 4096
         for a in range(0, n, chunk):
-            while sent[0] - processed[0] > window:
+            w0 = time.perf_counter()
+            while sent[0] - live.datagrams > window:
                 time.sleep(0.0002)
             b = min(n, a + chunk)
+            s0 = time.perf_counter()
             sent[0] += udp.send_batch("127.0.0.1", rxu.port, data, off[a:b], ln[a:b])
+            send_s[0] += time.perf_counter() - s0
+            send_s[1] += s0 - w0
 
-    tr = threading.Thread(target=receiver)
-    ts = threading.Thread(target=sender)
+    decoded = [0]
+
+    def on_batch(b):
+        m = min(b.n_records, pump.cap)
+        decoded[0] += int((b.row_status[:m] == cdr.CDR_OK).sum().item())
+        return False
+
+    ts = threading.Thread(target=sender, daemon=True)
     t0 = time.perf_counter()
-    tr.start()
     ts.start()
-    received = accepted = decoded = 0
-    gpu_s = 0.0
-    pend_o, pend_l = [], []
-    finished = False
-    idle_since = None
-    t_last = t0
-    while not finished:
-        try:
-            item = got_q.get(timeout=0.05)
-        except queue.Empty:
-            item = "idle"
-        if item is None:
-            finished = True
-        elif item != "idle":
-            pend_o.append(item[0])
-            pend_l.append(item[1])
-            idle_since = None
-            t_last = time.perf_counter()
-        elif not ts.is_alive():
-            idle_since = idle_since or time.perf_counter()
-            if time.perf_counter() - idle_since > 0.3:
-                done.set()
-        k = sum(len(x) for x in pend_o)
-        while k and (k >= batch // 2 or item == "idle" or finished):
-            allo, alll = np.concatenate(pend_o), np.concatenate(pend_l)
-            o, m = allo[:batch], alll[:batch]  # the rest stays pending for the next GPU batch
-            pend_o, pend_l = ([allo[batch:]], [alll[batch:]]) if len(allo) > batch else ([], [])
-            k -= len(o)
-            c = len(o)
-            h_off[:c].copy_(torch.from_numpy(o.view(np.int64)))
-            h_ln[:c].copy_(torch.from_numpy(m.view(np.int32)))
-            g0 = time.perf_counter()
-            rx.parse_batch_device(arena, h_off, h_ln, c, outs)
-            rx.ingest(arena, h_off, outs, iouts)
-            rx.cdr_decode(hello_t, arena, h_off, outs, rows, row_status)
-            rx.sync()
-            gpu_s += time.perf_counter() - g0
-            nr = int(outs["n_records"].item())
-            accepted += int(iouts["n_accepted"].item())
-            decoded += int((row_status[:nr] == cdr.CDR_OK).sum().item())
-            received += c
-            processed[0] = received
-            rel_q.put(o)
+    st = pump.run(wait_ms=5, stop_after=n, idle_stop_ms=2000, on_batch=on_batch)
     wall = time.perf_counter() - t0
-    busy = t_last - t0  # first send .. last datagram handed over (excludes the end-of-stream wait)
-    tr.join()
-    ts.join()
+    ts.join(timeout=5)
+    received = st.datagrams
+    busy = (st.last_ns - st.first_ns) / 1e9 if st.batches else float("nan")  # first batch .. last finished
     rxu.close()
     rx.close()
     # the CPU reference parse of the same datagrams (oracle, one thread), for scale
@@ -371,11 +320,12 @@ def c1_loopback(dev, stream, n=200_000, batch=16384):
     return {"config": "C1: hello-world publisher -> subscriber over UDP loopback, 64-B HelloWorldData samples",
             "receive_backend": {udp.IO_URING: "io_uring", udp.IO_URING_SQPOLL: "io_uring+sqpoll",
                                 udp.RECVMMSG: "recvmmsg"}[rxu.backend],
+            "loop": "native rtps_rx_pump, 2 batches in flight",
             "datagrams_built": n, "datagrams_sent": sent[0], "datagrams_received": received,
-            "dropped": sent[0] - received,
-            "samples_accepted": accepted, "samples_decoded": decoded, "wall_s": wall, "stream_s": busy,
-            "datagrams_per_s": received / busy, "gpu_busy_s": gpu_s,
-            "cpu_reference_parse_per_s_1_thread": n / cpu_s}
+            "dropped": sent[0] - received, "batches": st.batches,
+            "samples_accepted": st.accepted, "samples_decoded": decoded[0], "wall_s": wall, "stream_s": busy,
+            "datagrams_per_s": received / busy, "publisher_sendmmsg_s": send_s[0],
+            "publisher_flow_wait_s": send_s[1], "cpu_reference_parse_per_s_1_thread": n / cpu_s}
 
 
 def cpu_baseline(workload, n, target_cpu_s=10.0, match_table=None):

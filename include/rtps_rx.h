@@ -462,6 +462,77 @@ int rtps_udp_release(rtps_udp_rx* rx, const uint64_t* off, uint32_t n);
 int rtps_udp_send_batch(uint32_t ipv4_addr, uint16_t port, const uint8_t* arena, const uint64_t* off,
                         const uint32_t* len, uint32_t n);
 
+/* ---- native receive loop: UDP arena -> GPU parse -> ingest -> decode --------
+ * Replaces the per-datagram receive loop of the reference's event loop:
+ *   Domain::handle_event, Variant::DataRecv      io_uring/rtps/dp_event_loop.rs:162-211
+ *     buffer_from_cqe / try_fix_err (ENOBUFS)    io_uring/discovery/traffic.rs:167-189, 246-284
+ *     Bytes::copy_from_slice + handle_received_packet_2, then the reader's
+ *     handle_*_msg per submessage                 dp_event_loop.rs:206-211, 266-327
+ * with a batch loop on the calling thread: take every datagram that has
+ * landed in the arena (up to max_batch; the first one waits up to wait_ms),
+ * launch the parse (zero-copy from the arena), the history-cache ingest and
+ * the CDR decode on the context's stream, then finish the PREVIOUS batch while
+ * the GPU works: wait for it, hand its outputs to on_batch, give its slots
+ * back to the receive pool.  Two batches are in flight at most (double-
+ * buffered offsets, outputs and events).  The arena must be device-visible
+ * (pinned host memory, or memory the GPU maps). */
+#define RTPS_PUMP_INGEST 0x1u /* run rtps_rx_ingest on every batch (needs a match table) */
+#define RTPS_PUMP_CDR 0x2u    /* run rtps_rx_cdr_decode with cdr_prog on every batch       */
+typedef struct rtps_pump_buffers { /* outputs of one in-flight batch: caller-owned DEVICE memory */
+  rtps_rx_out out;          /* status [max_batch]; records / match [out.max_records]; n_records */
+  rtps_ingest_out ingest;   /* RTPS_PUMP_INGEST: accept / accepted [out.max_records], n_accepted */
+  uint8_t* rows;            /* RTPS_PUMP_CDR: [out.max_records * cdr_row_bytes] */
+  uint8_t* row_status;      /* RTPS_PUMP_CDR: [out.max_records] */
+} rtps_pump_buffers;
+typedef struct rtps_pump_batch {
+  uint64_t seq;                  /* batch number, from 0 */
+  uint32_t buffer;               /* which of the two rtps_pump_buffers holds the outputs */
+  uint32_t n_datagrams;
+  const uint64_t* dgram_off;     /* [n] host (pinned) arena offsets, arrival order */
+  const uint32_t* dgram_len;     /* [n] */
+  uint64_t n_records;            /* host copy of *out.n_records */
+  uint64_t n_accepted;           /* host copy of *ingest.n_accepted (0 without ingest) */
+} rtps_pump_batch;
+/* Called on the pump's thread once a batch's GPU work is done, before its
+ * slots are released (the arena bytes are still valid).  Non-zero: stop. */
+typedef int (*rtps_pump_fn)(void* user, const rtps_pump_batch* batch);
+typedef struct rtps_pump_config {
+  uint32_t abi_version;        /* RTPS_RX_ABI_VERSION */
+  uint32_t flags;              /* RTPS_PUMP_* */
+  uint32_t max_batch;          /* datagrams per GPU batch, 1..ctx max_datagrams */
+  int32_t wait_ms;             /* wait for the first datagram of a batch (>= 0) */
+  uint64_t stop_after;         /* stop after this many datagrams (0 = no limit) */
+  uint32_t idle_stop_ms;       /* stop after this long without a datagram (0 = no limit) */
+  uint32_t ingest_flags;       /* RTPS_INGEST_* for rtps_rx_ingest */
+  const rtps_cdr_op* cdr_prog; /* RTPS_PUMP_CDR: the sample type (see rtps_rx_cdr_decode) */
+  uint32_t cdr_n_ops;
+  uint32_t cdr_row_bytes;
+  const rtps_pump_buffers* buffers; /* [2]; a batch is cut where its record bound
+                                       sum((len-20)/4) would exceed out.max_records */
+  rtps_pump_fn on_batch;       /* optional */
+  void* user;
+  const volatile uint32_t* stop; /* optional: non-zero (from any thread) stops the loop */
+} rtps_pump_config;
+/* Updated while the loop runs (relaxed 64-bit stores: another thread may poll
+ * them, e.g. for flow control); final when rtps_rx_pump returns. */
+typedef struct rtps_pump_stats {
+  uint64_t datagrams;   /* received and handed to the GPU */
+  uint64_t completed;   /* datagrams of finished batches (slots released) */
+  uint64_t batches;
+  uint64_t records;
+  uint64_t accepted;
+  uint64_t truncated;   /* datagrams longer than a slot (dropped by the receive) */
+  uint64_t first_ns;    /* CLOCK_MONOTONIC when the first batch was received */
+  uint64_t last_ns;     /* CLOCK_MONOTONIC when the last batch finished */
+} rtps_pump_stats;
+/* arena / arena_len: the memory given to rtps_udp_open.  Returns RTPS_RX_OK
+ * when a stop condition ends the loop, or a negative code.  The batches in
+ * flight are finished before it returns; datagrams already received but left
+ * out of a batch by a capacity cut are dropped (their slots released) when the
+ * loop stops. */
+int rtps_rx_pump(rtps_rx_ctx* ctx, rtps_udp_rx* udp, const uint8_t* arena, uint64_t arena_len,
+                 const rtps_pump_config* cfg, rtps_pump_stats* stats);
+
 /* Upper bound on records for datagram lengths (host arrays): sum((len-20)/4). */
 uint64_t rtps_rx_max_records_host(const uint32_t* dgram_len, uint32_t n);
 

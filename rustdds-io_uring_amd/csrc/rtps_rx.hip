@@ -36,6 +36,7 @@
 #include "rtps_gen.h"
 #include "rtps_cdr.h"
 #include "rtps_frag.h"
+#include "rtps_ctx.h"
 #include "rtps_ingest.h"
 
 namespace {
@@ -1373,3 +1374,8 @@ int rtps_rx_debug_scratch(rtps_rx_ctx* c, uint64_t* host, uint32_t k) {
 }
 
 }  // extern "C"
+
+// internal accessors (rtps_ctx.h)
+hipStream_t rtps_ctx_stream(const rtps_rx_ctx* c) { return c->stream; }
+int rtps_ctx_device(const rtps_rx_ctx* c) { return c->device; }
+uint32_t rtps_ctx_max_datagrams(const rtps_rx_ctx* c) { return c->max_datagrams; }

@@ -65,7 +65,8 @@ EXPORTS = ["rtps_rx_create", "rtps_rx_destroy", "rtps_rx_set_stream", "rtps_rx_s
            "rtps_rx_generate", "rtps_rx_bucket_by_writer", "rtps_rx_set_spec_hint", "rtps_rx_cdr_decode",
            "rtps_rx_bucket_by_writer_padded", "rtps_rx_frag_assemble", "rtps_rx_frag_reset",
            "rtps_rx_bucket_descriptors", "rtps_rx_ingest", "rtps_rx_ingest_reset", "rtps_udp_open", "rtps_udp_close",
-           "rtps_udp_port", "rtps_udp_backend", "rtps_udp_recv_batch", "rtps_udp_release", "rtps_udp_send_batch"]
+           "rtps_udp_port", "rtps_udp_backend", "rtps_udp_recv_batch", "rtps_udp_release", "rtps_udp_send_batch",
+           "rtps_rx_pump"]
 
 
 def lib():

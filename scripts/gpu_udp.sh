@@ -1,7 +1,7 @@
 #!/bin/bash
 # UDP receive -> zero-copy GPU parse: parity tests, then the C1 loopback bench leg.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out; export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_udp_gpu.py tests/test_udp.py -x -v --timeout 120 --timeout-method thread \
+timeout -k 10 300 python -u -m pytest tests/test_udp_gpu.py tests/test_pump_gpu.py tests/test_udp.py -x -v --timeout 120 --timeout-method thread \
   > gpurun_out/pytest_udp.log 2>&1; rc=$?
 tail -12 gpurun_out/pytest_udp.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python bench.py --workload C2 --steps 10 --no-cpu-baseline --no-e2e --no-cdr --no-frag --no-ingest \
