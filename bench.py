@@ -255,7 +255,7 @@ def hello_world_datagrams(n):
     return a.reshape(-1), (np.arange(n, dtype=np.uint64) * L), np.full(n, L, dtype=np.uint32)
 
 
-def c1_loopback(dev, stream, n=200_000, batch=16384):
+def c1_loopback(dev, stream, n=200_000, batch=16384, publishers=1):
     """Config C1 (BASELINE.json configs[0]): hello-world publisher -> subscriber over UDP
     loopback, 64-B samples.  Publisher: sendmmsg on a thread, flow-controlled to two batches
     ahead of the subscriber (an unthrottled loopback sender outruns any receiver: what gets
@@ -281,19 +281,25 @@ def c1_loopback(dev, stream, n=200_000, batch=16384):
     sent = [0]
     window = 2 * batch
 
-    send_s = [0.0, 0.0]  # time inside sendmmsg, time waiting on flow control
+    send_s = [0.0, 0.0]  # time inside sendmmsg, time waiting on flow control (summed over publishers)
+    lock = threading.Lock()
 
-    def sender():
+    def sender(p):
+        # publisher p of `publishers` sends chunks p, p+publishers, ... (one writer: with several
+        # publishers its SNs arrive out of order, none twice, so every sample is still accepted)
         chunk = 4096
-        for a in range(0, n, chunk):
+        for a in range(p * chunk, n, chunk * publishers):
             w0 = time.perf_counter()
             while sent[0] - live.datagrams > window:
                 time.sleep(0.0002)
             b = min(n, a + chunk)
             s0 = time.perf_counter()
-            sent[0] += udp.send_batch("127.0.0.1", rxu.port, data, off[a:b], ln[a:b])
-            send_s[0] += time.perf_counter() - s0
-            send_s[1] += s0 - w0
+            k = udp.send_batch("127.0.0.1", rxu.port, data, off[a:b], ln[a:b])
+            s1 = time.perf_counter()
+            with lock:
+                sent[0] += k
+                send_s[0] += s1 - s0
+                send_s[1] += s0 - w0
 
     decoded = [0]
 
@@ -302,12 +308,14 @@ def c1_loopback(dev, stream, n=200_000, batch=16384):
         decoded[0] += int((b.row_status[:m] == cdr.CDR_OK).sum().item())
         return False
 
-    ts = threading.Thread(target=sender, daemon=True)
+    ths = [threading.Thread(target=sender, args=(p,), daemon=True) for p in range(publishers)]
     t0 = time.perf_counter()
-    ts.start()
+    for t in ths:
+        t.start()
     st = pump.run(wait_ms=5, stop_after=n, idle_stop_ms=2000, on_batch=on_batch)
     wall = time.perf_counter() - t0
-    ts.join(timeout=5)
+    for t in ths:
+        t.join(timeout=5)
     received = st.datagrams
     busy = (st.last_ns - st.first_ns) / 1e9 if st.batches else float("nan")  # first batch .. last finished
     rxu.close()
@@ -320,7 +328,7 @@ def c1_loopback(dev, stream, n=200_000, batch=16384):
     return {"config": "C1: hello-world publisher -> subscriber over UDP loopback, 64-B HelloWorldData samples",
             "receive_backend": {udp.IO_URING: "io_uring", udp.IO_URING_SQPOLL: "io_uring+sqpoll",
                                 udp.RECVMMSG: "recvmmsg"}[rxu.backend],
-            "loop": "native rtps_rx_pump, 2 batches in flight",
+            "loop": "native rtps_rx_pump, 2 batches in flight", "publishers": publishers,
             "datagrams_built": n, "datagrams_sent": sent[0], "datagrams_received": received,
             "dropped": sent[0] - received, "batches": st.batches,
             "samples_accepted": st.accepted, "samples_decoded": decoded[0], "wall_s": wall, "stream_s": busy,
@@ -543,6 +551,9 @@ def main():
         result["ingest"] = ingest_leg(rx, arena, off_t, outs, n_rec, recs, n_matched_writers, stream, args.steps)
     if world == 1 and not args.no_c1:
         result["c1_loopback"] = c1_loopback(dev, stream)
+        # the same subscriber fed by 4 publisher threads: what the receive loop sustains when
+        # one sendmmsg thread (the C1 bound above) is not the limit
+        result["c1_loopback_4_publishers"] = c1_loopback(dev, stream, n=400_000, publishers=4)
     if world == 1 and not args.no_e2e:
         result["end_to_end"] = end_to_end(rx, arena, off_t, ln_t, n, outs, n_rec, stream)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
