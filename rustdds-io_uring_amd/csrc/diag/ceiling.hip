@@ -81,3 +81,67 @@ extern "C" int diag_copy(int mode, const uint8_t* arena, const uint64_t* off, ui
   else return -1;
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+
+// ---- variants of mode 0 (read head + write record) probing the attainable rate ----
+// HB: head bytes read (32/48/64); NTL/NTS: non-temporal loads / stores; PER: datagrams per lane
+template <int HB, bool NTL, bool NTS, int PER>
+__global__ __launch_bounds__(256) void ceil_var_kernel(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
+                                                       uint32_t n, u32x4* rec, uint8_t* status, uint32_t* rb) {
+  const uint32_t base = blockIdx.x * 256 * PER + threadIdx.x;
+  u32x4 a[PER], b[PER], c[PER], d[PER];
+  uint32_t L[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const uint32_t i = base + k * 256;
+    a[k] = b[k] = c[k] = d[k] = u32x4{0, 0, 0, 0};
+    L[k] = 0;
+    if (i < n) {
+      const u32x4* h = reinterpret_cast<const u32x4*>(arena + off[i]);
+      L[k] = len[i];
+      if (NTL) {
+        a[k] = __builtin_nontemporal_load(h);
+        b[k] = __builtin_nontemporal_load(h + 1);
+        if (HB >= 48) c[k] = __builtin_nontemporal_load(h + 2);
+        if (HB >= 64) d[k] = __builtin_nontemporal_load(h + 3);
+      } else {
+        a[k] = h[0];
+        b[k] = h[1];
+        if (HB >= 48) c[k] = h[2];
+        if (HB >= 64) d[k] = h[3];
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const uint32_t i = base + k * 256;
+    if (i >= n) continue;
+    a[k][1] ^= L[k];
+    status[i] = (uint8_t)(a[k][0] ^ b[k][0] ^ c[k][0] ^ d[k][0]);
+    rb[i] = i;
+    u32x4* r = rec + (uint64_t)i * 4;
+    if (NTS) {
+      __builtin_nontemporal_store(a[k], r);
+      __builtin_nontemporal_store(b[k], r + 1);
+      __builtin_nontemporal_store(c[k], r + 2);
+      __builtin_nontemporal_store(d[k], r + 3);
+    } else {
+      r[0] = a[k]; r[1] = b[k]; r[2] = c[k]; r[3] = d[k];
+    }
+  }
+}
+extern "C" int diag_ceiling_var(int hb, int ntl, int nts, int per, const uint8_t* arena, const uint64_t* off,
+                                const uint32_t* len, uint32_t n, void* rec, uint8_t* status, uint32_t* rb,
+                                void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  dim3 b(256);
+#define V(HB, L, S, P)                                                                                   \
+  if (hb == HB && ntl == L && nts == S && per == P) {                                                    \
+    hipLaunchKernelGGL((ceil_var_kernel<HB, L, S, P>), dim3((n + 256 * P - 1) / (256 * P)), b, 0, s, arena, off, \
+                       len, n, (u32x4*)rec, status, rb);                                                 \
+    return hipGetLastError() == hipSuccess ? 0 : -2;                                                     \
+  }
+  V(64, 0, 0, 1) V(48, 0, 0, 1) V(32, 0, 0, 1) V(64, 1, 0, 1) V(64, 0, 1, 1) V(64, 1, 1, 1) V(48, 1, 1, 1)
+  V(64, 0, 0, 2) V(64, 0, 0, 4) V(48, 0, 1, 2) V(64, 1, 1, 2)
+#undef V
+  return -1;
+}
