@@ -331,10 +331,87 @@ constexpr uint32_t BMW = 1024;  // LDS bitmap words per wave: buffers of up to 3
 
 __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); }
 
+// The common run, decided without stepping: one new buffer (nothing carried
+// over), at most 64 records, each a single fragment of the writer's size with
+// the buffer's data size, all fragment numbers distinct and inside the
+// buffer.  Every record then sets one new bit, so the buffer completes at the
+// count-th record: with m <= count records it is complete iff m == count
+// (is_complete at the last record), else pending with exactly these bits.
+// The same outcome as walk_run_wave's replay below (which handles the rest);
+// returns false, having written nothing but LDS, when the run is not of this
+// form.
+__device__ bool walk_run_regular(const WalkArgs& A, uint64_t p0, uint64_t p1, uint32_t lane, uint32_t* bm,
+                                 const uint32_t g[4], int64_t sn, uint32_t F) {
+  const uint64_t p = p0 + lane;
+  const bool act = p < p1;
+  uint32_t ri = 0, fs = 1, fis = 1, fsz = F, dsz = 0, fl = 0;
+  if (act) {
+    ri = A.svals[p];
+    const rtps_record* r = A.recs + ri;
+    fs = r->u.frag.frag_start;
+    fis = r->u.frag.frags_in_sub;
+    fsz = r->u.frag.frag_size;
+    dsz = r->u.frag.data_size;
+    fl = r->flags;
+  }
+  const uint32_t ds0 = rl(dsz, 0);
+  const uint32_t count = ds0 / F + (ds0 % F > 0);  // AssemblyBuffer::new with the first record (fsz == F)
+  const uint32_t m = (uint32_t)(p1 - p0);
+  const uint64_t bit = (uint64_t)fs - 1;
+  const bool bad = act && (fis != 1 || fsz != F || dsz != ds0 || fs == 0 || bit >= count);
+  if (__any(bad) || m > count || count > BMW * 32) return false;
+  for (uint32_t w = lane; w < (count + 31) / 32; w += 64) bm[w] = 0u;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  bool dup = false;
+  if (act) dup = ((atomicOr(&bm[bit / 32], 1u << (bit & 31)) >> (bit & 31)) & 1u) != 0;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (__any(dup)) return false;  // a repeated fragment: replay in order
+  uint32_t e0 = NONE;
+  if (lane == 0) e0 = new_epoch(A, g, sn, (uint32_t)p0, (uint32_t)p0, (uint32_t)p1);
+  const uint32_t e = rl(e0, 0);
+  if (act) A.pos_epoch[p] = e;
+  if (m == count) {  // is_complete at the last record -> emit
+    const uint32_t rlast = rl(ri, m - 1), flast = rl(fl, m - 1);
+    if (lane == 0) {
+      Epoch& E = A.epochs[e];
+      E.data_size = ds0; E.count = count; E.nset = m; E.F = F; E.eflags = 0; E.state = E_DONE;
+      E.done_rec = rlast; E.rec_flags = flast; E.old_pend = NONE;
+      A.dmark[rlast] = e;
+      epoch_done(A, e);
+    }
+    return true;
+  }
+  // still incomplete: its bitmap goes to the pool for the pending store
+  uint64_t bits = 0;
+  bool got = true;
+  if (lane == 0) {
+    Epoch& E = A.epochs[e];
+    E.count = count;
+    got = alloc_bits(A, E);
+    bits = E.bits;
+  }
+  got = rl(got ? 1u : 0u, 0) != 0;
+  const uint64_t b = ((uint64_t)rl((uint32_t)(bits >> 32), 0) << 32) | rl((uint32_t)bits, 0);
+  if (got) {
+    for (uint32_t w = lane; w < (count + 31) / 32; w += 64) A.pool[b + w] = bm[w];
+    if (lane == 0) {
+      Epoch& E = A.epochs[e];
+      E.data_size = ds0; E.count = count; E.nset = m; E.F = F; E.eflags = 0; E.state = E_PENDING;
+      E.done_rec = NONE; E.rec_flags = 0; E.old_pend = NONE;
+      epoch_done(A, e);
+    }
+  }
+  return true;
+}
+
 // One key run replayed by a wave: each lane loads one record's fields, the
 // wave steps through them in order with the fragment bitmap in LDS.  Runs that
 // mix keys or need a bigger bitmap fall back to walk_run_serial on lane 0.
 __device__ void walk_run_wave(const WalkArgs& A, uint64_t p0, uint64_t p1, uint32_t lane, uint32_t* bm) {
+#if defined(ABL_WALK) && ABL_WALK == 2
+  if (p1 == 0x7fffffffffffull) A.seen[p0] = 1;
+  return;
+#endif
   const rtps_record* r0 = A.recs + A.svals[p0];
   uint32_t g[4];
   guid_of(r0, g);
@@ -361,6 +438,7 @@ __device__ void walk_run_wave(const WalkArgs& A, uint64_t p0, uint64_t p1, uint3
   }
   const uint32_t ws = wslot_find(A.wkey, writer_hash(g));
   const uint32_t F = ws == NONE ? 0u : (A.wF[ws] & 0xffffu);
+  if (j == NONE && p1 - p0 <= 64 && F != 0 && walk_run_regular(A, p0, p1, lane, bm, g, sn, F)) return;
   uint32_t e = NONE, nset = 0, count = 0, ds = 0, eflags = 0, old_pend = NONE;
   bool started = false;
   if (j != NONE) {  // continue the buffer carried over from the previous batch
@@ -398,7 +476,10 @@ __device__ void walk_run_wave(const WalkArgs& A, uint64_t p0, uint64_t p1, uint3
       fl = r->flags;
     }
     uint32_t my_e = NONE;
-    const uint32_t m = (uint32_t)min<uint64_t>(64, p1 - c);
+    uint32_t m = (uint32_t)min<uint64_t>(64, p1 - c);
+#if defined(ABL_WALK) && ABL_WALK == 1
+    m = 0;
+#endif
     for (uint32_t jj = 0; jj < m; ++jj) {
       const uint32_t rj = rl(ri, jj), fsj = rl(fs, jj), fz = rl(fisz, jj), dj = rl(dsz, jj);
       const uint32_t fis = fz & 0xffffu, fsz = fz >> 16;
@@ -596,11 +677,21 @@ __global__ __launch_bounds__(FT) void k_init(const Epoch* ep, const uint32_t* sp
 
 __device__ __forceinline__ uint4 ld16(const uint8_t* p) { uint4 v; __builtin_memcpy(&v, p, 16); return v; }
 __device__ __forceinline__ void st16(uint8_t* p, uint4 v) { __builtin_memcpy(p, &v, 16); }
+// the same store through a global (not flat) address: heap and pending store are device memory
+typedef __attribute__((address_space(1))) uint4 g_u4 __attribute__((aligned(1)));
+__device__ __forceinline__ void gst16(uint8_t* p, uint4 v) {
+#if defined(__HIP_DEVICE_COMPILE__)  // the host pass only type-checks device functions
+  *(g_u4*)(uintptr_t)p = v;
+#else
+  __builtin_memcpy(p, &v, 16);
+#endif
+}
 
 // regular epochs: every record writes its fragments' span.  A wave takes 64
 // sorted positions: each lane resolves one record (epoch, source, destination,
 // lengths), then the wave copies the 64 spans one after the other, 16 B per
 // lane (spans of one sample are adjacent in the heap).
+constexpr uint32_t SPAN_U = 6;  // 16-B loads in flight per lane in the span copy (1536 B per record per pass)
 __global__ __launch_bounds__(FT) void k_span(const rtps_record* recs, const uint8_t* arena, uint64_t arena_len,
                                              const uint64_t* dgram_off, const uint32_t* svals,
                                              const uint32_t* pos_epoch, const uint32_t* skeys, uint64_t max,
@@ -629,21 +720,46 @@ __global__ __launch_bounds__(FT) void k_span(const rtps_record* recs, const uint
         }
       }
     }
+    // four records at a time, one per quarter-wave: 16 lanes x 16 B = 256 B per
+    // instruction per record, SPAN_U loads in flight per lane before the stores
     uint64_t todo = __ballot(live);
+    const uint32_t q = lane >> 4, ql = lane & 15u;
     while (todo) {
-      const uint32_t j = (uint32_t)__builtin_ctzll(todo);
-      todo &= todo - 1;
-      const uint64_t sj = ((uint64_t)rl((uint32_t)(src >> 32), j) << 32) | rl((uint32_t)src, j);
-      uint8_t* d = (uint8_t*)(((uint64_t)rl((uint32_t)(dst >> 32), j) << 32) | rl((uint32_t)dst, j));
-      const uint32_t nvj = rl(nv, j), nj = rl(n, j);
+      uint32_t js[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        js[k] = todo ? (uint32_t)__builtin_ctzll(todo) : 64u;
+        todo &= todo - 1;
+      }
+      const uint32_t j = q == 0 ? js[0] : q == 1 ? js[1] : q == 2 ? js[2] : js[3];
+      const uint32_t jj = j & 63u;
+      const uint64_t sj = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(src >> 32), (int)jj, 64) << 32) |
+                          (uint32_t)__shfl((int)(uint32_t)src, (int)jj, 64);
+      const uint64_t dj = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(dst >> 32), (int)jj, 64) << 32) |
+                          (uint32_t)__shfl((int)(uint32_t)dst, (int)jj, 64);
+      // every lane takes part in each __shfl (a lane left out of the permute supplies no value)
+      const uint32_t nv_all = (uint32_t)__shfl((int)nv, (int)jj, 64);
+      const uint32_t n_all = (uint32_t)__shfl((int)n, (int)jj, 64);
+      const uint32_t nvj = j < 64u ? nv_all : 0u;
+      const uint32_t nj = j < 64u ? n_all : 0u;
       const uint8_t* sp = arena + sj;
-      for (uint32_t b = 16u * lane; b < nj; b += 1024u) {
-        if (b + 16 <= nvj) {
-          st16(d + b, ld16(sp + b));
-        } else if (b + 16 <= nj && b >= nvj) {
-          st16(d + b, make_uint4(0, 0, 0, 0));
-        } else {
-          for (uint32_t t = b; t < b + 16 && t < nj; ++t) d[t] = t < nvj ? sp[t] : (uint8_t)0;
+      uint8_t* d = (uint8_t*)dj;
+      for (uint32_t b0 = 16u * ql; b0 < nj; b0 += 256u * SPAN_U) {
+        uint4 v[SPAN_U];
+#pragma unroll
+        for (uint32_t k = 0; k < SPAN_U; ++k) {
+          const uint32_t b = b0 + 256u * k;
+          v[k] = make_uint4(0, 0, 0, 0);
+          if (b + 16 <= nvj) v[k] = ld16(sp + b);
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < SPAN_U; ++k) {
+          const uint32_t b = b0 + 256u * k;
+          if (b + 16 <= nj && (b + 16 <= nvj || b >= nvj)) {
+            gst16(d + b, v[k]);  // payload, or zeros past a short payload
+          } else if (b < nj) {
+            for (uint32_t t = b; t < b + 16 && t < nj; ++t) d[t] = t < nvj ? sp[t] : (uint8_t)0;
+          }
         }
       }
     }
