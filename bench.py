@@ -366,6 +366,8 @@ def main():
     ap.add_argument("--workload", default="T", choices=sorted(rtps_rx.WORKLOADS))
     ap.add_argument("--datagrams", type=int, default=1 << 20, help="datagrams per GPU")
     ap.add_argument("--writers", type=int, default=16)
+    ap.add_argument("--spec-hint", type=int, default=None,
+                    help="rtps_rx_set_spec_hint (records per datagram; 0 = mixed traffic, chained launch)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-e2e", action="store_true")
@@ -414,6 +416,8 @@ def main():
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     rx.set_stream(stream)
+    if args.spec_hint is not None:
+        rx.set_spec_hint(args.spec_hint)
     arena = torch.empty(size, dtype=torch.uint8, device=dev)
     off_t = torch.from_numpy(off.view(np.int64)).to(dev)
     ln_t = torch.from_numpy(ln.view(np.int32)).to(dev)

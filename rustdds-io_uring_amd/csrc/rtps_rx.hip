@@ -66,6 +66,8 @@ struct KParams {
   const uint16_t* mt_slots;
   uint32_t mt_mask;           // capacity - 1
   uint64_t* scratch;          // per-tile counts / prefixes (Scratch)
+  uint64_t* chain;            // per-tile look-back words (chained launch only), zeroed before it
+  uint32_t* mixed_out;        // pinned host [2]: tiles of the batch not uniform k_spec, tiles (launch choice)
 };
 
 // ---------------------------------------------------------------------------
@@ -644,10 +646,10 @@ struct TileCtx {
 
 // load this lane's (offset, length), build the wave's buffer descriptor
 // (base = min offset over the wave: no workgroup barrier) and the 64-byte head
-__device__ __forceinline__ void load_tile(const KParams& p, uint32_t tile, TileCtx& t) {
+__device__ __forceinline__ void load_tile(const KParams& p, uint32_t tile, TileCtx& t, bool enabled = true) {
   const uint32_t tid = threadIdx.x;
   t.i = tile * TILE + tid;
-  t.valid = t.i < p.n;
+  t.valid = enabled && t.i < p.n;
   const uint64_t off = t.valid ? p.dgram_off[t.i] : ~0ull;
   t.L = t.valid ? p.dgram_len[t.i] : 0u;
   uint64_t m = off;
@@ -690,8 +692,13 @@ __device__ __forceinline__ uint32_t count_lane(const KParams& p, TileCtx& t, uin
 // scratch layout (all written before being read in every launch, except flag[]):
 //   u32 flag[4]          flag[parity] = 1 if any tile of the launch is non-speculative
 //                        (plain stores of the same value); kernel B clears flag[parity ^ 1]
-//   u32 info[n_tiles]    records of the tile | nonspec << 31
+//   u32 info[n_tiles]    see below
 //   u16 dcount[n]        records per datagram, written for non-speculative tiles only
+// info[tile] = records | INFO_NONSPEC (B must account per datagram) | INFO_WRITTEN (the
+// chained kernel already wrote the tile at its exact position: B only counts it) |
+// INFO_MIXED (some datagram does not have k_spec records: sizes the next launch's choice)
+constexpr uint32_t INFO_NONSPEC = 0x80000000u, INFO_WRITTEN = 0x40000000u, INFO_MIXED = 0x20000000u,
+                   INFO_COUNT = 0x1fffffffu;
 struct Scratch {
   uint32_t* flag;
   uint32_t* info;
@@ -732,7 +739,7 @@ __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_spec_ker
   }
   Scratch x = scratch_of(p.scratch, n_tiles);
   if (tid == 0) {
-    x.info[tile] = agg | (nonspec << 31);  // read by kernel B (next launch)
+    x.info[tile] = agg | (nonspec ? INFO_NONSPEC | INFO_MIXED : 0u);  // read by kernel B (next launch)
     if (nonspec) x.flag[parity] = 1u;
   }
   if (t.valid) {
@@ -763,7 +770,8 @@ __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_spec_ker
   }
 }
 
-// sum of info[lo, hi) counts and min non-speculative index, over the workgroup
+
+// sum of info[lo, hi) counts and the first tile B must walk, over the workgroup
 __device__ __forceinline__ void reduce_info(const uint32_t* info, uint32_t lo, uint32_t hi, uint64_t* s_sum,
                                             uint32_t* s_min, uint64_t& sum, uint32_t& first_bad) {
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
@@ -771,8 +779,8 @@ __device__ __forceinline__ void reduce_info(const uint32_t* info, uint32_t lo, u
   uint32_t fb = 0xffffffffu;
   for (uint32_t t = lo + tid; t < hi; t += TILE) {
     uint32_t v = info[t];
-    acc += v & 0x7fffffffu;
-    if ((v >> 31) && t < fb) fb = t;
+    acc += v & INFO_COUNT;
+    if ((v & (INFO_NONSPEC | INFO_WRITTEN)) == INFO_NONSPEC && t < fb) fb = t;
   }
 #pragma unroll
   for (uint32_t d = 32; d >= 1; d >>= 1) {
@@ -806,13 +814,30 @@ __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_fix_kern
   if (blockIdx.x == 0 && tid == 0) x.flag[parity ^ 1u] = 0u;  // for the next launch
   if (__builtin_amdgcn_readfirstlane(x.flag[parity]) == 0u) {
     // every tile was speculative: every datagram has exactly k_spec records
-    if (blockIdx.x == 0 && tid == 0) *p.n_records = (uint64_t)p.n * k_spec;
+    if (blockIdx.x == 0 && tid == 0) {
+      *p.n_records = (uint64_t)p.n * k_spec;
+      p.mixed_out[0] = 0u;
+      p.mixed_out[1] = n_tiles;
+    }
     return;
   }
   uint64_t total;
   uint32_t first;
   reduce_info(x.info, 0, n_tiles, s_rsum, s_rmin, total, first);
-  if (blockIdx.x == 0 && tid == 0) *p.n_records = total;
+  if (blockIdx.x == 0) {
+    uint32_t mixed = 0;
+    for (uint32_t t = tid; t < n_tiles; t += TILE) mixed += (x.info[t] & INFO_MIXED) != 0u;
+#pragma unroll
+    for (uint32_t d = 32; d >= 1; d >>= 1) mixed += __shfl_xor(mixed, d, 64);
+    if (lane == 0) s_wave_sum[wave] = mixed;
+    __syncthreads();
+    if (tid == 0) {
+      *p.n_records = total;
+      p.mixed_out[0] = s_wave_sum[0] + s_wave_sum[1] + s_wave_sum[2] + s_wave_sum[3];
+      p.mixed_out[1] = n_tiles;
+    }
+    __syncthreads();  // s_wave_sum reuse below
+  }
   if (first > n_tiles) first = n_tiles;
   uint32_t tile = first + blockIdx.x;
   if (tile >= n_tiles) return;
@@ -827,7 +852,8 @@ __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_fix_kern
     // non-speculative tiles stored their per-datagram counts; speculative tiles
     // (after the first non-speculative one) have exactly k_spec per datagram
     uint32_t cnt = 0;
-    if (i < p.n) cnt = (info >> 31) ? (uint32_t)x.dcount[i] : k_spec;
+    if (i < p.n) cnt = (info & INFO_NONSPEC) ? (uint32_t)x.dcount[i] : k_spec;
+    const bool skip = (info & INFO_WRITTEN) != 0;  // written in place by the chained kernel
     const uint32_t incl = wave_incl_scan(cnt, lane);
     if (lane == 63) s_wave_sum[wave] = incl;
     __syncthreads();
@@ -837,7 +863,7 @@ __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_fix_kern
       if (w < wave) wave_off += s_wave_sum[w];
     const uint64_t my_first = prefix + wave_off + (incl - cnt);
     TileCtx t;
-    load_tile(p, tile, t);
+    load_tile(p, tile, t, !skip);
     if (t.valid) {
       if (p.rec_begin) p.rec_begin[t.i] = (uint32_t)my_first;
       if (cnt) {  // cnt > 0 implies status OK
@@ -856,6 +882,127 @@ __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_fix_kern
     reduce_info(x.info, tile, next, s_rsum, s_rmin, dummy_sum, dummy_min);
     prefix += dummy_sum;
     tile = next;
+  }
+}
+
+// Chained single launch for mixed traffic (C3: every tile non-speculative).
+// One workgroup per tile: count walk, publish the tile's record count, find the
+// tile's exact prefix from the predecessors' published counts, then the
+// writing walk at the exact position while the tile's lines are still in cache.
+// Prefixes are two-level so that a tile needs about two polls, not one per 64
+// predecessors: tiles form groups of 64; the last tile of a group to publish
+// (an arrival counter per group) sums the group and publishes the group total.
+// A tile's prefix = the totals of the earlier groups + the counts of the
+// earlier tiles of its group.  Every exchanged word is an agent-scope 8-byte
+// {state, value} word (no fences: a reader polls until the state is set).  A
+// tile that gives up waiting (a predecessor that never published: only if the
+// dispatcher ran tiles far out of order) stays unwritten and kernel B, launched
+// after it as always, walks it: results never depend on dispatch order or
+// timing.  chain[] (tile words, group words, group counters) is zeroed before
+// the launch.
+constexpr uint64_t CH_READY = 1ull << 62, CH_VAL = (1ull << 62) - 1;
+constexpr uint32_t CH_GROUP = 64;
+constexpr uint32_t CH_SPIN_LIMIT = 1u << 14;
+__host__ __device__ constexpr size_t chain_words(uint32_t tiles) {  // tile words, group words, group counters
+  return (size_t)tiles + 2 * (((size_t)tiles + CH_GROUP - 1) / CH_GROUP) + 2;
+}
+__device__ __forceinline__ uint64_t ch_load(const uint64_t* w) {
+  return __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void ch_store(uint64_t* w, uint64_t v) {
+  __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// sum of the CH_VAL parts of words w[0, n), n <= 64 (one per lane), polling until
+// every one is ready; false after CH_SPIN_LIMIT polls
+__device__ __forceinline__ bool ch_sum_ready(const uint64_t* w, uint32_t n, uint32_t lane, uint64_t& sum) {
+  for (uint32_t spins = 0;; ++spins) {
+    const uint64_t v = lane < n ? ch_load(w + lane) : CH_READY;
+    if (__all((v & CH_READY) != 0)) {
+      uint64_t x = v & CH_VAL;
+#pragma unroll
+      for (uint32_t d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+      sum = x;
+      return true;
+    }
+    if (spins >= CH_SPIN_LIMIT) return false;
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+__global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_chain_kernel(KParams p, uint32_t n_tiles,
+                                                                                      uint32_t k_spec, uint32_t parity) {
+  __shared__ uint32_t s_wave_bad[WAVES];
+  __shared__ uint32_t s_wave_sum[WAVES];
+  __shared__ uint64_t s_excl;
+  __shared__ uint32_t s_ok;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t tile = blockIdx.x;
+  mt_stage(p);  // visible after the __syncthreads below, before the writing walk
+  TileCtx t;
+  load_tile(p, tile, t);
+  uint32_t cnt;
+  const uint32_t st = count_lane(p, t, cnt);
+  const uint32_t incl = wave_incl_scan(cnt, lane);
+  const uint64_t bad = __ballot(t.valid && cnt != k_spec);
+  if (lane == 63) { s_wave_sum[wave] = incl; s_wave_bad[wave] = bad != 0ull; }
+  __syncthreads();
+  uint32_t wave_off = 0, agg = 0, mixed = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < WAVES; ++w) {
+    const uint32_t v = s_wave_sum[w];
+    if (w < wave) wave_off += v;
+    agg += v;
+    mixed |= s_wave_bad[w];
+  }
+  Scratch x = scratch_of(p.scratch, n_tiles);
+  if (t.valid) {
+    p.status[t.i] = (uint8_t)st;
+    x.dcount[t.i] = (uint16_t)cnt;
+  }
+  if (wave == 0) {
+    const uint32_t n_groups = (n_tiles + CH_GROUP - 1) / CH_GROUP;
+    uint64_t* tw = p.chain;                 // [n_tiles] tile counts
+    uint64_t* gw = p.chain + n_tiles;       // [n_groups] group totals
+    uint64_t* gc = gw + n_groups;           // [n_groups] arrival counters
+    const uint32_t g = tile / CH_GROUP, r = tile % CH_GROUP;
+    const uint32_t g_size = min(CH_GROUP, n_tiles - g * CH_GROUP);
+    uint64_t excl = 0, part = 0;
+    bool ok = true;
+    uint64_t arrived = 0;
+    if (lane == 0) {
+      ch_store(tw + tile, CH_READY | agg);
+      arrived = __hip_atomic_fetch_add(gc + g, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+    }
+    arrived = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(arrived >> 32)) << 32) |
+              __builtin_amdgcn_readfirstlane((uint32_t)arrived);
+    if (arrived == g_size) {  // last of its group: publish the group total
+      uint64_t gsum = 0;
+      ok = ch_sum_ready(tw + g * CH_GROUP, g_size, lane, gsum);
+      if (ok && lane == 0) ch_store(gw + g, CH_READY | gsum);
+    }
+#ifndef ABL_NO_LOOKBACK
+    for (uint32_t g0 = 0; ok && g0 < g; g0 += 64) {  // totals of the earlier groups
+      ok = ch_sum_ready(gw + g0, min(64u, g - g0), lane, part);
+      excl += part;
+    }
+    if (ok && r) {  // counts of the earlier tiles of its group
+      ok = ch_sum_ready(tw + g * CH_GROUP, r, lane, part);
+      excl += part;
+    }
+#endif
+    if (lane == 0) {
+      s_excl = excl;
+      s_ok = ok ? 1u : 0u;
+      x.info[tile] = agg | INFO_NONSPEC | (ok ? INFO_WRITTEN : 0u) | (mixed ? INFO_MIXED : 0u);  // read by B
+      if (tile == 0) x.flag[parity] = 1u;  // B never takes its all-speculative exit
+    }
+  }
+  __syncthreads();
+  if (!s_ok || !t.valid) return;
+  const uint64_t my_first = s_excl + wave_off + (incl - cnt);
+  if (p.rec_begin) p.rec_begin[t.i] = (uint32_t)my_first;
+  if (cnt) {
+    uint32_t n2;
+    walk<true>(p, t.s, t.H, t.L, t.i, my_first, n2);
   }
 }
 
@@ -1026,6 +1173,8 @@ struct rtps_rx_ctx {
   FragState* frag = nullptr;  // DataFrag reassembly state (created on first use)
   IngestState* ingest = nullptr;  // history-cache ingest state (created on first use)
   uint32_t mt_n = 0;              // match-table entries
+  uint64_t* chain = nullptr;      // look-back words of the chained launch [chain_words(tiles) + 2]
+  uint32_t* mixed = nullptr;      // pinned: {mixed tiles, tiles} of the last finished batch (kernel B)
 };
 
 static int hip_fail(hipError_t e) { return e == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP; }
@@ -1054,11 +1203,18 @@ int rtps_rx_create(const rtps_rx_config* cfg, rtps_rx_ctx** out_ctx) {
   // u32 flag[4] | u32 info[tiles rounded to 4] | u16 dcount[max_datagrams]
   c->scratch_words = 2 + ((tiles + 3) & ~(size_t)3) / 2 + ((size_t)cfg->max_datagrams + 3) / 4 + 2;
   if (hipMalloc(&c->scratch, c->scratch_words * sizeof(uint64_t)) != hipSuccess ||
-      hipMemset(c->scratch, 0, c->scratch_words * sizeof(uint64_t)) != hipSuccess) {
+      hipMemset(c->scratch, 0, c->scratch_words * sizeof(uint64_t)) != hipSuccess ||
+      hipMalloc(&c->chain, (chain_words((uint32_t)tiles) + 2) * sizeof(uint64_t)) != hipSuccess ||
+      hipHostMalloc(&c->mixed, 2 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
+    (void)hipFree(c->scratch);
+    (void)hipFree(c->chain);
+  if (c->mixed) (void)hipHostFree(c->mixed);
+  (void)hipFree(c->chain);
     (void)hipStreamDestroy(c->own_stream);
     delete c;
     return RTPS_RX_ENOMEM;
   }
+  c->mixed[0] = c->mixed[1] = 0u;
   *out_ctx = c;
   return RTPS_RX_OK;
 }
@@ -1169,9 +1325,26 @@ int rtps_rx_parse_batch(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len
   const uint32_t parity = c->launch_parity;
   const uint32_t mt_lds = (c->mt_active && c->mt_cap <= MT_LDS) ? mt_lds_bytes(c->mt_cap) : 0u;
   c->launch_parity ^= 1u;
-  hipLaunchKernelGGL(rtps_parse_spec_kernel, dim3(tiles), dim3(TILE), mt_lds, c->stream, p, tiles, c->k_spec, parity);
+  p.chain = c->chain;
+  p.mixed_out = c->mixed;
+  // Launch choice, a performance decision only (both give the same output): a
+  // chained single pass when the spec hint is 0, or when most tiles of the last
+  // finished batch were mixed (B reports that to pinned memory; read without a sync,
+  // so it may lag a batch); else the speculative pass.
+  const uint32_t mixed = __atomic_load_n(&c->mixed[0], __ATOMIC_RELAXED);
+  const uint32_t seen = __atomic_load_n(&c->mixed[1], __ATOMIC_RELAXED);
+  const bool chain = c->k_spec == 0 || (seen >= 16u && 2u * mixed > seen);
+  const uint32_t k = c->k_spec ? c->k_spec : 1u;
+  if (chain) {  // one chained pass, B only finishes (n_records, stragglers)
+    if (hipMemsetAsync(c->chain, 0, ((chain_words(tiles) * 8 + 15) & ~(size_t)15), c->stream) != hipSuccess)
+      return RTPS_RX_EHIP;
+    hipLaunchKernelGGL(rtps_parse_chain_kernel, dim3(tiles), dim3(TILE), mt_lds, c->stream, p, tiles, k, parity);
+  } else {
+    hipLaunchKernelGGL(rtps_parse_spec_kernel, dim3(tiles), dim3(TILE), mt_lds, c->stream, p, tiles, c->k_spec,
+                       parity);
+  }
   uint32_t grid = tiles < c->resident_blocks ? tiles : c->resident_blocks;
-  hipLaunchKernelGGL(rtps_parse_fix_kernel, dim3(grid), dim3(TILE), mt_lds, c->stream, p, tiles, c->k_spec, parity);
+  hipLaunchKernelGGL(rtps_parse_fix_kernel, dim3(grid), dim3(TILE), mt_lds, c->stream, p, tiles, k, parity);
   return hip_fail(hipGetLastError());
 }
 

@@ -249,6 +249,29 @@ def test_full_size_parity(rx, wl, name):
         assert (u[:, 1] == (980 if wl == 1 else 256)).all()
 
 
+@pytest.mark.parametrize("wl,name", [(3, "C3"), (1, "T")])
+def test_chained_launch_full_size(rx, wl, name):
+    """Spec hint 0 (mixed traffic): the chained look-back launch, bit-exact at 1M datagrams."""
+    n = 1 << 20
+    arena, off, ln = _device_gen(rx, wl, n)
+    rx.set_spec_hint(0)
+    try:
+        _parity(rx, arena, off, ln, f"{name}-1M-chained")
+    finally:
+        rx.set_spec_hint(1)
+
+
+def test_launch_choice_follows_traffic(rx):
+    """The speculative / chained choice follows the previous batch's mix (a lagging
+    hint): a mixed batch after mixed ones, a one-DATA batch after mixed ones (chained
+    with a stale hint), then one-DATA again; every batch bit-exact."""
+    c3 = oracle.gen(oracle.WL_C3, 16 * 256 + 77)
+    c2 = oracle.gen(oracle.WL_C2, 20 * 256 + 5)
+    for label, (a, o, l) in [("C3 first", c3), ("C3 again", c3), ("C2 after C3", c2), ("C2 again", c2),
+                             ("C3 after C2", c3)]:
+        _parity(rx, a, o, l, label)
+
+
 @pytest.mark.parametrize("world", [2, 3, 8])
 def test_bucket_by_writer_matches_reference(rx, world):
     from shard_ref import bucket_np
