@@ -530,7 +530,9 @@ def main():
         "roofline": {"bound": "hbm", "achieved": alg_total / (ev_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": alg_total / (ev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "traffic": traffic, "traffic_source": traffic_src,
-                     "kernel": "rtps_parse_spec_kernel + rtps_parse_fix_kernel (one launch pair)", "kernel_ms": ev_ms,
+                     "kernel": ("rtps_parse_spec_kernel (or rtps_parse_chain_kernel + its 16-B-aligned zeroing, chosen "
+                                "per batch from the traffic mix) + rtps_parse_fix_kernel: one rtps_rx_parse_batch"),
+                     "kernel_ms": ev_ms,
                      "alg_bytes_per_launch": alg_total, "alg_read_bytes": alg_reads, "alg_write_bytes": alg_writes,
                      "note": "zero-copy parse: payload bytes are not read (the reference's Bytes::split_off is "
                              "zero-copy too); alg bytes = header/fixed-field reads + record writes"},
