@@ -75,24 +75,41 @@ __device__ __forceinline__ uint32_t entry_of(const IngestTable& t, uint32_t a, u
   }
   return NONE;
 }
-// atomicOr(addr, m) for the active lanes, lanes that hit the same word first
-// combined (sequential SNs of a writer share bitmap words: without this, 32
-// same-address atomics per word).  Every lane of the wave must call it.
-__device__ __forceinline__ void wave_or(uint32_t* addr, uint32_t m, bool active) {
+// atomicOr(base[idx], m) for the active lanes, with every word's bits combined
+// across the wave first: one atomic per distinct word.  A writer's sequential
+// SNs share bitmap words (T: 4 lanes per word, 16 writers interleaved), while
+// mixed traffic has mostly distinct words (C3); a bitonic sort of the 64
+// (word, bits) pairs then a segmented OR over the runs of equal words costs a
+// fixed 21 + 12 shuffle steps for either.  Every lane of the wave must call it.
+__device__ __forceinline__ void wave_or(uint32_t* base, uint32_t* addr, uint32_t m, bool active) {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t a = (uint64_t)addr;
-  uint64_t todo = __ballot(active);
-  while (todo) {
-    const int leader = __builtin_ctzll(todo);
-    const uint64_t la = ((uint64_t)(uint32_t)__shfl((int)(a >> 32), leader, 64) << 32) |
-                        (uint32_t)__shfl((int)(uint32_t)a, leader, 64);
-    const bool mine = active && a == la;
-    uint32_t v = mine ? m : 0u;
+  uint32_t key = active ? (uint32_t)(addr - base) : 0xffffffffu;  // inactive lanes sort last
+  uint32_t v = active ? m : 0u;
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v |= (uint32_t)__shfl_xor((int)v, d, 64);
-    if (lane == (uint32_t)leader) atomicOr(addr, v);
-    todo &= ~__ballot(mine);
+  for (uint32_t k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      const uint32_t pk = (uint32_t)__shfl_xor((int)key, j, 64), pv = (uint32_t)__shfl_xor((int)v, j, 64);
+      const bool up = (lane & k) == 0, lower = (lane & j) == 0;
+      const bool take = lower == up ? pk < key : pk > key;
+      if (take) { key = pk; v = pv; }
+    }
   }
+  const uint32_t prev = (uint32_t)__shfl_up((int)key, 1, 64);
+  uint32_t start = (lane == 0 || prev != key) ? lane : 0u;  // first lane of this lane's run
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)start, d, 64);
+    if (lane >= d && y > start) start = y;
+  }
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)v, d, 64);
+    if (lane >= d && lane - d >= start) v |= y;
+  }
+  const uint32_t next = (uint32_t)__shfl_down((int)key, 1, 64);
+  const bool tail = lane == 63 || next != key;
+  if (key != 0xffffffffu && tail && v) atomicOr(base + key, v);
 }
 // first-cover key of record i in batch `epoch`: no reset between batches is needed
 __device__ __forceinline__ unsigned long long ekey(uint32_t epoch, uint32_t i) {
@@ -268,7 +285,7 @@ __global__ __launch_bounds__(IT) void k_marks_d(const uint64_t* n_rec, uint64_t 
         atomicMin(reinterpret_cast<unsigned long long*>(s.fc + (uint64_t)e * W) + off, ekey(epoch, (uint32_t)i));
       }
     }
-    if (gaps) wave_or(word, bit, act);  // the sample bitmap only serves k_marks_g
+    if (gaps) wave_or(s.dbits, word, bit, act);  // the sample bitmap only serves k_marks_g
   }
 }
 // then GAPs: a GAP's first-cover key matters only where a sample of the batch
@@ -356,7 +373,7 @@ __global__ __launch_bounds__(IT) void k_merge(const rtps_record* recs, const uin
     } else if (ev == EV_GAP) {
       gap_words(recs[i], arena, dgram_off, lo, [&](uint64_t w, uint32_t m) { atomicOr(bits + w, m); });
     }
-    wave_or(word, bit, act);
+    wave_or(s.bits, word, bit, act);
   }
 }
 
