@@ -12,8 +12,8 @@ for ex in descriptors records; do
     bench.py --gpus 2 --steps 10 --warmup 3 --backend gloo --datagrams 262144 --exchange $ex > gpurun_out/bench_n2_$ex.log 2>&1 || { echo "STOP bench n2 $ex"; tail -30 gpurun_out/bench_n2_$ex.log; exit 3; }
   python -c "import json; d=json.loads(open('gpurun_out/bench_n2_$ex.log').read().strip().splitlines()[-1]); print('$ex', d['value'], json.dumps(d['config']['exchange']), d['config']['received_records_rank0'])"
 done
-timeout -k 10 300 python bench.py --steps 20 --no-cpu-baseline --no-e2e --no-cdr --match none > gpurun_out/bench_nomatch.log 2>&1 && \
-timeout -k 10 300 python bench.py --steps 20 --no-cpu-baseline --no-e2e --no-cdr --match writers > gpurun_out/bench_match.log 2>&1 || exit 4
+timeout -k 10 300 python bench.py --steps 20 --no-cpu-baseline --no-e2e --no-cdr --no-c1 --no-ingest --match none > gpurun_out/bench_nomatch.log 2>&1 && \
+timeout -k 10 300 python bench.py --steps 20 --no-cpu-baseline --no-e2e --no-cdr --no-c1 --no-ingest --match writers > gpurun_out/bench_match.log 2>&1 || exit 4
 python -c "
 import json
 for f in ('nomatch','match'):
