@@ -68,6 +68,7 @@ struct KParams {
   uint64_t* scratch;          // per-tile counts / prefixes (Scratch)
   uint64_t* chain;            // per-tile look-back words (chained launch only), zeroed before it
   uint32_t* mixed_out;        // pinned host [2]: tiles of the batch not uniform k_spec, tiles (launch choice)
+  uint32_t ch_spin_limit;     // polls before a chained tile leaves itself to kernel B
 };
 
 // ---------------------------------------------------------------------------
@@ -914,7 +915,8 @@ __device__ __forceinline__ void ch_store(uint64_t* w, uint64_t v) {
 }
 // sum of the CH_VAL parts of words w[0, n), n <= 64 (one per lane), polling until
 // every one is ready; false after CH_SPIN_LIMIT polls
-__device__ __forceinline__ bool ch_sum_ready(const uint64_t* w, uint32_t n, uint32_t lane, uint64_t& sum) {
+__device__ __forceinline__ bool ch_sum_ready(const uint64_t* w, uint32_t n, uint32_t lane, uint32_t limit,
+                                             uint64_t& sum) {
   for (uint32_t spins = 0;; ++spins) {
     const uint64_t v = lane < n ? ch_load(w + lane) : CH_READY;
     if (__all((v & CH_READY) != 0)) {
@@ -924,7 +926,7 @@ __device__ __forceinline__ bool ch_sum_ready(const uint64_t* w, uint32_t n, uint
       sum = x;
       return true;
     }
-    if (spins >= CH_SPIN_LIMIT) return false;
+    if (spins >= limit) return false;
     __builtin_amdgcn_s_sleep(2);
   }
 }
@@ -976,16 +978,16 @@ __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_chain_ke
               __builtin_amdgcn_readfirstlane((uint32_t)arrived);
     if (arrived == g_size) {  // last of its group: publish the group total
       uint64_t gsum = 0;
-      ok = ch_sum_ready(tw + g * CH_GROUP, g_size, lane, gsum);
+      ok = ch_sum_ready(tw + g * CH_GROUP, g_size, lane, p.ch_spin_limit, gsum);
       if (ok && lane == 0) ch_store(gw + g, CH_READY | gsum);
     }
 #ifndef ABL_NO_LOOKBACK
     for (uint32_t g0 = 0; ok && g0 < g; g0 += 64) {  // totals of the earlier groups
-      ok = ch_sum_ready(gw + g0, min(64u, g - g0), lane, part);
+      ok = ch_sum_ready(gw + g0, min(64u, g - g0), lane, p.ch_spin_limit, part);
       excl += part;
     }
     if (ok && r) {  // counts of the earlier tiles of its group
-      ok = ch_sum_ready(tw + g * CH_GROUP, r, lane, part);
+      ok = ch_sum_ready(tw + g * CH_GROUP, r, lane, p.ch_spin_limit, part);
       excl += part;
     }
 #endif
@@ -1175,6 +1177,7 @@ struct rtps_rx_ctx {
   uint32_t mt_n = 0;              // match-table entries
   uint64_t* chain = nullptr;      // look-back words of the chained launch [chain_words(tiles) + 2]
   uint32_t* mixed = nullptr;      // pinned: {mixed tiles, tiles} of the last finished batch (kernel B)
+  uint32_t ch_spin_limit = CH_SPIN_LIMIT;
 };
 
 static int hip_fail(hipError_t e) { return e == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP; }
@@ -1327,6 +1330,7 @@ int rtps_rx_parse_batch(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len
   c->launch_parity ^= 1u;
   p.chain = c->chain;
   p.mixed_out = c->mixed;
+  p.ch_spin_limit = c->ch_spin_limit;
   // Launch choice, a performance decision only (both give the same output): a
   // chained single pass when the spec hint is 0, or when most tiles of the last
   // finished batch were mixed (B reports that to pinned memory; read without a sync,
@@ -1538,6 +1542,14 @@ int rtps_rx_ingest_reset(rtps_rx_ctx* c) {
 }
 
 uint32_t rtps_rx_record_size(void) { return (uint32_t)sizeof(rtps_record); }
+
+/* test hook (not part of the public header): polls before a chained tile gives up and
+   leaves itself to kernel B; 0 makes most tiles give up, exercising that fallback */
+int rtps_rx_debug_set_chain_spin_limit(rtps_rx_ctx* c, uint32_t limit) {
+  if (!c) return RTPS_RX_EINVAL;
+  c->ch_spin_limit = limit;
+  return RTPS_RX_OK;
+}
 
 /* diagnostics (not part of the public header): copy the first k scratch words */
 int rtps_rx_debug_scratch(rtps_rx_ctx* c, uint64_t* host, uint32_t k) {

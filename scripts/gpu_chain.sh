@@ -2,7 +2,7 @@
 # Chained look-back launch (spec hint 0) vs the two-launch parse: parity, then timings.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; R=$(pwd); mkdir -p gpurun_out; export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 200 --timeout-method thread \
-  -k "spec_hint or chained or workload_parity or golden or launch_choice" > gpurun_out/pytest_chain.log 2>&1; rc=$?
+  -k "spec_hint or chained or workload_parity or golden or launch_choice or fallback" > gpurun_out/pytest_chain.log 2>&1; rc=$?
 tail -4 gpurun_out/pytest_chain.log; [ $rc -eq 0 ] || exit $rc
 for wl in C3 T C2 C4; do for h in 1 0; do
   timeout -k 10 200 python bench.py --workload $wl --spec-hint $h --steps 30 --no-cpu-baseline --no-e2e --no-cdr --no-frag \

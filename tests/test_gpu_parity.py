@@ -261,6 +261,33 @@ def test_chained_launch_full_size(rx, wl, name):
         rx.set_spec_hint(1)
 
 
+@pytest.mark.parametrize("limit", [0, 1])
+def test_chained_fallback_to_fix_pass(rx, limit):
+    """Chained tiles that stop waiting for their predecessors (forced here with a
+    poll limit of 0 or 1) are left to kernel B: the output is still bit-exact."""
+    import ctypes
+    import rtps_rx
+    L = rtps_rx.lib()
+    L.rtps_rx_debug_set_chain_spin_limit.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+    a, o, l = oracle.gen(oracle.WL_C3, 200000)
+    rx.set_spec_hint(0)
+    assert L.rtps_rx_debug_set_chain_spin_limit(rx._h, limit) == 0
+    try:
+        _parity(rx, a, o, l, f"C3 chained, poll limit {limit}")
+        # scratch: u32 flag[4], then u32 info[tile] (INFO_WRITTEN = 1 << 30: written by the chained pass)
+        tiles = (len(l) + 255) // 256
+        words = 2 + (tiles + 1) // 2
+        buf = np.zeros(words, dtype=np.uint64)
+        L.rtps_rx_debug_scratch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]
+        assert L.rtps_rx_debug_scratch(rx._h, buf.ctypes.data, words) == 0
+        info = buf.view(np.uint32)[4:4 + tiles]
+        left = int(((info >> 30) & 1 == 0).sum())
+        assert left > 0, "no tile was left to kernel B: the fallback was not exercised"
+    finally:
+        L.rtps_rx_debug_set_chain_spin_limit(rx._h, 1 << 14)
+        rx.set_spec_hint(1)
+
+
 def test_launch_choice_follows_traffic(rx):
     """The speculative / chained choice follows the previous batch's mix (a lagging
     hint): a mixed batch after mixed ones, a one-DATA batch after mixed ones (chained
