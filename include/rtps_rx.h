@@ -212,7 +212,11 @@ int rtps_rx_sync(rtps_rx_ctx* ctx);
 /* Performance hint: the number of records most datagrams of the coming
  * batches produce (default 1: one DATA per datagram; 2 for INFO_TS+DATA).
  * Tiles of 256 datagrams that all match it are written in a single pass;
- * any other tile costs a second walk.  Results never depend on the hint. */
+ * any other tile costs a second walk.  When most tiles of the previous batch
+ * did not match, the context switches by itself to a chained pass made for
+ * mixed traffic (each tile counts, learns its exact position from its
+ * predecessors, then writes); 0 selects that pass always.  Results never
+ * depend on the hint. */
 int rtps_rx_set_spec_hint(rtps_rx_ctx* ctx, uint32_t records_per_datagram);
 const char* rtps_rx_strerror(int code);
 
