@@ -190,13 +190,17 @@ struct Pump {
       uint32_t k = 0;
       for (; k < n; ++k) {
         const uint32_t L = s.len[k];
-        const uint64_t r = (L >= 20 && L <= 65536u) ? (L - 20u) / 4u : 0u;
+        const uint64_t r = (L >= 20 && L <= RTPS_MAX_DATAGRAM) ? (L - 20u) / 4u : 0u;  // rtps_rx_max_records_host
         if (k && bound + r > cap) break;
         bound += r;
       }
       uncut(s, k, n);
       rc = launch(s, k, cur);
-      if (rc != RTPS_RX_OK) break;
+      if (rc != RTPS_RX_OK) {  // not in flight: wait for what was queued, then give its slots back
+        (void)hipStreamSynchronize(stream);
+        (void)rtps_udp_release(udp, s.off, k);
+        break;
+      }
       publish();
       cur ^= 1u;
       rc = finish(slot[cur], cur);  // the previous batch, while the GPU runs this one
