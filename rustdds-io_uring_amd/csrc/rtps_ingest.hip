@@ -75,6 +75,32 @@ __device__ __forceinline__ uint32_t entry_of(const IngestTable& t, uint32_t a, u
   }
   return NONE;
 }
+// Tables of up to ET_LDS slots are staged in LDS by k_classify (dynamic shared
+// memory: keys, then entry index with NONE for empty slots; 20 B per slot).
+constexpr uint32_t ET_LDS = 2048;
+extern __shared__ u32x4 s_et_dyn[];
+__host__ __device__ constexpr uint32_t et_lds_bytes(uint32_t slots) { return slots * 20u; }
+__device__ __forceinline__ void et_stage(const IngestTable& t) {
+  const u32x4* keys = reinterpret_cast<const u32x4*>(t.keys);
+  uint32_t* idx = reinterpret_cast<uint32_t*>(s_et_dyn + t.mask + 1u);
+  for (uint32_t i = threadIdx.x; i <= t.mask; i += blockDim.x) {
+    s_et_dyn[i] = keys[i];
+    idx[i] = t.slots[i] == RTPS_NO_MATCH ? NONE : t.index[i];
+  }
+  __syncthreads();
+}
+__device__ __forceinline__ uint32_t entry_of_lds(uint32_t mask, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  const uint32_t* idx = reinterpret_cast<const uint32_t*>(s_et_dyn + mask + 1u);
+  uint32_t i = guid_hash(a, b, c, d) & mask;
+  for (uint32_t probe = 0; probe <= mask; ++probe) {
+    const uint32_t e = idx[i];
+    if (e == NONE) return NONE;
+    const u32x4 k = s_et_dyn[i];
+    if (k[0] == a && k[1] == b && k[2] == c && k[3] == d) return e;
+    i = (i + 1u) & mask;
+  }
+  return NONE;
+}
 // atomicOr(base[idx], m) for the active lanes, with every word's bits combined
 // across the wave first: one atomic per distinct word.  A writer's sequential
 // SNs share bitmap words (T: 4 lanes per word, 16 writers interleaved), while
@@ -153,6 +179,8 @@ __global__ __launch_bounds__(IT) void k_classify(IngestTable t, const rtps_recor
                                                  uint64_t max, const rtps_frag_sample* frag, uint32_t flags,
                                                  Scratch x, uint64_t* ctr) {
   const uint64_t n = *n_rec < max ? *n_rec : max;
+  const bool lds = t.mask < ET_LDS;
+  if (lds) et_stage(t);
   uint32_t nh = 0, ng = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * IT + threadIdx.x; i < max; i += (uint64_t)gridDim.x * IT) {
     uint8_t ev = EV_NONE;
@@ -162,25 +190,32 @@ __global__ __launch_bounds__(IT) void k_classify(IngestTable t, const rtps_recor
       const uint32_t f = frag ? x.fidx[i] : NONE;
       if (f != NONE) {  // completed DataFrag sample, processed at its completing record (reader.rs:614-626)
         const uint32_t* g = reinterpret_cast<const uint32_t*>(frag[f].writer_guid);
-        e = entry_of(t, g[0], g[1], g[2], g[3]);
+        e = lds ? entry_of_lds(t.mask, g[0], g[1], g[2], g[3]) : entry_of(t, g[0], g[1], g[2], g[3]);
         if (e != NONE) { ev = EV_SAMPLE; sn = frag[f].sn; }
       } else {
-        const rtps_record r = recs[i];
-        if ((r.route & RTPS_ROUTE_PASS) && (r.route & RTPS_ROUTE_MATCHED)) {
-          const uint32_t* d = reinterpret_cast<const uint32_t*>(&r);
-          if (r.kind == RTPS_DATA) {
+        // bytes 0..31 of the record (kind @6, prefix||writer_id @8, route @30,
+        // payload_kind @31), then 32..47 (sn, gap.list_base) for the candidates:
+        // three of the record's four 16-B quads at most
+        const u32x4* q = reinterpret_cast<const u32x4*>(recs + i);
+        const u32x4 q0 = q[0], q1 = q[1];
+        const uint32_t kind = (q0[1] >> 16) & 0xffu, route = (q1[3] >> 16) & 0xffu, pk = q1[3] >> 24;
+        if ((route & RTPS_ROUTE_PASS) && (route & RTPS_ROUTE_MATCHED) &&
+            (kind == RTPS_DATA || kind == RTPS_HEARTBEAT || kind == RTPS_GAP)) {
+          const u32x4 q2 = q[2];
+          const int64_t rsn = (int64_t)(((uint64_t)q2[1] << 32) | q2[0]);
+          if (kind == RTPS_DATA) {
             // data_to_dds_data must succeed (reader.rs:552-558)
-            if (r.payload_kind == RTPS_PK_DATA || r.payload_kind == RTPS_PK_KEY || r.payload_kind == RTPS_PK_KEY_HASH)
-              ev = EV_SAMPLE;
-          } else if (r.kind == RTPS_HEARTBEAT) {
+            if (pk == RTPS_PK_DATA || pk == RTPS_PK_KEY || pk == RTPS_PK_KEY_HASH) ev = EV_SAMPLE;
+          } else if (kind == RTPS_HEARTBEAT) {
             if (!(flags & RTPS_INGEST_BEST_EFFORT)) ev = EV_HB;  // BestEffort: ignored (reader.rs:870-881)
-          } else if (r.kind == RTPS_GAP) {
-            if (r.sn > 0 && r.u.gap.list_base > 0) ev = EV_GAP;   // validity (reader.rs:1087-1102)
+          } else {
+            const int64_t list_base = (int64_t)(((uint64_t)q2[3] << 32) | q2[2]);
+            if (rsn > 0 && list_base > 0) ev = EV_GAP;  // validity (reader.rs:1087-1102)
           }
           if (ev != EV_NONE) {
-            e = entry_of(t, d[2], d[3], d[4], d[5]);
+            e = lds ? entry_of_lds(t.mask, q0[2], q0[3], q1[0], q1[1]) : entry_of(t, q0[2], q0[3], q1[0], q1[1]);
             if (e == NONE) ev = EV_NONE;
-            sn = r.sn;
+            sn = rsn;
           }
         }
       }
@@ -603,8 +638,8 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const IngestTable& t, cons
   if (with_frag)
     hipLaunchKernelGGL(k_fidx, dim3((uint32_t)hmin((max_frag + IT - 1) / IT, 4096)), dim3(IT), 0, st, frag, n_frag,
                        max_frag, max, x.fidx);
-  hipLaunchKernelGGL(k_classify, dim3(gb), dim3(IT), 0, st, t, records, n_records, max, with_frag ? frag : nullptr,
-                     flags, x, S.ctr);
+  hipLaunchKernelGGL(k_classify, dim3(gb), dim3(IT), t.mask < ET_LDS ? et_lds_bytes(t.mask + 1) : 0u, st, t, records,
+                     n_records, max, with_frag ? frag : nullptr, flags, x, S.ctr);
   // the batch's HEARTBEAT / GAP counts decide which stages run: one small read-back
   if (hipMemcpyAsync(s->hctr, S.ctr, C_COUNT * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipStreamSynchronize(st) != hipSuccess)
