@@ -8,7 +8,7 @@ while IFS= read -r grp; do
   [ -z "$grp" ] && continue
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $grp -d "$R/gpurun_out/pmc_c3_$i" -o run --output-format csv \
-    -- python3 "$R/bench.py" --workload ${WL:-C3} --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --no-cdr --no-frag \
+    -- python3 "$R/bench.py" --workload ${WL:-C3} --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --no-cdr --no-frag --no-ingest --no-c1 \
     > "$R/gpurun_out/pmc_c3_$i.log" 2>&1 || { echo "STOP pmc group $i ($grp)"; tail -3 "$R/gpurun_out/pmc_c3_$i.log"; exit 3; }
 done <<'GROUPS'
 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU
