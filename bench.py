@@ -352,10 +352,19 @@ def cpu_baseline(workload, n, target_cpu_s=10.0, match_table=None):
         if time.process_time() - c0 >= target_cpu_s or time.perf_counter() - t0 > 60:
             break
     dt = time.perf_counter() - t0
+    # one thread too (BASELINE.md section 2 plan): a quarter of the batch, best of 3
+    q = max(1, n // 4)
+    best = float("inf")
+    for _ in range(3):
+        s0 = time.perf_counter()
+        oracle.parse(arena, off[:q], ln[:q], threads=1, want_match=True, match_table=match_table)
+        best = min(best, time.perf_counter() - s0)
     return {"value": reps * n / dt, "unit": "datagrams/s", "cores": threads, "kind": "port",
             "gib_per_s": reps * float(ln.astype(np.int64).sum()) / dt / 2**30,
             "sample": f"{reps} x full {workload} batch ({n} datagrams, generated on host), oracle/rtps_oracle.c "
-                      f"on {threads} threads, {dt:.2f} s wall"}
+                      f"on {threads} threads, {dt:.2f} s wall",
+            "single_thread": {"value": q / best, "unit": "datagrams/s", "cores": 1,
+                              "sample": f"first {q} datagrams of the same batch, best of 3"}}
 
 
 def main():
