@@ -672,7 +672,17 @@ __device__ __forceinline__ void load_tile(const KParams& p, uint32_t tile, TileC
   t.addressable = t.valid && off <= p.arena_len && (uint64_t)t.L <= p.arena_len - off && rel + t.L <= avail;
   t.s.base = (uint32_t)rel;
   u32x4 a = {0u, 0u, 0u, 0u}, b = a, c = a, d = a;
-  if (t.addressable) { a = ld16(t.s, 0); b = ld16(t.s, 16); c = ld16(t.s, 32); d = ld16(t.s, 48); }
+  if (t.addressable) {
+    a = ld16(t.s, 0); b = ld16(t.s, 16); c = ld16(t.s, 32);
+    // bytes 48..63 serve only the first submessage's window, which a DATA there
+    // does not read (its fields and encapsulation end at byte 48): skipping them
+    // saves a line fetch wherever they begin a new 128-B line
+#ifdef ABL_HEAD_EAGER
+    d = ld16(t.s, 48);
+#else
+    if ((b[1] & 0xffu) != RTPS_DATA) d = ld16(t.s, 48);
+#endif
+  }
   t.H[0] = a[0]; t.H[1] = a[1]; t.H[2] = a[2]; t.H[3] = a[3];
   t.H[4] = b[0]; t.H[5] = b[1]; t.H[6] = b[2]; t.H[7] = b[3];
   t.H[8] = c[0]; t.H[9] = c[1]; t.H[10] = c[2]; t.H[11] = c[3];
