@@ -1221,8 +1221,7 @@ int rtps_rx_create(const rtps_rx_config* cfg, rtps_rx_ctx** out_ctx) {
       hipHostMalloc(&c->mixed, 2 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
     (void)hipFree(c->scratch);
     (void)hipFree(c->chain);
-  if (c->mixed) (void)hipHostFree(c->mixed);
-  (void)hipFree(c->chain);
+    if (c->mixed) (void)hipHostFree(c->mixed);
     (void)hipStreamDestroy(c->own_stream);
     delete c;
     return RTPS_RX_ENOMEM;
@@ -1237,6 +1236,8 @@ int rtps_rx_destroy(rtps_rx_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   (void)hipFree(c->scratch);
+  (void)hipFree(c->chain);
+  if (c->mixed) (void)hipHostFree(c->mixed);
   (void)hipFree(c->mt_keys);
   (void)hipFree(c->mt_slots);
   (void)hipFree(c->mt_index);
