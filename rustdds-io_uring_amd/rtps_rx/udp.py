@@ -12,7 +12,7 @@ import ctypes
 
 import numpy as np
 
-from . import lib, _check, ABI_VERSION, _Out, _IngestOut, INGEST_BEST_EFFORT
+from . import lib, _check, ABI_VERSION, _Out, _IngestOut, INGEST_BEST_EFFORT, RtpsRxError
 
 UDP_REUSE = 0x1
 UDP_FORCE_RECVMMSG = 0x2
@@ -181,6 +181,8 @@ class Pump:
 
     def __init__(self, rx, rxu, max_batch=16384, ingest=False, sample_type=None, best_effort=False,
                  max_recs=None, n_entries=1):
+        if isinstance(rxu.arena, np.ndarray) or not getattr(rxu.arena, "is_pinned", lambda: False)():
+            raise RtpsRxError("Pump: the receiver's arena must be a pinned torch tensor (the GPU parses it in place)")
         self.rx, self.rxu = rx, rxu
         cap = max_recs if max_recs is not None else max_batch * max(1, (rxu.slot_bytes - 20) // 4)
         self.cap = cap
