@@ -121,3 +121,13 @@ def test_bad_configuration():
             udp.UdpReceiver(arena, **kw)
     with pytest.raises(RtpsRxError):
         udp.UdpReceiver(np.zeros(48 * 3, dtype=np.uint8), slot_bytes=48)  # 3 slots: not a power of two
+
+
+def test_pump_refuses_unpinned_arena():
+    """The native receive loop parses the arena in place on the GPU: a numpy
+    (pageable) arena is refused before anything touches the device."""
+    arena = np.zeros(2048 * 16, dtype=np.uint8)
+    rx = udp.UdpReceiver(arena, slot_bytes=2048)
+    with pytest.raises(RtpsRxError):
+        udp.Pump(None, rx, max_batch=16)
+    rx.close()
