@@ -623,19 +623,22 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, uint32_t lane) {
 }
 
 // ---------------------------------------------------------------------------
-// Ordered output without inter-workgroup waiting:
+// Ordered output:
 //   A  rtps_parse_spec_kernel  one workgroup per tile of 256 datagrams (blockIdx
 //      order): walk 1 counts each datagram's records; a tile in which every
 //      datagram has exactly k_spec records ("speculative" tile) walks again and
 //      writes its records at tile*256*k_spec + local prefix, which is the final
 //      position whenever every earlier tile is speculative too.  Every tile
-//      publishes count | nonspec<<31.
-//   S  rtps_tile_scan_kernel   one workgroup: exclusive scan of the tile counts,
-//      first non-speculative tile f, total -> n_records.
-//   B  rtps_parse_fix_kernel   persistent: re-walks tiles f.. and writes them at
-//      their scanned positions (overwriting any speculative writes there).
+//      publishes its count and flags (info[], below).
+//   C  rtps_parse_chain_kernel  replaces A for mixed traffic: count walk, the
+//      exact prefix from the predecessors' published counts (two-level
+//      look-back, bounded polls), then the writing walk.
+//   B  rtps_parse_fix_kernel   persistent, after A or C: reduces the tile
+//      counts (n_records), reports the batch's mix for the next launch choice,
+//      and walks the tiles not yet written at their exact positions
+//      (overwriting any speculative writes there).
 // One-DATA-per-datagram traffic (T, C2, C4) finishes in A; mixed traffic (C3)
-// becomes an exact two-pass parse.  No spin-waits, tickets or grid barriers.
+// in C.  A and B have no spin-waits, tickets or grid barriers.
 // ---------------------------------------------------------------------------
 struct TileCtx {
   uint32_t i;      // datagram index of this lane
