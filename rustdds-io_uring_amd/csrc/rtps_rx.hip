@@ -1,6 +1,7 @@
 // rtps_rx.hip — MI355X (gfx950) RTPS receive-path parser + C ABI (include/rtps_rx.h).
 //
-// One kernel, rtps_parse_kernel, replaces for a whole batch of datagrams:
+// The parse kernels (A or C, then B: see "Ordered output" below) replace, for a
+// whole batch of datagrams:
 //   MessageReceiver::handle_received_packet_2      io_uring/rtps/message_receiver.rs:232-287
 //   Message::read_from_buffer + Submessage::read_from_buffer
 //                                                  rtps/message.rs:64-81, rtps/submessage.rs:56-295
@@ -14,14 +15,16 @@
 //     the submessage chain of a datagram is a serial pointer chase, so the
 //     parallelism is across datagrams;
 //   * the datagram bytes are never copied: each submessage is read through a
-//     48-byte register window (3 x 16-B buffer loads at the submessage start,
-//     every fixed field at a compile-time offset), variable-offset fields
-//     (inline-QoS parameters, AckNack count, ...) by 4-byte loads; payload
-//     bytes stay in HBM (zero-copy spans, like the reference's Bytes slices);
-//   * records are placed in the reference's order (ascending dgram, sub_off)
-//     by a single-pass decoupled look-back scan over tiles: walk 1 counts,
-//     the tile publishes its aggregate, looks back for its prefix, walk 2
-//     writes the 64-B records at their final index;
+//     register window (16-B buffer loads at the submessage start, the second
+//     16 B only for kinds that read them; every fixed field at a compile-time
+//     offset), variable-offset fields (inline-QoS parameters, AckNack count,
+//     ...) by 4-byte loads; payload bytes stay in HBM (zero-copy spans, like
+//     the reference's Bytes slices);
+//   * records are placed in the reference's order (ascending dgram, sub_off):
+//     walk 1 counts, walk 2 writes the 64-B records at their final index,
+//     speculatively (one record per datagram: kernel A), after a look-back
+//     over the predecessors' counts (mixed traffic: kernel C), or after all
+//     counts are known (kernel B);
 //   * all arena reads go through a bounds-checked buffer resource (reads past
 //     the arena return 0 and never fault).
 #include <hip/hip_runtime.h>
