@@ -27,6 +27,17 @@ off_t = torch.from_numpy(off.view(np.int64)).to(dev)
 ln_t = torch.from_numpy(ln.view(np.int32)).to(dev)
 rx.generate(wl, arena, off_t, ln_t, n)
 outs = rx.alloc_outputs(n, 4 * n)
+if "match" in sys.argv[2:]:  # subscribe to every writer of the batch, as bench.py does
+    from rtps_rx.records import RECORD_DTYPE, MATCH_DTYPE
+    rx.parse_batch_device(arena, off_t, ln_t, n, outs)
+    torch.cuda.synchronize()
+    r = outs["records"][:n].cpu().numpy().reshape(-1).view(RECORD_DTYPE)
+    g = np.concatenate([r["prefix"], r["writer_id"]], axis=1)
+    guids = np.unique(g.view(np.dtype((np.void, 16))).reshape(-1))
+    tbl = np.zeros(len(guids), dtype=MATCH_DTYPE)
+    tbl["writer_guid"] = np.frombuffer(guids.tobytes(), dtype=np.uint8).reshape(-1, 16)
+    rx.set_match_table(tbl)
+    print("match table:", len(guids), "writers")
 for _ in range(20):
     rx.parse_batch_device(arena, off_t, ln_t, n, outs)
 torch.cuda.synchronize()
