@@ -539,7 +539,8 @@ def main():
                    "datagrams_per_gpu": n, "bytes_per_gpu": int(total_bytes), "records_per_gpu": n_rec,
                    "ok_datagrams": int((status == 0).sum()), "matched_writers": n_matched_writers,
                    "parallelism": f"{world} ranks, datagram-sharded" + (
-                       ", writer-GUID all-to-all (RCCL)" if world > 1 else "")},
+                       ", writer-GUID all-to-all (" + ("RCCL" if args.backend == "nccl" else "gloo") + ")"
+                       if world > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": alg_total / (ev_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": alg_total / (ev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "traffic": traffic, "traffic_source": traffic_src,
