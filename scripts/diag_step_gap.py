@@ -45,7 +45,7 @@ torch.cuda.synchronize()
 
 def run(mode):
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
+    ends = [torch.cuda.Event(enable_timing=(mode != "evnt")) for _ in range(K)]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     if mode == "ev2":
@@ -54,7 +54,7 @@ def run(mode):
         if mode == "ev":
             starts[k].record(stream)
         rx.parse_batch_device(arena, off_t, ln_t, n, outs)
-        if mode == "ev":
+        if mode in ("ev", "evnt"):
             ends[k].record(stream)
     th = time.perf_counter() - t0
     if mode == "ev2":
@@ -70,7 +70,7 @@ def run(mode):
 
 
 for rep in range(2):
-    for mode in ("ev", "noev", "ev2"):
+    for mode in ("ev", "noev", "ev2", "evnt"):
         h, w, e = run(mode)
         print(f"{mode:5s} host/call {h:6.1f} us  wall/step {w:6.1f} us  event/step {e if e is None else round(e, 1)} us",
               flush=True)
