@@ -713,6 +713,9 @@ __global__ __launch_bounds__(FT) void k_span(const rtps_record* recs, const uint
           const uint64_t span_end = min<uint64_t>(from + fisF, E.data_size);
           const uint64_t to = min<uint64_t>(from + min<uint64_t>(fisF, r->u.frag.pl_len), E.data_size);
           src = dgram_off[r->dgram_idx] + r->u.frag.pl_off;
+#ifdef ABL_SPAN_ALIGN  // timing only (wrong output): 16-B-aligned source reads
+          src &= ~(uint64_t)15;
+#endif
           dst = (uint64_t)(epoch_dst(E, out, nbytes) + from);
           nv = (uint32_t)(to - from);
           n = (uint32_t)(span_end - from);
@@ -722,6 +725,10 @@ __global__ __launch_bounds__(FT) void k_span(const rtps_record* recs, const uint
     }
     // four records at a time, one per quarter-wave: 16 lanes x 16 B = 256 B per
     // instruction per record, SPAN_U loads in flight per lane before the stores
+#ifdef ABL_SPAN_NOCOPY  // timing only: resolve the records, copy nothing
+    if (live && n == 0xffffffffu) *(uint8_t*)(uintptr_t)dst = (uint8_t)src;
+    continue;
+#endif
     uint64_t todo = __ballot(live);
     const uint32_t q = lane >> 4, ql = lane & 15u;
     while (todo) {
@@ -958,7 +965,10 @@ int rtps_frag_assemble(FragState* s, hipStream_t st, const uint8_t* arena, uint6
                      s->pbytes[nw], s->pbits[nw], s->ctr);
   hipLaunchKernelGGL(k_init, dim3(1024), dim3(FT), 0, st, s->epochs, s->special, s->ctr, s->pend[o], s->pbytes[o],
                      s->pbytes[nw], *out);
-  hipLaunchKernelGGL(k_span, dim3((uint32_t)hmin((max + FT - 1) / FT, 8192)), dim3(FT), 0, st, records, arena,
+#ifndef SPAN_GRID
+#define SPAN_GRID 8192
+#endif
+  hipLaunchKernelGGL(k_span, dim3((uint32_t)hmin((max + FT - 1) / FT, SPAN_GRID)), dim3(FT), 0, st, records, arena,
                      arena_len, dgram_off, s->svals, s->pos_epoch, s->skeys, max, s->epochs, s->pbytes[nw], *out);
   hipLaunchKernelGGL(k_serial, dim3(1024), dim3(FT), 0, st, records, arena, dgram_off, s->svals, s->pos_epoch,
                      s->epochs, s->special, s->ctr, s->pend[o], s->pbytes[o], s->pbytes[nw], *out);
