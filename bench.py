@@ -544,7 +544,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": alg_total / (ev_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": alg_total / (ev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "traffic": traffic, "traffic_source": traffic_src,
-                     "kernel": ("rtps_parse_spec_kernel (or rtps_parse_chain_kernel + its 16-B-aligned zeroing, chosen "
+                     "kernel": ("rtps_parse_spec_kernel (or rtps_parse_chain_kernel, chosen "
                                 "per batch from the traffic mix) + rtps_parse_fix_kernel: one rtps_rx_parse_batch"),
                      "kernel_ms": ev_ms,
                      "kernel_ms_source": "HIP event pair on the parse stream around the K back-to-back steps, / K",

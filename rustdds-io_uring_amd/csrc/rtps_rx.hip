@@ -69,9 +69,13 @@ struct KParams {
   const uint16_t* mt_slots;
   uint32_t mt_mask;           // capacity - 1
   uint64_t* scratch;          // per-tile counts / prefixes (Scratch)
-  uint64_t* chain;            // per-tile look-back words (chained launch only), zeroed before it
+  uint64_t* chain;            // per-tile look-back words (chained launch only), tagged with ch_epoch
   uint32_t* mixed_out;        // pinned host [2]: tiles of the batch not uniform k_spec, tiles (launch choice)
   uint32_t ch_spin_limit;     // polls before a chained tile leaves itself to kernel B
+  uint32_t ch_epoch;          // chained launch number (never 0): tags the look-back words of this launch
+  uint64_t* ch_gc;            // [ch_gmax] group arrival counters of this launch (zero at its start)
+  uint64_t* ch_gc_next;       // [ch_gmax] the next chained launch's counters: zeroed by this one
+  uint32_t ch_gmax;
 };
 
 // ---------------------------------------------------------------------------
@@ -911,17 +915,24 @@ __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_fix_kern
 // (an arrival counter per group) sums the group and publishes the group total.
 // A tile's prefix = the totals of the earlier groups + the counts of the
 // earlier tiles of its group.  Every exchanged word is an agent-scope 8-byte
-// {state, value} word (no fences: a reader polls until the state is set).  A
-// tile that gives up waiting (a predecessor that never published: only if the
-// dispatcher ran tiles far out of order) stays unwritten and kernel B, launched
-// after it as always, walks it: results never depend on dispatch order or
-// timing.  chain[] (tile words, group words, group counters) is zeroed before
-// the launch.
-constexpr uint64_t CH_READY = 1ull << 62, CH_VAL = (1ull << 62) - 1;
+// {epoch, value} word (no fences: a reader polls until the word carries this
+// launch's epoch).  A tile that gives up waiting (a predecessor that never
+// published: only if the dispatcher ran tiles far out of order) stays
+// unwritten and kernel B, launched after it as always, walks it: results never
+// depend on dispatch order or timing.  Nothing is zeroed between launches:
+// words of earlier launches carry older epochs, and the group arrival counters
+// come in two sets, each launch clearing the set the next one uses.
+// look-back word = epoch << 32 | value; ready when its epoch is this launch's
+__device__ __forceinline__ uint64_t ch_word(uint32_t epoch, uint64_t value) { return (uint64_t)epoch << 32 | value; }
 constexpr uint32_t CH_GROUP = 64;
 constexpr uint32_t CH_SPIN_LIMIT = 1u << 14;
-__host__ __device__ constexpr size_t chain_words(uint32_t tiles) {  // tile words, group words, group counters
+__host__ __device__ constexpr size_t chain_words(uint32_t tiles) {  // tile words, group words, (unused) counters
   return (size_t)tiles + 2 * (((size_t)tiles + CH_GROUP - 1) / CH_GROUP) + 2;
+}
+__host__ __device__ constexpr uint32_t chain_groups(uint32_t tiles) { return (tiles + CH_GROUP - 1) / CH_GROUP; }
+// + 2 spare words, + two sets of group arrival counters (alternating by chained launch)
+__host__ __device__ constexpr size_t chain_alloc_words(uint32_t tiles) {
+  return chain_words(tiles) + 2 + 2 * (size_t)chain_groups(tiles);
 }
 __device__ __forceinline__ uint64_t ch_load(const uint64_t* w) {
   return __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -929,14 +940,14 @@ __device__ __forceinline__ uint64_t ch_load(const uint64_t* w) {
 __device__ __forceinline__ void ch_store(uint64_t* w, uint64_t v) {
   __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// sum of the CH_VAL parts of words w[0, n), n <= 64 (one per lane), polling until
+// sum of the value parts of words w[0, n), n <= 64 (one per lane), polling until
 // every one is ready; false after CH_SPIN_LIMIT polls
-__device__ __forceinline__ bool ch_sum_ready(const uint64_t* w, uint32_t n, uint32_t lane, uint32_t limit,
+__device__ __forceinline__ bool ch_sum_ready(const uint64_t* w, uint32_t n, uint32_t lane, uint32_t epoch, uint32_t limit,
                                              uint64_t& sum) {
   for (uint32_t spins = 0;; ++spins) {
-    const uint64_t v = lane < n ? ch_load(w + lane) : CH_READY;
-    if (__all((v & CH_READY) != 0)) {
-      uint64_t x = v & CH_VAL;
+    const uint64_t v = lane < n ? ch_load(w + lane) : ch_word(epoch, 0);
+    if (__all((uint32_t)(v >> 32) == epoch)) {
+      uint64_t x = v & 0xffffffffull;
 #pragma unroll
       for (uint32_t d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
       sum = x;
@@ -977,33 +988,35 @@ __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_chain_ke
     x.dcount[t.i] = (uint16_t)cnt;
   }
   if (wave == 0) {
-    const uint32_t n_groups = (n_tiles + CH_GROUP - 1) / CH_GROUP;
     uint64_t* tw = p.chain;                 // [n_tiles] tile counts
     uint64_t* gw = p.chain + n_tiles;       // [n_groups] group totals
-    uint64_t* gc = gw + n_groups;           // [n_groups] arrival counters
+    uint64_t* gc = p.ch_gc;                 // [n_groups] arrival counters (zeroed by the previous launch)
     const uint32_t g = tile / CH_GROUP, r = tile % CH_GROUP;
     const uint32_t g_size = min(CH_GROUP, n_tiles - g * CH_GROUP);
     uint64_t excl = 0, part = 0;
     bool ok = true;
     uint64_t arrived = 0;
+    const uint32_t ep = p.ch_epoch;
     if (lane == 0) {
-      ch_store(tw + tile, CH_READY | agg);
+      ch_store(tw + tile, ch_word(ep, agg));
       arrived = __hip_atomic_fetch_add(gc + g, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+      // counters alternate between two sets by launch: clear the next launch's set
+      for (uint32_t i = tile; i < p.ch_gmax; i += n_tiles) p.ch_gc_next[i] = 0ull;
     }
     arrived = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(arrived >> 32)) << 32) |
               __builtin_amdgcn_readfirstlane((uint32_t)arrived);
     if (arrived == g_size) {  // last of its group: publish the group total
       uint64_t gsum = 0;
-      ok = ch_sum_ready(tw + g * CH_GROUP, g_size, lane, p.ch_spin_limit, gsum);
-      if (ok && lane == 0) ch_store(gw + g, CH_READY | gsum);
+      ok = ch_sum_ready(tw + g * CH_GROUP, g_size, lane, ep, p.ch_spin_limit, gsum);
+      if (ok && lane == 0) ch_store(gw + g, ch_word(ep, gsum));  // < 64 * 256 * 16379 < 2^32
     }
 #ifndef ABL_NO_LOOKBACK
     for (uint32_t g0 = 0; ok && g0 < g; g0 += 64) {  // totals of the earlier groups
-      ok = ch_sum_ready(gw + g0, min(64u, g - g0), lane, p.ch_spin_limit, part);
+      ok = ch_sum_ready(gw + g0, min(64u, g - g0), lane, ep, p.ch_spin_limit, part);
       excl += part;
     }
     if (ok && r) {  // counts of the earlier tiles of its group
-      ok = ch_sum_ready(tw + g * CH_GROUP, r, lane, p.ch_spin_limit, part);
+      ok = ch_sum_ready(tw + g * CH_GROUP, r, lane, ep, p.ch_spin_limit, part);
       excl += part;
     }
 #endif
@@ -1194,6 +1207,8 @@ struct rtps_rx_ctx {
   uint64_t* chain = nullptr;      // look-back words of the chained launch [chain_words(tiles) + 2]
   uint32_t* mixed = nullptr;      // pinned: {mixed tiles, tiles} of the last finished batch (kernel B)
   uint32_t ch_spin_limit = CH_SPIN_LIMIT;
+  uint32_t ch_epoch = 0;          // last chained launch's epoch (words start zeroed: epoch 0 is never used)
+  uint32_t chain_tiles = 0;       // tiles the chain words are sized for
 };
 
 static int hip_fail(hipError_t e) { return e == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP; }
@@ -1223,7 +1238,8 @@ int rtps_rx_create(const rtps_rx_config* cfg, rtps_rx_ctx** out_ctx) {
   c->scratch_words = 2 + ((tiles + 3) & ~(size_t)3) / 2 + ((size_t)cfg->max_datagrams + 3) / 4 + 2;
   if (hipMalloc(&c->scratch, c->scratch_words * sizeof(uint64_t)) != hipSuccess ||
       hipMemset(c->scratch, 0, c->scratch_words * sizeof(uint64_t)) != hipSuccess ||
-      hipMalloc(&c->chain, (chain_words((uint32_t)tiles) + 2) * sizeof(uint64_t)) != hipSuccess ||
+      hipMalloc(&c->chain, chain_alloc_words((uint32_t)tiles) * sizeof(uint64_t)) != hipSuccess ||
+      hipMemset(c->chain, 0, chain_alloc_words((uint32_t)tiles) * sizeof(uint64_t)) != hipSuccess ||
       hipHostMalloc(&c->mixed, 2 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
     (void)hipFree(c->scratch);
     (void)hipFree(c->chain);
@@ -1233,6 +1249,7 @@ int rtps_rx_create(const rtps_rx_config* cfg, rtps_rx_ctx** out_ctx) {
     return RTPS_RX_ENOMEM;
   }
   c->mixed[0] = c->mixed[1] = 0u;
+  c->chain_tiles = (uint32_t)tiles;
   *out_ctx = c;
   return RTPS_RX_OK;
 }
@@ -1348,6 +1365,9 @@ int rtps_rx_parse_batch(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len
   p.chain = c->chain;
   p.mixed_out = c->mixed;
   p.ch_spin_limit = c->ch_spin_limit;
+  p.ch_epoch = 0u;  // set below for a chained launch
+  p.ch_gc = p.ch_gc_next = nullptr;
+  p.ch_gmax = 0u;
   // Launch choice, a performance decision only (both give the same output): a
   // chained single pass when the spec hint is 0, or when most tiles of the last
   // finished batch were mixed (B reports that to pinned memory; read without a sync,
@@ -1357,8 +1377,18 @@ int rtps_rx_parse_batch(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len
   const bool chain = c->k_spec == 0 || (seen >= 16u && 2u * mixed > seen);
   const uint32_t k = c->k_spec ? c->k_spec : 1u;
   if (chain) {  // one chained pass, B only finishes (n_records, stragglers)
-    if (hipMemsetAsync(c->chain, 0, ((chain_words(tiles) * 8 + 15) & ~(size_t)15), c->stream) != hipSuccess)
-      return RTPS_RX_EHIP;
+    // the look-back words carry this launch's epoch, so they need no zeroing; only
+    // when the 32-bit epoch wraps are stale words of the same epoch possible
+    if (++c->ch_epoch == 0u) {
+      c->ch_epoch = 1u;
+      if (hipMemsetAsync(c->chain, 0, chain_alloc_words(c->chain_tiles) * sizeof(uint64_t), c->stream) != hipSuccess)
+        return RTPS_RX_EHIP;
+    }
+    p.ch_epoch = c->ch_epoch;
+    p.ch_gmax = chain_groups(c->chain_tiles);
+    uint64_t* sets = c->chain + chain_words(c->chain_tiles) + 2;
+    p.ch_gc = sets + (size_t)(c->ch_epoch & 1u) * p.ch_gmax;
+    p.ch_gc_next = sets + (size_t)((c->ch_epoch & 1u) ^ 1u) * p.ch_gmax;
     hipLaunchKernelGGL(rtps_parse_chain_kernel, dim3(tiles), dim3(TILE), mt_lds, c->stream, p, tiles, k, parity);
   } else {
     hipLaunchKernelGGL(rtps_parse_spec_kernel, dim3(tiles), dim3(TILE), mt_lds, c->stream, p, tiles, c->k_spec,
@@ -1565,6 +1595,14 @@ uint32_t rtps_rx_record_size(void) { return (uint32_t)sizeof(rtps_record); }
 int rtps_rx_debug_set_chain_spin_limit(rtps_rx_ctx* c, uint32_t limit) {
   if (!c) return RTPS_RX_EINVAL;
   c->ch_spin_limit = limit;
+  return RTPS_RX_OK;
+}
+
+/* test hook (not part of the public header): the last chained launch's epoch, so
+   that a test can run chained launches across the 32-bit wrap */
+int rtps_rx_debug_set_chain_epoch(rtps_rx_ctx* c, uint32_t epoch) {
+  if (!c) return RTPS_RX_EINVAL;
+  c->ch_epoch = epoch;
   return RTPS_RX_OK;
 }
 

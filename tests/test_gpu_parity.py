@@ -288,6 +288,26 @@ def test_chained_fallback_to_fix_pass(rx, limit):
         rx.set_spec_hint(1)
 
 
+def test_chained_words_across_sizes_and_epoch_wrap(rx):
+    """The chained pass's look-back words are never zeroed: they carry the launch's
+    epoch, and the group arrival counters alternate between two sets.  Chained
+    batches of different sizes, run across the 32-bit epoch wrap (which zeroes
+    everything once), stay bit-exact."""
+    import ctypes
+    import rtps_rx
+    L = rtps_rx.lib()
+    L.rtps_rx_debug_set_chain_epoch.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+    big = oracle.gen(oracle.WL_C3, 70 * 256 + 13)
+    small = oracle.gen(oracle.WL_C3, 5 * 256 + 200)
+    rx.set_spec_hint(0)
+    try:
+        assert L.rtps_rx_debug_set_chain_epoch(rx._h, 0xfffffffd) == 0
+        for k, (a, o, l) in enumerate([big, small, big, small, big, big]):
+            _parity(rx, a, o, l, f"C3 chained #{k} ({len(l)} datagrams) across the epoch wrap")
+    finally:
+        rx.set_spec_hint(1)
+
+
 def test_launch_choice_follows_traffic(rx):
     """The speculative / chained choice follows the previous batch's mix (a lagging
     hint): a mixed batch after mixed ones, a one-DATA batch after mixed ones (chained
