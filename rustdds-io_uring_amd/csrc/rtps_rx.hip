@@ -924,7 +924,10 @@ __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_fix_kern
 // come in two sets, each launch clearing the set the next one uses.
 // look-back word = epoch << 32 | value; ready when its epoch is this launch's
 __device__ __forceinline__ uint64_t ch_word(uint32_t epoch, uint64_t value) { return (uint64_t)epoch << 32 | value; }
-constexpr uint32_t CH_GROUP = 64;
+#ifndef RTPS_CH_GROUP
+#define RTPS_CH_GROUP 64
+#endif
+constexpr uint32_t CH_GROUP = RTPS_CH_GROUP;  // <= 64: a group's tile words are summed by one wave
 constexpr uint32_t CH_SPIN_LIMIT = 1u << 14;
 __host__ __device__ constexpr size_t chain_words(uint32_t tiles) {  // tile words, group words, (unused) counters
   return (size_t)tiles + 2 * (((size_t)tiles + CH_GROUP - 1) / CH_GROUP) + 2;
