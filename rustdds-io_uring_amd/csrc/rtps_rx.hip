@@ -927,6 +927,9 @@ __device__ __forceinline__ uint64_t ch_word(uint32_t epoch, uint64_t value) { re
 #ifndef RTPS_CH_GROUP
 #define RTPS_CH_GROUP 64
 #endif
+#ifndef RTPS_CH_SLEEP
+#define RTPS_CH_SLEEP 32  // s_sleep units (64 clocks) between polls: 2 / 8 / 16 / 32 measured, DESIGN §3.3
+#endif
 constexpr uint32_t CH_GROUP = RTPS_CH_GROUP;  // <= 64: a group's tile words are summed by one wave
 constexpr uint32_t CH_SPIN_LIMIT = 1u << 14;
 __host__ __device__ constexpr size_t chain_words(uint32_t tiles) {  // tile words, group words, (unused) counters
@@ -957,7 +960,7 @@ __device__ __forceinline__ bool ch_sum_ready(const uint64_t* w, uint32_t n, uint
       return true;
     }
     if (spins >= limit) return false;
-    __builtin_amdgcn_s_sleep(2);
+    __builtin_amdgcn_s_sleep(RTPS_CH_SLEEP);
   }
 }
 __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_chain_kernel(KParams p, uint32_t n_tiles,
