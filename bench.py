@@ -38,7 +38,10 @@ WORKLOAD_DESC = {
     "C2": "1M x 300 B RTPS datagrams, one DATA each (256 B CDR payload), 16 writers",
     "C3": "1M mixed datagrams 128-1500 B: DATA/HEARTBEAT/ACKNACK/GAP/INFO_TS/INFO_DST/INFO_SRC, 16 writers",
     "C4": "1M x 1400 B DATA_FRAG datagrams (64 KiB samples, 1344 B fragments), 16 writers",
+    "C5": "64M datagrams of the C3 mix in total (64M / N per GPU, rank r's chunk at generator index r * 64M / N), "
+          "16 writers, records hash-sharded by writer GUID with one RCCL all-to-all over xGMI",
 }
+C5_TOTAL = 64 << 20
 
 
 def algorithmic_bytes(status, recs, n, record_bytes=64):
@@ -48,7 +51,7 @@ def algorithmic_bytes(status, recs, n, record_bytes=64):
             parsed datagram, per materialised submessage its 4-B header plus the
             fixed fields the reference reader consumes (+ inline QoS, + the 4-B
             encapsulation of a DATA payload);
-    writes: 1 B status + 4 B rec_begin per datagram, 64 B record + 2 B match slot
+    writes: 1 B status + 4 B rec_begin per datagram, 64 B record + 4 B target set
             per record.
     """
     k = recs["kind"]
@@ -67,18 +70,78 @@ def algorithmic_bytes(status, recs, n, record_bytes=64):
     qos = np.where((k == DATA) | (k == DATA_FRAG), recs["aux16"].astype(np.int64), 0)
     enc = np.where((k == DATA) & np.isin(recs["payload_kind"], (PK_DATA, PK_KEY)), 4, 0)
     reads = 12 * n + 20 * int((status == 0).sum()) + int((4 + fixed + qos + enc).sum())
-    writes = 5 * n + (record_bytes + 2) * len(recs)
+    writes = 5 * n + (record_bytes + 4) * len(recs)
     return reads + writes, reads, writes
 
 
-def pmc_traffic(workload):
-    """Calibrated HBM bytes per launch from the committed rocprofv3 PMC profile (profiles/)."""
-    path = os.path.join(REPO, "profiles", f"r1_pmc_{workload}.json")
-    if not os.path.exists(path):
-        return None, None
-    with open(path) as f:
+def pmc_profile(workload):
+    """Calibrated per-launch HBM bytes of the parse kernels from the newest committed
+    rocprofv3 PMC summary (profiles/r<NN>_pmc_<workload>.json, scripts/gpu_pmc.sh):
+    FETCH_SIZE (reads, scaled by the fetch calibration of MI355X_MICROARCH.md) and
+    WRITE_SIZE, in separate --pmc passes."""
+    import glob
+    import re
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_pmc_{workload}.json")),
+                   key=lambda f: int(re.search(r"r(\d+)_pmc", f).group(1)))
+    if not files:
+        return None
+    with open(files[-1]) as f:
         d = json.load(f)
-    return d.get("parse_traffic_bytes"), os.path.relpath(path, REPO)
+    d["_source"] = os.path.relpath(files[-1], REPO)
+    return d
+
+
+def time_dominant_kernel(rx, arena, off_t, ln_t, n, outs, stream, steps):
+    """Live HIP-event timing of the parse's dominant kernel alone (the first kernel of
+    rtps_rx_parse_batch: rtps_parse_spec_kernel, or rtps_parse_chain_kernel for mixed
+    traffic), K back-to-back launches on the parse stream, one event pair."""
+    which = 0
+    for _ in range(3):
+        which = rx.debug_parse_phases(arena, off_t, ln_t, n, outs, 1)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    a.record(stream)
+    for _ in range(steps):
+        rx.debug_parse_phases(arena, off_t, ln_t, n, outs, 1)
+    b.record(stream)
+    torch.cuda.synchronize()
+    ms = a.elapsed_time(b) / steps
+    for _ in range(2):  # full launches restore the per-launch bookkeeping
+        rx.parse_batch_device(arena, off_t, ln_t, n, outs)
+    torch.cuda.synchronize()
+    return ms, {1: "rtps_parse_spec_kernel", 2: "rtps_parse_chain_kernel"}[which]
+
+
+def time_ceilings(arena, off_t, ln_t, n, stream, steps):
+    """Live timing of the same-shape ceiling kernels (csrc/diag/ceiling.hip: no parse,
+    only the parse's memory traffic: 12 B (offset, length) + the 64-B head of every
+    datagram at its stride; 'read+write' adds the 64-B record through an LDS transpose
+    and the status / rec_begin stores).  None if the diagnostic library is absent."""
+    import ctypes
+    path = os.path.join(REPO, "rustdds-io_uring_amd", "libdiag_ceiling.so")
+    if not os.path.exists(path):
+        return None
+    D = ctypes.CDLL(path)
+    D.diag_ceiling.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 3 + [ctypes.c_uint32] + [ctypes.c_void_p] * 4
+    rec = torch.empty((n, 64), dtype=torch.uint8, device=arena.device)
+    status = torch.empty(n, dtype=torch.uint8, device=arena.device)
+    rb = torch.empty(n, dtype=torch.int32, device=arena.device)
+    res = {}
+    for name, mode in (("read_only", 1), ("read_write", 3)):
+        def run():
+            D.diag_ceiling(mode, arena.data_ptr(), off_t.data_ptr(), ln_t.data_ptr(), n, rec.data_ptr(),
+                           status.data_ptr(), rb.data_ptr(), ctypes.c_void_p(stream.cuda_stream))
+        for _ in range(3):
+            run()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        a.record(stream)
+        for _ in range(steps):
+            run()
+        b.record(stream)
+        torch.cuda.synchronize()
+        res[name] = a.elapsed_time(b) / steps
+    return res
 
 
 def end_to_end(rx, arena, off_t, ln_t, n, outs, n_rec, stream, reps=5):
@@ -96,7 +159,7 @@ def end_to_end(rx, arena, off_t, ln_t, n, outs, n_rec, stream, reps=5):
     h_ln.copy_(ln_t)
     h_outs = {"status": torch.empty(n, dtype=torch.uint8, pin_memory=True),
               "records": torch.empty((max(n_rec, 1), 64), dtype=torch.uint8, pin_memory=True),
-              "match": torch.empty(max(n_rec, 1), dtype=torch.int16, pin_memory=True),
+              "target": torch.empty(max(n_rec, 1), dtype=torch.int32, pin_memory=True),
               "rec_begin": torch.empty(n, dtype=torch.int32, pin_memory=True),
               "n_records": torch.zeros(1, dtype=torch.int64, pin_memory=True), "max_records": n_rec}
     torch.cuda.synchronize()
@@ -129,6 +192,49 @@ def end_to_end(rx, arena, off_t, ln_t, n, outs, n_rec, stream, reps=5):
     res["copy"]["pcie_bytes"] = arena.numel() + n + n_rec * 64
     res["best"] = max(("copy", "zero_copy"), key=lambda k: res[k]["datagrams_per_s"])
     return res
+
+
+def roofline(rx, args, arena, off_t, ln_t, n, outs, stream, total_bytes, alg_reads, alg_writes):
+    """SURVEY §8(d) roofline of the dominant parse kernel.  The algorithmic unit is the
+    datagram's bytes (Σ lengths) only if every byte streams (FETCH_SIZE >= Σ lengths);
+    the parse is zero-copy (payload bytes are never read, like the reference's
+    Bytes::split_off), so the fraction is on the FETCH_SIZE basis: calibrated HBM read
+    bytes of the kernel per launch (committed PMC summary) / its live launch time /
+    8 TB/s.  Writes (the 64-B records) are reported beside it, not in the numerator."""
+    ms, kname = time_dominant_kernel(rx, arena, off_t, ln_t, n, outs, stream, args.steps)
+    pmc = pmc_profile(args.workload)
+    key = "parse_spec" if kname == "rtps_parse_spec_kernel" else "parse_chain"
+    k = (pmc or {}).get(key) or {}
+    scale = (pmc or {}).get("fetch_scale") or 1.0
+    if pmc and pmc.get("datagrams_per_launch") == n and "FETCH_SIZE" in k:
+        read_b, write_b = k["FETCH_SIZE"] * scale, k.get("WRITE_SIZE")
+        basis = f"FETCH_SIZE x fetch_scale of {kname} ({pmc['_source']})"
+    else:
+        read_b, write_b = float(alg_reads), float(alg_writes)
+        basis = "algorithmic head/field reads (no PMC summary for this workload and size)"
+    achieved = read_b / (ms * 1e-3) / 1e9
+    r = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+         "traffic": (read_b + write_b) if write_b is not None else None,
+         "read_bytes": read_b, "write_bytes": write_b, "basis": basis,
+         "kernel": kname, "kernel_ms": ms,
+         "kernel_ms_source": "HIP events on the parse stream around K back-to-back launches of the kernel alone, / K",
+         "sum_datagram_bytes": total_bytes,
+         "alg_read_bytes": alg_reads, "alg_write_bytes": alg_writes,
+         "note": "zero-copy parse: FETCH_SIZE << sum of datagram bytes, so the fraction is on the FETCH basis; "
+                 ">= 70 % of HBM read bandwidth is structurally out of reach for a head-only parse (the read-only "
+                 "ceiling of this access shape is read_ceiling_frac)"}
+    if pmc:
+        r["pmc_source"] = pmc["_source"]
+    if kname == "rtps_parse_spec_kernel":
+        c = time_ceilings(arena, off_t, ln_t, n, stream, args.steps)
+        if c:
+            ceil_read = n * (12 + 64)  # the read-only ceiling's bytes: exact, its own shape
+            r["ceiling"] = {"kernel": "diag ceil_kernel (csrc/diag/ceiling.hip)", "read_only_ms": c["read_only"],
+                            "read_write_ms": c["read_write"],
+                            "read_only_gbs": ceil_read / (c["read_only"] * 1e-3) / 1e9}
+            r["read_ceiling_frac"] = r["ceiling"]["read_only_gbs"] / HBM_PEAK_GBS
+            r["attainable_frac"] = c["read_write"] / ms  # same-shape read+write ceiling time / kernel time
+    return r
 
 
 CDR_TYPES = {"T": "TSample", "C2": "C2Sample", "C3": "ShapeType", "C4": "C2Sample"}
@@ -213,9 +319,9 @@ def ingest_leg(rx, arena, off_t, outs, n_rec, recs, n_entries, stream, steps):
     na = int(iouts["n_accepted"].item())
     k = recs["kind"]
     events = int((((recs["route"] & 0x21) == 0x21) & np.isin(k, (DATA, HEARTBEAT, GAP))).sum())
-    # algorithmic bytes: every record read once (64 B), 1 accept byte written per record, 4 B per
-    # accepted index, per event 8 B of writer state read and 4 B of change-set bits touched
-    alg = n_rec * (64 + 1) + 4 * na + 12 * events
+    # algorithmic bytes: every record read once (64 B), 1 accept byte written per record, 8 B per
+    # delivery, per event 8 B of proxy state read and 4 B of change-set bits touched
+    alg = n_rec * (64 + 1) + 8 * na + 12 * events
     return {"kernel": "rtps_ingest (classify + heartbeat sort/scans + marks + decide + select + merge + state)",
             "ms": ms, "records": n_rec, "events": events, "accepted": na,
             "samples_per_s": na / (ms * 1e-3), "records_per_s": n_rec / (ms * 1e-3),
@@ -336,35 +442,54 @@ def c1_loopback(dev, stream, n=200_000, batch=16384, publishers=1):
             "publisher_flow_wait_s": send_s[1], "cpu_reference_parse_per_s_1_thread": n / cpu_s}
 
 
-def cpu_baseline(workload, n, target_cpu_s=10.0, match_table=None):
+def host_cpus():
+    """CPUs this process may use: the affinity mask, capped by a cgroup CPU quota
+    (a GPU box grants each GPU a share of the host: os.cpu_count() is the machine)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    use = aff if quota is None else max(1, min(aff, int(quota)))
+    return use, {"nproc": os.cpu_count(), "affinity": aff, "cgroup_quota_cpus": quota}
+
+
+def cpu_baseline(workload, n, match_table=None, samples=5, min_sample_s=0.25):
     """The oracle (C restatement of the reference parse) on this host's cores, with the
-    same match table as the device run."""
+    same readers as the device run: all usable cores (contiguous slices, one thread
+    each) and one thread; median of `samples` timed samples each.
+    A sample repeats the full batch until it has run `min_sample_s`."""
     import oracle
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads, cpus = host_cpus()
     arena, off, ln = oracle.gen(rtps_rx.WORKLOADS[workload], n)
-    oracle.parse(arena, off, ln, threads=threads, match_table=match_table)  # warm
-    t0 = time.perf_counter()
-    c0 = time.process_time()
-    reps = 0
-    while True:
-        oracle.parse(arena, off, ln, threads=threads, want_match=True, match_table=match_table)
-        reps += 1
-        if time.process_time() - c0 >= target_cpu_s or time.perf_counter() - t0 > 60:
-            break
-    dt = time.perf_counter() - t0
-    # one thread too (BASELINE.md section 2 plan): a quarter of the batch, best of 3
-    q = max(1, n // 4)
-    best = float("inf")
-    for _ in range(3):
-        s0 = time.perf_counter()
-        oracle.parse(arena, off[:q], ln[:q], threads=1, want_match=True, match_table=match_table)
-        best = min(best, time.perf_counter() - s0)
-    return {"value": reps * n / dt, "unit": "datagrams/s", "cores": threads, "kind": "port",
-            "gib_per_s": reps * float(ln.astype(np.int64).sum()) / dt / 2**30,
-            "sample": f"{reps} x full {workload} batch ({n} datagrams, generated on host), oracle/rtps_oracle.c "
-                      f"on {threads} threads, {dt:.2f} s wall",
-            "single_thread": {"value": q / best, "unit": "datagrams/s", "cores": 1,
-                              "sample": f"first {q} datagrams of the same batch, best of 3"}}
+
+    def rate(th, k):
+        o, l = off[:k], ln[:k]
+        oracle.parse(arena, o, l, threads=th, want_targets=False, match_table=match_table)  # warm
+        rates = []
+        for _ in range(samples):
+            t0 = time.perf_counter()
+            reps = 0
+            while True:
+                oracle.parse(arena, o, l, threads=th, want_targets=False, match_table=match_table)
+                reps += 1
+                if time.perf_counter() - t0 >= min_sample_s:
+                    break
+            rates.append(reps * k / (time.perf_counter() - t0))
+        return float(np.median(rates)), rates
+
+    v_all, r_all = rate(threads, n)
+    v_one, r_one = rate(1, n)
+    return {"value": v_all, "unit": "datagrams/s", "cores": threads, "kind": "port",
+            "host": cpus,
+            "sample": f"full {workload} batch ({n} datagrams, generated on host), oracle/rtps_oracle.c on "
+                      f"{threads} threads (contiguous slices), median of {samples} samples of >= {min_sample_s} s",
+            "samples": r_all,
+            "single_thread": {"value": v_one, "unit": "datagrams/s", "cores": 1,
+                              "sample": f"the same batch on 1 thread, median of {samples}", "samples": r_one}}
 
 
 def main():
@@ -372,13 +497,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--workload", default="T", choices=sorted(rtps_rx.WORKLOADS))
-    ap.add_argument("--datagrams", type=int, default=1 << 20, help="datagrams per GPU")
+    ap.add_argument("--workload", default=None, choices=sorted(rtps_rx.WORKLOADS) + ["C5"],
+                    help="default: T at N=1 (the headline config), C5 at N>1 (BASELINE config 8xMI355X)")
+    ap.add_argument("--datagrams", type=int, default=None, help="datagrams per GPU (default 1M; C5: 64M / N)")
     ap.add_argument("--writers", type=int, default=16)
     ap.add_argument("--spec-hint", type=int, default=None,
                     help="rtps_rx_set_spec_hint (records per datagram; 0 = mixed traffic, chained launch)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-cdr", action="store_true", help="skip the CDR decode (a18) measurement")
     ap.add_argument("--no-frag", action="store_true", help="skip the DataFrag reassembly measurement (C4)")
@@ -386,8 +511,9 @@ def main():
     ap.add_argument("--no-c1", action="store_true", help="skip the C1 UDP-loopback pipeline measurement")
     ap.add_argument("--match", default="writers", choices=["writers", "none"],
                     help="match table: every writer of the workload (a reader subscribed to all of them) or none")
-    ap.add_argument("--exchange", default="descriptors", choices=["descriptors", "records"],
-                    help="N>1: what crosses xGMI (16-B descriptors of matched records, or 64-B records)")
+    ap.add_argument("--exchange", default="records", choices=["records", "descriptors"],
+                    help="N>1: what crosses xGMI: the 64-B records of every writer / reader submessage, owner = "
+                         "writer-GUID hash % N (north_star), or 16-B descriptors of MATCHED records")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N>1 (gloo only to rehearse several ranks on one GPU)")
     args = ap.parse_args()
@@ -416,8 +542,12 @@ def main():
         dist.all_reduce(x, op=dist.ReduceOp.MAX)
         return x
 
-    wl = rtps_rx.WORKLOADS[args.workload]
-    n = args.datagrams
+    args.workload = args.workload or ("C5" if world > 1 else "T")
+    c5 = args.workload == "C5"
+    wl = rtps_rx.WL_C3 if c5 else rtps_rx.WORKLOADS[args.workload]
+    n = args.datagrams or ((C5_TOTAL // world) if c5 else 1 << 20)
+    if c5:  # the C5 batch is the C3 mix; what is not a parse / exchange measurement is skipped
+        args.no_cdr = args.no_frag = args.no_ingest = args.no_c1 = args.no_e2e = True
 
     # ---- input: this rank's chunk of the synthetic stream, generated in HBM ----
     off, ln, size = rtps_rx.gen_layout(wl, n, first_idx=rank * n, n_writers=args.writers)
@@ -447,7 +577,7 @@ def main():
         # GUIDs found in this batch, sorted (the same table, in the same order, on every rank)
         rx.parse_batch_device(arena, off_t, ln_t, n, outs)
         torch.cuda.synchronize(dev)
-        r = outs["records"][:n_rec].cpu().numpy().reshape(-1).view(RECORD_DTYPE)
+        r = outs["records"][:min(n_rec, 1 << 22)].cpu().numpy().reshape(-1).view(RECORD_DTYPE)
         wk = np.isin(r["kind"], [DATA, DATA_FRAG, HEARTBEAT, HEARTBEAT_FRAG, GAP])
         g = np.concatenate([r["prefix"][wk], r["writer_id"][wk]], axis=1)
         guids = np.unique(g.view(np.dtype((np.void, 16))).reshape(-1))
@@ -515,9 +645,17 @@ def main():
 
     # ---- results / sanity (outside the timed region) ----
     status = outs["status"][:n].cpu().numpy()
-    recs = outs["records"][:n_rec].cpu().numpy().reshape(-1).view(RECORD_DTYPE)
-    alg_total, alg_reads, alg_writes = algorithmic_bytes(status, recs, n)
-    traffic, traffic_src = pmc_traffic(args.workload) if world == 1 else (None, None)
+    alg_total = alg_reads = alg_writes = 0
+    recs = None
+    chunk = 1 << 23
+    for c0 in range(0, n_rec, chunk):  # in chunks: C5 at N=1 holds 256M records (16 GB)
+        rc = outs["records"][c0:min(n_rec, c0 + chunk)].cpu().numpy().reshape(-1).view(RECORD_DTYPE)
+        if n_rec <= chunk:
+            recs = rc
+        _, r_, w_ = algorithmic_bytes(status if c0 == 0 else status[:0], rc, n if c0 == 0 else 0)
+        alg_reads += r_
+        alg_writes += w_
+    alg_total = alg_reads + alg_writes
     total_bytes = float(ln.astype(np.int64).sum())
     ms_per_step = wall / args.steps * 1e3
     value = world * n / (wall / args.steps)
@@ -525,13 +663,15 @@ def main():
         "metric": "RTPS datagrams/s + GiB/s parsed (device-resident), 1/2/4/8 MI355X",
         "value": value,
         "unit": "datagrams/s",
-        "gib_per_s_parsed": world * total_bytes / (wall / args.steps) / 2**30,
+        # the datagram bytes the parse covers per second: NOT an HBM bandwidth (the parse is
+        # zero-copy and reads only headers and fixed fields; roofline below has the bytes it moves)
+        "gib_per_s_covered": world * total_bytes / (wall / args.steps) / 2**30,
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if c5 else "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (deterministic generator f(seed=0x52545053, idx), generated in HBM)",
@@ -541,32 +681,28 @@ def main():
                    "parallelism": f"{world} ranks, datagram-sharded" + (
                        ", writer-GUID all-to-all (" + ("RCCL" if args.backend == "nccl" else "gloo") + ")"
                        if world > 1 else "")},
-        "roofline": {"bound": "hbm", "achieved": alg_total / (ev_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": alg_total / (ev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                     "traffic": traffic, "traffic_source": traffic_src,
-                     "kernel": ("rtps_parse_spec_kernel (or rtps_parse_chain_kernel, chosen "
-                                "per batch from the traffic mix) + rtps_parse_fix_kernel: one rtps_rx_parse_batch"),
-                     "kernel_ms": ev_ms,
-                     "kernel_ms_source": "HIP event pair on the parse stream around the K back-to-back steps, / K",
-                     "alg_bytes_per_launch": alg_total, "alg_read_bytes": alg_reads, "alg_write_bytes": alg_writes,
-                     "note": "zero-copy parse: payload bytes are not read (the reference's Bytes::split_off is "
-                             "zero-copy too); alg bytes = header/fixed-field reads + record writes"},
     }
+    if world == 1:
+        result["roofline"] = roofline(rx, args, arena, off_t, ln_t, n, outs, stream, total_bytes, alg_reads,
+                                      alg_writes)
+    else:
+        result["roofline"] = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+                              "traffic": None, "kernel_ms": ev_ms,
+                              "note": "N>1: per-step time on the compute stream (parse + bucket, waiting for the "
+                                      "exchange two steps back); the kernel roofline is the N=1 line's"}
     if world > 1:
-        result["roofline"]["note"] += ("; kernel_ms here is the per-step time on the compute stream (parse + "
-                                       "bucket, waiting for the exchange two steps back)")
         got, split = exch[(args.warmup + args.steps - 1) & 1].gather_received()
         result["config"]["received_records_rank0"] = int(got.shape[0])
         ib = 16 if args.exchange == "descriptors" else 64
         result["config"]["exchange"] = {
             "mode": "padded equal-split all-to-all, pipelined with the next parse",
-            "item": (f"{ib}-B rtps_xdesc of matched records, owner = match-table entry % world"
+            "item": (f"{ib}-B rtps_xdesc of matched records, owner = writer set % world"
                      if ib == 16 else "64-B records, owner = writer-GUID hash % world"),
             "bucket_capacity": bcap, "bytes_sent_per_rank_per_step": world * bcap * ib,
             "overflow": any(e.overflowed() for e in exch)}
     if world == 1 and not args.no_cdr:
         result["cdr_decode"] = cdr_decode_leg(rx, args.workload, arena, off_t, outs, n_rec, stream, args.steps)
-    if world == 1 and not args.no_frag and args.workload == "C4":
+    if world == 1 and not args.no_frag and args.workload == "C4" and recs is not None:
         result["frag_assemble"] = frag_leg(rx, arena, off_t, outs, n_rec, recs, stream, args.steps)
     if world == 1 and not args.no_ingest and n_matched_writers:
         result["ingest"] = ingest_leg(rx, arena, off_t, outs, n_rec, recs, n_matched_writers, stream, args.steps)
@@ -578,7 +714,7 @@ def main():
     if world == 1 and not args.no_e2e:
         result["end_to_end"] = end_to_end(rx, arena, off_t, ln_t, n, outs, n_rec, stream)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args.workload, n, args.cpu_seconds, match_table=tbl)
+        result["cpu_baseline"] = cpu_baseline("C3" if c5 else args.workload, min(n, 1 << 20), match_table=tbl)
     if rank == 0:
         print(json.dumps(result), flush=True)
     rx.close()

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define RTPS_RX_ABI_VERSION 1u
+#define RTPS_RX_ABI_VERSION 2u /* 2: reader sets (rtps_rx_set_readers), u32 targets, deliveries */
 
 /* Largest datagram the record layout can address (u16 offsets).  The
  * reference's io_uring provided buffers are 64 KiB each
@@ -92,7 +92,10 @@ enum rtps_kind {
 #define RTPS_ROUTE_HAS_QOS 0x04u     /* DATA / DATA_FRAG: inline QoS present (Q flag)    */
 #define RTPS_ROUTE_HAS_PAYLOAD 0x08u /* DATA with D|K, DATA_FRAG: serialized payload    */
 #define RTPS_ROUTE_BUILTIN 0x10u     /* (reader_id, writer_id) is a builtin discovery pair */
-#define RTPS_ROUTE_MATCHED 0x20u     /* writer GUID found in the match table             */
+/* Writer kinds that are not a builtin pair go to the local readers
+ * (io_uring/rtps/dp_event_loop.rs:266-327): */
+#define RTPS_ROUTE_MATCHED 0x20u     /* some target reader has a writer proxy for the full writer GUID */
+#define RTPS_ROUTE_TARGETED 0x40u    /* some local reader contains_writer(writer_id) (reader.rs:474-484) */
 
 /* ---- rtps_record.payload_kind (Reader::data_to_dds_data, reader.rs:760-833) */
 enum rtps_payload_kind {
@@ -151,7 +154,55 @@ RTPS_RX_STATIC_ASSERT(offsetof(rtps_record, sn) == 32, "rtps_record.sn at 32");
 RTPS_RX_STATIC_ASSERT(offsetof(rtps_record, u) == 40, "rtps_record.u at 40");
 RTPS_RX_STATIC_ASSERT(offsetof(rtps_record, ts_sec) == 56, "rtps_record.ts_sec at 56");
 
-/* ---- writer GUID -> local reader slot (Reader::matched_writers) --------- */
+/* ---- local readers and their writer proxies (classification, a15) -------
+ * The reference routes a writer submessage that is not a builtin pair to
+ *   available_readers.values_mut().filter(|r| r.contains_writer(writer_id))
+ *                                          io_uring/rtps/dp_event_loop.rs:266-275
+ * where available_readers is a BTreeMap keyed by the reader's EntityId
+ * (io_uring/rtps/message_receiver.rs:129) and contains_writer tests the ENTITY
+ * ID of every matched writer, and is false for a stateless reader
+ * (io_uring/rtps/reader.rs:474-484).  Each target reader then looks its
+ * writer proxy up by the FULL writer GUID (matched_writers, a BTreeMap<GUID,
+ * RtpsWriterProxy>, reader.rs:145, 712-738): with a proxy the sample is
+ * deduplicated; without one it is dropped for a user-defined writer entity
+ * kind and accepted otherwise (reader.rs:734-739).
+ * The caller describes every reader and every (reader, writer GUID) proxy;
+ * the library turns them into TARGET SETS, one per distinct outcome:
+ *   - writer sets 0 .. W-1: one per distinct writer GUID that has a proxy in a
+ *     non-stateless reader, numbered in order of first appearance in proxies[];
+ *   - entity sets W .. W+E-1: one per distinct writer entity id of those
+ *     proxies, first-appearance order (a writer GUID with no proxy whose
+ *     entity id some reader contains).
+ * A set lists its target readers in EntityId order with, per reader, the
+ * proxy of the record's writer GUID (writer sets) or RTPS_NO_PROXY.  A
+ * writer-kind record that is not a builtin pair gets target = the writer set
+ * of prefix||writer_id if there is one (RTPS_ROUTE_MATCHED | TARGETED), else
+ * the entity set of writer_id (RTPS_ROUTE_TARGETED), else RTPS_NO_TARGET. */
+#define RTPS_READER_STATELESS 0x1u   /* like_stateless: never a target (reader.rs:474-484)            */
+#define RTPS_READER_BEST_EFFORT 0x2u /* Reliability BestEffort: HEARTBEATs ignored (reader.rs:870-881) */
+/* set by the library in rtps_target.reader_flags for a reader whose entity id is
+ * SPDP_BUILTIN_PARTICIPANT_READER: it accepts duplicate samples (reader.rs:712-722) */
+#define RTPS_TARGET_DUPLICATES_OK 0x8000u
+typedef struct rtps_reader {
+  uint8_t entity_id[4];  /* the reader's EntityId: its available_readers key (unique, orders the sets) */
+  uint16_t reader_slot;  /* caller-defined handle reported in targets and deliveries */
+  uint16_t flags;        /* RTPS_READER_* */
+} rtps_reader;
+typedef struct rtps_proxy {  /* one RtpsWriterProxy: an entry of the reader's matched_writers */
+  uint8_t writer_guid[16];   /* prefix[12] || entity_id[4]; unique per reader */
+  uint32_t reader;           /* index into the readers[] array */
+} rtps_proxy;
+typedef struct rtps_target {  /* one target reader of a target set */
+  uint16_t reader_slot;
+  uint16_t reader_flags;      /* the reader's RTPS_READER_* | RTPS_TARGET_DUPLICATES_OK */
+  uint32_t proxy;             /* index into proxies[] of (this reader, the writer GUID), or RTPS_NO_PROXY */
+} rtps_target;
+#define RTPS_NO_TARGET 0xFFFFFFFFu
+#define RTPS_NO_PROXY 0xFFFFFFFFu
+
+/* Compatibility form: (writer GUID, reader slot) pairs.  Every distinct slot
+ * becomes one reliable, stateful reader (EntityId order = order of first
+ * appearance), every pair one proxy of that reader (repeated pairs once). */
 typedef struct rtps_match {
   uint8_t writer_guid[16]; /* prefix[12] || entity_id[4] */
   uint16_t reader_slot;    /* caller-defined local reader index (< 0xFFFF) */
@@ -176,7 +227,7 @@ typedef struct rtps_rx_out {
   uint8_t* status;          /* [n]            required */
   rtps_record* records;     /* [max_records]  required */
   uint64_t max_records;
-  uint16_t* match;          /* [max_records]  optional: reader slot or RTPS_NO_MATCH */
+  uint32_t* target;         /* [max_records]  optional: target set of the record or RTPS_NO_TARGET */
   uint32_t* rec_begin;      /* [n]            optional: index of datagram i's first record */
   uint64_t* n_records;      /* [1]            required: total records of the batch */
 } rtps_rx_out;
@@ -199,8 +250,19 @@ int rtps_rx_destroy(rtps_rx_ctx* ctx);
  * (the default after rtps_rx_create). */
 #define RTPS_RX_OWN_STREAM ((void*)(intptr_t)-1)
 int rtps_rx_set_stream(rtps_rx_ctx* ctx, void* hip_stream);
-/* Replace the writer-GUID -> reader-slot table (first entry wins on duplicates). */
+/* Replace the local readers and their writer proxies (Domain registration +
+ * Reader::matched_writer_add).  RTPS_RX_EINVAL for a repeated reader entity id,
+ * a repeated (reader, writer GUID) proxy or a reader index out of range.
+ * Ingest state is kept per proxy index (see rtps_rx_ingest). */
+int rtps_rx_set_readers(rtps_rx_ctx* ctx, const rtps_reader* readers, uint32_t n_readers,
+                        const rtps_proxy* proxies, uint32_t n_proxies);
+/* Compatibility form of rtps_rx_set_readers (see rtps_match): proxy i = the
+ * i-th distinct (writer GUID, slot) pair. */
 int rtps_rx_set_match_table(rtps_rx_ctx* ctx, const rtps_match* table, uint32_t n);
+/* Host view of the current target sets: set t lists entries[first[t] .. first[t+1]).
+ * Valid until the next set_readers / set_match_table. */
+int rtps_rx_target_table(const rtps_rx_ctx* ctx, const uint32_t** first, const rtps_target** entries,
+                         uint32_t* n_sets);
 /* Parse n datagrams: datagram i = arena[dgram_off[i] .. dgram_off[i]+dgram_len[i]).
  * arena, dgram_off, dgram_len are DEVICE pointers.  Asynchronous on the
  * context's stream; call rtps_rx_sync (or synchronise the stream) before
@@ -222,7 +284,8 @@ const char* rtps_rx_strerror(int code);
 
 /* Multi-GPU sharding (>= 2 GPUs): stable partition of the writer/reader-kind
  * records (interpreter records are not exchanged) by owner GPU =
- * fnv1a32(prefix || writer_id) % n_dest (the same hash as the match table).
+ * fmix32(fnv1a32(prefix || writer_id)) % n_dest (FNV-1a over the GUID's four
+ * little-endian words, then the murmur3 finaliser).
  * recs/n_records are a parse_batch output (device); out has room for
  * max_records records; dest_counts[n_dest] (device u64) receives the bucket
  * sizes; bucket d starts at sum(dest_counts[0..d)).  Input order is kept
@@ -239,23 +302,46 @@ int rtps_rx_bucket_by_writer_padded(rtps_rx_ctx* ctx, const rtps_record* recs, c
 
 /* Exchange descriptors (>= 2 GPUs): the compact form of a matched writer's
  * record that crosses xGMI instead of the 64-byte record.  Only records with
- * RTPS_ROUTE_MATCHED are exchanged (writer submessages of writers in the match
- * table: what a reader's per-writer state consumes, io_uring/rtps/reader.rs
- * handle_*_msg).  Owner GPU = match-table entry index % n_dest: writers are
- * spread round-robin in the order the table lists them, so the owners are
- * balanced whatever the GUID hash does; payloads and full records stay on the
- * source GPU (rec_idx). */
+ * RTPS_ROUTE_MATCHED are exchanged (writer submessages of writers with a
+ * proxy: what a reader's per-writer state consumes, io_uring/rtps/reader.rs
+ * handle_*_msg).  Owner GPU = writer set index % n_dest: writers are spread
+ * round-robin in the order the proxies list them, so the owners are balanced
+ * whatever the GUID hash does; payloads and full records stay on the source
+ * GPU (rec_idx). */
 typedef struct rtps_xdesc {
   int64_t sn;            /* writer sequence number */
   uint32_t rec_idx;      /* index of the full record in the source rank's parse output */
-  uint32_t writer_kind;  /* match-table entry index << 8 | submessage kind */
+  uint32_t writer_kind;  /* writer set index << 8 | submessage kind */
 } rtps_xdesc;
 /* Stable partition of the MATCHED records' descriptors into n_dest buckets of
  * cap descriptors each (out[d*cap, (d+1)*cap)); dest_counts as in
- * rtps_rx_bucket_by_writer_padded.  Needs a match table (RTPS_RX_EINVAL without). */
+ * rtps_rx_bucket_by_writer_padded.  Needs readers (RTPS_RX_EINVAL without). */
 int rtps_rx_bucket_descriptors(rtps_rx_ctx* ctx, const rtps_record* recs, const uint64_t* n_records,
                                uint64_t max_records, uint32_t n_dest, uint64_t cap, rtps_xdesc* out,
                                uint64_t* dest_counts);
+
+/* ---- the exchange over RCCL (>= 2 GPUs) -------------------
+ * One process (rank) per GPU; the communicator is an RCCL ncclComm_t passed as
+ * void*: create it with rtps_rx_exchange_unique_id on one rank, an out-of-band
+ * broadcast of the 128 bytes (the host's own control channel), and
+ * rtps_rx_exchange_comm_init on every rank; or pass a ncclComm_t the host
+ * already has.  New: the reference has one process and no collective. */
+#define RTPS_RX_EXCHANGE_ID_BYTES 128
+int rtps_rx_exchange_unique_id(uint8_t id[RTPS_RX_EXCHANGE_ID_BYTES]);
+int rtps_rx_exchange_comm_init(const uint8_t id[RTPS_RX_EXCHANGE_ID_BYTES], int n_ranks, int rank, int device,
+                               void** comm);
+int rtps_rx_exchange_comm_destroy(void* comm);
+/* Equal-split all-to-all of fixed-capacity buckets (the output of
+ * rtps_rx_bucket_by_writer_padded or rtps_rx_bucket_descriptors): bucket d
+ * (send + d*cap*item_bytes) goes to rank d, rank s's bucket for this rank lands
+ * at recv + s*cap*item_bytes; the true bucket sizes travel alongside
+ * (send_counts[n_ranks] -> recv_counts[n_ranks], device u64; a size > cap means
+ * that bucket overflowed).  One ncclGroupStart/End of ncclSend/ncclRecv per
+ * peer on hip_stream (NULL: the context's stream; a separate stream lets the
+ * exchange of batch k overlap the parse of batch k+1): asynchronous, no host
+ * round trip. */
+int rtps_rx_exchange(rtps_rx_ctx* ctx, void* comm, void* hip_stream, const void* send, const uint64_t* send_counts,
+                     uint64_t cap, uint32_t item_bytes, void* recv, uint64_t* recv_counts);
 
 /* ---- batch CDR primitive decode (a18) ------------------------------------
  * Replaces, for fixed-layout sample types, the per-sample decode
@@ -365,9 +451,9 @@ int rtps_rx_frag_assemble(rtps_rx_ctx* ctx, const uint8_t* arena, uint64_t arena
 int rtps_rx_frag_reset(rtps_rx_ctx* ctx);
 
 /* ---- history-cache ingest ---------------------------
- * Replaces, for every matched writer (match-table entry) of a stateful reader,
- * the writer-proxy bookkeeping that decides which samples enter the history
- * cache:
+ * Replaces, for every target reader of every routed writer submessage, the
+ * writer-proxy bookkeeping that decides which samples enter that reader's
+ * history cache:
  *   Reader::handle_data_msg -> process_received_data      io_uring/rtps/reader.rs:514-561, 693-758
  *     RtpsWriterProxy::should_ignore_change, received_changes_add, advance_ack_base
  *                                                         rtps/rtps_writer_proxy.rs:202-224, 338-355
@@ -379,34 +465,48 @@ int rtps_rx_frag_reset(rtps_rx_ctx* ctx);
  *     for every listed SN                                 reader.rs:1060-1116, rtps_writer_proxy.rs:226-239
  *   TopicCache::add_change duplicate check, mark_reliably_received_before
  *                                                         structure/dds_cache.rs:200-262
- * Events are the records of a parse_batch output with RTPS_ROUTE_PASS and
- * RTPS_ROUTE_MATCHED, in record order: DATA with payload_kind DATA / KEY /
- * KEY_HASH and completed DataFrag samples (status != RTPS_FRAG_SHORT, placed
- * at their completing record) are samples; HEARTBEAT and GAP update the
- * writer's state.  A sample enters the cache (accept = 1) iff its writer proxy
- * does not ignore it: sn >= all_ackable_before and sn not in the writer's
- * change set (received or irrelevant).  Other records get accept = 0
- * (unmatched writers: the reference drops user-defined ones; discovery traffic
- * has its own path).  State per match-table entry (all_ackable_before, the
- * change set above it, received_heartbeat_count) persists in the context across
- * batches; it is indexed by entry position, so keep entries in place (append
- * new writers) or call rtps_rx_ingest_reset after reordering the table.
+ * Events are the records of a parse_batch output with RTPS_ROUTE_PASS, in
+ * record order, delivered to every reader of their target set in set order
+ * (dp_event_loop.rs:272-326): DATA with payload_kind DATA / KEY / KEY_HASH and
+ * completed DataFrag samples (status != RTPS_FRAG_SHORT, placed at their
+ * completing record) are samples; HEARTBEAT and GAP update the proxy's state.
+ * For one (record, target reader):
+ *   - a sample with a proxy enters the reader's cache iff the proxy does not
+ *     ignore it: sn >= all_ackable_before and sn not in the proxy's change set
+ *     (received or irrelevant), or always for a RTPS_TARGET_DUPLICATES_OK
+ *     reader (process_received_data, reader.rs:693-733);
+ *   - a sample without a proxy enters iff the writer's entity kind is not
+ *     user-defined (kind & 0xF0 != 0, reader.rs:734-739; guid.rs:168-170);
+ *   - HEARTBEAT / GAP without a proxy, HEARTBEAT for a BestEffort reader: no
+ *     effect (reader.rs:871-891, 1071-1086).
+ * Every accepted (record, reader) pair is one delivery.  State per proxy
+ * (all_ackable_before, the change set above it, received_heartbeat_count)
+ * persists in the context across batches; it is indexed by proxy position, so
+ * keep proxies in place (append new ones) or call rtps_rx_ingest_reset after
+ * reordering them.
  * Limit: the change set is kept for RTPS_INGEST_WINDOW sequence numbers from
  * all_ackable_before; a sample further ahead is accepted without the duplicate
  * check and counted in *n_window_overflow (the reference's BTreeMap has no bound). */
 #define RTPS_INGEST_WINDOW (1u << 17)
-#define RTPS_INGEST_BEST_EFFORT 0x1u /* flags: BestEffort reader, HEARTBEATs ignored (reader.rs:870-881) */
+#define RTPS_INGEST_BEST_EFFORT 0x1u /* flags: treat every reader as BestEffort (HEARTBEATs ignored) */
+typedef struct rtps_delivery {  /* one sample accepted into one reader's history cache */
+  uint32_t rec_idx;             /* the record (completing record of a DataFrag sample) */
+  uint16_t reader_slot;
+  uint16_t _r;
+} rtps_delivery;
 typedef struct rtps_ingest_out {
-  uint8_t* accept;              /* [max_records] device: 1 = this record's sample enters the cache */
-  uint32_t* accepted;           /* [max_records] device: indices of the accepting records, ascending */
-  uint64_t* n_accepted;         /* device u64 */
-  int64_t* ack_base;            /* device, optional: all_ackable_before() of every entry after the batch */
+  uint8_t* accept;              /* [max_records] device: readers whose cache the record's sample enters
+                                   (saturating at 255); 0 = none */
+  rtps_delivery* accepted;      /* [max_accepted] device: deliveries, ascending (record, set order) */
+  uint64_t max_accepted;        /* deliveries past it are counted but not written */
+  uint64_t* n_accepted;         /* device u64: deliveries of the batch */
+  int64_t* ack_base;            /* device, optional: all_ackable_before() of every proxy after the batch */
   uint64_t* n_window_overflow;  /* device u64, optional */
 } rtps_ingest_out;
 /* arena / dgram_off / records / n_records / max_records: the batch and its
  * parse_batch output (GAP bitmaps are read from the arena).  frag / n_frag /
  * max_frag: optional rtps_rx_frag_assemble output of the same batch (device;
- * NULL = none).  Asynchronous on the context's stream; needs a match table. */
+ * NULL = none).  Asynchronous on the context's stream; needs readers. */
 int rtps_rx_ingest(rtps_rx_ctx* ctx, const uint8_t* arena, uint64_t arena_len, const uint64_t* dgram_off,
                    const rtps_record* records, const uint64_t* n_records, uint64_t max_records,
                    const rtps_frag_sample* frag, const uint64_t* n_frag, uint64_t max_frag, uint32_t flags,

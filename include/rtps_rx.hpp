@@ -65,7 +65,7 @@ struct PassedSubmessage {
 struct BatchResult {
   std::vector<uint8_t> status;
   std::vector<rtps_record> records;
-  std::vector<uint16_t> match;
+  std::vector<uint32_t> target;  // target set per record (RTPS_NO_TARGET: none)
   std::vector<uint32_t> rec_begin;
   uint64_t n_records = 0;
 
@@ -108,6 +108,21 @@ class MessageReceiver {
   void set_match_table(const std::vector<rtps_match>& t) {
     check(rtps_rx_set_match_table(ctx_, t.data(), (uint32_t)t.size()), "rtps_rx_set_match_table");
   }
+  // available_readers + each Reader's matched_writers (see rtps_rx_set_readers)
+  void set_readers(const std::vector<rtps_reader>& readers, const std::vector<rtps_proxy>& proxies) {
+    check(rtps_rx_set_readers(ctx_, readers.data(), (uint32_t)readers.size(), proxies.data(),
+                              (uint32_t)proxies.size()),
+          "rtps_rx_set_readers");
+  }
+  // the target readers of a record's target set (empty for RTPS_NO_TARGET)
+  std::vector<rtps_target> targets(uint32_t target) const {
+    const uint32_t* first = nullptr;
+    const rtps_target* ent = nullptr;
+    uint32_t n = 0;
+    check(rtps_rx_target_table(ctx_, &first, &ent, &n), "rtps_rx_target_table");
+    if (target == RTPS_NO_TARGET || target >= n) return {};
+    return std::vector<rtps_target>(ent + first[target], ent + first[target + 1]);
+  }
 
   // host datagrams in (arena + offsets + lengths), host results out
   BatchResult handle_received_batch(const std::vector<uint8_t>& arena, const std::vector<uint64_t>& off,
@@ -119,11 +134,11 @@ class MessageReceiver {
     DeviceBuffer<uint32_t> d_len(n), d_rb(n);
     DeviceBuffer<uint8_t> d_status(n);
     DeviceBuffer<rtps_record> d_recs(cap);
-    DeviceBuffer<uint16_t> d_match(cap);
+    DeviceBuffer<uint32_t> d_target(cap);
     d_arena.upload(arena.data(), arena.size());
     d_off.upload(off.data(), n);
     d_len.upload(len.data(), n);
-    rtps_rx_out out{d_status.get(), d_recs.get(), cap, d_match.get(), d_rb.get(), d_n.get()};
+    rtps_rx_out out{d_status.get(), d_recs.get(), cap, d_target.get(), d_rb.get(), d_n.get()};
     check(rtps_rx_parse_batch(ctx_, d_arena.get(), arena.size(), d_off.get(), d_len.get(), n, &out),
           "rtps_rx_parse_batch");
     check(rtps_rx_sync(ctx_), "rtps_rx_sync");
@@ -133,11 +148,11 @@ class MessageReceiver {
     r.status.resize(n);
     r.rec_begin.resize(n);
     r.records.resize(kept);
-    r.match.resize(kept);
+    r.target.resize(kept);
     d_status.download(r.status.data(), n);
     d_rb.download(r.rec_begin.data(), n);
     d_recs.download(r.records.data(), kept);
-    d_match.download(r.match.data(), kept);
+    d_target.download(r.target.data(), kept);
     return r;
   }
 

@@ -14,7 +14,8 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _REPO = os.path.dirname(_HERE)
 sys.path.insert(0, os.path.join(_REPO, "rustdds-io_uring_amd"))
-from rtps_rx.records import RECORD_DTYPE, MATCH_DTYPE, FRAG_SAMPLE_DTYPE, max_records  # noqa: E402
+from rtps_rx.records import (RECORD_DTYPE, FRAG_SAMPLE_DTYPE, TARGET_DTYPE, DELIVERY_DTYPE,  # noqa: E402
+                             max_records, as_readers)
 
 LIB_PATH = os.path.join(_HERE, "librtps_oracle.so")
 _lib = None
@@ -36,8 +37,11 @@ def lib():
         L = ctypes.CDLL(LIB_PATH)
         P = ctypes.c_void_p
         L.rtps_oracle_parse.restype = ctypes.c_uint64
-        L.rtps_oracle_parse.argtypes = [P, P, P, ctypes.c_uint32, P, P, ctypes.c_uint32,
-                                        P, P, ctypes.c_uint64, P, P, ctypes.c_int]
+        L.rtps_oracle_parse.argtypes = [P, P, P, ctypes.c_uint32, P, P, ctypes.c_uint32, P, ctypes.c_uint32,
+                                        P, P, ctypes.c_uint64, P, ctypes.c_int]
+        L.rtps_oracle_targets.restype = ctypes.c_uint64
+        L.rtps_oracle_targets.argtypes = [P, ctypes.c_uint64, P, ctypes.c_uint32, P, ctypes.c_uint32, P, P,
+                                          ctypes.c_uint64]
         L.rtps_oracle_gen_layout.restype = ctypes.c_uint64
         L.rtps_oracle_gen_layout.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
                                              ctypes.c_uint32, P, P]
@@ -52,11 +56,13 @@ def lib():
         L.rtps_oracle_frag_batch.restype = ctypes.c_uint64
         L.rtps_oracle_frag_batch.argtypes = [P, P, P, P, ctypes.c_uint64, P, ctypes.c_uint64, P, ctypes.c_uint64, P]
         L.rtps_oracle_ingest_new.restype = P
-        L.rtps_oracle_ingest_new.argtypes = [P, ctypes.c_uint32]
+        L.rtps_oracle_ingest_new.argtypes = [P, ctypes.c_uint32, P, ctypes.c_uint32]
         L.rtps_oracle_ingest_free.argtypes = [P]
+        L.rtps_oracle_ingest_set_readers.restype = None
+        L.rtps_oracle_ingest_set_readers.argtypes = [P, P, ctypes.c_uint32, P, ctypes.c_uint32]
         L.rtps_oracle_ingest_batch.restype = ctypes.c_uint64
         L.rtps_oracle_ingest_batch.argtypes = [P, P, P, P, ctypes.c_uint64, P, ctypes.c_uint64, ctypes.c_uint32,
-                                               P, P, P]
+                                               P, P, ctypes.c_uint64, P]
         L.rtps_oracle_cdr_decode.restype = None
         L.rtps_oracle_cdr_decode.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32, P, P, P, ctypes.c_uint64, P, P]
         assert L.rtps_oracle_record_size() == RECORD_DTYPE.itemsize
@@ -82,8 +88,16 @@ def pack(datagrams, align=16):
     return arena, offs, lens
 
 
-def parse(arena, offs, lens, own=OWN_PREFIX, match_table=None, threads=1, want_match=True):
-    """Returns (status u8[n], records RECORD_DTYPE[m], match u16[m], rec_begin u32[n])."""
+def _rt_args(table):
+    rd = as_readers(table)
+    r, p = rd.readers, rd.proxies
+    return rd, (_ptr(r) if len(r) else None), len(r), (_ptr(p) if len(p) else None), len(p)
+
+
+def parse(arena, offs, lens, own=OWN_PREFIX, match_table=None, threads=1, want_targets=True):
+    """Returns (status u8[n], records RECORD_DTYPE[m], targets, rec_begin u32[n]).
+    match_table: readers as rtps_rx.records.as_readers accepts (None: no readers);
+    targets: (off u64[m+1], TARGET_DTYPE[k]) = the target readers of every record."""
     arena = np.ascontiguousarray(arena, dtype=np.uint8)
     offs = np.ascontiguousarray(offs, dtype=np.uint64)
     lens = np.ascontiguousarray(lens, dtype=np.uint32)
@@ -91,15 +105,37 @@ def parse(arena, offs, lens, own=OWN_PREFIX, match_table=None, threads=1, want_m
     cap = max(max_records(lens), 1)
     status = np.zeros(n, dtype=np.uint8)
     recs = np.zeros(cap, dtype=RECORD_DTYPE)
-    match = np.zeros(cap, dtype=np.uint16) if want_match else None
     rec_begin = np.zeros(max(n, 1), dtype=np.uint32)
     own_a = np.frombuffer(bytes(own), dtype=np.uint8).copy()
-    tbl = match_table if match_table is not None else np.zeros(0, dtype=MATCH_DTYPE)
-    tbl = np.ascontiguousarray(tbl, dtype=MATCH_DTYPE)
-    total = lib().rtps_oracle_parse(_ptr(arena), _ptr(offs), _ptr(lens), n, _ptr(own_a),
-                                    _ptr(tbl) if len(tbl) else None, len(tbl), _ptr(status), _ptr(recs),
-                                    cap, _ptr(match), _ptr(rec_begin), threads)
-    return status, recs[:total], (match[:total] if want_match else None), rec_begin[:n]
+    rd, rp, nr, pp, np_ = _rt_args(match_table)
+    total = lib().rtps_oracle_parse(_ptr(arena), _ptr(offs), _ptr(lens), n, _ptr(own_a), rp, nr, pp, np_,
+                                    _ptr(status), _ptr(recs), cap, _ptr(rec_begin), threads)
+    recs = recs[:total]
+    return status, recs, (targets(recs, rd) if want_targets else None), rec_begin[:n]
+
+
+def targets(recs, table):
+    """Target readers of every record (rtps_oracle_targets): (off u64[m+1], TARGET_DTYPE[k])."""
+    recs = np.ascontiguousarray(recs, dtype=RECORD_DTYPE)
+    m = len(recs)
+    rd, rp, nr, pp, np_ = _rt_args(table)
+    off = np.zeros(m + 1, dtype=np.uint64)
+    cap = max(m * _widest(rd), 1)
+    out = np.zeros(cap, dtype=TARGET_DTYPE)
+    k = lib().rtps_oracle_targets(_ptr(recs) if m else None, m, rp, nr, pp, np_, _ptr(off), _ptr(out), cap)
+    assert k <= cap
+    return off, out[:int(k)]
+
+
+def _widest(rd):
+    """The most target readers a record can have: readers sharing one matched entity id."""
+    from rtps_rx.records import READER_STATELESS
+    by_eid = {}
+    for p in rd.proxies:
+        r = int(p["reader"])
+        if not rd.readers[r]["flags"] & READER_STATELESS:
+            by_eid.setdefault(bytes(p["writer_guid"][12:]), set()).add(r)
+    return max((len(v) for v in by_eid.values()), default=0)
 
 
 def gen(workload, n, seed=SEED, first_idx=0, n_writers=16):
@@ -156,12 +192,21 @@ class FragAssembler:
 
 
 class HistoryIngest:
-    """Sequential writer-proxy restatement with state across batches (rtps_oracle_ingest_*)."""
+    """Sequential writer-proxy restatement with state across batches (rtps_oracle_ingest_*),
+    one proxy per (reader, writer GUID) of the readers table."""
 
     def __init__(self, match_table):
-        t = np.ascontiguousarray(match_table, dtype=MATCH_DTYPE)
-        self.n = len(t)
-        self.h = ctypes.c_void_p(lib().rtps_oracle_ingest_new(_ptr(t) if len(t) else None, len(t)))
+        self.readers = as_readers(match_table)
+        self.n = self.readers.n_proxies
+        rd, rp, nr, pp, np_ = _rt_args(self.readers)
+        self.h = ctypes.c_void_p(lib().rtps_oracle_ingest_new(rp, nr, pp, np_))
+
+    def set_readers(self, match_table):
+        """New readers / proxies; proxy state is kept by position (as on the device)."""
+        self.readers = as_readers(match_table)
+        self.n = self.readers.n_proxies
+        rd, rp, nr, pp, np_ = _rt_args(self.readers)
+        lib().rtps_oracle_ingest_set_readers(self.h, rp, nr, pp, np_)
 
     def __del__(self):
         if getattr(self, "h", None):
@@ -169,17 +214,18 @@ class HistoryIngest:
             self.h = None
 
     def batch(self, arena, offs, recs, frag_samples=None, best_effort=False):
-        """-> (accept u8[m], accepted u32[k], ack_base i64[n_entries])."""
+        """-> (accept u8[m], deliveries DELIVERY_DTYPE[k], ack_base i64[n_proxies])."""
         arena = np.ascontiguousarray(arena, dtype=np.uint8)
         offs = np.ascontiguousarray(offs, dtype=np.uint64)
         recs = np.ascontiguousarray(recs, dtype=RECORD_DTYPE)
         m = len(recs)
         fs = None if frag_samples is None else np.ascontiguousarray(frag_samples, dtype=FRAG_SAMPLE_DTYPE)
         accept = np.zeros(max(m, 1), dtype=np.uint8)
-        accepted = np.zeros(max(m, 1), dtype=np.uint32)
+        cap = max(m * _widest(self.readers), 1)
+        dels = np.zeros(cap, dtype=DELIVERY_DTYPE)
         ack = np.zeros(max(self.n, 1), dtype=np.int64)
         k = lib().rtps_oracle_ingest_batch(self.h, _ptr(arena), _ptr(offs), _ptr(recs) if m else None, m,
                                            _ptr(fs) if fs is not None and len(fs) else None,
                                            0 if fs is None else len(fs), 1 if best_effort else 0,
-                                           _ptr(accept), _ptr(accepted), _ptr(ack))
-        return accept[:m], accepted[:int(k)], ack[:self.n]
+                                           _ptr(accept), _ptr(dels), cap, _ptr(ack))
+        return accept[:m], dels[:int(k)], ack[:self.n]

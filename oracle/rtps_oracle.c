@@ -25,6 +25,9 @@
  *   interpreter (iter_next)         <- io_uring/rtps/message_receiver.rs:56-119, 618-665, 289-295
  *   data_to_dds_data_kind           <- io_uring/rtps/reader.rs:760-833
  *   builtin pairs                   <- io_uring/discovery/discovery.rs:2795-2816, 3075-3095
+ *   oracle_targets                  <- io_uring/rtps/dp_event_loop.rs:266-327 (available_readers
+ *                                      filtered by contains_writer, reader.rs:474-484), matched
+ *                                      writer proxy by full GUID (reader.rs:712-739)
  *   rtps_oracle_cdr_decode          <- cdr_adapters.rs:246-275 + cdr-encoding 0.10 rules
  *   rtps_oracle_frag_batch          <- rtps/fragment_assembler.rs:23-214, reader.rs:563-647
  *   rtps_oracle_ingest_batch        <- rtps/rtps_writer_proxy.rs:202-355, reader.rs:514-1116
@@ -346,13 +349,112 @@ static int builtin_reader_pair(const uint8_t rid[4], const uint8_t wid[4]) {
          (eid_eq(wid, E_P2P_W) && eid_eq(rid, E_P2P_R));
 }
 
-/* matched_writers lookup by full GUID (reader.rs:474-484, 712-738): first entry wins */
-static uint16_t match_lookup(const rtps_match* table, uint32_t n, const uint8_t prefix[12],
-                             const uint8_t wid[4]) {
-  for (uint32_t i = 0; i < n; ++i)
-    if (memcmp(table[i].writer_guid, prefix, 12) == 0 && memcmp(table[i].writer_guid + 12, wid, 4) == 0)
-      return table[i].reader_slot;
-  return RTPS_NO_MATCH;
+/* The local readers: MessageReceiver::available_readers, a BTreeMap<EntityId,
+ * Reader> (io_uring/rtps/message_receiver.rs:129), so iteration is in EntityId
+ * byte order (EntityId derives Ord over {entity_key, entity_kind}, structure/guid.rs:208-216).
+ * Each reader's matched_writers are the proxies naming it. */
+typedef struct ox_proxy { uint32_t reader; uint8_t guid[16]; uint32_t index; } ox_proxy;
+typedef struct ox_eid { uint8_t eid[4]; uint32_t order; uint32_t reader; } ox_eid;
+typedef struct oracle_readers {
+  const rtps_reader* r;
+  uint32_t nr;
+  const rtps_proxy* p;
+  uint32_t np;
+  uint32_t* order;  /* reader indices in EntityId order */
+  /* lookup structures (the same relation, indexed so that a 1M-datagram batch with
+   * hundreds of readers and proxies stays fast; oracle_targets gives their meaning) */
+  ox_eid* eids;     /* (matched writer entity id, reader) of non-stateless readers, by (eid, EntityId order) */
+  uint32_t n_eids;
+  ox_proxy* px;     /* proxies by (reader, GUID) */
+} oracle_readers;
+
+static const oracle_readers* g_sort_ctx;
+static int reader_cmp(const void* a, const void* b) {
+  return memcmp(g_sort_ctx->r[*(const uint32_t*)a].entity_id, g_sort_ctx->r[*(const uint32_t*)b].entity_id, 4);
+}
+static int eid_cmp(const void* a, const void* b) {
+  const ox_eid *x = (const ox_eid*)a, *y = (const ox_eid*)b;
+  int c = memcmp(x->eid, y->eid, 4);
+  return c ? c : (x->order > y->order) - (x->order < y->order);
+}
+static int px_cmp(const void* a, const void* b) {
+  const ox_proxy *x = (const ox_proxy*)a, *y = (const ox_proxy*)b;
+  if (x->reader != y->reader) return x->reader < y->reader ? -1 : 1;
+  return memcmp(x->guid, y->guid, 16);
+}
+static void oracle_readers_init(oracle_readers* R, const rtps_reader* r, uint32_t nr, const rtps_proxy* p, uint32_t np) {
+  R->r = r; R->nr = nr; R->p = p; R->np = np;
+  R->order = (uint32_t*)malloc(sizeof(uint32_t) * (nr ? nr : 1));
+  for (uint32_t i = 0; i < nr; ++i) R->order[i] = i;
+  g_sort_ctx = R;  /* single-threaded setup */
+  qsort(R->order, nr, sizeof(uint32_t), reader_cmp);
+  uint32_t* rank = (uint32_t*)malloc(sizeof(uint32_t) * (nr ? nr : 1));
+  for (uint32_t k = 0; k < nr; ++k) rank[R->order[k]] = k;
+  R->eids = (ox_eid*)malloc(sizeof(ox_eid) * (np ? np : 1));
+  R->px = (ox_proxy*)malloc(sizeof(ox_proxy) * (np ? np : 1));
+  uint32_t ne = 0;
+  for (uint32_t k = 0; k < np; ++k) {
+    R->px[k].reader = p[k].reader;
+    memcpy(R->px[k].guid, p[k].writer_guid, 16);
+    R->px[k].index = k;
+    if (p[k].reader >= nr || (r[p[k].reader].flags & RTPS_READER_STATELESS)) continue;
+    memcpy(R->eids[ne].eid, p[k].writer_guid + 12, 4);
+    R->eids[ne].order = rank[p[k].reader];
+    R->eids[ne].reader = p[k].reader;
+    ne++;
+  }
+  qsort(R->px, np, sizeof(ox_proxy), px_cmp);
+  qsort(R->eids, ne, sizeof(ox_eid), eid_cmp);
+  uint32_t w = 0;  /* one entry per (eid, reader) */
+  for (uint32_t k = 0; k < ne; ++k)
+    if (!w || memcmp(R->eids[w - 1].eid, R->eids[k].eid, 4) || R->eids[w - 1].reader != R->eids[k].reader)
+      R->eids[w++] = R->eids[k];
+  R->n_eids = w;
+  free(rank);
+}
+static void oracle_readers_free(oracle_readers* R) { free(R->order); free(R->eids); free(R->px); }
+
+/* matched_writers.get(&writer_guid) (reader.rs:712-739): the proxy index or RTPS_NO_PROXY */
+static uint32_t matched_writer(const oracle_readers* R, uint32_t reader, const uint8_t prefix[12],
+                               const uint8_t wid[4]) {
+  ox_proxy key;
+  key.reader = reader;
+  memcpy(key.guid, prefix, 12);
+  memcpy(key.guid + 12, wid, 4);
+  const ox_proxy* f = (const ox_proxy*)bsearch(&key, R->px, R->np, sizeof(ox_proxy), px_cmp);
+  return f ? f->index : RTPS_NO_PROXY;
+}
+static const uint8_t E_SPDP_R_ID[4] = {0x00, 0x01, 0x00, 0xc7};
+/* The target readers of a writer submessage that is not a builtin pair
+ * (Domain::handle_event, io_uring/rtps/dp_event_loop.rs:266-327):
+ *   available_readers.values_mut().filter(|r| r.contains_writer(writer_entity_id))
+ * i.e. in EntityId order, every reader that is not stateless and has a matched
+ * writer with this ENTITY ID (Reader::contains_writer, reader.rs:474-484), each
+ * with its proxy of the full writer GUID.  Writes up to cap targets into out
+ * (may be NULL), returns the count; *matched = some target has a proxy. */
+static uint32_t oracle_targets(const oracle_readers* R, const uint8_t prefix[12], const uint8_t wid[4],
+                               rtps_target* out, uint32_t cap, int* matched) {
+  *matched = 0;
+  /* first (eid, *) entry: lower bound on eid */
+  uint32_t lo = 0, hi = R->n_eids;
+  while (lo < hi) {
+    const uint32_t m = (lo + hi) / 2;
+    if (memcmp(R->eids[m].eid, wid, 4) < 0) lo = m + 1; else hi = m;
+  }
+  uint32_t n = 0;
+  for (uint32_t k = lo; k < R->n_eids && memcmp(R->eids[k].eid, wid, 4) == 0; ++k) {
+    const uint32_t r = R->eids[k].reader;
+    const uint32_t proxy = matched_writer(R, r, prefix, wid);
+    if (proxy != RTPS_NO_PROXY) *matched = 1;
+    if (out && n < cap) {
+      out[n].reader_slot = R->r[r].reader_slot;
+      out[n].reader_flags = (uint16_t)(R->r[r].flags |
+                                       (memcmp(R->r[r].entity_id, E_SPDP_R_ID, 4) == 0 ? RTPS_TARGET_DUPLICATES_OK : 0));
+      out[n].proxy = proxy;
+    }
+    n++;
+  }
+  return n;
 }
 
 /* Reader::data_to_dds_data (io_uring/rtps/reader.rs:760-833) +
@@ -374,8 +476,7 @@ static uint8_t data_to_dds_data_kind(const submsg* s) {
 /* ------------------------------------------------------------------------ */
 typedef struct oracle_cfg {
   uint8_t own[12];
-  const rtps_match* table;
-  uint32_t n_match;
+  const oracle_readers* readers;
 } oracle_cfg;
 
 #define MAX_SUBMSGS (RTPS_MAX_DATAGRAM / 4)
@@ -383,7 +484,7 @@ typedef struct oracle_cfg {
 /* returns status; writes up to cap records into recs (count in *n_out) */
 static uint8_t oracle_datagram(const oracle_cfg* cfg, const uint8_t* m, uint32_t L, uint32_t dgram_idx,
                                submsg* subs /* scratch [MAX_SUBMSGS] */, rtps_record* recs,
-                               uint16_t* match_out, uint32_t* n_out) {
+                               uint32_t* n_out) {
   *n_out = 0;
   if (L > RTPS_MAX_DATAGRAM) return RTPS_DGRAM_TOO_LONG;
   /* message_receiver.rs:238-251 */
@@ -419,7 +520,6 @@ static uint8_t oracle_datagram(const oracle_cfg* cfg, const uint8_t* m, uint32_t
     rec->sub_off = (uint16_t)s->off;
     rec->kind = s->kind;
     rec->flags = s->flags;
-    uint16_t mslot = RTPS_NO_MATCH;
     if (s->cls == BODY_INTERP) {
       /* handle_interpreter_submessage (message_receiver.rs:618-665) */
       switch (s->kind) {
@@ -457,8 +557,9 @@ static uint8_t oracle_datagram(const oracle_cfg* cfg, const uint8_t* m, uint32_t
         if (pass) rec->route |= RTPS_ROUTE_PASS;
         if (builtin_writer_pair(s->reader_id, s->writer_id)) rec->route |= RTPS_ROUTE_BUILTIN;
         else {
-          mslot = match_lookup(cfg->table, cfg->n_match, src, s->writer_id);
-          if (mslot != RTPS_NO_MATCH) rec->route |= RTPS_ROUTE_MATCHED;
+          int matched = 0;
+          if (oracle_targets(cfg->readers, src, s->writer_id, NULL, 0, &matched))
+            rec->route |= RTPS_ROUTE_TARGETED | (matched ? RTPS_ROUTE_MATCHED : 0);
         }
       } else {
         rec->route |= RTPS_ROUTE_PASS; /* reader submessages always pass (:88-113) */
@@ -527,7 +628,6 @@ static uint8_t oracle_datagram(const oracle_cfg* cfg, const uint8_t* m, uint32_t
       rec->ts_sec = ts_sec;
       rec->ts_frac = ts_frac;
     }
-    if (match_out) match_out[i] = mslot;
   }
   *n_out = nsub;
   return RTPS_DGRAM_OK;
@@ -544,7 +644,6 @@ typedef struct slice_job {
   uint32_t lo, hi;
   uint8_t* status;
   rtps_record* recs; /* thread-local */
-  uint16_t* match;   /* thread-local */
   uint32_t* counts;  /* per datagram */
   uint64_t n_recs, cap;
   submsg* scratch;
@@ -560,11 +659,9 @@ static void* run_slice(void* arg) {
     if (j->n_recs + need > j->cap) { /* grow thread-local buffers */
       uint64_t ncap = (j->cap + need) * 2 + 64;
       j->recs = (rtps_record*)realloc(j->recs, ncap * sizeof(rtps_record));
-      j->match = (uint16_t*)realloc(j->match, ncap * sizeof(uint16_t));
       j->cap = ncap;
     }
-    j->status[i] = oracle_datagram(j->cfg, j->arena + j->off[i], L, i, j->scratch, j->recs + j->n_recs,
-                                   j->match + j->n_recs, &nr);
+    j->status[i] = oracle_datagram(j->cfg, j->arena + j->off[i], L, i, j->scratch, j->recs + j->n_recs, &nr);
     j->counts[i] = nr;
     j->n_recs += nr;
   }
@@ -573,17 +670,19 @@ static void* run_slice(void* arg) {
 
 /* Parse a batch on `threads` host threads (contiguous slices).  Outputs are
  * identical to the device library's: status[n], records (ascending
- * (dgram_idx, sub_off)), match[], rec_begin[n] (optional), total count.
- * Returns the total number of records (records beyond max_records are not
- * written). */
+ * (dgram_idx, sub_off)), rec_begin[n] (optional), total count; readers /
+ * proxies as given to rtps_rx_set_readers.  Returns the total number of
+ * records (records beyond max_records are not written). */
 uint64_t rtps_oracle_parse(const uint8_t* arena, const uint64_t* off, const uint32_t* len, uint32_t n,
-                           const uint8_t own[12], const rtps_match* table, uint32_t n_match,
+                           const uint8_t own[12], const rtps_reader* readers, uint32_t n_readers,
+                           const rtps_proxy* proxies, uint32_t n_proxies,
                            uint8_t* status, rtps_record* records, uint64_t max_records,
-                           uint16_t* match, uint32_t* rec_begin, int threads) {
+                           uint32_t* rec_begin, int threads) {
   oracle_cfg cfg;
+  oracle_readers R;
+  oracle_readers_init(&R, readers, n_readers, proxies, n_proxies);
   memcpy(cfg.own, own, 12);
-  cfg.table = table;
-  cfg.n_match = n_match;
+  cfg.readers = &R;
   if (threads < 1) threads = 1;
   if ((uint32_t)threads > n && n > 0) threads = (int)n;
   uint32_t* counts = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
@@ -609,11 +708,9 @@ uint64_t rtps_oracle_parse(const uint8_t* arena, const uint64_t* off, const uint
     if (records && total < max_records) {
       uint64_t w = (total + k <= max_records) ? k : max_records - total;
       memcpy(records + total, jobs[t].recs, w * sizeof(rtps_record));
-      if (match) memcpy(match + total, jobs[t].match, w * sizeof(uint16_t));
     }
     total += k;
     free(jobs[t].recs);
-    free(jobs[t].match);
     free(jobs[t].scratch);
   }
   if (rec_begin) {
@@ -623,6 +720,35 @@ uint64_t rtps_oracle_parse(const uint8_t* arena, const uint64_t* off, const uint
   free(counts);
   free(jobs);
   free(tids);
+  oracle_readers_free(&R);
+  return total;
+}
+
+/* The target readers of every record (the user path of Domain::handle_event,
+ * see oracle_targets): for record i, out[off[i] .. off[i+1]).  Only writer
+ * kinds that are not a builtin pair have targets.  off: [m + 1].  Returns the
+ * total (targets past cap are counted, not written). */
+uint64_t rtps_oracle_targets(const rtps_record* recs, uint64_t m, const rtps_reader* readers, uint32_t n_readers,
+                             const rtps_proxy* proxies, uint32_t n_proxies, uint64_t* off, rtps_target* out,
+                             uint64_t cap) {
+  oracle_readers R;
+  oracle_readers_init(&R, readers, n_readers, proxies, n_proxies);
+  uint64_t total = 0;
+  rtps_target* tmp = (rtps_target*)malloc(sizeof(rtps_target) * (n_readers ? n_readers : 1));
+  for (uint64_t i = 0; i < m; ++i) {
+    off[i] = total;
+    const rtps_record* r = &recs[i];
+    const int writer_kind = r->kind == RTPS_DATA || r->kind == RTPS_DATA_FRAG || r->kind == RTPS_HEARTBEAT ||
+                            r->kind == RTPS_HEARTBEAT_FRAG || r->kind == RTPS_GAP;
+    if (!writer_kind || builtin_writer_pair(r->reader_id, r->writer_id)) continue;
+    int matched = 0;
+    const uint32_t k = oracle_targets(&R, r->prefix, r->writer_id, tmp, n_readers, &matched);
+    for (uint32_t j = 0; j < k; ++j, ++total)
+      if (total < cap) out[total] = tmp[j];
+  }
+  off[m] = total;
+  free(tmp);
+  oracle_readers_free(&R);
   return total;
 }
 
@@ -954,11 +1080,11 @@ typedef struct ig_proxy {
   int64_t* set; uint8_t* used; size_t cap, n;
 } ig_proxy;
 typedef struct rtps_oracle_ingest {
-  uint32_t n;           /* match-table entries */
-  rtps_match* table;
-  ig_proxy* p;          /* one writer proxy per entry */
-  uint32_t* hslot;      /* GUID hash -> entry index + 1 (first entry wins) */
-  size_t hcap;
+  oracle_readers R;     /* the local readers and their proxies (copies) */
+  rtps_reader* readers;
+  rtps_proxy* proxies;
+  ig_proxy* p;          /* one RtpsWriterProxy per proxy */
+  rtps_target* tmp;
 } rtps_oracle_ingest;
 
 static size_t ig_h(int64_t s) { uint64_t x = (uint64_t)s * 0x9e3779b97f4a7c15ull; return (size_t)(x ^ (x >> 31)); }
@@ -1007,95 +1133,123 @@ static void ig_irrelevant_range(ig_proxy* p, int64_t from, int64_t until) {
   }
 }
 
-static size_t ig_guid_h(const uint8_t g[16]) { return (size_t)fa_hash(g, 16); }
-rtps_oracle_ingest* rtps_oracle_ingest_new(const rtps_match* table, uint32_t n) {
+rtps_oracle_ingest* rtps_oracle_ingest_new(const rtps_reader* readers, uint32_t nr, const rtps_proxy* proxies,
+                                           uint32_t np) {
   rtps_oracle_ingest* h = (rtps_oracle_ingest*)calloc(1, sizeof(rtps_oracle_ingest));
-  h->n = n;
-  h->table = (rtps_match*)calloc(n ? n : 1, sizeof(rtps_match));
-  if (n) memcpy(h->table, table, n * sizeof(rtps_match));
-  h->p = (ig_proxy*)calloc(n ? n : 1, sizeof(ig_proxy));
-  for (uint32_t e = 0; e < n; ++e) h->p[e].ack_base = 1;
-  h->hcap = 16;
-  while (h->hcap < 2 * (size_t)n) h->hcap <<= 1;
-  h->hslot = (uint32_t*)calloc(h->hcap, sizeof(uint32_t));
-  for (uint32_t e = 0; e < n; ++e) {
-    size_t j = ig_guid_h(table[e].writer_guid) & (h->hcap - 1);
-    int dup = 0;
-    while (h->hslot[j]) {
-      if (!memcmp(h->table[h->hslot[j] - 1].writer_guid, table[e].writer_guid, 16)) { dup = 1; break; }
-      j = (j + 1) & (h->hcap - 1);
-    }
-    if (!dup) h->hslot[j] = e + 1;
-  }
+  h->readers = (rtps_reader*)calloc(nr ? nr : 1, sizeof(rtps_reader));
+  h->proxies = (rtps_proxy*)calloc(np ? np : 1, sizeof(rtps_proxy));
+  if (nr) memcpy(h->readers, readers, nr * sizeof(rtps_reader));
+  if (np) memcpy(h->proxies, proxies, np * sizeof(rtps_proxy));
+  oracle_readers_init(&h->R, h->readers, nr, h->proxies, np);
+  h->p = (ig_proxy*)calloc(np ? np : 1, sizeof(ig_proxy));
+  for (uint32_t e = 0; e < np; ++e) h->p[e].ack_base = 1; /* RtpsWriterProxy::new (rtps_writer_proxy.rs:96) */
+  h->tmp = (rtps_target*)malloc(sizeof(rtps_target) * (nr ? nr : 1));
   return h;
+}
+/* New readers / proxies for an existing ingest: proxy state is kept by
+ * position, as the device keeps it (rtps_rx_ingest: "indexed by proxy
+ * position"); proxies past the old count start fresh (RtpsWriterProxy::new). */
+void rtps_oracle_ingest_set_readers(rtps_oracle_ingest* h, const rtps_reader* readers, uint32_t nr,
+                                    const rtps_proxy* proxies, uint32_t np) {
+  const uint32_t old = h->R.np;
+  for (uint32_t e = np; e < old; ++e) { free(h->p[e].set); free(h->p[e].used); }
+  h->p = (ig_proxy*)realloc(h->p, sizeof(ig_proxy) * (np ? np : 1));
+  for (uint32_t e = old; e < np; ++e) { memset(&h->p[e], 0, sizeof(ig_proxy)); h->p[e].ack_base = 1; }
+  oracle_readers_free(&h->R);
+  free(h->readers); free(h->proxies); free(h->tmp);
+  h->readers = (rtps_reader*)calloc(nr ? nr : 1, sizeof(rtps_reader));
+  h->proxies = (rtps_proxy*)calloc(np ? np : 1, sizeof(rtps_proxy));
+  if (nr) memcpy(h->readers, readers, nr * sizeof(rtps_reader));
+  if (np) memcpy(h->proxies, proxies, np * sizeof(rtps_proxy));
+  oracle_readers_init(&h->R, h->readers, nr, h->proxies, np);
+  h->tmp = (rtps_target*)malloc(sizeof(rtps_target) * (nr ? nr : 1));
 }
 void rtps_oracle_ingest_free(rtps_oracle_ingest* h) {
   if (!h) return;
-  for (uint32_t e = 0; e < h->n; ++e) { free(h->p[e].set); free(h->p[e].used); }
-  free(h->p); free(h->table); free(h->hslot); free(h);
-}
-/* writer GUID -> entry index (first entry wins), or -1 */
-static int64_t ig_entry(const rtps_oracle_ingest* h, const uint8_t g[16]) {
-  for (size_t j = ig_guid_h(g) & (h->hcap - 1); h->hslot[j]; j = (j + 1) & (h->hcap - 1))
-    if (!memcmp(h->table[h->hslot[j] - 1].writer_guid, g, 16)) return (int64_t)h->hslot[j] - 1;
-  return -1;
+  for (uint32_t e = 0; e < h->R.np; ++e) { free(h->p[e].set); free(h->p[e].used); }
+  oracle_readers_free(&h->R);
+  free(h->p); free(h->readers); free(h->proxies); free(h->tmp); free(h);
 }
 
-/* One batch in record order (see rtps_rx_ingest in rtps_rx.h).  accept[m],
- * accepted[m] (returns their count), ack_base[n] (optional). */
+/* Reader::process_received_data for one target (io_uring/rtps/reader.rs:693-758):
+ * 1 = the sample enters the reader's cache. */
+static int ig_process_sample(rtps_oracle_ingest* h, const rtps_target* t, const uint8_t wid[4], int64_t sn) {
+  if (t->proxy != RTPS_NO_PROXY) {
+    ig_proxy* p = &h->p[t->proxy];
+    if (ig_should_ignore(p, sn) && !(t->reader_flags & RTPS_TARGET_DUPLICATES_OK)) return 0;
+    ig_received(p, sn);  /* writer_proxy.received_changes_add */
+    return 1;
+  }
+  /* no writer proxy: dropped for user-defined writers, accepted otherwise (:734-739) */
+  return (wid[3] & 0xF0) != 0x00;
+}
+
+/* One batch in record order (see rtps_rx_ingest in rtps_rx.h), every routed
+ * record handed to each of its target readers in turn as Domain::handle_event
+ * does (dp_event_loop.rs:266-327).  accept[m] = readers that took the record's
+ * sample (saturating at 255); deliveries (record, reader slot) in order, count
+ * returned (past max_del counted, not written); ack_base[n_proxies] (optional). */
 uint64_t rtps_oracle_ingest_batch(rtps_oracle_ingest* h, const uint8_t* arena, const uint64_t* offs,
                                   const rtps_record* recs, uint64_t m, const rtps_frag_sample* frag, uint64_t nf,
-                                  uint32_t flags, uint8_t* accept, uint32_t* accepted, int64_t* ack_base) {
+                                  uint32_t flags, uint8_t* accept, rtps_delivery* del, uint64_t max_del,
+                                  int64_t* ack_base) {
   uint32_t* fidx = (uint32_t*)malloc((m ? m : 1) * sizeof(uint32_t));
   for (uint64_t i = 0; i < m; ++i) fidx[i] = 0xffffffffu;
   for (uint64_t s = 0; s < nf; ++s)
     if (frag[s].rec_idx < m) fidx[frag[s].rec_idx] = (uint32_t)s;
-  uint64_t na = 0;
+  uint64_t nd = 0;
   for (uint64_t i = 0; i < m; ++i) {
     const rtps_record* r = &recs[i];
     accept[i] = 0;
-    const int routed = (r->route & RTPS_ROUTE_PASS) && (r->route & RTPS_ROUTE_MATCHED);
-    uint8_t g[16];
-    memcpy(g, r->prefix, 12);
-    memcpy(g + 12, r->writer_id, 4);
-    if (fidx[i] != 0xffffffffu) {  /* completed DataFrag sample (handle_datafrag_msg :614-626) */
-      const rtps_frag_sample* fs = &frag[fidx[i]];
-      int64_t e = ig_entry(h, fs->writer_guid);
-      if (fs->status != RTPS_FRAG_SHORT && e >= 0) {
-        ig_proxy* p = &h->p[e];
-        if (!ig_should_ignore(p, fs->sn)) { ig_received(p, fs->sn); accept[i] = 1; accepted[na++] = (uint32_t)i; }
+    /* SubmessageIter2 passed it, and it is not a builtin pair (Discovery2 takes those) */
+    if (!(r->route & RTPS_ROUTE_PASS) || builtin_writer_pair(r->reader_id, r->writer_id)) continue;
+    const int writer_kind = r->kind == RTPS_DATA || r->kind == RTPS_DATA_FRAG || r->kind == RTPS_HEARTBEAT ||
+                            r->kind == RTPS_HEARTBEAT_FRAG || r->kind == RTPS_GAP;
+    if (!writer_kind) continue;
+    int matched = 0;
+    const uint32_t nt = oracle_targets(&h->R, r->prefix, r->writer_id, h->tmp, h->R.nr, &matched);
+    uint32_t took = 0;
+    for (uint32_t k = 0; k < nt; ++k) {
+      const rtps_target* t = &h->tmp[k];
+      ig_proxy* p = t->proxy != RTPS_NO_PROXY ? &h->p[t->proxy] : NULL;
+      int acc = 0;
+      if (fidx[i] != 0xffffffffu) {  /* completed DataFrag sample (handle_datafrag_msg :614-626) */
+        const rtps_frag_sample* fs = &frag[fidx[i]];
+        if (fs->status != RTPS_FRAG_SHORT) acc = ig_process_sample(h, t, r->writer_id, fs->sn);
+      } else if (r->kind == RTPS_DATA) {
+        if (r->payload_kind != RTPS_PK_DATA && r->payload_kind != RTPS_PK_KEY && r->payload_kind != RTPS_PK_KEY_HASH)
+          continue;  /* data_to_dds_data failed: no process_received_data (reader.rs:552-558) */
+        acc = ig_process_sample(h, t, r->writer_id, r->sn);
+      } else if (r->kind == RTPS_HEARTBEAT) {
+        /* BestEffort (or stateless) readers ignore HEARTBEATs (:871-881), no proxy: ignored (:885-891) */
+        if ((flags & RTPS_INGEST_BEST_EFFORT) || (t->reader_flags & RTPS_READER_BEST_EFFORT) || !p) continue;
+        if (r->u.hb.count <= p->hb_count) continue;  /* already seen (reader.rs:902-905) */
+        p->hb_count = r->u.hb.count;
+        ig_irrelevant_range(p, 0, r->sn);            /* irrelevant_changes_up_to(first_sn) */
+      } else if (r->kind == RTPS_GAP) {
+        if (!p) continue;                            /* no writer proxy (:1076-1086) */
+        const int64_t start = r->sn, base = r->u.gap.list_base;
+        if (start <= 0 || base <= 0) continue;       /* validity (reader.rs:1087-1102) */
+        ig_irrelevant_range(p, start, base);
+        const uint8_t* bm = arena + offs[r->dgram_idx] + r->u.gap.bitmap_off;
+        const int le = r->flags & 1;
+        for (uint32_t b = 0; b < r->u.gap.num_bits; ++b) {  /* NumberSetIter (sequence_number.rs:543-557) */
+          const uint8_t* w = bm + 4 * (b / 32);
+          uint32_t word = le ? (uint32_t)w[0] | ((uint32_t)w[1] << 8) | ((uint32_t)w[2] << 16) | ((uint32_t)w[3] << 24)
+                             : ((uint32_t)w[0] << 24) | ((uint32_t)w[1] << 16) | ((uint32_t)w[2] << 8) | (uint32_t)w[3];
+          if (word & (1u << (31 - b % 32))) ig_irrelevant(p, base + (int64_t)b);
+        }
       }
-      continue;
-    }
-    if (!routed) continue;
-    int64_t e = ig_entry(h, g);
-    if (e < 0) continue;
-    ig_proxy* p = &h->p[e];
-    if (r->kind == RTPS_DATA) {
-      if (r->payload_kind != RTPS_PK_DATA && r->payload_kind != RTPS_PK_KEY && r->payload_kind != RTPS_PK_KEY_HASH)
-        continue;  /* data_to_dds_data failed: no process_received_data (reader.rs:552-558) */
-      if (!ig_should_ignore(p, r->sn)) { ig_received(p, r->sn); accept[i] = 1; accepted[na++] = (uint32_t)i; }
-    } else if (r->kind == RTPS_HEARTBEAT) {
-      if (flags & RTPS_INGEST_BEST_EFFORT) continue;
-      if (r->u.hb.count <= p->hb_count) continue;  /* already seen (reader.rs:902-905) */
-      p->hb_count = r->u.hb.count;
-      ig_irrelevant_range(p, 0, r->sn);            /* irrelevant_changes_up_to(first_sn) */
-    } else if (r->kind == RTPS_GAP) {
-      const int64_t start = r->sn, base = r->u.gap.list_base;
-      if (start <= 0 || base <= 0) continue;       /* validity (reader.rs:1087-1102) */
-      ig_irrelevant_range(p, start, base);
-      const uint8_t* bm = arena + offs[r->dgram_idx] + r->u.gap.bitmap_off;
-      const int le = r->flags & 1;
-      for (uint32_t b = 0; b < r->u.gap.num_bits; ++b) {  /* NumberSetIter (sequence_number.rs:543-557) */
-        const uint8_t* w = bm + 4 * (b / 32);
-        uint32_t word = le ? (uint32_t)w[0] | ((uint32_t)w[1] << 8) | ((uint32_t)w[2] << 16) | ((uint32_t)w[3] << 24)
-                           : ((uint32_t)w[0] << 24) | ((uint32_t)w[1] << 16) | ((uint32_t)w[2] << 8) | (uint32_t)w[3];
-        if (word & (1u << (31 - b % 32))) ig_irrelevant(p, base + (int64_t)b);
+      if (acc) {
+        if (nd < max_del) { del[nd].rec_idx = (uint32_t)i; del[nd].reader_slot = t->reader_slot; del[nd]._r = 0; }
+        nd++;
+        took++;
       }
     }
+    accept[i] = (uint8_t)(took < 255 ? took : 255);
   }
   if (ack_base)
-    for (uint32_t e = 0; e < h->n; ++e) ack_base[e] = h->p[e].ack_base;
+    for (uint32_t e = 0; e < h->R.np; ++e) ack_base[e] = h->p[e].ack_base;
   free(fidx);
-  return na;
+  return nd;
 }

@@ -5,25 +5,17 @@
 #include <stdint.h>
 
 #include "../../include/rtps_rx.h"
+#include "rtps_readers.h"
 
-// The context's match table (open addressing over fnv1a32(GUID), see
-// rtps_rx_set_match_table): keys, reader slots, entry index of every slot.
-struct IngestTable {
-  const void* keys;        // u32x4[mask + 1]
-  const uint16_t* slots;   // RTPS_NO_MATCH = empty
-  const uint32_t* index;   // entry position in the table the caller gave
-  uint32_t mask;
-  uint32_t n_entries;
-};
-
-struct IngestState;  // persistent per-entry writer-proxy state + per-batch scratch
+struct IngestState;  // persistent per-proxy writer-proxy state + per-batch scratch
 
 IngestState* rtps_ingest_state_new(int device);
 void rtps_ingest_state_free(IngestState* s);
 // Every writer proxy back to RtpsWriterProxy::new (asynchronous on `stream`).
 int rtps_ingest_state_reset(IngestState* s, hipStream_t stream);
-// One batch (asynchronous on `stream`); returns an RTPS_RX_* code.
-int rtps_ingest_batch(IngestState* s, hipStream_t stream, const IngestTable& t, const uint8_t* arena,
+// One batch (asynchronous on `stream`); returns an RTPS_RX_* code.  `t`: the
+// context's readers (target sets, proxies).
+int rtps_ingest_batch(IngestState* s, hipStream_t stream, const ReaderDev& t, const uint8_t* arena,
                       uint64_t arena_len, const uint64_t* dgram_off, const rtps_record* records,
                       const uint64_t* n_records, uint64_t max_records, const rtps_frag_sample* frag,
                       const uint64_t* n_frag, uint64_t max_frag, uint32_t flags, const rtps_ingest_out* out);

@@ -1,35 +1,49 @@
 // rtps_ingest.hip — history-cache ingest on the device.
 //
-// Replaces the stateful reader's per-writer bookkeeping that decides which
-// samples enter the history cache (RtpsWriterProxy, rtps/rtps_writer_proxy.rs;
+// Replaces the stateful readers' per-writer bookkeeping that decides which
+// samples enter which history cache (RtpsWriterProxy, rtps/rtps_writer_proxy.rs;
 // Reader::handle_data_msg / handle_datafrag_msg / handle_heartbeat_msg /
 // handle_gap_msg, io_uring/rtps/reader.rs:514-1116; TopicCache::add_change's
-// duplicate check, structure/dds_cache.rs:210-262).  The reference applies the
-// submessages one by one; a whole parsed batch is decided at once here.
+// duplicate check, structure/dds_cache.rs:210-262), for every target reader of
+// every routed record (Domain::handle_event, io_uring/rtps/dp_event_loop.rs:266-327).
+// The reference applies the submessages one by one, reader by reader; a whole
+// parsed batch is decided at once here.
+//
+// Events.  A record of the batch reaches every reader of its target set
+// (rtps_readers.h); each (record, reader) pair that can change something is an
+// EVENT: a sample (DATA / completed DATA_FRAG) with the reader's proxy of the
+// writer, or without one for a writer whose entity kind is not user-defined
+// (accepted unchecked, reader.rs:734-739); a HEARTBEAT with a proxy for a
+// reliable reader; a valid GAP with a proxy.  When no target set has more
+// than one reader, event i is record i ("identity" batches: the common case);
+// otherwise the events are laid out by a scan over the per-record counts, in
+// (record, set order) order.  Writer-proxy state is per PROXY.
 //
 // Why the batch can be decided in parallel.  Call a sequence number s of a
-// writer "covered" once a DATA / completed DATA_FRAG with sn s has been
-// processed, a valid GAP listed s or had s in [gapStart, gapList.base), or an
-// accepted HEARTBEAT had firstSN > s.  The proxy's all_ackable_before
-// (ack_base) is then always the smallest s >= 1 that is not covered (every
-// transition of rtps_writer_proxy.rs:202-355 keeps that invariant), so
+// proxy "covered" once a sample with sn s has been processed for it, a valid
+// GAP listed s or had s in [gapStart, gapList.base), or an accepted HEARTBEAT
+// had firstSN > s.  The proxy's all_ackable_before (ack_base) is then always
+// the smallest s >= 1 that is not covered (every transition of
+// rtps_writer_proxy.rs:202-355 keeps that invariant), so
 // should_ignore_change(s) = s < ack_base || changes.contains(s) is exactly
 // "s < 1 or s covered by an earlier event".  Only HEARTBEAT acceptance is
 // order-dependent (count > every earlier accepted count, reader.rs:902-905,
-// i.e. a strict prefix maximum), and it needs per-writer order only among the
+// i.e. a strict prefix maximum), and it needs per-proxy order only among the
 // HEARTBEATs.  So:
-//   1 classify  lane per record: event kind, writer entry (match table), sn;
-//   2 heartbeats stable radix sort of the HEARTBEAT events by entry, scans by
+//   1 classify  lane per record: target set, event count (identity: the event);
+//   1b expand   (non-identity batches) scan of the counts, lane per record
+//               writes its events;
+//   2 heartbeats stable radix sort of the HEARTBEAT events by proxy, scans by
 //               key: accepted = count > max(state count, earlier counts);
 //               running max of accepted firstSN (the coverage threshold);
-//   3 marks     lane per DATA / GAP: atomicMin(first covering record) over a
-//               per-writer window of RTPS_INGEST_WINDOW sequence numbers;
-//   4 decide    lane per sample: s >= 1, s >= ack_base, s >= threshold of the
-//               HEARTBEATs before it, not in the carried change set, and it is
-//               its sn's first covering event;
-//   5 select    accepted record indices (ascending);
+//   3 marks     lane per sample / GAP event: atomicMin(first covering event)
+//               over a per-proxy window of RTPS_INGEST_WINDOW sequence numbers;
+//   4 decide    lane per sample event: s >= 1, s >= ack_base, s >= threshold of
+//               the HEARTBEATs before it, not in the carried change set, and it
+//               is its sn's first covering event;
+//   5 select    accepted events -> deliveries (record, reader slot), ascending;
 //   6 merge     the batch's coverage into the persistent change-set bitmap;
-//   7 state     workgroup per writer: new ack_base = first uncovered s from
+//   7 state     workgroup per proxy: new ack_base = first uncovered s from
 //               max(ack_base, threshold), window re-anchored there, count.
 // The CPU restatement the tests hold this to (oracle/, test-only) is the
 // reference's sequential algorithm, so tests/ check this derivation too.
@@ -50,57 +64,17 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr uint32_t IT = 256;
 constexpr uint32_t NONE = 0xffffffffu;
-constexpr uint32_t W = RTPS_INGEST_WINDOW;  // sequence numbers tracked per writer
-constexpr uint32_t WW = W / 32;             // bitmap words per writer
-constexpr uint32_t ECAP_MAX = 1u << 14;     // writers (match-table entries)
+constexpr uint32_t W = RTPS_INGEST_WINDOW;  // sequence numbers tracked per proxy
+constexpr uint32_t WW = W / 32;             // bitmap words per proxy
+constexpr uint32_t ECAP_MAX = 1u << 14;     // writer proxies
 enum : uint8_t { EV_NONE = 0, EV_SAMPLE = 1, EV_HB = 2, EV_GAP = 3 };
-enum { C_OVF = 0, C_NSEL, C_SPREAD, C_COUNT = C_SPREAD + 2 * 64 };  // overflow, selected HEARTBEATs, then the
-// HEARTBEAT / GAP event counts in 64 slot pairs (one atomic per block, spread: no single hot address)
+// counters: window overflow, selected HEARTBEATs, selected deliveries, records of the batch, then
+// the HEARTBEAT / GAP / event counts in 64 slot triples (one atomic per block, spread: no hot address)
+enum { C_OVF = 0, C_NSEL, C_NDEL, C_NREC, C_SPREAD, C_COUNT = C_SPREAD + 3 * 64 };
+// event metadata: reader slot | flags << 16 (EVF_*)
+constexpr uint32_t EVF_DUP_OK = 1u << 16;  // RTPS_TARGET_DUPLICATES_OK reader
+constexpr uint32_t EVF_FREE = 1u << 17;    // sample without a proxy (writer kind not user-defined)
 
-__device__ __forceinline__ uint32_t guid_hash(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-  uint32_t h = 0x811c9dc5u;  // the match table's hash (rtps_rx.hip)
-  h = (h ^ a) * 0x01000193u; h = (h ^ b) * 0x01000193u;
-  h = (h ^ c) * 0x01000193u; h = (h ^ d) * 0x01000193u;
-  return h ^ (h >> 15);
-}
-// writer GUID -> match-table entry (first entry wins), or NONE
-__device__ __forceinline__ uint32_t entry_of(const IngestTable& t, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-  const u32x4* keys = reinterpret_cast<const u32x4*>(t.keys);
-  uint32_t i = guid_hash(a, b, c, d) & t.mask;
-  for (uint32_t probe = 0; probe <= t.mask; ++probe) {
-    if (t.slots[i] == RTPS_NO_MATCH) return NONE;
-    const u32x4 k = keys[i];
-    if (k[0] == a && k[1] == b && k[2] == c && k[3] == d) return t.index[i];
-    i = (i + 1u) & t.mask;
-  }
-  return NONE;
-}
-// Tables of up to ET_LDS slots are staged in LDS by k_classify (dynamic shared
-// memory: keys, then entry index with NONE for empty slots; 20 B per slot).
-constexpr uint32_t ET_LDS = 2048;
-extern __shared__ u32x4 s_et_dyn[];
-__host__ __device__ constexpr uint32_t et_lds_bytes(uint32_t slots) { return slots * 20u; }
-__device__ __forceinline__ void et_stage(const IngestTable& t) {
-  const u32x4* keys = reinterpret_cast<const u32x4*>(t.keys);
-  uint32_t* idx = reinterpret_cast<uint32_t*>(s_et_dyn + t.mask + 1u);
-  for (uint32_t i = threadIdx.x; i <= t.mask; i += blockDim.x) {
-    s_et_dyn[i] = keys[i];
-    idx[i] = t.slots[i] == RTPS_NO_MATCH ? NONE : t.index[i];
-  }
-  __syncthreads();
-}
-__device__ __forceinline__ uint32_t entry_of_lds(uint32_t mask, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-  const uint32_t* idx = reinterpret_cast<const uint32_t*>(s_et_dyn + mask + 1u);
-  uint32_t i = guid_hash(a, b, c, d) & mask;
-  for (uint32_t probe = 0; probe <= mask; ++probe) {
-    const uint32_t e = idx[i];
-    if (e == NONE) return NONE;
-    const u32x4 k = s_et_dyn[i];
-    if (k[0] == a && k[1] == b && k[2] == c && k[3] == d) return e;
-    i = (i + 1u) & mask;
-  }
-  return NONE;
-}
 // atomicOr(base[idx], m) for the active lanes, with every word's bits combined
 // across the wave first: one atomic per distinct word.  A writer's sequential
 // SNs share bitmap words (T: 4 lanes per word, 16 writers interleaved), while
@@ -137,9 +111,9 @@ __device__ __forceinline__ void wave_or(uint32_t* base, uint32_t* addr, uint32_t
   const bool tail = lane == 63 || next != key;
   if (key != 0xffffffffu && tail && v) atomicOr(base + key, v);
 }
-// first-cover key of record i in batch `epoch`: no reset between batches is needed
-__device__ __forceinline__ unsigned long long ekey(uint32_t epoch, uint32_t i) {
-  return ((unsigned long long)(0xffffffffu - epoch) << 32) | i;
+// first-cover key of event k in batch `epoch`: no reset between batches is needed
+__device__ __forceinline__ unsigned long long ekey(uint32_t epoch, uint32_t k) {
+  return ((unsigned long long)(0xffffffffu - epoch) << 32) | k;
 }
 __device__ __forceinline__ uint32_t rd32(const uint8_t* p, bool le) {
   const uint32_t x = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
@@ -147,11 +121,22 @@ __device__ __forceinline__ uint32_t rd32(const uint8_t* p, bool le) {
 }
 
 struct Scratch {
-  uint8_t* evt;     // event kind per record
-  uint32_t* ent;    // writer entry per record
-  int64_t* esn;     // sample sn (DATA / completed DATA_FRAG)
+  // per record
   uint32_t* fidx;   // completed DataFrag sample of a record, or NONE
-  uint32_t *hkey, *hval, *skey, *sval;  // HEARTBEAT sort (hkey: HB flag per record, then the keys)
+  uint32_t* rcnt;   // events of the record (non-identity batches), then their exclusive scan (roff)
+  uint32_t* roff;
+  uint32_t* rset;   // target set, record event kind, sample / event sn
+  uint8_t* rkind;
+  int64_t* rsn;
+  // per event
+  uint8_t* evt;     // event kind
+  uint32_t* ent;    // proxy, or NONE (a free sample)
+  int64_t* esn;     // sample sn
+  uint32_t* erec;   // record of the event
+  uint32_t* emeta;  // reader slot | EVF_* flags
+  uint8_t* eacc;    // accepted (non-identity batches; identity batches decide into accept[] directly)
+  uint32_t* sel;    // accepted event indices
+  uint32_t *hkey, *hval, *skey, *sval;  // HEARTBEAT sort (hkey: HB flag per event, then the keys)
   int32_t *hcnt, *hexcl;
   int64_t *hf, *hpre;
 };
@@ -159,10 +144,10 @@ struct State {
   int64_t* base;    // all_ackable_before
   int64_t* lo;      // first sequence number of the window (multiple of 32, <= base)
   int32_t* hbc;     // received_heartbeat_count
-  uint32_t* bits;   // change set: bit (s - lo) of writer e at bits[e * WW + ...]
-  uint64_t* fc;     // first covering record of (e, s - lo): (~epoch << 32 | record); older epochs compare larger
+  uint32_t* bits;   // change set: bit (s - lo) of proxy e at bits[e * WW + ...]
+  uint64_t* fc;     // first covering event of (e, s - lo): (~epoch << 32 | event); older epochs compare larger
   uint32_t* dbits;  // this batch's samples, same layout as bits (cleared by k_merge)
-  uint32_t* seg_b;  // HEARTBEAT segment of each entry in sorted order
+  uint32_t* seg_b;  // HEARTBEAT segment of each proxy in sorted order
   uint32_t* seg_e;
   uint64_t* ctr;
 };
@@ -175,73 +160,149 @@ __global__ __launch_bounds__(IT) void k_fidx(const rtps_frag_sample* frag, const
     if (frag[s].status != RTPS_FRAG_SHORT && frag[s].rec_idx < max) fidx[frag[s].rec_idx] = (uint32_t)s;
 }
 
-__global__ __launch_bounds__(IT) void k_classify(IngestTable t, const rtps_record* recs, const uint64_t* n_rec,
+// Does (record event kind, target x) make an event?  Sets ent / meta.
+__device__ __forceinline__ bool ev_of(uint8_t ev, const rtps_target& x, bool user_kind, bool reliable, uint32_t& ent,
+                                      uint32_t& meta) {
+  ent = x.proxy;
+  meta = x.reader_slot | ((x.reader_flags & RTPS_TARGET_DUPLICATES_OK) ? EVF_DUP_OK : 0u);
+  if (ev == EV_SAMPLE) {
+    if (x.proxy != RTPS_NO_PROXY) return true;
+    meta |= EVF_FREE;
+    return !user_kind;  // no proxy: dropped for user-defined writers, accepted otherwise (reader.rs:734-739)
+  }
+  if (x.proxy == RTPS_NO_PROXY) return false;  // HEARTBEAT / GAP need the proxy (reader.rs:885-891, 1076-1086)
+  if (ev == EV_HB) return reliable && !(x.reader_flags & RTPS_READER_BEST_EFFORT);  // (reader.rs:871-881)
+  return true;
+}
+
+// IDENT: no target set has more than one reader, so event i = record i.
+template <bool IDENT>
+__global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record* recs, const uint64_t* n_rec,
                                                  uint64_t max, const rtps_frag_sample* frag, uint32_t flags,
                                                  Scratch x, uint64_t* ctr) {
+  extern __shared__ uint32_t s_rt[];
   const uint64_t n = *n_rec < max ? *n_rec : max;
-  const bool lds = t.mask < ET_LDS;
-  if (lds) et_stage(t);
-  uint32_t nh = 0, ng = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) ctr[C_NREC] = n;
+  const bool lds = rt_fits_lds(t);
+  if (lds) { rt_stage(t, s_rt); __syncthreads(); }
+  const bool reliable = !(flags & RTPS_INGEST_BEST_EFFORT);
+  uint32_t nh = 0, ng = 0, ne = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * IT + threadIdx.x; i < max; i += (uint64_t)gridDim.x * IT) {
     uint8_t ev = EV_NONE;
-    uint32_t e = NONE;
+    uint32_t set = NONE;
     int64_t sn = 0;
+    bool user_kind = true;
     if (i < n) {
+      // bytes 0..31 of the record (kind @6, prefix||writer_id @8, route @30,
+      // payload_kind @31), then 32..47 (sn, gap.list_base) for the candidates:
+      // three of the record's four 16-B quads at most
+      const u32x4* q = reinterpret_cast<const u32x4*>(recs + i);
+      const u32x4 q0 = q[0], q1 = q[1];
+      const uint32_t kind = (q0[1] >> 16) & 0xffu, route = (q1[3] >> 16) & 0xffu, pk = q1[3] >> 24;
       const uint32_t f = frag ? x.fidx[i] : NONE;
-      if (f != NONE) {  // completed DataFrag sample, processed at its completing record (reader.rs:614-626)
-        const uint32_t* g = reinterpret_cast<const uint32_t*>(frag[f].writer_guid);
-        e = lds ? entry_of_lds(t.mask, g[0], g[1], g[2], g[3]) : entry_of(t, g[0], g[1], g[2], g[3]);
-        if (e != NONE) { ev = EV_SAMPLE; sn = frag[f].sn; }
-      } else {
-        // bytes 0..31 of the record (kind @6, prefix||writer_id @8, route @30,
-        // payload_kind @31), then 32..47 (sn, gap.list_base) for the candidates:
-        // three of the record's four 16-B quads at most
-        const u32x4* q = reinterpret_cast<const u32x4*>(recs + i);
-        const u32x4 q0 = q[0], q1 = q[1];
-        const uint32_t kind = (q0[1] >> 16) & 0xffu, route = (q1[3] >> 16) & 0xffu, pk = q1[3] >> 24;
-        if ((route & RTPS_ROUTE_PASS) && (route & RTPS_ROUTE_MATCHED) &&
-            (kind == RTPS_DATA || kind == RTPS_HEARTBEAT || kind == RTPS_GAP)) {
+      // records the receiver passes to the user readers (not a builtin pair: discovery's)
+      if ((route & RTPS_ROUTE_PASS) && (route & RTPS_ROUTE_TARGETED) && !(route & RTPS_ROUTE_BUILTIN)) {
+        if (f != NONE) {  // completed DataFrag sample, processed at its completing record (reader.rs:614-626)
+          ev = EV_SAMPLE;
+          sn = frag[f].sn;
+        } else if (kind == RTPS_DATA || kind == RTPS_HEARTBEAT || kind == RTPS_GAP) {
           const u32x4 q2 = q[2];
           const int64_t rsn = (int64_t)(((uint64_t)q2[1] << 32) | q2[0]);
           if (kind == RTPS_DATA) {
             // data_to_dds_data must succeed (reader.rs:552-558)
             if (pk == RTPS_PK_DATA || pk == RTPS_PK_KEY || pk == RTPS_PK_KEY_HASH) ev = EV_SAMPLE;
           } else if (kind == RTPS_HEARTBEAT) {
-            if (!(flags & RTPS_INGEST_BEST_EFFORT)) ev = EV_HB;  // BestEffort: ignored (reader.rs:870-881)
+            ev = EV_HB;
           } else {
             const int64_t list_base = (int64_t)(((uint64_t)q2[3] << 32) | q2[2]);
             if (rsn > 0 && list_base > 0) ev = EV_GAP;  // validity (reader.rs:1087-1102)
           }
-          if (ev != EV_NONE) {
-            e = lds ? entry_of_lds(t.mask, q0[2], q0[3], q1[0], q1[1]) : entry_of(t, q0[2], q0[3], q1[0], q1[1]);
-            if (e == NONE) ev = EV_NONE;
-            sn = rsn;
-          }
+          sn = rsn;
+        }
+        if (ev != EV_NONE) {
+          uint32_t r2 = 0;
+          set = lds ? rt_classify<true>(t, s_rt, q0[2], q0[3], q1[0], q1[1], r2)
+                    : rt_classify<false>(t, s_rt, q0[2], q0[3], q1[0], q1[1], r2);
+          if (set == NONE) ev = EV_NONE;
+          user_kind = (q1[1] >> 24 & 0xf0u) == 0u;  // EntityKind::is_user_defined (guid.rs:168-170)
         }
       }
     }
-    x.evt[i] = ev;
-    x.ent[i] = e;
-    x.esn[i] = sn;
-    x.hkey[i] = ev == EV_HB ? 1u : 0u;  // selection flag of the HEARTBEAT compaction
-    nh += ev == EV_HB;
-    ng += ev == EV_GAP;
+    // the record's events: one per target reader that the event concerns
+    uint32_t cnt = 0;
+    uint32_t ent = NONE, meta = 0;
+    if (ev != EV_NONE) {
+      const uint32_t b = t.set_first[set], e = t.set_first[set + 1];
+      for (uint32_t k = b; k < e; ++k) {
+        uint32_t en, me;
+        if (ev_of(ev, t.set_ent[k], user_kind, reliable, en, me)) {
+          ++cnt;
+          ent = en;
+          meta = me;
+          nh += ev == EV_HB;
+          ng += ev == EV_GAP;
+        }
+      }
+    }
+    ne += cnt;
+    if (IDENT) {  // at most one event: write it at index i
+      const uint8_t evi = cnt ? ev : EV_NONE;
+      x.evt[i] = evi;
+      x.ent[i] = ent;
+      x.esn[i] = sn;
+      x.erec[i] = (uint32_t)i;
+      x.emeta[i] = meta;
+      x.hkey[i] = evi == EV_HB ? 1u : 0u;  // selection flag of the HEARTBEAT compaction
+    } else {
+      x.rcnt[i] = cnt;
+      x.rset[i] = set;
+      x.rkind[i] = cnt ? (uint8_t)(ev | (user_kind ? 0x80u : 0u)) : EV_NONE;
+      x.rsn[i] = sn;
+    }
   }
-  __shared__ uint32_t s_n[2];
-  if (threadIdx.x == 0) { s_n[0] = 0; s_n[1] = 0; }
+  __shared__ uint32_t s_n[3];
+  if (threadIdx.x == 0) { s_n[0] = 0; s_n[1] = 0; s_n[2] = 0; }
   __syncthreads();
 #pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) { nh += __shfl_xor(nh, d, 64); ng += __shfl_xor(ng, d, 64); }
-  if ((threadIdx.x & 63u) == 0) { atomicAdd(&s_n[0], nh); atomicAdd(&s_n[1], ng); }
+  for (int d = 32; d >= 1; d >>= 1) {
+    nh += __shfl_xor(nh, d, 64); ng += __shfl_xor(ng, d, 64); ne += __shfl_xor(ne, d, 64);
+  }
+  if ((threadIdx.x & 63u) == 0) { atomicAdd(&s_n[0], nh); atomicAdd(&s_n[1], ng); atomicAdd(&s_n[2], ne); }
   __syncthreads();
-  if (threadIdx.x == 0 && (s_n[0] | s_n[1])) {
-    unsigned long long* c = reinterpret_cast<unsigned long long*>(ctr + C_SPREAD + 2u * (blockIdx.x & 63u));
+  if (threadIdx.x == 0 && (s_n[0] | s_n[1] | s_n[2])) {
+    unsigned long long* c = reinterpret_cast<unsigned long long*>(ctr + C_SPREAD + 3u * (blockIdx.x & 63u));
     if (s_n[0]) atomicAdd(c, (unsigned long long)s_n[0]);
     if (s_n[1]) atomicAdd(c + 1, (unsigned long long)s_n[1]);
+    if (s_n[2]) atomicAdd(c + 2, (unsigned long long)s_n[2]);
   }
 }
 
-// the compacted HEARTBEAT record indices (hval, record order) -> their writer entries (hkey)
+// 1b: lane per record writes its events at roff[i] (set order = EntityId order of the readers)
+__global__ __launch_bounds__(IT) void k_expand(ReaderDev t, uint64_t n, uint32_t flags, Scratch x) {
+  const bool reliable = !(flags & RTPS_INGEST_BEST_EFFORT);
+  for (uint64_t i = (uint64_t)blockIdx.x * IT + threadIdx.x; i < n; i += (uint64_t)gridDim.x * IT) {
+    const uint8_t rk = x.rkind[i];
+    if (rk == EV_NONE) continue;
+    const uint8_t ev = rk & 0x7fu;
+    const bool user_kind = (rk & 0x80u) != 0u;
+    const uint32_t set = x.rset[i];
+    uint32_t k = x.roff[i];
+    const int64_t sn = x.rsn[i];
+    for (uint32_t j = t.set_first[set], e = t.set_first[set + 1]; j < e; ++j) {
+      uint32_t en, me;
+      if (!ev_of(ev, t.set_ent[j], user_kind, reliable, en, me)) continue;
+      x.evt[k] = ev;
+      x.ent[k] = en;
+      x.esn[k] = sn;
+      x.erec[k] = (uint32_t)i;
+      x.emeta[k] = me;
+      x.hkey[k] = ev == EV_HB ? 1u : 0u;
+      ++k;
+    }
+  }
+}
+
+// the compacted HEARTBEAT event indices (hval, event order) -> their proxies (hkey)
 __global__ __launch_bounds__(IT) void k_hkeys(uint64_t n_hb, Scratch x) {
   for (uint64_t q = (uint64_t)blockIdx.x * IT + threadIdx.x; q < n_hb; q += (uint64_t)gridDim.x * IT)
     x.hkey[q] = x.ent[x.hval[q]];
@@ -251,18 +312,18 @@ __global__ __launch_bounds__(IT) void k_hkeys(uint64_t n_hb, Scratch x) {
 __global__ __launch_bounds__(IT) void k_hvals(const rtps_record* recs, uint64_t n_hb, Scratch x, State s) {
   for (uint64_t q = (uint64_t)blockIdx.x * IT + threadIdx.x; q < n_hb; q += (uint64_t)gridDim.x * IT) {
     const uint32_t k = x.skey[q];
-    x.hcnt[q] = recs[x.sval[q]].u.hb.count;
+    x.hcnt[q] = recs[x.erec[x.sval[q]]].u.hb.count;
     if (q == 0 || x.skey[q - 1] != k) s.seg_b[k] = (uint32_t)q;
     if (q + 1 == n_hb || x.skey[q + 1] != k) s.seg_e[k] = (uint32_t)q + 1u;
   }
 }
-// accepted iff count > max(state count, every earlier count of the writer) (reader.rs:902-905);
+// accepted iff count > max(state count, every earlier count of the proxy) (reader.rs:902-905);
 // an accepted HEARTBEAT covers [0, firstSN) (irrelevant_changes_up_to)
 __global__ __launch_bounds__(IT) void k_hacc(const rtps_record* recs, uint64_t n_hb, Scratch x, State s) {
   for (uint64_t q = (uint64_t)blockIdx.x * IT + threadIdx.x; q < n_hb; q += (uint64_t)gridDim.x * IT) {
     const uint32_t k = x.skey[q];
     const int32_t before = x.hexcl[q] > s.hbc[k] ? x.hexcl[q] : s.hbc[k];
-    x.hf[q] = x.hcnt[q] > before ? recs[x.sval[q]].sn : INT64_MIN;
+    x.hf[q] = x.hcnt[q] > before ? recs[x.erec[x.sval[q]]].sn : INT64_MIN;
   }
 }
 
@@ -270,7 +331,7 @@ __global__ __launch_bounds__(IT) void k_hacc(const rtps_record* recs, uint64_t n
 // The sequence numbers a valid GAP covers, as (window word, bit mask) pairs:
 // irrelevant_changes_range(gapStart, gapList.base) (a negative range changes
 // nothing) and set_irrelevant_change per listed SN (NumberSetIter,
-// sequence_number.rs:543-557), clipped to the writer's window [lo, lo + W).
+// sequence_number.rs:543-557), clipped to the proxy's window [lo, lo + W).
 template <typename F>
 __device__ __forceinline__ void gap_words(const rtps_record& r, const uint8_t* arena, const uint64_t* dgram_off,
                                           int64_t lo, F&& f) {
@@ -300,13 +361,15 @@ __device__ __forceinline__ void gap_words(const rtps_record& r, const uint8_t* a
   }
 }
 
+__device__ __forceinline__ bool proxied_sample(const Scratch& x, uint64_t k) {
+  return x.evt[k] == EV_SAMPLE && x.ent[k] != NONE;
+}
+
 // samples first: their sequence numbers (dbits) and first-cover keys
-__global__ __launch_bounds__(IT) void k_marks_d(const uint64_t* n_rec, uint64_t max, Scratch x, State s, uint32_t epoch,
-                                                bool gaps) {
-  const uint64_t n = *n_rec < max ? *n_rec : max;
+__global__ __launch_bounds__(IT) void k_marks_d(uint64_t n, Scratch x, State s, uint32_t epoch, bool gaps) {
   for (uint64_t i0 = (uint64_t)blockIdx.x * IT; i0 < n; i0 += (uint64_t)gridDim.x * IT) {  // wave-uniform trip count
     const uint64_t i = i0 + threadIdx.x;
-    bool act = i < n && x.evt[i] == EV_SAMPLE;
+    bool act = i < n && proxied_sample(x, i);
     uint32_t* word = s.dbits;
     uint32_t bit = 0;
     if (act) {
@@ -326,8 +389,7 @@ __global__ __launch_bounds__(IT) void k_marks_d(const uint64_t* n_rec, uint64_t 
 // then GAPs: a GAP's first-cover key matters only where a sample of the batch
 // has the same sequence number, so only those are marked (32 at a time)
 __global__ __launch_bounds__(IT) void k_marks_g(const rtps_record* recs, const uint8_t* arena, const uint64_t* dgram_off,
-                                                const uint64_t* n_rec, uint64_t max, Scratch x, State s, uint32_t epoch) {
-  const uint64_t n = *n_rec < max ? *n_rec : max;
+                                                uint64_t n, Scratch x, State s, uint32_t epoch) {
   for (uint64_t i = (uint64_t)blockIdx.x * IT + threadIdx.x; i < n; i += (uint64_t)gridDim.x * IT) {
     if (x.evt[i] != EV_GAP) continue;
     const uint32_t e = x.ent[i];
@@ -343,54 +405,82 @@ __global__ __launch_bounds__(IT) void k_marks_g(const rtps_record* recs, const u
         atomicMin(fc + (w << 5) + b, key);
       }
     };
-    gap_words(recs[i], arena, dgram_off, lo, mark_word);
+    gap_words(recs[x.erec[i]], arena, dgram_off, lo, mark_word);
   }
 }
 
-// ---- 4 decide ----
-__global__ __launch_bounds__(IT) void k_decide(const uint64_t* n_rec, uint64_t max, Scratch x, State s, uint8_t* accept,
+// ---- 4 decide ----  (acc[0, cap): entries past n are cleared)
+__global__ __launch_bounds__(IT) void k_decide(uint64_t n, uint64_t cap, Scratch x, State s, uint8_t* acc_out,
                                                bool reliable, uint32_t epoch) {
-  const uint64_t n = *n_rec < max ? *n_rec : max;
-  for (uint64_t i = (uint64_t)blockIdx.x * IT + threadIdx.x; i < max; i += (uint64_t)gridDim.x * IT) {
+  for (uint64_t i = (uint64_t)blockIdx.x * IT + threadIdx.x; i < cap; i += (uint64_t)gridDim.x * IT) {
     uint8_t acc = 0;
     if (i < n && x.evt[i] == EV_SAMPLE) {
-      const uint32_t e = x.ent[i];
-      const int64_t v = x.esn[i], lo = s.lo[e];
-      int64_t thr = s.base[e];
-      const uint32_t sb = s.seg_b[e], se = s.seg_e[e];
-      // accepted HEARTBEATs of this writer before record i (only needed when the
-      // writer's final threshold is above v)
-      if (reliable && se > sb && x.hpre[se - 1u] > v && v >= thr) {
-        uint32_t a = sb, b = se;
-        while (a < b) {  // first sorted position whose record is >= i
-          const uint32_t m = (a + b) >> 1;
-          if (x.sval[m] < (uint32_t)i) a = m + 1u; else b = m;
+      const uint32_t e = x.ent[i], meta = x.emeta[i];
+      if (e == NONE || (meta & EVF_DUP_OK)) {
+        acc = 1;  // no proxy (writer kind not user-defined), or the participant reader's duplicates (reader.rs:712-722)
+      } else {
+        const int64_t v = x.esn[i], lo = s.lo[e];
+        int64_t thr = s.base[e];
+        const uint32_t sb = s.seg_b[e], se = s.seg_e[e];
+        // accepted HEARTBEATs of this proxy before event i (only needed when the
+        // proxy's final threshold is above v)
+        if (reliable && se > sb && x.hpre[se - 1u] > v && v >= thr) {
+          uint32_t a = sb, b = se;
+          while (a < b) {  // first sorted position whose event is >= i
+            const uint32_t m = (a + b) >> 1;
+            if (x.sval[m] < (uint32_t)i) a = m + 1u; else b = m;
+          }
+          if (a > sb && x.hpre[a - 1u] > thr) thr = x.hpre[a - 1u];
         }
-        if (a > sb && x.hpre[a - 1u] > thr) thr = x.hpre[a - 1u];
-      }
-      if (v >= 1 && v >= thr) {
-        if (v >= lo + (int64_t)W) {  // beyond the tracked window: accepted unchecked
-          acc = 1;
-          atomicAdd(reinterpret_cast<unsigned long long*>(s.ctr + C_OVF), 1ull);
-        } else {
-          const uint64_t off = (uint64_t)(v - lo);
-          const bool known = (s.bits[(uint64_t)e * WW + (off >> 5)] >> (off & 31u)) & 1u;
-          acc = (!known && s.fc[(uint64_t)e * W + off] == ekey(epoch, (uint32_t)i)) ? 1 : 0;
+        if (v >= 1 && v >= thr) {
+          if (v >= lo + (int64_t)W) {  // beyond the tracked window: accepted unchecked
+            acc = 1;
+            atomicAdd(reinterpret_cast<unsigned long long*>(s.ctr + C_OVF), 1ull);
+          } else {
+            const uint64_t off = (uint64_t)(v - lo);
+            const bool known = (s.bits[(uint64_t)e * WW + (off >> 5)] >> (off & 31u)) & 1u;
+            acc = (!known && s.fc[(uint64_t)e * W + off] == ekey(epoch, (uint32_t)i)) ? 1 : 0;
+          }
         }
       }
     }
-    accept[i] = acc;
+    acc_out[i] = acc;
+  }
+}
+
+// ---- 5 deliveries: selected events -> (record, reader slot); per-record accept counts ----
+__global__ __launch_bounds__(IT) void k_deliver(const uint64_t* n_sel, uint64_t max_out, Scratch x, rtps_delivery* out,
+                                                uint64_t* n_out) {
+  const uint64_t ns = *n_sel;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *n_out = ns;
+  const uint64_t lim = ns < max_out ? ns : max_out;
+  for (uint64_t j = (uint64_t)blockIdx.x * IT + threadIdx.x; j < lim; j += (uint64_t)gridDim.x * IT) {
+    const uint32_t k = x.sel[j];
+    rtps_delivery d;
+    d.rec_idx = x.erec[k];
+    d.reader_slot = (uint16_t)(x.emeta[k] & 0xffffu);
+    d._r = 0;
+    out[j] = d;
+  }
+}
+__global__ __launch_bounds__(IT) void k_accept_counts(uint64_t n, uint64_t cap, Scratch x, uint8_t* accept) {
+  for (uint64_t i = (uint64_t)blockIdx.x * IT + threadIdx.x; i < cap; i += (uint64_t)gridDim.x * IT) {
+    uint32_t c = 0;
+    if (i < n && x.rkind[i] != EV_NONE)
+      for (uint32_t k = x.roff[i], e = k + x.rcnt[i]; k < e; ++k) c += x.eacc[k];
+    accept[i] = (uint8_t)(c < 255u ? c : 255u);
   }
 }
 
 // ---- 6 merge ----
 __global__ __launch_bounds__(IT) void k_merge(const rtps_record* recs, const uint8_t* arena, const uint64_t* dgram_off,
-                                              const uint64_t* n_rec, uint64_t max, Scratch x, State s, bool gaps) {
-  const uint64_t n = *n_rec < max ? *n_rec : max;
+                                              uint64_t n, Scratch x, State s, bool gaps) {
   for (uint64_t i0 = (uint64_t)blockIdx.x * IT; i0 < n; i0 += (uint64_t)gridDim.x * IT) {  // wave-uniform trip count
     const uint64_t i = i0 + threadIdx.x;
-    const uint8_t ev = i < n ? x.evt[i] : EV_NONE;
-    const uint32_t e = (ev == EV_SAMPLE || ev == EV_GAP) ? x.ent[i] : 0u;
+    uint8_t ev = i < n ? x.evt[i] : EV_NONE;
+    const uint32_t e0 = ev != EV_NONE ? x.ent[i] : NONE;
+    if (e0 == NONE) ev = EV_NONE;  // free samples touch no proxy
+    const uint32_t e = (ev == EV_SAMPLE || ev == EV_GAP) ? e0 : 0u;
     const int64_t lo = (ev == EV_SAMPLE || ev == EV_GAP) ? s.lo[e] : 0;
     uint32_t* bits = s.bits + (uint64_t)e * WW;
     bool act = false;
@@ -406,13 +496,13 @@ __global__ __launch_bounds__(IT) void k_merge(const rtps_record* recs, const uin
         if (gaps) s.dbits[(uint64_t)e * WW + w] = 0u;  // every mark of the batch is done (k_marks_g read them)
       }
     } else if (ev == EV_GAP) {
-      gap_words(recs[i], arena, dgram_off, lo, [&](uint64_t w, uint32_t m) { atomicOr(bits + w, m); });
+      gap_words(recs[x.erec[i]], arena, dgram_off, lo, [&](uint64_t w, uint32_t m) { atomicOr(bits + w, m); });
     }
     wave_or(s.bits, word, bit, act);
   }
 }
 
-// ---- 7 state: one workgroup per writer ----
+// ---- 7 state: one workgroup per proxy ----
 __global__ __launch_bounds__(IT) void k_state(uint32_t n_entries, Scratch x, State s, bool reliable, int64_t* ack_out) {
   __shared__ uint32_t sh[WW];
   __shared__ uint32_t s_first;
@@ -479,9 +569,10 @@ static inline uint64_t hmin(uint64_t a, uint64_t b) { return a < b ? a : b; }
 
 struct IngestState {
   int device = 0;
-  uint32_t ecap = 0;  // entries with state
+  uint32_t ecap = 0;  // proxies with state
   State st{};
-  uint64_t cap = 0;   // records of the scratch
+  uint64_t rcap = 0;  // records of the per-record scratch
+  uint64_t vcap = 0;  // events of the per-event scratch
   Scratch x{};
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
@@ -489,7 +580,6 @@ struct IngestState {
   uint64_t* hctr = nullptr;  // pinned host copy of the event counters
 };
 
-static uint64_t* S_fc(IngestState* s) { return s->st.fc; }
 static void free_state(IngestState* s) {
   void* p[] = {s->st.base, s->st.lo, s->st.hbc, s->st.bits, s->st.fc, s->st.dbits, s->st.seg_b, s->st.seg_e};
   for (void* q : p) if (q) (void)hipFree(q);
@@ -498,17 +588,27 @@ static void free_state(IngestState* s) {
   s->st.ctr = ctr;
   s->ecap = 0;
 }
-static void free_scratch(IngestState* s) {
-  void* p[] = {s->x.evt, s->x.ent, s->x.esn, s->x.fidx, s->x.hkey, s->x.hval, s->x.skey, s->x.sval, s->x.hcnt,
-               s->x.hexcl, s->x.hf, s->x.hpre, s->tmp};
+static void free_rscratch(IngestState* s) {
+  void* p[] = {s->x.fidx, s->x.rcnt, s->x.roff, s->x.rset, s->x.rkind, s->x.rsn};
   for (void* q : p) if (q) (void)hipFree(q);
+  s->x.fidx = nullptr; s->x.rcnt = nullptr; s->x.roff = nullptr; s->x.rset = nullptr; s->x.rkind = nullptr;
+  s->x.rsn = nullptr;
+  s->rcap = 0;
+}
+static void free_vscratch(IngestState* s) {
+  void* p[] = {s->x.evt, s->x.ent, s->x.esn, s->x.erec, s->x.emeta, s->x.eacc, s->x.sel, s->x.hkey, s->x.hval,
+               s->x.skey, s->x.sval, s->x.hcnt, s->x.hexcl, s->x.hf, s->x.hpre, s->tmp};
+  for (void* q : p) if (q) (void)hipFree(q);
+  Scratch keep = s->x;
   s->x = Scratch{};
+  s->x.fidx = keep.fidx; s->x.rcnt = keep.rcnt; s->x.roff = keep.roff; s->x.rset = keep.rset;
+  s->x.rkind = keep.rkind; s->x.rsn = keep.rsn;
   s->tmp = nullptr;
   s->tmp_bytes = 0;
-  s->cap = 0;
+  s->vcap = 0;
 }
 
-// per-entry state for n entries; existing entries keep theirs
+// per-proxy state for n proxies; existing proxies keep theirs
 static bool grow_state(IngestState* s, uint32_t n, hipStream_t st) {
   if (n <= s->ecap) return true;
   uint32_t ncap = s->ecap ? s->ecap : 16;
@@ -526,7 +626,7 @@ static bool grow_state(IngestState* s, uint32_t n, hipStream_t st) {
        hipMemsetAsync(m.dbits, 0, (uint64_t)ncap * WW * 4, st) == hipSuccess &&
        hipMemsetAsync(m.fc, 0xff, (uint64_t)ncap * W * 8, st) == hipSuccess;
   if (ok) hipLaunchKernelGGL(k_init_state, dim3((ncap + IT - 1) / IT), dim3(IT), 0, st, ncap, m);
-  if (ok && s->ecap) {  // carry the existing writers' state
+  if (ok && s->ecap) {  // carry the existing proxies' state
     const uint64_t e = s->ecap;
     ok = hipMemcpyAsync(m.base, o.base, e * 8, hipMemcpyDeviceToDevice, st) == hipSuccess &&
          hipMemcpyAsync(m.lo, o.lo, e * 8, hipMemcpyDeviceToDevice, st) == hipSuccess &&
@@ -535,30 +635,45 @@ static bool grow_state(IngestState* s, uint32_t n, hipStream_t st) {
   }
   ok = ok && hipStreamSynchronize(st) == hipSuccess;
   s->st = m;
-  const uint32_t old_cap = s->ecap;
   s->ecap = ncap;
   State dead = o;
   dead.ctr = nullptr;
   void* p[] = {dead.base, dead.lo, dead.hbc, dead.bits, dead.fc, dead.dbits, dead.seg_b, dead.seg_e};
   for (void* q : p) if (q) (void)hipFree(q);
-  (void)old_cap;
   if (!ok) { free_state(s); return false; }
   return true;
 }
 
-static bool grow_scratch(IngestState* s, uint64_t max, hipStream_t st) {
-  if (max <= s->cap) return true;
+static bool grow_rscratch(IngestState* s, uint64_t max, hipStream_t st) {
+  if (max <= s->rcap) return true;
   (void)hipStreamSynchronize(st);
-  free_scratch(s);
+  free_rscratch(s);
+  Scratch& x = s->x;
   const uint64_t n = max;
+  bool ok = hipMalloc(&x.fidx, n * 4) == hipSuccess && hipMalloc(&x.rcnt, n * 4) == hipSuccess &&
+            hipMalloc(&x.roff, n * 4) == hipSuccess && hipMalloc(&x.rset, n * 4) == hipSuccess &&
+            hipMalloc(&x.rkind, n) == hipSuccess && hipMalloc(&x.rsn, n * 8) == hipSuccess;
+  if (!ok) { free_rscratch(s); return false; }
+  s->rcap = n;
+  return true;
+}
+
+// event scratch + hipcub temporary storage for n events (the per-record scan needs rcap)
+static bool grow_vscratch(IngestState* s, uint64_t n, hipStream_t st) {
+  if (n <= s->vcap) return true;
+  (void)hipStreamSynchronize(st);
+  free_vscratch(s);
   Scratch& x = s->x;
   bool ok = hipMalloc(&x.evt, n) == hipSuccess && hipMalloc(&x.ent, n * 4) == hipSuccess &&
-            hipMalloc(&x.esn, n * 8) == hipSuccess && hipMalloc(&x.fidx, n * 4) == hipSuccess &&
+            hipMalloc(&x.esn, n * 8) == hipSuccess && hipMalloc(&x.erec, n * 4) == hipSuccess &&
+            hipMalloc(&x.emeta, n * 4) == hipSuccess && hipMalloc(&x.eacc, n) == hipSuccess &&
+            hipMalloc(&x.sel, n * 4) == hipSuccess &&
             hipMalloc(&x.hkey, n * 4) == hipSuccess && hipMalloc(&x.hval, n * 4) == hipSuccess &&
             hipMalloc(&x.skey, n * 4) == hipSuccess && hipMalloc(&x.sval, n * 4) == hipSuccess &&
             hipMalloc(&x.hcnt, n * 4) == hipSuccess && hipMalloc(&x.hexcl, n * 4) == hipSuccess &&
             hipMalloc(&x.hf, n * 8) == hipSuccess && hipMalloc(&x.hpre, n * 8) == hipSuccess;
-  size_t b1 = 0, b2 = 0, b3 = 0, b4 = 0;
+  const uint64_t nr = s->rcap > n ? s->rcap : n;
+  size_t b1 = 0, b2 = 0, b3 = 0, b4 = 0, b5 = 0, b6 = 0;
   ok = ok && hipcub::DeviceRadixSort::SortPairs(nullptr, b1, x.hkey, x.skey, x.hval, x.sval, (int)n, 0, 32, st) == hipSuccess;
   ok = ok && hipcub::DeviceScan::ExclusiveScanByKey(nullptr, b2, x.skey, x.hcnt, x.hexcl, hipcub::Max(), INT32_MIN,
                                                     (uint32_t)n, hipcub::Equality(), st) == hipSuccess;
@@ -566,18 +681,15 @@ static bool grow_scratch(IngestState* s, uint64_t max, hipStream_t st) {
                                                     hipcub::Equality(), st) == hipSuccess;
   ok = ok && hipcub::DeviceSelect::Flagged(nullptr, b4, hipcub::CountingInputIterator<uint32_t>(0), (uint8_t*)nullptr,
                                            (uint32_t*)nullptr, (uint64_t*)nullptr, (int64_t)n, st) == hipSuccess;
-  size_t b5 = 0;
   ok = ok && hipcub::DeviceSelect::Flagged(nullptr, b5, hipcub::CountingInputIterator<uint32_t>(0), x.hkey, x.hval,
                                            (uint64_t*)nullptr, (int64_t)n, st) == hipSuccess;
-  if (b5 > b4) b4 = b5;
+  ok = ok && hipcub::DeviceScan::ExclusiveSum(nullptr, b6, x.rcnt, x.roff, (uint32_t)nr, st) == hipSuccess;
   size_t tb = b1;
-  if (b2 > tb) tb = b2;
-  if (b3 > tb) tb = b3;
-  if (b4 > tb) tb = b4;
+  for (size_t b : {b2, b3, b4, b5, b6}) tb = b > tb ? b : tb;
   s->tmp_bytes = tb;
   ok = ok && hipMalloc(&s->tmp, tb) == hipSuccess;
-  if (!ok) { free_scratch(s); return false; }
-  s->cap = n;
+  if (!ok) { free_vscratch(s); return false; }
+  s->vcap = n;
   return true;
 }
 
@@ -596,7 +708,8 @@ IngestState* rtps_ingest_state_new(int device) {
 
 void rtps_ingest_state_free(IngestState* s) {
   if (!s) return;
-  free_scratch(s);
+  free_vscratch(s);
+  free_rscratch(s);
   free_state(s);
   if (s->st.ctr) (void)hipFree(s->st.ctr);
   if (s->hctr) (void)hipHostFree(s->hctr);
@@ -611,23 +724,26 @@ int rtps_ingest_state_reset(IngestState* s, hipStream_t st) {
   return ok && hipGetLastError() == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP;
 }
 
-int rtps_ingest_batch(IngestState* s, hipStream_t st, const IngestTable& t, const uint8_t* arena, uint64_t arena_len,
+int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const uint8_t* arena, uint64_t arena_len,
                       const uint64_t* dgram_off, const rtps_record* records, const uint64_t* n_records,
                       uint64_t max_records, const rtps_frag_sample* frag, const uint64_t* n_frag, uint64_t max_frag,
                       uint32_t flags, const rtps_ingest_out* out) {
   (void)arena_len;
-  if (t.n_entries > ECAP_MAX) return RTPS_RX_ETOOBIG;
+  if (t.n_proxies > ECAP_MAX) return RTPS_RX_ETOOBIG;
   if (max_records > 0x7fffffffull) return RTPS_RX_ETOOBIG;
-  if (!grow_state(s, t.n_entries ? t.n_entries : 1, st)) return RTPS_RX_ENOMEM;
+  if (!grow_state(s, t.n_proxies ? t.n_proxies : 1, st)) return RTPS_RX_ENOMEM;
   const uint64_t max = max_records ? max_records : 1;
-  if (!grow_scratch(s, max, st)) return RTPS_RX_ENOMEM;
+  if (!grow_rscratch(s, max, st)) return RTPS_RX_ENOMEM;
+  const bool ident = t.max_set <= 1u;
+  if (ident && !grow_vscratch(s, max, st)) return RTPS_RX_ENOMEM;
+  if (!ident && s->vcap == 0 && !grow_vscratch(s, 1, st)) return RTPS_RX_ENOMEM;
   const bool reliable = !(flags & RTPS_INGEST_BEST_EFFORT);
   if (++s->epoch == 0xffffffffu) {  // keys would wrap: clear the first-cover table
-    if (hipMemsetAsync(S_fc(s), 0xff, (uint64_t)s->ecap * W * 8, st) != hipSuccess) return RTPS_RX_EHIP;
+    if (hipMemsetAsync(s->st.fc, 0xff, (uint64_t)s->ecap * W * 8, st) != hipSuccess) return RTPS_RX_EHIP;
     s->epoch = 1;
   }
   uint32_t ebits = 1;
-  while ((1u << ebits) < t.n_entries) ++ebits;  // sort key width: entries < 2^ebits
+  while ((1u << ebits) < t.n_proxies) ++ebits;  // sort key width: proxies < 2^ebits
   const uint32_t gb = (uint32_t)hmin((max + IT - 1) / IT, 8192);
   Scratch& x = s->x;
   State& S = s->st;
@@ -638,24 +754,45 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const IngestTable& t, cons
   if (with_frag)
     hipLaunchKernelGGL(k_fidx, dim3((uint32_t)hmin((max_frag + IT - 1) / IT, 4096)), dim3(IT), 0, st, frag, n_frag,
                        max_frag, max, x.fidx);
-  hipLaunchKernelGGL(k_classify, dim3(gb), dim3(IT), t.mask < ET_LDS ? et_lds_bytes(t.mask + 1) : 0u, st, t, records,
-                     n_records, max, with_frag ? frag : nullptr, flags, x, S.ctr);
-  // the batch's HEARTBEAT / GAP counts decide which stages run: one small read-back
+  const uint32_t lds = rt_fits_lds(t) ? rt_lds_bytes(t.gmask + 1u, t.emask + 1u) : 0u;
+  if (ident)
+    hipLaunchKernelGGL(k_classify<true>, dim3(gb), dim3(IT), lds, st, t, records, n_records, max,
+                       with_frag ? frag : nullptr, flags, x, S.ctr);
+  else
+    hipLaunchKernelGGL(k_classify<false>, dim3(gb), dim3(IT), lds, st, t, records, n_records, max,
+                       with_frag ? frag : nullptr, flags, x, S.ctr);
+  // the batch's record / HEARTBEAT / GAP / event counts size the rest: one small read-back
   if (hipMemcpyAsync(s->hctr, S.ctr, C_COUNT * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipStreamSynchronize(st) != hipSuccess)
     return RTPS_RX_EHIP;
-  uint64_t n_hb = 0, n_gap = 0;
-  for (uint32_t k = 0; k < 64; ++k) { n_hb += s->hctr[C_SPREAD + 2 * k]; n_gap += s->hctr[C_SPREAD + 2 * k + 1]; }
-  if (!reliable) n_hb = 0;
-  const bool have_hb = n_hb > 0;
-  if (have_hb) {  // stable compaction of the HEARTBEAT events, sort by writer entry, scans by key
+  uint64_t n_hb = 0, n_gap = 0, n_ev = 0;
+  for (uint32_t k = 0; k < 64; ++k) {
+    n_hb += s->hctr[C_SPREAD + 3 * k];
+    n_gap += s->hctr[C_SPREAD + 3 * k + 1];
+    n_ev += s->hctr[C_SPREAD + 3 * k + 2];
+  }
+  const uint64_t n_rec = s->hctr[C_NREC];
+  // events live at [0, nev): record slots in identity batches, the expanded list otherwise
+  uint64_t nev = ident ? n_rec : n_ev;
+  if (!ident) {
+    if (n_ev > 0x7fffffffull) return RTPS_RX_ETOOBIG;
+    if (!grow_vscratch(s, n_ev ? n_ev : 1, st)) return RTPS_RX_ENOMEM;
+    size_t tb = s->tmp_bytes;
+    if (n_rec && hipcub::DeviceScan::ExclusiveSum(s->tmp, tb, x.rcnt, x.roff, (uint32_t)n_rec, st) != hipSuccess)
+      return RTPS_RX_EHIP;
+    if (n_rec)
+      hipLaunchKernelGGL(k_expand, dim3((uint32_t)hmin((n_rec + IT - 1) / IT, 8192)), dim3(IT), 0, st, t, n_rec, flags, x);
+  }
+  const uint32_t gv = (uint32_t)hmin((nev + IT - 1) / IT, 8192) ? (uint32_t)hmin((nev + IT - 1) / IT, 8192) : 1u;
+  const bool have_hb = reliable && n_hb > 0;
+  if (have_hb) {  // stable compaction of the HEARTBEAT events, sort by proxy, scans by key
     const uint32_t hb_blocks = (uint32_t)hmin((n_hb + IT - 1) / IT, 8192);
     ok = hipMemsetAsync(S.seg_b, 0, (uint64_t)s->ecap * 4, st) == hipSuccess &&
          hipMemsetAsync(S.seg_e, 0, (uint64_t)s->ecap * 4, st) == hipSuccess;
     if (!ok) return RTPS_RX_EHIP;
     size_t tb = s->tmp_bytes;
     if (hipcub::DeviceSelect::Flagged(s->tmp, tb, hipcub::CountingInputIterator<uint32_t>(0), x.hkey, x.hval,
-                                      S.ctr + C_NSEL, (int64_t)max, st) != hipSuccess)
+                                      S.ctr + C_NSEL, (int64_t)nev, st) != hipSuccess)
       return RTPS_RX_EHIP;
     hipLaunchKernelGGL(k_hkeys, dim3(hb_blocks), dim3(IT), 0, st, n_hb, x);
     tb = s->tmp_bytes;
@@ -673,17 +810,28 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const IngestTable& t, cons
                                                hipcub::Equality(), st) != hipSuccess)
       return RTPS_RX_EHIP;
   }
-  hipLaunchKernelGGL(k_marks_d, dim3(gb), dim3(IT), 0, st, n_records, max, x, S, s->epoch, n_gap > 0);
-  if (n_gap)
-    hipLaunchKernelGGL(k_marks_g, dim3(gb), dim3(IT), 0, st, records, arena, dgram_off, n_records, max, x, S, s->epoch);
-  hipLaunchKernelGGL(k_decide, dim3(gb), dim3(IT), 0, st, n_records, max, x, S, out->accept, have_hb, s->epoch);
+  if (nev) {
+    hipLaunchKernelGGL(k_marks_d, dim3(gv), dim3(IT), 0, st, nev, x, S, s->epoch, n_gap > 0);
+    if (n_gap)
+      hipLaunchKernelGGL(k_marks_g, dim3(gv), dim3(IT), 0, st, records, arena, dgram_off, nev, x, S, s->epoch);
+  }
+  // identity batches decide straight into accept[] (event i = record i: max slots, cleared past n)
+  uint8_t* acc = ident ? out->accept : x.eacc;
+  const uint64_t acc_cap = ident ? max : nev;
+  if (acc_cap)
+    hipLaunchKernelGGL(k_decide, dim3((uint32_t)hmin((acc_cap + IT - 1) / IT, 8192)), dim3(IT), 0, st, nev, acc_cap,
+                       x, S, acc, have_hb, s->epoch);
   size_t tb = s->tmp_bytes;
-  if (hipcub::DeviceSelect::Flagged(s->tmp, tb, hipcub::CountingInputIterator<uint32_t>(0), out->accept,
-                                    out->accepted, out->n_accepted, (int64_t)max, st) != hipSuccess)
+  if (hipcub::DeviceSelect::Flagged(s->tmp, tb, hipcub::CountingInputIterator<uint32_t>(0), acc, x.sel,
+                                    S.ctr + C_NDEL, (int64_t)acc_cap, st) != hipSuccess)
     return RTPS_RX_EHIP;
-  hipLaunchKernelGGL(k_merge, dim3(gb), dim3(IT), 0, st, records, arena, dgram_off, n_records, max, x, S, n_gap > 0);
-  if (t.n_entries)
-    hipLaunchKernelGGL(k_state, dim3(t.n_entries), dim3(IT), 0, st, t.n_entries, x, S, have_hb, out->ack_base);
+  hipLaunchKernelGGL(k_deliver, dim3(gv), dim3(IT), 0, st, S.ctr + C_NDEL, out->max_accepted, x, out->accepted,
+                     out->n_accepted);
+  if (!ident)
+    hipLaunchKernelGGL(k_accept_counts, dim3(gb), dim3(IT), 0, st, n_rec, max, x, out->accept);
+  if (nev) hipLaunchKernelGGL(k_merge, dim3(gv), dim3(IT), 0, st, records, arena, dgram_off, nev, x, S, n_gap > 0);
+  if (t.n_proxies)
+    hipLaunchKernelGGL(k_state, dim3(t.n_proxies), dim3(IT), 0, st, t.n_proxies, x, S, have_hb, out->ack_base);
   hipLaunchKernelGGL(k_finish, dim3(1), dim3(1), 0, st, S.ctr, out->n_window_overflow);
   return hipGetLastError() == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP;
 }

@@ -17,11 +17,12 @@ import os
 import numpy as np
 
 from .records import (RECORD_DTYPE, MATCH_DTYPE, FRAG_SAMPLE_DTYPE, STATUS_NAMES, KIND_NAMES, WRITER_KINDS, READER_KINDS,
-                      ROUTE_PASS, NO_MATCH, max_records, record_to_dict, pack_match_table)
+                      ROUTE_PASS, NO_MATCH, NO_TARGET, NO_PROXY, TARGET_DTYPE, DELIVERY_DTYPE, Readers, as_readers,
+                      max_records, record_to_dict, pack_match_table)
 
 _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RTPS_RX_LIB") or os.path.join(os.path.dirname(_PKG_DIR), "librtps_rx.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 WL_T, WL_C2, WL_C3, WL_C4 = 1, 2, 3, 4
 WORKLOADS = {"T": WL_T, "C2": WL_C2, "C3": WL_C3, "C4": WL_C4}
@@ -47,8 +48,8 @@ class _FragOut(ctypes.Structure):
 
 
 class _IngestOut(ctypes.Structure):
-    _fields_ = [("accept", ctypes.c_void_p), ("accepted", ctypes.c_void_p), ("n_accepted", ctypes.c_void_p),
-                ("ack_base", ctypes.c_void_p), ("n_window_overflow", ctypes.c_void_p)]
+    _fields_ = [("accept", ctypes.c_void_p), ("accepted", ctypes.c_void_p), ("max_accepted", ctypes.c_uint64),
+                ("n_accepted", ctypes.c_void_p), ("ack_base", ctypes.c_void_p), ("n_window_overflow", ctypes.c_void_p)]
 
 
 INGEST_BEST_EFFORT = 0x1
@@ -57,10 +58,11 @@ INGEST_WINDOW = 1 << 17
 
 class _Out(ctypes.Structure):
     _fields_ = [("status", ctypes.c_void_p), ("records", ctypes.c_void_p), ("max_records", ctypes.c_uint64),
-                ("match", ctypes.c_void_p), ("rec_begin", ctypes.c_void_p), ("n_records", ctypes.c_void_p)]
+                ("target", ctypes.c_void_p), ("rec_begin", ctypes.c_void_p), ("n_records", ctypes.c_void_p)]
 
 
 EXPORTS = ["rtps_rx_create", "rtps_rx_destroy", "rtps_rx_set_stream", "rtps_rx_set_match_table",
+           "rtps_rx_set_readers", "rtps_rx_target_table",
            "rtps_rx_parse_batch", "rtps_rx_sync", "rtps_rx_strerror", "rtps_rx_max_records_host",
            "rtps_rx_generate", "rtps_rx_bucket_by_writer", "rtps_rx_set_spec_hint", "rtps_rx_cdr_decode",
            "rtps_rx_bucket_by_writer_padded", "rtps_rx_frag_assemble", "rtps_rx_frag_reset",
@@ -81,6 +83,10 @@ def lib():
         L.rtps_rx_destroy.argtypes = [P]
         L.rtps_rx_set_stream.argtypes = [P, P]
         L.rtps_rx_set_match_table.argtypes = [P, P, U32]
+        L.rtps_rx_set_readers.argtypes = [P, P, U32, P, U32]
+        L.rtps_rx_set_readers.restype = I
+        L.rtps_rx_target_table.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(U32)]
+        L.rtps_rx_target_table.restype = I
         L.rtps_rx_parse_batch.argtypes = [P, P, U64, P, P, U32, ctypes.POINTER(_Out)]
         L.rtps_rx_sync.argtypes = [P]
         L.rtps_rx_strerror.argtypes = [I]
@@ -131,12 +137,12 @@ def gen_layout(workload, n, seed=SEED, first_idx=0, n_writers=16):
 
 
 class BatchResult:
-    """Host copies of one batch's outputs (status, records, match, rec_begin)."""
+    """Host copies of one batch's outputs (status, records, target sets, rec_begin)."""
 
-    def __init__(self, status, records, match, rec_begin, n_records):
+    def __init__(self, status, records, target, rec_begin, n_records):
         self.status = status
         self.records = records
-        self.match = match
+        self.target = target
         self.rec_begin = rec_begin
         self.n_records = n_records
 
@@ -176,6 +182,7 @@ class MessageReceiver:
         self.device = device
         self.max_datagrams = max_datagrams
         self.own_guid_prefix = own
+        self.readers = Readers()
 
     def close(self):
         if getattr(self, "_h", None):
@@ -194,11 +201,50 @@ class MessageReceiver:
         h = ctypes.c_void_p(-1) if stream is None else ctypes.c_void_p(stream.cuda_stream)
         _check(lib().rtps_rx_set_stream(self._h, h))
 
+    def set_readers(self, readers):
+        """The local readers and their writer proxies (a records.Readers, or what
+        records.as_readers accepts): Domain registration + Reader::matched_writer_add."""
+        rd = as_readers(readers)
+        r, p = rd.readers, rd.proxies
+        _check(lib().rtps_rx_set_readers(self._h, r.ctypes.data if len(r) else None, len(r),
+                                         p.ctypes.data if len(p) else None, len(p)))
+        self.readers = rd
+
     def set_match_table(self, entries):
-        """entries: MATCH_DTYPE array or iterable of (writer_guid bytes[16], reader_slot)."""
+        """Compatibility form: MATCH_DTYPE array or iterable of (writer_guid bytes[16], reader_slot);
+        every distinct slot becomes a reader, every distinct pair one of its proxies."""
         t = entries if isinstance(entries, np.ndarray) else pack_match_table(entries)
         t = np.ascontiguousarray(t, dtype=MATCH_DTYPE)
         _check(lib().rtps_rx_set_match_table(self._h, t.ctypes.data if len(t) else None, len(t)))
+        self.readers = as_readers(t)
+
+    def target_table(self):
+        """Host copy of the target sets: (first u32[n_sets + 1], entries TARGET_DTYPE)."""
+        first, ent, n = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint32()
+        _check(lib().rtps_rx_target_table(self._h, ctypes.byref(first), ctypes.byref(ent), ctypes.byref(n)))
+        k = int(n.value)
+        f = np.ctypeslib.as_array(ctypes.cast(first, ctypes.POINTER(ctypes.c_uint32)), shape=(k + 1,)).copy()
+        total = int(f[-1])
+        e = np.zeros(total, dtype=TARGET_DTYPE)
+        if total:
+            ctypes.memmove(e.ctypes.data, ent.value, total * TARGET_DTYPE.itemsize)
+        return f, e
+
+    def expand_targets(self, target):
+        """Per-record target readers from per-record target set ids: (off u64[m+1], TARGET_DTYPE[k])."""
+        first, ent = self.target_table()
+        target = np.asarray(target, dtype=np.uint32)
+        ok = target != NO_TARGET
+        cnt = np.zeros(len(target), dtype=np.uint64)
+        cnt[ok] = (first[target[ok] + 1] - first[target[ok]]).astype(np.uint64)
+        off = np.zeros(len(target) + 1, dtype=np.uint64)
+        np.cumsum(cnt, out=off[1:])
+        starts = first[target[ok]].astype(np.int64)
+        c = cnt[ok].astype(np.int64)
+        total = int(c.sum())
+        # entry j of record k: starts[k] + (j - first position of record k in the output)
+        sel = np.repeat(starts - (np.cumsum(c) - c), c) + np.arange(total, dtype=np.int64)
+        return off, ent[sel.astype(np.int64)]
 
     def set_spec_hint(self, records_per_datagram):
         """Performance hint only (results never depend on it): expected records per datagram."""
@@ -214,28 +260,44 @@ class MessageReceiver:
         return {
             "status": torch.empty(max(n, 1), dtype=torch.uint8, device=dev),
             "records": torch.empty((max(max_recs, 1), RECORD_DTYPE.itemsize), dtype=torch.uint8, device=dev),
-            "match": torch.empty(max(max_recs, 1), dtype=torch.int16, device=dev),
+            "target": torch.empty(max(max_recs, 1), dtype=torch.int32, device=dev),
             "rec_begin": torch.empty(max(n, 1), dtype=torch.int32, device=dev),
             "n_records": torch.zeros(1, dtype=torch.int64, device=dev),
             "max_records": max_recs,
         }
 
-    def parse_batch_device(self, arena, off, lens, n, outs, want_match=True, want_rec_begin=True):
+    def parse_batch_device(self, arena, off, lens, n, outs, want_target=True, want_rec_begin=True):
         """arena u8 / off i64 / lens i32 tensors (HBM, or pinned host memory for a
         zero-copy parse); outputs likewise.  Asynchronous on the context's stream."""
-        key = (want_match, want_rec_begin)
+        key = (want_target, want_rec_begin)
         o = outs.get("_c_out", {}).get(key)
         if o is None:
             o = _Out()
             o.status = outs["status"].data_ptr()
             o.records = outs["records"].data_ptr()
             o.max_records = outs["max_records"]
-            o.match = outs["match"].data_ptr() if want_match else None
+            o.target = outs["target"].data_ptr() if want_target else None
             o.rec_begin = outs["rec_begin"].data_ptr() if want_rec_begin else None
             o.n_records = outs["n_records"].data_ptr()
             outs.setdefault("_c_out", {})[key] = o
         _check(lib().rtps_rx_parse_batch(self._h, arena.data_ptr(), arena.numel(), off.data_ptr(),
                                          lens.data_ptr(), n, ctypes.byref(o)))
+
+    def debug_parse_phases(self, arena, off, lens, n, outs, phases):
+        """Measurement hook: launch only the parse's first kernel (phases=1) or only the
+        finishing kernel (phases=2); returns 1 (spec kernel A) or 2 (chained kernel C).
+        Run two full parse_batch_device calls afterwards."""
+        self.parse_batch_device(arena, off, lens, n, outs) if "_c_out" not in outs else None
+        o = outs["_c_out"][(True, True)]
+        L = lib()
+        fn = L.rtps_rx_debug_parse_phases
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                       ctypes.c_uint32, ctypes.POINTER(_Out), ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
+        fn.restype = ctypes.c_int
+        which = ctypes.c_uint32()
+        _check(fn(self._h, arena.data_ptr(), arena.numel(), off.data_ptr(), lens.data_ptr(), n, ctypes.byref(o),
+                  phases, ctypes.byref(which)))
+        return int(which.value)
 
     def generate(self, workload, arena, off, lens, n, seed=SEED, first_idx=0, n_writers=16):
         """Fill device arena with datagrams [first_idx, first_idx+n) of a synthetic workload."""
@@ -274,7 +336,7 @@ class MessageReceiver:
 
     def bucket_descriptors(self, outs, n_dest, cap, out_desc, dest_counts):
         """16-byte exchange descriptors of the MATCHED records in n_dest fixed buckets of cap
-        (owner = match-table entry index % n_dest); needs a match table."""
+        (owner = writer set index % n_dest); needs readers."""
         _check(lib().rtps_rx_bucket_descriptors(self._h, outs["records"].data_ptr(), outs["n_records"].data_ptr(),
                                                 outs["max_records"], n_dest, cap, out_desc.data_ptr(),
                                                 dest_counts.data_ptr()))
@@ -332,8 +394,8 @@ class MessageReceiver:
         total = int(outs["n_records"].item())
         kept = min(total, cap)
         recs = outs["records"][:kept].cpu().numpy().reshape(-1).view(RECORD_DTYPE)
-        match = outs["match"][:kept].cpu().numpy().view(np.uint16)
-        res = BatchResult(outs["status"][:n].cpu().numpy(), recs, match,
+        target = outs["target"][:kept].cpu().numpy().view(np.uint32)
+        res = BatchResult(outs["status"][:n].cpu().numpy(), recs, target,
                           outs["rec_begin"][:n].cpu().numpy().view(np.uint32), total)
         ns = int(fouts["n_samples"].item())
         used = int(fouts["heap_used"].item())
@@ -342,13 +404,19 @@ class MessageReceiver:
         return res, samples, heap, ns, used, int(fouts["n_pending"].item())
 
     # ---- history-cache ingest (writer-proxy state persists in the context) ----
-    def alloc_ingest_outputs(self, max_recs, n_entries):
+    def alloc_ingest_outputs(self, max_recs, n_proxies, max_accepted=None):
+        """max_accepted: deliveries room (default max_recs x the largest target set)."""
         import torch
         dev = torch.device("cuda", self.device)
+        if max_accepted is None:
+            first, _ = self.target_table()
+            widest = int(np.max(np.diff(first))) if len(first) > 1 else 1
+            max_accepted = max_recs * max(widest, 1)
         return {"accept": torch.empty(max(max_recs, 1), dtype=torch.uint8, device=dev),
-                "accepted": torch.empty(max(max_recs, 1), dtype=torch.int32, device=dev),
+                "accepted": torch.empty((max(max_accepted, 1), DELIVERY_DTYPE.itemsize), dtype=torch.uint8, device=dev),
+                "max_accepted": max_accepted,
                 "n_accepted": torch.zeros(1, dtype=torch.int64, device=dev),
-                "ack_base": torch.zeros(max(n_entries, 1), dtype=torch.int64, device=dev),
+                "ack_base": torch.zeros(max(n_proxies, 1), dtype=torch.int64, device=dev),
                 "n_window_overflow": torch.zeros(1, dtype=torch.int64, device=dev)}
 
     def ingest(self, arena, off, outs, iouts, fouts=None, best_effort=False):
@@ -360,6 +428,7 @@ class MessageReceiver:
             o = _IngestOut()
             o.accept = iouts["accept"].data_ptr()
             o.accepted = iouts["accepted"].data_ptr()
+            o.max_accepted = iouts["max_accepted"]
             o.n_accepted = iouts["n_accepted"].data_ptr()
             o.ack_base = iouts["ack_base"].data_ptr()
             o.n_window_overflow = iouts["n_window_overflow"].data_ptr()
@@ -374,9 +443,9 @@ class MessageReceiver:
     def ingest_reset(self):
         _check(lib().rtps_rx_ingest_reset(self._h))
 
-    def ingest_batch(self, arena_np, off_np, len_np, n_entries, frag=False, best_effort=False):
-        """Parse (+ reassemble) + ingest host arrays -> (BatchResult, accept u8[m], accepted u32[k],
-        ack_base i64[n_entries], n_window_overflow, frag samples or None)."""
+    def ingest_batch(self, arena_np, off_np, len_np, n_proxies, frag=False, best_effort=False):
+        """Parse (+ reassemble) + ingest host arrays -> (BatchResult, accept u8[m], deliveries
+        DELIVERY_DTYPE[k], ack_base i64[n_proxies], n_window_overflow, frag samples or None)."""
         import torch
         n = len(len_np)
         dev = torch.device("cuda", self.device)
@@ -385,7 +454,7 @@ class MessageReceiver:
         lens = torch.from_numpy(np.ascontiguousarray(len_np, dtype=np.uint32).view(np.int32)).to(dev)
         cap = max_records(len_np)
         outs = self.alloc_outputs(n, cap)
-        iouts = self.alloc_ingest_outputs(cap, n_entries)
+        iouts = self.alloc_ingest_outputs(cap, n_proxies)
         fouts = self.alloc_frag_outputs(cap, int(arena.numel()) + 16 * cap + (1 << 20)) if frag else None
         torch.cuda.synchronize(dev)
         self.parse_batch_device(arena, off, lens, n, outs)
@@ -396,16 +465,17 @@ class MessageReceiver:
         total = int(outs["n_records"].item())
         kept = min(total, cap)
         recs = outs["records"][:kept].cpu().numpy().reshape(-1).view(RECORD_DTYPE)
-        match = outs["match"][:kept].cpu().numpy().view(np.uint16)
-        res = BatchResult(outs["status"][:n].cpu().numpy(), recs, match,
+        target = outs["target"][:kept].cpu().numpy().view(np.uint32)
+        res = BatchResult(outs["status"][:n].cpu().numpy(), recs, target,
                           outs["rec_begin"][:n].cpu().numpy().view(np.uint32), total)
         na = int(iouts["n_accepted"].item())
         samples = None
         if frag:
             ns = min(int(fouts["n_samples"].item()), cap)
             samples = fouts["samples"][:ns].cpu().numpy().reshape(-1).view(FRAG_SAMPLE_DTYPE)
-        return (res, iouts["accept"][:kept].cpu().numpy(), iouts["accepted"][:na].cpu().numpy().view(np.uint32),
-                iouts["ack_base"][:n_entries].cpu().numpy(), int(iouts["n_window_overflow"].item()), samples)
+        dels = iouts["accepted"][:min(na, iouts["max_accepted"])].cpu().numpy().reshape(-1).view(DELIVERY_DTYPE)
+        return (res, iouts["accept"][:kept].cpu().numpy(), dels,
+                iouts["ack_base"][:n_proxies].cpu().numpy(), int(iouts["n_window_overflow"].item()), samples)
 
     # ---- convenience: host datagrams in, host results out ----
     def handle_received_batch(self, arena_np, off_np, len_np):
@@ -424,8 +494,8 @@ class MessageReceiver:
         total = int(outs["n_records"].item())
         kept = min(total, cap)
         recs = outs["records"][:kept].cpu().numpy().reshape(-1).view(RECORD_DTYPE)
-        match = outs["match"][:kept].cpu().numpy().view(np.uint16)
-        return BatchResult(outs["status"][:n].cpu().numpy(), recs, match,
+        target = outs["target"][:kept].cpu().numpy().view(np.uint32)
+        return BatchResult(outs["status"][:n].cpu().numpy(), recs, target,
                            outs["rec_begin"][:n].cpu().numpy().view(np.uint32), total)
 
     def take_batch(self, sample_type, arena_np, off_np, len_np):
@@ -447,7 +517,7 @@ class MessageReceiver:
         total = int(outs["n_records"].item())
         kept = min(total, cap)
         recs = outs["records"][:kept].cpu().numpy().reshape(-1).view(RECORD_DTYPE)
-        match = outs["match"][:kept].cpu().numpy().view(np.uint16)
-        res = BatchResult(outs["status"][:n].cpu().numpy(), recs, match,
+        target = outs["target"][:kept].cpu().numpy().view(np.uint32)
+        res = BatchResult(outs["status"][:n].cpu().numpy(), recs, target,
                           outs["rec_begin"][:n].cpu().numpy().view(np.uint32), total)
         return res, sample_type.rows(rows[:kept].cpu().numpy()), row_status[:kept].cpu().numpy()

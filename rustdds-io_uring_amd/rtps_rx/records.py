@@ -23,13 +23,16 @@ WRITER_KINDS = (DATA, DATA_FRAG, HEARTBEAT, HEARTBEAT_FRAG, GAP)
 READER_KINDS = (ACKNACK, NACK_FRAG)
 INTERPRETER_KINDS = (INFO_TS, INFO_SRC, INFO_DST, INFO_REPLY)
 
-ROUTE_PASS, ROUTE_TS_VALID, ROUTE_HAS_QOS, ROUTE_HAS_PAYLOAD, ROUTE_BUILTIN, ROUTE_MATCHED = \
-    0x01, 0x02, 0x04, 0x08, 0x10, 0x20
+ROUTE_PASS, ROUTE_TS_VALID, ROUTE_HAS_QOS, ROUTE_HAS_PAYLOAD, ROUTE_BUILTIN, ROUTE_MATCHED, ROUTE_TARGETED = \
+    0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40
 
 PK_NONE, PK_DATA, PK_KEY, PK_KEY_HASH = 0, 1, 2, 3
 PK_ERR_NO_CONTENT, PK_ERR_AMBIGUOUS, PK_ERR_SHORT = 0x81, 0x82, 0x83
 
 NO_MATCH = 0xFFFF
+NO_TARGET = 0xFFFFFFFF
+NO_PROXY = 0xFFFFFFFF
+READER_STATELESS, READER_BEST_EFFORT, TARGET_DUPLICATES_OK = 0x1, 0x2, 0x8000
 MAX_DATAGRAM = 65536
 
 RECORD_DTYPE = np.dtype([
@@ -58,6 +61,13 @@ UNION_BY_KIND = {DATA: U_DATA, DATA_FRAG: U_FRAG, HEARTBEAT: U_HB, HEARTBEAT_FRA
                  ACKNACK: U_ACKNACK, NACK_FRAG: U_NACKFRAG, INFO_SRC: U_INFOSRC, INFO_REPLY: U_INFOREPLY}
 
 MATCH_DTYPE = np.dtype([("writer_guid", "u1", (16,)), ("reader_slot", "<u2"), ("_pad", "<u2")])
+# local readers and their writer proxies (rtps_reader / rtps_proxy / rtps_target / rtps_delivery)
+READER_DTYPE = np.dtype([("entity_id", "u1", (4,)), ("reader_slot", "<u2"), ("flags", "<u2")])
+PROXY_DTYPE = np.dtype([("writer_guid", "u1", (16,)), ("reader", "<u4")])
+TARGET_DTYPE = np.dtype([("reader_slot", "<u2"), ("reader_flags", "<u2"), ("proxy", "<u4")])
+DELIVERY_DTYPE = np.dtype([("rec_idx", "<u4"), ("reader_slot", "<u2"), ("_r", "<u2")])
+assert READER_DTYPE.itemsize == 8 and PROXY_DTYPE.itemsize == 20 and TARGET_DTYPE.itemsize == 8
+assert DELIVERY_DTYPE.itemsize == 8
 
 # exchange descriptor (rtps_xdesc): the compact cross-GPU form of a matched writer's record
 XDESC_DTYPE = np.dtype([("sn", "<i8"), ("rec_idx", "<u4"), ("writer_kind", "<u4")])
@@ -110,3 +120,58 @@ def pack_match_table(entries):
         t[i]["writer_guid"] = np.frombuffer(bytes(g), dtype=np.uint8)
         t[i]["reader_slot"] = slot
     return t
+
+
+class Readers:
+    """The local readers and their writer proxies (rtps_rx_set_readers): the
+    reference's available_readers (io_uring/rtps/message_receiver.rs:129), each
+    Reader's matched_writers (io_uring/rtps/reader.rs:145)."""
+
+    def __init__(self, readers=(), proxies=()):
+        """readers: iterable of (entity_id bytes[4], reader_slot, flags);
+        proxies: iterable of (writer_guid bytes[16], reader index)."""
+        readers, proxies = list(readers), list(proxies)
+        self.readers = np.zeros(len(readers), dtype=READER_DTYPE)
+        for i, (eid, slot, flags) in enumerate(readers):
+            assert len(eid) == 4
+            self.readers[i]["entity_id"] = np.frombuffer(bytes(eid), dtype=np.uint8)
+            self.readers[i]["reader_slot"] = slot
+            self.readers[i]["flags"] = flags
+        self.proxies = np.zeros(len(proxies), dtype=PROXY_DTYPE)
+        for i, (g, r) in enumerate(proxies):
+            assert len(g) == 16
+            self.proxies[i]["writer_guid"] = np.frombuffer(bytes(g), dtype=np.uint8)
+            self.proxies[i]["reader"] = r
+
+    @property
+    def n_proxies(self):
+        return len(self.proxies)
+
+    @classmethod
+    def from_match(cls, entries):
+        """The compatibility form (rtps_rx_set_match_table): every distinct slot is one
+        reliable stateful reader (EntityId order = first appearance), every distinct
+        (writer GUID, slot) pair one proxy."""
+        t = entries if isinstance(entries, np.ndarray) else pack_match_table(entries)
+        slots, readers, proxies, seen = {}, [], [], set()
+        for e in t:
+            slot = int(e["reader_slot"])
+            if slot not in slots:
+                r = len(readers)
+                slots[slot] = r
+                readers.append((bytes([(r >> 16) & 255, (r >> 8) & 255, r & 255, 0x07]), slot, 0))
+            g = bytes(e["writer_guid"])
+            if (slots[slot], g) in seen:
+                continue
+            seen.add((slots[slot], g))
+            proxies.append((g, slots[slot]))
+        return cls(readers, proxies)
+
+
+def as_readers(table):
+    """A Readers, a MATCH_DTYPE array, an iterable of (guid, slot) pairs, or None (no readers)."""
+    if table is None:
+        return Readers()
+    if isinstance(table, Readers):
+        return table
+    return Readers.from_match(table)

@@ -2,7 +2,7 @@
 
 Each rank parses its own contiguous chunk of datagrams; the records of the
 writer and reader submessages are then partitioned by owner rank =
-fnv1a32(prefix || writer_id) % world (stable, on the device:
+fmix32(fnv1a32(prefix || writer_id)) % world (stable, on the device:
 rtps_rx_bucket_by_writer) and exchanged with ONE all-to-all.  The owner then
 holds every record of its writers (ready for per-writer ordering, dedup and
 fragment assembly).  The reference has a single process and no exchange;
@@ -12,9 +12,15 @@ What crosses xGMI (item):
   * "records": the 64-byte records of every writer/reader submessage, owner =
     GUID hash % world (rtps_rx_bucket_by_writer[_padded]);
   * "descriptors": 16-byte rtps_xdesc of the MATCHED records only, owner =
-    match-table entry index % world (rtps_rx_bucket_descriptors): 4x fewer
+    writer set index % world (rtps_rx_bucket_descriptors): 4x fewer
     bytes, and owners balanced by the table order instead of a hash of a few
     writer GUIDs.  Full records and payloads stay on the source GPU.
+
+Transport: with the "nccl" (RCCL) process group the buckets move through the
+library's own RCCL exchange (rtps_rx_exchange: grouped ncclSend/ncclRecv per
+peer on a dedicated HIP stream, the same entry point a Rust host binds;
+torch.distributed only bootstraps the communicator's unique id).  The "gloo"
+group (CPU tensors) rehearses several ranks on one GPU, which RCCL cannot.
 
 Two modes:
   * contiguous (cap=None): buckets back to back, split sizes read back to the
@@ -26,18 +32,66 @@ Two modes:
     the parse of batch k+1.  Overflow (a bucket > C) is reported by
     overflowed(); C is sized from the previous batch's counts.
 """
+import ctypes
+
 import torch
 
 RECORD_BYTES = 64
+_COMMS = {}
+
+
+def destroy_comms():
+    """Destroy the library RCCL communicators of this process (call before the process group goes)."""
+    from . import lib
+    while _COMMS:
+        _, c = _COMMS.popitem()
+        lib().rtps_rx_exchange_comm_destroy.argtypes = [ctypes.c_void_p]
+        lib().rtps_rx_exchange_comm_destroy(c)
+
+
+def rccl_comm(rx, dist, device):
+    """This process's RCCL communicator for the library's exchange (one per world/rank):
+    rank 0 makes the unique id, torch.distributed broadcasts it, every rank inits."""
+    from . import lib, _check
+    key = (dist.get_world_size(), dist.get_rank())
+    if key not in _COMMS:
+        L = lib()
+        L.rtps_rx_exchange_unique_id.argtypes = [ctypes.c_void_p]
+        L.rtps_rx_exchange_comm_init.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                 ctypes.POINTER(ctypes.c_void_p)]
+        uid = (ctypes.c_uint8 * 128)()
+        if key[1] == 0:
+            _check(L.rtps_rx_exchange_unique_id(uid))
+        obj = [bytes(uid)]
+        dist.broadcast_object_list(obj, src=0)
+        uid = (ctypes.c_uint8 * 128).from_buffer_copy(obj[0])
+        comm = ctypes.c_void_p()
+        _check(L.rtps_rx_exchange_comm_init(uid, key[0], key[1], device.index, ctypes.byref(comm)))
+        _COMMS[key] = comm
+    return _COMMS[key]
 ITEM_BYTES = {"records": 64, "descriptors": 16}
 
 
 def owner_hash_words(words):
-    """fnv1a32 over 4 little-endian u32 words, then h ^ (h >> 15) (same as the device)."""
+    """fnv1a32 over 4 little-endian u32 words, then the murmur3 finaliser fmix32 (the device's owner_hash)."""
     h = 0x811C9DC5
     for w in words:
         h = ((h ^ int(w)) * 0x01000193) & 0xFFFFFFFF
-    return h ^ (h >> 15)
+    h ^= h >> 16
+    h = (h * 0x85EBCA6B) & 0xFFFFFFFF
+    h ^= h >> 13
+    h = (h * 0xC2B2AE35) & 0xFFFFFFFF
+    return h ^ (h >> 16)
+
+
+class _StreamWork:
+    """wait(): the caller's current stream waits for the exchange (like a collective's Work)."""
+
+    def __init__(self, event, device):
+        self.event, self.device = event, device
+
+    def wait(self):
+        torch.cuda.current_stream(self.device).wait_event(self.event)
 
 
 class Exchange:
@@ -59,6 +113,9 @@ class Exchange:
         self.received = torch.empty((max(slots, 1), ib), dtype=torch.uint8, device=device) if cap else None
         backend = dist.get_backend() if dist is not None else None
         self.host_collectives = backend == "gloo"  # gloo moves CPU tensors only
+        # RCCL: the library's exchange on a dedicated stream (padded mode)
+        self.comm = rccl_comm(rx, dist, device) if (dist is not None and not self.host_collectives and cap) else None
+        self.xstream = torch.cuda.Stream(device) if self.comm is not None else None
 
     def bucket(self, outs):
         """Stable partition of this rank's records by owner rank (asynchronous)."""
@@ -108,9 +165,18 @@ class Exchange:
             self.recv_counts.copy_(rc)
             self.received.copy_(rv)
             return []
-        w1 = dist.all_to_all_single(self.recv_counts, self.counts, async_op=True)
-        w2 = dist.all_to_all_single(self.received, self.bucketed, async_op=True)
-        return [w1, w2]
+        from . import lib, _check
+        cur = torch.cuda.current_stream(self.device)
+        self.xstream.wait_stream(cur)  # the buckets are complete
+        L = lib()
+        L.rtps_rx_exchange.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p,
+                                                               ctypes.c_void_p]
+        _check(L.rtps_rx_exchange(self.rx._h, self.comm, ctypes.c_void_p(self.xstream.cuda_stream),
+                                  self.bucketed.data_ptr(), self.counts.data_ptr(), self.cap,
+                                  ITEM_BYTES[self.item], self.received.data_ptr(), self.recv_counts.data_ptr()))
+        done = torch.cuda.Event()
+        done.record(self.xstream)
+        return [_StreamWork(done, self.device)]
 
     def gather_received(self):
         """Host view after exchange_async completed: the valid items from every source in

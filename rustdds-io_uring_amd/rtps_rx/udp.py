@@ -194,12 +194,13 @@ class Pump:
             rows = rx.alloc_rows(sample_type, cap) if sample_type is not None else (None, None)
             o = arr[b].out
             o.status, o.records, o.max_records = outs["status"].data_ptr(), outs["records"].data_ptr(), cap
-            o.match, o.rec_begin, o.n_records = (outs["match"].data_ptr(), outs["rec_begin"].data_ptr(),
-                                                 outs["n_records"].data_ptr())
+            o.target, o.rec_begin, o.n_records = (outs["target"].data_ptr(), outs["rec_begin"].data_ptr(),
+                                                  outs["n_records"].data_ptr())
             if ingest:
                 g = arr[b].ingest
                 g.accept, g.accepted, g.n_accepted = (iouts["accept"].data_ptr(), iouts["accepted"].data_ptr(),
                                                       iouts["n_accepted"].data_ptr())
+                g.max_accepted = iouts["max_accepted"]
                 g.ack_base, g.n_window_overflow = iouts["ack_base"].data_ptr(), iouts["n_window_overflow"].data_ptr()
             if sample_type is not None:
                 arr[b].rows, arr[b].row_status = rows[0].data_ptr(), rows[1].data_ptr()

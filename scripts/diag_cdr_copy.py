@@ -6,7 +6,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "rustdds-io_uring_amd")]
 import torch, rtps_rx
 from rtps_rx import cdr
-D = ctypes.CDLL(os.path.join(REPO, "build", "libdiag_ceiling.so"))
+D = ctypes.CDLL(os.path.join(REPO, "rustdds-io_uring_amd", "libdiag_ceiling.so"))
 D.diag_copy.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
                         ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
 dev = torch.device("cuda", 0)

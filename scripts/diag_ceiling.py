@@ -4,7 +4,7 @@ import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "rustdds-io_uring_amd")]
 import torch, rtps_rx
-D = ctypes.CDLL(os.path.join(REPO, "build", "libdiag_ceiling.so"))
+D = ctypes.CDLL(os.path.join(REPO, "rustdds-io_uring_amd", "libdiag_ceiling.so"))
 D.diag_ceiling.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 3 + [ctypes.c_uint32] + [ctypes.c_void_p] * 4
 dev = torch.device("cuda", 0)
 for wlname in (sys.argv[1:] or ["T", "C2"]):

@@ -2,7 +2,12 @@
 its chunk on the device, parses it, buckets by writer GUID on the device and
 exchanges records (gloo on a 1-GPU box, nccl=RCCL across GPUs); every rank
 verifies what it received against the CPU oracle.  Launch with
-python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 scripts/shard_check.py [backend] [padded]"""
+python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 scripts/shard_check.py [backend] [padded|desc] [c5]
+
+c5: each rank's chunk starts at generator index rank * 8M, as BASELINE config C5
+(64M datagrams over 8 GPUs) lays the stream out (reduced n per rank).  With the
+nccl backend and padded buckets the records move through the library's own RCCL
+exchange (rtps_rx_exchange); one rank exchanges with itself."""
 import os
 import sys
 
@@ -22,13 +27,15 @@ from shard_ref import owner_np
 backend = sys.argv[1] if len(sys.argv) > 1 else "gloo"
 padded = len(sys.argv) > 2 and sys.argv[2] in ("padded", "desc")
 desc = len(sys.argv) > 2 and sys.argv[2] == "desc"
+c5 = "c5" in sys.argv[2:]
 rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
 ngpu = torch.cuda.device_count()
 dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")) % ngpu)
 torch.cuda.set_device(dev)
 dist.init_process_group(backend)
 n = 20000
-off, ln, size = rtps_rx.gen_layout(rtps_rx.WL_C3, n, first_idx=rank * n)
+stride = (8 << 20) if c5 else n  # generator index of rank r's first datagram: r * stride
+off, ln, size = rtps_rx.gen_layout(rtps_rx.WL_C3, n, first_idx=rank * stride)
 rx = rtps_rx.MessageReceiver(oracle.OWN_PREFIX, device=dev.index, max_datagrams=n)
 st = torch.cuda.Stream(dev)
 torch.cuda.set_stream(st)
@@ -36,7 +43,7 @@ rx.set_stream(st)
 arena = torch.zeros(size, dtype=torch.uint8, device=dev)
 off_t = torch.from_numpy(off.view(np.int64)).to(dev)
 ln_t = torch.from_numpy(ln.view(np.int32)).to(dev)
-rx.generate(rtps_rx.WL_C3, arena, off_t, ln_t, n, first_idx=rank * n)
+rx.generate(rtps_rx.WL_C3, arena, off_t, ln_t, n, first_idx=rank * stride)
 cap = rtps_rx.max_records(ln)
 outs = rx.alloc_outputs(n, cap)
 table = None
@@ -70,7 +77,7 @@ if desc:
     got = got.cpu().numpy().reshape(-1).view(XDESC_DTYPE)
     exp = []
     for r in range(world):
-        a, o, l = oracle.gen(oracle.WL_C3, n, first_idx=r * n)
+        a, o, l = oracle.gen(oracle.WL_C3, n, first_idx=r * stride)
         _, recs, _, _ = oracle.parse(a, o, l, match_table=table)
         exp.append(desc_bucket_np(recs, [bytes(t["writer_guid"]) for t in table], world)[rank])
     exp = np.concatenate(exp)
@@ -78,13 +85,17 @@ else:
     got = got.cpu().numpy().reshape(-1).view(RECORD_DTYPE)
     exp = []
     for r in range(world):
-        a, o, l = oracle.gen(oracle.WL_C3, n, first_idx=r * n)
+        a, o, l = oracle.gen(oracle.WL_C3, n, first_idx=r * stride)
         _, recs, _, _ = oracle.parse(a, o, l)
         exp.append(recs[owner_np(recs, world) == rank])
     exp = np.concatenate(exp)
 ok = got.tobytes() == exp.tobytes()
-print(f"rank {rank}/{world} ({backend}{', desc' if desc else ', padded' if padded else ''}): received {len(got)} records, expected {len(exp)}, "
+via = "library RCCL exchange" if getattr(ex, "comm", None) is not None else "torch.distributed " + backend
+print(f"rank {rank}/{world} ({via}{', desc' if desc else ', padded' if padded else ''}{', C5 indices' if c5 else ''}): "
+      f"received {len(got)} records, expected {len(exp)}, "
       f"{'OK' if ok else 'MISMATCH'}", flush=True)
 dist.barrier()
+from rtps_rx.shard import destroy_comms
+destroy_comms()
 dist.destroy_process_group()
 sys.exit(0 if ok else 1)

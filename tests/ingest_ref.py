@@ -114,63 +114,85 @@ class Proxy:
 
 
 class IngestRef:
-    """Sequential model over the records of successive batches."""
+    """Sequential model over the records of successive batches: every record the
+    receiver passes (ROUTE_PASS) that is not a builtin pair (ROUTE_BUILTIN) goes to
+    the readers that contain its writer's entity id, in EntityId order
+    (dp_event_loop.rs:266-327, reader.rs:474-484), one writer proxy per
+    (reader, writer GUID) (reader.rs:693-758)."""
 
-    def __init__(self, table_guids):
-        self.entry = {}
-        for i, g in enumerate(table_guids):
-            self.entry.setdefault(bytes(g), i)
-        self.proxies = [Proxy() for _ in table_guids]
+    def __init__(self, readers):
+        from rtps_rx.records import as_readers, READER_STATELESS
+        rd = as_readers(readers)
+        self.slot = [int(r["reader_slot"]) for r in rd.readers]
+        self.flags = [int(r["flags"]) for r in rd.readers]
+        self.eid = [bytes(r["entity_id"]) for r in rd.readers]
+        self.order = sorted(range(len(rd.readers)), key=lambda i: self.eid[i])
+        self.proxy_of = {}
+        self.contains = [set() for _ in rd.readers]
+        for k, p in enumerate(rd.proxies):
+            g, r = bytes(p["writer_guid"]), int(p["reader"])
+            self.proxy_of[(r, g)] = k
+            if not self.flags[r] & READER_STATELESS:
+                self.contains[r].add(g[12:])
+        self.proxies = [Proxy() for _ in rd.proxies]
+
+    def targets(self, guid):
+        return [(r, self.proxy_of.get((r, guid))) for r in self.order if guid[12:] in self.contains[r]]
+
+    def _sample(self, r, k, guid, sn):
+        if k is None:
+            return guid[15] & 0xF0 != 0  # no proxy: only a writer whose kind is not user-defined
+        p = self.proxies[k]
+        if p.should_ignore(sn) and self.eid[r] != SPDP_PARTICIPANT_READER:
+            return False
+        p.received_add(sn)
+        return True
 
     def batch(self, arena, offs, recs, frag_samples=(), best_effort=False):
-        at = {int(s["rec_idx"]): s for s in frag_samples}
-        accepted = []
+        """-> (deliveries [(record, reader slot)], ack_base per proxy)."""
+        from rtps_rx.records import ROUTE_BUILTIN, WRITER_KINDS, READER_BEST_EFFORT
+        at = {int(s["rec_idx"]): s for s in (frag_samples if frag_samples is not None else ())}
+        out = []
         for i, r in enumerate(recs):
-            if i in at:
-                s = at[i]
-                e = self.entry.get(bytes(s["writer_guid"]))
-                if int(s["status"]) != 1 and e is not None:
-                    p = self.proxies[e]
-                    if not p.should_ignore(int(s["sn"])):
-                        p.received_add(int(s["sn"]))
-                        accepted.append(i)
+            route, kind = int(r["route"]), int(r["kind"])
+            if not route & ROUTE_PASS or route & ROUTE_BUILTIN or kind not in WRITER_KINDS:
                 continue
-            route = int(r["route"])
-            if not (route & ROUTE_PASS and route & ROUTE_MATCHED):
-                continue
-            e = self.entry.get(bytes(r["prefix"]) + bytes(r["writer_id"]))
-            if e is None:
-                continue
-            p = self.proxies[e]
-            kind, sn = int(r["kind"]), int(r["sn"])
-            u = r["u"].tobytes()
-            if kind == DATA:
-                if int(r["payload_kind"]) not in (PK_DATA, PK_KEY, PK_KEY_HASH):
-                    continue
-                if not p.should_ignore(sn):
-                    p.received_add(sn)
-                    accepted.append(i)
-            elif kind == HEARTBEAT and not best_effort:
-                count = struct.unpack_from("<i", u, 8)[0]
-                if count <= p.hb_count:
-                    continue
-                p.hb_count = count
-                p.irrelevant_range(0, sn)
-            elif kind == GAP:
-                base, nb, boff = struct.unpack_from("<qIH", u, 0)
-                if sn <= 0 or base <= 0:
-                    continue
-                p.irrelevant_range(sn, base)
-                bm = int(offs[int(r["dgram_idx"])]) + boff
-                le = int(r["flags"]) & 1
-                for b in range(nb):
-                    w = bytes(arena[bm + 4 * (b // 32):bm + 4 * (b // 32) + 4])
-                    word = struct.unpack("<I" if le else ">I", w)[0]
-                    if word & (1 << (31 - b % 32)):
-                        p.set_irrelevant(base + b)
-        return accepted, [p.ack_base for p in self.proxies]
+            guid = bytes(r["prefix"]) + bytes(r["writer_id"])
+            for rd, k in self.targets(guid):
+                p = self.proxies[k] if k is not None else None
+                sn = int(r["sn"])
+                u = r["u"].tobytes()
+                if i in at:
+                    s = at[i]
+                    if int(s["status"]) != 1 and self._sample(rd, k, guid, int(s["sn"])):
+                        out.append((i, self.slot[rd]))
+                elif kind == DATA:
+                    if int(r["payload_kind"]) in (PK_DATA, PK_KEY, PK_KEY_HASH) and self._sample(rd, k, guid, sn):
+                        out.append((i, self.slot[rd]))
+                elif kind == HEARTBEAT:
+                    if best_effort or self.flags[rd] & READER_BEST_EFFORT or p is None:
+                        continue
+                    count = struct.unpack_from("<i", u, 8)[0]
+                    if count <= p.hb_count:
+                        continue
+                    p.hb_count = count
+                    p.irrelevant_range(0, sn)
+                elif kind == GAP:
+                    base, nb, boff = struct.unpack_from("<qIH", u, 0)
+                    if p is None or sn <= 0 or base <= 0:
+                        continue
+                    p.irrelevant_range(sn, base)
+                    bm = int(offs[int(r["dgram_idx"])]) + boff
+                    le = int(r["flags"]) & 1
+                    for b in range(nb):
+                        w = bytes(arena[bm + 4 * (b // 32):bm + 4 * (b // 32) + 4])
+                        word = struct.unpack("<I" if le else ">I", w)[0]
+                        if word & (1 << (31 - b % 32)):
+                            p.set_irrelevant(base + b)
+        return out, [p.ack_base for p in self.proxies]
 
 
+SPDP_PARTICIPANT_READER = bytes([0x00, 0x01, 0x00, 0xC7])
 PREFIXES = [bytes([0xA0 + k] * 12) for k in range(4)]
 OWN = bytes([0x01, 0x03, 0x00, 0x0c, 0x29, 0x2d, 0x31, 0xa2, 0x28, 0x20, 0x02, 0x08])
 
@@ -180,22 +202,25 @@ def writer_key(k):
 
 
 def table(n_prefix=3, n_writer=3):
-    """Match table: writers (prefix p, key k) for p < n_prefix, k < n_writer, reader slot = p*n_writer+k.
-    One duplicate entry (first wins) and one unmatched writer (prefix 3) stay out of the table."""
+    """Match table (compatibility form): writers (prefix p, key k) for p < n_prefix, k < n_writer,
+    reader slot = p*n_writer+k; writer (prefix 0, key 0) also goes to a second reader (slot 77);
+    writers of prefix 3 have no proxy."""
     from rtps_rx.records import pack_match_table
     ents = [(PREFIXES[p] + writer_key(k), p * n_writer + k) for p in range(n_prefix) for k in range(n_writer)]
     ents.append((PREFIXES[0] + writer_key(0), 77))
     return pack_match_table(ents), [g for g, _ in ents]
 
 
-def stream(n, seed, sn_hi=60, n_prefix=4, n_writer=3):
+def stream(n, seed, sn_hi=60, n_prefix=4, n_writer=3, keys=None):
     """n datagrams of reliable-reader traffic with every case the proxies have to
     replay in order: duplicate and out-of-order DATA, KEY and KEY_HASH samples,
     DATA whose payload decision fails, HEARTBEATs with stale counts and any
     firstSN (<= 0 too), valid and invalid GAPs with ranges and bitmaps, big- and
     little-endian submessages, writers outside the match table, and writer
-    submessages after an INFO_DST to another participant (not passed)."""
+    submessages after an INFO_DST to another participant (not passed).
+    keys: writer entity ids to draw from (default writer_key(0 .. n_writer-1))."""
     rng = np.random.default_rng(seed)
+    keys = [writer_key(k) for k in range(n_writer)] if keys is None else list(keys)
     out = []
     for _ in range(n):
         p = int(rng.integers(n_prefix))
@@ -203,10 +228,9 @@ def stream(n, seed, sn_hi=60, n_prefix=4, n_writer=3):
         if rng.random() < 0.05:
             subs.append(info_dst_sub(bytes([7] * 12)))
         for _ in range(int(rng.integers(1, 4))):
-            k = int(rng.integers(n_writer))
+            wk = keys[int(rng.integers(len(keys)))]
             le = bool(rng.random() < 0.8)
             x = rng.random()
-            wk = writer_key(k)
             if x < 0.55:
                 sn = int(rng.integers(-1, sn_hi))
                 y = rng.random()
@@ -229,3 +253,34 @@ def stream(n, seed, sn_hi=60, n_prefix=4, n_writer=3):
                 subs.append(gap_sub(wk, start, base, bits, le))
         out.append(datagram(PREFIXES[p], subs))
     return out
+
+
+# ---- a15: reader sets (dp_event_loop.rs:266-327, reader.rs:474-484, 693-758) ----
+BUILTIN_KIND_KEY = bytes([0, 0, 9, 0xC2])   # a writer entity of builtin kind that is no discovery pair
+VENDOR_KIND_KEY = bytes([0, 0, 10, 0x42])   # vendor-specific kind: not user-defined either
+
+
+def a15_readers():
+    """Readers listed out of EntityId order: two readers on one writer, a stateless reader with
+    proxies, a BestEffort reader, the SPDP participant reader id (accepts duplicates), and
+    builtin- / vendor-kind writers."""
+    from rtps_rx.records import Readers, READER_STATELESS, READER_BEST_EFFORT
+    P, wk = PREFIXES, writer_key
+    readers = [(bytes([0, 0, 2, 0x07]), 11, 0),
+               (bytes([0, 0, 1, 0x07]), 10, 0),
+               (bytes([0, 0, 0, 0x04]), 12, READER_STATELESS),
+               (bytes([0, 0, 3, 0x07]), 13, READER_BEST_EFFORT),
+               (SPDP_PARTICIPANT_READER, 14, 0)]
+    proxies = [(P[0] + wk(0), 1), (P[0] + wk(0), 0),     # one writer, two readers
+               (P[1] + wk(0), 0), (P[0] + wk(1), 0),
+               (P[0] + wk(2), 2), (P[1] + wk(2), 2),     # the stateless reader's: never targeted
+               (P[2] + wk(1), 3),                         # BestEffort reader
+               (P[0] + BUILTIN_KIND_KEY, 1),
+               (P[1] + VENDOR_KIND_KEY, 4),
+               (P[0] + wk(0), 4)]                         # the participant reader on writer 0 too
+    return Readers(readers, proxies)
+
+
+def a15_stream(n, seed, sn_hi=40):
+    return stream(n, seed, sn_hi=sn_hi, keys=[writer_key(0), writer_key(1), writer_key(2), BUILTIN_KIND_KEY,
+                                              VENDOR_KIND_KEY])

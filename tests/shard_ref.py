@@ -9,7 +9,12 @@ def owner_np(recs, world):
     h = np.full(len(recs), 0x811C9DC5, dtype=np.uint64)
     for k in range(4):
         h = ((h ^ w[:, k]) * np.uint64(0x01000193)) & np.uint64(0xFFFFFFFF)
-    h ^= h >> np.uint64(15)
+    m = np.uint64(0xFFFFFFFF)  # murmur3 fmix32
+    h ^= h >> np.uint64(16)
+    h = (h * np.uint64(0x85EBCA6B)) & m
+    h ^= h >> np.uint64(13)
+    h = (h * np.uint64(0xC2B2AE35)) & m
+    h ^= h >> np.uint64(16)
     owner = (h % np.uint64(world)).astype(np.int64)
     exch = np.isin(recs["kind"], WRITER_KINDS + READER_KINDS)
     return np.where(exch, owner, -1)
@@ -27,11 +32,12 @@ def bucket_np(recs, world):
 
 def desc_bucket_np(recs, table_guids, world):
     """numpy reference of rtps_rx_bucket_descriptors: MATCHED records of table writers,
-    owner = first table index % world, stable; returns (list per owner of XDESC rows)."""
+    owner = writer set index (rank of the GUID's first appearance) % world, stable; returns
+    (list per owner of XDESC rows)."""
     from rtps_rx.records import XDESC_DTYPE, ROUTE_MATCHED
     index = {}
-    for k, g in enumerate(table_guids):
-        index.setdefault(bytes(g), k)
+    for g in table_guids:
+        index.setdefault(bytes(g), len(index))
     out = [[] for _ in range(world)]
     for i, r in enumerate(recs):
         if not (int(r["route"]) & ROUTE_MATCHED):

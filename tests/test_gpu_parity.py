@@ -1,7 +1,9 @@
 """GPU parity: the HIP parser (through the C ABI) vs the CPU oracle, bit-exact.
 
-Every record byte, every status byte, the match slots, rec_begin and the
-record count must be identical.  Inputs: the reference's golden vectors,
+Every record byte, every status byte, every record's target readers (the
+GPU's target set expanded through the library's set table against the
+oracle's literal available_readers scan), rec_begin and the record count must
+be identical.  Inputs: the reference's golden vectors,
 the four synthetic BASELINE workloads (generated on the device and copied
 back for the oracle), misaligned packing, byte-flip fuzz, edge cases
 (empty batch, 64 KiB datagrams, max-records datagrams, arena tail), and the
@@ -14,7 +16,8 @@ import pytest
 
 import oracle
 from golden_cases import cases, check_case, shape_type_from_payload
-from rtps_rx.records import record_to_dict, RECORD_DTYPE, DGRAM_OK, DATA, max_records
+import rtps_rx.records as rtps_records
+from rtps_rx.records import record_to_dict, RECORD_DTYPE, DGRAM_OK, DATA, max_records, NO_TARGET
 
 pytestmark = pytest.mark.gpu
 
@@ -29,8 +32,8 @@ def rx():
     r.close()
 
 
-def _assert_same(gpu, ora, label):
-    st, recs, match, rb = ora
+def _assert_same(gpu, ora, label, rx=None):
+    st, recs, tg, rb = ora
     assert np.array_equal(gpu.status, st), f"{label}: status differs at {np.nonzero(gpu.status != st)[0][:10]}"
     assert gpu.n_records == len(recs), f"{label}: {gpu.n_records} records vs oracle {len(recs)}"
     g = gpu.records.view(np.uint8).reshape(-1, 64)
@@ -40,20 +43,27 @@ def _assert_same(gpu, ora, label):
         i = int(bad[0])
         raise AssertionError(f"{label}: {len(bad)} records differ; first #{i}: gpu {record_to_dict(gpu.records[i])}"
                              f" oracle {record_to_dict(recs[i])}")
-    assert np.array_equal(gpu.match, match), f"{label}: match slots differ"
     assert np.array_equal(gpu.rec_begin, rb), f"{label}: rec_begin differs"
+    if rx is not None and tg is not None:
+        g_off, g_ent = rx.expand_targets(gpu.target)
+        o_off, o_ent = tg
+        assert np.array_equal(g_off, o_off), f"{label}: target counts differ at {np.nonzero(g_off != o_off)[0][:10]}"
+        assert g_ent.tobytes() == o_ent.tobytes(), f"{label}: target readers differ"
 
 
 def _parity(rx, arena, off, ln, label, own=None, table=None):
     if table is not None:
-        rx.set_match_table(table)
+        if isinstance(table, rtps_records.Readers):
+            rx.set_readers(table)
+        else:
+            rx.set_match_table(table)
     try:
         gpu = rx.handle_received_batch(arena, off, ln)
         ora = oracle.parse(arena, off, ln, own=own or oracle.OWN_PREFIX, match_table=table, threads=8)
+        _assert_same(gpu, ora, label, rx)
     finally:
         if table is not None:
             rx.set_match_table([])
-    _assert_same(gpu, ora, label)
     return gpu
 
 
@@ -131,10 +141,51 @@ def test_match_table(rx):
     # matched writers: 10 of the 16 generated writers, slot = writer index; plus duplicates (first wins)
     st, recs, _, _ = oracle.parse(arena, off, ln)
     guids = sorted({bytes(r["prefix"]) + bytes(r["writer_id"]) for r in recs if r["kind"] == DATA})
+    # compatibility form; guids[0] also goes to a second reader (slot 99): one writer, two readers
     entries = [(g, i % 7) for i, g in enumerate(guids[:40])] + [(guids[0], 99)]
     table = rtps_rx.pack_match_table(entries)
     gpu = _parity(rx, arena, off, ln, "match", table=table)
-    assert (gpu.match != 0xFFFF).sum() > 0
+    assert (gpu.target != NO_TARGET).sum() > 0
+
+
+def _c3_reader_sets(recs):
+    """Readers for C3 traffic (a15): two readers on the same writers, a stateless reader
+    with proxies, a BestEffort reader matched to writers of a foreign prefix (its
+    records are targeted by entity id only), readers listed out of EntityId order."""
+    from rtps_rx.records import READER_STATELESS, READER_BEST_EFFORT
+    guids = sorted({bytes(r["prefix"]) + bytes(r["writer_id"]) for r in recs if r["kind"] == DATA})
+    readers = [(bytes([0, 0, 5, 0x07]), 3, 0), (bytes([0, 0, 1, 0x07]), 1, 0),
+               (bytes([0, 0, 2, 0x04]), 2, READER_STATELESS), (bytes([0, 0, 4, 0x07]), 4, READER_BEST_EFFORT)]
+    foreign = sorted({bytes([0x55] * 12) + g[12:] for g in guids[10:]})
+    proxies = [(g, 1) for g in guids[::2]] + [(g, 0) for g in guids[:6]] + [(g, 2) for g in guids[6:10]] + \
+              [(g, 3) for g in foreign]
+    return rtps_records.Readers(readers, proxies)
+
+
+def test_reader_sets(rx):
+    """a15 (dp_event_loop.rs:266-327, reader.rs:474-484, 712-739): one writer to several
+    readers, stateless readers never targeted, writers known by entity id only, builtin-
+    and vendor-kind writers: every record's target readers == the oracle's scan."""
+    import ingest_ref as R
+    A, O, L = oracle.pack(R.a15_stream(6000, 3), align=1)
+    gpu = _parity(rx, A, O, L, "a15 stream", table=R.a15_readers())
+    assert (gpu.target != NO_TARGET).sum() > 1000
+    arena, off, ln = oracle.gen(oracle.WL_C3, 30000)
+    _, recs, _, _ = oracle.parse(arena, off, ln)
+    _parity(rx, arena, off, ln, "C3 reader sets", table=_c3_reader_sets(recs))
+
+
+@pytest.mark.parametrize("hint", [1, 0])
+def test_reader_sets_full_size_c3(rx, hint):
+    """1M C3 datagrams with the multi-reader table, speculative and chained launches."""
+    n = 1 << 20
+    arena, off, ln = _device_gen(rx, 3, n)
+    _, recs, _, _ = oracle.parse(arena[:4 << 20], off[:2000], ln[:2000])
+    rx.set_spec_hint(hint)
+    try:
+        _parity(rx, arena, off, ln, f"C3-1M reader sets hint {hint}", table=_c3_reader_sets(recs))
+    finally:
+        rx.set_spec_hint(1)
 
 
 def test_misaligned_packing(rx):
@@ -396,21 +447,39 @@ def test_bucket_descriptors_matches_reference(rx, world):
         rx.set_match_table([])
 
 
-@pytest.mark.parametrize("mode", ["", "padded", "desc"])
+@pytest.mark.parametrize("mode", ["", "padded", "desc", "padded c5"])
 def test_sharded_path_two_ranks_gloo(mode):
     """Full N=2 path (device parse + device bucket + all-to-all) on one GPU with gloo;
-    "padded" = fixed-capacity buckets with the equal-split exchange."""
+    "padded" = fixed-capacity buckets with the equal-split exchange; "c5" = the ranks'
+    chunks at C5's generator indices (rank * 8M): every owner's received record
+    multiset equals the oracle's."""
+    _shard_check(2, "gloo", mode.split())
+
+
+def test_rccl_exchange_one_rank():
+    """The library's own RCCL exchange (rtps_rx_exchange, what a Rust host binds) on the
+    box's one GPU: a one-rank communicator sends every bucket to itself."""
+    out = _shard_check(1, "nccl", ["padded", "c5"])
+    assert "library RCCL exchange" in out
+
+
+def _shard_check(nproc, backend, args):
     import os
+    import socket
     import subprocess
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-                        "--master-addr=127.0.0.1", "--master-port=29517",
-                        os.path.join(repo, "scripts", "shard_check.py"), "gloo"] + ([mode] if mode else []),
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+                        "--master-addr=127.0.0.1", f"--master-port={port}",
+                        os.path.join(repo, "scripts", "shard_check.py"), backend] + args,
                        capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
-    assert r.stdout.count(" OK") == 2
+    assert r.stdout.count(" OK") == nproc, r.stdout
+    return r.stdout
 
 
 @pytest.mark.parametrize("wl", [1, 3])
@@ -423,7 +492,7 @@ def test_zero_copy_host_memory(rx, wl):
     cap = max_records(ln)
     outs = {"status": torch.empty(len(ln), dtype=torch.uint8).pin_memory(),
             "records": torch.empty((cap, 64), dtype=torch.uint8).pin_memory(),
-            "match": torch.empty(cap, dtype=torch.int16).pin_memory(),
+            "target": torch.empty(cap, dtype=torch.int32).pin_memory(),
             "rec_begin": torch.empty(len(ln), dtype=torch.int32).pin_memory(),
             "n_records": torch.zeros(1, dtype=torch.int64).pin_memory(), "max_records": cap}
     rx.parse_batch_device(A, O, L, len(ln), outs)

@@ -1,16 +1,18 @@
 """GPU parity of the history-cache ingest (rtps_rx_ingest) with the CPU
-oracle's sequential writer-proxy restatement: every accept flag, the accepted
-record list and every writer's all_ackable_before, batch after batch (state
-carried in the context), on random reliable / best-effort corpora, completed
-DataFrag samples, the C3 and T workloads at full size, and the edges (window
-overflow, empty batches, reset, a growing match table)."""
+oracle's sequential writer-proxy restatement: every per-record accept count,
+the delivery list (record, reader slot) and every proxy's all_ackable_before,
+batch after batch (state carried in the context), on random reliable /
+best-effort corpora, reader sets (several readers per writer, stateless /
+BestEffort / participant readers, writers known by entity id only),
+completed DataFrag samples, the C3 and T workloads at full size, and the
+edges (window overflow, empty batches, reset, a growing table)."""
 import numpy as np
 import pytest
 
 import frag_ref
 import ingest_ref as R
 import oracle
-from rtps_rx.records import pack_match_table, DATA_FRAG
+from rtps_rx.records import pack_match_table, DATA_FRAG, Readers, DELIVERY_DTYPE
 
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
@@ -24,19 +26,38 @@ def rx():
     r.close()
 
 
+def _n_proxies(tbl):
+    return tbl.n_proxies if isinstance(tbl, Readers) else len(Readers.from_match(tbl).proxies)
+
+
 def _batch(rx, ing, tbl, dgrams, label, frag=False, fa=None, best_effort=False, align=4):
     arena, off, ln = oracle.pack(dgrams, align=align)
-    res, acc, accepted, ack, ovf, samples = rx.ingest_batch(arena, off, ln, len(tbl), frag=frag,
+    res, acc, accepted, ack, ovf, samples = rx.ingest_batch(arena, off, ln, _n_proxies(tbl), frag=frag,
                                                             best_effort=best_effort)
     st, recs, _, _ = oracle.parse(arena, off, ln, match_table=tbl, threads=8)
     assert res.records.tobytes() == recs.tobytes(), f"{label}: parse differs"
     o_samples = fa.batch(arena, off, recs)[0] if frag else None
     o_acc, o_accepted, o_ack = ing.batch(arena, off, recs, o_samples, best_effort=best_effort)
     assert np.array_equal(acc, o_acc), f"{label}: accept flags differ at {np.nonzero(acc != o_acc)[0][:10]}"
-    assert np.array_equal(accepted, o_accepted), f"{label}: accepted list"
+    assert accepted.tobytes() == o_accepted.tobytes(), f"{label}: deliveries"
     assert np.array_equal(ack, o_ack), f"{label}: ack_base {ack[ack != o_ack][:5]} vs {o_ack[ack != o_ack][:5]}"
     assert ovf == 0
     return acc, accepted, ack
+
+
+@pytest.mark.parametrize("seed", [5, 6])
+@pytest.mark.parametrize("best_effort", [False, True])
+def test_reader_sets_across_batches(rx, seed, best_effort):
+    """a15: several target readers per record (expanded events), per-proxy state."""
+    rd = R.a15_readers()
+    rx.set_readers(rd)
+    ing = oracle.HistoryIngest(rd)
+    dgrams = R.a15_stream(6000, seed)
+    multi = 0
+    for a, b in [(0, 1), (1, 2500), (2500, 2501), (2501, 6000)]:
+        acc, dels, _ = _batch(rx, ing, rd, dgrams[a:b], f"a15 seed {seed} {a}:{b}", best_effort=best_effort)
+        multi += int((acc > 1).sum())
+    assert multi > 0
 
 
 @pytest.mark.parametrize("seed", [1, 2, 3])
@@ -86,7 +107,7 @@ def test_window_overflow_counted(rx):
     d = [R.datagram(R.PREFIXES[0], [R.data_sub(w, 1), R.data_sub(w, far), R.data_sub(w, 2)])]
     arena, off, ln = oracle.pack(d)
     _, acc, accepted, ack, ovf, _ = rx.ingest_batch(arena, off, ln, 1)
-    assert accepted.tolist() == [0, 1, 2] and ovf == 1 and ack.tolist() == [3]
+    assert accepted["rec_idx"].tolist() == [0, 1, 2] and ovf == 1 and ack.tolist() == [3]
 
 
 def test_empty_and_eventless_batches(rx):
@@ -104,27 +125,16 @@ def test_reset_and_growing_table(rx):
     ing = oracle.HistoryIngest(tbl)
     dgrams = R.stream(3000, 21)
     _batch(rx, ing, tbl, dgrams[:1000], "small table")
-    # append writers: existing entries keep their proxies (oracle: same, by entry position)
+    # append entries: existing proxies keep their state by position on both sides
     big, _ = R.table(n_prefix=4, n_writer=3)
     order = [bytes(g) for g in tbl["writer_guid"]]
     extra = [e for e in big if bytes(e["writer_guid"]) not in order]
     tbl2 = np.concatenate([tbl, np.array(extra, dtype=tbl.dtype)])
     rx.set_match_table(tbl2)
-    ing2 = oracle.HistoryIngest(tbl2)
-    ing2_warm = _replay(ing2, tbl2, dgrams[:1000])
-    _batch(rx, ing2_warm, tbl2, dgrams[1000:3000], "grown table")
+    ing.set_readers(tbl2)
+    _batch(rx, ing, tbl2, dgrams[1000:3000], "grown table")
     rx.ingest_reset()
     _batch(rx, oracle.HistoryIngest(tbl2), tbl2, dgrams[:1000], "after reset")
-
-
-def _replay(ing, tbl, dgrams):
-    """oracle state equivalent to the device's after `dgrams` were ingested with the first table:
-    the entries present then got the same events (later entries were unmatched: no events)."""
-    arena, off, ln = oracle.pack(dgrams, align=4)
-    first = tbl[:len(R.table(n_prefix=2, n_writer=2)[0])]
-    _, recs, _, _ = oracle.parse(arena, off, ln, match_table=first)
-    ing.batch(arena, off, recs)
-    return ing
 
 
 def _device_batch(rx, wl, n):
@@ -139,8 +149,9 @@ def _device_batch(rx, wl, n):
     return arena, off_t, ln_t, off, ln
 
 
-@pytest.mark.parametrize("wl,n", [(3, 20000), (3, 1 << 20), (1, 1 << 20)])
-def test_workload_parity(rx, wl, n):
+@pytest.mark.parametrize("wl,n,multi", [(3, 20000, False), (3, 1 << 20, False), (1, 1 << 20, False),
+                                         (3, 1 << 20, True)])
+def test_workload_parity(rx, wl, n, multi):
     import rtps_rx
     arena, off_t, ln_t, off, ln = _device_batch(rx, wl, n)
     host = arena.cpu().numpy()
@@ -148,6 +159,9 @@ def test_workload_parity(rx, wl, n):
     wk = np.isin(recs0["kind"], (0x15, 0x07, 0x08))
     guids = sorted({bytes(r["prefix"]) + bytes(r["writer_id"]) for r in recs0[wk]})
     tbl = pack_match_table([(g, i) for i, g in enumerate(guids)])
+    if multi:  # every writer to reader 100, even writers to reader 101 too, odd ones to 102 (a15)
+        tbl = pack_match_table([(g, 100) for g in guids] + [(g, 101) for g in guids[::2]] +
+                               [(g, 102) for g in guids[1::2]])
     rx.set_match_table(tbl)
     cap = rtps_rx.max_records(ln)
     outs = rx.alloc_outputs(n, cap)
@@ -164,10 +178,13 @@ def test_workload_parity(rx, wl, n):
         acc = iouts["accept"][:m].cpu().numpy()
         na = int(iouts["n_accepted"].item())
         assert np.array_equal(acc, o_acc), f"wl {wl} rep {rep}: accept"
-        assert np.array_equal(iouts["accepted"][:na].cpu().numpy().view(np.uint32), o_accepted)
+        got = iouts["accepted"][:na].cpu().numpy().reshape(-1).view(DELIVERY_DTYPE)
+        assert got.tobytes() == o_accepted.tobytes()
         assert np.array_equal(iouts["ack_base"][:len(tbl)].cpu().numpy(), o_ack)
         assert int(iouts["n_window_overflow"].item()) == 0
         if rep == 1:
             assert na == 0
         elif wl == 1:
             assert na == n
+        elif multi:
+            assert int((acc > 1).sum()) > 10000

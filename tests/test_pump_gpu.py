@@ -3,8 +3,8 @@ loopback are received into a pinned arena, parsed in place, ingested into the
 history cache and CDR-decoded, batch by batch, with two batches in flight.
 Every batch is checked inside its callback (while its slots still hold the
 datagrams) against the CPU oracle run on the same slots: status, records,
-match slots, accept flags (the oracle's writer proxies carried across the same
-batch split) and decoded rows.  Edges: batches cut by the record capacity,
+target readers, accept counts and deliveries (the oracle's writer proxies
+carried across the same batch split) and decoded rows.  Edges: batches cut by the record capacity,
 stop_after, an idle link, a callback that stops the loop."""
 import threading
 import time
@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 
 import oracle
-from rtps_rx.records import pack_match_table, DATA
+from rtps_rx.records import pack_match_table, DATA, DELIVERY_DTYPE
 
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
@@ -44,8 +44,8 @@ def _hello_type():
 class _Checker:
     """on_batch: compare one batch with the oracle on the same arena slots."""
 
-    def __init__(self, host, tbl, sample_type=None, ingest=True):
-        self.host, self.tbl, self.t = host, tbl, sample_type
+    def __init__(self, host, tbl, sample_type=None, ingest=True, rx=None):
+        self.host, self.tbl, self.t, self.rx = host, tbl, sample_type, rx
         self.ing = oracle.HistoryIngest(tbl) if ingest else None
         self.got = []
         self.batches = 0
@@ -57,16 +57,19 @@ class _Checker:
         n = b.n_datagrams
         off, ln = b.off, b.len
         self.got += [self.host[int(x):int(x) + int(y)].tobytes() for x, y in zip(off, ln)]
-        st, recs, match, _ = oracle.parse(self.host, off, ln, match_table=self.tbl)
+        st, recs, (t_off, t_ent), _ = oracle.parse(self.host, off, ln, match_table=self.tbl)
         m = b.n_records
         assert m == len(recs), f"batch {b.seq}: {m} records, oracle {len(recs)}"
         assert np.array_equal(b.outs["status"][:n].cpu().numpy(), st), f"batch {b.seq}: status"
         assert b.outs["records"][:m].cpu().numpy().tobytes() == recs.tobytes(), f"batch {b.seq}: records"
-        assert np.array_equal(b.outs["match"][:m].cpu().numpy().view(np.uint16), match), f"batch {b.seq}: match"
+        g_off, g_ent = self.rx.expand_targets(b.outs["target"][:m].cpu().numpy().view(np.uint32))
+        assert np.array_equal(g_off, t_off) and g_ent.tobytes() == t_ent.tobytes(), f"batch {b.seq}: targets"
         if self.ing is not None:
             o_acc, o_accepted, _ = self.ing.batch(self.host, off, recs)
             assert np.array_equal(b.iouts["accept"][:m].cpu().numpy(), o_acc), f"batch {b.seq}: accept"
             assert b.n_accepted == len(o_accepted)
+            got = b.iouts["accepted"][:b.n_accepted].cpu().numpy().reshape(-1).view(DELIVERY_DTYPE)
+            assert got.tobytes() == o_accepted.tobytes(), f"batch {b.seq}: deliveries"
             self.accepted += b.n_accepted
         if self.t is not None:
             o_rows, o_status = oracle.cdr_decode(self.t, self.host, off, recs)
@@ -106,7 +109,7 @@ def test_pump_c3_ingest_decode(cut):
     # cut: a record capacity of 3000 cuts most batches (C3 bounds are up to 370 per datagram)
     pump = udp.Pump(rx, rxu, max_batch=4096, ingest=True, sample_type=t, max_recs=3000 if cut else None,
                     n_entries=len(tbl))
-    chk = _Checker(arena.numpy(), tbl, t)
+    chk = _Checker(arena.numpy(), tbl, t, rx=rx)
     th = _sender(rxu, pump.stats, sent)
     stats = pump.run(wait_ms=5, stop_after=len(sent), idle_stop_ms=10000, on_batch=chk)
     th.join()
@@ -128,7 +131,7 @@ def test_pump_hello_world_all_accepted_and_decoded():
     tbl = pack_match_table([(bench.HELLO_PREFIX + bench.HELLO_WRITER, 0)])
     rx.set_match_table(tbl)
     pump = udp.Pump(rx, rxu, max_batch=4096, ingest=True, sample_type=_hello_type(), n_entries=1)
-    chk = _Checker(arena.numpy(), tbl, _hello_type())
+    chk = _Checker(arena.numpy(), tbl, _hello_type(), rx=rx)
     th = _sender(rxu, pump.stats, sent, burst=512, window=2048)
     stats = pump.run(wait_ms=5, stop_after=len(sent), idle_stop_ms=10000, on_batch=chk)
     th.join()
@@ -154,7 +157,7 @@ def test_pump_idle_and_callback_stop():
     stats = pump.run(wait_ms=50, idle_stop_ms=2000, on_batch=lambda b: seen.append(b.n_datagrams) or True)
     assert 1 <= len(seen) <= 2 and stats.completed == stats.datagrams == sum(seen) < len(sent)
     # the rest is still there for the next run, in order
-    chk = _Checker(arena.numpy(), tbl, ingest=False)
+    chk = _Checker(arena.numpy(), tbl, ingest=False, rx=rx)
     stats2 = pump.run(wait_ms=20, idle_stop_ms=300, on_batch=chk)
     assert stats.datagrams + stats2.datagrams == len(sent)
     assert chk.got == sent[stats.datagrams:]

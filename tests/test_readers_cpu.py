@@ -1,0 +1,105 @@
+"""CPU checks of the reader-set contract (a15, no GPU needed): the target sets the
+library's host builder makes (rtps_rx_debug_target_sets, the code behind
+rtps_rx_set_readers) against the oracle's literal available_readers scan
+(dp_event_loop.rs:266-327, reader.rs:474-484, 712-739), their numbering, and the
+validation errors."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import ingest_ref as R
+import oracle
+from rtps_rx.records import (RECORD_DTYPE, TARGET_DTYPE, DATA, Readers, READER_STATELESS, NO_PROXY)
+
+
+def _build(rd):
+    import rtps_rx
+    L = rtps_rx.lib()
+    fn = L.rtps_rx_debug_target_sets
+    fn.restype = ctypes.c_int
+    P, U32 = ctypes.c_void_p, ctypes.c_uint32
+    fn.argtypes = [P, U32, P, U32, P, U32, P, U32, ctypes.POINTER(U32), ctypes.POINTER(U32)]
+    cap = 4096
+    first = np.zeros(cap + 1, dtype=np.uint32)
+    ent = np.zeros(cap, dtype=TARGET_DTYPE)
+    ns, nw = U32(), U32()
+    r, p = rd.readers, rd.proxies
+    rc = fn(r.ctypes.data if len(r) else None, len(r), p.ctypes.data if len(p) else None, len(p),
+            first.ctypes.data, cap, ent.ctypes.data, cap, ctypes.byref(ns), ctypes.byref(nw))
+    if rc:
+        return rc, None, None, 0
+    return 0, first[:ns.value + 1], ent[:first[ns.value]], nw.value
+
+
+def _fake_records(guids):
+    recs = np.zeros(len(guids), dtype=RECORD_DTYPE)
+    for i, g in enumerate(guids):
+        recs[i]["kind"] = DATA
+        recs[i]["prefix"] = np.frombuffer(g[:12], dtype=np.uint8)
+        recs[i]["writer_id"] = np.frombuffer(g[12:], dtype=np.uint8)
+    return recs
+
+
+def _check_sets(rd):
+    rc, first, ent, nw = _build(rd)
+    assert rc == 0
+    # writer sets: distinct GUIDs of non-stateless readers' proxies, first-appearance order
+    wg = []
+    for p in rd.proxies:
+        if rd.readers[int(p["reader"])]["flags"] & READER_STATELESS:
+            continue
+        g = bytes(p["writer_guid"])
+        if g not in wg:
+            wg.append(g)
+    eids = []
+    for g in wg:
+        if g[12:] not in eids:
+            eids.append(g[12:])
+    assert nw == len(wg) and len(first) - 1 == len(wg) + len(eids)
+    unknown = bytes([0xEE] * 12)  # a prefix no proxy has: entity-only targeting
+    o_off, o_ent = oracle.targets(_fake_records(wg + [unknown + e for e in eids]), rd)
+    for s in range(len(first) - 1):
+        got = ent[first[s]:first[s + 1]]
+        exp = o_ent[int(o_off[s]):int(o_off[s + 1])]
+        assert got.tobytes() == exp.tobytes(), s
+        if s >= nw:
+            assert (got["proxy"] == NO_PROXY).all()
+    return first, ent
+
+
+def test_a15_sets_match_oracle_scan():
+    first, ent = _check_sets(R.a15_readers())
+    assert np.max(np.diff(first)) >= 3  # writer 0: readers 10, 11 and the participant reader
+
+
+def test_compat_table_sets_match_oracle_scan():
+    tbl, _ = R.table()
+    _check_sets(Readers.from_match(tbl))
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_random_tables_match_oracle_scan(seed):
+    rng = np.random.default_rng(seed)
+    nr = int(rng.integers(1, 9))
+    eids = rng.choice(200, size=nr, replace=False)
+    readers = [(bytes([0, int(e) // 16, int(e) % 16, 0x07]), 100 + k, int(rng.integers(0, 4)) & 3)
+               for k, e in enumerate(eids)]
+    proxies, seen = [], set()
+    for _ in range(int(rng.integers(0, 40))):
+        g = R.PREFIXES[int(rng.integers(4))] + R.writer_key(int(rng.integers(5)))
+        r = int(rng.integers(nr))
+        if (g, r) not in seen:
+            seen.add((g, r))
+            proxies.append((g, r))
+    _check_sets(Readers(readers, proxies))
+
+
+def test_validation_errors():
+    P = R.PREFIXES
+    dup_reader = Readers([(b"\0\0\1\7", 1, 0), (b"\0\0\1\7", 2, 0)], [])
+    dup_proxy = Readers([(b"\0\0\1\7", 1, 0)], [(P[0] + R.writer_key(0), 0)] * 2)
+    bad_index = Readers([(b"\0\0\1\7", 1, 0)], [(P[0] + R.writer_key(0), 1)])
+    for rd in (dup_reader, dup_proxy, bad_index):
+        assert _build(rd)[0] == -1  # RTPS_RX_EINVAL
+    assert _build(Readers())[0] == 0

@@ -48,7 +48,7 @@ def test_loopback_zero_copy_parse(force_recvmmsg):
     guids = sorted({bytes(r["prefix"]) + bytes(r["writer_id"]) for r in recs[wk]})
     tbl = pack_match_table([(g, i) for i, g in enumerate(guids)])
     rx.set_match_table(tbl)
-    st, recs, match, rb = oracle.parse(host, off, ln, match_table=tbl, threads=8)
+    st, recs, (t_off, t_ent), rb = oracle.parse(host, off, ln, match_table=tbl, threads=8)
     # offsets / lengths in pinned memory too: the whole input is read over PCIe in place
     off_t = torch.from_numpy(off.view(np.int64)).pin_memory()
     ln_t = torch.from_numpy(ln.view(np.int32)).pin_memory()
@@ -62,7 +62,8 @@ def test_loopback_zero_copy_parse(force_recvmmsg):
     assert m == len(recs)
     assert np.array_equal(outs["status"][:n].cpu().numpy(), st)
     assert outs["records"][:m].cpu().numpy().tobytes() == recs.tobytes()
-    assert np.array_equal(outs["match"][:m].cpu().numpy().view(np.uint16), match)
+    g_off, g_ent = rx.expand_targets(outs["target"][:m].cpu().numpy().view(np.uint32))
+    assert np.array_equal(g_off, t_off) and g_ent.tobytes() == t_ent.tobytes()
     ing = oracle.HistoryIngest(tbl)
     o_acc, o_accepted, o_ack = ing.batch(host, off, recs)
     assert np.array_equal(iouts["accept"][:m].cpu().numpy(), o_acc)
