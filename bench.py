@@ -109,7 +109,7 @@ def time_dominant_kernel(rx, arena, off_t, ln_t, n, outs, stream, steps):
     for _ in range(2):  # full launches restore the per-launch bookkeeping
         rx.parse_batch_device(arena, off_t, ln_t, n, outs)
     torch.cuda.synchronize()
-    return ms, {1: "rtps_parse_spec_kernel", 2: "rtps_parse_chain_kernel"}[which]
+    return ms, {1: "rtps_parse_spec_kernel", 2: "rtps_parse_chain_kernel", 3: "rtps_parse_lds_kernel"}[which]
 
 
 def time_ceilings(arena, off_t, ln_t, n, stream, steps):
@@ -203,7 +203,8 @@ def roofline(rx, args, arena, off_t, ln_t, n, outs, stream, total_bytes, alg_rea
     8 TB/s.  Writes (the 64-B records) are reported beside it, not in the numerator."""
     ms, kname = time_dominant_kernel(rx, arena, off_t, ln_t, n, outs, stream, args.steps)
     pmc = pmc_profile(args.workload)
-    key = "parse_spec" if kname == "rtps_parse_spec_kernel" else "parse_chain"
+    key = {"rtps_parse_spec_kernel": "parse_spec", "rtps_parse_chain_kernel": "parse_chain",
+           "rtps_parse_lds_kernel": "parse_lds"}[kname]
     k = (pmc or {}).get(key) or {}
     scale = (pmc or {}).get("fetch_scale") or 1.0
     if pmc and pmc.get("datagrams_per_launch") == n and "FETCH_SIZE" in k:

@@ -108,6 +108,16 @@ enum rtps_payload_kind {
   RTPS_PK_ERR_SHORT = 0x83       /* payload shorter than the 4-byte encapsulation header */
 };
 
+/* ---- rtps_record.u.data.change_kind: the sample's ChangeKind
+ * (Reader::deduce_change_kind, reader.rs:1158-1182, for key / key-hash payload
+ * kinds; Data -> Alive, ddsdata.rs:45-50) */
+enum rtps_change_kind {
+  RTPS_CK_ALIVE = 0,
+  RTPS_CK_NOT_ALIVE_DISPOSED = 1,
+  RTPS_CK_NOT_ALIVE_UNREGISTERED = 2,
+  RTPS_CK_NONE = 0xFF         /* payload_kind is not a sample (RTPS_PK_ERR_*)       */
+};
+
 /* ---- one parsed submessage (64 bytes) ----------------------------------- */
 typedef struct rtps_record {
   uint32_t dgram_idx;   /*  0 index of the datagram in the batch                   */
@@ -128,7 +138,8 @@ typedef struct rtps_record {
                               HEARTBEAT: firstSN; GAP: gapStart; ACKNACK: readerSNState.base */
   union {               /* 40 kind-specific (16 bytes)                             */
     struct { uint16_t pl_off, pl_len; uint8_t rep_id[2], rep_opts[2];
-             uint16_t key_hash_off, status_info_off, rsi_off, _r; } data;
+             uint16_t key_hash_off, status_info_off, rsi_off;
+             uint8_t change_kind, _r; } data;   /* change_kind: rtps_change_kind */
     struct { uint16_t pl_off, pl_len; uint32_t frag_start;
              uint16_t frags_in_sub, frag_size; uint32_t data_size; } frag;
     struct { int64_t last_sn; int32_t count; uint32_t _r; } hb;
@@ -449,6 +460,16 @@ int rtps_rx_frag_assemble(rtps_rx_ctx* ctx, const uint8_t* arena, uint64_t arena
                           const rtps_frag_out* out);
 /* Drop every incomplete buffer and the writer fragment sizes (a new reader). */
 int rtps_rx_frag_reset(rtps_rx_ctx* ctx);
+/* Assembly-buffer expiry (FragmentAssembler::garbage_collect_before,
+ * fragment_assembler.rs:216-224, called by the reader with now - expiry,
+ * reader.rs:1338-1340).  set_clock: the time (ns; any monotonic u64 clock) the
+ * next batches stamp on every buffer they create or extend (AssemblyBuffer::
+ * modified_time :54-61, :139).  gc: drop the incomplete buffers last modified
+ * before expire_before_ns (asynchronous); *n_pending (device u64) = the buffers
+ * left.  A dropped (writer, SN) that receives fragments later starts a new
+ * buffer, as in the reference. */
+int rtps_rx_frag_set_clock(rtps_rx_ctx* ctx, uint64_t now_ns);
+int rtps_rx_frag_gc(rtps_rx_ctx* ctx, uint64_t expire_before_ns, uint64_t* n_pending);
 
 /* ---- history-cache ingest ---------------------------
  * Replaces, for every target reader of every routed writer submessage, the

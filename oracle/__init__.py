@@ -53,6 +53,10 @@ def lib():
         L.rtps_oracle_frag_free.argtypes = [P]
         L.rtps_oracle_frag_pending.restype = ctypes.c_uint64
         L.rtps_oracle_frag_pending.argtypes = [P]
+        L.rtps_oracle_frag_set_clock.restype = None
+        L.rtps_oracle_frag_set_clock.argtypes = [P, ctypes.c_uint64]
+        L.rtps_oracle_frag_gc.restype = ctypes.c_uint64
+        L.rtps_oracle_frag_gc.argtypes = [P, ctypes.c_uint64]
         L.rtps_oracle_frag_batch.restype = ctypes.c_uint64
         L.rtps_oracle_frag_batch.argtypes = [P, P, P, P, ctypes.c_uint64, P, ctypes.c_uint64, P, ctypes.c_uint64, P]
         L.rtps_oracle_ingest_new.restype = P
@@ -175,6 +179,14 @@ class FragAssembler:
 
     def pending(self):
         return int(lib().rtps_oracle_frag_pending(self.h))
+
+    def set_clock(self, now_ns):
+        """The time the next batches stamp on the buffers they create or extend."""
+        lib().rtps_oracle_frag_set_clock(self.h, now_ns)
+
+    def gc(self, expire_before_ns):
+        """garbage_collect_before: drop buffers last modified before expire_before; -> pending left."""
+        return int(lib().rtps_oracle_frag_gc(self.h, expire_before_ns))
 
     def batch(self, arena, offs, recs, max_samples=None, heap_bytes=None):
         """-> (samples FRAG_SAMPLE_DTYPE[n], heap u8[heap_used], n_completed, heap_used)."""

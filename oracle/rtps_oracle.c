@@ -24,6 +24,7 @@
  *   handle_received_packet_2        <- io_uring/rtps/message_receiver.rs:232-287
  *   interpreter (iter_next)         <- io_uring/rtps/message_receiver.rs:56-119, 618-665, 289-295
  *   data_to_dds_data_kind           <- io_uring/rtps/reader.rs:760-833
+ *   deduce_change_kind              <- io_uring/rtps/reader.rs:1158-1182, elements/inline_qos.rs:27-42,139-175
  *   builtin pairs                   <- io_uring/discovery/discovery.rs:2795-2816, 3075-3095
  *   oracle_targets                  <- io_uring/rtps/dp_event_loop.rs:266-327 (available_readers
  *                                      filtered by contains_writer, reader.rs:474-484), matched
@@ -104,6 +105,8 @@ typedef struct submsg {
   int has_qos, has_payload;
   uint32_t qos_len, pl_off, pl_len;
   uint32_t key_hash_off, status_info_off, rsi_off;
+  int si_seen;
+  uint32_t si_len;
   uint32_t frag_start, frags_in_sub, frag_size, data_size;
   /* interpreter */
   uint8_t prefix[12];
@@ -128,7 +131,7 @@ static int parameter_list_read(cursor* c, uint32_t dgram_base, submsg* s) {
     if (c->pos + plen > c->len) return -1; /* reader.read_vec(length) */
     uint32_t value_off = dgram_base + (uint32_t)c->pos;
     if (pid == 0x0070 && !seen_kh) { seen_kh = 1; if (plen == 16) s->key_hash_off = value_off; }
-    if (pid == 0x0071 && !seen_si) { seen_si = 1; s->status_info_off = value_off; }
+    if (pid == 0x0071 && !seen_si) { seen_si = 1; s->status_info_off = value_off; s->si_seen = 1; s->si_len = plen; }
     if ((pid == 0x0083 || pid == 0x800f) && !seen_rsi) { seen_rsi = 1; s->rsi_off = value_off; }
     c->pos += plen;
   }
@@ -470,6 +473,26 @@ static uint8_t data_to_dds_data_kind(const submsg* s) {
   return s->key_hash_off ? RTPS_PK_KEY_HASH : RTPS_PK_ERR_NO_CONTENT;
 }
 
+/* Reader::deduce_change_kind (reader.rs:1158-1182) for the payload kinds that call it:
+ * key (:779-785) and key hash (:787-813); Data is Alive (ddsdata.rs:45-50).
+ * inline_qos None -> NotAliveDisposed.  InlineQos::status_info (inline_qos.rs:27-42):
+ * the first PID_STATUS_INFO, or StatusInfo::empty() (Alive) if there is none;
+ * StatusInfo::read_from reads four u8 (em[3], flags: :139-147), so a value shorter
+ * than 4 bytes is an error -> NotAliveDisposed, and the byte order (rep id from the
+ * E flag, submessage_flag.rs:25-31) never matters.  StatusInfo::change_kind
+ * (:164-175): Disposed (0x1) first, then Unregistered (0x2), else Alive. */
+static uint8_t deduce_change_kind(uint8_t pk, const submsg* s, const uint8_t* m) {
+  if (pk == RTPS_PK_DATA) return RTPS_CK_ALIVE;
+  if (pk != RTPS_PK_KEY && pk != RTPS_PK_KEY_HASH) return RTPS_CK_NONE;
+  if (!s->has_qos) return RTPS_CK_NOT_ALIVE_DISPOSED;
+  if (!s->si_seen) return RTPS_CK_ALIVE;
+  if (s->si_len < 4) return RTPS_CK_NOT_ALIVE_DISPOSED;
+  const uint8_t f = m[s->status_info_off + 3];
+  if (f & 0x1) return RTPS_CK_NOT_ALIVE_DISPOSED;
+  if (f & 0x2) return RTPS_CK_NOT_ALIVE_UNREGISTERED;
+  return RTPS_CK_ALIVE;
+}
+
 /* ------------------------------------------------------------------------ */
 /* one datagram: handle_received_packet_2 + Message::read_from_buffer +      */
 /* the SubmessageIter2 interpreter                                            */
@@ -580,6 +603,7 @@ static uint8_t oracle_datagram(const oracle_cfg* cfg, const uint8_t* m, uint32_t
           rec->u.data.key_hash_off = (uint16_t)s->key_hash_off;
           rec->u.data.status_info_off = (uint16_t)s->status_info_off;
           rec->u.data.rsi_off = (uint16_t)s->rsi_off;
+          rec->u.data.change_kind = deduce_change_kind(rec->payload_kind, s, m);
           break;
         case RTPS_DATA_FRAG:
           rec->aux16 = (uint16_t)s->qos_len;
@@ -914,11 +938,13 @@ typedef struct fa_buf {      /* AssemblyBuffer (:23-33) */
   uint32_t data_size, count, nset;
   uint8_t* bytes;            /* buffer_bytes, zero-initialised (:49-50) */
   uint8_t* bits;             /* received_bitmap */
+  uint64_t modified;         /* modified_time (:31, :61, :139): the batch clock of its last fragment */
   int used;
 } fa_buf;
 typedef struct rtps_oracle_frag {
   fa_writer* w; size_t wcap, wn;
   fa_buf* b; size_t bcap, bn;
+  uint64_t now;              /* the batch clock (Timestamp::now() of the batch's fragments) */
 } rtps_oracle_frag;
 
 static uint64_t fa_hash(const uint8_t* k, size_t n) {
@@ -997,6 +1023,20 @@ void rtps_oracle_frag_free(rtps_oracle_frag* f) {
   free(f->b); free(f->w); free(f);
 }
 uint64_t rtps_oracle_frag_pending(const rtps_oracle_frag* f) { return f->bn; }
+void rtps_oracle_frag_set_clock(rtps_oracle_frag* f, uint64_t now_ns) { f->now = now_ns; }
+/* FragmentAssembler::garbage_collect_before (rtps/fragment_assembler.rs:216-224): drop every
+ * buffer whose modified_time < expire_before.  Returns the buffers left. */
+uint64_t rtps_oracle_frag_gc(rtps_oracle_frag* f, uint64_t expire_before_ns) {
+  for (size_t i = 0; i < f->bcap; ++i)
+    if (f->b[i].used == 1 && f->b[i].modified < expire_before_ns) {
+      free(f->b[i].bytes); free(f->b[i].bits);
+      f->b[i].bytes = NULL; f->b[i].bits = NULL;
+      f->b[i].used = 2;
+      f->bn--;
+    }
+  if (f->bcap) fa_buf_rehash(f, f->bcap);
+  return f->bn;
+}
 
 /* One batch: every RTPS_DATA_FRAG record with ROUTE_PASS, in record order.
  * Returns the number of completed samples (descriptors beyond max_samples and
@@ -1025,6 +1065,7 @@ uint64_t rtps_oracle_frag_batch(rtps_oracle_frag* f, const uint8_t* arena, const
       b->bytes = (uint8_t*)calloc(ds ? ds : 1, 1);
       b->bits = (uint8_t*)calloc(b->count ? b->count : 1, 1);
     }
+    b->modified = f->now;  /* AssemblyBuffer::new (:54-61) / insert_frags (:139) */
     /* insert_frags (:65-140) with frag_size = the assembler's F */
     const uint64_t start0 = (uint64_t)rec->u.frag.frag_start - 1;
     const uint64_t fis = rec->u.frag.frags_in_sub;

@@ -52,7 +52,7 @@ constexpr uint64_t PBYTES = 1ull << 28;  // pending byte store (per side)
 constexpr uint64_t PWORDS = 1ull << 22;  // pending bitmap words (per side)
 
 // counters (device u64)
-enum { C_OLD_N = 0, C_NEW_N, C_NEW_BYTES, C_NEW_WORDS, C_SPECIAL, C_POOL, C_OVERFLOW, C_COUNT };
+enum { C_OLD_N = 0, C_NEW_N, C_NEW_BYTES, C_NEW_WORDS, C_SPECIAL, C_POOL, C_OVERFLOW, C_LIVE, C_COUNT };
 
 enum EpochState : uint32_t { E_PENDING = 0, E_DONE = 1, E_DEAD = 2 };  // DEAD: bitmap allocation failed
 enum EpochFlags : uint32_t { EF_IRREGULAR = 1, EF_SKIP = 2 };  // SKIP: no bytes to write (no room)
@@ -74,9 +74,10 @@ struct Epoch {
 struct Pend {
   uint32_t guid[4];
   int64_t sn;
-  uint32_t data_size, count, nset, consumed;
-  uint64_t bytes;  // offset in the pending byte store
-  uint64_t bits;   // word offset in the pending bitmap store
+  uint32_t data_size, count, nset, consumed;  // consumed: continued by this batch, or expired by gc
+  uint64_t bytes;     // offset in the pending byte store
+  uint64_t bits;      // word offset in the pending bitmap store
+  uint64_t modified;  // clock of the last batch that inserted fragments (AssemblyBuffer::modified_time)
 };
 
 __device__ __forceinline__ void guid_of(const rtps_record* r, uint32_t g[4]) {
@@ -408,10 +409,6 @@ __device__ bool walk_run_regular(const WalkArgs& A, uint64_t p0, uint64_t p1, ui
 // wave steps through them in order with the fragment bitmap in LDS.  Runs that
 // mix keys or need a bigger bitmap fall back to walk_run_serial on lane 0.
 __device__ void walk_run_wave(const WalkArgs& A, uint64_t p0, uint64_t p1, uint32_t lane, uint32_t* bm) {
-#if defined(ABL_WALK) && ABL_WALK == 2
-  if (p1 == 0x7fffffffffffull) A.seen[p0] = 1;
-  return;
-#endif
   const rtps_record* r0 = A.recs + A.svals[p0];
   uint32_t g[4];
   guid_of(r0, g);
@@ -477,9 +474,6 @@ __device__ void walk_run_wave(const WalkArgs& A, uint64_t p0, uint64_t p1, uint3
     }
     uint32_t my_e = NONE;
     uint32_t m = (uint32_t)min<uint64_t>(64, p1 - c);
-#if defined(ABL_WALK) && ABL_WALK == 1
-    m = 0;
-#endif
     for (uint32_t jj = 0; jj < m; ++jj) {
       const uint32_t rj = rl(ri, jj), fsj = rl(fs, jj), fz = rl(fisz, jj), dj = rl(dsz, jj);
       const uint32_t fis = fz & 0xffffu, fsz = fz >> 16;
@@ -601,7 +595,7 @@ __global__ __launch_bounds__(FT) void k_samples(const uint32_t* dmark, Epoch* ep
 
 // pending epochs: room in the new pending store + carry their bitmaps
 __global__ __launch_bounds__(FT) void k_pend_alloc(Epoch* ep, const uint32_t* special, Pend* np, uint32_t* nbits,
-                                                   const uint32_t* pool, uint64_t* ctr) {
+                                                   const uint32_t* pool, uint64_t* ctr, uint64_t now) {
   const uint64_t ns = ctr[C_SPECIAL];
   for (uint64_t i = (uint64_t)blockIdx.x * FT + threadIdx.x; i < ns; i += (uint64_t)gridDim.x * FT) {
     Epoch& E = ep[special[i]];
@@ -619,6 +613,7 @@ __global__ __launch_bounds__(FT) void k_pend_alloc(Epoch* ep, const uint32_t* sp
     for (int k = 0; k < 4; ++k) P.guid[k] = E.guid[k];
     P.sn = E.sn; P.data_size = E.data_size; P.count = E.count; P.nset = E.nset; P.consumed = 0;
     P.bytes = b; P.bits = w;
+    P.modified = now;  // a pending epoch had fragments in this batch (insert_frags :139)
     for (uint64_t t = 0; t < words; ++t) nbits[w + t] = pool[E.bits + t];
     E.new_pend = (uint32_t)j;
     E.dst = b;
@@ -713,9 +708,6 @@ __global__ __launch_bounds__(FT) void k_span(const rtps_record* recs, const uint
           const uint64_t span_end = min<uint64_t>(from + fisF, E.data_size);
           const uint64_t to = min<uint64_t>(from + min<uint64_t>(fisF, r->u.frag.pl_len), E.data_size);
           src = dgram_off[r->dgram_idx] + r->u.frag.pl_off;
-#ifdef ABL_SPAN_ALIGN  // timing only (wrong output): 16-B-aligned source reads
-          src &= ~(uint64_t)15;
-#endif
           dst = (uint64_t)(epoch_dst(E, out, nbytes) + from);
           nv = (uint32_t)(to - from);
           n = (uint32_t)(span_end - from);
@@ -725,10 +717,6 @@ __global__ __launch_bounds__(FT) void k_span(const rtps_record* recs, const uint
     }
     // four records at a time, one per quarter-wave: 16 lanes x 16 B = 256 B per
     // instruction per record, SPAN_U loads in flight per lane before the stores
-#ifdef ABL_SPAN_NOCOPY  // timing only: resolve the records, copy nothing
-    if (live && n == 0xffffffffu) *(uint8_t*)(uintptr_t)dst = (uint8_t)src;
-    continue;
-#endif
     uint64_t todo = __ballot(live);
     const uint32_t q = lane >> 4, ql = lane & 15u;
     while (todo) {
@@ -819,6 +807,32 @@ __global__ __launch_bounds__(FT) void k_ptable(const Pend* np, const uint64_t* c
     while (atomicCAS(&ptable[s], NONE, (uint32_t)j) != NONE) s = (s + 1) & (PTCAP - 1);
   }
 }
+// garbage_collect_before (fragment_assembler.rs:216-224): the carried buffers last
+// modified before `expire` are marked consumed (the next batch neither finds nor
+// carries them) and the lookup table is rebuilt over the live ones
+__global__ __launch_bounds__(FT) void k_gc_mark(Pend* op, uint64_t* ctr, uint64_t expire) {
+  const uint64_t n = min<uint64_t>(ctr[C_OLD_N], PCAP);
+  uint32_t live = 0;
+  for (uint64_t j = (uint64_t)blockIdx.x * FT + threadIdx.x; j < n; j += (uint64_t)gridDim.x * FT) {
+    if (op[j].consumed) continue;
+    if (op[j].modified < expire) op[j].consumed = 1u;
+    else live++;
+  }
+#pragma unroll
+  for (uint32_t d = 32; d >= 1; d >>= 1) live += __shfl_xor(live, d, 64);
+  if ((threadIdx.x & 63u) == 0 && live) atomicAdd((unsigned long long*)&ctr[C_LIVE], (unsigned long long)live);
+}
+__global__ __launch_bounds__(FT) void k_ptable_live(const Pend* op, const uint64_t* ctr, uint32_t* ptable) {
+  const uint64_t n = min<uint64_t>(ctr[C_OLD_N], PCAP);
+  for (uint64_t j = (uint64_t)blockIdx.x * FT + threadIdx.x; j < n; j += (uint64_t)gridDim.x * FT) {
+    if (op[j].consumed) continue;
+    uint32_t g[4] = {op[j].guid[0], op[j].guid[1], op[j].guid[2], op[j].guid[3]};
+    uint32_t s = key_hash(g, op[j].sn) & (PTCAP - 1);
+    while (atomicCAS(&ptable[s], NONE, (uint32_t)j) != NONE) s = (s + 1) & (PTCAP - 1);
+  }
+}
+__global__ void k_gc_finish(const uint64_t* ctr, uint64_t* n_pending) { *n_pending = ctr[C_LIVE]; }
+
 __global__ void k_finish(uint64_t* ctr, uint64_t* n_pending) {
   const uint64_t n = min<uint64_t>(ctr[C_NEW_N], PCAP);
   *n_pending = n | (ctr[C_OVERFLOW] ? (1ull << 63) : 0ull);
@@ -832,6 +846,7 @@ static inline uint64_t hmin(uint64_t a, uint64_t b) { return a < b ? a : b; }
 struct FragState {
   int device = 0;
   int cur = 0;  // pending side holding the previous batch's buffers
+  uint64_t now = 0;  // clock stamped on the buffers the next batches create or extend
   uint64_t* wkey = nullptr;
   uint32_t* wfirst = nullptr;
   uint32_t* wF = nullptr;
@@ -960,7 +975,7 @@ int rtps_frag_assemble(FragState* s, hipStream_t st, const uint8_t* arena, uint6
   hipLaunchKernelGGL(k_samples, dim3(gb), dim3(FT), 0, st, s->dmark, s->epochs, s->cnt, s->rank, s->dsz, s->hoff,
                      max, *out);
   hipLaunchKernelGGL(k_pend_alloc, dim3(64), dim3(FT), 0, st, s->epochs, s->special, s->pend[nw], s->pbits[nw],
-                     s->pool, s->ctr);
+                     s->pool, s->ctr, s->now);
   hipLaunchKernelGGL(k_carry, dim3(1024), dim3(FT), 0, st, s->pend[o], s->pbytes[o], s->pbits[o], s->pend[nw],
                      s->pbytes[nw], s->pbits[nw], s->ctr);
   hipLaunchKernelGGL(k_init, dim3(1024), dim3(FT), 0, st, s->epochs, s->special, s->ctr, s->pend[o], s->pbytes[o],
@@ -977,4 +992,17 @@ int rtps_frag_assemble(FragState* s, hipStream_t st, const uint8_t* arena, uint6
   if (hipGetLastError() != hipSuccess) return RTPS_RX_EHIP;
   s->cur = nw;
   return RTPS_RX_OK;
+}
+
+void rtps_frag_set_clock(FragState* s, uint64_t now) { s->now = now; }
+
+int rtps_frag_gc(FragState* s, hipStream_t st, uint64_t expire_before, uint64_t* n_pending) {
+  const int o = s->cur;
+  if (hipMemsetAsync(s->ctr + C_LIVE, 0, 8, st) != hipSuccess ||
+      hipMemsetAsync(s->ptable[o], 0xff, PTCAP * 4, st) != hipSuccess)
+    return RTPS_RX_EHIP;
+  hipLaunchKernelGGL(k_gc_mark, dim3(PCAP / FT), dim3(FT), 0, st, s->pend[o], s->ctr, expire_before);
+  hipLaunchKernelGGL(k_ptable_live, dim3(PCAP / FT), dim3(FT), 0, st, s->pend[o], s->ctr, s->ptable[o]);
+  hipLaunchKernelGGL(k_gc_finish, dim3(1), dim3(1), 0, st, s->ctr, n_pending);
+  return hipGetLastError() == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP;
 }

@@ -29,6 +29,7 @@
 //     the arena return 0 and never fault).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <mutex>
@@ -73,9 +74,6 @@ struct KParams {
   uint32_t* mixed_out;        // pinned host [2]: tiles of the batch not uniform k_spec, tiles (launch choice)
   uint32_t ch_spin_limit;     // polls before a chained tile leaves itself to kernel B
   uint32_t ch_epoch;          // chained launch number (never 0): tags the look-back words of this launch
-  uint64_t* ch_gc;            // [ch_gmax] group arrival counters of this launch (zero at its start)
-  uint64_t* ch_gc_next;       // [ch_gmax] the next chained launch's counters: zeroed by this one
-  uint32_t ch_gmax;
 };
 
 // ---------------------------------------------------------------------------
@@ -111,6 +109,25 @@ __device__ __forceinline__ uint32_t ld4(const Src& s, uint32_t o) {
   return r;
 }
 
+// The same reads from a datagram staged in LDS (rtps_parse_lds_kernel): w = the
+// tile image as words, base = the datagram's 16-B aligned byte offset in it.
+// Unaligned reads combine two aligned words (v_alignbyte).
+struct LSrc {
+  const uint32_t* w;
+  uint32_t base;
+};
+__device__ __forceinline__ uint32_t ld4(const LSrc& s, uint32_t o) {
+  const uint32_t a = s.base + o, i = a >> 2, sh = a & 3u;
+  const uint32_t lo = s.w[i], hi = s.w[i + 1];
+  return __builtin_amdgcn_alignbyte(hi, lo, sh);
+}
+__device__ __forceinline__ u32x4 ld16(const LSrc& s, uint32_t o) {
+  const uint32_t a = s.base + o, i = a >> 2, sh = a & 3u;
+  const uint32_t w0 = s.w[i], w1 = s.w[i + 1], w2 = s.w[i + 2], w3 = s.w[i + 3], w4 = s.w[i + 4];
+  return u32x4{__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+               __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh)};
+}
+
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 // wire dword -> value in the submessage byte order
 __device__ __forceinline__ uint32_t e32(uint32_t raw, bool le) { return le ? raw : bswap32(raw); }
@@ -129,7 +146,8 @@ __device__ __forceinline__ int64_t sn_of(uint32_t hi_raw, uint32_t lo_raw, bool 
 struct Win {
   uint32_t w[12];
 };
-__device__ __forceinline__ void load_win(const Src& s, uint32_t o, Win& W) {
+template <class S>
+__device__ __forceinline__ void load_win(const S& s, uint32_t o, Win& W) {
   u32x4 a = ld16(s, o), b = ld16(s, o + 16);
   W.w[0] = a[0]; W.w[1] = a[1]; W.w[2] = a[2]; W.w[3] = a[3];
   W.w[4] = b[0]; W.w[5] = b[1]; W.w[6] = b[2]; W.w[7] = b[3];
@@ -148,8 +166,8 @@ __device__ __forceinline__ bool win_needs_tail(uint32_t kind) {
   if (kind == RTPS_DATA_FRAG) return true;
   return kind < 32u && (((WRITE ? write_mask : count_mask) >> kind) & 1u);
 }
-template <bool WRITE>
-__device__ __forceinline__ void load_win_lazy(const Src& s, uint32_t o, Win& W) {
+template <bool WRITE, class S>
+__device__ __forceinline__ void load_win_lazy(const S& s, uint32_t o, Win& W) {
   const u32x4 a = ld16(s, o);
   W.w[0] = a[0]; W.w[1] = a[1]; W.w[2] = a[2]; W.w[3] = a[3];
   const uint32_t kind = a[0] & 0xffu;
@@ -161,7 +179,8 @@ __device__ __forceinline__ void load_win_lazy(const Src& s, uint32_t o, Win& W) 
 }
 // prefetch form: header + body 0..28 (DATA_FRAG's sampleSize dword is fetched
 // when the kind is known)
-__device__ __forceinline__ void load_win_pf(const Src& s, uint32_t o, Win& W) {
+template <class S>
+__device__ __forceinline__ void load_win_pf(const S& s, uint32_t o, Win& W) {
   const u32x4 a = ld16(s, o), b = ld16(s, o + 16);
   W.w[0] = a[0]; W.w[1] = a[1]; W.w[2] = a[2]; W.w[3] = a[3];
   W.w[4] = b[0]; W.w[5] = b[1]; W.w[6] = b[2]; W.w[7] = b[3];
@@ -231,10 +250,15 @@ __device__ __forceinline__ void rec_store(rtps_record* dst, const Rec& r) {
 
 // ParameterList::read_from (elements/parameter_list.rs:79-102) over the body
 // starting at body position pos; records the first KEY_HASH (16-byte value
-// required, dds/key.rs:64-68), STATUS_INFO and RELATED_SAMPLE_IDENTITY values.
+// required, dds/key.rs:64-68), STATUS_INFO and RELATED_SAMPLE_IDENTITY values,
+// and the first STATUS_INFO's flags octet (SI_ABSENT / SI_ERROR: none / shorter
+// than the 4 octets StatusInfo::read_from reads, inline_qos.rs:139-147).
 // Returns false on a read error.
-__device__ __forceinline__ bool param_list(const Src& s, uint32_t body_off, uint32_t blen, bool le,
-                                           uint32_t& pos, uint32_t& kh, uint32_t& si, uint32_t& rsi) {
+constexpr uint32_t SI_ABSENT = 0x100u, SI_ERROR = 0x200u;
+template <class S>
+__device__ __forceinline__ bool param_list(const S& s, uint32_t body_off, uint32_t blen, bool le,
+                                           uint32_t& pos, uint32_t& kh, uint32_t& si, uint32_t& rsi,
+                                           uint32_t& si_flags) {
   bool seen_kh = false, seen_si = false, seen_rsi = false;
   for (;;) {
     if (pos + 4u > blen) return false;
@@ -245,7 +269,11 @@ __device__ __forceinline__ bool param_list(const Src& s, uint32_t body_off, uint
     if (pos + plen > blen) return false;
     uint32_t voff = body_off + pos;
     if (pid == 0x0070u && !seen_kh) { seen_kh = true; if (plen == 16u) kh = voff; }
-    if (pid == 0x0071u && !seen_si) { seen_si = true; si = voff; }
+    if (pid == 0x0071u && !seen_si) {
+      seen_si = true;
+      si = voff;
+      si_flags = plen >= 4u ? (ld4(s, voff) >> 24) : SI_ERROR;  // octets em[3], then the flags
+    }
     if ((pid == 0x0083u || pid == 0x800fu) && !seen_rsi) { seen_rsi = true; rsi = voff; }
     pos += plen;
   }
@@ -265,6 +293,21 @@ __device__ __forceinline__ uint32_t eff_len(uint32_t kind, uint32_t clen, uint32
   return clen != 0u ? clen : ((kind == RTPS_PAD || kind == RTPS_INFO_TS) ? 0u : rem - 4u);
 }
 
+// Reader::deduce_change_kind (reader.rs:1158-1182) for the DATA payload kinds that
+// call it (key: :779-785, key hash: :787-813); Data -> Alive (ddsdata.rs:45-50).
+// No inline QoS -> NotAliveDisposed; inline QoS without STATUS_INFO ->
+// StatusInfo::empty() -> Alive (inline_qos.rs:27-42); a STATUS_INFO shorter than
+// 4 octets fails to deserialise -> NotAliveDisposed; else StatusInfo::change_kind
+// (inline_qos.rs:164-175): Disposed bit, then Unregistered bit, else Alive.  The
+// octet order never matters: StatusInfo reads four u8.
+__device__ __forceinline__ uint32_t change_kind(uint32_t pk, bool q, uint32_t si_flags) {
+  if (pk == RTPS_PK_DATA) return RTPS_CK_ALIVE;
+  if (pk != RTPS_PK_KEY && pk != RTPS_PK_KEY_HASH) return RTPS_CK_NONE;
+  if (!q || si_flags == SI_ERROR) return RTPS_CK_NOT_ALIVE_DISPOSED;
+  if (si_flags == SI_ABSENT) return RTPS_CK_ALIVE;
+  return (si_flags & 1u) ? RTPS_CK_NOT_ALIVE_DISPOSED : (si_flags & 2u) ? RTPS_CK_NOT_ALIVE_UNREGISTERED : RTPS_CK_ALIVE;
+}
+
 // What the body reader of one submessage produced.
 struct SubOut {
   uint32_t cls;  // 0 not materialised, 1 writer kind, 2 reader kind, 3 interpreter kind
@@ -276,8 +319,8 @@ struct SubOut {
 // reference reader rejects; WRITE additionally fills the kind-specific record
 // words R.d[8..13] (and R.d[2..4] / R.d[10..11] for INFO_DST / INFO_SRC /
 // INFO_REPLY).  Returns false on a read error (the datagram is dropped).
-template <bool WRITE>
-__device__ __forceinline__ bool sub_body(const Src& s, const Win& W, uint32_t kind, uint32_t flags, bool le,
+template <bool WRITE, class S>
+__device__ __forceinline__ bool sub_body(const S& s, const Win& W, uint32_t kind, uint32_t flags, bool le,
                                          uint32_t body, uint32_t blen, Rec& R, SubOut& so) {
   so.cls = 0; so.route = 0; so.pk = 0; so.aux16 = blen; so.rid = 0; so.wid = 0;
   switch (kind) {
@@ -289,8 +332,8 @@ __device__ __forceinline__ bool sub_body(const Src& s, const Win& W, uint32_t ki
       if (otq > 16u) { pos = 4u + otq; if (pos > blen) return false; }
       uint32_t fl = flags & 0x1fu;
       bool q = (fl & 0x02u) != 0u, dk = (fl & 0x0cu) != 0u;
-      uint32_t qstart = pos, kh = 0, si = 0, rsi = 0;
-      if (q && !param_list(s, body, blen, le, pos, kh, si, rsi)) return false;
+      uint32_t qstart = pos, kh = 0, si = 0, rsi = 0, si_flags = SI_ABSENT;
+      if (q && !param_list(s, body, blen, le, pos, kh, si, rsi, si_flags)) return false;
       so.cls = 1;
       if (WRITE) {
         so.rid = W.w[2]; so.wid = W.w[3];
@@ -316,7 +359,7 @@ __device__ __forceinline__ bool sub_body(const Src& s, const Win& W, uint32_t ki
         R.d[10] = pl_off | (pl_len << 16);
         R.d[11] = enc;
         R.d[12] = kh | (si << 16);
-        R.d[13] = rsi;
+        R.d[13] = rsi | (change_kind(so.pk, q, si_flags) << 16);
       }
       return true;
     }
@@ -327,8 +370,8 @@ __device__ __forceinline__ bool sub_body(const Src& s, const Win& W, uint32_t ki
       uint32_t pos = 32u;
       if (otq > 28u) { pos = 4u + otq; if (pos > blen) return false; }
       bool q = (flags & 0x02u) != 0u;
-      uint32_t qstart = pos, kh = 0, si = 0, rsi = 0;
-      if (q && !param_list(s, body, blen, le, pos, kh, si, rsi)) return false;
+      uint32_t qstart = pos, kh = 0, si = 0, rsi = 0, si_flags = SI_ABSENT;
+      if (q && !param_list(s, body, blen, le, pos, kh, si, rsi, si_flags)) return false;
       int64_t sn = sn_of(W.w[4], W.w[5], le);
       if (sn < 1) return false;
       uint32_t frag_start = e32(W.w[6], le);
@@ -577,9 +620,6 @@ __device__ uint32_t walk(const KParams& p, const Src& s, const uint32_t* H, uint
           q[3] = u32x4{R.d[12], R.d[13], R.d[14], R.d[15]};
           stage_match[r - stage_first] = mslot;
         } else if (r < p.max_records) {
-#ifdef ABL_NO_REC_STORE
-          if (R.d[0] == 0xdeadbeefu)
-#endif
           rec_store(p.records + r, R);
           if (p.target_out) p.target_out[r] = mslot;
         }
@@ -628,10 +668,11 @@ struct TileCtx {
 
 // load this lane's (offset, length), build the wave's buffer descriptor
 // (base = min offset over the wave: no workgroup barrier) and the 64-byte head
+template <uint32_t TS = TILE>
 __device__ __forceinline__ void load_tile(const KParams& p, uint32_t tile, TileCtx& t, bool enabled = true) {
   const uint32_t tid = threadIdx.x;
-  t.i = tile * TILE + tid;
-  t.valid = enabled && t.i < p.n;
+  t.i = tile * TS + tid;
+  t.valid = enabled && tid < TS && t.i < p.n;
   const uint64_t off = t.valid ? p.dgram_off[t.i] : ~0ull;
   t.L = t.valid ? p.dgram_len[t.i] : 0u;
   uint64_t m = off;
@@ -658,11 +699,7 @@ __device__ __forceinline__ void load_tile(const KParams& p, uint32_t tile, TileC
     // bytes 48..63 serve only the first submessage's window, which a DATA there
     // does not read (its fields and encapsulation end at byte 48): skipping them
     // saves a line fetch wherever they begin a new 128-B line
-#ifdef ABL_HEAD_EAGER
-    d = ld16(t.s, 48);
-#else
     if ((b[1] & 0xffu) != RTPS_DATA) d = ld16(t.s, 48);
-#endif
   }
   t.H[0] = a[0]; t.H[1] = a[1]; t.H[2] = a[2]; t.H[3] = a[3];
   t.H[4] = b[0]; t.H[5] = b[1]; t.H[6] = b[2]; t.H[7] = b[3];
@@ -796,6 +833,8 @@ __device__ __forceinline__ void reduce_info(const uint32_t* info, uint32_t lo, u
 // per 1M datagrams, L2-resident) to find the first non-speculative tile f and
 // the total; workgroup 0 publishes the total.  Tiles f.. are then re-walked in
 // a grid-stride loop, each at its exact prefix.
+// TS: datagrams per tile of the first kernel (256 for A and C, LT for the LDS-tile kernel D)
+template <uint32_t TS>
 __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_fix_kernel(KParams p, uint32_t n_tiles,
                                                                                     uint32_t k_spec, uint32_t parity) {
   __shared__ uint32_t s_wave_sum[WAVES];
@@ -840,11 +879,11 @@ __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_fix_kern
   reduce_info(x.info, 0, tile, s_rsum, s_rmin, prefix, dummy_min);
   for (;;) {
     const uint32_t info = x.info[tile];
-    const uint32_t i = tile * TILE + tid;
+    const uint32_t i = tile * TS + tid;
     // non-speculative tiles stored their per-datagram counts; speculative tiles
     // (after the first non-speculative one) have exactly k_spec per datagram
     uint32_t cnt = 0;
-    if (i < p.n) cnt = (info & INFO_NONSPEC) ? (uint32_t)x.dcount[i] : k_spec;
+    if (tid < TS && i < p.n) cnt = (info & INFO_NONSPEC) ? (uint32_t)x.dcount[i] : k_spec;
     const bool skip = (info & INFO_WRITTEN) != 0;  // written in place by the chained kernel
     const uint32_t incl = wave_incl_scan(cnt, lane);
     if (lane == 63) s_wave_sum[wave] = incl;
@@ -855,17 +894,12 @@ __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_fix_kern
       if (w < wave) wave_off += s_wave_sum[w];
     const uint64_t my_first = prefix + wave_off + (incl - cnt);
     TileCtx t;
-    load_tile(p, tile, t, !skip);
+    load_tile<TS>(p, tile, t, !skip);
     if (t.valid) {
       if (p.rec_begin) p.rec_begin[t.i] = (uint32_t)my_first;
       if (cnt) {  // cnt > 0 implies status OK
         uint32_t n2;
-#ifdef ABL_COUNT_IN_FIX
-        walk<false>(p, t.s, t.H, t.L, t.i, my_first, n2);
-        if (n2 == 12345u) p.status[0] = 9;
-#else
         walk<true>(p, t.s, t.H, t.L, t.i, my_first, n2);
-#endif
       }
     }
     __syncthreads();  // s_wave_sum reuse
@@ -881,18 +915,20 @@ __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_fix_kern
 // One workgroup per tile: count walk, publish the tile's record count, find the
 // tile's exact prefix from the predecessors' published counts, then the
 // writing walk at the exact position while the tile's lines are still in cache.
-// Prefixes are two-level so that a tile needs about two polls, not one per 64
-// predecessors: tiles form groups of 64; the last tile of a group to publish
-// (an arrival counter per group) sums the group and publishes the group total.
-// A tile's prefix = the totals of the earlier groups + the counts of the
-// earlier tiles of its group.  Every exchanged word is an agent-scope 8-byte
-// {epoch, value} word (no fences: a reader polls until the word carries this
-// launch's epoch).  A tile that gives up waiting (a predecessor that never
-// published: only if the dispatcher ran tiles far out of order) stays
-// unwritten and kernel B, launched after it as always, walks it: results never
-// depend on dispatch order or timing.  Nothing is zeroed between launches:
-// words of earlier launches carry older epochs, and the group arrival counters
-// come in two sets, each launch clearing the set the next one uses.
+// Prefixes are three-level so that a tile needs one poll, not one per 64
+// predecessors: tiles form groups of 64, groups supergroups of 64.  The LAST
+// tile of a group sums its group's earlier counts (which it needs for its own
+// prefix anyway) and publishes the group total; the last tile of the last group
+// of a supergroup likewise the supergroup total.  A tile's prefix = the totals
+// of the earlier supergroups + of the earlier groups of its supergroup + the
+// counts of the earlier tiles of its group, the three polled together.  Every
+// exchanged word is an agent-scope 8-byte {epoch, value} word (no fences, no
+// read-modify-write: a reader polls until the word carries this launch's
+// epoch).  A tile that gives up waiting (a predecessor that never published:
+// only if the dispatcher ran tiles far out of order) stays unwritten and kernel
+// B, launched after it as always, walks it: results never depend on dispatch
+// order or timing.  Nothing is zeroed between launches: words of earlier
+// launches carry older epochs.
 // look-back word = epoch << 32 | value; ready when its epoch is this launch's
 __device__ __forceinline__ uint64_t ch_word(uint32_t epoch, uint64_t value) { return (uint64_t)epoch << 32 | value; }
 #ifndef RTPS_CH_GROUP
@@ -902,14 +938,17 @@ __device__ __forceinline__ uint64_t ch_word(uint32_t epoch, uint64_t value) { re
 #define RTPS_CH_SLEEP 32  // s_sleep units (64 clocks) between polls: 2 / 8 / 16 / 32 measured, DESIGN §3.3
 #endif
 constexpr uint32_t CH_GROUP = RTPS_CH_GROUP;  // <= 64: a group's tile words are summed by one wave
-constexpr uint32_t CH_SPIN_LIMIT = 1u << 14;
-__host__ __device__ constexpr size_t chain_words(uint32_t tiles) {  // tile words, group words, (unused) counters
-  return (size_t)tiles + 2 * (((size_t)tiles + CH_GROUP - 1) / CH_GROUP) + 2;
-}
+static_assert(RTPS_CH_GROUP >= 1 && RTPS_CH_GROUP <= 64, "a group's words are summed by one wave of 64 lanes");
+// polls before a tile gives up (about 1 ms whatever the sleep between polls)
+constexpr uint32_t CH_SPIN_LIMIT = (1u << 15) / (RTPS_CH_SLEEP > 0 ? RTPS_CH_SLEEP : 1);
+// Look-back words, three levels: [tiles] tile counts | [groups] group totals |
+// [supers] supergroup totals | 2 spare.
 __host__ __device__ constexpr uint32_t chain_groups(uint32_t tiles) { return (tiles + CH_GROUP - 1) / CH_GROUP; }
-// + 2 spare words, + two sets of group arrival counters (alternating by chained launch)
-__host__ __device__ constexpr size_t chain_alloc_words(uint32_t tiles) {
-  return chain_words(tiles) + 2 + 2 * (size_t)chain_groups(tiles);
+__host__ __device__ constexpr uint32_t chain_supers(uint32_t tiles) {
+  return (chain_groups(tiles) + CH_GROUP - 1) / CH_GROUP;
+}
+__host__ __device__ constexpr size_t chain_words(uint32_t tiles) {
+  return (size_t)tiles + chain_groups(tiles) + chain_supers(tiles) + 2;
 }
 __device__ __forceinline__ uint64_t ch_load(const uint64_t* w) {
   return __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -917,14 +956,20 @@ __device__ __forceinline__ uint64_t ch_load(const uint64_t* w) {
 __device__ __forceinline__ void ch_store(uint64_t* w, uint64_t v) {
   __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// sum of the value parts of words w[0, n), n <= 64 (one per lane), polling until
-// every one is ready; false after CH_SPIN_LIMIT polls
-__device__ __forceinline__ bool ch_sum_ready(const uint64_t* w, uint32_t n, uint32_t lane, uint32_t epoch, uint32_t limit,
-                                             uint64_t& sum) {
+// sum of the value parts of words a[0, na) + b[0, nb) + c[0, nc) (each <= 64, one
+// per lane), polling all three together until every word is ready; false after
+// `limit` polls
+__device__ __forceinline__ bool ch_sum_ready(const uint64_t* a, uint32_t na, const uint64_t* b, uint32_t nb,
+                                             const uint64_t* c, uint32_t nc, uint32_t lane, uint32_t epoch,
+                                             uint32_t limit, uint64_t& sum) {
+  const uint64_t none = ch_word(epoch, 0);
   for (uint32_t spins = 0;; ++spins) {
-    const uint64_t v = lane < n ? ch_load(w + lane) : ch_word(epoch, 0);
-    if (__all((uint32_t)(v >> 32) == epoch)) {
-      uint64_t x = v & 0xffffffffull;
+    const uint64_t va = lane < na ? ch_load(a + lane) : none;
+    const uint64_t vb = lane < nb ? ch_load(b + lane) : none;
+    const uint64_t vc = lane < nc ? ch_load(c + lane) : none;
+    const bool ready = (uint32_t)(va >> 32) == epoch && (uint32_t)(vb >> 32) == epoch && (uint32_t)(vc >> 32) == epoch;
+    if (__all(ready)) {
+      uint64_t x = (va & 0xffffffffull) + (vb & 0xffffffffull) + (vc & 0xffffffffull);
 #pragma unroll
       for (uint32_t d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
       sum = x;
@@ -934,6 +979,53 @@ __device__ __forceinline__ bool ch_sum_ready(const uint64_t* w, uint32_t n, uint
     __builtin_amdgcn_s_sleep(RTPS_CH_SLEEP);
   }
 }
+// The exact record prefix of `tile` (one wave, all 64 lanes): publish the tile's
+// count (and, as the last tile of its group / supergroup, the group's /
+// supergroup's total), then sum the totals of the earlier supergroups, of the
+// earlier groups of its supergroup and the counts of the earlier tiles of its
+// group.  Every word is an agent-scope {epoch, 32-bit value} word (a supergroup
+// holds at most 64^2 tiles' records: < 2^32 for tiles of 256 datagrams of 16379
+// records, and rec_begin is 32-bit anyway).  false: a poll gave up (the tile is
+// left to B).
+__device__ bool chain_prefix(const KParams& p, uint32_t tile, uint32_t n_tiles, uint64_t agg, uint32_t lane,
+                             uint64_t& excl) {
+  uint64_t* tw = p.chain;
+  const uint32_t ng = chain_groups(n_tiles);
+  uint64_t* gw = tw + n_tiles;
+  uint64_t* sw = gw + ng;
+  const uint32_t g = tile / CH_GROUP, r = tile % CH_GROUP, sg = g / CH_GROUP, rg = g % CH_GROUP;
+  const uint32_t g_size = min(CH_GROUP, n_tiles - g * CH_GROUP), sg_size = min(CH_GROUP, ng - sg * CH_GROUP);
+  const uint32_t ep = p.ch_epoch, lim = p.ch_spin_limit;
+  if (lane == 0) ch_store(tw + tile, ch_word(ep, agg));
+  bool ok = true;
+  uint64_t tiles_sum = 0, groups_sum = 0, part = 0;
+  bool have_tiles = false, have_groups = false;
+  if (r + 1 == g_size) {  // last tile of its group: publish the group total
+    ok = ch_sum_ready(tw + g * CH_GROUP, r, nullptr, 0, nullptr, 0, lane, ep, lim, tiles_sum);
+    have_tiles = true;
+    const uint64_t gtot = tiles_sum + agg;
+    if (ok && lane == 0) ch_store(gw + g, ch_word(ep, gtot));
+    if (ok && rg + 1 == sg_size) {  // ... and of the last group of its supergroup: the supergroup total
+      ok = ch_sum_ready(gw + sg * CH_GROUP, rg, nullptr, 0, nullptr, 0, lane, ep, lim, groups_sum);
+      have_groups = true;
+      if (ok && lane == 0) ch_store(sw + sg, ch_word(ep, groups_sum + gtot));
+    }
+  }
+  // earlier supergroups beyond the first 64 (batches over 64^3 tiles only)
+  excl = 0;
+  uint32_t s0 = 0;
+  for (; ok && s0 + 64 < sg; s0 += 64) {
+    ok = ch_sum_ready(sw + s0, 64, nullptr, 0, nullptr, 0, lane, ep, lim, part);
+    excl += part;
+  }
+  if (ok) {
+    ok = ch_sum_ready(sw + s0, sg - s0, have_groups ? nullptr : gw + sg * CH_GROUP, have_groups ? 0u : rg,
+                      have_tiles ? nullptr : tw + g * CH_GROUP, have_tiles ? 0u : r, lane, ep, lim, part);
+    excl += part + tiles_sum + groups_sum;
+  }
+  return ok;
+}
+
 __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_chain_kernel(KParams p, uint32_t n_tiles,
                                                                                       uint32_t k_spec, uint32_t parity) {
   __shared__ uint32_t s_wave_bad[WAVES];
@@ -965,38 +1057,8 @@ __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_chain_ke
     x.dcount[t.i] = (uint16_t)cnt;
   }
   if (wave == 0) {
-    uint64_t* tw = p.chain;                 // [n_tiles] tile counts
-    uint64_t* gw = p.chain + n_tiles;       // [n_groups] group totals
-    uint64_t* gc = p.ch_gc;                 // [n_groups] arrival counters (zeroed by the previous launch)
-    const uint32_t g = tile / CH_GROUP, r = tile % CH_GROUP;
-    const uint32_t g_size = min(CH_GROUP, n_tiles - g * CH_GROUP);
-    uint64_t excl = 0, part = 0;
-    bool ok = true;
-    uint64_t arrived = 0;
-    const uint32_t ep = p.ch_epoch;
-    if (lane == 0) {
-      ch_store(tw + tile, ch_word(ep, agg));
-      arrived = __hip_atomic_fetch_add(gc + g, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-      // counters alternate between two sets by launch: clear the next launch's set
-      for (uint32_t i = tile; i < p.ch_gmax; i += n_tiles) p.ch_gc_next[i] = 0ull;
-    }
-    arrived = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(arrived >> 32)) << 32) |
-              __builtin_amdgcn_readfirstlane((uint32_t)arrived);
-    if (arrived == g_size) {  // last of its group: publish the group total
-      uint64_t gsum = 0;
-      ok = ch_sum_ready(tw + g * CH_GROUP, g_size, lane, ep, p.ch_spin_limit, gsum);
-      if (ok && lane == 0) ch_store(gw + g, ch_word(ep, gsum));  // < 64 * 256 * 16379 < 2^32
-    }
-#ifndef ABL_NO_LOOKBACK
-    for (uint32_t g0 = 0; ok && g0 < g; g0 += 64) {  // totals of the earlier groups
-      ok = ch_sum_ready(gw + g0, min(64u, g - g0), lane, ep, p.ch_spin_limit, part);
-      excl += part;
-    }
-    if (ok && r) {  // counts of the earlier tiles of its group
-      ok = ch_sum_ready(tw + g * CH_GROUP, r, lane, ep, p.ch_spin_limit, part);
-      excl += part;
-    }
-#endif
+    uint64_t excl = 0;
+    const bool ok = chain_prefix(p, tile, n_tiles, agg, lane, excl);
     if (lane == 0) {
       s_excl = excl;
       s_ok = ok ? 1u : 0u;
@@ -1012,6 +1074,372 @@ __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_chain_ke
     uint32_t n2;
     walk<true>(p, t.s, t.H, t.L, t.i, my_first, n2);
   }
+}
+
+// ---------------------------------------------------------------------------
+// D  rtps_parse_lds_kernel: mixed traffic through LDS tiles.
+// A lane walking its datagram's submessage chain in global memory waits on one
+// dependent load per submessage, and the kind-divergent body readers serialise
+// their own loads on top: C3 spends most of its cycles waiting (r1 counters).
+// Here a workgroup takes LT consecutive datagrams and:
+//   1 stages their bytes, packed 16-B aligned, into an LDS image with
+//     coalesced 16-B loads, every load of the tile in flight at once;
+//   2 walks each datagram's submessage headers in LDS (lane per datagram),
+//     twice: counting, then writing one ITEM per materialised submessage
+//     (offset, length, kind, flags, and the interpreter state in effect: the
+//     source prefix, the dest filter, the governing INFO_TS);
+//   3 runs the per-kind body readers over the items (lane per item, the same
+//     sub_body / rec_finish code as the global walk, reading LDS): validity
+//     (any error drops the datagram) and the finished 64-B records;
+//   4 learns the tile's exact record prefix from the chained look-back;
+//   5 writes the records through the LDS image (now free) as contiguous,
+//     coalesced 16-B stores.
+// Tiles whose bytes or items do not fit fall back to the lane walk in global
+// memory (wave 0, one lane per datagram), with the same look-back.  LT = 32
+// datagrams of at most 1500 B (the Ethernet MTU's RTPS payload) always fit the
+// 48 KiB image, so only jumbo datagrams take the fallback.
+// ---------------------------------------------------------------------------
+#ifndef RTPS_LDS_LT
+#define RTPS_LDS_LT 32u
+#endif
+constexpr uint32_t LT = RTPS_LDS_LT;  // datagrams per LDS tile
+static_assert(LT >= 1 && LT <= 64, "one wave-0 lane per datagram");
+#ifndef RTPS_LDS_IMG
+#define RTPS_LDS_IMG (48u * 1024u)
+#endif
+#ifndef RTPS_LDS_ITEMS
+#define RTPS_LDS_ITEMS 512u
+#endif
+#ifndef RTPS_LDS_WG_PER_CU
+#define RTPS_LDS_WG_PER_CU 2
+#endif
+#ifndef RTPS_LDS_RT  // 1: stage the reader tables in LDS for D too (costs occupancy); 0: probe them in L2
+#define RTPS_LDS_RT 0
+#endif
+// per-phase timestamps of kernel D into a device array (tuning builds only)
+#ifdef RTPS_LDS_STAMPS
+constexpr uint32_t STAMP_TILES = 1u << 16, STAMP_N = 8;
+__device__ uint64_t g_lds_stamps[STAMP_TILES * STAMP_N];
+#define LDS_STAMP(k) \
+  do { if (tid == 0 && tile < STAMP_TILES) g_lds_stamps[tile * STAMP_N + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define LDS_STAMP(k) do {} while (0)
+#endif
+constexpr uint32_t LIMG = RTPS_LDS_IMG;       // image bytes
+constexpr uint32_t LMAXIT = RTPS_LDS_ITEMS;   // items (materialised submessages) per tile
+static_assert(LIMG <= 65536u - 64u, "items hold 16-bit image offsets");
+static_assert(LT % WAVES == 0, "the staging gives every wave LT / WAVES datagrams");
+constexpr uint32_t LDPW = LT / WAVES;  // datagrams staged per wave
+constexpr uint32_t LSTAGE_R = 2;       // 16-B chunks per lane per datagram kept in flight (2 KiB)
+static_assert(LMAXIT * 64u <= LIMG, "the record stage reuses the image");
+static_assert(LMAXIT % TILE == 0, "items in whole rounds");
+constexpr uint32_t LIT_ROUNDS = LMAXIT / TILE;
+constexpr uint32_t IT_NO_TS = 0xffffu;
+
+// item words: [0] image offset of the submessage | eff length << 16
+//             [1] kind | flags << 8 | datagram (tile-local) << 16 | dst_ok << 24
+//             [2] image offset of the source prefix | governing INFO_TS item << 16 (IT_NO_TS: none)
+//             [3] unused
+// One walk over a datagram staged in LDS at image offset `base` (lane per datagram):
+// header checks, the length rules and the interpreter state; WRITE appends the
+// items at it0.  Returns the status (RTPS_DGRAM_*; SUBMSG_ERR only for length /
+// header errors: body errors come from the item pass) and the item count.  As in
+// walk(), a submessage's record carries the interpreter state AFTER the
+// submessage's own transition (INFO_SRC: its prefix; INFO_TS: its time).
+template <bool WRITE>
+__device__ uint32_t lds_walk(const KParams& p, const uint32_t* img, uint32_t base, uint32_t L, uint32_t dlocal,
+                             u32x4* items, uint32_t it0, uint32_t& nit) {
+  nit = 0;
+  const LSrc s{img, base};
+  if (L > RTPS_MAX_DATAGRAM) return RTPS_DGRAM_TOO_LONG;
+  const uint32_t MAGIC_RTPS = 0x53505452u, MAGIC_RTPX = 0x58505452u;
+  const uint32_t h0 = L >= 4u ? ld4(s, 0) : 0u;
+  if (L < 20u) {  // message_receiver.rs:238-251
+    if (L >= 16u && h0 == MAGIC_RTPS && (ld4(s, 8) >> 8) == 0x534444u && ld4(s, 12) == 0x474e4950u)
+      return RTPS_DGRAM_PING;
+    return RTPS_DGRAM_SHORT;
+  }
+  if (h0 != MAGIC_RTPS) return h0 == MAGIC_RTPX ? RTPS_DGRAM_RTPX : RTPS_DGRAM_BAD_MAGIC;
+  if ((ld4(s, 4) & 0xffu) > 2u) return RTPS_DGRAM_BAD_HEADER;
+  // handle_parsed_message_2 (:289-295): src := header prefix, dest := own, ts := None
+  uint32_t src_off = base + 8u, ts_item = IT_NO_TS;
+  bool dst_ok = true;
+  uint32_t o = 20;
+  while (o < L) {
+    const uint32_t rem = L - o;
+    if (rem < 4u) { nit = 0; return RTPS_DGRAM_SUBMSG_ERR; }
+    const uint32_t h = ld4(s, o);
+    const uint32_t kind = h & 0xffu, flags = (h >> 8) & 0xffu;
+    const bool le = (flags & 1u) != 0u;
+    const uint32_t eff = eff_len(kind, e16(h, 1, le), rem);
+    if (4u + eff > rem) { nit = 0; return RTPS_DGRAM_SUBMSG_ERR; }
+    if (emits(kind)) {
+      // interpreter transitions (message_receiver.rs:618-665); a malformed INFO_*
+      // drops the datagram in the item pass, so its state never matters
+      if (kind == RTPS_INFO_TS) {
+        ts_item = (flags & 0x02u) ? IT_NO_TS : it0 + nit;  // Invalidate flag -> None
+      } else if (kind == RTPS_INFO_SRC) {
+        src_off = base + o + 12u;  // header, unused u32, version, vendor, then the prefix
+        ts_item = IT_NO_TS;
+      } else if (kind == RTPS_INFO_DST) {
+        const uint32_t a = ld4(s, o + 4u), b = ld4(s, o + 8u), c = ld4(s, o + 12u);
+        dst_ok = ((a | b | c) == 0u) || (a == p.own0 && b == p.own1 && c == p.own2);
+      }
+      if (WRITE) {
+        u32x4 it;
+        it[0] = (base + o) | (eff << 16);
+        it[1] = kind | (flags << 8) | (dlocal << 16) | ((dst_ok ? 1u : 0u) << 24);
+        it[2] = src_off | (ts_item << 16);
+        it[3] = 0u;
+        items[it0 + nit] = it;
+      }
+      nit++;
+    }
+    o += 4u + eff;
+  }
+  return RTPS_DGRAM_OK;
+}
+
+__global__ __launch_bounds__(TILE, RTPS_LDS_WG_PER_CU) void rtps_parse_lds_kernel(KParams p, uint32_t n_tiles,
+                                                                                   uint32_t k_spec, uint32_t parity) {
+  __shared__ u32x4 s_img[LIMG / 16u + 4u];  // + 64 B: window reads past the last datagram stay inside
+  __shared__ u32x4 s_it[LMAXIT];            // items; after the item pass: the records' target sets
+  __shared__ uint32_t s_doff[LT + 1];       // image offset of each datagram (16-B aligned), total at LT
+  __shared__ uint32_t s_rel[LT];            // datagram offset from the tile's descriptor base
+  __shared__ uint32_t s_ibase[LT + 1];      // first item of each datagram, total at LT
+  __shared__ uint32_t s_rbase[LT];          // first tile-local record of each datagram (NONE: dropped)
+  __shared__ uint32_t s_bad[LT];            // a body reader failed (the datagram is dropped)
+  __shared__ uint32_t s_mode, s_ok, s_agg;  // mode 1: LDS tile, 0: lane-walk fallback
+  __shared__ uint64_t s_excl, s_tb;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t tile = blockIdx.x;
+  uint32_t* img = reinterpret_cast<uint32_t*>(s_img);
+  Scratch x = scratch_of(p.scratch, n_tiles);
+  // ---- 0 (wave 0, lane = tile-local datagram): lengths, image offsets, descriptor base ----
+  const uint32_t i = tile * LT + lane;
+  uint32_t L = 0;
+  bool valid = false, addressable = false;
+  if (wave == 0) {
+    valid = lane < LT && i < p.n;
+    const uint64_t off = valid ? p.dgram_off[i] : ~0ull;
+    L = valid ? p.dgram_len[i] : 0u;
+    addressable = valid && off <= p.arena_len && (uint64_t)L <= p.arena_len - off;
+    const uint32_t psz = (addressable && L <= RTPS_MAX_DATAGRAM) ? ((L + 15u) & ~15u) : 0u;
+    const uint32_t incl = wave_incl_scan(psz, lane);
+    if (lane < LT) s_doff[lane] = incl - psz;
+    if (lane == 63) s_doff[LT] = incl;
+    uint64_t lo = addressable ? off : ~0ull, hi = addressable ? off + L : 0ull;
+#pragma unroll
+    for (uint32_t d = 32; d >= 1; d >>= 1) {
+      const uint64_t a = __shfl_xor(lo, d, 64), b = __shfl_xor(hi, d, 64);
+      lo = a < lo ? a : lo;
+      hi = b > hi ? b : hi;
+    }
+    const uint64_t tb = lo == ~0ull ? 0ull : lo;
+    if (lane < LT) {
+      s_rel[lane] = addressable ? (uint32_t)(off - tb) : 0u;
+      s_bad[lane] = 0u;
+    }
+    const uint32_t total = __shfl(incl, 63, 64);
+    if (lane == 0) {
+      s_tb = tb;
+      // the LDS path needs the image to fit and the tile's bytes inside one 4 GiB descriptor
+      s_mode = (total <= LIMG && (lo == ~0ull || hi - lo < 0xfffff000ull)) ? 1u : 0u;
+    }
+  }
+  LDS_STAMP(0);
+  mt_stage(p);  // reader tables, for the record pass
+  __syncthreads();
+  LDS_STAMP(1);
+  uint32_t st = RTPS_DGRAM_OK, nit = 0;
+  if (s_mode) {
+    // ---- 1: stage the bytes: wave w copies datagrams w, w + WAVES, ...; its lanes take 16-B
+    // chunks lane, lane + 64 of each (1 KiB per instruction), every load in flight at once ----
+    const uint64_t tb = s_tb;
+    const uint64_t avail64 = p.arena_len - tb;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(p.arena + tb), (short)0,
+        (int)(avail64 > 0xffffffffull ? 0xffffffffu : (uint32_t)avail64), 0x00020000);
+    u32x4 v[LDPW][LSTAGE_R];
+    uint32_t nch[LDPW];
+#pragma unroll
+    for (uint32_t j = 0; j < LDPW; ++j) {
+      const uint32_t d = wave + WAVES * j;
+      nch[j] = (s_doff[d + 1] - s_doff[d]) >> 4;  // 0 for datagrams not staged
+      const uint32_t rel = s_rel[d];
+#pragma unroll
+      for (uint32_t r = 0; r < LSTAGE_R; ++r) {
+        const uint32_t k = r * 64u + lane;
+        v[j][r] = u32x4{0u, 0u, 0u, 0u};
+        if (k < nch[j]) v[j][r] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, rel + 16u * k, 0, 0);
+      }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < LDPW; ++j) {
+      const uint32_t d = wave + WAVES * j;
+      u32x4* dst = s_img + (s_doff[d] >> 4);
+#pragma unroll
+      for (uint32_t r = 0; r < LSTAGE_R; ++r) {
+        const uint32_t k = r * 64u + lane;
+        if (k < nch[j]) dst[k] = v[j][r];
+      }
+      // datagrams over 2 KiB (rare: jumbo frames): the rest chunk by chunk
+      for (uint32_t k = LSTAGE_R * 64u + lane; k < nch[j]; k += 64u)
+        dst[k] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, s_rel[d] + 16u * k, 0, 0);
+    }
+    __syncthreads();
+    LDS_STAMP(2);
+    // ---- 2a: count walk (wave 0): status from the headers and length rules, items per datagram ----
+    if (wave == 0) {
+      if (valid) st = addressable ? lds_walk<false>(p, img, s_doff[lane], L, lane, s_it, 0, nit)
+                                  : (uint32_t)RTPS_DGRAM_TOO_LONG;
+      const uint32_t incl = wave_incl_scan(nit, lane);
+      if (lane < LT) s_ibase[lane] = incl - nit;
+      if (lane == 63) {
+        s_ibase[LT] = incl;
+        if (incl > LMAXIT) s_mode = 0u;  // too many submessages: the lane walk takes the tile
+      }
+    }
+    __syncthreads();
+  }
+  if (!s_mode) {
+    // ---- fallback: lane walk in global memory (wave 0), the same look-back ----
+    if (wave != 0) return;
+    TileCtx t;
+    load_tile<LT>(p, tile, t);
+    uint32_t cnt;
+    const uint32_t st2 = count_lane(p, t, cnt);
+    const uint32_t incl = wave_incl_scan(cnt, lane);
+    const uint32_t agg = __shfl(incl, 63, 64);
+    const bool mixed = __ballot(t.valid && cnt != k_spec) != 0ull;
+    if (t.valid) {
+      p.status[t.i] = (uint8_t)st2;
+      x.dcount[t.i] = (uint16_t)cnt;
+    }
+    uint64_t excl = 0;
+    const bool ok = chain_prefix(p, tile, n_tiles, agg, lane, excl);
+    if (lane == 0) {
+      x.info[tile] = agg | INFO_NONSPEC | (ok ? INFO_WRITTEN : 0u) | (mixed ? INFO_MIXED : 0u);  // read by B
+      if (tile == 0) x.flag[parity] = 1u;  // B never takes its all-speculative exit
+    }
+    if (!ok || !t.valid) return;
+    const uint64_t my_first = excl + (incl - cnt);
+    if (p.rec_begin) p.rec_begin[t.i] = (uint32_t)my_first;
+    if (cnt) {
+      uint32_t n2;
+      walk<true>(p, t.s, t.H, t.L, t.i, my_first, n2);
+    }
+    return;
+  }
+  LDS_STAMP(3);
+  // ---- 2b: item walk (wave 0) ----
+  if (wave == 0 && valid && st == RTPS_DGRAM_OK) {
+    uint32_t n2;
+    lds_walk<true>(p, img, s_doff[lane], L, lane, s_it, s_ibase[lane], n2);
+  }
+  __syncthreads();
+  LDS_STAMP(4);
+  // ---- 3: item pass: body readers + the records (lane per item) ----
+  const uint32_t nitems = s_ibase[LT];
+  Rec R[LIT_ROUNDS];
+  uint32_t tgt[LIT_ROUNDS], dl[LIT_ROUNDS];
+  const LSrc whole{img, 0u};
+#pragma unroll
+  for (uint32_t r = 0; r < LIT_ROUNDS; ++r) {
+    const uint32_t k = r * TILE + tid;
+    rec_clear(R[r]);
+    tgt[r] = RTPS_NO_TARGET;
+    dl[r] = 0u;
+    if (k < nitems) {
+      const u32x4 it = s_it[k];
+      const uint32_t oabs = it[0] & 0xffffu, eff = it[0] >> 16;
+      const uint32_t kind = it[1] & 0xffu, flags = (it[1] >> 8) & 0xffu, d = (it[1] >> 16) & 0xffu;
+      const uint32_t base = s_doff[d], o = oabs - base;
+      const LSrc ds{img, base};
+      dl[r] = d;
+      const bool le = (flags & 1u) != 0u;
+      Win W;
+      load_win(ds, o, W);
+      SubOut so;
+      if (!sub_body<true>(ds, W, kind, flags, le, o + 4u, eff, R[r], so)) {
+        s_bad[d] = 1u;
+      } else {
+        Interp ist;
+        const uint32_t so_off = it[2] & 0xffffu, ts_it = it[2] >> 16;
+        ist.src0 = ld4(whole, so_off); ist.src1 = ld4(whole, so_off + 4u); ist.src2 = ld4(whole, so_off + 8u);
+        ist.dst_ok = (it[1] >> 24) != 0u;
+        ist.ts_valid = ts_it != IT_NO_TS;
+        ist.ts_sec = 0u; ist.ts_frac = 0u;
+        if (ist.ts_valid) {
+          const u32x4 ti = s_it[ts_it];
+          const uint32_t to = ti[0] & 0xffffu;
+          const bool tle = ((ti[1] >> 8) & 1u) != 0u;
+          ist.ts_sec = e32(ld4(whole, to + 4u), tle);
+          ist.ts_frac = e32(ld4(whole, to + 8u), tle);
+        }
+        R[r].d[0] = tile * LT + d;
+        R[r].d[1] = o | (kind << 16) | (flags << 24);
+        tgt[r] = rec_finish(p, R[r], so, kind, ist);
+      }
+    }
+  }
+  __syncthreads();
+  LDS_STAMP(5);
+  // ---- 4 (wave 0): statuses, counts, the tile prefix (look-back) ----
+  if (wave == 0) {
+    uint32_t st2 = st;
+    if (valid && st2 == RTPS_DGRAM_OK && s_bad[lane]) st2 = RTPS_DGRAM_SUBMSG_ERR;
+    const uint32_t cnt = (valid && st2 == RTPS_DGRAM_OK) ? s_ibase[lane + 1] - s_ibase[lane] : 0u;
+    const uint32_t incl = wave_incl_scan(cnt, lane);
+    const uint32_t agg = __shfl(incl, 63, 64);
+    if (lane < LT) s_rbase[lane] = (valid && st2 == RTPS_DGRAM_OK) ? incl - cnt : 0xffffffffu;
+    const bool mixed = __ballot(valid && cnt != k_spec) != 0ull;
+    if (valid) {
+      p.status[i] = (uint8_t)st2;
+      x.dcount[i] = (uint16_t)cnt;
+    }
+    uint64_t excl = 0;
+    const bool ok = chain_prefix(p, tile, n_tiles, agg, lane, excl);
+    if (ok && valid && p.rec_begin) p.rec_begin[i] = (uint32_t)(excl + incl - cnt);
+    if (lane == 0) {
+      s_excl = excl;
+      s_ok = ok ? 1u : 0u;
+      s_agg = agg;
+      x.info[tile] = agg | INFO_NONSPEC | (ok ? INFO_WRITTEN : 0u) | (mixed ? INFO_MIXED : 0u);  // read by B
+      if (tile == 0) x.flag[parity] = 1u;  // B never takes its all-speculative exit
+    }
+  }
+  __syncthreads();
+  LDS_STAMP(6);
+  if (!s_ok) return;  // B walks the tile
+  // ---- 5: records into the (now free) image at their tile-local positions ----
+  uint32_t* s_tgt = reinterpret_cast<uint32_t*>(s_it);
+#pragma unroll
+  for (uint32_t r = 0; r < LIT_ROUNDS; ++r) {
+    const uint32_t k = r * TILE + tid;
+    if (k < nitems) {
+      const uint32_t rb = s_rbase[dl[r]];
+      if (rb != 0xffffffffu) {
+        const uint32_t pos = rb + (k - s_ibase[dl[r]]);
+        u32x4* q = s_img + pos * 4u;
+        q[0] = u32x4{R[r].d[0], R[r].d[1], R[r].d[2], R[r].d[3]};
+        q[1] = u32x4{R[r].d[4], R[r].d[5], R[r].d[6], R[r].d[7]};
+        q[2] = u32x4{R[r].d[8], R[r].d[9], R[r].d[10], R[r].d[11]};
+        q[3] = u32x4{R[r].d[12], R[r].d[13], R[r].d[14], R[r].d[15]};
+        s_tgt[pos] = tgt[r];
+      }
+    }
+  }
+  __syncthreads();
+  // ---- 6: coalesced copy-out: the tile's records are contiguous at excl ----
+  const uint64_t excl = s_excl;
+  const uint64_t lim = p.max_records > excl ? p.max_records - excl : 0ull;
+  const uint32_t nrec = s_agg < lim ? s_agg : (uint32_t)lim;
+  u32x4* dst = reinterpret_cast<u32x4*>(p.records + excl);
+  for (uint32_t q = tid; q < nrec * 4u; q += TILE) dst[q] = s_img[q];
+  if (p.target_out)
+    for (uint32_t q = tid; q < nrec; q += TILE) p.target_out[excl + q] = s_tgt[q];
+  LDS_STAMP(7);
 }
 
 // device-side synthetic generator: one lane per datagram
@@ -1185,6 +1613,7 @@ struct rtps_rx_ctx {
   uint32_t ch_spin_limit = CH_SPIN_LIMIT;
   uint32_t ch_epoch = 0;          // last chained launch's epoch (words start zeroed: epoch 0 is never used)
   uint32_t chain_tiles = 0;       // tiles the chain words are sized for
+  uint32_t mixed_pass = 0;        // chained pass for mixed traffic: 0 = lane walk (C, default), 1 = LDS tiles (D)
 };
 
 static int hip_fail(hipError_t e) { return e == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP; }
@@ -1202,20 +1631,23 @@ int rtps_rx_create(const rtps_rx_config* cfg, rtps_rx_ctx** out_ctx) {
   if (hipSetDevice(c->device) != hipSuccess) { delete c; return RTPS_RX_EHIP; }
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) { delete c; return RTPS_RX_EHIP; }
   c->stream = c->own_stream;
+  if (const char* e = getenv("RTPS_RX_MIXED_PASS")) c->mixed_pass = (e[0] == '1') ? 1u : 0u;  // A/B measurements
   {
     int cus = 0, per_cu = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess && cus > 0 &&
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rtps_parse_fix_kernel, TILE, 0) == hipSuccess && per_cu > 0)
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rtps_parse_fix_kernel<TILE>, TILE, 0) == hipSuccess &&
+        per_cu > 0)
       c->resident_blocks = (uint32_t)cus * (uint32_t)per_cu;
   }
-  size_t tiles = ((size_t)cfg->max_datagrams + TILE - 1) / TILE;
+  // scratch and look-back words sized for the smallest tile (LT datagrams, kernel D)
+  size_t tiles = ((size_t)cfg->max_datagrams + LT - 1) / LT;
   if (tiles == 0) tiles = 1;
   // u32 flag[4] | u32 info[tiles rounded to 4] | u16 dcount[max_datagrams]
   c->scratch_words = 2 + ((tiles + 3) & ~(size_t)3) / 2 + ((size_t)cfg->max_datagrams + 3) / 4 + 2;
   if (hipMalloc(&c->scratch, c->scratch_words * sizeof(uint64_t)) != hipSuccess ||
       hipMemset(c->scratch, 0, c->scratch_words * sizeof(uint64_t)) != hipSuccess ||
-      hipMalloc(&c->chain, chain_alloc_words((uint32_t)tiles) * sizeof(uint64_t)) != hipSuccess ||
-      hipMemset(c->chain, 0, chain_alloc_words((uint32_t)tiles) * sizeof(uint64_t)) != hipSuccess ||
+      hipMalloc(&c->chain, chain_words((uint32_t)tiles) * sizeof(uint64_t)) != hipSuccess ||
+      hipMemset(c->chain, 0, chain_words((uint32_t)tiles) * sizeof(uint64_t)) != hipSuccess ||
       hipHostMalloc(&c->mixed, 2 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
     (void)hipFree(c->scratch);
     (void)hipFree(c->chain);
@@ -1314,8 +1746,6 @@ static int parse_launch(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len
   p.mixed_out = c->mixed;
   p.ch_spin_limit = c->ch_spin_limit;
   p.ch_epoch = 0u;  // set below for a chained launch
-  p.ch_gc = p.ch_gc_next = nullptr;
-  p.ch_gmax = 0u;
   // Launch choice, a performance decision only (both give the same output): a
   // chained single pass when the spec hint is 0, or when most tiles of the last
   // finished batch were mixed (B reports that to pinned memory; read without a sync,
@@ -1324,29 +1754,36 @@ static int parse_launch(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len
   const uint32_t seen = __atomic_load_n(&c->mixed[1], __ATOMIC_RELAXED);
   const bool chain = c->k_spec == 0 || (seen >= 16u && 2u * mixed > seen);
   const uint32_t k = c->k_spec ? c->k_spec : 1u;
-  if (first_kernel) *first_kernel = chain ? 2u : 1u;
+  const bool lds = chain && c->mixed_pass == 1u;
+  if (lds) tiles = (n + LT - 1) / LT;  // kernel D: tiles of LT datagrams (B follows the same tiling)
+  if (first_kernel) *first_kernel = lds ? 3u : chain ? 2u : 1u;
   if (!(phases & 1u)) {
   } else if (chain) {  // one chained pass, B only finishes (n_records, stragglers)
     // the look-back words carry this launch's epoch, so they need no zeroing; only
     // when the 32-bit epoch wraps are stale words of the same epoch possible
     if (++c->ch_epoch == 0u) {
       c->ch_epoch = 1u;
-      if (hipMemsetAsync(c->chain, 0, chain_alloc_words(c->chain_tiles) * sizeof(uint64_t), c->stream) != hipSuccess)
+      if (hipMemsetAsync(c->chain, 0, chain_words(c->chain_tiles) * sizeof(uint64_t), c->stream) != hipSuccess)
         return RTPS_RX_EHIP;
     }
     p.ch_epoch = c->ch_epoch;
-    p.ch_gmax = chain_groups(c->chain_tiles);
-    uint64_t* sets = c->chain + chain_words(c->chain_tiles) + 2;
-    p.ch_gc = sets + (size_t)(c->ch_epoch & 1u) * p.ch_gmax;
-    p.ch_gc_next = sets + (size_t)((c->ch_epoch & 1u) ^ 1u) * p.ch_gmax;
-    hipLaunchKernelGGL(rtps_parse_chain_kernel, dim3(tiles), dim3(TILE), mt_lds, c->stream, p, tiles, k, parity);
+    if (lds) {
+      KParams pd = p;
+      if (!RTPS_LDS_RT) pd.rt_lds = 0u;  // occupancy: the image needs the LDS
+      hipLaunchKernelGGL(rtps_parse_lds_kernel, dim3(tiles), dim3(TILE), pd.rt_lds ? mt_lds : 0u, c->stream, pd,
+                         tiles, k, parity);
+    }
+    else
+      hipLaunchKernelGGL(rtps_parse_chain_kernel, dim3(tiles), dim3(TILE), mt_lds, c->stream, p, tiles, k, parity);
   } else {
     hipLaunchKernelGGL(rtps_parse_spec_kernel, dim3(tiles), dim3(TILE), mt_lds, c->stream, p, tiles, c->k_spec,
                        parity);
   }
   uint32_t grid = tiles < c->resident_blocks ? tiles : c->resident_blocks;
-  if (phases & 2u)
-    hipLaunchKernelGGL(rtps_parse_fix_kernel, dim3(grid), dim3(TILE), mt_lds, c->stream, p, tiles, k, parity);
+  if ((phases & 2u) && lds)
+    hipLaunchKernelGGL(rtps_parse_fix_kernel<LT>, dim3(grid), dim3(TILE), mt_lds, c->stream, p, tiles, k, parity);
+  else if (phases & 2u)
+    hipLaunchKernelGGL(rtps_parse_fix_kernel<TILE>, dim3(grid), dim3(TILE), mt_lds, c->stream, p, tiles, k, parity);
   return hip_fail(hipGetLastError());
 }
 
@@ -1527,6 +1964,24 @@ int rtps_rx_frag_reset(rtps_rx_ctx* c) {
   return rtps_frag_state_reset(c->frag, c->stream);
 }
 
+int rtps_rx_frag_set_clock(rtps_rx_ctx* c, uint64_t now_ns) {
+  if (!c) return RTPS_RX_EINVAL;
+  (void)hipSetDevice(c->device);
+  if (!c->frag) {
+    c->frag = rtps_frag_state_new(c->device);
+    if (!c->frag) return RTPS_RX_ENOMEM;
+  }
+  rtps_frag_set_clock(c->frag, now_ns);
+  return RTPS_RX_OK;
+}
+
+int rtps_rx_frag_gc(rtps_rx_ctx* c, uint64_t expire_before_ns, uint64_t* n_pending) {
+  if (!c || !n_pending) return RTPS_RX_EINVAL;
+  (void)hipSetDevice(c->device);
+  if (!c->frag) return hipMemsetAsync(n_pending, 0, 8, c->stream) == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP;
+  return rtps_frag_gc(c->frag, c->stream, expire_before_ns, n_pending);
+}
+
 /* history-cache ingest (rtps_ingest.hip) */
 int rtps_rx_ingest(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len, const uint64_t* dgram_off,
                    const rtps_record* records, const uint64_t* n_records, uint64_t max_records,
@@ -1561,6 +2016,31 @@ uint32_t rtps_rx_record_size(void) { return (uint32_t)sizeof(rtps_record); }
 int rtps_rx_debug_set_chain_spin_limit(rtps_rx_ctx* c, uint32_t limit) {
   if (!c) return RTPS_RX_EINVAL;
   c->ch_spin_limit = limit;
+  return RTPS_RX_OK;
+}
+
+/* tuning hook (not part of the public header): kernel D's per-tile phase stamps
+   (s_memrealtime, 100 MHz; STAMP_N per tile) of the last launch, in builds with
+   RTPS_LDS_STAMPS; RTPS_RX_EINVAL otherwise */
+int rtps_rx_debug_lds_stamps(rtps_rx_ctx* c, uint64_t* host, uint64_t n) {
+#ifdef RTPS_LDS_STAMPS
+  if (!c || !host) return RTPS_RX_EINVAL;
+  if (n > (uint64_t)STAMP_TILES * STAMP_N) n = (uint64_t)STAMP_TILES * STAMP_N;
+  (void)hipSetDevice(c->device);
+  if (hipStreamSynchronize(c->stream) != hipSuccess) return RTPS_RX_EHIP;
+  return hip_fail(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_lds_stamps), n * 8, 0, hipMemcpyDeviceToHost));
+#else
+  (void)c; (void)host; (void)n;
+  return RTPS_RX_EINVAL;
+#endif
+}
+
+/* test / measurement hook (not part of the public header): the chained pass used
+   for mixed traffic, 0 = the lane walk in global memory (rtps_parse_chain_kernel,
+   the default), 1 = LDS tiles (rtps_parse_lds_kernel). */
+int rtps_rx_debug_set_mixed_pass(rtps_rx_ctx* c, uint32_t pass) {
+  if (!c || pass > 1u) return RTPS_RX_EINVAL;
+  c->mixed_pass = pass;
   return RTPS_RX_OK;
 }
 

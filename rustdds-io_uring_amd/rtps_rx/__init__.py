@@ -66,6 +66,7 @@ EXPORTS = ["rtps_rx_create", "rtps_rx_destroy", "rtps_rx_set_stream", "rtps_rx_s
            "rtps_rx_parse_batch", "rtps_rx_sync", "rtps_rx_strerror", "rtps_rx_max_records_host",
            "rtps_rx_generate", "rtps_rx_bucket_by_writer", "rtps_rx_set_spec_hint", "rtps_rx_cdr_decode",
            "rtps_rx_bucket_by_writer_padded", "rtps_rx_frag_assemble", "rtps_rx_frag_reset",
+           "rtps_rx_frag_set_clock", "rtps_rx_frag_gc",
            "rtps_rx_bucket_descriptors", "rtps_rx_ingest", "rtps_rx_ingest_reset", "rtps_udp_open", "rtps_udp_close",
            "rtps_udp_port", "rtps_udp_backend", "rtps_udp_recv_batch", "rtps_udp_release", "rtps_udp_send_batch",
            "rtps_rx_pump"]
@@ -285,7 +286,8 @@ class MessageReceiver:
 
     def debug_parse_phases(self, arena, off, lens, n, outs, phases):
         """Measurement hook: launch only the parse's first kernel (phases=1) or only the
-        finishing kernel (phases=2); returns 1 (spec kernel A) or 2 (chained kernel C).
+        finishing kernel (phases=2); returns 1 (spec kernel A), 2 (chained lane walk C) or
+        3 (LDS tiles D).
         Run two full parse_batch_device calls afterwards."""
         self.parse_batch_device(arena, off, lens, n, outs) if "_c_out" not in outs else None
         o = outs["_c_out"][(True, True)]
@@ -298,6 +300,12 @@ class MessageReceiver:
         _check(fn(self._h, arena.data_ptr(), arena.numel(), off.data_ptr(), lens.data_ptr(), n, ctypes.byref(o),
                   phases, ctypes.byref(which)))
         return int(which.value)
+
+    def debug_set_mixed_pass(self, lds):
+        """The chained pass for mixed traffic: LDS tiles (True, the default) or the lane walk."""
+        fn = lib().rtps_rx_debug_set_mixed_pass
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+        _check(fn(self._h, 1 if lds else 0))
 
     def generate(self, workload, arena, off, lens, n, seed=SEED, first_idx=0, n_writers=16):
         """Fill device arena with datagrams [first_idx, first_idx+n) of a synthetic workload."""
@@ -372,6 +380,22 @@ class MessageReceiver:
 
     def frag_reset(self):
         _check(lib().rtps_rx_frag_reset(self._h))
+
+    def frag_set_clock(self, now_ns):
+        """Clock (ns) the next batches stamp on the assembly buffers they create or extend."""
+        L = lib()
+        L.rtps_rx_frag_set_clock.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+        _check(L.rtps_rx_frag_set_clock(self._h, now_ns))
+
+    def frag_gc(self, expire_before_ns):
+        """Drop the incomplete buffers last modified before expire_before_ns -> buffers left (host sync)."""
+        import torch
+        L = lib()
+        L.rtps_rx_frag_gc.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+        n = torch.zeros(1, dtype=torch.int64, device=torch.device("cuda", self.device))
+        _check(L.rtps_rx_frag_gc(self._h, expire_before_ns, n.data_ptr()))
+        self.sync()
+        return int(n.item())
 
     def assemble_batch(self, arena_np, off_np, len_np, max_samples=None, heap_bytes=None):
         """Parse + reassemble host arrays -> (BatchResult, samples FRAG_SAMPLE_DTYPE, heap u8, n_samples,

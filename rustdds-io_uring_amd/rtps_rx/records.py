@@ -27,6 +27,7 @@ ROUTE_PASS, ROUTE_TS_VALID, ROUTE_HAS_QOS, ROUTE_HAS_PAYLOAD, ROUTE_BUILTIN, ROU
     0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40
 
 PK_NONE, PK_DATA, PK_KEY, PK_KEY_HASH = 0, 1, 2, 3
+CK_ALIVE, CK_NOT_ALIVE_DISPOSED, CK_NOT_ALIVE_UNREGISTERED, CK_NONE = 0, 1, 2, 0xFF  # rtps_change_kind
 PK_ERR_NO_CONTENT, PK_ERR_AMBIGUOUS, PK_ERR_SHORT = 0x81, 0x82, 0x83
 
 NO_MATCH = 0xFFFF
@@ -44,7 +45,7 @@ RECORD_DTYPE = np.dtype([
 assert RECORD_DTYPE.itemsize == 64
 
 U_DATA = np.dtype([("pl_off", "<u2"), ("pl_len", "<u2"), ("rep_id", "u1", (2,)), ("rep_opts", "u1", (2,)),
-                   ("key_hash_off", "<u2"), ("status_info_off", "<u2"), ("rsi_off", "<u2"), ("_r", "<u2")])
+                   ("key_hash_off", "<u2"), ("status_info_off", "<u2"), ("rsi_off", "<u2"), ("change_kind", "u1"), ("_r", "u1")])
 U_FRAG = np.dtype([("pl_off", "<u2"), ("pl_len", "<u2"), ("frag_start", "<u4"),
                    ("frags_in_sub", "<u2"), ("frag_size", "<u2"), ("data_size", "<u4")])
 U_HB = np.dtype([("last_sn", "<i8"), ("count", "<i4"), ("_r", "<u4")])

@@ -39,8 +39,14 @@ class FragRef:
     def __init__(self):
         self.writer_f = {}
         self.bufs = {}
+        self.now = 0
 
     def pending(self):
+        return len(self.bufs)
+
+    def gc(self, expire_before):
+        """FragmentAssembler::garbage_collect_before (fragment_assembler.rs:216-224)."""
+        self.bufs = {k: b for k, b in self.bufs.items() if b["modified"] >= expire_before}
         return len(self.bufs)
 
     def batch(self, arena, offs, recs):
@@ -58,6 +64,7 @@ class FragRef:
             if k not in self.bufs:
                 self.bufs[k] = {"bytes": bytearray(ds), "count": ds // fsz + (ds % fsz > 0), "bits": set()}
             b = self.bufs[k]
+            b["modified"] = self.now  # AssemblyBuffer::new / insert_frags (:54-61, :139)
             frm = (start - 1) * F
             to = min(frm + min(fis * F, pl_len), len(b["bytes"]))
             base = int(offs[int(r["dgram_idx"])]) + pl_off

@@ -125,6 +125,22 @@ def _sub(kind, le, body, extra_flags=0):
     return WRAP_HEADER + bytes([kind, flags]) + ln + body
 
 
+# S1 (speedy read_from_buffer accepts trailing bytes): Message::read_from_buffer reads the
+# 20-B Header with speedy's Header::read_from_buffer over the WHOLE datagram
+# (rtps/message.rs:66-67), and the reference's own capture tests unwrap() that
+# (message.rs:584-794): the speedy readers ignore bytes past the value.  The
+# fixed-size bodies use the same reader on the submessage's content
+# (Heartbeat::read_from_buffer_with_ctx, rtps/submessage.rs:183; AckNack :167;
+# Gap :159; InfoDestination :200; InfoSource :207), so a body longer than its
+# fields parses, with the same field values.  Derived from the reference's vectors:
+TRAILING = {  # name: (source body vector, kind, extra bytes)
+    "s1_heartbeat_trailing": ("body_heartbeat", HEARTBEAT, 4),
+    "s1_heartbeat_trailing_odd": ("body_heartbeat", HEARTBEAT, 3),
+    "s1_info_destination_trailing": ("body_info_destination", INFO_DST, 8),
+    "s1_info_source_trailing": ("body_info_source", INFO_SRC, 1),
+}
+
+
 def cases():
     """[(name, datagram, own_prefix, status, [(off, kind)], {off: fields})]"""
     v = vectors()
@@ -141,6 +157,11 @@ def cases():
             body = bytes.fromhex(bodies[name]["le" if le else "be"])
             out.append((f"{name}_{'le' if le else 'be'}", _sub(kind, le, body), OWN, DGRAM_OK, [(20, kind)],
                         {20: exp}))
+    for name, (src, kind, extra) in TRAILING.items():
+        for le in (True, False):
+            body = bytes.fromhex(bodies[src]["le" if le else "be"]) + bytes(range(0xA0, 0xA0 + extra))
+            out.append((f"{name}_{'le' if le else 'be'}", _sub(kind, le, body), OWN, DGRAM_OK, [(20, kind)],
+                        {20: BODIES[src][1]}))
     rid, wid = bytes.fromhex(RID), bytes.fromhex(WID)
     for name, (base, nb) in SNSETS.items():
         for le in (True, False):

@@ -94,3 +94,51 @@ def test_c4_workload(rx, n, batches):
         g = _run(rx, fa, lambda: (sub, sub_off, ln[a:b]), f"C4 {a}:{b}")
         total += g[3]
     assert total >= n // 49 - 16
+
+
+def test_gc_across_batches(rx):
+    """rtps_rx_frag_gc = garbage_collect_before (fragment_assembler.rs:216-224): batch b
+    runs at clock t0 + b; after it the buffers last modified before t0 + b - 1 are
+    dropped on the device and in the oracle; later fragments of a dropped (writer, SN)
+    start new buffers, which the next batches' outputs then show."""
+    dgrams = frag_ref.soup(4000, 11)
+    fa = oracle.FragAssembler()
+    t0 = 1_700_000_000 * 10**9
+    dropped = 0
+    for b, a in enumerate(range(0, len(dgrams), 250)):
+        rx.frag_set_clock(t0 + b)
+        fa.set_clock(t0 + b)
+        g = _run(rx, fa, dgrams[a:a + 250], f"batch {b}")
+        left = rx.frag_gc(t0 + b - 1)
+        assert left == fa.gc(t0 + b - 1) == fa.pending(), f"batch {b}: {left} left vs {fa.pending()}"
+        dropped += g[5] - left
+    assert dropped > 0
+    assert rx.frag_gc(t0 + 10**6) == 0 and fa.gc(t0 + 10**6) == 0  # everything expires
+
+
+def test_c4_lossy_pending_bounded(rx):
+    """A lossy C4 stream (1 % of datagrams lost: about 40 % of the 49-fragment samples never
+    complete): without gc the pending buffers only grow; with gc after every batch
+    (expiring what no fragment touched for two batches) n_pending stays bounded, and the
+    samples and pending counts match the oracle batch after batch."""
+    n, batches = 20000, 8
+    rng = np.random.default_rng(5)
+    fa = oracle.FragAssembler()
+    t0 = 10**12
+    pend, pend_nogc = [], []
+    fa_nogc = oracle.FragAssembler()
+    for b in range(batches):
+        arena, off, ln = oracle.gen(oracle.WL_C4, n, first_idx=b * n)
+        keep = rng.random(n) > 0.01
+        sub = (arena, np.ascontiguousarray(off[keep]), np.ascontiguousarray(ln[keep]))
+        rx.frag_set_clock(t0 + b)
+        fa.set_clock(t0 + b)
+        _run(rx, fa, lambda: sub, f"lossy C4 batch {b}")
+        left = rx.frag_gc(t0 + b - 1)
+        assert left == fa.gc(t0 + b - 1)
+        pend.append(left)
+        st, recs, _, _ = oracle.parse(*sub, threads=8)
+        fa_nogc.batch(sub[0], sub[1], recs)
+        pend_nogc.append(fa_nogc.pending())
+    assert pend_nogc[-1] > 3 * max(pend[1:]), (pend, pend_nogc)
+    assert max(pend[2:]) <= 3 * n // 49 // 2, pend  # about two batches of lost samples at most

@@ -71,6 +71,30 @@ def test_oracle_state_across_batches(cuts):
     assert total > 50
 
 
+@pytest.mark.parametrize("keep", [1, 2, 4])
+def test_oracle_gc_across_batches(keep):
+    """FragmentAssembler::garbage_collect_before (fragment_assembler.rs:216-224), called the
+    way the reader does after each batch (reader.rs:1338-1340 with its expiry window): batch
+    b runs at clock b; buffers last modified before b - keep + 1 are dropped, so their later
+    fragments start fresh buffers that never complete."""
+    dgrams = frag_ref.soup(2400, 11)
+    f = oracle.FragAssembler()
+    model = frag_ref.FragRef()
+    step = 200
+    dropped = 0
+    t0 = 10**9  # ns clock (u64)
+    for b, a in enumerate(range(0, len(dgrams), step)):
+        f.set_clock(t0 + b)
+        model.now = t0 + b
+        arena, off, recs, st = _parse(dgrams[a:a + step])
+        samples, heap, n, used = f.batch(arena, off, recs)
+        _check_against_model(samples, heap, model.batch(arena, off, recs), f"batch {b}")
+        before = model.pending()
+        assert f.gc(t0 + b - keep + 1) == model.gc(t0 + b - keep + 1) == f.pending()
+        dropped += before - model.pending()
+    assert dropped > 0
+
+
 def test_capacity_limits():
     arena, off, recs, st = _parse(frag_ref.soup(800, 4))
     full, fheap, n, used = oracle.FragAssembler().batch(arena, off, recs)

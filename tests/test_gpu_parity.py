@@ -302,8 +302,10 @@ def test_full_size_parity(rx, wl, name):
 
 @pytest.mark.parametrize("wl,name", [(3, "C3"), (1, "T")])
 def test_chained_launch_full_size(rx, wl, name):
-    """Spec hint 0 (mixed traffic): the chained look-back launch, bit-exact at 1M datagrams."""
-    n = 1 << 20
+    """Spec hint 0 (mixed traffic): the chained look-back launch, bit-exact at 1M datagrams
+    (C3: 1M + 64K, 4352 tiles of 256, so that the look-back spans two supergroups of 64 x 64
+    tiles)."""
+    n = (1 << 20) + (1 << 16 if wl == 3 else 0)
     arena, off, ln = _device_gen(rx, wl, n)
     rx.set_spec_hint(0)
     try:
@@ -312,21 +314,72 @@ def test_chained_launch_full_size(rx, wl, name):
         rx.set_spec_hint(1)
 
 
+@pytest.mark.parametrize("lds", [True, False])
+@pytest.mark.parametrize("wl", [3, 1])
+def test_mixed_passes_agree(rx, wl, lds):
+    """The two chained passes for mixed traffic, LDS tiles (D) and the lane walk (C),
+    bit-exact with the oracle on the same batch (C3, and one-DATA traffic forced
+    through the chained pass), misaligned packing included."""
+    a, o, l = oracle.gen(wl, 60000, first_idx=777)
+    dg = [a[int(x):int(x) + int(y)].tobytes() for x, y in zip(o[:3000], l[:3000])]
+    rx.set_spec_hint(0)
+    rx.debug_set_mixed_pass(lds)
+    try:
+        _parity(rx, a, o, l, f"wl {wl} {'LDS' if lds else 'lane walk'}")
+        for align in (1, 2, 3):
+            A, O, L = oracle.pack(dg, align=align)
+            O = O + align  # offsets = align mod 16, unaligned for the 16-B staging loads
+            A2 = np.zeros(len(A) + 16, np.uint8)
+            A2[align:align + len(A)] = A
+            _parity(rx, A2, O, L, f"wl {wl} align {align}")
+    finally:
+        rx.debug_set_mixed_pass(False)
+        rx.set_spec_hint(1)
+
+
+def test_lds_tile_fallbacks(rx):
+    """Tiles the LDS pass cannot stage (bytes beyond the image: 64 KiB datagrams; more
+    materialised submessages than item slots: INFO_TS-only datagrams) take the lane
+    walk inside the same kernel; neighbouring tiles stay on the LDS path."""
+    a, o, l = oracle.gen(oracle.WL_C3, 500)
+    c3 = [a[int(x):int(x) + int(y)].tobytes() for x, y in zip(o, l)]
+    hdr = b"RTPS\x02\x04\x01\x0f" + bytes(range(12))
+    many = hdr + b"\x09\x03\x00\x00" * 1000          # 1000 INFO_TS (Invalidate): 1000 records
+    big_data = hdr + bytes([0x15, 0x05]) + (65000 - 24).to_bytes(2, "little") + bytes(2) + \
+        (16).to_bytes(2, "little") + bytes(16) + b"\x00\x01\x00\x00" + bytes(65000 - 48)
+    assert len(big_data) == 65000
+    dg = c3[:100] + [many] + c3[100:230] + [big_data, big_data[:64000]] * 2 + c3[230:]
+    A, O, L = oracle.pack(dg, align=4)
+    rx.set_spec_hint(0)
+    rx.debug_set_mixed_pass(True)
+    try:
+        gpu = _parity(rx, A, O, L, "LDS fallbacks")
+        assert int(gpu.status[100]) == DGRAM_OK and len(gpu.submessages(100)) == 1000
+        assert int(gpu.status[231]) == DGRAM_OK and int(gpu.status[232]) != DGRAM_OK
+    finally:
+        rx.debug_set_mixed_pass(False)
+        rx.set_spec_hint(1)
+
+
+@pytest.mark.parametrize("lds", [False, True])
 @pytest.mark.parametrize("limit", [0, 1])
-def test_chained_fallback_to_fix_pass(rx, limit):
+def test_chained_fallback_to_fix_pass(rx, limit, lds):
     """Chained tiles that stop waiting for their predecessors (forced here with a
-    poll limit of 0 or 1) are left to kernel B: the output is still bit-exact."""
+    poll limit of 0 or 1) are left to kernel B: the output is still bit-exact, for
+    both chained passes (lane walk C: B tiles of 256 datagrams; LDS tiles D: of 32)."""
     import ctypes
     import rtps_rx
     L = rtps_rx.lib()
     L.rtps_rx_debug_set_chain_spin_limit.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
     a, o, l = oracle.gen(oracle.WL_C3, 200000)
     rx.set_spec_hint(0)
+    rx.debug_set_mixed_pass(lds)
     assert L.rtps_rx_debug_set_chain_spin_limit(rx._h, limit) == 0
     try:
         _parity(rx, a, o, l, f"C3 chained, poll limit {limit}")
-        # scratch: u32 flag[4], then u32 info[tile] (INFO_WRITTEN = 1 << 30: written by the chained pass)
-        tiles = (len(l) + 255) // 256
+        # scratch: u32 flag[4], then u32 info[tile] (INFO_WRITTEN = 1 << 30: written by the chained pass);
+        tsz = 32 if lds else 256
+        tiles = (len(l) + tsz - 1) // tsz
         words = 2 + (tiles + 1) // 2
         buf = np.zeros(words, dtype=np.uint64)
         L.rtps_rx_debug_scratch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]
@@ -335,15 +388,15 @@ def test_chained_fallback_to_fix_pass(rx, limit):
         left = int(((info >> 30) & 1 == 0).sum())
         assert left > 0, "no tile was left to kernel B: the fallback was not exercised"
     finally:
-        L.rtps_rx_debug_set_chain_spin_limit(rx._h, 1 << 14)
+        L.rtps_rx_debug_set_chain_spin_limit(rx._h, 1 << 10)
+        rx.debug_set_mixed_pass(False)
         rx.set_spec_hint(1)
 
 
 def test_chained_words_across_sizes_and_epoch_wrap(rx):
     """The chained pass's look-back words are never zeroed: they carry the launch's
-    epoch, and the group arrival counters alternate between two sets.  Chained
-    batches of different sizes, run across the 32-bit epoch wrap (which zeroes
-    everything once), stay bit-exact."""
+    epoch.  Chained batches of different sizes, run across the 32-bit epoch wrap
+    (which zeroes everything once), stay bit-exact."""
     import ctypes
     import rtps_rx
     L = rtps_rx.lib()
