@@ -32,6 +32,8 @@
 // bytes read + the same bytes written + 64 B of the record read.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+
+#include "rtps_sort.h"
 #include <string.h>
 
 #include <new>
@@ -893,7 +895,7 @@ static bool grow(FragState* s, uint64_t max, hipStream_t st) {
   ok = ok && hipMalloc(&s->epochs, n * sizeof(Epoch)) == hipSuccess &&
        hipMalloc(&s->pool, s->pool_words * 4) == hipSuccess;
   size_t b1 = 0, b2 = 0, b3 = 0;
-  ok = ok && hipcub::DeviceRadixSort::SortPairs(nullptr, b1, s->keys, s->skeys, s->vals, s->svals, (int)n, 0, 32, st) == hipSuccess;
+  ok = ok && rtps_sort_pairs(nullptr, b1, s->keys, s->skeys, s->vals, s->svals, (uint32_t)n, (int)32, st) == hipSuccess;
   ok = ok && hipcub::DeviceScan::ExclusiveSum(nullptr, b2, s->cnt, s->rank, (int)n, st) == hipSuccess;
   ok = ok && hipcub::DeviceScan::ExclusiveSum(nullptr, b3, s->dsz, s->hoff, (int)n, st) == hipSuccess;
   s->tmp_bytes = b1 > b2 ? (b1 > b3 ? b1 : b3) : (b2 > b3 ? b2 : b3);
@@ -958,7 +960,7 @@ int rtps_frag_assemble(FragState* s, hipStream_t st, const uint8_t* arena, uint6
   hipLaunchKernelGGL(k_keys, dim3(gb), dim3(FT), 0, st, records, n_records, max, s->keys, s->vals, s->pos_epoch,
                      s->dmark, s->seen);
   size_t tb = s->tmp_bytes;
-  if (hipcub::DeviceRadixSort::SortPairs(s->tmp, tb, s->keys, s->skeys, s->vals, s->svals, (int)max, 0, 32, st) !=
+  if (rtps_sort_pairs(s->tmp, tb, s->keys, s->skeys, s->vals, s->svals, (uint32_t)max, (int)32, st) !=
       hipSuccess)
     return RTPS_RX_EHIP;
   hipLaunchKernelGGL(k_writers, dim3(gb), dim3(FT), 0, st, records, s->skeys, s->svals, max, s->wkey, s->wfirst,

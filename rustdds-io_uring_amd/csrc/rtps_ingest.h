@@ -19,3 +19,8 @@ int rtps_ingest_batch(IngestState* s, hipStream_t stream, const ReaderDev& t, co
                       uint64_t arena_len, const uint64_t* dgram_off, const rtps_record* records,
                       const uint64_t* n_records, uint64_t max_records, const rtps_frag_sample* frag,
                       const uint64_t* n_frag, uint64_t max_frag, uint32_t flags, const rtps_ingest_out* out);
+// Test / measurement hook: 0 = path chosen per batch, 1 = global marks / merge,
+// 2 = per-proxy workgroups (results are the same).
+void rtps_ingest_set_path(IngestState* s, uint32_t path);
+// Tuning builds with RTPS_PROXY_STAMPS: the per-proxy phase sums of the last per-proxy batch.
+int rtps_ingest_proxy_stamps(uint64_t* host, uint64_t n);

@@ -52,6 +52,8 @@
 // state per event); no MFMA.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+
+#include "rtps_sort.h"
 #include <string.h>
 
 #include <new>
@@ -63,6 +65,7 @@ namespace {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr uint32_t IT = 256;
+constexpr uint32_t WAVES_I = IT / 64;
 constexpr uint32_t NONE = 0xffffffffu;
 constexpr uint32_t W = RTPS_INGEST_WINDOW;  // sequence numbers tracked per proxy
 constexpr uint32_t WW = W / 32;             // bitmap words per proxy
@@ -70,7 +73,8 @@ constexpr uint32_t ECAP_MAX = 1u << 14;     // writer proxies
 enum : uint8_t { EV_NONE = 0, EV_SAMPLE = 1, EV_HB = 2, EV_GAP = 3 };
 // counters: window overflow, selected HEARTBEATs, selected deliveries, records of the batch, then
 // the HEARTBEAT / GAP / event counts in 64 slot triples (one atomic per block, spread: no hot address)
-enum { C_OVF = 0, C_NSEL, C_NDEL, C_NREC, C_SPREAD, C_COUNT = C_SPREAD + 3 * 64 };
+// the HEARTBEAT / GAP / event / proxy-less sample counts in 64 slot quads (one atomic per block, spread: no hot address)
+enum { C_OVF = 0, C_NSEL, C_NDEL, C_NREC, C_SPREAD, C_COUNT = C_SPREAD + 4 * 64 };
 // event metadata: reader slot | flags << 16 (EVF_*)
 constexpr uint32_t EVF_DUP_OK = 1u << 16;  // RTPS_TARGET_DUPLICATES_OK reader
 constexpr uint32_t EVF_FREE = 1u << 17;    // sample without a proxy (writer kind not user-defined)
@@ -186,7 +190,7 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
   const bool lds = rt_fits_lds(t);
   if (lds) { rt_stage(t, s_rt); __syncthreads(); }
   const bool reliable = !(flags & RTPS_INGEST_BEST_EFFORT);
-  uint32_t nh = 0, ng = 0, ne = 0;
+  uint32_t nh = 0, ng = 0, ne = 0, nf = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * IT + threadIdx.x; i < max; i += (uint64_t)gridDim.x * IT) {
     uint8_t ev = EV_NONE;
     uint32_t set = NONE;
@@ -241,6 +245,7 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
           meta = me;
           nh += ev == EV_HB;
           ng += ev == EV_GAP;
+          nf += en == NONE;
         }
       }
     }
@@ -260,21 +265,21 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
       x.rsn[i] = sn;
     }
   }
-  __shared__ uint32_t s_n[3];
-  if (threadIdx.x == 0) { s_n[0] = 0; s_n[1] = 0; s_n[2] = 0; }
+  __shared__ uint32_t s_n[4];
+  if (threadIdx.x < 4) s_n[threadIdx.x] = 0;
   __syncthreads();
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) {
     nh += __shfl_xor(nh, d, 64); ng += __shfl_xor(ng, d, 64); ne += __shfl_xor(ne, d, 64);
+    nf += __shfl_xor(nf, d, 64);
   }
-  if ((threadIdx.x & 63u) == 0) { atomicAdd(&s_n[0], nh); atomicAdd(&s_n[1], ng); atomicAdd(&s_n[2], ne); }
+  if ((threadIdx.x & 63u) == 0) {
+    atomicAdd(&s_n[0], nh); atomicAdd(&s_n[1], ng); atomicAdd(&s_n[2], ne); atomicAdd(&s_n[3], nf);
+  }
   __syncthreads();
-  if (threadIdx.x == 0 && (s_n[0] | s_n[1] | s_n[2])) {
-    unsigned long long* c = reinterpret_cast<unsigned long long*>(ctr + C_SPREAD + 3u * (blockIdx.x & 63u));
-    if (s_n[0]) atomicAdd(c, (unsigned long long)s_n[0]);
-    if (s_n[1]) atomicAdd(c + 1, (unsigned long long)s_n[1]);
-    if (s_n[2]) atomicAdd(c + 2, (unsigned long long)s_n[2]);
-  }
+  if (threadIdx.x < 4 && s_n[threadIdx.x])
+    atomicAdd(reinterpret_cast<unsigned long long*>(ctr + C_SPREAD + 4u * (blockIdx.x & 63u) + threadIdx.x),
+              (unsigned long long)s_n[threadIdx.x]);
 }
 
 // 1b: lane per record writes its events at roff[i] (set order = EntityId order of the readers)
@@ -332,10 +337,14 @@ __global__ __launch_bounds__(IT) void k_hacc(const rtps_record* recs, uint64_t n
 // irrelevant_changes_range(gapStart, gapList.base) (a negative range changes
 // nothing) and set_irrelevant_change per listed SN (NumberSetIter,
 // sequence_number.rs:543-557), clipped to the proxy's window [lo, lo + W).
-template <typename F>
-__device__ __forceinline__ void gap_words(const rtps_record& r, const uint8_t* arena, const uint64_t* dgram_off,
-                                          int64_t lo, F&& f) {
-  const int64_t start = r.sn, base = r.u.gap.list_base;
+// The window words a valid GAP covers, (word, bits) pairs to f: the range
+// [gapStart, gapList.base) (irrelevant_changes_range; a negative range changes
+// nothing) and the listed SNs (set_irrelevant_change per NumberSetIter element,
+// sequence_number.rs:543-557), clipped to the window [lo, lo + W).  word(w): the
+// bitmap's w-th u32 in host order (MSB first = SN base + 32 w).
+template <typename WF, typename F>
+__device__ __forceinline__ void gap_cover_w(int64_t start, int64_t base, uint32_t num_bits, WF&& word_of, int64_t lo,
+                                            F&& f) {
   if (start <= base) {
     const int64_t a = (start > lo ? start : lo) - lo, b = (base < lo + (int64_t)W ? base : lo + (int64_t)W) - lo;
     for (int64_t w = a >> 5; a < b && (w << 5) < b; ++w) {
@@ -344,11 +353,9 @@ __device__ __forceinline__ void gap_words(const rtps_record& r, const uint8_t* a
       if (m) f((uint64_t)w, m);
     }
   }
-  const uint8_t* bm = arena + dgram_off[r.dgram_idx] + r.u.gap.bitmap_off;
-  const bool le = (r.flags & 1u) != 0u;
-  for (uint32_t w = 0; w * 32u < r.u.gap.num_bits; ++w) {
-    uint32_t word = rd32(bm + 4u * w, le);
-    const uint32_t valid = r.u.gap.num_bits - w * 32u;
+  for (uint32_t w = 0; w * 32u < num_bits; ++w) {
+    uint32_t word = word_of(w);
+    const uint32_t valid = num_bits - w * 32u;
     if (valid < 32u) word &= ~(0xffffffffu >> valid);
     uint64_t src = __builtin_bitreverse32(word);  // bit j = SN base + 32 w + j
     int64_t off = base + (int64_t)(w * 32u) - lo;
@@ -359,6 +366,17 @@ __device__ __forceinline__ void gap_words(const rtps_record& r, const uint8_t* a
     if ((uint32_t)v2) f(dw, (uint32_t)v2);
     if ((uint32_t)(v2 >> 32) && dw + 1u < WW) f(dw + 1u, (uint32_t)(v2 >> 32));
   }
+}
+template <typename F>
+__device__ __forceinline__ void gap_cover(int64_t start, int64_t base, const uint8_t* bm, uint32_t num_bits, bool le,
+                                          int64_t lo, F&& f) {
+  gap_cover_w(start, base, num_bits, [&](uint32_t w) { return rd32(bm + 4u * w, le); }, lo, f);
+}
+template <typename F>
+__device__ __forceinline__ void gap_words(const rtps_record& r, const uint8_t* arena, const uint64_t* dgram_off,
+                                          int64_t lo, F&& f) {
+  gap_cover(r.sn, r.u.gap.list_base, arena + dgram_off[r.dgram_idx] + r.u.gap.bitmap_off, r.u.gap.num_bits,
+            (r.flags & 1u) != 0u, lo, f);
 }
 
 __device__ __forceinline__ bool proxied_sample(const Scratch& x, uint64_t k) {
@@ -554,6 +572,313 @@ __global__ __launch_bounds__(IT) void k_state(uint32_t n_entries, Scratch x, Sta
   }
 }
 
+// ---- per-proxy path (batches over many proxies) ----
+// Global atomics execute at the memory side (about 20 G scattered atomics/s for
+// the whole chip), so marks / merge over a few million events of hundreds of
+// writers cost ~130 us each.  When the events spread over many proxies, they are
+// instead sorted (stably) by proxy and ONE workgroup per proxy replays its events
+// in order, 256 at a time, against the proxy's change-set window held in LDS:
+// HEARTBEAT acceptance and thresholds by block scans, a sample's coverage by the
+// window (earlier chunks and carried state), an LDS hash (earlier samples of the
+// chunk) and the chunk's earlier GAPs; then the chunk's coverage is ORed into the
+// window.  The same decisions as marks / decide / merge / state, with no global
+// atomics; a proxy with very many events would serialise on one workgroup, so the
+// host picks this path only when the mean load per proxy is small.
+#ifdef RTPS_PROXY_STAMPS  // tuning builds: per-phase time sums of k_proxy, per proxy
+constexpr uint32_t PST_N = 8;
+__device__ unsigned long long g_proxy_stamps[16384 * PST_N];
+#define PST_DECL uint64_t pst_t = __builtin_amdgcn_s_memrealtime(), pst_acc[PST_N] = {0, 0, 0, 0, 0, 0, 0, 0}
+#define PST(k) do { const uint64_t t_ = __builtin_amdgcn_s_memrealtime(); pst_acc[k] += t_ - pst_t; pst_t = t_; } while (0)
+#define PST_FLUSH(e) do { if (threadIdx.x == 0) for (uint32_t k_ = 0; k_ < PST_N; ++k_) g_proxy_stamps[(e) * PST_N + k_] = pst_acc[k_]; } while (0)
+#else
+#define PST_DECL do {} while (0)
+#define PST(k) do {} while (0)
+#define PST_FLUSH(e) do {} while (0)
+#endif
+constexpr uint32_t PT = 512;             // threads of the per-proxy workgroup (one per CU: 8 waves)
+constexpr uint32_t PPT = 4;              // consecutive events per thread
+constexpr uint32_t PCH = PT * PPT;       // events per chunk
+constexpr uint32_t PH = 2 * PCH;         // chunk hash slots (>= 2 x events per chunk)
+constexpr uint32_t PH_BITS = 12;
+static_assert((1u << PH_BITS) == PH, "hash width");
+constexpr uint32_t PWAVES = PT / 64;
+constexpr uint32_t PM_DUP = 4u, PM_LE = 8u, PM_INL = 16u;
+
+// One proxied event as the proxy's workgroup reads it (the sort's value): the
+// fields it needs gathered in event order, so that the per-proxy pass reads its
+// events contiguously.  m = kind (2 bits) | DUP_OK << 2 | little-endian << 3 |
+// inline bitmap << 4 | GAP numBits << 8; a = HEARTBEAT count or GAP list base;
+// bw = a GAP's bitmap words (host order, numBits <= 64) or its arena offset.
+struct PEv {
+  int64_t sn;
+  int64_t a;
+  uint64_t bw;
+  uint32_t m;
+  uint32_t k;  // event index (accept[] slot)
+};
+static_assert(sizeof(PEv) == 32, "PEv layout");
+
+// selection flags: events that touch proxy state
+__global__ __launch_bounds__(IT) void k_pflag(uint64_t n, Scratch x) {
+  uint8_t* flag = reinterpret_cast<uint8_t*>(x.hkey);
+  for (uint64_t k = (uint64_t)blockIdx.x * IT + threadIdx.x; k < n; k += (uint64_t)gridDim.x * IT)
+    flag[k] = (x.evt[k] != EV_NONE && x.ent[k] != NONE) ? 1 : 0;
+}
+// the selected events (x.hval[0, n), ascending) -> sort keys (proxy) and PEv values
+__global__ __launch_bounds__(IT) void k_pack(const rtps_record* recs, const uint8_t* arena, const uint64_t* dgram_off,
+                                             uint64_t n, Scratch x, PEv* out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * IT + threadIdx.x; i < n; i += (uint64_t)gridDim.x * IT) {
+    const uint32_t k = x.hval[i];
+    const uint8_t ev = x.evt[k];
+    PEv P;
+    P.sn = x.esn[k];
+    P.a = 0;
+    P.bw = 0;
+    P.k = k;
+    P.m = ev | ((x.emeta[k] & EVF_DUP_OK) ? PM_DUP : 0u);
+    if (ev == EV_HB) {
+      P.a = recs[x.erec[k]].u.hb.count;
+    } else if (ev == EV_GAP) {
+      const rtps_record& r = recs[x.erec[k]];
+      P.a = r.u.gap.list_base;
+      const bool le = (r.flags & 1u) != 0u;
+      P.m |= (le ? PM_LE : 0u) | (r.u.gap.num_bits << 8);
+      P.bw = dgram_off[r.dgram_idx] + r.u.gap.bitmap_off;
+      if (r.u.gap.num_bits <= 64u) {  // the bitmap itself: the proxy's pass reads no arena
+        const uint8_t* p = arena + P.bw;
+        const uint32_t w0 = r.u.gap.num_bits ? rd32(p, le) : 0u, w1 = r.u.gap.num_bits > 32u ? rd32(p + 4, le) : 0u;
+        P.bw = (uint64_t)w0 | ((uint64_t)w1 << 32);
+        P.m |= PM_INL;
+      }
+    }
+    x.hkey[i] = x.ent[k];
+    x.sval[i] = (uint32_t)i;  // sort value: the packed event's position
+    out[i] = P;
+  }
+}
+// sorted keys -> each proxy's segment [seg_b, seg_e) (seg_* zeroed before)
+__global__ __launch_bounds__(IT) void k_pseg(uint64_t n, Scratch x, State s) {
+  for (uint64_t q = (uint64_t)blockIdx.x * IT + threadIdx.x; q < n; q += (uint64_t)gridDim.x * IT) {
+    const uint32_t key = x.skey[q];
+    if (q == 0 || x.skey[q - 1] != key) s.seg_b[key] = (uint32_t)q;
+    if (q + 1 == n || x.skey[q + 1] != key) s.seg_e[key] = (uint32_t)q + 1u;
+  }
+}
+// accept[] for the events no proxy decides: samples without a proxy (writer kind
+// not user-defined, reader.rs:734-739) are accepted; everything else starts at 0
+__global__ __launch_bounds__(IT) void k_decide_free(uint64_t n, uint64_t cap, Scratch x, uint8_t* acc_out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * IT + threadIdx.x; i < cap; i += (uint64_t)gridDim.x * IT)
+    acc_out[i] = (i < n && x.evt[i] == EV_SAMPLE && x.ent[i] == NONE) ? 1 : 0;
+}
+
+// block-wide EXCLUSIVE scan of max (int64) over threads; `carry` joins from the left;
+// *total = the block's max (with the carry)
+__device__ __forceinline__ int64_t block_max_excl(int64_t v, int64_t carry, int64_t* s_w, int64_t& total) {
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  int64_t inc = v;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const int64_t y = __shfl_up(inc, d, 64);
+    if (lane >= d && y > inc) inc = y;
+  }
+  int64_t ex = __shfl_up(inc, 1, 64);
+  if (lane == 0) ex = INT64_MIN;
+  if (lane == 63) s_w[wave] = inc;
+  __syncthreads();
+  int64_t pre = carry;
+  total = carry;
+  for (uint32_t w = 0; w < PWAVES; ++w) {
+    if (w < wave) pre = s_w[w] > pre ? s_w[w] : pre;
+    total = s_w[w] > total ? s_w[w] : total;
+  }
+  __syncthreads();
+  return ex > pre ? ex : pre;
+}
+__device__ __forceinline__ uint32_t ph_hash(uint32_t off) { return (off * 0x9e3779b1u) >> (32 - PH_BITS); }
+__device__ __forceinline__ uint32_t ph_find(const uint32_t* h_key, uint32_t off) {
+  for (uint32_t h = ph_hash(off);; h = (h + 1) & (PH - 1)) {
+    const uint32_t k = h_key[h];
+    if (k == off) return h;
+    if (k == NONE) return NONE;
+  }
+}
+
+// One workgroup per proxy: its events (sorted by proxy, event order kept: `order`
+// holds positions in the packed events `pev`) replayed in chunks of PCH against
+// the proxy's change-set window in LDS.
+__global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* pev, const uint32_t* order,
+                                              uint32_t n_proxies, State s, uint8_t* acc_out, int64_t* ack_out) {
+  __shared__ uint32_t sb[WW];                           // the change set window [lo, lo + W)
+  __shared__ uint32_t pres[WW];                         // window offsets of the chunk's samples
+  __shared__ uint32_t h_key[PH], h_min[PH], h_gap[PH];  // window offset -> first sample / GAP position
+  __shared__ int64_t s_w[PWAVES];
+  __shared__ uint32_t s_first;
+  const uint32_t e = blockIdx.x, tid = threadIdx.x;
+  if (e >= n_proxies) return;
+  const int64_t lo = s.lo[e], base = s.base[e];
+  uint32_t* gbits = s.bits + (uint64_t)e * WW;
+  for (uint32_t w = tid; w < WW; w += PT) { sb[w] = gbits[w]; pres[w] = 0u; }
+  for (uint32_t h = tid; h < PH; h += PT) { h_key[h] = NONE; h_min[h] = NONE; h_gap[h] = NONE; }
+  const uint32_t qb = s.seg_b[e], qe = s.seg_e[e];
+  int64_t run_cnt = s.hbc[e], run_thr = base;  // max HEARTBEAT count so far; max accepted firstSN (>= base)
+  uint64_t n_ovf = 0;
+  PST_DECL;
+  __syncthreads();
+  PST(0);
+  for (uint32_t q0 = qb; q0 < qe; q0 += PCH) {
+    uint32_t m[PPT], slot[PPT], kk[PPT];
+    int64_t v[PPT], a[PPT];
+    uint64_t bwj[PPT];
+    int64_t cmax = INT64_MIN;
+#pragma unroll
+    for (uint32_t j = 0; j < PPT; ++j) {
+      const uint32_t q = q0 + tid * PPT + j;
+      PEv P{0, 0, 0, 0, 0};
+      if (q < qe) P = pev[order[q]];
+      m[j] = P.m;
+      v[j] = P.sn;
+      a[j] = P.a;
+      bwj[j] = P.bw;
+      kk[j] = P.k;
+      if ((m[j] & 3u) == EV_HB && a[j] > cmax) cmax = a[j];
+    }
+    // HEARTBEATs: accepted iff count > every earlier count and the state's (reader.rs:902-905);
+    // an accepted one covers [0, firstSN) (irrelevant_changes_up_to)
+    PST(1);
+    int64_t cnt_total;
+    int64_t c_ex = block_max_excl(cmax, run_cnt, s_w, cnt_total);
+    int64_t fmax = INT64_MIN, f[PPT];
+#pragma unroll
+    for (uint32_t j = 0; j < PPT; ++j) {
+      const bool hb = (m[j] & 3u) == EV_HB;
+      f[j] = (hb && a[j] > c_ex) ? v[j] : INT64_MIN;
+      if (hb && a[j] > c_ex) c_ex = a[j];
+      if (f[j] > fmax) fmax = f[j];
+    }
+    int64_t thr_total;
+    int64_t thr = block_max_excl(fmax, run_thr, s_w, thr_total);
+    run_cnt = cnt_total;
+    run_thr = thr_total;
+    PST(2);
+    // samples in the window -> the chunk hash (first position per sequence number)
+#pragma unroll
+    for (uint32_t j = 0; j < PPT; ++j) {
+      slot[j] = NONE;
+      const int64_t vj = v[j];
+      if ((m[j] & 3u) == EV_SAMPLE && vj >= lo && vj < lo + (int64_t)W) {
+        const uint32_t off = (uint32_t)(vj - lo);
+        uint32_t h = ph_hash(off);
+        for (;;) {
+          const uint32_t prev = atomicCAS(&h_key[h], NONE, off);
+          if (prev == NONE || prev == off) break;
+          h = (h + 1) & (PH - 1);
+        }
+        slot[j] = h;
+        atomicMin(&h_min[h], q0 + tid * PPT + j);
+        atomicOr(&pres[off >> 5], 1u << (off & 31u));
+      }
+    }
+    __syncthreads();
+    PST(3);
+    // GAPs: their first covering position for the chunk's sample sequence numbers (only
+    // window words holding a sample of the chunk are looked up: the presence bitmap)
+#pragma unroll
+    for (uint32_t j = 0; j < PPT; ++j) {
+      if ((m[j] & 3u) != EV_GAP) continue;
+      const uint32_t q = q0 + tid * PPT + j;
+      const uint64_t bw = bwj[j];
+      auto mark = [&](uint64_t w, uint32_t bits) {
+        bits &= pres[w];
+        while (bits) {
+          const uint32_t b = (uint32_t)__builtin_ctz(bits);
+          bits &= bits - 1u;
+          const uint32_t h = ph_find(h_key, (uint32_t)(w * 32u + b));
+          if (h != NONE) atomicMin(&h_gap[h], q);
+        }
+      };
+      if (m[j] & PM_INL)
+        gap_cover_w(v[j], a[j], m[j] >> 8, [&](uint32_t w) { return (uint32_t)(bw >> (32u * w)); }, lo, mark);
+      else
+        gap_cover(v[j], a[j], arena + bw, m[j] >> 8, (m[j] & PM_LE) != 0u, lo, mark);
+    }
+    __syncthreads();
+    PST(4);
+    // decide (should_ignore_change: rtps_writer_proxy.rs:202-230, reader.rs:693-758)
+    int64_t t_run = thr;
+#pragma unroll
+    for (uint32_t j = 0; j < PPT; ++j) {
+      if (f[j] > t_run) t_run = f[j];
+      if ((m[j] & 3u) != EV_SAMPLE) continue;
+      const uint32_t q = q0 + tid * PPT + j;
+      uint8_t acc = 0;
+      const int64_t vj = v[j];
+      if (m[j] & PM_DUP) {
+        acc = 1;  // the participant reader's duplicates (reader.rs:712-722)
+      } else if (vj >= 1 && vj >= t_run) {
+        if (slot[j] == NONE) {
+          acc = 1;  // beyond the tracked window: accepted unchecked
+          ++n_ovf;
+        } else {
+          const uint32_t off = (uint32_t)(vj - lo);
+          acc = (((sb[off >> 5] >> (off & 31u)) & 1u) == 0u && h_min[slot[j]] == q && h_gap[slot[j]] > q) ? 1 : 0;
+        }
+      }
+      acc_out[kk[j]] = acc;
+    }
+    __syncthreads();
+    PST(5);
+    // merge the chunk's coverage into the window, clear the hash and the presence bits
+#pragma unroll
+    for (uint32_t j = 0; j < PPT; ++j) {
+      if (slot[j] != NONE) {
+        const uint32_t off = (uint32_t)(v[j] - lo);
+        atomicOr(&sb[off >> 5], 1u << (off & 31u));
+        pres[off >> 5] = 0u;
+        h_key[slot[j]] = NONE; h_min[slot[j]] = NONE; h_gap[slot[j]] = NONE;
+      } else if ((m[j] & 3u) == EV_GAP) {
+        const uint64_t bw = bwj[j];
+        auto orw = [&](uint64_t w, uint32_t bits) { atomicOr(&sb[w], bits); };
+        if (m[j] & PM_INL)
+          gap_cover_w(v[j], a[j], m[j] >> 8, [&](uint32_t w) { return (uint32_t)(bw >> (32u * w)); }, lo, orw);
+        else
+          gap_cover(v[j], a[j], arena + bw, m[j] >> 8, (m[j] & PM_LE) != 0u, lo, orw);
+      }
+    }
+    __syncthreads();
+    PST(6);
+  }
+  if (n_ovf) atomicAdd(reinterpret_cast<unsigned long long*>(s.ctr + C_OVF), (unsigned long long)n_ovf);
+  // state (as k_state): ack_base = first sequence number >= threshold outside the change set
+  int64_t nb = run_thr;
+  if (run_thr < lo + (int64_t)W) {
+    const uint32_t off0 = (uint32_t)(run_thr - lo);
+    if (tid == 0) s_first = NONE;
+    __syncthreads();
+    for (uint32_t w0 = (off0 >> 5); w0 < WW; w0 += PT) {  // rounds of PT words, stop at the first hit
+      const uint32_t w = w0 + tid;
+      uint32_t word = w < WW ? sb[w] : 0xffffffffu;
+      if (w == (off0 >> 5)) word |= (1u << (off0 & 31u)) - 1u;
+      const uint64_t open = __ballot(word != 0xffffffffu);  // lowest lane first: one LDS atomic per wave
+      if (open && (tid & 63u) == (uint32_t)__builtin_ctzll(open))
+        atomicMin(&s_first, w * 32u + (uint32_t)__builtin_ctz(~word));
+      __syncthreads();
+      if (s_first != NONE) break;
+    }
+    nb = lo + (int64_t)(s_first != NONE ? s_first : W);
+  }
+  const int64_t nlo = nb & ~(int64_t)31;
+  const uint64_t shift = (uint64_t)(nlo - lo) >> 5;
+  for (uint32_t w = tid; w < WW; w += PT) gbits[w] = (w + shift < WW) ? sb[w + shift] : 0u;
+  if (tid == 0) {
+    s.base[e] = nb;
+    s.lo[e] = nlo;
+    s.hbc[e] = (int32_t)run_cnt;
+    if (ack_out) ack_out[e] = nb;
+  }
+  PST(7);
+  PST_FLUSH(e);
+}
+
 __global__ void k_init_state(uint32_t n, State s) {
   for (uint32_t e = blockIdx.x * IT + threadIdx.x; e < n; e += gridDim.x * IT) {
     s.base[e] = 1;  // RtpsWriterProxy::new: ack_base = SequenceNumber::new(1)
@@ -578,7 +903,39 @@ struct IngestState {
   size_t tmp_bytes = 0;
   uint32_t epoch = 0;  // batches since the first-cover table was last cleared
   uint64_t* hctr = nullptr;  // pinned host copy of the event counters
+  uint32_t path = 0;         // 0: chosen per batch, 1: global marks / merge, 2: per-proxy workgroups
+  PEv* pev = nullptr;  // per-proxy path: the proxied events, packed in event order
+  uint64_t pcap = 0;
 };
+
+static void free_pscratch(IngestState* s) {
+  if (s->pev) (void)hipFree(s->pev);
+  s->pev = nullptr;
+  s->pcap = 0;
+}
+// packed events for n proxied events (sort keys / values in the HEARTBEAT scratch: vcap >= n)
+static bool grow_pscratch(IngestState* s, uint64_t n, hipStream_t st) {
+  if (n <= s->pcap) return true;
+  (void)hipStreamSynchronize(st);
+  free_pscratch(s);
+  if (hipMalloc(&s->pev, n * sizeof(PEv)) != hipSuccess) return false;
+  s->pcap = n;
+  return true;
+}
+
+void rtps_ingest_set_path(IngestState* s, uint32_t path) { s->path = path; }
+
+// tuning builds (RTPS_PROXY_STAMPS): k_proxy's per-proxy phase sums (100 MHz ticks), PST_N per proxy
+int rtps_ingest_proxy_stamps(uint64_t* host, uint64_t n) {
+#ifdef RTPS_PROXY_STAMPS
+  if (n > 16384ull * PST_N) n = 16384ull * PST_N;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_proxy_stamps), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess
+             ? RTPS_RX_OK : RTPS_RX_EHIP;
+#else
+  (void)host; (void)n;
+  return RTPS_RX_EINVAL;
+#endif
+}
 
 static void free_state(IngestState* s) {
   void* p[] = {s->st.base, s->st.lo, s->st.hbc, s->st.bits, s->st.fc, s->st.dbits, s->st.seg_b, s->st.seg_e};
@@ -674,7 +1031,7 @@ static bool grow_vscratch(IngestState* s, uint64_t n, hipStream_t st) {
             hipMalloc(&x.hf, n * 8) == hipSuccess && hipMalloc(&x.hpre, n * 8) == hipSuccess;
   const uint64_t nr = s->rcap > n ? s->rcap : n;
   size_t b1 = 0, b2 = 0, b3 = 0, b4 = 0, b5 = 0, b6 = 0;
-  ok = ok && hipcub::DeviceRadixSort::SortPairs(nullptr, b1, x.hkey, x.skey, x.hval, x.sval, (int)n, 0, 32, st) == hipSuccess;
+  ok = ok && rtps_sort_pairs(nullptr, b1, x.hkey, x.skey, x.hval, x.sval, (uint32_t)n, (int)32, st) == hipSuccess;
   ok = ok && hipcub::DeviceScan::ExclusiveScanByKey(nullptr, b2, x.skey, x.hcnt, x.hexcl, hipcub::Max(), INT32_MIN,
                                                     (uint32_t)n, hipcub::Equality(), st) == hipSuccess;
   ok = ok && hipcub::DeviceScan::InclusiveScanByKey(nullptr, b3, x.skey, x.hf, x.hpre, hipcub::Max(), (uint32_t)n,
@@ -708,6 +1065,7 @@ IngestState* rtps_ingest_state_new(int device) {
 
 void rtps_ingest_state_free(IngestState* s) {
   if (!s) return;
+  free_pscratch(s);
   free_vscratch(s);
   free_rscratch(s);
   free_state(s);
@@ -765,11 +1123,12 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
   if (hipMemcpyAsync(s->hctr, S.ctr, C_COUNT * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipStreamSynchronize(st) != hipSuccess)
     return RTPS_RX_EHIP;
-  uint64_t n_hb = 0, n_gap = 0, n_ev = 0;
+  uint64_t n_hb = 0, n_gap = 0, n_ev = 0, n_free = 0;
   for (uint32_t k = 0; k < 64; ++k) {
-    n_hb += s->hctr[C_SPREAD + 3 * k];
-    n_gap += s->hctr[C_SPREAD + 3 * k + 1];
-    n_ev += s->hctr[C_SPREAD + 3 * k + 2];
+    n_hb += s->hctr[C_SPREAD + 4 * k];
+    n_gap += s->hctr[C_SPREAD + 4 * k + 1];
+    n_ev += s->hctr[C_SPREAD + 4 * k + 2];
+    n_free += s->hctr[C_SPREAD + 4 * k + 3];
   }
   const uint64_t n_rec = s->hctr[C_NREC];
   // events live at [0, nev): record slots in identity batches, the expanded list otherwise
@@ -784,7 +1143,41 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
       hipLaunchKernelGGL(k_expand, dim3((uint32_t)hmin((n_rec + IT - 1) / IT, 8192)), dim3(IT), 0, st, t, n_rec, flags, x);
   }
   const uint32_t gv = (uint32_t)hmin((nev + IT - 1) / IT, 8192) ? (uint32_t)hmin((nev + IT - 1) / IT, 8192) : 1u;
-  const bool have_hb = reliable && n_hb > 0;
+  // per-proxy workgroups when the events spread over many proxies (mean load bounded:
+  // one workgroup replays a proxy's events in order); global marks / merge otherwise
+  const bool per_proxy = t.n_proxies > 0 && nev > 0 &&
+                         (s->path == 2 || (s->path == 0 && t.n_proxies >= 64 && n_ev <= (uint64_t)t.n_proxies * 32768u));
+  uint8_t* acc = ident ? out->accept : x.eacc;
+  const uint64_t acc_cap = ident ? max : nev;
+  if (per_proxy) {
+    // the proxied events, in event order (order-preserving select), packed, sorted by proxy (stable)
+    const uint64_t n_px = n_ev - n_free;
+    if (!grow_pscratch(s, n_px ? n_px : 1, st)) return RTPS_RX_ENOMEM;
+    uint32_t kb = 1;
+    while ((1u << kb) < t.n_proxies) ++kb;  // keys 0..n_proxies-1
+    ok = hipMemsetAsync(S.seg_b, 0, (uint64_t)s->ecap * 4, st) == hipSuccess &&
+         hipMemsetAsync(S.seg_e, 0, (uint64_t)s->ecap * 4, st) == hipSuccess;
+    if (!ok) return RTPS_RX_EHIP;
+    if (n_px) {
+      hipLaunchKernelGGL(k_pflag, dim3(gv), dim3(IT), 0, st, nev, x);
+      size_t tb = s->tmp_bytes;
+      if (hipcub::DeviceSelect::Flagged(s->tmp, tb, hipcub::CountingInputIterator<uint32_t>(0),
+                                        reinterpret_cast<uint8_t*>(x.hkey), x.hval, S.ctr + C_NSEL, (int64_t)nev,
+                                        st) != hipSuccess)
+        return RTPS_RX_EHIP;
+      const uint32_t gp = (uint32_t)hmin((n_px + IT - 1) / IT, 8192);
+      hipLaunchKernelGGL(k_pack, dim3(gp), dim3(IT), 0, st, records, arena, dgram_off, n_px, x, s->pev);
+      tb = s->tmp_bytes;  // (proxy, packed position) pairs: 8 B per event per pass, not the 32-B events
+      if (rtps_sort_pairs(s->tmp, tb, x.hkey, x.skey, x.sval, x.hval, (uint32_t)n_px, (int)kb, st) != hipSuccess)
+        return RTPS_RX_EHIP;
+      hipLaunchKernelGGL(k_pseg, dim3(gp), dim3(IT), 0, st, n_px, x, S);
+    }
+    hipLaunchKernelGGL(k_decide_free, dim3((uint32_t)hmin((acc_cap + IT - 1) / IT, 8192)), dim3(IT), 0, st, nev,
+                       acc_cap, x, acc);
+    hipLaunchKernelGGL(k_proxy, dim3(t.n_proxies), dim3(PT), 0, st, arena, s->pev, x.hval, t.n_proxies, S, acc,
+                       out->ack_base);
+  }
+  const bool have_hb = reliable && n_hb > 0 && !per_proxy;
   if (have_hb) {  // stable compaction of the HEARTBEAT events, sort by proxy, scans by key
     const uint32_t hb_blocks = (uint32_t)hmin((n_hb + IT - 1) / IT, 8192);
     ok = hipMemsetAsync(S.seg_b, 0, (uint64_t)s->ecap * 4, st) == hipSuccess &&
@@ -796,7 +1189,7 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
       return RTPS_RX_EHIP;
     hipLaunchKernelGGL(k_hkeys, dim3(hb_blocks), dim3(IT), 0, st, n_hb, x);
     tb = s->tmp_bytes;
-    if (hipcub::DeviceRadixSort::SortPairs(s->tmp, tb, x.hkey, x.skey, x.hval, x.sval, (int)n_hb, 0, (int)ebits, st) !=
+    if (rtps_sort_pairs(s->tmp, tb, x.hkey, x.skey, x.hval, x.sval, (uint32_t)n_hb, (int)ebits, st) !=
         hipSuccess)
       return RTPS_RX_EHIP;
     hipLaunchKernelGGL(k_hvals, dim3(hb_blocks), dim3(IT), 0, st, records, n_hb, x, S);
@@ -810,15 +1203,13 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
                                                hipcub::Equality(), st) != hipSuccess)
       return RTPS_RX_EHIP;
   }
-  if (nev) {
+  if (nev && !per_proxy) {
     hipLaunchKernelGGL(k_marks_d, dim3(gv), dim3(IT), 0, st, nev, x, S, s->epoch, n_gap > 0);
     if (n_gap)
       hipLaunchKernelGGL(k_marks_g, dim3(gv), dim3(IT), 0, st, records, arena, dgram_off, nev, x, S, s->epoch);
   }
   // identity batches decide straight into accept[] (event i = record i: max slots, cleared past n)
-  uint8_t* acc = ident ? out->accept : x.eacc;
-  const uint64_t acc_cap = ident ? max : nev;
-  if (acc_cap)
+  if (acc_cap && !per_proxy)
     hipLaunchKernelGGL(k_decide, dim3((uint32_t)hmin((acc_cap + IT - 1) / IT, 8192)), dim3(IT), 0, st, nev, acc_cap,
                        x, S, acc, have_hb, s->epoch);
   size_t tb = s->tmp_bytes;
@@ -829,8 +1220,9 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
                      out->n_accepted);
   if (!ident)
     hipLaunchKernelGGL(k_accept_counts, dim3(gb), dim3(IT), 0, st, n_rec, max, x, out->accept);
-  if (nev) hipLaunchKernelGGL(k_merge, dim3(gv), dim3(IT), 0, st, records, arena, dgram_off, nev, x, S, n_gap > 0);
-  if (t.n_proxies)
+  if (nev && !per_proxy)
+    hipLaunchKernelGGL(k_merge, dim3(gv), dim3(IT), 0, st, records, arena, dgram_off, nev, x, S, n_gap > 0);
+  if (t.n_proxies && !per_proxy)
     hipLaunchKernelGGL(k_state, dim3(t.n_proxies), dim3(IT), 0, st, t.n_proxies, x, S, have_hb, out->ack_base);
   hipLaunchKernelGGL(k_finish, dim3(1), dim3(1), 0, st, S.ctr, out->n_window_overflow);
   return hipGetLastError() == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP;

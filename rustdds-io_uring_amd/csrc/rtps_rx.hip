@@ -2002,6 +2002,28 @@ int rtps_rx_ingest(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len, con
                            frag, n_frag, max_frag, flags, out);
 }
 
+/* test / measurement hook (not part of the public header): the ingest's
+   per-batch path, 0 = chosen per batch, 1 = global marks / merge, 2 = one
+   workgroup per proxy (same results) */
+int rtps_rx_debug_ingest_path(rtps_rx_ctx* c, uint32_t path) {
+  if (!c || path > 2u) return RTPS_RX_EINVAL;
+  (void)hipSetDevice(c->device);
+  if (!c->ingest) {
+    c->ingest = rtps_ingest_state_new(c->device);
+    if (!c->ingest) return RTPS_RX_ENOMEM;
+  }
+  rtps_ingest_set_path(c->ingest, path);
+  return RTPS_RX_OK;
+}
+
+/* tuning hook (not part of the public header): see rtps_ingest_proxy_stamps */
+int rtps_rx_debug_proxy_stamps(rtps_rx_ctx* c, uint64_t* host, uint64_t n) {
+  if (!c || !host) return RTPS_RX_EINVAL;
+  (void)hipSetDevice(c->device);
+  if (hipStreamSynchronize(c->stream) != hipSuccess) return RTPS_RX_EHIP;
+  return rtps_ingest_proxy_stamps(host, n);
+}
+
 int rtps_rx_ingest_reset(rtps_rx_ctx* c) {
   if (!c) return RTPS_RX_EINVAL;
   if (!c->ingest) return RTPS_RX_OK;

@@ -301,6 +301,12 @@ class MessageReceiver:
                   phases, ctypes.byref(which)))
         return int(which.value)
 
+    def debug_ingest_path(self, path):
+        """Ingest path: 0 chosen per batch, 1 global marks / merge, 2 one workgroup per proxy."""
+        fn = lib().rtps_rx_debug_ingest_path
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+        _check(fn(self._h, path))
+
     def debug_set_mixed_pass(self, lds):
         """The chained pass for mixed traffic: LDS tiles (True, the default) or the lane walk."""
         fn = lib().rtps_rx_debug_set_mixed_pass
@@ -447,6 +453,9 @@ class MessageReceiver:
         """Decide which samples of a parsed batch enter the history cache (the
         stateful reader's writer proxies, Reader::handle_data_msg / _heartbeat_ /
         _gap_); fouts: frag_assemble outputs of the same batch.  Asynchronous."""
+        if iouts["accept"].numel() < max(outs["max_records"], 1):  # the ingest writes accept[0, max_records)
+            raise ValueError(f"ingest: accept holds {iouts['accept'].numel()} bytes, the batch's record capacity "
+                             f"is {outs['max_records']} (alloc_ingest_outputs(max_records, ...))")
         o = iouts.get("_c")
         if o is None:
             o = _IngestOut()

@@ -2,7 +2,7 @@
 oracle's sequential writer-proxy restatement: every per-record accept count,
 the delivery list (record, reader slot) and every proxy's all_ackable_before,
 batch after batch (state carried in the context), on random reliable /
-best-effort corpora, reader sets (several readers per writer, stateless /
+best-effort corpora, on both ingest paths, reader sets (several readers per writer, stateless /
 BestEffort / participant readers, writers known by entity id only),
 completed DataFrag samples, the C3 and T workloads at full size, and the
 edges (window overflow, empty batches, reset, a growing table)."""
@@ -18,10 +18,13 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
-@pytest.fixture()
-def rx():
+@pytest.fixture(params=[1, 2], ids=["global", "per_proxy"])
+def rx(request):
+    """Every test runs on both ingest paths (forced): global marks / merge, and one
+    workgroup per proxy replaying its events in order against an LDS window."""
     import rtps_rx
     r = rtps_rx.MessageReceiver(oracle.OWN_PREFIX, max_datagrams=1 << 21)
+    r.debug_ingest_path(request.param)
     yield r
     r.close()
 
