@@ -136,7 +136,11 @@ __device__ __forceinline__ uint32_t wslot_find(const uint64_t* wkey, uint64_t h)
 // ---- 1: sort keys ----
 __global__ __launch_bounds__(FT) void k_keys(const rtps_record* recs, const uint64_t* n_rec, uint64_t max,
                                              uint32_t* keys, uint32_t* vals, uint32_t* pos_epoch, uint32_t* dmark,
-                                             uint8_t* seen) {
+                                             uint8_t* seen, uint64_t* ctr, uint32_t* new_ptable) {
+  // the batch's counters and the next pending table start empty (instead of two memsets)
+  if (blockIdx.x == 0 && threadIdx.x < C_COUNT - C_NEW_N) ctr[C_NEW_N + threadIdx.x] = 0ull;
+  for (uint64_t t = (uint64_t)blockIdx.x * FT + threadIdx.x; t < PTCAP; t += (uint64_t)gridDim.x * FT)
+    new_ptable[t] = NONE;
   const uint64_t n = min(*n_rec, max);
   for (uint64_t i = (uint64_t)blockIdx.x * FT + threadIdx.x; i < max; i += (uint64_t)gridDim.x * FT) {
     uint32_t k = SENT;
@@ -686,9 +690,30 @@ __device__ __forceinline__ void gst16(uint8_t* p, uint4 v) {
 
 // regular epochs: every record writes its fragments' span.  A wave takes 64
 // sorted positions: each lane resolves one record (epoch, source, destination,
-// lengths), then the wave copies the 64 spans one after the other, 16 B per
-// lane (spans of one sample are adjacent in the heap).
-constexpr uint32_t SPAN_U = 6;  // 16-B loads in flight per lane in the span copy (1536 B per record per pass)
+// lengths), then the wave copies the 64 spans SR at a time, SL lanes per record,
+// 16 B per lane (spans of one sample are adjacent in the heap).
+#ifndef RTPS_SPAN_LANES
+#define RTPS_SPAN_LANES 32  // 16 / 32 / 64 measured on C4: 0.983 / 0.970 / 0.955 ms per frag step
+#endif
+#ifndef RTPS_SPAN_NT
+#define RTPS_SPAN_NT 1      // non-temporal heap stores: 32 lanes 0.970 -> 0.944 ms (scripts/gpu_frag_ab.sh)
+#endif
+#ifndef RTPS_SPAN_U
+#define RTPS_SPAN_U (96 / RTPS_SPAN_LANES)
+#endif
+constexpr uint32_t SL = RTPS_SPAN_LANES;   // lanes per record
+constexpr uint32_t SR = 64 / SL;           // records per wave instruction
+constexpr uint32_t SPAN_U = RTPS_SPAN_U;   // 16-B loads in flight per lane (SL x 16 x SPAN_U B per record per pass)
+static_assert(SL == 16 || SL == 32 || SL == 64, "lanes per record");
+__device__ __forceinline__ void span_st16(uint8_t* p, uint4 v) {
+#if RTPS_SPAN_NT  // non-temporal heap stores (written once, read by the host side later)
+  typedef uint32_t nt_u4 __attribute__((ext_vector_type(4)));
+  nt_u4 w = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(w, reinterpret_cast<nt_u4*>(p));
+#else
+  gst16(p, v);
+#endif
+}
 __global__ __launch_bounds__(FT) void k_span(const rtps_record* recs, const uint8_t* arena, uint64_t arena_len,
                                              const uint64_t* dgram_off, const uint32_t* svals,
                                              const uint32_t* pos_epoch, const uint32_t* skeys, uint64_t max,
@@ -717,18 +742,18 @@ __global__ __launch_bounds__(FT) void k_span(const rtps_record* recs, const uint
         }
       }
     }
-    // four records at a time, one per quarter-wave: 16 lanes x 16 B = 256 B per
-    // instruction per record, SPAN_U loads in flight per lane before the stores
+    // SR records at a time, one per SL-lane group: SL x 16 B per instruction per
+    // record, SPAN_U loads in flight per lane before the stores
     uint64_t todo = __ballot(live);
-    const uint32_t q = lane >> 4, ql = lane & 15u;
+    const uint32_t q = lane / SL, ql = lane % SL;
     while (todo) {
-      uint32_t js[4];
+      uint32_t j = 64u;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        js[k] = todo ? (uint32_t)__builtin_ctzll(todo) : 64u;
+      for (uint32_t k = 0; k < SR; ++k) {
+        const uint32_t jk = todo ? (uint32_t)__builtin_ctzll(todo) : 64u;
         todo &= todo - 1;
+        if (k == q) j = jk;
       }
-      const uint32_t j = q == 0 ? js[0] : q == 1 ? js[1] : q == 2 ? js[2] : js[3];
       const uint32_t jj = j & 63u;
       const uint64_t sj = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(src >> 32), (int)jj, 64) << 32) |
                           (uint32_t)__shfl((int)(uint32_t)src, (int)jj, 64);
@@ -741,19 +766,19 @@ __global__ __launch_bounds__(FT) void k_span(const rtps_record* recs, const uint
       const uint32_t nj = j < 64u ? n_all : 0u;
       const uint8_t* sp = arena + sj;
       uint8_t* d = (uint8_t*)dj;
-      for (uint32_t b0 = 16u * ql; b0 < nj; b0 += 256u * SPAN_U) {
+      for (uint32_t b0 = 16u * ql; b0 < nj; b0 += 16u * SL * SPAN_U) {
         uint4 v[SPAN_U];
 #pragma unroll
         for (uint32_t k = 0; k < SPAN_U; ++k) {
-          const uint32_t b = b0 + 256u * k;
+          const uint32_t b = b0 + 16u * SL * k;
           v[k] = make_uint4(0, 0, 0, 0);
           if (b + 16 <= nvj) v[k] = ld16(sp + b);
         }
 #pragma unroll
         for (uint32_t k = 0; k < SPAN_U; ++k) {
-          const uint32_t b = b0 + 256u * k;
+          const uint32_t b = b0 + 16u * SL * k;
           if (b + 16 <= nj && (b + 16 <= nvj || b >= nvj)) {
-            gst16(d + b, v[k]);  // payload, or zeros past a short payload
+            span_st16(d + b, v[k]);  // payload, or zeros past a short payload
           } else if (b < nj) {
             for (uint32_t t = b; t < b + 16 && t < nj; ++t) d[t] = t < nvj ? sp[t] : (uint8_t)0;
           }
@@ -800,9 +825,14 @@ __global__ __launch_bounds__(FT) void k_serial(const rtps_record* recs, const ui
   }
 }
 
-// new pending hash table (for the next batch's walk)
-__global__ __launch_bounds__(FT) void k_ptable(const Pend* np, const uint64_t* ctr, uint32_t* ptable) {
+// new pending hash table (for the next batch's walk); block 0 also finishes the batch
+// (k_finish's work: n_pending, and the pending count the next batch starts from)
+__global__ __launch_bounds__(FT) void k_ptable(const Pend* np, uint64_t* ctr, uint32_t* ptable, uint64_t* n_pending) {
   const uint64_t n = min<uint64_t>(ctr[C_NEW_N], PCAP);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *n_pending = n | (ctr[C_OVERFLOW] ? (1ull << 63) : 0ull);
+    ctr[C_OLD_N] = n;
+  }
   for (uint64_t j = (uint64_t)blockIdx.x * FT + threadIdx.x; j < n; j += (uint64_t)gridDim.x * FT) {
     uint32_t g[4] = {np[j].guid[0], np[j].guid[1], np[j].guid[2], np[j].guid[3]};
     uint32_t s = key_hash(g, np[j].sn) & (PTCAP - 1);
@@ -835,11 +865,6 @@ __global__ __launch_bounds__(FT) void k_ptable_live(const Pend* op, const uint64
 }
 __global__ void k_gc_finish(const uint64_t* ctr, uint64_t* n_pending) { *n_pending = ctr[C_LIVE]; }
 
-__global__ void k_finish(uint64_t* ctr, uint64_t* n_pending) {
-  const uint64_t n = min<uint64_t>(ctr[C_NEW_N], PCAP);
-  *n_pending = n | (ctr[C_OVERFLOW] ? (1ull << 63) : 0ull);
-  ctr[C_OLD_N] = n;
-}
 
 }  // namespace
 
@@ -950,15 +975,12 @@ int rtps_frag_assemble(FragState* s, hipStream_t st, const uint8_t* arena, uint6
   if (!grow(s, max, st)) return RTPS_RX_ENOMEM;
   const int o = s->cur, nw = s->cur ^ 1;
   const uint32_t gb = (uint32_t)hmin((max + FT - 1) / FT, 8192);
-  bool ok = hipMemsetAsync(s->ctr + C_NEW_N, 0, (C_COUNT - C_NEW_N) * 8, st) == hipSuccess &&
-            hipMemsetAsync(s->ptable[nw], 0xff, PTCAP * 4, st) == hipSuccess;
-  if (!ok) return RTPS_RX_EHIP;
   if (max_records == 0) {
     (void)hipMemsetAsync(out->n_samples, 0, 8, st);
     (void)hipMemsetAsync(out->heap_used, 0, 8, st);
   }
   hipLaunchKernelGGL(k_keys, dim3(gb), dim3(FT), 0, st, records, n_records, max, s->keys, s->vals, s->pos_epoch,
-                     s->dmark, s->seen);
+                     s->dmark, s->seen, s->ctr, s->ptable[nw]);
   size_t tb = s->tmp_bytes;
   if (rtps_sort_pairs(s->tmp, tb, s->keys, s->skeys, s->vals, s->svals, (uint32_t)max, (int)32, st) !=
       hipSuccess)
@@ -989,8 +1011,7 @@ int rtps_frag_assemble(FragState* s, hipStream_t st, const uint8_t* arena, uint6
                      arena_len, dgram_off, s->svals, s->pos_epoch, s->skeys, max, s->epochs, s->pbytes[nw], *out);
   hipLaunchKernelGGL(k_serial, dim3(1024), dim3(FT), 0, st, records, arena, dgram_off, s->svals, s->pos_epoch,
                      s->epochs, s->special, s->ctr, s->pend[o], s->pbytes[o], s->pbytes[nw], *out);
-  hipLaunchKernelGGL(k_ptable, dim3(PCAP / FT), dim3(FT), 0, st, s->pend[nw], s->ctr, s->ptable[nw]);
-  hipLaunchKernelGGL(k_finish, dim3(1), dim3(1), 0, st, s->ctr, out->n_pending);
+  hipLaunchKernelGGL(k_ptable, dim3(PCAP / FT), dim3(FT), 0, st, s->pend[nw], s->ctr, s->ptable[nw], out->n_pending);
   if (hipGetLastError() != hipSuccess) return RTPS_RX_EHIP;
   s->cur = nw;
   return RTPS_RX_OK;
