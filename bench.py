@@ -720,6 +720,9 @@ def main():
         print(json.dumps(result), flush=True)
     rx.close()
     if dist:
+        if exch is not None:
+            from rtps_rx.shard import destroy_comms
+            destroy_comms()  # the library's RCCL communicators, before the process group goes
         dist.destroy_process_group()
 
 

@@ -179,14 +179,46 @@ __device__ __forceinline__ bool ev_of(uint8_t ev, const rtps_target& x, bool use
   return true;
 }
 
+constexpr uint32_t PM_DUP = 4u, PM_LE = 8u, PM_INL = 16u;
+// One proxied event as the proxy's workgroup reads it (the sort's value): the
+// fields it needs gathered in event order, so that the per-proxy pass reads its
+// events contiguously.  m = kind (2 bits) | DUP_OK << 2 | little-endian << 3 |
+// inline bitmap << 4 | GAP numBits << 8; a = HEARTBEAT count or GAP list base;
+// bw = a GAP's bitmap words (host order, numBits <= 64) or its arena offset.
+struct PEv {
+  int64_t sn;
+  int64_t a;
+  uint64_t bw;
+  uint32_t m;
+  uint32_t k;  // event index (accept[] slot)
+};
+static_assert(sizeof(PEv) == 32, "PEv layout");
+
+// What the per-proxy path of an identity batch needs from classify (FAST): the
+// packed events at their record slots, the sort pairs (proxy or n_proxies, slot),
+// accept[] initialised (proxy-less samples accepted) and the proxy segments cleared.
+struct FastOut {
+  PEv* pev;
+  uint8_t* acc;
+  const uint8_t* arena;
+  const uint64_t* dgram_off;
+  uint32_t* seg_b;
+  uint32_t* seg_e;
+  uint32_t n_seg;
+};
+
 // IDENT: no target set has more than one reader, so event i = record i.
-template <bool IDENT>
+// FAST (IDENT only): also the per-proxy path's inputs (FastOut), so that an identity
+// batch on that path needs no host read-back of the counts.
+template <bool IDENT, bool FAST>
 __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record* recs, const uint64_t* n_rec,
                                                  uint64_t max, const rtps_frag_sample* frag, uint32_t flags,
-                                                 Scratch x, uint64_t* ctr) {
+                                                 Scratch x, uint64_t* ctr, FastOut fo) {
   extern __shared__ uint32_t s_rt[];
   const uint64_t n = *n_rec < max ? *n_rec : max;
   if (blockIdx.x == 0 && threadIdx.x == 0) ctr[C_NREC] = n;
+  if (FAST)
+    for (uint32_t e = blockIdx.x * IT + threadIdx.x; e < fo.n_seg; e += gridDim.x * IT) { fo.seg_b[e] = 0u; fo.seg_e[e] = 0u; }
   const bool lds = rt_fits_lds(t);
   if (lds) { rt_stage(t, s_rt); __syncthreads(); }
   const bool reliable = !(flags & RTPS_INGEST_BEST_EFFORT);
@@ -196,12 +228,14 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
     uint32_t set = NONE;
     int64_t sn = 0;
     bool user_kind = true;
+    u32x4 q0 = {0u, 0u, 0u, 0u}, q2 = q0, q3 = q0;  // FAST: the record's fields for the packed event
     if (i < n) {
       // bytes 0..31 of the record (kind @6, prefix||writer_id @8, route @30,
       // payload_kind @31), then 32..47 (sn, gap.list_base) for the candidates:
       // three of the record's four 16-B quads at most
       const u32x4* q = reinterpret_cast<const u32x4*>(recs + i);
-      const u32x4 q0 = q[0], q1 = q[1];
+      q0 = q[0];
+      const u32x4 q1 = q[1];
       const uint32_t kind = (q0[1] >> 16) & 0xffu, route = (q1[3] >> 16) & 0xffu, pk = q1[3] >> 24;
       const uint32_t f = frag ? x.fidx[i] : NONE;
       // records the receiver passes to the user readers (not a builtin pair: discovery's)
@@ -210,7 +244,8 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
           ev = EV_SAMPLE;
           sn = frag[f].sn;
         } else if (kind == RTPS_DATA || kind == RTPS_HEARTBEAT || kind == RTPS_GAP) {
-          const u32x4 q2 = q[2];
+          q2 = q[2];
+          if (FAST && kind != RTPS_DATA) q3 = q[3];
           const int64_t rsn = (int64_t)(((uint64_t)q2[1] << 32) | q2[0]);
           if (kind == RTPS_DATA) {
             // data_to_dds_data must succeed (reader.rs:552-558)
@@ -252,12 +287,45 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
     ne += cnt;
     if (IDENT) {  // at most one event: write it at index i
       const uint8_t evi = cnt ? ev : EV_NONE;
-      x.evt[i] = evi;
-      x.ent[i] = ent;
-      x.esn[i] = sn;
-      x.erec[i] = (uint32_t)i;
       x.emeta[i] = meta;
-      x.hkey[i] = evi == EV_HB ? 1u : 0u;  // selection flag of the HEARTBEAT compaction
+      x.erec[i] = (uint32_t)i;
+      if (!FAST) {  // (the per-proxy identity path reads the packed events instead)
+        x.evt[i] = evi;
+        x.ent[i] = ent;
+        x.esn[i] = sn;
+      }
+      if (!FAST) {
+        x.hkey[i] = evi == EV_HB ? 1u : 0u;  // selection flag of the HEARTBEAT compaction
+      } else {
+        const bool px = evi != EV_NONE && ent != NONE;
+        x.hkey[i] = px ? ent : t.n_proxies;  // sort pairs: (proxy, slot); n_proxies sorts last
+        x.sval[i] = (uint32_t)i;
+        fo.acc[i] = (evi == EV_SAMPLE && ent == NONE) ? 1 : 0;  // proxy-less samples (reader.rs:734-739)
+        if (px) {
+          PEv P;
+          P.sn = sn;
+          P.a = 0;
+          P.bw = 0;
+          P.k = (uint32_t)i;
+          P.m = evi | ((meta & EVF_DUP_OK) ? PM_DUP : 0u);
+          if (evi == EV_HB) {
+            P.a = (int32_t)q3[0];  // u.hb.count
+          } else if (evi == EV_GAP) {
+            P.a = (int64_t)(((uint64_t)q2[3] << 32) | q2[2]);  // u.gap.list_base
+            const uint32_t nbits = q3[0], fl = q0[1] >> 24;
+            const bool le = (fl & 1u) != 0u;
+            P.m |= (le ? PM_LE : 0u) | (nbits << 8);
+            P.bw = fo.dgram_off[q0[0]] + (q3[1] & 0xffffu);  // dgram_idx, u.gap.bitmap_off
+            if (nbits <= 64u) {
+              const uint8_t* bp = fo.arena + P.bw;
+              const uint32_t w0 = nbits ? rd32(bp, le) : 0u, w1 = nbits > 32u ? rd32(bp + 4, le) : 0u;
+              P.bw = (uint64_t)w0 | ((uint64_t)w1 << 32);
+              P.m |= PM_INL;
+            }
+          }
+          fo.pev[i] = P;
+        }
+      }
     } else {
       x.rcnt[i] = cnt;
       x.rset[i] = set;
@@ -602,21 +670,6 @@ constexpr uint32_t PH = 2 * PCH;         // chunk hash slots (>= 2 x events per 
 constexpr uint32_t PH_BITS = 12;
 static_assert((1u << PH_BITS) == PH, "hash width");
 constexpr uint32_t PWAVES = PT / 64;
-constexpr uint32_t PM_DUP = 4u, PM_LE = 8u, PM_INL = 16u;
-
-// One proxied event as the proxy's workgroup reads it (the sort's value): the
-// fields it needs gathered in event order, so that the per-proxy pass reads its
-// events contiguously.  m = kind (2 bits) | DUP_OK << 2 | little-endian << 3 |
-// inline bitmap << 4 | GAP numBits << 8; a = HEARTBEAT count or GAP list base;
-// bw = a GAP's bitmap words (host order, numBits <= 64) or its arena offset.
-struct PEv {
-  int64_t sn;
-  int64_t a;
-  uint64_t bw;
-  uint32_t m;
-  uint32_t k;  // event index (accept[] slot)
-};
-static_assert(sizeof(PEv) == 32, "PEv layout");
 
 // selection flags: events that touch proxy state
 __global__ __launch_bounds__(IT) void k_pflag(uint64_t n, Scratch x) {
@@ -656,10 +709,11 @@ __global__ __launch_bounds__(IT) void k_pack(const rtps_record* recs, const uint
     out[i] = P;
   }
 }
-// sorted keys -> each proxy's segment [seg_b, seg_e) (seg_* zeroed before)
-__global__ __launch_bounds__(IT) void k_pseg(uint64_t n, Scratch x, State s) {
+// sorted keys -> each proxy's segment [seg_b, seg_e) (seg_* zeroed before; keys >= n_proxies: none)
+__global__ __launch_bounds__(IT) void k_pseg(uint64_t n, uint32_t n_proxies, Scratch x, State s) {
   for (uint64_t q = (uint64_t)blockIdx.x * IT + threadIdx.x; q < n; q += (uint64_t)gridDim.x * IT) {
     const uint32_t key = x.skey[q];
+    if (key >= n_proxies) continue;
     if (q == 0 || x.skey[q - 1] != key) s.seg_b[key] = (uint32_t)q;
     if (q + 1 == n || x.skey[q + 1] != key) s.seg_e[key] = (uint32_t)q + 1u;
   }
@@ -904,8 +958,12 @@ struct IngestState {
   uint32_t epoch = 0;  // batches since the first-cover table was last cleared
   uint64_t* hctr = nullptr;  // pinned host copy of the event counters
   uint32_t path = 0;         // 0: chosen per batch, 1: global marks / merge, 2: per-proxy workgroups
-  PEv* pev = nullptr;  // per-proxy path: the proxied events, packed in event order
+  PEv* pev = nullptr;  // per-proxy path: the proxied events, packed (event order, or record slots)
   uint64_t pcap = 0;
+  uint64_t* hctr2 = nullptr;  // pinned: the last per-proxy identity batch's counts (no sync)
+  hipEvent_t hnev_ev = nullptr;
+  bool hnev_ready = false;
+  uint64_t last_nev = 0;      // events of the last batch whose counts were read
 };
 
 static void free_pscratch(IngestState* s) {
@@ -1055,9 +1113,10 @@ IngestState* rtps_ingest_state_new(int device) {
   if (!s) return nullptr;
   s->device = device;
   if (hipMalloc(&s->st.ctr, C_COUNT * 8) != hipSuccess) { delete s; return nullptr; }
-  if (hipHostMalloc(&s->hctr, C_COUNT * 8, hipHostMallocDefault) != hipSuccess) {
-    (void)hipFree(s->st.ctr);
-    delete s;
+  if (hipHostMalloc(&s->hctr, C_COUNT * 8, hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc(&s->hctr2, C_COUNT * 8, hipHostMallocDefault) != hipSuccess ||
+      hipEventCreateWithFlags(&s->hnev_ev, hipEventDisableTiming) != hipSuccess) {
+    rtps_ingest_state_free(s);
     return nullptr;
   }
   return s;
@@ -1071,6 +1130,8 @@ void rtps_ingest_state_free(IngestState* s) {
   free_state(s);
   if (s->st.ctr) (void)hipFree(s->st.ctr);
   if (s->hctr) (void)hipHostFree(s->hctr);
+  if (s->hctr2) (void)hipHostFree(s->hctr2);
+  if (s->hnev_ev) (void)hipEventDestroy(s->hnev_ev);
   delete s;
 }
 
@@ -1113,12 +1174,57 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
     hipLaunchKernelGGL(k_fidx, dim3((uint32_t)hmin((max_frag + IT - 1) / IT, 4096)), dim3(IT), 0, st, frag, n_frag,
                        max_frag, max, x.fidx);
   const uint32_t lds = rt_fits_lds(t) ? rt_lds_bytes(t.gmask + 1u, t.emask + 1u) : 0u;
-  if (ident)
-    hipLaunchKernelGGL(k_classify<true>, dim3(gb), dim3(IT), lds, st, t, records, n_records, max,
-                       with_frag ? frag : nullptr, flags, x, S.ctr);
+  // Identity batches over many proxies take the per-proxy path with no host read-back:
+  // classify writes the path's inputs, the sort runs over every record slot. The choice
+  // uses the previous batch's counts (mean events per proxy), read without a sync.
+  if (s->hnev_ready && hipEventQuery(s->hnev_ev) == hipSuccess) {
+    uint64_t ne = 0;
+    for (uint32_t k = 0; k < 64; ++k) ne += s->hctr2[C_SPREAD + 4 * k + 2];
+    s->last_nev = ne;
+    s->hnev_ready = false;
+  }
+  const bool fast = ident && t.n_proxies > 0 &&
+                    (s->path == 2 || (s->path == 0 && t.n_proxies >= 64 &&
+                                      s->last_nev <= (uint64_t)t.n_proxies * 32768u));
+  FastOut fo{nullptr, nullptr, arena, dgram_off, S.seg_b, S.seg_e, s->ecap};
+  if (fast) {
+    if (!grow_pscratch(s, max, st)) return RTPS_RX_ENOMEM;
+    fo.pev = s->pev;
+    fo.acc = out->accept;
+  }
+  if (ident && fast)
+    hipLaunchKernelGGL((k_classify<true, true>), dim3(gb), dim3(IT), lds, st, t, records, n_records, max,
+                       with_frag ? frag : nullptr, flags, x, S.ctr, fo);
+  else if (ident)
+    hipLaunchKernelGGL((k_classify<true, false>), dim3(gb), dim3(IT), lds, st, t, records, n_records, max,
+                       with_frag ? frag : nullptr, flags, x, S.ctr, fo);
   else
-    hipLaunchKernelGGL(k_classify<false>, dim3(gb), dim3(IT), lds, st, t, records, n_records, max,
-                       with_frag ? frag : nullptr, flags, x, S.ctr);
+    hipLaunchKernelGGL((k_classify<false, false>), dim3(gb), dim3(IT), lds, st, t, records, n_records, max,
+                       with_frag ? frag : nullptr, flags, x, S.ctr, fo);
+  if (fast) {
+    uint32_t kb = 1;
+    while ((1u << kb) <= t.n_proxies) ++kb;  // keys 0..n_proxies (n_proxies: no proxy, sorts last)
+    size_t tb = s->tmp_bytes;
+    if (rtps_sort_pairs(s->tmp, tb, x.hkey, x.skey, x.sval, x.hval, (uint32_t)max, (int)kb, st) != hipSuccess)
+      return RTPS_RX_EHIP;
+    const uint32_t gm = (uint32_t)hmin((max + IT - 1) / IT, 8192);
+    hipLaunchKernelGGL(k_pseg, dim3(gm), dim3(IT), 0, st, max, t.n_proxies, x, S);
+    hipLaunchKernelGGL(k_proxy, dim3(t.n_proxies), dim3(PT), 0, st, arena, s->pev, x.hval, t.n_proxies, S,
+                       out->accept, out->ack_base);
+    size_t tb2 = s->tmp_bytes;
+    if (hipcub::DeviceSelect::Flagged(s->tmp, tb2, hipcub::CountingInputIterator<uint32_t>(0), out->accept, x.sel,
+                                      S.ctr + C_NDEL, (int64_t)max, st) != hipSuccess)
+      return RTPS_RX_EHIP;
+    hipLaunchKernelGGL(k_deliver, dim3(gm), dim3(IT), 0, st, S.ctr + C_NDEL, out->max_accepted, x, out->accepted,
+                       out->n_accepted);
+    hipLaunchKernelGGL(k_finish, dim3(1), dim3(1), 0, st, S.ctr, out->n_window_overflow);
+    // this batch's counts for the next batch's choice (pinned, read without a sync)
+    if (hipMemcpyAsync(s->hctr2, S.ctr, C_COUNT * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipEventRecord(s->hnev_ev, st) != hipSuccess)
+      return RTPS_RX_EHIP;
+    s->hnev_ready = true;
+    return hipGetLastError() == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP;
+  }
   // the batch's record / HEARTBEAT / GAP / event counts size the rest: one small read-back
   if (hipMemcpyAsync(s->hctr, S.ctr, C_COUNT * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipStreamSynchronize(st) != hipSuccess)
@@ -1170,7 +1276,7 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
       tb = s->tmp_bytes;  // (proxy, packed position) pairs: 8 B per event per pass, not the 32-B events
       if (rtps_sort_pairs(s->tmp, tb, x.hkey, x.skey, x.sval, x.hval, (uint32_t)n_px, (int)kb, st) != hipSuccess)
         return RTPS_RX_EHIP;
-      hipLaunchKernelGGL(k_pseg, dim3(gp), dim3(IT), 0, st, n_px, x, S);
+      hipLaunchKernelGGL(k_pseg, dim3(gp), dim3(IT), 0, st, n_px, t.n_proxies, x, S);
     }
     hipLaunchKernelGGL(k_decide_free, dim3((uint32_t)hmin((acc_cap + IT - 1) / IT, 8192)), dim3(IT), 0, st, nev,
                        acc_cap, x, acc);
