@@ -691,6 +691,18 @@ def main():
                               "traffic": None, "kernel_ms": ev_ms,
                               "note": "N>1: per-step time on the compute stream (parse + bucket, waiting for the "
                                       "exchange two steps back); the kernel roofline is the N=1 line's"}
+    if world > 1 and c5:
+        # the driver's N = 1 line is T (the headline config); C5's own one-GPU rate, for a
+        # same-workload comparison, is the committed C5 N = 1 line (64M datagrams on one GPU)
+        import glob
+        ref = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_bench_C5_n1.json")))
+        if ref:
+            try:
+                d1 = json.loads([l for l in open(ref[-1]) if l.startswith("{")][-1])
+                result["config"]["c5_one_gpu"] = {"value": d1["value"], "unit": d1["unit"],
+                                                  "source": os.path.relpath(ref[-1], REPO)}
+            except (OSError, ValueError, KeyError, IndexError):
+                pass
     if world > 1:
         got, split = exch[(args.warmup + args.steps - 1) & 1].gather_received()
         result["config"]["received_records_rank0"] = int(got.shape[0])
