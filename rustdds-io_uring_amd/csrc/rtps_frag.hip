@@ -134,59 +134,76 @@ __device__ __forceinline__ uint32_t wslot_find(const uint64_t* wkey, uint64_t h)
 }
 
 // ---- 1: sort keys ----
+// Also registers the batch's writers (step 2's input): each workgroup dedupes its
+// records' writers in LDS (the smallest record index per writer), then inserts each
+// distinct writer once into the persistent table and atomicMins its first record
+// there, so that only (workgroup, writer) pairs touch global atomics.
+constexpr uint32_t KW_SLOTS = 512;  // >= 2 x records per workgroup pass
 __global__ __launch_bounds__(FT) void k_keys(const rtps_record* recs, const uint64_t* n_rec, uint64_t max,
                                              uint32_t* keys, uint32_t* vals, uint32_t* pos_epoch, uint32_t* dmark,
-                                             uint8_t* seen, uint64_t* ctr, uint32_t* new_ptable) {
+                                             uint8_t* seen, uint64_t* ctr, uint32_t* new_ptable, uint64_t* wkey,
+                                             uint32_t* wfirst, const uint32_t* wF) {
+  __shared__ unsigned long long s_wk[KW_SLOTS];
+  __shared__ uint32_t s_wr[KW_SLOTS];
   // the batch's counters and the next pending table start empty (instead of two memsets)
   if (blockIdx.x == 0 && threadIdx.x < C_COUNT - C_NEW_N) ctr[C_NEW_N + threadIdx.x] = 0ull;
   for (uint64_t t = (uint64_t)blockIdx.x * FT + threadIdx.x; t < PTCAP; t += (uint64_t)gridDim.x * FT)
     new_ptable[t] = NONE;
+  for (uint32_t j = threadIdx.x; j < KW_SLOTS; j += FT) { s_wk[j] = 0ull; s_wr[j] = NONE; }
+  __syncthreads();
   const uint64_t n = min(*n_rec, max);
-  for (uint64_t i = (uint64_t)blockIdx.x * FT + threadIdx.x; i < max; i += (uint64_t)gridDim.x * FT) {
-    uint32_t k = SENT;
-    if (i < n && is_frag(recs + i)) {
-      uint32_t g[4];
-      guid_of(recs + i, g);
-      k = key_hash(g, recs[i].sn);
+  for (uint64_t i0 = (uint64_t)blockIdx.x * FT; i0 < max; i0 += (uint64_t)gridDim.x * FT) {  // uniform trips
+    const uint64_t i = i0 + threadIdx.x;
+    if (i < max) {
+      uint32_t k = SENT;
+      if (i < n && is_frag(recs + i)) {
+        uint32_t g[4];
+        guid_of(recs + i, g);
+        k = key_hash(g, recs[i].sn);
+        const uint64_t wh = writer_hash(g);
+        uint32_t h = (uint32_t)(wh >> 7) & (KW_SLOTS - 1);
+        for (;;) {  // fewer distinct writers than slots: always ends
+          const unsigned long long old = atomicCAS(&s_wk[h], 0ull, (unsigned long long)wh);
+          if (old == 0ull || old == wh) break;
+          h = (h + 1) & (KW_SLOTS - 1);
+        }
+        atomicMin(&s_wr[h], (uint32_t)i);
+      }
+      keys[i] = k;
+      vals[i] = (uint32_t)i;
+      pos_epoch[i] = NONE;  // per-batch state, reset here instead of three memsets
+      dmark[i] = NONE;
+      seen[i] = 0;
     }
-    keys[i] = k;
-    vals[i] = (uint32_t)i;
-    pos_epoch[i] = NONE;  // per-batch state, reset here instead of three memsets
-    dmark[i] = NONE;
-    seen[i] = 0;
+    __syncthreads();
+    // flush the pass's writers: one persistent-table insert + atomicMin each
+    for (uint32_t j = threadIdx.x; j < KW_SLOTS; j += FT) {
+      const uint64_t wh = s_wk[j];
+      if (!wh) continue;
+      const uint32_t r = s_wr[j];
+      s_wk[j] = 0ull;
+      s_wr[j] = NONE;
+      uint32_t s = (uint32_t)(wh >> 7) & (WCAP - 1);
+      uint32_t t = 0;
+      for (; t < WCAP; ++t, s = (s + 1) & (WCAP - 1)) {
+        const uint64_t old = atomicCAS((unsigned long long*)&wkey[s], 0ull, (unsigned long long)wh);
+        if (old == 0 || old == wh) break;
+      }
+      if (t == WCAP) { ctr[C_COUNT] = 1ull; continue; }  // table full: reported by k_writers_fix
+      if (!(wF[s] & FIXED)) atomicMin(&wfirst[s], r);
+    }
+    __syncthreads();
   }
 }
 
-// ---- 2: writers (first DATA_FRAG of each new writer) ----
-__global__ __launch_bounds__(FT) void k_writers(const rtps_record* recs, const uint32_t* skeys, const uint32_t* svals,
-                                                uint64_t max, uint64_t* wkey, uint32_t* wfirst, const uint32_t* wF,
-                                                uint64_t* ctr) {
-  for (uint64_t p = (uint64_t)blockIdx.x * FT + threadIdx.x; p < max; p += (uint64_t)gridDim.x * FT) {
-    const uint32_t k = skeys[p];
-    if (k == SENT) continue;
-    const uint32_t r = svals[p];
-    uint32_t g[4];
-    guid_of(recs + r, g);
-    if (p > 0 && skeys[p - 1] == k) {  // inside a run: only where the full key changes (collisions)
-      uint32_t h[4];
-      const uint32_t q = svals[p - 1];
-      guid_of(recs + q, h);
-      if (same_key(g, recs[r].sn, h, recs[q].sn)) continue;
-    }
-    const uint64_t wh = writer_hash(g);
-    uint32_t s = (uint32_t)(wh >> 7) & (WCAP - 1);
-    uint32_t i = 0;
-    for (; i < WCAP; ++i, s = (s + 1) & (WCAP - 1)) {
-      const uint64_t old = atomicCAS((unsigned long long*)&wkey[s], 0ull, (unsigned long long)wh);
-      if (old == 0 || old == wh) break;
-    }
-    if (i == WCAP) { atomicOr((unsigned long long*)&ctr[C_OVERFLOW], 1ull); continue; }
-    if (!(wF[s] & FIXED)) atomicMin(&wfirst[s], r);
-  }
-}
+// ---- 2: writers: the fragment size of a writer is its first DATA_FRAG's ever (registered by k_keys) ----
 __global__ __launch_bounds__(FT) void k_writers_fix(const rtps_record* recs, const uint64_t* wkey, uint32_t* wfirst,
-                                                    uint32_t* wF) {
+                                                    uint32_t* wF, uint64_t* ctr) {
   const uint32_t s = blockIdx.x * FT + threadIdx.x;
+  if (s == 0 && ctr[C_COUNT]) {  // k_keys found the writer table full
+    atomicOr((unsigned long long*)&ctr[C_OVERFLOW], 1ull);
+    ctr[C_COUNT] = 0ull;
+  }
   if (s >= WCAP || wkey[s] == 0 || (wF[s] & FIXED) || wfirst[s] == NONE) return;
   wF[s] = (uint32_t)recs[wfirst[s]].u.frag.frag_size | FIXED;
   wfirst[s] = NONE;
@@ -935,7 +952,7 @@ FragState* rtps_frag_state_new(int device) {
   if (!s) return nullptr;
   s->device = device;
   bool ok = hipMalloc(&s->wkey, WCAP * 8) == hipSuccess && hipMalloc(&s->wfirst, WCAP * 4) == hipSuccess &&
-            hipMalloc(&s->wF, WCAP * 4) == hipSuccess && hipMalloc(&s->ctr, C_COUNT * 8) == hipSuccess;
+            hipMalloc(&s->wF, WCAP * 4) == hipSuccess && hipMalloc(&s->ctr, (C_COUNT + 1) * 8) == hipSuccess;  // + the writer-table-full word
   for (int k = 0; k < 2 && ok; ++k)
     ok = hipMalloc(&s->pend[k], PCAP * sizeof(Pend)) == hipSuccess && hipMalloc(&s->pbytes[k], PBYTES) == hipSuccess &&
          hipMalloc(&s->pbits[k], PWORDS * 4) == hipSuccess && hipMalloc(&s->ptable[k], PTCAP * 4) == hipSuccess;
@@ -960,7 +977,7 @@ int rtps_frag_state_reset(FragState* s, hipStream_t st) {
   bool ok = hipMemsetAsync(s->wkey, 0, WCAP * 8, st) == hipSuccess &&
             hipMemsetAsync(s->wfirst, 0xff, WCAP * 4, st) == hipSuccess &&
             hipMemsetAsync(s->wF, 0, WCAP * 4, st) == hipSuccess &&
-            hipMemsetAsync(s->ctr, 0, C_COUNT * 8, st) == hipSuccess &&
+            hipMemsetAsync(s->ctr, 0, (C_COUNT + 1) * 8, st) == hipSuccess &&
             hipMemsetAsync(s->ptable[0], 0xff, PTCAP * 4, st) == hipSuccess &&
             hipMemsetAsync(s->ptable[1], 0xff, PTCAP * 4, st) == hipSuccess;
   s->cur = 0;
@@ -980,14 +997,12 @@ int rtps_frag_assemble(FragState* s, hipStream_t st, const uint8_t* arena, uint6
     (void)hipMemsetAsync(out->heap_used, 0, 8, st);
   }
   hipLaunchKernelGGL(k_keys, dim3(gb), dim3(FT), 0, st, records, n_records, max, s->keys, s->vals, s->pos_epoch,
-                     s->dmark, s->seen, s->ctr, s->ptable[nw]);
+                     s->dmark, s->seen, s->ctr, s->ptable[nw], s->wkey, s->wfirst, s->wF);
   size_t tb = s->tmp_bytes;
   if (rtps_sort_pairs(s->tmp, tb, s->keys, s->skeys, s->vals, s->svals, (uint32_t)max, (int)32, st) !=
       hipSuccess)
     return RTPS_RX_EHIP;
-  hipLaunchKernelGGL(k_writers, dim3(gb), dim3(FT), 0, st, records, s->skeys, s->svals, max, s->wkey, s->wfirst,
-                     s->wF, s->ctr);
-  hipLaunchKernelGGL(k_writers_fix, dim3(WCAP / FT), dim3(FT), 0, st, records, s->wkey, s->wfirst, s->wF);
+  hipLaunchKernelGGL(k_writers_fix, dim3(WCAP / FT), dim3(FT), 0, st, records, s->wkey, s->wfirst, s->wF, s->ctr);
   WalkArgs A{records, s->skeys, s->svals, max, s->wkey, s->wF, s->pend[o], s->ptable[o], s->pbits[o], s->epochs,
              s->special, s->pool, s->pool_words, s->pos_epoch, s->dmark, s->seen, s->ctr};
   hipLaunchKernelGGL(k_walk, dim3((uint32_t)hmin((max + FT - 1) / FT, 8192)), dim3(FT), 0, st, A);

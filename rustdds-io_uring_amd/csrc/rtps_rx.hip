@@ -1026,7 +1026,12 @@ __device__ bool chain_prefix(const KParams& p, uint32_t tile, uint32_t n_tiles, 
   return ok;
 }
 
-__global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_chain_kernel(KParams p, uint32_t n_tiles,
+// 8 waves per SIMD fit the chained kernel in 64 VGPRs without scratch (C3: 411-414 against
+// 427-428 us at 6; the speculative kernel would spill there, so it keeps 6)
+#ifndef RTPS_CH_WAVES_PER_SIMD
+#define RTPS_CH_WAVES_PER_SIMD 8
+#endif
+__global__ __launch_bounds__(TILE, RTPS_CH_WAVES_PER_SIMD) void rtps_parse_chain_kernel(KParams p, uint32_t n_tiles,
                                                                                       uint32_t k_spec, uint32_t parity) {
   __shared__ uint32_t s_wave_bad[WAVES];
   __shared__ uint32_t s_wave_sum[WAVES];
