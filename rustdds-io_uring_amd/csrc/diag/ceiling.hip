@@ -73,6 +73,48 @@ __global__ __launch_bounds__(256) void copy_flat_kernel(const uint8_t* arena, co
     *(u128u*)(rows + r * row_bytes + 16 * q) = *(const u128u*)(arena + off[r] + skip + 16 * q);
   }
 }
+// ---- copy ceilings for the DataFrag reassembly's shape (C4: 1344 B at datagram offset 56 -> heap) ----
+// one wave per record, W-byte elements (W = 4 / 8 / 16), U elements in flight per lane, optional
+// non-temporal stores; src alignment is whatever skip gives (56: 8-B aligned in the 16-B-aligned arena)
+template <int W, int U, bool NT>
+__global__ __launch_bounds__(256) void copy_w_kernel(const uint8_t* arena, const uint64_t* off, uint32_t n,
+                                                     uint8_t* rows, uint32_t row_bytes, uint32_t skip) {
+  typedef uint32_t e_t __attribute__((ext_vector_type(W / 4)));
+  const uint32_t lane = threadIdx.x & 63, ne = row_bytes / W;
+  for (uint64_t r = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < n; r += (uint64_t)gridDim.x * 4) {
+    const uint8_t* src = arena + off[r] + skip;
+    uint8_t* dst = rows + r * row_bytes;
+    for (uint32_t q0 = lane; q0 < ne; q0 += 64 * U) {
+      e_t v[U];
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const uint32_t q = q0 + 64 * k;
+        if (q < ne) __builtin_memcpy(&v[k], src + (uint64_t)W * q, W);
+      }
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const uint32_t q = q0 + 64 * k;
+        if (q < ne) {
+          if (NT) __builtin_nontemporal_store(v[k], reinterpret_cast<e_t*>(dst + (uint64_t)W * q));
+          else *reinterpret_cast<e_t*>(dst + (uint64_t)W * q) = v[k];
+        }
+      }
+    }
+  }
+}
+extern "C" int diag_copy_w(int w, int u, int nt, const uint8_t* arena, const uint64_t* off, uint32_t n, uint8_t* rows,
+                           uint32_t row_bytes, uint32_t skip, uint32_t blocks, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+#define V(W, U, NT)                                                                                        \
+  if (w == W && u == U && nt == NT) {                                                                      \
+    hipLaunchKernelGGL((copy_w_kernel<W, U, NT>), dim3(blocks), dim3(256), 0, s, arena, off, n, rows, row_bytes, skip); \
+    return hipGetLastError() == hipSuccess ? 0 : -2;                                                       \
+  }
+  V(16, 1, 0) V(16, 2, 0) V(16, 1, 1) V(16, 2, 1) V(8, 1, 1) V(8, 2, 1) V(8, 3, 1) V(4, 3, 1) V(4, 6, 1)
+#undef V
+  return -1;
+}
+
 extern "C" int diag_copy(int mode, const uint8_t* arena, const uint64_t* off, uint32_t n, uint8_t* rows,
                          uint32_t row_bytes, uint32_t skip, uint32_t blocks, void* stream) {
   hipStream_t s = (hipStream_t)stream;

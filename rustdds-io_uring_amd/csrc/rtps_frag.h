@@ -20,6 +20,7 @@ int rtps_frag_assemble(FragState* s, hipStream_t stream, const uint8_t* arena, u
                        uint64_t max_records, const rtps_frag_out* out);
 // The clock stamped on buffers the next batches create or extend.
 void rtps_frag_set_clock(FragState* s, uint64_t now);
+void rtps_frag_set_sort(FragState* s, int mode);  // tests: 1 = rocprim device sort always
 // Drops the carried buffers last modified before expire_before; the live count
 // goes to the device u64 *n_pending (asynchronous on `stream`).
 int rtps_frag_gc(FragState* s, hipStream_t stream, uint64_t expire_before, uint64_t* n_pending);

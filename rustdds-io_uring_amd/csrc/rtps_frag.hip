@@ -31,8 +31,8 @@
 // Roofline: HBM-bound.  Algorithmic bytes per DATA_FRAG record = its payload
 // bytes read + the same bytes written + 64 B of the record read.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
+#include "rtps_bsort.h"
 #include "rtps_sort.h"
 #include <string.h>
 
@@ -580,39 +580,121 @@ __global__ __launch_bounds__(FT) void k_walk(WalkArgs A) {
 }
 
 // ---- 4: place ----
-__global__ __launch_bounds__(FT) void k_place_in(const uint32_t* dmark, const Epoch* ep, uint64_t max,
-                                                 uint32_t* cnt, uint64_t* dsz) {
-  for (uint64_t r = (uint64_t)blockIdx.x * FT + threadIdx.x; r < max; r += (uint64_t)gridDim.x * FT) {
-    const uint32_t e = dmark[r];
-    cnt[r] = e != NONE;
-    dsz[r] = e != NONE ? ((uint64_t)ep[e].data_size + 15) & ~15ull : 0ull;
+// Completed samples are ranked by completing record, and their heap offsets are
+// the exclusive sum of the preceding completions' 16-B-aligned sizes: a
+// two-level scan over 4096-position tiles, 16 consecutive positions per thread.
+constexpr uint32_t PPT = 16, PTILE = FT * PPT;
+__device__ __forceinline__ void dmark16(const uint32_t* dmark, uint64_t base, uint64_t max, uint32_t d[PPT]) {
+  if (base + PPT <= max) {
+    const uint4* q = reinterpret_cast<const uint4*>(dmark + base);
+#pragma unroll
+    for (uint32_t k = 0; k < PPT / 4; ++k) {
+      const uint4 v = q[k];
+      d[4 * k] = v.x; d[4 * k + 1] = v.y; d[4 * k + 2] = v.z; d[4 * k + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (uint32_t k = 0; k < PPT; ++k) d[k] = base + k < max ? dmark[base + k] : NONE;
   }
 }
-__global__ __launch_bounds__(FT) void k_samples(const uint32_t* dmark, Epoch* ep, const uint32_t* cnt,
-                                                const uint32_t* rank, const uint64_t* dsz, const uint64_t* hoff,
-                                                uint64_t max, rtps_frag_out out) {
-  for (uint64_t r = (uint64_t)blockIdx.x * FT + threadIdx.x; r < max; r += (uint64_t)gridDim.x * FT) {
-    if (r == max - 1) {
-      *out.n_samples = (uint64_t)rank[r] + cnt[r];
-      *out.heap_used = hoff[r] + dsz[r];
-    }
-    const uint32_t e = dmark[r];
+__device__ __forceinline__ uint64_t sample_bytes(const Epoch* ep, uint32_t e) {
+  return ((uint64_t)ep[e].data_size + 15) & ~15ull;
+}
+// workgroup-wide exclusive scan of (count, bytes); returns the totals too
+__device__ __forceinline__ void blk_scan_cb(uint32_t c, uint64_t b, uint32_t& ce, uint64_t& be, uint32_t& ct,
+                                            uint64_t& bt) {
+  __shared__ uint32_t wc[FT / 64];
+  __shared__ uint64_t wb[FT / 64];
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  uint32_t xc = c;
+  uint64_t xb = b;
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t yc = (uint32_t)__shfl_up((int)xc, d, 64);
+    const uint32_t ylo = (uint32_t)__shfl_up((int)(uint32_t)xb, d, 64);
+    const uint32_t yhi = (uint32_t)__shfl_up((int)(uint32_t)(xb >> 32), d, 64);
+    if (lane >= d) { xc += yc; xb += ((uint64_t)yhi << 32) | ylo; }
+  }
+  if (lane == 63) { wc[w] = xc; wb[w] = xb; }
+  __syncthreads();
+  uint32_t pc = 0;
+  uint64_t pb = 0;
+  ct = 0; bt = 0;
+  for (uint32_t k = 0; k < FT / 64; ++k) {
+    if (k < w) { pc += wc[k]; pb += wb[k]; }
+    ct += wc[k]; bt += wb[k];
+  }
+  ce = pc + xc - c;
+  be = pb + xb - b;
+  __syncthreads();
+}
+// per tile: completions and their bytes
+__global__ __launch_bounds__(FT) void k_place_tiles(const uint32_t* dmark, const Epoch* ep, uint64_t max,
+                                                    uint32_t* tc, uint64_t* tb) {
+  const uint64_t base = (uint64_t)blockIdx.x * PTILE + (uint64_t)threadIdx.x * PPT;
+  uint32_t d[PPT];
+  dmark16(dmark, base, max, d);
+  uint32_t c = 0;
+  uint64_t b = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < PPT; ++k)
+    if (d[k] != NONE) { ++c; b += sample_bytes(ep, d[k]); }
+  uint32_t ce, ct;
+  uint64_t be, bt;
+  blk_scan_cb(c, b, ce, be, ct, bt);
+  if (threadIdx.x == 0) { tc[blockIdx.x] = ct; tb[blockIdx.x] = bt; }
+}
+// one workgroup: exclusive scan of the tile totals, and the batch's sample count and heap use
+__global__ __launch_bounds__(FT) void k_place_scan(uint32_t* tc, uint64_t* tb, uint64_t T, rtps_frag_out out) {
+  uint32_t cc = 0;
+  uint64_t cb = 0;
+  for (uint64_t t0 = 0; t0 < T; t0 += FT) {
+    const uint64_t t = t0 + threadIdx.x;
+    const uint32_t c = t < T ? tc[t] : 0u;
+    const uint64_t b = t < T ? tb[t] : 0ull;
+    uint32_t ce, ct;
+    uint64_t be, bt;
+    blk_scan_cb(c, b, ce, be, ct, bt);
+    if (t < T) { tc[t] = cc + ce; tb[t] = cb + be; }
+    cc += ct; cb += bt;
+  }
+  if (threadIdx.x == 0) { *out.n_samples = cc; *out.heap_used = cb; }
+}
+__global__ __launch_bounds__(FT) void k_samples(const uint32_t* dmark, Epoch* ep, const uint32_t* tc,
+                                                const uint64_t* tb, uint64_t max, rtps_frag_out out) {
+  const uint64_t base = (uint64_t)blockIdx.x * PTILE + (uint64_t)threadIdx.x * PPT;
+  uint32_t d[PPT];
+  dmark16(dmark, base, max, d);
+  uint32_t c = 0;
+  uint64_t b = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < PPT; ++k)
+    if (d[k] != NONE) { ++c; b += sample_bytes(ep, d[k]); }
+  uint32_t ce, ct;
+  uint64_t be, bt;
+  blk_scan_cb(c, b, ce, be, ct, bt);
+  if (c == 0) return;
+  uint64_t k_rank = (uint64_t)tc[blockIdx.x] + ce, hoff = tb[blockIdx.x] + be;
+  for (uint32_t k = 0; k < PPT; ++k) {
+    const uint32_t e = d[k];
     if (e == NONE) continue;
     Epoch& E = ep[e];
-    E.dst = hoff[r];
-    const uint64_t k = rank[r];
-    if (k >= out.max_samples) { E.eflags |= EF_SKIP; continue; }
+    const uint64_t sz = ((uint64_t)E.data_size + 15) & ~15ull;
+    E.dst = hoff;
+    const uint64_t kk = k_rank;
+    hoff += sz;
+    ++k_rank;
+    if (kk >= out.max_samples) { E.eflags |= EF_SKIP; continue; }
     rtps_frag_sample s;
     memset(&s, 0, sizeof(s));
     memcpy(s.writer_guid, E.guid, 16);
     s.sn = E.sn;
     s.heap_off = E.dst;
     s.data_size = E.data_size;
-    s.rec_idx = (uint32_t)r;
+    s.rec_idx = (uint32_t)(base + k);
     s.flags = (uint8_t)E.rec_flags;
     s.status = E.data_size < 4 ? RTPS_FRAG_SHORT : RTPS_FRAG_OK;
     if (E.dst + E.data_size > out.heap_bytes) { s.status = RTPS_FRAG_NO_ROOM; E.eflags |= EF_SKIP; }
-    out.samples[k] = s;
+    out.samples[kk] = s;
   }
 }
 
@@ -902,7 +984,9 @@ struct FragState {
   // per-batch scratch (grown on demand)
   uint64_t cap = 0;
   uint32_t *keys = nullptr, *vals = nullptr, *skeys = nullptr, *svals = nullptr;
-  uint32_t *pos_epoch = nullptr, *dmark = nullptr, *cnt = nullptr, *rank = nullptr, *special = nullptr;
+  uint32_t *pos_epoch = nullptr, *dmark = nullptr, *special = nullptr;
+  uint32_t* tcnt = nullptr;   // per 4096-position tile: completions, then their exclusive scan
+  uint64_t* tbytes = nullptr; // per tile: heap bytes, then their exclusive scan
   uint8_t* seen = nullptr;
   uint64_t *dsz = nullptr, *hoff = nullptr;
   Epoch* epochs = nullptr;
@@ -910,14 +994,19 @@ struct FragState {
   uint64_t pool_words = 0;
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
+  // the key sort (rtps_bsort.h) for batches of up to rtps_bsort::MAX_N records
+  uint32_t* bh = nullptr;
+  uint64_t *bk = nullptr, *bk2 = nullptr;
+  int sort_mode = 0;  // 0: rtps_bsort where it applies, 1: rocprim's device sort always (tests)
 };
 
 static void free_scratch(FragState* s) {
-  void* ptrs[] = {s->keys, s->vals, s->skeys, s->svals, s->pos_epoch, s->dmark, s->cnt, s->rank, s->special,
-                  s->seen, s->dsz, s->hoff, s->epochs, s->pool, s->tmp};
+  void* ptrs[] = {s->keys, s->vals, s->skeys, s->svals, s->pos_epoch, s->dmark, s->tcnt, s->special,
+                  s->seen, s->tbytes, s->epochs, s->pool, s->tmp, s->bh, s->bk, s->bk2};
   for (void* p : ptrs) if (p) (void)hipFree(p);
-  s->keys = s->vals = s->skeys = s->svals = s->pos_epoch = s->dmark = s->cnt = s->rank = s->special = nullptr;
-  s->seen = nullptr; s->dsz = s->hoff = nullptr; s->epochs = nullptr; s->pool = nullptr; s->tmp = nullptr;
+  s->keys = s->vals = s->skeys = s->svals = s->pos_epoch = s->dmark = s->tcnt = s->special = nullptr;
+  s->seen = nullptr; s->tbytes = nullptr; s->epochs = nullptr; s->pool = nullptr; s->tmp = nullptr;
+  s->bh = nullptr; s->bk = s->bk2 = nullptr;
   s->cap = 0; s->tmp_bytes = 0;
 }
 
@@ -929,18 +1018,17 @@ static bool grow(FragState* s, uint64_t max, hipStream_t st) {
   bool ok = hipMalloc(&s->keys, n * 4) == hipSuccess && hipMalloc(&s->vals, n * 4) == hipSuccess &&
             hipMalloc(&s->skeys, n * 4) == hipSuccess && hipMalloc(&s->svals, n * 4) == hipSuccess &&
             hipMalloc(&s->pos_epoch, n * 4) == hipSuccess && hipMalloc(&s->dmark, n * 4) == hipSuccess &&
-            hipMalloc(&s->cnt, n * 4) == hipSuccess && hipMalloc(&s->rank, n * 4) == hipSuccess &&
-            hipMalloc(&s->special, n * 4) == hipSuccess &&
-            hipMalloc(&s->seen, n) == hipSuccess && hipMalloc(&s->dsz, n * 8) == hipSuccess &&
-            hipMalloc(&s->hoff, n * 8) == hipSuccess;
+            hipMalloc(&s->tcnt, (n / PTILE + 1) * 4) == hipSuccess && hipMalloc(&s->special, n * 4) == hipSuccess &&
+            hipMalloc(&s->seen, n) == hipSuccess && hipMalloc(&s->tbytes, (n / PTILE + 1) * 8) == hipSuccess;
   s->pool_words = 4 * n + PWORDS;
+  const uint64_t nb = n < rtps_bsort::MAX_N ? n : rtps_bsort::MAX_N;
+  ok = ok && hipMalloc(&s->bh, rtps_bsort::hist_words(nb) * 4) == hipSuccess &&
+       hipMalloc(&s->bk, nb * 8) == hipSuccess && hipMalloc(&s->bk2, nb * 8) == hipSuccess;
   ok = ok && hipMalloc(&s->epochs, n * sizeof(Epoch)) == hipSuccess &&
        hipMalloc(&s->pool, s->pool_words * 4) == hipSuccess;
-  size_t b1 = 0, b2 = 0, b3 = 0;
+  size_t b1 = 0;
   ok = ok && rtps_sort_pairs(nullptr, b1, s->keys, s->skeys, s->vals, s->svals, (uint32_t)n, (int)32, st) == hipSuccess;
-  ok = ok && hipcub::DeviceScan::ExclusiveSum(nullptr, b2, s->cnt, s->rank, (int)n, st) == hipSuccess;
-  ok = ok && hipcub::DeviceScan::ExclusiveSum(nullptr, b3, s->dsz, s->hoff, (int)n, st) == hipSuccess;
-  s->tmp_bytes = b1 > b2 ? (b1 > b3 ? b1 : b3) : (b2 > b3 ? b2 : b3);
+  s->tmp_bytes = b1;
   ok = ok && hipMalloc(&s->tmp, s->tmp_bytes) == hipSuccess;
   if (!ok) { free_scratch(s); return false; }
   s->cap = n;
@@ -999,20 +1087,23 @@ int rtps_frag_assemble(FragState* s, hipStream_t st, const uint8_t* arena, uint6
   hipLaunchKernelGGL(k_keys, dim3(gb), dim3(FT), 0, st, records, n_records, max, s->keys, s->vals, s->pos_epoch,
                      s->dmark, s->seen, s->ctr, s->ptable[nw], s->wkey, s->wfirst, s->wF);
   size_t tb = s->tmp_bytes;
-  if (rtps_sort_pairs(s->tmp, tb, s->keys, s->skeys, s->vals, s->svals, (uint32_t)max, (int)32, st) !=
-      hipSuccess)
+  if (s->sort_mode == 0 && max <= rtps_bsort::MAX_N) {
+    if (rtps_bsort::sort_pairs(s->keys, (uint32_t)max, s->bh, s->bk, s->bk2, s->skeys, s->svals, st) != hipSuccess)
+      return RTPS_RX_EHIP;
+  } else if (rtps_sort_pairs(s->tmp, tb, s->keys, s->skeys, s->vals, s->svals, (uint32_t)max, (int)32, st) !=
+             hipSuccess) {
     return RTPS_RX_EHIP;
+  }
   hipLaunchKernelGGL(k_writers_fix, dim3(WCAP / FT), dim3(FT), 0, st, records, s->wkey, s->wfirst, s->wF, s->ctr);
   WalkArgs A{records, s->skeys, s->svals, max, s->wkey, s->wF, s->pend[o], s->ptable[o], s->pbits[o], s->epochs,
              s->special, s->pool, s->pool_words, s->pos_epoch, s->dmark, s->seen, s->ctr};
   hipLaunchKernelGGL(k_walk, dim3((uint32_t)hmin((max + FT - 1) / FT, 8192)), dim3(FT), 0, st, A);
-  hipLaunchKernelGGL(k_place_in, dim3(gb), dim3(FT), 0, st, s->dmark, s->epochs, max, s->cnt, s->dsz);
-  tb = s->tmp_bytes;
-  if (hipcub::DeviceScan::ExclusiveSum(s->tmp, tb, s->cnt, s->rank, (int)max, st) != hipSuccess) return RTPS_RX_EHIP;
-  tb = s->tmp_bytes;
-  if (hipcub::DeviceScan::ExclusiveSum(s->tmp, tb, s->dsz, s->hoff, (int)max, st) != hipSuccess) return RTPS_RX_EHIP;
-  hipLaunchKernelGGL(k_samples, dim3(gb), dim3(FT), 0, st, s->dmark, s->epochs, s->cnt, s->rank, s->dsz, s->hoff,
-                     max, *out);
+  const uint64_t tiles = (max + PTILE - 1) / PTILE;
+  hipLaunchKernelGGL(k_place_tiles, dim3((uint32_t)tiles), dim3(FT), 0, st, s->dmark, s->epochs, max, s->tcnt,
+                     s->tbytes);
+  hipLaunchKernelGGL(k_place_scan, dim3(1), dim3(FT), 0, st, s->tcnt, s->tbytes, tiles, *out);
+  hipLaunchKernelGGL(k_samples, dim3((uint32_t)tiles), dim3(FT), 0, st, s->dmark, s->epochs, s->tcnt, s->tbytes, max,
+                     *out);
   hipLaunchKernelGGL(k_pend_alloc, dim3(64), dim3(FT), 0, st, s->epochs, s->special, s->pend[nw], s->pbits[nw],
                      s->pool, s->ctr, s->now);
   hipLaunchKernelGGL(k_carry, dim3(1024), dim3(FT), 0, st, s->pend[o], s->pbytes[o], s->pbits[o], s->pend[nw],
@@ -1033,6 +1124,7 @@ int rtps_frag_assemble(FragState* s, hipStream_t st, const uint8_t* arena, uint6
 }
 
 void rtps_frag_set_clock(FragState* s, uint64_t now) { s->now = now; }
+void rtps_frag_set_sort(FragState* s, int mode) { s->sort_mode = mode; }
 
 int rtps_frag_gc(FragState* s, hipStream_t st, uint64_t expire_before, uint64_t* n_pending) {
   const int o = s->cur;

@@ -2021,6 +2021,20 @@ int rtps_rx_debug_ingest_path(rtps_rx_ctx* c, uint32_t path) {
   return RTPS_RX_OK;
 }
 
+/* test hook (not part of the public header): the reassembly's key sort, 0 = the
+   bucket sort of rtps_bsort.h up to its size limit, 1 = rocprim's device sort always
+   (same results) */
+int rtps_rx_debug_frag_sort(rtps_rx_ctx* c, uint32_t mode) {
+  if (!c || mode > 1u) return RTPS_RX_EINVAL;
+  (void)hipSetDevice(c->device);
+  if (!c->frag) {
+    c->frag = rtps_frag_state_new(c->device);
+    if (!c->frag) return RTPS_RX_ENOMEM;
+  }
+  rtps_frag_set_sort(c->frag, (int)mode);
+  return RTPS_RX_OK;
+}
+
 /* tuning hook (not part of the public header): see rtps_ingest_proxy_stamps */
 int rtps_rx_debug_proxy_stamps(rtps_rx_ctx* c, uint64_t* host, uint64_t n) {
   if (!c || !host) return RTPS_RX_EINVAL;

@@ -307,8 +307,14 @@ class MessageReceiver:
         fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
         _check(fn(self._h, path))
 
+    def debug_frag_sort(self, mode):
+        """Reassembly key sort: 0 the bucket sort (default, up to 1.5M records), 1 rocprim's device sort."""
+        fn = lib().rtps_rx_debug_frag_sort
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+        _check(fn(self._h, mode))
+
     def debug_set_mixed_pass(self, lds):
-        """The chained pass for mixed traffic: LDS tiles (True, the default) or the lane walk."""
+        """The chained pass for mixed traffic: the lane walk (False, the default) or LDS tiles."""
         fn = lib().rtps_rx_debug_set_mixed_pass
         fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
         _check(fn(self._h, 1 if lds else 0))

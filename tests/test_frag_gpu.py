@@ -44,8 +44,9 @@ def _run(rx, fa, dgrams_or_gen, label, **kw):
     return gpu
 
 
-@pytest.mark.parametrize("seed", [1, 2, 3])
-def test_soup_single_batch(rx, seed):
+@pytest.mark.parametrize("seed,sort", [(1, 0), (2, 0), (3, 0), (1, 1)])
+def test_soup_single_batch(rx, seed, sort):
+    rx.debug_frag_sort(sort)
     fa = oracle.FragAssembler()
     g = _run(rx, fa, frag_ref.soup(3000, seed), f"soup{seed}", align=1)
     assert g[3] > 100
@@ -80,8 +81,9 @@ def test_empty_and_no_frag_batches(rx):
     _run(rx, fa, lambda: oracle.gen(oracle.WL_C3, 5000), "C3 (no DATA_FRAG)")
 
 
-@pytest.mark.parametrize("n,batches", [(20000, 1), (20000, 7), (1 << 20, 1)])
-def test_c4_workload(rx, n, batches):
+@pytest.mark.parametrize("n,batches,sort", [(20000, 1, 0), (20000, 7, 0), (1 << 20, 1, 0), (1 << 20, 1, 1)])
+def test_c4_workload(rx, n, batches, sort):
+    rx.debug_frag_sort(sort)  # 1: rocprim's device sort instead of the bucket sort
     arena, off, ln = oracle.gen(oracle.WL_C4, n)
     fa = oracle.FragAssembler()
     step = (n + batches - 1) // batches
@@ -142,3 +144,48 @@ def test_c4_lossy_pending_bounded(rx):
         pend_nogc.append(fa_nogc.pending())
     assert pend_nogc[-1] > 3 * max(pend[1:]), (pend, pend_nogc)
     assert max(pend[2:]) <= 3 * n // 49 // 2, pend  # about two batches of lost samples at most
+
+
+def _key_hash(prefix, writer_key, sn):
+    """The device's 32-bit sort key of (writer GUID, SN) (rtps_frag.hip key_hash), vectorised over sn."""
+    g = np.frombuffer(bytes(prefix) + bytes(writer_key), dtype="<u4").astype(np.uint64)
+    sn = np.asarray(sn, dtype=np.int64).view(np.uint64)
+    m = np.uint64(0xFFFFFFFF)
+    h = np.full(sn.shape, 0x811C9DC5, dtype=np.uint64)
+    for x in (g[0], g[1], g[2], g[3], sn & m, (sn >> np.uint64(32)) & m):
+        h = ((h ^ x) * np.uint64(0x01000193)) & m
+    for sh, mul in ((16, 0x85EBCA6B), (13, 0xC2B2AE35)):
+        h ^= h >> np.uint64(sh)
+        h = (h * np.uint64(mul)) & m
+    h ^= h >> np.uint64(16)
+    return np.where(h == m, m - np.uint64(1), h)
+
+
+@pytest.mark.parametrize("sort", [0, 1])
+def test_bucket_sort_oversized_buckets(rx, sort):
+    """The bucket sort's two large-bucket paths (rtps_bsort.h): 12000 fragments of one
+    sample (one key: the bucket is already in key order) and 9000 one-fragment samples
+    whose keys share their top byte, in shuffled SN order (an LSD pass per key byte),
+    each beside a soup of other traffic; the same with rocprim's sort (sort=1)."""
+    rx.debug_frag_sort(sort)
+    rng = np.random.default_rng(7)
+    prefix, wk = bytes(range(100, 112)), b"\x00\x01\x05\x02"
+    fsz, nf = 16, 12000
+    order = rng.permutation(nf) + 1
+    payload = rng.integers(0, 256, nf * fsz, dtype=np.uint8).tobytes()
+    big = [frag_ref.datagram(prefix, [frag_ref.datafrag_sub(wk, 77, int(f), 1, fsz, nf * fsz,
+                                                            payload[(f - 1) * fsz:f * fsz])]) for f in order]
+    fa = oracle.FragAssembler()
+    g = _run(rx, fa, big, "one 12000-fragment sample")
+    assert g[3] == 1
+    sns = np.arange(1, 3_000_000, dtype=np.int64)
+    hit = sns[(_key_hash(prefix, wk, sns) >> np.uint64(24)) == np.uint64(0x5A)][:9000]
+    assert len(hit) == 9000
+    rng.shuffle(hit)
+    many = [frag_ref.datagram(prefix, [frag_ref.datafrag_sub(wk, int(sn), 1, 1, 8, 8, bytes([int(sn) & 255] * 8))])
+            for sn in hit]
+    mixed = many[:4500] + frag_ref.soup(600, 4) + many[4500:]
+    rx.frag_reset()  # the writer's fragment size is fixed per context: start over with the oracle
+    fa = oracle.FragAssembler()
+    g = _run(rx, fa, mixed, "9000 keys in one bucket")
+    assert g[3] >= 9000
