@@ -121,6 +121,7 @@ __device__ __forceinline__ void blk_zero(uint8_t* d, uint64_t n) {
   for (; b + 16 <= n; b += 16ull * FT) __builtin_memcpy(d + b, &z, 16);
   for (uint64_t t = (n & ~15ull) + threadIdx.x; t < n; t += FT) d[t] = 0;
 }
+__device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); }
 __device__ __forceinline__ bool is_frag(const rtps_record* r) { return r->kind == RTPS_DATA_FRAG && (r->route & RTPS_ROUTE_PASS); }
 
 __device__ __forceinline__ uint32_t wslot_find(const uint64_t* wkey, uint64_t h) {
@@ -134,8 +135,9 @@ __device__ __forceinline__ uint32_t wslot_find(const uint64_t* wkey, uint64_t h)
 }
 
 // ---- 1: sort keys ----
-// Also registers the batch's writers (step 2's input): each workgroup dedupes its
-// records' writers in LDS (the smallest record index per writer), then inserts each
+// Also registers the batch's writers (step 2's input): each wave dedupes its
+// records' writers with ballots (one LDS insert per distinct writer, by its first
+// lane: the smallest record index), each workgroup in LDS, then inserts each
 // distinct writer once into the persistent table and atomicMins its first record
 // there, so that only (workgroup, writer) pairs touch global atomics.
 constexpr uint32_t KW_SLOTS = 512;  // >= 2 x records per workgroup pass
@@ -152,28 +154,40 @@ __global__ __launch_bounds__(FT) void k_keys(const rtps_record* recs, const uint
   for (uint32_t j = threadIdx.x; j < KW_SLOTS; j += FT) { s_wk[j] = 0ull; s_wr[j] = NONE; }
   __syncthreads();
   const uint64_t n = min(*n_rec, max);
+  const uint32_t lane = threadIdx.x & 63u;
   for (uint64_t i0 = (uint64_t)blockIdx.x * FT; i0 < max; i0 += (uint64_t)gridDim.x * FT) {  // uniform trips
     const uint64_t i = i0 + threadIdx.x;
+    bool f = false;
+    uint64_t wh = 0;
     if (i < max) {
       uint32_t k = SENT;
       if (i < n && is_frag(recs + i)) {
         uint32_t g[4];
         guid_of(recs + i, g);
         k = key_hash(g, recs[i].sn);
-        const uint64_t wh = writer_hash(g);
-        uint32_t h = (uint32_t)(wh >> 7) & (KW_SLOTS - 1);
+        wh = writer_hash(g);
+        f = true;
+      }
+      keys[i] = k;
+      if (vals) vals[i] = (uint32_t)i;  // the device sort's values (the bucket sort derives them)
+      pos_epoch[i] = NONE;  // per-batch state, reset here instead of three memsets
+      dmark[i] = NONE;
+      seen[i] = 0;
+    }
+    // one LDS insert per distinct writer of the wave, by its lowest lane
+    for (uint64_t todo = __ballot(f); todo;) {
+      const uint32_t l = (uint32_t)__builtin_ctzll(todo);
+      const uint64_t lh = ((uint64_t)rl((uint32_t)(wh >> 32), l) << 32) | rl((uint32_t)wh, l);
+      todo &= ~__ballot(f && wh == lh);
+      if (lane == l) {
+        uint32_t h = (uint32_t)(lh >> 7) & (KW_SLOTS - 1);
         for (;;) {  // fewer distinct writers than slots: always ends
-          const unsigned long long old = atomicCAS(&s_wk[h], 0ull, (unsigned long long)wh);
-          if (old == 0ull || old == wh) break;
+          const unsigned long long old = atomicCAS(&s_wk[h], 0ull, (unsigned long long)lh);
+          if (old == 0ull || old == lh) break;
           h = (h + 1) & (KW_SLOTS - 1);
         }
         atomicMin(&s_wr[h], (uint32_t)i);
       }
-      keys[i] = k;
-      vals[i] = (uint32_t)i;
-      pos_epoch[i] = NONE;  // per-batch state, reset here instead of three memsets
-      dmark[i] = NONE;
-      seen[i] = 0;
     }
     __syncthreads();
     // flush the pass's writers: one persistent-table insert + atomicMin each
@@ -186,6 +200,11 @@ __global__ __launch_bounds__(FT) void k_keys(const rtps_record* recs, const uint
       uint32_t s = (uint32_t)(wh >> 7) & (WCAP - 1);
       uint32_t t = 0;
       for (; t < WCAP; ++t, s = (s + 1) & (WCAP - 1)) {
+        // a plain probe first: slots only go from 0 to a writer, and a writer seen in an
+        // earlier batch is found without an atomic (thousands of workgroups, few writers)
+        const uint64_t cur = __atomic_load_n((const unsigned long long*)&wkey[s], __ATOMIC_RELAXED);
+        if (cur == wh) break;
+        if (cur != 0) continue;
         const uint64_t old = atomicCAS((unsigned long long*)&wkey[s], 0ull, (unsigned long long)wh);
         if (old == 0 || old == wh) break;
       }
@@ -353,7 +372,6 @@ __device__ void walk_run_serial(const WalkArgs& A, uint64_t p, uint64_t p1) {
 
 constexpr uint32_t BMW = 1024;  // LDS bitmap words per wave: buffers of up to 32768 fragments
 
-__device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); }
 
 // The common run, decided without stepping: one new buffer (nothing carried
 // over), at most 64 records, each a single fragment of the writer's size with
@@ -364,20 +382,34 @@ __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t l) { return (uint32_
 // The same outcome as walk_run_wave's replay below (which handles the rest);
 // returns false, having written nothing but LDS, when the run is not of this
 // form.
-__device__ bool walk_run_regular(const WalkArgs& A, uint64_t p0, uint64_t p1, uint32_t lane, uint32_t* bm,
-                                 const uint32_t g[4], int64_t sn, uint32_t F) {
-  const uint64_t p = p0 + lane;
-  const bool act = p < p1;
-  uint32_t ri = 0, fs = 1, fis = 1, fsz = F, dsz = 0, fl = 0;
-  if (act) {
-    ri = A.svals[p];
-    const rtps_record* r = A.recs + ri;
-    fs = r->u.frag.frag_start;
-    fis = r->u.frag.frags_in_sub;
-    fsz = r->u.frag.frag_size;
-    dsz = r->u.frag.data_size;
-    fl = r->flags;
+// one lane's record of a short run (position p0 + lane), loaded once
+struct LaneRec {
+  bool act;
+  uint32_t ri, g[4], fs, fis, fsz, dsz, fl;
+  int64_t sn;
+};
+__device__ __forceinline__ LaneRec lane_rec(const WalkArgs& A, uint64_t p, uint64_t p1) {
+  LaneRec L;
+  L.act = p < p1;
+  L.ri = 0; L.g[0] = L.g[1] = L.g[2] = L.g[3] = 0; L.fs = 1; L.fis = 1; L.fsz = 0; L.dsz = 0; L.fl = 0; L.sn = 0;
+  if (L.act) {
+    L.ri = A.svals[p];
+    const rtps_record* r = A.recs + L.ri;
+    guid_of(r, L.g);
+    L.sn = r->sn;
+    L.fs = r->u.frag.frag_start;
+    L.fis = r->u.frag.frags_in_sub;
+    L.fsz = r->u.frag.frag_size;
+    L.dsz = r->u.frag.data_size;
+    L.fl = r->flags;
   }
+  return L;
+}
+__device__ bool walk_run_regular(const WalkArgs& A, uint64_t p0, uint64_t p1, uint32_t lane, uint32_t* bm,
+                                 const uint32_t g[4], int64_t sn, uint32_t F, const LaneRec& L) {
+  const uint64_t p = p0 + lane;
+  const bool act = L.act;
+  const uint32_t ri = L.ri, fs = L.fs, fis = L.fis, fsz = act ? L.fsz : F, dsz = L.dsz, fl = L.fl;
   const uint32_t ds0 = rl(dsz, 0);
   const uint32_t count = ds0 / F + (ds0 % F > 0);  // AssemblyBuffer::new with the first record (fsz == F)
   const uint32_t m = (uint32_t)(p1 - p0);
@@ -431,7 +463,27 @@ __device__ bool walk_run_regular(const WalkArgs& A, uint64_t p0, uint64_t p1, ui
 // One key run replayed by a wave: each lane loads one record's fields, the
 // wave steps through them in order with the fragment bitmap in LDS.  Runs that
 // mix keys or need a bigger bitmap fall back to walk_run_serial on lane 0.
-__device__ void walk_run_wave(const WalkArgs& A, uint64_t p0, uint64_t p1, uint32_t lane, uint32_t* bm) {
+__device__ void walk_run_wave(const WalkArgs& A, uint64_t p0, uint64_t p1, uint32_t lane, uint32_t* bm,
+                              uint32_t key) {
+  if (p1 - p0 <= 64) {
+    // a short run: every lane loads its record once; the run's key, the carried-over
+    // buffer and the writer's fragment size are then looked up with independent loads
+    const LaneRec L = lane_rec(A, p0 + lane, p1);
+    uint32_t g[4];
+    for (int k = 0; k < 4; ++k) g[k] = rl(L.g[k], 0);
+    const int64_t sn = (int64_t)(((uint64_t)rl((uint32_t)((uint64_t)L.sn >> 32), 0) << 32) | rl((uint32_t)L.sn, 0));
+    const bool bad = L.act && (!same_key(g, sn, L.g, L.sn) ||
+                               (uint64_t)(L.dsz / L.fsz + (L.dsz % L.fsz > 0)) > (uint64_t)BMW * 32);
+    const uint64_t wh = writer_hash(g);
+    const uint32_t ps = key & (PTCAP - 1), ws0 = (uint32_t)(wh >> 7) & (WCAP - 1);
+    const uint32_t pj = A.old_ptable[ps];
+    const uint64_t wk = A.wkey[ws0];
+    if (!__any(bad) && pj == NONE) {  // nothing carried over (the first probe is empty)
+      const uint32_t ws = wk == wh ? ws0 : (wk == 0 ? NONE : wslot_find(A.wkey, wh));
+      const uint32_t F = ws == NONE ? 0u : (A.wF[ws] & 0xffffu);
+      if (F != 0 && walk_run_regular(A, p0, p1, lane, bm, g, sn, F, L)) return;
+    }
+  }
   const rtps_record* r0 = A.recs + A.svals[p0];
   uint32_t g[4];
   guid_of(r0, g);
@@ -449,7 +501,6 @@ __device__ void walk_run_wave(const WalkArgs& A, uint64_t p0, uint64_t p1, uint3
     }
     ok = !__any(bad);
   }
-  const uint32_t key = A.skeys[p0];
   const uint32_t j = pend_lookup(A.old_ptable, A.old_pend, key, g, sn);
   if (ok && j != NONE && (uint64_t)A.old_pend[j].count > (uint64_t)BMW * 32) ok = false;
   if (!ok) {
@@ -458,7 +509,8 @@ __device__ void walk_run_wave(const WalkArgs& A, uint64_t p0, uint64_t p1, uint3
   }
   const uint32_t ws = wslot_find(A.wkey, writer_hash(g));
   const uint32_t F = ws == NONE ? 0u : (A.wF[ws] & 0xffffu);
-  if (j == NONE && p1 - p0 <= 64 && F != 0 && walk_run_regular(A, p0, p1, lane, bm, g, sn, F)) return;
+  if (j == NONE && p1 - p0 <= 64 && F != 0 && walk_run_regular(A, p0, p1, lane, bm, g, sn, F, lane_rec(A, p0 + lane, p1)))
+    return;
   uint32_t e = NONE, nset = 0, count = 0, ds = 0, eflags = 0, old_pend = NONE;
   bool started = false;
   if (j != NONE) {  // continue the buffer carried over from the previous batch
@@ -574,7 +626,7 @@ __global__ __launch_bounds__(FT) void k_walk(WalkArgs A) {
         if (b) { p1 += __builtin_ctzll(b); break; }
         p1 += 64;
       }
-      walk_run_wave(A, p0, p1, lane, bms[wave]);
+      walk_run_wave(A, p0, p1, lane, bms[wave], k0);
     }
   }
 }
@@ -659,8 +711,12 @@ __global__ __launch_bounds__(FT) void k_place_scan(uint32_t* tc, uint64_t* tb, u
   }
   if (threadIdx.x == 0) { *out.n_samples = cc; *out.heap_used = cb; }
 }
+// tc / tb: the tiles' exclusive prefixes (k_place_scan), or with self_scan (up to
+// SELF_SCAN tiles) their raw totals, which each workgroup then sums itself
+constexpr uint64_t SELF_SCAN = 2048;
 __global__ __launch_bounds__(FT) void k_samples(const uint32_t* dmark, Epoch* ep, const uint32_t* tc,
-                                                const uint64_t* tb, uint64_t max, rtps_frag_out out) {
+                                                const uint64_t* tb, uint64_t max, uint32_t self_scan,
+                                                rtps_frag_out out) {
   const uint64_t base = (uint64_t)blockIdx.x * PTILE + (uint64_t)threadIdx.x * PPT;
   uint32_t d[PPT];
   dmark16(dmark, base, max, d);
@@ -672,8 +728,22 @@ __global__ __launch_bounds__(FT) void k_samples(const uint32_t* dmark, Epoch* ep
   uint32_t ce, ct;
   uint64_t be, bt;
   blk_scan_cb(c, b, ce, be, ct, bt);
+  uint64_t pc, pb;
+  if (self_scan) {
+    pc = 0; pb = 0;
+    for (uint32_t t0 = 0; t0 < blockIdx.x; t0 += FT) {
+      const uint32_t t = t0 + threadIdx.x;
+      uint32_t xe, xt;
+      uint64_t ye, yt;
+      blk_scan_cb(t < blockIdx.x ? tc[t] : 0u, t < blockIdx.x ? tb[t] : 0ull, xe, ye, xt, yt);
+      pc += xt; pb += yt;
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) { *out.n_samples = pc + ct; *out.heap_used = pb + bt; }
+  } else {
+    pc = tc[blockIdx.x]; pb = tb[blockIdx.x];
+  }
   if (c == 0) return;
-  uint64_t k_rank = (uint64_t)tc[blockIdx.x] + ce, hoff = tb[blockIdx.x] + be;
+  uint64_t k_rank = pc + ce, hoff = pb + be;
   for (uint32_t k = 0; k < PPT; ++k) {
     const uint32_t e = d[k];
     if (e == NONE) continue;
@@ -699,10 +769,10 @@ __global__ __launch_bounds__(FT) void k_samples(const uint32_t* dmark, Epoch* ep
 }
 
 // pending epochs: room in the new pending store + carry their bitmaps
-__global__ __launch_bounds__(FT) void k_pend_alloc(Epoch* ep, const uint32_t* special, Pend* np, uint32_t* nbits,
-                                                   const uint32_t* pool, uint64_t* ctr, uint64_t now) {
+__device__ void pend_alloc_wg(Epoch* ep, const uint32_t* special, Pend* np, uint32_t* nbits, const uint32_t* pool,
+                              uint64_t* ctr, uint64_t now, uint32_t bid, uint32_t nb) {
   const uint64_t ns = ctr[C_SPECIAL];
-  for (uint64_t i = (uint64_t)blockIdx.x * FT + threadIdx.x; i < ns; i += (uint64_t)gridDim.x * FT) {
+  for (uint64_t i = (uint64_t)bid * FT + threadIdx.x; i < ns; i += (uint64_t)nb * FT) {
     Epoch& E = ep[special[i]];
     if (E.state != E_PENDING) continue;
     const uint64_t words = ((uint64_t)E.count + 31) / 32;
@@ -726,12 +796,12 @@ __global__ __launch_bounds__(FT) void k_pend_alloc(Epoch* ep, const uint32_t* sp
 }
 
 // old pending entries no record of this batch continued: move to the new store
-__global__ __launch_bounds__(FT) void k_carry(const Pend* op, const uint8_t* obytes, const uint32_t* obits,
-                                              Pend* np, uint8_t* nbytes, uint32_t* nbits, uint64_t* ctr) {
+__device__ void carry_wg(const Pend* op, const uint8_t* obytes, const uint32_t* obits, Pend* np, uint8_t* nbytes,
+                         uint32_t* nbits, uint64_t* ctr, uint32_t bid, uint32_t nb) {
   const uint64_t n_old = ctr[C_OLD_N];
   __shared__ uint64_t sj, sb, sw;
   __shared__ int ok;
-  for (uint64_t i = blockIdx.x; i < n_old; i += gridDim.x) {
+  for (uint64_t i = bid; i < n_old; i += nb) {
     const Pend& P = op[i];
     if (P.consumed) continue;
     const uint64_t words = ((uint64_t)P.count + 31) / 32;
@@ -752,16 +822,25 @@ __global__ __launch_bounds__(FT) void k_carry(const Pend* op, const uint8_t* oby
   }
 }
 
+// pending epochs and old entries no record continued get room in the new store
+// (one launch: workgroups [0, PA_WG) allocate, the rest carry)
+constexpr uint32_t PA_WG = 64, CARRY_WG = 1024;
+__global__ __launch_bounds__(FT) void k_pend(Epoch* ep, const uint32_t* special, const uint32_t* pool, uint64_t now,
+                                             const Pend* op, const uint8_t* obytes, const uint32_t* obits, Pend* np,
+                                             uint8_t* nbytes, uint32_t* nbits, uint64_t* ctr) {
+  if (blockIdx.x < PA_WG) pend_alloc_wg(ep, special, np, nbits, pool, ctr, now, blockIdx.x, PA_WG);
+  else carry_wg(op, obytes, obits, np, nbytes, nbits, ctr, blockIdx.x - PA_WG, gridDim.x - PA_WG);
+}
+
 // ---- 5: copy ----
 __device__ __forceinline__ uint8_t* epoch_dst(const Epoch& E, const rtps_frag_out& out, uint8_t* nbytes) {
   return E.state == E_DONE ? out.heap + E.dst : nbytes + E.dst;
 }
 // regular epochs: carried-over bytes (or zeros for a new pending buffer) first
-__global__ __launch_bounds__(FT) void k_init(const Epoch* ep, const uint32_t* special, const uint64_t* ctr,
-                                             const Pend* op, const uint8_t* obytes, uint8_t* nbytes,
-                                             rtps_frag_out out) {
+__device__ void init_wg(const Epoch* ep, const uint32_t* special, const uint64_t* ctr, const Pend* op,
+                        const uint8_t* obytes, uint8_t* nbytes, const rtps_frag_out& out, uint32_t bid, uint32_t nb) {
   const uint64_t ns = ctr[C_SPECIAL];
-  for (uint64_t i = blockIdx.x; i < ns; i += gridDim.x) {
+  for (uint64_t i = bid; i < ns; i += nb) {
     const Epoch& E = ep[special[i]];
     if (E.eflags & (EF_IRREGULAR | EF_SKIP)) continue;
     if (E.state == E_DONE && E.old_pend == NONE) continue;  // its spans cover every byte
@@ -889,13 +968,12 @@ __global__ __launch_bounds__(FT) void k_span(const rtps_record* recs, const uint
 
 // irregular epochs: the sequential replay (zero buffer, carried bytes, then every
 // record's clamped copy in record order), one workgroup each
-__global__ __launch_bounds__(FT) void k_serial(const rtps_record* recs, const uint8_t* arena,
-                                               const uint64_t* dgram_off, const uint32_t* svals,
-                                               const uint32_t* pos_epoch, const Epoch* ep, const uint32_t* special,
-                                               const uint64_t* ctr, const Pend* op, const uint8_t* obytes,
-                                               uint8_t* nbytes, rtps_frag_out out) {
+__device__ void serial_wg(const rtps_record* recs, const uint8_t* arena, const uint64_t* dgram_off,
+                          const uint32_t* svals, const uint32_t* pos_epoch, const Epoch* ep, const uint32_t* special,
+                          const uint64_t* ctr, const Pend* op, const uint8_t* obytes, uint8_t* nbytes,
+                          const rtps_frag_out& out, uint32_t bid, uint32_t nb) {
   const uint64_t ns = ctr[C_SPECIAL];
-  for (uint64_t i = blockIdx.x; i < ns; i += gridDim.x) {
+  for (uint64_t i = bid; i < ns; i += nb) {
     const uint32_t e = special[i];
     const Epoch& E = ep[e];
     if (!(E.eflags & EF_IRREGULAR) || (E.eflags & EF_SKIP)) continue;
@@ -926,17 +1004,35 @@ __global__ __launch_bounds__(FT) void k_serial(const rtps_record* recs, const ui
 
 // new pending hash table (for the next batch's walk); block 0 also finishes the batch
 // (k_finish's work: n_pending, and the pending count the next batch starts from)
-__global__ __launch_bounds__(FT) void k_ptable(const Pend* np, uint64_t* ctr, uint32_t* ptable, uint64_t* n_pending) {
+__device__ void ptable_wg(const Pend* np, uint64_t* ctr, uint32_t* ptable, uint64_t* n_pending, uint32_t bid,
+                          uint32_t nb) {
   const uint64_t n = min<uint64_t>(ctr[C_NEW_N], PCAP);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  if (bid == 0 && threadIdx.x == 0) {
     *n_pending = n | (ctr[C_OVERFLOW] ? (1ull << 63) : 0ull);
     ctr[C_OLD_N] = n;
   }
-  for (uint64_t j = (uint64_t)blockIdx.x * FT + threadIdx.x; j < n; j += (uint64_t)gridDim.x * FT) {
+  for (uint64_t j = (uint64_t)bid * FT + threadIdx.x; j < n; j += (uint64_t)nb * FT) {
     uint32_t g[4] = {np[j].guid[0], np[j].guid[1], np[j].guid[2], np[j].guid[3]};
     uint32_t s = key_hash(g, np[j].sn) & (PTCAP - 1);
     while (atomicCAS(&ptable[s], NONE, (uint32_t)j) != NONE) s = (s + 1) & (PTCAP - 1);
   }
+}
+
+// before the span copy, one launch: carried-over bytes / zeros of regular epochs
+// (k_span then writes their spans), the irregular epochs' serial replays (their
+// own bytes, disjoint from every span), and the next batch's pending table
+constexpr uint32_t INIT_WG = 1024, SERIAL_WG = 1024, PTAB_WG = PCAP / FT;
+__global__ __launch_bounds__(FT) void k_fill(const rtps_record* recs, const uint8_t* arena, const uint64_t* dgram_off,
+                                             const uint32_t* svals, const uint32_t* pos_epoch, const Epoch* ep,
+                                             const uint32_t* special, uint64_t* ctr, const Pend* op,
+                                             const uint8_t* obytes, uint8_t* nbytes, const Pend* np,
+                                             uint32_t* ptable, uint64_t* n_pending, rtps_frag_out out) {
+  const uint32_t b = blockIdx.x;
+  if (b < INIT_WG) init_wg(ep, special, ctr, op, obytes, nbytes, out, b, INIT_WG);
+  else if (b < INIT_WG + SERIAL_WG)
+    serial_wg(recs, arena, dgram_off, svals, pos_epoch, ep, special, ctr, op, obytes, nbytes, out, b - INIT_WG,
+              SERIAL_WG);
+  else ptable_wg(np, ctr, ptable, n_pending, b - INIT_WG - SERIAL_WG, PTAB_WG);
 }
 // garbage_collect_before (fragment_assembler.rs:216-224): the carried buffers last
 // modified before `expire` are marked consumed (the next batch neither finds nor
@@ -1084,10 +1180,11 @@ int rtps_frag_assemble(FragState* s, hipStream_t st, const uint8_t* arena, uint6
     (void)hipMemsetAsync(out->n_samples, 0, 8, st);
     (void)hipMemsetAsync(out->heap_used, 0, 8, st);
   }
-  hipLaunchKernelGGL(k_keys, dim3(gb), dim3(FT), 0, st, records, n_records, max, s->keys, s->vals, s->pos_epoch,
-                     s->dmark, s->seen, s->ctr, s->ptable[nw], s->wkey, s->wfirst, s->wF);
+  const bool bsort = s->sort_mode == 0 && max <= rtps_bsort::MAX_N;
+  hipLaunchKernelGGL(k_keys, dim3(gb), dim3(FT), 0, st, records, n_records, max, s->keys, bsort ? nullptr : s->vals,
+                     s->pos_epoch, s->dmark, s->seen, s->ctr, s->ptable[nw], s->wkey, s->wfirst, s->wF);
   size_t tb = s->tmp_bytes;
-  if (s->sort_mode == 0 && max <= rtps_bsort::MAX_N) {
+  if (bsort) {
     if (rtps_bsort::sort_pairs(s->keys, (uint32_t)max, s->bh, s->bk, s->bk2, s->skeys, s->svals, st) != hipSuccess)
       return RTPS_RX_EHIP;
   } else if (rtps_sort_pairs(s->tmp, tb, s->keys, s->skeys, s->vals, s->svals, (uint32_t)max, (int)32, st) !=
@@ -1101,23 +1198,20 @@ int rtps_frag_assemble(FragState* s, hipStream_t st, const uint8_t* arena, uint6
   const uint64_t tiles = (max + PTILE - 1) / PTILE;
   hipLaunchKernelGGL(k_place_tiles, dim3((uint32_t)tiles), dim3(FT), 0, st, s->dmark, s->epochs, max, s->tcnt,
                      s->tbytes);
-  hipLaunchKernelGGL(k_place_scan, dim3(1), dim3(FT), 0, st, s->tcnt, s->tbytes, tiles, *out);
+  const uint32_t self_scan = tiles <= SELF_SCAN;
+  if (!self_scan) hipLaunchKernelGGL(k_place_scan, dim3(1), dim3(FT), 0, st, s->tcnt, s->tbytes, tiles, *out);
   hipLaunchKernelGGL(k_samples, dim3((uint32_t)tiles), dim3(FT), 0, st, s->dmark, s->epochs, s->tcnt, s->tbytes, max,
-                     *out);
-  hipLaunchKernelGGL(k_pend_alloc, dim3(64), dim3(FT), 0, st, s->epochs, s->special, s->pend[nw], s->pbits[nw],
-                     s->pool, s->ctr, s->now);
-  hipLaunchKernelGGL(k_carry, dim3(1024), dim3(FT), 0, st, s->pend[o], s->pbytes[o], s->pbits[o], s->pend[nw],
-                     s->pbytes[nw], s->pbits[nw], s->ctr);
-  hipLaunchKernelGGL(k_init, dim3(1024), dim3(FT), 0, st, s->epochs, s->special, s->ctr, s->pend[o], s->pbytes[o],
-                     s->pbytes[nw], *out);
+                     self_scan, *out);
+  hipLaunchKernelGGL(k_pend, dim3(PA_WG + CARRY_WG), dim3(FT), 0, st, s->epochs, s->special, s->pool, s->now,
+                     s->pend[o], s->pbytes[o], s->pbits[o], s->pend[nw], s->pbytes[nw], s->pbits[nw], s->ctr);
+  hipLaunchKernelGGL(k_fill, dim3(INIT_WG + SERIAL_WG + PTAB_WG), dim3(FT), 0, st, records, arena, dgram_off, s->svals,
+                     s->pos_epoch, s->epochs, s->special, s->ctr, s->pend[o], s->pbytes[o], s->pbytes[nw], s->pend[nw],
+                     s->ptable[nw], out->n_pending, *out);
 #ifndef SPAN_GRID
 #define SPAN_GRID 8192
 #endif
   hipLaunchKernelGGL(k_span, dim3((uint32_t)hmin((max + FT - 1) / FT, SPAN_GRID)), dim3(FT), 0, st, records, arena,
                      arena_len, dgram_off, s->svals, s->pos_epoch, s->skeys, max, s->epochs, s->pbytes[nw], *out);
-  hipLaunchKernelGGL(k_serial, dim3(1024), dim3(FT), 0, st, records, arena, dgram_off, s->svals, s->pos_epoch,
-                     s->epochs, s->special, s->ctr, s->pend[o], s->pbytes[o], s->pbytes[nw], *out);
-  hipLaunchKernelGGL(k_ptable, dim3(PCAP / FT), dim3(FT), 0, st, s->pend[nw], s->ctr, s->ptable[nw], out->n_pending);
   if (hipGetLastError() != hipSuccess) return RTPS_RX_EHIP;
   s->cur = nw;
   return RTPS_RX_OK;

@@ -9,7 +9,7 @@ for v in $libs; do
   RTPS_RX_LIB=$v timeout -k 10 300 python -u -m pytest tests/test_frag_gpu.py -m gpu -x -q --timeout 200 \
     --timeout-method thread > gpurun_out/pytest_frag_$n.log 2>&1 || { echo "$n parity FAILED"; grep -E "^E " gpurun_out/pytest_frag_$n.log | head; exit 5; }
 done
-for round in 1 2; do
+for round in $(seq ${ROUNDS:-2}); do
   for v in $libs; do
     n=$(basename "$v" .so)
     RTPS_RX_LIB=$v timeout -k 10 200 python bench.py --workload C4 --no-c1 --no-cpu-baseline --no-e2e --no-cdr \
