@@ -883,11 +883,16 @@ constexpr uint32_t SL = RTPS_SPAN_LANES;   // lanes per record
 constexpr uint32_t SR = 64 / SL;           // records per wave instruction
 constexpr uint32_t SPAN_U = RTPS_SPAN_U;   // 16-B loads in flight per lane (SL x 16 x SPAN_U B per record per pass)
 static_assert(SL == 16 || SL == 32 || SL == 64, "lanes per record");
+typedef uint32_t nt_u4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) nt_u4 g_nt_u4 __attribute__((aligned(16)));
 __device__ __forceinline__ void span_st16(uint8_t* p, uint4 v) {
 #if RTPS_SPAN_NT  // non-temporal heap stores (written once, read by the host side later)
-  typedef uint32_t nt_u4 __attribute__((ext_vector_type(4)));
   nt_u4 w = {v.x, v.y, v.z, v.w};
-  __builtin_nontemporal_store(w, reinterpret_cast<nt_u4*>(p));
+#if defined(__HIP_DEVICE_COMPILE__)  // a global (not flat) store: heap and pending store are device memory
+  __builtin_nontemporal_store(w, (g_nt_u4*)(uintptr_t)p);
+#else
+  __builtin_memcpy(p, &w, 16);
+#endif
 #else
   gst16(p, v);
 #endif
