@@ -216,9 +216,11 @@ __global__ __launch_bounds__(FT) void k_keys(const rtps_record* recs, const uint
 }
 
 // ---- 2: writers: the fragment size of a writer is its first DATA_FRAG's ever (registered by k_keys) ----
-__global__ __launch_bounds__(FT) void k_writers_fix(const rtps_record* recs, const uint64_t* wkey, uint32_t* wfirst,
-                                                    uint32_t* wF, uint64_t* ctr) {
-  const uint32_t s = blockIdx.x * FT + threadIdx.x;
+// The walk reads it through writer_F (the batch's first record of a new writer);
+// after the walk, writers_fix_wg stores it for the next batches.
+__device__ void writers_fix_wg(const rtps_record* recs, const uint64_t* wkey, uint32_t* wfirst, uint32_t* wF,
+                               uint64_t* ctr, uint32_t bid) {
+  const uint32_t s = bid * FT + threadIdx.x;
   if (s == 0 && ctr[C_COUNT]) {  // k_keys found the writer table full
     atomicOr((unsigned long long*)&ctr[C_OVERFLOW], 1ull);
     ctr[C_COUNT] = 0ull;
@@ -247,6 +249,7 @@ struct WalkArgs {
   uint64_t max;
   const uint64_t* wkey;
   const uint32_t* wF;
+  const uint32_t* wfirst;
   Pend* old_pend;
   const uint32_t* old_ptable;
   const uint32_t* old_bits;
@@ -259,6 +262,16 @@ struct WalkArgs {
   uint8_t* seen;  // per position: consumed by a walk pass (collision runs)
   uint64_t* ctr;
 };
+
+// FragmentAssembler's fragment size of writer slot ws: fixed in an earlier batch, or
+// its first DATA_FRAG in this one (k_keys' atomicMin), or 0 for no writer
+__device__ __forceinline__ uint32_t writer_F(const WalkArgs& A, uint32_t ws) {
+  if (ws == NONE) return 0u;
+  const uint32_t f = A.wF[ws];
+  if (f & FIXED) return f & 0xffffu;
+  const uint32_t r = A.wfirst[ws];
+  return r == NONE ? 0u : (uint32_t)A.recs[r].u.frag.frag_size;
+}
 
 // Epoch ids are the sorted position where the epoch starts (its first record,
 // or the run's first position for a buffer carried over): distinct, no counter.
@@ -304,7 +317,7 @@ __device__ void walk_run_serial(const WalkArgs& A, uint64_t p, uint64_t p1) {
     const int64_t sn = r0->sn;
     const uint64_t wh = writer_hash(g);
     const uint32_t ws = wslot_find(A.wkey, wh);
-    const uint32_t F = ws == NONE ? 0u : (A.wF[ws] & 0xffffu);
+    const uint32_t F = writer_F(A, ws);
     // continue the buffer carried over from the previous batch
     uint32_t e = NONE;
     bool started = false;
@@ -480,7 +493,7 @@ __device__ void walk_run_wave(const WalkArgs& A, uint64_t p0, uint64_t p1, uint3
     const uint64_t wk = A.wkey[ws0];
     if (!__any(bad) && pj == NONE) {  // nothing carried over (the first probe is empty)
       const uint32_t ws = wk == wh ? ws0 : (wk == 0 ? NONE : wslot_find(A.wkey, wh));
-      const uint32_t F = ws == NONE ? 0u : (A.wF[ws] & 0xffffu);
+      const uint32_t F = writer_F(A, ws);
       if (F != 0 && walk_run_regular(A, p0, p1, lane, bm, g, sn, F, L)) return;
     }
   }
@@ -508,7 +521,7 @@ __device__ void walk_run_wave(const WalkArgs& A, uint64_t p0, uint64_t p1, uint3
     return;
   }
   const uint32_t ws = wslot_find(A.wkey, writer_hash(g));
-  const uint32_t F = ws == NONE ? 0u : (A.wF[ws] & 0xffffu);
+  const uint32_t F = writer_F(A, ws);
   if (j == NONE && p1 - p0 <= 64 && F != 0 && walk_run_regular(A, p0, p1, lane, bm, g, sn, F, lane_rec(A, p0 + lane, p1)))
     return;
   uint32_t e = NONE, nset = 0, count = 0, ds = 0, eflags = 0, old_pend = NONE;
@@ -714,10 +727,9 @@ __global__ __launch_bounds__(FT) void k_place_scan(uint32_t* tc, uint64_t* tb, u
 // tc / tb: the tiles' exclusive prefixes (k_place_scan), or with self_scan (up to
 // SELF_SCAN tiles) their raw totals, which each workgroup then sums itself
 constexpr uint64_t SELF_SCAN = 2048;
-__global__ __launch_bounds__(FT) void k_samples(const uint32_t* dmark, Epoch* ep, const uint32_t* tc,
-                                                const uint64_t* tb, uint64_t max, uint32_t self_scan,
-                                                rtps_frag_out out) {
-  const uint64_t base = (uint64_t)blockIdx.x * PTILE + (uint64_t)threadIdx.x * PPT;
+__device__ void samples_wg(const uint32_t* dmark, Epoch* ep, const uint32_t* tc, const uint64_t* tb, uint64_t max,
+                           uint32_t self_scan, const rtps_frag_out& out, uint32_t bid, uint32_t ntiles) {
+  const uint64_t base = (uint64_t)bid * PTILE + (uint64_t)threadIdx.x * PPT;
   uint32_t d[PPT];
   dmark16(dmark, base, max, d);
   uint32_t c = 0;
@@ -731,16 +743,16 @@ __global__ __launch_bounds__(FT) void k_samples(const uint32_t* dmark, Epoch* ep
   uint64_t pc, pb;
   if (self_scan) {
     pc = 0; pb = 0;
-    for (uint32_t t0 = 0; t0 < blockIdx.x; t0 += FT) {
+    for (uint32_t t0 = 0; t0 < bid; t0 += FT) {
       const uint32_t t = t0 + threadIdx.x;
       uint32_t xe, xt;
       uint64_t ye, yt;
-      blk_scan_cb(t < blockIdx.x ? tc[t] : 0u, t < blockIdx.x ? tb[t] : 0ull, xe, ye, xt, yt);
+      blk_scan_cb(t < bid ? tc[t] : 0u, t < bid ? tb[t] : 0ull, xe, ye, xt, yt);
       pc += xt; pb += yt;
     }
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) { *out.n_samples = pc + ct; *out.heap_used = pb + bt; }
+    if (bid == ntiles - 1 && threadIdx.x == 0) { *out.n_samples = pc + ct; *out.heap_used = pb + bt; }
   } else {
-    pc = tc[blockIdx.x]; pb = tb[blockIdx.x];
+    pc = tc[bid]; pb = tb[bid];
   }
   if (c == 0) return;
   uint64_t k_rank = pc + ce, hoff = pb + be;
@@ -822,14 +834,40 @@ __device__ void carry_wg(const Pend* op, const uint8_t* obytes, const uint32_t* 
   }
 }
 
-// pending epochs and old entries no record continued get room in the new store
-// (one launch: workgroups [0, PA_WG) allocate, the rest carry)
-constexpr uint32_t PA_WG = 64, CARRY_WG = 1024;
-__global__ __launch_bounds__(FT) void k_pend(Epoch* ep, const uint32_t* special, const uint32_t* pool, uint64_t now,
-                                             const Pend* op, const uint8_t* obytes, const uint32_t* obits, Pend* np,
-                                             uint8_t* nbytes, uint32_t* nbits, uint64_t* ctr) {
-  if (blockIdx.x < PA_WG) pend_alloc_wg(ep, special, np, nbits, pool, ctr, now, blockIdx.x, PA_WG);
-  else carry_wg(op, obytes, obits, np, nbytes, nbits, ctr, blockIdx.x - PA_WG, gridDim.x - PA_WG);
+// after the walk, one launch: completed samples (one workgroup per position tile),
+// pending epochs' room in the new store, old entries no record continued carried
+// over, and the batch's new writers' fragment sizes stored
+constexpr uint32_t PA_WG = 64, CARRY_WG = 1024, WFIX_WG = WCAP / FT;
+struct PlaceArgs {
+  const uint32_t* dmark;
+  Epoch* ep;
+  const uint32_t* tc;
+  const uint64_t* tb;
+  uint64_t max;
+  uint32_t self_scan, ntiles;
+  const uint32_t* special;
+  const uint32_t* pool;
+  uint64_t now;
+  const Pend* op;
+  const uint8_t* obytes;
+  const uint32_t* obits;
+  Pend* np;
+  uint8_t* nbytes;
+  uint32_t* nbits;
+  uint64_t* ctr;
+  const rtps_record* recs;
+  const uint64_t* wkey;
+  uint32_t* wfirst;
+  uint32_t* wF;
+};
+__global__ __launch_bounds__(FT) void k_place(PlaceArgs P, rtps_frag_out out) {
+  uint32_t b = blockIdx.x;
+  if (b < P.ntiles) { samples_wg(P.dmark, P.ep, P.tc, P.tb, P.max, P.self_scan, out, b, P.ntiles); return; }
+  b -= P.ntiles;
+  if (b < PA_WG) { pend_alloc_wg(P.ep, P.special, P.np, P.nbits, P.pool, P.ctr, P.now, b, PA_WG); return; }
+  b -= PA_WG;
+  if (b < CARRY_WG) { carry_wg(P.op, P.obytes, P.obits, P.np, P.nbytes, P.nbits, P.ctr, b, CARRY_WG); return; }
+  writers_fix_wg(P.recs, P.wkey, P.wfirst, P.wF, P.ctr, b - CARRY_WG);
 }
 
 // ---- 5: copy ----
@@ -1196,8 +1234,7 @@ int rtps_frag_assemble(FragState* s, hipStream_t st, const uint8_t* arena, uint6
              hipSuccess) {
     return RTPS_RX_EHIP;
   }
-  hipLaunchKernelGGL(k_writers_fix, dim3(WCAP / FT), dim3(FT), 0, st, records, s->wkey, s->wfirst, s->wF, s->ctr);
-  WalkArgs A{records, s->skeys, s->svals, max, s->wkey, s->wF, s->pend[o], s->ptable[o], s->pbits[o], s->epochs,
+  WalkArgs A{records, s->skeys, s->svals, max, s->wkey, s->wF, s->wfirst, s->pend[o], s->ptable[o], s->pbits[o], s->epochs,
              s->special, s->pool, s->pool_words, s->pos_epoch, s->dmark, s->seen, s->ctr};
   hipLaunchKernelGGL(k_walk, dim3((uint32_t)hmin((max + FT - 1) / FT, 8192)), dim3(FT), 0, st, A);
   const uint64_t tiles = (max + PTILE - 1) / PTILE;
@@ -1205,10 +1242,10 @@ int rtps_frag_assemble(FragState* s, hipStream_t st, const uint8_t* arena, uint6
                      s->tbytes);
   const uint32_t self_scan = tiles <= SELF_SCAN;
   if (!self_scan) hipLaunchKernelGGL(k_place_scan, dim3(1), dim3(FT), 0, st, s->tcnt, s->tbytes, tiles, *out);
-  hipLaunchKernelGGL(k_samples, dim3((uint32_t)tiles), dim3(FT), 0, st, s->dmark, s->epochs, s->tcnt, s->tbytes, max,
-                     self_scan, *out);
-  hipLaunchKernelGGL(k_pend, dim3(PA_WG + CARRY_WG), dim3(FT), 0, st, s->epochs, s->special, s->pool, s->now,
-                     s->pend[o], s->pbytes[o], s->pbits[o], s->pend[nw], s->pbytes[nw], s->pbits[nw], s->ctr);
+  const PlaceArgs P{s->dmark, s->epochs, s->tcnt, s->tbytes, max, self_scan, (uint32_t)tiles, s->special, s->pool,
+                    s->now, s->pend[o], s->pbytes[o], s->pbits[o], s->pend[nw], s->pbytes[nw], s->pbits[nw], s->ctr,
+                    records, s->wkey, s->wfirst, s->wF};
+  hipLaunchKernelGGL(k_place, dim3((uint32_t)tiles + PA_WG + CARRY_WG + WFIX_WG), dim3(FT), 0, st, P, *out);
   hipLaunchKernelGGL(k_fill, dim3(INIT_WG + SERIAL_WG + PTAB_WG), dim3(FT), 0, st, records, arena, dgram_off, s->svals,
                      s->pos_epoch, s->epochs, s->special, s->ctr, s->pend[o], s->pbytes[o], s->pbytes[nw], s->pend[nw],
                      s->ptable[nw], out->n_pending, *out);
