@@ -69,8 +69,17 @@ __global__ __launch_bounds__(BT) void k_hist(const uint32_t* keys, uint32_t n, u
   for (uint32_t b = threadIdx.x; b < NB; b += BT) H[(uint64_t)b * T + t] = h[b];
 }
 
-// per bucket b: H[b][t] -> exclusive prefix over tiles t, tot[b] = the bucket's count
-__global__ __launch_bounds__(BT) void k_colscan(uint32_t* H, uint32_t T, uint32_t* tot) {
+// per bucket b: H[b][t] -> exclusive prefix over tiles t, tot[b] = the bucket's count.
+// Workgroups past the NB buckets run the caller's side job (side(i), i < side.wgs,
+// BT threads): work that needs the keys' producer finished and must be done
+// before the sorted output is used, without a launch of its own.
+struct NoSide {
+  uint32_t wgs = 0;
+  __device__ void operator()(uint32_t) const {}
+};
+template <class Side>
+__global__ __launch_bounds__(BT) void k_colscan(uint32_t* H, uint32_t T, uint32_t* tot, Side side) {
+  if (blockIdx.x >= NB) { side(blockIdx.x - NB); return; }
   __shared__ uint32_t s[BT];
   uint32_t* h = H + (uint64_t)blockIdx.x * T;
   const uint32_t t0 = 2 * threadIdx.x;
@@ -264,13 +273,14 @@ __global__ __launch_bounds__(ST) void k_sub(uint64_t* bk, uint64_t* tmp, uint32_
 // scratch: H = NB x ceil(n / 4096) + NB u32, bk and tmp = n u64 each; n <= MAX_N
 inline size_t hist_words(uint64_t n) { return (size_t)NB * (size_t)((n + TILE - 1) / TILE) + NB; }
 
+template <class Side = NoSide>
 inline hipError_t sort_pairs(const uint32_t* keys, uint32_t n, uint32_t* H, uint64_t* bk, uint64_t* tmp,
-                             uint32_t* skeys, uint32_t* svals, hipStream_t st) {
+                             uint32_t* skeys, uint32_t* svals, hipStream_t st, const Side& side = Side()) {
   if (n == 0 || n > MAX_N) return hipErrorInvalidValue;
   const uint32_t T = (n + TILE - 1) / TILE;
   uint32_t* tot = H + (size_t)NB * T;
   hipLaunchKernelGGL(k_hist, dim3(T), dim3(BT), 0, st, keys, n, T, H);
-  hipLaunchKernelGGL(k_colscan, dim3(NB), dim3(BT), 0, st, H, T, tot);
+  hipLaunchKernelGGL(k_colscan<Side>, dim3(NB + side.wgs), dim3(BT), 0, st, H, T, tot, side);
   hipLaunchKernelGGL(k_scatter, dim3(T), dim3(BT), 0, st, keys, n, T, H, tot, bk);
   hipLaunchKernelGGL(k_sub, dim3(NR), dim3(ST), 0, st, bk, tmp, n, tot, skeys, svals);
   return hipGetLastError();

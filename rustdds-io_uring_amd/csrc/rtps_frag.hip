@@ -135,84 +135,122 @@ __device__ __forceinline__ uint32_t wslot_find(const uint64_t* wkey, uint64_t h)
 }
 
 // ---- 1: sort keys ----
-// Also registers the batch's writers (step 2's input): each wave dedupes its
+// Also collects the batch's writers (step 2's input): each wave dedupes its
 // records' writers with ballots (one LDS insert per distinct writer, by its first
-// lane: the smallest record index), each workgroup in LDS, then inserts each
-// distinct writer once into the persistent table and atomicMins its first record
-// there, so that only (workgroup, writer) pairs touch global atomics.
-constexpr uint32_t KW_SLOTS = 512;  // >= 2 x records per workgroup pass
+// lane: the smallest record index), each workgroup in LDS, and stages its first
+// WST distinct writers with their first records (no global atomics: a thousand
+// workgroups would all hit the same few writers' words).  writers_reg_wg merges
+// the stages into the persistent table; a workgroup's writers past WST go there
+// directly.
+constexpr uint32_t WST = 8;       // staged writers per k_keys workgroup
+constexpr uint32_t KGRID = 2048;  // k_keys workgroups at most
+__device__ void writer_insert(uint64_t wh, uint32_t r, uint64_t* wkey, uint32_t* wfirst, const uint32_t* wF,
+                              uint64_t* ctr) {
+  uint32_t s = (uint32_t)(wh >> 7) & (WCAP - 1);
+  uint32_t t = 0;
+  for (; t < WCAP; ++t, s = (s + 1) & (WCAP - 1)) {
+    // a plain probe first: slots only go from 0 to a writer
+    const uint64_t cur = __atomic_load_n((const unsigned long long*)&wkey[s], __ATOMIC_RELAXED);
+    if (cur == wh) break;
+    if (cur != 0) continue;
+    const uint64_t old = atomicCAS((unsigned long long*)&wkey[s], 0ull, (unsigned long long)wh);
+    if (old == 0 || old == wh) break;
+  }
+  if (t == WCAP) { ctr[C_COUNT] = 1ull; return; }  // table full: reported by writers_fix_wg
+  // wfirst only decreases: a plain read skips the atomic when an earlier record is in
+  if (!(wF[s] & FIXED) && r < __atomic_load_n(&wfirst[s], __ATOMIC_RELAXED)) atomicMin(&wfirst[s], r);
+}
+constexpr uint32_t KPT = 4, KPASS = FT * KPT;  // records per thread / per workgroup pass
+constexpr uint32_t KW_SLOTS = 2 * KPASS;       // >= 2 x records per workgroup pass
 __global__ __launch_bounds__(FT) void k_keys(const rtps_record* recs, const uint64_t* n_rec, uint64_t max,
                                              uint32_t* keys, uint32_t* vals, uint32_t* pos_epoch, uint32_t* dmark,
                                              uint8_t* seen, uint64_t* ctr, uint32_t* new_ptable, uint64_t* wkey,
-                                             uint32_t* wfirst, const uint32_t* wF) {
+                                             uint32_t* wfirst, const uint32_t* wF, uint64_t* wst_key,
+                                             uint32_t* wst_rec) {
   __shared__ unsigned long long s_wk[KW_SLOTS];
   __shared__ uint32_t s_wr[KW_SLOTS];
+  __shared__ uint32_t s_nst;
   // the batch's counters and the next pending table start empty (instead of two memsets)
   if (blockIdx.x == 0 && threadIdx.x < C_COUNT - C_NEW_N) ctr[C_NEW_N + threadIdx.x] = 0ull;
   for (uint64_t t = (uint64_t)blockIdx.x * FT + threadIdx.x; t < PTCAP; t += (uint64_t)gridDim.x * FT)
     new_ptable[t] = NONE;
   for (uint32_t j = threadIdx.x; j < KW_SLOTS; j += FT) { s_wk[j] = 0ull; s_wr[j] = NONE; }
+  if (threadIdx.x == 0) s_nst = 0u;
   __syncthreads();
   const uint64_t n = min(*n_rec, max);
   const uint32_t lane = threadIdx.x & 63u;
-  for (uint64_t i0 = (uint64_t)blockIdx.x * FT; i0 < max; i0 += (uint64_t)gridDim.x * FT) {  // uniform trips
-    const uint64_t i = i0 + threadIdx.x;
-    bool f = false;
-    uint64_t wh = 0;
-    if (i < max) {
-      uint32_t k = SENT;
-      if (i < n && is_frag(recs + i)) {
-        uint32_t g[4];
-        guid_of(recs + i, g);
-        k = key_hash(g, recs[i].sn);
-        wh = writer_hash(g);
-        f = true;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * KPASS; i0 < max; i0 += (uint64_t)gridDim.x * KPASS) {  // uniform trips
+    // each thread's KPT records: bytes 0..39 (kind @6, GUID @8..23, route @30, sn @32)
+    // loaded together, without a dependent second load for DATA_FRAG records
+    uint4 ra[KPT], rb[KPT];
+    uint64_t rs[KPT];
+#pragma unroll
+    for (uint32_t k = 0; k < KPT; ++k) {
+      const uint64_t i = i0 + k * FT + threadIdx.x;
+      ra[k] = rb[k] = make_uint4(0, 0, 0, 0);
+      rs[k] = 0;
+      if (i < n) {
+        const uint4* q = reinterpret_cast<const uint4*>(recs + i);
+        ra[k] = q[0];
+        rb[k] = q[1];
+        rs[k] = *reinterpret_cast<const uint64_t*>(q + 2);
       }
-      keys[i] = k;
-      if (vals) vals[i] = (uint32_t)i;  // the device sort's values (the bucket sort derives them)
-      pos_epoch[i] = NONE;  // per-batch state, reset here instead of three memsets
-      dmark[i] = NONE;
-      seen[i] = 0;
     }
-    // one LDS insert per distinct writer of the wave, by its lowest lane
-    for (uint64_t todo = __ballot(f); todo;) {
-      const uint32_t l = (uint32_t)__builtin_ctzll(todo);
-      const uint64_t lh = ((uint64_t)rl((uint32_t)(wh >> 32), l) << 32) | rl((uint32_t)wh, l);
-      todo &= ~__ballot(f && wh == lh);
-      if (lane == l) {
-        uint32_t h = (uint32_t)(lh >> 7) & (KW_SLOTS - 1);
-        for (;;) {  // fewer distinct writers than slots: always ends
-          const unsigned long long old = atomicCAS(&s_wk[h], 0ull, (unsigned long long)lh);
-          if (old == 0ull || old == lh) break;
-          h = (h + 1) & (KW_SLOTS - 1);
+#pragma unroll
+    for (uint32_t kk = 0; kk < KPT; ++kk) {
+      const uint64_t i = i0 + kk * FT + threadIdx.x;
+      bool f = false;
+      uint64_t wh = 0;
+      if (i < max) {
+        uint32_t k = SENT;
+        const uint32_t kind = (ra[kk].y >> 16) & 0xffu, route = (rb[kk].w >> 16) & 0xffu;
+        if (i < n && kind == RTPS_DATA_FRAG && (route & RTPS_ROUTE_PASS)) {  // is_frag
+          const uint32_t g[4] = {ra[kk].z, ra[kk].w, rb[kk].x, rb[kk].y};  // guid_of
+          k = key_hash(g, (int64_t)rs[kk]);
+          wh = writer_hash(g);
+          f = true;
         }
-        atomicMin(&s_wr[h], (uint32_t)i);
+        keys[i] = k;
+        if (vals) vals[i] = (uint32_t)i;  // the device sort's values (the bucket sort derives them)
+        pos_epoch[i] = NONE;  // per-batch state, reset here instead of three memsets
+        dmark[i] = NONE;
+        seen[i] = 0;
+      }
+      // one LDS insert per distinct writer of the wave, by its lowest lane
+      for (uint64_t todo = __ballot(f); todo;) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(todo);
+        const uint64_t lh = ((uint64_t)rl((uint32_t)(wh >> 32), l) << 32) | rl((uint32_t)wh, l);
+        todo &= ~__ballot(f && wh == lh);
+        if (lane == l) {
+          uint32_t h = (uint32_t)(lh >> 7) & (KW_SLOTS - 1);
+          for (;;) {  // fewer distinct writers than slots: always ends
+            const unsigned long long old = atomicCAS(&s_wk[h], 0ull, (unsigned long long)lh);
+            if (old == 0ull || old == lh) break;
+            h = (h + 1) & (KW_SLOTS - 1);
+          }
+          atomicMin(&s_wr[h], (uint32_t)i);
+        }
       }
     }
     __syncthreads();
-    // flush the pass's writers: one persistent-table insert + atomicMin each
+    // stage the pass's writers (or insert them directly past WST)
     for (uint32_t j = threadIdx.x; j < KW_SLOTS; j += FT) {
       const uint64_t wh = s_wk[j];
       if (!wh) continue;
       const uint32_t r = s_wr[j];
       s_wk[j] = 0ull;
       s_wr[j] = NONE;
-      uint32_t s = (uint32_t)(wh >> 7) & (WCAP - 1);
-      uint32_t t = 0;
-      for (; t < WCAP; ++t, s = (s + 1) & (WCAP - 1)) {
-        // a plain probe first: slots only go from 0 to a writer, and a writer seen in an
-        // earlier batch is found without an atomic (thousands of workgroups, few writers)
-        const uint64_t cur = __atomic_load_n((const unsigned long long*)&wkey[s], __ATOMIC_RELAXED);
-        if (cur == wh) break;
-        if (cur != 0) continue;
-        const uint64_t old = atomicCAS((unsigned long long*)&wkey[s], 0ull, (unsigned long long)wh);
-        if (old == 0 || old == wh) break;
+      const uint32_t q = atomicAdd(&s_nst, 1u);
+      if (q < WST) {
+        wst_key[(uint64_t)blockIdx.x * WST + q] = wh;
+        wst_rec[(uint64_t)blockIdx.x * WST + q] = r;
+      } else {
+        writer_insert(wh, r, wkey, wfirst, wF, ctr);
       }
-      if (t == WCAP) { ctr[C_COUNT] = 1ull; continue; }  // table full: reported by k_writers_fix
-      if (!(wF[s] & FIXED)) atomicMin(&wfirst[s], r);
     }
     __syncthreads();
   }
+  for (uint32_t q = s_nst + threadIdx.x; q < WST; q += FT) wst_key[(uint64_t)blockIdx.x * WST + q] = 0ull;
 }
 
 // ---- 2: writers: the fragment size of a writer is its first DATA_FRAG's ever (registered by k_keys) ----
@@ -229,6 +267,59 @@ __device__ void writers_fix_wg(const rtps_record* recs, const uint64_t* wkey, ui
   wF[s] = (uint32_t)recs[wfirst[s]].u.frag.frag_size | FIXED;
   wfirst[s] = NONE;
 }
+
+// merge k_keys' staged writers into the persistent table: WREG_WG workgroups take
+// a range of the stages each (all loads in flight at once), dedupe it in LDS, and
+// insert each distinct writer: a few workgroups per writer's words, not a thousand
+constexpr uint32_t WREG_WG = 16, WR_SLOTS = 1024, WR_U = 4;
+__device__ void writers_reg_wg(const uint64_t* wst_key, const uint32_t* wst_rec, uint32_t n_st, uint64_t* wkey,
+                               uint32_t* wfirst, const uint32_t* wF, uint64_t* ctr, uint32_t part) {
+  __shared__ unsigned long long s_k[WR_SLOTS];
+  __shared__ uint32_t s_r[WR_SLOTS];
+  for (uint32_t j = threadIdx.x; j < WR_SLOTS; j += FT) { s_k[j] = 0ull; s_r[j] = NONE; }
+  __syncthreads();
+  const uint32_t per = (n_st + WREG_WG - 1) / WREG_WG, lo = part * per, hi = min(lo + per, n_st);
+  for (uint32_t e0 = lo; e0 < hi; e0 += FT * WR_U) {
+    uint64_t k[WR_U];
+    uint32_t r[WR_U];
+#pragma unroll
+    for (uint32_t u = 0; u < WR_U; ++u) {
+      const uint32_t e = e0 + u * FT + threadIdx.x;
+      k[u] = e < hi ? wst_key[e] : 0ull;
+      r[u] = e < hi ? wst_rec[e] : NONE;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < WR_U; ++u) {
+      if (!k[u]) continue;
+      uint32_t h = (uint32_t)(k[u] >> 23) & (WR_SLOTS - 1), t = 0;
+      for (; t < WR_SLOTS; ++t, h = (h + 1) & (WR_SLOTS - 1)) {
+        const unsigned long long old = atomicCAS(&s_k[h], 0ull, (unsigned long long)k[u]);
+        if (old == 0ull || old == k[u]) break;
+      }
+      if (t < WR_SLOTS) atomicMin(&s_r[h], r[u]);
+      else writer_insert(k[u], r[u], wkey, wfirst, wF, ctr);  // more writers than LDS slots
+    }
+  }
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < WR_SLOTS; j += FT)
+    if (s_k[j]) writer_insert(s_k[j], s_r[j], wkey, wfirst, wF, ctr);
+}
+__global__ __launch_bounds__(FT) void k_wreg(const uint64_t* wst_key, const uint32_t* wst_rec, uint32_t n_st,
+                                             uint64_t* wkey, uint32_t* wfirst, const uint32_t* wF, uint64_t* ctr) {
+  writers_reg_wg(wst_key, wst_rec, n_st, wkey, wfirst, wF, ctr, blockIdx.x);
+}
+// the same as the bucket sort's side job
+struct WregSide {
+  uint32_t wgs;
+  const uint64_t* wst_key;
+  const uint32_t* wst_rec;
+  uint32_t n_st;
+  uint64_t* wkey;
+  uint32_t* wfirst;
+  const uint32_t* wF;
+  uint64_t* ctr;
+  __device__ void operator()(uint32_t i) const { writers_reg_wg(wst_key, wst_rec, n_st, wkey, wfirst, wF, ctr, i); }
+};
 
 // ---- 3: walk ----
 __device__ uint32_t pend_lookup(const uint32_t* ptable, const Pend* pend, uint32_t kh, const uint32_t g[4],
@@ -1115,6 +1206,8 @@ struct FragState {
   uint64_t* wkey = nullptr;
   uint32_t* wfirst = nullptr;
   uint32_t* wF = nullptr;
+  uint64_t* wst_key = nullptr;  // k_keys' staged writers (KGRID x WST)
+  uint32_t* wst_rec = nullptr;
   Pend* pend[2] = {nullptr, nullptr};
   uint8_t* pbytes[2] = {nullptr, nullptr};
   uint32_t* pbits[2] = {nullptr, nullptr};
@@ -1179,7 +1272,8 @@ FragState* rtps_frag_state_new(int device) {
   if (!s) return nullptr;
   s->device = device;
   bool ok = hipMalloc(&s->wkey, WCAP * 8) == hipSuccess && hipMalloc(&s->wfirst, WCAP * 4) == hipSuccess &&
-            hipMalloc(&s->wF, WCAP * 4) == hipSuccess && hipMalloc(&s->ctr, (C_COUNT + 1) * 8) == hipSuccess;  // + the writer-table-full word
+            hipMalloc(&s->wF, WCAP * 4) == hipSuccess && hipMalloc(&s->ctr, (C_COUNT + 1) * 8) == hipSuccess &&
+            hipMalloc(&s->wst_key, KGRID * WST * 8) == hipSuccess && hipMalloc(&s->wst_rec, KGRID * WST * 4) == hipSuccess;  // + the writer-table-full word
   for (int k = 0; k < 2 && ok; ++k)
     ok = hipMalloc(&s->pend[k], PCAP * sizeof(Pend)) == hipSuccess && hipMalloc(&s->pbytes[k], PBYTES) == hipSuccess &&
          hipMalloc(&s->pbits[k], PWORDS * 4) == hipSuccess && hipMalloc(&s->ptable[k], PTCAP * 4) == hipSuccess;
@@ -1194,7 +1288,7 @@ FragState* rtps_frag_state_new(int device) {
 void rtps_frag_state_free(FragState* s) {
   if (!s) return;
   free_scratch(s);
-  void* ptrs[] = {s->wkey, s->wfirst, s->wF, s->ctr, s->pend[0], s->pend[1], s->pbytes[0], s->pbytes[1],
+  void* ptrs[] = {s->wkey, s->wfirst, s->wF, s->ctr, s->wst_key, s->wst_rec, s->pend[0], s->pend[1], s->pbytes[0], s->pbytes[1],
                   s->pbits[0], s->pbits[1], s->ptable[0], s->ptable[1]};
   for (void* p : ptrs) if (p) (void)hipFree(p);
   delete s;
@@ -1218,21 +1312,26 @@ int rtps_frag_assemble(FragState* s, hipStream_t st, const uint8_t* arena, uint6
   const uint64_t max = max_records ? max_records : 1;
   if (!grow(s, max, st)) return RTPS_RX_ENOMEM;
   const int o = s->cur, nw = s->cur ^ 1;
-  const uint32_t gb = (uint32_t)hmin((max + FT - 1) / FT, 8192);
+  const uint32_t gk = (uint32_t)hmin((max + KPASS - 1) / KPASS, KGRID);
   if (max_records == 0) {
     (void)hipMemsetAsync(out->n_samples, 0, 8, st);
     (void)hipMemsetAsync(out->heap_used, 0, 8, st);
   }
   const bool bsort = s->sort_mode == 0 && max <= rtps_bsort::MAX_N;
-  hipLaunchKernelGGL(k_keys, dim3(gb), dim3(FT), 0, st, records, n_records, max, s->keys, bsort ? nullptr : s->vals,
-                     s->pos_epoch, s->dmark, s->seen, s->ctr, s->ptable[nw], s->wkey, s->wfirst, s->wF);
+  hipLaunchKernelGGL(k_keys, dim3(gk), dim3(FT), 0, st, records, n_records, max, s->keys, bsort ? nullptr : s->vals,
+                     s->pos_epoch, s->dmark, s->seen, s->ctr, s->ptable[nw], s->wkey, s->wfirst, s->wF, s->wst_key,
+                     s->wst_rec);
   size_t tb = s->tmp_bytes;
-  if (bsort) {
-    if (rtps_bsort::sort_pairs(s->keys, (uint32_t)max, s->bh, s->bk, s->bk2, s->skeys, s->svals, st) != hipSuccess)
+  const WregSide wreg{WREG_WG, s->wst_key, s->wst_rec, gk * WST, s->wkey, s->wfirst, s->wF, s->ctr};
+  if (bsort) {  // the writers' merge rides on the sort's column-scan launch
+    if (rtps_bsort::sort_pairs(s->keys, (uint32_t)max, s->bh, s->bk, s->bk2, s->skeys, s->svals, st, wreg) !=
+        hipSuccess)
       return RTPS_RX_EHIP;
-  } else if (rtps_sort_pairs(s->tmp, tb, s->keys, s->skeys, s->vals, s->svals, (uint32_t)max, (int)32, st) !=
-             hipSuccess) {
-    return RTPS_RX_EHIP;
+  } else {
+    if (rtps_sort_pairs(s->tmp, tb, s->keys, s->skeys, s->vals, s->svals, (uint32_t)max, (int)32, st) != hipSuccess)
+      return RTPS_RX_EHIP;
+    hipLaunchKernelGGL(k_wreg, dim3(WREG_WG), dim3(FT), 0, st, s->wst_key, s->wst_rec, gk * WST, s->wkey, s->wfirst,
+                       s->wF, s->ctr);
   }
   WalkArgs A{records, s->skeys, s->svals, max, s->wkey, s->wF, s->wfirst, s->pend[o], s->ptable[o], s->pbits[o], s->epochs,
              s->special, s->pool, s->pool_words, s->pos_epoch, s->dmark, s->seen, s->ctr};

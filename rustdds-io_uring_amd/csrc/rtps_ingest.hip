@@ -65,7 +65,6 @@ namespace {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr uint32_t IT = 256;
-constexpr uint32_t WAVES_I = IT / 64;
 constexpr uint32_t NONE = 0xffffffffu;
 constexpr uint32_t W = RTPS_INGEST_WINDOW;  // sequence numbers tracked per proxy
 constexpr uint32_t WW = W / 32;             // bitmap words per proxy
