@@ -163,7 +163,7 @@ __device__ void writer_insert(uint64_t wh, uint32_t r, uint64_t* wkey, uint32_t*
 constexpr uint32_t KPT = 4, KPASS = FT * KPT;  // records per thread / per workgroup pass
 constexpr uint32_t KW_SLOTS = 2 * KPASS;       // >= 2 x records per workgroup pass
 __global__ __launch_bounds__(FT) void k_keys(const rtps_record* recs, const uint64_t* n_rec, uint64_t max,
-                                             uint32_t* keys, uint32_t* vals, uint32_t* pos_epoch, uint32_t* dmark,
+                                             uint32_t* keys, uint32_t* vals, uint32_t* rec_epoch, uint32_t* dmark,
                                              uint8_t* seen, uint64_t* ctr, uint32_t* new_ptable, uint64_t* wkey,
                                              uint32_t* wfirst, const uint32_t* wF, uint64_t* wst_key,
                                              uint32_t* wst_rec) {
@@ -212,7 +212,7 @@ __global__ __launch_bounds__(FT) void k_keys(const rtps_record* recs, const uint
         }
         keys[i] = k;
         if (vals) vals[i] = (uint32_t)i;  // the device sort's values (the bucket sort derives them)
-        pos_epoch[i] = NONE;  // per-batch state, reset here instead of three memsets
+        rec_epoch[i] = NONE;  // per-batch state, reset here instead of three memsets
         dmark[i] = NONE;
         seen[i] = 0;
       }
@@ -348,7 +348,7 @@ struct WalkArgs {
   uint32_t* special; // epochs needing more than their records' spans: continued, pending or irregular
   uint32_t* pool;
   uint64_t pool_words;
-  uint32_t* pos_epoch;
+  uint32_t* rec_epoch;  // per record: its epoch (NONE: not assembled)
   uint32_t* dmark;
   uint8_t* seen;  // per position: consumed by a walk pass (collision runs)
   uint64_t* ctr;
@@ -442,13 +442,13 @@ __device__ void walk_run_serial(const WalkArgs& A, uint64_t p, uint64_t p1) {
         E.data_size = ds;
         E.count = ds / fsz + (ds % fsz > 0);
         E.F = F;
-        if (!alloc_bits(A, E)) { A.pos_epoch[q] = NONE; continue; }
+        if (!alloc_bits(A, E)) { A.rec_epoch[ri] = NONE; continue; }
         for (uint64_t w = 0; w < ((uint64_t)E.count + 31) / 32; ++w) A.pool[E.bits + w] = 0u;
         if (F != fsz) E.eflags |= EF_IRREGULAR;  // spans do not tile the buffer
         started = true;
       }
       Epoch& E = A.epochs[e];
-      A.pos_epoch[q] = e;
+      A.rec_epoch[ri] = e;
       // insert_frags (:65-140): byte range and fragment bits
       const uint64_t start0 = (uint64_t)r->u.frag.frag_start - 1, fis = r->u.frag.frags_in_sub;
       const uint64_t from = start0 * E.F;
@@ -511,7 +511,6 @@ __device__ __forceinline__ LaneRec lane_rec(const WalkArgs& A, uint64_t p, uint6
 }
 __device__ bool walk_run_regular(const WalkArgs& A, uint64_t p0, uint64_t p1, uint32_t lane, uint32_t* bm,
                                  const uint32_t g[4], int64_t sn, uint32_t F, const LaneRec& L) {
-  const uint64_t p = p0 + lane;
   const bool act = L.act;
   const uint32_t ri = L.ri, fs = L.fs, fis = L.fis, fsz = act ? L.fsz : F, dsz = L.dsz, fl = L.fl;
   const uint32_t ds0 = rl(dsz, 0);
@@ -529,7 +528,7 @@ __device__ bool walk_run_regular(const WalkArgs& A, uint64_t p0, uint64_t p1, ui
   uint32_t e0 = NONE;
   if (lane == 0) e0 = new_epoch(A, g, sn, (uint32_t)p0, (uint32_t)p0, (uint32_t)p1);
   const uint32_t e = rl(e0, 0);
-  if (act) A.pos_epoch[p] = e;
+  if (act) A.rec_epoch[ri] = e;
   if (m == count) {  // is_complete at the last record -> emit
     const uint32_t rlast = rl(ri, m - 1), flast = rl(fl, m - 1);
     if (lane == 0) {
@@ -688,7 +687,7 @@ __device__ void walk_run_wave(const WalkArgs& A, uint64_t p0, uint64_t p1, uint3
         started = false;
       }
     }
-    if (p < p1) A.pos_epoch[p] = my_e;
+    if (p < p1) A.rec_epoch[ri] = my_e;
   }
   if (started) {  // still incomplete: its bitmap goes to the pool for the pending store
     uint64_t bits = 0;
@@ -995,23 +994,29 @@ __device__ __forceinline__ void gst16(uint8_t* p, uint4 v) {
 #endif
 }
 
-// regular epochs: every record writes its fragments' span.  A wave takes 64
-// sorted positions: each lane resolves one record (epoch, source, destination,
-// lengths), then the wave copies the 64 spans SR at a time, SL lanes per record,
-// 16 B per lane (spans of one sample are adjacent in the heap).
-#ifndef RTPS_SPAN_LANES
-#define RTPS_SPAN_LANES 32  // 16 / 32 / 64 measured on C4: 0.983 / 0.970 / 0.955 ms per frag step
-#endif
+// regular epochs: every record writes its fragments' span (payload, then zeros
+// for a short payload).  k_fill resolves each record's span into a descriptor in
+// record order; k_span then copies them one wave per record, the waves striding
+// over the records, so that the waves resident at any time read and write two
+// narrow windows of the arena and the heap (consecutive records are mostly
+// consecutive fragments of one sample, and samples are placed in completion
+// order).  Copying 64 records per wave in sorted order instead touched samples
+// all over both: 619 us on C4 against the same-shape copy ceiling's 524 us
+// (scripts/diag_frag_copy.py), and 603 us in record order with 64 per wave.
 #ifndef RTPS_SPAN_NT
-#define RTPS_SPAN_NT 1      // non-temporal heap stores: 32 lanes 0.970 -> 0.944 ms (scripts/gpu_frag_ab.sh)
+#define RTPS_SPAN_NT 1      // non-temporal heap stores
 #endif
 #ifndef RTPS_SPAN_U
-#define RTPS_SPAN_U (96 / RTPS_SPAN_LANES)
+#define RTPS_SPAN_U 1       // 16-B loads in flight per lane (1 KiB per wave per step)
 #endif
-constexpr uint32_t SL = RTPS_SPAN_LANES;   // lanes per record
-constexpr uint32_t SR = 64 / SL;           // records per wave instruction
-constexpr uint32_t SPAN_U = RTPS_SPAN_U;   // 16-B loads in flight per lane (SL x 16 x SPAN_U B per record per pass)
-static_assert(SL == 16 || SL == 32 || SL == 64, "lanes per record");
+#ifndef SPAN_GRID
+#define SPAN_GRID 8192
+#endif
+constexpr uint32_t SPAN_U = RTPS_SPAN_U;
+struct SpanDesc {  // 32 B: arena offset of the payload, heap / pending-store address, bytes
+  uint64_t src, dst;
+  uint32_t nv, n, _r[2];
+};
 typedef uint32_t nt_u4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) nt_u4 g_nt_u4 __attribute__((aligned(16)));
 __device__ __forceinline__ void span_st16(uint8_t* p, uint4 v) {
@@ -1026,74 +1031,60 @@ __device__ __forceinline__ void span_st16(uint8_t* p, uint4 v) {
   gst16(p, v);
 #endif
 }
-__global__ __launch_bounds__(FT) void k_span(const rtps_record* recs, const uint8_t* arena, uint64_t arena_len,
-                                             const uint64_t* dgram_off, const uint32_t* svals,
-                                             const uint32_t* pos_epoch, const uint32_t* skeys, uint64_t max,
-                                             const Epoch* ep, uint8_t* nbytes, rtps_frag_out out) {
-  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-  for (uint64_t c = ((uint64_t)blockIdx.x * (FT / 64) + wave) * 64; c < max; c += (uint64_t)gridDim.x * FT) {
-    const uint64_t p = c + lane;
+__device__ void desc_wg(const rtps_record* recs, const uint64_t* dgram_off, const uint32_t* rec_epoch, uint64_t max,
+                        const Epoch* ep, uint8_t* nbytes, const rtps_frag_out& out, SpanDesc* desc, uint32_t bid,
+                        uint32_t nb) {
+  for (uint64_t p = (uint64_t)bid * FT + threadIdx.x; p < max; p += (uint64_t)nb * FT) {
     uint64_t src = 0, dst = 0;
     uint32_t nv = 0, n = 0;
-    bool live = false;
-    if (p < max && skeys[p] != SENT) {
-      const uint32_t e = pos_epoch[p];
-      if (e != NONE) {
-        const Epoch& E = ep[e];
-        if (!(E.eflags & (EF_IRREGULAR | EF_SKIP)) && E.state != E_DEAD) {
-          const rtps_record* r = recs + svals[p];
-          const uint64_t from = (uint64_t)(r->u.frag.frag_start - 1) * E.F;
-          const uint64_t fisF = (uint64_t)r->u.frag.frags_in_sub * E.F;
-          const uint64_t span_end = min<uint64_t>(from + fisF, E.data_size);
-          const uint64_t to = min<uint64_t>(from + min<uint64_t>(fisF, r->u.frag.pl_len), E.data_size);
+    const uint32_t e = rec_epoch[p];
+    if (e != NONE) {
+      const Epoch& E = ep[e];
+      if (!(E.eflags & (EF_IRREGULAR | EF_SKIP)) && E.state != E_DEAD) {
+        const rtps_record* r = recs + p;
+        const uint64_t from = (uint64_t)(r->u.frag.frag_start - 1) * E.F;
+        const uint64_t fisF = (uint64_t)r->u.frag.frags_in_sub * E.F;
+        const uint64_t span_end = min<uint64_t>(from + fisF, E.data_size);
+        const uint64_t to = min<uint64_t>(from + min<uint64_t>(fisF, r->u.frag.pl_len), E.data_size);
+        if (span_end > from) {
           src = dgram_off[r->dgram_idx] + r->u.frag.pl_off;
-          dst = (uint64_t)(epoch_dst(E, out, nbytes) + from);
+          dst = (uint64_t)(uintptr_t)(epoch_dst(E, out, nbytes) + from);
           nv = (uint32_t)(to - from);
           n = (uint32_t)(span_end - from);
-          live = n > 0;
         }
       }
     }
-    // SR records at a time, one per SL-lane group: SL x 16 B per instruction per
-    // record, SPAN_U loads in flight per lane before the stores
-    uint64_t todo = __ballot(live);
-    const uint32_t q = lane / SL, ql = lane % SL;
-    while (todo) {
-      uint32_t j = 64u;
+    uint4* q = reinterpret_cast<uint4*>(desc + p);
+    q[0] = make_uint4((uint32_t)src, (uint32_t)(src >> 32), (uint32_t)dst, (uint32_t)(dst >> 32));
+    q[1] = make_uint4(nv, n, 0u, 0u);
+  }
+}
+__global__ __launch_bounds__(FT) void k_span(const uint8_t* arena, const SpanDesc* desc, uint64_t max) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t nw = (uint64_t)gridDim.x * (FT / 64);
+  const uint32_t w0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * (FT / 64) + (threadIdx.x >> 6)));
+  for (uint64_t r = w0; r < max; r += nw) {
+    const uint4* q = reinterpret_cast<const uint4*>(desc + r);
+    const uint4 a = q[0], b = q[1];
+    const uint32_t nv = b.x, n = b.y;
+    if (n == 0) continue;
+    const uint8_t* sp = arena + (((uint64_t)a.y << 32) | a.x);
+    uint8_t* d = (uint8_t*)(uintptr_t)(((uint64_t)a.w << 32) | a.z);
+    for (uint32_t b0 = 16u * lane; b0 < n; b0 += 16u * 64u * SPAN_U) {
+      uint4 v[SPAN_U];
 #pragma unroll
-      for (uint32_t k = 0; k < SR; ++k) {
-        const uint32_t jk = todo ? (uint32_t)__builtin_ctzll(todo) : 64u;
-        todo &= todo - 1;
-        if (k == q) j = jk;
+      for (uint32_t k = 0; k < SPAN_U; ++k) {
+        const uint32_t bb = b0 + 16u * 64u * k;
+        v[k] = make_uint4(0, 0, 0, 0);
+        if (bb + 16 <= nv) v[k] = ld16(sp + bb);
       }
-      const uint32_t jj = j & 63u;
-      const uint64_t sj = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(src >> 32), (int)jj, 64) << 32) |
-                          (uint32_t)__shfl((int)(uint32_t)src, (int)jj, 64);
-      const uint64_t dj = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(dst >> 32), (int)jj, 64) << 32) |
-                          (uint32_t)__shfl((int)(uint32_t)dst, (int)jj, 64);
-      // every lane takes part in each __shfl (a lane left out of the permute supplies no value)
-      const uint32_t nv_all = (uint32_t)__shfl((int)nv, (int)jj, 64);
-      const uint32_t n_all = (uint32_t)__shfl((int)n, (int)jj, 64);
-      const uint32_t nvj = j < 64u ? nv_all : 0u;
-      const uint32_t nj = j < 64u ? n_all : 0u;
-      const uint8_t* sp = arena + sj;
-      uint8_t* d = (uint8_t*)dj;
-      for (uint32_t b0 = 16u * ql; b0 < nj; b0 += 16u * SL * SPAN_U) {
-        uint4 v[SPAN_U];
 #pragma unroll
-        for (uint32_t k = 0; k < SPAN_U; ++k) {
-          const uint32_t b = b0 + 16u * SL * k;
-          v[k] = make_uint4(0, 0, 0, 0);
-          if (b + 16 <= nvj) v[k] = ld16(sp + b);
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < SPAN_U; ++k) {
-          const uint32_t b = b0 + 16u * SL * k;
-          if (b + 16 <= nj && (b + 16 <= nvj || b >= nvj)) {
-            span_st16(d + b, v[k]);  // payload, or zeros past a short payload
-          } else if (b < nj) {
-            for (uint32_t t = b; t < b + 16 && t < nj; ++t) d[t] = t < nvj ? sp[t] : (uint8_t)0;
-          }
+      for (uint32_t k = 0; k < SPAN_U; ++k) {
+        const uint32_t bb = b0 + 16u * 64u * k;
+        if (bb + 16 <= n && (bb + 16 <= nv || bb >= nv)) {
+          span_st16(d + bb, v[k]);  // payload, or zeros past a short payload
+        } else if (bb < n) {
+          for (uint32_t t = bb; t < bb + 16 && t < n; ++t) d[t] = t < nv ? sp[t] : (uint8_t)0;
         }
       }
     }
@@ -1103,7 +1094,7 @@ __global__ __launch_bounds__(FT) void k_span(const rtps_record* recs, const uint
 // irregular epochs: the sequential replay (zero buffer, carried bytes, then every
 // record's clamped copy in record order), one workgroup each
 __device__ void serial_wg(const rtps_record* recs, const uint8_t* arena, const uint64_t* dgram_off,
-                          const uint32_t* svals, const uint32_t* pos_epoch, const Epoch* ep, const uint32_t* special,
+                          const uint32_t* svals, const uint32_t* rec_epoch, const Epoch* ep, const uint32_t* special,
                           const uint64_t* ctr, const Pend* op, const uint8_t* obytes, uint8_t* nbytes,
                           const rtps_frag_out& out, uint32_t bid, uint32_t nb) {
   const uint64_t ns = ctr[C_SPECIAL];
@@ -1121,8 +1112,9 @@ __device__ void serial_wg(const rtps_record* recs, const uint8_t* arena, const u
     __threadfence();
     __syncthreads();
     for (uint64_t p = E.p0; p < E.p1; ++p) {
-      if (pos_epoch[p] != e) continue;
-      const rtps_record* r = recs + svals[p];
+      const uint32_t ri = svals[p];
+      if (rec_epoch[ri] != e) continue;
+      const rtps_record* r = recs + ri;
       const uint64_t from = (uint64_t)(r->u.frag.frag_start - 1) * E.F;
       const uint64_t to = min<uint64_t>(from + min<uint64_t>((uint64_t)r->u.frag.frags_in_sub * E.F, r->u.frag.pl_len),
                                         E.data_size);
@@ -1155,16 +1147,21 @@ __device__ void ptable_wg(const Pend* np, uint64_t* ctr, uint32_t* ptable, uint6
 // before the span copy, one launch: carried-over bytes / zeros of regular epochs
 // (k_span then writes their spans), the irregular epochs' serial replays (their
 // own bytes, disjoint from every span), and the next batch's pending table
-constexpr uint32_t INIT_WG = 1024, SERIAL_WG = 1024, PTAB_WG = PCAP / FT;
+constexpr uint32_t INIT_WG = 1024, SERIAL_WG = 1024, PTAB_WG = PCAP / FT, DESC_WG = 2048;
 __global__ __launch_bounds__(FT) void k_fill(const rtps_record* recs, const uint8_t* arena, const uint64_t* dgram_off,
-                                             const uint32_t* svals, const uint32_t* pos_epoch, const Epoch* ep,
+                                             const uint32_t* svals, const uint32_t* rec_epoch, const Epoch* ep,
                                              const uint32_t* special, uint64_t* ctr, const Pend* op,
                                              const uint8_t* obytes, uint8_t* nbytes, const Pend* np,
-                                             uint32_t* ptable, uint64_t* n_pending, rtps_frag_out out) {
+                                             uint32_t* ptable, uint64_t* n_pending, uint64_t max, SpanDesc* desc,
+                                             rtps_frag_out out) {
   const uint32_t b = blockIdx.x;
+  if (b >= INIT_WG + SERIAL_WG + PTAB_WG) {
+    desc_wg(recs, dgram_off, rec_epoch, max, ep, nbytes, out, desc, b - INIT_WG - SERIAL_WG - PTAB_WG, DESC_WG);
+    return;
+  }
   if (b < INIT_WG) init_wg(ep, special, ctr, op, obytes, nbytes, out, b, INIT_WG);
   else if (b < INIT_WG + SERIAL_WG)
-    serial_wg(recs, arena, dgram_off, svals, pos_epoch, ep, special, ctr, op, obytes, nbytes, out, b - INIT_WG,
+    serial_wg(recs, arena, dgram_off, svals, rec_epoch, ep, special, ctr, op, obytes, nbytes, out, b - INIT_WG,
               SERIAL_WG);
   else ptable_wg(np, ctr, ptable, n_pending, b - INIT_WG - SERIAL_WG, PTAB_WG);
 }
@@ -1216,7 +1213,7 @@ struct FragState {
   // per-batch scratch (grown on demand)
   uint64_t cap = 0;
   uint32_t *keys = nullptr, *vals = nullptr, *skeys = nullptr, *svals = nullptr;
-  uint32_t *pos_epoch = nullptr, *dmark = nullptr, *special = nullptr;
+  uint32_t *rec_epoch = nullptr, *dmark = nullptr, *special = nullptr;
   uint32_t* tcnt = nullptr;   // per 4096-position tile: completions, then their exclusive scan
   uint64_t* tbytes = nullptr; // per tile: heap bytes, then their exclusive scan
   uint8_t* seen = nullptr;
@@ -1229,16 +1226,17 @@ struct FragState {
   // the key sort (rtps_bsort.h) for batches of up to rtps_bsort::MAX_N records
   uint32_t* bh = nullptr;
   uint64_t *bk = nullptr, *bk2 = nullptr;
+  SpanDesc* desc = nullptr;  // per record: its span copy
   int sort_mode = 0;  // 0: rtps_bsort where it applies, 1: rocprim's device sort always (tests)
 };
 
 static void free_scratch(FragState* s) {
-  void* ptrs[] = {s->keys, s->vals, s->skeys, s->svals, s->pos_epoch, s->dmark, s->tcnt, s->special,
-                  s->seen, s->tbytes, s->epochs, s->pool, s->tmp, s->bh, s->bk, s->bk2};
+  void* ptrs[] = {s->keys, s->vals, s->skeys, s->svals, s->rec_epoch, s->dmark, s->tcnt, s->special,
+                  s->seen, s->tbytes, s->epochs, s->pool, s->tmp, s->bh, s->bk, s->bk2, s->desc};
   for (void* p : ptrs) if (p) (void)hipFree(p);
-  s->keys = s->vals = s->skeys = s->svals = s->pos_epoch = s->dmark = s->tcnt = s->special = nullptr;
+  s->keys = s->vals = s->skeys = s->svals = s->rec_epoch = s->dmark = s->tcnt = s->special = nullptr;
   s->seen = nullptr; s->tbytes = nullptr; s->epochs = nullptr; s->pool = nullptr; s->tmp = nullptr;
-  s->bh = nullptr; s->bk = s->bk2 = nullptr;
+  s->bh = nullptr; s->bk = s->bk2 = nullptr; s->desc = nullptr;
   s->cap = 0; s->tmp_bytes = 0;
 }
 
@@ -1249,13 +1247,14 @@ static bool grow(FragState* s, uint64_t max, hipStream_t st) {
   const uint64_t n = max;
   bool ok = hipMalloc(&s->keys, n * 4) == hipSuccess && hipMalloc(&s->vals, n * 4) == hipSuccess &&
             hipMalloc(&s->skeys, n * 4) == hipSuccess && hipMalloc(&s->svals, n * 4) == hipSuccess &&
-            hipMalloc(&s->pos_epoch, n * 4) == hipSuccess && hipMalloc(&s->dmark, n * 4) == hipSuccess &&
+            hipMalloc(&s->rec_epoch, n * 4) == hipSuccess && hipMalloc(&s->dmark, n * 4) == hipSuccess &&
             hipMalloc(&s->tcnt, (n / PTILE + 1) * 4) == hipSuccess && hipMalloc(&s->special, n * 4) == hipSuccess &&
             hipMalloc(&s->seen, n) == hipSuccess && hipMalloc(&s->tbytes, (n / PTILE + 1) * 8) == hipSuccess;
   s->pool_words = 4 * n + PWORDS;
   const uint64_t nb = n < rtps_bsort::MAX_N ? n : rtps_bsort::MAX_N;
   ok = ok && hipMalloc(&s->bh, rtps_bsort::hist_words(nb) * 4) == hipSuccess &&
        hipMalloc(&s->bk, nb * 8) == hipSuccess && hipMalloc(&s->bk2, nb * 8) == hipSuccess;
+  ok = ok && hipMalloc(&s->desc, n * sizeof(SpanDesc)) == hipSuccess;
   ok = ok && hipMalloc(&s->epochs, n * sizeof(Epoch)) == hipSuccess &&
        hipMalloc(&s->pool, s->pool_words * 4) == hipSuccess;
   size_t b1 = 0;
@@ -1319,7 +1318,7 @@ int rtps_frag_assemble(FragState* s, hipStream_t st, const uint8_t* arena, uint6
   }
   const bool bsort = s->sort_mode == 0 && max <= rtps_bsort::MAX_N;
   hipLaunchKernelGGL(k_keys, dim3(gk), dim3(FT), 0, st, records, n_records, max, s->keys, bsort ? nullptr : s->vals,
-                     s->pos_epoch, s->dmark, s->seen, s->ctr, s->ptable[nw], s->wkey, s->wfirst, s->wF, s->wst_key,
+                     s->rec_epoch, s->dmark, s->seen, s->ctr, s->ptable[nw], s->wkey, s->wfirst, s->wF, s->wst_key,
                      s->wst_rec);
   size_t tb = s->tmp_bytes;
   const WregSide wreg{WREG_WG, s->wst_key, s->wst_rec, gk * WST, s->wkey, s->wfirst, s->wF, s->ctr};
@@ -1334,7 +1333,7 @@ int rtps_frag_assemble(FragState* s, hipStream_t st, const uint8_t* arena, uint6
                        s->wF, s->ctr);
   }
   WalkArgs A{records, s->skeys, s->svals, max, s->wkey, s->wF, s->wfirst, s->pend[o], s->ptable[o], s->pbits[o], s->epochs,
-             s->special, s->pool, s->pool_words, s->pos_epoch, s->dmark, s->seen, s->ctr};
+             s->special, s->pool, s->pool_words, s->rec_epoch, s->dmark, s->seen, s->ctr};
   hipLaunchKernelGGL(k_walk, dim3((uint32_t)hmin((max + FT - 1) / FT, 8192)), dim3(FT), 0, st, A);
   const uint64_t tiles = (max + PTILE - 1) / PTILE;
   hipLaunchKernelGGL(k_place_tiles, dim3((uint32_t)tiles), dim3(FT), 0, st, s->dmark, s->epochs, max, s->tcnt,
@@ -1345,14 +1344,11 @@ int rtps_frag_assemble(FragState* s, hipStream_t st, const uint8_t* arena, uint6
                     s->now, s->pend[o], s->pbytes[o], s->pbits[o], s->pend[nw], s->pbytes[nw], s->pbits[nw], s->ctr,
                     records, s->wkey, s->wfirst, s->wF};
   hipLaunchKernelGGL(k_place, dim3((uint32_t)tiles + PA_WG + CARRY_WG + WFIX_WG), dim3(FT), 0, st, P, *out);
-  hipLaunchKernelGGL(k_fill, dim3(INIT_WG + SERIAL_WG + PTAB_WG), dim3(FT), 0, st, records, arena, dgram_off, s->svals,
-                     s->pos_epoch, s->epochs, s->special, s->ctr, s->pend[o], s->pbytes[o], s->pbytes[nw], s->pend[nw],
-                     s->ptable[nw], out->n_pending, *out);
-#ifndef SPAN_GRID
-#define SPAN_GRID 8192
-#endif
-  hipLaunchKernelGGL(k_span, dim3((uint32_t)hmin((max + FT - 1) / FT, SPAN_GRID)), dim3(FT), 0, st, records, arena,
-                     arena_len, dgram_off, s->svals, s->pos_epoch, s->skeys, max, s->epochs, s->pbytes[nw], *out);
+  hipLaunchKernelGGL(k_fill, dim3(INIT_WG + SERIAL_WG + PTAB_WG + DESC_WG), dim3(FT), 0, st, records, arena,
+                     dgram_off, s->svals, s->rec_epoch, s->epochs, s->special, s->ctr, s->pend[o], s->pbytes[o],
+                     s->pbytes[nw], s->pend[nw], s->ptable[nw], out->n_pending, max, s->desc, *out);
+  hipLaunchKernelGGL(k_span, dim3((uint32_t)hmin((max + FT / 64 - 1) / (FT / 64), SPAN_GRID)), dim3(FT), 0, st, arena,
+                     s->desc, max);
   if (hipGetLastError() != hipSuccess) return RTPS_RX_EHIP;
   s->cur = nw;
   return RTPS_RX_OK;
