@@ -55,6 +55,7 @@ extern "C" int diag_ceiling(int mode, const uint8_t* arena, const uint64_t* off,
 // mode 0: one wave per record, 16 B per lane (the decode's wide-slot shape)
 // mode 1: flat grid, one 16-B quad per thread (pure streaming gather)
 typedef uint4 u128u __attribute__((aligned(1)));
+typedef uint4 u128u_v;
 __global__ __launch_bounds__(256) void copy_wave_kernel(const uint8_t* arena, const uint64_t* off, uint32_t n,
                                                         uint8_t* rows, uint32_t row_bytes, uint32_t skip) {
   const uint32_t lane = threadIdx.x & 63, nq = row_bytes / 16;
@@ -101,6 +102,52 @@ __global__ __launch_bounds__(256) void copy_w_kernel(const uint8_t* arena, const
       }
     }
   }
+}
+// R consecutive rows per wave as one flat list of 16-B chunks (lane l takes chunks l, l + 64, ...):
+// every lane's loads of the R rows are in flight together (R x 1344 B per wave), and no lane idles
+// on a row's 20-chunk tail
+template <int R, bool NT>
+__global__ __launch_bounds__(256) void copy_group_kernel(const uint8_t* arena, const uint64_t* off, uint32_t n,
+                                                         uint8_t* rows, uint32_t row_bytes, uint32_t skip) {
+  constexpr int MAXC = (R * 84 + 63) / 64;  // chunks per lane for rows of <= 1344 B
+  const uint32_t lane = threadIdx.x & 63, ne = row_bytes / 16, tot = R * ne;
+  const uint64_t nw = (uint64_t)gridDim.x * 4;
+  for (uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); g * R < n; g += nw) {
+    u128u_v v[MAXC];
+#pragma unroll
+    for (int k = 0; k < MAXC; ++k) {
+      const uint32_t c = lane + 64u * k, j = c / ne, q = c - j * ne;
+      const uint64_t r = g * R + j;
+      if (c < tot && r < n) v[k] = *(const u128u*)(arena + off[r] + skip + 16 * q);
+    }
+#pragma unroll
+    for (int k = 0; k < MAXC; ++k) {
+      const uint32_t c = lane + 64u * k, j = c / ne, q = c - j * ne;
+      const uint64_t r = g * R + j;
+      if (c < tot && r < n) {
+        uint4* d = reinterpret_cast<uint4*>(rows + r * row_bytes + 16 * q);
+        if (NT) {
+          u32x4 w = {v[k].x, v[k].y, v[k].z, v[k].w};
+          __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(d));
+        } else {
+          *d = v[k];
+        }
+      }
+    }
+  }
+}
+extern "C" int diag_copy_group(int r, int nt, const uint8_t* arena, const uint64_t* off, uint32_t n, uint8_t* rows,
+                               uint32_t row_bytes, uint32_t skip, uint32_t blocks, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (row_bytes > 1344) return -1;
+#define V(R, NT)                                                                                              \
+  if (r == R && nt == NT) {                                                                                   \
+    hipLaunchKernelGGL((copy_group_kernel<R, NT>), dim3(blocks), dim3(256), 0, s, arena, off, n, rows, row_bytes, skip); \
+    return hipGetLastError() == hipSuccess ? 0 : -2;                                                          \
+  }
+  V(1, 1) V(2, 1) V(3, 1) V(4, 1) V(6, 1) V(3, 0)
+#undef V
+  return -1;
 }
 extern "C" int diag_copy_w(int w, int u, int nt, const uint8_t* arena, const uint64_t* off, uint32_t n, uint8_t* rows,
                            uint32_t row_bytes, uint32_t skip, uint32_t blocks, void* stream) {

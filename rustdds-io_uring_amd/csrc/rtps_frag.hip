@@ -1007,7 +1007,7 @@ __device__ __forceinline__ void gst16(uint8_t* p, uint4 v) {
 #define RTPS_SPAN_NT 1      // non-temporal heap stores
 #endif
 #ifndef RTPS_SPAN_U
-#define RTPS_SPAN_U 1       // 16-B loads in flight per lane (1 KiB per wave per step)
+#define RTPS_SPAN_U 3       // 16-B loads in flight per lane (3 KiB per wave per step: two C4 records)
 #endif
 #ifndef SPAN_GRID
 #define SPAN_GRID 8192
@@ -1059,32 +1059,73 @@ __device__ void desc_wg(const rtps_record* recs, const uint64_t* dgram_off, cons
     q[1] = make_uint4(nv, n, 0u, 0u);
   }
 }
+// SPAN_R consecutive records per wave step, copied as one flat list of 16-B
+// chunks (lane l takes chunks l, l + 64, ...): the loads of both records are in
+// flight together and no lane idles on a record's tail (C4: 84 chunks per
+// record, 20 of them in a second, mostly idle, pass with one record per wave).
+// The copy ceiling of this shape (scripts/diag_frag_group.py): 515 us with one
+// record per wave, 505 us with two, 515 / 553 us with three / four.
+#ifndef RTPS_SPAN_R
+#define RTPS_SPAN_R 2
+#endif
+constexpr uint32_t SPAN_R = RTPS_SPAN_R;
+static_assert(SPAN_R >= 1 && SPAN_R <= 4, "records per wave step");
+template <class T>
+__device__ __forceinline__ T span_pick(const T (&a)[SPAN_R], uint32_t j) {
+  T v = a[0];
+#pragma unroll
+  for (uint32_t t = 1; t < SPAN_R; ++t) v = j == t ? a[t] : v;
+  return v;
+}
 __global__ __launch_bounds__(FT) void k_span(const uint8_t* arena, const SpanDesc* desc, uint64_t max) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t nw = (uint64_t)gridDim.x * (FT / 64);
   const uint32_t w0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * (FT / 64) + (threadIdx.x >> 6)));
-  for (uint64_t r = w0; r < max; r += nw) {
-    const uint4* q = reinterpret_cast<const uint4*>(desc + r);
-    const uint4 a = q[0], b = q[1];
-    const uint32_t nv = b.x, n = b.y;
-    if (n == 0) continue;
-    const uint8_t* sp = arena + (((uint64_t)a.y << 32) | a.x);
-    uint8_t* d = (uint8_t*)(uintptr_t)(((uint64_t)a.w << 32) | a.z);
-    for (uint32_t b0 = 16u * lane; b0 < n; b0 += 16u * 64u * SPAN_U) {
+  for (uint64_t g = w0; g * SPAN_R < max; g += nw) {
+    const uint8_t* sp[SPAN_R];
+    uint8_t* dp[SPAN_R];
+    uint32_t nv[SPAN_R], nn[SPAN_R], cb[SPAN_R];  // cb: first chunk of record t in the flat list
+    uint32_t tot = 0;
+#pragma unroll
+    for (uint32_t t = 0; t < SPAN_R; ++t) {
+      const uint64_t r = g * SPAN_R + t;
+      uint4 a = make_uint4(0, 0, 0, 0), b = a;
+      if (r < max) {
+        const uint4* q = reinterpret_cast<const uint4*>(desc + r);
+        a = q[0]; b = q[1];
+      }
+      sp[t] = arena + (((uint64_t)a.y << 32) | a.x);
+      dp[t] = (uint8_t*)(uintptr_t)(((uint64_t)a.w << 32) | a.z);
+      nv[t] = b.x; nn[t] = b.y;
+      cb[t] = tot;
+      tot += (b.y + 15u) >> 4;
+    }
+    for (uint32_t c0 = lane; c0 < tot; c0 += 64u * SPAN_U) {
       uint4 v[SPAN_U];
 #pragma unroll
       for (uint32_t k = 0; k < SPAN_U; ++k) {
-        const uint32_t bb = b0 + 16u * 64u * k;
+        const uint32_t c = c0 + 64u * k;
+        uint32_t j = 0;
+#pragma unroll
+        for (uint32_t t = 1; t < SPAN_R; ++t) j += c >= cb[t] ? 1u : 0u;
+        const uint32_t bb = 16u * (c - span_pick(cb, j));
         v[k] = make_uint4(0, 0, 0, 0);
-        if (bb + 16 <= nv) v[k] = ld16(sp + bb);
+        if (c < tot && bb + 16 <= span_pick(nv, j)) v[k] = ld16(span_pick(sp, j) + bb);
       }
 #pragma unroll
       for (uint32_t k = 0; k < SPAN_U; ++k) {
-        const uint32_t bb = b0 + 16u * 64u * k;
-        if (bb + 16 <= n && (bb + 16 <= nv || bb >= nv)) {
+        const uint32_t c = c0 + 64u * k;
+        if (c >= tot) continue;
+        uint32_t j = 0;
+#pragma unroll
+        for (uint32_t t = 1; t < SPAN_R; ++t) j += c >= cb[t] ? 1u : 0u;
+        const uint32_t bb = 16u * (c - span_pick(cb, j)), n = span_pick(nn, j), vn = span_pick(nv, j);
+        uint8_t* d = span_pick(dp, j);
+        if (bb + 16 <= n && (bb + 16 <= vn || bb >= vn)) {
           span_st16(d + bb, v[k]);  // payload, or zeros past a short payload
-        } else if (bb < n) {
-          for (uint32_t t = bb; t < bb + 16 && t < n; ++t) d[t] = t < nv ? sp[t] : (uint8_t)0;
+        } else {
+          const uint8_t* s = span_pick(sp, j);
+          for (uint32_t t = bb; t < bb + 16 && t < n; ++t) d[t] = t < vn ? s[t] : (uint8_t)0;
         }
       }
     }
