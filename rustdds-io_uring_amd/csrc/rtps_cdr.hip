@@ -146,9 +146,6 @@ __device__ uint8_t cdr_validate(const CdrProg& P, const uint8_t* v, uint32_t len
 #ifndef CDR_RUN_N
 #define CDR_RUN_N 2
 #endif
-#ifndef CDR_ABLATE
-#define CDR_ABLATE 0  // timing ablations (wrong output): 1 phase A only, 2 no narrow slots, 3 no wide slots
-#endif
 #ifndef CDR_GRID_MULT
 #define CDR_GRID_MULT 1  // grid cap = resident blocks x this
 #endif
@@ -374,18 +371,10 @@ void cdr_decode_kernel(CdrProg P, CdrArgs a) {
         seg_copy(P, S, a, nv, lane, vbase, rowc);
         continue;
       }
-#if CDR_ABLATE == 1
-      continue;  // timing ablation: phase A only
-#endif
       if (S.dwords >= CDR_WIDE_DWORDS) {
-#if CDR_ABLATE != 3
         wide_slot(P, S, a, hdr, nv, lane, meta, vbase, posT, lenT, rowc);
-#endif
         continue;
       }
-#if CDR_ABLATE == 2
-      continue;  // timing ablation: no narrow slots
-#endif
       const uint32_t total = nv * S.dwords;
       const bool swap8 = S.size == 8;
       const float inv_dwords = 1.0f / (float)S.dwords;
