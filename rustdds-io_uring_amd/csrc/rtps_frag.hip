@@ -8,9 +8,10 @@
 // (the CPU restatement that tests/ check it against):
 //
 //  1 sort   every DATA_FRAG record with ROUTE_PASS is keyed by a 32-bit hash of
-//           (writer GUID, SN); a stable radix sort (hipCUB) groups each
-//           assembly buffer's fragments in record order (hash collisions are
-//           resolved by the walk, which compares full keys).
+//           (writer GUID, SN); a stable sort (rtps_bsort.h: top-byte buckets,
+//           then an LDS radix sort per bucket) groups each assembly buffer's
+//           fragments in record order (hash collisions are resolved by the
+//           walk, which compares full keys).
 //  2 writers the fragment size of a writer is the one of its first DATA_FRAG
 //           ever (FragmentAssembler::new): persistent open-addressing table,
 //           atomicMin over the batch's first records of new writers.
@@ -24,8 +25,8 @@
 //  5 copy   a regular epoch (no repeated fragment, fragment size equal to the
 //           writer's, no clamping) tiles its buffer with its fragments' spans,
 //           so every record copies its span (payload, then zeros for a short
-//           payload) in parallel, one wave per record, after the carried-over
-//           bytes were copied.  Irregular epochs replay the copies in record
+//           payload) in parallel, two records per wave step, after the
+//           carried-over bytes were copied.  Irregular epochs replay the copies in record
 //           order in one workgroup each (rare).
 //
 // Roofline: HBM-bound.  Algorithmic bytes per DATA_FRAG record = its payload
