@@ -141,7 +141,7 @@ __device__ uint8_t cdr_validate(const CdrProg& P, const uint8_t* v, uint32_t len
 }
 
 #ifndef CDR_UNROLL_N
-#define CDR_UNROLL_N 8
+#define CDR_UNROLL_N 6  // narrow-slot words per lane per round: 6 keeps 6 waves / SIMD without scratch
 #endif
 #ifndef CDR_RUN_N
 #define CDR_RUN_N 2
@@ -150,7 +150,7 @@ __device__ uint8_t cdr_validate(const CdrProg& P, const uint8_t* v, uint32_t len
 #define CDR_GRID_MULT 1  // grid cap = resident blocks x this
 #endif
 #ifndef CDR_WAVES_PER_EU
-#define CDR_WAVES_PER_EU 1
+#define CDR_WAVES_PER_EU 6  // 80 VGPRs: C2 162 -> 135 us, C3 211 -> 200 us, T unchanged (scripts/gpu_cdr_ab.sh)
 #endif
 constexpr uint32_t CDR_UNROLL = CDR_UNROLL_N;
 constexpr uint32_t CDR_WIDE_DWORDS = 8;   // slots at least this long take the 16-B-per-lane path
