@@ -1484,7 +1484,12 @@ __global__ __launch_bounds__(TILE) void rtps_item_diag_kernel(KParams p, const r
     const bool le = (flags & 1u) != 0u;
     const uint32_t eff = eff_len(kind, e16(W.w[0], 1, le), L - o);
     SubOut so;
-    sub_body<true>(s, W, kind, flags, le, o + 4u, eff, R, so);
+    if (mode & 2u) {  // ablation: no per-kind reader (the window loads stay)
+      so.cls = kind == RTPS_DATA ? 1u : 3u; so.route = 0; so.pk = 0; so.aux16 = eff; so.rid = W.w[2]; so.wid = W.w[3];
+      R.d[8] = W.w[4] ^ W.w[5] ^ W.w[6] ^ W.w[7] ^ W.w[8];
+    } else {
+      sub_body<true>(s, W, kind, flags, le, o + 4u, eff, R, so);
+    }
     Interp st;
     st.src0 = a[2]; st.src1 = a[3]; st.src2 = z[0];
     if (kind == RTPS_INFO_DST || (st.src0 == hp[0] && st.src1 == hp[1] && st.src2 == hp[2])) {
@@ -1495,9 +1500,19 @@ __global__ __launch_bounds__(TILE) void rtps_item_diag_kernel(KParams p, const r
     st.ts_sec = t[2]; st.ts_frac = t[3];
     R.d[0] = d;
     R.d[1] = a[1];
-    tgt = rec_finish(p, R, so, kind, st);
+    if (mode & 4u) {  // ablation: no classification (no reader-table probe)
+      R.d[2] = st.src0; R.d[3] = st.src1; R.d[4] = st.src2; R.d[5] = so.wid; R.d[6] = so.rid;
+      R.d[7] = so.aux16 | (so.route << 16) | (so.pk << 24); R.d[14] = st.ts_sec; R.d[15] = st.ts_frac;
+    } else {
+      tgt = rec_finish(p, R, so, kind, st);
+    }
   }
-  if (mode == 0) {
+  if (mode & 8u) {  // ablation: no record stores (one word per record keeps the work live)
+    if (live) p.target_out[r] = tgt ^ R.d[0] ^ R.d[1] ^ R.d[2] ^ R.d[3] ^ R.d[4] ^ R.d[5] ^ R.d[6] ^ R.d[7] ^ R.d[8] ^
+                                R.d[9] ^ R.d[10] ^ R.d[11] ^ R.d[12] ^ R.d[13] ^ R.d[14] ^ R.d[15];
+    return;
+  }
+  if ((mode & 1u) == 0) {
     if (live) rec_store(p.records + r, R);
   } else {
     s_t[tid * 4 + 0] = u32x4{R.d[0], R.d[1], R.d[2], R.d[3]};

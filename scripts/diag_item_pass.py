@@ -26,7 +26,8 @@ rx.parse_batch_device(arena, off_t, ln_t, n, outs)
 torch.cuda.synchronize()
 m = int(outs["n_records"].item())
 r = outs["records"][:m].cpu().numpy().reshape(-1).view(RECORD_DTYPE)
-g = np.concatenate([r["prefix"], r["writer_id"]], axis=1)
+wk = np.isin(r["kind"], [0x15, 0x16, 0x07, 0x13, 0x08])  # writer kinds, as bench.py subscribes
+g = np.concatenate([r["prefix"][wk], r["writer_id"][wk]], axis=1)
 guids = np.unique(g.view(np.dtype((np.void, 16))).reshape(-1))
 tbl = np.zeros(len(guids), dtype=MATCH_DTYPE)
 tbl["writer_guid"] = np.frombuffer(guids.tobytes(), dtype=np.uint8).reshape(-1, 16)
@@ -75,4 +76,8 @@ for rep in range(2):
     t1 = timeit(lambda: item(1))
     print(f"parse step {tp:7.1f} us   item pass: per-lane stores {t0:7.1f} us, LDS-transposed stores {t1:7.1f} us",
           flush=True)
+# ablations (wrong output, timing only): 2 no per-kind reader, 4 no classification, 8 no record stores
+for mode, what in ((1 | 2, "no per-kind reader"), (1 | 4, "no classification"), (8, "no record stores"),
+                   (2 | 4 | 8, "window + interpreter loads only")):
+    print(f"ablation {what:32s} {timeit(lambda: item(mode)):7.1f} us", flush=True)
 rx.close()
