@@ -118,8 +118,10 @@ __device__ __forceinline__ void wave_or(uint32_t* base, uint32_t* addr, uint32_t
 __device__ __forceinline__ unsigned long long ekey(uint32_t epoch, uint32_t k) {
   return ((unsigned long long)(0xffffffffu - epoch) << 32) | k;
 }
+typedef uint32_t u32u __attribute__((aligned(1)));
+// one unaligned dword load (gfx950 global loads need no alignment), not four byte loads
 __device__ __forceinline__ uint32_t rd32(const uint8_t* p, bool le) {
-  const uint32_t x = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+  const uint32_t x = *reinterpret_cast<const u32u*>(p);
   return le ? x : __builtin_bswap32(x);
 }
 
