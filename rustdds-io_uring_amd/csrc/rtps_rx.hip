@@ -2093,7 +2093,7 @@ int rtps_rx_ingest(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len, con
    per-batch path, 0 = chosen per batch, 1 = global marks / merge, 2 = one
    workgroup per proxy (same results) */
 int rtps_rx_debug_ingest_path(rtps_rx_ctx* c, uint32_t path) {
-  if (!c || path > 2u) return RTPS_RX_EINVAL;
+  if (!c || path > 3u) return RTPS_RX_EINVAL;
   (void)hipSetDevice(c->device);
   if (!c->ingest) {
     c->ingest = rtps_ingest_state_new(c->device);

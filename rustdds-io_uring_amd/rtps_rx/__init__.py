@@ -302,7 +302,8 @@ class MessageReceiver:
         return int(which.value)
 
     def debug_ingest_path(self, path):
-        """Ingest path: 0 chosen per batch, 1 global marks / merge, 2 one workgroup per proxy."""
+        """Ingest path: 0 chosen per batch, 1 global marks / merge, 2 one workgroup per proxy,
+        3 global with the first-cover-key merge (k_fcmerge) forced for GAP-free batches."""
         fn = lib().rtps_rx_debug_ingest_path
         fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
         _check(fn(self._h, path))

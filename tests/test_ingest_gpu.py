@@ -18,10 +18,12 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
-@pytest.fixture(params=[1, 2], ids=["global", "per_proxy"])
+@pytest.fixture(params=[1, 2, 3], ids=["global", "per_proxy", "global_fcmerge"])
 def rx(request):
-    """Every test runs on both ingest paths (forced): global marks / merge, and one
-    workgroup per proxy replaying its events in order against an LDS window."""
+    """Every test runs on every ingest path (forced): global marks / merge, one
+    workgroup per proxy replaying its events in order against an LDS window, and the
+    global path whose GAP-free batches merge their coverage from the first-cover keys
+    (k_fcmerge, chosen by size for large batches over few proxies, forced here)."""
     import rtps_rx
     r = rtps_rx.MessageReceiver(oracle.OWN_PREFIX, max_datagrams=1 << 21)
     r.debug_ingest_path(request.param)
