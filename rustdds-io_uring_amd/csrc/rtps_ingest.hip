@@ -682,10 +682,13 @@ __device__ unsigned long long g_proxy_stamps[16384 * PST_N];
 #define PST_FLUSH(e) do {} while (0)
 #endif
 constexpr uint32_t PT = 512;             // threads of the per-proxy workgroup (one per CU: 8 waves)
-constexpr uint32_t PPT = 4;              // consecutive events per thread
+#ifndef RTPS_PROXY_PPT
+#define RTPS_PROXY_PPT 4
+#endif
+constexpr uint32_t PPT = RTPS_PROXY_PPT;  // consecutive events per thread
 constexpr uint32_t PCH = PT * PPT;       // events per chunk
 constexpr uint32_t PH = 2 * PCH;         // chunk hash slots (>= 2 x events per chunk)
-constexpr uint32_t PH_BITS = 12;
+constexpr uint32_t PH_BITS = PPT == 2 ? 11 : PPT == 4 ? 12 : PPT == 8 ? 13 : 0;
 static_assert((1u << PH_BITS) == PH, "hash width");
 constexpr uint32_t PWAVES = PT / 64;
 
