@@ -536,19 +536,108 @@ __global__ __launch_bounds__(IT) void k_decide(uint64_t n, uint64_t cap, Scratch
 }
 
 // ---- 5 deliveries: selected events -> (record, reader slot); per-record accept counts ----
-__global__ __launch_bounds__(IT) void k_deliver(const uint64_t* n_sel, uint64_t max_out, Scratch x, rtps_delivery* out,
-                                                uint64_t* n_out) {
-  const uint64_t ns = *n_sel;
-  if (blockIdx.x == 0 && threadIdx.x == 0) *n_out = ns;
-  const uint64_t lim = ns < max_out ? ns : max_out;
-  for (uint64_t j = (uint64_t)blockIdx.x * IT + threadIdx.x; j < lim; j += (uint64_t)gridDim.x * IT) {
-    const uint32_t k = x.sel[j];
-    rtps_delivery d;
-    d.rec_idx = x.erec[k];
-    d.reader_slot = (uint16_t)(x.emeta[k] & 0xffffu);
-    d._r = 0;
-    out[j] = d;
+// The flagged events in order, as deliveries, in two launches (instead of a device
+// select of the indices and a gather): k_dcount counts each tile of DT flags;
+// k_dwrite sums the earlier tiles' counts again per workgroup (from L2: a few KB),
+// ranks its tile's flags with a block scan and writes the deliveries.
+#ifndef RTPS_DPT
+#define RTPS_DPT 8
+#endif
+constexpr uint32_t DPT = RTPS_DPT, DT = IT * DPT;  // flags per thread / per tile
+static_assert(DPT % 8 == 0 && DPT <= 32, "whole 8-B flag groups per thread");
+// nonzero bytes of a word
+__device__ __forceinline__ uint32_t nz_bytes(uint32_t v) {
+  const uint32_t t = ~(((v & 0x7f7f7f7fu) + 0x7f7f7f7fu) | v | 0x7f7f7f7fu);  // 0x80 in the zero bytes
+  return 4u - (uint32_t)__builtin_popcount(t);
+}
+__device__ __forceinline__ void dflags(const uint8_t* flag, uint64_t n, uint64_t b0, uint32_t (&w)[DPT / 4]) {
+  if (b0 + DPT <= n) {
+#pragma unroll
+    for (uint32_t q = 0; q < DPT / 8; ++q) {  // any alignment of the caller's flag array
+      uint2 a;
+      __builtin_memcpy(&a, flag + b0 + 8u * q, 8);
+      w[2 * q] = a.x; w[2 * q + 1] = a.y;
+    }
+  } else {
+#pragma unroll
+    for (uint32_t q = 0; q < DPT / 4; ++q) w[q] = 0u;
+    for (uint64_t i = b0; i < n; ++i) w[(i - b0) >> 2] |= (flag[i] ? 1u : 0u) << (8u * ((i - b0) & 3u));
   }
+}
+__device__ __forceinline__ uint64_t block_sum64(uint64_t v, uint64_t* s_w) {
+#pragma unroll
+  for (uint32_t d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  __syncthreads();
+  if ((threadIdx.x & 63u) == 0) s_w[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint64_t t = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < IT / 64; ++w) t += s_w[w];
+  return t;
+}
+__global__ __launch_bounds__(IT) void k_dcount(const uint8_t* flag, uint64_t n, uint32_t* tcnt) {
+  __shared__ uint64_t s_w[IT / 64];
+  uint32_t w[DPT / 4];
+  const uint64_t b0 = (uint64_t)blockIdx.x * DT + threadIdx.x * DPT;
+  uint32_t c = 0;
+  if (b0 < n) {
+    dflags(flag, n, b0, w);
+#pragma unroll
+    for (uint32_t q = 0; q < DPT / 4; ++q) c += nz_bytes(w[q]);
+  }
+  const uint64_t t = block_sum64(c, s_w);
+  if (threadIdx.x == 0) tcnt[blockIdx.x] = (uint32_t)t;
+}
+__global__ __launch_bounds__(IT) void k_dwrite(const uint8_t* flag, uint64_t n, const uint32_t* tcnt, uint32_t ntiles,
+                                               Scratch x, bool ident, uint64_t max_out, rtps_delivery* out,
+                                               uint64_t* n_out) {
+  __shared__ uint64_t s_w[IT / 64];
+  __shared__ uint32_t s_c[IT / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  uint64_t pre = 0;
+  for (uint32_t t = tid; t < blockIdx.x; t += IT) pre += tcnt[t];
+  pre = block_sum64(pre, s_w);
+  uint32_t w[DPT / 4];
+  const uint64_t b0 = (uint64_t)blockIdx.x * DT + tid * DPT;
+  uint32_t c = 0;
+  if (b0 < n) {
+    dflags(flag, n, b0, w);
+#pragma unroll
+    for (uint32_t q = 0; q < DPT / 4; ++q) c += nz_bytes(w[q]);
+  }
+  uint32_t incl = c;  // block-wide inclusive scan of the per-thread counts
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  if (lane == 63) s_c[wave] = incl;
+  __syncthreads();
+  uint32_t woff = 0, tot = 0;
+#pragma unroll
+  for (uint32_t v = 0; v < IT / 64; ++v) {
+    if (v < wave) woff += s_c[v];
+    tot += s_c[v];
+  }
+  uint64_t o = pre + woff + incl - c;
+  if (c) {
+#pragma unroll
+    for (uint32_t q = 0; q < DPT / 4; ++q) {
+      for (uint32_t j = 0; j < 4; ++j) {
+        if (!((w[q] >> (8u * j)) & 0xffu)) continue;
+        const uint64_t k = b0 + 4u * q + j;
+        if (o < max_out) {
+          rtps_delivery d;
+          d.rec_idx = ident ? (uint32_t)k : x.erec[k];
+          d.reader_slot = (uint16_t)(x.emeta[k] & 0xffffu);
+          d._r = 0;
+          out[o] = d;
+        }
+        ++o;
+      }
+    }
+  }
+  if (blockIdx.x + 1 == ntiles && tid == 0) *n_out = pre + tot;
 }
 __global__ __launch_bounds__(IT) void k_accept_counts(uint64_t n, uint64_t cap, Scratch x, uint8_t* accept) {
   for (uint64_t i = (uint64_t)blockIdx.x * IT + threadIdx.x; i < cap; i += (uint64_t)gridDim.x * IT) {
@@ -965,6 +1054,19 @@ __global__ void k_finish(const uint64_t* ctr, uint64_t* ovf) { if (ovf) *ovf = c
 
 static inline uint64_t hmin(uint64_t a, uint64_t b) { return a < b ? a : b; }
 
+// accepted flags[0, n) -> deliveries (k_dcount + k_dwrite; x.sel holds the tile counts)
+static void deliver(const uint8_t* flag, uint64_t n, const Scratch& x, bool ident, const rtps_ingest_out* out,
+                    hipStream_t st) {
+  const uint32_t ntiles = (uint32_t)((n + DT - 1) / DT);
+  if (ntiles == 0) {
+    (void)hipMemsetAsync(out->n_accepted, 0, sizeof(uint64_t), st);
+    return;
+  }
+  hipLaunchKernelGGL(k_dcount, dim3(ntiles), dim3(IT), 0, st, flag, n, x.sel);
+  hipLaunchKernelGGL(k_dwrite, dim3(ntiles), dim3(IT), 0, st, flag, n, x.sel, ntiles, x, ident, out->max_accepted,
+                     out->accepted, out->n_accepted);
+}
+
 }  // namespace
 
 struct IngestState {
@@ -1233,12 +1335,7 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
     hipLaunchKernelGGL(k_pseg, dim3(gm), dim3(IT), 0, st, max, t.n_proxies, x, S);
     hipLaunchKernelGGL(k_proxy, dim3(t.n_proxies), dim3(PT), 0, st, arena, s->pev, x.hval, t.n_proxies, S,
                        out->accept, out->ack_base);
-    size_t tb2 = s->tmp_bytes;
-    if (hipcub::DeviceSelect::Flagged(s->tmp, tb2, hipcub::CountingInputIterator<uint32_t>(0), out->accept, x.sel,
-                                      S.ctr + C_NDEL, (int64_t)max, st) != hipSuccess)
-      return RTPS_RX_EHIP;
-    hipLaunchKernelGGL(k_deliver, dim3(gm), dim3(IT), 0, st, S.ctr + C_NDEL, out->max_accepted, x, out->accepted,
-                       out->n_accepted);
+    deliver(out->accept, max, x, true, out, st);
     hipLaunchKernelGGL(k_finish, dim3(1), dim3(1), 0, st, S.ctr, out->n_window_overflow);
     // this batch's counts for the next batch's choice (pinned, read without a sync)
     if (hipMemcpyAsync(s->hctr2, S.ctr, C_COUNT * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -1340,12 +1437,7 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
   if (acc_cap && !per_proxy)
     hipLaunchKernelGGL(k_decide, dim3((uint32_t)hmin((acc_cap + IT - 1) / IT, 8192)), dim3(IT), 0, st, nev, acc_cap,
                        x, S, acc, have_hb, s->epoch);
-  size_t tb = s->tmp_bytes;
-  if (hipcub::DeviceSelect::Flagged(s->tmp, tb, hipcub::CountingInputIterator<uint32_t>(0), acc, x.sel,
-                                    S.ctr + C_NDEL, (int64_t)acc_cap, st) != hipSuccess)
-    return RTPS_RX_EHIP;
-  hipLaunchKernelGGL(k_deliver, dim3(gv), dim3(IT), 0, st, S.ctr + C_NDEL, out->max_accepted, x, out->accepted,
-                     out->n_accepted);
+  deliver(acc, acc_cap, x, ident, out, st);
   if (!ident)
     hipLaunchKernelGGL(k_accept_counts, dim3(gb), dim3(IT), 0, st, n_rec, max, x, out->accept);
   if (nev && !per_proxy && n_gap == 0 && (s->path == 3 || (uint64_t)t.n_proxies * W <= 4ull * nev))
