@@ -289,7 +289,7 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
     if (IDENT) {  // at most one event: write it at index i
       const uint8_t evi = cnt ? ev : EV_NONE;
       x.emeta[i] = meta;
-      x.erec[i] = (uint32_t)i;
+      if (!FAST) x.erec[i] = (uint32_t)i;  // (the per-proxy identity path reads no event -> record map)
       if (!FAST) {  // (the per-proxy identity path reads the packed events instead)
         x.evt[i] = evi;
         x.ent[i] = ent;
