@@ -264,6 +264,12 @@ __device__ __forceinline__ void wide_slot(const CdrProg& P, const CdrSlot& S, co
 
 // Segment of an all-little-endian chunk: a plain block copy of dwords*4 bytes
 // per record from value + wire_off, 16 B per lane, rpi records per pass.
+// WIDE (a separate kernel instantiation, for programs with a segment of more than
+// 32 quads: one record per pass, T's 976-B arrays): four records' quads are loaded
+// before any is stored, so a lane's loads are in flight together (a store between
+// them would order them).  T 446 -> 433-441 us; in the instantiation every program
+// uses it cost C2 (four records per pass) 145 -> 162-198 us, hence the template.
+template <bool WIDE>
 __device__ __forceinline__ void seg_copy(const CdrProg& P, const CdrSlot& S, const CdrArgs& a, uint32_t nv,
                                          uint32_t lane, const uint64_t* vbase, uint8_t* rowc) {
   const uint32_t nb = 4u * S.dwords;
@@ -277,7 +283,23 @@ __device__ __forceinline__ void seg_copy(const CdrProg& P, const CdrSlot& S, con
     if (q >= nq) break;
     const uint32_t bq = 16u * q;
     const bool full = bq + 16 <= nb;
-    for (uint32_t rr = lr; rr < nv; rr += rpi) {
+    uint32_t rr = lr;
+    if (WIDE && rpi == 1u && full && a.arena_len >= 16) {
+      for (; rr + 3u < nv; rr += 4u) {
+        uint4 v[4];
+        bool fast = true;
+#pragma unroll
+        for (uint32_t u = 0; u < 4u; ++u) {
+          const uint64_t abs = vbase[rr + u] + S.count + bq;
+          fast = fast && abs + 16 <= a.arena_len;
+          v[u] = ld16u(a.arena + (abs + 16 <= a.arena_len ? abs : 0));
+        }
+        if (!fast) break;  // the arena tail: the per-record loop below
+#pragma unroll
+        for (uint32_t u = 0; u < 4u; ++u) st16u(rowc + (uint64_t)(rr + u) * P.row_bytes + S.out_off + bq, v[u]);
+      }
+    }
+    for (; rr < nv; rr += rpi) {
       const uint64_t abs = vbase[rr] + S.count + bq;
       uint8_t* d = rowc + (uint64_t)rr * P.row_bytes + S.out_off + bq;
       if (full && abs + 16 <= a.arena_len) {
@@ -307,6 +329,7 @@ extern __shared__ uint8_t cdr_lds[];
 // table).  Phase B: the wave writes the chunk's rows slot by slot, one 4-byte
 // word per lane and item (item = record x word of the slot), so consecutive
 // lanes store consecutive words and every row byte is written exactly once.
+template <bool WIDE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CDR_WAVES_PER_EU)))
 void cdr_decode_kernel(CdrProg P, CdrArgs a) {
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, wpb = blockDim.x >> 6;
@@ -368,7 +391,7 @@ void cdr_decode_kernel(CdrProg P, CdrArgs a) {
       const uint32_t hdr = (S.kind == RTPS_CDR_STRING || S.kind == RTPS_CDR_SEQ) ? 1u : 0u;
       if (all_okle && (S.flags & CDR_IN_SEG)) continue;
       if (all_okle && S.kind == CDR_SLOT_SEG) {
-        seg_copy(P, S, a, nv, lane, vbase, rowc);
+        seg_copy<WIDE>(P, S, a, nv, lane, vbase, rowc);
         continue;
       }
       if (S.dwords >= CDR_WIDE_DWORDS) {
@@ -531,6 +554,13 @@ int rtps_cdr_launch(hipStream_t s, const CdrProg& P, const CdrArgs& a, uint32_t 
   uint64_t blocks = (chunks + wpb - 1) / wpb;
   if (blocks > (uint64_t)max_blocks * CDR_GRID_MULT) blocks = (uint64_t)max_blocks * CDR_GRID_MULT;
   if (blocks == 0) return 0;
-  hipLaunchKernelGGL(cdr_decode_kernel, dim3((uint32_t)blocks), dim3(64 * wpb), wpb * P.lds_per_wave, s, P, a);
+  bool wide = false;  // a segment of more than 32 quads: one record per pass (seg_copy<true>)
+  for (uint32_t i = 0; i < P.n_slots; ++i)
+    wide = wide || (P.slots[i].kind == CDR_SLOT_SEG && (P.slots[i].dwords + 3u) / 4u > 32u);
+  if (wide)
+    hipLaunchKernelGGL(cdr_decode_kernel<true>, dim3((uint32_t)blocks), dim3(64 * wpb), wpb * P.lds_per_wave, s, P, a);
+  else
+    hipLaunchKernelGGL(cdr_decode_kernel<false>, dim3((uint32_t)blocks), dim3(64 * wpb), wpb * P.lds_per_wave, s, P,
+                       a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
