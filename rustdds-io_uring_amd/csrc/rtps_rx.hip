@@ -1447,86 +1447,8 @@ __global__ __launch_bounds__(TILE, RTPS_LDS_WG_PER_CU) void rtps_parse_lds_kerne
   LDS_STAMP(7);
 }
 
-#ifdef RTPS_ITEM_DIAG
-// Diagnostic (variant builds only): the cost of a record-parallel write pass that
-// knows every record's (datagram, submessage offset) already, as a chained
-// kernel would after a count walk that left those items behind.  Thread per
-// record: reload the window (+ the header prefix and the first submessage, as
-// the interpreter state would need), run the per-kind reader and the record tail,
-// store the record (mode 0 per lane, mode 1 through an LDS transpose).
-__global__ __launch_bounds__(TILE) void rtps_item_diag_kernel(KParams p, const rtps_record* rin, uint64_t nrec,
-                                                              uint32_t mode) {
-  __shared__ u32x4 s_t[TILE * 4];
-  mt_stage(p);
-  __syncthreads();
-  const uint32_t tid = threadIdx.x;
-  const uint64_t r = (uint64_t)blockIdx.x * TILE + tid;
-  const bool live = r < nrec;
-  Rec R;
-  rec_clear(R);
-  uint32_t tgt = RTPS_NO_TARGET;
-  if (live) {
-    const u32x4 a = reinterpret_cast<const u32x4*>(rin + r)[0];
-    const u32x4 z = reinterpret_cast<const u32x4*>(rin + r)[1];
-    const u32x4 t = reinterpret_cast<const u32x4*>(rin + r)[3];
-    const uint32_t d = a[0], o = a[1] & 0xffffu, kind = (a[1] >> 16) & 0xffu, flags = a[1] >> 24;
-    const uint32_t route_in = (z[3] >> 16) & 0xffu;
-    Src s;
-    const uint64_t al = p.arena_len;
-    s.avail = al > 0xffffffffull ? 0xffffffffu : (uint32_t)al;
-    s.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p.arena), (short)0, (int)s.avail, 0x00020000);
-    s.base = (uint32_t)p.dgram_off[d];
-    const uint32_t L = p.dgram_len[d];
-    Win W;
-    load_win_pf(s, o, W);
-    const u32x4 hp = ld16(s, 8u), first = ld16(s, 20u);
-    if (kind == RTPS_DATA_FRAG) W.w[8] = ld4(s, o + 32u);
-    const bool le = (flags & 1u) != 0u;
-    const uint32_t eff = eff_len(kind, e16(W.w[0], 1, le), L - o);
-    SubOut so;
-    if (mode & 2u) {  // ablation: no per-kind reader (the window loads stay)
-      so.cls = kind == RTPS_DATA ? 1u : 3u; so.route = 0; so.pk = 0; so.aux16 = eff; so.rid = W.w[2]; so.wid = W.w[3];
-      R.d[8] = W.w[4] ^ W.w[5] ^ W.w[6] ^ W.w[7] ^ W.w[8];
-    } else {
-      sub_body<true>(s, W, kind, flags, le, o + 4u, eff, R, so);
-    }
-    Interp st;
-    st.src0 = a[2]; st.src1 = a[3]; st.src2 = z[0];
-    if (kind == RTPS_INFO_DST || (st.src0 == hp[0] && st.src1 == hp[1] && st.src2 == hp[2])) {
-      st.src0 = hp[0]; st.src1 = hp[1]; st.src2 = hp[2];
-    }
-    st.dst_ok = (route_in & RTPS_ROUTE_PASS) != 0u || (first[0] & 0xffu) == 0xffu;
-    st.ts_valid = (route_in & RTPS_ROUTE_TS_VALID) != 0u;
-    st.ts_sec = t[2]; st.ts_frac = t[3];
-    R.d[0] = d;
-    R.d[1] = a[1];
-    if (mode & 4u) {  // ablation: no classification (no reader-table probe)
-      R.d[2] = st.src0; R.d[3] = st.src1; R.d[4] = st.src2; R.d[5] = so.wid; R.d[6] = so.rid;
-      R.d[7] = so.aux16 | (so.route << 16) | (so.pk << 24); R.d[14] = st.ts_sec; R.d[15] = st.ts_frac;
-    } else {
-      tgt = rec_finish(p, R, so, kind, st);
-    }
-  }
-  if (mode & 8u) {  // ablation: no record stores (one word per record keeps the work live)
-    if (live) p.target_out[r] = tgt ^ R.d[0] ^ R.d[1] ^ R.d[2] ^ R.d[3] ^ R.d[4] ^ R.d[5] ^ R.d[6] ^ R.d[7] ^ R.d[8] ^
-                                R.d[9] ^ R.d[10] ^ R.d[11] ^ R.d[12] ^ R.d[13] ^ R.d[14] ^ R.d[15];
-    return;
-  }
-  if ((mode & 1u) == 0) {
-    if (live) rec_store(p.records + r, R);
-  } else {
-    s_t[tid * 4 + 0] = u32x4{R.d[0], R.d[1], R.d[2], R.d[3]};
-    s_t[tid * 4 + 1] = u32x4{R.d[4], R.d[5], R.d[6], R.d[7]};
-    s_t[tid * 4 + 2] = u32x4{R.d[8], R.d[9], R.d[10], R.d[11]};
-    s_t[tid * 4 + 3] = u32x4{R.d[12], R.d[13], R.d[14], R.d[15]};
-    __syncthreads();
-    const uint64_t r0 = (uint64_t)blockIdx.x * TILE;
-    const uint32_t nv = (uint32_t)min<uint64_t>(TILE, nrec - r0);
-    u32x4* dst = reinterpret_cast<u32x4*>(p.records + r0);
-    for (uint32_t q = tid; q < nv * 4u; q += TILE) dst[q] = s_t[q];
-  }
-  if (live && p.target_out) p.target_out[r] = tgt;
-}
+#ifdef RTPS_ITEM_DIAG  // diagnostic variant builds only (scripts/diag_item_pass.py)
+#include "diag/item_pass_kernel.inc"
 #endif
 
 // device-side synthetic generator: one lane per datagram
@@ -2176,23 +2098,7 @@ int rtps_rx_debug_set_chain_epoch(rtps_rx_ctx* c, uint32_t epoch) {
 }
 
 #ifdef RTPS_ITEM_DIAG
-/* diagnostic (variant builds): the record-parallel write pass over a parse's records */
-int rtps_rx_debug_item_pass(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len, const uint64_t* dgram_off,
-                            const uint32_t* dgram_len, uint32_t n, const rtps_record* rin, uint64_t nrec,
-                            const rtps_rx_out* out, uint32_t mode) {
-  if (!c || !out || !rin) return RTPS_RX_EINVAL;
-  (void)hipSetDevice(c->device);
-  KParams p{};
-  p.arena = arena; p.arena_len = arena_len; p.dgram_off = dgram_off; p.dgram_len = dgram_len; p.n = n;
-  memcpy(&p.own0, c->own + 0, 4); memcpy(&p.own1, c->own + 4, 4); memcpy(&p.own2, c->own + 8, 4);
-  p.records = out->records; p.max_records = out->max_records; p.target_out = out->target;
-  p.rt = rt_dev(c->readers);
-  p.rt_lds = rt_fits_lds(p.rt) ? 1u : 0u;
-  const uint32_t mt_lds = p.rt_lds ? rt_lds_bytes(p.rt.gmask + 1u, p.rt.emask + 1u) : 0u;
-  const uint32_t grid = (uint32_t)((nrec + TILE - 1) / TILE);
-  hipLaunchKernelGGL(rtps_item_diag_kernel, dim3(grid), dim3(TILE), mt_lds, c->stream, p, rin, nrec, mode);
-  return hip_fail(hipGetLastError());
-}
+#include "diag/item_pass_host.inc"
 #endif
 
 /* diagnostics (not part of the public header): copy the first k scratch words */
