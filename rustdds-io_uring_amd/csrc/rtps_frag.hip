@@ -1011,7 +1011,7 @@ __device__ __forceinline__ void gst16(uint8_t* p, uint4 v) {
 #define RTPS_SPAN_U 3       // 16-B loads in flight per lane (3 KiB per wave per step: two C4 records)
 #endif
 #ifndef SPAN_GRID
-#define SPAN_GRID 8192
+#define SPAN_GRID 16384  // span-copy workgroups at most: 16384 0.687-0.688 ms per C4 step, 8192 0.692-0.694, 4096 0.697-0.699
 #endif
 constexpr uint32_t SPAN_U = RTPS_SPAN_U;
 struct SpanDesc {  // 32 B: arena offset of the payload, heap / pending-store address, bytes
