@@ -193,3 +193,24 @@ def test_workload_parity(rx, wl, n, multi):
             assert na == n
         elif multi:
             assert int((acc > 1).sum()) > 10000
+
+
+import reader_known  # noqa: E402
+
+
+@pytest.mark.parametrize("case", reader_known.cases(), ids=[c["name"] for c in reader_known.cases()])
+def test_reader_known_answers(rx, case):
+    """The reference's Reader unit tests (io_uring/rtps/reader.rs:1537-1988) through
+    rtps_rx_parse_batch + rtps_rx_ingest on every ingest path: all_ackable_before 3 -> 5 -> 6
+    (GAP, DATA, GAP), HEARTBEAT counts, the stateless reader, the delivered change's fields."""
+    state = {}
+
+    def fn(rd, arena, off, ln):
+        if not state:
+            rx.set_readers(rd)
+            rx.ingest_reset()
+            state["set"] = True
+        res, acc, dels, ack, ovf, _ = rx.ingest_batch(arena, off, ln, rd.n_proxies)
+        assert ovf == 0
+        return res.records, dels, ack, res.target
+    reader_known.check(case, fn)

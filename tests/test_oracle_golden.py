@@ -71,3 +71,16 @@ def test_threads_equal_single():
             assert all(np.array_equal(u, v) for u, v in zip(x, y))
         else:
             assert np.array_equal(x, y)
+
+
+import reader_known  # noqa: E402
+
+READER_CASES = reader_known.cases()
+
+
+@pytest.mark.parametrize("case", READER_CASES, ids=[c["name"] for c in READER_CASES])
+def test_oracle_reader_known_answers(case):
+    """The reference's Reader unit tests (io_uring/rtps/reader.rs:1537-1988): all_ackable_before
+    3 -> 5 -> 6 over GAP / DATA / GAP, duplicate HEARTBEAT counts ignored, no proxy in a stateless
+    reader, the topic-cache change of a default DATA; through the oracle's parse + ingest."""
+    reader_known.check(case, reader_known.oracle_batch_fn())
