@@ -4,6 +4,7 @@
 // available_readers BTreeMap<EntityId, Reader> (io_uring/rtps/message_receiver.rs:129;
 // EntityId derives Ord over {entity_key[3], entity_kind}: byte order, structure/guid.rs:208-216).
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -42,28 +43,42 @@ struct ReaderTable {
   uint32_t *gkeys = nullptr, *gset = nullptr, *ekeys = nullptr, *eset = nullptr, *dfirst = nullptr;
   rtps_target* dent = nullptr;
   uint32_t gcap = 0, ecap = 0;
-  size_t first_cap = 0, ent_cap = 0;
 };
 
 ReaderTable* rt_new() { return new (std::nothrow) ReaderTable(); }
 
+// Device memory of the tables.  rt_set builds every image into fresh buffers and
+// swaps them in only when all of them are uploaded, so a failed call leaves the
+// previous table whole (readers and proxies of the last successful call).  The
+// operations are indirect so that a CPU test can run rt_set on host memory with
+// an injected allocation failure (rtps_rx_debug_rt_* below).
+struct DevMem {
+  void* (*alloc)(size_t);
+  void (*release)(void*);
+  bool (*upload)(void* dst, const void* src, size_t n);
+  bool (*sync)(hipStream_t);
+};
+namespace {
+void* hip_alloc(size_t n) {
+  void* p = nullptr;
+  return hipMalloc(&p, n ? n : 1) == hipSuccess ? p : nullptr;
+}
+void hip_release(void* p) { if (p) (void)hipFree(p); }
+bool hip_upload(void* d, const void* s, size_t n) { return !n || hipMemcpy(d, s, n, hipMemcpyHostToDevice) == hipSuccess; }
+bool hip_sync(hipStream_t st) { return hipStreamSynchronize(st) == hipSuccess; }
+int g_fail_at = -1, g_allocs = 0;  // host-memory test mode: fail the g_fail_at-th allocation
+void* host_alloc(size_t n) { return g_allocs++ == g_fail_at ? nullptr : malloc(n ? n : 1); }
+void host_release(void* p) { free(p); }
+bool host_upload(void* d, const void* s, size_t n) { if (n) memcpy(d, s, n); return true; }
+bool host_sync(hipStream_t) { return true; }
+DevMem g_mem = {hip_alloc, hip_release, hip_upload, hip_sync};
+}  // namespace
+
 void rt_free(ReaderTable* t) {
   if (!t) return;
   void* p[] = {t->gkeys, t->gset, t->ekeys, t->eset, t->dfirst, t->dent};
-  for (void* q : p)
-    if (q) (void)hipFree(q);
+  for (void* q : p) g_mem.release(q);
   delete t;
-}
-
-template <typename T>
-static bool ensure(T*& p, size_t& cap, size_t n) {
-  if (n <= cap && p) return true;
-  if (p) (void)hipFree(p);
-  p = nullptr;
-  cap = 0;
-  if (hipMalloc(&p, (n ? n : 1) * sizeof(T)) != hipSuccess) return false;
-  cap = n;
-  return true;
 }
 
 namespace {
@@ -186,26 +201,26 @@ int rt_set(ReaderTable* t, const rtps_reader* readers, uint32_t nr, const rtps_p
   const uint32_t gcap = b.gcap, ecap = b.ecap;
   std::vector<uint32_t>&gkeys = b.gkeys, &gset = b.gset, &ekeys = b.ekeys, &eset = b.eset, &first = b.first;
   std::vector<rtps_target>& ent = b.ent;
-  // ---- upload (the previous batch may still read the old tables) ----
-  if (hipStreamSynchronize(stream) != hipSuccess) return RTPS_RX_EHIP;
-  size_t c1 = t->gcap * 4, c2 = t->gcap, c3 = t->ecap, c4 = t->ecap;
-  if (gcap > t->gcap) {
-    if (!ensure(t->gkeys, c1, (size_t)gcap * 4) || !ensure(t->gset, c2, gcap)) return RTPS_RX_ENOMEM;
-    t->gcap = gcap;
+  // ---- upload into new buffers; swap them in only when every step succeeded ----
+  if (!g_mem.sync(stream)) return RTPS_RX_EHIP;  // the previous batch may still read the old tables
+  void* nb[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  const void* src[6] = {gkeys.data(), gset.data(), ekeys.data(), eset.data(), first.data(), ent.data()};
+  const size_t bytes[6] = {gkeys.size() * 4, gset.size() * 4, ekeys.size() * 4, eset.size() * 4, first.size() * 4,
+                           ent.size() * sizeof(rtps_target)};
+  int err = RTPS_RX_OK;
+  for (int k = 0; k < 6 && !err; ++k) {
+    nb[k] = g_mem.alloc(bytes[k]);
+    if (!nb[k]) err = RTPS_RX_ENOMEM;
+    else if (!g_mem.upload(nb[k], src[k], bytes[k])) err = RTPS_RX_EHIP;
   }
-  if (ecap > t->ecap) {
-    if (!ensure(t->ekeys, c3, ecap) || !ensure(t->eset, c4, ecap)) return RTPS_RX_ENOMEM;
-    t->ecap = ecap;
+  if (err) {
+    for (void* q : nb) g_mem.release(q);
+    return err;
   }
-  if (!ensure(t->dfirst, t->first_cap, first.size()) || !ensure(t->dent, t->ent_cap, ent.size())) return RTPS_RX_ENOMEM;
-  // the device tables are written at their own capacity (gmask/emask = the new capacities)
-  if (hipMemcpy(t->gkeys, gkeys.data(), gkeys.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(t->gset, gset.data(), gset.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(t->ekeys, ekeys.data(), ekeys.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(t->eset, eset.data(), eset.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(t->dfirst, first.data(), first.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-      (!ent.empty() && hipMemcpy(t->dent, ent.data(), ent.size() * sizeof(rtps_target), hipMemcpyHostToDevice) != hipSuccess))
-    return RTPS_RX_EHIP;
+  void* old[6] = {t->gkeys, t->gset, t->ekeys, t->eset, t->dfirst, t->dent};
+  for (void* q : old) g_mem.release(q);
+  t->gkeys = (uint32_t*)nb[0]; t->gset = (uint32_t*)nb[1]; t->ekeys = (uint32_t*)nb[2]; t->eset = (uint32_t*)nb[3];
+  t->dfirst = (uint32_t*)nb[4]; t->dent = (rtps_target*)nb[5];
   t->gcap = gcap;  // the images above are exactly gcap / ecap slots
   t->ecap = ecap;
   t->first.swap(first);
@@ -286,4 +301,27 @@ extern "C" int rtps_rx_debug_target_sets(const rtps_reader* readers, uint32_t nr
   memcpy(first, b.first.data(), b.first.size() * 4);
   if (!b.ent.empty()) memcpy(ent, b.ent.data(), b.ent.size() * sizeof(rtps_target));
   return RTPS_RX_OK;
+}
+
+/* test hooks (not part of the public header, no GPU needed): a reader table on
+   host memory whose fail_at-th buffer allocation fails (-1: none), to check that
+   a failed rtps_rx_set_readers leaves the previous table in place. */
+extern "C" {
+int rtps_rx_debug_rt_host_mode(int fail_at) {
+  g_mem = {host_alloc, host_release, host_upload, host_sync};
+  g_fail_at = fail_at;
+  g_allocs = 0;
+  return RTPS_RX_OK;
+}
+void* rtps_rx_debug_rt_new(void) { return rt_new(); }
+void rtps_rx_debug_rt_free(void* t) { rt_free(static_cast<ReaderTable*>(t)); }
+int rtps_rx_debug_rt_set(void* t, const rtps_reader* readers, uint32_t nr, const rtps_proxy* proxies, uint32_t np) {
+  return rt_set(static_cast<ReaderTable*>(t), readers, nr, proxies, np, nullptr);
+}
+/* the device view rt_dev returns (pointers into the table's buffers) */
+int rtps_rx_debug_rt_view(const void* t, ReaderDev* out) {
+  if (!out) return RTPS_RX_EINVAL;
+  *out = rt_dev(static_cast<const ReaderTable*>(t));
+  return RTPS_RX_OK;
+}
 }

@@ -103,3 +103,65 @@ def test_validation_errors():
     for rd in (dup_reader, dup_proxy, bad_index):
         assert _build(rd)[0] == -1  # RTPS_RX_EINVAL
     assert _build(Readers())[0] == 0
+
+
+_RT_FAIL_SCRIPT = r'''
+import ctypes, sys
+import numpy as np
+sys.path[:0] = sys.argv[1:3]
+import rtps_rx
+from rtps_rx.records import Readers
+L = rtps_rx.lib()
+P, U32 = ctypes.c_void_p, ctypes.c_uint32
+class View(ctypes.Structure):
+    _fields_ = [(n, P) for n in ("gkeys", "gset", "ekeys", "eset", "set_first", "set_ent")] + \
+               [(n, U32) for n in ("gmask", "emask", "n_writer_sets", "n_sets", "n_proxies", "max_set")]
+L.rtps_rx_debug_rt_new.restype = P
+L.rtps_rx_debug_rt_free.argtypes = [P]
+L.rtps_rx_debug_rt_set.argtypes = [P, P, U32, P, U32]
+L.rtps_rx_debug_rt_view.argtypes = [P, ctypes.POINTER(View)]
+def table(n_writers, slot):
+    rd = Readers([(bytes([0, 0, slot, 7]), slot, 0)], [(bytes([9] * 12) + bytes([0, 0, w, 2]), 0) for w in range(n_writers)])
+    return rd.readers, rd.proxies
+def rt_set(t, rd):
+    return L.rtps_rx_debug_rt_set(t, rd[0].ctypes.data, len(rd[0]), rd[1].ctypes.data, len(rd[1]))
+def view(t):
+    v = View(); L.rtps_rx_debug_rt_view(t, ctypes.byref(v)); return v
+def words(addr, n):
+    return np.ctypeslib.as_array(ctypes.cast(addr, ctypes.POINTER(ctypes.c_uint32)), shape=(n,)).copy()
+L.rtps_rx_debug_rt_host_mode(-1)
+t = L.rtps_rx_debug_rt_new()
+a, b = table(3, 1), table(40, 2)
+assert rt_set(t, a) == 0
+va = view(t)
+ga = words(va.gset, va.gmask + 1)
+for fail_at in range(6):  # every one of the six table buffers
+    L.rtps_rx_debug_rt_host_mode(fail_at)
+    assert rt_set(t, b) == -3, fail_at             # RTPS_RX_ENOMEM
+    v = view(t)
+    assert (v.gkeys, v.gset, v.ekeys, v.eset, v.set_first, v.set_ent) == \
+           (va.gkeys, va.gset, va.ekeys, va.eset, va.set_first, va.set_ent), fail_at
+    assert (v.gmask, v.n_sets, v.n_proxies) == (va.gmask, va.n_sets, va.n_proxies) == (va.gmask, 6, 3)
+    assert np.array_equal(words(v.gset, v.gmask + 1), ga)
+L.rtps_rx_debug_rt_host_mode(-1)
+assert rt_set(t, b) == 0
+vb = view(t)
+assert vb.n_proxies == 40 and vb.n_sets == 80 and vb.gkeys
+assert sorted(words(vb.gset, vb.gmask + 1).tolist())[:40] == list(range(40))
+L.rtps_rx_debug_rt_free(t)
+print("ok")
+'''
+
+
+def test_failed_set_readers_keeps_previous_table():
+    """ADVICE r2: a set_readers whose allocation fails part-way must leave the previous
+    device tables whole (build into new buffers, swap on success).  Host-memory mode of the
+    table's allocator, failing each of the six buffers in turn (isolated process)."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    repo = os.path.dirname(here)
+    r = subprocess.run([sys.executable, "-c", _RT_FAIL_SCRIPT, os.path.join(repo, "rustdds-io_uring_amd"), repo],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stdout + r.stderr
