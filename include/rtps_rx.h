@@ -354,6 +354,90 @@ int rtps_rx_exchange_comm_destroy(void* comm);
 int rtps_rx_exchange(rtps_rx_ctx* ctx, void* comm, void* hip_stream, const void* send, const uint64_t* send_counts,
                      uint64_t cap, uint32_t item_bytes, void* recv, uint64_t* recv_counts);
 
+/* ---- owner-side exchange: what a writer's owner GPU consumes (>= 2 GPUs) ----
+ * The per-writer state of the receive path (fragment assembly and the writer
+ * proxies: io_uring/rtps/reader.rs:563-758, rtps/rtps_writer_proxy.rs:202-355,
+ * structure/dds_cache.rs:241-252) is only right where ALL of a writer's
+ * submessages meet: on its owner GPU.  rtps_rx_shard_* move there every record
+ * that state consumes, so that the owner runs rtps_rx_frag_assemble and
+ * rtps_rx_ingest as one GPU would on the whole stream:
+ *   - items: every writer-kind record that passes (RTPS_ROUTE_PASS: DATA,
+ *     DATA_FRAG, HEARTBEAT, HEARTBEAT_FRAG, GAP), owner = fmix32(fnv1a32(prefix ||
+ *     writer_id)) % n_ranks (as rtps_rx_bucket_by_writer), each with its "blob":
+ *     the arena bytes the owner's consumers read (a GAP's bitmap words, a
+ *     DATA_FRAG's payload), 16-byte aligned.  DATA payloads stay on the source
+ *     GPU (zero-copy): an owner record names its origin instead;
+ *   - order: rank r parses the r-th contiguous chunk of the stream, so the
+ *     records an owner receives, concatenated in source-rank order, are its
+ *     writers' records in stream order;
+ *   - capacity: round 0 moves fixed slots (cap records and bcap blob bytes per
+ *     peer: equal splits, no host round trip).  A source's records past its slot
+ *     go in a second round of exact size (the spill) once the host has read the
+ *     counts, so nothing is dropped whatever the traffic mix.
+ * Sequence per batch: rtps_rx_parse_batch, rtps_rx_shard_pack (context stream),
+ * rtps_rx_shard_exchange (round 0, asynchronous), rtps_rx_shard_finish (waits
+ * for the counts; spill round if needed), rtps_rx_shard_unpack -> an owner batch
+ * for rtps_rx_frag_assemble / rtps_rx_ingest on the same context.
+ * New: the reference has one process and no exchange. */
+typedef struct rtps_shard rtps_shard;
+typedef struct rtps_shard_counts {  /* one (source, destination) pair */
+  uint64_t n;          /* records */
+  uint64_t bytes;      /* blob bytes (multiple of 16) */
+  uint64_t cut;        /* records in the fixed slot: the first `cut` (the rest is spill) */
+  uint64_t cut_bytes;  /* blob bytes of those records */
+} rtps_shard_counts;
+#define RTPS_SHARD_LEAD 65536u  /* zero bytes ahead of the owner arena's blobs */
+typedef struct rtps_owner_batch {  /* DEVICE pointers owned by the shard, valid until its next unpack */
+  const uint8_t* arena;            /* RTPS_SHARD_LEAD zero bytes, then the received blobs */
+  uint64_t arena_len;
+  const uint64_t* dgram_off;       /* [n_records]: record i's dgram_idx is i, its blob is at
+                                      arena + dgram_off[i] + (u.gap.bitmap_off | u.frag.pl_off) */
+  const rtps_record* records;      /* [n_records], stream order; every field as parsed except dgram_idx */
+  const uint64_t* origin;          /* [n_records]: source rank << 32 | the record's dgram_idx in the source
+                                      rank's batch (with sub_off it names the submessage) */
+  const uint64_t* n_records_dev;   /* device u64 (for the consumers' n_records argument) */
+  uint64_t n_records;              /* host copy */
+} rtps_owner_batch;
+/* cap: records per peer slot (>= 1); bcap: blob bytes per peer slot (a multiple of 16). */
+int rtps_rx_shard_create(rtps_rx_ctx* ctx, uint32_t n_ranks, uint64_t cap, uint64_t bcap, rtps_shard** out);
+int rtps_rx_shard_destroy(rtps_shard* s);
+/* Source side: partition this rank's parse output by owner into the fixed slots and
+ * the spill, with the blobs (asynchronous on the context's stream). */
+int rtps_rx_shard_pack(rtps_shard* s, const uint8_t* arena, uint64_t arena_len, const uint64_t* dgram_off,
+                       const rtps_record* records, const uint64_t* n_records, uint64_t max_records);
+/* Round 0 over RCCL (comm as for rtps_rx_exchange): one ncclGroupStart/End of, per peer,
+ * the counts, the record slot and the blob slot, on hip_stream (NULL: the context's
+ * stream), after the pack; then the counts are copied to the host.  Asynchronous. */
+int rtps_rx_shard_exchange(rtps_shard* s, void* comm, void* hip_stream);
+/* Waits for round 0's counts; if any pair overflowed its slot, moves the spill in a
+ * second group of exact sizes (both ends know them from the counts).  After an
+ * RTPS_RX_EHIP from either call the communicator is aborted and unusable. */
+int rtps_rx_shard_finish(rtps_shard* s, void* comm, void* hip_stream);
+/* Owner side: every received record as one batch (reads the received counts: a host sync). */
+int rtps_rx_shard_unpack(rtps_shard* s, rtps_owner_batch* out);
+/* The same protocol over a host-driven transport (e.g. gloo): the buffers round 0
+ * moves and the spill areas.  Spill layouts: send side, destination d's records at
+ * sum_{d' < d} n_d' and its bytes at sum_{d' < d} bytes_d' (the spilled ones are
+ * [cut, n) / [cut_bytes, bytes) of that range); receive side, source s's spilled
+ * records at sum_{s' < s} (n - cut), its bytes at sum_{s' < s} (bytes - cut_bytes). */
+typedef struct rtps_shard_buffers {
+  void* send_slots;        /* [n_ranks * cap] records; peer d's slot at d * cap */
+  void* send_blob;         /* [n_ranks * bcap] */
+  void* send_counts;       /* [n_ranks] rtps_shard_counts */
+  void* recv_slots;
+  void* recv_blob;
+  void* recv_counts;
+  void* send_spill;
+  void* send_blob_spill;
+  void* recv_spill;
+  void* recv_blob_spill;
+  uint64_t recv_spill_cap;       /* records */
+  uint64_t recv_blob_spill_cap;  /* bytes */
+} rtps_shard_buffers;
+int rtps_rx_shard_buffers(rtps_shard* s, rtps_shard_buffers* out);
+/* Grow the receive spill to hold `records` records and `bytes` blob bytes. */
+int rtps_rx_shard_reserve_spill(rtps_shard* s, uint64_t records, uint64_t bytes);
+
 /* ---- batch CDR primitive decode (a18) ------------------------------------
  * Replaces, for fixed-layout sample types, the per-sample decode
  *   SimpleDataReader::deserialize_with -> DA::from_bytes_with(&payload.value, rep_id, ..)

@@ -2,8 +2,8 @@
 //
 // One rank per GPU parses its contiguous chunk of datagrams; the writer /
 // reader records are bucketed by owner rank on the device
-// (rtps_rx_bucket_by_writer_padded: owner = fnv1a32(prefix || writer_id) % world,
-// or rtps_rx_bucket_descriptors) into fixed-capacity buckets, and this file
+// (rtps_rx_bucket_by_writer_padded: owner = fmix32(fnv1a32(prefix || writer_id))
+// % world, or rtps_rx_bucket_descriptors) into fixed-capacity buckets, and this file
 // moves bucket d to rank d: ONE grouped ncclSend / ncclRecv per peer
 // (ncclGroupStart / ncclGroupEnd) of the equal-split buckets plus their true
 // counts, on the context's stream.  Equal splits need no device-to-host round
@@ -11,12 +11,24 @@
 // reference has one process and no collective; this is the path's only one.
 // xGMI is point-to-point (one link per peer pair on an 8-GPU MI355X node), so
 // per-peer send/recv is the natural all-to-all there.
+//
+// The owner-side exchange (rtps_rx_shard_exchange / _finish, state in
+// rtps_shard.h) moves what the owner's fragment assembly and ingest consume:
+// round 0 is the same equal-split group (counts, record slot, blob slot per
+// peer); round 1 moves, only for the pairs whose items did not fit the slots,
+// the exact remainder, whose size both ends read from round 0's counts.
+//
+// Failure: if enqueuing a send or receive fails part-way, the peers would wait
+// for operations that were never posted, so the group is ended and the
+// communicator aborted (ncclCommAbort): the caller gets RTPS_RX_EHIP and must
+// make a new communicator.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <string.h>
 
 #include "../../include/rtps_rx.h"
 #include "rtps_ctx.h"
+#include "rtps_shard.h"
 
 static_assert(RTPS_RX_EXCHANGE_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "unique id size");
 
@@ -68,7 +80,96 @@ int rtps_rx_exchange(rtps_rx_ctx* ctx, void* comm, void* hip_stream, const void*
          ncclRecv(r + (size_t)p * bytes, bytes, ncclUint8, p, c, st) == ncclSuccess;
   }
   const bool ended = ncclGroupEnd() == ncclSuccess;
-  return ok && ended ? RTPS_RX_OK : RTPS_RX_EHIP;
+  if (!ok || !ended) {
+    (void)ncclCommAbort(c);
+    return RTPS_RX_EHIP;
+  }
+  return RTPS_RX_OK;
+}
+
+int rtps_rx_shard_exchange(rtps_shard* s, void* comm, void* hip_stream) {
+  if (!s || !comm) return RTPS_RX_EINVAL;
+  ncclComm_t c = (ncclComm_t)comm;
+  int world = 0;
+  if (ncclCommCount(c, &world) != ncclSuccess) return RTPS_RX_EHIP;
+  if ((uint32_t)world != s->n_ranks) return RTPS_RX_EINVAL;
+  if (hipSetDevice(s->device) != hipSuccess) return RTPS_RX_EHIP;
+  hipStream_t st = hip_stream ? (hipStream_t)hip_stream : rtps_ctx_stream(s->ctx);
+  if (hipStreamWaitEvent(st, s->packed, 0) != hipSuccess) return RTPS_RX_EHIP;  // the slots are complete
+  const size_t rb = (size_t)s->cap * sizeof(rtps_record), bb = (size_t)s->bcap;
+  const size_t cw = sizeof(rtps_shard_counts) / sizeof(uint64_t);
+  if (ncclGroupStart() != ncclSuccess) return RTPS_RX_EHIP;
+  bool ok = true;
+  for (int p = 0; p < world && ok; ++p) {
+    ok = ncclSend(s->s_counts + p, cw, ncclUint64, p, c, st) == ncclSuccess &&
+         ncclRecv(s->r_counts + p, cw, ncclUint64, p, c, st) == ncclSuccess &&
+         ncclSend(reinterpret_cast<const uint8_t*>(s->s_slots) + p * rb, rb, ncclUint8, p, c, st) == ncclSuccess &&
+         ncclRecv(reinterpret_cast<uint8_t*>(s->r_slots) + p * rb, rb, ncclUint8, p, c, st) == ncclSuccess &&
+         (bb == 0 || (ncclSend(s->s_blob + p * bb, bb, ncclUint8, p, c, st) == ncclSuccess &&
+                      ncclRecv(s->r_blob + p * bb, bb, ncclUint8, p, c, st) == ncclSuccess));
+  }
+  const bool ended = ncclGroupEnd() == ncclSuccess;
+  if (!ok || !ended) {
+    (void)ncclCommAbort(c);
+    return RTPS_RX_EHIP;
+  }
+  const size_t nb = (size_t)world * sizeof(rtps_shard_counts);
+  if (hipMemcpyAsync(s->h_send, s->s_counts, nb, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipMemcpyAsync(s->h_recv, s->r_counts, nb, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipEventRecord(s->counts_ev, st) != hipSuccess || hipEventRecord(s->done, st) != hipSuccess)
+    return RTPS_RX_EHIP;
+  s->exchanged = true;
+  return RTPS_RX_OK;
+}
+
+int rtps_rx_shard_finish(rtps_shard* s, void* comm, void* hip_stream) {
+  if (!s || !comm) return RTPS_RX_EINVAL;
+  if (!s->exchanged) return RTPS_RX_EINVAL;  // no round 0 to finish
+  ncclComm_t c = (ncclComm_t)comm;
+  if (hipSetDevice(s->device) != hipSuccess) return RTPS_RX_EHIP;
+  hipStream_t st = hip_stream ? (hipStream_t)hip_stream : rtps_ctx_stream(s->ctx);
+  if (hipEventSynchronize(s->counts_ev) != hipSuccess) return RTPS_RX_EHIP;
+  const uint32_t world = s->n_ranks;
+  // spill sizes: what this rank still sends to each peer, what it still receives
+  uint64_t need_r = 0, need_b = 0, any = 0;
+  for (uint32_t p = 0; p < world; ++p) {
+    const rtps_shard_counts& r = s->h_recv[p];
+    const rtps_shard_counts& q = s->h_send[p];
+    if (r.cut > r.n || r.cut_bytes > r.bytes || q.cut > q.n || q.cut_bytes > q.bytes) return RTPS_RX_EINVAL;
+    need_r += r.n - r.cut;
+    need_b += r.bytes - r.cut_bytes;
+    any |= (r.n - r.cut) | (q.n - q.cut) | (r.bytes - r.cut_bytes) | (q.bytes - q.cut_bytes);
+  }
+  if (!any) return RTPS_RX_OK;
+  const int rc = rtps_rx_shard_reserve_spill(s, need_r, need_b);
+  if (rc) {
+    (void)ncclCommAbort(c);  // the peers' spill sends cannot be received
+    return rc;
+  }
+  if (ncclGroupStart() != ncclSuccess) return RTPS_RX_EHIP;
+  bool ok = true;
+  uint64_t sb = 0, sbb = 0, rs = 0, rsb = 0;  // send-side exact-layout bases, receive-side spill offsets
+  for (uint32_t p = 0; p < world && ok; ++p) {
+    const rtps_shard_counts& q = s->h_send[p];
+    const rtps_shard_counts& r = s->h_recv[p];
+    const uint64_t sn = q.n - q.cut, sbytes = q.bytes - q.cut_bytes, rn = r.n - r.cut, rbytes = r.bytes - r.cut_bytes;
+    if (sn)
+      ok = ok && ncclSend(s->s_spill + sb + q.cut, sn * sizeof(rtps_record), ncclUint8, (int)p, c, st) == ncclSuccess;
+    if (sbytes)
+      ok = ok && ncclSend(s->s_bspill + sbb + q.cut_bytes, sbytes, ncclUint8, (int)p, c, st) == ncclSuccess;
+    if (rn) ok = ok && ncclRecv(s->r_spill + rs, rn * sizeof(rtps_record), ncclUint8, (int)p, c, st) == ncclSuccess;
+    if (rbytes) ok = ok && ncclRecv(s->r_bspill + rsb, rbytes, ncclUint8, (int)p, c, st) == ncclSuccess;
+    sb += q.n;
+    sbb += q.bytes;
+    rs += rn;
+    rsb += rbytes;
+  }
+  const bool ended = ncclGroupEnd() == ncclSuccess;
+  if (!ok || !ended) {
+    (void)ncclCommAbort(c);
+    return RTPS_RX_EHIP;
+  }
+  return hipEventRecord(s->done, st) == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP;
 }
 
 }  // extern "C"

@@ -1,0 +1,60 @@
+// rtps_shard.h — internal state of the owner-side exchange (rtps_shard.hip:
+// pack / unpack kernels; rtps_exchange.cpp: the RCCL rounds).  Not installed;
+// the public contract is the rtps_rx_shard_* section of include/rtps_rx.h.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/rtps_rx.h"
+
+constexpr uint32_t SHARD_MAX_RANKS = 64;
+
+struct rtps_shard {
+  rtps_rx_ctx* ctx = nullptr;
+  int device = 0;
+  uint32_t n_ranks = 0;
+  uint64_t cap = 0, bcap = 0;  // fixed slot per peer: records, blob bytes (multiple of 16)
+  // ---- send side (this rank as a source) ----
+  rtps_record* s_slots = nullptr;         // [n_ranks * cap]
+  uint8_t* s_blob = nullptr;              // [n_ranks * bcap]
+  rtps_shard_counts* s_counts = nullptr;  // [n_ranks] device
+  rtps_record* s_spill = nullptr;         // exact layout: dest d at sum_{d' < d} n_d'
+  uint64_t s_spill_cap = 0;
+  uint8_t* s_bspill = nullptr;            // exact layout: dest d at sum_{d' < d} bytes_d'
+  uint64_t s_bspill_cap = 0;
+  uint32_t* hist = nullptr;               // [tiles * n_ranks] x {records, bytes}
+  uint64_t* hscan = nullptr;              // [tiles * n_ranks] x {record offset, byte offset}
+  uint64_t hist_tiles = 0;
+  // ---- receive side (this rank as the owner) ----
+  rtps_record* r_slots = nullptr;         // [n_ranks * cap]: source s's slot at s * cap
+  uint8_t* r_blob = nullptr;              // [n_ranks * bcap]
+  rtps_shard_counts* r_counts = nullptr;  // [n_ranks] device: what source s sent this rank
+  rtps_record* r_spill = nullptr;         // source s's spill at sum_{s' < s} (n - cut)
+  uint64_t r_spill_cap = 0;
+  uint8_t* r_bspill = nullptr;            // source s's spilled bytes at sum_{s' < s} (bytes - cut_bytes)
+  uint64_t r_bspill_cap = 0;
+  // ---- host copies of the counts (pinned), filled by the exchange ----
+  rtps_shard_counts* h_send = nullptr;
+  rtps_shard_counts* h_recv = nullptr;
+  hipEvent_t packed = nullptr;     // recorded after pack on the context stream
+  hipEvent_t counts_ev = nullptr;  // recorded after the counts' device-to-host copies (exchange stream)
+  hipEvent_t done = nullptr;       // recorded after the last exchange round (exchange stream)
+  bool exchanged = false;          // the counts were copied by rtps_rx_shard_exchange
+  // ---- the owner batch ----
+  rtps_record* o_rec = nullptr;
+  uint64_t* o_off = nullptr;
+  uint64_t* o_origin = nullptr;
+  uint64_t* o_size = nullptr;  // blob bytes per record, then (scanned in place) its blob offset
+  uint64_t* o_boff = nullptr;
+  uint64_t o_cap = 0;
+  uint8_t* o_arena = nullptr;
+  uint64_t o_arena_cap = 0;
+  uint64_t* o_n = nullptr;  // device u64
+  void* seg = nullptr;      // device segment table of the unpack copy
+  uint64_t* h_seg = nullptr;  // pinned staging of the segment table
+  void* cub_tmp = nullptr;
+  size_t cub_bytes = 0;
+};
+
+// grow-only device buffer (contents are not kept); false on allocation failure
+bool shard_reserve(void** p, uint64_t* cap, uint64_t need_bytes);

@@ -1,0 +1,575 @@
+// rtps_shard.hip — the owner-side exchange for >= 2 GPUs (include/rtps_rx.h,
+// rtps_rx_shard_*): pack on the source, unpack on the owner.  The RCCL rounds
+// between them are in rtps_exchange.cpp.
+//
+// Why it exists: the reference keeps per-writer state — one FragmentAssembler
+// and one RtpsWriterProxy per matched writer (io_uring/rtps/reader.rs:563-758,
+// rtps/rtps_writer_proxy.rs:202-355) — and it is only right where every
+// submessage of that writer is seen, in order.  With the stream split over N
+// GPUs by datagram, that place is the writer's owner GPU.
+//
+// Pack (source rank), three launches over the parse output:
+//   1. shard_hist    per 256-record tile and destination: items and blob bytes;
+//   2. shard_scan    per destination, exclusive scans of both over the tiles
+//                    (its records' positions and blob offsets) and the totals;
+//   3. shard_scatter every item to its destination's fixed slot when it fits
+//                    (position < cap and blob end <= bcap: a prefix of the
+//                    destination's items, since both grow with position), else
+//                    to the spill at its exact-layout position; the first item
+//                    that does not fit sets the cut (atomicMin).  The blobs go
+//                    with their records: small ones copied by their lane, long
+//                    DATA_FRAG payloads by whole waves (16 B per lane).
+// Unpack (owner), with the counts on the host:
+//   1. shard_segments one flat copy of the received slots and spills into the
+//                    owner's contiguous records and arena (≤ 4 segments / source);
+//   2. shard_fix      per record: origin, blob size, dgram_idx := record index;
+//   3. exclusive sum of the blob sizes (hipCUB) = each blob's arena offset;
+//   4. shard_offsets  dgram_off = LEAD + blob offset - the blob's offset in its
+//                    datagram, so the consumers' arena + dgram_off[dgram_idx] +
+//                    pl_off / bitmap_off lands on the blob.
+// Blob streams are concatenated in source order, the same order as the
+// records, so one global scan gives every blob's place.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <string.h>
+
+#include <new>
+
+#include "../../include/rtps_rx.h"
+#include "rtps_ctx.h"
+#include "rtps_shard.h"
+
+namespace {
+
+constexpr uint32_t ST = 256;   // threads per workgroup, one record each
+constexpr uint32_t SW = ST / 64;
+constexpr uint32_t SMALL_BLOB = 64;  // blobs up to this many bytes are copied by their own lane
+constexpr uint32_t NONE = 0xffffffffu;
+
+__device__ __forceinline__ uint32_t owner_hash(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  uint32_t h = 0x811c9dc5u;  // FNV-1a over the writer GUID's four words, then fmix32 (rtps_rx.hip owner_hash)
+  h = (h ^ a) * 0x01000193u; h = (h ^ b) * 0x01000193u;
+  h = (h ^ c) * 0x01000193u; h = (h ^ d) * 0x01000193u;
+  h ^= h >> 16; h *= 0x85ebca6bu;
+  h ^= h >> 13; h *= 0xc2b2ae35u;
+  return h ^ (h >> 16);
+}
+
+// What the owner's consumers read of a record in the arena: (offset in its datagram, bytes)
+struct Blob {
+  uint32_t rel, len;
+};
+__device__ __forceinline__ Blob blob_of(const uint32_t* w) {  // w: the record's 16 words
+  const uint32_t kind = (w[1] >> 16) & 0xffu;
+  if (kind == RTPS_GAP) {  // u.gap: list_base (w10, w11), num_bits (w12), bitmap_off (w13 low)
+    const uint32_t nb = w[12];
+    return Blob{w[13] & 0xffffu, nb ? 4u * ((nb + 31u) >> 5) : 0u};
+  }
+  if (kind == RTPS_DATA_FRAG) return Blob{w[10] & 0xffffu, w[10] >> 16};  // u.frag.pl_off, pl_len
+  return Blob{0u, 0u};
+}
+__device__ __forceinline__ uint32_t round16(uint32_t x) { return (x + 15u) & ~15u; }
+
+// Destination of a record (NONE: not an item) and its blob
+__device__ __forceinline__ uint32_t item_of(const uint32_t* w, uint32_t n_dest, Blob& b) {
+  const uint32_t kind = (w[1] >> 16) & 0xffu;
+  const uint32_t route = (w[7] >> 16) & 0xffu;
+  const bool writer = kind == RTPS_DATA || kind == RTPS_DATA_FRAG || kind == RTPS_HEARTBEAT || kind == RTPS_GAP ||
+                      kind == RTPS_HEARTBEAT_FRAG;
+  b = Blob{0u, 0u};
+  if (!writer || !(route & RTPS_ROUTE_PASS)) return NONE;
+  b = blob_of(w);
+  return owner_hash(w[2], w[3], w[4], w[5]) % n_dest;
+}
+
+__device__ __forceinline__ void load_record(const rtps_record* r, uint32_t* w) {
+  const uint4* q = reinterpret_cast<const uint4*>(r);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint4 v = q[k];
+    w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+  }
+}
+__device__ __forceinline__ void store_record(rtps_record* r, const uint32_t* w) {
+  uint4* q = reinterpret_cast<uint4*>(r);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) q[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+}
+
+__device__ __forceinline__ uint4 ld16u(const uint8_t* p) {  // any alignment (one unaligned dwordx4 on gfx950)
+  uint4 v;
+  __builtin_memcpy(&v, p, 16);
+  return v;
+}
+// chunk [c, c + 16) of a blob of len bytes at src into aligned dst (zero past len); the
+// bytes past len are never read, so a blob that ends at the arena's end cannot fault
+__device__ __forceinline__ void copy_chunk(const uint8_t* src, uint8_t* dst, uint32_t c, uint32_t len) {
+  uint4 v = make_uint4(0, 0, 0, 0);
+  if (c + 16u <= len) {
+    v = ld16u(src + c);
+  } else {
+    uint32_t t[4] = {0, 0, 0, 0};
+    for (uint32_t k = c; k < len; ++k) t[(k - c) >> 2] |= (uint32_t)src[k] << (8u * ((k - c) & 3u));
+    v = make_uint4(t[0], t[1], t[2], t[3]);
+  }
+  *reinterpret_cast<uint4*>(dst + c) = v;
+}
+
+__device__ __forceinline__ uint32_t wave_incl(uint32_t x, uint32_t lane) {
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  return x;
+}
+__device__ __forceinline__ uint64_t wave_incl64(uint64_t x, uint32_t lane) {
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  return x;
+}
+
+// 1. per tile t and destination d: hist[2 (t n + d)] = items, [+1] = blob bytes
+__global__ __launch_bounds__(ST) void shard_hist(const rtps_record* recs, const uint64_t* n_rec, uint32_t n_dest,
+                                                 uint32_t* hist) {
+  __shared__ uint32_t h[2 * SHARD_MAX_RANKS];
+  if (threadIdx.x < 2 * n_dest) h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * ST + threadIdx.x;
+  if (i < *n_rec) {
+    uint32_t w[16];
+    load_record(recs + i, w);
+    Blob b;
+    const uint32_t o = item_of(w, n_dest, b);
+    if (o != NONE) {
+      atomicAdd(&h[2 * o], 1u);
+      if (b.len) atomicAdd(&h[2 * o + 1], round16(b.len));
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * n_dest) hist[(uint64_t)blockIdx.x * 2 * n_dest + threadIdx.x] = h[threadIdx.x];
+}
+
+// 2. one workgroup per destination d: exclusive scans over the tiles -> hscan[2 (t n + d)] =
+//    {first position, first blob offset} of tile t's items for d; counts[d] = totals, cut = totals
+__global__ __launch_bounds__(ST) void shard_scan(const uint32_t* hist, uint64_t tiles, uint32_t n_dest,
+                                                 uint64_t* hscan, rtps_shard_counts* counts) {
+  __shared__ uint64_t wsum[2][SW];
+  const uint32_t d = blockIdx.x, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  uint64_t carry_n = 0, carry_b = 0;
+  for (uint64_t t0 = 0; t0 < tiles; t0 += ST) {
+    const uint64_t t = t0 + tid;
+    const uint64_t vn = t < tiles ? hist[2 * (t * n_dest + d)] : 0u;
+    const uint64_t vb = t < tiles ? hist[2 * (t * n_dest + d) + 1] : 0u;
+    const uint64_t in = wave_incl64(vn, lane), ib = wave_incl64(vb, lane);
+    if (lane == 63) { wsum[0][wave] = in; wsum[1][wave] = ib; }
+    __syncthreads();
+    uint64_t bn = carry_n, bb = carry_b, tn = carry_n, tb = carry_b;
+    for (uint32_t w = 0; w < SW; ++w) {
+      if (w < wave) { bn += wsum[0][w]; bb += wsum[1][w]; }
+      tn += wsum[0][w]; tb += wsum[1][w];
+    }
+    if (t < tiles) {
+      hscan[2 * (t * n_dest + d)] = bn + in - vn;
+      hscan[2 * (t * n_dest + d) + 1] = bb + ib - vb;
+    }
+    carry_n = tn; carry_b = tb;
+    __syncthreads();
+  }
+  if (tid == 0) counts[d] = rtps_shard_counts{carry_n, carry_b, carry_n, carry_b};
+}
+
+struct PackArgs {
+  const uint8_t* arena;
+  uint64_t arena_len;
+  const uint64_t* dgram_off;
+  const rtps_record* recs;
+  const uint64_t* n_rec;
+  uint32_t n_dest;
+  uint64_t cap, bcap;
+  const uint64_t* hscan;
+  rtps_shard_counts* counts;
+  rtps_record* slots;
+  uint8_t* blob;
+  rtps_record* spill;
+  uint8_t* bspill;
+};
+
+// 3. items to their slots or the spill, with their blobs
+__global__ __launch_bounds__(ST) void shard_scatter(PackArgs a) {
+  __shared__ uint32_t wcnt[SW][SHARD_MAX_RANKS], wbyt[SW][SHARD_MAX_RANKS];
+  __shared__ uint64_t sbase[SHARD_MAX_RANKS], bsbase[SHARD_MAX_RANKS];
+  __shared__ uint64_t big_src[ST], big_dst[ST];
+  __shared__ uint32_t big_len[ST], n_big;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6, n = a.n_dest;
+  if (tid == 0) {
+    uint64_t rn = 0, rb = 0;
+    for (uint32_t d = 0; d < n; ++d) {
+      sbase[d] = rn; bsbase[d] = rb;
+      rn += a.counts[d].n; rb += a.counts[d].bytes;
+    }
+    n_big = 0;
+  }
+  const uint64_t i = (uint64_t)blockIdx.x * ST + tid;
+  uint32_t w[16];
+  uint32_t o = NONE;
+  Blob b{0u, 0u};
+  if (i < *a.n_rec) {
+    load_record(a.recs + i, w);
+    o = item_of(w, n, b);
+  }
+  const uint32_t size = round16(b.len);
+  uint32_t rank = 0, bex = 0;
+  const uint64_t lt = lane ? (~0ull >> (64u - lane)) : 0ull;
+  for (uint32_t d = 0; d < n; ++d) {
+    const uint64_t m = __ballot(o == d);
+    if (m == 0) {
+      if (lane == 0) { wcnt[wave][d] = 0; wbyt[wave][d] = 0; }
+      continue;
+    }
+    const uint32_t v = o == d ? size : 0u;
+    const uint32_t incl = wave_incl(v, lane);
+    if (o == d) { rank = (uint32_t)__popcll(m & lt); bex = incl - v; }
+    if (lane == 63) { wcnt[wave][d] = (uint32_t)__popcll(m); wbyt[wave][d] = incl; }
+  }
+  __syncthreads();
+  if (o != NONE) {
+    uint64_t pos = a.hscan[2 * ((uint64_t)blockIdx.x * n + o)] + rank;
+    uint64_t boff = a.hscan[2 * ((uint64_t)blockIdx.x * n + o) + 1] + bex;
+    for (uint32_t v = 0; v < wave; ++v) { pos += wcnt[v][o]; boff += wbyt[v][o]; }
+    const bool slot = pos < a.cap && boff + size <= a.bcap;
+    rtps_record* rd = slot ? a.slots + (uint64_t)o * a.cap + pos : a.spill + sbase[o] + pos;
+    uint8_t* bd = slot ? a.blob + (uint64_t)o * a.bcap + boff : a.bspill + bsbase[o] + boff;
+    if (!slot) {
+      atomicMin((unsigned long long*)&a.counts[o].cut, (unsigned long long)pos);
+      atomicMin((unsigned long long*)&a.counts[o].cut_bytes, (unsigned long long)boff);
+    }
+    store_record(rd, w);
+    if (b.len) {
+      const uint8_t* src = a.arena + a.dgram_off[w[0]] + b.rel;
+      if (size <= SMALL_BLOB) {
+        for (uint32_t c = 0; c < size; c += 16u) copy_chunk(src, bd, c, b.len);
+      } else {
+        const uint32_t k = atomicAdd(&n_big, 1u);
+        big_src[k] = (uint64_t)(uintptr_t)src;
+        big_dst[k] = (uint64_t)(uintptr_t)bd;
+        big_len[k] = b.len;
+      }
+    }
+  }
+  __syncthreads();
+  // long blobs (DATA_FRAG payloads): one wave per blob, 16 B per lane per step
+  for (uint32_t k = wave; k < n_big; k += SW) {
+    const uint8_t* src = (const uint8_t*)(uintptr_t)big_src[k];
+    uint8_t* dst = (uint8_t*)(uintptr_t)big_dst[k];
+    const uint32_t len = big_len[k], sz = round16(len);
+    for (uint32_t c = 16u * lane; c < sz; c += 1024u) copy_chunk(src, dst, c, len);
+  }
+}
+
+// ---- unpack ----
+struct Seg {  // one contiguous copy: 16-B chunks [c0, c0 + nc) of the flat chunk space
+  uint64_t src, dst, c0, nc;
+};
+__global__ __launch_bounds__(ST) void shard_segments(const Seg* seg, uint32_t n_seg, uint64_t total_chunks) {
+  const uint64_t stride = (uint64_t)gridDim.x * ST;
+  for (uint64_t c = (uint64_t)blockIdx.x * ST + threadIdx.x; c < total_chunks; c += stride) {
+    uint32_t lo = 0, hi = n_seg;  // last segment with c0 <= c
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (seg[mid].c0 <= c) lo = mid; else hi = mid;
+    }
+    const Seg s = seg[lo];
+    const uint64_t k = c - s.c0;
+    const uint4* src = reinterpret_cast<const uint4*>((uintptr_t)s.src) + k;
+    uint4* dst = reinterpret_cast<uint4*>((uintptr_t)s.dst) + k;
+    *dst = *src;
+  }
+}
+
+struct FixArgs {
+  rtps_record* rec;
+  uint64_t* origin;
+  uint64_t* size;
+  uint64_t n;
+  uint32_t n_src;
+  uint64_t first[SHARD_MAX_RANKS + 1];  // owner record index of source s's first record
+};
+__global__ __launch_bounds__(ST) void shard_fix(FixArgs a) {
+  const uint64_t j = (uint64_t)blockIdx.x * ST + threadIdx.x;
+  if (j >= a.n) return;
+  uint32_t s = 0;
+  while (s + 1 < a.n_src && a.first[s + 1] <= j) ++s;
+  uint32_t* w = reinterpret_cast<uint32_t*>(a.rec + j);
+  const uint4 q2 = reinterpret_cast<const uint4*>(a.rec + j)[2];
+  uint32_t w16[16];
+  w16[0] = w[0]; w16[1] = w[1];
+  w16[10] = q2.z; w16[11] = q2.w;
+  const uint4 q3 = reinterpret_cast<const uint4*>(a.rec + j)[3];
+  w16[12] = q3.x; w16[13] = q3.y;
+  const Blob b = blob_of(w16);
+  a.origin[j] = ((uint64_t)s << 32) | w16[0];
+  a.size[j] = round16(b.len);
+  w[0] = (uint32_t)j;
+}
+__global__ __launch_bounds__(ST) void shard_offsets(const rtps_record* rec, const uint64_t* boff, uint64_t* off,
+                                                    uint64_t n) {
+  const uint64_t j = (uint64_t)blockIdx.x * ST + threadIdx.x;
+  if (j >= n) return;
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(rec + j);
+  uint32_t w16[16];
+  w16[1] = w[1]; w16[10] = w[10]; w16[12] = w[12]; w16[13] = w[13];
+  const Blob b = blob_of(w16);
+  off[j] = RTPS_SHARD_LEAD + boff[j] - b.rel;
+}
+
+__global__ void shard_set_n(uint64_t* p, uint64_t v) { *p = v; }
+
+int hip_rc(hipError_t e) { return e == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP; }
+
+}  // namespace
+
+bool shard_reserve(void** p, uint64_t* cap, uint64_t need) {
+  if (*p && need <= *cap) return true;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  if (hipMalloc(p, need ? need : 16) != hipSuccess) {
+    *p = nullptr;
+    return false;
+  }
+  *cap = need;
+  return true;
+}
+
+extern "C" {
+
+int rtps_rx_shard_create(rtps_rx_ctx* ctx, uint32_t n_ranks, uint64_t cap, uint64_t bcap, rtps_shard** out) {
+  if (!ctx || !out || n_ranks < 1 || n_ranks > SHARD_MAX_RANKS || cap == 0 || (bcap & 15u)) return RTPS_RX_EINVAL;
+  rtps_shard* s = new (std::nothrow) rtps_shard();
+  if (!s) return RTPS_RX_ENOMEM;
+  s->ctx = ctx;
+  s->device = rtps_ctx_device(ctx);
+  s->n_ranks = n_ranks;
+  s->cap = cap;
+  s->bcap = bcap;
+  (void)hipSetDevice(s->device);
+  const size_t slots = (size_t)n_ranks * cap * sizeof(rtps_record), blobs = (size_t)n_ranks * bcap;
+  bool ok = hipMalloc(&s->s_slots, slots) == hipSuccess && hipMalloc(&s->r_slots, slots) == hipSuccess &&
+            hipMalloc(&s->s_blob, blobs ? blobs : 16) == hipSuccess &&
+            hipMalloc(&s->r_blob, blobs ? blobs : 16) == hipSuccess &&
+            hipMalloc(&s->s_counts, n_ranks * sizeof(rtps_shard_counts)) == hipSuccess &&
+            hipMalloc(&s->r_counts, n_ranks * sizeof(rtps_shard_counts)) == hipSuccess &&
+            hipMemset(s->r_counts, 0, n_ranks * sizeof(rtps_shard_counts)) == hipSuccess &&
+            hipMemset(s->s_counts, 0, n_ranks * sizeof(rtps_shard_counts)) == hipSuccess &&
+            hipHostMalloc(&s->h_send, n_ranks * sizeof(rtps_shard_counts), hipHostMallocDefault) == hipSuccess &&
+            hipHostMalloc(&s->h_recv, n_ranks * sizeof(rtps_shard_counts), hipHostMallocDefault) == hipSuccess &&
+            hipHostMalloc(&s->h_seg, 4 * SHARD_MAX_RANKS * sizeof(Seg), hipHostMallocDefault) == hipSuccess &&
+            hipMalloc(&s->seg, 4 * SHARD_MAX_RANKS * sizeof(Seg)) == hipSuccess &&
+            hipMalloc(&s->o_n, sizeof(uint64_t)) == hipSuccess &&
+            hipMemset(s->o_n, 0, sizeof(uint64_t)) == hipSuccess &&
+            hipEventCreateWithFlags(&s->packed, hipEventDisableTiming) == hipSuccess &&
+            hipEventCreateWithFlags(&s->counts_ev, hipEventDisableTiming) == hipSuccess &&
+            hipEventCreateWithFlags(&s->done, hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
+    rtps_rx_shard_destroy(s);
+    return RTPS_RX_ENOMEM;
+  }
+  *out = s;
+  return RTPS_RX_OK;
+}
+
+int rtps_rx_shard_destroy(rtps_shard* s) {
+  if (!s) return RTPS_RX_EINVAL;
+  (void)hipSetDevice(s->device);
+  (void)hipDeviceSynchronize();
+  void* dev[] = {s->s_slots, s->s_blob, s->s_counts, s->s_spill, s->s_bspill, s->hist, s->hscan, s->r_slots,
+                 s->r_blob, s->r_counts, s->r_spill, s->r_bspill, s->o_rec, s->o_off, s->o_origin, s->o_size,
+                 s->o_boff, s->o_arena, s->o_n, s->seg, s->cub_tmp};
+  for (void* p : dev)
+    if (p) (void)hipFree(p);
+  if (s->h_send) (void)hipHostFree(s->h_send);
+  if (s->h_recv) (void)hipHostFree(s->h_recv);
+  if (s->h_seg) (void)hipHostFree(s->h_seg);
+  hipEvent_t ev[] = {s->packed, s->counts_ev, s->done};
+  for (hipEvent_t e : ev)
+    if (e) (void)hipEventDestroy(e);
+  delete s;
+  return RTPS_RX_OK;
+}
+
+int rtps_rx_shard_pack(rtps_shard* s, const uint8_t* arena, uint64_t arena_len, const uint64_t* dgram_off,
+                       const rtps_record* records, const uint64_t* n_records, uint64_t max_records) {
+  if (!s || !records || !n_records || (max_records && (!arena || !dgram_off))) return RTPS_RX_EINVAL;
+  (void)hipSetDevice(s->device);
+  hipStream_t st = rtps_ctx_stream(s->ctx);
+  const uint32_t n = s->n_ranks;
+  const uint64_t tiles = (max_records + ST - 1) / ST;
+  if (tiles > 0xffffffffull) return RTPS_RX_ETOOBIG;
+  if (tiles > s->hist_tiles) {
+    if (hipStreamSynchronize(st) != hipSuccess) return RTPS_RX_EHIP;  // the last pack may still use them
+    uint64_t c1 = 0, c2 = 0;
+    (void)hipFree(s->hist); (void)hipFree(s->hscan);
+    s->hist = nullptr; s->hscan = nullptr; s->hist_tiles = 0;
+    if (!shard_reserve((void**)&s->hist, &c1, tiles * n * 2 * sizeof(uint32_t)) ||
+        !shard_reserve((void**)&s->hscan, &c2, tiles * n * 2 * sizeof(uint64_t)))
+      return RTPS_RX_ENOMEM;
+    s->hist_tiles = tiles;
+  }
+  // the spill holds every item in the worst case: all records, and blobs that are
+  // disjoint byte ranges of the arena plus < 16 B of rounding each
+  const uint64_t need_rec = max_records * sizeof(rtps_record), need_b = arena_len + 16ull * max_records;
+  if (need_rec > s->s_spill_cap * sizeof(rtps_record) || need_b > s->s_bspill_cap) {
+    if (hipStreamSynchronize(st) != hipSuccess) return RTPS_RX_EHIP;
+    uint64_t cap_bytes = s->s_spill_cap * sizeof(rtps_record);
+    if (!shard_reserve((void**)&s->s_spill, &cap_bytes, need_rec)) return RTPS_RX_ENOMEM;
+    s->s_spill_cap = cap_bytes / sizeof(rtps_record);
+    if (!shard_reserve((void**)&s->s_bspill, &s->s_bspill_cap, need_b)) return RTPS_RX_ENOMEM;
+  }
+  if (tiles == 0) {
+    if (hipMemsetAsync(s->s_counts, 0, n * sizeof(rtps_shard_counts), st) != hipSuccess) return RTPS_RX_EHIP;
+  } else {
+    hipLaunchKernelGGL(shard_hist, dim3((uint32_t)tiles), dim3(ST), 0, st, records, n_records, n, s->hist);
+    hipLaunchKernelGGL(shard_scan, dim3(n), dim3(ST), 0, st, s->hist, tiles, n, s->hscan, s->s_counts);
+    PackArgs a{arena, arena_len, dgram_off, records, n_records, n, s->cap, s->bcap, s->hscan, s->s_counts,
+               s->s_slots, s->s_blob, s->s_spill, s->s_bspill};
+    hipLaunchKernelGGL(shard_scatter, dim3((uint32_t)tiles), dim3(ST), 0, st, a);
+  }
+  if (hipGetLastError() != hipSuccess) return RTPS_RX_EHIP;
+  s->exchanged = false;
+  return hip_rc(hipEventRecord(s->packed, st));
+}
+
+int rtps_rx_shard_buffers(rtps_shard* s, rtps_shard_buffers* o) {
+  if (!s || !o) return RTPS_RX_EINVAL;
+  o->send_slots = s->s_slots; o->send_blob = s->s_blob; o->send_counts = s->s_counts;
+  o->recv_slots = s->r_slots; o->recv_blob = s->r_blob; o->recv_counts = s->r_counts;
+  o->send_spill = s->s_spill; o->send_blob_spill = s->s_bspill;
+  o->recv_spill = s->r_spill; o->recv_blob_spill = s->r_bspill;
+  o->recv_spill_cap = s->r_spill_cap;
+  o->recv_blob_spill_cap = s->r_bspill_cap;
+  return RTPS_RX_OK;
+}
+
+int rtps_rx_shard_reserve_spill(rtps_shard* s, uint64_t records, uint64_t bytes) {
+  if (!s) return RTPS_RX_EINVAL;
+  (void)hipSetDevice(s->device);
+  if (records > s->r_spill_cap || bytes > s->r_bspill_cap) {
+    if (hipDeviceSynchronize() != hipSuccess) return RTPS_RX_EHIP;  // an unpack may still read the old ones
+    uint64_t cap_bytes = s->r_spill_cap * sizeof(rtps_record);
+    if (records > s->r_spill_cap) {
+      if (!shard_reserve((void**)&s->r_spill, &cap_bytes, records * sizeof(rtps_record))) return RTPS_RX_ENOMEM;
+      s->r_spill_cap = cap_bytes / sizeof(rtps_record);
+    }
+    if (bytes > s->r_bspill_cap && !shard_reserve((void**)&s->r_bspill, &s->r_bspill_cap, bytes))
+      return RTPS_RX_ENOMEM;
+  }
+  return RTPS_RX_OK;
+}
+
+int rtps_rx_shard_unpack(rtps_shard* s, rtps_owner_batch* out) {
+  if (!s || !out) return RTPS_RX_EINVAL;
+  (void)hipSetDevice(s->device);
+  hipStream_t st = rtps_ctx_stream(s->ctx);
+  const uint32_t n = s->n_ranks;
+  // the received counts (after rtps_rx_shard_finish, or a host-driven transport's copies)
+  if (s->exchanged && hipStreamWaitEvent(st, s->done, 0) != hipSuccess) return RTPS_RX_EHIP;
+  if (hipMemcpyAsync(s->h_recv, s->r_counts, n * sizeof(rtps_shard_counts), hipMemcpyDeviceToHost, st) !=
+          hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return RTPS_RX_EHIP;
+  uint64_t total = 0, bytes = 0, sp = 0, bsp = 0;
+  FixArgs fa;
+  memset(&fa, 0, sizeof fa);
+  for (uint32_t k = 0; k < n; ++k) {
+    const rtps_shard_counts& c = s->h_recv[k];
+    if (c.cut > c.n || c.cut_bytes > c.bytes || c.cut > s->cap || c.cut_bytes > s->bcap || (c.bytes & 15u))
+      return RTPS_RX_EINVAL;  // not counts this protocol wrote
+    fa.first[k] = total;
+    total += c.n;
+    bytes += c.bytes;
+    sp += c.n - c.cut;
+    bsp += c.bytes - c.cut_bytes;
+  }
+  fa.first[n] = total;
+  if (sp > s->r_spill_cap || bsp > s->r_bspill_cap) return RTPS_RX_ETOOBIG;  // spill not received
+  if (total > s->o_cap) {
+    uint64_t c[5] = {0, 0, 0, 0, 0};
+    void** p[5] = {(void**)&s->o_rec, (void**)&s->o_off, (void**)&s->o_origin, (void**)&s->o_size,
+                   (void**)&s->o_boff};
+    const size_t b[5] = {sizeof(rtps_record), 8, 8, 8, 8};
+    for (int k = 0; k < 5; ++k) {
+      (void)hipFree(*p[k]);
+      *p[k] = nullptr;
+    }
+    s->o_cap = 0;
+    for (int k = 0; k < 5; ++k)
+      if (!shard_reserve(p[k], &c[k], total * b[k])) return RTPS_RX_ENOMEM;
+    s->o_cap = total;
+  }
+  const uint64_t arena_need = RTPS_SHARD_LEAD + bytes;
+  if (arena_need > s->o_arena_cap) {
+    if (!shard_reserve((void**)&s->o_arena, &s->o_arena_cap, arena_need) ||
+        hipMemset(s->o_arena, 0, RTPS_SHARD_LEAD) != hipSuccess)
+      return RTPS_RX_ENOMEM;
+  }
+  // segment table: per source, slot records, spilled records, slot blob bytes, spilled bytes
+  Seg* seg = reinterpret_cast<Seg*>(s->h_seg);
+  uint32_t ns = 0;
+  uint64_t chunks = 0, rpos = 0, bpos = 0, rsp = 0, bsp2 = 0;
+  auto add = [&](const void* src, void* dst, uint64_t nbytes) {
+    if (!nbytes) return;
+    seg[ns++] = Seg{(uint64_t)(uintptr_t)src, (uint64_t)(uintptr_t)dst, chunks, nbytes / 16};
+    chunks += nbytes / 16;
+  };
+  for (uint32_t k = 0; k < n; ++k) {
+    const rtps_shard_counts& c = s->h_recv[k];
+    add(s->r_slots + (uint64_t)k * s->cap, s->o_rec + rpos, c.cut * sizeof(rtps_record));
+    add(s->r_spill + rsp, s->o_rec + rpos + c.cut, (c.n - c.cut) * sizeof(rtps_record));
+    add(s->r_blob + (uint64_t)k * s->bcap, s->o_arena + RTPS_SHARD_LEAD + bpos, c.cut_bytes);
+    add(s->r_bspill + bsp2, s->o_arena + RTPS_SHARD_LEAD + bpos + c.cut_bytes, c.bytes - c.cut_bytes);
+    rpos += c.n;
+    bpos += c.bytes;
+    rsp += c.n - c.cut;
+    bsp2 += c.bytes - c.cut_bytes;
+  }
+  if (ns && (hipMemcpyAsync(s->seg, seg, ns * sizeof(Seg), hipMemcpyHostToDevice, st) != hipSuccess))
+    return RTPS_RX_EHIP;
+  if (ns) {
+    const uint64_t blocks = (chunks + ST - 1) / ST;
+    hipLaunchKernelGGL(shard_segments, dim3((uint32_t)(blocks < 16384 ? blocks : 16384)), dim3(ST), 0, st,
+                       (const Seg*)s->seg, ns, chunks);
+  }
+  if (total) {
+    fa.rec = s->o_rec; fa.origin = s->o_origin; fa.size = s->o_size; fa.n = total; fa.n_src = n;
+    const uint32_t g = (uint32_t)((total + ST - 1) / ST);
+    hipLaunchKernelGGL(shard_fix, dim3(g), dim3(ST), 0, st, fa);
+    size_t tb = 0;
+    if (hipcub::DeviceScan::ExclusiveSum(nullptr, tb, s->o_size, s->o_boff, (int64_t)total, st) != hipSuccess)
+      return RTPS_RX_EHIP;
+    if (tb > s->cub_bytes) {
+      uint64_t cb = s->cub_bytes;
+      if (!shard_reserve(&s->cub_tmp, &cb, tb)) return RTPS_RX_ENOMEM;
+      s->cub_bytes = cb;
+    }
+    if (hipcub::DeviceScan::ExclusiveSum(s->cub_tmp, tb, s->o_size, s->o_boff, (int64_t)total, st) != hipSuccess)
+      return RTPS_RX_EHIP;
+    hipLaunchKernelGGL(shard_offsets, dim3(g), dim3(ST), 0, st, s->o_rec, s->o_boff, s->o_off, total);
+  }
+  hipLaunchKernelGGL(shard_set_n, dim3(1), dim3(1), 0, st, s->o_n, total);
+  if (hipGetLastError() != hipSuccess) return RTPS_RX_EHIP;
+  out->arena = s->o_arena;
+  out->arena_len = arena_need;
+  out->dgram_off = s->o_off;
+  out->records = s->o_rec;
+  out->origin = s->o_origin;
+  out->n_records_dev = s->o_n;
+  out->n_records = total;
+  s->exchanged = false;
+  return RTPS_RX_OK;
+}
+
+}  // extern "C"

@@ -188,3 +188,256 @@ class Exchange:
     def overflowed(self):
         """True if a bucket of the last bucket() call had more than cap records (host sync)."""
         return bool(self.cap) and int(self.counts.max().item()) > self.cap
+
+
+# ---------------------------------------------------------------------------
+# Owner-side exchange (rtps_rx_shard_*, include/rtps_rx.h): every writer-kind
+# record that passes goes to its writer's owner with the bytes the owner's
+# fragment assembly and ingest read (GAP bitmaps, DATA_FRAG payloads), so the
+# owner runs rtps_rx_frag_assemble / rtps_rx_ingest on all of its writers'
+# submessages in stream order.  Fixed slots first (equal splits, no host round
+# trip), then the exact spill of whatever did not fit: no record is dropped.
+# ---------------------------------------------------------------------------
+import numpy as _np
+
+SHARD_COUNTS_DTYPE = _np.dtype([("n", "<u8"), ("bytes", "<u8"), ("cut", "<u8"), ("cut_bytes", "<u8")])
+SHARD_LEAD = 65536
+_HIP = None
+
+
+def _hip():
+    """HIP runtime (ctypes) for raw device-pointer copies of the library-owned buffers."""
+    global _HIP
+    if _HIP is None:
+        _HIP = ctypes.CDLL("libamdhip64.so")
+        _HIP.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        _HIP.hipMemcpy.restype = ctypes.c_int
+    return _HIP
+
+
+def dev_copy(dst, src, nbytes):
+    """hipMemcpy(dst, src, n, hipMemcpyDefault) between raw pointers (host or device)."""
+    if nbytes:
+        rc = _hip().hipMemcpy(ctypes.c_void_p(dst), ctypes.c_void_p(src), nbytes, 4)
+        if rc != 0:
+            raise RuntimeError(f"hipMemcpy failed ({rc})")
+
+
+def dev_to_numpy(ptr, nbytes, dtype=_np.uint8):
+    a = _np.empty(nbytes, dtype=_np.uint8)
+    dev_copy(a.ctypes.data, ptr, nbytes)
+    return a.view(dtype)
+
+
+class DevPtr:
+    """A library-owned device buffer in the tensor shape the MessageReceiver methods take
+    (data_ptr / numel)."""
+
+    def __init__(self, ptr, nbytes):
+        self.ptr, self.nbytes = int(ptr or 0), int(nbytes)
+
+    def data_ptr(self):
+        return self.ptr
+
+    def numel(self):
+        return self.nbytes
+
+
+class _ShardBuffers(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("send_slots", "send_blob", "send_counts", "recv_slots", "recv_blob",
+                                               "recv_counts", "send_spill", "send_blob_spill", "recv_spill",
+                                               "recv_blob_spill")] + \
+               [("recv_spill_cap", ctypes.c_uint64), ("recv_blob_spill_cap", ctypes.c_uint64)]
+
+
+class _OwnerBatch(ctypes.Structure):
+    _fields_ = [("arena", ctypes.c_void_p), ("arena_len", ctypes.c_uint64), ("dgram_off", ctypes.c_void_p),
+                ("records", ctypes.c_void_p), ("origin", ctypes.c_void_p), ("n_records_dev", ctypes.c_void_p),
+                ("n_records", ctypes.c_uint64)]
+
+
+class OwnerBatch:
+    """The owner's received records as a batch for rx.frag_assemble / rx.ingest (device,
+    library-owned, valid until the next unpack): `arena`, `off` and `outs` go where a parse's
+    arena / offsets / outputs go."""
+
+    def __init__(self, ob):
+        n = int(ob.n_records)
+        self.n_records = n
+        self.arena = DevPtr(ob.arena, ob.arena_len)
+        self.off = DevPtr(ob.dgram_off, 8 * n)
+        self.origin_ptr = int(ob.origin or 0)
+        self.outs = {"records": DevPtr(ob.records, 64 * n), "n_records": DevPtr(ob.n_records_dev, 8),
+                     "max_records": n}
+
+    def records(self):
+        from .records import RECORD_DTYPE
+        return dev_to_numpy(self.outs["records"].ptr, 64 * self.n_records, RECORD_DTYPE)
+
+    def origin(self):
+        """(source rank u32[n], source dgram_idx u32[n])."""
+        o = dev_to_numpy(self.origin_ptr, 8 * self.n_records, _np.uint64)
+        return (o >> _np.uint64(32)).astype(_np.uint32), (o & _np.uint64(0xFFFFFFFF)).astype(_np.uint32)
+
+    def dgram_off(self):
+        return dev_to_numpy(self.off.ptr, 8 * self.n_records, _np.uint64)
+
+    def arena_bytes(self):
+        return dev_to_numpy(self.arena.ptr, self.arena.nbytes)
+
+
+def shard_lib():
+    from . import lib
+    L = lib()
+    if not getattr(L, "_shard_bound", False):
+        P, U32, U64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
+        L.rtps_rx_shard_create.argtypes = [P, U32, U64, U64, ctypes.POINTER(P)]
+        L.rtps_rx_shard_destroy.argtypes = [P]
+        L.rtps_rx_shard_pack.argtypes = [P, P, U64, P, P, P, U64]
+        L.rtps_rx_shard_exchange.argtypes = [P, P, P]
+        L.rtps_rx_shard_finish.argtypes = [P, P, P]
+        L.rtps_rx_shard_unpack.argtypes = [P, ctypes.POINTER(_OwnerBatch)]
+        L.rtps_rx_shard_buffers.argtypes = [P, ctypes.POINTER(_ShardBuffers)]
+        L.rtps_rx_shard_reserve_spill.argtypes = [P, U64, U64]
+        for f in ("rtps_rx_shard_create", "rtps_rx_shard_destroy", "rtps_rx_shard_pack", "rtps_rx_shard_exchange",
+                  "rtps_rx_shard_finish", "rtps_rx_shard_unpack", "rtps_rx_shard_buffers",
+                  "rtps_rx_shard_reserve_spill"):
+            getattr(L, f).restype = ctypes.c_int
+        L._shard_bound = True
+    return L
+
+
+def spill_plan(send_counts, recv_counts):
+    """Round 1 of the protocol from round 0's counts (SHARD_COUNTS_DTYPE [world] each):
+    per peer (send record range, send byte range) in the send spill's exact layout and
+    (receive record offset + count, byte offset + count) in the receive spill."""
+    s, r = send_counts, recv_counts
+    sb = _np.concatenate([[0], _np.cumsum(s["n"].astype(_np.int64))[:-1]])
+    sbb = _np.concatenate([[0], _np.cumsum(s["bytes"].astype(_np.int64))[:-1]])
+    rn = (r["n"] - r["cut"]).astype(_np.int64)
+    rb = (r["bytes"] - r["cut_bytes"]).astype(_np.int64)
+    rs = _np.concatenate([[0], _np.cumsum(rn)[:-1]])
+    rsb = _np.concatenate([[0], _np.cumsum(rb)[:-1]])
+    plan = []
+    for p in range(len(s)):
+        plan.append({"send_rec": (int(sb[p] + s["cut"][p]), int(s["n"][p] - s["cut"][p])),
+                     "send_bytes": (int(sbb[p] + s["cut_bytes"][p]), int(s["bytes"][p] - s["cut_bytes"][p])),
+                     "recv_rec": (int(rs[p]), int(rn[p])), "recv_bytes": (int(rsb[p]), int(rb[p]))})
+    return plan
+
+
+class OwnerShard:
+    """One rank's owner-side exchange (rtps_rx_shard_*).  Transport: the library's RCCL
+    rounds (rtps_rx_shard_exchange / _finish) with the "nccl" group, or the same protocol
+    moved by torch.distributed over host memory with "gloo" (one-GPU rehearsals)."""
+
+    def __init__(self, rx, world, dist, device, cap, bcap):
+        L = shard_lib()
+        self.rx, self.world, self.dist, self.device = rx, world, dist, device
+        self.cap, self.bcap = int(cap), int(bcap) + (-int(bcap)) % 16
+        h = ctypes.c_void_p()
+        from . import _check
+        _check(L.rtps_rx_shard_create(rx._h, world, self.cap, self.bcap, ctypes.byref(h)))
+        self._h = h
+        backend = dist.get_backend() if dist is not None else "gloo"
+        self.host_collectives = backend == "gloo"
+        self.comm = None if self.host_collectives else rccl_comm(rx, dist, device)
+        self.xstream = None if self.host_collectives else torch.cuda.Stream(device)
+        self.last_spill = 0
+
+    def close(self):
+        if getattr(self, "_h", None):
+            shard_lib().rtps_rx_shard_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def buffers(self):
+        b = _ShardBuffers()
+        from . import _check
+        _check(shard_lib().rtps_rx_shard_buffers(self._h, ctypes.byref(b)))
+        return b
+
+    def pack(self, arena, off, outs):
+        """Source side: this rank's parse output into the slots and the spill (asynchronous)."""
+        from . import _check
+        _check(shard_lib().rtps_rx_shard_pack(self._h, arena.data_ptr(), arena.numel(), off.data_ptr(),
+                                              outs["records"].data_ptr(), outs["n_records"].data_ptr(),
+                                              outs["max_records"]))
+
+    def counts(self, side="send"):
+        b = self.buffers()
+        p = b.send_counts if side == "send" else b.recv_counts
+        torch.cuda.synchronize(self.device)
+        return dev_to_numpy(p, self.world * 32, SHARD_COUNTS_DTYPE)
+
+    def exchange(self):
+        """Round 0 (RCCL: asynchronous on the exchange stream; gloo: the whole protocol)."""
+        if self.host_collectives:
+            return self._exchange_host()
+        from . import _check
+        _check(shard_lib().rtps_rx_shard_exchange(self._h, self.comm, ctypes.c_void_p(self.xstream.cuda_stream)))
+
+    def finish(self):
+        """Waits for round 0's counts; moves any spill (RCCL).  No-op after a gloo exchange."""
+        if self.host_collectives:
+            return
+        from . import _check
+        _check(shard_lib().rtps_rx_shard_finish(self._h, self.comm, ctypes.c_void_p(self.xstream.cuda_stream)))
+
+    def unpack(self):
+        """Owner side -> OwnerBatch (host sync on the received counts)."""
+        from . import _check
+        ob = _OwnerBatch()
+        _check(shard_lib().rtps_rx_shard_unpack(self._h, ctypes.byref(ob)))
+        return OwnerBatch(ob)
+
+    def _exchange_host(self):
+        """The protocol over torch.distributed with CPU tensors (gloo): counts, slots and
+        blob slots with equal splits, then the spill with the exact splits round 0's counts
+        give, into the library's receive buffers."""
+        dist, w = self.dist, self.world
+        torch.cuda.synchronize(self.device)
+        b = self.buffers()
+        sc = dev_to_numpy(b.send_counts, w * 32, SHARD_COUNTS_DTYPE)
+        rc = _np.zeros(w, dtype=SHARD_COUNTS_DTYPE)
+        self._a2a(sc.view(_np.uint8), rc.view(_np.uint8))
+        dev_copy(b.recv_counts, rc.ctypes.data, rc.nbytes)
+        for sp, rp, nb in ((b.send_slots, b.recv_slots, self.cap * 64), (b.send_blob, b.recv_blob, self.bcap)):
+            if nb:
+                s_host = dev_to_numpy(sp, w * nb)
+                r_host = _np.empty(w * nb, dtype=_np.uint8)
+                self._a2a(s_host, r_host)
+                dev_copy(rp, r_host.ctypes.data, r_host.nbytes)
+        plan = spill_plan(sc, rc)
+        rn = sum(p["recv_rec"][1] for p in plan)
+        rbn = sum(p["recv_bytes"][1] for p in plan)
+        anyn = sum(p["send_rec"][1] + p["send_bytes"][1] for p in plan) + rn + rbn
+        self.last_spill = rn
+        if dist is not None:
+            t = torch.tensor([anyn], dtype=torch.int64)
+            dist.all_reduce(t)  # gloo's all_to_all needs every rank; skip round 1 only if nobody spills
+            anyn = int(t.item())
+        if anyn:
+            from . import _check
+            _check(shard_lib().rtps_rx_shard_reserve_spill(self._h, rn, rbn))
+            b = self.buffers()
+            for key, sp, rp, unit in (("rec", b.send_spill, b.recv_spill, 64), ("bytes", b.send_blob_spill,
+                                                                                  b.recv_blob_spill, 1)):
+                sends = [dev_to_numpy(sp + p[f"send_{key}"][0] * unit, p[f"send_{key}"][1] * unit) for p in plan]
+                recv = _np.empty(sum(p[f"recv_{key}"][1] for p in plan) * unit, dtype=_np.uint8)
+                self._a2a(_np.concatenate(sends) if sends else _np.zeros(0, _np.uint8), recv,
+                          [len(x) for x in sends], [p[f"recv_{key}"][1] * unit for p in plan])
+                dev_copy(rp, recv.ctypes.data, recv.nbytes)
+        torch.cuda.synchronize(self.device)
+
+    def _a2a(self, send, recv, send_splits=None, recv_splits=None):
+        if self.dist is None:  # one rank: the exchange is a copy
+            recv[:] = send
+            return
+        out = torch.from_numpy(recv)
+        self.dist.all_to_all_single(out, torch.from_numpy(_np.ascontiguousarray(send)), recv_splits, send_splits)

@@ -1,0 +1,232 @@
+"""GPU checks of the owner-side exchange (rtps_rx_shard_*):
+
+  * the device pack (shard_hist / shard_scan / shard_scatter) against the numpy
+    model (tests/shard_ref.py): counts, cut, every slot and spill record, every
+    blob byte, for 1 / 2 / 3 / 8 destinations, slots large and small;
+  * the device unpack against the model, with the receive buffers filled as W
+    sources would fill them;
+  * one rank end to end (pack -> host-driven exchange -> unpack -> reassembly +
+    ingest on the owner batch) against the oracle, with forced spill;
+  * two ranks on the box's GPU over gloo at C5's generator indices, and one rank
+    through the library's RCCL rounds (scripts/owner_check.py);
+  * the full C5 per-rank size (8M datagrams) through pack + the one-rank RCCL
+    rounds + unpack, and through rtps_rx_bucket_by_writer_padded + rtps_rx_exchange
+    (scripts/c5_full_check.py)."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle
+from rtps_rx.records import RECORD_DTYPE, DELIVERY_DTYPE, pack_match_table, WRITER_KINDS, max_records
+from shard_ref import COUNTS_DTYPE, shard_pack_np, shard_unpack_np
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def rx():
+    import rtps_rx
+    r = rtps_rx.MessageReceiver(oracle.OWN_PREFIX, max_datagrams=1 << 16)
+    yield r
+    r.close()
+
+
+def _device_batch(rx, arena, off, ln, tbl=None):
+    dev = torch.device("cuda", 0)
+    A = torch.from_numpy(arena).to(dev)
+    O = torch.from_numpy(off.view(np.int64)).to(dev)
+    L = torch.from_numpy(ln.view(np.int32)).to(dev)
+    rx.set_match_table(tbl if tbl is not None else [])
+    outs = rx.alloc_outputs(len(ln), max_records(ln))
+    rx.parse_batch_device(A, O, L, len(ln), outs)
+    rx.sync()
+    return A, O, outs
+
+
+def _corpora():
+    a3, o3, l3 = oracle.gen(oracle.WL_C3, 6000, first_idx=3 << 23)
+    a4, o4, l4 = oracle.gen(oracle.WL_C4, 2000)
+    return {"C3": (a3, o3, l3), "C4": (a4, o4, l4)}
+
+
+CORPORA = _corpora()
+
+
+@pytest.mark.parametrize("wl", ["C3", "C4"])
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+@pytest.mark.parametrize("small", [False, True])
+def test_pack_matches_model(rx, wl, world, small):
+    from rtps_rx.shard import OwnerShard, dev_to_numpy
+    arena, off, ln = CORPORA[wl]
+    A, O, outs = _device_batch(rx, arena, off, ln)
+    _, recs, _, _ = oracle.parse(arena, off, ln)
+    cap, bcap = (37, 1024) if small else (len(recs), 64 << 20)
+    sh = OwnerShard(rx, world, None, torch.device("cuda", 0), cap, bcap)
+    try:
+        sh.pack(A, O, outs)
+        rx.sync()
+        exp = shard_pack_np(arena, off, recs, world, cap, bcap)
+        b = sh.buffers()
+        counts = dev_to_numpy(b.send_counts, 32 * world, COUNTS_DTYPE)
+        slots = dev_to_numpy(b.send_slots, 64 * world * cap, RECORD_DTYPE)
+        blob = dev_to_numpy(b.send_blob, world * bcap)
+        tot_n = int(counts["n"].sum())
+        tot_b = int(counts["bytes"].sum())
+        spill = dev_to_numpy(b.send_spill, 64 * tot_n, RECORD_DTYPE)
+        bspill = dev_to_numpy(b.send_blob_spill, tot_b)
+        sb = sbb = 0
+        spilled = 0
+        for d in range(world):
+            e, c = exp[d], counts[d]
+            assert c.tobytes() == e["counts"][0].tobytes(), (d, c, e["counts"])
+            cut, cb, n, nb = int(c["cut"]), int(c["cut_bytes"]), int(c["n"]), int(c["bytes"])
+            assert slots[d * cap:d * cap + cut].tobytes() == e["slot_recs"].tobytes()
+            assert blob[d * bcap:d * bcap + cb].tobytes() == e["slot_blob"].tobytes()
+            assert spill[sb + cut:sb + n].tobytes() == e["spill_recs"].tobytes()
+            assert bspill[sbb + cb:sbb + nb].tobytes() == e["spill_blob"].tobytes()
+            sb += n
+            sbb += nb
+            spilled += n - cut
+        assert (spilled > 0) == small
+    finally:
+        sh.close()
+
+
+@pytest.mark.parametrize("wl", ["C3", "C4"])
+@pytest.mark.parametrize("small", [False, True])
+def test_unpack_matches_model(rx, wl, small):
+    """Receive buffers filled as 3 sources (3 chunks of the stream) would fill them."""
+    from rtps_rx.shard import OwnerShard, dev_copy, dev_to_numpy
+    world = 3
+    arena, off, ln = CORPORA[wl]
+    cap, bcap = (29, 512) if small else (20000, 64 << 20)
+    sh = OwnerShard(rx, world, None, torch.device("cuda", 0), cap, bcap)
+    try:
+        received = []
+        per = len(ln) // world
+        for s in range(world):
+            o, l = off[s * per:(s + 1) * per], ln[s * per:(s + 1) * per]
+            _, recs, _, _ = oracle.parse(arena, o, l)
+            received.append(shard_pack_np(arena, o, recs, world, cap, bcap)[1])  # what owner 1 gets from source s
+        b = sh.buffers()
+        rc = np.concatenate([x["counts"] for x in received])
+        sp = sum(int(c["n"] - c["cut"]) for c in rc)
+        spb = sum(int(c["bytes"] - c["cut_bytes"]) for c in rc)
+        from rtps_rx.shard import shard_lib
+        assert shard_lib().rtps_rx_shard_reserve_spill(sh._h, sp, spb) == 0
+        b = sh.buffers()
+        dev_copy(b.recv_counts, rc.ctypes.data, rc.nbytes)
+        rs = rbs = 0
+        for s, x in enumerate(received):
+            dev_copy(b.recv_slots + s * cap * 64, x["slot_recs"].ctypes.data, x["slot_recs"].nbytes)
+            dev_copy(b.recv_blob + s * bcap, x["slot_blob"].ctypes.data, x["slot_blob"].nbytes)
+            sr = np.ascontiguousarray(x["spill_recs"])
+            dev_copy((b.recv_spill or 0) + rs * 64, sr.ctypes.data, sr.nbytes)
+            dev_copy((b.recv_blob_spill or 0) + rbs, x["spill_blob"].ctypes.data, x["spill_blob"].nbytes)
+            rs += len(sr)
+            rbs += len(x["spill_blob"])
+        assert (rs > 0) == small
+        ob = sh.unpack()
+        erecs, eoff, earena, (erank, edidx) = shard_unpack_np(received)
+        assert ob.n_records == len(erecs) > 100
+        assert ob.records().tobytes() == erecs.tobytes()
+        assert np.array_equal(ob.dgram_off(), eoff)
+        assert ob.arena_bytes()[:len(earena)].tobytes() == earena.tobytes()
+        grank, gdidx = ob.origin()
+        assert np.array_equal(grank, erank) and np.array_equal(gdidx, edidx)
+        n_dev = dev_to_numpy(ob.outs["n_records"].ptr, 8, np.uint64)
+        assert int(n_dev[0]) == ob.n_records
+    finally:
+        sh.close()
+
+
+@pytest.mark.parametrize("wl,cap,bcap", [("C3", 100000, 1 << 20), ("C3", 300, 512), ("C4", 100, 4096)])
+def test_one_rank_owner_pipeline(rx, wl, cap, bcap):
+    """pack -> exchange (one rank: the host transport copies) -> unpack -> frag + ingest on the
+    owner batch == the oracle's reassembly + ingest of the batch itself."""
+    from rtps_rx.shard import OwnerShard
+    from rtps_rx.records import FRAG_SAMPLE_DTYPE
+    arena, off, ln = CORPORA[wl]
+    _, r0, _, _ = oracle.parse(arena, off, ln)
+    guids = sorted({bytes(r["prefix"]) + bytes(r["writer_id"]) for r in r0[np.isin(r0["kind"], WRITER_KINDS)]})
+    tbl = pack_match_table([(g, 5) for g in guids] + [(g, 6) for g in guids[1::3]])
+    A, O, outs = _device_batch(rx, arena, off, ln, tbl)
+    rx.ingest_reset()
+    rx.frag_reset()
+    sh = OwnerShard(rx, 1, None, torch.device("cuda", 0), cap, bcap)
+    try:
+        sh.pack(A, O, outs)
+        sh.exchange()
+        sh.finish()
+        ob = sh.unpack()
+        m = ob.n_records
+        fouts = rx.alloc_frag_outputs(max(m, 1), ob.arena.nbytes + 16 * m + (1 << 20))
+        iouts = rx.alloc_ingest_outputs(max(m, 1), len(tbl))
+        rx.frag_assemble(ob.arena, ob.off, ob.outs, fouts)
+        rx.ingest(ob.arena, ob.off, ob.outs, iouts, fouts)
+        rx.sync()
+        na = int(iouts["n_accepted"].item())
+        dels = iouts["accepted"][:na].cpu().numpy().reshape(-1).view(DELIVERY_DTYPE)
+        ack = iouts["ack_base"][:len(tbl)].cpu().numpy()
+        # oracle on the whole batch; its deliveries name records of the whole batch
+        _, recs, _, _ = oracle.parse(arena, off, ln, match_table=tbl)
+        samples = oracle.FragAssembler().batch(arena, off, recs)[0]
+        _, odels, oack = oracle.HistoryIngest(tbl).batch(arena, off, recs, samples)
+        index = {(int(r["dgram_idx"]), int(r["sub_off"])): i for i, r in enumerate(recs)}
+        orecs = ob.records()
+        _, didx = ob.origin()
+        got = [(index[(int(didx[int(d["rec_idx"])]), int(orecs[int(d["rec_idx"])]["sub_off"]))], int(d["reader_slot"]))
+               for d in dels]
+        assert got == [(int(d["rec_idx"]), int(d["reader_slot"])) for d in odels]
+        assert np.array_equal(ack, oack) and na > 100
+        if wl == "C4":
+            ns = int(fouts["n_samples"].item())
+            assert ns == len(samples) > 10
+            s = fouts["samples"][:ns].cpu().numpy().reshape(-1).view(FRAG_SAMPLE_DTYPE)
+            assert np.array_equal(s["sn"], samples["sn"]) and np.array_equal(s["writer_guid"], samples["writer_guid"])
+    finally:
+        sh.close()
+        rx.set_match_table([])
+
+
+def _torchrun(nproc, script, args, timeout=600):
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+                        "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(REPO, "scripts", script)]
+                       + args, capture_output=True, text=True, timeout=timeout, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return r.stdout
+
+
+@pytest.mark.parametrize("args", [["gloo", "c3"], ["gloo", "c3", "small"], ["gloo", "c4"], ["gloo", "c4", "small"]])
+def test_owner_two_ranks_gloo(args):
+    """two ranks at C5 generator indices (rank * 8M; C4: consecutive chunks so
+    samples straddle them), device parse -> pack -> exchange -> unpack -> reassembly + ingest on
+    each owner; every owner's deliveries and ack_base equal the single-rank oracle ingest of the
+    whole stream for its writers; "small" forces most items through the spill round."""
+    out = _torchrun(2, "owner_check.py", args)
+    assert out.count(" OK") == 2, out
+
+
+def test_owner_one_rank_rccl():
+    """The library's RCCL rounds (rtps_rx_shard_exchange / _finish) with a one-rank communicator,
+    slots small enough that the spill round runs too."""
+    out = _torchrun(1, "owner_check.py", ["nccl", "c3", "small"])
+    assert out.count(" OK") == 1 and "library RCCL" in out, out
+
+
+def test_c5_full_per_rank_size():
+    """8M C3 datagrams (C5's per-rank size at 8 GPUs) through pack + the
+    one-rank RCCL rounds + unpack, and through bucket_by_writer_padded + rtps_rx_exchange:
+    no overflow, no truncation, every item received intact."""
+    out = _torchrun(1, "c5_full_check.py", [], timeout=900)
+    assert "C5 full OK" in out, out
