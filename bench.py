@@ -4,9 +4,14 @@
 One step = parse one batch of synthetic datagrams already resident in HBM
 (the whole receive-path parse: header + submessage walk + interpreter +
 classification + ordered 64-B records).  At N >= 2 GPUs (one process per
-GPU, torch.distributed over RCCL) each rank parses its own batch (weak
-scaling) and the step adds the writer-GUID sharding exchange: stable
-bucket kernel + one RCCL all-to-all of the records.
+GPU, torch.distributed over RCCL) the default workload is C5 (64M datagrams
+in total, rank r parses the r-th chunk: strong scaling) and the step adds the
+owner-side exchange: every writer record that passes goes to
+its writer's owner (writer-GUID hash) with its GAP bitmap / DATA_FRAG payload
+bytes, in fixed slots over one grouped RCCL send/recv per peer (pipelined
+with the next parse) plus an exact spill round when a slot overflows, and is
+unpacked there as one batch.  C5 then times the same steps again with every
+owner's history-cache ingest added (`pipeline_with_ingest`).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload T|C2|C3|C4]
 
@@ -512,9 +517,13 @@ def main():
     ap.add_argument("--no-c1", action="store_true", help="skip the C1 UDP-loopback pipeline measurement")
     ap.add_argument("--match", default="writers", choices=["writers", "none"],
                     help="match table: every writer of the workload (a reader subscribed to all of them) or none")
-    ap.add_argument("--exchange", default="records", choices=["records", "descriptors"],
-                    help="N>1: what crosses xGMI: the 64-B records of every writer / reader submessage, owner = "
-                         "writer-GUID hash % N (north_star), or 16-B descriptors of MATCHED records")
+    ap.add_argument("--exchange", default="owner", choices=["owner", "records", "descriptors"],
+                    help="N>1: what crosses xGMI: 'owner' (default) = every writer record that passes, with its "
+                         "GAP bitmap / DATA_FRAG payload, to its writer's owner (writer-GUID hash % N), unpacked "
+                         "there for reassembly and ingest; 'records' = the 64-B records of every writer / reader "
+                         "submessage; 'descriptors' = 16-B descriptors of MATCHED records")
+    ap.add_argument("--no-owner-ingest", action="store_true",
+                    help="C5: skip the second timed loop that adds the owners' history-cache ingest")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N>1 (gloo only to rehearse several ranks on one GPU)")
     args = ap.parse_args()
@@ -532,6 +541,16 @@ def main():
             dist.init_process_group("gloo")
     dev = torch.device("cuda", local_rank % max(torch.cuda.device_count(), 1))
     torch.cuda.set_device(dev)
+
+    def allreduce_sum(x):
+        if dist is None:
+            return x
+        if args.backend == "gloo":
+            y = x.cpu()
+            dist.all_reduce(y)
+            return y.to(x.device)
+        dist.all_reduce(x)
+        return x
 
     def allreduce_max(x):
         if dist is None:
@@ -573,7 +592,7 @@ def main():
     del probe
     n_matched_writers = 0
     tbl = None
-    if args.match == "writers" or (world > 1 and args.exchange == "descriptors"):
+    if args.match == "writers" or (world > 1 and args.exchange in ("descriptors", "owner")):
         # the reader is subscribed to every writer of the stream: match table = the writer
         # GUIDs found in this batch, sorted (the same table, in the same order, on every rank)
         rx.parse_batch_device(arena, off_t, ln_t, n, outs)
@@ -587,13 +606,15 @@ def main():
         rx.set_match_table(tbl)
         n_matched_writers = len(guids)
     exch = None
+    shards = None
     works = [[], []]
     bcap = 0
-    if world > 1:
-        # Pipelined exchange: two buffer sets; the equal-split all-to-all of batch k
-        # (padded buckets, counts alongside, no host round trip) runs on the RCCL
-        # stream while batch k+1 is parsed.  Bucket capacity = the largest bucket of
-        # this batch over all ranks (the batch repeats every step, so it never overflows;
+    owner = world > 1 and args.exchange == "owner"
+    if world > 1 and not owner:
+        # Record / descriptor exchange (round 2's path): two buffer sets; the equal-split
+        # all-to-all of batch k (padded buckets, counts alongside, no host round trip) runs
+        # on the RCCL stream while batch k+1 is parsed.  Bucket capacity = the largest bucket
+        # of this batch over all ranks (the batch repeats every step, so it never overflows;
         # overflow is checked after the timed region).
         from rtps_rx.shard import Exchange
         item = args.exchange
@@ -605,44 +626,125 @@ def main():
         del probe_ex
         exch = [Exchange(rx, n_rec, world, dist, dev, cap=bcap, item=item) for _ in range(2)]
         outs_pp = [outs, rx.alloc_outputs(n, n_rec)]
+    slot = (0, 0)
+    owned = [None, None]
+    iouts = None
+    if owner:
+        # Owner-side exchange (rtps_rx_shard_*): every writer record that passes goes to its
+        # writer's owner with its GAP bitmap / DATA_FRAG payload bytes.  Slots sized from a
+        # first pack of this batch (largest (source, owner) pair over all ranks); anything
+        # that does not fit would cross in the exact spill round, never be dropped.
+        from rtps_rx.shard import OwnerShard
+        probe_sh = OwnerShard(rx, world, dist, dev, 1, 0)
+        rx.parse_batch_device(arena, off_t, ln_t, n, outs)
+        probe_sh.pack(arena, off_t, outs)
+        c = probe_sh.counts("send")
+        probe_sh.close()
+        mx = allreduce_max(torch.tensor([int(c["n"].max()), int(c["bytes"].max())], dtype=torch.int64, device=dev))
+        slot = (max(int(mx[0].item()), 1), int(mx[1].item()))
+        shards = [OwnerShard(rx, world, dist, dev, slot[0], slot[1]) for _ in range(2)]
+        outs_pp = [outs, rx.alloc_outputs(n, n_rec)]
+    pending = [False, False]
+    with_ingest = [False]
+
+    def owner_ingest(b):
+        """The owner's history-cache ingest of what batch b delivered to it (fresh writer proxies
+        each step, so every step does the same work: all first copies accepted)."""
+        nonlocal iouts
+        ob = owned[b]
+        if iouts is None or iouts["accept"].numel() < max(ob.n_records, 1):
+            iouts = rx.alloc_ingest_outputs(max(ob.n_records, 1), n_matched_writers)
+        rx.ingest_reset()
+        rx.ingest(ob.arena, ob.off, ob.outs, iouts)
+
+    def drain(b):
+        if pending[b]:
+            shards[b].finish()
+            owned[b] = shards[b].unpack()
+            pending[b] = False
+            if with_ingest[0]:
+                owner_ingest(b)
 
     def step(k):
         if world == 1:
             rx.parse_batch_device(arena, off_t, ln_t, n, outs)
+            if with_ingest[0]:
+                if iouts is None:
+                    owner_ingest_n1()
+                rx.ingest_reset()
+                rx.ingest(arena, off_t, outs, iouts)
             return
         b = k & 1
+        if owner:
+            # batch k: parse + pack on the compute stream; meanwhile the host finishes batch
+            # k-1 (its round 0 ran on the RCCL stream during this parse) and unpacks it for its
+            # owners; then round 0 of batch k goes out
+            rx.parse_batch_device(arena, off_t, ln_t, n, outs_pp[b])
+            shards[b].pack(arena, off_t, outs_pp[b])
+            drain(1 - b)
+            shards[b].exchange()
+            pending[b] = True
+            return
         for w in works[b]:  # the exchange that last used buffer set b is done
             w.wait()
         rx.parse_batch_device(arena, off_t, ln_t, n, outs_pp[b])
         exch[b].bucket(outs_pp[b])
         works[b] = exch[b].exchange_async()
 
-    for k in range(args.warmup):
-        step(k)
-    # One event pair around the whole timed region, on the parse stream: an event
-    # recorded between steps costs each step 7-11 us of dispatch gap on MI355X
-    # (scripts/diag_step_gap.py), so the kernel time is the per-step average over
-    # back-to-back launches (both kernels plus the gaps between them).
-    ev_start = torch.cuda.Event(enable_timing=True)
-    ev_end = torch.cuda.Event(enable_timing=True)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    ev_start.record(stream)
-    for k in range(args.steps):
-        step(args.warmup + k)
-    ev_end.record(stream)
-    for ws in works:
-        for w in ws:
-            w.wait()
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    wall = time.perf_counter() - t0
-    if dist:
-        wall = float(allreduce_max(torch.tensor([wall], dtype=torch.float64, device=dev)).item())
-    ev_ms = ev_start.elapsed_time(ev_end) / args.steps
+    def owner_ingest_n1():
+        nonlocal iouts
+        iouts = rx.alloc_ingest_outputs(max(n_rec, 1), n_matched_writers)
+
+    def timed(steps, warmup):
+        for k in range(warmup):
+            step(k)
+        if owner:  # the warmup's last batch is finished before the clock starts
+            drain(0)
+            drain(1)
+        # One event pair around the whole timed region, on the parse stream: an event
+        # recorded between steps costs each step 7-11 us of dispatch gap on MI355X
+        # (scripts/diag_step_gap.py), so the kernel time is the per-step average over
+        # back-to-back launches (both kernels plus the gaps between them).
+        ev_start = torch.cuda.Event(enable_timing=True)
+        ev_end = torch.cuda.Event(enable_timing=True)
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        ev_start.record(stream)
+        for k in range(steps):
+            step(warmup + k)
+        if owner:  # the last batch's rounds and unpack belong to the timed steps
+            drain((warmup + steps - 1) & 1)
+        ev_end.record(stream)
+        for ws in works:
+            for w in ws:
+                w.wait()
+        torch.cuda.synchronize(dev)
+        if dist:
+            dist.barrier()
+        wall = time.perf_counter() - t0
+        if dist:
+            wall = float(allreduce_max(torch.tensor([wall], dtype=torch.float64, device=dev)).item())
+        return wall, ev_start.elapsed_time(ev_end) / steps
+
+    wall, ev_ms = timed(args.steps, args.warmup)
+    pipeline = None
+    if c5 and not args.no_owner_ingest and n_matched_writers:
+        # the same steps ending where the N = 1 receive path ends: every owner ingests its
+        # writers' records into the history cache (deliveries), timed as a second loop
+        with_ingest[0] = True
+        w2, e2 = timed(args.steps, args.warmup)
+        with_ingest[0] = False
+        torch.cuda.synchronize(dev)
+        na = int(iouts["n_accepted"].item())
+        na_all = int(allreduce_sum(torch.tensor([na], dtype=torch.int64, device=dev)).item())
+        pipeline = {"what": "parse + owner exchange (pack, RCCL rounds, unpack) + history-cache ingest on every "
+                            "owner (fresh writer proxies each step)" if world > 1 else
+                            "parse + history-cache ingest (fresh writer proxies each step)",
+                    "value": world * n / (w2 / args.steps), "unit": "datagrams/s",
+                    "ms_per_step": w2 / args.steps * 1e3, "deliveries_per_step_all_ranks": na_all,
+                    "deliveries_per_s": na_all / (w2 / args.steps)}
 
     # ---- results / sanity (outside the timed region) ----
     status = outs["status"][:n].cpu().numpy()
@@ -703,7 +805,19 @@ def main():
                                                   "source": os.path.relpath(ref[-1], REPO)}
             except (OSError, ValueError, KeyError, IndexError):
                 pass
-    if world > 1:
+    if world > 1 and owner:
+        last = owned[(args.warmup + args.steps - 1) & 1]
+        result["config"]["received_records_rank0"] = int(last.n_records) if last is not None else 0
+        rcv = shards[(args.warmup + args.steps - 1) & 1].counts("recv")
+        result["config"]["exchange"] = {
+            "mode": "owner-side exchange: fixed slots (equal-split RCCL group, pipelined with the next parse) "
+                    "+ exact spill round when a slot overflows",
+            "item": "64-B records of the writer submessages that pass + their GAP bitmap / DATA_FRAG payload "
+                    "bytes, owner = writer-GUID hash % world; unpacked on the owner as one batch",
+            "slot_records": slot[0], "slot_blob_bytes": slot[1],
+            "bytes_sent_per_rank_per_step": world * (slot[0] * 64 + slot[1]),
+            "spilled_records_rank0": int((rcv["n"] - rcv["cut"]).sum()), "overflow": False}
+    elif world > 1:
         got, split = exch[(args.warmup + args.steps - 1) & 1].gather_received()
         result["config"]["received_records_rank0"] = int(got.shape[0])
         ib = 16 if args.exchange == "descriptors" else 64
@@ -713,6 +827,8 @@ def main():
                      if ib == 16 else "64-B records, owner = writer-GUID hash % world"),
             "bucket_capacity": bcap, "bytes_sent_per_rank_per_step": world * bcap * ib,
             "overflow": any(e.overflowed() for e in exch)}
+    if pipeline is not None:
+        result["pipeline_with_ingest"] = pipeline
     if world == 1 and not args.no_cdr:
         result["cdr_decode"] = cdr_decode_leg(rx, args.workload, arena, off_t, outs, n_rec, stream, args.steps)
     if world == 1 and not args.no_frag and args.workload == "C4" and recs is not None:
@@ -732,7 +848,10 @@ def main():
         print(json.dumps(result), flush=True)
     rx.close()
     if dist:
-        if exch is not None:
+        if shards is not None:
+            for sh in shards:
+                sh.close()
+        if exch is not None or shards is not None:
             from rtps_rx.shard import destroy_comms
             destroy_comms()  # the library's RCCL communicators, before the process group goes
         dist.destroy_process_group()

@@ -32,6 +32,29 @@
 
 static_assert(RTPS_RX_EXCHANGE_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "unique id size");
 
+// Point-to-point messages are cut into pieces of at most XCHUNK bytes, posted in
+// order inside the same group (NCCL matches a peer's sends and receives in
+// order).  Measured on MI355X with RCCL 2.26: a single 1.2-1.4 GB ncclSend /
+// ncclRecv pair (one rank exchanging with itself at C5's per-rank size) delivered
+// only the first half of the bytes; pieces of this size arrive whole.
+constexpr size_t XCHUNK = size_t(64) << 20;
+static bool send_bytes(const void* buf, size_t n, int peer, ncclComm_t c, hipStream_t st) {
+  const uint8_t* p = static_cast<const uint8_t*>(buf);
+  for (size_t o = 0; o < n; o += XCHUNK) {
+    const size_t k = n - o < XCHUNK ? n - o : XCHUNK;
+    if (ncclSend(p + o, k, ncclUint8, peer, c, st) != ncclSuccess) return false;
+  }
+  return true;
+}
+static bool recv_bytes(void* buf, size_t n, int peer, ncclComm_t c, hipStream_t st) {
+  uint8_t* p = static_cast<uint8_t*>(buf);
+  for (size_t o = 0; o < n; o += XCHUNK) {
+    const size_t k = n - o < XCHUNK ? n - o : XCHUNK;
+    if (ncclRecv(p + o, k, ncclUint8, peer, c, st) != ncclSuccess) return false;
+  }
+  return true;
+}
+
 extern "C" {
 
 int rtps_rx_exchange_unique_id(uint8_t id[RTPS_RX_EXCHANGE_ID_BYTES]) {
@@ -76,8 +99,7 @@ int rtps_rx_exchange(rtps_rx_ctx* ctx, void* comm, void* hip_stream, const void*
   for (int p = 0; p < world && ok; ++p) {
     ok = ncclSend(send_counts + p, 1, ncclUint64, p, c, st) == ncclSuccess &&
          ncclRecv(recv_counts + p, 1, ncclUint64, p, c, st) == ncclSuccess &&
-         ncclSend(s + (size_t)p * bytes, bytes, ncclUint8, p, c, st) == ncclSuccess &&
-         ncclRecv(r + (size_t)p * bytes, bytes, ncclUint8, p, c, st) == ncclSuccess;
+         send_bytes(s + (size_t)p * bytes, bytes, p, c, st) && recv_bytes(r + (size_t)p * bytes, bytes, p, c, st);
   }
   const bool ended = ncclGroupEnd() == ncclSuccess;
   if (!ok || !ended) {
@@ -103,10 +125,9 @@ int rtps_rx_shard_exchange(rtps_shard* s, void* comm, void* hip_stream) {
   for (int p = 0; p < world && ok; ++p) {
     ok = ncclSend(s->s_counts + p, cw, ncclUint64, p, c, st) == ncclSuccess &&
          ncclRecv(s->r_counts + p, cw, ncclUint64, p, c, st) == ncclSuccess &&
-         ncclSend(reinterpret_cast<const uint8_t*>(s->s_slots) + p * rb, rb, ncclUint8, p, c, st) == ncclSuccess &&
-         ncclRecv(reinterpret_cast<uint8_t*>(s->r_slots) + p * rb, rb, ncclUint8, p, c, st) == ncclSuccess &&
-         (bb == 0 || (ncclSend(s->s_blob + p * bb, bb, ncclUint8, p, c, st) == ncclSuccess &&
-                      ncclRecv(s->r_blob + p * bb, bb, ncclUint8, p, c, st) == ncclSuccess));
+         send_bytes(reinterpret_cast<const uint8_t*>(s->s_slots) + p * rb, rb, p, c, st) &&
+         recv_bytes(reinterpret_cast<uint8_t*>(s->r_slots) + p * rb, rb, p, c, st) &&
+         send_bytes(s->s_blob + p * bb, bb, p, c, st) && recv_bytes(s->r_blob + p * bb, bb, p, c, st);
   }
   const bool ended = ncclGroupEnd() == ncclSuccess;
   if (!ok || !ended) {
@@ -153,12 +174,10 @@ int rtps_rx_shard_finish(rtps_shard* s, void* comm, void* hip_stream) {
     const rtps_shard_counts& q = s->h_send[p];
     const rtps_shard_counts& r = s->h_recv[p];
     const uint64_t sn = q.n - q.cut, sbytes = q.bytes - q.cut_bytes, rn = r.n - r.cut, rbytes = r.bytes - r.cut_bytes;
-    if (sn)
-      ok = ok && ncclSend(s->s_spill + sb + q.cut, sn * sizeof(rtps_record), ncclUint8, (int)p, c, st) == ncclSuccess;
-    if (sbytes)
-      ok = ok && ncclSend(s->s_bspill + sbb + q.cut_bytes, sbytes, ncclUint8, (int)p, c, st) == ncclSuccess;
-    if (rn) ok = ok && ncclRecv(s->r_spill + rs, rn * sizeof(rtps_record), ncclUint8, (int)p, c, st) == ncclSuccess;
-    if (rbytes) ok = ok && ncclRecv(s->r_bspill + rsb, rbytes, ncclUint8, (int)p, c, st) == ncclSuccess;
+    ok = send_bytes(s->s_spill + sb + q.cut, sn * sizeof(rtps_record), (int)p, c, st) &&
+         send_bytes(s->s_bspill + sbb + q.cut_bytes, sbytes, (int)p, c, st) &&
+         recv_bytes(s->r_spill + rs, rn * sizeof(rtps_record), (int)p, c, st) &&
+         recv_bytes(s->r_bspill + rsb, rbytes, (int)p, c, st);
     sb += q.n;
     sbb += q.bytes;
     rs += rn;

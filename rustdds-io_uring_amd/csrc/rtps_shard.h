@@ -50,8 +50,6 @@ struct rtps_shard {
   uint8_t* o_arena = nullptr;
   uint64_t o_arena_cap = 0;
   uint64_t* o_n = nullptr;  // device u64
-  void* seg = nullptr;      // device segment table of the unpack copy
-  uint64_t* h_seg = nullptr;  // pinned staging of the segment table
   void* cub_tmp = nullptr;
   size_t cub_bytes = 0;
 };

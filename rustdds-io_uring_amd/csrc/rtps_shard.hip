@@ -274,18 +274,58 @@ __global__ __launch_bounds__(ST) void shard_scatter(PackArgs a) {
 struct Seg {  // one contiguous copy: 16-B chunks [c0, c0 + nc) of the flat chunk space
   uint64_t src, dst, c0, nc;
 };
-__global__ __launch_bounds__(ST) void shard_segments(const Seg* seg, uint32_t n_seg, uint64_t total_chunks) {
+struct SegArgs {
+  const rtps_shard_counts* counts;  // [n_src] received counts (device)
+  uint32_t n_src;
+  uint64_t cap, bcap;
+  const rtps_record* r_slots;
+  const uint8_t* r_blob;
+  const rtps_record* r_spill;
+  const uint8_t* r_bspill;
+  rtps_record* o_rec;
+  uint8_t* o_blob;  // owner arena + RTPS_SHARD_LEAD
+};
+// Per source: its slot records, its spilled records, its slot blob bytes, its spilled
+// bytes, each one contiguous copy.  Every workgroup builds the (<= 4 x 64 entry)
+// table from the device counts, so no host staging is involved.
+__global__ __launch_bounds__(ST) void shard_segments(SegArgs a) {
+  __shared__ Seg seg[4 * SHARD_MAX_RANKS];
+  __shared__ uint32_t n_seg;
+  __shared__ uint64_t total;
+  if (threadIdx.x == 0) {
+    uint32_t ns = 0;
+    uint64_t chunks = 0, rpos = 0, bpos = 0, rsp = 0, bsp = 0;
+    auto add = [&](const void* src, void* dst, uint64_t nbytes) {
+      if (!nbytes) return;
+      seg[ns++] = Seg{(uint64_t)(uintptr_t)src, (uint64_t)(uintptr_t)dst, chunks, nbytes / 16};
+      chunks += nbytes / 16;
+    };
+    for (uint32_t k = 0; k < a.n_src; ++k) {
+      const rtps_shard_counts c = a.counts[k];
+      add(a.r_slots + (uint64_t)k * a.cap, a.o_rec + rpos, c.cut * sizeof(rtps_record));
+      add(a.r_spill + rsp, a.o_rec + rpos + c.cut, (c.n - c.cut) * sizeof(rtps_record));
+      add(a.r_blob + (uint64_t)k * a.bcap, a.o_blob + bpos, c.cut_bytes);
+      add(a.r_bspill + bsp, a.o_blob + bpos + c.cut_bytes, c.bytes - c.cut_bytes);
+      rpos += c.n;
+      bpos += c.bytes;
+      rsp += c.n - c.cut;
+      bsp += c.bytes - c.cut_bytes;
+    }
+    n_seg = ns;
+    total = chunks;
+  }
+  __syncthreads();
   const uint64_t stride = (uint64_t)gridDim.x * ST;
-  for (uint64_t c = (uint64_t)blockIdx.x * ST + threadIdx.x; c < total_chunks; c += stride) {
+  for (uint64_t c = (uint64_t)blockIdx.x * ST + threadIdx.x; c < total; c += stride) {
     uint32_t lo = 0, hi = n_seg;  // last segment with c0 <= c
     while (hi - lo > 1) {
       const uint32_t mid = (lo + hi) >> 1;
       if (seg[mid].c0 <= c) lo = mid; else hi = mid;
     }
-    const Seg s = seg[lo];
-    const uint64_t k = c - s.c0;
-    const uint4* src = reinterpret_cast<const uint4*>((uintptr_t)s.src) + k;
-    uint4* dst = reinterpret_cast<uint4*>((uintptr_t)s.dst) + k;
+    const Seg sg = seg[lo];
+    const uint64_t k = c - sg.c0;
+    const uint4* src = reinterpret_cast<const uint4*>((uintptr_t)sg.src) + k;
+    uint4* dst = reinterpret_cast<uint4*>((uintptr_t)sg.dst) + k;
     *dst = *src;
   }
 }
@@ -367,8 +407,6 @@ int rtps_rx_shard_create(rtps_rx_ctx* ctx, uint32_t n_ranks, uint64_t cap, uint6
             hipMemset(s->s_counts, 0, n_ranks * sizeof(rtps_shard_counts)) == hipSuccess &&
             hipHostMalloc(&s->h_send, n_ranks * sizeof(rtps_shard_counts), hipHostMallocDefault) == hipSuccess &&
             hipHostMalloc(&s->h_recv, n_ranks * sizeof(rtps_shard_counts), hipHostMallocDefault) == hipSuccess &&
-            hipHostMalloc(&s->h_seg, 4 * SHARD_MAX_RANKS * sizeof(Seg), hipHostMallocDefault) == hipSuccess &&
-            hipMalloc(&s->seg, 4 * SHARD_MAX_RANKS * sizeof(Seg)) == hipSuccess &&
             hipMalloc(&s->o_n, sizeof(uint64_t)) == hipSuccess &&
             hipMemset(s->o_n, 0, sizeof(uint64_t)) == hipSuccess &&
             hipEventCreateWithFlags(&s->packed, hipEventDisableTiming) == hipSuccess &&
@@ -388,12 +426,11 @@ int rtps_rx_shard_destroy(rtps_shard* s) {
   (void)hipDeviceSynchronize();
   void* dev[] = {s->s_slots, s->s_blob, s->s_counts, s->s_spill, s->s_bspill, s->hist, s->hscan, s->r_slots,
                  s->r_blob, s->r_counts, s->r_spill, s->r_bspill, s->o_rec, s->o_off, s->o_origin, s->o_size,
-                 s->o_boff, s->o_arena, s->o_n, s->seg, s->cub_tmp};
+                 s->o_boff, s->o_arena, s->o_n, s->cub_tmp};
   for (void* p : dev)
     if (p) (void)hipFree(p);
   if (s->h_send) (void)hipHostFree(s->h_send);
   if (s->h_recv) (void)hipHostFree(s->h_recv);
-  if (s->h_seg) (void)hipHostFree(s->h_seg);
   hipEvent_t ev[] = {s->packed, s->counts_ev, s->done};
   for (hipEvent_t e : ev)
     if (e) (void)hipEventDestroy(e);
@@ -475,12 +512,16 @@ int rtps_rx_shard_unpack(rtps_shard* s, rtps_owner_batch* out) {
   (void)hipSetDevice(s->device);
   hipStream_t st = rtps_ctx_stream(s->ctx);
   const uint32_t n = s->n_ranks;
-  // the received counts (after rtps_rx_shard_finish, or a host-driven transport's copies)
-  if (s->exchanged && hipStreamWaitEvent(st, s->done, 0) != hipSuccess) return RTPS_RX_EHIP;
-  if (hipMemcpyAsync(s->h_recv, s->r_counts, n * sizeof(rtps_shard_counts), hipMemcpyDeviceToHost, st) !=
-          hipSuccess ||
-      hipStreamSynchronize(st) != hipSuccess)
+  // the received counts: the RCCL rounds left them in pinned memory (no sync beyond
+  // round 0's counts); after a host-driven transport they are read from the device
+  if (s->exchanged) {
+    if (hipEventSynchronize(s->counts_ev) != hipSuccess || hipStreamWaitEvent(st, s->done, 0) != hipSuccess)
+      return RTPS_RX_EHIP;
+  } else if (hipMemcpyAsync(s->h_recv, s->r_counts, n * sizeof(rtps_shard_counts), hipMemcpyDeviceToHost, st) !=
+                 hipSuccess ||
+             hipStreamSynchronize(st) != hipSuccess) {
     return RTPS_RX_EHIP;
+  }
   uint64_t total = 0, bytes = 0, sp = 0, bsp = 0;
   FixArgs fa;
   memset(&fa, 0, sizeof fa);
@@ -516,32 +557,13 @@ int rtps_rx_shard_unpack(rtps_shard* s, rtps_owner_batch* out) {
         hipMemset(s->o_arena, 0, RTPS_SHARD_LEAD) != hipSuccess)
       return RTPS_RX_ENOMEM;
   }
-  // segment table: per source, slot records, spilled records, slot blob bytes, spilled bytes
-  Seg* seg = reinterpret_cast<Seg*>(s->h_seg);
-  uint32_t ns = 0;
-  uint64_t chunks = 0, rpos = 0, bpos = 0, rsp = 0, bsp2 = 0;
-  auto add = [&](const void* src, void* dst, uint64_t nbytes) {
-    if (!nbytes) return;
-    seg[ns++] = Seg{(uint64_t)(uintptr_t)src, (uint64_t)(uintptr_t)dst, chunks, nbytes / 16};
-    chunks += nbytes / 16;
-  };
-  for (uint32_t k = 0; k < n; ++k) {
-    const rtps_shard_counts& c = s->h_recv[k];
-    add(s->r_slots + (uint64_t)k * s->cap, s->o_rec + rpos, c.cut * sizeof(rtps_record));
-    add(s->r_spill + rsp, s->o_rec + rpos + c.cut, (c.n - c.cut) * sizeof(rtps_record));
-    add(s->r_blob + (uint64_t)k * s->bcap, s->o_arena + RTPS_SHARD_LEAD + bpos, c.cut_bytes);
-    add(s->r_bspill + bsp2, s->o_arena + RTPS_SHARD_LEAD + bpos + c.cut_bytes, c.bytes - c.cut_bytes);
-    rpos += c.n;
-    bpos += c.bytes;
-    rsp += c.n - c.cut;
-    bsp2 += c.bytes - c.cut_bytes;
-  }
-  if (ns && (hipMemcpyAsync(s->seg, seg, ns * sizeof(Seg), hipMemcpyHostToDevice, st) != hipSuccess))
-    return RTPS_RX_EHIP;
-  if (ns) {
+  {
+    SegArgs sa{s->r_counts, n, s->cap, s->bcap, s->r_slots, s->r_blob, s->r_spill, s->r_bspill, s->o_rec,
+               s->o_arena + RTPS_SHARD_LEAD};
+    const uint64_t chunks = (total * sizeof(rtps_record) + bytes) / 16;
     const uint64_t blocks = (chunks + ST - 1) / ST;
-    hipLaunchKernelGGL(shard_segments, dim3((uint32_t)(blocks < 16384 ? blocks : 16384)), dim3(ST), 0, st,
-                       (const Seg*)s->seg, ns, chunks);
+    if (chunks)
+      hipLaunchKernelGGL(shard_segments, dim3((uint32_t)(blocks < 16384 ? blocks : 16384)), dim3(ST), 0, st, sa);
   }
   if (total) {
     fa.rec = s->o_rec; fa.origin = s->o_origin; fa.size = s->o_size; fa.n = total; fa.n_src = n;

@@ -25,7 +25,7 @@ import rtps_rx
 from rtps_rx.shard import OwnerShard, Exchange, destroy_comms, dev_copy
 
 OWN = bytes.fromhex("0103000c292d31a228200208")
-n = 8 << 20
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 8 << 20
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
 dist.init_process_group("nccl", device_id=dev)
@@ -89,6 +89,11 @@ bmo = exp[gi, 52:54].contiguous().view(torch.int16).reshape(-1).to(torch.int64) 
 src = off_t[exp[gi, 0:4].contiguous().view(torch.int32).reshape(-1).to(torch.int64)] + bmo
 dst = goff[gi] + bmo
 bm_ok = torch.equal(arena[src], oarena[dst]) and torch.equal(arena[src + 3], oarena[dst + 3])
+if not body_ok:
+    bad = torch.nonzero((got[:, 4:] != exp[:, 4:]).any(dim=1)).reshape(-1)
+    i = int(bad[0].item())
+    print(f"  {len(bad)} rows differ, first {i}: got {got[i].cpu().numpy().tobytes().hex()} "
+          f"exp {exp[i].cpu().numpy().tobytes().hex()}", flush=True)
 ok &= ob.n_records == n_items and spill == 0 and idx_ok and body_ok and org_ok and bm_ok
 print(f"owner exchange (library RCCL rounds): {n_items} items, {blob_total} blob bytes, spill {spill}, "
       f"records {'ok' if body_ok and idx_ok else 'BAD'}, origin {'ok' if org_ok else 'BAD'}, "
@@ -106,6 +111,11 @@ over = ex.overflowed()
 got, split = ex.exchange()
 torch.cuda.synchronize()
 rec_ok = got.shape[0] == n_exch and torch.equal(got, recs[exch_kind])
+if not rec_ok and got.shape[0] == n_exch:
+    bad = torch.nonzero((got != recs[exch_kind]).any(dim=1)).reshape(-1)
+    i = int(bad[0].item())
+    print(f"  {len(bad)} rows differ, first {i}: got {got[i].cpu().numpy().tobytes().hex()} "
+          f"exp {recs[exch_kind][i].cpu().numpy().tobytes().hex()}", flush=True)
 ok &= rec_ok and not over
 print(f"record exchange (rtps_rx_exchange): {n_exch} records, overflow {over}, "
       f"received {'== bucketed' if rec_ok else 'MISMATCH'}, {time.time() - t0:.0f} s", flush=True)
