@@ -267,6 +267,10 @@ def cdr_decode_leg(rx, workload, arena, off_t, outs, n_rec, stream, steps):
     # algorithmic bytes: 40 B of each record read, 1 status byte + one row written per record,
     # and for decoded rows the value bytes consumed (= row_bytes for these all-primitive types)
     alg = n_rec * (40 + 1 + t.row_bytes) + ok * t.row_bytes
+    if ok == 0:  # nothing decoded (e.g. C4: its samples are DATA_FRAG, decoded after reassembly): no rate
+        return {"sample_type": CDR_TYPES[workload], "records": n_rec, "decoded_ok": 0,
+                "status_hist": np.bincount(st, minlength=7).tolist(),
+                "note": "no DATA record of this batch decodes as this type, so no rate is reported"}
     return {"sample_type": CDR_TYPES[workload], "row_bytes": t.row_bytes, "records": n_rec, "decoded_ok": ok,
             "status_hist": np.bincount(st, minlength=7).tolist(), "kernel": "cdr_decode_kernel", "kernel_ms": ms,
             "rows_per_s": ok / (ms * 1e-3), "alg_bytes_per_launch": alg,
@@ -730,7 +734,7 @@ def main():
 
     wall, ev_ms = timed(args.steps, args.warmup)
     pipeline = None
-    if c5 and not args.no_owner_ingest and n_matched_writers:
+    if c5 and (owner or world == 1) and not args.no_owner_ingest and n_matched_writers:
         # the same steps ending where the N = 1 receive path ends: every owner ingests its
         # writers' records into the history cache (deliveries), timed as a second loop
         with_ingest[0] = True

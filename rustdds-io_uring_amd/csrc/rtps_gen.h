@@ -110,10 +110,33 @@ RG_HD static inline void rg_rtps_header(rg_w* w, const uint8_t prefix[12], uint3
   rg_put_bytes(w, prefix, 12);
 }
 
-/* DATA submessage with MessageBuilder::data_msg layout (otq = 16). */
+/* A ShapeType sample {color: String, x: i32, y: i32, shapesize: i32} (the shapes demo
+ * type of the reference's receiver test, rtps/message_receiver.rs:1250-1254) in classic
+ * CDR after the encapsulation header, byte order le; values from the fill key (no rng
+ * draws, so the rest of the datagram does not depend on it).  Returns bytes written,
+ * 0 if n is too short (then the payload stays fill bytes). */
+RG_HD static inline uint32_t rg_shape(rg_w* w, int le, uint32_t n) {
+  const char* colors[8] = {"RED", "GREEN", "BLUE", "YELLOW", "ORANGE", "CYAN", "MAGENTA", "PURPLE"};
+  const uint64_t h = rg_mix(w->fill_key ^ ((uint64_t)w->pos << 20));
+  const char* c = colors[h & 7u];
+  uint32_t len = 0;
+  while (c[len]) ++len;
+  const uint32_t str = 4u + ((len + 1u + 3u) & ~3u);
+  if (n < str + 12u) return 0;
+  rg_put32(w, len + 1u, le);
+  for (uint32_t i = 0; i < len; ++i) rg_put8(w, (uint8_t)c[i]);
+  for (uint32_t i = len; i < str - 4u; ++i) rg_put8(w, 0);  /* NUL + alignment of x */
+  rg_put32(w, (uint32_t)((h >> 8) % 300u), le);
+  rg_put32(w, (uint32_t)((h >> 24) % 300u), le);
+  rg_put32(w, 10u + (uint32_t)((h >> 40) % 50u), le);
+  return str + 12u;
+}
+
+/* DATA submessage with MessageBuilder::data_msg layout (otq = 16).  shape: a D payload
+ * starts with a ShapeType sample (the C3 mix), the rest is fill. */
 RG_HD static inline void rg_data(rg_w* w, int le, uint32_t flags_extra, const uint8_t rid[4],
                                  const uint8_t wid[4], int64_t sn, uint32_t qos_bytes,
-                                 rg_rng* r, uint32_t payload) {
+                                 rg_rng* r, uint32_t payload, int shape) {
   uint32_t flags = (le ? 0x01u : 0x00u) | flags_extra;
   rg_put8(w, 0x15); rg_put8(w, flags);
   rg_put16(w, 20u + qos_bytes + payload, le);
@@ -135,7 +158,8 @@ RG_HD static inline void rg_data(rg_w* w, int le, uint32_t flags_extra, const ui
   if (payload) {
     /* SerializedPayload: encapsulation (CDR_LE / CDR_BE) + options, then data */
     rg_put8(w, 0x00); rg_put8(w, le ? 0x01 : 0x00); rg_put8(w, 0); rg_put8(w, 0);
-    rg_put_fill(w, payload - 4);
+    const uint32_t used = (shape && (flags & 0x04u)) ? rg_shape(w, le, payload - 4) : 0u;
+    rg_put_fill(w, payload - 4 - used);
   }
 }
 
@@ -156,7 +180,7 @@ RG_HD static inline uint32_t rtps_gen_datagram(int wl, uint64_t seed, uint64_t i
     rg_writer_prefix(seed, wr, prefix);
     rg_writer_eid(wr, wid);
     rg_rtps_header(&w, prefix, 2);
-    rg_data(&w, 1, 0x04, zero_eid, wid, sn, 0, &r, payload);
+    rg_data(&w, 1, 0x04, zero_eid, wid, sn, 0, &r, payload, 0);
     return w.pos;
   }
 
@@ -247,10 +271,10 @@ RG_HD static inline uint32_t rtps_gen_datagram(int wl, uint64_t seed, uint64_t i
       if (malformed == 8 && !have_data) {
         /* octetsToInlineQos < 16 -> DATA error (data.rs:86-91) */
         uint32_t at = w.pos;
-        rg_data(&w, le, fl, zero_eid, weid, sn, qos, &r, payload);
+        rg_data(&w, le, fl, zero_eid, weid, sn, qos, &r, payload, 1);
         if (out) { if (le) { out[at + 6] = 8; out[at + 7] = 0; } else { out[at + 6] = 0; out[at + 7] = 8; } }
       } else {
-        rg_data(&w, le, fl, zero_eid, weid, sn, qos, &r, payload);
+        rg_data(&w, le, fl, zero_eid, weid, sn, qos, &r, payload, 1);
       }
       have_data = 1;
     } else if (pick < 75) { /* HEARTBEAT (heartbeat.rs:21-49) */

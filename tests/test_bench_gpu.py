@@ -51,10 +51,10 @@ def test_bench_one_rank_line(workload):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("exchange", ["records", "descriptors"])
+@pytest.mark.parametrize("exchange", ["owner", "records", "descriptors"])
 def test_bench_two_ranks_gloo_exchange(exchange):
-    """N=2 default: the C5 config (C3 mix, 64M / N per rank, here reduced) with the
-    writer-GUID hash record exchange; descriptors as the option."""
+    """N=2: the C5 config (C3 mix, 64M / N per rank, here reduced) with the owner-side
+    exchange (default) and its ingest pipeline; the record and descriptor exchanges as options."""
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
@@ -67,7 +67,14 @@ def test_bench_two_ranks_gloo_exchange(exchange):
     ex = d["config"]["exchange"]
     assert ex["overflow"] is False
     got, per = d["config"]["received_records_rank0"], d["config"]["records_per_gpu"]
-    if exchange == "records":
+    if exchange == "owner":
+        # rank 0 owns about half of both ranks' writer records that pass (about 2.3 of the 3.8
+        # records per C3 datagram); the second timed loop adds every owner's ingest
+        assert "owner-side" in ex["mode"] and ex["spilled_records_rank0"] == 0
+        assert 0.35 * per < got < 0.8 * per, (got, per)
+        p = d["pipeline_with_ingest"]
+        assert p["value"] > 0 and p["deliveries_per_step_all_ranks"] > 0.5 * per
+    elif exchange == "records":
         # owner = writer-GUID hash % 2 over 256 writers: rank 0 receives about half of both ranks'
         # writer / reader records (about 2.8 of the 3.8 records per C3 datagram)
         assert "writer-GUID hash" in ex["item"]
