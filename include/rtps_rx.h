@@ -506,8 +506,19 @@ int rtps_rx_cdr_decode(rtps_rx_ctx* ctx, const rtps_cdr_op* prog, uint32_t n_ops
  *     fragment bits (insert_frags :65-140);
  *   - when every bit is set the sample is emitted and the buffer dropped
  *     (new_datafrag :172-214, is_complete :142-144).
- * State (writer fragment sizes, incomplete buffers) persists in the context
- * across batches.  Completed samples are emitted in completing-record order;
+ * With readers set (rtps_rx_set_readers), every reader has its own assembler per
+ * writer, as every Reader has its own FragmentAssembler per writer GUID
+ * (reader.rs:617-619, 638-647): a DATA_FRAG record is assembled once for every
+ * reader of its target set (records that are a builtin pair or reach no reader are
+ * not assembled: Discovery2 / nobody takes them), the fragment size is the one of
+ * that reader's first DATA_FRAG of the writer, and a reader whose Lifespan
+ * (rtps_rx_set_reader_lifespan) has expired for the record's source timestamp
+ * skips it (handle_datafrag_msg :578-589).  A reader added later starts with no
+ * buffers; the others keep theirs.  Without readers, one assembler per writer
+ * takes every DATA_FRAG that passes (the form the reader-less tests use).
+ * State (fragment sizes, incomplete buffers) persists in the context
+ * across batches.  Completed samples are emitted in completing-record order
+ * (then target-set order), each with the reader whose assembler completed it;
  * their SerializedPayload bytes (incl. the 4-byte encapsulation) are written
  * back to back (16-byte aligned) into `heap`.  Inputs the reference rejects
  * by panicking (fragment bits past the buffer's count, byte ranges past its
@@ -520,7 +531,8 @@ typedef struct rtps_frag_sample {
   uint32_t rec_idx;        /* record (of this batch) that completed the sample */
   uint8_t flags;           /* DATA_FRAG flags of the completing record (0x04 Key: dispose by key) */
   uint8_t status;          /* rtps_frag_status */
-  uint16_t _r;
+  uint16_t reader_slot;    /* the reader whose assembler completed it; RTPS_NO_MATCH (no readers set):
+                              every reader of the completing record's target set */
   uint32_t _r2;
 } rtps_frag_sample;
 enum rtps_frag_status {
@@ -554,6 +566,14 @@ int rtps_rx_frag_reset(rtps_rx_ctx* ctx);
  * buffer, as in the reference. */
 int rtps_rx_frag_set_clock(rtps_rx_ctx* ctx, uint64_t now_ns);
 int rtps_rx_frag_gc(rtps_rx_ctx* ctx, uint64_t expire_before_ns, uint64_t* n_pending);
+/* Lifespan QoS of a reader (by reader_slot) for the DataFrag assembly: a DATA_FRAG
+ * whose source timestamp is older than the receive time by more than the lifespan
+ * is dropped for that reader (reader.rs:578-589, Duration/Timestamp tick arithmetic,
+ * structure/time.rs:85-113).  lifespan_ns < 0: none (the default). */
+int rtps_rx_set_reader_lifespan(rtps_rx_ctx* ctx, uint16_t reader_slot, int64_t lifespan_ns);
+/* The receive time (Timestamp::now(), ns since the UNIX epoch) the next batches'
+ * Lifespan checks use; 0 (the default): the host's clock at each assemble call. */
+int rtps_rx_frag_set_receive_time(rtps_rx_ctx* ctx, uint64_t unix_ns);
 
 /* ---- history-cache ingest ---------------------------
  * Replaces, for every target reader of every routed writer submessage, the
@@ -582,6 +602,9 @@ int rtps_rx_frag_gc(rtps_rx_ctx* ctx, uint64_t expire_before_ns, uint64_t* n_pen
  *     reader (process_received_data, reader.rs:693-733);
  *   - a sample without a proxy enters iff the writer's entity kind is not
  *     user-defined (kind & 0xF0 != 0, reader.rs:734-739; guid.rs:168-170);
+ *   - a completed DataFrag sample goes only to the reader whose assembler
+ *     completed it (rtps_frag_sample.reader_slot; RTPS_NO_MATCH: every reader of
+ *     the record's target set); at most 64 readers per target set take such samples;
  *   - HEARTBEAT / GAP without a proxy, HEARTBEAT for a BestEffort reader: no
  *     effect (reader.rs:871-891, 1071-1086).
  * Every accepted (record, reader) pair is one delivery.  State per proxy

@@ -59,6 +59,9 @@ def lib():
         L.rtps_oracle_frag_gc.argtypes = [P, ctypes.c_uint64]
         L.rtps_oracle_frag_batch.restype = ctypes.c_uint64
         L.rtps_oracle_frag_batch.argtypes = [P, P, P, P, ctypes.c_uint64, P, ctypes.c_uint64, P, ctypes.c_uint64, P]
+        L.rtps_oracle_frag_batch_readers.restype = ctypes.c_uint64
+        L.rtps_oracle_frag_batch_readers.argtypes = [P, P, P, P, ctypes.c_uint64, P, P, P, ctypes.c_uint64, P,
+                                                     ctypes.c_uint64, P, ctypes.c_uint64, P]
         L.rtps_oracle_ingest_new.restype = P
         L.rtps_oracle_ingest_new.argtypes = [P, ctypes.c_uint32, P, ctypes.c_uint32]
         L.rtps_oracle_ingest_free.argtypes = [P]
@@ -201,6 +204,43 @@ class FragAssembler:
         n = lib().rtps_oracle_frag_batch(self.h, _ptr(arena), _ptr(offs), _ptr(recs) if len(recs) else None,
                                          len(recs), _ptr(samples), ms, _ptr(heap), hb, ctypes.byref(used))
         return samples[:min(n, ms)], heap[:min(used.value, hb)], int(n), int(used.value)
+
+    def batch_readers(self, arena, offs, recs, readers, lifespan_ns=None, recv_ns=0, max_samples=None,
+                      heap_bytes=None):
+        """With readers: one assembler per (reader, writer), each target reader fed in turn,
+        Lifespans {reader_slot: ns} checked against the receive time recv_ns
+        (rtps_oracle_frag_batch_readers) -> as batch()."""
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        recs = np.ascontiguousarray(recs, dtype=RECORD_DTYPE)
+        toff, tent = targets(recs, readers)
+        tent = np.ascontiguousarray(tent) if len(tent) else np.zeros(1, dtype=TARGET_DTYPE)
+        life = None
+        if lifespan_ns:
+            life = np.full(65536, np.iinfo(np.int64).max, dtype=np.int64)
+            for slot, ns in lifespan_ns.items():
+                life[slot] = duration_ticks(ns)
+        ms = max(len(recs) * max(_widest(as_readers(readers)), 1), 1) if max_samples is None else max_samples
+        hb = (int(arena.nbytes) * 4 + 16 * ms + (1 << 22)) if heap_bytes is None else heap_bytes
+        samples = np.zeros(max(ms, 1), dtype=FRAG_SAMPLE_DTYPE)
+        heap = np.zeros(max(hb, 1), dtype=np.uint8)
+        used = ctypes.c_uint64()
+        n = lib().rtps_oracle_frag_batch_readers(self.h, _ptr(arena), _ptr(offs), _ptr(recs) if len(recs) else None,
+                                                 len(recs), _ptr(toff), _ptr(tent), _ptr(life),
+                                                 timestamp_ticks(recv_ns), _ptr(samples), ms, _ptr(heap), hb,
+                                                 ctypes.byref(used))
+        return samples[:min(n, ms)], heap[:min(used.value, hb)], int(n), int(used.value)
+
+
+def timestamp_ticks(unix_ns):
+    """Timestamp::from_nanos (structure/time.rs:78-83) as ticks (seconds << 32 | fraction)."""
+    return ((unix_ns // 10**9) << 32) + (((unix_ns % 10**9) << 32) // 10**9)
+
+
+def duration_ticks(ns):
+    """Duration::from_nanos (structure/duration.rs:60-67) as ticks (i64)."""
+    sec, frac = int(ns) // 10**9, ((int(ns) % 10**9) << 32) // 10**9
+    return (sec << 32) + frac
 
 
 class HistoryIngest:

@@ -931,9 +931,14 @@ void rtps_oracle_cdr_decode(const rtps_cdr_op* prog, uint32_t n_ops, uint32_t ro
 /*   driven by Reader::handle_datafrag_msg io_uring/rtps/reader.rs:563-647    */
 /* Sequential restatement with state kept across batches.                    */
 /* ------------------------------------------------------------------------ */
-typedef struct fa_writer { uint8_t guid[16]; uint16_t frag_size; int used; } fa_writer;
+/* Assemblers are keyed by (writer GUID, reader word): one FragmentAssembler per
+ * writer of each Reader (reader.rs:617-619, 638-647).  The reader word is 0 in the
+ * reader-less form (rtps_oracle_frag_batch: one assembler per writer) and
+ * slot | 0x10000 in rtps_oracle_frag_batch_readers. */
+#define FA_KEY 20
+typedef struct fa_writer { uint8_t guid[FA_KEY]; uint16_t frag_size; int used; } fa_writer;
 typedef struct fa_buf {      /* AssemblyBuffer (:23-33) */
-  uint8_t guid[16];
+  uint8_t guid[FA_KEY];
   int64_t sn;
   uint32_t data_size, count, nset;
   uint8_t* bytes;            /* buffer_bytes, zero-initialised (:49-50) */
@@ -952,36 +957,38 @@ static uint64_t fa_hash(const uint8_t* k, size_t n) {
   for (size_t i = 0; i < n; ++i) { h ^= k[i]; h *= 1099511628211ull; }
   return h ^ (h >> 29);
 }
-static fa_writer* fa_writer_get(rtps_oracle_frag* f, const uint8_t guid[16], int create) {
+static fa_writer* fa_writer_get(rtps_oracle_frag* f, const uint8_t guid[FA_KEY], int create) {
   if (create && (f->wn + 1) * 2 > f->wcap) {
     size_t ncap = f->wcap ? f->wcap * 2 : 64;
     fa_writer* nw = (fa_writer*)calloc(ncap, sizeof(fa_writer));
     for (size_t i = 0; i < f->wcap; ++i)
       if (f->w[i].used) {
-        size_t j = fa_hash(f->w[i].guid, 16) & (ncap - 1);
+        size_t j = fa_hash(f->w[i].guid, FA_KEY) & (ncap - 1);
         while (nw[j].used) j = (j + 1) & (ncap - 1);
         nw[j] = f->w[i];
       }
     free(f->w); f->w = nw; f->wcap = ncap;
   }
   if (!f->wcap) return NULL;
-  size_t j = fa_hash(guid, 16) & (f->wcap - 1);
+  size_t j = fa_hash(guid, FA_KEY) & (f->wcap - 1);
   while (f->w[j].used) {
-    if (!memcmp(f->w[j].guid, guid, 16)) return &f->w[j];
+    if (!memcmp(f->w[j].guid, guid, FA_KEY)) return &f->w[j];
     j = (j + 1) & (f->wcap - 1);
   }
   if (!create) return NULL;
-  f->w[j].used = 1; memcpy(f->w[j].guid, guid, 16); f->wn++;
+  f->w[j].used = 1; memcpy(f->w[j].guid, guid, FA_KEY); f->wn++;
   return &f->w[j];
 }
-static void fa_key(uint8_t k[24], const uint8_t guid[16], int64_t sn) { memcpy(k, guid, 16); memcpy(k + 16, &sn, 8); }
-static fa_buf* fa_buf_find(rtps_oracle_frag* f, const uint8_t guid[16], int64_t sn, size_t* slot) {
+static void fa_key(uint8_t k[FA_KEY + 8], const uint8_t guid[FA_KEY], int64_t sn) {
+  memcpy(k, guid, FA_KEY); memcpy(k + FA_KEY, &sn, 8);
+}
+static fa_buf* fa_buf_find(rtps_oracle_frag* f, const uint8_t guid[FA_KEY], int64_t sn, size_t* slot) {
   if (!f->bcap) return NULL;
-  uint8_t k[24];
+  uint8_t k[FA_KEY + 8];
   fa_key(k, guid, sn);
-  size_t j = fa_hash(k, 24) & (f->bcap - 1);
+  size_t j = fa_hash(k, FA_KEY + 8) & (f->bcap - 1);
   while (f->b[j].used) {
-    if (f->b[j].used == 1 && f->b[j].sn == sn && !memcmp(f->b[j].guid, guid, 16)) { if (slot) *slot = j; return &f->b[j]; }
+    if (f->b[j].used == 1 && f->b[j].sn == sn && !memcmp(f->b[j].guid, guid, FA_KEY)) { if (slot) *slot = j; return &f->b[j]; }
     j = (j + 1) & (f->bcap - 1);
   }
   return NULL;
@@ -990,22 +997,22 @@ static void fa_buf_rehash(rtps_oracle_frag* f, size_t ncap) {
   fa_buf* nb = (fa_buf*)calloc(ncap, sizeof(fa_buf));
   for (size_t i = 0; i < f->bcap; ++i)
     if (f->b[i].used == 1) {
-      uint8_t k[24];
+      uint8_t k[FA_KEY + 8];
       fa_key(k, f->b[i].guid, f->b[i].sn);
-      size_t j = fa_hash(k, 24) & (ncap - 1);
+      size_t j = fa_hash(k, FA_KEY + 8) & (ncap - 1);
       while (nb[j].used) j = (j + 1) & (ncap - 1);
       nb[j] = f->b[i];
     }
   free(f->b); f->b = nb; f->bcap = ncap;
 }
-static fa_buf* fa_buf_new(rtps_oracle_frag* f, const uint8_t guid[16], int64_t sn) {
+static fa_buf* fa_buf_new(rtps_oracle_frag* f, const uint8_t guid[FA_KEY], int64_t sn) {
   if ((f->bn + 1) * 2 > f->bcap) fa_buf_rehash(f, f->bcap ? f->bcap * 2 : 64);
-  uint8_t k[24];
+  uint8_t k[FA_KEY + 8];
   fa_key(k, guid, sn);
-  size_t j = fa_hash(k, 24) & (f->bcap - 1);
+  size_t j = fa_hash(k, FA_KEY + 8) & (f->bcap - 1);
   while (f->b[j].used == 1) j = (j + 1) & (f->bcap - 1);
   memset(&f->b[j], 0, sizeof(fa_buf));
-  f->b[j].used = 1; memcpy(f->b[j].guid, guid, 16); f->b[j].sn = sn; f->bn++;
+  f->b[j].used = 1; memcpy(f->b[j].guid, guid, FA_KEY); f->b[j].sn = sn; f->bn++;
   return &f->b[j];
 }
 static void fa_buf_drop(rtps_oracle_frag* f, fa_buf* b) {
@@ -1038,9 +1045,66 @@ uint64_t rtps_oracle_frag_gc(rtps_oracle_frag* f, uint64_t expire_before_ns) {
   return f->bn;
 }
 
-/* One batch: every RTPS_DATA_FRAG record with ROUTE_PASS, in record order.
- * Returns the number of completed samples (descriptors beyond max_samples and
- * bytes beyond heap_bytes are not written, as in rtps_rx_frag_assemble). */
+/* Reader::handle_datafrag_msg's assembler step for one DATA_FRAG record and one
+ * assembler key (writer GUID || reader word): FragmentAssembler::new on first use
+ * (fragment size of that first DATA_FRAG), AssemblyBuffer::new / insert_frags /
+ * is_complete (fragment_assembler.rs:35-214).  A completed buffer becomes a sample
+ * (descriptors beyond max_samples and bytes beyond heap_bytes are not written). */
+static void fa_insert(rtps_oracle_frag* f, const uint8_t key[FA_KEY], const rtps_record* rec, uint64_t r,
+                      uint16_t reader_slot, const uint8_t* arena, const uint64_t* off, rtps_frag_sample* samples,
+                      uint64_t max_samples, uint8_t* heap, uint64_t heap_bytes, uint64_t* ns, uint64_t* used) {
+  /* Reader::fragment_assembler_mutable: or_insert_with(FragmentAssembler::new(datafrag.fragment_size)) */
+  fa_writer* w = fa_writer_get(f, key, 0);
+  if (!w) { w = fa_writer_get(f, key, 1); w->frag_size = rec->u.frag.frag_size; }
+  const uint32_t F = w->frag_size;
+  /* assembly_buffers.entry(writer_sn).or_insert_with(|| AssemblyBuffer::new(datafrag)) */
+  fa_buf* b = fa_buf_find(f, key, rec->sn, NULL);
+  if (!b) {
+    b = fa_buf_new(f, key, rec->sn);
+    const uint32_t ds = rec->u.frag.data_size, fs = rec->u.frag.frag_size;  /* 1 <= fs <= ds (parse) */
+    b->data_size = ds;
+    b->count = ds / fs + (ds % fs > 0);  /* total_number_of_fragments, data_frag.rs:97-119 */
+    b->bytes = (uint8_t*)calloc(ds ? ds : 1, 1);
+    b->bits = (uint8_t*)calloc(b->count ? b->count : 1, 1);
+  }
+  b->modified = f->now;  /* AssemblyBuffer::new (:54-61) / insert_frags (:139) */
+  /* insert_frags (:65-140) with frag_size = the assembler's F */
+  const uint64_t start0 = (uint64_t)rec->u.frag.frag_start - 1;
+  const uint64_t fis = rec->u.frag.frags_in_sub;
+  const uint64_t pl_len = rec->u.frag.pl_len;
+  const uint64_t from = start0 * F;
+  uint64_t to = from + (fis * F < pl_len ? fis * F : pl_len);
+  if (to > b->data_size) to = b->data_size;
+  if (to > from)  /* reference: to < from panics (usize underflow); clamped to nothing here */
+    memcpy(b->bytes + from, arena + off[rec->dgram_idx] + rec->u.frag.pl_off, (size_t)(to - from));
+  for (uint64_t k = 0; k < fis; ++k) {
+    const uint64_t bit = start0 + k;
+    if (bit >= b->count) break;  /* reference: BitVec::set panics; ignored here */
+    if (!b->bits[bit]) { b->bits[bit] = 1; b->nset++; }
+  }
+  if (b->nset == b->count) {  /* is_complete -> remove, SerializedPayload::from_bytes */
+    if (*ns < max_samples) {
+      rtps_frag_sample* sm = &samples[*ns];
+      memset(sm, 0, sizeof(*sm));
+      memcpy(sm->writer_guid, key, 16);
+      sm->sn = rec->sn;
+      sm->data_size = b->data_size;
+      sm->rec_idx = (uint32_t)r;
+      sm->flags = rec->flags;
+      sm->reader_slot = reader_slot;
+      sm->heap_off = *used;
+      sm->status = b->data_size < 4 ? RTPS_FRAG_SHORT : RTPS_FRAG_OK;
+      if (*used + b->data_size <= heap_bytes) memcpy(heap + *used, b->bytes, b->data_size);
+      else sm->status = RTPS_FRAG_NO_ROOM;
+    }
+    *used += ((uint64_t)b->data_size + 15) & ~15ull;
+    (*ns)++;
+    fa_buf_drop(f, b);
+  }
+}
+
+/* One batch without readers: every RTPS_DATA_FRAG record with ROUTE_PASS, in record
+ * order, one assembler per writer (reader word 0).  Returns the completed samples. */
 uint64_t rtps_oracle_frag_batch(rtps_oracle_frag* f, const uint8_t* arena, const uint64_t* off,
                                 const rtps_record* recs, uint64_t n_recs, rtps_frag_sample* samples,
                                 uint64_t max_samples, uint8_t* heap, uint64_t heap_bytes, uint64_t* heap_used) {
@@ -1048,55 +1112,47 @@ uint64_t rtps_oracle_frag_batch(rtps_oracle_frag* f, const uint8_t* arena, const
   for (uint64_t r = 0; r < n_recs; ++r) {
     const rtps_record* rec = &recs[r];
     if (rec->kind != RTPS_DATA_FRAG || !(rec->route & RTPS_ROUTE_PASS)) continue;
-    uint8_t guid[16];
-    memcpy(guid, rec->prefix, 12);
-    memcpy(guid + 12, rec->writer_id, 4);
-    /* Reader::fragment_assembler_mutable: or_insert_with(FragmentAssembler::new(datafrag.fragment_size)) */
-    fa_writer* w = fa_writer_get(f, guid, 0);
-    if (!w) { w = fa_writer_get(f, guid, 1); w->frag_size = rec->u.frag.frag_size; }
-    const uint32_t F = w->frag_size;
-    /* assembly_buffers.entry(writer_sn).or_insert_with(|| AssemblyBuffer::new(datafrag)) */
-    fa_buf* b = fa_buf_find(f, guid, rec->sn, NULL);
-    if (!b) {
-      b = fa_buf_new(f, guid, rec->sn);
-      const uint32_t ds = rec->u.frag.data_size, fs = rec->u.frag.frag_size;  /* 1 <= fs <= ds (parse) */
-      b->data_size = ds;
-      b->count = ds / fs + (ds % fs > 0);  /* total_number_of_fragments, data_frag.rs:97-119 */
-      b->bytes = (uint8_t*)calloc(ds ? ds : 1, 1);
-      b->bits = (uint8_t*)calloc(b->count ? b->count : 1, 1);
-    }
-    b->modified = f->now;  /* AssemblyBuffer::new (:54-61) / insert_frags (:139) */
-    /* insert_frags (:65-140) with frag_size = the assembler's F */
-    const uint64_t start0 = (uint64_t)rec->u.frag.frag_start - 1;
-    const uint64_t fis = rec->u.frag.frags_in_sub;
-    const uint64_t pl_len = rec->u.frag.pl_len;
-    const uint64_t from = start0 * F;
-    uint64_t to = from + (fis * F < pl_len ? fis * F : pl_len);
-    if (to > b->data_size) to = b->data_size;
-    if (to > from)  /* reference: to < from panics (usize underflow); clamped to nothing here */
-      memcpy(b->bytes + from, arena + off[rec->dgram_idx] + rec->u.frag.pl_off, (size_t)(to - from));
-    for (uint64_t k = 0; k < fis; ++k) {
-      const uint64_t bit = start0 + k;
-      if (bit >= b->count) break;  /* reference: BitVec::set panics; ignored here */
-      if (!b->bits[bit]) { b->bits[bit] = 1; b->nset++; }
-    }
-    if (b->nset == b->count) {  /* is_complete -> remove, SerializedPayload::from_bytes */
-      if (ns < max_samples) {
-        rtps_frag_sample* s = &samples[ns];
-        memset(s, 0, sizeof(*s));
-        memcpy(s->writer_guid, guid, 16);
-        s->sn = rec->sn;
-        s->data_size = b->data_size;
-        s->rec_idx = (uint32_t)r;
-        s->flags = rec->flags;
-        s->heap_off = used;
-        s->status = b->data_size < 4 ? RTPS_FRAG_SHORT : RTPS_FRAG_OK;
-        if (used + b->data_size <= heap_bytes) memcpy(heap + used, b->bytes, b->data_size);
-        else s->status = RTPS_FRAG_NO_ROOM;
+    uint8_t key[FA_KEY];
+    memcpy(key, rec->prefix, 12);
+    memcpy(key + 12, rec->writer_id, 4);
+    memset(key + 16, 0, 4);
+    fa_insert(f, key, rec, r, RTPS_NO_MATCH, arena, off, samples, max_samples, heap, heap_bytes, &ns, &used);
+  }
+  if (heap_used) *heap_used = used;
+  return ns;
+}
+
+/* One batch with readers: Domain::handle_event hands each DATA_FRAG the receiver passes
+ * to user readers (not a builtin pair) to every reader of its target set in turn
+ * (dp_event_loop.rs:266-327; toff / tent = rtps_oracle_targets), and each reader's
+ * handle_datafrag_msg (io_uring/rtps/reader.rs:563-636) first drops it when its
+ * Lifespan has expired for the source timestamp (:578-589: lifespan.duration <
+ * receive_timestamp.duration_since(source), Timestamp ticks wrapping-subtracted as
+ * an i64 Duration, structure/time.rs:103-113), then feeds its own assembler for the
+ * writer (:617-619, 638-647).  life: the Lifespan of each reader slot in Duration
+ * ticks ([65536], INT64_MAX: none; NULL: none at all); recv_ticks: the batch's
+ * Timestamp::now() as ticks.  Samples in completing order, each with its reader. */
+uint64_t rtps_oracle_frag_batch_readers(rtps_oracle_frag* f, const uint8_t* arena, const uint64_t* off,
+                                        const rtps_record* recs, uint64_t n_recs, const uint64_t* toff,
+                                        const rtps_target* tent, const int64_t* life, uint64_t recv_ticks,
+                                        rtps_frag_sample* samples, uint64_t max_samples, uint8_t* heap,
+                                        uint64_t heap_bytes, uint64_t* heap_used) {
+  uint64_t ns = 0, used = 0;
+  for (uint64_t r = 0; r < n_recs; ++r) {
+    const rtps_record* rec = &recs[r];
+    if (rec->kind != RTPS_DATA_FRAG || !(rec->route & RTPS_ROUTE_PASS) || (rec->route & RTPS_ROUTE_BUILTIN)) continue;
+    for (uint64_t k = toff[r]; k < toff[r + 1]; ++k) {
+      const uint16_t slot = tent[k].reader_slot;
+      if (life && life[slot] != INT64_MAX && (rec->route & RTPS_ROUTE_TS_VALID)) {
+        const uint64_t src = ((uint64_t)rec->ts_sec << 32) | rec->ts_frac;
+        if (life[slot] < (int64_t)(recv_ticks - src)) continue;  /* lifespan exceeded: return */
       }
-      used += ((uint64_t)b->data_size + 15) & ~15ull;
-      ns++;
-      fa_buf_drop(f, b);
+      uint8_t key[FA_KEY];
+      memcpy(key, rec->prefix, 12);
+      memcpy(key + 12, rec->writer_id, 4);
+      const uint32_t word = (uint32_t)slot | 0x10000u;
+      memcpy(key + 16, &word, 4);
+      fa_insert(f, key, rec, r, slot, arena, off, samples, max_samples, heap, heap_bytes, &ns, &used);
     }
   }
   if (heap_used) *heap_used = used;
@@ -1234,9 +1290,12 @@ uint64_t rtps_oracle_ingest_batch(rtps_oracle_ingest* h, const uint8_t* arena, c
                                   const rtps_record* recs, uint64_t m, const rtps_frag_sample* frag, uint64_t nf,
                                   uint32_t flags, uint8_t* accept, rtps_delivery* del, uint64_t max_del,
                                   int64_t* ack_base) {
+  /* the first completed sample of each record: the samples of one record are consecutive
+   * (completing order), one per reader whose assembler completed it (or RTPS_NO_MATCH:
+   * every reader of the record) */
   uint32_t* fidx = (uint32_t*)malloc((m ? m : 1) * sizeof(uint32_t));
   for (uint64_t i = 0; i < m; ++i) fidx[i] = 0xffffffffu;
-  for (uint64_t s = 0; s < nf; ++s)
+  for (uint64_t s = nf; s-- > 0;)
     if (frag[s].rec_idx < m) fidx[frag[s].rec_idx] = (uint32_t)s;
   uint64_t nd = 0;
   for (uint64_t i = 0; i < m; ++i) {
@@ -1255,8 +1314,10 @@ uint64_t rtps_oracle_ingest_batch(rtps_oracle_ingest* h, const uint8_t* arena, c
       ig_proxy* p = t->proxy != RTPS_NO_PROXY ? &h->p[t->proxy] : NULL;
       int acc = 0;
       if (fidx[i] != 0xffffffffu) {  /* completed DataFrag sample (handle_datafrag_msg :614-626) */
-        const rtps_frag_sample* fs = &frag[fidx[i]];
-        if (fs->status != RTPS_FRAG_SHORT) acc = ig_process_sample(h, t, r->writer_id, fs->sn);
+        const rtps_frag_sample* fs = NULL;  /* this reader's, or a writer-keyed one */
+        for (uint64_t s = fidx[i]; s < nf && frag[s].rec_idx == i && !fs; ++s)
+          if (frag[s].reader_slot == RTPS_NO_MATCH || frag[s].reader_slot == t->reader_slot) fs = &frag[s];
+        if (fs && fs->status != RTPS_FRAG_SHORT) acc = ig_process_sample(h, t, r->writer_id, fs->sn);
       } else if (r->kind == RTPS_DATA) {
         if (r->payload_kind != RTPS_PK_DATA && r->payload_kind != RTPS_PK_KEY && r->payload_kind != RTPS_PK_KEY_HASH)
           continue;  /* data_to_dds_data failed: no process_received_data (reader.rs:552-558) */

@@ -14,10 +14,13 @@ FragState* rtps_frag_state_new(int device);
 void rtps_frag_state_free(FragState* s);
 // Drops writers and pending buffers (asynchronous on `stream`).
 int rtps_frag_state_reset(FragState* s, hipStream_t stream);
-// One batch (asynchronous on `stream`); returns an rtps_rx_status code.
+// One batch (asynchronous on `stream`); returns an rtps_rx_status code.  rmask: the
+// reader word of the assembly keys (record bytes 24..28 & rmask; 0 = one assembler
+// per writer).  emap (optional): position -> record of the parse, for an expanded
+// batch (the samples' rec_idx go through it).
 int rtps_frag_assemble(FragState* s, hipStream_t stream, const uint8_t* arena, uint64_t arena_len,
                        const uint64_t* dgram_off, const rtps_record* records, const uint64_t* n_records,
-                       uint64_t max_records, const rtps_frag_out* out);
+                       uint64_t max_records, const rtps_frag_out* out, uint32_t rmask, const uint32_t* emap);
 // The clock stamped on buffers the next batches create or extend.
 void rtps_frag_set_clock(FragState* s, uint64_t now);
 void rtps_frag_set_sort(FragState* s, int mode);  // tests: 1 = rocprim device sort always

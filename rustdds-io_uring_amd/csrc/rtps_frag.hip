@@ -47,6 +47,14 @@ constexpr uint32_t FT = 256;             // threads per block
 constexpr uint32_t NONE = 0xffffffffu;
 constexpr uint32_t SENT = 0xffffffffu;   // sort key of records that are not assembled
 constexpr uint32_t FIXED = 0x80000000u;  // writer table: fragment size resolved
+// Assembly keys are five words: the writer GUID (prefix || writer_id, record
+// bytes 8..24) and a reader word (record bytes 24..28, ANDed with the batch's
+// rmask).  Without readers rmask is 0: one assembler per writer.  With readers
+// the batch is an expansion with one copy of a DATA_FRAG record per target
+// reader whose reader_id field holds that reader (rtps_rx.hip frag_expand), so
+// every (reader, writer) pair has its own assembler, as every Reader has its own
+// FragmentAssembler per writer (io_uring/rtps/reader.rs:617-619, 638-647).
+constexpr int KW = 5;
 
 constexpr uint32_t WCAP = 1u << 16;      // writers
 constexpr uint32_t PCAP = 1u << 16;      // pending buffers
@@ -61,7 +69,7 @@ enum EpochState : uint32_t { E_PENDING = 0, E_DONE = 1, E_DEAD = 2 };  // DEAD: 
 enum EpochFlags : uint32_t { EF_IRREGULAR = 1, EF_SKIP = 2 };  // SKIP: no bytes to write (no room)
 
 struct Epoch {
-  uint32_t guid[4];
+  uint32_t guid[KW];
   int64_t sn;
   uint32_t data_size, count, nset, F;
   uint32_t state, eflags;
@@ -75,7 +83,7 @@ struct Epoch {
 };
 
 struct Pend {
-  uint32_t guid[4];
+  uint32_t guid[KW];
   int64_t sn;
   uint32_t data_size, count, nset, consumed;  // consumed: continued by this batch, or expired by gc
   uint64_t bytes;     // offset in the pending byte store
@@ -83,28 +91,29 @@ struct Pend {
   uint64_t modified;  // clock of the last batch that inserted fragments (AssemblyBuffer::modified_time)
 };
 
-__device__ __forceinline__ void guid_of(const rtps_record* r, uint32_t g[4]) {
+__device__ __forceinline__ void guid_of(const rtps_record* r, uint32_t g[KW], uint32_t rmask) {
   const uint4 v = *(const uint4*)((const uint8_t*)r + 8);  // prefix[12] @8, writer_id @20
   g[0] = v.x; g[1] = v.y; g[2] = v.z; g[3] = v.w;
+  g[4] = *(const uint32_t*)((const uint8_t*)r + 24) & rmask;  // reader_id @24: the reader word
 }
 __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
   h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
   return h;
 }
-__device__ __forceinline__ uint32_t key_hash(const uint32_t g[4], int64_t sn) {
+__device__ __forceinline__ uint32_t key_hash(const uint32_t g[KW], int64_t sn) {
   uint32_t h = 0x811c9dc5u;
   h = (h ^ g[0]) * 0x01000193u; h = (h ^ g[1]) * 0x01000193u; h = (h ^ g[2]) * 0x01000193u;
-  h = (h ^ g[3]) * 0x01000193u; h = (h ^ (uint32_t)sn) * 0x01000193u; h = (h ^ (uint32_t)(sn >> 32)) * 0x01000193u;
+  h = (h ^ g[3]) * 0x01000193u; h = (h ^ g[4]) * 0x01000193u; h = (h ^ (uint32_t)sn) * 0x01000193u; h = (h ^ (uint32_t)(sn >> 32)) * 0x01000193u;
   h = fmix32(h);
   return h == SENT ? SENT - 1 : h;
 }
-__device__ __forceinline__ uint64_t writer_hash(const uint32_t g[4]) {
+__device__ __forceinline__ uint64_t writer_hash(const uint32_t g[KW]) {
   uint32_t a = 0x811c9dc5u, b = 0x9e3779b9u;
-  for (int k = 0; k < 4; ++k) { a = (a ^ g[k]) * 0x01000193u; b = fmix32(b ^ g[k]) + 0x7f4a7c15u; }
+  for (int k = 0; k < KW; ++k) { a = (a ^ g[k]) * 0x01000193u; b = fmix32(b ^ g[k]) + 0x7f4a7c15u; }
   return (((uint64_t)fmix32(a) << 32) | fmix32(b)) | 1ull;
 }
-__device__ __forceinline__ bool same_key(const uint32_t a[4], int64_t asn, const uint32_t b[4], int64_t bsn) {
-  return a[0] == b[0] && a[1] == b[1] && a[2] == b[2] && a[3] == b[3] && asn == bsn;
+__device__ __forceinline__ bool same_key(const uint32_t a[KW], int64_t asn, const uint32_t b[KW], int64_t bsn) {
+  return a[0] == b[0] && a[1] == b[1] && a[2] == b[2] && a[3] == b[3] && a[4] == b[4] && asn == bsn;
 }
 // workgroup-wide copy / zero fill of n bytes, 16 B per thread where possible
 __device__ __forceinline__ void blk_copy(uint8_t* d, const uint8_t* s, uint64_t n) {
@@ -167,7 +176,7 @@ __global__ __launch_bounds__(FT) void k_keys(const rtps_record* recs, const uint
                                              uint32_t* keys, uint32_t* vals, uint32_t* rec_epoch, uint32_t* dmark,
                                              uint8_t* seen, uint64_t* ctr, uint32_t* new_ptable, uint64_t* wkey,
                                              uint32_t* wfirst, const uint32_t* wF, uint64_t* wst_key,
-                                             uint32_t* wst_rec) {
+                                             uint32_t* wst_rec, uint32_t rmask) {
   __shared__ unsigned long long s_wk[KW_SLOTS];
   __shared__ uint32_t s_wr[KW_SLOTS];
   __shared__ uint32_t s_nst;
@@ -206,7 +215,7 @@ __global__ __launch_bounds__(FT) void k_keys(const rtps_record* recs, const uint
         uint32_t k = SENT;
         const uint32_t kind = (ra[kk].y >> 16) & 0xffu, route = (rb[kk].w >> 16) & 0xffu;
         if (i < n && kind == RTPS_DATA_FRAG && (route & RTPS_ROUTE_PASS)) {  // is_frag
-          const uint32_t g[4] = {ra[kk].z, ra[kk].w, rb[kk].x, rb[kk].y};  // guid_of
+          const uint32_t g[KW] = {ra[kk].z, ra[kk].w, rb[kk].x, rb[kk].y, rb[kk].z & rmask};  // guid_of
           k = key_hash(g, (int64_t)rs[kk]);
           wh = writer_hash(g);
           f = true;
@@ -323,7 +332,7 @@ struct WregSide {
 };
 
 // ---- 3: walk ----
-__device__ uint32_t pend_lookup(const uint32_t* ptable, const Pend* pend, uint32_t kh, const uint32_t g[4],
+__device__ uint32_t pend_lookup(const uint32_t* ptable, const Pend* pend, uint32_t kh, const uint32_t g[KW],
                                 int64_t sn) {
   uint32_t s = kh & (PTCAP - 1);
   for (uint32_t i = 0; i < PTCAP; ++i, s = (s + 1) & (PTCAP - 1)) {
@@ -353,6 +362,7 @@ struct WalkArgs {
   uint32_t* dmark;
   uint8_t* seen;  // per position: consumed by a walk pass (collision runs)
   uint64_t* ctr;
+  uint32_t rmask;  // reader word mask of the assembly keys (0: one assembler per writer)
 };
 
 // FragmentAssembler's fragment size of writer slot ws: fixed in an earlier batch, or
@@ -367,11 +377,11 @@ __device__ __forceinline__ uint32_t writer_F(const WalkArgs& A, uint32_t ws) {
 
 // Epoch ids are the sorted position where the epoch starts (its first record,
 // or the run's first position for a buffer carried over): distinct, no counter.
-__device__ uint32_t new_epoch(const WalkArgs& A, const uint32_t g[4], int64_t sn, uint32_t start, uint32_t p0,
+__device__ uint32_t new_epoch(const WalkArgs& A, const uint32_t g[KW], int64_t sn, uint32_t start, uint32_t p0,
                               uint32_t p1) {
   const uint32_t e = start;
   Epoch& E = A.epochs[e];
-  for (int k = 0; k < 4; ++k) E.guid[k] = g[k];
+  for (int k = 0; k < KW; ++k) E.guid[k] = g[k];
   E.sn = sn; E.state = E_PENDING; E.eflags = 0; E.done_rec = NONE; E.old_pend = NONE; E.new_pend = NONE;
   E.p0 = p0; E.p1 = p1; E.nset = 0; E.rec_flags = 0; E.dst = 0; E.bits = 0;
   return e;
@@ -403,9 +413,9 @@ __device__ void walk_run_serial(const WalkArgs& A, uint64_t p, uint64_t p1) {
   // one pass per distinct full key of the run (more than one only on a hash collision)
   for (uint64_t q0 = p; q0 < p1; ++q0) {
     if (A.seen[q0]) continue;
-    uint32_t g[4];
+    uint32_t g[KW];
     const rtps_record* r0 = A.recs + A.svals[q0];
-    guid_of(r0, g);
+    guid_of(r0, g, A.rmask);
     const int64_t sn = r0->sn;
     const uint64_t wh = writer_hash(g);
     const uint32_t ws = wslot_find(A.wkey, wh);
@@ -432,8 +442,8 @@ __device__ void walk_run_serial(const WalkArgs& A, uint64_t p, uint64_t p1) {
       if (A.seen[q]) continue;
       const uint32_t ri = A.svals[q];
       const rtps_record* r = A.recs + ri;
-      uint32_t h[4];
-      guid_of(r, h);
+      uint32_t h[KW];
+      guid_of(r, h, A.rmask);
       if (!same_key(g, sn, h, r->sn)) continue;
       A.seen[q] = 1;
       const uint32_t ds = r->u.frag.data_size, fsz = r->u.frag.frag_size;
@@ -490,17 +500,17 @@ constexpr uint32_t BMW = 1024;  // LDS bitmap words per wave: buffers of up to 3
 // one lane's record of a short run (position p0 + lane), loaded once
 struct LaneRec {
   bool act;
-  uint32_t ri, g[4], fs, fis, fsz, dsz, fl;
+  uint32_t ri, g[KW], fs, fis, fsz, dsz, fl;
   int64_t sn;
 };
 __device__ __forceinline__ LaneRec lane_rec(const WalkArgs& A, uint64_t p, uint64_t p1) {
   LaneRec L;
   L.act = p < p1;
-  L.ri = 0; L.g[0] = L.g[1] = L.g[2] = L.g[3] = 0; L.fs = 1; L.fis = 1; L.fsz = 0; L.dsz = 0; L.fl = 0; L.sn = 0;
+  L.ri = 0; L.g[0] = L.g[1] = L.g[2] = L.g[3] = L.g[4] = 0; L.fs = 1; L.fis = 1; L.fsz = 0; L.dsz = 0; L.fl = 0; L.sn = 0;
   if (L.act) {
     L.ri = A.svals[p];
     const rtps_record* r = A.recs + L.ri;
-    guid_of(r, L.g);
+    guid_of(r, L.g, A.rmask);
     L.sn = r->sn;
     L.fs = r->u.frag.frag_start;
     L.fis = r->u.frag.frags_in_sub;
@@ -511,7 +521,7 @@ __device__ __forceinline__ LaneRec lane_rec(const WalkArgs& A, uint64_t p, uint6
   return L;
 }
 __device__ bool walk_run_regular(const WalkArgs& A, uint64_t p0, uint64_t p1, uint32_t lane, uint32_t* bm,
-                                 const uint32_t g[4], int64_t sn, uint32_t F, const LaneRec& L) {
+                                 const uint32_t g[KW], int64_t sn, uint32_t F, const LaneRec& L) {
   const bool act = L.act;
   const uint32_t ri = L.ri, fs = L.fs, fis = L.fis, fsz = act ? L.fsz : F, dsz = L.dsz, fl = L.fl;
   const uint32_t ds0 = rl(dsz, 0);
@@ -573,8 +583,8 @@ __device__ void walk_run_wave(const WalkArgs& A, uint64_t p0, uint64_t p1, uint3
     // a short run: every lane loads its record once; the run's key, the carried-over
     // buffer and the writer's fragment size are then looked up with independent loads
     const LaneRec L = lane_rec(A, p0 + lane, p1);
-    uint32_t g[4];
-    for (int k = 0; k < 4; ++k) g[k] = rl(L.g[k], 0);
+    uint32_t g[KW];
+    for (int k = 0; k < KW; ++k) g[k] = rl(L.g[k], 0);
     const int64_t sn = (int64_t)(((uint64_t)rl((uint32_t)((uint64_t)L.sn >> 32), 0) << 32) | rl((uint32_t)L.sn, 0));
     const bool bad = L.act && (!same_key(g, sn, L.g, L.sn) ||
                                (uint64_t)(L.dsz / L.fsz + (L.dsz % L.fsz > 0)) > (uint64_t)BMW * 32);
@@ -589,8 +599,8 @@ __device__ void walk_run_wave(const WalkArgs& A, uint64_t p0, uint64_t p1, uint3
     }
   }
   const rtps_record* r0 = A.recs + A.svals[p0];
-  uint32_t g[4];
-  guid_of(r0, g);
+  uint32_t g[KW];
+  guid_of(r0, g, A.rmask);
   const int64_t sn = r0->sn;
   bool ok = true;
   for (uint64_t c = p0; c < p1 && ok; c += 64) {
@@ -598,8 +608,8 @@ __device__ void walk_run_wave(const WalkArgs& A, uint64_t p0, uint64_t p1, uint3
     bool bad = false;
     if (p < p1) {
       const rtps_record* r = A.recs + A.svals[p];
-      uint32_t h[4];
-      guid_of(r, h);
+      uint32_t h[KW];
+      guid_of(r, h, A.rmask);
       const uint32_t ds = r->u.frag.data_size, fsz = r->u.frag.frag_size;
       bad = !same_key(g, sn, h, r->sn) || (uint64_t)(ds / fsz + (ds % fsz > 0)) > (uint64_t)BMW * 32;
     }
@@ -819,7 +829,8 @@ __global__ __launch_bounds__(FT) void k_place_scan(uint32_t* tc, uint64_t* tb, u
 // SELF_SCAN tiles) their raw totals, which each workgroup then sums itself
 constexpr uint64_t SELF_SCAN = 2048;
 __device__ void samples_wg(const uint32_t* dmark, Epoch* ep, const uint32_t* tc, const uint64_t* tb, uint64_t max,
-                           uint32_t self_scan, const rtps_frag_out& out, uint32_t bid, uint32_t ntiles) {
+                           uint32_t self_scan, const rtps_frag_out& out, uint32_t bid, uint32_t ntiles,
+                           const uint32_t* emap) {
   const uint64_t base = (uint64_t)bid * PTILE + (uint64_t)threadIdx.x * PPT;
   uint32_t d[PPT];
   dmark16(dmark, base, max, d);
@@ -863,7 +874,10 @@ __device__ void samples_wg(const uint32_t* dmark, Epoch* ep, const uint32_t* tc,
     s.sn = E.sn;
     s.heap_off = E.dst;
     s.data_size = E.data_size;
-    s.rec_idx = (uint32_t)(base + k);
+    // an expanded batch (one copy per target reader): the copy's record of the parse, and
+    // the reader of the key's reader word (slot | 0x10000); else every reader of the record
+    s.rec_idx = emap ? emap[base + k] : (uint32_t)(base + k);
+    s.reader_slot = E.guid[4] ? (uint16_t)(E.guid[4] & 0xffffu) : (uint16_t)RTPS_NO_MATCH;
     s.flags = (uint8_t)E.rec_flags;
     s.status = E.data_size < 4 ? RTPS_FRAG_SHORT : RTPS_FRAG_OK;
     if (E.dst + E.data_size > out.heap_bytes) { s.status = RTPS_FRAG_NO_ROOM; E.eflags |= EF_SKIP; }
@@ -888,7 +902,7 @@ __device__ void pend_alloc_wg(Epoch* ep, const uint32_t* special, Pend* np, uint
       continue;
     }
     Pend& P = np[j];
-    for (int k = 0; k < 4; ++k) P.guid[k] = E.guid[k];
+    for (int k = 0; k < KW; ++k) P.guid[k] = E.guid[k];
     P.sn = E.sn; P.data_size = E.data_size; P.count = E.count; P.nset = E.nset; P.consumed = 0;
     P.bytes = b; P.bits = w;
     P.modified = now;  // a pending epoch had fragments in this batch (insert_frags :139)
@@ -950,10 +964,11 @@ struct PlaceArgs {
   const uint64_t* wkey;
   uint32_t* wfirst;
   uint32_t* wF;
+  const uint32_t* emap;  // expanded batch: position -> record of the parse (nullptr: none)
 };
 __global__ __launch_bounds__(FT) void k_place(PlaceArgs P, rtps_frag_out out) {
   uint32_t b = blockIdx.x;
-  if (b < P.ntiles) { samples_wg(P.dmark, P.ep, P.tc, P.tb, P.max, P.self_scan, out, b, P.ntiles); return; }
+  if (b < P.ntiles) { samples_wg(P.dmark, P.ep, P.tc, P.tb, P.max, P.self_scan, out, b, P.ntiles, P.emap); return; }
   b -= P.ntiles;
   if (b < PA_WG) { pend_alloc_wg(P.ep, P.special, P.np, P.nbits, P.pool, P.ctr, P.now, b, PA_WG); return; }
   b -= PA_WG;
@@ -1180,7 +1195,7 @@ __device__ void ptable_wg(const Pend* np, uint64_t* ctr, uint32_t* ptable, uint6
     ctr[C_OLD_N] = n;
   }
   for (uint64_t j = (uint64_t)bid * FT + threadIdx.x; j < n; j += (uint64_t)nb * FT) {
-    uint32_t g[4] = {np[j].guid[0], np[j].guid[1], np[j].guid[2], np[j].guid[3]};
+    uint32_t g[KW] = {np[j].guid[0], np[j].guid[1], np[j].guid[2], np[j].guid[3], np[j].guid[4]};
     uint32_t s = key_hash(g, np[j].sn) & (PTCAP - 1);
     while (atomicCAS(&ptable[s], NONE, (uint32_t)j) != NONE) s = (s + 1) & (PTCAP - 1);
   }
@@ -1226,7 +1241,7 @@ __global__ __launch_bounds__(FT) void k_ptable_live(const Pend* op, const uint64
   const uint64_t n = min<uint64_t>(ctr[C_OLD_N], PCAP);
   for (uint64_t j = (uint64_t)blockIdx.x * FT + threadIdx.x; j < n; j += (uint64_t)gridDim.x * FT) {
     if (op[j].consumed) continue;
-    uint32_t g[4] = {op[j].guid[0], op[j].guid[1], op[j].guid[2], op[j].guid[3]};
+    uint32_t g[KW] = {op[j].guid[0], op[j].guid[1], op[j].guid[2], op[j].guid[3], op[j].guid[4]};
     uint32_t s = key_hash(g, op[j].sn) & (PTCAP - 1);
     while (atomicCAS(&ptable[s], NONE, (uint32_t)j) != NONE) s = (s + 1) & (PTCAP - 1);
   }
@@ -1348,7 +1363,7 @@ int rtps_frag_state_reset(FragState* s, hipStream_t st) {
 
 int rtps_frag_assemble(FragState* s, hipStream_t st, const uint8_t* arena, uint64_t arena_len,
                        const uint64_t* dgram_off, const rtps_record* records, const uint64_t* n_records,
-                       uint64_t max_records, const rtps_frag_out* out) {
+                       uint64_t max_records, const rtps_frag_out* out, uint32_t rmask, const uint32_t* emap) {
   if (max_records > 0x7fffffffull) return RTPS_RX_ETOOBIG;
   const uint64_t max = max_records ? max_records : 1;
   if (!grow(s, max, st)) return RTPS_RX_ENOMEM;
@@ -1361,7 +1376,7 @@ int rtps_frag_assemble(FragState* s, hipStream_t st, const uint8_t* arena, uint6
   const bool bsort = s->sort_mode == 0 && max <= rtps_bsort::MAX_N;
   hipLaunchKernelGGL(k_keys, dim3(gk), dim3(FT), 0, st, records, n_records, max, s->keys, bsort ? nullptr : s->vals,
                      s->rec_epoch, s->dmark, s->seen, s->ctr, s->ptable[nw], s->wkey, s->wfirst, s->wF, s->wst_key,
-                     s->wst_rec);
+                     s->wst_rec, rmask);
   size_t tb = s->tmp_bytes;
   const WregSide wreg{WREG_WG, s->wst_key, s->wst_rec, gk * WST, s->wkey, s->wfirst, s->wF, s->ctr};
   if (bsort) {  // the writers' merge rides on the sort's column-scan launch
@@ -1375,7 +1390,7 @@ int rtps_frag_assemble(FragState* s, hipStream_t st, const uint8_t* arena, uint6
                        s->wF, s->ctr);
   }
   WalkArgs A{records, s->skeys, s->svals, max, s->wkey, s->wF, s->wfirst, s->pend[o], s->ptable[o], s->pbits[o], s->epochs,
-             s->special, s->pool, s->pool_words, s->rec_epoch, s->dmark, s->seen, s->ctr};
+             s->special, s->pool, s->pool_words, s->rec_epoch, s->dmark, s->seen, s->ctr, rmask};
   hipLaunchKernelGGL(k_walk, dim3((uint32_t)hmin((max + FT - 1) / FT, 8192)), dim3(FT), 0, st, A);
   const uint64_t tiles = (max + PTILE - 1) / PTILE;
   hipLaunchKernelGGL(k_place_tiles, dim3((uint32_t)tiles), dim3(FT), 0, st, s->dmark, s->epochs, max, s->tcnt,
@@ -1384,7 +1399,7 @@ int rtps_frag_assemble(FragState* s, hipStream_t st, const uint8_t* arena, uint6
   if (!self_scan) hipLaunchKernelGGL(k_place_scan, dim3(1), dim3(FT), 0, st, s->tcnt, s->tbytes, tiles, *out);
   const PlaceArgs P{s->dmark, s->epochs, s->tcnt, s->tbytes, max, self_scan, (uint32_t)tiles, s->special, s->pool,
                     s->now, s->pend[o], s->pbytes[o], s->pbits[o], s->pend[nw], s->pbytes[nw], s->pbits[nw], s->ctr,
-                    records, s->wkey, s->wfirst, s->wF};
+                    records, s->wkey, s->wfirst, s->wF, emap};
   hipLaunchKernelGGL(k_place, dim3((uint32_t)tiles + PA_WG + CARRY_WG + WFIX_WG), dim3(FT), 0, st, P, *out);
   hipLaunchKernelGGL(k_fill, dim3(INIT_WG + SERIAL_WG + PTAB_WG + DESC_WG), dim3(FT), 0, st, records, arena,
                      dgram_off, s->svals, s->rec_epoch, s->epochs, s->special, s->ctr, s->pend[o], s->pbytes[o],

@@ -128,6 +128,7 @@ __device__ __forceinline__ uint32_t rd32(const uint8_t* p, bool le) {
 struct Scratch {
   // per record
   uint32_t* fidx;   // completed DataFrag sample of a record, or NONE
+  uint64_t* fmask;  // the target-set entries (bit k: entry k) whose assembler completed it at the record
   uint32_t* rcnt;   // events of the record (non-identity batches), then their exclusive scan (roff)
   uint32_t* roff;
   uint32_t* rset;   // target set, record event kind, sample / event sn
@@ -158,11 +159,29 @@ struct State {
 };
 
 // ---- 1 classify ----
+// A per-reader sample (reader_slot != RTPS_NO_MATCH) goes to that reader only: its
+// entry of the completing record's target set (handle_datafrag_msg runs per reader,
+// reader.rs:563-636); a writer-keyed sample to every entry.
 __global__ __launch_bounds__(IT) void k_fidx(const rtps_frag_sample* frag, const uint64_t* n_frag, uint64_t max_frag,
-                                             uint64_t max, uint32_t* fidx) {
+                                             uint64_t max, uint32_t* fidx, uint64_t* fmask, ReaderDev t,
+                                             const rtps_record* recs) {
   const uint64_t nf = n_frag ? (*n_frag < max_frag ? *n_frag : max_frag) : 0;
-  for (uint64_t s = (uint64_t)blockIdx.x * IT + threadIdx.x; s < nf; s += (uint64_t)gridDim.x * IT)
-    if (frag[s].status != RTPS_FRAG_SHORT && frag[s].rec_idx < max) fidx[frag[s].rec_idx] = (uint32_t)s;
+  for (uint64_t s = (uint64_t)blockIdx.x * IT + threadIdx.x; s < nf; s += (uint64_t)gridDim.x * IT) {
+    const rtps_frag_sample& f = frag[s];
+    if (f.status == RTPS_FRAG_SHORT || f.rec_idx >= max) continue;
+    fidx[f.rec_idx] = (uint32_t)s;  // (samples of one record share the writer and SN)
+    uint64_t bit = ~0ull;
+    if (f.reader_slot != RTPS_NO_MATCH) {
+      const uint32_t* d = reinterpret_cast<const uint32_t*>(recs + f.rec_idx);
+      uint32_t r2 = 0;
+      const uint32_t set = rt_classify<false>(t, nullptr, d[2], d[3], d[4], d[5], r2);
+      bit = 0;
+      if (set != NONE)
+        for (uint32_t k = t.set_first[set], e = t.set_first[set + 1]; k < e; ++k)
+          if (t.set_ent[k].reader_slot == f.reader_slot && k - t.set_first[set] < 64u) bit = 1ull << (k - t.set_first[set]);
+    }
+    atomicOr(reinterpret_cast<unsigned long long*>(fmask + f.rec_idx), (unsigned long long)bit);
+  }
 }
 
 // Does (record event kind, target x) make an event?  Sets ent / meta.
@@ -268,14 +287,17 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
         }
       }
     }
-    // the record's events: one per target reader that the event concerns
+    // the record's events: one per target reader that the event concerns (a completed
+    // DataFrag sample: the readers whose assembler completed it)
     uint32_t cnt = 0;
     uint32_t ent = NONE, meta = 0;
     if (ev != EV_NONE) {
       const uint32_t b = t.set_first[set], e = t.set_first[set + 1];
+      const uint64_t fm = (frag && x.fidx[i] != NONE) ? x.fmask[i] : ~0ull;
       for (uint32_t k = b; k < e; ++k) {
         uint32_t en, me;
-        if (ev_of(ev, t.set_ent[k], user_kind, reliable, en, me)) {
+        if (((fm >> ((k - b) & 63u)) & 1ull) && (k - b < 64u || fm == ~0ull) &&
+            ev_of(ev, t.set_ent[k], user_kind, reliable, en, me)) {
           ++cnt;
           ent = en;
           meta = me;
@@ -352,7 +374,7 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
 }
 
 // 1b: lane per record writes its events at roff[i] (set order = EntityId order of the readers)
-__global__ __launch_bounds__(IT) void k_expand(ReaderDev t, uint64_t n, uint32_t flags, Scratch x) {
+__global__ __launch_bounds__(IT) void k_expand(ReaderDev t, uint64_t n, uint32_t flags, Scratch x, bool with_frag) {
   const bool reliable = !(flags & RTPS_INGEST_BEST_EFFORT);
   for (uint64_t i = (uint64_t)blockIdx.x * IT + threadIdx.x; i < n; i += (uint64_t)gridDim.x * IT) {
     const uint8_t rk = x.rkind[i];
@@ -362,8 +384,10 @@ __global__ __launch_bounds__(IT) void k_expand(ReaderDev t, uint64_t n, uint32_t
     const uint32_t set = x.rset[i];
     uint32_t k = x.roff[i];
     const int64_t sn = x.rsn[i];
-    for (uint32_t j = t.set_first[set], e = t.set_first[set + 1]; j < e; ++j) {
+    const uint64_t fm = (with_frag && x.fidx[i] != NONE) ? x.fmask[i] : ~0ull;
+    for (uint32_t j = t.set_first[set], b = j, e = t.set_first[set + 1]; j < e; ++j) {
       uint32_t en, me;
+      if (!((fm >> ((j - b) & 63u)) & 1ull) || (j - b >= 64u && fm != ~0ull)) continue;
       if (!ev_of(ev, t.set_ent[j], user_kind, reliable, en, me)) continue;
       x.evt[k] = ev;
       x.ent[k] = en;
@@ -1128,8 +1152,9 @@ static void free_state(IngestState* s) {
   s->ecap = 0;
 }
 static void free_rscratch(IngestState* s) {
-  void* p[] = {s->x.fidx, s->x.rcnt, s->x.roff, s->x.rset, s->x.rkind, s->x.rsn};
+  void* p[] = {s->x.fidx, s->x.fmask, s->x.rcnt, s->x.roff, s->x.rset, s->x.rkind, s->x.rsn};
   for (void* q : p) if (q) (void)hipFree(q);
+  s->x.fmask = nullptr;
   s->x.fidx = nullptr; s->x.rcnt = nullptr; s->x.roff = nullptr; s->x.rset = nullptr; s->x.rkind = nullptr;
   s->x.rsn = nullptr;
   s->rcap = 0;
@@ -1140,7 +1165,7 @@ static void free_vscratch(IngestState* s) {
   for (void* q : p) if (q) (void)hipFree(q);
   Scratch keep = s->x;
   s->x = Scratch{};
-  s->x.fidx = keep.fidx; s->x.rcnt = keep.rcnt; s->x.roff = keep.roff; s->x.rset = keep.rset;
+  s->x.fidx = keep.fidx; s->x.fmask = keep.fmask; s->x.rcnt = keep.rcnt; s->x.roff = keep.roff; s->x.rset = keep.rset;
   s->x.rkind = keep.rkind; s->x.rsn = keep.rsn;
   s->tmp = nullptr;
   s->tmp_bytes = 0;
@@ -1189,7 +1214,8 @@ static bool grow_rscratch(IngestState* s, uint64_t max, hipStream_t st) {
   free_rscratch(s);
   Scratch& x = s->x;
   const uint64_t n = max;
-  bool ok = hipMalloc(&x.fidx, n * 4) == hipSuccess && hipMalloc(&x.rcnt, n * 4) == hipSuccess &&
+  bool ok = hipMalloc(&x.fidx, n * 4) == hipSuccess && hipMalloc(&x.fmask, n * 8) == hipSuccess &&
+            hipMalloc(&x.rcnt, n * 4) == hipSuccess &&
             hipMalloc(&x.roff, n * 4) == hipSuccess && hipMalloc(&x.rset, n * 4) == hipSuccess &&
             hipMalloc(&x.rkind, n) == hipSuccess && hipMalloc(&x.rsn, n * 8) == hipSuccess;
   if (!ok) { free_rscratch(s); return false; }
@@ -1292,11 +1318,12 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
   State& S = s->st;
   bool ok = hipMemsetAsync(S.ctr, 0, C_COUNT * 8, st) == hipSuccess;
   const bool with_frag = frag && n_frag && max_frag;
-  if (with_frag) ok = ok && hipMemsetAsync(x.fidx, 0xff, max * 4, st) == hipSuccess;
+  if (with_frag) ok = ok && hipMemsetAsync(x.fidx, 0xff, max * 4, st) == hipSuccess &&
+                     hipMemsetAsync(x.fmask, 0, max * 8, st) == hipSuccess;
   if (!ok) return RTPS_RX_EHIP;
   if (with_frag)
     hipLaunchKernelGGL(k_fidx, dim3((uint32_t)hmin((max_frag + IT - 1) / IT, 4096)), dim3(IT), 0, st, frag, n_frag,
-                       max_frag, max, x.fidx);
+                       max_frag, max, x.fidx, x.fmask, t, records);
   const uint32_t lds = rt_fits_lds(t) ? rt_lds_bytes(t.gmask + 1u, t.emask + 1u) : 0u;
   // Identity batches over many proxies take the per-proxy path with no host read-back:
   // classify writes the path's inputs, the sort runs over every record slot. The choice
@@ -1365,7 +1392,7 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
     if (n_rec && hipcub::DeviceScan::ExclusiveSum(s->tmp, tb, x.rcnt, x.roff, (uint32_t)n_rec, st) != hipSuccess)
       return RTPS_RX_EHIP;
     if (n_rec)
-      hipLaunchKernelGGL(k_expand, dim3((uint32_t)hmin((n_rec + IT - 1) / IT, 8192)), dim3(IT), 0, st, t, n_rec, flags, x);
+      hipLaunchKernelGGL(k_expand, dim3((uint32_t)hmin((n_rec + IT - 1) / IT, 8192)), dim3(IT), 0, st, t, n_rec, flags, x, with_frag);
   }
   const uint32_t gv = (uint32_t)hmin((nev + IT - 1) / IT, 8192) ? (uint32_t)hmin((nev + IT - 1) / IT, 8192) : 1u;
   // per-proxy workgroups when the events spread over many proxies (mean load bounded:

@@ -28,7 +28,9 @@
 //   * all arena reads go through a bounds-checked buffer resource (reads past
 //     the arena return 0 and never fault).
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 #include <stdint.h>
+#include <time.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -1596,6 +1598,92 @@ __global__ __launch_bounds__(TILE) void bucket_scatter_kernel(const rtps_record*
   }
 }
 
+// ---------------------------------------------------------------------------
+// per-reader DataFrag assembly (rtps_rx_frag_assemble with readers set): every
+// reader has its own FragmentAssembler per writer (Reader::fragment_assembler_mutable,
+// io_uring/rtps/reader.rs:617-619, 638-647), fed the DATA_FRAGs Domain::handle_event
+// routes to it (dp_event_loop.rs:266-327) minus those its Lifespan drops
+// (handle_datafrag_msg :578-589).  The batch is expanded into one copy of each
+// such record per target reader, the reader word (slot | 0x10000) in the copy's
+// reader_id; the assembly keys (rtps_frag.hip) include that word.
+// ---------------------------------------------------------------------------
+constexpr int64_t NO_LIFESPAN = INT64_MAX;
+struct FragX {
+  const rtps_record* recs;
+  const uint64_t* n_rec;
+  uint64_t max;
+  ReaderDev rt;
+  const int64_t* life;   // [65536] Lifespan of reader slot s in Duration ticks, NO_LIFESPAN: none
+  uint64_t recv_ticks;   // Timestamp::now() of the batch as ticks (seconds << 32 | fraction)
+  uint32_t any_life;
+  uint32_t* cnt;         // [max] copies of record i
+  uint32_t* off;         // [max] exclusive scan of cnt
+  rtps_record* xrec;     // [max_x] the copies
+  uint32_t* emap;        // [max_x] copy -> record
+  uint64_t* n_x;
+};
+// the target-set entries [b, e) of a DATA_FRAG record the user readers receive, or b == e
+__device__ __forceinline__ void frag_targets(const FragX& a, const rtps_record* r, uint32_t& b, uint32_t& e) {
+  b = e = 0;
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(r);
+  const uint32_t kind = (d[1] >> 16) & 0xffu, route = (d[7] >> 16) & 0xffu;
+  if (kind != RTPS_DATA_FRAG || !(route & RTPS_ROUTE_PASS) || !(route & RTPS_ROUTE_TARGETED) ||
+      (route & RTPS_ROUTE_BUILTIN))
+    return;
+  uint32_t r2 = 0;
+  const uint32_t set = rt_classify<false>(a.rt, nullptr, d[2], d[3], d[4], d[5], r2);
+  if (set == RTPS_NO_TARGET) return;
+  b = a.rt.set_first[set];
+  e = a.rt.set_first[set + 1];
+}
+// Lifespan check of handle_datafrag_msg (reader.rs:578-589): a source timestamp and a
+// Lifespan, and lifespan.duration < receive_timestamp.duration_since(source)
+// (structure/time.rs:85-113: wrapping tick difference as i64; Duration orders as ticks)
+__device__ __forceinline__ bool frag_expired(const FragX& a, const rtps_record* r, uint32_t slot) {
+  if (!a.any_life) return false;
+  const int64_t L = a.life[slot];
+  if (L == NO_LIFESPAN || !(r->route & RTPS_ROUTE_TS_VALID)) return false;
+  const uint64_t src = ((uint64_t)r->ts_sec << 32) | r->ts_frac;
+  return L < (int64_t)(a.recv_ticks - src);
+}
+__global__ __launch_bounds__(TILE) void frag_x_count(FragX a) {
+  const uint64_t n = *a.n_rec < a.max ? *a.n_rec : a.max;
+  for (uint64_t i = (uint64_t)blockIdx.x * TILE + threadIdx.x; i < a.max; i += (uint64_t)gridDim.x * TILE) {
+    uint32_t c = 0;
+    if (i < n) {
+      uint32_t b, e;
+      frag_targets(a, a.recs + i, b, e);
+      for (uint32_t k = b; k < e; ++k) c += frag_expired(a, a.recs + i, a.rt.set_ent[k].reader_slot) ? 0u : 1u;
+    }
+    a.cnt[i] = c;
+  }
+}
+__global__ __launch_bounds__(TILE) void frag_x_fill(FragX a) {
+  const uint64_t n = *a.n_rec < a.max ? *a.n_rec : a.max;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *a.n_x = a.max ? (uint64_t)a.off[a.max - 1] + a.cnt[a.max - 1] : 0ull;
+  for (uint64_t i = (uint64_t)blockIdx.x * TILE + threadIdx.x; i < n; i += (uint64_t)gridDim.x * TILE) {
+    if (!a.cnt[i]) continue;
+    uint32_t b, e;
+    frag_targets(a, a.recs + i, b, e);
+    const rtps_record* r = a.recs + i;
+    uint32_t w[16];
+    const u32x4* q = reinterpret_cast<const u32x4*>(r);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { const u32x4 v = q[k]; w[4 * k] = v[0]; w[4 * k + 1] = v[1]; w[4 * k + 2] = v[2]; w[4 * k + 3] = v[3]; }
+    uint32_t o = a.off[i];
+    for (uint32_t k = b; k < e; ++k) {
+      const uint32_t slot = a.rt.set_ent[k].reader_slot;
+      if (frag_expired(a, r, slot)) continue;
+      w[6] = slot | 0x10000u;  // reader_id: the reader word of the assembly key
+      u32x4* d = reinterpret_cast<u32x4*>(a.xrec + o);
+      d[0] = u32x4{w[0], w[1], w[2], w[3]}; d[1] = u32x4{w[4], w[5], w[6], w[7]};
+      d[2] = u32x4{w[8], w[9], w[10], w[11]}; d[3] = u32x4{w[12], w[13], w[14], w[15]};
+      a.emap[o] = (uint32_t)i;
+      ++o;
+    }
+  }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -1623,6 +1711,16 @@ struct rtps_rx_ctx {
   uint32_t ch_epoch = 0;          // last chained launch's epoch (words start zeroed: epoch 0 is never used)
   uint32_t chain_tiles = 0;       // tiles the chain words are sized for
   uint32_t mixed_pass = 0;        // chained pass for mixed traffic: 0 = lane walk (C, default), 1 = LDS tiles (D)
+  // per-reader DataFrag assembly (frag_x_*): Lifespans by reader slot, the batch's receive time, the expansion
+  int64_t* life = nullptr;        // [65536] device, NO_LIFESPAN where none
+  bool any_life = false;
+  uint64_t recv_ns = 0;           // rtps_rx_frag_set_receive_time (0: the host's clock at each assemble)
+  uint32_t *fx_cnt = nullptr, *fx_off = nullptr, *fx_emap = nullptr;
+  rtps_record* fx_rec = nullptr;
+  uint64_t* fx_n = nullptr;
+  uint64_t fx_cap = 0, fx_xcap = 0;
+  void* fx_tmp = nullptr;
+  size_t fx_tmp_bytes = 0;
 };
 
 static int hip_fail(hipError_t e) { return e == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP; }
@@ -1682,6 +1780,10 @@ int rtps_rx_destroy(rtps_rx_ctx* c) {
   (void)hipFree(c->bucket_hist);
   rtps_frag_state_free(c->frag);
   rtps_ingest_state_free(c->ingest);
+  {
+    void* fx[] = {c->life, c->fx_cnt, c->fx_off, c->fx_emap, c->fx_rec, c->fx_n, c->fx_tmp};
+    for (void* q : fx) if (q) (void)hipFree(q);
+  }
   (void)hipStreamDestroy(c->own_stream);
   delete c;
   return RTPS_RX_OK;
@@ -1963,7 +2065,92 @@ int rtps_rx_frag_assemble(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_l
     c->frag = rtps_frag_state_new(c->device);
     if (!c->frag) return RTPS_RX_ENOMEM;
   }
-  return rtps_frag_assemble(c->frag, c->stream, arena, arena_len, dgram_off, records, n_records, max_records, out);
+  const ReaderDev rd = rt_dev(c->readers);
+  if (rd.gkeys == nullptr)  // no readers: one assembler per writer for every DATA_FRAG that passes
+    return rtps_frag_assemble(c->frag, c->stream, arena, arena_len, dgram_off, records, n_records, max_records, out,
+                              0u, nullptr);
+  // readers: one assembler per (reader, writer), over the batch expanded per target reader
+  const uint64_t max_x = max_records * (rd.max_set ? rd.max_set : 1u);
+  if (max_x > 0x7fffffffull) return RTPS_RX_ETOOBIG;
+  if (max_records > c->fx_cap || max_x > c->fx_xcap || !c->fx_n) {
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return RTPS_RX_EHIP;
+    void* fx[] = {c->fx_cnt, c->fx_off, c->fx_emap, c->fx_rec, c->fx_n, c->fx_tmp};
+    for (void* q : fx) if (q) (void)hipFree(q);
+    c->fx_cnt = c->fx_off = c->fx_emap = nullptr; c->fx_rec = nullptr; c->fx_n = nullptr; c->fx_tmp = nullptr;
+    c->fx_cap = c->fx_xcap = 0; c->fx_tmp_bytes = 0;
+    const uint64_t m = max_records ? max_records : 1, x = max_x ? max_x : 1;
+    size_t tb = 0;
+    if (hipMalloc(&c->fx_cnt, m * 4) != hipSuccess || hipMalloc(&c->fx_off, m * 4) != hipSuccess ||
+        hipMalloc(&c->fx_emap, x * 4) != hipSuccess || hipMalloc(&c->fx_rec, x * sizeof(rtps_record)) != hipSuccess ||
+        hipMalloc(&c->fx_n, 8) != hipSuccess ||
+        hipcub::DeviceScan::ExclusiveSum(nullptr, tb, c->fx_cnt, c->fx_off, (int)m, c->stream) != hipSuccess ||
+        hipMalloc(&c->fx_tmp, tb ? tb : 16) != hipSuccess)
+      return RTPS_RX_ENOMEM;
+    c->fx_tmp_bytes = tb;
+    c->fx_cap = m;
+    c->fx_xcap = x;
+  }
+  if (!c->life) {
+    if (hipMalloc(&c->life, 65536 * sizeof(int64_t)) != hipSuccess) return RTPS_RX_ENOMEM;
+    std::vector<int64_t> none(65536, NO_LIFESPAN);
+    if (hipMemcpy(c->life, none.data(), 65536 * sizeof(int64_t), hipMemcpyHostToDevice) != hipSuccess)
+      return RTPS_RX_EHIP;
+  }
+  uint64_t now_ns = c->recv_ns;
+  if (!now_ns) {  // Timestamp::now() (structure/time.rs:58-65): the host's wall clock at this batch
+    struct timespec ts;
+    clock_gettime(CLOCK_REALTIME, &ts);
+    now_ns = (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+  }
+  // Timestamp::from_nanos (time.rs:78-83) as ticks
+  const uint64_t recv_ticks = ((now_ns / 1000000000ull) << 32) + (((now_ns % 1000000000ull) << 32) / 1000000000ull);
+  const uint64_t m = max_records ? max_records : 1;
+  FragX a{records, n_records, max_records, rd, c->life, recv_ticks, c->any_life ? 1u : 0u, c->fx_cnt, c->fx_off,
+          c->fx_rec, c->fx_emap, c->fx_n};
+  const uint32_t g = (uint32_t)((m + TILE - 1) / TILE < 8192 ? (m + TILE - 1) / TILE : 8192);
+  if (max_records == 0) {
+    if (hipMemsetAsync(c->fx_n, 0, 8, c->stream) != hipSuccess) return RTPS_RX_EHIP;
+  } else {
+    hipLaunchKernelGGL(frag_x_count, dim3(g), dim3(TILE), 0, c->stream, a);
+    size_t tb = c->fx_tmp_bytes;
+    if (hipcub::DeviceScan::ExclusiveSum(c->fx_tmp, tb, c->fx_cnt, c->fx_off, (int)max_records, c->stream) !=
+        hipSuccess)
+      return RTPS_RX_EHIP;
+    hipLaunchKernelGGL(frag_x_fill, dim3(g), dim3(TILE), 0, c->stream, a);
+  }
+  if (hipGetLastError() != hipSuccess) return RTPS_RX_EHIP;
+  return rtps_frag_assemble(c->frag, c->stream, arena, arena_len, dgram_off, c->fx_rec, c->fx_n, max_x, out,
+                            0xffffffffu, c->fx_emap);
+}
+
+/* per-reader Lifespan QoS for the DataFrag assembly (reader.rs:578-589): lifespan_ns < 0 = none */
+int rtps_rx_set_reader_lifespan(rtps_rx_ctx* c, uint16_t reader_slot, int64_t lifespan_ns) {
+  if (!c) return RTPS_RX_EINVAL;
+  (void)hipSetDevice(c->device);
+  if (!c->life) {
+    if (hipMalloc(&c->life, 65536 * sizeof(int64_t)) != hipSuccess) return RTPS_RX_ENOMEM;
+    std::vector<int64_t> none(65536, NO_LIFESPAN);
+    if (hipMemcpy(c->life, none.data(), 65536 * sizeof(int64_t), hipMemcpyHostToDevice) != hipSuccess)
+      return RTPS_RX_EHIP;
+  }
+  int64_t ticks = NO_LIFESPAN;
+  if (lifespan_ns >= 0) {  // Duration::from_nanos (structure/duration.rs:60-67) as ticks
+    const int64_t sec = lifespan_ns / 1000000000ll, frac = ((lifespan_ns % 1000000000ll) << 32) / 1000000000ll;
+    ticks = (int64_t)(((uint64_t)(int64_t)(int32_t)sec << 32) + (uint64_t)(uint32_t)frac);
+    c->any_life = true;
+  }
+  if (hipStreamSynchronize(c->stream) != hipSuccess ||
+      hipMemcpy(c->life + reader_slot, &ticks, sizeof ticks, hipMemcpyHostToDevice) != hipSuccess)
+    return RTPS_RX_EHIP;
+  return RTPS_RX_OK;
+}
+
+/* the receive time (Timestamp::now(), ns since the UNIX epoch) of the next batches' DATA_FRAGs for
+   the Lifespan check; 0: the host's clock at each rtps_rx_frag_assemble */
+int rtps_rx_frag_set_receive_time(rtps_rx_ctx* c, uint64_t unix_ns) {
+  if (!c) return RTPS_RX_EINVAL;
+  c->recv_ns = unix_ns;
+  return RTPS_RX_OK;
 }
 
 int rtps_rx_frag_reset(rtps_rx_ctx* c) {

@@ -400,6 +400,18 @@ class MessageReceiver:
         L.rtps_rx_frag_set_clock.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
         _check(L.rtps_rx_frag_set_clock(self._h, now_ns))
 
+    def set_reader_lifespan(self, reader_slot, lifespan_ns):
+        """Lifespan QoS of a reader for the DataFrag assembly (reader.rs:578-589); None: none."""
+        L = lib()
+        L.rtps_rx_set_reader_lifespan.argtypes = [ctypes.c_void_p, ctypes.c_uint16, ctypes.c_int64]
+        _check(L.rtps_rx_set_reader_lifespan(self._h, reader_slot, -1 if lifespan_ns is None else lifespan_ns))
+
+    def frag_set_receive_time(self, unix_ns):
+        """Timestamp::now() of the next batches for the Lifespan checks (0: the host clock)."""
+        L = lib()
+        L.rtps_rx_frag_set_receive_time.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+        _check(L.rtps_rx_frag_set_receive_time(self._h, unix_ns))
+
     def frag_gc(self, expire_before_ns):
         """Drop the incomplete buffers last modified before expire_before_ns -> buffers left (host sync)."""
         import torch

@@ -78,7 +78,7 @@ assert XDESC_DTYPE.itemsize == 16
 FRAG_OK, FRAG_SHORT, FRAG_NO_ROOM = 0, 1, 2
 FRAG_SAMPLE_DTYPE = np.dtype([("writer_guid", "u1", (16,)), ("sn", "<i8"), ("heap_off", "<u8"),
                               ("data_size", "<u4"), ("rec_idx", "<u4"), ("flags", "u1"), ("status", "u1"),
-                              ("_r", "<u2"), ("_r2", "<u4")])
+                              ("reader_slot", "<u2"), ("_r2", "<u4")])
 assert FRAG_SAMPLE_DTYPE.itemsize == 48
 assert MATCH_DTYPE.itemsize == 20
 

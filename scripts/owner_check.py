@@ -88,7 +88,7 @@ spilled = int(sum(int(c["n"] - c["cut"]) for c in sh.counts("recv")))
 
 # ---- the single-rank oracle over the whole stream, restricted to this rank's writers ----
 _, recs, _, _ = oracle.parse(wa, wo, wlen, match_table=tbl, threads=8)
-samples = oracle.FragAssembler().batch(wa, wo, recs)[0]
+samples = oracle.FragAssembler().batch_readers(wa, wo, recs, tbl)[0]
 _, odels, oack = oracle.HistoryIngest(tbl).batch(wa, wo, recs, samples)
 mine = np.array([owner_hash_words(r.view(np.uint32)[2:6]) % world == rank for r in recs.view(np.uint8).reshape(-1, 64)])
 index = {(int(r["dgram_idx"]), int(r["sub_off"])): i for i, r in enumerate(recs)}

@@ -151,3 +151,112 @@ def soup(n, seed, prefix_count=3, writers_per_prefix=2):
                                     bytes(rng.integers(0, 256, w2, dtype=np.uint8)), key=key2)
         out.append(datagram(p, [sub]))
     return out
+
+
+class ReaderFragRef:
+    """Per-reader model: Domain::handle_event hands a DATA_FRAG the receiver passes to
+    user readers (ROUTE_PASS, not ROUTE_BUILTIN) to every reader that contains the
+    writer's entity id, in EntityId order (dp_event_loop.rs:266-327; the targets of
+    ingest_ref.IngestRef); each reader drops it when its Lifespan is exceeded
+    (reader.rs:578-589: the receive Timestamp minus the source Timestamp, in ticks,
+    wrapping, as a signed Duration) and otherwise feeds its own FragmentAssembler for
+    the writer (:617-619, 638-647), modelled by a FragRef per (reader, writer)."""
+
+    def __init__(self, readers, lifespan_ns=None, recv_ns=0):
+        from ingest_ref import IngestRef
+        self.route = IngestRef(readers)
+        self.life = dict(lifespan_ns or {})
+        self.recv_ns = recv_ns
+        self.asm = {}
+
+    def set_readers(self, readers):
+        from ingest_ref import IngestRef
+        self.route = IngestRef(readers)
+
+    @staticmethod
+    def _ticks(ns, signed=False):
+        return ((ns // 10**9) << 32) + (((ns % 10**9) << 32) // 10**9)
+
+    def batch(self, arena, offs, recs):
+        from rtps_rx.records import ROUTE_BUILTIN, ROUTE_TS_VALID
+        out = []  # (reader slot, guid, sn, bytes, rec_idx, flags)
+        now = self._ticks(self.recv_ns)
+        for ri, r in enumerate(recs):
+            if int(r["kind"]) != DATA_FRAG or not (int(r["route"]) & ROUTE_PASS) or int(r["route"]) & ROUTE_BUILTIN:
+                continue
+            guid = bytes(r["prefix"]) + bytes(r["writer_id"])
+            for reader, _proxy in self.route.targets(guid):
+                slot = self.route.slot[reader]
+                if slot in self.life and int(r["route"]) & ROUTE_TS_VALID:
+                    src = (int(r["ts_sec"]) << 32) | int(r["ts_frac"])
+                    elapsed = (now - src) & 0xFFFFFFFFFFFFFFFF
+                    elapsed = elapsed - (1 << 64) if elapsed >= 1 << 63 else elapsed
+                    if self._ticks(self.life[slot]) < elapsed:
+                        continue
+                a = self.asm.setdefault((slot, guid), FragRef())
+                for g, sn, data, rj, fl in a.batch(arena, offs, recs[ri:ri + 1]):
+                    out.append((slot, g, sn, data, ri, fl))
+        return out
+
+
+# ---- the per-reader scenario (VERDICT r2 item 5): two readers of one writer, one with a
+# Lifespan, a third reader added mid-stream, a writer that changes its fragment size ----
+RS_PREFIX = [bytes([0x01, 0x0f, 0xaa, k, 0, 0, 0, 0, 1, 0, 0, 0]) for k in (1, 2)]
+RS_WRITER = [bytes([0, 1, k, 0x02]) for k in (1, 2)]
+RS_READER = {11: bytes([0, 0, 1, 0x07]), 12: bytes([0, 0, 2, 0x07]), 13: bytes([0, 0, 3, 0x07])}
+RS_RECV_NS = 1_700_000_100 * 10**9
+RS_LIFESPAN = {12: 2 * 10**9}  # reader slot 12 (B): Lifespan 2 s
+
+
+def reader_scenario_readers(with_c):
+    """Readers A (11), B (12) and, from the second batch on, C (13); proxies appended so
+    that existing proxies keep their positions."""
+    from rtps_rx.records import Readers
+    readers = [(RS_READER[11], 11, 0), (RS_READER[12], 12, 0)] + ([(RS_READER[13], 13, 0)] if with_c else [])
+    g1, g2 = RS_PREFIX[0] + RS_WRITER[0], RS_PREFIX[1] + RS_WRITER[1]
+    proxies = [(g1, 0), (g1, 1), (g2, 1)] + ([(g1, 2), (g2, 2)] if with_c else [])
+    return Readers(readers, proxies)
+
+
+def info_ts_sub(sec, frac, le=True, invalidate=False):
+    e = "<" if le else ">"
+    if invalidate:
+        return bytes([0x09, (1 if le else 0) | 2]) + struct.pack(e + "H", 0)
+    return bytes([0x09, 1 if le else 0]) + struct.pack(e + "HII", 8, sec, frac)
+
+
+def reader_scenario(n, seed, sn0, frag_size):
+    """n datagrams: samples of both writers fragmented at frag_size (W1) / 48 (W2),
+    fragments shuffled across the batch, some repeated; each datagram may start with an
+    INFO_TS 0.5, 1.5, 3 or 10 s before RS_RECV_NS (or none, or an invalidating one)."""
+    rng = np.random.default_rng(seed)
+    now_s = RS_RECV_NS // 10**9
+    frags = []
+    sn = {0: sn0, 1: sn0}
+    while len(frags) < n:
+        w = int(rng.integers(0, 2))
+        F = frag_size if w == 0 else 48
+        ds = int(rng.choice([F, 2 * F + 7, 3 * F, 5 * F - 1]))
+        cnt = ds // F + (ds % F > 0)
+        for k in range(1, cnt + 1):
+            plen = min(F, ds - (k - 1) * F)
+            frags.append((w, sn[w], k, F, ds, bytes(rng.integers(0, 256, plen, dtype=np.uint8))))
+        sn[w] += 1
+    order = rng.permutation(len(frags))
+    out = []
+    for i in order[:n]:
+        w, s, k, F, ds, pl = frags[int(i)]
+        subs = []
+        t = rng.random()
+        if t < 0.7:
+            age = float(rng.choice([0.5, 1.5, 3.0, 10.0]))
+            sec = now_s - int(age) - (1 if age % 1 else 0)
+            frac = (1 << 31) if age % 1 else 0
+            subs.append(info_ts_sub(sec, frac))
+        elif t < 0.8:
+            subs.append(info_ts_sub(0, 0, invalidate=True))
+        subs.append(datafrag_sub(RS_WRITER[w], s, k, 1, F, ds, pl, le=bool(rng.random() < 0.85)))
+        out.append(datagram(RS_PREFIX[w], subs))
+        if rng.random() < 0.05:  # a repeated fragment
+            out.append(datagram(RS_PREFIX[w], subs))
+    return out[:n]

@@ -189,3 +189,61 @@ def test_bucket_sort_oversized_buckets(rx, sort):
     fa = oracle.FragAssembler()
     g = _run(rx, fa, mixed, "9000 keys in one bucket")
     assert g[3] >= 9000
+
+
+@pytest.mark.parametrize("ingest_path", [1, 2])
+def test_per_reader_assembly_and_ingest(rx, ingest_path):
+    """two readers of one writer, one with a Lifespan (reader.rs:578-589),
+    a reader added mid-stream, a writer changing its fragment size: every (reader, writer)
+    pair has its own assembler (reader.rs:617-619, 638-647).  Samples (with their reader),
+    heap bytes, deliveries and every proxy's ack_base bit-exact against the oracle, on both
+    ingest paths."""
+    from rtps_rx.records import FRAG_SAMPLE_DTYPE, DELIVERY_DTYPE, max_records
+    dev = torch.device("cuda", 0)
+    rx.debug_ingest_path(ingest_path)
+    rx.set_reader_lifespan(12, frag_ref.RS_LIFESPAN[12])
+    rx.frag_set_receive_time(frag_ref.RS_RECV_NS)
+    fa = oracle.FragAssembler()
+    ing = None
+    per_reader = {}
+    batches = [(frag_ref.reader_scenario_readers(False), frag_ref.reader_scenario(400, 1, 1, 64)),
+               (frag_ref.reader_scenario_readers(True), frag_ref.reader_scenario(600, 2, 200, 32))]
+    for k, (rd, dgrams) in enumerate(batches):
+        rx.set_readers(rd)
+        if ing is None:
+            ing = oracle.HistoryIngest(rd)
+        else:
+            ing.set_readers(rd)
+        arena, off, ln = oracle.pack(dgrams, align=4)
+        A = torch.from_numpy(arena).to(dev)
+        O = torch.from_numpy(off.view(np.int64)).to(dev)
+        L = torch.from_numpy(ln.view(np.int32)).to(dev)
+        cap = max_records(ln)
+        heap_bytes = 4 * len(arena) + (1 << 20)
+        outs = rx.alloc_outputs(len(ln), cap)
+        fouts = rx.alloc_frag_outputs(3 * cap, heap_bytes)
+        iouts = rx.alloc_ingest_outputs(cap, rd.n_proxies)
+        rx.parse_batch_device(A, O, L, len(ln), outs)
+        rx.frag_assemble(A, O, outs, fouts)
+        rx.ingest(A, O, outs, iouts, fouts)
+        rx.sync()
+        _, recs, _, _ = oracle.parse(arena, off, ln, match_table=rd)
+        o_s, o_heap, o_n, o_used = fa.batch_readers(arena, off, recs, rd, frag_ref.RS_LIFESPAN, frag_ref.RS_RECV_NS,
+                                                    max_samples=3 * cap, heap_bytes=heap_bytes)
+        ns = int(fouts["n_samples"].item())
+        assert ns == o_n > 0, (k, ns, o_n)
+        assert int(fouts["heap_used"].item()) == o_used
+        s = fouts["samples"][:ns].cpu().numpy().reshape(-1).view(FRAG_SAMPLE_DTYPE)
+        assert s.tobytes() == o_s.tobytes(), f"batch {k}: sample descriptors differ"
+        heap = fouts["heap"].cpu().numpy()
+        for x in s:
+            o, d = int(x["heap_off"]), int(x["data_size"])
+            assert heap[o:o + d].tobytes() == o_heap[o:o + d].tobytes()
+            per_reader[int(x["reader_slot"])] = per_reader.get(int(x["reader_slot"]), 0) + 1
+        o_acc, o_dels, o_ack = ing.batch(arena, off, recs, o_s)
+        na = int(iouts["n_accepted"].item())
+        dels = iouts["accepted"][:na].cpu().numpy().reshape(-1).view(DELIVERY_DTYPE)
+        assert dels.tobytes() == o_dels.tobytes(), f"batch {k}: deliveries differ"
+        assert np.array_equal(iouts["accept"][:len(recs)].cpu().numpy(), o_acc)
+        assert np.array_equal(iouts["ack_base"][:rd.n_proxies].cpu().numpy(), o_ack)
+    assert per_reader[11] > per_reader[12] > 0 and per_reader.get(13, 0) > 0

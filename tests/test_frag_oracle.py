@@ -135,3 +135,33 @@ def test_c4_samples_are_their_fragments():
         o = int(s["heap_off"])
         assert heap[o:o + 65536].tobytes() == data
         assert int(s["rec_idx"]) == max(idx)  # the last fragment to arrive completes it
+
+
+def _reader_batches():
+    """Batch 1: readers A, B; batch 2: C added, W1 switches to 32-byte fragments."""
+    import frag_ref as F
+    return [(F.reader_scenario_readers(False), F.reader_scenario(400, 1, 1, 64)),
+            (F.reader_scenario_readers(True), F.reader_scenario(600, 2, 200, 32))]
+
+
+def test_oracle_per_reader_assembly_matches_model():
+    """one assembler per (reader, writer) with the reader's own fragment
+    size, the Lifespan drop (reader.rs:578-589) and a reader added mid-stream: the oracle
+    (rtps_oracle_frag_batch_readers) against the independent Python model, batch after batch."""
+    import frag_ref as F
+    fa = oracle.FragAssembler()
+    model = F.ReaderFragRef(F.reader_scenario_readers(False), F.RS_LIFESPAN, F.RS_RECV_NS)
+    per_reader = {}
+    for rd, dgrams in _reader_batches():
+        model.set_readers(rd)
+        arena, off, ln = oracle.pack(dgrams, align=4)
+        _, recs, _, _ = oracle.parse(arena, off, ln, match_table=rd)
+        samples, heap, n, used = fa.batch_readers(arena, off, recs, rd, F.RS_LIFESPAN, F.RS_RECV_NS)
+        exp = model.batch(arena, off, recs)
+        assert n == len(exp) > 0
+        for s, (slot, g, sn, data, ri, fl) in zip(samples, exp):
+            assert (int(s["reader_slot"]), bytes(s["writer_guid"]), int(s["sn"]), int(s["rec_idx"])) == (slot, g, sn, ri)
+            assert heap[int(s["heap_off"]):int(s["heap_off"]) + int(s["data_size"])].tobytes() == data
+            per_reader[slot] = per_reader.get(slot, 0) + 1
+    # the scenario makes the readers differ: B loses samples to its Lifespan, C only has batch 2's
+    assert per_reader[11] > per_reader[12] > 0 and per_reader.get(13, 0) > 0

@@ -41,7 +41,7 @@ def _batch(rx, ing, tbl, dgrams, label, frag=False, fa=None, best_effort=False, 
                                                             best_effort=best_effort)
     st, recs, _, _ = oracle.parse(arena, off, ln, match_table=tbl, threads=8)
     assert res.records.tobytes() == recs.tobytes(), f"{label}: parse differs"
-    o_samples = fa.batch(arena, off, recs)[0] if frag else None
+    o_samples = fa.batch_readers(arena, off, recs, tbl)[0] if frag else None
     o_acc, o_accepted, o_ack = ing.batch(arena, off, recs, o_samples, best_effort=best_effort)
     assert np.array_equal(acc, o_acc), f"{label}: accept flags differ at {np.nonzero(acc != o_acc)[0][:10]}"
     assert accepted.tobytes() == o_accepted.tobytes(), f"{label}: deliveries"

@@ -176,7 +176,7 @@ def test_one_rank_owner_pipeline(rx, wl, cap, bcap):
         ack = iouts["ack_base"][:len(tbl)].cpu().numpy()
         # oracle on the whole batch; its deliveries name records of the whole batch
         _, recs, _, _ = oracle.parse(arena, off, ln, match_table=tbl)
-        samples = oracle.FragAssembler().batch(arena, off, recs)[0]
+        samples = oracle.FragAssembler().batch_readers(arena, off, recs, tbl)[0]
         _, odels, oack = oracle.HistoryIngest(tbl).batch(arena, off, recs, samples)
         index = {(int(r["dgram_idx"]), int(r["sub_off"])): i for i, r in enumerate(recs)}
         orecs = ob.records()

@@ -118,7 +118,7 @@ def _worker(rank, world, port, wl, n, stride, cap, bcap, tbl, q):
             rbs += nb - cb
         orecs, ooff, oarena, (orank, odidx) = shard_unpack_np(received)
         fa = oracle.FragAssembler()
-        samples = fa.batch(oarena, ooff, orecs)[0]
+        samples = fa.batch_readers(oarena, ooff, orecs, tbl)[0]
         ing = oracle.HistoryIngest(tbl)
         acc, dels, ack = ing.batch(oarena, ooff, orecs, samples)
         q.put((rank, dels.tobytes(), ack.tobytes(), orank.tobytes(), odidx.tobytes(),
@@ -147,7 +147,7 @@ def _run(world, wl, n, stride, cap, bcap):
     # one rank's oracle over the whole stream
     a, o, l = _whole(wl, world, n, stride)
     _, recs, _, rb = oracle.parse(a, o, l, match_table=tbl)
-    samples = oracle.FragAssembler().batch(a, o, recs)[0]
+    samples = oracle.FragAssembler().batch_readers(a, o, recs, tbl)[0]
     _, dels, ack = oracle.HistoryIngest(tbl).batch(a, o, recs, samples)
     index = {(int(r["dgram_idx"]), int(r["sub_off"])): i for i, r in enumerate(recs)}
     got, spilled, items = [], 0, 0
