@@ -149,6 +149,39 @@ def time_ceilings(arena, off_t, ln_t, n, stream, steps):
     return res
 
 
+def time_hops_ceilings(arena, off_t, ln_t, n, outs, n_rec, stream, steps):
+    """Live timing of the mixed-traffic floor (csrc/diag/ceiling.hip ceil_hops_kernel): the
+    parse's dependent header hops (one 16-B window per submessage) and a 64-B record store per
+    materialised submessage at the parse's own positions (its status / rec_begin), no field
+    decode, no validation, no classification; one walk, and two walks (count, then write) as the
+    chained kernel does.  None if the diagnostic library is absent."""
+    import ctypes
+    path = os.path.join(REPO, "rustdds-io_uring_amd", "libdiag_ceiling.so")
+    if not os.path.exists(path):
+        return None
+    D = ctypes.CDLL(path)
+    D.diag_ceiling_hops.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64] + [ctypes.c_void_p] * 2 + \
+        [ctypes.c_uint32] + [ctypes.c_void_p] * 4
+    rec = torch.empty((max(n_rec, 1), 64), dtype=torch.uint8, device=arena.device)
+    res = {}
+    for walks in (1, 2):
+        def run():
+            D.diag_ceiling_hops(walks, arena.data_ptr(), arena.numel(), off_t.data_ptr(), ln_t.data_ptr(), n,
+                                outs["status"].data_ptr(), outs["rec_begin"].data_ptr(), rec.data_ptr(),
+                                ctypes.c_void_p(stream.cuda_stream))
+        for _ in range(3):
+            run()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        a.record(stream)
+        for _ in range(steps):
+            run()
+        b.record(stream)
+        torch.cuda.synchronize()
+        res[walks] = a.elapsed_time(b) / steps
+    return res
+
+
 def end_to_end(rx, arena, off_t, ln_t, n, outs, n_rec, stream, reps=5):
     """Host-memory-in / host-memory-out rate (the path starts in io_uring receive
     buffers and ends in the history cache).  Two modes, both checked against the
@@ -231,6 +264,17 @@ def roofline(rx, args, arena, off_t, ln_t, n, outs, stream, total_bytes, alg_rea
                  "ceiling of this access shape is read_ceiling_frac)"}
     if pmc:
         r["pmc_source"] = pmc["_source"]
+    if kname == "rtps_parse_chain_kernel":
+        torch.cuda.synchronize()
+        n_rec = int(outs["n_records"].item())
+        c = time_hops_ceilings(arena, off_t, ln_t, n, outs, n_rec, stream, args.steps)
+        if c:
+            r["ceiling"] = {"kernel": "diag ceil_hops_kernel (csrc/diag/ceiling.hip): the same dependent header "
+                                      "hops per datagram + a 64-B record store per materialised submessage at the "
+                                      "parse's positions, no field decode",
+                            "one_walk_ms": c[1], "two_walk_ms": c[2]}
+            r["attainable_frac"] = c[1] / ms  # same-shape one-walk floor / kernel time
+            r["attainable_frac_two_walk"] = c[2] / ms
     if kname == "rtps_parse_spec_kernel":
         c = time_ceilings(arena, off_t, ln_t, n, stream, args.steps)
         if c:

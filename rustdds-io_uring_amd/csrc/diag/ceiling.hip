@@ -234,3 +234,76 @@ extern "C" int diag_ceiling_var(int hb, int ntl, int nts, int per, const uint8_t
 #undef V
   return -1;
 }
+
+// ---- the mixed-traffic (C3) floor: the parse's dependent header hops + its record stores ----
+// Lane per datagram.  One hop per submessage: a 16-B load at the submessage start (the first
+// from the 64-B head, as the parse), its length from the header (octetsToNextHeader in the
+// submessage's byte order; 0 = to the end), then the next.  Every submessage the parse
+// materialises gets a 64-B record built from the loaded window (no field decode, no validation,
+// no classification) at the parse's own position (rec_begin, from the real parse; datagrams the
+// parse dropped store nothing).  WALKS = 2: a first walk without stores before the storing one,
+// as a count-then-write parse does.
+__device__ __forceinline__ uint32_t hop_e16(uint32_t raw, bool le) {
+  const uint32_t v = raw >> 16;
+  return le ? v : (((v & 0xffu) << 8) | (v >> 8));
+}
+template <int WALKS>
+__global__ __launch_bounds__(256) void ceil_hops_kernel(const uint8_t* arena, uint64_t arena_len, const uint64_t* off,
+                                                        const uint32_t* len, uint32_t n, const uint8_t* status,
+                                                        const uint32_t* rb, u32x4* rec) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t* d = arena + off[i];
+  const uint32_t L = len[i];
+  const u32x4* h = reinterpret_cast<const u32x4*>(d);
+  u32x4 h0 = {0u, 0u, 0u, 0u}, h1 = h0, h2 = h0, h3 = h0;
+  if (off[i] + 64u <= arena_len) { h0 = h[0]; h1 = h[1]; h2 = h[2]; h3 = h[3]; }
+  const bool ok = status[i] == 0;
+  uint64_t r = rb[i];
+  uint32_t guard = 0;
+#pragma unroll 1
+  for (int walk = 0; walk < WALKS; ++walk) {
+    const bool store = walk == WALKS - 1 && ok;
+    uint32_t o = 20;
+    while (o + 4u <= L && guard < 20000u) {
+      ++guard;
+      u32x4 w;
+      if (o == 20u) {
+        w = u32x4{h1[1], h1[2], h1[3], h2[0]};
+      } else if (o + 16u <= ((L + 15u) & ~15u)) {  // inside the datagram's 16-B slot of the arena
+        __builtin_memcpy(&w, d + o, 16);
+      } else {
+        w = u32x4{0u, 0u, 0u, 0u};
+        for (uint32_t k = 0; k < 4; ++k) w[0] |= (uint32_t)d[o + k] << (8u * k);
+      }
+      const uint32_t kind = w[0] & 0xffu;
+      const bool le = (w[0] >> 8) & 1u;
+      uint32_t blen = hop_e16(w[0], le);
+      if (blen == 0u && kind != 0x01u && kind != 0x09u) blen = L - o - 4u;
+      const bool emits = kind == 0x06u || kind == 0x07u || kind == 0x08u || kind == 0x09u || kind == 0x0cu ||
+                         kind == 0x0eu || kind == 0x0fu || kind == 0x12u || kind == 0x13u || kind == 0x15u ||
+                         kind == 0x16u;
+      if (store && emits) {
+        u32x4* q = rec + r * 4;
+        q[0] = u32x4{i, o | (kind << 16), h0[2], h0[3]};
+        q[1] = u32x4{h1[0], w[1], w[2], blen};
+        q[2] = u32x4{w[3], w[1] ^ w[2], h3[0], h3[1]};
+        q[3] = u32x4{w[0], h2[1], h2[2], h2[3]};
+        ++r;
+      }
+      o += 4u + blen;
+    }
+  }
+}
+extern "C" int diag_ceiling_hops(int walks, const uint8_t* arena, uint64_t arena_len, const uint64_t* off,
+                                 const uint32_t* len, uint32_t n, const uint8_t* status, const uint32_t* rb, void* rec,
+                                 void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  dim3 g((n + 255) / 256), b(256);
+  if (walks == 1)
+    hipLaunchKernelGGL(ceil_hops_kernel<1>, g, b, 0, s, arena, arena_len, off, len, n, status, rb, (u32x4*)rec);
+  else if (walks == 2)
+    hipLaunchKernelGGL(ceil_hops_kernel<2>, g, b, 0, s, arena, arena_len, off, len, n, status, rb, (u32x4*)rec);
+  else return -1;
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
