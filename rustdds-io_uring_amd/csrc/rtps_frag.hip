@@ -48,12 +48,18 @@ constexpr uint32_t NONE = 0xffffffffu;
 constexpr uint32_t SENT = 0xffffffffu;   // sort key of records that are not assembled
 constexpr uint32_t FIXED = 0x80000000u;  // writer table: fragment size resolved
 // Assembly keys are five words: the writer GUID (prefix || writer_id, record
-// bytes 8..24) and a reader word (record bytes 24..28, ANDed with the batch's
-// rmask).  Without readers rmask is 0: one assembler per writer.  With readers
-// the batch is an expansion with one copy of a DATA_FRAG record per target
-// reader whose reader_id field holds that reader (rtps_rx.hip frag_expand), so
-// every (reader, writer) pair has its own assembler, as every Reader has its own
-// FragmentAssembler per writer (io_uring/rtps/reader.rs:617-619, 638-647).
+// bytes 8..24) and a reader word, kept per batch position in rword[] by k_keys
+// (FragSel):
+//   mode 0, no readers: word 0, every DATA_FRAG that passes: one assembler per writer;
+//   mode 1, readers, every target set of at most one reader: k_keys looks up the
+//     record's reader (the target set, rtps_readers.h) and its Lifespan, word =
+//     slot | 0x10000, records that reach no reader (or whose Lifespan has expired
+//     for that reader) are not assembled;
+//   mode 2, readers with larger sets: the batch is an expansion with one copy of a
+//     DATA_FRAG record per target reader (rtps_rx.hip frag_x_*), the word in the
+//     copy's reader_id field.
+// So every (reader, writer) pair has its own assembler, as every Reader has its
+// own FragmentAssembler per writer (io_uring/rtps/reader.rs:617-619, 638-647).
 constexpr int KW = 5;
 
 constexpr uint32_t WCAP = 1u << 16;      // writers
@@ -91,10 +97,10 @@ struct Pend {
   uint64_t modified;  // clock of the last batch that inserted fragments (AssemblyBuffer::modified_time)
 };
 
-__device__ __forceinline__ void guid_of(const rtps_record* r, uint32_t g[KW], uint32_t rmask) {
+__device__ __forceinline__ void guid_of(const rtps_record* r, uint32_t word, uint32_t g[KW]) {
   const uint4 v = *(const uint4*)((const uint8_t*)r + 8);  // prefix[12] @8, writer_id @20
   g[0] = v.x; g[1] = v.y; g[2] = v.z; g[3] = v.w;
-  g[4] = *(const uint32_t*)((const uint8_t*)r + 24) & rmask;  // reader_id @24: the reader word
+  g[4] = word;
 }
 __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
   h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
@@ -144,6 +150,28 @@ __device__ __forceinline__ uint32_t wslot_find(const uint64_t* wkey, uint64_t h)
   return NONE;
 }
 
+// Which DATA_FRAG records (that pass) the batch assembles, and their reader word (FragSel)
+__device__ __forceinline__ bool frag_select(const FragSel& sel, const rtps_record* r, const uint4& ra, const uint4& rb,
+                                            uint32_t& word) {
+  word = 0;
+  if (sel.mode == 0) return true;
+  if (sel.mode == 2) { word = rb.z; return true; }  // an expanded copy: its reader_id
+  // mode 1: the record's one target reader (Domain::handle_event, dp_event_loop.rs:266-327)
+  const uint32_t route = (rb.w >> 16) & 0xffu;
+  if (!(route & RTPS_ROUTE_TARGETED) || (route & RTPS_ROUTE_BUILTIN)) return false;
+  uint32_t r2 = 0;
+  const uint32_t set = rt_classify<false>(sel.rt, nullptr, ra.z, ra.w, rb.x, rb.y, r2);
+  if (set == RTPS_NO_TARGET || sel.rt.set_first[set] == sel.rt.set_first[set + 1]) return false;
+  const uint32_t slot = sel.rt.set_ent[sel.rt.set_first[set]].reader_slot;
+  if (sel.any_life && (route & RTPS_ROUTE_TS_VALID)) {  // handle_datafrag_msg's Lifespan drop (reader.rs:578-589)
+    const int64_t L = sel.life[slot];
+    const uint64_t src = ((uint64_t)r->ts_sec << 32) | r->ts_frac;
+    if (L != INT64_MAX && L < (int64_t)(sel.recv_ticks - src)) return false;
+  }
+  word = slot | 0x10000u;
+  return true;
+}
+
 // ---- 1: sort keys ----
 // Also collects the batch's writers (step 2's input): each wave dedupes its
 // records' writers with ballots (one LDS insert per distinct writer, by its first
@@ -176,7 +204,7 @@ __global__ __launch_bounds__(FT) void k_keys(const rtps_record* recs, const uint
                                              uint32_t* keys, uint32_t* vals, uint32_t* rec_epoch, uint32_t* dmark,
                                              uint8_t* seen, uint64_t* ctr, uint32_t* new_ptable, uint64_t* wkey,
                                              uint32_t* wfirst, const uint32_t* wF, uint64_t* wst_key,
-                                             uint32_t* wst_rec, uint32_t rmask) {
+                                             uint32_t* wst_rec, FragSel sel, uint32_t* rword) {
   __shared__ unsigned long long s_wk[KW_SLOTS];
   __shared__ uint32_t s_wr[KW_SLOTS];
   __shared__ uint32_t s_nst;
@@ -214,13 +242,16 @@ __global__ __launch_bounds__(FT) void k_keys(const rtps_record* recs, const uint
       if (i < max) {
         uint32_t k = SENT;
         const uint32_t kind = (ra[kk].y >> 16) & 0xffu, route = (rb[kk].w >> 16) & 0xffu;
-        if (i < n && kind == RTPS_DATA_FRAG && (route & RTPS_ROUTE_PASS)) {  // is_frag
-          const uint32_t g[KW] = {ra[kk].z, ra[kk].w, rb[kk].x, rb[kk].y, rb[kk].z & rmask};  // guid_of
+        uint32_t word = 0;
+        if (i < n && kind == RTPS_DATA_FRAG && (route & RTPS_ROUTE_PASS) &&
+            frag_select(sel, recs + i, ra[kk], rb[kk], word)) {  // is_frag
+          const uint32_t g[KW] = {ra[kk].z, ra[kk].w, rb[kk].x, rb[kk].y, word};  // guid_of
           k = key_hash(g, (int64_t)rs[kk]);
           wh = writer_hash(g);
           f = true;
         }
         keys[i] = k;
+        rword[i] = word;
         if (vals) vals[i] = (uint32_t)i;  // the device sort's values (the bucket sort derives them)
         rec_epoch[i] = NONE;  // per-batch state, reset here instead of three memsets
         dmark[i] = NONE;
@@ -362,8 +393,11 @@ struct WalkArgs {
   uint32_t* dmark;
   uint8_t* seen;  // per position: consumed by a walk pass (collision runs)
   uint64_t* ctr;
-  uint32_t rmask;  // reader word mask of the assembly keys (0: one assembler per writer)
+  const uint32_t* rword;  // per position: the reader word of its assembly key (k_keys)
 };
+__device__ __forceinline__ void guid_at(const WalkArgs& A, uint32_t ri, uint32_t g[KW]) {
+  guid_of(A.recs + ri, A.rword[ri], g);
+}
 
 // FragmentAssembler's fragment size of writer slot ws: fixed in an earlier batch, or
 // its first DATA_FRAG in this one (k_keys' atomicMin), or 0 for no writer
@@ -415,7 +449,7 @@ __device__ void walk_run_serial(const WalkArgs& A, uint64_t p, uint64_t p1) {
     if (A.seen[q0]) continue;
     uint32_t g[KW];
     const rtps_record* r0 = A.recs + A.svals[q0];
-    guid_of(r0, g, A.rmask);
+    guid_at(A, A.svals[q0], g);
     const int64_t sn = r0->sn;
     const uint64_t wh = writer_hash(g);
     const uint32_t ws = wslot_find(A.wkey, wh);
@@ -443,7 +477,7 @@ __device__ void walk_run_serial(const WalkArgs& A, uint64_t p, uint64_t p1) {
       const uint32_t ri = A.svals[q];
       const rtps_record* r = A.recs + ri;
       uint32_t h[KW];
-      guid_of(r, h, A.rmask);
+      guid_at(A, ri, h);
       if (!same_key(g, sn, h, r->sn)) continue;
       A.seen[q] = 1;
       const uint32_t ds = r->u.frag.data_size, fsz = r->u.frag.frag_size;
@@ -510,7 +544,7 @@ __device__ __forceinline__ LaneRec lane_rec(const WalkArgs& A, uint64_t p, uint6
   if (L.act) {
     L.ri = A.svals[p];
     const rtps_record* r = A.recs + L.ri;
-    guid_of(r, L.g, A.rmask);
+    guid_at(A, L.ri, L.g);
     L.sn = r->sn;
     L.fs = r->u.frag.frag_start;
     L.fis = r->u.frag.frags_in_sub;
@@ -600,7 +634,7 @@ __device__ void walk_run_wave(const WalkArgs& A, uint64_t p0, uint64_t p1, uint3
   }
   const rtps_record* r0 = A.recs + A.svals[p0];
   uint32_t g[KW];
-  guid_of(r0, g, A.rmask);
+  guid_at(A, A.svals[p0], g);
   const int64_t sn = r0->sn;
   bool ok = true;
   for (uint64_t c = p0; c < p1 && ok; c += 64) {
@@ -609,7 +643,7 @@ __device__ void walk_run_wave(const WalkArgs& A, uint64_t p0, uint64_t p1, uint3
     if (p < p1) {
       const rtps_record* r = A.recs + A.svals[p];
       uint32_t h[KW];
-      guid_of(r, h, A.rmask);
+      guid_at(A, A.svals[p], h);
       const uint32_t ds = r->u.frag.data_size, fsz = r->u.frag.frag_size;
       bad = !same_key(g, sn, h, r->sn) || (uint64_t)(ds / fsz + (ds % fsz > 0)) > (uint64_t)BMW * 32;
     }
@@ -1270,7 +1304,7 @@ struct FragState {
   // per-batch scratch (grown on demand)
   uint64_t cap = 0;
   uint32_t *keys = nullptr, *vals = nullptr, *skeys = nullptr, *svals = nullptr;
-  uint32_t *rec_epoch = nullptr, *dmark = nullptr, *special = nullptr;
+  uint32_t *rec_epoch = nullptr, *dmark = nullptr, *special = nullptr, *rword = nullptr;
   uint32_t* tcnt = nullptr;   // per 4096-position tile: completions, then their exclusive scan
   uint64_t* tbytes = nullptr; // per tile: heap bytes, then their exclusive scan
   uint8_t* seen = nullptr;
@@ -1289,9 +1323,9 @@ struct FragState {
 
 static void free_scratch(FragState* s) {
   void* ptrs[] = {s->keys, s->vals, s->skeys, s->svals, s->rec_epoch, s->dmark, s->tcnt, s->special,
-                  s->seen, s->tbytes, s->epochs, s->pool, s->tmp, s->bh, s->bk, s->bk2, s->desc};
+                  s->seen, s->tbytes, s->epochs, s->pool, s->tmp, s->bh, s->bk, s->bk2, s->desc, s->rword};
   for (void* p : ptrs) if (p) (void)hipFree(p);
-  s->keys = s->vals = s->skeys = s->svals = s->rec_epoch = s->dmark = s->tcnt = s->special = nullptr;
+  s->keys = s->vals = s->skeys = s->svals = s->rec_epoch = s->dmark = s->tcnt = s->special = s->rword = nullptr;
   s->seen = nullptr; s->tbytes = nullptr; s->epochs = nullptr; s->pool = nullptr; s->tmp = nullptr;
   s->bh = nullptr; s->bk = s->bk2 = nullptr; s->desc = nullptr;
   s->cap = 0; s->tmp_bytes = 0;
@@ -1305,6 +1339,7 @@ static bool grow(FragState* s, uint64_t max, hipStream_t st) {
   bool ok = hipMalloc(&s->keys, n * 4) == hipSuccess && hipMalloc(&s->vals, n * 4) == hipSuccess &&
             hipMalloc(&s->skeys, n * 4) == hipSuccess && hipMalloc(&s->svals, n * 4) == hipSuccess &&
             hipMalloc(&s->rec_epoch, n * 4) == hipSuccess && hipMalloc(&s->dmark, n * 4) == hipSuccess &&
+            hipMalloc(&s->rword, n * 4) == hipSuccess &&
             hipMalloc(&s->tcnt, (n / PTILE + 1) * 4) == hipSuccess && hipMalloc(&s->special, n * 4) == hipSuccess &&
             hipMalloc(&s->seen, n) == hipSuccess && hipMalloc(&s->tbytes, (n / PTILE + 1) * 8) == hipSuccess;
   s->pool_words = 4 * n + PWORDS;
@@ -1363,7 +1398,7 @@ int rtps_frag_state_reset(FragState* s, hipStream_t st) {
 
 int rtps_frag_assemble(FragState* s, hipStream_t st, const uint8_t* arena, uint64_t arena_len,
                        const uint64_t* dgram_off, const rtps_record* records, const uint64_t* n_records,
-                       uint64_t max_records, const rtps_frag_out* out, uint32_t rmask, const uint32_t* emap) {
+                       uint64_t max_records, const rtps_frag_out* out, const FragSel& sel, const uint32_t* emap) {
   if (max_records > 0x7fffffffull) return RTPS_RX_ETOOBIG;
   const uint64_t max = max_records ? max_records : 1;
   if (!grow(s, max, st)) return RTPS_RX_ENOMEM;
@@ -1376,7 +1411,7 @@ int rtps_frag_assemble(FragState* s, hipStream_t st, const uint8_t* arena, uint6
   const bool bsort = s->sort_mode == 0 && max <= rtps_bsort::MAX_N;
   hipLaunchKernelGGL(k_keys, dim3(gk), dim3(FT), 0, st, records, n_records, max, s->keys, bsort ? nullptr : s->vals,
                      s->rec_epoch, s->dmark, s->seen, s->ctr, s->ptable[nw], s->wkey, s->wfirst, s->wF, s->wst_key,
-                     s->wst_rec, rmask);
+                     s->wst_rec, sel, s->rword);
   size_t tb = s->tmp_bytes;
   const WregSide wreg{WREG_WG, s->wst_key, s->wst_rec, gk * WST, s->wkey, s->wfirst, s->wF, s->ctr};
   if (bsort) {  // the writers' merge rides on the sort's column-scan launch
@@ -1390,7 +1425,7 @@ int rtps_frag_assemble(FragState* s, hipStream_t st, const uint8_t* arena, uint6
                        s->wF, s->ctr);
   }
   WalkArgs A{records, s->skeys, s->svals, max, s->wkey, s->wF, s->wfirst, s->pend[o], s->ptable[o], s->pbits[o], s->epochs,
-             s->special, s->pool, s->pool_words, s->rec_epoch, s->dmark, s->seen, s->ctr, rmask};
+             s->special, s->pool, s->pool_words, s->rec_epoch, s->dmark, s->seen, s->ctr, s->rword};
   hipLaunchKernelGGL(k_walk, dim3((uint32_t)hmin((max + FT - 1) / FT, 8192)), dim3(FT), 0, st, A);
   const uint64_t tiles = (max + PTILE - 1) / PTILE;
   hipLaunchKernelGGL(k_place_tiles, dim3((uint32_t)tiles), dim3(FT), 0, st, s->dmark, s->epochs, max, s->tcnt,

@@ -71,7 +71,6 @@ constexpr uint32_t WW = W / 32;             // bitmap words per proxy
 constexpr uint32_t ECAP_MAX = 1u << 14;     // writer proxies
 enum : uint8_t { EV_NONE = 0, EV_SAMPLE = 1, EV_HB = 2, EV_GAP = 3 };
 // counters: window overflow, selected HEARTBEATs, selected deliveries, records of the batch, then
-// the HEARTBEAT / GAP / event counts in 64 slot triples (one atomic per block, spread: no hot address)
 // the HEARTBEAT / GAP / event / proxy-less sample counts in 64 slot quads (one atomic per block, spread: no hot address)
 enum { C_OVF = 0, C_NSEL, C_NDEL, C_NREC, C_SPREAD, C_COUNT = C_SPREAD + 4 * 64 };
 // event metadata: reader slot | flags << 16 (EVF_*)

@@ -2066,10 +2066,36 @@ int rtps_rx_frag_assemble(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_l
     if (!c->frag) return RTPS_RX_ENOMEM;
   }
   const ReaderDev rd = rt_dev(c->readers);
+  FragSel sel;
+  memset(&sel, 0, sizeof sel);
   if (rd.gkeys == nullptr)  // no readers: one assembler per writer for every DATA_FRAG that passes
     return rtps_frag_assemble(c->frag, c->stream, arena, arena_len, dgram_off, records, n_records, max_records, out,
-                              0u, nullptr);
-  // readers: one assembler per (reader, writer), over the batch expanded per target reader
+                              sel, nullptr);
+  if (!c->life) {
+    if (hipMalloc(&c->life, 65536 * sizeof(int64_t)) != hipSuccess) return RTPS_RX_ENOMEM;
+    std::vector<int64_t> none(65536, NO_LIFESPAN);
+    if (hipMemcpy(c->life, none.data(), 65536 * sizeof(int64_t), hipMemcpyHostToDevice) != hipSuccess)
+      return RTPS_RX_EHIP;
+  }
+  uint64_t now_ns = c->recv_ns;
+  if (!now_ns) {  // Timestamp::now() (structure/time.rs:58-65): the host's wall clock at this batch
+    struct timespec ts;
+    clock_gettime(CLOCK_REALTIME, &ts);
+    now_ns = (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+  }
+  // Timestamp::from_nanos (time.rs:78-83) as ticks
+  const uint64_t recv_ticks = ((now_ns / 1000000000ull) << 32) + (((now_ns % 1000000000ull) << 32) / 1000000000ull);
+  sel.rt = rd;
+  sel.life = c->life;
+  sel.any_life = c->any_life ? 1u : 0u;
+  sel.recv_ticks = recv_ticks;
+  if (rd.max_set <= 1u) {  // every record reaches one reader at most: select it in place, no copies
+    sel.mode = 1;
+    return rtps_frag_assemble(c->frag, c->stream, arena, arena_len, dgram_off, records, n_records, max_records, out,
+                              sel, nullptr);
+  }
+  // larger target sets: one assembler per (reader, writer), over the batch expanded per target reader
+  sel.mode = 2;
   const uint64_t max_x = max_records * (rd.max_set ? rd.max_set : 1u);
   if (max_x > 0x7fffffffull) return RTPS_RX_ETOOBIG;
   if (max_records > c->fx_cap || max_x > c->fx_xcap || !c->fx_n) {
@@ -2090,20 +2116,6 @@ int rtps_rx_frag_assemble(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_l
     c->fx_cap = m;
     c->fx_xcap = x;
   }
-  if (!c->life) {
-    if (hipMalloc(&c->life, 65536 * sizeof(int64_t)) != hipSuccess) return RTPS_RX_ENOMEM;
-    std::vector<int64_t> none(65536, NO_LIFESPAN);
-    if (hipMemcpy(c->life, none.data(), 65536 * sizeof(int64_t), hipMemcpyHostToDevice) != hipSuccess)
-      return RTPS_RX_EHIP;
-  }
-  uint64_t now_ns = c->recv_ns;
-  if (!now_ns) {  // Timestamp::now() (structure/time.rs:58-65): the host's wall clock at this batch
-    struct timespec ts;
-    clock_gettime(CLOCK_REALTIME, &ts);
-    now_ns = (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
-  }
-  // Timestamp::from_nanos (time.rs:78-83) as ticks
-  const uint64_t recv_ticks = ((now_ns / 1000000000ull) << 32) + (((now_ns % 1000000000ull) << 32) / 1000000000ull);
   const uint64_t m = max_records ? max_records : 1;
   FragX a{records, n_records, max_records, rd, c->life, recv_ticks, c->any_life ? 1u : 0u, c->fx_cnt, c->fx_off,
           c->fx_rec, c->fx_emap, c->fx_n};
@@ -2119,8 +2131,8 @@ int rtps_rx_frag_assemble(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_l
     hipLaunchKernelGGL(frag_x_fill, dim3(g), dim3(TILE), 0, c->stream, a);
   }
   if (hipGetLastError() != hipSuccess) return RTPS_RX_EHIP;
-  return rtps_frag_assemble(c->frag, c->stream, arena, arena_len, dgram_off, c->fx_rec, c->fx_n, max_x, out,
-                            0xffffffffu, c->fx_emap);
+  return rtps_frag_assemble(c->frag, c->stream, arena, arena_len, dgram_off, c->fx_rec, c->fx_n, max_x, out, sel,
+                            c->fx_emap);
 }
 
 /* per-reader Lifespan QoS for the DataFrag assembly (reader.rs:578-589): lifespan_ns < 0 = none */

@@ -218,6 +218,14 @@ def reader_scenario_readers(with_c):
     return Readers(readers, proxies)
 
 
+def reader_scenario_single_readers():
+    """Readers A (11) of W1 and B (12) of W2: every target set holds one reader (the
+    library selects in place, without the per-target expansion)."""
+    from rtps_rx.records import Readers
+    g1, g2 = RS_PREFIX[0] + RS_WRITER[0], RS_PREFIX[1] + RS_WRITER[1]
+    return Readers([(RS_READER[11], 11, 0), (RS_READER[12], 12, 0)], [(g1, 0), (g2, 1)])
+
+
 def info_ts_sub(sec, frac, le=True, invalidate=False):
     e = "<" if le else ">"
     if invalidate:

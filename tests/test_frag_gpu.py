@@ -191,13 +191,15 @@ def test_bucket_sort_oversized_buckets(rx, sort):
     assert g[3] >= 9000
 
 
-@pytest.mark.parametrize("ingest_path", [1, 2])
-def test_per_reader_assembly_and_ingest(rx, ingest_path):
+@pytest.mark.parametrize("ingest_path,sets", [(1, "multi"), (2, "multi"), (1, "single"), (2, "single")])
+def test_per_reader_assembly_and_ingest(rx, ingest_path, sets):
     """two readers of one writer, one with a Lifespan (reader.rs:578-589),
     a reader added mid-stream, a writer changing its fragment size: every (reader, writer)
     pair has its own assembler (reader.rs:617-619, 638-647).  Samples (with their reader),
     heap bytes, deliveries and every proxy's ack_base bit-exact against the oracle, on both
-    ingest paths."""
+    ingest paths.  sets "single": the first batch's target sets hold one reader each (the
+    in-place selection), the second one's two (the per-target expansion), with fragments
+    pending across the switch."""
     from rtps_rx.records import FRAG_SAMPLE_DTYPE, DELIVERY_DTYPE, max_records
     dev = torch.device("cuda", 0)
     rx.debug_ingest_path(ingest_path)
@@ -206,7 +208,8 @@ def test_per_reader_assembly_and_ingest(rx, ingest_path):
     fa = oracle.FragAssembler()
     ing = None
     per_reader = {}
-    batches = [(frag_ref.reader_scenario_readers(False), frag_ref.reader_scenario(400, 1, 1, 64)),
+    first = frag_ref.reader_scenario_readers(False) if sets == "multi" else frag_ref.reader_scenario_single_readers()
+    batches = [(first, frag_ref.reader_scenario(400, 1, 1, 64)),
                (frag_ref.reader_scenario_readers(True), frag_ref.reader_scenario(600, 2, 200, 32))]
     for k, (rd, dgrams) in enumerate(batches):
         rx.set_readers(rd)
@@ -246,4 +249,6 @@ def test_per_reader_assembly_and_ingest(rx, ingest_path):
         assert dels.tobytes() == o_dels.tobytes(), f"batch {k}: deliveries differ"
         assert np.array_equal(iouts["accept"][:len(recs)].cpu().numpy(), o_acc)
         assert np.array_equal(iouts["ack_base"][:rd.n_proxies].cpu().numpy(), o_ack)
-    assert per_reader[11] > per_reader[12] > 0 and per_reader.get(13, 0) > 0
+    assert per_reader[11] > 0 and per_reader[12] > 0 and per_reader.get(13, 0) > 0
+    if sets == "multi":
+        assert per_reader[11] > per_reader[12]
