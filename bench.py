@@ -345,34 +345,38 @@ def frag_leg(rx, arena, off_t, outs, n_rec, recs, stream, steps):
     ns = int(fouts["n_samples"].item())
     # algorithmic bytes: each fragment's payload read once and written once + its 64-B record read
     alg = 2 * payload + 64 * int(frag.sum())
-    return {"kernel": "rtps_frag_assemble (sort + walk + place + copy launches)", "ms": ms,
+    return fouts, {"kernel": "rtps_frag_assemble (sort + walk + place + copy launches)", "ms": ms,
             "samples": ns, "pending": int(fouts["n_pending"].item()), "fragments": int(frag.sum()),
             "samples_per_s": ns / (ms * 1e-3), "gib_per_s_assembled": int(fouts["heap_used"].item()) / (ms * 1e-3) / 2**30,
             "alg_bytes_per_launch": alg, "achieved_gbs": alg / (ms * 1e-3) / 1e9,
             "frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
 
-def ingest_leg(rx, arena, off_t, outs, n_rec, recs, n_entries, stream, steps):
+def ingest_leg(rx, arena, off_t, outs, n_rec, recs, n_entries, stream, steps, fouts=None):
     """History-cache ingest (§8f rank 2) of this batch's samples / HEARTBEATs / GAPs,
     timed separately (HIP events on the launch stream).  Every step starts from
     fresh writer proxies (the reset is outside the timed region), so every step
-    does the same work: all first copies accepted."""
+    does the same work: all first copies accepted.  fouts: the batch's reassembled
+    DataFrag samples (C4), ingested at their completing records."""
     iouts = rx.alloc_ingest_outputs(n_rec, n_entries)
+    fa = (fouts,) if fouts is not None else ()
     for _ in range(2):
         rx.ingest_reset()
-        rx.ingest(arena, off_t, outs, iouts)
+        rx.ingest(arena, off_t, outs, iouts, *fa)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     torch.cuda.synchronize()
     for a, b in ev:
         rx.ingest_reset()
         a.record(stream)
-        rx.ingest(arena, off_t, outs, iouts)
+        rx.ingest(arena, off_t, outs, iouts, *fa)
         b.record(stream)
     torch.cuda.synchronize()
     ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     na = int(iouts["n_accepted"].item())
     k = recs["kind"]
     events = int((((recs["route"] & 0x21) == 0x21) & np.isin(k, (DATA, HEARTBEAT, GAP))).sum())
+    if fouts is not None:  # + the completed DataFrag samples
+        events += int(fouts["n_samples"].item())
     # algorithmic bytes: every record read once (64 B), 1 accept byte written per record, 8 B per
     # delivery, per event 8 B of proxy state read and 4 B of change-set bits touched
     alg = n_rec * (64 + 1) + 8 * na + 12 * events
@@ -879,10 +883,12 @@ def main():
         result["pipeline_with_ingest"] = pipeline
     if world == 1 and not args.no_cdr:
         result["cdr_decode"] = cdr_decode_leg(rx, args.workload, arena, off_t, outs, n_rec, stream, args.steps)
+    fouts = None
     if world == 1 and not args.no_frag and args.workload == "C4" and recs is not None:
-        result["frag_assemble"] = frag_leg(rx, arena, off_t, outs, n_rec, recs, stream, args.steps)
+        fouts, result["frag_assemble"] = frag_leg(rx, arena, off_t, outs, n_rec, recs, stream, args.steps)
     if world == 1 and not args.no_ingest and n_matched_writers:
-        result["ingest"] = ingest_leg(rx, arena, off_t, outs, n_rec, recs, n_matched_writers, stream, args.steps)
+        result["ingest"] = ingest_leg(rx, arena, off_t, outs, n_rec, recs, n_matched_writers, stream, args.steps,
+                                      fouts=fouts)
     if world == 1 and not args.no_c1:
         result["c1_loopback"] = c1_loopback(dev, stream)
         # the same subscriber fed by 4 publisher threads: what the receive loop sustains when

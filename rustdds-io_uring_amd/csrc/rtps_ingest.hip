@@ -66,6 +66,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr uint32_t IT = 256;
 constexpr uint32_t NONE = 0xffffffffu;
+#ifndef RTPS_CLS_ABL  // timing-only ablations of the classify pass (variant builds): 1 GAP
+#define RTPS_CLS_ABL 0  // bitmap reads, 2 packed-event stores, 4 target-set probes, 8 sort-pair / accept stores
+#endif
 constexpr uint32_t W = RTPS_INGEST_WINDOW;  // sequence numbers tracked per proxy
 constexpr uint32_t WW = W / 32;             // bitmap words per proxy
 constexpr uint32_t ECAP_MAX = 1u << 14;     // writer proxies
@@ -279,8 +282,9 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
         }
         if (ev != EV_NONE) {
           uint32_t r2 = 0;
-          set = lds ? rt_classify<true>(t, s_rt, q0[2], q0[3], q1[0], q1[1], r2)
-                    : rt_classify<false>(t, s_rt, q0[2], q0[3], q1[0], q1[1], r2);
+          set = (RTPS_CLS_ABL & 4) ? 0u
+                : lds ? rt_classify<true>(t, s_rt, q0[2], q0[3], q1[0], q1[1], r2)
+                      : rt_classify<false>(t, s_rt, q0[2], q0[3], q1[0], q1[1], r2);
           if (set == NONE) ev = EV_NONE;
           user_kind = (q1[1] >> 24 & 0xf0u) == 0u;  // EntityKind::is_user_defined (guid.rs:168-170)
         }
@@ -309,7 +313,7 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
     ne += cnt;
     if (IDENT) {  // at most one event: write it at index i
       const uint8_t evi = cnt ? ev : EV_NONE;
-      x.emeta[i] = meta;
+      if (!(RTPS_CLS_ABL & 8)) x.emeta[i] = meta;
       if (!FAST) x.erec[i] = (uint32_t)i;  // (the per-proxy identity path reads no event -> record map)
       if (!FAST) {  // (the per-proxy identity path reads the packed events instead)
         x.evt[i] = evi;
@@ -320,9 +324,11 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
         x.hkey[i] = evi == EV_HB ? 1u : 0u;  // selection flag of the HEARTBEAT compaction
       } else {
         const bool px = evi != EV_NONE && ent != NONE;
-        x.hkey[i] = px ? ent : t.n_proxies;  // sort pairs: (proxy, slot); n_proxies sorts last
-        x.sval[i] = (uint32_t)i;
-        fo.acc[i] = (evi == EV_SAMPLE && ent == NONE) ? 1 : 0;  // proxy-less samples (reader.rs:734-739)
+        if (!(RTPS_CLS_ABL & 8)) {
+          x.hkey[i] = px ? ent : t.n_proxies;  // sort pairs: (proxy, slot); n_proxies sorts last
+          x.sval[i] = (uint32_t)i;
+          fo.acc[i] = (evi == EV_SAMPLE && ent == NONE) ? 1 : 0;  // proxy-less samples (reader.rs:734-739)
+        }
         if (px) {
           PEv P;
           P.sn = sn;
@@ -338,14 +344,14 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
             const bool le = (fl & 1u) != 0u;
             P.m |= (le ? PM_LE : 0u) | (nbits << 8);
             P.bw = fo.dgram_off[q0[0]] + (q3[1] & 0xffffu);  // dgram_idx, u.gap.bitmap_off
-            if (nbits <= 64u) {
+            if (nbits <= 64u && !(RTPS_CLS_ABL & 1)) {
               const uint8_t* bp = fo.arena + P.bw;
               const uint32_t w0 = nbits ? rd32(bp, le) : 0u, w1 = nbits > 32u ? rd32(bp + 4, le) : 0u;
               P.bw = (uint64_t)w0 | ((uint64_t)w1 << 32);
               P.m |= PM_INL;
             }
           }
-          fo.pev[i] = P;
+          if (!(RTPS_CLS_ABL & 2)) fo.pev[i] = P;
         }
       }
     } else {
@@ -719,7 +725,9 @@ __global__ __launch_bounds__(IT) void k_merge(const rtps_record* recs, const uin
 }
 
 // ---- 7 state: one workgroup per proxy ----
-__global__ __launch_bounds__(IT) void k_state(uint32_t n_entries, Scratch x, State s, bool reliable, int64_t* ack_out) {
+// (workgroup 0 also reports the window-overflow count: every decision is made by now)
+__global__ __launch_bounds__(IT) void k_state(uint32_t n_entries, Scratch x, State s, bool reliable, int64_t* ack_out,
+                                              uint64_t* ovf_out) {
   __shared__ uint32_t sh[WW];
   __shared__ uint32_t s_first;
   const uint32_t e = blockIdx.x, tid = threadIdx.x;
@@ -767,6 +775,7 @@ __global__ __launch_bounds__(IT) void k_state(uint32_t n_entries, Scratch x, Sta
     s.lo[e] = nlo;
     s.hbc[e] = hbc;
     if (ack_out) ack_out[e] = nb;
+    if (e == 0 && ovf_out) *ovf_out = s.ctr[C_OVF];
   }
 }
 
@@ -1472,7 +1481,9 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
   else if (nev && !per_proxy)
     hipLaunchKernelGGL(k_merge, dim3(gv), dim3(IT), 0, st, records, arena, dgram_off, nev, x, S, n_gap > 0);
   if (t.n_proxies && !per_proxy)
-    hipLaunchKernelGGL(k_state, dim3(t.n_proxies), dim3(IT), 0, st, t.n_proxies, x, S, have_hb, out->ack_base);
-  hipLaunchKernelGGL(k_finish, dim3(1), dim3(1), 0, st, S.ctr, out->n_window_overflow);
+    hipLaunchKernelGGL(k_state, dim3(t.n_proxies), dim3(IT), 0, st, t.n_proxies, x, S, have_hb, out->ack_base,
+                       out->n_window_overflow);
+  else
+    hipLaunchKernelGGL(k_finish, dim3(1), dim3(1), 0, st, S.ctr, out->n_window_overflow);
   return hipGetLastError() == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP;
 }
