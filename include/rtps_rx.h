@@ -311,20 +311,22 @@ int rtps_rx_bucket_by_writer_padded(rtps_rx_ctx* ctx, const rtps_record* recs, c
                                     uint64_t max_records, uint32_t n_dest, uint64_t cap, rtps_record* out,
                                     uint64_t* dest_counts);
 
-/* Exchange descriptors (>= 2 GPUs): the compact form of a matched writer's
+/* Exchange descriptors (>= 2 GPUs): the compact form of a targeted writer's
  * record that crosses xGMI instead of the 64-byte record.  Only records with
- * RTPS_ROUTE_MATCHED are exchanged (writer submessages of writers with a
- * proxy: what a reader's per-writer state consumes, io_uring/rtps/reader.rs
- * handle_*_msg).  Owner GPU = writer set index % n_dest: writers are spread
- * round-robin in the order the proxies list them, so the owners are balanced
- * whatever the GUID hash does; payloads and full records stay on the source
- * GPU (rec_idx). */
+ * RTPS_ROUTE_MATCHED or RTPS_ROUTE_TARGETED are exchanged (writer submessages
+ * that reach some reader, with or without a proxy: what a reader's per-writer
+ * state consumes, io_uring/rtps/reader.rs handle_*_msg, and the proxy-less
+ * samples of non-user-defined writers it accepts, :734-739).  Owner GPU =
+ * target set index % n_dest (writer sets first, in the order the proxies list
+ * them, then entity sets): writers are spread round-robin, so the owners are
+ * balanced whatever the GUID hash does; payloads and full records stay on the
+ * source GPU (rec_idx). */
 typedef struct rtps_xdesc {
   int64_t sn;            /* writer sequence number */
   uint32_t rec_idx;      /* index of the full record in the source rank's parse output */
-  uint32_t writer_kind;  /* writer set index << 8 | submessage kind */
+  uint32_t writer_kind;  /* target set index << 8 | submessage kind */
 } rtps_xdesc;
-/* Stable partition of the MATCHED records' descriptors into n_dest buckets of
+/* Stable partition of the targeted records' descriptors into n_dest buckets of
  * cap descriptors each (out[d*cap, (d+1)*cap)); dest_counts as in
  * rtps_rx_bucket_by_writer_padded.  Needs readers (RTPS_RX_EINVAL without). */
 int rtps_rx_bucket_descriptors(rtps_rx_ctx* ctx, const rtps_record* recs, const uint64_t* n_records,

@@ -1491,14 +1491,17 @@ __device__ __forceinline__ uint32_t owner_of(const rtps_record* r, uint32_t n_de
   return owner_hash(d[2], d[3], d[4], d[5]) % n_dest;
 }
 
-// descriptor mode: MATCHED writer records only, owner = writer set index % n_dest
+// descriptor mode: writer records that reach a reader (MATCHED, or TARGETED by entity id
+// only: the proxy-less samples a reader accepts from non-user-defined writers,
+// reader.rs:734-739), owner = target set index % n_dest
 struct DescOwner {
   ReaderDev rt;
 };
 __device__ __forceinline__ uint32_t desc_entry(const rtps_record* r, const DescOwner& m) {
-  if (!(r->route & RTPS_ROUTE_MATCHED)) return 0xffffffffu;
+  if (!(r->route & (RTPS_ROUTE_MATCHED | RTPS_ROUTE_TARGETED))) return 0xffffffffu;
   const uint32_t* d = reinterpret_cast<const uint32_t*>(r);
-  const uint32_t t = rt_writer_set<false>(m.rt, nullptr, d[2], d[3], d[4], d[5]);
+  uint32_t r2 = 0;
+  const uint32_t t = rt_classify<false>(m.rt, nullptr, d[2], d[3], d[4], d[5], r2);
   return t == RTPS_NO_TARGET ? 0xffffffffu : t;
 }
 template <bool DESC>

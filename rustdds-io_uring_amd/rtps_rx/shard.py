@@ -11,8 +11,9 @@ this is the only collective of the path.
 What crosses xGMI (item):
   * "records": the 64-byte records of every writer/reader submessage, owner =
     GUID hash % world (rtps_rx_bucket_by_writer[_padded]);
-  * "descriptors": 16-byte rtps_xdesc of the MATCHED records only, owner =
-    writer set index % world (rtps_rx_bucket_descriptors): 4x fewer
+  * "descriptors": 16-byte rtps_xdesc of the records that reach a reader (MATCHED, or
+    TARGETED by entity id only), owner = target set index % world
+    (rtps_rx_bucket_descriptors): 4x fewer
     bytes, and owners balanced by the table order instead of a hash of a few
     writer GUIDs.  Full records and payloads stay on the source GPU.
 

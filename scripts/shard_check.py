@@ -79,7 +79,18 @@ if desc:
     for r in range(world):
         a, o, l = oracle.gen(oracle.WL_C3, n, first_idx=r * stride)
         _, recs, _, _ = oracle.parse(a, o, l, match_table=table)
-        exp.append(desc_bucket_np(recs, [bytes(t["writer_guid"]) for t in table], world)[rank])
+        # the target set numbers of rank r's records (TARGETED-only records go to their entity
+        # set's owner): rank r's chunk parsed again here with the same table
+        off_r, ln_r, size_r = rtps_rx.gen_layout(rtps_rx.WL_C3, n, first_idx=r * stride)
+        arena_r = torch.zeros(size_r, dtype=torch.uint8, device=dev)
+        off_rt = torch.from_numpy(off_r.view(np.int64)).to(dev)
+        ln_rt = torch.from_numpy(ln_r.view(np.int32)).to(dev)
+        outs_r = rx.alloc_outputs(n, rtps_rx.max_records(ln_r))
+        rx.generate(rtps_rx.WL_C3, arena_r, off_rt, ln_rt, n, first_idx=r * stride)
+        rx.parse_batch_device(arena_r, off_rt, ln_rt, n, outs_r)
+        torch.cuda.synchronize(dev)
+        sets = outs_r["target"][:len(recs)].cpu().numpy().view(np.uint32)
+        exp.append(desc_bucket_np(recs, [bytes(t["writer_guid"]) for t in table], world, entity_sets=sets)[rank])
     exp = np.concatenate(exp)
 else:
     got = got.cpu().numpy().reshape(-1).view(RECORD_DTYPE)

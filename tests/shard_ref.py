@@ -30,20 +30,27 @@ def bucket_np(recs, world):
     return recs[order], counts
 
 
-def desc_bucket_np(recs, table_guids, world):
+def desc_bucket_np(recs, table_guids, world, entity_sets=None):
     """numpy reference of rtps_rx_bucket_descriptors: MATCHED records of table writers,
-    owner = writer set index (rank of the GUID's first appearance) % world, stable; returns
-    (list per owner of XDESC rows)."""
-    from rtps_rx.records import XDESC_DTYPE, ROUTE_MATCHED
+    owner = writer set index (rank of the GUID's first appearance) % world, and TARGETED-only
+    records (a reader contains the writer's entity id, no proxy for the GUID) with owner =
+    their entity set index % world (entity_sets[i]: the record's target set, numbered after
+    the writer sets); stable; returns (list per owner of XDESC rows)."""
+    from rtps_rx.records import XDESC_DTYPE, ROUTE_MATCHED, ROUTE_TARGETED
     index = {}
     for g in table_guids:
         index.setdefault(bytes(g), len(index))
     out = [[] for _ in range(world)]
     for i, r in enumerate(recs):
-        if not (int(r["route"]) & ROUTE_MATCHED):
-            continue
-        k = index.get(bytes(r["prefix"]) + bytes(r["writer_id"]))
-        if k is None:
+        route = int(r["route"])
+        if route & ROUTE_MATCHED:
+            k = index.get(bytes(r["prefix"]) + bytes(r["writer_id"]))
+            if k is None:
+                continue
+        elif route & ROUTE_TARGETED and entity_sets is not None:
+            k = int(entity_sets[i])
+            assert k >= len(index), "a TARGETED-only record's set is an entity set"
+        else:
             continue
         out[k % world].append((int(r["sn"]), i, (k << 8) | int(r["kind"])))
     return [np.array(o, dtype=XDESC_DTYPE) for o in out]

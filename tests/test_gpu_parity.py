@@ -483,7 +483,14 @@ def test_bucket_descriptors_matches_reference(rx, world):
         torch.cuda.synchronize()
         rx.parse_batch_device(A, O, L, len(ln), outs)
         _, recs, _, _ = oracle.parse(arena, off, ln, match_table=tbl)
-        exp = desc_bucket_np(recs, table_guids, world)
+        # TARGETED-only records (the unmatched writers share entity ids with matched ones) go to
+        # the owner of their entity set; their set numbers come from the parse's target output,
+        # itself held to the oracle's target readers by test_reader_sets
+        from rtps_rx.records import ROUTE_MATCHED, ROUTE_TARGETED
+        sets = outs["target"][:len(recs)].cpu().numpy().view(np.uint32)
+        only_t = ((recs["route"] & ROUTE_TARGETED) != 0) & ((recs["route"] & ROUTE_MATCHED) == 0)
+        assert only_t.sum() > 100
+        exp = desc_bucket_np(recs, table_guids, world, entity_sets=sets)
         sizes = [len(e) for e in exp]
         assert sum(sizes) > 1000
         for pcap in (max(sizes) + 3, max(min(sizes) // 2, 1)):
