@@ -3,15 +3,17 @@
 
 One step = parse one batch of synthetic datagrams already resident in HBM
 (the whole receive-path parse: header + submessage walk + interpreter +
-classification + ordered 64-B records).  At N >= 2 GPUs (one process per
-GPU, torch.distributed over RCCL) the default workload is C5 (64M datagrams
-in total, rank r parses the r-th chunk: strong scaling) and the step adds the
-owner-side exchange: every writer record that passes goes to
-its writer's owner (writer-GUID hash) with its GAP bitmap / DATA_FRAG payload
-bytes, in fixed slots over one grouped RCCL send/recv per peer (pipelined
-with the next parse) plus an exact spill round when a slot overflows, and is
-unpacked there as one batch.  C5 then times the same steps again with every
-owner's history-cache ingest added (`pipeline_with_ingest`).
+classification + ordered 64-B records).  The default workload is T at every N
+(1M x 1 KiB datagrams per GPU: weak scaling).  At N >= 2 GPUs (one process per
+GPU, torch.distributed over RCCL) the step adds the owner-side exchange
+(SURVEY.md §8e): every writer record that passes goes to its writer's owner
+(writer-GUID hash) with its GAP bitmap / DATA_FRAG payload bytes, in fixed
+slots over one grouped RCCL send/recv per peer (pipelined with the next parse)
+plus an exact spill round when a slot overflows, and is unpacked there as one
+batch; the same steps are then timed again with every owner's history-cache
+ingest added (`pipeline_with_ingest`).  N >= 2 then measures BASELINE's 8-GPU
+config C5 (64M datagrams of the C3 mix in total, rank r parses the r-th chunk:
+strong scaling) the same way, reported as `c5`.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload T|C2|C3|C4]
 
@@ -556,7 +558,8 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default=None, choices=sorted(rtps_rx.WORKLOADS) + ["C5"],
-                    help="default: T at N=1 (the headline config), C5 at N>1 (BASELINE config 8xMI355X)")
+                    help="default: T at every N (the headline config; N>1 adds the owner exchange and a C5 "
+                         "measurement, BASELINE config 8xMI355X, as `c5`)")
     ap.add_argument("--datagrams", type=int, default=None, help="datagrams per GPU (default 1M; C5: 64M / N)")
     ap.add_argument("--writers", type=int, default=16)
     ap.add_argument("--spec-hint", type=int, default=None,
@@ -575,7 +578,9 @@ def main():
                          "there for reassembly and ingest; 'records' = the 64-B records of every writer / reader "
                          "submessage; 'descriptors' = 16-B descriptors of MATCHED records")
     ap.add_argument("--no-owner-ingest", action="store_true",
-                    help="C5: skip the second timed loop that adds the owners' history-cache ingest")
+                    help="N>1 / C5: skip the second timed loop that adds the owners' history-cache ingest")
+    ap.add_argument("--no-c5", action="store_true",
+                    help="N>1: skip the C5 measurement (64M datagrams in total) that follows the T line")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N>1 (gloo only to rehearse several ranks on one GPU)")
     args = ap.parse_args()
@@ -614,7 +619,29 @@ def main():
         dist.all_reduce(x, op=dist.ReduceOp.MAX)
         return x
 
-    args.workload = args.workload or ("C5" if world > 1 else "T")
+    # the headline config at every N (weak scaling: 1M T datagrams per GPU, plus the owner-side
+    # exchange at N >= 2), so that the 1/2/4/8-GPU lines measure one workload; BASELINE's
+    # 8-GPU config C5 (64M datagrams in total: strong scaling) rides along at N >= 2 as `c5`
+    explicit = args.workload is not None
+    args.workload = args.workload or "T"
+    result = measure(args, world, rank, dist, dev, allreduce_sum, allreduce_max)
+    if world > 1 and not explicit and not args.no_c5:
+        a5 = argparse.Namespace(**vars(args))
+        a5.workload = "C5"  # (--datagrams, when given, sizes both: tests)
+        a5.steps, a5.warmup = min(args.steps, 20), min(args.warmup, 5)
+        r5 = measure(a5, world, rank, dist, dev, allreduce_sum, allreduce_max)
+        result["c5"] = {k: r5[k] for k in ("value", "unit", "ms_per_step", "steps", "warmup", "scaling",
+                                          "gib_per_s_covered", "config", "pipeline_with_ingest") if k in r5}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist:
+        from rtps_rx.shard import destroy_comms
+        destroy_comms()  # the library's RCCL communicators, before the process group goes
+        dist.destroy_process_group()
+
+
+def measure(args, world, rank, dist, dev, allreduce_sum, allreduce_max):
+    """One workload at this N: the timed steps and (N = 1) the downstream legs; returns the line."""
     c5 = args.workload == "C5"
     wl = rtps_rx.WL_C3 if c5 else rtps_rx.WORKLOADS[args.workload]
     n = args.datagrams or ((C5_TOTAL // world) if c5 else 1 << 20)
@@ -782,7 +809,7 @@ def main():
 
     wall, ev_ms = timed(args.steps, args.warmup)
     pipeline = None
-    if c5 and (owner or world == 1) and not args.no_owner_ingest and n_matched_writers:
+    if (c5 or owner) and (owner or world == 1) and not args.no_owner_ingest and n_matched_writers:
         # the same steps ending where the N = 1 receive path ends: every owner ingests its
         # writers' records into the history cache (deliveries), timed as a second loop
         with_ingest[0] = True
@@ -898,17 +925,13 @@ def main():
         result["end_to_end"] = end_to_end(rx, arena, off_t, ln_t, n, outs, n_rec, stream)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline("C3" if c5 else args.workload, min(n, 1 << 20), match_table=tbl)
-    if rank == 0:
-        print(json.dumps(result), flush=True)
     rx.close()
-    if dist:
-        if shards is not None:
-            for sh in shards:
-                sh.close()
-        if exch is not None or shards is not None:
-            from rtps_rx.shard import destroy_comms
-            destroy_comms()  # the library's RCCL communicators, before the process group goes
-        dist.destroy_process_group()
+    if shards is not None:
+        for sh in shards:
+            sh.close()
+    torch.cuda.synchronize(dev)
+    torch.cuda.empty_cache()
+    return result
 
 
 if __name__ == "__main__":

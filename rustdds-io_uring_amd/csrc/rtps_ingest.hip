@@ -227,29 +227,74 @@ struct FastOut {
   uint32_t* seg_b;
   uint32_t* seg_e;
   uint32_t n_seg;
+  uint32_t* bk_cnt;  // BUCKET: per (workgroup, proxy) proxied events, workgroup-major: [block * n_proxies + proxy]
+  uint32_t* bk_lst;  //         the proxy's first position inside the workgroup's region
 };
+
+// Proxy bucketing (BUCKET: identity batches over at most PB_MAX proxies and
+// BK_MAX workgroups).  Classify takes CHR consecutive record slots per
+// workgroup (wave w the w-th quarter, 64 slots per step) and keeps every
+// proxied event's packed form in registers; after a workgroup-wide count per
+// proxy it writes the packed events into the workgroup's own region of pev[]
+// (CHR entries), grouped by proxy with slot order kept (a bitonic sort of
+// (proxy << 6 | lane) ranks each step's 64 slots; each wave's running offset
+// per proxy advances by its runs), plus the (workgroup, proxy) counts and
+// first positions.  k_proxy<true> then walks its proxy's pieces of every
+// workgroup's region in workgroup order (a scan of the counts in LDS): the
+// proxy's events in slot order, with no sort of the record slots and no
+// separate scatter pass (the radix sort it replaces takes two 8-bit Onesweep
+// passes over every slot at 256 proxies).
+constexpr uint32_t PB_MAX = 1024;  // proxies of the bucketing path (LDS counters: 4 x PB_MAX words)
+constexpr uint32_t BK_MAX = 4096;  // classify workgroups of the bucketing path (k_proxy's LDS tables)
+#ifndef RTPS_PB_CHR
+#define RTPS_PB_CHR 1024
+#endif
+constexpr uint32_t CHR = RTPS_PB_CHR;         // record slots per classify workgroup
+constexpr uint32_t PB_SUB = CHR / (IT / 64);  // slots per wave
+constexpr uint32_t PB_STEPS = PB_SUB / 64;
+static_assert(PB_SUB % 64 == 0 && PB_MAX <= (1u << 20) && PB_MAX % IT == 0, "bucketing steps and sort words");
+
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x, uint32_t lane) {
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+    if (lane >= d) x += y;
+  }
+  return x;
+}
 
 // IDENT: no target set has more than one reader, so event i = record i.
 // FAST (IDENT only): also the per-proxy path's inputs (FastOut), so that an identity
 // batch on that path needs no host read-back of the counts.
-template <bool IDENT, bool FAST>
+// BUCKET (FAST only): CHR consecutive slots per workgroup and the per-proxy counts
+// (the proxy bucketing above) instead of the radix sort's (key, slot) pairs.
+template <bool IDENT, bool FAST, bool BUCKET = false>
 __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record* recs, const uint64_t* n_rec,
                                                  uint64_t max, const rtps_frag_sample* frag, uint32_t flags,
                                                  Scratch x, uint64_t* ctr, FastOut fo) {
   extern __shared__ uint32_t s_rt[];
+  __shared__ uint32_t s_cnt[BUCKET ? IT / 64 : 1][BUCKET ? PB_MAX : 1];  // per (wave, proxy)
+  __shared__ uint32_t s_part[IT / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const uint64_t n = *n_rec < max ? *n_rec : max;
-  if (blockIdx.x == 0 && threadIdx.x == 0) ctr[C_NREC] = n;
-  if (FAST)
-    for (uint32_t e = blockIdx.x * IT + threadIdx.x; e < fo.n_seg; e += gridDim.x * IT) { fo.seg_b[e] = 0u; fo.seg_e[e] = 0u; }
+  if (blockIdx.x == 0 && tid == 0) ctr[C_NREC] = n;
+  if (FAST && !BUCKET)
+    for (uint32_t e = blockIdx.x * IT + tid; e < fo.n_seg; e += gridDim.x * IT) { fo.seg_b[e] = 0u; fo.seg_e[e] = 0u; }
+  if (BUCKET)
+    for (uint32_t e = lane; e < t.n_proxies; e += 64) s_cnt[wave][e] = 0u;
   const bool lds = rt_fits_lds(t);
-  if (lds) { rt_stage(t, s_rt); __syncthreads(); }
+  if (lds) rt_stage(t, s_rt);
+  if (lds || BUCKET) __syncthreads();
   const bool reliable = !(flags & RTPS_INGEST_BEST_EFFORT);
   uint32_t nh = 0, ng = 0, ne = 0, nf = 0;
-  for (uint64_t i = (uint64_t)blockIdx.x * IT + threadIdx.x; i < max; i += (uint64_t)gridDim.x * IT) {
+  // record slot i: its events; FAST: *key = the proxy of its proxied event (NONE: none)
+  // and *P its packed form, stored at pev[i] unless BUCKET (which places it itself)
+  auto body = [&](uint64_t i, uint32_t& key, PEv& P) {
     uint8_t ev = EV_NONE;
     uint32_t set = NONE;
     int64_t sn = 0;
     bool user_kind = true;
+    key = NONE;
     u32x4 q0 = {0u, 0u, 0u, 0u}, q2 = q0, q3 = q0;  // FAST: the record's fields for the packed event
     if (i < n) {
       // bytes 0..31 of the record (kind @6, prefix||writer_id @8, route @30,
@@ -325,12 +370,14 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
       } else {
         const bool px = evi != EV_NONE && ent != NONE;
         if (!(RTPS_CLS_ABL & 8)) {
-          x.hkey[i] = px ? ent : t.n_proxies;  // sort pairs: (proxy, slot); n_proxies sorts last
-          x.sval[i] = (uint32_t)i;
+          if (!BUCKET) {
+            x.hkey[i] = px ? ent : t.n_proxies;  // sort pairs: (proxy, slot); n_proxies sorts last
+            x.sval[i] = (uint32_t)i;
+          }
           fo.acc[i] = (evi == EV_SAMPLE && ent == NONE) ? 1 : 0;  // proxy-less samples (reader.rs:734-739)
         }
         if (px) {
-          PEv P;
+          key = ent;
           P.sn = sn;
           P.a = 0;
           P.bw = 0;
@@ -351,7 +398,7 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
               P.m |= PM_INL;
             }
           }
-          if (!(RTPS_CLS_ABL & 2)) fo.pev[i] = P;
+          if (!BUCKET && !(RTPS_CLS_ABL & 2)) fo.pev[i] = P;
         }
       }
     } else {
@@ -360,22 +407,108 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
       x.rkind[i] = cnt ? (uint8_t)(ev | (user_kind ? 0x80u : 0u)) : EV_NONE;
       x.rsn[i] = sn;
     }
+  };
+  if (!BUCKET) {
+    for (uint64_t i = (uint64_t)blockIdx.x * IT + tid; i < max; i += (uint64_t)gridDim.x * IT) {
+      uint32_t key;
+      PEv P;
+      body(i, key, P);
+    }
+  } else {
+    // wave w: slots [c0, c0 + PB_SUB) in PB_STEPS steps of 64; the proxied events stay in registers
+    const uint64_t c0 = (uint64_t)blockIdx.x * CHR + (uint64_t)wave * PB_SUB;
+    uint32_t key[PB_STEPS];
+    PEv P[PB_STEPS];
+#pragma unroll
+    for (uint32_t j = 0; j < PB_STEPS; ++j) {
+      const uint64_t i = c0 + j * 64u + lane;
+      key[j] = NONE;
+      if (i < max) body(i, key[j], P[j]);
+      if (key[j] != NONE) atomicAdd(&s_cnt[wave][key[j]], 1u);
+    }
+    __syncthreads();
+    // the workgroup's region: proxies in order, each proxy's events in slot order (waves in
+    // order); thread t owns proxies [t * PPB, t * PPB + PPB)
+    constexpr uint32_t PPB = PB_MAX / IT;
+    const uint32_t np = t.n_proxies;
+    uint32_t tot[PPB], sum = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < PPB; ++r) {
+      const uint32_t e = tid * PPB + r;
+      tot[r] = 0;
+      if (e < np)
+        for (uint32_t w = 0; w < IT / 64; ++w) tot[r] += s_cnt[w][e];
+      sum += tot[r];
+    }
+    const uint32_t incl = wave_incl_sum(sum, lane);
+    if (lane == 63u) s_part[wave] = incl;
+    __syncthreads();
+    uint32_t run = incl - sum;
+    for (uint32_t w = 0; w < wave; ++w) run += s_part[w];
+    const uint64_t tb = (uint64_t)blockIdx.x * np;
+#pragma unroll
+    for (uint32_t r = 0; r < PPB; ++r) {
+      const uint32_t e = tid * PPB + r;
+      if (e >= np) break;
+      fo.bk_cnt[tb + e] = tot[r];
+      fo.bk_lst[tb + e] = run;
+      for (uint32_t w = 0; w < IT / 64; ++w) {
+        const uint32_t c = s_cnt[w][e];
+        s_cnt[w][e] = run;
+        run += c;
+      }
+    }
+    __syncthreads();
+    PEv* region = fo.pev + (uint64_t)blockIdx.x * CHR;
+#pragma unroll
+    for (uint32_t j = 0; j < PB_STEPS; ++j) {
+      // stable rank among the step's equal proxies: bitonic sort of (proxy << 6 | lane)
+      uint32_t v = ((key[j] != NONE ? key[j] : PB_MAX) << 6) | lane;
+#pragma unroll
+      for (uint32_t kk = 2; kk <= 64; kk <<= 1) {
+#pragma unroll
+        for (uint32_t d = kk >> 1; d > 0; d >>= 1) {
+          const uint32_t p = (uint32_t)__shfl_xor((int)v, d, 64);
+          const bool up = (lane & kk) == 0, lower = (lane & d) == 0;
+          v = (lower == up) ? (p < v ? p : v) : (p > v ? p : v);
+        }
+      }
+      const uint32_t sk = v >> 6, sl = v & 63u;
+      const uint32_t prev = (uint32_t)__shfl_up((int)sk, 1, 64);
+      uint32_t start = (lane == 0 || prev != sk) ? lane : 0u;  // first lane of this lane's run
+#pragma unroll
+      for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)start, d, 64);
+        if (lane >= d && y > start) start = y;
+      }
+      const uint32_t next = (uint32_t)__shfl_down((int)sk, 1, 64);
+      const bool tail = lane == 63u || next != sk;
+      uint32_t pos = 0;
+      if (sk < PB_MAX) {
+        const uint32_t base = s_cnt[wave][sk];  // read by every lane of the run before its tail advances it
+        pos = base + (lane - start);
+        if (tail) s_cnt[wave][sk] = pos + 1u;
+      }
+      // the position back to the slot's own lane (forward permute: lane sl receives it)
+      pos = (uint32_t)__builtin_amdgcn_ds_permute((int)(sl << 2), (int)pos);
+      if (key[j] != NONE && !(RTPS_CLS_ABL & 2)) region[pos] = P[j];
+    }
   }
   __shared__ uint32_t s_n[4];
-  if (threadIdx.x < 4) s_n[threadIdx.x] = 0;
+  if (tid < 4) s_n[tid] = 0;
   __syncthreads();
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) {
     nh += __shfl_xor(nh, d, 64); ng += __shfl_xor(ng, d, 64); ne += __shfl_xor(ne, d, 64);
     nf += __shfl_xor(nf, d, 64);
   }
-  if ((threadIdx.x & 63u) == 0) {
+  if (lane == 0) {
     atomicAdd(&s_n[0], nh); atomicAdd(&s_n[1], ng); atomicAdd(&s_n[2], ne); atomicAdd(&s_n[3], nf);
   }
   __syncthreads();
-  if (threadIdx.x < 4 && s_n[threadIdx.x])
-    atomicAdd(reinterpret_cast<unsigned long long*>(ctr + C_SPREAD + 4u * (blockIdx.x & 63u) + threadIdx.x),
-              (unsigned long long)s_n[threadIdx.x]);
+  if (tid < 4 && s_n[tid])
+    atomicAdd(reinterpret_cast<unsigned long long*>(ctr + C_SPREAD + 4u * (blockIdx.x & 63u) + tid),
+              (unsigned long long)s_n[tid]);
 }
 
 // 1b: lane per record writes its events at roff[i] (set order = EntityId order of the readers)
@@ -899,15 +1032,50 @@ __device__ __forceinline__ uint32_t ph_find(const uint32_t* h_key, uint32_t off)
   }
 }
 
-// One workgroup per proxy: its events (sorted by proxy, event order kept: `order`
-// holds positions in the packed events `pev`) replayed in chunks of PCH against
-// the proxy's change-set window in LDS.
+// the proxy bucketing's tables (k_classify<.., true>): per (classify workgroup, proxy)
+// event counts and first positions in the workgroup's region of pev, nb workgroups
+struct BkIn {
+  const uint32_t* cnt;
+  const uint32_t* lst;
+  uint32_t nb;
+};
+// block-wide EXCLUSIVE sum over the PT threads; *total = the block's sum
+__device__ __forceinline__ uint32_t block_sum_excl(uint32_t v, uint32_t* s_w, uint32_t& total) {
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  uint32_t inc = v;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)inc, d, 64);
+    if (lane >= d) inc += y;
+  }
+  if (lane == 63) s_w[wave] = inc;
+  __syncthreads();
+  uint32_t pre = 0;
+  total = 0;
+  for (uint32_t w = 0; w < PWAVES; ++w) {
+    if (w < wave) pre += s_w[w];
+    total += s_w[w];
+  }
+  __syncthreads();
+  return pre + inc - v;
+}
+
+// One workgroup per proxy: its events in slot order replayed in chunks of PCH
+// against the proxy's change-set window in LDS.  The events: BK = false, sorted by
+// proxy (`order` holds positions in the packed events `pev`, the proxy's segment
+// [seg_b, seg_e)); BK = true, the proxy's pieces of every classify workgroup's
+// region of pev, in workgroup order (the bucketing's tables, scanned into LDS).
+template <bool BK>
 __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* pev, const uint32_t* order,
-                                              uint32_t n_proxies, State s, uint8_t* acc_out, int64_t* ack_out) {
+                                              uint32_t n_proxies, State s, uint8_t* acc_out, int64_t* ack_out,
+                                              BkIn bk) {
   __shared__ uint32_t sb[WW];                           // the change set window [lo, lo + W)
   __shared__ uint32_t pres[WW];                         // window offsets of the chunk's samples
   __shared__ uint32_t h_key[PH], h_min[PH], h_gap[PH];  // window offset -> first sample / GAP position
   __shared__ int64_t s_w[PWAVES];
+  __shared__ uint32_t s_w32[PWAVES];
+  __shared__ uint32_t s_pre[BK ? BK_MAX : 1];   // BK: the proxy's events before workgroup b's piece
+  __shared__ uint32_t s_base[BK ? BK_MAX : 1];  // BK: pev index of the proxy's event q in piece b = s_base[b] + q
   __shared__ uint32_t s_first;
   const uint32_t e = blockIdx.x, tid = threadIdx.x;
   if (e >= n_proxies) return;
@@ -915,7 +1083,24 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
   uint32_t* gbits = s.bits + (uint64_t)e * WW;
   for (uint32_t w = tid; w < WW; w += PT) { sb[w] = gbits[w]; pres[w] = 0u; }
   for (uint32_t h = tid; h < PH; h += PT) { h_key[h] = NONE; h_min[h] = NONE; h_gap[h] = NONE; }
-  const uint32_t qb = s.seg_b[e], qe = s.seg_e[e];
+  uint32_t qb = 0, qe = 0;
+  if (BK) {
+    for (uint32_t b0 = 0; b0 < bk.nb; b0 += PT) {
+      const uint32_t b = b0 + tid;
+      const uint32_t c = b < bk.nb ? bk.cnt[(uint64_t)b * n_proxies + e] : 0u;
+      const uint32_t l = b < bk.nb ? bk.lst[(uint64_t)b * n_proxies + e] : 0u;
+      uint32_t tot;
+      const uint32_t ex = qe + block_sum_excl(c, s_w32, tot);
+      if (b < bk.nb) {
+        s_pre[b] = ex;
+        s_base[b] = b * CHR + l - ex;
+      }
+      qe += tot;
+    }
+  } else {
+    qb = s.seg_b[e];
+    qe = s.seg_e[e];
+  }
   int64_t run_cnt = s.hbc[e], run_thr = base;  // max HEARTBEAT count so far; max accepted firstSN (>= base)
   uint64_t n_ovf = 0;
   PST_DECL;
@@ -926,11 +1111,26 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
     int64_t v[PPT], a[PPT];
     uint64_t bwj[PPT];
     int64_t cmax = INT64_MIN;
+    uint32_t pb = 0;  // BK: the piece of the thread's first event (the largest b with s_pre[b] <= q)
+    if (BK && q0 + tid * PPT < qe) {
+      const uint32_t q = q0 + tid * PPT;
+      for (uint32_t hi = bk.nb; hi - pb > 1u;) {
+        const uint32_t mid = (pb + hi) >> 1;
+        if (s_pre[mid] <= q) pb = mid; else hi = mid;
+      }
+    }
 #pragma unroll
     for (uint32_t j = 0; j < PPT; ++j) {
       const uint32_t q = q0 + tid * PPT + j;
       PEv P{0, 0, 0, 0, 0};
-      if (q < qe) P = pev[order[q]];
+      if (BK) {
+        if (q < qe) {
+          while (pb + 1u < bk.nb && s_pre[pb + 1u] <= q) ++pb;
+          P = pev[s_base[pb] + q];
+        }
+      } else if (q < qe) {
+        P = pev[order[q]];
+      }
       m[j] = P.m;
       v[j] = P.sn;
       a[j] = P.a;
@@ -1120,7 +1320,29 @@ struct IngestState {
   hipEvent_t hnev_ev = nullptr;
   bool hnev_ready = false;
   uint64_t last_nev = 0;      // events of the last batch whose counts were read
+  uint32_t* bk_cnt = nullptr;  // proxy bucketing: per (classify workgroup, proxy) events and first positions
+  uint32_t* bk_lst = nullptr;
+  uint64_t bkcap = 0;
 };
+
+static void free_bk(IngestState* s) {
+  if (s->bk_cnt) (void)hipFree(s->bk_cnt);
+  if (s->bk_lst) (void)hipFree(s->bk_lst);
+  s->bk_cnt = nullptr;
+  s->bk_lst = nullptr;
+  s->bkcap = 0;
+}
+static bool grow_bk(IngestState* s, uint64_t n, hipStream_t st) {
+  if (n <= s->bkcap) return true;
+  (void)hipStreamSynchronize(st);
+  free_bk(s);
+  if (hipMalloc(&s->bk_cnt, n * 4) != hipSuccess || hipMalloc(&s->bk_lst, n * 4) != hipSuccess) {
+    free_bk(s);
+    return false;
+  }
+  s->bkcap = n;
+  return true;
+}
 
 static void free_pscratch(IngestState* s) {
   if (s->pev) (void)hipFree(s->pev);
@@ -1282,6 +1504,7 @@ IngestState* rtps_ingest_state_new(int device) {
 
 void rtps_ingest_state_free(IngestState* s) {
   if (!s) return;
+  free_bk(s);
   free_pscratch(s);
   free_vscratch(s);
   free_rscratch(s);
@@ -1343,15 +1566,25 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
     s->hnev_ready = false;
   }
   const bool fast = ident && t.n_proxies > 0 &&
-                    (s->path == 2 || (s->path == 0 && t.n_proxies >= 64 &&
-                                      s->last_nev <= (uint64_t)t.n_proxies * 32768u));
-  FastOut fo{nullptr, nullptr, arena, dgram_off, S.seg_b, S.seg_e, s->ecap};
+                    (s->path == 2 || s->path == 4 || (s->path == 0 && t.n_proxies >= 64 &&
+                                                      s->last_nev <= (uint64_t)t.n_proxies * 32768u));
+  // the proxy bucketing (k_classify<.., BUCKET>, k_proxy<true>) unless the proxies or the
+  // classify workgroups exceed its LDS tables (or path 4: the radix sort, tests)
+  const uint64_t nblk = (max + CHR - 1) / CHR;
+  const bool bucket = fast && t.n_proxies <= PB_MAX && nblk <= BK_MAX && s->path != 4;
+  FastOut fo{nullptr, nullptr, arena, dgram_off, S.seg_b, S.seg_e, s->ecap, nullptr, nullptr};
   if (fast) {
-    if (!grow_pscratch(s, max, st)) return RTPS_RX_ENOMEM;
+    if (!grow_pscratch(s, bucket ? nblk * CHR : max, st)) return RTPS_RX_ENOMEM;
     fo.pev = s->pev;
     fo.acc = out->accept;
   }
-  if (ident && fast)
+  if (bucket) {
+    if (!grow_bk(s, (uint64_t)t.n_proxies * nblk, st)) return RTPS_RX_ENOMEM;
+    fo.bk_cnt = s->bk_cnt;
+    fo.bk_lst = s->bk_lst;
+    hipLaunchKernelGGL((k_classify<true, true, true>), dim3((uint32_t)nblk), dim3(IT), lds, st, t, records,
+                       n_records, max, with_frag ? frag : nullptr, flags, x, S.ctr, fo);
+  } else if (ident && fast)
     hipLaunchKernelGGL((k_classify<true, true>), dim3(gb), dim3(IT), lds, st, t, records, n_records, max,
                        with_frag ? frag : nullptr, flags, x, S.ctr, fo);
   else if (ident)
@@ -1360,7 +1593,10 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
   else
     hipLaunchKernelGGL((k_classify<false, false>), dim3(gb), dim3(IT), lds, st, t, records, n_records, max,
                        with_frag ? frag : nullptr, flags, x, S.ctr, fo);
-  if (fast) {
+  if (bucket) {
+    hipLaunchKernelGGL(k_proxy<true>, dim3(t.n_proxies), dim3(PT), 0, st, arena, s->pev, x.hval, t.n_proxies, S,
+                       out->accept, out->ack_base, BkIn{s->bk_cnt, s->bk_lst, (uint32_t)nblk});
+  } else if (fast) {
     uint32_t kb = 1;
     while ((1u << kb) <= t.n_proxies) ++kb;  // keys 0..n_proxies (n_proxies: no proxy, sorts last)
     size_t tb = s->tmp_bytes;
@@ -1368,8 +1604,10 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
       return RTPS_RX_EHIP;
     const uint32_t gm = (uint32_t)hmin((max + IT - 1) / IT, 8192);
     hipLaunchKernelGGL(k_pseg, dim3(gm), dim3(IT), 0, st, max, t.n_proxies, x, S);
-    hipLaunchKernelGGL(k_proxy, dim3(t.n_proxies), dim3(PT), 0, st, arena, s->pev, x.hval, t.n_proxies, S,
-                       out->accept, out->ack_base);
+    hipLaunchKernelGGL(k_proxy<false>, dim3(t.n_proxies), dim3(PT), 0, st, arena, s->pev, x.hval, t.n_proxies, S,
+                       out->accept, out->ack_base, BkIn{});
+  }
+  if (fast) {
     deliver(out->accept, max, x, true, out, st);
     hipLaunchKernelGGL(k_finish, dim3(1), dim3(1), 0, st, S.ctr, out->n_window_overflow);
     // this batch's counts for the next batch's choice (pinned, read without a sync)
@@ -1406,7 +1644,7 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
   // per-proxy workgroups when the events spread over many proxies (mean load bounded:
   // one workgroup replays a proxy's events in order); global marks / merge otherwise
   const bool per_proxy = t.n_proxies > 0 && nev > 0 &&
-                         (s->path == 2 || (s->path == 0 && t.n_proxies >= 64 && n_ev <= (uint64_t)t.n_proxies * 32768u));
+                         (s->path == 2 || s->path == 4 || (s->path == 0 && t.n_proxies >= 64 && n_ev <= (uint64_t)t.n_proxies * 32768u));
   uint8_t* acc = ident ? out->accept : x.eacc;
   const uint64_t acc_cap = ident ? max : nev;
   if (per_proxy) {
@@ -1434,8 +1672,8 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
     }
     hipLaunchKernelGGL(k_decide_free, dim3((uint32_t)hmin((acc_cap + IT - 1) / IT, 8192)), dim3(IT), 0, st, nev,
                        acc_cap, x, acc);
-    hipLaunchKernelGGL(k_proxy, dim3(t.n_proxies), dim3(PT), 0, st, arena, s->pev, x.hval, t.n_proxies, S, acc,
-                       out->ack_base);
+    hipLaunchKernelGGL(k_proxy<false>, dim3(t.n_proxies), dim3(PT), 0, st, arena, s->pev, x.hval, t.n_proxies, S,
+                       acc, out->ack_base, BkIn{});
   }
   const bool have_hb = reliable && n_hb > 0 && !per_proxy;
   if (have_hb) {  // stable compaction of the HEARTBEAT events, sort by proxy, scans by key

@@ -2215,9 +2215,10 @@ int rtps_rx_ingest(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len, con
 
 /* test / measurement hook (not part of the public header): the ingest's
    per-batch path, 0 = chosen per batch, 1 = global marks / merge, 2 = one
-   workgroup per proxy (same results) */
+   workgroup per proxy (same results), 3 = global with the first-cover-key merge,
+   4 = per proxy with the radix sort instead of the proxy bucketing */
 int rtps_rx_debug_ingest_path(rtps_rx_ctx* c, uint32_t path) {
-  if (!c || path > 3u) return RTPS_RX_EINVAL;
+  if (!c || path > 4u) return RTPS_RX_EINVAL;
   (void)hipSetDevice(c->device);
   if (!c->ingest) {
     c->ingest = rtps_ingest_state_new(c->device);

@@ -5,7 +5,8 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; R=$(pwd); mkdir -p gpurun_out; export TMPDIR=/tmp
 SKIP="--no-c1 --no-cpu-baseline --no-e2e --no-cdr --steps 20 --warmup 5"
 cd /tmp
-for job in ${JOBS:-"C3 --no-frag" "T --no-frag" "C4 --no-ingest"}; do
+IFS=";" read -ra JL <<< "${JOBS:-C3 --no-frag;T --no-frag;C4 --no-ingest}"
+for job in "${JL[@]}"; do
   set -- $job; wl=$1; shift
   echo "== $wl ($(date +%T))"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/legs_$wl" -o run --output-format csv \

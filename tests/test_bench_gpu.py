@@ -53,16 +53,28 @@ def test_bench_one_rank_line(workload):
 @pytest.mark.gpu
 @pytest.mark.parametrize("exchange", ["owner", "records", "descriptors"])
 def test_bench_two_ranks_gloo_exchange(exchange):
-    """N=2: the C5 config (C3 mix, 64M / N per rank, here reduced) with the owner-side
-    exchange (default) and its ingest pipeline; the record and descriptor exchanges as options."""
+    """N=2 as the driver runs it (owner: no --workload): the T line (the headline config, weak
+    scaling) with the owner-side exchange and its ingest pipeline, then the C5 config (C3 mix,
+    64M / N per rank, here reduced) as `c5`; the record and descriptor exchanges (options) on C5."""
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
-           "--backend", "gloo", "--exchange", exchange] + SMALL
+           "--backend", "gloo", "--exchange", exchange] + SMALL + ([] if exchange == "owner" else ["--workload", "C5"])
     r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json_line(r.stdout)
     assert d["n_gpus"] == 2 and d["value"] > 0
+    if exchange == "owner":
+        assert d["config"]["workload"].startswith("T") and d["scaling"] == "weak"
+        ex = d["config"]["exchange"]
+        assert ex["overflow"] is False and "owner-side" in ex["mode"] and ex["spilled_records_rank0"] == 0
+        # T: one DATA per datagram from 16 writers; rank 0 owns the writers whose GUID hashes to it
+        got, per = d["config"]["received_records_rank0"], d["config"]["records_per_gpu"]
+        assert 0.1 * per < got < 1.9 * per, (got, per)
+        p = d["pipeline_with_ingest"]
+        assert p["value"] > 0 and p["deliveries_per_step_all_ranks"] == 2 * per
+        d = d["c5"]
+        assert d["value"] > 0 and d["scaling"] == "strong"
     assert d["config"]["workload"].startswith("C5") and d["scaling"] == "strong"
     ex = d["config"]["exchange"]
     assert ex["overflow"] is False

@@ -18,10 +18,11 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
-@pytest.fixture(params=[1, 2, 3], ids=["global", "per_proxy", "global_fcmerge"])
+@pytest.fixture(params=[1, 2, 3, 4], ids=["global", "per_proxy", "global_fcmerge", "per_proxy_radix"])
 def rx(request):
     """Every test runs on every ingest path (forced): global marks / merge, one
-    workgroup per proxy replaying its events in order against an LDS window, and the
+    workgroup per proxy replaying its events in order against an LDS window (its
+    events grouped by the proxy bucketing, or by the radix sort: per_proxy_radix), and the
     global path whose GAP-free batches merge their coverage from the first-cover keys
     (k_fcmerge, chosen by size for large batches over few proxies, forced here)."""
     import rtps_rx
