@@ -752,7 +752,7 @@ __global__ __launch_bounds__(IT) void k_dcount(const uint8_t* flag, uint64_t n, 
 }
 __global__ __launch_bounds__(IT) void k_dwrite(const uint8_t* flag, uint64_t n, const uint32_t* tcnt, uint32_t ntiles,
                                                Scratch x, bool ident, uint64_t max_out, rtps_delivery* out,
-                                               uint64_t* n_out) {
+                                               uint64_t* n_out, const uint64_t* ctr, uint64_t* ovf_out) {
   __shared__ uint64_t s_w[IT / 64];
   __shared__ uint32_t s_c[IT / 64];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
@@ -799,7 +799,10 @@ __global__ __launch_bounds__(IT) void k_dwrite(const uint8_t* flag, uint64_t n, 
       }
     }
   }
-  if (blockIdx.x + 1 == ntiles && tid == 0) *n_out = pre + tot;
+  if (blockIdx.x + 1 == ntiles && tid == 0) {
+    *n_out = pre + tot;
+    if (ovf_out) *ovf_out = ctr[C_OVF];  // the batch's window overflows (counted before the select)
+  }
 }
 __global__ __launch_bounds__(IT) void k_accept_counts(uint64_t n, uint64_t cap, Scratch x, uint8_t* accept) {
   for (uint64_t i = (uint64_t)blockIdx.x * IT + threadIdx.x; i < cap; i += (uint64_t)gridDim.x * IT) {
@@ -1287,16 +1290,18 @@ __global__ void k_finish(const uint64_t* ctr, uint64_t* ovf) { if (ovf) *ovf = c
 static inline uint64_t hmin(uint64_t a, uint64_t b) { return a < b ? a : b; }
 
 // accepted flags[0, n) -> deliveries (k_dcount + k_dwrite; x.sel holds the tile counts)
+// ovf: also copy the batch's window-overflow count out (the paths whose last kernel this is)
 static void deliver(const uint8_t* flag, uint64_t n, const Scratch& x, bool ident, const rtps_ingest_out* out,
-                    hipStream_t st) {
+                    hipStream_t st, const uint64_t* ctr = nullptr, bool ovf = false) {
   const uint32_t ntiles = (uint32_t)((n + DT - 1) / DT);
   if (ntiles == 0) {
     (void)hipMemsetAsync(out->n_accepted, 0, sizeof(uint64_t), st);
+    if (ovf && out->n_window_overflow) hipLaunchKernelGGL(k_finish, dim3(1), dim3(1), 0, st, ctr, out->n_window_overflow);
     return;
   }
   hipLaunchKernelGGL(k_dcount, dim3(ntiles), dim3(IT), 0, st, flag, n, x.sel);
   hipLaunchKernelGGL(k_dwrite, dim3(ntiles), dim3(IT), 0, st, flag, n, x.sel, ntiles, x, ident, out->max_accepted,
-                     out->accepted, out->n_accepted);
+                     out->accepted, out->n_accepted, ctr, ovf ? out->n_window_overflow : nullptr);
 }
 
 }  // namespace
@@ -1608,8 +1613,7 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
                        out->accept, out->ack_base, BkIn{});
   }
   if (fast) {
-    deliver(out->accept, max, x, true, out, st);
-    hipLaunchKernelGGL(k_finish, dim3(1), dim3(1), 0, st, S.ctr, out->n_window_overflow);
+    deliver(out->accept, max, x, true, out, st, S.ctr, true);
     // this batch's counts for the next batch's choice (pinned, read without a sync)
     if (hipMemcpyAsync(s->hctr2, S.ctr, C_COUNT * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipEventRecord(s->hnev_ev, st) != hipSuccess)
@@ -1710,7 +1714,8 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
   if (acc_cap && !per_proxy)
     hipLaunchKernelGGL(k_decide, dim3((uint32_t)hmin((acc_cap + IT - 1) / IT, 8192)), dim3(IT), 0, st, nev, acc_cap,
                        x, S, acc, have_hb, s->epoch);
-  deliver(acc, acc_cap, x, ident, out, st);
+  const bool state_pass = t.n_proxies && !per_proxy;  // k_state copies the overflow count out, else the select does
+  deliver(acc, acc_cap, x, ident, out, st, S.ctr, !state_pass);
   if (!ident)
     hipLaunchKernelGGL(k_accept_counts, dim3(gb), dim3(IT), 0, st, n_rec, max, x, out->accept);
   if (nev && !per_proxy && n_gap == 0 && (s->path == 3 || (uint64_t)t.n_proxies * W <= 4ull * nev))
@@ -1718,10 +1723,8 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
                        t.n_proxies, S, s->epoch);
   else if (nev && !per_proxy)
     hipLaunchKernelGGL(k_merge, dim3(gv), dim3(IT), 0, st, records, arena, dgram_off, nev, x, S, n_gap > 0);
-  if (t.n_proxies && !per_proxy)
+  if (state_pass)
     hipLaunchKernelGGL(k_state, dim3(t.n_proxies), dim3(IT), 0, st, t.n_proxies, x, S, have_hb, out->ack_base,
                        out->n_window_overflow);
-  else
-    hipLaunchKernelGGL(k_finish, dim3(1), dim3(1), 0, st, S.ctr, out->n_window_overflow);
   return hipGetLastError() == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP;
 }
