@@ -246,6 +246,7 @@ struct FastOut {
 // passes over every slot at 256 proxies).
 constexpr uint32_t PB_MAX = 1024;  // proxies of the bucketing path (LDS counters: 4 x PB_MAX words)
 constexpr uint32_t BK_MAX = 4096;  // classify workgroups of the bucketing path (k_proxy's LDS tables)
+constexpr uint32_t BK_IDX = 4096;  // k_proxy's sampled piece index: proxies of up to 4 x BK_IDX events
 #ifndef RTPS_PB_CHR
 #define RTPS_PB_CHR 1024
 #endif
@@ -1077,8 +1078,9 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
   __shared__ uint32_t h_key[PH], h_min[PH], h_gap[PH];  // window offset -> first sample / GAP position
   __shared__ int64_t s_w[PWAVES];
   __shared__ uint32_t s_w32[PWAVES];
-  __shared__ uint32_t s_pre[BK ? BK_MAX : 1];   // BK: the proxy's events before workgroup b's piece
-  __shared__ uint32_t s_base[BK ? BK_MAX : 1];  // BK: pev index of the proxy's event q in piece b = s_base[b] + q
+  __shared__ uint32_t s_pre[BK ? BK_MAX + 1 : 1];  // BK: the proxy's events before workgroup b's piece
+  __shared__ uint32_t s_base[BK ? BK_MAX : 1];     // BK: pev index of the proxy's event q in piece b = s_base[b] + q
+  __shared__ uint32_t s_idx[BK ? BK_IDX : 1];      // BK: the piece holding event 4m (when the proxy has <= 4 BK_IDX)
   __shared__ uint32_t s_first;
   const uint32_t e = blockIdx.x, tid = threadIdx.x;
   if (e >= n_proxies) return;
@@ -1087,18 +1089,36 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
   for (uint32_t w = tid; w < WW; w += PT) { sb[w] = gbits[w]; pres[w] = 0u; }
   for (uint32_t h = tid; h < PH; h += PT) { h_key[h] = NONE; h_min[h] = NONE; h_gap[h] = NONE; }
   uint32_t qb = 0, qe = 0;
+  bool idx = false;
   if (BK) {
-    for (uint32_t b0 = 0; b0 < bk.nb; b0 += PT) {
-      const uint32_t b = b0 + tid;
-      const uint32_t c = b < bk.nb ? bk.cnt[(uint64_t)b * n_proxies + e] : 0u;
-      const uint32_t l = b < bk.nb ? bk.lst[(uint64_t)b * n_proxies + e] : 0u;
-      uint32_t tot;
-      const uint32_t ex = qe + block_sum_excl(c, s_w32, tot);
-      if (b < bk.nb) {
+    // thread t: pieces [t K, t K + K), every table load issued before the one block scan
+    constexpr uint32_t K = BK_MAX / PT;
+    const uint32_t kp = (bk.nb + PT - 1) / PT;
+    uint32_t c[K], l[K], sum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < K; ++k) {
+      const uint32_t b = tid * kp + k;
+      c[k] = (k < kp && b < bk.nb) ? bk.cnt[(uint64_t)b * n_proxies + e] : 0u;
+      l[k] = (k < kp && b < bk.nb) ? bk.lst[(uint64_t)b * n_proxies + e] : 0u;
+      sum += c[k];
+    }
+    uint32_t ex = block_sum_excl(sum, s_w32, qe);
+#pragma unroll
+    for (uint32_t k = 0; k < K; ++k) {
+      const uint32_t b = tid * kp + k;
+      if (k < kp && b < bk.nb) {
         s_pre[b] = ex;
-        s_base[b] = b * CHR + l - ex;
+        s_base[b] = b * CHR + l[k] - ex;
       }
-      qe += tot;
+      ex += c[k];
+    }
+    if (tid == 0) s_pre[bk.nb] = qe;
+    // the sampled index: each piece names itself at the multiples of PPT it holds
+    idx = qe <= PPT * BK_IDX;
+    if (idx) {
+      __syncthreads();
+      for (uint32_t b = tid; b < bk.nb; b += PT)
+        for (uint32_t m = (s_pre[b] + PPT - 1) / PPT; m * PPT < s_pre[b + 1]; ++m) s_idx[m] = b;
     }
   } else {
     qb = s.seg_b[e];
@@ -1109,38 +1129,53 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
   PST_DECL;
   __syncthreads();
   PST(0);
+  // the chunk at c0's events of this thread (BK: found through the piece tables)
+  auto load_chunk = [&](uint32_t c0, PEv (&dst)[PPT]) {
+    uint32_t pb = 0;  // BK: the piece of the thread's first event (the largest b with s_pre[b] <= q)
+    if (BK && c0 + tid * PPT < qe) {
+      const uint32_t q = c0 + tid * PPT;  // a multiple of PPT
+      if (idx) {
+        pb = s_idx[q / PPT];
+      } else {
+        for (uint32_t hi = bk.nb; hi - pb > 1u;) {
+          const uint32_t mid = (pb + hi) >> 1;
+          if (s_pre[mid] <= q) pb = mid; else hi = mid;
+        }
+      }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < PPT; ++j) {
+      const uint32_t q = c0 + tid * PPT + j;
+      dst[j] = PEv{0, 0, 0, 0, 0};
+      if (BK) {
+        if (q < qe) {
+          while (s_pre[pb + 1u] <= q) ++pb;  // (s_pre[nb] = the proxy's events > q)
+          dst[j] = pev[s_base[pb] + q];
+        }
+      } else if (q < qe) {
+        dst[j] = pev[order[q]];
+      }
+    }
+  };
+  // the events are loaded one chunk ahead: the next chunk's loads are in flight while
+  // this chunk is decided (its barriers are LDS-only: plain loads survive them)
+  PEv nx[PPT];
+  if (qb < qe) load_chunk(qb, nx);
   for (uint32_t q0 = qb; q0 < qe; q0 += PCH) {
     uint32_t m[PPT], slot[PPT], kk[PPT];
     int64_t v[PPT], a[PPT];
     uint64_t bwj[PPT];
     int64_t cmax = INT64_MIN;
-    uint32_t pb = 0;  // BK: the piece of the thread's first event (the largest b with s_pre[b] <= q)
-    if (BK && q0 + tid * PPT < qe) {
-      const uint32_t q = q0 + tid * PPT;
-      for (uint32_t hi = bk.nb; hi - pb > 1u;) {
-        const uint32_t mid = (pb + hi) >> 1;
-        if (s_pre[mid] <= q) pb = mid; else hi = mid;
-      }
-    }
 #pragma unroll
     for (uint32_t j = 0; j < PPT; ++j) {
-      const uint32_t q = q0 + tid * PPT + j;
-      PEv P{0, 0, 0, 0, 0};
-      if (BK) {
-        if (q < qe) {
-          while (pb + 1u < bk.nb && s_pre[pb + 1u] <= q) ++pb;
-          P = pev[s_base[pb] + q];
-        }
-      } else if (q < qe) {
-        P = pev[order[q]];
-      }
-      m[j] = P.m;
-      v[j] = P.sn;
-      a[j] = P.a;
-      bwj[j] = P.bw;
-      kk[j] = P.k;
+      m[j] = nx[j].m;
+      v[j] = nx[j].sn;
+      a[j] = nx[j].a;
+      bwj[j] = nx[j].bw;
+      kk[j] = nx[j].k;
       if ((m[j] & 3u) == EV_HB && a[j] > cmax) cmax = a[j];
     }
+    if (q0 + PCH < qe) load_chunk(q0 + PCH, nx);
     // HEARTBEATs: accepted iff count > every earlier count and the state's (reader.rs:902-905);
     // an accepted one covers [0, firstSN) (irrelevant_changes_up_to)
     PST(1);

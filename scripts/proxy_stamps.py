@@ -37,7 +37,7 @@ tbl = np.zeros(len(guids), dtype=MATCH_DTYPE)
 tbl["writer_guid"] = np.frombuffer(guids.tobytes(), dtype=np.uint8).reshape(-1, 16)
 rx.set_match_table(tbl)
 rx.parse_batch_device(arena, off_t, ln_t, n, outs)
-rx.debug_ingest_path(2)
+rx.debug_ingest_path(int(os.environ.get("INGEST_PATH", "2")))  # 4: the radix-sort layout
 iouts = rx.alloc_ingest_outputs(outs["max_records"], len(guids))
 for _ in range(3):
     rx.ingest_reset()
