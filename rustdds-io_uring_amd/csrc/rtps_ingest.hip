@@ -272,9 +272,11 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x, uint32_t lane) {
 template <bool IDENT, bool FAST, bool BUCKET = false>
 __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record* recs, const uint64_t* n_rec,
                                                  uint64_t max, const rtps_frag_sample* frag, uint32_t flags,
-                                                 Scratch x, uint64_t* ctr, FastOut fo) {
+                                                 Scratch x, uint64_t* ctr, FastOut fo, uint64_t* ctr_next) {
   extern __shared__ uint32_t s_rt[];
   __shared__ uint32_t s_cnt[BUCKET ? IT / 64 : 1][BUCKET ? PB_MAX : 1];  // per (wave, proxy)
+  if (blockIdx.x == gridDim.x - 1u)  // the next batch's counters start at zero (no memset launch)
+    for (uint32_t c = threadIdx.x; c < C_COUNT; c += IT) ctr_next[c] = 0ull;
   __shared__ uint32_t s_part[IT / 64];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const uint64_t n = *n_rec < max ? *n_rec : max;
@@ -753,7 +755,8 @@ __global__ __launch_bounds__(IT) void k_dcount(const uint8_t* flag, uint64_t n, 
 }
 __global__ __launch_bounds__(IT) void k_dwrite(const uint8_t* flag, uint64_t n, const uint32_t* tcnt, uint32_t ntiles,
                                                Scratch x, bool ident, uint64_t max_out, rtps_delivery* out,
-                                               uint64_t* n_out, const uint64_t* ctr, uint64_t* ovf_out) {
+                                               uint64_t* n_out, const uint64_t* ctr, uint64_t* ovf_out,
+                                               uint64_t* hev) {
   __shared__ uint64_t s_w[IT / 64];
   __shared__ uint32_t s_c[IT / 64];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
@@ -803,6 +806,11 @@ __global__ __launch_bounds__(IT) void k_dwrite(const uint8_t* flag, uint64_t n, 
   if (blockIdx.x + 1 == ntiles && tid == 0) {
     *n_out = pre + tot;
     if (ovf_out) *ovf_out = ctr[C_OVF];  // the batch's window overflows (counted before the select)
+    if (hev) {  // the batch's events, for the next batch's path choice (pinned host memory, read without a sync)
+      uint64_t ne = 0;
+      for (uint32_t k = 0; k < 64; ++k) ne += ctr[C_SPREAD + 4 * k + 2];
+      *hev = ne;
+    }
   }
 }
 __global__ __launch_bounds__(IT) void k_accept_counts(uint64_t n, uint64_t cap, Scratch x, uint8_t* accept) {
@@ -1321,22 +1329,29 @@ __global__ void k_init_state(uint32_t n, State s) {
   }
 }
 __global__ void k_finish(const uint64_t* ctr, uint64_t* ovf) { if (ovf) *ovf = ctr[C_OVF]; }
+__global__ void k_hev(const uint64_t* ctr, uint64_t* hev) {
+  uint64_t ne = 0;
+  for (uint32_t k = 0; k < 64; ++k) ne += ctr[C_SPREAD + 4 * k + 2];
+  *hev = ne;
+}
 
 static inline uint64_t hmin(uint64_t a, uint64_t b) { return a < b ? a : b; }
 
 // accepted flags[0, n) -> deliveries (k_dcount + k_dwrite; x.sel holds the tile counts)
 // ovf: also copy the batch's window-overflow count out (the paths whose last kernel this is)
+// hev: also write the batch's event count there (pinned host memory)
 static void deliver(const uint8_t* flag, uint64_t n, const Scratch& x, bool ident, const rtps_ingest_out* out,
-                    hipStream_t st, const uint64_t* ctr = nullptr, bool ovf = false) {
+                    hipStream_t st, const uint64_t* ctr = nullptr, bool ovf = false, uint64_t* hev = nullptr) {
   const uint32_t ntiles = (uint32_t)((n + DT - 1) / DT);
   if (ntiles == 0) {
     (void)hipMemsetAsync(out->n_accepted, 0, sizeof(uint64_t), st);
     if (ovf && out->n_window_overflow) hipLaunchKernelGGL(k_finish, dim3(1), dim3(1), 0, st, ctr, out->n_window_overflow);
+    if (hev) hipLaunchKernelGGL(k_hev, dim3(1), dim3(1), 0, st, ctr, hev);
     return;
   }
   hipLaunchKernelGGL(k_dcount, dim3(ntiles), dim3(IT), 0, st, flag, n, x.sel);
   hipLaunchKernelGGL(k_dwrite, dim3(ntiles), dim3(IT), 0, st, flag, n, x.sel, ntiles, x, ident, out->max_accepted,
-                     out->accepted, out->n_accepted, ctr, ovf ? out->n_window_overflow : nullptr);
+                     out->accepted, out->n_accepted, ctr, ovf ? out->n_window_overflow : nullptr, hev);
 }
 
 }  // namespace
@@ -1356,7 +1371,9 @@ struct IngestState {
                              // 3: global, merged by k_fcmerge whenever the batch has no GAPs (tests)
   PEv* pev = nullptr;  // per-proxy path: the proxied events, packed (event order, or record slots)
   uint64_t pcap = 0;
-  uint64_t* hctr2 = nullptr;  // pinned: the last per-proxy identity batch's counts (no sync)
+  uint64_t* hctr2 = nullptr;  // pinned: [0] = the last per-proxy identity batch's events (no sync)
+  uint64_t* ctr_base = nullptr;  // two counter sets: a batch uses ctr_base[cpar], its classify zeroes the other
+  uint32_t cpar = 0;
   hipEvent_t hnev_ev = nullptr;
   bool hnev_ready = false;
   uint64_t last_nev = 0;      // events of the last batch whose counts were read
@@ -1532,7 +1549,13 @@ IngestState* rtps_ingest_state_new(int device) {
   IngestState* s = new (std::nothrow) IngestState();
   if (!s) return nullptr;
   s->device = device;
-  if (hipMalloc(&s->st.ctr, C_COUNT * 8) != hipSuccess) { delete s; return nullptr; }
+  if (hipMalloc(&s->ctr_base, 2 * C_COUNT * 8) != hipSuccess) { delete s; return nullptr; }
+  if (hipMemset(s->ctr_base, 0, 2 * C_COUNT * 8) != hipSuccess) {
+    (void)hipFree(s->ctr_base);
+    delete s;
+    return nullptr;
+  }
+  s->st.ctr = s->ctr_base;
   if (hipHostMalloc(&s->hctr, C_COUNT * 8, hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc(&s->hctr2, C_COUNT * 8, hipHostMallocDefault) != hipSuccess ||
       hipEventCreateWithFlags(&s->hnev_ev, hipEventDisableTiming) != hipSuccess) {
@@ -1549,7 +1572,7 @@ void rtps_ingest_state_free(IngestState* s) {
   free_vscratch(s);
   free_rscratch(s);
   free_state(s);
-  if (s->st.ctr) (void)hipFree(s->st.ctr);
+  if (s->ctr_base) (void)hipFree(s->ctr_base);
   if (s->hctr) (void)hipHostFree(s->hctr);
   if (s->hctr2) (void)hipHostFree(s->hctr2);
   if (s->hnev_ev) (void)hipEventDestroy(s->hnev_ev);
@@ -1587,7 +1610,10 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
   const uint32_t gb = (uint32_t)hmin((max + IT - 1) / IT, 8192);
   Scratch& x = s->x;
   State& S = s->st;
-  bool ok = hipMemsetAsync(S.ctr, 0, C_COUNT * 8, st) == hipSuccess;
+  // counters: this batch's set is zero (the previous classify zeroed it); this classify zeroes the other
+  S.ctr = s->ctr_base + (uint64_t)s->cpar * C_COUNT;
+  uint64_t* const ctr_next = s->ctr_base + (uint64_t)(s->cpar ^ 1u) * C_COUNT;
+  bool ok = true;
   const bool with_frag = frag && n_frag && max_frag;
   if (with_frag) ok = ok && hipMemsetAsync(x.fidx, 0xff, max * 4, st) == hipSuccess &&
                      hipMemsetAsync(x.fmask, 0, max * 8, st) == hipSuccess;
@@ -1600,9 +1626,7 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
   // classify writes the path's inputs, the sort runs over every record slot. The choice
   // uses the previous batch's counts (mean events per proxy), read without a sync.
   if (s->hnev_ready && hipEventQuery(s->hnev_ev) == hipSuccess) {
-    uint64_t ne = 0;
-    for (uint32_t k = 0; k < 64; ++k) ne += s->hctr2[C_SPREAD + 4 * k + 2];
-    s->last_nev = ne;
+    s->last_nev = s->hctr2[0];
     s->hnev_ready = false;
   }
   const bool fast = ident && t.n_proxies > 0 &&
@@ -1623,16 +1647,17 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
     fo.bk_cnt = s->bk_cnt;
     fo.bk_lst = s->bk_lst;
     hipLaunchKernelGGL((k_classify<true, true, true>), dim3((uint32_t)nblk), dim3(IT), lds, st, t, records,
-                       n_records, max, with_frag ? frag : nullptr, flags, x, S.ctr, fo);
+                       n_records, max, with_frag ? frag : nullptr, flags, x, S.ctr, fo, ctr_next);
   } else if (ident && fast)
     hipLaunchKernelGGL((k_classify<true, true>), dim3(gb), dim3(IT), lds, st, t, records, n_records, max,
-                       with_frag ? frag : nullptr, flags, x, S.ctr, fo);
+                       with_frag ? frag : nullptr, flags, x, S.ctr, fo, ctr_next);
   else if (ident)
     hipLaunchKernelGGL((k_classify<true, false>), dim3(gb), dim3(IT), lds, st, t, records, n_records, max,
-                       with_frag ? frag : nullptr, flags, x, S.ctr, fo);
+                       with_frag ? frag : nullptr, flags, x, S.ctr, fo, ctr_next);
   else
     hipLaunchKernelGGL((k_classify<false, false>), dim3(gb), dim3(IT), lds, st, t, records, n_records, max,
-                       with_frag ? frag : nullptr, flags, x, S.ctr, fo);
+                       with_frag ? frag : nullptr, flags, x, S.ctr, fo, ctr_next);
+  s->cpar ^= 1u;  // the next batch uses the set this classify zeroes
   if (bucket) {
     hipLaunchKernelGGL(k_proxy<true>, dim3(t.n_proxies), dim3(PT), 0, st, arena, s->pev, x.hval, t.n_proxies, S,
                        out->accept, out->ack_base, BkIn{s->bk_cnt, s->bk_lst, (uint32_t)nblk});
@@ -1648,11 +1673,10 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
                        out->accept, out->ack_base, BkIn{});
   }
   if (fast) {
-    deliver(out->accept, max, x, true, out, st, S.ctr, true);
-    // this batch's counts for the next batch's choice (pinned, read without a sync)
-    if (hipMemcpyAsync(s->hctr2, S.ctr, C_COUNT * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipEventRecord(s->hnev_ev, st) != hipSuccess)
-      return RTPS_RX_EHIP;
+    // the select also writes this batch's event count for the next batch's choice (pinned, read
+    // without a sync once the event has passed)
+    deliver(out->accept, max, x, true, out, st, S.ctr, true, s->hctr2);
+    if (hipEventRecord(s->hnev_ev, st) != hipSuccess) return RTPS_RX_EHIP;
     s->hnev_ready = true;
     return hipGetLastError() == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP;
   }
