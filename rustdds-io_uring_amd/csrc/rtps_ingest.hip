@@ -947,14 +947,17 @@ __device__ unsigned long long g_proxy_stamps[16384 * PST_N];
 #define PST(k) do {} while (0)
 #define PST_FLUSH(e) do {} while (0)
 #endif
-constexpr uint32_t PT = 512;             // threads of the per-proxy workgroup (one per CU: 8 waves)
+#ifndef RTPS_PROXY_PT
+#define RTPS_PROXY_PT 512
+#endif
+constexpr uint32_t PT = RTPS_PROXY_PT;   // threads of the per-proxy workgroup (one per CU)
 #ifndef RTPS_PROXY_PPT
 #define RTPS_PROXY_PPT 4
 #endif
 constexpr uint32_t PPT = RTPS_PROXY_PPT;  // consecutive events per thread
 constexpr uint32_t PCH = PT * PPT;       // events per chunk
 constexpr uint32_t PH = 2 * PCH;         // chunk hash slots (>= 2 x events per chunk)
-constexpr uint32_t PH_BITS = PPT == 2 ? 11 : PPT == 4 ? 12 : PPT == 8 ? 13 : 0;
+constexpr uint32_t PH_BITS = PH == 2048 ? 11 : PH == 4096 ? 12 : PH == 8192 ? 13 : 0;
 static_assert((1u << PH_BITS) == PH, "hash width");
 constexpr uint32_t PWAVES = PT / 64;
 
@@ -1072,6 +1075,17 @@ __device__ __forceinline__ uint32_t block_sum_excl(uint32_t v, uint32_t* s_w, ui
   return pre + inc - v;
 }
 
+// a GAP of the chunk as the GAP phases read it from LDS (the event's own registers are its thread's)
+struct GapE {
+  int64_t v, a;  // gapStart, gapList.base
+  uint64_t bw;   // inline bitmap words or the bitmap's arena offset
+  uint32_t m, q; // PEv.m, the event's position
+};
+constexpr uint32_t GCAP = 512;  // GAPs per chunk spread one per thread; the rest stay with their threads
+#ifndef RTPS_PROXY_ABL  // timing-only ablations of k_proxy (variant builds, wrong results): 1 no GAP
+#define RTPS_PROXY_ABL 0  // marks / GAP merge, 2 no hash inserts, 4 no HEARTBEAT scans
+#endif
+
 // One workgroup per proxy: its events in slot order replayed in chunks of PCH
 // against the proxy's change-set window in LDS.  The events: BK = false, sorted by
 // proxy (`order` holds positions in the packed events `pev`, the proxy's segment
@@ -1090,8 +1104,11 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
   __shared__ uint32_t s_base[BK ? BK_MAX : 1];     // BK: pev index of the proxy's event q in piece b = s_base[b] + q
   __shared__ uint32_t s_idx[BK ? BK_IDX : 1];      // BK: the piece holding event 4m (when the proxy has <= 4 BK_IDX)
   __shared__ uint32_t s_first;
+  __shared__ GapE s_gap[GCAP];  // the chunk's GAPs (the first GCAP), one per thread in the GAP phases
+  __shared__ uint32_t s_ngap;
   const uint32_t e = blockIdx.x, tid = threadIdx.x;
   if (e >= n_proxies) return;
+  if (tid == 0) s_ngap = 0u;
   const int64_t lo = s.lo[e], base = s.base[e];
   uint32_t* gbits = s.bits + (uint64_t)e * WW;
   for (uint32_t w = tid; w < WW; w += PT) { sb[w] = gbits[w]; pres[w] = 0u; }
@@ -1188,7 +1205,9 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
     // an accepted one covers [0, firstSN) (irrelevant_changes_up_to)
     PST(1);
     int64_t cnt_total;
-    int64_t c_ex = block_max_excl(cmax, run_cnt, s_w, cnt_total);
+    int64_t c_ex = run_cnt;
+    cnt_total = run_cnt;
+    if (!(RTPS_PROXY_ABL & 4)) c_ex = block_max_excl(cmax, run_cnt, s_w, cnt_total);
     int64_t fmax = INT64_MIN, f[PPT];
 #pragma unroll
     for (uint32_t j = 0; j < PPT; ++j) {
@@ -1198,7 +1217,9 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
       if (f[j] > fmax) fmax = f[j];
     }
     int64_t thr_total;
-    int64_t thr = block_max_excl(fmax, run_thr, s_w, thr_total);
+    int64_t thr = run_thr;
+    thr_total = run_thr;
+    if (!(RTPS_PROXY_ABL & 4)) thr = block_max_excl(fmax, run_thr, s_w, thr_total);
     run_cnt = cnt_total;
     run_thr = thr_total;
     PST(2);
@@ -1207,7 +1228,7 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
     for (uint32_t j = 0; j < PPT; ++j) {
       slot[j] = NONE;
       const int64_t vj = v[j];
-      if ((m[j] & 3u) == EV_SAMPLE && vj >= lo && vj < lo + (int64_t)W) {
+      if (!(RTPS_PROXY_ABL & 2) && (m[j] & 3u) == EV_SAMPLE && vj >= lo && vj < lo + (int64_t)W) {
         const uint32_t off = (uint32_t)(vj - lo);
         uint32_t h = ph_hash(off);
         for (;;) {
@@ -1220,15 +1241,32 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
         atomicOr(&pres[off >> 5], 1u << (off & 31u));
       }
     }
+    // the thread's GAPs into the chunk's GAP list: their coverage walks (a dependent chain of
+    // LDS probes each) then run one GAP per thread instead of PPT in a row per thread
+    uint32_t listed = 0;
+    {
+      uint32_t ngj = 0;
+#pragma unroll
+      for (uint32_t j = 0; j < PPT; ++j) ngj += (m[j] & 3u) == EV_GAP;
+      if (ngj) {
+        uint32_t g = atomicAdd(&s_ngap, ngj);
+#pragma unroll
+        for (uint32_t j = 0; j < PPT; ++j) {
+          if ((m[j] & 3u) != EV_GAP) continue;
+          if (g < GCAP) {
+            s_gap[g] = GapE{v[j], a[j], bwj[j], m[j], q0 + tid * PPT + j};
+            listed |= 1u << j;
+          }
+          ++g;
+        }
+      }
+    }
     __syncthreads();
     PST(3);
+    const uint32_t ngap = s_ngap < GCAP ? s_ngap : GCAP;
     // GAPs: their first covering position for the chunk's sample sequence numbers (only
     // window words holding a sample of the chunk are looked up: the presence bitmap)
-#pragma unroll
-    for (uint32_t j = 0; j < PPT; ++j) {
-      if ((m[j] & 3u) != EV_GAP) continue;
-      const uint32_t q = q0 + tid * PPT + j;
-      const uint64_t bw = bwj[j];
+    auto gap_mark = [&](int64_t gv, int64_t ga, uint64_t bw, uint32_t gm, uint32_t q) {
       auto mark = [&](uint64_t w, uint32_t bits) {
         bits &= pres[w];
         while (bits) {
@@ -1238,13 +1276,21 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
           if (h != NONE) atomicMin(&h_gap[h], q);
         }
       };
-      if (m[j] & PM_INL)
-        gap_cover_w(v[j], a[j], m[j] >> 8, [&](uint32_t w) { return (uint32_t)(bw >> (32u * w)); }, lo, mark);
+      if (gm & PM_INL)
+        gap_cover_w(gv, ga, gm >> 8, [&](uint32_t w) { return (uint32_t)(bw >> (32u * w)); }, lo, mark);
       else
-        gap_cover(v[j], a[j], arena + bw, m[j] >> 8, (m[j] & PM_LE) != 0u, lo, mark);
+        gap_cover(gv, ga, arena + bw, gm >> 8, (gm & PM_LE) != 0u, lo, mark);
+    };
+    for (uint32_t g = tid; g < ((RTPS_PROXY_ABL & 1) ? 0u : ngap); g += PT) {
+      const GapE ge = s_gap[g];
+      gap_mark(ge.v, ge.a, ge.bw, ge.m, ge.q);
     }
+#pragma unroll
+    for (uint32_t j = 0; j < PPT; ++j)
+      if ((m[j] & 3u) == EV_GAP && !((listed >> j) & 1u)) gap_mark(v[j], a[j], bwj[j], m[j], q0 + tid * PPT + j);
     __syncthreads();
     PST(4);
+    if (tid == 0) s_ngap = 0u;  // (every thread read it before the barrier above; the next list is built after barriers)
     // decide (should_ignore_change: rtps_writer_proxy.rs:202-230, reader.rs:693-758)
     int64_t t_run = thr;
 #pragma unroll
@@ -1270,6 +1316,13 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
     __syncthreads();
     PST(5);
     // merge the chunk's coverage into the window, clear the hash and the presence bits
+    auto gap_or = [&](int64_t gv, int64_t ga, uint64_t bw, uint32_t gm) {
+      auto orw = [&](uint64_t w, uint32_t bits) { atomicOr(&sb[w], bits); };
+      if (gm & PM_INL)
+        gap_cover_w(gv, ga, gm >> 8, [&](uint32_t w) { return (uint32_t)(bw >> (32u * w)); }, lo, orw);
+      else
+        gap_cover(gv, ga, arena + bw, gm >> 8, (gm & PM_LE) != 0u, lo, orw);
+    };
 #pragma unroll
     for (uint32_t j = 0; j < PPT; ++j) {
       if (slot[j] != NONE) {
@@ -1277,14 +1330,13 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
         atomicOr(&sb[off >> 5], 1u << (off & 31u));
         pres[off >> 5] = 0u;
         h_key[slot[j]] = NONE; h_min[slot[j]] = NONE; h_gap[slot[j]] = NONE;
-      } else if ((m[j] & 3u) == EV_GAP) {
-        const uint64_t bw = bwj[j];
-        auto orw = [&](uint64_t w, uint32_t bits) { atomicOr(&sb[w], bits); };
-        if (m[j] & PM_INL)
-          gap_cover_w(v[j], a[j], m[j] >> 8, [&](uint32_t w) { return (uint32_t)(bw >> (32u * w)); }, lo, orw);
-        else
-          gap_cover(v[j], a[j], arena + bw, m[j] >> 8, (m[j] & PM_LE) != 0u, lo, orw);
+      } else if ((m[j] & 3u) == EV_GAP && !((listed >> j) & 1u)) {
+        gap_or(v[j], a[j], bwj[j], m[j]);
       }
+    }
+    for (uint32_t g = tid; g < ((RTPS_PROXY_ABL & 1) ? 0u : ngap); g += PT) {
+      const GapE ge = s_gap[g];
+      gap_or(ge.v, ge.a, ge.bw, ge.m);
     }
     __syncthreads();
     PST(6);

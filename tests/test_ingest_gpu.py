@@ -80,6 +80,31 @@ def test_stream_across_batches(rx, seed, best_effort):
     assert total > 20
 
 
+def test_gap_heavy_single_proxy(rx):
+    """One writer whose chunks hold more GAPs than the per-proxy kernel's chunk GAP list
+    (GCAP = 512 of 2048 events): the listed GAPs run one per thread, the rest stay with
+    their threads; both must give the oracle's decisions and ack_base."""
+    tbl, _ = R.table(n_prefix=1, n_writer=1)
+    rx.set_match_table(tbl)
+    ing = oracle.HistoryIngest(tbl)
+    rng = np.random.default_rng(11)
+    wk = R.writer_key(0)
+    dgrams = []
+    for _ in range(3000):
+        subs = []
+        for _ in range(3):
+            sn = int(rng.integers(1, 4000))
+            if rng.random() < 0.8:
+                nb = int(rng.integers(0, 100))
+                subs.append(R.gap_sub(wk, sn, sn + int(rng.integers(-2, 6)), [bool(b) for b in rng.random(nb) < 0.3],
+                                      bool(rng.random() < 0.8)))
+            else:
+                subs.append(R.data_sub(wk, sn, bool(rng.random() < 0.8)))
+        dgrams.append(R.datagram(R.PREFIXES[0], subs))
+    for a, b in [(0, 1500), (1500, 3000)]:
+        _batch(rx, ing, tbl, dgrams[a:b], f"gaps {a}:{b}")
+
+
 def test_dense_duplicates_wide_sn(rx):
     tbl, _ = R.table()
     rx.set_match_table(tbl)
