@@ -928,7 +928,8 @@ __global__ __launch_bounds__(IT) void k_state(uint32_t n_entries, Scratch x, Sta
 // Global atomics execute at the memory side (about 20 G scattered atomics/s for
 // the whole chip), so marks / merge over a few million events of hundreds of
 // writers cost ~130 us each.  When the events spread over many proxies, they are
-// instead sorted (stably) by proxy and ONE workgroup per proxy replays its events
+// instead grouped by proxy in event order (identity batches: the proxy bucketing
+// in classify; otherwise a stable radix sort) and ONE workgroup per proxy replays its events
 // in order, 256 at a time, against the proxy's change-set window held in LDS:
 // HEARTBEAT acceptance and thresholds by block scans, a sample's coverage by the
 // window (earlier chunks and carried state), an LDS hash (earlier samples of the
