@@ -668,8 +668,15 @@ struct TileCtx {
   uint32_t H[16];  // datagram bytes 0..64
 };
 
+// arenas below this size are addressed from their start (datagram offset + in-datagram
+// offset < 2^32 - 2^17); larger ones from each wave's smallest datagram offset
+#ifndef RTPS_ARENA_DIRECT
+#define RTPS_ARENA_DIRECT ((1ull << 32) - (1ull << 17))
+#endif
+constexpr uint64_t ARENA_DIRECT = RTPS_ARENA_DIRECT;  // (0: every arena per wave; variant builds)
 // load this lane's (offset, length), build the wave's buffer descriptor
-// (base = min offset over the wave: no workgroup barrier) and the 64-byte head
+// (base = the arena, or for arenas of 4 GiB and more the min offset over the wave:
+// no workgroup barrier) and the 64-byte head
 template <uint32_t TS = TILE>
 __device__ __forceinline__ void load_tile(const KParams& p, uint32_t tile, TileCtx& t, bool enabled = true) {
   const uint32_t tid = threadIdx.x;
@@ -677,16 +684,19 @@ __device__ __forceinline__ void load_tile(const KParams& p, uint32_t tile, TileC
   t.valid = enabled && tid < TS && t.i < p.n;
   const uint64_t off = t.valid ? p.dgram_off[t.i] : ~0ull;
   t.L = t.valid ? p.dgram_len[t.i] : 0u;
-  uint64_t m = off;
+  uint64_t tb = 0;  // descriptor base: the arena itself when every in-datagram offset fits 32 bits
+  if (p.arena_len >= ARENA_DIRECT) {  // (uniform) larger arenas: the wave's smallest datagram offset
+    uint64_t m = off;
 #pragma unroll
-  for (uint32_t d = 32; d >= 1; d >>= 1) {
-    uint64_t y = __shfl_xor(m, d, 64);
-    m = y < m ? y : m;
+    for (uint32_t d = 32; d >= 1; d >>= 1) {
+      uint64_t y = __shfl_xor(m, d, 64);
+      m = y < m ? y : m;
+    }
+    tb = m > p.arena_len ? p.arena_len : m;
+    uint32_t tb_lo = __builtin_amdgcn_readfirstlane((uint32_t)tb);
+    uint32_t tb_hi = __builtin_amdgcn_readfirstlane((uint32_t)(tb >> 32));
+    tb = ((uint64_t)tb_hi << 32) | tb_lo;
   }
-  uint64_t tb = m > p.arena_len ? p.arena_len : m;
-  uint32_t tb_lo = __builtin_amdgcn_readfirstlane((uint32_t)tb);
-  uint32_t tb_hi = __builtin_amdgcn_readfirstlane((uint32_t)(tb >> 32));
-  tb = ((uint64_t)tb_hi << 32) | tb_lo;
   uint64_t avail64 = p.arena_len - tb;
   uint32_t avail = __builtin_amdgcn_readfirstlane(avail64 > 0xffffffffull ? 0xffffffffu : (uint32_t)avail64);
   t.s.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p.arena + tb), (short)0, (int)avail,
