@@ -229,7 +229,10 @@ struct FastOut {
   uint32_t n_seg;
   uint32_t* bk_cnt;  // BUCKET: per (workgroup, proxy) proxied events, workgroup-major: [block * n_proxies + proxy]
   uint32_t* bk_lst;  //         the proxy's first position inside the workgroup's region
+  uint32_t sets_lds; // classify: set_first / set_ent staged in LDS behind the hash tables
 };
+// bytes of the target sets' LDS image (set_first words, then 8-B entries)
+__host__ __device__ inline uint32_t sets_lds_bytes(const ReaderDev& t) { return (t.n_sets + 1u) * 4u + t.n_ent * 8u; }
 
 // Proxy bucketing (BUCKET: identity batches over at most PB_MAX proxies and
 // BK_MAX workgroups).  Classify takes CHR consecutive record slots per
@@ -287,6 +290,18 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
     for (uint32_t e = lane; e < t.n_proxies; e += 64) s_cnt[wave][e] = 0u;
   const bool lds = rt_fits_lds(t);
   if (lds) rt_stage(t, s_rt);
+  // the target sets behind the hash tables (when the host sized the LDS for them): a record's
+  // set entries then cost two LDS reads instead of two dependent global loads
+  uint32_t* const s_sf = s_rt + rt_lds_bytes(t.gmask + 1u, t.emask + 1u) / 4u;
+  const rtps_target* const s_se = reinterpret_cast<const rtps_target*>(s_sf + t.n_sets + 1u);
+  if (fo.sets_lds) {
+    for (uint32_t i = tid; i <= t.n_sets; i += IT) s_sf[i] = t.set_first[i];
+    const uint32_t* ge = reinterpret_cast<const uint32_t*>(t.set_ent);
+    uint32_t* le = s_sf + t.n_sets + 1u;
+    for (uint32_t i = tid; i < 2u * t.n_ent; i += IT) le[i] = ge[i];
+  }
+  const uint32_t* const sfirst = fo.sets_lds ? s_sf : t.set_first;
+  const rtps_target* const sent = fo.sets_lds ? s_se : t.set_ent;
   if (lds || BUCKET) __syncthreads();
   const bool reliable = !(flags & RTPS_INGEST_BEST_EFFORT);
   uint32_t nh = 0, ng = 0, ne = 0, nf = 0;
@@ -343,12 +358,12 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
     uint32_t cnt = 0;
     uint32_t ent = NONE, meta = 0;
     if (ev != EV_NONE) {
-      const uint32_t b = t.set_first[set], e = t.set_first[set + 1];
+      const uint32_t b = sfirst[set], e = sfirst[set + 1];
       const uint64_t fm = (frag && x.fidx[i] != NONE) ? x.fmask[i] : ~0ull;
       for (uint32_t k = b; k < e; ++k) {
         uint32_t en, me;
         if (((fm >> ((k - b) & 63u)) & 1ull) && (k - b < 64u || fm == ~0ull) &&
-            ev_of(ev, t.set_ent[k], user_kind, reliable, en, me)) {
+            ev_of(ev, sent[k], user_kind, reliable, en, me)) {
           ++cnt;
           ent = en;
           meta = me;
@@ -1674,7 +1689,10 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
   if (with_frag)
     hipLaunchKernelGGL(k_fidx, dim3((uint32_t)hmin((max_frag + IT - 1) / IT, 4096)), dim3(IT), 0, st, frag, n_frag,
                        max_frag, max, x.fidx, x.fmask, t, records);
-  const uint32_t lds = rt_fits_lds(t) ? rt_lds_bytes(t.gmask + 1u, t.emask + 1u) : 0u;
+  uint32_t lds = rt_fits_lds(t) ? rt_lds_bytes(t.gmask + 1u, t.emask + 1u) : 0u;
+  // the target sets join the hash tables in LDS when both fit the tables' own limit
+  const bool sets_lds = lds && lds + sets_lds_bytes(t) <= RT_LDS_MAX;
+  if (sets_lds) lds += sets_lds_bytes(t);
   // Identity batches over many proxies take the per-proxy path with no host read-back:
   // classify writes the path's inputs, the sort runs over every record slot. The choice
   // uses the previous batch's counts (mean events per proxy), read without a sync.
@@ -1689,7 +1707,7 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
   // classify workgroups exceed its LDS tables (or path 4: the radix sort, tests)
   const uint64_t nblk = (max + CHR - 1) / CHR;
   const bool bucket = fast && t.n_proxies <= PB_MAX && nblk <= BK_MAX && s->path != 4;
-  FastOut fo{nullptr, nullptr, arena, dgram_off, S.seg_b, S.seg_e, s->ecap, nullptr, nullptr};
+  FastOut fo{nullptr, nullptr, arena, dgram_off, S.seg_b, S.seg_e, s->ecap, nullptr, nullptr, sets_lds ? 1u : 0u};
   if (fast) {
     if (!grow_pscratch(s, bucket ? nblk * CHR : max, st)) return RTPS_RX_ENOMEM;
     fo.pev = s->pev;

@@ -274,6 +274,7 @@ ReaderDev rt_dev(const ReaderTable* t) {
   r.n_sets = (uint32_t)t->first.size() - 1;
   r.n_proxies = t->n_proxies;
   r.max_set = t->max_set;
+  r.n_ent = t->first.empty() ? 0u : t->first.back();
   return r;
 }
 

@@ -26,6 +26,7 @@ struct ReaderDev {             // device view (kernel argument by value); gkeys 
   const rtps_target* set_ent;  // [set_first[n_sets]]
   uint32_t gmask, emask;
   uint32_t n_writer_sets, n_sets, n_proxies, max_set;
+  uint32_t n_ent;              // set_first[n_sets]: target entries of all sets
 };
 
 __host__ __device__ inline uint32_t rt_hash16(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
