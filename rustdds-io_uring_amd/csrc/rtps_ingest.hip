@@ -321,6 +321,9 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
       const u32x4* q = reinterpret_cast<const u32x4*>(recs + i);
       q0 = q[0];
       const u32x4 q1 = q[1];
+#ifdef RTPS_CLS_WHOLE  // variant builds: all four quads loaded up front (one load round, the whole record fetched)
+      const u32x4 qa = q[2], qb = q[3];
+#endif
       const uint32_t kind = (q0[1] >> 16) & 0xffu, route = (q1[3] >> 16) & 0xffu, pk = q1[3] >> 24;
       const uint32_t f = frag ? x.fidx[i] : NONE;
       // records the receiver passes to the user readers (not a builtin pair: discovery's)
@@ -329,8 +332,13 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
           ev = EV_SAMPLE;
           sn = frag[f].sn;
         } else if (kind == RTPS_DATA || kind == RTPS_HEARTBEAT || kind == RTPS_GAP) {
+#ifdef RTPS_CLS_WHOLE
+          q2 = qa;
+          if (FAST && kind != RTPS_DATA) q3 = qb;
+#else
           q2 = q[2];
           if (FAST && kind != RTPS_DATA) q3 = q[3];
+#endif
           const int64_t rsn = (int64_t)(((uint64_t)q2[1] << 32) | q2[0]);
           if (kind == RTPS_DATA) {
             // data_to_dds_data must succeed (reader.rs:552-558)
