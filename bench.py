@@ -98,25 +98,40 @@ def pmc_profile(workload):
     return d
 
 
-def time_dominant_kernel(rx, arena, off_t, ln_t, n, outs, stream, steps):
-    """Live HIP-event timing of the parse's dominant kernel alone (the first kernel of
-    rtps_rx_parse_batch: rtps_parse_spec_kernel, or rtps_parse_chain_kernel for mixed
-    traffic), K back-to-back launches on the parse stream, one event pair."""
+KERNEL_NAMES = {1: "rtps_parse_spec_kernel", 2: "rtps_parse_chain_kernel", 3: "rtps_parse_lds_kernel",
+                4: "rtps_parse_item_kernel"}
+
+
+def _time_phases(rx, arena, off_t, ln_t, n, outs, stream, steps, phases):
     which = 0
     for _ in range(3):
-        which = rx.debug_parse_phases(arena, off_t, ln_t, n, outs, 1)
+        which = rx.debug_parse_phases(arena, off_t, ln_t, n, outs, phases)
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     a.record(stream)
     for _ in range(steps):
-        rx.debug_parse_phases(arena, off_t, ln_t, n, outs, 1)
+        rx.debug_parse_phases(arena, off_t, ln_t, n, outs, phases)
     b.record(stream)
     torch.cuda.synchronize()
-    ms = a.elapsed_time(b) / steps
+    return a.elapsed_time(b) / steps, which
+
+
+def time_dominant_kernel(rx, arena, off_t, ln_t, n, outs, stream, steps):
+    """Live HIP-event timing of the parse's dominant kernel alone (the first kernel of
+    rtps_rx_parse_batch: rtps_parse_spec_kernel; for mixed traffic the item pass's
+    rtps_parse_item_kernel, or the chained kernels), K back-to-back launches on the parse
+    stream, one event pair.  For the item pass the finishing launches (the tile scan and the
+    record pass rtps_parse_emit_kernel) are timed the same way; the dominant kernel is the
+    slower of the item walk and the record pass."""
+    ms, which = _time_phases(rx, arena, off_t, ln_t, n, outs, stream, steps, 1)
+    kname, extra = KERNEL_NAMES[which], {}
+    if which == 4:
+        ms2, _ = _time_phases(rx, arena, off_t, ln_t, n, outs, stream, steps, 2)
+        extra = {"item_kernel_ms": ms, "scan_plus_emit_ms": ms2}
     for _ in range(2):  # full launches restore the per-launch bookkeeping
         rx.parse_batch_device(arena, off_t, ln_t, n, outs)
     torch.cuda.synchronize()
-    return ms, {1: "rtps_parse_spec_kernel", 2: "rtps_parse_chain_kernel", 3: "rtps_parse_lds_kernel"}[which]
+    return ms, kname, extra
 
 
 def time_ceilings(arena, off_t, ln_t, n, stream, steps):
@@ -241,10 +256,10 @@ def roofline(rx, args, arena, off_t, ln_t, n, outs, stream, total_bytes, alg_rea
     Bytes::split_off), so the fraction is on the FETCH_SIZE basis: calibrated HBM read
     bytes of the kernel per launch (committed PMC summary) / its live launch time /
     8 TB/s.  Writes (the 64-B records) are reported beside it, not in the numerator."""
-    ms, kname = time_dominant_kernel(rx, arena, off_t, ln_t, n, outs, stream, args.steps)
+    ms, kname, extra = time_dominant_kernel(rx, arena, off_t, ln_t, n, outs, stream, args.steps)
     pmc = pmc_profile(args.workload)
     key = {"rtps_parse_spec_kernel": "parse_spec", "rtps_parse_chain_kernel": "parse_chain",
-           "rtps_parse_lds_kernel": "parse_lds"}[kname]
+           "rtps_parse_lds_kernel": "parse_lds", "rtps_parse_item_kernel": "parse_item"}[kname]
     k = (pmc or {}).get(key) or {}
     scale = (pmc or {}).get("fetch_scale") or 1.0
     if pmc and pmc.get("datagrams_per_launch") == n and "FETCH_SIZE" in k:
@@ -266,7 +281,8 @@ def roofline(rx, args, arena, off_t, ln_t, n, outs, stream, total_bytes, alg_rea
                  "ceiling of this access shape is read_ceiling_frac)"}
     if pmc:
         r["pmc_source"] = pmc["_source"]
-    if kname == "rtps_parse_chain_kernel":
+    r.update(extra)
+    if kname in ("rtps_parse_chain_kernel", "rtps_parse_item_kernel"):
         torch.cuda.synchronize()
         n_rec = int(outs["n_records"].item())
         c = time_hops_ceilings(arena, off_t, ln_t, n, outs, n_rec, stream, args.steps)
@@ -275,8 +291,10 @@ def roofline(rx, args, arena, off_t, ln_t, n, outs, stream, total_bytes, alg_rea
                                       "hops per datagram + a 64-B record store per materialised submessage at the "
                                       "parse's positions, no field decode",
                             "one_walk_ms": c[1], "two_walk_ms": c[2]}
-            r["attainable_frac"] = c[1] / ms  # same-shape one-walk floor / kernel time
-            r["attainable_frac_two_walk"] = c[2] / ms
+            # same-shape one-walk floor / the parse's kernel time (the item pass: all three launches)
+            pm = ms + extra.get("scan_plus_emit_ms", 0.0)
+            r["attainable_frac"] = c[1] / pm
+            r["attainable_frac_two_walk"] = c[2] / pm
     if kname == "rtps_parse_spec_kernel":
         c = time_ceilings(arena, off_t, ln_t, n, stream, args.steps)
         if c:
@@ -292,35 +310,63 @@ def roofline(rx, args, arena, off_t, ln_t, n, outs, stream, total_bytes, alg_rea
 CDR_TYPES = {"T": "TSample", "C2": "C2Sample", "C3": "ShapeType", "C4": "C2Sample"}
 
 
-def cdr_decode_leg(rx, workload, arena, off_t, outs, n_rec, stream, steps):
-    """a18: batch CDR decode of this batch's DATA payloads into fixed-layout rows,
-    timed separately from the parse step (HIP events on the launch stream)."""
-    from rtps_rx import cdr
-    t = getattr(cdr, CDR_TYPES[workload])
-    rows, row_status = rx.alloc_rows(t, n_rec)
+def _time_launches(fn, stream, steps):
     for _ in range(3):
-        rx.cdr_decode(t, arena, off_t, outs, rows, row_status)
+        fn()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     a.record(stream)  # back-to-back launches, one event pair (see main's timed loop)
     for _ in range(steps):
-        rx.cdr_decode(t, arena, off_t, outs, rows, row_status)
+        fn()
     b.record(stream)
     torch.cuda.synchronize()
-    ms = a.elapsed_time(b) / steps
+    return a.elapsed_time(b) / steps
+
+
+def cdr_decode_leg(rx, workload, arena, off_t, outs, n_rec, stream, steps, iouts=None):
+    """a18: batch CDR decode of this batch's samples into fixed-layout rows, timed separately
+    from the parse step (HIP events on the launch stream).  With the ingest's deliveries
+    (iouts) the rows are COMPACT: one per sample that entered a history cache
+    (rtps_rx_cdr_decode_list over the delivery list), as the reference decodes only the
+    samples a DataReader takes; the per-record layout (a row per record, zero rows for the
+    records that are not samples) is timed beside it."""
+    from rtps_rx import cdr
+    t = getattr(cdr, CDR_TYPES[workload])
+    rows, row_status = rx.alloc_rows(t, n_rec)
+    ms_rec = _time_launches(lambda: rx.cdr_decode(t, arena, off_t, outs, rows, row_status), stream, steps)
     st = row_status[:n_rec].cpu().numpy()
     ok = int((st == cdr.CDR_OK).sum())
     # algorithmic bytes: 40 B of each record read, 1 status byte + one row written per record,
     # and for decoded rows the value bytes consumed (= row_bytes for these all-primitive types)
-    alg = n_rec * (40 + 1 + t.row_bytes) + ok * t.row_bytes
+    alg_rec = n_rec * (40 + 1 + t.row_bytes) + ok * t.row_bytes
     if ok == 0:  # nothing decoded (e.g. C4: its samples are DATA_FRAG, decoded after reassembly): no rate
         return {"sample_type": CDR_TYPES[workload], "records": n_rec, "decoded_ok": 0,
                 "status_hist": np.bincount(st, minlength=7).tolist(),
                 "note": "no DATA record of this batch decodes as this type, so no rate is reported"}
-    return {"sample_type": CDR_TYPES[workload], "row_bytes": t.row_bytes, "records": n_rec, "decoded_ok": ok,
-            "status_hist": np.bincount(st, minlength=7).tolist(), "kernel": "cdr_decode_kernel", "kernel_ms": ms,
-            "rows_per_s": ok / (ms * 1e-3), "alg_bytes_per_launch": alg,
-            "achieved_gbs": alg / (ms * 1e-3) / 1e9, "frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+    per_record = {"layout": "a row per record (rtps_rx_cdr_decode)", "kernel_ms": ms_rec, "rows": n_rec,
+                  "alg_bytes_per_launch": alg_rec, "achieved_gbs": alg_rec / (ms_rec * 1e-3) / 1e9,
+                  "frac": alg_rec / (ms_rec * 1e-3) / 1e9 / HBM_PEAK_GBS}
+    r = {"sample_type": CDR_TYPES[workload], "row_bytes": t.row_bytes, "records": n_rec, "decoded_ok": ok,
+         "status_hist": np.bincount(st, minlength=7).tolist(), "kernel": "cdr_decode_kernel"}
+    if iouts is None:
+        r.update({"layout": per_record["layout"], "kernel_ms": ms_rec, "rows_per_s": ok / (ms_rec * 1e-3),
+                  "alg_bytes_per_launch": alg_rec, "achieved_gbs": per_record["achieved_gbs"],
+                  "frac": per_record["frac"]})
+        return r
+    na = int(iouts["n_accepted"].item())
+    lrows, lst = rx.alloc_rows(t, max(na, 1))
+    ms = _time_launches(lambda: rx.cdr_decode_list(t, arena, off_t, outs, iouts["accepted"], 8, iouts["n_accepted"],
+                                                   na, lrows, lst), stream, steps)
+    lsv = lst[:na].cpu().numpy()
+    lok = int((lsv == cdr.CDR_OK).sum())
+    # compact rows: 8 B of delivery + 40 B of its record read, the value bytes consumed, one row
+    # + 1 status byte written per delivery
+    alg = na * (8 + 40 + 1 + t.row_bytes) + lok * t.row_bytes
+    r.update({"layout": "compact: a row per delivery (rtps_rx_cdr_decode_list over the ingest's deliveries)",
+              "rows": na, "rows_ok": lok, "kernel_ms": ms, "rows_per_s": lok / (ms * 1e-3),
+              "alg_bytes_per_launch": alg, "achieved_gbs": alg / (ms * 1e-3) / 1e9,
+              "frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "per_record_layout": per_record})
+    return r
 
 
 def frag_leg(rx, arena, off_t, outs, n_rec, recs, stream, steps):
@@ -382,7 +428,7 @@ def ingest_leg(rx, arena, off_t, outs, n_rec, recs, n_entries, stream, steps, fo
     # algorithmic bytes: every record read once (64 B), 1 accept byte written per record, 8 B per
     # delivery, per event 8 B of proxy state read and 4 B of change-set bits touched
     alg = n_rec * (64 + 1) + 8 * na + 12 * events
-    return {"kernel": "rtps_ingest (classify + heartbeat sort/scans + marks + decide + select + merge + state)",
+    return iouts, {"kernel": "rtps_ingest (classify + heartbeat sort/scans + marks + decide + select + merge + state)",
             "ms": ms, "records": n_rec, "events": events, "accepted": na,
             "samples_per_s": na / (ms * 1e-3), "records_per_s": n_rec / (ms * 1e-3),
             "window_overflow": int(iouts["n_window_overflow"].item()),
@@ -911,14 +957,16 @@ def measure(args, world, rank, dist, dev, allreduce_sum, allreduce_max):
             "overflow": any(e.overflowed() for e in exch)}
     if pipeline is not None:
         result["pipeline_with_ingest"] = pipeline
-    if world == 1 and not args.no_cdr:
-        result["cdr_decode"] = cdr_decode_leg(rx, args.workload, arena, off_t, outs, n_rec, stream, args.steps)
     fouts = None
     if world == 1 and not args.no_frag and args.workload == "C4" and recs is not None:
         fouts, result["frag_assemble"] = frag_leg(rx, arena, off_t, outs, n_rec, recs, stream, args.steps)
+    leg_iouts = None
     if world == 1 and not args.no_ingest and n_matched_writers:
-        result["ingest"] = ingest_leg(rx, arena, off_t, outs, n_rec, recs, n_matched_writers, stream, args.steps,
-                                      fouts=fouts)
+        leg_iouts, result["ingest"] = ingest_leg(rx, arena, off_t, outs, n_rec, recs, n_matched_writers, stream,
+                                                 args.steps, fouts=fouts)
+    if world == 1 and not args.no_cdr:
+        result["cdr_decode"] = cdr_decode_leg(rx, args.workload, arena, off_t, outs, n_rec, stream, args.steps,
+                                              iouts=leg_iouts)
     if world == 1 and not args.no_c1:
         result["c1_loopback"] = c1_loopback(dev, stream)
         # the same subscriber fed by 4 publisher threads: what the receive loop sustains when

@@ -252,6 +252,8 @@ typedef struct rtps_rx_ctx rtps_rx_ctx;
 #define RTPS_RX_ENOMEM (-3)
 #define RTPS_RX_ETOOBIG (-4)
 #define RTPS_RX_EABI (-5)
+#define RTPS_RX_EABORTED (-6) /* the RCCL communicator was aborted (and freed) after a failed
+                                 group: forget the handle, do not destroy it, make a new one */
 
 /* MessageReceiver::new(participant_guid_prefix, None)  (message_receiver.rs:158-182) */
 int rtps_rx_create(const rtps_rx_config* cfg, rtps_rx_ctx** out_ctx);
@@ -412,8 +414,11 @@ int rtps_rx_shard_pack(rtps_shard* s, const uint8_t* arena, uint64_t arena_len, 
  * stream), after the pack; then the counts are copied to the host.  Asynchronous. */
 int rtps_rx_shard_exchange(rtps_shard* s, void* comm, void* hip_stream);
 /* Waits for round 0's counts; if any pair overflowed its slot, moves the spill in a
- * second group of exact sizes (both ends know them from the counts).  After an
- * RTPS_RX_EHIP from either call the communicator is aborted and unusable. */
+ * second group of exact sizes (both ends know them from the counts).  Every failure
+ * of rtps_rx_shard_finish, and a failed group in rtps_rx_shard_exchange /
+ * rtps_rx_exchange, aborts the communicator (RTPS_RX_EABORTED): it is freed, and the
+ * peers' pending operations fail instead of waiting forever.  rtps_rx_shard_unpack
+ * refuses (RTPS_RX_EINVAL) a batch with a spill that rtps_rx_shard_finish did not move. */
 int rtps_rx_shard_finish(rtps_shard* s, void* comm, void* hip_stream);
 /* Owner side: every received record as one batch (reads the received counts: a host sync). */
 int rtps_rx_shard_unpack(rtps_shard* s, rtps_owner_batch* out);
@@ -492,6 +497,20 @@ int rtps_rx_cdr_decode(rtps_rx_ctx* ctx, const rtps_cdr_op* prog, uint32_t n_ops
                        const uint8_t* arena, uint64_t arena_len, const uint64_t* dgram_off,
                        const rtps_record* records, const uint64_t* n_records, uint64_t max_records,
                        uint8_t* rows, uint8_t* row_status);
+/* The same decode into COMPACT rows: row k decodes the record named by list entry k, a
+ * u32 record index at list + k * list_stride (device), for k < min(*n_list, max_list):
+ * e.g. the rtps_ingest_out deliveries (list = accepted, list_stride =
+ * sizeof(rtps_delivery), n_list = n_accepted), so only the samples that entered a
+ * history cache are decoded, as the reference decodes only the samples a DataReader
+ * takes (SimpleDataReader::deserialize_with per cache change,
+ * io_uring/dds/with_key/simpledatareader.rs:137-237).  A list entry naming a record
+ * that is not a DATA sample (or >= min(*n_records, max_records)) gets
+ * RTPS_CDR_NOT_DATA and a zero row.  list_stride: a multiple of 4, >= 4. */
+int rtps_rx_cdr_decode_list(rtps_rx_ctx* ctx, const rtps_cdr_op* prog, uint32_t n_ops, uint32_t row_bytes,
+                            const uint8_t* arena, uint64_t arena_len, const uint64_t* dgram_off,
+                            const rtps_record* records, const uint64_t* n_records, uint64_t max_records,
+                            const void* list, uint32_t list_stride, const uint64_t* n_list, uint64_t max_list,
+                            uint8_t* rows, uint8_t* row_status);
 
 /* ---- DataFrag reassembly ---------------------------
  * Replaces the per-reader FragmentAssembler / AssemblyBuffer

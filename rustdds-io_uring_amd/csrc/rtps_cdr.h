@@ -47,6 +47,12 @@ struct CdrArgs {
   uint64_t max_records;
   uint8_t* rows;
   uint8_t* row_status;
+  // list mode (list != nullptr): row k decodes record *(u32*)(list + k * list_stride), for
+  // k < min(*n_list, max_list); otherwise row r decodes record r
+  const uint8_t* list;
+  uint32_t list_stride;
+  const uint64_t* n_list;
+  uint64_t max_list;
 };
 
 // Builds the slot list from validated ops (host).  Returns false if slots overlap

@@ -325,8 +325,8 @@ __device__ __forceinline__ void wave_sync() {
 
 extern __shared__ uint8_t cdr_lds[];
 
-// One wave per chunk of 64 records.  Phase A: lane = record (validation, LDS
-// table).  Phase B: the wave writes the chunk's rows slot by slot, one 4-byte
+// One wave per chunk of 64 rows (a row = a record, or in list mode a list entry
+// naming a record).  Phase A: lane = row (validation, LDS table).  Phase B: the wave writes the chunk's rows slot by slot, one 4-byte
 // word per lane and item (item = record x word of the slot), so consecutive
 // lanes store consecutive words and every row byte is written exactly once.
 template <bool WIDE>
@@ -338,7 +338,8 @@ void cdr_decode_kernel(CdrProg P, CdrArgs a) {
   uint64_t* vbase = (uint64_t*)(T + 256);    // [64] arena offset of the value
   uint32_t* posT = (uint32_t*)(T + 768);     // [n_ops][64]
   uint32_t* lenT = posT + P.n_ops * 64u;     // [n_ops][64]
-  const uint64_t n = min(*a.n_records, a.max_records);
+  const uint64_t n = a.list ? min(*a.n_list, a.max_list) : min(*a.n_records, a.max_records);
+  const uint64_t nrec = min(*a.n_records, a.max_records);
   const uint64_t chunks = (n + 63) / 64;
   for (uint64_t c = (uint64_t)blockIdx.x * wpb + wave; c < chunks; c += (uint64_t)gridDim.x * wpb) {
     const uint64_t r0 = c * 64;
@@ -347,7 +348,9 @@ void cdr_decode_kernel(CdrProg P, CdrArgs a) {
     uint32_t st = 0xff, le = 1;
     uint64_t vb = 0;
     if (lane < nv) {
-      const rtps_record* rec = a.records + r0 + lane;
+      // the row's record: the row itself, or its list entry (a delivery, a sample index)
+      const uint64_t ri = a.list ? *reinterpret_cast<const uint32_t*>(a.list + (r0 + lane) * a.list_stride) : r0 + lane;
+      const rtps_record* rec = a.records + (ri < nrec ? ri : 0);
       // bytes 0..31 (dgram_idx @0, kind @6, payload_kind @31) and 40..47 (pl_off, pl_len, rep_id)
       const uint4 h0 = *(const uint4*)rec;
       const uint4 h1 = *(const uint4*)((const uint8_t*)rec + 16);
@@ -355,7 +358,7 @@ void cdr_decode_kernel(CdrProg P, CdrArgs a) {
       const uint32_t kind = (h0.y >> 16) & 0xff, pk = h1.w >> 24;
       const uint32_t pl_off = u0.x & 0xffff, pl_len = u0.x >> 16;
       const uint32_t id0 = u0.y & 0xff, id1 = (u0.y >> 8) & 0xff;
-      if (kind != RTPS_DATA || pk != RTPS_PK_DATA || pl_len < 4) {
+      if (ri >= nrec || kind != RTPS_DATA || pk != RTPS_PK_DATA || pl_len < 4) {
         st = RTPS_CDR_NOT_DATA;
       } else if (id0 != 0 || (id1 != 0 && id1 != 1 && id1 != 3)) {
         st = RTPS_CDR_BAD_ENCODING;
@@ -546,11 +549,11 @@ bool rtps_cdr_build_slots(CdrProg& P) {
   return true;
 }
 
-// Host launcher, called by rtps_rx_cdr_decode (rtps_rx.hip) after validation.
+// Host launcher, called by rtps_rx_cdr_decode / _list (rtps_rx.hip) after validation.
 int rtps_cdr_launch(hipStream_t s, const CdrProg& P, const CdrArgs& a, uint32_t max_blocks) {
   uint32_t wpb = 65536u / P.lds_per_wave;
   wpb = wpb < 1 ? 1 : (wpb > 4 ? 4 : wpb);
-  const uint64_t chunks = (a.max_records + 63) / 64;
+  const uint64_t chunks = ((a.list ? a.max_list : a.max_records) + 63) / 64;
   uint64_t blocks = (chunks + wpb - 1) / wpb;
   if (blocks > (uint64_t)max_blocks * CDR_GRID_MULT) blocks = (uint64_t)max_blocks * CDR_GRID_MULT;
   if (blocks == 0) return 0;

@@ -20,8 +20,11 @@
 //
 // Failure: if enqueuing a send or receive fails part-way, the peers would wait
 // for operations that were never posted, so the group is ended and the
-// communicator aborted (ncclCommAbort): the caller gets RTPS_RX_EHIP and must
-// make a new communicator.
+// communicator aborted (ncclCommAbort, which frees it): the caller gets
+// RTPS_RX_EABORTED, must forget the handle (never destroy it) and make a new
+// communicator.  Every failure of rtps_rx_shard_finish aborts too: the peers post
+// their spill rounds after round 0, so a rank that returns without its own would
+// leave them waiting.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <string.h>
@@ -53,6 +56,12 @@ static bool recv_bytes(void* buf, size_t n, int peer, ncclComm_t c, hipStream_t 
     if (ncclRecv(p + o, k, ncclUint8, peer, c, st) != ncclSuccess) return false;
   }
   return true;
+}
+
+// the communicator is unusable (a group was cut short): abort (frees it) and say so
+static int abort_comm(ncclComm_t c) {
+  (void)ncclCommAbort(c);
+  return RTPS_RX_EABORTED;
 }
 
 extern "C" {
@@ -102,10 +111,7 @@ int rtps_rx_exchange(rtps_rx_ctx* ctx, void* comm, void* hip_stream, const void*
          send_bytes(s + (size_t)p * bytes, bytes, p, c, st) && recv_bytes(r + (size_t)p * bytes, bytes, p, c, st);
   }
   const bool ended = ncclGroupEnd() == ncclSuccess;
-  if (!ok || !ended) {
-    (void)ncclCommAbort(c);
-    return RTPS_RX_EHIP;
-  }
+  if (!ok || !ended) return abort_comm(c);
   return RTPS_RX_OK;
 }
 
@@ -130,16 +136,14 @@ int rtps_rx_shard_exchange(rtps_shard* s, void* comm, void* hip_stream) {
          send_bytes(s->s_blob + p * bb, bb, p, c, st) && recv_bytes(s->r_blob + p * bb, bb, p, c, st);
   }
   const bool ended = ncclGroupEnd() == ncclSuccess;
-  if (!ok || !ended) {
-    (void)ncclCommAbort(c);
-    return RTPS_RX_EHIP;
-  }
+  if (!ok || !ended) return abort_comm(c);
   const size_t nb = (size_t)world * sizeof(rtps_shard_counts);
   if (hipMemcpyAsync(s->h_send, s->s_counts, nb, hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipMemcpyAsync(s->h_recv, s->r_counts, nb, hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipEventRecord(s->counts_ev, st) != hipSuccess || hipEventRecord(s->done, st) != hipSuccess)
     return RTPS_RX_EHIP;
   s->exchanged = true;
+  s->finished = false;
   return RTPS_RX_OK;
 }
 
@@ -147,27 +151,27 @@ int rtps_rx_shard_finish(rtps_shard* s, void* comm, void* hip_stream) {
   if (!s || !comm) return RTPS_RX_EINVAL;
   if (!s->exchanged) return RTPS_RX_EINVAL;  // no round 0 to finish
   ncclComm_t c = (ncclComm_t)comm;
-  if (hipSetDevice(s->device) != hipSuccess) return RTPS_RX_EHIP;
+  // from here on every failure aborts: the peers post their spill rounds regardless
+  if (hipSetDevice(s->device) != hipSuccess) return abort_comm(c);
   hipStream_t st = hip_stream ? (hipStream_t)hip_stream : rtps_ctx_stream(s->ctx);
-  if (hipEventSynchronize(s->counts_ev) != hipSuccess) return RTPS_RX_EHIP;
+  if (hipEventSynchronize(s->counts_ev) != hipSuccess) return abort_comm(c);
   const uint32_t world = s->n_ranks;
   // spill sizes: what this rank still sends to each peer, what it still receives
   uint64_t need_r = 0, need_b = 0, any = 0;
   for (uint32_t p = 0; p < world; ++p) {
     const rtps_shard_counts& r = s->h_recv[p];
     const rtps_shard_counts& q = s->h_send[p];
-    if (r.cut > r.n || r.cut_bytes > r.bytes || q.cut > q.n || q.cut_bytes > q.bytes) return RTPS_RX_EINVAL;
+    if (r.cut > r.n || r.cut_bytes > r.bytes || q.cut > q.n || q.cut_bytes > q.bytes) return abort_comm(c);
     need_r += r.n - r.cut;
     need_b += r.bytes - r.cut_bytes;
     any |= (r.n - r.cut) | (q.n - q.cut) | (r.bytes - r.cut_bytes) | (q.bytes - q.cut_bytes);
   }
-  if (!any) return RTPS_RX_OK;
-  const int rc = rtps_rx_shard_reserve_spill(s, need_r, need_b);
-  if (rc) {
-    (void)ncclCommAbort(c);  // the peers' spill sends cannot be received
-    return rc;
+  if (!any) {
+    s->finished = true;
+    return RTPS_RX_OK;
   }
-  if (ncclGroupStart() != ncclSuccess) return RTPS_RX_EHIP;
+  if (rtps_rx_shard_reserve_spill(s, need_r, need_b) != RTPS_RX_OK) return abort_comm(c);  // spill not receivable
+  if (ncclGroupStart() != ncclSuccess) return abort_comm(c);
   bool ok = true;
   uint64_t sb = 0, sbb = 0, rs = 0, rsb = 0;  // send-side exact-layout bases, receive-side spill offsets
   for (uint32_t p = 0; p < world && ok; ++p) {
@@ -184,11 +188,10 @@ int rtps_rx_shard_finish(rtps_shard* s, void* comm, void* hip_stream) {
     rsb += rbytes;
   }
   const bool ended = ncclGroupEnd() == ncclSuccess;
-  if (!ok || !ended) {
-    (void)ncclCommAbort(c);
-    return RTPS_RX_EHIP;
-  }
-  return hipEventRecord(s->done, st) == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP;
+  if (!ok || !ended) return abort_comm(c);
+  if (hipEventRecord(s->done, st) != hipSuccess) return abort_comm(c);
+  s->finished = true;
+  return RTPS_RX_OK;
 }
 
 }  // extern "C"

@@ -154,9 +154,6 @@ __device__ __forceinline__ uint32_t wslot_find(const uint64_t* wkey, uint64_t h)
 __device__ __forceinline__ bool frag_select(const FragSel& sel, const rtps_record* r, const uint4& ra, const uint4& rb,
                                             uint32_t& word) {
   word = 0;
-#ifdef RTPS_FRAG_ABL_SEL0  // timing-only variant builds: no reader selection (every record one assembler per writer)
-  return true;
-#endif
   if (sel.mode == 0) return true;
   if (sel.mode == 2) { word = rb.z; return true; }  // an expanded copy: its reader_id
   // mode 1: the record's one target reader (Domain::handle_event, dp_event_loop.rs:266-327)

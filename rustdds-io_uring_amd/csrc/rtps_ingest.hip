@@ -66,9 +66,6 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr uint32_t IT = 256;
 constexpr uint32_t NONE = 0xffffffffu;
-#ifndef RTPS_CLS_ABL  // timing-only ablations of the classify pass (variant builds): 1 GAP
-#define RTPS_CLS_ABL 0  // bitmap reads, 2 packed-event stores, 4 target-set probes, 8 sort-pair / accept stores
-#endif
 constexpr uint32_t W = RTPS_INGEST_WINDOW;  // sequence numbers tracked per proxy
 constexpr uint32_t WW = W / 32;             // bitmap words per proxy
 constexpr uint32_t ECAP_MAX = 1u << 14;     // writer proxies
@@ -321,9 +318,6 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
       const u32x4* q = reinterpret_cast<const u32x4*>(recs + i);
       q0 = q[0];
       const u32x4 q1 = q[1];
-#ifdef RTPS_CLS_WHOLE  // variant builds: all four quads loaded up front (one load round, the whole record fetched)
-      const u32x4 qa = q[2], qb = q[3];
-#endif
       const uint32_t kind = (q0[1] >> 16) & 0xffu, route = (q1[3] >> 16) & 0xffu, pk = q1[3] >> 24;
       const uint32_t f = frag ? x.fidx[i] : NONE;
       // records the receiver passes to the user readers (not a builtin pair: discovery's)
@@ -332,13 +326,8 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
           ev = EV_SAMPLE;
           sn = frag[f].sn;
         } else if (kind == RTPS_DATA || kind == RTPS_HEARTBEAT || kind == RTPS_GAP) {
-#ifdef RTPS_CLS_WHOLE
-          q2 = qa;
-          if (FAST && kind != RTPS_DATA) q3 = qb;
-#else
           q2 = q[2];
           if (FAST && kind != RTPS_DATA) q3 = q[3];
-#endif
           const int64_t rsn = (int64_t)(((uint64_t)q2[1] << 32) | q2[0]);
           if (kind == RTPS_DATA) {
             // data_to_dds_data must succeed (reader.rs:552-558)
@@ -353,9 +342,8 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
         }
         if (ev != EV_NONE) {
           uint32_t r2 = 0;
-          set = (RTPS_CLS_ABL & 4) ? 0u
-                : lds ? rt_classify<true>(t, s_rt, q0[2], q0[3], q1[0], q1[1], r2)
-                      : rt_classify<false>(t, s_rt, q0[2], q0[3], q1[0], q1[1], r2);
+          set = lds ? rt_classify<true>(t, s_rt, q0[2], q0[3], q1[0], q1[1], r2)
+                    : rt_classify<false>(t, s_rt, q0[2], q0[3], q1[0], q1[1], r2);
           if (set == NONE) ev = EV_NONE;
           user_kind = (q1[1] >> 24 & 0xf0u) == 0u;  // EntityKind::is_user_defined (guid.rs:168-170)
         }
@@ -384,7 +372,7 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
     ne += cnt;
     if (IDENT) {  // at most one event: write it at index i
       const uint8_t evi = cnt ? ev : EV_NONE;
-      if (!(RTPS_CLS_ABL & 8)) x.emeta[i] = meta;
+      x.emeta[i] = meta;
       if (!FAST) x.erec[i] = (uint32_t)i;  // (the per-proxy identity path reads no event -> record map)
       if (!FAST) {  // (the per-proxy identity path reads the packed events instead)
         x.evt[i] = evi;
@@ -395,13 +383,11 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
         x.hkey[i] = evi == EV_HB ? 1u : 0u;  // selection flag of the HEARTBEAT compaction
       } else {
         const bool px = evi != EV_NONE && ent != NONE;
-        if (!(RTPS_CLS_ABL & 8)) {
-          if (!BUCKET) {
-            x.hkey[i] = px ? ent : t.n_proxies;  // sort pairs: (proxy, slot); n_proxies sorts last
-            x.sval[i] = (uint32_t)i;
-          }
-          fo.acc[i] = (evi == EV_SAMPLE && ent == NONE) ? 1 : 0;  // proxy-less samples (reader.rs:734-739)
+        if (!BUCKET) {
+          x.hkey[i] = px ? ent : t.n_proxies;  // sort pairs: (proxy, slot); n_proxies sorts last
+          x.sval[i] = (uint32_t)i;
         }
+        fo.acc[i] = (evi == EV_SAMPLE && ent == NONE) ? 1 : 0;  // proxy-less samples (reader.rs:734-739)
         if (px) {
           key = ent;
           P.sn = sn;
@@ -417,14 +403,14 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
             const bool le = (fl & 1u) != 0u;
             P.m |= (le ? PM_LE : 0u) | (nbits << 8);
             P.bw = fo.dgram_off[q0[0]] + (q3[1] & 0xffffu);  // dgram_idx, u.gap.bitmap_off
-            if (nbits <= 64u && !(RTPS_CLS_ABL & 1)) {
+            if (nbits <= 64u) {
               const uint8_t* bp = fo.arena + P.bw;
               const uint32_t w0 = nbits ? rd32(bp, le) : 0u, w1 = nbits > 32u ? rd32(bp + 4, le) : 0u;
               P.bw = (uint64_t)w0 | ((uint64_t)w1 << 32);
               P.m |= PM_INL;
             }
           }
-          if (!BUCKET && !(RTPS_CLS_ABL & 2)) fo.pev[i] = P;
+          if (!BUCKET) fo.pev[i] = P;
         }
       }
     } else {
@@ -517,7 +503,7 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
       }
       // the position back to the slot's own lane (forward permute: lane sl receives it)
       pos = (uint32_t)__builtin_amdgcn_ds_permute((int)(sl << 2), (int)pos);
-      if (key[j] != NONE && !(RTPS_CLS_ABL & 2)) region[pos] = P[j];
+      if (key[j] != NONE) region[pos] = P[j];
     }
   }
   __shared__ uint32_t s_n[4];
@@ -1106,9 +1092,6 @@ struct GapE {
   uint32_t m, q; // PEv.m, the event's position
 };
 constexpr uint32_t GCAP = 512;  // GAPs per chunk spread one per thread; the rest stay with their threads
-#ifndef RTPS_PROXY_ABL  // timing-only ablations of k_proxy (variant builds, wrong results): 1 no GAP
-#define RTPS_PROXY_ABL 0  // marks / GAP merge, 2 no hash inserts, 4 no HEARTBEAT scans
-#endif
 
 // One workgroup per proxy: its events in slot order replayed in chunks of PCH
 // against the proxy's change-set window in LDS.  The events: BK = false, sorted by
@@ -1231,7 +1214,7 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
     int64_t cnt_total;
     int64_t c_ex = run_cnt;
     cnt_total = run_cnt;
-    if (!(RTPS_PROXY_ABL & 4)) c_ex = block_max_excl(cmax, run_cnt, s_w, cnt_total);
+    c_ex = block_max_excl(cmax, run_cnt, s_w, cnt_total);
     int64_t fmax = INT64_MIN, f[PPT];
 #pragma unroll
     for (uint32_t j = 0; j < PPT; ++j) {
@@ -1243,7 +1226,7 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
     int64_t thr_total;
     int64_t thr = run_thr;
     thr_total = run_thr;
-    if (!(RTPS_PROXY_ABL & 4)) thr = block_max_excl(fmax, run_thr, s_w, thr_total);
+    thr = block_max_excl(fmax, run_thr, s_w, thr_total);
     run_cnt = cnt_total;
     run_thr = thr_total;
     PST(2);
@@ -1252,7 +1235,7 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
     for (uint32_t j = 0; j < PPT; ++j) {
       slot[j] = NONE;
       const int64_t vj = v[j];
-      if (!(RTPS_PROXY_ABL & 2) && (m[j] & 3u) == EV_SAMPLE && vj >= lo && vj < lo + (int64_t)W) {
+      if ((m[j] & 3u) == EV_SAMPLE && vj >= lo && vj < lo + (int64_t)W) {
         const uint32_t off = (uint32_t)(vj - lo);
         uint32_t h = ph_hash(off);
         for (;;) {
@@ -1305,7 +1288,7 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
       else
         gap_cover(gv, ga, arena + bw, gm >> 8, (gm & PM_LE) != 0u, lo, mark);
     };
-    for (uint32_t g = tid; g < ((RTPS_PROXY_ABL & 1) ? 0u : ngap); g += PT) {
+    for (uint32_t g = tid; g < ngap; g += PT) {
       const GapE ge = s_gap[g];
       gap_mark(ge.v, ge.a, ge.bw, ge.m, ge.q);
     }
@@ -1358,7 +1341,7 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
         gap_or(v[j], a[j], bwj[j], m[j]);
       }
     }
-    for (uint32_t g = tid; g < ((RTPS_PROXY_ABL & 1) ? 0u : ngap); g += PT) {
+    for (uint32_t g = tid; g < ngap; g += PT) {
       const GapE ge = s_gap[g];
       gap_or(ge.v, ge.a, ge.bw, ge.m);
     }

@@ -320,6 +320,11 @@ int rtps_rx_debug_rt_set(void* t, const rtps_reader* readers, uint32_t nr, const
   return rt_set(static_cast<ReaderTable*>(t), readers, nr, proxies, np, nullptr);
 }
 /* the device view rt_dev returns (pointers into the table's buffers) */
+/* sizeof(ReaderDev): a debug hook's caller must mirror the struct exactly (rtps_rx_debug_rt_view
+   writes the whole struct) */
+uint32_t rtps_rx_debug_rt_view_size(void) { return (uint32_t)sizeof(ReaderDev); }
+static_assert(sizeof(ReaderDev) == 6 * sizeof(void*) + 8 * sizeof(uint32_t),
+              "ReaderDev changed: update the debug mirrors (tests/test_readers_cpu.py View)");
 int rtps_rx_debug_rt_view(const void* t, ReaderDev* out) {
   if (!out) return RTPS_RX_EINVAL;
   *out = rt_dev(static_cast<const ReaderTable*>(t));

@@ -1094,6 +1094,328 @@ __global__ __launch_bounds__(TILE, RTPS_CH_WAVES_PER_SIMD) void rtps_parse_chain
 }
 
 // ---------------------------------------------------------------------------
+// E / S / W: the item pass for mixed traffic (the default
+// since round 4).  The chained kernel C spends its time in three places: the
+// count walk, the look-back wait, and a second walk that re-fetches every
+// submessage to write it.  Here the count walk leaves behind what the write
+// needs, so no kernel waits on another tile and no lane chases a chain twice:
+//   E rtps_parse_item_kernel  one workgroup per tile of 256 datagrams: the count
+//     walk (status, records per datagram) appends one 16-B ITEM per materialised
+//     submessage to its wave's slab of CAPW items, at a position taken with a
+//     wave ballot in the walk loop (no atomics, no ordering between tiles):
+//       [0] sub_off | src_off << 16   src_off: datagram offset of the source prefix
+//                                     in effect (8: the header's; INFO_SRC at o: o + 12)
+//       [1] j | lane << 16 | dst_ok << 22 | ts_valid << 23 | kind << 24
+//                                     j: the record's index inside its datagram
+//       [2] ts_sec  [3] ts_frac       the timestamp in effect (host order)
+//     A wave whose items overflow its slab is flagged; W walks its datagrams.
+//   S rtps_parse_scan_kernel  one workgroup: exclusive scan of the tile counts,
+//     n_records, the launch-choice report (what kernel B does after A / C).
+//   W rtps_parse_emit_kernel  one workgroup per tile: one thread per item, in slab
+//     order (coalesced item loads): the item names the kind, so the submessage
+//     window is ONE gather issued at once (16 B, + 16 B for kinds that read body
+//     bytes past 12), the source prefix comes from a per-datagram LDS stage, the
+//     interpreter state from the item; the per-kind reader and the record tail are
+//     the walk's own (sub_body / rec_finish); the record goes to tile prefix +
+//     datagram's local first record + j.
+// ---------------------------------------------------------------------------
+#ifndef RTPS_IT_CAPW
+#define RTPS_IT_CAPW 512u
+#endif
+constexpr uint32_t CAPW = RTPS_IT_CAPW;  // items per wave slab (C3 averages 243 per 64 datagrams)
+constexpr uint32_t WCNT_OVERFLOW = 0x80000000u;
+#ifndef RTPS_IT_WAVES_PER_SIMD
+#define RTPS_IT_WAVES_PER_SIMD 8
+#endif
+#ifndef RTPS_EM_WAVES_PER_SIMD
+#define RTPS_EM_WAVES_PER_SIMD 8
+#endif
+
+// The count walk of walk<false> plus the items.  wpos: the wave's slab position,
+// the same in every active lane (each iteration advances it by the ballot's count).
+__device__ uint32_t item_walk(const KParams& p, const Src& s, const uint32_t* H, uint32_t L, uint32_t lane,
+                              u32x4* slab, uint32_t& wpos, uint32_t& nrec) {
+  nrec = 0;
+  if (L > RTPS_MAX_DATAGRAM) return RTPS_DGRAM_TOO_LONG;
+  const uint32_t MAGIC_RTPS = 0x53505452u, MAGIC_RTPX = 0x58505452u;
+  if (L < 20u) {  // message_receiver.rs:238-251
+    if (L >= 16u && H[0] == MAGIC_RTPS && (H[2] >> 8) == 0x534444u && H[3] == 0x474e4950u) return RTPS_DGRAM_PING;
+    return RTPS_DGRAM_SHORT;
+  }
+  if (H[0] != MAGIC_RTPS) return H[0] == MAGIC_RTPX ? RTPS_DGRAM_RTPX : RTPS_DGRAM_BAD_MAGIC;
+  if ((H[1] & 0xffu) > 2u) return RTPS_DGRAM_BAD_HEADER;
+  // handle_parsed_message_2 (:289-295): src := header prefix, dest := own, ts := None
+  Interp st{H[2], H[3], H[4], true, false, 0u, 0u};
+  uint32_t src_off = 8u;
+  const uint64_t lt = lane ? (~0ull >> (64u - lane)) : 0ull;
+  uint32_t o = 20;
+  while (o < L) {
+    const uint32_t rem = L - o;
+    if (rem < 4u) return RTPS_DGRAM_SUBMSG_ERR;
+    Win W;
+    if (o == 20u) head_win(H, W);
+    else load_win_lazy<false>(s, o, W);
+    const uint32_t kind = W.w[0] & 0xffu, flags = (W.w[0] >> 8) & 0xffu;
+    const bool le = (flags & 1u) != 0u;
+    const uint32_t eff = eff_len(kind, e16(W.w[0], 1, le), rem);
+    if (4u + eff > rem) return RTPS_DGRAM_SUBMSG_ERR;
+    Rec R;
+    SubOut so;
+    if (!sub_body<false>(s, W, kind, flags, le, o + 4u, eff, R, so)) return RTPS_DGRAM_SUBMSG_ERR;
+    interp_update(p, st, W, kind, flags, le);  // (INFO_SRC's prefix words are not loaded here: src_off)
+    if (kind == RTPS_INFO_SRC) src_off = o + 12u;
+    const bool em = so.cls != 0u;
+    const uint64_t m = __ballot(em);
+    if (em) {
+      const uint32_t pos = wpos + (uint32_t)__popcll(m & lt);
+      if (pos < CAPW)
+        slab[pos] = u32x4{o | (src_off << 16),
+                          nrec | (lane << 16) | ((st.dst_ok ? 1u : 0u) << 22) | ((st.ts_valid ? 1u : 0u) << 23) |
+                              (kind << 24),
+                          st.ts_sec, st.ts_frac};
+      nrec++;
+    }
+    wpos += (uint32_t)__popcll(m);
+    o += 4u + eff;
+  }
+  return RTPS_DGRAM_OK;
+}
+
+__global__ __launch_bounds__(TILE, RTPS_IT_WAVES_PER_SIMD) void rtps_parse_item_kernel(KParams p, uint32_t n_tiles,
+                                                                                     uint32_t k_spec, u32x4* items,
+                                                                                     uint32_t* wcnt) {
+  __shared__ uint32_t s_wave_sum[WAVES], s_wave_bad[WAVES];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t tile = blockIdx.x;
+  TileCtx t;
+  load_tile(p, tile, t);
+  u32x4* slab = items + (size_t)(tile * WAVES + wave) * CAPW;
+  uint32_t cnt = 0, wpos = 0, st = RTPS_DGRAM_OK;
+  if (t.valid) {
+    if (!t.addressable) st = RTPS_DGRAM_TOO_LONG;
+    else st = item_walk(p, t.s, t.H, t.L, lane, slab, wpos, cnt);
+    if (st != RTPS_DGRAM_OK) cnt = 0;
+  }
+  // the wave's item total: the position of the lane that walked longest
+  uint32_t wtot = wpos, wsum = cnt;
+#pragma unroll
+  for (uint32_t d = 32; d >= 1; d >>= 1) {
+    const uint32_t y = __shfl_xor(wtot, d, 64);
+    wtot = y > wtot ? y : wtot;
+    wsum += __shfl_xor(wsum, d, 64);
+  }
+  const uint64_t bad = __ballot(t.valid && cnt != k_spec);
+  if (lane == 0) {
+    s_wave_sum[wave] = wsum;
+    s_wave_bad[wave] = bad != 0ull;
+    wcnt[tile * WAVES + wave] = wtot > CAPW ? WCNT_OVERFLOW : wtot;
+  }
+  Scratch x = scratch_of(p.scratch, n_tiles);
+  if (t.valid) {
+    p.status[t.i] = (uint8_t)st;
+    x.dcount[t.i] = (uint16_t)cnt;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t agg = 0, mixed = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < WAVES; ++w) { agg += s_wave_sum[w]; mixed |= s_wave_bad[w]; }
+    x.info[tile] = agg | INFO_NONSPEC | (mixed ? INFO_MIXED : 0u);
+  }
+}
+
+// S: one workgroup of 1024 threads, 4 tiles per thread per round
+constexpr uint32_t SCAN_T = 1024;
+__global__ __launch_bounds__(SCAN_T) void rtps_parse_scan_kernel(KParams p, uint32_t n_tiles, uint32_t parity,
+                                                                 uint64_t* tprefix) {
+  __shared__ uint64_t s_w[SCAN_T / 64];
+  __shared__ uint32_t s_m[SCAN_T / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  Scratch x = scratch_of(p.scratch, n_tiles);
+  uint64_t carry = 0;
+  uint32_t mixed = 0;
+  for (uint32_t base = 0; base < n_tiles; base += 4u * SCAN_T) {
+    const uint32_t t0 = base + 4u * tid;
+    uint32_t c[4];
+    if (t0 + 3u < n_tiles) {
+      const u32x4 v = *reinterpret_cast<const u32x4*>(x.info + t0);  // info is 16-B aligned
+      c[0] = v[0]; c[1] = v[1]; c[2] = v[2]; c[3] = v[3];
+    } else {
+#pragma unroll
+      for (uint32_t k = 0; k < 4; ++k) c[k] = t0 + k < n_tiles ? x.info[t0 + k] : 0u;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) { mixed += (c[k] & INFO_MIXED) != 0u; c[k] &= INFO_COUNT; }
+    const uint64_t own = (uint64_t)c[0] + c[1] + c[2] + c[3];
+    uint64_t incl = own;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const uint64_t y = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += y;
+    }
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    uint64_t before = carry, total = carry;
+#pragma unroll
+    for (uint32_t w = 0; w < SCAN_T / 64; ++w) {
+      const uint64_t v = s_w[w];
+      if (w < wave) before += v;
+      total += v;
+    }
+    uint64_t e = before + incl - own;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      if (t0 + k < n_tiles) tprefix[t0 + k] = e;
+      e += c[k];
+    }
+    carry = total;
+    __syncthreads();  // s_w reuse
+  }
+#pragma unroll
+  for (uint32_t d = 32; d >= 1; d >>= 1) mixed += __shfl_xor(mixed, d, 64);
+  if (lane == 0) s_m[wave] = mixed;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t m = 0;
+    for (uint32_t w = 0; w < SCAN_T / 64; ++w) m += s_m[w];
+    *p.n_records = carry;
+    p.mixed_out[0] = m;
+    p.mixed_out[1] = n_tiles;
+    x.flag[parity ^ 1u] = 0u;  // kernel B's invariant for the next launch (B does not run after S)
+  }
+}
+
+__global__ __launch_bounds__(TILE, RTPS_EM_WAVES_PER_SIMD) void rtps_parse_emit_kernel(KParams p, uint32_t n_tiles,
+                                                                                     const u32x4* items,
+                                                                                     const uint32_t* wcnt,
+                                                                                     const uint64_t* tprefix) {
+  __shared__ uint32_t s_rbase[TILE];   // tile-local first record of each datagram (NONE: no records)
+  __shared__ uint32_t s_doff[TILE];    // datagram start relative to the workgroup's descriptor base
+  __shared__ uint32_t s_len[TILE];
+  __shared__ uint32_t s_pfx[TILE * 3]; // header GuidPrefix of each datagram
+  __shared__ uint32_t s_wsum[WAVES], s_nit[WAVES + 1];
+  __shared__ uint64_t s_lo[WAVES], s_hi[WAVES];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t tile = blockIdx.x;
+  mt_stage(p);  // visible after the __syncthreads below
+  Scratch x = scratch_of(p.scratch, n_tiles);
+  const uint64_t prefix = tprefix[tile];
+  const uint32_t wc = wcnt[tile * WAVES + wave];
+  const uint32_t i = tile * TILE + tid;
+  const bool valid = i < p.n;
+  const uint32_t cnt = valid ? (uint32_t)x.dcount[i] : 0u;
+  const uint64_t off = (valid && cnt) ? p.dgram_off[i] : 0ull;
+  const uint32_t L = (valid && cnt) ? p.dgram_len[i] : 0u;
+  const uint32_t incl = wave_incl_scan(cnt, lane);
+  // descriptor base: the arena when every offset fits 32 bits, else the tile's smallest
+  // offset (a tile spanning 4 GiB or more takes the lane walk)
+  const bool wide = p.arena_len >= ARENA_DIRECT;
+  uint64_t lo = cnt ? off : ~0ull, hi = cnt ? off + L : 0ull;
+  if (wide) {
+#pragma unroll
+    for (uint32_t d = 32; d >= 1; d >>= 1) {
+      const uint64_t a = __shfl_xor(lo, d, 64), b = __shfl_xor(hi, d, 64);
+      lo = a < lo ? a : lo;
+      hi = b > hi ? b : hi;
+    }
+  }
+  if (lane == 63) s_wsum[wave] = incl;
+  if (lane == 0) { s_nit[wave] = (wc & WCNT_OVERFLOW) ? 0u : wc; s_lo[wave] = lo; s_hi[wave] = hi; }
+  __syncthreads();
+  uint32_t wave_off = 0;
+  uint64_t tlo = ~0ull, thi = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < WAVES; ++w) {
+    if (w < wave) wave_off += s_wsum[w];
+    tlo = s_lo[w] < tlo ? s_lo[w] : tlo;
+    thi = s_hi[w] > thi ? s_hi[w] : thi;
+  }
+  const uint64_t tb = (wide && tlo != ~0ull) ? tlo : 0ull;
+  const bool tile_walk = wide && tlo != ~0ull && thi - tlo >= 0xffff0000ull;
+  const bool walk_wave = tile_walk || (wc & WCNT_OVERFLOW) != 0u;
+  const uint32_t local = wave_off + incl - cnt;
+  if (valid && p.rec_begin) p.rec_begin[i] = (uint32_t)(prefix + local);
+  if (walk_wave) {  // the items did not fit (or cannot be addressed): walk the wave's datagrams
+    s_rbase[tid] = 0xffffffffu;
+    TileCtx t;
+    load_tile(p, tile, t);
+    if (t.valid && cnt) {
+      uint32_t n2;
+      walk<true>(p, t.s, t.H, t.L, t.i, prefix + local, n2);
+    }
+  }
+  const uint64_t avail64 = p.arena_len - tb;
+  const uint32_t avail = avail64 > 0xffffffffull ? 0xffffffffu : (uint32_t)avail64;
+  Src s;
+  s.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p.arena + tb), (short)0, (int)avail, 0x00020000);
+  s.avail = avail;
+  if (!walk_wave) {
+    s_rbase[tid] = cnt ? local : 0xffffffffu;
+    s_doff[tid] = (uint32_t)(off - tb);
+    s_len[tid] = L;
+    if (cnt) {
+      s.base = (uint32_t)(off - tb);
+      const u32x4 h = ld16(s, 8u);
+      s_pfx[tid * 3 + 0] = h[0]; s_pfx[tid * 3 + 1] = h[1]; s_pfx[tid * 3 + 2] = h[2];
+    }
+  }
+  if (tid == 0) {
+    uint32_t a = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < WAVES; ++w) { const uint32_t v = tile_walk ? 0u : s_nit[w]; s_nit[w] = a; a += v; }
+    s_nit[WAVES] = a;
+  }
+  __syncthreads();
+  const uint32_t total = s_nit[WAVES];
+  const u32x4* tslab = items + (size_t)tile * WAVES * CAPW;
+  for (uint32_t k = tid; k < total; k += TILE) {
+    const uint32_t w = (k >= s_nit[1]) + (k >= s_nit[2]) + (k >= s_nit[3]);
+    const u32x4 it = tslab[w * CAPW + (k - s_nit[w])];
+    const uint32_t o = it[0] & 0xffffu, src_off = it[0] >> 16;
+    const uint32_t j = it[1] & 0xffffu, d = w * 64u + ((it[1] >> 16) & 63u), kind = it[1] >> 24;
+    const uint32_t rb = s_rbase[d];
+    if (rb == 0xffffffffu) continue;  // the datagram was dropped after this item (or has no records)
+    s.base = s_doff[d];
+    Win W;
+    {
+      const u32x4 a = ld16(s, o);
+      u32x4 b = {0u, 0u, 0u, 0u};
+      if (win_needs_tail<true>(kind)) b = ld16(s, o + 16u);
+      W.w[0] = a[0]; W.w[1] = a[1]; W.w[2] = a[2]; W.w[3] = a[3];
+      W.w[4] = b[0]; W.w[5] = b[1]; W.w[6] = b[2]; W.w[7] = b[3];
+      W.w[8] = kind == RTPS_DATA_FRAG ? ld4(s, o + 32u) : 0u;
+      W.w[9] = 0u; W.w[10] = 0u; W.w[11] = 0u;
+    }
+    Interp st;
+    if (src_off == 8u) {
+      st.src0 = s_pfx[d * 3 + 0]; st.src1 = s_pfx[d * 3 + 1]; st.src2 = s_pfx[d * 3 + 2];
+    } else {
+      const u32x4 q = ld16(s, src_off);
+      st.src0 = q[0]; st.src1 = q[1]; st.src2 = q[2];
+    }
+    st.dst_ok = ((it[1] >> 22) & 1u) != 0u;
+    st.ts_valid = ((it[1] >> 23) & 1u) != 0u;
+    st.ts_sec = it[2];
+    st.ts_frac = it[3];
+    const uint32_t flags = (W.w[0] >> 8) & 0xffu;
+    const bool le = (flags & 1u) != 0u;
+    const uint32_t eff = eff_len(kind, e16(W.w[0], 1, le), s_len[d] - o);
+    Rec R;
+    rec_clear(R);
+    SubOut so;
+    sub_body<true>(s, W, kind, flags, le, o + 4u, eff, R, so);  // validated by E's walk
+    R.d[0] = tile * TILE + d;
+    R.d[1] = o | (kind << 16) | (flags << 24);
+    const uint32_t tgt = rec_finish(p, R, so, kind, st);
+    const uint64_t r = prefix + rb + j;
+    if (r < p.max_records) {
+      rec_store(p.records + r, R);
+      if (p.target_out) p.target_out[r] = tgt;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // D  rtps_parse_lds_kernel: mixed traffic through LDS tiles.
 // A lane walking its datagram's submessage chain in global memory waits on one
 // dependent load per submessage, and the kind-divergent body readers serialise
@@ -1723,7 +2045,12 @@ struct rtps_rx_ctx {
   uint32_t ch_spin_limit = CH_SPIN_LIMIT;
   uint32_t ch_epoch = 0;          // last chained launch's epoch (words start zeroed: epoch 0 is never used)
   uint32_t chain_tiles = 0;       // tiles the chain words are sized for
-  uint32_t mixed_pass = 0;        // chained pass for mixed traffic: 0 = lane walk (C, default), 1 = LDS tiles (D)
+  uint32_t mixed_pass = 2;        // pass for mixed traffic: 2 = item pass (E/S/W, default), 0 = chained lane walk (C),
+                                  // 1 = chained LDS tiles (D)
+  u32x4* it_items = nullptr;      // item pass: wave slabs [tiles * WAVES * CAPW]
+  uint32_t* it_wcnt = nullptr;    // item pass: items per wave slab [tiles * WAVES]
+  uint64_t* it_prefix = nullptr;  // item pass: tile record prefixes [tiles]
+  uint32_t it_tiles = 0;          // tiles the item-pass buffers are sized for
   // per-reader DataFrag assembly (frag_x_*): Lifespans by reader slot, the batch's receive time, the expansion
   int64_t* life = nullptr;        // [65536] device, NO_LIFESPAN where none
   bool any_life = false;
@@ -1751,7 +2078,8 @@ int rtps_rx_create(const rtps_rx_config* cfg, rtps_rx_ctx** out_ctx) {
   if (hipSetDevice(c->device) != hipSuccess) { delete c; return RTPS_RX_EHIP; }
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) { delete c; return RTPS_RX_EHIP; }
   c->stream = c->own_stream;
-  if (const char* e = getenv("RTPS_RX_MIXED_PASS")) c->mixed_pass = (e[0] == '1') ? 1u : 0u;  // A/B measurements
+  if (const char* e = getenv("RTPS_RX_MIXED_PASS"))  // A/B measurements
+    c->mixed_pass = (e[0] == '1') ? 1u : (e[0] == '0') ? 0u : 2u;
   {
     int cus = 0, per_cu = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess && cus > 0 &&
@@ -1793,6 +2121,10 @@ int rtps_rx_destroy(rtps_rx_ctx* c) {
   (void)hipFree(c->bucket_hist);
   rtps_frag_state_free(c->frag);
   rtps_ingest_state_free(c->ingest);
+  {
+    void* it[] = {c->it_items, c->it_wcnt, c->it_prefix};
+    for (void* q : it) if (q) (void)hipFree(q);
+  }
   {
     void* fx[] = {c->life, c->fx_cnt, c->fx_off, c->fx_emap, c->fx_rec, c->fx_n, c->fx_tmp};
     for (void* q : fx) if (q) (void)hipFree(q);
@@ -1879,8 +2211,33 @@ static int parse_launch(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len
   const bool chain = c->k_spec == 0 || (seen >= 16u && 2u * mixed > seen);
   const uint32_t k = c->k_spec ? c->k_spec : 1u;
   const bool lds = chain && c->mixed_pass == 1u;
+  const bool item = chain && c->mixed_pass == 2u;
   if (lds) tiles = (n + LT - 1) / LT;  // kernel D: tiles of LT datagrams (B follows the same tiling)
-  if (first_kernel) *first_kernel = lds ? 3u : chain ? 2u : 1u;
+  if (first_kernel) *first_kernel = item ? 4u : lds ? 3u : chain ? 2u : 1u;
+  if (item) {  // E (phases 1), then S and W (phases 2); no kernel B
+    if (tiles > c->it_tiles) {
+      if (hipStreamSynchronize(c->stream) != hipSuccess) return RTPS_RX_EHIP;
+      void* q[] = {c->it_items, c->it_wcnt, c->it_prefix};
+      for (void* b : q) if (b) (void)hipFree(b);
+      c->it_items = nullptr; c->it_wcnt = nullptr; c->it_prefix = nullptr; c->it_tiles = 0;
+      const uint32_t t = (uint32_t)(((size_t)c->max_datagrams + TILE - 1) / TILE) > tiles
+                             ? (uint32_t)(((size_t)c->max_datagrams + TILE - 1) / TILE) : tiles;
+      if (hipMalloc(&c->it_items, (size_t)t * WAVES * CAPW * sizeof(u32x4)) != hipSuccess ||
+          hipMalloc(&c->it_wcnt, (size_t)t * WAVES * sizeof(uint32_t)) != hipSuccess ||
+          hipMalloc(&c->it_prefix, (size_t)t * sizeof(uint64_t)) != hipSuccess)
+        return RTPS_RX_ENOMEM;
+      c->it_tiles = t;
+    }
+    if (phases & 1u)
+      hipLaunchKernelGGL(rtps_parse_item_kernel, dim3(tiles), dim3(TILE), 0, c->stream, p, tiles, k, c->it_items,
+                         c->it_wcnt);
+    if (phases & 2u) {
+      hipLaunchKernelGGL(rtps_parse_scan_kernel, dim3(1), dim3(SCAN_T), 0, c->stream, p, tiles, parity, c->it_prefix);
+      hipLaunchKernelGGL(rtps_parse_emit_kernel, dim3(tiles), dim3(TILE), mt_lds, c->stream, p, tiles, c->it_items,
+                         c->it_wcnt, c->it_prefix);
+    }
+    return hip_fail(hipGetLastError());
+  }
   if (!(phases & 1u)) {
   } else if (chain) {  // one chained pass, B only finishes (n_records, stragglers)
     // the look-back words carry this launch's epoch, so they need no zeroing; only
@@ -1917,9 +2274,10 @@ int rtps_rx_parse_batch(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len
 }
 
 /* measurement hook (not part of the public header): launch only the parse's first
-   kernel (phases 1) or only B (phases 2), so bench.py can time the dominant kernel
-   alone with HIP events.  A full rtps_rx_parse_batch afterwards restores the
-   per-launch bookkeeping (run two).  *first_kernel: 1 = spec (A), 2 = chained (C). */
+   kernel (phases 1) or only the finishing kernels (phases 2: B, or the item pass's S and
+   W), so bench.py can time the kernels alone with HIP events.  A full
+   rtps_rx_parse_batch afterwards restores the per-launch bookkeeping (run two).
+   *first_kernel: 1 = spec (A), 2 = chained (C), 3 = chained LDS tiles (D), 4 = item pass (E). */
 int rtps_rx_debug_parse_phases(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len, const uint64_t* dgram_off,
                                const uint32_t* dgram_len, uint32_t n, const rtps_rx_out* out, uint32_t phases,
                                uint32_t* first_kernel) {
@@ -1945,6 +2303,7 @@ const char* rtps_rx_strerror(int code) {
     case RTPS_RX_ENOMEM: return "out of device memory";
     case RTPS_RX_ETOOBIG: return "batch larger than the context's max_datagrams";
     case RTPS_RX_EABI: return "ABI version mismatch";
+    case RTPS_RX_EABORTED: return "RCCL communicator aborted (freed): make a new one";
     default: return "unknown error";
   }
 }
@@ -2032,14 +2391,9 @@ int rtps_rx_bucket_descriptors(rtps_rx_ctx* c, const rtps_record* recs, const ui
 
 /* a18: batch CDR decode (rtps_cdr.hip).  The program is validated here so
  * the kernel can trust every op (sizes, slot bounds inside the row). */
-int rtps_rx_cdr_decode(rtps_rx_ctx* c, const rtps_cdr_op* prog, uint32_t n_ops, uint32_t row_bytes,
-                       const uint8_t* arena, uint64_t arena_len, const uint64_t* dgram_off,
-                       const rtps_record* records, const uint64_t* n_records, uint64_t max_records,
-                       uint8_t* rows, uint8_t* row_status) {
-  if (!c || !prog || n_ops > RTPS_CDR_MAX_OPS || row_bytes == 0 || (row_bytes & 3u) || row_bytes > (1u << 20))
+static int cdr_prog(const rtps_cdr_op* prog, uint32_t n_ops, uint32_t row_bytes, CdrProg& P) {
+  if (!prog || n_ops > RTPS_CDR_MAX_OPS || row_bytes == 0 || (row_bytes & 3u) || row_bytes > (1u << 20))
     return RTPS_RX_EINVAL;
-  if (!records || !n_records || (max_records && (!arena || !dgram_off || !rows || !row_status))) return RTPS_RX_EINVAL;
-  CdrProg P;
   memset(&P, 0, sizeof(P));
   for (uint32_t k = 0; k < n_ops; ++k) {
     const rtps_cdr_op& op = prog[k];
@@ -2059,10 +2413,39 @@ int rtps_rx_cdr_decode(rtps_rx_ctx* c, const rtps_cdr_op* prog, uint32_t n_ops, 
   }
   P.n_ops = n_ops;
   P.row_bytes = row_bytes;
-  if (!rtps_cdr_build_slots(P)) return RTPS_RX_EINVAL;
+  return rtps_cdr_build_slots(P) ? RTPS_RX_OK : RTPS_RX_EINVAL;
+}
+
+int rtps_rx_cdr_decode(rtps_rx_ctx* c, const rtps_cdr_op* prog, uint32_t n_ops, uint32_t row_bytes,
+                       const uint8_t* arena, uint64_t arena_len, const uint64_t* dgram_off,
+                       const rtps_record* records, const uint64_t* n_records, uint64_t max_records,
+                       uint8_t* rows, uint8_t* row_status) {
+  if (!c) return RTPS_RX_EINVAL;
+  CdrProg P;
+  const int rc = cdr_prog(prog, n_ops, row_bytes, P);
+  if (rc) return rc;
+  if (!records || !n_records || (max_records && (!arena || !dgram_off || !rows || !row_status))) return RTPS_RX_EINVAL;
   if (max_records == 0) return RTPS_RX_OK;
   (void)hipSetDevice(c->device);
-  CdrArgs a{arena, arena_len, dgram_off, records, n_records, max_records, rows, row_status};
+  CdrArgs a{arena, arena_len, dgram_off, records, n_records, max_records, rows, row_status, nullptr, 0, nullptr, 0};
+  return rtps_cdr_launch(c->stream, P, a, c->resident_blocks) == 0 ? RTPS_RX_OK : RTPS_RX_EHIP;
+}
+
+int rtps_rx_cdr_decode_list(rtps_rx_ctx* c, const rtps_cdr_op* prog, uint32_t n_ops, uint32_t row_bytes,
+                            const uint8_t* arena, uint64_t arena_len, const uint64_t* dgram_off,
+                            const rtps_record* records, const uint64_t* n_records, uint64_t max_records,
+                            const void* list, uint32_t list_stride, const uint64_t* n_list, uint64_t max_list,
+                            uint8_t* rows, uint8_t* row_status) {
+  if (!c) return RTPS_RX_EINVAL;
+  CdrProg P;
+  const int rc = cdr_prog(prog, n_ops, row_bytes, P);
+  if (rc) return rc;
+  if (!records || !n_records || !n_list || list_stride < 4 || (list_stride & 3u)) return RTPS_RX_EINVAL;
+  if (max_list && (!list || !arena || !dgram_off || !rows || !row_status)) return RTPS_RX_EINVAL;
+  if (max_list == 0) return RTPS_RX_OK;
+  (void)hipSetDevice(c->device);
+  CdrArgs a{arena, arena_len, dgram_off, records, n_records, max_records, rows, row_status,
+            static_cast<const uint8_t*>(list), list_stride, n_list, max_list};
   return rtps_cdr_launch(c->stream, P, a, c->resident_blocks) == 0 ? RTPS_RX_OK : RTPS_RX_EHIP;
 }
 
@@ -2293,11 +2676,12 @@ int rtps_rx_debug_lds_stamps(rtps_rx_ctx* c, uint64_t* host, uint64_t n) {
 #endif
 }
 
-/* test / measurement hook (not part of the public header): the chained pass used
-   for mixed traffic, 0 = the lane walk in global memory (rtps_parse_chain_kernel,
-   the default), 1 = LDS tiles (rtps_parse_lds_kernel). */
+/* test / measurement hook (not part of the public header): the pass used for mixed
+   traffic, 2 = the item pass (rtps_parse_item_kernel / scan / emit, the default),
+   0 = the chained lane walk in global memory (rtps_parse_chain_kernel), 1 = chained
+   LDS tiles (rtps_parse_lds_kernel).  Same results. */
 int rtps_rx_debug_set_mixed_pass(rtps_rx_ctx* c, uint32_t pass) {
-  if (!c || pass > 1u) return RTPS_RX_EINVAL;
+  if (!c || pass > 2u) return RTPS_RX_EINVAL;
   c->mixed_pass = pass;
   return RTPS_RX_OK;
 }

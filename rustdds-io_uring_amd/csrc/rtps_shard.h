@@ -40,6 +40,7 @@ struct rtps_shard {
   hipEvent_t counts_ev = nullptr;  // recorded after the counts' device-to-host copies (exchange stream)
   hipEvent_t done = nullptr;       // recorded after the last exchange round (exchange stream)
   bool exchanged = false;          // the counts were copied by rtps_rx_shard_exchange
+  bool finished = false;           // rtps_rx_shard_finish ran after that exchange (the spill, if any, moved)
   // ---- the owner batch ----
   rtps_record* o_rec = nullptr;
   uint64_t* o_off = nullptr;

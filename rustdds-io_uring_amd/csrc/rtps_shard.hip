@@ -477,6 +477,7 @@ int rtps_rx_shard_pack(rtps_shard* s, const uint8_t* arena, uint64_t arena_len, 
   }
   if (hipGetLastError() != hipSuccess) return RTPS_RX_EHIP;
   s->exchanged = false;
+  s->finished = false;
   return hip_rc(hipEventRecord(s->packed, st));
 }
 
@@ -537,6 +538,9 @@ int rtps_rx_shard_unpack(rtps_shard* s, rtps_owner_batch* out) {
   }
   fa.first[n] = total;
   if (sp > s->r_spill_cap || bsp > s->r_bspill_cap) return RTPS_RX_ETOOBIG;  // spill not received
+  // after RCCL round 0, a spill is in the spill buffers only once rtps_rx_shard_finish moved it
+  // (otherwise they may still hold an earlier batch's)
+  if (s->exchanged && !s->finished && (sp || bsp)) return RTPS_RX_EINVAL;
   if (total > s->o_cap) {
     uint64_t c[5] = {0, 0, 0, 0, 0};
     void** p[5] = {(void**)&s->o_rec, (void**)&s->o_off, (void**)&s->o_origin, (void**)&s->o_size,
@@ -591,6 +595,7 @@ int rtps_rx_shard_unpack(rtps_shard* s, rtps_owner_batch* out) {
   out->n_records_dev = s->o_n;
   out->n_records = total;
   s->exchanged = false;
+  s->finished = false;
   return RTPS_RX_OK;
 }
 

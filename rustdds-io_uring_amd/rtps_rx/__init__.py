@@ -25,6 +25,7 @@ LIB_PATH = os.environ.get("RTPS_RX_LIB") or os.path.join(os.path.dirname(_PKG_DI
 ABI_VERSION = 2
 
 WL_T, WL_C2, WL_C3, WL_C4 = 1, 2, 3, 4
+MIXED_CHAIN, MIXED_LDS, MIXED_ITEM = 0, 1, 2  # passes for mixed traffic (debug_set_mixed_pass)
 WORKLOADS = {"T": WL_T, "C2": WL_C2, "C3": WL_C3, "C4": WL_C4}
 SEED = 0x52545053
 
@@ -32,7 +33,12 @@ _lib = None
 
 
 class RtpsRxError(RuntimeError):
-    pass
+    def __init__(self, msg, code=None):
+        super().__init__(msg)
+        self.code = code
+
+
+RTPS_RX_EABORTED = -6  # the library aborted (and freed) an RCCL communicator
 
 
 class _Config(ctypes.Structure):
@@ -116,6 +122,8 @@ def lib():
         L.rtps_rx_set_spec_hint.restype = I
         L.rtps_rx_cdr_decode.argtypes = [P, P, U32, U32, P, U64, P, P, P, U64, P, P]
         L.rtps_rx_cdr_decode.restype = I
+        L.rtps_rx_cdr_decode_list.argtypes = [P, P, U32, U32, P, U64, P, P, P, U64, P, U32, P, U64, P, P]
+        L.rtps_rx_cdr_decode_list.restype = I
         for fn in ("rtps_rx_create", "rtps_rx_destroy", "rtps_rx_set_stream", "rtps_rx_set_match_table",
                    "rtps_rx_parse_batch", "rtps_rx_sync", "rtps_rx_generate"):
             getattr(L, fn).restype = I
@@ -126,7 +134,7 @@ def lib():
 
 def _check(rc):
     if rc != 0:
-        raise RtpsRxError(lib().rtps_rx_strerror(rc).decode())
+        raise RtpsRxError(lib().rtps_rx_strerror(rc).decode(), rc)
 
 
 def gen_layout(workload, n, seed=SEED, first_idx=0, n_writers=16):
@@ -286,8 +294,8 @@ class MessageReceiver:
 
     def debug_parse_phases(self, arena, off, lens, n, outs, phases):
         """Measurement hook: launch only the parse's first kernel (phases=1) or only the
-        finishing kernel (phases=2); returns 1 (spec kernel A), 2 (chained lane walk C) or
-        3 (LDS tiles D).
+        finishing kernels (phases=2); returns 1 (spec kernel A), 2 (chained lane walk C),
+        3 (LDS tiles D) or 4 (the item pass: E, then S + W).
         Run two full parse_batch_device calls afterwards."""
         self.parse_batch_device(arena, off, lens, n, outs) if "_c_out" not in outs else None
         o = outs["_c_out"][(True, True)]
@@ -314,11 +322,15 @@ class MessageReceiver:
         fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
         _check(fn(self._h, mode))
 
-    def debug_set_mixed_pass(self, lds):
-        """The chained pass for mixed traffic: the lane walk (False, the default) or LDS tiles."""
+    def debug_set_mixed_pass(self, pass_):
+        """The pass for mixed traffic (same results): MIXED_ITEM (2, the default: item walk,
+        tile scan, record pass), MIXED_CHAIN (0: chained lane walk) or MIXED_LDS (1: chained
+        LDS tiles).  True / False select LDS tiles / the chained lane walk."""
+        if pass_ is True or pass_ is False:
+            pass_ = MIXED_LDS if pass_ else MIXED_CHAIN
         fn = lib().rtps_rx_debug_set_mixed_pass
         fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
-        _check(fn(self._h, 1 if lds else 0))
+        _check(fn(self._h, int(pass_)))
 
     def generate(self, workload, arena, off, lens, n, seed=SEED, first_idx=0, n_writers=16):
         """Fill device arena with datagrams [first_idx, first_idx+n) of a synthetic workload."""
@@ -347,6 +359,17 @@ class MessageReceiver:
                                         arena.data_ptr(), arena.numel(), off.data_ptr(), outs["records"].data_ptr(),
                                         outs["n_records"].data_ptr(), outs["max_records"], rows.data_ptr(),
                                         row_status.data_ptr()))
+
+    def cdr_decode_list(self, sample_type, arena, off, outs, lst, stride, n_list, max_list, rows, row_status):
+        """Compact decode: row k decodes the record named by the u32 at byte k * stride of the
+        device tensor `lst` (e.g. the ingest deliveries: iouts["accepted"], stride 8, n_list =
+        iouts["n_accepted"]), for k < min(n_list, max_list); row_status[k] a cdr.CDR_* code."""
+        ops = sample_type.ops
+        _check(lib().rtps_rx_cdr_decode_list(self._h, ops.ctypes.data, len(ops), sample_type.row_bytes,
+                                             arena.data_ptr(), arena.numel(), off.data_ptr(),
+                                             outs["records"].data_ptr(), outs["n_records"].data_ptr(),
+                                             outs["max_records"], lst.data_ptr(), stride, n_list.data_ptr(),
+                                             max_list, rows.data_ptr(), row_status.data_ptr()))
 
     def bucket_by_writer_padded(self, outs, n_dest, cap, out_records, dest_counts):
         """Same partition into n_dest fixed buckets of cap records (out_records[d*cap:(d+1)*cap]);

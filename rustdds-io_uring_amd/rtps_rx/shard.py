@@ -41,6 +41,22 @@ RECORD_BYTES = 64
 _COMMS = {}
 
 
+def _forget_comm(comm):
+    """The library aborted this communicator (RTPS_RX_EABORTED), which frees it: drop it from
+    the cache so it is neither handed out again nor destroyed a second time."""
+    for k, c in list(_COMMS.items()):
+        if c is comm:
+            del _COMMS[k]
+
+
+def _check_comm(rc, comm):
+    """_check for the calls that may abort the communicator."""
+    from . import _check, RTPS_RX_EABORTED
+    if rc == RTPS_RX_EABORTED:
+        _forget_comm(comm)
+    _check(rc)
+
+
 def destroy_comms():
     """Destroy the library RCCL communicators of this process (call before the process group goes)."""
     from . import lib
@@ -172,9 +188,10 @@ class Exchange:
         L = lib()
         L.rtps_rx_exchange.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p,
                                                                ctypes.c_void_p]
-        _check(L.rtps_rx_exchange(self.rx._h, self.comm, ctypes.c_void_p(self.xstream.cuda_stream),
-                                  self.bucketed.data_ptr(), self.counts.data_ptr(), self.cap,
-                                  ITEM_BYTES[self.item], self.received.data_ptr(), self.recv_counts.data_ptr()))
+        _check_comm(L.rtps_rx_exchange(self.rx._h, self.comm, ctypes.c_void_p(self.xstream.cuda_stream),
+                                       self.bucketed.data_ptr(), self.counts.data_ptr(), self.cap,
+                                       ITEM_BYTES[self.item], self.received.data_ptr(), self.recv_counts.data_ptr()),
+                    self.comm)
         done = torch.cuda.Event()
         done.record(self.xstream)
         return [_StreamWork(done, self.device)]
@@ -380,15 +397,15 @@ class OwnerShard:
         """Round 0 (RCCL: asynchronous on the exchange stream; gloo: the whole protocol)."""
         if self.host_collectives:
             return self._exchange_host()
-        from . import _check
-        _check(shard_lib().rtps_rx_shard_exchange(self._h, self.comm, ctypes.c_void_p(self.xstream.cuda_stream)))
+        _check_comm(shard_lib().rtps_rx_shard_exchange(self._h, self.comm, ctypes.c_void_p(self.xstream.cuda_stream)),
+                    self.comm)
 
     def finish(self):
         """Waits for round 0's counts; moves any spill (RCCL).  No-op after a gloo exchange."""
         if self.host_collectives:
             return
-        from . import _check
-        _check(shard_lib().rtps_rx_shard_finish(self._h, self.comm, ctypes.c_void_p(self.xstream.cuda_stream)))
+        _check_comm(shard_lib().rtps_rx_shard_finish(self._h, self.comm, ctypes.c_void_p(self.xstream.cuda_stream)),
+                    self.comm)
 
     def unpack(self):
         """Owner side -> OwnerBatch (host sync on the received counts)."""

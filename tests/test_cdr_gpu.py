@@ -117,3 +117,42 @@ def test_c2_full_size(rx):
     for i in k[:64]:
         base = int(off[i]) + 44 + 4
         assert np.array_equal(raw[i], arena[base:base + cdr.C2Sample.row_bytes])
+
+
+@pytest.mark.parametrize("wl,t", [(3, "ShapeType"), (1, "TSample"), (3, "MIXED")])
+def test_list_decode_parity(rx, wl, t):
+    """Compact rows (rtps_rx_cdr_decode_list): row k decodes the record of list entry k.  The
+    list is every DATA sample's record index (the rows the per-record layout fills), then the
+    same list with a stride of 8 (the rtps_delivery layout) and with entries that name
+    non-sample records and out-of-range indices (RTPS_CDR_NOT_DATA, zero rows)."""
+    typ = cdr_ref.MIXED if t == "MIXED" else getattr(cdr, t)
+    arena, off, ln = _device_gen(rx, wl, 20000)
+    st, recs, _, _ = oracle.parse(arena, off, ln, threads=8)
+    o_rows, o_status = oracle.cdr_decode(typ, arena, off, recs)
+    dev = torch.device("cuda", 0)
+    a_t = torch.from_numpy(arena).to(dev)
+    off_t = torch.from_numpy(off.view(np.int64)).to(dev)
+    ln_t = torch.from_numpy(ln.view(np.int32)).to(dev)
+    outs = rx.alloc_outputs(len(ln), max(len(recs), 1))
+    rx.parse_batch_device(a_t, off_t, ln_t, len(ln), outs)
+    samples = np.nonzero(o_status != cdr.CDR_NOT_DATA)[0].astype(np.uint32)
+    others = np.nonzero(o_status == cdr.CDR_NOT_DATA)[0][:50].astype(np.uint32)
+    mixed = np.concatenate([samples[:300], others, np.array([len(recs), 0xFFFFFFFF], np.uint32), samples[300:]])
+    for lst, stride in ((samples, 4), (mixed, 8)):
+        wide = np.zeros((len(lst), stride // 4), np.uint32)
+        wide[:, 0] = lst
+        wide[:, 1:] = 0xABCDEF01  # the rest of a delivery entry is not read
+        l_t = torch.from_numpy(wide.reshape(-1).view(np.int32)).to(dev)
+        n_t = torch.tensor([len(lst)], dtype=torch.int64, device=dev)
+        rows, rst = rx.alloc_rows(typ, len(lst))
+        rx.cdr_decode_list(typ, a_t, off_t, outs, l_t, stride, n_t, len(lst), rows, rst)
+        torch.cuda.synchronize()
+        rows = rows.cpu().numpy()[:len(lst)]
+        rst = rst.cpu().numpy()[:len(lst)]
+        ok = lst < len(recs)
+        exp_st = np.full(len(lst), cdr.CDR_NOT_DATA, np.uint8)
+        exp_st[ok] = o_status[lst[ok]]
+        assert np.array_equal(rst, exp_st), f"list stride {stride}: row status differs"
+        exp_rows = np.zeros((len(lst), typ.row_bytes), np.uint8)
+        exp_rows[ok] = o_rows[lst[ok]]
+        assert np.array_equal(rows, exp_rows), f"list stride {stride}: rows differ"

@@ -219,30 +219,7 @@ def test_fuzz_byte_flips(rx):
 
 def test_random_submessage_soup(rx):
     """Random kinds/lengths/flags: exercises every error path of every reader."""
-    rng = np.random.default_rng(11)
-    kinds = [0x01, 0x06, 0x07, 0x08, 0x09, 0x0c, 0x0d, 0x0e, 0x0f, 0x12, 0x13, 0x15, 0x16, 0x30, 0x80, 0x02]
-    dgrams = []
-    for i in range(20000):
-        d = bytearray(b"RTPS\x02\x04\x01\x12") + bytearray(rng.integers(0, 256, 12, dtype=np.uint8))
-        for _ in range(int(rng.integers(1, 6))):
-            kind = int(rng.choice(kinds))
-            le = int(rng.integers(0, 2))
-            flags = int(rng.integers(0, 256)) & ~1 | le
-            blen = int(rng.choice([0, 4, 8, 12, 16, 20, 24, 28, 32, 36, 40, 44, 48, 60, 64, int(rng.integers(0, 90))]))
-            body = bytearray(rng.integers(0, 256, blen, dtype=np.uint8))
-            if blen >= 4 and rng.random() < 0.7:  # plausible otq / numBits
-                struct.pack_into("<H" if le else ">H", body, 2, int(rng.choice([16, 28, 17, 30, 8, 0])))
-            if kind in (0x06, 0x08, 0x12) and blen >= 28 and rng.random() < 0.7:
-                struct.pack_into("<I" if le else ">I", body, {0x06: 16, 0x08: 24, 0x12: 20}[kind],
-                                 int(rng.choice([0, 1, 31, 32, 33, 64, 256, 257])))
-            if kind in (0x15, 0x16) and blen >= 36 and rng.random() < 0.5:  # inline QoS params
-                flags |= 2
-            declared = blen if rng.random() < 0.9 else int(rng.integers(0, 120))
-            d += bytes([kind, flags]) + struct.pack("<H" if le else ">H", declared) + body
-        if rng.random() < 0.05:
-            d += bytes(rng.integers(0, 256, int(rng.integers(1, 4)), dtype=np.uint8))
-        dgrams.append(bytes(d))
-    arena, off, ln = oracle.pack(dgrams)
+    arena, off, ln = _soup(20000)
     _parity(rx, arena, off, ln, "soup")
 
 
@@ -300,47 +277,56 @@ def test_full_size_parity(rx, wl, name):
         assert (u[:, 1] == (980 if wl == 1 else 256)).all()
 
 
+MIXED_PASSES = [(2, "item"), (0, "chain"), (1, "lds")]
+
+
+@pytest.mark.parametrize("mp", [2, 0])
 @pytest.mark.parametrize("wl,name", [(3, "C3"), (1, "T")])
-def test_chained_launch_full_size(rx, wl, name):
-    """Spec hint 0 (mixed traffic): the chained look-back launch, bit-exact at 1M datagrams
-    (C3: 1M + 64K, 4352 tiles of 256, so that the look-back spans two supergroups of 64 x 64
-    tiles)."""
+def test_chained_launch_full_size(rx, wl, name, mp):
+    """Spec hint 0 (mixed traffic): the item pass (E/S/W) and the chained look-back launch,
+    bit-exact at 1M datagrams (C3: 1M + 64K, 4352 tiles of 256, so that the chained
+    look-back spans two supergroups of 64 x 64 tiles)."""
     n = (1 << 20) + (1 << 16 if wl == 3 else 0)
     arena, off, ln = _device_gen(rx, wl, n)
     rx.set_spec_hint(0)
+    rx.debug_set_mixed_pass(mp)
     try:
-        _parity(rx, arena, off, ln, f"{name}-1M-chained")
+        _parity(rx, arena, off, ln, f"{name}-1M-{'item' if mp == 2 else 'chained'}")
     finally:
+        rx.debug_set_mixed_pass(2)
         rx.set_spec_hint(1)
 
 
-@pytest.mark.parametrize("lds", [True, False])
+@pytest.mark.parametrize("mp,mname", MIXED_PASSES)
 @pytest.mark.parametrize("wl", [3, 1])
-def test_mixed_passes_agree(rx, wl, lds):
-    """The two chained passes for mixed traffic, LDS tiles (D) and the lane walk (C),
-    bit-exact with the oracle on the same batch (C3, and one-DATA traffic forced
-    through the chained pass), misaligned packing included."""
+def test_mixed_passes_agree(rx, wl, mp, mname):
+    """The three passes for mixed traffic, the item pass (E/S/W), LDS tiles (D) and the
+    chained lane walk (C), bit-exact with the oracle on the same batch (C3, and one-DATA
+    traffic forced through the mixed pass), misaligned packing included."""
     a, o, l = oracle.gen(wl, 60000, first_idx=777)
     dg = [a[int(x):int(x) + int(y)].tobytes() for x, y in zip(o[:3000], l[:3000])]
     rx.set_spec_hint(0)
-    rx.debug_set_mixed_pass(lds)
+    rx.debug_set_mixed_pass(mp)
     try:
-        _parity(rx, a, o, l, f"wl {wl} {'LDS' if lds else 'lane walk'}")
+        _parity(rx, a, o, l, f"wl {wl} {mname}")
         for align in (1, 2, 3):
             A, O, L = oracle.pack(dg, align=align)
             O = O + align  # offsets = align mod 16, unaligned for the 16-B staging loads
             A2 = np.zeros(len(A) + 16, np.uint8)
             A2[align:align + len(A)] = A
-            _parity(rx, A2, O, L, f"wl {wl} align {align}")
+            _parity(rx, A2, O, L, f"wl {wl} {mname} align {align}")
     finally:
-        rx.debug_set_mixed_pass(False)
+        rx.debug_set_mixed_pass(2)
         rx.set_spec_hint(1)
 
 
-def test_lds_tile_fallbacks(rx):
+@pytest.mark.parametrize("mp", [1, 2])
+def test_lds_tile_fallbacks(rx, mp):
     """Tiles the LDS pass cannot stage (bytes beyond the image: 64 KiB datagrams; more
     materialised submessages than item slots: INFO_TS-only datagrams) take the lane
-    walk inside the same kernel; neighbouring tiles stay on the LDS path."""
+    walk inside the same kernel; neighbouring tiles stay on the LDS path.  The same batch
+    through the item pass: the wave holding the 1000-record datagram overflows its item
+    slab (512) and the record pass walks that wave's datagrams instead."""
     a, o, l = oracle.gen(oracle.WL_C3, 500)
     c3 = [a[int(x):int(x) + int(y)].tobytes() for x, y in zip(o, l)]
     hdr = b"RTPS\x02\x04\x01\x0f" + bytes(range(12))
@@ -351,13 +337,13 @@ def test_lds_tile_fallbacks(rx):
     dg = c3[:100] + [many] + c3[100:230] + [big_data, big_data[:64000]] * 2 + c3[230:]
     A, O, L = oracle.pack(dg, align=4)
     rx.set_spec_hint(0)
-    rx.debug_set_mixed_pass(True)
+    rx.debug_set_mixed_pass(mp)
     try:
-        gpu = _parity(rx, A, O, L, "LDS fallbacks")
+        gpu = _parity(rx, A, O, L, "LDS fallbacks" if mp == 1 else "item-slab overflow")
         assert int(gpu.status[100]) == DGRAM_OK and len(gpu.submessages(100)) == 1000
         assert int(gpu.status[231]) == DGRAM_OK and int(gpu.status[232]) != DGRAM_OK
     finally:
-        rx.debug_set_mixed_pass(False)
+        rx.debug_set_mixed_pass(2)
         rx.set_spec_hint(1)
 
 
@@ -389,14 +375,15 @@ def test_chained_fallback_to_fix_pass(rx, limit, lds):
         assert left > 0, "no tile was left to kernel B: the fallback was not exercised"
     finally:
         L.rtps_rx_debug_set_chain_spin_limit(rx._h, 1 << 10)
-        rx.debug_set_mixed_pass(False)
+        rx.debug_set_mixed_pass(2)
         rx.set_spec_hint(1)
 
 
 def test_chained_words_across_sizes_and_epoch_wrap(rx):
     """The chained pass's look-back words are never zeroed: they carry the launch's
     epoch.  Chained batches of different sizes, run across the 32-bit epoch wrap
-    (which zeroes everything once), stay bit-exact."""
+    (which zeroes everything once), stay bit-exact; item-pass batches in between
+    leave the words alone."""
     import ctypes
     import rtps_rx
     L = rtps_rx.lib()
@@ -407,8 +394,62 @@ def test_chained_words_across_sizes_and_epoch_wrap(rx):
     try:
         assert L.rtps_rx_debug_set_chain_epoch(rx._h, 0xfffffffd) == 0
         for k, (a, o, l) in enumerate([big, small, big, small, big, big]):
+            rx.debug_set_mixed_pass(2 if k == 3 else 0)
             _parity(rx, a, o, l, f"C3 chained #{k} ({len(l)} datagrams) across the epoch wrap")
     finally:
+        rx.debug_set_mixed_pass(2)
+        rx.set_spec_hint(1)
+
+
+def _soup(n, seed=11):
+    rng = np.random.default_rng(seed)
+    kinds = [0x01, 0x06, 0x07, 0x08, 0x09, 0x0c, 0x0d, 0x0e, 0x0f, 0x12, 0x13, 0x15, 0x16, 0x30, 0x80, 0x02]
+    dgrams = []
+    for i in range(n):
+        d = bytearray(b"RTPS\x02\x04\x01\x12") + bytearray(rng.integers(0, 256, 12, dtype=np.uint8))
+        for _ in range(int(rng.integers(1, 6))):
+            kind = int(rng.choice(kinds))
+            le = int(rng.integers(0, 2))
+            flags = int(rng.integers(0, 256)) & ~1 | le
+            blen = int(rng.choice([0, 4, 8, 12, 16, 20, 24, 28, 32, 36, 40, 44, 48, 60, 64, int(rng.integers(0, 90))]))
+            body = bytearray(rng.integers(0, 256, blen, dtype=np.uint8))
+            if blen >= 4 and rng.random() < 0.7:  # plausible otq / numBits
+                struct.pack_into("<H" if le else ">H", body, 2, int(rng.choice([16, 28, 17, 30, 8, 0])))
+            if kind in (0x06, 0x08, 0x12) and blen >= 28 and rng.random() < 0.7:
+                struct.pack_into("<I" if le else ">I", body, {0x06: 16, 0x08: 24, 0x12: 20}[kind],
+                                 int(rng.choice([0, 1, 31, 32, 33, 64, 256, 257])))
+            if kind in (0x15, 0x16) and blen >= 36 and rng.random() < 0.5:  # inline QoS params
+                flags |= 2
+            declared = blen if rng.random() < 0.9 else int(rng.integers(0, 120))
+            d += bytes([kind, flags]) + struct.pack("<H" if le else ">H", declared) + body
+        if rng.random() < 0.05:
+            d += bytes(rng.integers(0, 256, int(rng.integers(1, 4)), dtype=np.uint8))
+        dgrams.append(bytes(d))
+    return oracle.pack(dgrams)
+
+
+@pytest.mark.parametrize("mp,mname", MIXED_PASSES)
+def test_mixed_pass_malformed_inputs(rx, mp, mname):
+    """Every pass for mixed traffic on the inputs that hit the error paths: the random
+    submessage soup (a datagram dropped after some of its submessages already produced
+    items), header byte flips, INFO_SRC / INFO_DST / INFO_TS interleavings of the a15
+    reader-set stream, all bit-exact against the oracle."""
+    import ingest_ref as R
+    rx.set_spec_hint(0)
+    rx.debug_set_mixed_pass(mp)
+    try:
+        arena, off, ln = _soup(12000, seed=23)
+        _parity(rx, arena, off, ln, f"soup {mname}")
+        rng = np.random.default_rng(5)
+        a, o, l = oracle.gen(oracle.WL_C3, 12000)
+        a = a.copy()
+        for x, y in zip(o[::2], l[::2]):
+            a[int(x) + int(rng.integers(0, min(int(y), 96)))] = rng.integers(0, 256)
+        _parity(rx, a, o, l, f"fuzz-headers {mname}")
+        A, O, L = oracle.pack(R.a15_stream(4000, 5), align=1)
+        _parity(rx, A, O, L, f"a15 stream {mname}", table=R.a15_readers())
+    finally:
+        rx.debug_set_mixed_pass(2)
         rx.set_spec_hint(1)
 
 

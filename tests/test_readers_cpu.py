@@ -115,7 +115,9 @@ L = rtps_rx.lib()
 P, U32 = ctypes.c_void_p, ctypes.c_uint32
 class View(ctypes.Structure):
     _fields_ = [(n, P) for n in ("gkeys", "gset", "ekeys", "eset", "set_first", "set_ent")] + \
-               [(n, U32) for n in ("gmask", "emask", "n_writer_sets", "n_sets", "n_proxies", "max_set")]
+               [(n, U32) for n in ("gmask", "emask", "n_writer_sets", "n_sets", "n_proxies", "max_set", "n_ent")]
+L.rtps_rx_debug_rt_view_size.restype = U32
+assert ctypes.sizeof(View) == L.rtps_rx_debug_rt_view_size(), "View must mirror ReaderDev exactly"
 L.rtps_rx_debug_rt_new.restype = P
 L.rtps_rx_debug_rt_free.argtypes = [P]
 L.rtps_rx_debug_rt_set.argtypes = [P, P, U32, P, U32]
