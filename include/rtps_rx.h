@@ -609,8 +609,8 @@ int rtps_rx_frag_set_receive_time(rtps_rx_ctx* ctx, uint64_t unix_ns);
  *   Reader::handle_gap_msg: gapStart > 0 and gapList.base > 0, then
  *     irrelevant_changes_range(gapStart, gapList.base) and set_irrelevant_change
  *     for every listed SN                                 reader.rs:1060-1116, rtps_writer_proxy.rs:226-239
- *   TopicCache::add_change duplicate check, mark_reliably_received_before
- *                                                         structure/dds_cache.rs:200-262
+ *   TopicCache::add_change (flags & RTPS_INGEST_TOPIC_CACHE: see below)
+ *                                                         structure/dds_cache.rs:210-284
  * Events are the records of a parse_batch output with RTPS_ROUTE_PASS, in
  * record order, delivered to every reader of their target set in set order
  * (dp_event_loop.rs:272-326): DATA with payload_kind DATA / KEY / KEY_HASH and
@@ -628,7 +628,13 @@ int rtps_rx_frag_set_receive_time(rtps_rx_ctx* ctx, uint64_t unix_ns);
  *     the record's target set); at most 64 readers per target set take such samples;
  *   - HEARTBEAT / GAP without a proxy, HEARTBEAT for a BestEffort reader: no
  *     effect (reader.rs:871-891, 1071-1086).
- * Every accepted (record, reader) pair is one delivery.  State per proxy
+ * Every accepted (record, reader) pair is one delivery: process_received_data
+ * returned true (reader.rs:693-758), so Domain::handle_event calls on_read for a
+ * DATA (dp_event_loop.rs:284-299) and the reader hands the change to its topic's
+ * TopicCache::add_change (make_cache_change, reader.rs:1185-1205).  Whether that
+ * add_change STORES it is the topic cache's own duplicate check, which this call
+ * decides too when flags has RTPS_INGEST_TOPIC_CACHE: the delivery's
+ * RTPS_DELIVERY_CACHED flag (see "topic caches" below).  State per proxy
  * (all_ackable_before, the change set above it, received_heartbeat_count)
  * persists in the context across batches; it is indexed by proxy position, so
  * keep proxies in place (append new ones) or call rtps_rx_ingest_reset after
@@ -638,11 +644,15 @@ int rtps_rx_frag_set_receive_time(rtps_rx_ctx* ctx, uint64_t unix_ns);
  * check and counted in *n_window_overflow (the reference's BTreeMap has no bound). */
 #define RTPS_INGEST_WINDOW (1u << 17)
 #define RTPS_INGEST_BEST_EFFORT 0x1u /* flags: treat every reader as BestEffort (HEARTBEATs ignored) */
-typedef struct rtps_delivery {  /* one sample accepted into one reader's history cache */
+#define RTPS_INGEST_TOPIC_CACHE 0x2u /* flags: also run the topic caches' add_change (RTPS_DELIVERY_CACHED) */
+typedef struct rtps_delivery {  /* one sample a reader accepted (process_received_data == true) */
   uint32_t rec_idx;             /* the record (completing record of a DataFrag sample) */
   uint16_t reader_slot;
-  uint16_t _r;
+  uint16_t flags;               /* RTPS_DELIVERY_*; 0 without RTPS_INGEST_TOPIC_CACHE */
 } rtps_delivery;
+/* TopicCache::add_change stored the change: its (writer GUID, SN) was not in the topic's
+ * cache (find_by_sn missed, structure/dds_cache.rs:241-276) */
+#define RTPS_DELIVERY_CACHED 0x1u
 typedef struct rtps_ingest_out {
   uint8_t* accept;              /* [max_records] device: readers whose cache the record's sample enters
                                    (saturating at 255); 0 = none */
@@ -660,8 +670,41 @@ int rtps_rx_ingest(rtps_rx_ctx* ctx, const uint8_t* arena, uint64_t arena_len, c
                    const rtps_record* records, const uint64_t* n_records, uint64_t max_records,
                    const rtps_frag_sample* frag, const uint64_t* n_frag, uint64_t max_frag, uint32_t flags,
                    const rtps_ingest_out* out);
-/* Forget every writer proxy's state (all_ackable_before = 1, empty change set, count 0). */
+/* Forget every writer proxy's state (all_ackable_before = 1, empty change set, count 0)
+ * and empty every topic cache. */
 int rtps_rx_ingest_reset(rtps_rx_ctx* ctx);
+
+/* ---- topic caches (TopicCache::add_change, structure/dds_cache.rs:113-420) ----
+ * A reader hands every change it accepts to its topic's TopicCache (one per topic
+ * name, shared by every reader of the topic: DDSCache, io_uring/dds/cache.rs:10-41),
+ * whose add_change
+ *   1. garbage-collects first when the change's SN is a multiple of 64
+ *      (add_change_internal :230-238 -> remove_changes_before(ZERO) :367-420):
+ *      the oldest changes (receive-instant order = insertion order) are removed
+ *      until at most max_keep_samples remain;
+ *   2. drops the change if the topic already holds (writer GUID, SN) (find_by_sn
+ *      :241-252, 270-276), else stores it.
+ * max_keep_samples = max(ResourceLimits.max_samples (default 64), KeepLast depth)
+ * over the topic's QoS, and at least 1 (update_keep_limits :165-197).  A reader slot
+ * without a topic here has a topic cache of its own with max_keep_samples 64 (the
+ * reference's defaults).  The periodic DDSCache::garbage_collect (the CacheCleaning
+ * timer, io_uring/rtps/dp_event_loop.rs:385-389, io_uring/dds/cache.rs:43-51) is
+ * rtps_rx_topic_gc.  Set the topics before the readers receive traffic: setting them
+ * empties every topic cache. */
+typedef struct rtps_topic {
+  uint32_t topic;             /* caller-defined topic id */
+  uint32_t max_keep_samples;  /* >= 1 */
+} rtps_topic;
+typedef struct rtps_topic_reader {
+  uint16_t reader_slot;       /* a reader (rtps_reader.reader_slot) ... */
+  uint16_t _r;
+  uint32_t topic;             /* ... of this topic (one of topics[].topic) */
+} rtps_topic_reader;
+int rtps_rx_set_topics(rtps_rx_ctx* ctx, const rtps_topic* topics, uint32_t n_topics,
+                       const rtps_topic_reader* readers, uint32_t n_readers);
+/* DDSCache::garbage_collect: every topic cache trimmed to its max_keep_samples
+ * newest changes (asynchronous). */
+int rtps_rx_topic_gc(rtps_rx_ctx* ctx);
 
 /* ---- UDP batch receive into a datagram arena -----
  * Replaces the receive side of the reference: a UDPListener per locator with

@@ -70,6 +70,13 @@ def lib():
         L.rtps_oracle_ingest_batch.restype = ctypes.c_uint64
         L.rtps_oracle_ingest_batch.argtypes = [P, P, P, P, ctypes.c_uint64, P, ctypes.c_uint64, ctypes.c_uint32,
                                                P, P, ctypes.c_uint64, P]
+        L.rtps_oracle_topics_new.restype = P
+        L.rtps_oracle_topics_new.argtypes = [P, ctypes.c_uint32, P, ctypes.c_uint32]
+        L.rtps_oracle_topics_free.argtypes = [P]
+        L.rtps_oracle_topics_gc.restype = None
+        L.rtps_oracle_topics_gc.argtypes = [P]
+        L.rtps_oracle_topics_apply.restype = ctypes.c_uint64
+        L.rtps_oracle_topics_apply.argtypes = [P, P, ctypes.c_uint64, P, ctypes.c_uint64]
         L.rtps_oracle_cdr_decode.restype = None
         L.rtps_oracle_cdr_decode.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32, P, P, P, ctypes.c_uint64, P, P]
         assert L.rtps_oracle_record_size() == RECORD_DTYPE.itemsize
@@ -281,3 +288,41 @@ class HistoryIngest:
                                            0 if fs is None else len(fs), 1 if best_effort else 0,
                                            _ptr(accept), _ptr(dels), cap, _ptr(ack))
         return accept[:m], dels[:int(k)], ack[:self.n]
+
+
+def topic_args(topics, topic_readers):
+    """(topics [(topic id, max_keep_samples)], readers [(reader slot, topic id)]) -> the two arrays."""
+    from rtps_rx.records import TOPIC_DTYPE, TOPIC_READER_DTYPE
+    t = np.zeros(len(topics), dtype=TOPIC_DTYPE)
+    for i, (tid, k) in enumerate(topics):
+        t[i] = (tid, k)
+    r = np.zeros(len(topic_readers), dtype=TOPIC_READER_DTYPE)
+    for i, (slot, tid) in enumerate(topic_readers):
+        r[i]["reader_slot"], r[i]["topic"] = slot, tid
+    return t, r
+
+
+class TopicCaches:
+    """Sequential TopicCache::add_change restatement (rtps_oracle_topics_*): one cache per topic,
+    state across batches; apply() over a batch's deliveries (in order) sets DELIVERY_CACHED."""
+
+    def __init__(self, topics=(), topic_readers=()):
+        self.t, self.r = topic_args(topics, topic_readers)
+        self.h = ctypes.c_void_p(lib().rtps_oracle_topics_new(_ptr(self.t) if len(self.t) else None, len(self.t),
+                                                              _ptr(self.r) if len(self.r) else None, len(self.r)))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().rtps_oracle_topics_free(self.h)
+            self.h = None
+
+    def gc(self):
+        lib().rtps_oracle_topics_gc(self.h)
+
+    def apply(self, recs, deliveries):
+        """-> a copy of deliveries with flags set (DELIVERY_CACHED where the change was stored)."""
+        recs = np.ascontiguousarray(recs, dtype=RECORD_DTYPE)
+        d = np.ascontiguousarray(deliveries, dtype=DELIVERY_DTYPE).copy()
+        if len(d):
+            lib().rtps_oracle_topics_apply(self.h, _ptr(recs) if len(recs) else None, len(recs), _ptr(d), len(d))
+        return d

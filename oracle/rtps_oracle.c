@@ -32,6 +32,7 @@
  *   rtps_oracle_cdr_decode          <- cdr_adapters.rs:246-275 + cdr-encoding 0.10 rules
  *   rtps_oracle_frag_batch          <- rtps/fragment_assembler.rs:23-214, reader.rs:563-647
  *   rtps_oracle_ingest_batch        <- rtps/rtps_writer_proxy.rs:202-355, reader.rs:514-1116
+ *   rtps_oracle_topics_apply        <- TopicCache::add_change, structure/dds_cache.rs:210-284, 367-420
  */
 #include <pthread.h>
 #include <stdint.h>
@@ -1343,7 +1344,7 @@ uint64_t rtps_oracle_ingest_batch(rtps_oracle_ingest* h, const uint8_t* arena, c
         }
       }
       if (acc) {
-        if (nd < max_del) { del[nd].rec_idx = (uint32_t)i; del[nd].reader_slot = t->reader_slot; del[nd]._r = 0; }
+        if (nd < max_del) { del[nd].rec_idx = (uint32_t)i; del[nd].reader_slot = t->reader_slot; del[nd].flags = 0; }
         nd++;
         took++;
       }
@@ -1354,4 +1355,105 @@ uint64_t rtps_oracle_ingest_batch(rtps_oracle_ingest* h, const uint8_t* arena, c
     for (uint32_t e = 0; e < h->R.np; ++e) ack_base[e] = h->p[e].ack_base;
   free(fidx);
   return nd;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Topic caches: TopicCache::add_change (structure/dds_cache.rs:210-284)    */
+/* over the deliveries of rtps_oracle_ingest_batch, in order.  The cache's   */
+/* `changes` BTreeMap is keyed by receive instant, i.e. insertion order; the */
+/* garbage collection remove_changes_before(ZERO) (:367-420) removes only    */
+/* the oldest (`ts < ZERO` never holds, so may_remove never exceeds          */
+/* must_remove), so the live changes are always the insertions with index   */
+/* in [E, I) (I = insertions so far, E = removed so far), and a GC sets      */
+/* E = max(E, I - max_keep).  sequence_numbers (:134-135) maps (writer GUID, */
+/* SN) to a live change: here the key's last insertion index, live iff >= E. */
+/* ------------------------------------------------------------------------ */
+typedef struct tc_ent { uint8_t guid[16]; int64_t sn; uint32_t topic; uint64_t idx; } tc_ent;
+typedef struct rtps_oracle_topics {
+  uint32_t nt;           /* topics: [0, nt) configured, then one private topic per unmapped slot */
+  uint32_t topic_of[65536];
+  uint64_t* I; uint64_t* E; uint32_t* K;
+  uint32_t cap_t;
+  tc_ent* map; uint8_t* used; size_t cap, n;
+} rtps_oracle_topics;
+
+static size_t tc_h(const uint8_t g[16], int64_t sn, uint32_t t) {
+  uint64_t x = 0x9e3779b97f4a7c15ull ^ t;
+  for (int i = 0; i < 16; ++i) x = (x ^ g[i]) * 0x100000001b3ull;
+  x = (x ^ (uint64_t)sn) * 0xff51afd7ed558ccdull;
+  return (size_t)(x ^ (x >> 29));
+}
+static tc_ent* tc_find(rtps_oracle_topics* h, const uint8_t g[16], int64_t sn, uint32_t t) {
+  if (!h->cap) return NULL;
+  for (size_t j = tc_h(g, sn, t) & (h->cap - 1); h->used[j]; j = (j + 1) & (h->cap - 1))
+    if (h->map[j].topic == t && h->map[j].sn == sn && !memcmp(h->map[j].guid, g, 16)) return &h->map[j];
+  return NULL;
+}
+static void tc_put(rtps_oracle_topics* h, const uint8_t g[16], int64_t sn, uint32_t t, uint64_t idx) {
+  tc_ent* e = tc_find(h, g, sn, t);
+  if (e) { e->idx = idx; return; }
+  if ((h->n + 1) * 2 > h->cap) {
+    size_t ncap = h->cap ? h->cap * 2 : 1024;
+    tc_ent* nm = (tc_ent*)calloc(ncap, sizeof(tc_ent));
+    uint8_t* nu = (uint8_t*)calloc(ncap, 1);
+    for (size_t i = 0; i < h->cap; ++i)
+      if (h->used[i]) {
+        size_t j = tc_h(h->map[i].guid, h->map[i].sn, h->map[i].topic) & (ncap - 1);
+        while (nu[j]) j = (j + 1) & (ncap - 1);
+        nu[j] = 1; nm[j] = h->map[i];
+      }
+    free(h->map); free(h->used); h->map = nm; h->used = nu; h->cap = ncap;
+  }
+  size_t j = tc_h(g, sn, t) & (h->cap - 1);
+  while (h->used[j]) j = (j + 1) & (h->cap - 1);
+  h->used[j] = 1;
+  memcpy(h->map[j].guid, g, 16); h->map[j].sn = sn; h->map[j].topic = t; h->map[j].idx = idx;
+  h->n++;
+}
+/* topics[n] = (topic id, max_keep_samples); readers[m] = (reader slot, topic id) */
+rtps_oracle_topics* rtps_oracle_topics_new(const rtps_topic* topics, uint32_t n, const rtps_topic_reader* readers,
+                                           uint32_t m) {
+  rtps_oracle_topics* h = (rtps_oracle_topics*)calloc(1, sizeof(rtps_oracle_topics));
+  h->nt = n;
+  h->cap_t = n + 65536u;
+  h->I = (uint64_t*)calloc(h->cap_t, 8); h->E = (uint64_t*)calloc(h->cap_t, 8); h->K = (uint32_t*)calloc(h->cap_t, 4);
+  for (uint32_t t = 0; t < n; ++t) h->K[t] = topics[t].max_keep_samples ? topics[t].max_keep_samples : 1u;
+  for (uint32_t s = 0; s < 65536u; ++s) { h->topic_of[s] = n + s; h->K[n + s] = 64; }  /* private topic per slot */
+  for (uint32_t r = 0; r < m; ++r)
+    for (uint32_t t = 0; t < n; ++t)
+      if (topics[t].topic == readers[r].topic) h->topic_of[readers[r].reader_slot] = t;
+  return h;
+}
+void rtps_oracle_topics_free(rtps_oracle_topics* h) {
+  if (!h) return;
+  free(h->I); free(h->E); free(h->K); free(h->map); free(h->used); free(h);
+}
+/* remove_changes_before(ZERO) on every topic (DDSCache::garbage_collect) */
+void rtps_oracle_topics_gc(rtps_oracle_topics* h) {
+  for (uint32_t t = 0; t < h->cap_t; ++t)
+    if (h->I[t] - h->E[t] > h->K[t]) h->E[t] = h->I[t] - h->K[t];
+}
+/* add_change for every delivery in order (the change of record rec_idx: writer GUID =
+ * prefix || writer_id, SN = the record's sn, which a DATA_FRAG's completed sample shares);
+ * sets RTPS_DELIVERY_CACHED in del[k].flags when it is stored.  Returns the stored count. */
+uint64_t rtps_oracle_topics_apply(rtps_oracle_topics* h, const rtps_record* recs, uint64_t m, rtps_delivery* del,
+                                  uint64_t nd) {
+  uint64_t stored = 0;
+  for (uint64_t k = 0; k < nd; ++k) {
+    del[k].flags &= (uint16_t)~RTPS_DELIVERY_CACHED;
+    if (del[k].rec_idx >= m) continue;
+    const rtps_record* r = &recs[del[k].rec_idx];
+    uint8_t g[16];
+    memcpy(g, r->prefix, 12); memcpy(g + 12, r->writer_id, 4);
+    const uint32_t t = h->topic_of[del[k].reader_slot];
+    /* garbage collection first, at every 64th sequence number ((sn as usize) % 64 == 0, :230-238) */
+    if (((uint64_t)r->sn & 63u) == 0 && h->I[t] - h->E[t] > h->K[t]) h->E[t] = h->I[t] - h->K[t];
+    const tc_ent* e = tc_find(h, g, r->sn, t);
+    if (e && e->idx >= h->E[t]) continue;  /* find_by_sn hit: duplicate, not stored (:241-252) */
+    tc_put(h, g, r->sn, t, h->I[t]);       /* insert_sn + changes.insert (:254-256) */
+    h->I[t]++;
+    del[k].flags |= RTPS_DELIVERY_CACHED;
+    stored++;
+  }
+  return stored;
 }

@@ -805,7 +805,7 @@ __global__ __launch_bounds__(IT) void k_dwrite(const uint8_t* flag, uint64_t n, 
           rtps_delivery d;
           d.rec_idx = ident ? (uint32_t)k : x.erec[k];
           d.reader_slot = (uint16_t)(x.emeta[k] & 0xffffu);
-          d._r = 0;
+          d.flags = 0;
           out[o] = d;
         }
         ++o;

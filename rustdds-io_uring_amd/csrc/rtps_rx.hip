@@ -45,6 +45,7 @@
 #include "rtps_ctx.h"
 #include "rtps_ingest.h"
 #include "rtps_readers.h"
+#include "rtps_topic.h"
 
 namespace {
 
@@ -2040,6 +2041,7 @@ struct rtps_rx_ctx {
   uint32_t k_spec = 1;  // speculated records per datagram (0 disables nothing: see set_spec_hint)
   FragState* frag = nullptr;  // DataFrag reassembly state (created on first use)
   IngestState* ingest = nullptr;  // history-cache ingest state (created on first use)
+  TopicState* topics = nullptr;   // topic caches (created on first use)
   uint64_t* chain = nullptr;      // look-back words of the chained launch [chain_words(tiles) + 2]
   uint32_t* mixed = nullptr;      // pinned: {mixed tiles, tiles} of the last finished batch (kernel B)
   uint32_t ch_spin_limit = CH_SPIN_LIMIT;
@@ -2121,6 +2123,7 @@ int rtps_rx_destroy(rtps_rx_ctx* c) {
   (void)hipFree(c->bucket_hist);
   rtps_frag_state_free(c->frag);
   rtps_ingest_state_free(c->ingest);
+  rtps_topic_state_free(c->topics);
   {
     void* it[] = {c->it_items, c->it_wcnt, c->it_prefix};
     for (void* q : it) if (q) (void)hipFree(q);
@@ -2145,19 +2148,62 @@ static int readers_table(rtps_rx_ctx* c) {
   return c->readers ? RTPS_RX_OK : RTPS_RX_ENOMEM;
 }
 
+// the topic caches follow the readers (which topics have one reader, fresh proxies)
+static int topics_follow(rtps_rx_ctx* c) {
+  if (!c->topics) return RTPS_RX_OK;
+  const uint32_t* first = nullptr;
+  const rtps_target* ent = nullptr;
+  uint32_t n_sets = 0;
+  rt_host(c->readers, &first, &ent, &n_sets);
+  return rtps_topic_readers_changed(c->topics, first, ent, n_sets, c->stream);
+}
+
 int rtps_rx_set_readers(rtps_rx_ctx* c, const rtps_reader* readers, uint32_t n_readers, const rtps_proxy* proxies,
                         uint32_t n_proxies) {
   if (!c) return RTPS_RX_EINVAL;
   (void)hipSetDevice(c->device);
-  const int rc = readers_table(c);
-  return rc ? rc : rt_set(c->readers, readers, n_readers, proxies, n_proxies, c->stream);
+  int rc = readers_table(c);
+  if (!rc) rc = rt_set(c->readers, readers, n_readers, proxies, n_proxies, c->stream);
+  return rc ? rc : topics_follow(c);
 }
 
 int rtps_rx_set_match_table(rtps_rx_ctx* c, const rtps_match* t, uint32_t n) {
   if (!c) return RTPS_RX_EINVAL;
   (void)hipSetDevice(c->device);
-  const int rc = readers_table(c);
-  return rc ? rc : rt_set_match(c->readers, t, n, c->stream);
+  int rc = readers_table(c);
+  if (!rc) rc = rt_set_match(c->readers, t, n, c->stream);
+  return rc ? rc : topics_follow(c);
+}
+
+static int topics_state(rtps_rx_ctx* c) {
+  if (c->topics) return RTPS_RX_OK;
+  c->topics = rtps_topic_state_new(c->device);
+  if (!c->topics) return RTPS_RX_ENOMEM;
+  const uint32_t* first = nullptr;
+  const rtps_target* ent = nullptr;
+  uint32_t n_sets = 0;
+  if (c->readers) rt_host(c->readers, &first, &ent, &n_sets);
+  return rtps_topic_configure(c->topics, nullptr, 0, nullptr, 0, first, ent, n_sets, c->stream);
+}
+
+int rtps_rx_set_topics(rtps_rx_ctx* c, const rtps_topic* topics, uint32_t n_topics, const rtps_topic_reader* readers,
+                       uint32_t n_readers) {
+  if (!c) return RTPS_RX_EINVAL;
+  (void)hipSetDevice(c->device);
+  int rc = topics_state(c);
+  if (rc) return rc;
+  const uint32_t* first = nullptr;
+  const rtps_target* ent = nullptr;
+  uint32_t n_sets = 0;
+  if (c->readers) rt_host(c->readers, &first, &ent, &n_sets);
+  return rtps_topic_configure(c->topics, topics, n_topics, readers, n_readers, first, ent, n_sets, c->stream);
+}
+
+int rtps_rx_topic_gc(rtps_rx_ctx* c) {
+  if (!c) return RTPS_RX_EINVAL;
+  if (!c->topics) return RTPS_RX_OK;
+  (void)hipSetDevice(c->device);
+  return rtps_topic_gc(c->topics, c->stream);
 }
 
 int rtps_rx_target_table(const rtps_rx_ctx* c, const uint32_t** first, const rtps_target** entries, uint32_t* n_sets) {
@@ -2595,15 +2641,20 @@ int rtps_rx_ingest(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len, con
   const ReaderDev rd = rt_dev(c->readers);
   if (rd.gkeys == nullptr) return RTPS_RX_EINVAL;
   if (max_records && (!arena || !dgram_off)) return RTPS_RX_EINVAL;
-  if (flags & ~RTPS_INGEST_BEST_EFFORT) return RTPS_RX_EINVAL;
+  if (flags & ~(RTPS_INGEST_BEST_EFFORT | RTPS_INGEST_TOPIC_CACHE)) return RTPS_RX_EINVAL;
   if (frag && (!n_frag || !max_frag)) return RTPS_RX_EINVAL;
   (void)hipSetDevice(c->device);
   if (!c->ingest) {
     c->ingest = rtps_ingest_state_new(c->device);
     if (!c->ingest) return RTPS_RX_ENOMEM;
   }
-  return rtps_ingest_batch(c->ingest, c->stream, rd, arena, arena_len, dgram_off, records, n_records, max_records,
-                           frag, n_frag, max_frag, flags, out);
+  int rc = rtps_ingest_batch(c->ingest, c->stream, rd, arena, arena_len, dgram_off, records, n_records, max_records,
+                             frag, n_frag, max_frag, flags & ~RTPS_INGEST_TOPIC_CACHE, out);
+  if (rc || !(flags & RTPS_INGEST_TOPIC_CACHE)) return rc;
+  // the topic caches' add_change over the deliveries (rtps_topic.hip)
+  rc = topics_state(c);
+  return rc ? rc : rtps_topic_apply(c->topics, c->stream, records, n_records, max_records, out->accepted,
+                                    out->n_accepted, out->max_accepted);
 }
 
 /* test / measurement hook (not part of the public header): the ingest's
@@ -2645,9 +2696,10 @@ int rtps_rx_debug_proxy_stamps(rtps_rx_ctx* c, uint64_t* host, uint64_t n) {
 
 int rtps_rx_ingest_reset(rtps_rx_ctx* c) {
   if (!c) return RTPS_RX_EINVAL;
-  if (!c->ingest) return RTPS_RX_OK;
   (void)hipSetDevice(c->device);
-  return rtps_ingest_state_reset(c->ingest, c->stream);
+  const int rc = c->ingest ? rtps_ingest_state_reset(c->ingest, c->stream) : RTPS_RX_OK;
+  if (rc || !c->topics) return rc;
+  return rtps_topic_reset(c->topics, c->stream);
 }
 
 uint32_t rtps_rx_record_size(void) { return (uint32_t)sizeof(rtps_record); }

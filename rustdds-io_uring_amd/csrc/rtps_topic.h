@@ -1,0 +1,30 @@
+// rtps_topic.h — internal interface of the topic caches (rtps_topic.hip) used by the C
+// ABI in rtps_rx.hip.  Not installed; see include/rtps_rx.h ("topic caches").
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/rtps_rx.h"
+
+struct TopicState;  // per-topic insertion counters + the live (writer GUID, SN) index, batch scratch
+
+TopicState* rtps_topic_state_new(int device);
+void rtps_topic_state_free(TopicState* s);
+// rtps_rx_set_topics: the topic table and the readers' topics; empties every cache.
+// set_first / ent / n_sets: the context's target sets (host view), for the readers' flags.
+int rtps_topic_configure(TopicState* s, const rtps_topic* topics, uint32_t n_topics, const rtps_topic_reader* readers,
+                         uint32_t n_readers, const uint32_t* set_first, const rtps_target* ent, uint32_t n_sets,
+                         hipStream_t st);
+// After rtps_rx_set_readers: new readers / proxies (their private topics, which topics
+// have one reader); fresh proxies may re-accept changes a topic still holds, so every
+// topic checks each delivery against its live changes until those have aged out.
+int rtps_topic_readers_changed(TopicState* s, const uint32_t* set_first, const rtps_target* ent, uint32_t n_sets,
+                               hipStream_t st);
+// Every topic cache emptied (rtps_rx_ingest_reset).
+int rtps_topic_reset(TopicState* s, hipStream_t st);
+// DDSCache::garbage_collect.
+int rtps_topic_gc(TopicState* s, hipStream_t st);
+// TopicCache::add_change for every delivery of the batch, in order: sets or clears
+// RTPS_DELIVERY_CACHED in del[k].flags (asynchronous).
+int rtps_topic_apply(TopicState* s, hipStream_t st, const rtps_record* recs, const uint64_t* n_records,
+                     uint64_t max_records, rtps_delivery* del, const uint64_t* n_del, uint64_t max_del);

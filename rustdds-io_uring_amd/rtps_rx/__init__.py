@@ -59,6 +59,7 @@ class _IngestOut(ctypes.Structure):
 
 
 INGEST_BEST_EFFORT = 0x1
+INGEST_TOPIC_CACHE = 0x2  # also run the topic caches' add_change (DELIVERY_CACHED on the deliveries)
 INGEST_WINDOW = 1 << 17
 
 
@@ -75,7 +76,7 @@ EXPORTS = ["rtps_rx_create", "rtps_rx_destroy", "rtps_rx_set_stream", "rtps_rx_s
            "rtps_rx_frag_set_clock", "rtps_rx_frag_gc",
            "rtps_rx_bucket_descriptors", "rtps_rx_ingest", "rtps_rx_ingest_reset", "rtps_udp_open", "rtps_udp_close",
            "rtps_udp_port", "rtps_udp_backend", "rtps_udp_recv_batch", "rtps_udp_release", "rtps_udp_send_batch",
-           "rtps_rx_pump"]
+           "rtps_rx_pump", "rtps_rx_set_topics", "rtps_rx_topic_gc", "rtps_rx_cdr_decode_list"]
 
 
 def lib():
@@ -118,6 +119,10 @@ def lib():
         L.rtps_rx_ingest.restype = I
         L.rtps_rx_ingest_reset.argtypes = [P]
         L.rtps_rx_ingest_reset.restype = I
+        L.rtps_rx_set_topics.argtypes = [P, P, U32, P, U32]
+        L.rtps_rx_set_topics.restype = I
+        L.rtps_rx_topic_gc.argtypes = [P]
+        L.rtps_rx_topic_gc.restype = I
         L.rtps_rx_set_spec_hint.argtypes = [P, U32]
         L.rtps_rx_set_spec_hint.restype = I
         L.rtps_rx_cdr_decode.argtypes = [P, P, U32, U32, P, U64, P, P, P, U64, P, P]
@@ -491,10 +496,28 @@ class MessageReceiver:
                 "ack_base": torch.zeros(max(n_proxies, 1), dtype=torch.int64, device=dev),
                 "n_window_overflow": torch.zeros(1, dtype=torch.int64, device=dev)}
 
-    def ingest(self, arena, off, outs, iouts, fouts=None, best_effort=False):
-        """Decide which samples of a parsed batch enter the history cache (the
-        stateful reader's writer proxies, Reader::handle_data_msg / _heartbeat_ /
-        _gap_); fouts: frag_assemble outputs of the same batch.  Asynchronous."""
+    def set_topics(self, topics, topic_readers):
+        """Topic caches: topics [(topic id, max_keep_samples)], topic_readers [(reader slot, topic id)];
+        unmapped readers keep a cache of their own (max_keep 64).  Empties every topic cache."""
+        from .records import TOPIC_DTYPE, TOPIC_READER_DTYPE
+        t = np.zeros(len(topics), dtype=TOPIC_DTYPE)
+        for i, (tid, k) in enumerate(topics):
+            t[i] = (tid, k)
+        r = np.zeros(len(topic_readers), dtype=TOPIC_READER_DTYPE)
+        for i, (slot, tid) in enumerate(topic_readers):
+            r[i]["reader_slot"], r[i]["topic"] = slot, tid
+        _check(lib().rtps_rx_set_topics(self._h, t.ctypes.data if len(t) else None, len(t),
+                                        r.ctypes.data if len(r) else None, len(r)))
+
+    def topic_gc(self):
+        """DDSCache::garbage_collect: every topic cache trimmed to its max_keep_samples newest changes."""
+        _check(lib().rtps_rx_topic_gc(self._h))
+
+    def ingest(self, arena, off, outs, iouts, fouts=None, best_effort=False, topic_cache=False):
+        """Decide which samples of a parsed batch the readers accept (the stateful
+        reader's writer proxies, Reader::handle_data_msg / _heartbeat_ / _gap_) and,
+        with topic_cache, which of them their topic caches store (DELIVERY_CACHED);
+        fouts: frag_assemble outputs of the same batch.  Asynchronous."""
         if iouts["accept"].numel() < max(outs["max_records"], 1):  # the ingest writes accept[0, max_records)
             raise ValueError(f"ingest: accept holds {iouts['accept'].numel()} bytes, the batch's record capacity "
                              f"is {outs['max_records']} (alloc_ingest_outputs(max_records, ...))")
@@ -513,12 +536,13 @@ class MessageReceiver:
         mfrag = fouts["max_samples"] if fouts is not None else 0
         _check(lib().rtps_rx_ingest(self._h, arena.data_ptr(), arena.numel(), off.data_ptr(),
                                     outs["records"].data_ptr(), outs["n_records"].data_ptr(), outs["max_records"],
-                                    frag, nfrag, mfrag, INGEST_BEST_EFFORT if best_effort else 0, ctypes.byref(o)))
+                                    frag, nfrag, mfrag, (INGEST_BEST_EFFORT if best_effort else 0) |
+                                    (INGEST_TOPIC_CACHE if topic_cache else 0), ctypes.byref(o)))
 
     def ingest_reset(self):
         _check(lib().rtps_rx_ingest_reset(self._h))
 
-    def ingest_batch(self, arena_np, off_np, len_np, n_proxies, frag=False, best_effort=False):
+    def ingest_batch(self, arena_np, off_np, len_np, n_proxies, frag=False, best_effort=False, topic_cache=False):
         """Parse (+ reassemble) + ingest host arrays -> (BatchResult, accept u8[m], deliveries
         DELIVERY_DTYPE[k], ack_base i64[n_proxies], n_window_overflow, frag samples or None)."""
         import torch
@@ -535,7 +559,7 @@ class MessageReceiver:
         self.parse_batch_device(arena, off, lens, n, outs)
         if frag:
             self.frag_assemble(arena, off, outs, fouts)
-        self.ingest(arena, off, outs, iouts, fouts, best_effort=best_effort)
+        self.ingest(arena, off, outs, iouts, fouts, best_effort=best_effort, topic_cache=topic_cache)
         self.sync()
         total = int(outs["n_records"].item())
         kept = min(total, cap)

@@ -66,7 +66,11 @@ MATCH_DTYPE = np.dtype([("writer_guid", "u1", (16,)), ("reader_slot", "<u2"), ("
 READER_DTYPE = np.dtype([("entity_id", "u1", (4,)), ("reader_slot", "<u2"), ("flags", "<u2")])
 PROXY_DTYPE = np.dtype([("writer_guid", "u1", (16,)), ("reader", "<u4")])
 TARGET_DTYPE = np.dtype([("reader_slot", "<u2"), ("reader_flags", "<u2"), ("proxy", "<u4")])
-DELIVERY_DTYPE = np.dtype([("rec_idx", "<u4"), ("reader_slot", "<u2"), ("_r", "<u2")])
+DELIVERY_DTYPE = np.dtype([("rec_idx", "<u4"), ("reader_slot", "<u2"), ("flags", "<u2")])
+DELIVERY_CACHED = 0x1  # rtps_delivery.flags: TopicCache::add_change stored the change
+# topic caches (rtps_topic / rtps_topic_reader)
+TOPIC_DTYPE = np.dtype([("topic", "<u4"), ("max_keep_samples", "<u4")])
+TOPIC_READER_DTYPE = np.dtype([("reader_slot", "<u2"), ("_r", "<u2"), ("topic", "<u4")])
 assert READER_DTYPE.itemsize == 8 and PROXY_DTYPE.itemsize == 20 and TARGET_DTYPE.itemsize == 8
 assert DELIVERY_DTYPE.itemsize == 8
 
