@@ -367,10 +367,13 @@ int rtps_rx_exchange(rtps_rx_ctx* ctx, void* comm, void* hip_stream, const void*
  * rtps_rx_ingest as one GPU would on the whole stream:
  *   - items: every writer-kind record that passes (RTPS_ROUTE_PASS: DATA,
  *     DATA_FRAG, HEARTBEAT, HEARTBEAT_FRAG, GAP), owner = fmix32(fnv1a32(prefix ||
- *     writer_id)) % n_ranks (as rtps_rx_bucket_by_writer), each with its "blob":
- *     the arena bytes the owner's consumers read (a GAP's bitmap words, a
- *     DATA_FRAG's payload), 16-byte aligned.  DATA payloads stay on the source
- *     GPU (zero-copy): an owner record names its origin instead;
+ *     writer_id)) % n_ranks (as rtps_rx_bucket_by_writer).  What crosses is a
+ *     32-byte rtps_shard_item per record and a "blob": a DATA is its item alone
+ *     (writer GUID, SN, kind, flags, route, payload kind: what the owner's ingest
+ *     reads; its payload stays on the source GPU, zero-copy, and `origin` names the
+ *     record there); any other kind sends its whole 64-byte record in the blob,
+ *     followed by the arena bytes the owner's consumers read (a GAP's bitmap words,
+ *     a DATA_FRAG's payload), 16-byte aligned;
  *   - order: rank r parses the r-th contiguous chunk of the stream, so the
  *     records an owner receives, concatenated in source-rank order, are its
  *     writers' records in stream order;
@@ -384,11 +387,19 @@ int rtps_rx_exchange(rtps_rx_ctx* ctx, void* comm, void* hip_stream, const void*
  * for rtps_rx_frag_assemble / rtps_rx_ingest on the same context.
  * New: the reference has one process and no exchange. */
 typedef struct rtps_shard rtps_shard;
+typedef struct rtps_shard_item {  /* one exchanged writer record (32 bytes) */
+  uint32_t w[4];       /* DATA: the writer GUID (prefix || writer_id, as in the record); else w[0] = the
+                          item's blob bytes (64 + its consumers' bytes, rounded to 16), w[1..3] = 0 */
+  int64_t sn;          /* DATA: writer SN; else 0 */
+  uint8_t kind, flags, route, payload_kind;
+  uint32_t src_rec;    /* the record's index in the source rank's parse output */
+} rtps_shard_item;
+RTPS_RX_STATIC_ASSERT(sizeof(rtps_shard_item) == 32, "rtps_shard_item must be 32 bytes");
 typedef struct rtps_shard_counts {  /* one (source, destination) pair */
-  uint64_t n;          /* records */
+  uint64_t n;          /* items */
   uint64_t bytes;      /* blob bytes (multiple of 16) */
-  uint64_t cut;        /* records in the fixed slot: the first `cut` (the rest is spill) */
-  uint64_t cut_bytes;  /* blob bytes of those records */
+  uint64_t cut;        /* items in the fixed slot: the first `cut` (the rest is spill) */
+  uint64_t cut_bytes;  /* blob bytes of those items */
 } rtps_shard_counts;
 #define RTPS_SHARD_LEAD 65536u  /* zero bytes ahead of the owner arena's blobs */
 typedef struct rtps_owner_batch {  /* DEVICE pointers owned by the shard, valid until its next unpack */
@@ -396,13 +407,15 @@ typedef struct rtps_owner_batch {  /* DEVICE pointers owned by the shard, valid 
   uint64_t arena_len;
   const uint64_t* dgram_off;       /* [n_records]: record i's dgram_idx is i, its blob is at
                                       arena + dgram_off[i] + (u.gap.bitmap_off | u.frag.pl_off) */
-  const rtps_record* records;      /* [n_records], stream order; every field as parsed except dgram_idx */
-  const uint64_t* origin;          /* [n_records]: source rank << 32 | the record's dgram_idx in the source
-                                      rank's batch (with sub_off it names the submessage) */
+  const rtps_record* records;      /* [n_records], stream order; every field as parsed except dgram_idx,
+                                      for a DATA only kind, flags, route, payload_kind, the writer GUID
+                                      and sn (the rest stays at its origin) */
+  const uint64_t* origin;          /* [n_records]: source rank << 32 | the record's index in the source
+                                      rank's parse output */
   const uint64_t* n_records_dev;   /* device u64 (for the consumers' n_records argument) */
   uint64_t n_records;              /* host copy */
 } rtps_owner_batch;
-/* cap: records per peer slot (>= 1); bcap: blob bytes per peer slot (a multiple of 16). */
+/* cap: items per peer slot (>= 1); bcap: blob bytes per peer slot (a multiple of 16). */
 int rtps_rx_shard_create(rtps_rx_ctx* ctx, uint32_t n_ranks, uint64_t cap, uint64_t bcap, rtps_shard** out);
 int rtps_rx_shard_destroy(rtps_shard* s);
 /* Source side: partition this rank's parse output by owner into the fixed slots and
@@ -428,7 +441,7 @@ int rtps_rx_shard_unpack(rtps_shard* s, rtps_owner_batch* out);
  * [cut, n) / [cut_bytes, bytes) of that range); receive side, source s's spilled
  * records at sum_{s' < s} (n - cut), its bytes at sum_{s' < s} (bytes - cut_bytes). */
 typedef struct rtps_shard_buffers {
-  void* send_slots;        /* [n_ranks * cap] records; peer d's slot at d * cap */
+  void* send_slots;        /* [n_ranks * cap] rtps_shard_item; peer d's slot at d * cap */
   void* send_blob;         /* [n_ranks * bcap] */
   void* send_counts;       /* [n_ranks] rtps_shard_counts */
   void* recv_slots;
@@ -438,7 +451,7 @@ typedef struct rtps_shard_buffers {
   void* send_blob_spill;
   void* recv_spill;
   void* recv_blob_spill;
-  uint64_t recv_spill_cap;       /* records */
+  uint64_t recv_spill_cap;       /* items */
   uint64_t recv_blob_spill_cap;  /* bytes */
 } rtps_shard_buffers;
 int rtps_rx_shard_buffers(rtps_shard* s, rtps_shard_buffers* out);

@@ -124,7 +124,7 @@ int rtps_rx_shard_exchange(rtps_shard* s, void* comm, void* hip_stream) {
   if (hipSetDevice(s->device) != hipSuccess) return RTPS_RX_EHIP;
   hipStream_t st = hip_stream ? (hipStream_t)hip_stream : rtps_ctx_stream(s->ctx);
   if (hipStreamWaitEvent(st, s->packed, 0) != hipSuccess) return RTPS_RX_EHIP;  // the slots are complete
-  const size_t rb = (size_t)s->cap * sizeof(rtps_record), bb = (size_t)s->bcap;
+  const size_t rb = (size_t)s->cap * sizeof(shard_item), bb = (size_t)s->bcap;
   const size_t cw = sizeof(rtps_shard_counts) / sizeof(uint64_t);
   if (ncclGroupStart() != ncclSuccess) return RTPS_RX_EHIP;
   bool ok = true;
@@ -178,9 +178,9 @@ int rtps_rx_shard_finish(rtps_shard* s, void* comm, void* hip_stream) {
     const rtps_shard_counts& q = s->h_send[p];
     const rtps_shard_counts& r = s->h_recv[p];
     const uint64_t sn = q.n - q.cut, sbytes = q.bytes - q.cut_bytes, rn = r.n - r.cut, rbytes = r.bytes - r.cut_bytes;
-    ok = send_bytes(s->s_spill + sb + q.cut, sn * sizeof(rtps_record), (int)p, c, st) &&
+    ok = send_bytes(s->s_spill + sb + q.cut, sn * sizeof(shard_item), (int)p, c, st) &&
          send_bytes(s->s_bspill + sbb + q.cut_bytes, sbytes, (int)p, c, st) &&
-         recv_bytes(s->r_spill + rs, rn * sizeof(rtps_record), (int)p, c, st) &&
+         recv_bytes(s->r_spill + rs, rn * sizeof(shard_item), (int)p, c, st) &&
          recv_bytes(s->r_bspill + rsb, rbytes, (int)p, c, st);
     sb += q.n;
     sbb += q.bytes;

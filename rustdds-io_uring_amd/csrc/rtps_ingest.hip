@@ -269,10 +269,13 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x, uint32_t lane) {
 // batch on that path needs no host read-back of the counts.
 // BUCKET (FAST only): CHR consecutive slots per workgroup and the per-proxy counts
 // (the proxy bucketing above) instead of the radix sort's (key, slot) pairs.
-template <bool IDENT, bool FAST, bool BUCKET = false>
+// MARK (IDENT, not FAST): also the samples' first-cover keys (the marks of the global path,
+// k_marks_d's atomicMin), so that the global path needs no separate marks pass.
+template <bool IDENT, bool FAST, bool BUCKET = false, bool MARK = false>
 __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record* recs, const uint64_t* n_rec,
                                                  uint64_t max, const rtps_frag_sample* frag, uint32_t flags,
-                                                 Scratch x, uint64_t* ctr, FastOut fo, uint64_t* ctr_next) {
+                                                 Scratch x, uint64_t* ctr, FastOut fo, uint64_t* ctr_next, State st,
+                                                 uint32_t epoch) {
   extern __shared__ uint32_t s_rt[];
   __shared__ uint32_t s_cnt[BUCKET ? IT / 64 : 1][BUCKET ? PB_MAX : 1];  // per (wave, proxy)
   if (blockIdx.x == gridDim.x - 1u)  // the next batch's counters start at zero (no memset launch)
@@ -378,6 +381,12 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
         x.evt[i] = evi;
         x.ent[i] = ent;
         x.esn[i] = sn;
+        if (MARK && evi == EV_SAMPLE && ent != NONE) {  // k_marks_d's first-cover key
+          const int64_t lo = st.lo[ent];
+          if (sn >= lo && sn < lo + (int64_t)W)
+            atomicMin(reinterpret_cast<unsigned long long*>(st.fc + (uint64_t)ent * W) + (uint64_t)(sn - lo),
+                      ekey(epoch, (uint32_t)i));
+        }
       }
       if (!FAST) {
         x.hkey[i] = evi == EV_HB ? 1u : 0u;  // selection flag of the HEARTBEAT compaction
@@ -627,7 +636,8 @@ __device__ __forceinline__ bool proxied_sample(const Scratch& x, uint64_t k) {
 }
 
 // samples first: their sequence numbers (dbits) and first-cover keys
-__global__ __launch_bounds__(IT) void k_marks_d(uint64_t n, Scratch x, State s, uint32_t epoch, bool gaps) {
+__global__ __launch_bounds__(IT) void k_marks_d(uint64_t n, Scratch x, State s, uint32_t epoch, bool gaps,
+                                                bool keys = true) {
   for (uint64_t i0 = (uint64_t)blockIdx.x * IT; i0 < n; i0 += (uint64_t)gridDim.x * IT) {  // wave-uniform trip count
     const uint64_t i = i0 + threadIdx.x;
     bool act = i < n && proxied_sample(x, i);
@@ -641,7 +651,7 @@ __global__ __launch_bounds__(IT) void k_marks_d(uint64_t n, Scratch x, State s, 
         const uint64_t off = (uint64_t)(v - lo);
         word = s.dbits + (uint64_t)e * WW + (off >> 5);
         bit = 1u << (off & 31u);
-        atomicMin(reinterpret_cast<unsigned long long*>(s.fc + (uint64_t)e * W) + off, ekey(epoch, (uint32_t)i));
+        if (keys) atomicMin(reinterpret_cast<unsigned long long*>(s.fc + (uint64_t)e * W) + off, ekey(epoch, (uint32_t)i));
       }
     }
     if (gaps) wave_or(s.dbits, word, bit, act);  // the sample bitmap only serves k_marks_g
@@ -670,42 +680,54 @@ __global__ __launch_bounds__(IT) void k_marks_g(const rtps_record* recs, const u
   }
 }
 
-// ---- 4 decide ----  (acc[0, cap): entries past n are cleared)
+// ---- 4 decide ----
+// one sample event: accepted?  pe / poff / merge: the proxy and window offset of a sample
+// whose position the change-set merge sets (an accepted sample in the window, or any sample
+// of a DUPLICATES_OK reader's proxy in it: received_changes_add runs for those too)
+__device__ __forceinline__ uint8_t decide_one(uint64_t i, uint64_t n, const Scratch& x, const State& s, bool reliable,
+                                              uint32_t epoch, uint32_t& pe, uint64_t& poff, bool& merge) {
+  merge = false;
+  if (i >= n || x.evt[i] != EV_SAMPLE) return 0;
+  const uint32_t e = x.ent[i], meta = x.emeta[i];
+  if (e == NONE) return 1;  // no proxy: the writer kind is not user-defined (reader.rs:734-739)
+  const int64_t v = x.esn[i], lo = s.lo[e];
+  const bool in_win = v >= lo && v < lo + (int64_t)W;
+  pe = e;
+  poff = (uint64_t)(v - lo);
+  if (meta & EVF_DUP_OK) {  // the participant reader's duplicates (reader.rs:712-722)
+    merge = in_win;
+    return 1;
+  }
+  int64_t thr = s.base[e];
+  const uint32_t sb = s.seg_b[e], se = s.seg_e[e];
+  // accepted HEARTBEATs of this proxy before event i (only needed when the
+  // proxy's final threshold is above v)
+  if (reliable && se > sb && x.hpre[se - 1u] > v && v >= thr) {
+    uint32_t a = sb, b = se;
+    while (a < b) {  // first sorted position whose event is >= i
+      const uint32_t m = (a + b) >> 1;
+      if (x.sval[m] < (uint32_t)i) a = m + 1u; else b = m;
+    }
+    if (a > sb && x.hpre[a - 1u] > thr) thr = x.hpre[a - 1u];
+  }
+  if (v < 1 || v < thr) return 0;
+  if (v >= lo + (int64_t)W) {  // beyond the tracked window: accepted unchecked
+    atomicAdd(reinterpret_cast<unsigned long long*>(s.ctr + C_OVF), 1ull);
+    return 1;
+  }
+  const bool known = (s.bits[(uint64_t)e * WW + (poff >> 5)] >> (poff & 31u)) & 1u;
+  const uint8_t acc = (!known && s.fc[(uint64_t)e * W + poff] == ekey(epoch, (uint32_t)i)) ? 1 : 0;
+  merge = acc != 0;
+  return acc;
+}
+// (acc[0, cap): entries past n are cleared)
 __global__ __launch_bounds__(IT) void k_decide(uint64_t n, uint64_t cap, Scratch x, State s, uint8_t* acc_out,
                                                bool reliable, uint32_t epoch) {
   for (uint64_t i = (uint64_t)blockIdx.x * IT + threadIdx.x; i < cap; i += (uint64_t)gridDim.x * IT) {
-    uint8_t acc = 0;
-    if (i < n && x.evt[i] == EV_SAMPLE) {
-      const uint32_t e = x.ent[i], meta = x.emeta[i];
-      if (e == NONE || (meta & EVF_DUP_OK)) {
-        acc = 1;  // no proxy (writer kind not user-defined), or the participant reader's duplicates (reader.rs:712-722)
-      } else {
-        const int64_t v = x.esn[i], lo = s.lo[e];
-        int64_t thr = s.base[e];
-        const uint32_t sb = s.seg_b[e], se = s.seg_e[e];
-        // accepted HEARTBEATs of this proxy before event i (only needed when the
-        // proxy's final threshold is above v)
-        if (reliable && se > sb && x.hpre[se - 1u] > v && v >= thr) {
-          uint32_t a = sb, b = se;
-          while (a < b) {  // first sorted position whose event is >= i
-            const uint32_t m = (a + b) >> 1;
-            if (x.sval[m] < (uint32_t)i) a = m + 1u; else b = m;
-          }
-          if (a > sb && x.hpre[a - 1u] > thr) thr = x.hpre[a - 1u];
-        }
-        if (v >= 1 && v >= thr) {
-          if (v >= lo + (int64_t)W) {  // beyond the tracked window: accepted unchecked
-            acc = 1;
-            atomicAdd(reinterpret_cast<unsigned long long*>(s.ctr + C_OVF), 1ull);
-          } else {
-            const uint64_t off = (uint64_t)(v - lo);
-            const bool known = (s.bits[(uint64_t)e * WW + (off >> 5)] >> (off & 31u)) & 1u;
-            acc = (!known && s.fc[(uint64_t)e * W + off] == ekey(epoch, (uint32_t)i)) ? 1 : 0;
-          }
-        }
-      }
-    }
-    acc_out[i] = acc;
+    uint32_t e;
+    uint64_t off;
+    bool w;
+    acc_out[i] = decide_one(i, n, x, s, reliable, epoch, e, off, w);
   }
 }
 
@@ -749,6 +771,45 @@ __device__ __forceinline__ uint64_t block_sum64(uint64_t v, uint64_t* s_w) {
   for (uint32_t w = 0; w < IT / 64; ++w) t += s_w[w];
   return t;
 }
+// Global identity path: decide + the delivery tile counts (k_dcount's) in one pass, DPT
+// consecutive events per thread (tiles of DT, the tiling k_dwrite reads), and for GAP-free
+// batches (MERGE) the change-set merge: a window position is set by its accepted first
+// cover (or by a DUPLICATES_OK reader's samples, whose proxy's decisions read no bits), so
+// no decision of the pass reads a bit the pass sets for another event; the positions of
+// the other samples lie below the new ack_base (v < 1 or below a HEARTBEAT threshold) or
+// are set already, so k_merge's extra bits there change nothing k_state reads.
+template <bool MERGE>
+__global__ __launch_bounds__(IT) void k_decide_t(uint64_t n, uint64_t cap, Scratch x, State s, uint8_t* acc_out,
+                                                 bool reliable, uint32_t epoch, uint32_t* tcnt) {
+  __shared__ uint64_t s_w[IT / 64];
+  const uint64_t b0 = (uint64_t)blockIdx.x * DT + threadIdx.x * DPT;
+  uint32_t w[DPT / 4];
+#pragma unroll
+  for (uint32_t q = 0; q < DPT / 4; ++q) w[q] = 0u;
+  uint32_t c = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < DPT; ++j) {
+    uint32_t e = 0;
+    uint64_t off = 0;
+    bool merge = false;
+    const uint8_t a = decide_one(b0 + j, n, x, s, reliable, epoch, e, off, merge);
+    w[j >> 2] |= (uint32_t)a << (8u * (j & 3u));
+    c += a;
+    if (MERGE) wave_or(s.bits, merge ? s.bits + (uint64_t)e * WW + (off >> 5) : s.bits, 1u << (off & 31u), merge);
+  }
+  if (b0 + DPT <= cap) {
+#pragma unroll
+    for (uint32_t q = 0; q < DPT / 8; ++q) {
+      uint2 v = make_uint2(w[2 * q], w[2 * q + 1]);
+      __builtin_memcpy(acc_out + b0 + 8u * q, &v, 8);
+    }
+  } else {
+    for (uint64_t i = b0; i < cap; ++i) acc_out[i] = (uint8_t)(w[(i - b0) >> 2] >> (8u * ((i - b0) & 3u)));
+  }
+  const uint64_t t = block_sum64(c, s_w);
+  if (threadIdx.x == 0) tcnt[blockIdx.x] = (uint32_t)t;
+}
+
 __global__ __launch_bounds__(IT) void k_dcount(const uint8_t* flag, uint64_t n, uint32_t* tcnt) {
   __shared__ uint64_t s_w[IT / 64];
   uint32_t w[DPT / 4];
@@ -762,18 +823,16 @@ __global__ __launch_bounds__(IT) void k_dcount(const uint8_t* flag, uint64_t n, 
   const uint64_t t = block_sum64(c, s_w);
   if (threadIdx.x == 0) tcnt[blockIdx.x] = (uint32_t)t;
 }
-__global__ __launch_bounds__(IT) void k_dwrite(const uint8_t* flag, uint64_t n, const uint32_t* tcnt, uint32_t ntiles,
-                                               Scratch x, bool ident, uint64_t max_out, rtps_delivery* out,
-                                               uint64_t* n_out, const uint64_t* ctr, uint64_t* ovf_out,
-                                               uint64_t* hev) {
-  __shared__ uint64_t s_w[IT / 64];
-  __shared__ uint32_t s_c[IT / 64];
+__device__ __forceinline__ void dwrite_tile(uint32_t blk, const uint8_t* flag, uint64_t n, const uint32_t* tcnt,
+                                            uint32_t ntiles, const Scratch& x, bool ident, uint64_t max_out,
+                                            rtps_delivery* out, uint64_t* n_out, const uint64_t* ctr, uint64_t* ovf_out,
+                                            uint64_t* hev, uint64_t* s_w, uint32_t* s_c) {
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   uint64_t pre = 0;
-  for (uint32_t t = tid; t < blockIdx.x; t += IT) pre += tcnt[t];
+  for (uint32_t t = tid; t < blk; t += IT) pre += tcnt[t];
   pre = block_sum64(pre, s_w);
   uint32_t w[DPT / 4];
-  const uint64_t b0 = (uint64_t)blockIdx.x * DT + tid * DPT;
+  const uint64_t b0 = (uint64_t)blk * DT + tid * DPT;
   uint32_t c = 0;
   if (b0 < n) {
     dflags(flag, n, b0, w);
@@ -812,7 +871,7 @@ __global__ __launch_bounds__(IT) void k_dwrite(const uint8_t* flag, uint64_t n, 
       }
     }
   }
-  if (blockIdx.x + 1 == ntiles && tid == 0) {
+  if (blk + 1 == ntiles && tid == 0) {
     *n_out = pre + tot;
     if (ovf_out) *ovf_out = ctr[C_OVF];  // the batch's window overflows (counted before the select)
     if (hev) {  // the batch's events, for the next batch's path choice (pinned host memory, read without a sync)
@@ -821,6 +880,14 @@ __global__ __launch_bounds__(IT) void k_dwrite(const uint8_t* flag, uint64_t n, 
       *hev = ne;
     }
   }
+}
+__global__ __launch_bounds__(IT) void k_dwrite(const uint8_t* flag, uint64_t n, const uint32_t* tcnt, uint32_t ntiles,
+                                               Scratch x, bool ident, uint64_t max_out, rtps_delivery* out,
+                                               uint64_t* n_out, const uint64_t* ctr, uint64_t* ovf_out,
+                                               uint64_t* hev) {
+  __shared__ uint64_t s_w[IT / 64];
+  __shared__ uint32_t s_c[IT / 64];
+  dwrite_tile(blockIdx.x, flag, n, tcnt, ntiles, x, ident, max_out, out, n_out, ctr, ovf_out, hev, s_w, s_c);
 }
 __global__ __launch_bounds__(IT) void k_accept_counts(uint64_t n, uint64_t cap, Scratch x, uint8_t* accept) {
   for (uint64_t i = (uint64_t)blockIdx.x * IT + threadIdx.x; i < cap; i += (uint64_t)gridDim.x * IT) {
@@ -879,13 +946,12 @@ __global__ __launch_bounds__(IT) void k_merge(const rtps_record* recs, const uin
 }
 
 // ---- 7 state: one workgroup per proxy ----
-// (workgroup 0 also reports the window-overflow count: every decision is made by now)
-__global__ __launch_bounds__(IT) void k_state(uint32_t n_entries, Scratch x, State s, bool reliable, int64_t* ack_out,
-                                              uint64_t* ovf_out) {
-  __shared__ uint32_t sh[WW];
-  __shared__ uint32_t s_first;
-  const uint32_t e = blockIdx.x, tid = threadIdx.x;
-  if (e >= n_entries) return;
+// The proxy's window is read once into LDS (16 words per thread, all loads in flight), the
+// first uncovered sequence number at or above the threshold found with one block-wide
+// minimum, and the window re-anchored at the new ack_base from the LDS copy.
+__device__ __forceinline__ void state_proxy(uint32_t e, const Scratch& x, const State& s, bool reliable,
+                                            int64_t* ack_out, uint32_t* sh, uint32_t& s_first) {
+  const uint32_t tid = threadIdx.x;
   const int64_t lo = s.lo[e];
   int64_t thr = s.base[e];
   int32_t hbc = s.hbc[e];
@@ -897,39 +963,63 @@ __global__ __launch_bounds__(IT) void k_state(uint32_t n_entries, Scratch x, Sta
     if (c > hbc) hbc = c;
   }
   uint32_t* bits = s.bits + (uint64_t)e * WW;
+  const u32x4* b4 = reinterpret_cast<const u32x4*>(bits);
+  u32x4* sh4 = reinterpret_cast<u32x4*>(sh);
+  for (uint32_t q = tid; q < WW / 4; q += IT) sh4[q] = b4[q];
+  if (tid == 0) s_first = NONE;
+  __syncthreads();
   // advance_ack_base: the first sequence number >= thr outside the change set
   int64_t nb = thr;
   if (thr < lo + (int64_t)W) {
-    const uint32_t off0 = (uint32_t)(thr - lo);
-    if (tid == 0) s_first = NONE;
-    __syncthreads();
-    for (uint32_t w0 = off0 >> 5; w0 < WW; w0 += IT) {
-      const uint32_t w = w0 + tid;
-      if (w < WW) {
-        uint32_t word = bits[w];
-        if (w == (off0 >> 5)) word |= (1u << (off0 & 31u)) - 1u;  // below thr: covered
-        if (word != 0xffffffffu) atomicMin(&s_first, w * 32u + (uint32_t)__builtin_ctz(~word));
+    const uint32_t off0 = (uint32_t)(thr - lo), w0 = off0 >> 5;
+    for (uint32_t w = w0 + tid; w < WW; w += IT) {  // a thread's words ascend: its first hit is its least
+      uint32_t word = sh[w];
+      if (w == w0) word |= (1u << (off0 & 31u)) - 1u;  // below thr: covered
+      if (word != 0xffffffffu) {
+        atomicMin(&s_first, w * 32u + (uint32_t)__builtin_ctz(~word));
+        break;
       }
-      __syncthreads();
-      if (s_first != NONE) break;
-      __syncthreads();
     }
+    __syncthreads();
     nb = lo + (int64_t)(s_first != NONE ? s_first : W);
   }
   // re-anchor the window at the new ack_base (bits below it are no longer needed)
   const int64_t nlo = nb & ~(int64_t)31;
   if (nlo != lo) {
     const uint64_t shift = (uint64_t)(nlo - lo) >> 5;
-    for (uint32_t w = tid; w < WW; w += IT) sh[w] = (w + shift < WW) ? bits[w + shift] : 0u;
-    __syncthreads();
-    for (uint32_t w = tid; w < WW; w += IT) bits[w] = sh[w];
+    for (uint32_t w = tid; w < WW; w += IT) bits[w] = (w + shift < WW) ? sh[w + shift] : 0u;
   }
   if (tid == 0) {
     s.base[e] = nb;
     s.lo[e] = nlo;
     s.hbc[e] = hbc;
     if (ack_out) ack_out[e] = nb;
-    if (e == 0 && ovf_out) *ovf_out = s.ctr[C_OVF];
+  }
+}
+// (workgroup 0 also reports the window-overflow count: every decision is made by now)
+__global__ __launch_bounds__(IT) void k_state(uint32_t n_entries, Scratch x, State s, bool reliable, int64_t* ack_out,
+                                              uint64_t* ovf_out) {
+  __shared__ uint32_t sh[WW];
+  __shared__ uint32_t s_first;
+  const uint32_t e = blockIdx.x;
+  if (e >= n_entries) return;
+  state_proxy(e, x, s, reliable, ack_out, sh, s_first);
+  if (threadIdx.x == 0 && e == 0 && ovf_out) *ovf_out = s.ctr[C_OVF];
+}
+// Global identity path, last launch: workgroups [0, ntiles) write the deliveries (k_dwrite;
+// the last one also the overflow count), the next n_entries one proxy's state each.
+__global__ __launch_bounds__(IT) void k_dstate(const uint8_t* flag, uint64_t n, const uint32_t* tcnt, uint32_t ntiles,
+                                               Scratch x, uint64_t max_out, rtps_delivery* out, uint64_t* n_out,
+                                               const uint64_t* ctr, uint64_t* ovf_out, uint32_t n_entries, State s,
+                                               bool reliable, int64_t* ack_out) {
+  __shared__ uint64_t s_w[IT / 64];
+  __shared__ uint32_t s_c[IT / 64];
+  __shared__ uint32_t sh[WW];
+  __shared__ uint32_t s_first;
+  if (blockIdx.x < ntiles) {
+    dwrite_tile(blockIdx.x, flag, n, tcnt, ntiles, x, true, max_out, out, n_out, ctr, ovf_out, nullptr, s_w, s_c);
+  } else if (blockIdx.x - ntiles < n_entries) {
+    state_proxy(blockIdx.x - ntiles, x, s, reliable, ack_out, sh, s_first);
   }
 }
 
@@ -1709,16 +1799,16 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
     fo.bk_cnt = s->bk_cnt;
     fo.bk_lst = s->bk_lst;
     hipLaunchKernelGGL((k_classify<true, true, true>), dim3((uint32_t)nblk), dim3(IT), lds, st, t, records,
-                       n_records, max, with_frag ? frag : nullptr, flags, x, S.ctr, fo, ctr_next);
+                       n_records, max, with_frag ? frag : nullptr, flags, x, S.ctr, fo, ctr_next, S, s->epoch);
   } else if (ident && fast)
     hipLaunchKernelGGL((k_classify<true, true>), dim3(gb), dim3(IT), lds, st, t, records, n_records, max,
-                       with_frag ? frag : nullptr, flags, x, S.ctr, fo, ctr_next);
-  else if (ident)
-    hipLaunchKernelGGL((k_classify<true, false>), dim3(gb), dim3(IT), lds, st, t, records, n_records, max,
-                       with_frag ? frag : nullptr, flags, x, S.ctr, fo, ctr_next);
+                       with_frag ? frag : nullptr, flags, x, S.ctr, fo, ctr_next, S, s->epoch);
+  else if (ident)  // the global path's marks ride along (harmless keys of this epoch if the batch goes per proxy)
+    hipLaunchKernelGGL((k_classify<true, false, false, true>), dim3(gb), dim3(IT), lds, st, t, records, n_records,
+                       max, with_frag ? frag : nullptr, flags, x, S.ctr, fo, ctr_next, S, s->epoch);
   else
     hipLaunchKernelGGL((k_classify<false, false>), dim3(gb), dim3(IT), lds, st, t, records, n_records, max,
-                       with_frag ? frag : nullptr, flags, x, S.ctr, fo, ctr_next);
+                       with_frag ? frag : nullptr, flags, x, S.ctr, fo, ctr_next, S, s->epoch);
   s->cpar ^= 1u;  // the next batch uses the set this classify zeroes
   if (bucket) {
     hipLaunchKernelGGL(k_proxy<true>, dim3(t.n_proxies), dim3(PT), 0, st, arena, s->pev, x.hval, t.n_proxies, S,
@@ -1825,6 +1915,31 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
     if (hipcub::DeviceScan::InclusiveScanByKey(s->tmp, tb, x.skey, x.hf, x.hpre, hipcub::Max(), (uint32_t)n_hb,
                                                hipcub::Equality(), st) != hipSuccess)
       return RTPS_RX_EHIP;
+  }
+  if (ident && !per_proxy && nev) {
+    // identity batches, global path: the marks ran in classify; decide + tile counts (+ the
+    // merge for GAP-free batches), then the deliveries and every proxy's state in one launch
+    if (n_gap) {  // the samples' bitmap for the GAP marks (the keys are set)
+      hipLaunchKernelGGL(k_marks_d, dim3(gv), dim3(IT), 0, st, nev, x, S, s->epoch, true, false);
+      hipLaunchKernelGGL(k_marks_g, dim3(gv), dim3(IT), 0, st, records, arena, dgram_off, nev, x, S, s->epoch);
+    }
+    const uint32_t ntiles = (uint32_t)((acc_cap + DT - 1) / DT);
+    const bool fc_merge = n_gap == 0 && s->path == 3;  // (the first-cover-key merge: test path)
+    if (n_gap == 0 && !fc_merge)
+      hipLaunchKernelGGL(k_decide_t<true>, dim3(ntiles), dim3(IT), 0, st, nev, acc_cap, x, S, acc, have_hb, s->epoch,
+                         x.sel);
+    else
+      hipLaunchKernelGGL(k_decide_t<false>, dim3(ntiles), dim3(IT), 0, st, nev, acc_cap, x, S, acc, have_hb, s->epoch,
+                         x.sel);
+    if (fc_merge)
+      hipLaunchKernelGGL(k_fcmerge, dim3((uint32_t)hmin((uint64_t)t.n_proxies * W / IT, 8192)), dim3(IT), 0, st,
+                         t.n_proxies, S, s->epoch);
+    else if (n_gap)
+      hipLaunchKernelGGL(k_merge, dim3(gv), dim3(IT), 0, st, records, arena, dgram_off, nev, x, S, true);
+    hipLaunchKernelGGL(k_dstate, dim3(ntiles + t.n_proxies), dim3(IT), 0, st, acc, acc_cap, x.sel, ntiles, x,
+                       out->max_accepted, out->accepted, out->n_accepted, S.ctr, out->n_window_overflow, t.n_proxies,
+                       S, have_hb, out->ack_base);
+    return hipGetLastError() == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP;
   }
   if (nev && !per_proxy) {
     hipLaunchKernelGGL(k_marks_d, dim3(gv), dim3(IT), 0, st, nev, x, S, s->epoch, n_gap > 0);

@@ -1286,10 +1286,17 @@ __global__ __launch_bounds__(SCAN_T) void rtps_parse_scan_kernel(KParams p, uint
   }
 }
 
-__global__ __launch_bounds__(TILE, RTPS_EM_WAVES_PER_SIMD) void rtps_parse_emit_kernel(KParams p, uint32_t n_tiles,
-                                                                                     const u32x4* items,
-                                                                                     const uint32_t* wcnt,
-                                                                                     const uint64_t* tprefix) {
+// W runs EMT threads per tile (the first TILE do the per-datagram prologue), so that most
+// threads take one item: a thread that loops over items waits, before each next item's
+// loads can be used, for the previous item's record stores (vmcnt counts stores too).
+#ifndef RTPS_EM_THREADS
+#define RTPS_EM_THREADS 1024
+#endif
+constexpr uint32_t EMT = RTPS_EM_THREADS;
+static_assert(EMT % TILE == 0, "the prologue threads are the first TILE");
+__global__ __launch_bounds__(EMT) __attribute__((amdgpu_waves_per_eu(RTPS_EM_WAVES_PER_SIMD)))
+void rtps_parse_emit_kernel(KParams p, uint32_t n_tiles, const u32x4* items, const uint32_t* wcnt,
+                            const uint64_t* tprefix) {
   __shared__ uint32_t s_rbase[TILE];   // tile-local first record of each datagram (NONE: no records)
   __shared__ uint32_t s_doff[TILE];    // datagram start relative to the workgroup's descriptor base
   __shared__ uint32_t s_len[TILE];
@@ -1297,13 +1304,14 @@ __global__ __launch_bounds__(TILE, RTPS_EM_WAVES_PER_SIMD) void rtps_parse_emit_
   __shared__ uint32_t s_wsum[WAVES], s_nit[WAVES + 1];
   __shared__ uint64_t s_lo[WAVES], s_hi[WAVES];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const bool pro = tid < TILE;  // a prologue thread: datagram tid of the tile
   const uint32_t tile = blockIdx.x;
   mt_stage(p);  // visible after the __syncthreads below
   Scratch x = scratch_of(p.scratch, n_tiles);
   const uint64_t prefix = tprefix[tile];
-  const uint32_t wc = wcnt[tile * WAVES + wave];
+  const uint32_t wc = pro ? wcnt[tile * WAVES + wave] : 0u;
   const uint32_t i = tile * TILE + tid;
-  const bool valid = i < p.n;
+  const bool valid = pro && i < p.n;
   const uint32_t cnt = valid ? (uint32_t)x.dcount[i] : 0u;
   const uint64_t off = (valid && cnt) ? p.dgram_off[i] : 0ull;
   const uint32_t L = (valid && cnt) ? p.dgram_len[i] : 0u;
@@ -1320,8 +1328,8 @@ __global__ __launch_bounds__(TILE, RTPS_EM_WAVES_PER_SIMD) void rtps_parse_emit_
       hi = b > hi ? b : hi;
     }
   }
-  if (lane == 63) s_wsum[wave] = incl;
-  if (lane == 0) { s_nit[wave] = (wc & WCNT_OVERFLOW) ? 0u : wc; s_lo[wave] = lo; s_hi[wave] = hi; }
+  if (pro && lane == 63) s_wsum[wave] = incl;
+  if (pro && lane == 0) { s_nit[wave] = (wc & WCNT_OVERFLOW) ? 0u : wc; s_lo[wave] = lo; s_hi[wave] = hi; }
   __syncthreads();
   uint32_t wave_off = 0;
   uint64_t tlo = ~0ull, thi = 0;
@@ -1333,7 +1341,7 @@ __global__ __launch_bounds__(TILE, RTPS_EM_WAVES_PER_SIMD) void rtps_parse_emit_
   }
   const uint64_t tb = (wide && tlo != ~0ull) ? tlo : 0ull;
   const bool tile_walk = wide && tlo != ~0ull && thi - tlo >= 0xffff0000ull;
-  const bool walk_wave = tile_walk || (wc & WCNT_OVERFLOW) != 0u;
+  const bool walk_wave = pro && (tile_walk || (wc & WCNT_OVERFLOW) != 0u);
   const uint32_t local = wave_off + incl - cnt;
   if (valid && p.rec_begin) p.rec_begin[i] = (uint32_t)(prefix + local);
   if (walk_wave) {  // the items did not fit (or cannot be addressed): walk the wave's datagrams
@@ -1350,7 +1358,7 @@ __global__ __launch_bounds__(TILE, RTPS_EM_WAVES_PER_SIMD) void rtps_parse_emit_
   Src s;
   s.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p.arena + tb), (short)0, (int)avail, 0x00020000);
   s.avail = avail;
-  if (!walk_wave) {
+  if (pro && !walk_wave) {
     s_rbase[tid] = cnt ? local : 0xffffffffu;
     s_doff[tid] = (uint32_t)(off - tb);
     s_len[tid] = L;
@@ -1360,6 +1368,7 @@ __global__ __launch_bounds__(TILE, RTPS_EM_WAVES_PER_SIMD) void rtps_parse_emit_
       s_pfx[tid * 3 + 0] = h[0]; s_pfx[tid * 3 + 1] = h[1]; s_pfx[tid * 3 + 2] = h[2];
     }
   }
+  __syncthreads();  // (every s_nit read above happened before this)
   if (tid == 0) {
     uint32_t a = 0;
 #pragma unroll
@@ -1369,7 +1378,7 @@ __global__ __launch_bounds__(TILE, RTPS_EM_WAVES_PER_SIMD) void rtps_parse_emit_
   __syncthreads();
   const uint32_t total = s_nit[WAVES];
   const u32x4* tslab = items + (size_t)tile * WAVES * CAPW;
-  for (uint32_t k = tid; k < total; k += TILE) {
+  for (uint32_t k = tid; k < total; k += EMT) {
     const uint32_t w = (k >= s_nit[1]) + (k >= s_nit[2]) + (k >= s_nit[3]);
     const u32x4 it = tslab[w * CAPW + (k - s_nit[w])];
     const uint32_t o = it[0] & 0xffffu, src_off = it[0] >> 16;
@@ -2279,7 +2288,7 @@ static int parse_launch(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len
                          c->it_wcnt);
     if (phases & 2u) {
       hipLaunchKernelGGL(rtps_parse_scan_kernel, dim3(1), dim3(SCAN_T), 0, c->stream, p, tiles, parity, c->it_prefix);
-      hipLaunchKernelGGL(rtps_parse_emit_kernel, dim3(tiles), dim3(TILE), mt_lds, c->stream, p, tiles, c->it_items,
+      hipLaunchKernelGGL(rtps_parse_emit_kernel, dim3(tiles), dim3(EMT), mt_lds, c->stream, p, tiles, c->it_items,
                          c->it_wcnt, c->it_prefix);
     }
     return hip_fail(hipGetLastError());

@@ -8,6 +8,10 @@
 #include "../../include/rtps_rx.h"
 
 constexpr uint32_t SHARD_MAX_RANKS = 64;
+// what crosses xGMI per writer record: rtps_shard_item (include/rtps_rx.h); a DATA is the item
+// alone, any other kind the item + its 64-B record + the bytes its consumers read, in the blob
+typedef rtps_shard_item shard_item;
+static_assert(sizeof(shard_item) == 32, "32-B exchange items");
 
 struct rtps_shard {
   rtps_rx_ctx* ctx = nullptr;
@@ -15,10 +19,10 @@ struct rtps_shard {
   uint32_t n_ranks = 0;
   uint64_t cap = 0, bcap = 0;  // fixed slot per peer: records, blob bytes (multiple of 16)
   // ---- send side (this rank as a source) ----
-  rtps_record* s_slots = nullptr;         // [n_ranks * cap]
+  shard_item* s_slots = nullptr;         // [n_ranks * cap]
   uint8_t* s_blob = nullptr;              // [n_ranks * bcap]
   rtps_shard_counts* s_counts = nullptr;  // [n_ranks] device
-  rtps_record* s_spill = nullptr;         // exact layout: dest d at sum_{d' < d} n_d'
+  shard_item* s_spill = nullptr;         // exact layout: dest d at sum_{d' < d} n_d'
   uint64_t s_spill_cap = 0;
   uint8_t* s_bspill = nullptr;            // exact layout: dest d at sum_{d' < d} bytes_d'
   uint64_t s_bspill_cap = 0;
@@ -26,10 +30,10 @@ struct rtps_shard {
   uint64_t* hscan = nullptr;              // [tiles * n_ranks] x {record offset, byte offset}
   uint64_t hist_tiles = 0;
   // ---- receive side (this rank as the owner) ----
-  rtps_record* r_slots = nullptr;         // [n_ranks * cap]: source s's slot at s * cap
+  shard_item* r_slots = nullptr;         // [n_ranks * cap]: source s's slot at s * cap
   uint8_t* r_blob = nullptr;              // [n_ranks * bcap]
   rtps_shard_counts* r_counts = nullptr;  // [n_ranks] device: what source s sent this rank
-  rtps_record* r_spill = nullptr;         // source s's spill at sum_{s' < s} (n - cut)
+  shard_item* r_spill = nullptr;         // source s's spill at sum_{s' < s} (n - cut)
   uint64_t r_spill_cap = 0;
   uint8_t* r_bspill = nullptr;            // source s's spilled bytes at sum_{s' < s} (bytes - cut_bytes)
   uint64_t r_bspill_cap = 0;
@@ -42,6 +46,7 @@ struct rtps_shard {
   bool exchanged = false;          // the counts were copied by rtps_rx_shard_exchange
   bool finished = false;           // rtps_rx_shard_finish ran after that exchange (the spill, if any, moved)
   // ---- the owner batch ----
+  shard_item* o_item = nullptr;  // the received items, source order
   rtps_record* o_rec = nullptr;
   uint64_t* o_off = nullptr;
   uint64_t* o_origin = nullptr;

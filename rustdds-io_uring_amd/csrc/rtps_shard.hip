@@ -8,6 +8,10 @@
 // submessage of that writer is seen, in order.  With the stream split over N
 // GPUs by datagram, that place is the writer's owner GPU.
 //
+// What crosses per writer record is a 32-B item (rtps_shard_item): a DATA's item holds
+// everything the owner's ingest reads of it (writer GUID, SN, kind, flags, route,
+// payload kind), so a DATA costs 32 B instead of its 64-B record; any other kind
+// sends its 64-B record in its blob, ahead of the bytes its consumers read.
 // Pack (source rank), three launches over the parse output:
 //   1. shard_hist    per 256-record tile and destination: items and blob bytes;
 //   2. shard_scan    per destination, exclusive scans of both over the tiles
@@ -21,12 +25,14 @@
 //                    DATA_FRAG payloads by whole waves (16 B per lane).
 // Unpack (owner), with the counts on the host:
 //   1. shard_segments one flat copy of the received slots and spills into the
-//                    owner's contiguous records and arena (≤ 4 segments / source);
-//   2. shard_fix      per record: origin, blob size, dgram_idx := record index;
+//                    owner's contiguous items and arena (≤ 4 segments / source);
+//   2. shard_fix      per item: origin, blob size;
 //   3. exclusive sum of the blob sizes (hipCUB) = each blob's arena offset;
-//   4. shard_offsets  dgram_off = LEAD + blob offset - the blob's offset in its
-//                    datagram, so the consumers' arena + dgram_off[dgram_idx] +
-//                    pl_off / bitmap_off lands on the blob.
+//   4. shard_expand   the owner's 64-B records: a DATA's from its item, any other
+//                    from the copy in its blob; dgram_idx := record index; dgram_off =
+//                    LEAD + blob offset + 64 - the bytes' offset in their datagram, so
+//                    the consumers' arena + dgram_off[dgram_idx] + pl_off / bitmap_off
+//                    lands on them.
 // Blob streams are concatenated in source order, the same order as the
 // records, so one global scan gives every blob's place.
 #include <hip/hip_runtime.h>
@@ -69,6 +75,10 @@ __device__ __forceinline__ Blob blob_of(const uint32_t* w) {  // w: the record's
   return Blob{0u, 0u};
 }
 __device__ __forceinline__ uint32_t round16(uint32_t x) { return (x + 15u) & ~15u; }
+// blob bytes of an item: none for a DATA, else its record + its consumers' bytes
+__device__ __forceinline__ uint32_t item_bytes(uint32_t kind, const Blob& b) {
+  return kind == RTPS_DATA ? 0u : 64u + round16(b.len);
+}
 
 // Destination of a record (NONE: not an item) and its blob
 __device__ __forceinline__ uint32_t item_of(const uint32_t* w, uint32_t n_dest, Blob& b) {
@@ -146,7 +156,8 @@ __global__ __launch_bounds__(ST) void shard_hist(const rtps_record* recs, const 
     const uint32_t o = item_of(w, n_dest, b);
     if (o != NONE) {
       atomicAdd(&h[2 * o], 1u);
-      if (b.len) atomicAdd(&h[2 * o + 1], round16(b.len));
+      const uint32_t ib = item_bytes((w[1] >> 16) & 0xffu, b);
+      if (ib) atomicAdd(&h[2 * o + 1], ib);
     }
   }
   __syncthreads();
@@ -192,9 +203,9 @@ struct PackArgs {
   uint64_t cap, bcap;
   const uint64_t* hscan;
   rtps_shard_counts* counts;
-  rtps_record* slots;
+  shard_item* slots;
   uint8_t* blob;
-  rtps_record* spill;
+  shard_item* spill;
   uint8_t* bspill;
 };
 
@@ -221,7 +232,8 @@ __global__ __launch_bounds__(ST) void shard_scatter(PackArgs a) {
     load_record(a.recs + i, w);
     o = item_of(w, n, b);
   }
-  const uint32_t size = round16(b.len);
+  const uint32_t kind = o != NONE ? (w[1] >> 16) & 0xffu : 0u;
+  const uint32_t size = o != NONE ? item_bytes(kind, b) : 0u;
   uint32_t rank = 0, bex = 0;
   const uint64_t lt = lane ? (~0ull >> (64u - lane)) : 0ull;
   for (uint32_t d = 0; d < n; ++d) {
@@ -241,22 +253,34 @@ __global__ __launch_bounds__(ST) void shard_scatter(PackArgs a) {
     uint64_t boff = a.hscan[2 * ((uint64_t)blockIdx.x * n + o) + 1] + bex;
     for (uint32_t v = 0; v < wave; ++v) { pos += wcnt[v][o]; boff += wbyt[v][o]; }
     const bool slot = pos < a.cap && boff + size <= a.bcap;
-    rtps_record* rd = slot ? a.slots + (uint64_t)o * a.cap + pos : a.spill + sbase[o] + pos;
+    shard_item* it = slot ? a.slots + (uint64_t)o * a.cap + pos : a.spill + sbase[o] + pos;
     uint8_t* bd = slot ? a.blob + (uint64_t)o * a.bcap + boff : a.bspill + bsbase[o] + boff;
     if (!slot) {
       atomicMin((unsigned long long*)&a.counts[o].cut, (unsigned long long)pos);
       atomicMin((unsigned long long*)&a.counts[o].cut_bytes, (unsigned long long)boff);
     }
-    store_record(rd, w);
-    if (b.len) {
-      const uint8_t* src = a.arena + a.dgram_off[w[0]] + b.rel;
-      if (size <= SMALL_BLOB) {
-        for (uint32_t c = 0; c < size; c += 16u) copy_chunk(src, bd, c, b.len);
-      } else {
-        const uint32_t k = atomicAdd(&n_big, 1u);
-        big_src[k] = (uint64_t)(uintptr_t)src;
-        big_dst[k] = (uint64_t)(uintptr_t)bd;
-        big_len[k] = b.len;
+    const uint32_t tail = kind | (w[1] & 0xff000000u) >> 16 | (w[7] & 0xffff0000u);  // kind, flags, route, pk
+    uint4* q = reinterpret_cast<uint4*>(it);
+    if (kind == RTPS_DATA) {
+      q[0] = make_uint4(w[2], w[3], w[4], w[5]);  // writer GUID
+      q[1] = make_uint4(w[8], w[9], tail, (uint32_t)i);
+    } else {
+      q[0] = make_uint4(size, 0u, 0u, 0u);
+      q[1] = make_uint4(0u, 0u, tail, (uint32_t)i);
+      const uint32_t didx = w[0];
+      w[0] = (uint32_t)i;  // the record's copy names its source record
+      store_record(reinterpret_cast<rtps_record*>(bd), w);
+      bd += 64;
+      if (b.len) {
+        const uint8_t* src = a.arena + a.dgram_off[didx] + b.rel;
+        if (round16(b.len) <= SMALL_BLOB) {
+          for (uint32_t c = 0; c < round16(b.len); c += 16u) copy_chunk(src, bd, c, b.len);
+        } else {
+          const uint32_t k = atomicAdd(&n_big, 1u);
+          big_src[k] = (uint64_t)(uintptr_t)src;
+          big_dst[k] = (uint64_t)(uintptr_t)bd;
+          big_len[k] = b.len;
+        }
       }
     }
   }
@@ -278,11 +302,11 @@ struct SegArgs {
   const rtps_shard_counts* counts;  // [n_src] received counts (device)
   uint32_t n_src;
   uint64_t cap, bcap;
-  const rtps_record* r_slots;
+  const shard_item* r_slots;
   const uint8_t* r_blob;
-  const rtps_record* r_spill;
+  const shard_item* r_spill;
   const uint8_t* r_bspill;
-  rtps_record* o_rec;
+  shard_item* o_item;
   uint8_t* o_blob;  // owner arena + RTPS_SHARD_LEAD
 };
 // Per source: its slot records, its spilled records, its slot blob bytes, its spilled
@@ -302,8 +326,8 @@ __global__ __launch_bounds__(ST) void shard_segments(SegArgs a) {
     };
     for (uint32_t k = 0; k < a.n_src; ++k) {
       const rtps_shard_counts c = a.counts[k];
-      add(a.r_slots + (uint64_t)k * a.cap, a.o_rec + rpos, c.cut * sizeof(rtps_record));
-      add(a.r_spill + rsp, a.o_rec + rpos + c.cut, (c.n - c.cut) * sizeof(rtps_record));
+      add(a.r_slots + (uint64_t)k * a.cap, a.o_item + rpos, c.cut * sizeof(shard_item));
+      add(a.r_spill + rsp, a.o_item + rpos + c.cut, (c.n - c.cut) * sizeof(shard_item));
       add(a.r_blob + (uint64_t)k * a.bcap, a.o_blob + bpos, c.cut_bytes);
       add(a.r_bspill + bsp, a.o_blob + bpos + c.cut_bytes, c.bytes - c.cut_bytes);
       rpos += c.n;
@@ -331,7 +355,7 @@ __global__ __launch_bounds__(ST) void shard_segments(SegArgs a) {
 }
 
 struct FixArgs {
-  rtps_record* rec;
+  const shard_item* item;
   uint64_t* origin;
   uint64_t* size;
   uint64_t n;
@@ -343,27 +367,33 @@ __global__ __launch_bounds__(ST) void shard_fix(FixArgs a) {
   if (j >= a.n) return;
   uint32_t s = 0;
   while (s + 1 < a.n_src && a.first[s + 1] <= j) ++s;
-  uint32_t* w = reinterpret_cast<uint32_t*>(a.rec + j);
-  const uint4 q2 = reinterpret_cast<const uint4*>(a.rec + j)[2];
-  uint32_t w16[16];
-  w16[0] = w[0]; w16[1] = w[1];
-  w16[10] = q2.z; w16[11] = q2.w;
-  const uint4 q3 = reinterpret_cast<const uint4*>(a.rec + j)[3];
-  w16[12] = q3.x; w16[13] = q3.y;
-  const Blob b = blob_of(w16);
-  a.origin[j] = ((uint64_t)s << 32) | w16[0];
-  a.size[j] = round16(b.len);
-  w[0] = (uint32_t)j;
+  const uint4* q = reinterpret_cast<const uint4*>(a.item + j);
+  const uint4 q0 = q[0], q1 = q[1];
+  a.origin[j] = ((uint64_t)s << 32) | q1.w;                 // src_rec
+  a.size[j] = (q1.z & 0xffu) == RTPS_DATA ? 0u : q0.x;  // the blob bytes (record + consumers' bytes)
 }
-__global__ __launch_bounds__(ST) void shard_offsets(const rtps_record* rec, const uint64_t* boff, uint64_t* off,
-                                                    uint64_t n) {
+// the owner's records: a DATA's from its item, the others' from the copy in their blob
+__global__ __launch_bounds__(ST) void shard_expand(const shard_item* item, const uint8_t* arena, const uint64_t* boff,
+                                                   rtps_record* rec, uint64_t* off, uint64_t n) {
   const uint64_t j = (uint64_t)blockIdx.x * ST + threadIdx.x;
   if (j >= n) return;
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(rec + j);
-  uint32_t w16[16];
-  w16[1] = w[1]; w16[10] = w[10]; w16[12] = w[12]; w16[13] = w[13];
-  const Blob b = blob_of(w16);
-  off[j] = RTPS_SHARD_LEAD + boff[j] - b.rel;
+  const uint4* q = reinterpret_cast<const uint4*>(item + j);
+  const uint4 q0 = q[0], q1 = q[1];
+  const uint32_t kind = q1.z & 0xffu;
+  uint32_t w[16];
+  if (kind == RTPS_DATA) {
+    for (int k = 0; k < 16; ++k) w[k] = 0u;
+    w[1] = (kind << 16) | ((q1.z >> 8) & 0xffu) << 24;  // sub_off 0, kind, flags
+    w[2] = q0.x; w[3] = q0.y; w[4] = q0.z; w[5] = q0.w;  // writer GUID
+    w[7] = q1.z & 0xffff0000u;                           // route, payload_kind
+    w[8] = q1.x; w[9] = q1.y;                            // sn
+    off[j] = RTPS_SHARD_LEAD;                            // (no bytes in the owner arena)
+  } else {
+    load_record(reinterpret_cast<const rtps_record*>(arena + RTPS_SHARD_LEAD + boff[j]), w);
+    off[j] = RTPS_SHARD_LEAD + boff[j] + 64u - blob_of(w).rel;
+  }
+  w[0] = (uint32_t)j;
+  store_record(rec + j, w);
 }
 
 __global__ void shard_set_n(uint64_t* p, uint64_t v) { *p = v; }
@@ -397,7 +427,7 @@ int rtps_rx_shard_create(rtps_rx_ctx* ctx, uint32_t n_ranks, uint64_t cap, uint6
   s->cap = cap;
   s->bcap = bcap;
   (void)hipSetDevice(s->device);
-  const size_t slots = (size_t)n_ranks * cap * sizeof(rtps_record), blobs = (size_t)n_ranks * bcap;
+  const size_t slots = (size_t)n_ranks * cap * sizeof(shard_item), blobs = (size_t)n_ranks * bcap;
   bool ok = hipMalloc(&s->s_slots, slots) == hipSuccess && hipMalloc(&s->r_slots, slots) == hipSuccess &&
             hipMalloc(&s->s_blob, blobs ? blobs : 16) == hipSuccess &&
             hipMalloc(&s->r_blob, blobs ? blobs : 16) == hipSuccess &&
@@ -426,7 +456,7 @@ int rtps_rx_shard_destroy(rtps_shard* s) {
   (void)hipDeviceSynchronize();
   void* dev[] = {s->s_slots, s->s_blob, s->s_counts, s->s_spill, s->s_bspill, s->hist, s->hscan, s->r_slots,
                  s->r_blob, s->r_counts, s->r_spill, s->r_bspill, s->o_rec, s->o_off, s->o_origin, s->o_size,
-                 s->o_boff, s->o_arena, s->o_n, s->cub_tmp};
+                 s->o_boff, s->o_arena, s->o_n, s->cub_tmp, s->o_item};
   for (void* p : dev)
     if (p) (void)hipFree(p);
   if (s->h_send) (void)hipHostFree(s->h_send);
@@ -456,14 +486,14 @@ int rtps_rx_shard_pack(rtps_shard* s, const uint8_t* arena, uint64_t arena_len, 
       return RTPS_RX_ENOMEM;
     s->hist_tiles = tiles;
   }
-  // the spill holds every item in the worst case: all records, and blobs that are
-  // disjoint byte ranges of the arena plus < 16 B of rounding each
-  const uint64_t need_rec = max_records * sizeof(rtps_record), need_b = arena_len + 16ull * max_records;
-  if (need_rec > s->s_spill_cap * sizeof(rtps_record) || need_b > s->s_bspill_cap) {
+  // the spill holds every item in the worst case: all records, and blobs that are a
+  // record copy plus disjoint byte ranges of the arena plus < 16 B of rounding each
+  const uint64_t need_rec = max_records * sizeof(shard_item), need_b = arena_len + 80ull * max_records;
+  if (need_rec > s->s_spill_cap * sizeof(shard_item) || need_b > s->s_bspill_cap) {
     if (hipStreamSynchronize(st) != hipSuccess) return RTPS_RX_EHIP;
-    uint64_t cap_bytes = s->s_spill_cap * sizeof(rtps_record);
+    uint64_t cap_bytes = s->s_spill_cap * sizeof(shard_item);
     if (!shard_reserve((void**)&s->s_spill, &cap_bytes, need_rec)) return RTPS_RX_ENOMEM;
-    s->s_spill_cap = cap_bytes / sizeof(rtps_record);
+    s->s_spill_cap = cap_bytes / sizeof(shard_item);
     if (!shard_reserve((void**)&s->s_bspill, &s->s_bspill_cap, need_b)) return RTPS_RX_ENOMEM;
   }
   if (tiles == 0) {
@@ -497,10 +527,10 @@ int rtps_rx_shard_reserve_spill(rtps_shard* s, uint64_t records, uint64_t bytes)
   (void)hipSetDevice(s->device);
   if (records > s->r_spill_cap || bytes > s->r_bspill_cap) {
     if (hipDeviceSynchronize() != hipSuccess) return RTPS_RX_EHIP;  // an unpack may still read the old ones
-    uint64_t cap_bytes = s->r_spill_cap * sizeof(rtps_record);
+    uint64_t cap_bytes = s->r_spill_cap * sizeof(shard_item);
     if (records > s->r_spill_cap) {
-      if (!shard_reserve((void**)&s->r_spill, &cap_bytes, records * sizeof(rtps_record))) return RTPS_RX_ENOMEM;
-      s->r_spill_cap = cap_bytes / sizeof(rtps_record);
+      if (!shard_reserve((void**)&s->r_spill, &cap_bytes, records * sizeof(shard_item))) return RTPS_RX_ENOMEM;
+      s->r_spill_cap = cap_bytes / sizeof(shard_item);
     }
     if (bytes > s->r_bspill_cap && !shard_reserve((void**)&s->r_bspill, &s->r_bspill_cap, bytes))
       return RTPS_RX_ENOMEM;
@@ -542,16 +572,16 @@ int rtps_rx_shard_unpack(rtps_shard* s, rtps_owner_batch* out) {
   // (otherwise they may still hold an earlier batch's)
   if (s->exchanged && !s->finished && (sp || bsp)) return RTPS_RX_EINVAL;
   if (total > s->o_cap) {
-    uint64_t c[5] = {0, 0, 0, 0, 0};
-    void** p[5] = {(void**)&s->o_rec, (void**)&s->o_off, (void**)&s->o_origin, (void**)&s->o_size,
-                   (void**)&s->o_boff};
-    const size_t b[5] = {sizeof(rtps_record), 8, 8, 8, 8};
-    for (int k = 0; k < 5; ++k) {
+    uint64_t c[6] = {0, 0, 0, 0, 0, 0};
+    void** p[6] = {(void**)&s->o_rec, (void**)&s->o_off, (void**)&s->o_origin, (void**)&s->o_size,
+                   (void**)&s->o_boff, (void**)&s->o_item};
+    const size_t b[6] = {sizeof(rtps_record), 8, 8, 8, 8, sizeof(shard_item)};
+    for (int k = 0; k < 6; ++k) {
       (void)hipFree(*p[k]);
       *p[k] = nullptr;
     }
     s->o_cap = 0;
-    for (int k = 0; k < 5; ++k)
+    for (int k = 0; k < 6; ++k)
       if (!shard_reserve(p[k], &c[k], total * b[k])) return RTPS_RX_ENOMEM;
     s->o_cap = total;
   }
@@ -562,15 +592,15 @@ int rtps_rx_shard_unpack(rtps_shard* s, rtps_owner_batch* out) {
       return RTPS_RX_ENOMEM;
   }
   {
-    SegArgs sa{s->r_counts, n, s->cap, s->bcap, s->r_slots, s->r_blob, s->r_spill, s->r_bspill, s->o_rec,
+    SegArgs sa{s->r_counts, n, s->cap, s->bcap, s->r_slots, s->r_blob, s->r_spill, s->r_bspill, s->o_item,
                s->o_arena + RTPS_SHARD_LEAD};
-    const uint64_t chunks = (total * sizeof(rtps_record) + bytes) / 16;
+    const uint64_t chunks = (total * sizeof(shard_item) + bytes) / 16;
     const uint64_t blocks = (chunks + ST - 1) / ST;
     if (chunks)
       hipLaunchKernelGGL(shard_segments, dim3((uint32_t)(blocks < 16384 ? blocks : 16384)), dim3(ST), 0, st, sa);
   }
   if (total) {
-    fa.rec = s->o_rec; fa.origin = s->o_origin; fa.size = s->o_size; fa.n = total; fa.n_src = n;
+    fa.item = s->o_item; fa.origin = s->o_origin; fa.size = s->o_size; fa.n = total; fa.n_src = n;
     const uint32_t g = (uint32_t)((total + ST - 1) / ST);
     hipLaunchKernelGGL(shard_fix, dim3(g), dim3(ST), 0, st, fa);
     size_t tb = 0;
@@ -583,7 +613,8 @@ int rtps_rx_shard_unpack(rtps_shard* s, rtps_owner_batch* out) {
     }
     if (hipcub::DeviceScan::ExclusiveSum(s->cub_tmp, tb, s->o_size, s->o_boff, (int64_t)total, st) != hipSuccess)
       return RTPS_RX_EHIP;
-    hipLaunchKernelGGL(shard_offsets, dim3(g), dim3(ST), 0, st, s->o_rec, s->o_boff, s->o_off, total);
+    hipLaunchKernelGGL(shard_expand, dim3(g), dim3(ST), 0, st, s->o_item, s->o_arena, s->o_boff, s->o_rec, s->o_off,
+                       total);
   }
   hipLaunchKernelGGL(shard_set_n, dim3(1), dim3(1), 0, st, s->o_n, total);
   if (hipGetLastError() != hipSuccess) return RTPS_RX_EHIP;

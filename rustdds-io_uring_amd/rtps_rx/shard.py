@@ -87,6 +87,7 @@ def rccl_comm(rx, dist, device):
         _COMMS[key] = comm
     return _COMMS[key]
 ITEM_BYTES = {"records": 64, "descriptors": 16}
+ITEM_BYTES_OWNER = 32  # rtps_shard_item: what the owner-side exchange moves per writer record
 
 
 def owner_hash_words(words):
@@ -293,7 +294,7 @@ class OwnerBatch:
         return dev_to_numpy(self.outs["records"].ptr, 64 * self.n_records, RECORD_DTYPE)
 
     def origin(self):
-        """(source rank u32[n], source dgram_idx u32[n])."""
+        """(source rank u32[n], the record's index in the source rank's parse output u32[n])."""
         o = dev_to_numpy(self.origin_ptr, 8 * self.n_records, _np.uint64)
         return (o >> _np.uint64(32)).astype(_np.uint32), (o & _np.uint64(0xFFFFFFFF)).astype(_np.uint32)
 
@@ -425,7 +426,8 @@ class OwnerShard:
         rc = _np.zeros(w, dtype=SHARD_COUNTS_DTYPE)
         self._a2a(sc.view(_np.uint8), rc.view(_np.uint8))
         dev_copy(b.recv_counts, rc.ctypes.data, rc.nbytes)
-        for sp, rp, nb in ((b.send_slots, b.recv_slots, self.cap * 64), (b.send_blob, b.recv_blob, self.bcap)):
+        for sp, rp, nb in ((b.send_slots, b.recv_slots, self.cap * ITEM_BYTES_OWNER), (b.send_blob, b.recv_blob,
+                                                                                        self.bcap)):
             if nb:
                 s_host = dev_to_numpy(sp, w * nb)
                 r_host = _np.empty(w * nb, dtype=_np.uint8)
@@ -444,8 +446,8 @@ class OwnerShard:
             from . import _check
             _check(shard_lib().rtps_rx_shard_reserve_spill(self._h, rn, rbn))
             b = self.buffers()
-            for key, sp, rp, unit in (("rec", b.send_spill, b.recv_spill, 64), ("bytes", b.send_blob_spill,
-                                                                                  b.recv_blob_spill, 1)):
+            for key, sp, rp, unit in (("rec", b.send_spill, b.recv_spill, ITEM_BYTES_OWNER),
+                                      ("bytes", b.send_blob_spill, b.recv_blob_spill, 1)):
                 sends = [dev_to_numpy(sp + p[f"send_{key}"][0] * unit, p[f"send_{key}"][1] * unit) for p in plan]
                 recv = _np.empty(sum(p[f"recv_{key}"][1] for p in plan) * unit, dtype=_np.uint8)
                 self._a2a(_np.concatenate(sends) if sends else _np.zeros(0, _np.uint8), recv,

@@ -5,8 +5,10 @@ itself), checked on the device without host copies of the 2-GB record arrays:
   * owner-side exchange: rtps_rx_shard_pack -> rtps_rx_shard_exchange / _finish
     (library RCCL rounds) -> rtps_rx_shard_unpack, slots sized from the batch: no
     spill, and the owner batch holds every writer-kind PASS record in order
-    (all 64 bytes but dgram_idx, which becomes the record index; origin = the
-    original dgram_idx), with every GAP bitmap at arena + dgram_off + bitmap_off;
+    (all 64 bytes but dgram_idx, which becomes the record index, for the kinds that
+    cross whole; kind, flags, writer GUID, route, payload kind and SN of a DATA, which
+    crosses as its 32-B item; origin = the record's index in the parse output), with
+    every GAP bitmap at arena + dgram_off + bitmap_off;
   * record exchange: rtps_rx_bucket_by_writer_padded -> rtps_rx_exchange: no
     overflow, received == bucketed.
 Launch: python -m torch.distributed.run --nproc-per-node 1 --master-addr 127.0.0.1 scripts/c5_full_check.py"""
@@ -57,7 +59,8 @@ n_items = int(items.sum().item())
 gap = items & (kind == 0x08)
 nb = recs[:, 48:52].contiguous().view(torch.int32).reshape(-1).to(torch.int64)
 gap_bytes = torch.where(gap & (nb > 0), ((4 * ((nb + 31) // 32)) + 15) // 16 * 16, torch.zeros_like(nb))
-blob_total = int(gap_bytes.sum().item())
+# blob bytes: every item that is not a DATA sends its 64-B record (C3 has no DATA_FRAG)
+blob_total = int(gap_bytes.sum().item()) + 64 * int((items & (kind != 0x15)).sum().item())
 ok = True
 
 # ---- owner-side exchange, one rank, slots sized to the batch ----
@@ -73,11 +76,15 @@ dev_copy(got.data_ptr(), ob.outs["records"].ptr, 64 * ob.n_records)
 exp = recs[items]
 idx_ok = torch.equal(got[:, 0:4].contiguous().view(torch.int32).reshape(-1),
                      torch.arange(ob.n_records, dtype=torch.int32, device=dev))
-body_ok = torch.equal(got[:, 4:], exp[:, 4:])
+# a DATA crosses as its item: kind, flags, writer GUID, route, payload kind, sn (the rest zero)
+is_data = exp[:, 6] == 0x15
+keep = torch.zeros(64, dtype=torch.bool, device=dev)
+keep[[6, 7] + list(range(8, 24)) + [30, 31] + list(range(32, 40))] = True
+exp_d = torch.where(is_data[:, None] & ~keep[None, :], torch.zeros_like(exp), exp)
+body_ok = torch.equal(got[:, 4:], exp_d[:, 4:])
 origin = torch.empty(ob.n_records, dtype=torch.int64, device=dev)
 dev_copy(origin.data_ptr(), ob.origin_ptr, 8 * ob.n_records)
-org_ok = torch.equal((origin & 0xFFFFFFFF).to(torch.int32), exp[:, 0:4].contiguous().view(torch.int32).reshape(-1)) \
-    and int((origin >> 32).max().item()) == 0
+org_ok = torch.equal(origin & 0xFFFFFFFF, torch.nonzero(items).reshape(-1)) and int((origin >> 32).max().item()) == 0
 # every GAP bitmap word where the owner's consumers read it
 goff = torch.empty(ob.n_records, dtype=torch.int64, device=dev)
 dev_copy(goff.data_ptr(), ob.off.ptr, 8 * ob.n_records)
@@ -90,10 +97,10 @@ src = off_t[exp[gi, 0:4].contiguous().view(torch.int32).reshape(-1).to(torch.int
 dst = goff[gi] + bmo
 bm_ok = torch.equal(arena[src], oarena[dst]) and torch.equal(arena[src + 3], oarena[dst + 3])
 if not body_ok:
-    bad = torch.nonzero((got[:, 4:] != exp[:, 4:]).any(dim=1)).reshape(-1)
+    bad = torch.nonzero((got[:, 4:] != exp_d[:, 4:]).any(dim=1)).reshape(-1)
     i = int(bad[0].item())
     print(f"  {len(bad)} rows differ, first {i}: got {got[i].cpu().numpy().tobytes().hex()} "
-          f"exp {exp[i].cpu().numpy().tobytes().hex()}", flush=True)
+          f"exp {exp_d[i].cpu().numpy().tobytes().hex()}", flush=True)
 ok &= ob.n_records == n_items and spill == 0 and idx_ok and body_ok and org_ok and bm_ok
 print(f"owner exchange (library RCCL rounds): {n_items} items, {blob_total} blob bytes, spill {spill}, "
       f"records {'ok' if body_ok and idx_ok else 'BAD'}, origin {'ok' if org_ok else 'BAD'}, "

@@ -83,7 +83,7 @@ na = int(iouts["n_accepted"].item())
 dels = iouts["accepted"][:na].cpu().numpy().reshape(-1).view(DELIVERY_DTYPE)
 ack = iouts["ack_base"][:len(tbl)].cpu().numpy()
 orecs = ob.records()
-orank, odidx = ob.origin()
+orank, osrc = ob.origin()
 spilled = int(sum(int(c["n"] - c["cut"]) for c in sh.counts("recv")))
 
 # ---- the single-rank oracle over the whole stream, restricted to this rank's writers ----
@@ -91,9 +91,9 @@ _, recs, _, _ = oracle.parse(wa, wo, wlen, match_table=tbl, threads=8)
 samples = oracle.FragAssembler().batch_readers(wa, wo, recs, tbl)[0]
 _, odels, oack = oracle.HistoryIngest(tbl).batch(wa, wo, recs, samples)
 mine = np.array([owner_hash_words(r.view(np.uint32)[2:6]) % world == rank for r in recs.view(np.uint8).reshape(-1, 64)])
-index = {(int(r["dgram_idx"]), int(r["sub_off"])): i for i, r in enumerate(recs)}
-got = [(index[(int(orank[j]) * n + int(odidx[j]), int(orecs[j]["sub_off"]))], int(d["reader_slot"]))
-       for d in dels for j in [int(d["rec_idx"])]]
+# origin names (source rank, record index in that rank's parse); rank r parsed datagrams [r n, (r+1) n)
+first_rec = np.searchsorted(recs["dgram_idx"], np.arange(world) * n)
+got = [(int(first_rec[int(orank[j])]) + int(osrc[j]), int(d["reader_slot"])) for d in dels for j in [int(d["rec_idx"])]]
 exp = [(int(d["rec_idx"]), int(d["reader_slot"])) for d in odels if mine[int(d["rec_idx"])]]
 owned_proxy = np.array([owner_hash_words(np.frombuffer(bytes(t["writer_guid"]), np.uint32)) % world == rank
                         for t in tbl])

@@ -87,20 +87,42 @@ def shard_items(recs, world):
     return np.where(writer, o, -1)
 
 
+ITEM_DTYPE = np.dtype([("w", "<u4", (4,)), ("sn", "<i8"), ("kind", "u1"), ("flags", "u1"), ("route", "u1"),
+                       ("payload_kind", "u1"), ("src_rec", "<u4")])
+assert ITEM_DTYPE.itemsize == 32
+
+
+def _item_and_blob(arena, offs, r, i):
+    """(rtps_shard_item, blob bytes) of record r (index i of the source's parse output): a DATA is
+    its item alone; any other kind sends its record (dgram_idx := i) and its consumers' bytes."""
+    from rtps_rx.records import DATA
+    it = np.zeros(1, dtype=ITEM_DTYPE)[0]
+    it["kind"], it["flags"], it["route"], it["payload_kind"] = r["kind"], r["flags"], r["route"], r["payload_kind"]
+    it["src_rec"] = i
+    if int(r["kind"]) == DATA:
+        it["w"] = np.frombuffer(bytes(r["prefix"]) + bytes(r["writer_id"]), dtype="<u4")
+        it["sn"] = r["sn"]
+        return it, np.zeros(0, np.uint8)
+    rel, ln = _blob(r)
+    rc = r.copy()
+    rc["dgram_idx"] = i
+    b = np.zeros(64 + _r16(ln), dtype=np.uint8)
+    b[:64] = np.frombuffer(rc.tobytes(), dtype=np.uint8)
+    src = int(offs[int(r["dgram_idx"])]) + rel
+    b[64:64 + ln] = arena[src:src + ln]
+    it["w"][0] = len(b)
+    return it, b
+
+
 def shard_pack_np(arena, offs, recs, world, cap, bcap):
-    """Per destination d: dict(counts, slot_recs, slot_blob (bcap bytes), spill_recs, spill_blob)."""
+    """Per destination d: dict(counts, slot_items, slot_blob (bcap bytes), spill_items, spill_blob)."""
     o = shard_items(recs, world)
     out = []
     for d in range(world):
         idx = np.nonzero(o == d)[0]
-        items = recs[idx]
-        blobs = []
-        for r in items:
-            rel, ln = _blob(r)
-            b = np.zeros(_r16(ln), dtype=np.uint8)
-            src = int(offs[int(r["dgram_idx"])]) + rel
-            b[:ln] = arena[src:src + ln]
-            blobs.append(b)
+        pairs = [_item_and_blob(arena, offs, recs[i], int(i)) for i in idx]
+        items = np.array([p[0] for p in pairs], dtype=ITEM_DTYPE) if pairs else np.zeros(0, ITEM_DTYPE)
+        blobs = [p[1] for p in pairs]
         sizes = np.array([len(b) for b in blobs], dtype=np.int64)
         boff = np.concatenate([[0], np.cumsum(sizes)[:-1]]) if len(sizes) else np.zeros(0, np.int64)
         fits = (np.arange(len(items)) < cap) & (boff + sizes <= bcap)
@@ -110,30 +132,41 @@ def shard_pack_np(arena, offs, recs, world, cap, bcap):
         stream = np.concatenate(blobs) if blobs else np.zeros(0, np.uint8)
         c = np.zeros(1, dtype=COUNTS_DTYPE)
         c[0] = (len(items), int(sizes.sum()), cut, cut_bytes)
-        out.append({"counts": c, "slot_recs": items[:cut], "slot_blob": stream[:cut_bytes],
-                    "spill_recs": items[cut:], "spill_blob": stream[cut_bytes:]})
+        out.append({"counts": c, "slot_items": items[:cut], "slot_blob": stream[:cut_bytes],
+                    "spill_items": items[cut:], "spill_blob": stream[cut_bytes:]})
     return out
 
 
 def shard_unpack_np(received):
     """received: per source s (rank order) the dict shard_pack_np made for this owner.
-    -> (records with dgram_idx = i, dgram_off u64, arena u8, origin (rank u32, dgram_idx u32))."""
-    rank, didx = [], []
-    recs = [np.concatenate([x["slot_recs"], x["spill_recs"]]) for x in received]
-    for s, r in enumerate(recs):
-        rank.append(np.full(len(r), s, dtype=np.uint32))
-        didx.append(r["dgram_idx"].astype(np.uint32))
-    allr = np.concatenate(recs) if recs else np.zeros(0, dtype=received[0]["slot_recs"].dtype)
+    -> (records with dgram_idx = i, dgram_off u64, arena u8, origin (rank u32, source record u32))."""
+    from rtps_rx.records import RECORD_DTYPE, DATA
+    rank, src = [], []
+    items = [np.concatenate([x["slot_items"], x["spill_items"]]) for x in received]
+    for s, it in enumerate(items):
+        rank.append(np.full(len(it), s, dtype=np.uint32))
+        src.append(it["src_rec"].astype(np.uint32))
+    allit = np.concatenate(items) if items else np.zeros(0, dtype=ITEM_DTYPE)
     blobs = np.concatenate([np.zeros(LEAD, np.uint8)] + [np.concatenate([x["slot_blob"], x["spill_blob"]])
                                                           for x in received])
-    out = allr.copy()
+    out = np.zeros(len(allit), dtype=RECORD_DTYPE)
     off = np.zeros(len(out), dtype=np.uint64)
     pos = LEAD
-    for i, r in enumerate(out):
-        rel, ln = _blob(r)
-        off[i] = pos - rel
-        pos += _r16(ln)
+    for i, it in enumerate(allit):
+        if int(it["kind"]) == DATA:
+            g = it["w"].astype("<u4").tobytes()
+            out[i]["kind"], out[i]["flags"] = it["kind"], it["flags"]
+            out[i]["prefix"] = np.frombuffer(g[:12], np.uint8)
+            out[i]["writer_id"] = np.frombuffer(g[12:], np.uint8)
+            out[i]["route"], out[i]["payload_kind"] = it["route"], it["payload_kind"]
+            out[i]["sn"] = it["sn"]
+            off[i] = LEAD
+        else:
+            out[i] = np.frombuffer(blobs[pos:pos + 64].tobytes(), dtype=RECORD_DTYPE)[0]
+            rel, _ = _blob(out[i])
+            off[i] = pos + 64 - rel
+            pos += int(it["w"][0])
         out[i]["dgram_idx"] = i
     assert pos == len(blobs)
     return out, off, blobs, (np.concatenate(rank) if rank else np.zeros(0, np.uint32),
-                             np.concatenate(didx) if didx else np.zeros(0, np.uint32))
+                             np.concatenate(src) if src else np.zeros(0, np.uint32))

@@ -1,8 +1,9 @@
 """GPU checks of the owner-side exchange (rtps_rx_shard_*):
 
   * the device pack (shard_hist / shard_scan / shard_scatter) against the numpy
-    model (tests/shard_ref.py): counts, cut, every slot and spill record, every
-    blob byte, for 1 / 2 / 3 / 8 destinations, slots large and small;
+    model (tests/shard_ref.py): counts, cut, every slot and spill item (32-B
+    rtps_shard_item), every blob byte (the records of non-DATA kinds and their
+    consumers' bytes), for 1 / 2 / 3 / 8 destinations, slots large and small;
   * the device unpack against the model, with the receive buffers filled as W
     sources would fill them;
   * one rank end to end (pack -> host-driven exchange -> unpack -> reassembly +
@@ -22,7 +23,7 @@ import pytest
 
 import oracle
 from rtps_rx.records import RECORD_DTYPE, DELIVERY_DTYPE, pack_match_table, WRITER_KINDS, max_records
-from shard_ref import COUNTS_DTYPE, shard_pack_np, shard_unpack_np
+from shard_ref import COUNTS_DTYPE, ITEM_DTYPE, shard_pack_np, shard_unpack_np
 
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
@@ -74,11 +75,11 @@ def test_pack_matches_model(rx, wl, world, small):
         exp = shard_pack_np(arena, off, recs, world, cap, bcap)
         b = sh.buffers()
         counts = dev_to_numpy(b.send_counts, 32 * world, COUNTS_DTYPE)
-        slots = dev_to_numpy(b.send_slots, 64 * world * cap, RECORD_DTYPE)
+        slots = dev_to_numpy(b.send_slots, 32 * world * cap, ITEM_DTYPE)
         blob = dev_to_numpy(b.send_blob, world * bcap)
         tot_n = int(counts["n"].sum())
         tot_b = int(counts["bytes"].sum())
-        spill = dev_to_numpy(b.send_spill, 64 * tot_n, RECORD_DTYPE)
+        spill = dev_to_numpy(b.send_spill, 32 * tot_n, ITEM_DTYPE)
         bspill = dev_to_numpy(b.send_blob_spill, tot_b)
         sb = sbb = 0
         spilled = 0
@@ -86,9 +87,9 @@ def test_pack_matches_model(rx, wl, world, small):
             e, c = exp[d], counts[d]
             assert c.tobytes() == e["counts"][0].tobytes(), (d, c, e["counts"])
             cut, cb, n, nb = int(c["cut"]), int(c["cut_bytes"]), int(c["n"]), int(c["bytes"])
-            assert slots[d * cap:d * cap + cut].tobytes() == e["slot_recs"].tobytes()
+            assert slots[d * cap:d * cap + cut].tobytes() == e["slot_items"].tobytes()
             assert blob[d * bcap:d * bcap + cb].tobytes() == e["slot_blob"].tobytes()
-            assert spill[sb + cut:sb + n].tobytes() == e["spill_recs"].tobytes()
+            assert spill[sb + cut:sb + n].tobytes() == e["spill_items"].tobytes()
             assert bspill[sbb + cb:sbb + nb].tobytes() == e["spill_blob"].tobytes()
             sb += n
             sbb += nb
@@ -124,10 +125,10 @@ def test_unpack_matches_model(rx, wl, small):
         dev_copy(b.recv_counts, rc.ctypes.data, rc.nbytes)
         rs = rbs = 0
         for s, x in enumerate(received):
-            dev_copy(b.recv_slots + s * cap * 64, x["slot_recs"].ctypes.data, x["slot_recs"].nbytes)
+            dev_copy(b.recv_slots + s * cap * 32, x["slot_items"].ctypes.data, x["slot_items"].nbytes)
             dev_copy(b.recv_blob + s * bcap, x["slot_blob"].ctypes.data, x["slot_blob"].nbytes)
-            sr = np.ascontiguousarray(x["spill_recs"])
-            dev_copy((b.recv_spill or 0) + rs * 64, sr.ctypes.data, sr.nbytes)
+            sr = np.ascontiguousarray(x["spill_items"])
+            dev_copy((b.recv_spill or 0) + rs * 32, sr.ctypes.data, sr.nbytes)
             dev_copy((b.recv_blob_spill or 0) + rbs, x["spill_blob"].ctypes.data, x["spill_blob"].nbytes)
             rs += len(sr)
             rbs += len(x["spill_blob"])
@@ -178,11 +179,8 @@ def test_one_rank_owner_pipeline(rx, wl, cap, bcap):
         _, recs, _, _ = oracle.parse(arena, off, ln, match_table=tbl)
         samples = oracle.FragAssembler().batch_readers(arena, off, recs, tbl)[0]
         _, odels, oack = oracle.HistoryIngest(tbl).batch(arena, off, recs, samples)
-        index = {(int(r["dgram_idx"]), int(r["sub_off"])): i for i, r in enumerate(recs)}
-        orecs = ob.records()
-        _, didx = ob.origin()
-        got = [(index[(int(didx[int(d["rec_idx"])]), int(orecs[int(d["rec_idx"])]["sub_off"]))], int(d["reader_slot"]))
-               for d in dels]
+        _, src = ob.origin()  # each owner record's index in the (one) source's parse output
+        got = [(int(src[int(d["rec_idx"])]), int(d["reader_slot"])) for d in dels]
         assert got == [(int(d["rec_idx"]), int(d["reader_slot"])) for d in odels]
         assert np.array_equal(ack, oack) and na > (20 if wl == "C4" else 100)
         if wl == "C4":

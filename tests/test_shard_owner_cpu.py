@@ -21,7 +21,7 @@ import torch.multiprocessing as mp
 import oracle
 from rtps_rx.records import RECORD_DTYPE, DELIVERY_DTYPE, FRAG_SAMPLE_DTYPE, pack_match_table, WRITER_KINDS
 from rtps_rx.shard import spill_plan
-from shard_ref import COUNTS_DTYPE, shard_pack_np, shard_unpack_np
+from shard_ref import COUNTS_DTYPE, ITEM_DTYPE, shard_pack_np, shard_unpack_np
 
 C5_STRIDE = 8 << 20  # rank r's chunk starts at generator index r * 8M (BASELINE C5: 64M over 8 GPUs)
 
@@ -61,18 +61,18 @@ def _table(wl, world, n, stride):
 
 
 def _layout(packed, world, cap, bcap):
-    """The library's send buffers: slots [world * cap] records, blob slots [world * bcap],
+    """The library's send buffers: slots [world * cap] items, blob slots [world * bcap],
     exact-layout spills, counts."""
-    slots = np.zeros(world * cap, dtype=RECORD_DTYPE)
+    slots = np.zeros(world * cap, dtype=ITEM_DTYPE)
     blob = np.zeros(world * bcap, dtype=np.uint8)
     counts = np.zeros(world, dtype=COUNTS_DTYPE)
     spill_r, spill_b = [], []
     for d, x in enumerate(packed):
         c = x["counts"][0]
         counts[d] = c
-        slots[d * cap:d * cap + int(c["cut"])] = x["slot_recs"]
+        slots[d * cap:d * cap + int(c["cut"])] = x["slot_items"]
         blob[d * bcap:d * bcap + int(c["cut_bytes"])] = x["slot_blob"]
-        spill_r.append(np.concatenate([np.zeros(int(c["cut"]), RECORD_DTYPE), x["spill_recs"]]))
+        spill_r.append(np.concatenate([np.zeros(int(c["cut"]), ITEM_DTYPE), x["spill_items"]]))
         spill_b.append(np.concatenate([np.zeros(int(c["cut_bytes"]), np.uint8), x["spill_blob"]]))
     return slots, blob, counts, np.concatenate(spill_r), np.concatenate(spill_b)
 
@@ -100,30 +100,29 @@ def _worker(rank, world, port, wl, n, stride, cap, bcap, tbl, q):
         # round 1: the exact spill, from the counts alone
         plan = spill_plan(sc, rc)
         sr = sspill.view(np.uint8)
-        sends = [sr[p["send_rec"][0] * 64:(p["send_rec"][0] + p["send_rec"][1]) * 64] for p in plan]
-        rspill = np.zeros(sum(p["recv_rec"][1] for p in plan) * 64, np.uint8)
-        _a2a(np.concatenate(sends), rspill, [len(x) for x in sends], [p["recv_rec"][1] * 64 for p in plan])
+        sends = [sr[p["send_rec"][0] * 32:(p["send_rec"][0] + p["send_rec"][1]) * 32] for p in plan]
+        rspill = np.zeros(sum(p["recv_rec"][1] for p in plan) * 32, np.uint8)
+        _a2a(np.concatenate(sends), rspill, [len(x) for x in sends], [p["recv_rec"][1] * 32 for p in plan])
         sends = [sbspill[p["send_bytes"][0]:p["send_bytes"][0] + p["send_bytes"][1]] for p in plan]
         rbspill = np.zeros(sum(p["recv_bytes"][1] for p in plan), np.uint8)
         _a2a(np.concatenate(sends), rbspill, [len(x) for x in sends], [p["recv_bytes"][1] for p in plan])
-        rspill = rspill.view(RECORD_DTYPE)
+        rspill = rspill.view(ITEM_DTYPE)
         # what each source sent this owner, rebuilt from the receive buffers as the device unpack reads them
         received, rs, rbs = [], 0, 0
         for s in range(world):
             c = rc[s]
             cut, cb, nn, nb = int(c["cut"]), int(c["cut_bytes"]), int(c["n"]), int(c["bytes"])
-            received.append({"slot_recs": rslots[s * cap:s * cap + cut], "slot_blob": rblob[s * bcap:s * bcap + cb],
-                             "spill_recs": rspill[rs:rs + nn - cut], "spill_blob": rbspill[rbs:rbs + nb - cb]})
+            received.append({"slot_items": rslots[s * cap:s * cap + cut], "slot_blob": rblob[s * bcap:s * bcap + cb],
+                             "spill_items": rspill[rs:rs + nn - cut], "spill_blob": rbspill[rbs:rbs + nb - cb]})
             rs += nn - cut
             rbs += nb - cb
-        orecs, ooff, oarena, (orank, odidx) = shard_unpack_np(received)
+        orecs, ooff, oarena, (orank, osrc) = shard_unpack_np(received)
         fa = oracle.FragAssembler()
         samples = fa.batch_readers(oarena, ooff, orecs, tbl)[0]
         ing = oracle.HistoryIngest(tbl)
         acc, dels, ack = ing.batch(oarena, ooff, orecs, samples)
-        q.put((rank, dels.tobytes(), ack.tobytes(), orank.tobytes(), odidx.tobytes(),
-               orecs["sub_off"].tobytes(), samples.tobytes(), int(sum(p["recv_rec"][1] for p in plan)),
-               len(orecs)))
+        q.put((rank, dels.tobytes(), ack.tobytes(), orank.tobytes(), osrc.tobytes(),
+               samples.tobytes(), int(sum(p["recv_rec"][1] for p in plan)), len(orecs)))
     finally:
         dist.destroy_process_group()
 
@@ -149,20 +148,19 @@ def _run(world, wl, n, stride, cap, bcap):
     _, recs, _, rb = oracle.parse(a, o, l, match_table=tbl)
     samples = oracle.FragAssembler().batch_readers(a, o, recs, tbl)[0]
     _, dels, ack = oracle.HistoryIngest(tbl).batch(a, o, recs, samples)
-    index = {(int(r["dgram_idx"]), int(r["sub_off"])): i for i, r in enumerate(recs)}
+    # origin = (source rank, record index in that rank's parse); rank r parsed datagrams [r n, (r+1) n)
+    first_rec = np.searchsorted(recs["dgram_idx"], np.arange(world) * n)
     got, spilled, items = [], 0, 0
     owner_ack = np.ones(len(ack), dtype=np.int64)
     for rank in range(world):
-        d, k, orank, odidx, osub, osamp, sp, ni = res[rank]
+        d, k, orank, osrc, osamp, sp, ni = res[rank]
         d = np.frombuffer(d, DELIVERY_DTYPE)
-        orank, odidx = np.frombuffer(orank, np.uint32), np.frombuffer(odidx, np.uint32)
-        osub = np.frombuffer(osub, np.uint16)
+        orank, osrc = np.frombuffer(orank, np.uint32), np.frombuffer(osrc, np.uint32)
         spilled += sp
         items += ni
         for x in d:
             j = int(x["rec_idx"])
-            gdg = int(orank[j]) * n + int(odidx[j])
-            got.append((index[(gdg, int(osub[j]))], int(x["reader_slot"])))
+            got.append((int(first_rec[int(orank[j])]) + int(osrc[j]), int(x["reader_slot"])))
         k = np.frombuffer(k, np.int64)
         moved = k != 1
         assert not (moved & (owner_ack != 1)).any(), "two owners advanced one proxy"
@@ -179,7 +177,7 @@ def _run(world, wl, n, stride, cap, bcap):
 def test_owner_ingest_c3_at_c5_indices(world):
     """C3 mix (DATA / HEARTBEAT / GAP with bitmaps / INFO_*) with the ranks' chunks at C5's
     generator indices; slots large enough for everything (no spill)."""
-    spilled, items = _run(world, oracle.WL_C3, 2500, C5_STRIDE, cap=12000, bcap=64 << 10)
+    spilled, items = _run(world, oracle.WL_C3, 2500, C5_STRIDE, cap=12000, bcap=1 << 20)
     assert spilled == 0 and items > 5000
 
 
