@@ -400,6 +400,36 @@ def frag_leg(rx, arena, off_t, outs, n_rec, recs, stream, steps):
             "frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
 
+XGMI_LINK_GBS = 153.0  # one xGMI link, one direction (8-GPU node: one link per peer pair, 7 per GPU)
+
+
+def exchange_prediction(rx, arena, off_t, outs, dev, worlds=(2, 4, 8)):
+    """What the owner-side exchange of THIS batch would move at N ranks (weak scaling: every
+    rank parses a batch like this one): the library's pack with n_ranks = N, its per-destination
+    counts (32-B items + blob bytes), the bytes each rank sends to its peers per step and the
+    xGMI time they take at the link rate (every peer on its own link, all in parallel: the
+    largest per-peer volume bounds the round)."""
+    from rtps_rx.shard import OwnerShard
+    out = {}
+    for w in worlds:
+        sh = OwnerShard(rx, w, None, dev, 1, 0)
+        try:
+            sh.pack(arena, off_t, outs)
+            c = sh.counts("send")
+        finally:
+            sh.close()
+        n, b = c["n"].astype(np.int64), c["bytes"].astype(np.int64)
+        # rank 0's view: destination 0 stays local; the others cross a link each
+        peer = 32 * n[1:] + b[1:] + 32
+        out[str(w)] = {"items_per_dest": [int(v) for v in n], "blob_bytes_per_dest": [int(v) for v in b],
+                       "bytes_sent_per_rank_per_step": int(peer.sum()),
+                       "max_bytes_per_peer": int(peer.max()),
+                       "predicted_xgmi_ms": float(peer.max()) / (XGMI_LINK_GBS * 1e9) * 1e3}
+    return {"what": "owner-side exchange volume of this batch at N ranks (rank 0's sends; library pack with "
+                    "n_ranks = N on this GPU), predicted round time at one xGMI link per peer",
+            "link_gbs": XGMI_LINK_GBS, "item_bytes": 32, **out}
+
+
 def ingest_leg(rx, arena, off_t, outs, n_rec, recs, n_entries, stream, steps, fouts=None):
     """History-cache ingest (§8f rank 2) of this batch's samples / HEARTBEATs / GAPs,
     timed separately (HIP events on the launch stream).  Every step starts from
@@ -940,10 +970,12 @@ def measure(args, world, rank, dist, dev, allreduce_sum, allreduce_max):
         result["config"]["exchange"] = {
             "mode": "owner-side exchange: fixed slots (equal-split RCCL group, pipelined with the next parse) "
                     "+ exact spill round when a slot overflows",
-            "item": "64-B records of the writer submessages that pass + their GAP bitmap / DATA_FRAG payload "
-                    "bytes, owner = writer-GUID hash % world; unpacked on the owner as one batch",
-            "slot_records": slot[0], "slot_blob_bytes": slot[1],
-            "bytes_sent_per_rank_per_step": world * (slot[0] * 64 + slot[1]),
+            "item": "32-B rtps_shard_item per writer submessage that passes (a DATA: GUID, SN, kind, flags, "
+                    "route, payload kind; any other kind: its 64-B record + GAP bitmap / DATA_FRAG payload bytes "
+                    "in the blob), owner = writer-GUID hash % world; unpacked on the owner as one batch",
+            "slot_items": slot[0], "slot_blob_bytes": slot[1],
+            "bytes_sent_per_rank_per_step": (world - 1) * (slot[0] * 32 + slot[1] + 32),
+            "predicted_xgmi_ms": (slot[0] * 32 + slot[1] + 32) / (XGMI_LINK_GBS * 1e9) * 1e3,
             "spilled_records_rank0": int((rcv["n"] - rcv["cut"]).sum()), "overflow": False}
     elif world > 1:
         got, split = exch[(args.warmup + args.steps - 1) & 1].gather_received()
@@ -964,6 +996,8 @@ def measure(args, world, rank, dist, dev, allreduce_sum, allreduce_max):
     if world == 1 and not args.no_ingest and n_matched_writers:
         leg_iouts, result["ingest"] = ingest_leg(rx, arena, off_t, outs, n_rec, recs, n_matched_writers, stream,
                                                  args.steps, fouts=fouts)
+    if world == 1 and n_matched_writers and not c5:
+        result["exchange_prediction"] = exchange_prediction(rx, arena, off_t, outs, dev)
     if world == 1 and not args.no_cdr:
         result["cdr_decode"] = cdr_decode_leg(rx, args.workload, arena, off_t, outs, n_rec, stream, args.steps,
                                               iouts=leg_iouts)

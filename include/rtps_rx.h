@@ -652,9 +652,14 @@ int rtps_rx_frag_set_receive_time(rtps_rx_ctx* ctx, uint64_t unix_ns);
  * persists in the context across batches; it is indexed by proxy position, so
  * keep proxies in place (append new ones) or call rtps_rx_ingest_reset after
  * reordering them.
- * Limit: the change set is kept for RTPS_INGEST_WINDOW sequence numbers from
- * all_ackable_before; a sample further ahead is accepted without the duplicate
- * check and counted in *n_window_overflow (the reference's BTreeMap has no bound). */
+ * The change set is a bitmap over RTPS_INGEST_WINDOW sequence numbers from
+ * all_ackable_before plus, per proxy, a sorted set of up to RTPS_INGEST_FAR_CAP
+ * covered SNs beyond that window (samples and GAPs further ahead: decided exactly,
+ * replayed in event order; all_ackable_before continues through the set).  Only
+ * past those capacities (a full far set, more than 8192 far events in a batch) is
+ * a sample accepted without the duplicate check; those are counted in
+ * *n_window_overflow (the reference's BTreeMap has no bound). */
+#define RTPS_INGEST_FAR_CAP 1024u
 #define RTPS_INGEST_WINDOW (1u << 17)
 #define RTPS_INGEST_BEST_EFFORT 0x1u /* flags: treat every reader as BestEffort (HEARTBEATs ignored) */
 #define RTPS_INGEST_TOPIC_CACHE 0x2u /* flags: also run the topic caches' add_change (RTPS_DELIVERY_CACHED) */

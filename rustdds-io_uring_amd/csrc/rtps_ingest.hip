@@ -72,46 +72,37 @@ constexpr uint32_t ECAP_MAX = 1u << 14;     // writer proxies
 enum : uint8_t { EV_NONE = 0, EV_SAMPLE = 1, EV_HB = 2, EV_GAP = 3 };
 // counters: window overflow, selected HEARTBEATs, selected deliveries, records of the batch, then
 // the HEARTBEAT / GAP / event / proxy-less sample counts in 64 slot quads (one atomic per block, spread: no hot address)
-enum { C_OVF = 0, C_NSEL, C_NDEL, C_NREC, C_SPREAD, C_COUNT = C_SPREAD + 4 * 64 };
+// (C_FARC: classify's far-SN candidates, the host's cue for k_far; C_NFAR: far items appended)
+enum { C_OVF = 0, C_NSEL, C_NDEL, C_NREC, C_FARC, C_NFAR, C_SPREAD, C_COUNT = C_SPREAD + 4 * 64 };
 // event metadata: reader slot | flags << 16 (EVF_*)
 constexpr uint32_t EVF_DUP_OK = 1u << 16;  // RTPS_TARGET_DUPLICATES_OK reader
 constexpr uint32_t EVF_FREE = 1u << 17;    // sample without a proxy (writer kind not user-defined)
 
-// atomicOr(base[idx], m) for the active lanes, with every word's bits combined
-// across the wave first: one atomic per distinct word.  A writer's sequential
-// SNs share bitmap words (T: 4 lanes per word, 16 writers interleaved), while
-// mixed traffic has mostly distinct words (C3); a bitonic sort of the 64
-// (word, bits) pairs then a segmented OR over the runs of equal words costs a
-// fixed 21 + 12 shuffle steps for either.  Every lane of the wave must call it.
+// atomicOr(*addr, m) for the active lanes, the bits of a word shared by several lanes
+// combined first.  A writer's sequential SNs share bitmap words (T: a few distinct
+// words per wave), while mixed traffic has mostly distinct words (C3), where combining
+// gains nothing.  So: up to WOR_ROUNDS rounds of "the first pending lane's word: OR of
+// every lane on it, one atomic", then a plain atomic per lane still pending.  A round
+// is a ballot, a read-lane and a 6-step OR reduction.  Every lane of the wave must call it.
+constexpr uint32_t WOR_ROUNDS = 4;
 __device__ __forceinline__ void wave_or(uint32_t* base, uint32_t* addr, uint32_t m, bool active) {
   const uint32_t lane = threadIdx.x & 63u;
-  uint32_t key = active ? (uint32_t)(addr - base) : 0xffffffffu;  // inactive lanes sort last
-  uint32_t v = active ? m : 0u;
+  const uint32_t key = (uint32_t)(addr - base);
+  bool todo = active && m != 0u;
 #pragma unroll
-  for (uint32_t k = 2; k <= 64; k <<= 1) {
+  for (uint32_t r = 0; r < WOR_ROUNDS; ++r) {
+    const uint64_t t = __ballot(todo);
+    if (t == 0) return;
+    const uint32_t leader = (uint32_t)__builtin_ctzll(t);
+    const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)key, (int)leader);
+    const bool mine = todo && key == k;
+    uint32_t v = mine ? m : 0u;
 #pragma unroll
-    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      const uint32_t pk = (uint32_t)__shfl_xor((int)key, j, 64), pv = (uint32_t)__shfl_xor((int)v, j, 64);
-      const bool up = (lane & k) == 0, lower = (lane & j) == 0;
-      const bool take = lower == up ? pk < key : pk > key;
-      if (take) { key = pk; v = pv; }
-    }
+    for (uint32_t d = 1; d < 64; d <<= 1) v |= (uint32_t)__shfl_xor((int)v, d, 64);
+    if (lane == leader) atomicOr(base + k, v);
+    todo = todo && !mine;
   }
-  const uint32_t prev = (uint32_t)__shfl_up((int)key, 1, 64);
-  uint32_t start = (lane == 0 || prev != key) ? lane : 0u;  // first lane of this lane's run
-#pragma unroll
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const uint32_t y = (uint32_t)__shfl_up((int)start, d, 64);
-    if (lane >= d && y > start) start = y;
-  }
-#pragma unroll
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const uint32_t y = (uint32_t)__shfl_up((int)v, d, 64);
-    if (lane >= d && lane - d >= start) v |= y;
-  }
-  const uint32_t next = (uint32_t)__shfl_down((int)key, 1, 64);
-  const bool tail = lane == 63 || next != key;
-  if (key != 0xffffffffu && tail && v) atomicOr(base + key, v);
+  if (todo) atomicOr(addr, m);
 }
 // first-cover key of event k in batch `epoch`: no reset between batches is needed
 __device__ __forceinline__ unsigned long long ekey(uint32_t epoch, uint32_t k) {
@@ -145,6 +136,7 @@ struct Scratch {
   int32_t *hcnt, *hexcl;
   int64_t *hf, *hpre;
 };
+struct FarItem;
 struct State {
   int64_t* base;    // all_ackable_before
   int64_t* lo;      // first sequence number of the window (multiple of 32, <= base)
@@ -155,6 +147,9 @@ struct State {
   uint32_t* seg_b;  // HEARTBEAT segment of each proxy in sorted order
   uint32_t* seg_e;
   uint64_t* ctr;
+  int64_t* far;      // the far set of proxy e: far[e * FCAP, + far_n[e]), ascending, all >= lo + W
+  uint32_t* far_n;
+  FarItem* fl;       // this batch's far items (global paths), C_NFAR of them
 };
 
 // ---- 1 classify ----
@@ -212,6 +207,40 @@ struct PEv {
   uint32_t k;  // event index (accept[] slot)
 };
 static_assert(sizeof(PEv) == 32, "PEv layout");
+
+// ---- far sequence numbers: the change set beyond the window ----
+// The window [lo, lo + W) holds the change set as bits; the reference's BTreeMap has no
+// bound, so the SNs a proxy has covered at or above lo + W (a writer that jumped ahead,
+// a GAP reaching past the window) are kept per proxy in a sorted array of at most FCAP
+// SNs, the FAR SET.  A batch's events beyond the window, FAR ITEMS (samples past it,
+// DUPLICATES_OK samples there, GAPs whose coverage reaches past it), are decided
+// provisionally by the parallel passes (samples accepted), then replayed per proxy in
+// event order against the far set (k_far on the global paths, the tail of k_proxy on the
+// per-proxy one): a sample already covered is rejected, every SN an item covers joins the
+// set.  The state pass continues all_ackable_before through the set when the window is
+// covered up to its end, re-anchors, and moves the set's SNs the new window spans into
+// its bits.  Inexact only past the capacities (a full far set, more than FL_CAP far items
+// in a batch, more than FPX for one proxy on the per-proxy path): counted in
+// *n_window_overflow, those samples accepted unchecked.
+constexpr uint32_t FCAP = RTPS_INGEST_FAR_CAP;  // far SNs per proxy
+constexpr uint32_t FHS = 2 * FCAP;  // the replay's LDS hash slots
+constexpr uint32_t FL_CAP = 8192;   // far items per batch (global list)
+constexpr uint32_t FPX = 1024;      // far items one k_proxy workgroup replays
+enum : uint32_t { FI_SAMPLE = 1, FI_DUP = 2, FI_GAP = 3 };
+struct FarItem {
+  PEv p;        // the event as the per-proxy pass packs it (p.k: its accept slot)
+  int64_t lim;  // lo + W when it was decided: the SNs at or above it are the far part
+  uint32_t e, kind;
+};
+static_assert(sizeof(FarItem) == 48 && FHS == 2048, "FarItem layout, replay hash width");
+// its list position, or NONE: the list is full (the item is lost: its sample stays accepted,
+// its SNs unrecorded)
+__device__ __forceinline__ uint32_t far_push(uint64_t* ctr, FarItem* fl, const FarItem& it) {
+  const unsigned long long pos = atomicAdd(reinterpret_cast<unsigned long long*>(ctr + C_NFAR), 1ull);
+  if (pos >= FL_CAP) return 0xffffffffu;
+  fl[pos] = it;
+  return (uint32_t)pos;
+}
 
 // What the per-proxy path of an identity batch needs from classify (FAST): the
 // packed events at their record slots, the sort pairs (proxy or n_proxies, slot),
@@ -304,7 +333,7 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
   const rtps_target* const sent = fo.sets_lds ? s_se : t.set_ent;
   if (lds || BUCKET) __syncthreads();
   const bool reliable = !(flags & RTPS_INGEST_BEST_EFFORT);
-  uint32_t nh = 0, ng = 0, ne = 0, nf = 0;
+  uint32_t nh = 0, ng = 0, ne = 0, nf = 0, nfar = 0;
   // record slot i: its events; FAST: *key = the proxy of its proxied event (NONE: none)
   // and *P its packed form, stored at pev[i] unless BUCKET (which places it itself)
   auto body = [&](uint64_t i, uint32_t& key, PEv& P) {
@@ -330,7 +359,7 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
           sn = frag[f].sn;
         } else if (kind == RTPS_DATA || kind == RTPS_HEARTBEAT || kind == RTPS_GAP) {
           q2 = q[2];
-          if (FAST && kind != RTPS_DATA) q3 = q[3];
+          if ((FAST && kind != RTPS_DATA) || (MARK && kind == RTPS_GAP)) q3 = q[3];
           const int64_t rsn = (int64_t)(((uint64_t)q2[1] << 32) | q2[0]);
           if (kind == RTPS_DATA) {
             // data_to_dds_data must succeed (reader.rs:552-558)
@@ -381,11 +410,20 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
         x.evt[i] = evi;
         x.ent[i] = ent;
         x.esn[i] = sn;
+#ifndef RTPS_EXP_NOMARK
         if (MARK && evi == EV_SAMPLE && ent != NONE) {  // k_marks_d's first-cover key
+#else
+        if (false) {
+#endif
           const int64_t lo = st.lo[ent];
           if (sn >= lo && sn < lo + (int64_t)W)
             atomicMin(reinterpret_cast<unsigned long long*>(st.fc + (uint64_t)ent * W) + (uint64_t)(sn - lo),
                       ekey(epoch, (uint32_t)i));
+          else if (sn >= lo + (int64_t)W)
+            ++nfar;  // a far-item candidate: the host launches k_far
+        } else if (MARK && evi == EV_GAP) {
+          const int64_t list_base = (int64_t)(((uint64_t)q2[3] << 32) | q2[2]);
+          if (list_base + (int64_t)q3[0] > st.lo[ent] + (int64_t)W) ++nfar;  // coverage past the window
         }
       }
       if (!FAST) {
@@ -530,6 +568,7 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
   if (tid < 4 && s_n[tid])
     atomicAdd(reinterpret_cast<unsigned long long*>(ctr + C_SPREAD + 4u * (blockIdx.x & 63u) + tid),
               (unsigned long long)s_n[tid]);
+  if (MARK && nfar) atomicAdd(reinterpret_cast<unsigned long long*>(ctr + C_FARC), (unsigned long long)nfar);
 }
 
 // 1b: lane per record writes its events at roff[i] (set order = EntityId order of the readers)
@@ -684,10 +723,29 @@ __global__ __launch_bounds__(IT) void k_marks_g(const rtps_record* recs, const u
 // one sample event: accepted?  pe / poff / merge: the proxy and window offset of a sample
 // whose position the change-set merge sets (an accepted sample in the window, or any sample
 // of a DUPLICATES_OK reader's proxy in it: received_changes_add runs for those too)
+// Far items go to the batch's list (recs / dgram_off: a GAP's fields; the bitmap stays in the arena).
+struct FarSrc {
+  const rtps_record* recs;
+  const uint64_t* dgram_off;
+};
 __device__ __forceinline__ uint8_t decide_one(uint64_t i, uint64_t n, const Scratch& x, const State& s, bool reliable,
-                                              uint32_t epoch, uint32_t& pe, uint64_t& poff, bool& merge) {
+                                              uint32_t epoch, const FarSrc& fs, uint32_t& pe, uint64_t& poff,
+                                              bool& merge) {
   merge = false;
-  if (i >= n || x.evt[i] != EV_SAMPLE) return 0;
+  if (i >= n) return 0;
+  const uint8_t ev = x.evt[i];
+  if (ev == EV_GAP) {  // its coverage past the window is the far replay's
+    const uint32_t e = x.ent[i];
+    const rtps_record& r = fs.recs[x.erec[i]];
+    const int64_t lim = s.lo[e] + (int64_t)W;
+    if (r.u.gap.list_base + (int64_t)r.u.gap.num_bits > lim)
+      far_push(s.ctr, s.fl,
+               FarItem{PEv{r.sn, r.u.gap.list_base, fs.dgram_off[r.dgram_idx] + r.u.gap.bitmap_off,
+                           EV_GAP | ((r.flags & 1u) ? PM_LE : 0u) | (r.u.gap.num_bits << 8), (uint32_t)i},
+                       lim, e, FI_GAP});
+    return 0;
+  }
+  if (ev != EV_SAMPLE) return 0;
   const uint32_t e = x.ent[i], meta = x.emeta[i];
   if (e == NONE) return 1;  // no proxy: the writer kind is not user-defined (reader.rs:734-739)
   const int64_t v = x.esn[i], lo = s.lo[e];
@@ -696,6 +754,7 @@ __device__ __forceinline__ uint8_t decide_one(uint64_t i, uint64_t n, const Scra
   poff = (uint64_t)(v - lo);
   if (meta & EVF_DUP_OK) {  // the participant reader's duplicates (reader.rs:712-722)
     merge = in_win;
+    if (v >= lo + (int64_t)W) far_push(s.ctr, s.fl, FarItem{PEv{v, 0, 0, EV_SAMPLE, (uint32_t)i}, lo + (int64_t)W, e, FI_DUP});
     return 1;
   }
   int64_t thr = s.base[e];
@@ -711,8 +770,8 @@ __device__ __forceinline__ uint8_t decide_one(uint64_t i, uint64_t n, const Scra
     if (a > sb && x.hpre[a - 1u] > thr) thr = x.hpre[a - 1u];
   }
   if (v < 1 || v < thr) return 0;
-  if (v >= lo + (int64_t)W) {  // beyond the tracked window: accepted unchecked
-    atomicAdd(reinterpret_cast<unsigned long long*>(s.ctr + C_OVF), 1ull);
+  if (v >= lo + (int64_t)W) {  // beyond the window: accepted until the far replay (k_far) decides
+    far_push(s.ctr, s.fl, FarItem{PEv{v, 0, 0, EV_SAMPLE, (uint32_t)i}, lo + (int64_t)W, e, FI_SAMPLE});
     return 1;
   }
   const bool known = (s.bits[(uint64_t)e * WW + (poff >> 5)] >> (poff & 31u)) & 1u;
@@ -722,12 +781,12 @@ __device__ __forceinline__ uint8_t decide_one(uint64_t i, uint64_t n, const Scra
 }
 // (acc[0, cap): entries past n are cleared)
 __global__ __launch_bounds__(IT) void k_decide(uint64_t n, uint64_t cap, Scratch x, State s, uint8_t* acc_out,
-                                               bool reliable, uint32_t epoch) {
+                                               bool reliable, uint32_t epoch, FarSrc fs) {
   for (uint64_t i = (uint64_t)blockIdx.x * IT + threadIdx.x; i < cap; i += (uint64_t)gridDim.x * IT) {
     uint32_t e;
     uint64_t off;
     bool w;
-    acc_out[i] = decide_one(i, n, x, s, reliable, epoch, e, off, w);
+    acc_out[i] = decide_one(i, n, x, s, reliable, epoch, fs, e, off, w);
   }
 }
 
@@ -780,7 +839,7 @@ __device__ __forceinline__ uint64_t block_sum64(uint64_t v, uint64_t* s_w) {
 // are set already, so k_merge's extra bits there change nothing k_state reads.
 template <bool MERGE>
 __global__ __launch_bounds__(IT) void k_decide_t(uint64_t n, uint64_t cap, Scratch x, State s, uint8_t* acc_out,
-                                                 bool reliable, uint32_t epoch, uint32_t* tcnt) {
+                                                 bool reliable, uint32_t epoch, uint32_t* tcnt, FarSrc fs) {
   __shared__ uint64_t s_w[IT / 64];
   const uint64_t b0 = (uint64_t)blockIdx.x * DT + threadIdx.x * DPT;
   uint32_t w[DPT / 4];
@@ -792,10 +851,15 @@ __global__ __launch_bounds__(IT) void k_decide_t(uint64_t n, uint64_t cap, Scrat
     uint32_t e = 0;
     uint64_t off = 0;
     bool merge = false;
-    const uint8_t a = decide_one(b0 + j, n, x, s, reliable, epoch, e, off, merge);
+    const uint8_t a = decide_one(b0 + j, n, x, s, reliable, epoch, fs, e, off, merge);
     w[j >> 2] |= (uint32_t)a << (8u * (j & 3u));
     c += a;
-    if (MERGE) wave_or(s.bits, merge ? s.bits + (uint64_t)e * WW + (off >> 5) : s.bits, 1u << (off & 31u), merge);
+#ifdef RTPS_EXP_NOMERGE
+    if (false)
+#else
+    if (MERGE)
+#endif
+      wave_or(s.bits, merge ? s.bits + (uint64_t)e * WW + (off >> 5) : s.bits, 1u << (off & 31u), merge);
   }
   if (b0 + DPT <= cap) {
 #pragma unroll
@@ -898,6 +962,205 @@ __global__ __launch_bounds__(IT) void k_accept_counts(uint64_t n, uint64_t cap, 
   }
 }
 
+// ---- far replay (see "far sequence numbers" above) ----
+__device__ __forceinline__ uint32_t fh_slot(int64_t v) {
+  return (uint32_t)(((uint64_t)v * 0x9e3779b97f4a7c15ull) >> 53);  // 11 bits: FHS slots
+}
+__device__ bool fh_has(const int64_t* h, int64_t v) {
+  for (uint32_t j = fh_slot(v);; j = (j + 1u) & (FHS - 1u)) {
+    const int64_t k = h[j];
+    if (k == v) return true;
+    if (k == INT64_MAX) return false;
+  }
+}
+// v into the set (n: its size); false when it is full
+__device__ bool fh_add(int64_t* h, uint32_t& n, int64_t v) {
+  uint32_t j = fh_slot(v);
+  for (;; j = (j + 1u) & (FHS - 1u)) {
+    const int64_t k = h[j];
+    if (k == v) return true;
+    if (k == INT64_MAX) break;
+  }
+  if (n >= FCAP) return false;
+  h[j] = v;
+  ++n;
+  return true;
+}
+// The SNs >= lim a GAP covers (what gap_cover_w clips at the window's end): the range
+// [gapStart, gapList.base) when not negative, then the listed SNs.  f(sn) false: the set
+// is full; *miss counts what was not recorded.
+template <typename WF, typename F>
+__device__ void gap_far(int64_t start, int64_t base, uint32_t num_bits, WF&& word_of, int64_t lim, F&& f,
+                        uint64_t& miss) {
+  if (start <= base)
+    for (int64_t v = start > lim ? start : lim; v < base; ++v)
+      if (!f(v)) { miss += (uint64_t)(base - v); break; }
+  for (uint32_t w = 0; w * 32u < num_bits; ++w) {
+    uint32_t word = word_of(w);
+    const uint32_t valid = num_bits - w * 32u;
+    if (valid < 32u) word &= ~(0xffffffffu >> valid);
+    while (word) {
+      const uint32_t b = (uint32_t)__builtin_clz(word);  // MSB first: SN base + 32 w + b
+      word &= ~(0x80000000u >> b);
+      const int64_t v = base + (int64_t)(w * 32u + b);
+      if (v >= lim && !f(v)) ++miss;
+    }
+  }
+}
+// one far item, in the proxy's event order: a sample the set (or an earlier item) covers is
+// rejected (acc 0; tcnt: its delivery tile's count); everything covered joins the set
+__device__ uint64_t far_apply(const FarItem& it, int64_t* h, uint32_t& n, const uint8_t* arena, uint8_t* acc,
+                              uint32_t* tcnt) {
+  uint64_t miss = 0;
+  const PEv& P = it.p;
+  if (it.kind == FI_SAMPLE) {
+    if (fh_has(h, P.sn)) {
+      acc[P.k] = 0;
+      if (tcnt) atomicSub(&tcnt[P.k / DT], 1u);
+    } else if (!fh_add(h, n, P.sn)) {
+      ++miss;
+    }
+  } else if (it.kind == FI_DUP) {
+    if (!fh_add(h, n, P.sn)) ++miss;
+  } else {
+    auto f = [&](int64_t v) { return fh_add(h, n, v); };
+    if (P.m & PM_INL)
+      gap_far(P.sn, P.a, P.m >> 8, [&](uint32_t w) { return (uint32_t)(P.bw >> (32u * w)); }, it.lim, f, miss);
+    else
+      gap_far(P.sn, P.a, P.m >> 8, [&](uint32_t w) { return rd32(arena + P.bw + 4u * w, (P.m & PM_LE) != 0u); },
+              it.lim, f, miss);
+  }
+  return miss;
+}
+// ascending bitonic sort of a power-of-two LDS array by the whole block (nt threads)
+template <typename T>
+__device__ void lds_sort(T* a, uint32_t len, uint32_t nt) {
+  for (uint32_t k = 2; k <= len; k <<= 1)
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = threadIdx.x; i < len; i += nt) {
+        const uint32_t l = i ^ j;
+        if (l > i) {
+          const T x = a[i], y = a[l];
+          if (((i & k) == 0) ? (x > y) : (x < y)) { a[i] = y; a[l] = x; }
+        }
+      }
+      __syncthreads();
+    }
+}
+// Proxy e's far set into the LDS hash h (block-wide), the items' replay by thread 0 (items(k)
+// for k < m, in event order), the set back to global memory ascending.  Returns the misses
+// (thread 0).  Every thread of the block calls it.
+template <typename IF>
+__device__ uint64_t far_replay(uint32_t e, const State& s, int64_t* h, uint32_t m, IF&& items, const uint8_t* arena,
+                               uint8_t* acc, uint32_t* tcnt, uint32_t nt, uint32_t* s_cnt) {
+  int64_t* F = s.far + (uint64_t)e * FCAP;
+  const uint32_t n0 = s.far_n[e];
+  for (uint32_t j = threadIdx.x; j < FHS; j += nt) h[j] = INT64_MAX;
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < n0; j += nt) {  // distinct SNs: one CAS each
+    const unsigned long long v = (unsigned long long)F[j];
+    for (uint32_t q = fh_slot(F[j]);; q = (q + 1u) & (FHS - 1u))
+      if (atomicCAS(reinterpret_cast<unsigned long long*>(h + q), (unsigned long long)INT64_MAX, v) ==
+          (unsigned long long)INT64_MAX)
+        break;
+  }
+  __syncthreads();
+  uint64_t miss = 0;
+  if (threadIdx.x == 0) {
+    uint32_t n = n0;
+    for (uint32_t k = 0; k < m; ++k) miss += far_apply(items(k), h, n, arena, acc, tcnt);
+    *s_cnt = n;
+  }
+  __syncthreads();
+  lds_sort(h, FHS, nt);  // the set first (INT64_MAX: free slots last)
+  const uint32_t n1 = *s_cnt;
+  for (uint32_t j = threadIdx.x; j < n1; j += nt) F[j] = h[j];
+  if (threadIdx.x == 0) s.far_n[e] = n1;
+  __threadfence();  // later reads of the set in this kernel (far_extend / far_pull) see it
+  __syncthreads();
+  return miss;
+}
+
+// The global paths' far items (after decide, before the deliveries): sorted by (proxy,
+// event), each proxy's replayed by far_replay.  One workgroup; launched when classify
+// counted candidates (identity batches) or always (expanded batches).
+constexpr uint32_t KF = 1024;
+__global__ __launch_bounds__(KF) void k_far(State s, const uint8_t* arena, uint8_t* acc, uint32_t* tcnt) {
+  __shared__ unsigned long long key[FL_CAP];  // proxy << 44 | event << 13 | item
+  __shared__ int64_t h[FHS];
+  __shared__ uint32_t s_cnt, s_end;
+  const uint64_t nf = s.ctr[C_NFAR];
+  const uint32_t m = (uint32_t)(nf < FL_CAP ? nf : FL_CAP);
+  if (m == 0) return;
+  uint32_t len = 1;
+  while (len < m) len <<= 1;
+  for (uint32_t k = threadIdx.x; k < len; k += KF)
+    key[k] = k < m ? ((unsigned long long)s.fl[k].e << 44) | ((unsigned long long)s.fl[k].p.k << 13) | k : ~0ull;
+  __syncthreads();
+  lds_sort(key, len, KF);
+  uint64_t miss = nf - m;  // items past the list: their samples stay accepted, their SNs unrecorded
+  for (uint32_t b = 0; b < m;) {
+    const uint32_t e = (uint32_t)(key[b] >> 44);
+    if (threadIdx.x == 0) {
+      uint32_t end = b + 1;
+      while (end < m && (uint32_t)(key[end] >> 44) == e) ++end;
+      s_end = end;
+    }
+    __syncthreads();
+    const uint32_t end = s_end;
+    miss += far_replay(e, s, h, end - b, [&](uint32_t k) { return s.fl[key[b + k] & 8191u]; }, arena, acc, tcnt, KF,
+                       &s_cnt);
+    b = end;
+  }
+  if (threadIdx.x == 0 && miss) atomicAdd(reinterpret_cast<unsigned long long*>(s.ctr + C_OVF), (unsigned long long)miss);
+}
+
+// State, after the window pass found nb (the first uncovered SN >= the threshold inside the
+// window, or >= lo + W: every position covered, or the threshold past the window): nb
+// continues through the far set (thread 0; *s_nb), returned to every thread.
+__device__ int64_t far_extend(uint32_t e, const State& s, int64_t lo, int64_t nb, int64_t* s_nb) {
+  const uint32_t n = s.far_n[e];
+  if (n == 0 || nb < lo + (int64_t)W) return nb;
+  if (threadIdx.x == 0) {
+    const int64_t* F = s.far + (uint64_t)e * FCAP;
+    uint32_t a = 0, b = n;
+    while (a < b) {
+      const uint32_t mid = (a + b) >> 1;
+      if (F[mid] < nb) a = mid + 1u; else b = mid;
+    }
+    while (a < n && F[a] == nb) { ++nb; ++a; }
+    *s_nb = nb;
+  }
+  __syncthreads();
+  return *s_nb;
+}
+// ...and after the window was re-anchored at nlo (its bits written): the far SNs the new
+// window spans set their bits there, those below it are dropped (below the new ack_base),
+// the rest move to the front of the set.  stage: FCAP int64 of LDS.
+__device__ void far_pull(uint32_t e, const State& s, int64_t nlo, int64_t* stage, uint32_t nt) {
+  const uint32_t n = s.far_n[e];
+  if (n == 0) return;
+  __syncthreads();  // the window's bits are written
+  int64_t* F = s.far + (uint64_t)e * FCAP;
+  uint32_t* bits = s.bits + (uint64_t)e * WW;
+  const int64_t hi = nlo + (int64_t)W;
+  uint32_t keep = 0;
+  for (uint32_t j = threadIdx.x; j < n; j += nt) {
+    const int64_t v = F[j];
+    stage[j] = v;
+    if (v >= nlo && v < hi) atomicOr(bits + ((uint64_t)(v - nlo) >> 5), 1u << ((uint64_t)(v - nlo) & 31u));
+  }
+  __syncthreads();
+  uint32_t a = 0, b = n;  // first kept: the first >= hi (ascending)
+  while (a < b) {
+    const uint32_t mid = (a + b) >> 1;
+    if (stage[mid] < hi) a = mid + 1u; else b = mid;
+  }
+  keep = n - a;
+  for (uint32_t j = threadIdx.x; j < keep; j += nt) F[j] = stage[a + j];
+  if (threadIdx.x == 0) s.far_n[e] = keep;
+}
+
 // ---- 6 merge ----
 // Batches without GAPs whose proxies' windows are few against their events (T:
 // 16 proxies x 2^17 positions for 1M samples): the batch's sample coverage is
@@ -950,7 +1213,7 @@ __global__ __launch_bounds__(IT) void k_merge(const rtps_record* recs, const uin
 // first uncovered sequence number at or above the threshold found with one block-wide
 // minimum, and the window re-anchored at the new ack_base from the LDS copy.
 __device__ __forceinline__ void state_proxy(uint32_t e, const Scratch& x, const State& s, bool reliable,
-                                            int64_t* ack_out, uint32_t* sh, uint32_t& s_first) {
+                                            int64_t* ack_out, uint32_t* sh, uint32_t& s_first, int64_t* s_nb) {
   const uint32_t tid = threadIdx.x;
   const int64_t lo = s.lo[e];
   int64_t thr = s.base[e];
@@ -983,12 +1246,14 @@ __device__ __forceinline__ void state_proxy(uint32_t e, const Scratch& x, const 
     __syncthreads();
     nb = lo + (int64_t)(s_first != NONE ? s_first : W);
   }
+  nb = far_extend(e, s, lo, nb, s_nb);
   // re-anchor the window at the new ack_base (bits below it are no longer needed)
   const int64_t nlo = nb & ~(int64_t)31;
   if (nlo != lo) {
     const uint64_t shift = (uint64_t)(nlo - lo) >> 5;
     for (uint32_t w = tid; w < WW; w += IT) bits[w] = (w + shift < WW) ? sh[w + shift] : 0u;
   }
+  far_pull(e, s, nlo, reinterpret_cast<int64_t*>(sh), IT);
   if (tid == 0) {
     s.base[e] = nb;
     s.lo[e] = nlo;
@@ -999,11 +1264,12 @@ __device__ __forceinline__ void state_proxy(uint32_t e, const Scratch& x, const 
 // (workgroup 0 also reports the window-overflow count: every decision is made by now)
 __global__ __launch_bounds__(IT) void k_state(uint32_t n_entries, Scratch x, State s, bool reliable, int64_t* ack_out,
                                               uint64_t* ovf_out) {
-  __shared__ uint32_t sh[WW];
+  __shared__ __attribute__((aligned(16))) uint32_t sh[WW];
   __shared__ uint32_t s_first;
+  __shared__ int64_t s_nb;
   const uint32_t e = blockIdx.x;
   if (e >= n_entries) return;
-  state_proxy(e, x, s, reliable, ack_out, sh, s_first);
+  state_proxy(e, x, s, reliable, ack_out, sh, s_first, &s_nb);
   if (threadIdx.x == 0 && e == 0 && ovf_out) *ovf_out = s.ctr[C_OVF];
 }
 // Global identity path, last launch: workgroups [0, ntiles) write the deliveries (k_dwrite;
@@ -1014,12 +1280,13 @@ __global__ __launch_bounds__(IT) void k_dstate(const uint8_t* flag, uint64_t n, 
                                                bool reliable, int64_t* ack_out) {
   __shared__ uint64_t s_w[IT / 64];
   __shared__ uint32_t s_c[IT / 64];
-  __shared__ uint32_t sh[WW];
+  __shared__ __attribute__((aligned(16))) uint32_t sh[WW];
   __shared__ uint32_t s_first;
+  __shared__ int64_t s_nb;
   if (blockIdx.x < ntiles) {
     dwrite_tile(blockIdx.x, flag, n, tcnt, ntiles, x, true, max_out, out, n_out, ctr, ovf_out, nullptr, s_w, s_c);
   } else if (blockIdx.x - ntiles < n_entries) {
-    state_proxy(blockIdx.x - ntiles, x, s, reliable, ack_out, sh, s_first);
+    state_proxy(blockIdx.x - ntiles, x, s, reliable, ack_out, sh, s_first, &s_nb);
   }
 }
 
@@ -1193,8 +1460,9 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
                                               uint32_t n_proxies, State s, uint8_t* acc_out, int64_t* ack_out,
                                               BkIn bk) {
   __shared__ uint32_t sb[WW];                           // the change set window [lo, lo + W)
-  __shared__ uint32_t pres[WW];                         // window offsets of the chunk's samples
-  __shared__ uint32_t h_key[PH], h_min[PH], h_gap[PH];  // window offset -> first sample / GAP position
+  __shared__ __attribute__((aligned(16))) uint32_t pres[WW];  // window offsets of the chunk's samples
+  // window offset -> first sample / GAP position (h_key / h_min: the far replay's hash and keys at the end)
+  __shared__ __attribute__((aligned(16))) uint32_t h_key[PH], h_min[PH], h_gap[PH];
   __shared__ int64_t s_w[PWAVES];
   __shared__ uint32_t s_w32[PWAVES];
   __shared__ uint32_t s_pre[BK ? BK_MAX + 1 : 1];  // BK: the proxy's events before workgroup b's piece
@@ -1203,9 +1471,14 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
   __shared__ uint32_t s_first;
   __shared__ GapE s_gap[GCAP];  // the chunk's GAPs (the first GCAP), one per thread in the GAP phases
   __shared__ uint32_t s_ngap;
+  __shared__ uint32_t s_nfi, s_fcnt;  // far items pushed by this workgroup; the replay's set size
+  __shared__ uint32_t s_fpos[FPX];     // their list positions (the list is shared by every proxy's workgroup)
+  __shared__ int64_t s_nb;
+  static_assert(PH * 4u >= FHS * 8u && PH * 4u >= FPX * 8u && WW * 4u >= FCAP * 8u && FPX <= FL_CAP,
+                "far replay LDS reuse");
   const uint32_t e = blockIdx.x, tid = threadIdx.x;
   if (e >= n_proxies) return;
-  if (tid == 0) s_ngap = 0u;
+  if (tid == 0) { s_ngap = 0u; s_nfi = 0u; }
   const int64_t lo = s.lo[e], base = s.base[e];
   uint32_t* gbits = s.bits + (uint64_t)e * WW;
   for (uint32_t w = tid; w < WW; w += PT) { sb[w] = gbits[w]; pres[w] = 0u; }
@@ -1390,19 +1663,28 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
     if (tid == 0) s_ngap = 0u;  // (every thread read it before the barrier above; the next list is built after barriers)
     // decide (should_ignore_change: rtps_writer_proxy.rs:202-230, reader.rs:693-758)
     int64_t t_run = thr;
+    const int64_t lim = lo + (int64_t)W;
+    auto far = [&](uint32_t j, uint32_t kind) {  // a far item (rare): to the list, replayed at the end
+      const uint32_t pos = far_push(s.ctr, s.fl, FarItem{PEv{v[j], a[j], bwj[j], m[j], kk[j]}, lim, e, kind});
+      const uint32_t c = pos != NONE ? atomicAdd(&s_nfi, 1u) : FPX;
+      if (c < FPX) s_fpos[c] = pos;
+      else ++n_ovf;  // past the list or the replay's capacity: its sample stays accepted
+    };
 #pragma unroll
     for (uint32_t j = 0; j < PPT; ++j) {
       if (f[j] > t_run) t_run = f[j];
+      if ((m[j] & 3u) == EV_GAP && a[j] + (int64_t)(m[j] >> 8) > lim) far(j, FI_GAP);
       if ((m[j] & 3u) != EV_SAMPLE) continue;
       const uint32_t q = q0 + tid * PPT + j;
       uint8_t acc = 0;
       const int64_t vj = v[j];
       if (m[j] & PM_DUP) {
         acc = 1;  // the participant reader's duplicates (reader.rs:712-722)
+        if (vj >= lim) far(j, FI_DUP);
       } else if (vj >= 1 && vj >= t_run) {
         if (slot[j] == NONE) {
-          acc = 1;  // beyond the tracked window: accepted unchecked
-          ++n_ovf;
+          acc = 1;  // beyond the window (vj >= t_run >= lo): the far replay decides
+          far(j, FI_SAMPLE);
         } else {
           const uint32_t off = (uint32_t)(vj - lo);
           acc = (((sb[off >> 5] >> (off & 31u)) & 1u) == 0u && h_min[slot[j]] == q && h_gap[slot[j]] > q) ? 1 : 0;
@@ -1438,6 +1720,21 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
     __syncthreads();
     PST(6);
   }
+  // the far items (this proxy's, from the batch list) replayed in event order against the far set
+  __syncthreads();
+  if (s_nfi) {
+    __threadfence();  // this workgroup's items in the list are visible to all its threads
+    const uint32_t mi = s_nfi < FPX ? s_nfi : FPX;
+    unsigned long long* fk = reinterpret_cast<unsigned long long*>(h_min);  // FPX keys: event << 13 | item
+    for (uint32_t c = tid; c < mi; c += PT) fk[c] = ((unsigned long long)s.fl[s_fpos[c]].p.k << 13) | s_fpos[c];
+    uint32_t len = 1;
+    while (len < mi) len <<= 1;
+    for (uint32_t k = mi + tid; k < len; k += PT) fk[k] = ~0ull;
+    __syncthreads();
+    lds_sort(fk, len, PT);
+    n_ovf += far_replay(e, s, reinterpret_cast<int64_t*>(h_key), mi,
+                        [&](uint32_t k) { return s.fl[fk[k] & 8191u]; }, arena, acc_out, nullptr, PT, &s_fcnt);
+  }
   if (n_ovf) atomicAdd(reinterpret_cast<unsigned long long*>(s.ctr + C_OVF), (unsigned long long)n_ovf);
   // state (as k_state): ack_base = first sequence number >= threshold outside the change set
   int64_t nb = run_thr;
@@ -1457,9 +1754,11 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
     }
     nb = lo + (int64_t)(s_first != NONE ? s_first : W);
   }
+  nb = far_extend(e, s, lo, nb, &s_nb);
   const int64_t nlo = nb & ~(int64_t)31;
   const uint64_t shift = (uint64_t)(nlo - lo) >> 5;
   for (uint32_t w = tid; w < WW; w += PT) gbits[w] = (w + shift < WW) ? sb[w + shift] : 0u;
+  far_pull(e, s, nlo, reinterpret_cast<int64_t*>(pres), PT);
   if (tid == 0) {
     s.base[e] = nb;
     s.lo[e] = nlo;
@@ -1475,6 +1774,7 @@ __global__ void k_init_state(uint32_t n, State s) {
     s.base[e] = 1;  // RtpsWriterProxy::new: ack_base = SequenceNumber::new(1)
     s.lo[e] = 0;
     s.hbc[e] = 0;
+    s.far_n[e] = 0;
   }
 }
 __global__ void k_finish(const uint64_t* ctr, uint64_t* ovf) { if (ovf) *ovf = ctr[C_OVF]; }
@@ -1580,7 +1880,8 @@ int rtps_ingest_proxy_stamps(uint64_t* host, uint64_t n) {
 }
 
 static void free_state(IngestState* s) {
-  void* p[] = {s->st.base, s->st.lo, s->st.hbc, s->st.bits, s->st.fc, s->st.dbits, s->st.seg_b, s->st.seg_e};
+  void* p[] = {s->st.base, s->st.lo, s->st.hbc, s->st.bits, s->st.fc, s->st.dbits, s->st.seg_b, s->st.seg_e,
+               s->st.far, s->st.far_n, s->st.fl};
   for (void* q : p) if (q) (void)hipFree(q);
   uint64_t* ctr = s->st.ctr;
   s->st = State{};
@@ -1621,7 +1922,8 @@ static bool grow_state(IngestState* s, uint32_t n, hipStream_t st) {
             hipMalloc(&m.hbc, ncap * 4ull) == hipSuccess && hipMalloc(&m.bits, (uint64_t)ncap * WW * 4) == hipSuccess &&
             hipMalloc(&m.fc, (uint64_t)ncap * W * 8) == hipSuccess && hipMalloc(&m.seg_b, ncap * 4ull) == hipSuccess &&
             hipMalloc(&m.dbits, (uint64_t)ncap * WW * 4) == hipSuccess &&
-            hipMalloc(&m.seg_e, ncap * 4ull) == hipSuccess;
+            hipMalloc(&m.seg_e, ncap * 4ull) == hipSuccess && hipMalloc(&m.far, (uint64_t)ncap * FCAP * 8) == hipSuccess &&
+            hipMalloc(&m.far_n, ncap * 4ull) == hipSuccess && hipMalloc(&m.fl, FL_CAP * sizeof(FarItem)) == hipSuccess;
   ok = ok && hipMemsetAsync(m.bits, 0, (uint64_t)ncap * WW * 4, st) == hipSuccess &&
        hipMemsetAsync(m.dbits, 0, (uint64_t)ncap * WW * 4, st) == hipSuccess &&
        hipMemsetAsync(m.fc, 0xff, (uint64_t)ncap * W * 8, st) == hipSuccess;
@@ -1631,14 +1933,17 @@ static bool grow_state(IngestState* s, uint32_t n, hipStream_t st) {
     ok = hipMemcpyAsync(m.base, o.base, e * 8, hipMemcpyDeviceToDevice, st) == hipSuccess &&
          hipMemcpyAsync(m.lo, o.lo, e * 8, hipMemcpyDeviceToDevice, st) == hipSuccess &&
          hipMemcpyAsync(m.hbc, o.hbc, e * 4, hipMemcpyDeviceToDevice, st) == hipSuccess &&
-         hipMemcpyAsync(m.bits, o.bits, e * WW * 4, hipMemcpyDeviceToDevice, st) == hipSuccess;
+         hipMemcpyAsync(m.bits, o.bits, e * WW * 4, hipMemcpyDeviceToDevice, st) == hipSuccess &&
+         hipMemcpyAsync(m.far, o.far, e * FCAP * 8, hipMemcpyDeviceToDevice, st) == hipSuccess &&
+         hipMemcpyAsync(m.far_n, o.far_n, e * 4, hipMemcpyDeviceToDevice, st) == hipSuccess;
   }
   ok = ok && hipStreamSynchronize(st) == hipSuccess;
   s->st = m;
   s->ecap = ncap;
   State dead = o;
   dead.ctr = nullptr;
-  void* p[] = {dead.base, dead.lo, dead.hbc, dead.bits, dead.fc, dead.dbits, dead.seg_b, dead.seg_e};
+  void* p[] = {dead.base, dead.lo, dead.hbc, dead.bits, dead.fc, dead.dbits, dead.seg_b, dead.seg_e,
+               dead.far, dead.far_n, dead.fl};
   for (void* q : p) if (q) (void)hipFree(q);
   if (!ok) { free_state(s); return false; }
   return true;
@@ -1750,6 +2055,7 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
   if (ident && !grow_vscratch(s, max, st)) return RTPS_RX_ENOMEM;
   if (!ident && s->vcap == 0 && !grow_vscratch(s, 1, st)) return RTPS_RX_ENOMEM;
   const bool reliable = !(flags & RTPS_INGEST_BEST_EFFORT);
+  const FarSrc fs{records, dgram_off};
   if (++s->epoch == 0xffffffffu) {  // keys would wrap: clear the first-cover table
     if (hipMemsetAsync(s->st.fc, 0xff, (uint64_t)s->ecap * W * 8, st) != hipSuccess) return RTPS_RX_EHIP;
     s->epoch = 1;
@@ -1927,10 +2233,12 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
     const bool fc_merge = n_gap == 0 && s->path == 3;  // (the first-cover-key merge: test path)
     if (n_gap == 0 && !fc_merge)
       hipLaunchKernelGGL(k_decide_t<true>, dim3(ntiles), dim3(IT), 0, st, nev, acc_cap, x, S, acc, have_hb, s->epoch,
-                         x.sel);
+                         x.sel, fs);
     else
       hipLaunchKernelGGL(k_decide_t<false>, dim3(ntiles), dim3(IT), 0, st, nev, acc_cap, x, S, acc, have_hb, s->epoch,
-                         x.sel);
+                         x.sel, fs);
+    if (s->hctr[C_FARC])  // samples / GAPs past some window: their replay (fixes accept[] and the tile counts)
+      hipLaunchKernelGGL(k_far, dim3(1), dim3(KF), 0, st, S, arena, acc, x.sel);
     if (fc_merge)
       hipLaunchKernelGGL(k_fcmerge, dim3((uint32_t)hmin((uint64_t)t.n_proxies * W / IT, 8192)), dim3(IT), 0, st,
                          t.n_proxies, S, s->epoch);
@@ -1947,9 +2255,12 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
       hipLaunchKernelGGL(k_marks_g, dim3(gv), dim3(IT), 0, st, records, arena, dgram_off, nev, x, S, s->epoch);
   }
   // identity batches decide straight into accept[] (event i = record i: max slots, cleared past n)
-  if (acc_cap && !per_proxy)
+  if (acc_cap && !per_proxy) {
     hipLaunchKernelGGL(k_decide, dim3((uint32_t)hmin((acc_cap + IT - 1) / IT, 8192)), dim3(IT), 0, st, nev, acc_cap,
-                       x, S, acc, have_hb, s->epoch);
+                       x, S, acc, have_hb, s->epoch, fs);
+    // the far replay (expanded batches: classify cannot tell their proxies' windows; an empty list returns at once)
+    hipLaunchKernelGGL(k_far, dim3(1), dim3(KF), 0, st, S, arena, acc, (uint32_t*)nullptr);
+  }
   const bool state_pass = t.n_proxies && !per_proxy;  // k_state copies the overflow count out, else the select does
   deliver(acc, acc_cap, x, ident, out, st, S.ctr, !state_pass);
   if (!ident)

@@ -1378,11 +1378,60 @@ void rtps_parse_emit_kernel(KParams p, uint32_t n_tiles, const u32x4* items, con
   __syncthreads();
   const uint32_t total = s_nit[WAVES];
   const u32x4* tslab = items + (size_t)tile * WAVES * CAPW;
+#ifdef RTPS_EM_SORT
+  // tuning variant: the tile's items bucketed by kind in LDS first, so that a wave's lanes
+  // run the same per-kind reader (the slab order interleaves kinds)
+  constexpr uint32_t NCL = 8, RND = WAVES * CAPW / EMT, SLOTS = RND * (EMT / 64);
+  __shared__ u32x4 s_it[WAVES * CAPW];
+  __shared__ uint32_t s_cc[NCL][SLOTS];
+  {
+    const uint64_t lt = lane ? (~0ull >> (64u - lane)) : 0ull;
+    u32x4 mine[RND];
+    uint32_t cls[RND], rk[RND];
+#pragma unroll
+    for (uint32_t r = 0; r < RND; ++r) {
+      const uint32_t k = tid + r * EMT;
+      cls[r] = NCL;
+      if (k < total) {
+        const uint32_t w = (k >= s_nit[1]) + (k >= s_nit[2]) + (k >= s_nit[3]);
+        mine[r] = tslab[w * CAPW + (k - s_nit[w])];
+        mine[r][1] |= w << 14;  // (j < 2^14: a datagram holds fewer submessages)
+        const uint32_t kd = mine[r][1] >> 24;
+        cls[r] = kd == RTPS_DATA ? 0u : kd == RTPS_DATA_FRAG ? 1u : kd == RTPS_HEARTBEAT ? 2u : kd == RTPS_GAP ? 3u
+               : kd == RTPS_ACKNACK ? 4u : kd == RTPS_NACK_FRAG ? 5u : kd == RTPS_HEARTBEAT_FRAG ? 6u : 7u;
+      }
+#pragma unroll
+      for (uint32_t c = 0; c < NCL; ++c) {
+        const uint64_t m = __ballot(cls[r] == c);
+        if (cls[r] == c) rk[r] = (uint32_t)__popcll(m & lt);
+        if (lane == 0) s_cc[c][r * (EMT / 64) + wave] = (uint32_t)__popcll(m);
+      }
+    }
+    __syncthreads();
+    if (tid < NCL) {  // class c's slots: exclusive prefix, after every earlier class
+      uint32_t before = 0;
+      for (uint32_t c = 0; c < tid; ++c)
+        for (uint32_t q = 0; q < SLOTS; ++q) before += s_cc[c][q];
+      for (uint32_t q = 0; q < SLOTS; ++q) { const uint32_t v = s_cc[tid][q]; s_cc[tid][q] = before; before += v; }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t r = 0; r < RND; ++r)
+      if (cls[r] < NCL) s_it[s_cc[cls[r]][r * (EMT / 64) + wave] + rk[r]] = mine[r];
+    __syncthreads();
+  }
+  for (uint32_t k = tid; k < total; k += EMT) {
+    const u32x4 it = s_it[k];
+    const uint32_t w = (it[1] >> 14) & 3u, jmask = 0x3fffu;
+    const uint32_t o = it[0] & 0xffffu, src_off = it[0] >> 16;
+#else
   for (uint32_t k = tid; k < total; k += EMT) {
     const uint32_t w = (k >= s_nit[1]) + (k >= s_nit[2]) + (k >= s_nit[3]);
     const u32x4 it = tslab[w * CAPW + (k - s_nit[w])];
+    const uint32_t jmask = 0xffffu;
     const uint32_t o = it[0] & 0xffffu, src_off = it[0] >> 16;
-    const uint32_t j = it[1] & 0xffffu, d = w * 64u + ((it[1] >> 16) & 63u), kind = it[1] >> 24;
+#endif
+    const uint32_t j = it[1] & jmask, d = w * 64u + ((it[1] >> 16) & 63u), kind = it[1] >> 24;
     const uint32_t rb = s_rbase[d];
     if (rb == 0xffffffffu) continue;  // the datagram was dropped after this item (or has no records)
     s.base = s_doff[d];

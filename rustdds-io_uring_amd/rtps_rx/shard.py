@@ -231,13 +231,18 @@ def _hip():
         _HIP = ctypes.CDLL("libamdhip64.so")
         _HIP.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
         _HIP.hipMemcpy.restype = ctypes.c_int
+        _HIP.hipDeviceSynchronize.restype = ctypes.c_int
     return _HIP
 
 
 def dev_copy(dst, src, nbytes):
-    """hipMemcpy(dst, src, n, hipMemcpyDefault) between raw pointers (host or device)."""
+    """hipMemcpy(dst, src, n, hipMemcpyDefault) between raw pointers (host or device), ordered
+    after all work queued on the device and before what follows: the copy goes on the null
+    stream, which does not wait for non-blocking streams (torch's, the context's)."""
     if nbytes:
-        rc = _hip().hipMemcpy(ctypes.c_void_p(dst), ctypes.c_void_p(src), nbytes, 4)
+        H = _hip()
+        rc = H.hipDeviceSynchronize() or H.hipMemcpy(ctypes.c_void_p(dst), ctypes.c_void_p(src), nbytes, 4) \
+            or H.hipDeviceSynchronize()
         if rc != 0:
             raise RuntimeError(f"hipMemcpy failed ({rc})")
 

@@ -96,6 +96,12 @@ bmo = exp[gi, 52:54].contiguous().view(torch.int16).reshape(-1).to(torch.int64) 
 src = off_t[exp[gi, 0:4].contiguous().view(torch.int32).reshape(-1).to(torch.int64)] + bmo
 dst = goff[gi] + bmo
 bm_ok = torch.equal(arena[src], oarena[dst]) and torch.equal(arena[src + 3], oarena[dst + 3])
+if not org_ok:
+    want = torch.nonzero(items).reshape(-1)
+    bad = torch.nonzero((origin & 0xFFFFFFFF) != want).reshape(-1)
+    i = int(bad[0].item()) if len(bad) else -1
+    print(f"  {len(bad)} origins differ, first {i}: got {int(origin[i].item()):#x} want {int(want[i].item())}; "
+          f"{len(origin)} vs {len(want)}", flush=True)
 if not body_ok:
     bad = torch.nonzero((got[:, 4:] != exp_d[:, 4:]).any(dim=1)).reshape(-1)
     i = int(bad[0].item())

@@ -6,7 +6,7 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 3
   -k "mixed or chained or lds or soup or edge or reader_sets or full_size or launch_choice or spec_hint" > gpurun_out/r4_item_pytest.log 2>&1; rc=$?
 tail -3 gpurun_out/r4_item_pytest.log
 [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" gpurun_out/r4_item_pytest.log | head -20; exit $rc; }
-timeout -k 10 600 python -u -m pytest tests/test_topic_gpu.py tests/test_cdr_gpu.py tests/test_ingest_gpu.py -x -v --timeout 300 --timeout-method thread > gpurun_out/r4_ing_pytest.log 2>&1; rc=$?
+timeout -k 10 900 python -u -m pytest tests/test_shard_gpu.py tests/test_topic_gpu.py tests/test_cdr_gpu.py tests/test_ingest_gpu.py -x -v --timeout 300 --timeout-method thread > gpurun_out/r4_ing_pytest.log 2>&1; rc=$?
 tail -3 gpurun_out/r4_ing_pytest.log
 [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" gpurun_out/r4_ing_pytest.log | head -20; exit $rc; }
 for mp in 2 0; do

@@ -211,15 +211,18 @@ def table(n_prefix=3, n_writer=3):
     return pack_match_table(ents), [g for g, _ in ents]
 
 
-def stream(n, seed, sn_hi=60, n_prefix=4, n_writer=3, keys=None):
+def stream(n, seed, sn_hi=60, n_prefix=4, n_writer=3, keys=None, sn_draw=None, gap_len=None):
     """n datagrams of reliable-reader traffic with every case the proxies have to
     replay in order: duplicate and out-of-order DATA, KEY and KEY_HASH samples,
     DATA whose payload decision fails, HEARTBEATs with stale counts and any
     firstSN (<= 0 too), valid and invalid GAPs with ranges and bitmaps, big- and
     little-endian submessages, writers outside the match table, and writer
     submessages after an INFO_DST to another participant (not passed).
-    keys: writer entity ids to draw from (default writer_key(0 .. n_writer-1))."""
+    keys: writer entity ids to draw from (default writer_key(0 .. n_writer-1)).
+    sn_draw(rng): the SN of a DATA, a HEARTBEAT's firstSN, a GAP's gapStart (default
+    uniform in [-1, sn_hi)); gap_len(rng, start): a GAP's gapList.base (default start + [-3, 8))."""
     rng = np.random.default_rng(seed)
+    draw = sn_draw or (lambda g: int(g.integers(-1, sn_hi)))
     keys = [writer_key(k) for k in range(n_writer)] if keys is None else list(keys)
     out = []
     for _ in range(n):
@@ -232,7 +235,7 @@ def stream(n, seed, sn_hi=60, n_prefix=4, n_writer=3, keys=None):
             le = bool(rng.random() < 0.8)
             x = rng.random()
             if x < 0.55:
-                sn = int(rng.integers(-1, sn_hi))
+                sn = draw(rng)
                 y = rng.random()
                 if y < 0.08:
                     subs.append(data_sub(wk, sn, le, key=True))
@@ -243,11 +246,11 @@ def stream(n, seed, sn_hi=60, n_prefix=4, n_writer=3, keys=None):
                 else:
                     subs.append(data_sub(wk, sn, le))
             elif x < 0.75:
-                first = int(rng.integers(-2, sn_hi))
+                first = int(rng.integers(-2, sn_hi)) if sn_draw is None else draw(rng)
                 subs.append(hb_sub(wk, first, first + int(rng.integers(0, 20)), int(rng.integers(-1, 12)), le))
             else:
-                start = int(rng.integers(-1, sn_hi))
-                base = start + int(rng.integers(-3, 8))
+                start = draw(rng)
+                base = start + int(rng.integers(-3, 8)) if gap_len is None else gap_len(rng, start)
                 nb = int(rng.integers(0, 70))
                 bits = [bool(b) for b in rng.random(nb) < 0.4]
                 subs.append(gap_sub(wk, start, base, bits, le))

@@ -129,16 +129,98 @@ def test_completed_datafrag_samples(rx):
     assert n > 10
 
 
-def test_window_overflow_counted(rx):
+def _far_draw(g):
+    """SNs for the far-set tests: near ones, the window's edge, three anchors far past the
+    window (duplicates included), so that samples, HEARTBEAT firstSNs and GAPs land beyond it."""
+    import rtps_rx
+    W = rtps_rx.INGEST_WINDOW
+    x = g.random()
+    if x < 0.5:
+        return int(g.integers(-1, 80))
+    if x < 0.6:
+        return W - 3 + int(g.integers(0, 8))
+    return int(g.choice([W + 40, 2 * W + 7, 5 * W])) + int(g.integers(0, 40))
+
+
+def _far_gap_len(g, start):
+    return start + (int(g.integers(30, 120)) if g.random() < 0.1 else int(g.integers(-3, 8)))
+
+
+def test_far_sample_exact(rx):
+    """a sample further than RTPS_INGEST_WINDOW ahead of the window is
+    decided exactly (the far set, rtps_writer_proxy.rs:202-224), not accepted unchecked: a
+    re-sent far SN is a duplicate in the same batch and in the next one."""
+    import rtps_rx
     tbl = pack_match_table([(R.PREFIXES[0] + R.writer_key(0), 0)])
     rx.set_match_table(tbl)
-    import rtps_rx
+    ing = oracle.HistoryIngest(tbl)
     w = R.writer_key(0)
     far = 1 + rtps_rx.INGEST_WINDOW + 5
-    d = [R.datagram(R.PREFIXES[0], [R.data_sub(w, 1), R.data_sub(w, far), R.data_sub(w, 2)])]
+    d = [R.datagram(R.PREFIXES[0], [R.data_sub(w, 1), R.data_sub(w, far), R.data_sub(w, 2), R.data_sub(w, far)])]
+    acc, dels, ack = _batch(rx, ing, tbl, d, "far, batch 1")
+    assert dels["rec_idx"].tolist() == [0, 1, 2] and ack.tolist() == [3]
+    d = [R.datagram(R.PREFIXES[0], [R.data_sub(w, far), R.data_sub(w, far + 1), R.data_sub(w, 3)])]
+    acc, dels, ack = _batch(rx, ing, tbl, d, "far, batch 2")
+    assert dels["rec_idx"].tolist() == [1, 2] and ack.tolist() == [4]
+
+
+def test_far_window_filled_up_to_the_far_set(rx):
+    """The window covered up to its end: all_ackable_before continues through the far set
+    (advance_ack_base, rtps_writer_proxy.rs:338-355), and the re-anchored window takes the
+    far SNs it now spans."""
+    import rtps_rx
+    W = rtps_rx.INGEST_WINDOW
+    tbl = pack_match_table([(R.PREFIXES[0] + R.writer_key(0), 0)])
+    rx.set_match_table(tbl)
+    ing = oracle.HistoryIngest(tbl)
+    w = R.writer_key(0)
+    far = [W + 1, W + 2, W + 3, W + 5, 2 * W + 9, 3 * W]
+    _batch(rx, ing, tbl, [R.datagram(R.PREFIXES[0], [R.data_sub(w, v) for v in far])], "far first")
+    # a GAP covering [1, W + 1): the window fills, ack_base runs through W+1..W+3, stops at W+4
+    _, _, ack = _batch(rx, ing, tbl, [R.datagram(R.PREFIXES[0], [R.gap_sub(w, 1, W + 1, [])])], "gap fills")
+    assert ack.tolist() == [W + 4]
+    d = [R.datagram(R.PREFIXES[0], [R.data_sub(w, v) for v in (W + 4, W + 5, 2 * W + 9, 2 * W + 8, 3 * W)])]
+    _, dels, _ = _batch(rx, ing, tbl, d, "after the pull")
+    assert dels["rec_idx"].tolist() == [0, 3]
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_far_stream_across_batches(rx, seed):
+    """Random reliable traffic whose SNs, HEARTBEAT firstSNs and GAPs reach past the window
+    (three anchors up to 5 W ahead, duplicates, GAP ranges crossing the window's end),
+    batch after batch: bit-exact with the oracle's unbounded change sets, nothing counted."""
+    tbl, _ = R.table()
+    rx.set_match_table(tbl)
+    ing = oracle.HistoryIngest(tbl)
+    dgrams = R.stream(5000, 100 + seed, sn_draw=_far_draw, gap_len=_far_gap_len)
+    for a, b in [(0, 1), (1, 1500), (1500, 1501), (1501, 5000)]:
+        _batch(rx, ing, tbl, dgrams[a:b], f"far seed {seed} {a}:{b}")
+
+
+def test_far_reader_sets(rx):
+    """The same with several readers per record (expanded events) and the SPDP participant
+    reader (DUPLICATES_OK: its far samples are all accepted and recorded)."""
+    rd = R.a15_readers()
+    rx.set_readers(rd)
+    ing = oracle.HistoryIngest(rd)
+    dgrams = R.stream(4000, 77, sn_draw=_far_draw, gap_len=_far_gap_len,
+                      keys=[R.writer_key(0), R.writer_key(1), R.writer_key(2), R.BUILTIN_KIND_KEY])
+    for a, b in [(0, 2000), (2000, 4000)]:
+        _batch(rx, ing, rd, dgrams[a:b], f"far a15 {a}:{b}")
+
+
+def test_far_set_capacity_counted(rx):
+    """Past FCAP (1024) far SNs of one proxy the set is full: the rest are accepted unchecked
+    and counted in n_window_overflow (the decisions still equal the reference's here)."""
+    import rtps_rx
+    tbl = pack_match_table([(R.PREFIXES[0] + R.writer_key(0), 0)])
+    rx.set_match_table(tbl)
+    w = R.writer_key(0)
+    far = 2 * rtps_rx.INGEST_WINDOW
+    d = [R.datagram(R.PREFIXES[0], [R.data_sub(w, far + 3 * k + j) for j in range(3)]) for k in range(500)]
     arena, off, ln = oracle.pack(d)
     _, acc, accepted, ack, ovf, _ = rx.ingest_batch(arena, off, ln, 1)
-    assert accepted["rec_idx"].tolist() == [0, 1, 2] and ovf == 1 and ack.tolist() == [3]
+    assert len(accepted) == 1500 and ovf == 1500 - 1024 and ack.tolist() == [1]
 
 
 def test_empty_and_eventless_batches(rx):
