@@ -56,6 +56,8 @@
 #include "rtps_sort.h"
 #include <string.h>
 
+#include <atomic>
+#include <chrono>
 #include <new>
 
 #include "rtps_ingest.h"
@@ -73,7 +75,13 @@ enum : uint8_t { EV_NONE = 0, EV_SAMPLE = 1, EV_HB = 2, EV_GAP = 3 };
 // counters: window overflow, selected HEARTBEATs, selected deliveries, records of the batch, then
 // the HEARTBEAT / GAP / event / proxy-less sample counts in 64 slot quads (one atomic per block, spread: no hot address)
 // (C_FARC: classify's far-SN candidates, the host's cue for k_far; C_NFAR: far items appended)
-enum { C_OVF = 0, C_NSEL, C_NDEL, C_NREC, C_FARC, C_NFAR, C_SPREAD, C_COUNT = C_SPREAD + 4 * 64 };
+// (C_DONE: classify workgroups finished, for the count signal to the host)
+enum { C_OVF = 0, C_NSEL, C_NDEL, C_NREC, C_FARC, C_NFAR, C_DONE, C_DTOP = C_DONE + 8, C_SPREAD,
+       C_COUNT = C_SPREAD + 4 * 64 };
+// the batch's counts as classify's last workgroup signals them to pinned host memory:
+// [0] = the batch's tag (written last), HEARTBEAT / GAP / event / proxy-less sample counts,
+// records, far-item candidates
+enum { SIG_TAG = 0, SIG_HB, SIG_GAP, SIG_EV, SIG_FREE, SIG_NREC, SIG_FARC, SIG_WORDS = 8 };
 // event metadata: reader slot | flags << 16 (EVF_*)
 constexpr uint32_t EVF_DUP_OK = 1u << 16;  // RTPS_TARGET_DUPLICATES_OK reader
 constexpr uint32_t EVF_FREE = 1u << 17;    // sample without a proxy (writer kind not user-defined)
@@ -119,6 +127,7 @@ struct Scratch {
   // per record
   uint32_t* fidx;   // completed DataFrag sample of a record, or NONE
   uint64_t* fmask;  // the target-set entries (bit k: entry k) whose assembler completed it at the record
+  uint8_t* fall;    // a writer-keyed sample (every entry) completed at the record
   uint32_t* rcnt;   // events of the record (non-identity batches), then their exclusive scan (roff)
   uint32_t* roff;
   uint32_t* rset;   // target set, record event kind, sample / event sn
@@ -155,9 +164,10 @@ struct State {
 // ---- 1 classify ----
 // A per-reader sample (reader_slot != RTPS_NO_MATCH) goes to that reader only: its
 // entry of the completing record's target set (handle_datafrag_msg runs per reader,
-// reader.rs:563-636); a writer-keyed sample to every entry.
+// reader.rs:563-636; entries 0..63 of a set: the mask's bits); a writer-keyed sample to
+// every entry (fall).
 __global__ __launch_bounds__(IT) void k_fidx(const rtps_frag_sample* frag, const uint64_t* n_frag, uint64_t max_frag,
-                                             uint64_t max, uint32_t* fidx, uint64_t* fmask, ReaderDev t,
+                                             uint64_t max, uint32_t* fidx, uint64_t* fmask, uint8_t* fall, ReaderDev t,
                                              const rtps_record* recs) {
   const uint64_t nf = n_frag ? (*n_frag < max_frag ? *n_frag : max_frag) : 0;
   for (uint64_t s = (uint64_t)blockIdx.x * IT + threadIdx.x; s < nf; s += (uint64_t)gridDim.x * IT) {
@@ -165,6 +175,7 @@ __global__ __launch_bounds__(IT) void k_fidx(const rtps_frag_sample* frag, const
     if (f.status == RTPS_FRAG_SHORT || f.rec_idx >= max) continue;
     fidx[f.rec_idx] = (uint32_t)s;  // (samples of one record share the writer and SN)
     uint64_t bit = ~0ull;
+    if (f.reader_slot == RTPS_NO_MATCH) fall[f.rec_idx] = 1u;
     if (f.reader_slot != RTPS_NO_MATCH) {
       const uint32_t* d = reinterpret_cast<const uint32_t*>(recs + f.rec_idx);
       uint32_t r2 = 0;
@@ -176,6 +187,13 @@ __global__ __launch_bounds__(IT) void k_fidx(const rtps_frag_sample* frag, const
     }
     atomicOr(reinterpret_cast<unsigned long long*>(fmask + f.rec_idx), (unsigned long long)bit);
   }
+}
+
+// Does entry `pos` of the record's target set take its completed DataFrag sample?  fm: the
+// entries whose assembler completed it (bits 0..63), all: a writer-keyed sample (every entry);
+// a record without one: fm = ~0, all.
+__device__ __forceinline__ bool frag_takes(uint64_t fm, bool all, uint32_t pos) {
+  return pos < 64u ? ((fm >> pos) & 1ull) != 0ull : all;
 }
 
 // Does (record event kind, target x) make an event?  Sets ent / meta.
@@ -256,6 +274,8 @@ struct FastOut {
   uint32_t* bk_cnt;  // BUCKET: per (workgroup, proxy) proxied events, workgroup-major: [block * n_proxies + proxy]
   uint32_t* bk_lst;  //         the proxy's first position inside the workgroup's region
   uint32_t sets_lds; // classify: set_first / set_ent staged in LDS behind the hash tables
+  uint64_t* hsig;     // pinned host words (SIG_*) the last workgroup writes, or null
+  uint64_t tag;
 };
 // bytes of the target sets' LDS image (set_first words, then 8-B entries)
 __host__ __device__ inline uint32_t sets_lds_bytes(const ReaderDev& t) { return (t.n_sets + 1u) * 4u + t.n_ent * 8u; }
@@ -312,7 +332,8 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
   __shared__ uint32_t s_part[IT / 64];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const uint64_t n = *n_rec < max ? *n_rec : max;
-  if (blockIdx.x == 0 && tid == 0) ctr[C_NREC] = n;
+  if (blockIdx.x == 0 && tid == 0)  // (write-through: the signalling workgroup reads it)
+    __hip_atomic_store(ctr + C_NREC, (uint64_t)n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (FAST && !BUCKET)
     for (uint32_t e = blockIdx.x * IT + tid; e < fo.n_seg; e += gridDim.x * IT) { fo.seg_b[e] = 0u; fo.seg_e[e] = 0u; }
   if (BUCKET)
@@ -387,11 +408,12 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
     uint32_t ent = NONE, meta = 0;
     if (ev != EV_NONE) {
       const uint32_t b = sfirst[set], e = sfirst[set + 1];
-      const uint64_t fm = (frag && x.fidx[i] != NONE) ? x.fmask[i] : ~0ull;
+      const bool fs = frag && x.fidx[i] != NONE;
+      const uint64_t fm = fs ? x.fmask[i] : ~0ull;
+      const bool fa = !fs || x.fall[i] != 0u;
       for (uint32_t k = b; k < e; ++k) {
         uint32_t en, me;
-        if (((fm >> ((k - b) & 63u)) & 1ull) && (k - b < 64u || fm == ~0ull) &&
-            ev_of(ev, sent[k], user_kind, reliable, en, me)) {
+        if (frag_takes(fm, fa, k - b) && ev_of(ev, sent[k], user_kind, reliable, en, me)) {
           ++cnt;
           ent = en;
           meta = me;
@@ -410,11 +432,7 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
         x.evt[i] = evi;
         x.ent[i] = ent;
         x.esn[i] = sn;
-#ifndef RTPS_EXP_NOMARK
         if (MARK && evi == EV_SAMPLE && ent != NONE) {  // k_marks_d's first-cover key
-#else
-        if (false) {
-#endif
           const int64_t lo = st.lo[ent];
           if (sn >= lo && sn < lo + (int64_t)W)
             atomicMin(reinterpret_cast<unsigned long long*>(st.fc + (uint64_t)ent * W) + (uint64_t)(sn - lo),
@@ -569,6 +587,38 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
     atomicAdd(reinterpret_cast<unsigned long long*>(ctr + C_SPREAD + 4u * (blockIdx.x & 63u) + tid),
               (unsigned long long)s_n[tid]);
   if (MARK && nfar) atomicAdd(reinterpret_cast<unsigned long long*>(ctr + C_FARC), (unsigned long long)nfar);
+  if (fo.hsig) {
+    // The last workgroup to finish signals the batch's counts to the host.  The counts are
+    // agent-scope atomics (performed past the per-XCD L2s); each workgroup's are drained
+    // (vmcnt) before its ticket, the last ticket (its returned value) reads them with atomics:
+    // no L2 write-back fence per workgroup (MI355X_MICROARCH.md, inter-workgroup visibility).
+    // (tickets sharded 8 ways, then one top counter: one word takes about 88 returning adds
+    // per microsecond, fewer than a classify grid's workgroups finish)
+    __shared__ uint32_t s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const uint32_t sh = blockIdx.x & 7u, in_shard = (gridDim.x - sh + 7u) >> 3;
+      const uint32_t shards = gridDim.x < 8u ? gridDim.x : 8u;
+      s_last = atomicAdd(reinterpret_cast<unsigned long long*>(ctr + C_DONE + sh), 1ull) == in_shard - 1u &&
+               atomicAdd(reinterpret_cast<unsigned long long*>(ctr + C_DTOP), 1ull) == shards - 1u;
+    }
+    __syncthreads();
+    if (s_last && tid < 64) {  // one wave: the sums, then the pinned words, the tag last
+      uint64_t v = 0;
+      if (tid < 4) {
+        for (uint32_t k = 0; k < 64; ++k)
+          v += atomicAdd(reinterpret_cast<unsigned long long*>(ctr + C_SPREAD + 4u * k + tid), 0ull);
+      } else if (tid == 4) {
+        v = atomicAdd(reinterpret_cast<unsigned long long*>(ctr + C_NREC), 0ull);
+      } else if (tid == 5) {
+        v = atomicAdd(reinterpret_cast<unsigned long long*>(ctr + C_FARC), 0ull);
+      }
+      if (tid < 6) __hip_atomic_store(fo.hsig + SIG_HB + tid, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (tid == 0) __hip_atomic_store(fo.hsig + SIG_TAG, fo.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 // 1b: lane per record writes its events at roff[i] (set order = EntityId order of the readers)
@@ -582,10 +632,12 @@ __global__ __launch_bounds__(IT) void k_expand(ReaderDev t, uint64_t n, uint32_t
     const uint32_t set = x.rset[i];
     uint32_t k = x.roff[i];
     const int64_t sn = x.rsn[i];
-    const uint64_t fm = (with_frag && x.fidx[i] != NONE) ? x.fmask[i] : ~0ull;
+    const bool fs = with_frag && x.fidx[i] != NONE;
+    const uint64_t fm = fs ? x.fmask[i] : ~0ull;
+    const bool fa = !fs || x.fall[i] != 0u;
     for (uint32_t j = t.set_first[set], b = j, e = t.set_first[set + 1]; j < e; ++j) {
       uint32_t en, me;
-      if (!((fm >> ((j - b) & 63u)) & 1ull) || (j - b >= 64u && fm != ~0ull)) continue;
+      if (!frag_takes(fm, fa, j - b)) continue;
       if (!ev_of(ev, t.set_ent[j], user_kind, reliable, en, me)) continue;
       x.evt[k] = ev;
       x.ent[k] = en;
@@ -837,11 +889,34 @@ __device__ __forceinline__ uint64_t block_sum64(uint64_t v, uint64_t* s_w) {
 // no decision of the pass reads a bit the pass sets for another event; the positions of
 // the other samples lie below the new ack_base (v < 1 or below a HEARTBEAT threshold) or
 // are set already, so k_merge's extra bits there change nothing k_state reads.
-template <bool MERGE>
+// MERGE 2 (GAP-free batches whose proxies' windows are few against their events, T): the
+// merge is the first-cover keys instead: workgroups [ntiles, grid) scan every proxy's window
+// of keys and write each word's positions that carry this batch's epoch into dbits (every
+// word written, zeros too), which state_proxy ORs into the window and clears.  The decisions
+// read `bits` only, so the scan runs beside them; it replaces k_merge's per-sample wave_or.
+constexpr uint32_t FCM_POS = 16384;  // window positions per scanning workgroup
+static_assert(FCM_POS % (IT * 2) == 0 && W % FCM_POS == 0, "whole waves of 64 positions");
+template <int MERGE>
 __global__ __launch_bounds__(IT) void k_decide_t(uint64_t n, uint64_t cap, Scratch x, State s, uint8_t* acc_out,
-                                                 bool reliable, uint32_t epoch, uint32_t* tcnt, FarSrc fs) {
+                                                 bool reliable, uint32_t epoch, uint32_t* tcnt, FarSrc fs,
+                                                 uint32_t ntiles) {
   __shared__ uint64_t s_w[IT / 64];
-  const uint64_t b0 = (uint64_t)blockIdx.x * DT + threadIdx.x * DPT;
+  // (MERGE 2: the key-scanning workgroups come first, so that they run beside the decisions)
+  const uint32_t nfcm = MERGE == 2 ? gridDim.x - ntiles : 0u;
+  if (MERGE == 2 && blockIdx.x < nfcm) {
+    const uint64_t p0 = (uint64_t)blockIdx.x * FCM_POS;  // a multiple of W / FCM_POS per proxy
+    const uint32_t tag = 0xffffffffu - epoch, lane = threadIdx.x & 63u;
+#pragma unroll 4
+    for (uint32_t r = 0; r < FCM_POS / IT; ++r) {
+      const uint64_t pos = p0 + r * IT + threadIdx.x;
+      const uint64_t m = __ballot((uint32_t)(s.fc[pos] >> 32) == tag);
+      if (lane == 0) s.dbits[pos >> 5] = (uint32_t)m;
+      if (lane == 32) s.dbits[pos >> 5] = (uint32_t)(m >> 32);
+    }
+    return;
+  }
+  const uint32_t blk = blockIdx.x - nfcm;  // the delivery tile
+  const uint64_t b0 = (uint64_t)blk * DT + threadIdx.x * DPT;
   uint32_t w[DPT / 4];
 #pragma unroll
   for (uint32_t q = 0; q < DPT / 4; ++q) w[q] = 0u;
@@ -854,11 +929,7 @@ __global__ __launch_bounds__(IT) void k_decide_t(uint64_t n, uint64_t cap, Scrat
     const uint8_t a = decide_one(b0 + j, n, x, s, reliable, epoch, fs, e, off, merge);
     w[j >> 2] |= (uint32_t)a << (8u * (j & 3u));
     c += a;
-#ifdef RTPS_EXP_NOMERGE
-    if (false)
-#else
-    if (MERGE)
-#endif
+    if (MERGE == 1)
       wave_or(s.bits, merge ? s.bits + (uint64_t)e * WW + (off >> 5) : s.bits, 1u << (off & 31u), merge);
   }
   if (b0 + DPT <= cap) {
@@ -871,7 +942,7 @@ __global__ __launch_bounds__(IT) void k_decide_t(uint64_t n, uint64_t cap, Scrat
     for (uint64_t i = b0; i < cap; ++i) acc_out[i] = (uint8_t)(w[(i - b0) >> 2] >> (8u * ((i - b0) & 3u)));
   }
   const uint64_t t = block_sum64(c, s_w);
-  if (threadIdx.x == 0) tcnt[blockIdx.x] = (uint32_t)t;
+  if (threadIdx.x == 0) tcnt[blk] = (uint32_t)t;
 }
 
 __global__ __launch_bounds__(IT) void k_dcount(const uint8_t* flag, uint64_t n, uint32_t* tcnt) {
@@ -1212,8 +1283,10 @@ __global__ __launch_bounds__(IT) void k_merge(const rtps_record* recs, const uin
 // The proxy's window is read once into LDS (16 words per thread, all loads in flight), the
 // first uncovered sequence number at or above the threshold found with one block-wide
 // minimum, and the window re-anchored at the new ack_base from the LDS copy.
+// fcm: the batch's coverage is in dbits (k_decide_t<2>): OR it into the window, clear it
 __device__ __forceinline__ void state_proxy(uint32_t e, const Scratch& x, const State& s, bool reliable,
-                                            int64_t* ack_out, uint32_t* sh, uint32_t& s_first, int64_t* s_nb) {
+                                            int64_t* ack_out, uint32_t* sh, uint32_t& s_first, int64_t* s_nb,
+                                            bool fcm = false) {
   const uint32_t tid = threadIdx.x;
   const int64_t lo = s.lo[e];
   int64_t thr = s.base[e];
@@ -1228,7 +1301,15 @@ __device__ __forceinline__ void state_proxy(uint32_t e, const Scratch& x, const 
   uint32_t* bits = s.bits + (uint64_t)e * WW;
   const u32x4* b4 = reinterpret_cast<const u32x4*>(bits);
   u32x4* sh4 = reinterpret_cast<u32x4*>(sh);
-  for (uint32_t q = tid; q < WW / 4; q += IT) sh4[q] = b4[q];
+  if (fcm) {
+    u32x4* d4 = reinterpret_cast<u32x4*>(s.dbits + (uint64_t)e * WW);
+    for (uint32_t q = tid; q < WW / 4; q += IT) {
+      sh4[q] = b4[q] | d4[q];
+      d4[q] = u32x4{0u, 0u, 0u, 0u};
+    }
+  } else {
+    for (uint32_t q = tid; q < WW / 4; q += IT) sh4[q] = b4[q];
+  }
   if (tid == 0) s_first = NONE;
   __syncthreads();
   // advance_ack_base: the first sequence number >= thr outside the change set
@@ -1277,7 +1358,7 @@ __global__ __launch_bounds__(IT) void k_state(uint32_t n_entries, Scratch x, Sta
 __global__ __launch_bounds__(IT) void k_dstate(const uint8_t* flag, uint64_t n, const uint32_t* tcnt, uint32_t ntiles,
                                                Scratch x, uint64_t max_out, rtps_delivery* out, uint64_t* n_out,
                                                const uint64_t* ctr, uint64_t* ovf_out, uint32_t n_entries, State s,
-                                               bool reliable, int64_t* ack_out) {
+                                               bool reliable, int64_t* ack_out, bool fcm) {
   __shared__ uint64_t s_w[IT / 64];
   __shared__ uint32_t s_c[IT / 64];
   __shared__ __attribute__((aligned(16))) uint32_t sh[WW];
@@ -1286,7 +1367,7 @@ __global__ __launch_bounds__(IT) void k_dstate(const uint8_t* flag, uint64_t n, 
   if (blockIdx.x < ntiles) {
     dwrite_tile(blockIdx.x, flag, n, tcnt, ntiles, x, true, max_out, out, n_out, ctr, ovf_out, nullptr, s_w, s_c);
   } else if (blockIdx.x - ntiles < n_entries) {
-    state_proxy(blockIdx.x - ntiles, x, s, reliable, ack_out, sh, s_first, &s_nb);
+    state_proxy(blockIdx.x - ntiles, x, s, reliable, ack_out, sh, s_first, &s_nb, fcm);
   }
 }
 
@@ -1826,6 +1907,8 @@ struct IngestState {
   hipEvent_t hnev_ev = nullptr;
   bool hnev_ready = false;
   uint64_t last_nev = 0;      // events of the last batch whose counts were read
+  uint64_t* hsig = nullptr;    // pinned, coherent: classify's count signal (SIG_*)
+  uint64_t sig_tag = 0;
   uint32_t* bk_cnt = nullptr;  // proxy bucketing: per (classify workgroup, proxy) events and first positions
   uint32_t* bk_lst = nullptr;
   uint64_t bkcap = 0;
@@ -1889,9 +1972,10 @@ static void free_state(IngestState* s) {
   s->ecap = 0;
 }
 static void free_rscratch(IngestState* s) {
-  void* p[] = {s->x.fidx, s->x.fmask, s->x.rcnt, s->x.roff, s->x.rset, s->x.rkind, s->x.rsn};
+  void* p[] = {s->x.fidx, s->x.fmask, s->x.fall, s->x.rcnt, s->x.roff, s->x.rset, s->x.rkind, s->x.rsn};
   for (void* q : p) if (q) (void)hipFree(q);
   s->x.fmask = nullptr;
+  s->x.fall = nullptr;
   s->x.fidx = nullptr; s->x.rcnt = nullptr; s->x.roff = nullptr; s->x.rset = nullptr; s->x.rkind = nullptr;
   s->x.rsn = nullptr;
   s->rcap = 0;
@@ -1902,7 +1986,7 @@ static void free_vscratch(IngestState* s) {
   for (void* q : p) if (q) (void)hipFree(q);
   Scratch keep = s->x;
   s->x = Scratch{};
-  s->x.fidx = keep.fidx; s->x.fmask = keep.fmask; s->x.rcnt = keep.rcnt; s->x.roff = keep.roff; s->x.rset = keep.rset;
+  s->x.fidx = keep.fidx; s->x.fmask = keep.fmask; s->x.fall = keep.fall; s->x.rcnt = keep.rcnt; s->x.roff = keep.roff; s->x.rset = keep.rset;
   s->x.rkind = keep.rkind; s->x.rsn = keep.rsn;
   s->tmp = nullptr;
   s->tmp_bytes = 0;
@@ -1956,6 +2040,7 @@ static bool grow_rscratch(IngestState* s, uint64_t max, hipStream_t st) {
   Scratch& x = s->x;
   const uint64_t n = max;
   bool ok = hipMalloc(&x.fidx, n * 4) == hipSuccess && hipMalloc(&x.fmask, n * 8) == hipSuccess &&
+            hipMalloc(&x.fall, n) == hipSuccess &&
             hipMalloc(&x.rcnt, n * 4) == hipSuccess &&
             hipMalloc(&x.roff, n * 4) == hipSuccess && hipMalloc(&x.rset, n * 4) == hipSuccess &&
             hipMalloc(&x.rkind, n) == hipSuccess && hipMalloc(&x.rsn, n * 8) == hipSuccess;
@@ -2012,6 +2097,7 @@ IngestState* rtps_ingest_state_new(int device) {
   s->st.ctr = s->ctr_base;
   if (hipHostMalloc(&s->hctr, C_COUNT * 8, hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc(&s->hctr2, C_COUNT * 8, hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc(&s->hsig, SIG_WORDS * 8, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
       hipEventCreateWithFlags(&s->hnev_ev, hipEventDisableTiming) != hipSuccess) {
     rtps_ingest_state_free(s);
     return nullptr;
@@ -2029,6 +2115,7 @@ void rtps_ingest_state_free(IngestState* s) {
   if (s->ctr_base) (void)hipFree(s->ctr_base);
   if (s->hctr) (void)hipHostFree(s->hctr);
   if (s->hctr2) (void)hipHostFree(s->hctr2);
+  if (s->hsig) (void)hipHostFree(s->hsig);
   if (s->hnev_ev) (void)hipEventDestroy(s->hnev_ev);
   delete s;
 }
@@ -2071,11 +2158,12 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
   bool ok = true;
   const bool with_frag = frag && n_frag && max_frag;
   if (with_frag) ok = ok && hipMemsetAsync(x.fidx, 0xff, max * 4, st) == hipSuccess &&
-                     hipMemsetAsync(x.fmask, 0, max * 8, st) == hipSuccess;
+                     hipMemsetAsync(x.fmask, 0, max * 8, st) == hipSuccess &&
+                     hipMemsetAsync(x.fall, 0, max, st) == hipSuccess;
   if (!ok) return RTPS_RX_EHIP;
   if (with_frag)
     hipLaunchKernelGGL(k_fidx, dim3((uint32_t)hmin((max_frag + IT - 1) / IT, 4096)), dim3(IT), 0, st, frag, n_frag,
-                       max_frag, max, x.fidx, x.fmask, t, records);
+                       max_frag, max, x.fidx, x.fmask, x.fall, t, records);
   uint32_t lds = rt_fits_lds(t) ? rt_lds_bytes(t.gmask + 1u, t.emask + 1u) : 0u;
   // the target sets join the hash tables in LDS when both fit the tables' own limit
   const bool sets_lds = lds && lds + sets_lds_bytes(t) <= RT_LDS_MAX;
@@ -2094,7 +2182,9 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
   // classify workgroups exceed its LDS tables (or path 4: the radix sort, tests)
   const uint64_t nblk = (max + CHR - 1) / CHR;
   const bool bucket = fast && t.n_proxies <= PB_MAX && nblk <= BK_MAX && s->path != 4;
-  FastOut fo{nullptr, nullptr, arena, dgram_off, S.seg_b, S.seg_e, s->ecap, nullptr, nullptr, sets_lds ? 1u : 0u};
+  // (the paths that wait for the counts: classify signals them to pinned memory, the host spins)
+  FastOut fo{nullptr, nullptr, arena, dgram_off, S.seg_b, S.seg_e, s->ecap, nullptr, nullptr, sets_lds ? 1u : 0u,
+             fast ? nullptr : s->hsig, ++s->sig_tag};
   if (fast) {
     if (!grow_pscratch(s, bucket ? nblk * CHR : max, st)) return RTPS_RX_ENOMEM;
     fo.pev = s->pev;
@@ -2138,18 +2228,24 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
     s->hnev_ready = true;
     return hipGetLastError() == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP;
   }
-  // the batch's record / HEARTBEAT / GAP / event counts size the rest: one small read-back
-  if (hipMemcpyAsync(s->hctr, S.ctr, C_COUNT * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
-      hipStreamSynchronize(st) != hipSuccess)
-    return RTPS_RX_EHIP;
-  uint64_t n_hb = 0, n_gap = 0, n_ev = 0, n_free = 0;
-  for (uint32_t k = 0; k < 64; ++k) {
-    n_hb += s->hctr[C_SPREAD + 4 * k];
-    n_gap += s->hctr[C_SPREAD + 4 * k + 1];
-    n_ev += s->hctr[C_SPREAD + 4 * k + 2];
-    n_free += s->hctr[C_SPREAD + 4 * k + 3];
+  // the batch's record / HEARTBEAT / GAP / event counts size the rest: classify's last workgroup
+  // writes them to pinned memory, the host spins on the tag (no copy, no interrupt-driven wait);
+  // a wait past the limit falls back to a stream sync (a failed launch surfaces there)
+  if (hipGetLastError() != hipSuccess) return RTPS_RX_EHIP;
+  {
+    volatile uint64_t* hs = s->hsig;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 0; hs[SIG_TAG] != fo.tag; ++spin) {
+      if ((spin & 1023u) == 1023u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
+        if (hipStreamSynchronize(st) != hipSuccess || hs[SIG_TAG] != fo.tag) return RTPS_RX_EHIP;
+        break;
+      }
+      __builtin_ia32_pause();
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
   }
-  const uint64_t n_rec = s->hctr[C_NREC];
+  const uint64_t n_hb = s->hsig[SIG_HB], n_gap = s->hsig[SIG_GAP], n_ev = s->hsig[SIG_EV], n_free = s->hsig[SIG_FREE];
+  const uint64_t n_rec = s->hsig[SIG_NREC], farc = s->hsig[SIG_FARC];
   // events live at [0, nev): record slots in identity batches, the expanded list otherwise
   uint64_t nev = ident ? n_rec : n_ev;
   if (!ident) {
@@ -2230,23 +2326,26 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
       hipLaunchKernelGGL(k_marks_g, dim3(gv), dim3(IT), 0, st, records, arena, dgram_off, nev, x, S, s->epoch);
     }
     const uint32_t ntiles = (uint32_t)((acc_cap + DT - 1) / DT);
-    const bool fc_merge = n_gap == 0 && s->path == 3;  // (the first-cover-key merge: test path)
-    if (n_gap == 0 && !fc_merge)
-      hipLaunchKernelGGL(k_decide_t<true>, dim3(ntiles), dim3(IT), 0, st, nev, acc_cap, x, S, acc, have_hb, s->epoch,
-                         x.sel, fs);
-    else
-      hipLaunchKernelGGL(k_decide_t<false>, dim3(ntiles), dim3(IT), 0, st, nev, acc_cap, x, S, acc, have_hb, s->epoch,
-                         x.sel, fs);
-    if (s->hctr[C_FARC])  // samples / GAPs past some window: their replay (fixes accept[] and the tile counts)
-      hipLaunchKernelGGL(k_far, dim3(1), dim3(KF), 0, st, S, arena, acc, x.sel);
+    // GAP-free batches merge in decide: from the first-cover keys when the proxies' windows are
+    // few against the events (T; path 3 forces it), else by the samples' wave_or
+    const bool fc_merge = n_gap == 0 && (s->path == 3 || (s->path != 1 && (uint64_t)t.n_proxies * W <= 4ull * nev));
+    const uint32_t nfcm = fc_merge ? (uint32_t)((uint64_t)t.n_proxies * W / FCM_POS) : 0u;
     if (fc_merge)
-      hipLaunchKernelGGL(k_fcmerge, dim3((uint32_t)hmin((uint64_t)t.n_proxies * W / IT, 8192)), dim3(IT), 0, st,
-                         t.n_proxies, S, s->epoch);
-    else if (n_gap)
+      hipLaunchKernelGGL(k_decide_t<2>, dim3(ntiles + nfcm), dim3(IT), 0, st, nev, acc_cap, x, S, acc, have_hb,
+                         s->epoch, x.sel, fs, ntiles);
+    else if (n_gap == 0)
+      hipLaunchKernelGGL(k_decide_t<1>, dim3(ntiles), dim3(IT), 0, st, nev, acc_cap, x, S, acc, have_hb, s->epoch,
+                         x.sel, fs, ntiles);
+    else
+      hipLaunchKernelGGL(k_decide_t<0>, dim3(ntiles), dim3(IT), 0, st, nev, acc_cap, x, S, acc, have_hb, s->epoch,
+                         x.sel, fs, ntiles);
+    if (farc)  // samples / GAPs past some window: their replay (fixes accept[] and the tile counts)
+      hipLaunchKernelGGL(k_far, dim3(1), dim3(KF), 0, st, S, arena, acc, x.sel);
+    if (n_gap)
       hipLaunchKernelGGL(k_merge, dim3(gv), dim3(IT), 0, st, records, arena, dgram_off, nev, x, S, true);
     hipLaunchKernelGGL(k_dstate, dim3(ntiles + t.n_proxies), dim3(IT), 0, st, acc, acc_cap, x.sel, ntiles, x,
                        out->max_accepted, out->accepted, out->n_accepted, S.ctr, out->n_window_overflow, t.n_proxies,
-                       S, have_hb, out->ack_base);
+                       S, have_hb, out->ack_base, fc_merge);
     return hipGetLastError() == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP;
   }
   if (nev && !per_proxy) {

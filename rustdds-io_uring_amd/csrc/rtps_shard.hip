@@ -248,17 +248,36 @@ __global__ __launch_bounds__(ST) void shard_scatter(PackArgs a) {
     if (lane == 63) { wcnt[wave][d] = (uint32_t)__popcll(m); wbyt[wave][d] = incl; }
   }
   __syncthreads();
+  uint64_t pos = 0, boff = 0;
+  bool slot = true;
   if (o != NONE) {
-    uint64_t pos = a.hscan[2 * ((uint64_t)blockIdx.x * n + o)] + rank;
-    uint64_t boff = a.hscan[2 * ((uint64_t)blockIdx.x * n + o) + 1] + bex;
+    pos = a.hscan[2 * ((uint64_t)blockIdx.x * n + o)] + rank;
+    boff = a.hscan[2 * ((uint64_t)blockIdx.x * n + o) + 1] + bex;
     for (uint32_t v = 0; v < wave; ++v) { pos += wcnt[v][o]; boff += wbyt[v][o]; }
-    const bool slot = pos < a.cap && boff + size <= a.bcap;
+    slot = pos < a.cap && boff + size <= a.bcap;
+  }
+  // each destination's first spilled item and byte: the minimum over the wave's spilled
+  // lanes, one atomic per (wave, destination) (a batch that mostly spills would otherwise
+  // serialise on two addresses)
+  for (uint32_t d = 0; d < n; ++d) {
+    const bool sp = o == d && !slot;
+    const uint64_t mm = __ballot(sp);
+    if (mm == 0) continue;
+    uint64_t mp = sp ? pos : ~0ull, mb = sp ? boff : ~0ull;
+#pragma unroll
+    for (uint32_t sft = 1; sft < 64; sft <<= 1) {
+      const uint64_t yp = __shfl_xor(mp, sft, 64), yb = __shfl_xor(mb, sft, 64);
+      mp = yp < mp ? yp : mp;
+      mb = yb < mb ? yb : mb;
+    }
+    if (lane == (uint32_t)__builtin_ctzll(mm)) {
+      atomicMin((unsigned long long*)&a.counts[d].cut, (unsigned long long)mp);
+      atomicMin((unsigned long long*)&a.counts[d].cut_bytes, (unsigned long long)mb);
+    }
+  }
+  if (o != NONE) {
     shard_item* it = slot ? a.slots + (uint64_t)o * a.cap + pos : a.spill + sbase[o] + pos;
     uint8_t* bd = slot ? a.blob + (uint64_t)o * a.bcap + boff : a.bspill + bsbase[o] + boff;
-    if (!slot) {
-      atomicMin((unsigned long long*)&a.counts[o].cut, (unsigned long long)pos);
-      atomicMin((unsigned long long*)&a.counts[o].cut_bytes, (unsigned long long)boff);
-    }
     const uint32_t tail = kind | (w[1] & 0xff000000u) >> 16 | (w[7] & 0xffff0000u);  // kind, flags, route, pk
     uint4* q = reinterpret_cast<uint4*>(it);
     if (kind == RTPS_DATA) {

@@ -5,10 +5,13 @@ Alive (dds/ddsdata.rs:45-50).  InlineQos::status_info (elements/inline_qos.rs:27
 takes the first PID_STATUS_INFO or StatusInfo::empty(); StatusInfo::read_from reads
 four u8 (:139-147); StatusInfo::change_kind (:164-175).
 
-Known answers below are derived by hand from those lines (no reference fixture
-covers the change kind: parity of this field is pinned by the restatement only);
-the CPU test checks the oracle against them, the GPU test the device against the
-oracle on the same datagrams, both byte orders."""
+Known answers below are derived by hand from those lines; the StatusInfo bytes the
+reference's own test uses (inline_qos.rs:198-238, `inline_qos_status_info`: the four
+octets 00 00 00 03 read as Disposed | Unregistered under both CDR_LE and CDR_BE) are
+the "si both" case, in both byte orders of the submessage, whose change kind follows
+from StatusInfo::change_kind (:164-175: Disposed first).  The CPU test checks the
+oracle against them, the GPU test the device against the oracle on the same
+datagrams, both byte orders."""
 import struct
 
 import numpy as np
@@ -40,6 +43,9 @@ def _data(le, dflag, kflag, params=None, payload=b"\x00\x01\x00\x00abcd"):
     return bytes([0x15, flags]) + struct.pack(e + "H", len(body)) + body
 
 
+REF_SI_BYTES = bytes([0x00, 0x00, 0x00, 0x03])  # inline_qos.rs:207, 227 (LE and BE alike: four octets)
+
+
 def _si(flags, n=4):
     return (b"\x00\x00\x00" + bytes([flags]))[:n] if n <= 4 else b"\x00\x00\x00" + bytes([flags]) + bytes(n - 4)
 
@@ -52,7 +58,8 @@ CASES = [
     ("key, qos without si", 0, 1, [(0x0F, b"\x01\x02\x03\x04")], PK_KEY, CK_ALIVE),    # StatusInfo::empty()
     ("key, si disposed", 0, 1, [(0x71, _si(1))], PK_KEY, CK_NOT_ALIVE_DISPOSED),
     ("key, si unregistered", 0, 1, [(0x71, _si(2))], PK_KEY, CK_NOT_ALIVE_UNREGISTERED),
-    ("key, si both", 0, 1, [(0x71, _si(3))], PK_KEY, CK_NOT_ALIVE_DISPOSED),            # Disposed first
+    # the reference's vector (inline_qos.rs:198-238): 00 00 00 03 = Disposed | Unregistered; Disposed first
+    ("key, si both", 0, 1, [(0x71, REF_SI_BYTES)], PK_KEY, CK_NOT_ALIVE_DISPOSED),
     ("key, si filtered", 0, 1, [(0x71, _si(4))], PK_KEY, CK_ALIVE),
     ("key, si unknown bits", 0, 1, [(0x71, _si(0xF8 | 2))], PK_KEY, CK_NOT_ALIVE_UNREGISTERED),  # truncated bits
     ("key, si short", 0, 1, [(0x71, _si(2, 3))], PK_KEY, CK_NOT_ALIVE_DISPOSED),       # read error -> None
