@@ -99,7 +99,7 @@ def pmc_profile(workload):
 
 
 KERNEL_NAMES = {1: "rtps_parse_spec_kernel", 2: "rtps_parse_chain_kernel", 3: "rtps_parse_lds_kernel",
-                4: "rtps_parse_item_kernel"}
+                4: "rtps_parse_item_kernel", 5: "rtps_parse_rslab_kernel"}
 
 
 def _time_phases(rx, arena, off_t, ln_t, n, outs, stream, steps, phases):
@@ -125,7 +125,7 @@ def time_dominant_kernel(rx, arena, off_t, ln_t, n, outs, stream, steps):
     slower of the item walk and the record pass."""
     ms, which = _time_phases(rx, arena, off_t, ln_t, n, outs, stream, steps, 1)
     kname, extra = KERNEL_NAMES[which], {}
-    if which == 4:
+    if which in (4, 5):
         ms2, _ = _time_phases(rx, arena, off_t, ln_t, n, outs, stream, steps, 2)
         extra = {"item_kernel_ms": ms, "scan_plus_emit_ms": ms2}
     for _ in range(2):  # full launches restore the per-launch bookkeeping

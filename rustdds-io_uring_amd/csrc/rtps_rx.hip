@@ -1475,6 +1475,184 @@ void rtps_parse_emit_kernel(KParams p, uint32_t n_tiles, const u32x4* items, con
 }
 
 // ---------------------------------------------------------------------------
+// E' / S / W': the record-slab pass (mixed pass 3).  Like the item pass, but the
+// walk itself builds each record (sub_body<true> + rec_finish, the windows it
+// already holds) and appends the finished 64-B record to its wave's slab with its
+// (record index in its datagram, lane); W' only copies every slab record to tile
+// prefix + datagram's first record + j.  The record pass no longer re-gathers any
+// datagram bytes: its loads are the slab's, coalesced.
+#ifndef RTPS_RS_CAPR
+#define RTPS_RS_CAPR 384u
+#endif
+constexpr uint32_t CAPR = RTPS_RS_CAPR;  // records per wave slab (C3 averages 243 per 64 datagrams)
+
+__device__ uint32_t rslab_walk(const KParams& p, const Src& s, const uint32_t* H, uint32_t L, uint32_t dgram_idx,
+                               uint32_t lane, u32x4* rslab, uint32_t* mslab, uint32_t* tslab, uint32_t& wpos,
+                               uint32_t& nrec) {
+  nrec = 0;
+  if (L > RTPS_MAX_DATAGRAM) return RTPS_DGRAM_TOO_LONG;
+  const uint32_t MAGIC_RTPS = 0x53505452u, MAGIC_RTPX = 0x58505452u;
+  if (L < 20u) {  // message_receiver.rs:238-251
+    if (L >= 16u && H[0] == MAGIC_RTPS && (H[2] >> 8) == 0x534444u && H[3] == 0x474e4950u) return RTPS_DGRAM_PING;
+    return RTPS_DGRAM_SHORT;
+  }
+  if (H[0] != MAGIC_RTPS) return H[0] == MAGIC_RTPX ? RTPS_DGRAM_RTPX : RTPS_DGRAM_BAD_MAGIC;
+  if ((H[1] & 0xffu) > 2u) return RTPS_DGRAM_BAD_HEADER;
+  Interp st{H[2], H[3], H[4], true, false, 0u, 0u};  // handle_parsed_message_2 (:289-295)
+  const uint64_t lt = lane ? (~0ull >> (64u - lane)) : 0ull;
+  uint32_t o = 20;
+  Win Wn;  // the next submessage's window, loaded before this record's stores (as walk<true>)
+  head_win(H, Wn);
+  while (o < L) {
+    const uint32_t rem = L - o;
+    if (rem < 4u) return RTPS_DGRAM_SUBMSG_ERR;
+    Win W = Wn;
+    if (o != 20u && (W.w[0] & 0xffu) == RTPS_DATA_FRAG) W.w[8] = ld4(s, o + 32u);
+    const uint32_t kind = W.w[0] & 0xffu, flags = (W.w[0] >> 8) & 0xffu;
+    const bool le = (flags & 1u) != 0u;
+    const uint32_t eff = eff_len(kind, e16(W.w[0], 1, le), rem);
+    if (4u + eff > rem) return RTPS_DGRAM_SUBMSG_ERR;
+    if (o + 4u + eff < L) load_win_pf(s, o + 4u + eff, Wn);
+    Rec R;
+    rec_clear(R);
+    SubOut so;
+    if (!sub_body<true>(s, W, kind, flags, le, o + 4u, eff, R, so)) return RTPS_DGRAM_SUBMSG_ERR;
+    interp_update(p, st, W, kind, flags, le);
+    const bool em = so.cls != 0u;
+    uint32_t tgt = RTPS_NO_TARGET;
+    if (em) {
+      R.d[0] = dgram_idx;
+      R.d[1] = o | (kind << 16) | (flags << 24);
+      tgt = rec_finish(p, R, so, kind, st);
+    }
+    const uint64_t m = __ballot(em);
+    if (em) {
+      const uint32_t pos = wpos + (uint32_t)__popcll(m & lt);
+      if (pos < CAPR) {
+        rec_store(reinterpret_cast<rtps_record*>(rslab + (size_t)pos * 4u), R);
+        mslab[pos] = nrec | (lane << 16);
+        if (p.target_out) tslab[pos] = tgt;
+      }
+      nrec++;
+    }
+    wpos += (uint32_t)__popcll(m);
+    o += 4u + eff;
+  }
+  return RTPS_DGRAM_OK;
+}
+
+#ifndef RTPS_RS_WAVES_PER_SIMD
+#define RTPS_RS_WAVES_PER_SIMD 6  // (8 spills the record and both windows to scratch)
+#endif
+__global__ __launch_bounds__(TILE, RTPS_RS_WAVES_PER_SIMD) void rtps_parse_rslab_kernel(KParams p, uint32_t n_tiles,
+                                                                                      uint32_t k_spec, u32x4* recs,
+                                                                                      uint32_t* meta, uint32_t* tgts,
+                                                                                      uint32_t* wcnt) {
+  __shared__ uint32_t s_wave_sum[WAVES], s_wave_bad[WAVES];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t tile = blockIdx.x;
+  mt_stage(p);
+  TileCtx t;
+  load_tile(p, tile, t);
+  __syncthreads();  // the match table's LDS image (rec_finish)
+  const size_t w0 = (size_t)(tile * WAVES + wave) * CAPR;
+  uint32_t cnt = 0, wpos = 0, st = RTPS_DGRAM_OK;
+  if (t.valid) {
+    if (!t.addressable) st = RTPS_DGRAM_TOO_LONG;
+    else st = rslab_walk(p, t.s, t.H, t.L, t.i, lane, recs + w0 * 4u, meta + w0, tgts + w0, wpos, cnt);
+    if (st != RTPS_DGRAM_OK) cnt = 0;
+  }
+  uint32_t wtot = wpos, wsum = cnt;
+#pragma unroll
+  for (uint32_t d = 32; d >= 1; d >>= 1) {
+    const uint32_t y = __shfl_xor(wtot, d, 64);
+    wtot = y > wtot ? y : wtot;
+    wsum += __shfl_xor(wsum, d, 64);
+  }
+  const uint64_t bad = __ballot(t.valid && cnt != k_spec);
+  if (lane == 0) {
+    s_wave_sum[wave] = wsum;
+    s_wave_bad[wave] = bad != 0ull;
+    wcnt[tile * WAVES + wave] = wtot > CAPR ? WCNT_OVERFLOW : wtot;
+  }
+  Scratch x = scratch_of(p.scratch, n_tiles);
+  if (t.valid) {
+    p.status[t.i] = (uint8_t)st;
+    x.dcount[t.i] = (uint16_t)cnt;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t agg = 0, mixed = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < WAVES; ++w) { agg += s_wave_sum[w]; mixed |= s_wave_bad[w]; }
+    x.info[tile] = agg | INFO_NONSPEC | (mixed ? INFO_MIXED : 0u);
+  }
+}
+
+// W': the slab records to their places (a wave whose slab overflowed walks its datagrams)
+__global__ __launch_bounds__(EMT) void rtps_parse_rcopy_kernel(KParams p, uint32_t n_tiles, const u32x4* recs,
+                                                               const uint32_t* meta, const uint32_t* tgts,
+                                                               const uint32_t* wcnt, const uint64_t* tprefix) {
+  __shared__ uint32_t s_rbase[TILE];  // tile-local first record of each datagram (NONE: no records)
+  __shared__ uint32_t s_wsum[WAVES], s_nit[WAVES + 1];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const bool pro = tid < TILE;
+  const uint32_t tile = blockIdx.x;
+  mt_stage(p);  // (the overflow walk's rec_finish)
+  Scratch x = scratch_of(p.scratch, n_tiles);
+  const uint64_t prefix = tprefix[tile];
+  const uint32_t wc = pro ? wcnt[tile * WAVES + wave] : 0u;
+  const uint32_t i = tile * TILE + tid;
+  const bool valid = pro && i < p.n;
+  const uint32_t cnt = valid ? (uint32_t)x.dcount[i] : 0u;
+  const uint32_t incl = wave_incl_scan(cnt, lane);
+  if (pro && lane == 63) s_wsum[wave] = incl;
+  if (pro && lane == 0) s_nit[wave] = (wc & WCNT_OVERFLOW) ? 0u : wc;
+  __syncthreads();
+  uint32_t wave_off = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < WAVES; ++w)
+    if (w < wave) wave_off += s_wsum[w];
+  const uint32_t local = wave_off + incl - cnt;
+  if (valid && p.rec_begin) p.rec_begin[i] = (uint32_t)(prefix + local);
+  if (pro) s_rbase[tid] = cnt ? local : 0xffffffffu;
+  if (pro && (wc & WCNT_OVERFLOW)) {  // the records did not fit the slab: walk the wave's datagrams
+    s_rbase[tid] = 0xffffffffu;
+    TileCtx t;
+    load_tile(p, tile, t);
+    if (t.valid && cnt) {
+      uint32_t n2;
+      walk<true>(p, t.s, t.H, t.L, t.i, prefix + local, n2);
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t a = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < WAVES; ++w) { const uint32_t v = s_nit[w]; s_nit[w] = a; a += v; }
+    s_nit[WAVES] = a;
+  }
+  __syncthreads();
+  const uint32_t total = s_nit[WAVES];
+  const size_t t0 = (size_t)tile * WAVES * CAPR;
+  for (uint32_t k = tid; k < total; k += EMT) {
+    const uint32_t w = (k >= s_nit[1]) + (k >= s_nit[2]) + (k >= s_nit[3]);
+    const size_t e = t0 + (size_t)w * CAPR + (k - s_nit[w]);
+    const uint32_t m = meta[e];
+    const uint32_t rb = s_rbase[w * 64u + (m >> 16)];
+    if (rb == 0xffffffffu) continue;  // the datagram was dropped after this record
+    const uint64_t r = prefix + rb + (m & 0xffffu);
+    if (r < p.max_records) {
+      const u32x4* q = recs + e * 4u;
+      u32x4* d = reinterpret_cast<u32x4*>(p.records + r);
+      const u32x4 a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
+      d[0] = a0; d[1] = a1; d[2] = a2; d[3] = a3;
+      if (p.target_out) p.target_out[r] = tgts[e];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // D  rtps_parse_lds_kernel: mixed traffic through LDS tiles.
 // A lane walking its datagram's submessage chain in global memory waits on one
 // dependent load per submessage, and the kind-divergent body readers serialise
@@ -2111,6 +2289,10 @@ struct rtps_rx_ctx {
   uint32_t* it_wcnt = nullptr;    // item pass: items per wave slab [tiles * WAVES]
   uint64_t* it_prefix = nullptr;  // item pass: tile record prefixes [tiles]
   uint32_t it_tiles = 0;          // tiles the item-pass buffers are sized for
+  u32x4* rs_recs = nullptr;       // record-slab pass: wave slabs of records [tiles * WAVES * CAPR * 4]
+  uint32_t* rs_meta = nullptr;    //   (j | lane << 16) per slab record
+  uint32_t* rs_tgt = nullptr;     //   target set per slab record
+  uint32_t rs_tiles = 0;
   // per-reader DataFrag assembly (frag_x_*): Lifespans by reader slot, the batch's receive time, the expansion
   int64_t* life = nullptr;        // [65536] device, NO_LIFESPAN where none
   bool any_life = false;
@@ -2139,7 +2321,7 @@ int rtps_rx_create(const rtps_rx_config* cfg, rtps_rx_ctx** out_ctx) {
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) { delete c; return RTPS_RX_EHIP; }
   c->stream = c->own_stream;
   if (const char* e = getenv("RTPS_RX_MIXED_PASS"))  // A/B measurements
-    c->mixed_pass = (e[0] == '1') ? 1u : (e[0] == '0') ? 0u : 2u;
+    c->mixed_pass = (e[0] == '1') ? 1u : (e[0] == '0') ? 0u : (e[0] == '3') ? 3u : 2u;
   {
     int cus = 0, per_cu = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess && cus > 0 &&
@@ -2183,7 +2365,7 @@ int rtps_rx_destroy(rtps_rx_ctx* c) {
   rtps_ingest_state_free(c->ingest);
   rtps_topic_state_free(c->topics);
   {
-    void* it[] = {c->it_items, c->it_wcnt, c->it_prefix};
+    void* it[] = {c->it_items, c->it_wcnt, c->it_prefix, c->rs_recs, c->rs_meta, c->rs_tgt};
     for (void* q : it) if (q) (void)hipFree(q);
   }
   {
@@ -2316,14 +2498,46 @@ static int parse_launch(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len
   const uint32_t k = c->k_spec ? c->k_spec : 1u;
   const bool lds = chain && c->mixed_pass == 1u;
   const bool item = chain && c->mixed_pass == 2u;
+  const bool rslab = chain && c->mixed_pass == 3u;
   if (lds) tiles = (n + LT - 1) / LT;  // kernel D: tiles of LT datagrams (B follows the same tiling)
-  if (first_kernel) *first_kernel = item ? 4u : lds ? 3u : chain ? 2u : 1u;
+  if (first_kernel) *first_kernel = rslab ? 5u : item ? 4u : lds ? 3u : chain ? 2u : 1u;
+  if (rslab) {  // E' (phases 1), then S and W' (phases 2); no kernel B
+    const uint32_t t = (uint32_t)(((size_t)c->max_datagrams + TILE - 1) / TILE) > tiles
+                           ? (uint32_t)(((size_t)c->max_datagrams + TILE - 1) / TILE) : tiles;
+    if (tiles > c->it_tiles || tiles > c->rs_tiles) {
+      if (hipStreamSynchronize(c->stream) != hipSuccess) return RTPS_RX_EHIP;
+      void* q[] = {c->it_wcnt, c->it_prefix, c->rs_recs, c->rs_meta, c->rs_tgt};
+      for (void* b : q) if (b) (void)hipFree(b);
+      c->it_wcnt = nullptr; c->it_prefix = nullptr; c->rs_recs = nullptr; c->rs_meta = nullptr; c->rs_tgt = nullptr;
+      c->rs_tiles = 0;
+      if (c->it_items) (void)hipFree(c->it_items);
+      c->it_items = nullptr; c->it_tiles = 0;
+      const size_t slots = (size_t)t * WAVES * CAPR;
+      if (hipMalloc(&c->rs_recs, slots * 4u * sizeof(u32x4)) != hipSuccess ||
+          hipMalloc(&c->rs_meta, slots * sizeof(uint32_t)) != hipSuccess ||
+          hipMalloc(&c->rs_tgt, slots * sizeof(uint32_t)) != hipSuccess ||
+          hipMalloc(&c->it_wcnt, (size_t)t * WAVES * sizeof(uint32_t)) != hipSuccess ||
+          hipMalloc(&c->it_prefix, (size_t)t * sizeof(uint64_t)) != hipSuccess)
+        return RTPS_RX_ENOMEM;
+      c->rs_tiles = t;
+    }
+    if (phases & 1u)
+      hipLaunchKernelGGL(rtps_parse_rslab_kernel, dim3(tiles), dim3(TILE), mt_lds, c->stream, p, tiles, k, c->rs_recs,
+                         c->rs_meta, c->rs_tgt, c->it_wcnt);
+    if (phases & 2u) {
+      hipLaunchKernelGGL(rtps_parse_scan_kernel, dim3(1), dim3(SCAN_T), 0, c->stream, p, tiles, parity, c->it_prefix);
+      hipLaunchKernelGGL(rtps_parse_rcopy_kernel, dim3(tiles), dim3(EMT), mt_lds, c->stream, p, tiles, c->rs_recs,
+                         c->rs_meta, c->rs_tgt, c->it_wcnt, c->it_prefix);
+    }
+    return hip_fail(hipGetLastError());
+  }
   if (item) {  // E (phases 1), then S and W (phases 2); no kernel B
-    if (tiles > c->it_tiles) {
+    if (tiles > c->it_tiles || !c->it_items) {
       if (hipStreamSynchronize(c->stream) != hipSuccess) return RTPS_RX_EHIP;
       void* q[] = {c->it_items, c->it_wcnt, c->it_prefix};
       for (void* b : q) if (b) (void)hipFree(b);
       c->it_items = nullptr; c->it_wcnt = nullptr; c->it_prefix = nullptr; c->it_tiles = 0;
+      c->rs_tiles = 0;  // (the wave counts and prefixes are shared)
       const uint32_t t = (uint32_t)(((size_t)c->max_datagrams + TILE - 1) / TILE) > tiles
                              ? (uint32_t)(((size_t)c->max_datagrams + TILE - 1) / TILE) : tiles;
       if (hipMalloc(&c->it_items, (size_t)t * WAVES * CAPW * sizeof(u32x4)) != hipSuccess ||
@@ -2791,7 +3005,7 @@ int rtps_rx_debug_lds_stamps(rtps_rx_ctx* c, uint64_t* host, uint64_t n) {
    0 = the chained lane walk in global memory (rtps_parse_chain_kernel), 1 = chained
    LDS tiles (rtps_parse_lds_kernel).  Same results. */
 int rtps_rx_debug_set_mixed_pass(rtps_rx_ctx* c, uint32_t pass) {
-  if (!c || pass > 2u) return RTPS_RX_EINVAL;
+  if (!c || pass > 3u) return RTPS_RX_EINVAL;
   c->mixed_pass = pass;
   return RTPS_RX_OK;
 }

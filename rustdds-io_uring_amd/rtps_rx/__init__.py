@@ -25,7 +25,7 @@ LIB_PATH = os.environ.get("RTPS_RX_LIB") or os.path.join(os.path.dirname(_PKG_DI
 ABI_VERSION = 2
 
 WL_T, WL_C2, WL_C3, WL_C4 = 1, 2, 3, 4
-MIXED_CHAIN, MIXED_LDS, MIXED_ITEM = 0, 1, 2  # passes for mixed traffic (debug_set_mixed_pass)
+MIXED_CHAIN, MIXED_LDS, MIXED_ITEM, MIXED_RSLAB = 0, 1, 2, 3  # passes for mixed traffic (debug_set_mixed_pass)
 WORKLOADS = {"T": WL_T, "C2": WL_C2, "C3": WL_C3, "C4": WL_C4}
 SEED = 0x52545053
 
@@ -330,7 +330,8 @@ class MessageReceiver:
 
     def debug_set_mixed_pass(self, pass_):
         """The pass for mixed traffic (same results): MIXED_ITEM (2, the default: item walk,
-        tile scan, record pass), MIXED_CHAIN (0: chained lane walk) or MIXED_LDS (1: chained
+        tile scan, record pass), MIXED_RSLAB (3: the walk builds the records into wave slabs,
+        tile scan, slab copy), MIXED_CHAIN (0: chained lane walk) or MIXED_LDS (1: chained
         LDS tiles).  True / False select LDS tiles / the chained lane walk."""
         if pass_ is True or pass_ is False:
             pass_ = MIXED_LDS if pass_ else MIXED_CHAIN

@@ -277,7 +277,7 @@ def test_full_size_parity(rx, wl, name):
         assert (u[:, 1] == (980 if wl == 1 else 256)).all()
 
 
-MIXED_PASSES = [(2, "item"), (0, "chain"), (1, "lds")]
+MIXED_PASSES = [(2, "item"), (3, "rslab"), (0, "chain"), (1, "lds")]
 
 
 @pytest.mark.parametrize("mp", [2, 0])
