@@ -128,6 +128,9 @@ struct Scratch {
   uint32_t* fidx;   // completed DataFrag sample of a record, or NONE
   uint64_t* fmask;  // the target-set entries (bit k: entry k) whose assembler completed it at the record
   uint8_t* fall;    // a writer-keyed sample (every entry) completed at the record
+  const rtps_frag_sample* frag;  // this batch's completed samples (entries past 64: their readers)
+  const uint64_t* n_frag;
+  uint64_t max_frag;
   uint32_t* rcnt;   // events of the record (non-identity batches), then their exclusive scan (roff)
   uint32_t* roff;
   uint32_t* rset;   // target set, record event kind, sample / event sn
@@ -173,7 +176,9 @@ __global__ __launch_bounds__(IT) void k_fidx(const rtps_frag_sample* frag, const
   for (uint64_t s = (uint64_t)blockIdx.x * IT + threadIdx.x; s < nf; s += (uint64_t)gridDim.x * IT) {
     const rtps_frag_sample& f = frag[s];
     if (f.status == RTPS_FRAG_SHORT || f.rec_idx >= max) continue;
-    fidx[f.rec_idx] = (uint32_t)s;  // (samples of one record share the writer and SN)
+    // the record's first sample (samples of one record share the writer and SN, and are
+    // adjacent: completing-record order)
+    atomicMin(&fidx[f.rec_idx], (uint32_t)s);
     uint64_t bit = ~0ull;
     if (f.reader_slot == RTPS_NO_MATCH) fall[f.rec_idx] = 1u;
     if (f.reader_slot != RTPS_NO_MATCH) {
@@ -189,11 +194,18 @@ __global__ __launch_bounds__(IT) void k_fidx(const rtps_frag_sample* frag, const
   }
 }
 
-// Does entry `pos` of the record's target set take its completed DataFrag sample?  fm: the
-// entries whose assembler completed it (bits 0..63), all: a writer-keyed sample (every entry);
-// a record without one: fm = ~0, all.
-__device__ __forceinline__ bool frag_takes(uint64_t fm, bool all, uint32_t pos) {
-  return pos < 64u ? ((fm >> pos) & 1ull) != 0ull : all;
+// Does entry `pos` (reader `slot`) of record i's target set take its completed DataFrag
+// sample?  fm: the entries whose assembler completed it (bits 0..63), all: a writer-keyed
+// sample (every entry); a record without one: fm = ~0, all.  Entries past 64 look for
+// their reader among the record's samples (adjacent, from its first, fidx).
+__device__ __forceinline__ bool frag_takes(uint64_t fm, bool all, uint32_t pos, const Scratch& x, uint64_t i,
+                                           uint16_t slot) {
+  if (pos < 64u) return ((fm >> pos) & 1ull) != 0ull;
+  if (all) return true;
+  const uint64_t nf = *x.n_frag < x.max_frag ? *x.n_frag : x.max_frag;
+  for (uint64_t f = x.fidx[i]; f < nf && x.frag[f].rec_idx == i; ++f)
+    if (x.frag[f].status != RTPS_FRAG_SHORT && x.frag[f].reader_slot == slot) return true;
+  return false;
 }
 
 // Does (record event kind, target x) make an event?  Sets ent / meta.
@@ -413,7 +425,7 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
       const bool fa = !fs || x.fall[i] != 0u;
       for (uint32_t k = b; k < e; ++k) {
         uint32_t en, me;
-        if (frag_takes(fm, fa, k - b) && ev_of(ev, sent[k], user_kind, reliable, en, me)) {
+        if (frag_takes(fm, fa, k - b, x, i, sent[k].reader_slot) && ev_of(ev, sent[k], user_kind, reliable, en, me)) {
           ++cnt;
           ent = en;
           meta = me;
@@ -637,7 +649,7 @@ __global__ __launch_bounds__(IT) void k_expand(ReaderDev t, uint64_t n, uint32_t
     const bool fa = !fs || x.fall[i] != 0u;
     for (uint32_t j = t.set_first[set], b = j, e = t.set_first[set + 1]; j < e; ++j) {
       uint32_t en, me;
-      if (!frag_takes(fm, fa, j - b)) continue;
+      if (!frag_takes(fm, fa, j - b, x, i, t.set_ent[j].reader_slot)) continue;
       if (!ev_of(ev, t.set_ent[j], user_kind, reliable, en, me)) continue;
       x.evt[k] = ev;
       x.ent[k] = en;
@@ -2157,6 +2169,9 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
   uint64_t* const ctr_next = s->ctr_base + (uint64_t)(s->cpar ^ 1u) * C_COUNT;
   bool ok = true;
   const bool with_frag = frag && n_frag && max_frag;
+  x.frag = frag;
+  x.n_frag = n_frag;
+  x.max_frag = max_frag;
   if (with_frag) ok = ok && hipMemsetAsync(x.fidx, 0xff, max * 4, st) == hipSuccess &&
                      hipMemsetAsync(x.fmask, 0, max * 8, st) == hipSuccess &&
                      hipMemsetAsync(x.fall, 0, max, st) == hipSuccess;

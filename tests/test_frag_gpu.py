@@ -252,3 +252,53 @@ def test_per_reader_assembly_and_ingest(rx, ingest_path, sets):
     assert per_reader[11] > 0 and per_reader[12] > 0 and per_reader.get(13, 0) > 0
     if sets == "multi":
         assert per_reader[11] > per_reader[12]
+
+
+def test_target_set_past_64_readers(rx):
+    """a target set of 70 readers on one writer, each with its own assembler (one
+    with a Lifespan, so that the completions differ between readers): entries 64 and up take a
+    completed sample exactly when their own assembler completed it (found among the record's
+    samples), as the oracle's per-reader restatement does; deliveries and ack_base bit-exact."""
+    from rtps_rx.records import FRAG_SAMPLE_DTYPE, DELIVERY_DTYPE, Readers, max_records
+    dev = torch.device("cuda", 0)
+    n_r = 70
+    slots = [100 + k for k in range(n_r)]
+    readers = [(bytes([0, 0, 1 + k, 0x07]), slots[k], 0) for k in range(n_r)]
+    g1 = frag_ref.RS_PREFIX[0] + frag_ref.RS_WRITER[0]
+    g2 = frag_ref.RS_PREFIX[1] + frag_ref.RS_WRITER[1]
+    rd = Readers(readers, [(g1, k) for k in range(n_r)] + [(g2, k) for k in range(0, n_r, 3)])
+    life = {slots[66]: 2 * 10**9, slots[3]: 2 * 10**9}
+    rx.set_readers(rd)
+    for sl, ns in life.items():
+        rx.set_reader_lifespan(sl, ns)
+    rx.frag_set_receive_time(frag_ref.RS_RECV_NS)
+    fa = oracle.FragAssembler()
+    ing = oracle.HistoryIngest(rd)
+    dgrams = frag_ref.reader_scenario(300, 5, 1, 64)
+    arena, off, ln = oracle.pack(dgrams, align=4)
+    A = torch.from_numpy(arena).to(dev)
+    O = torch.from_numpy(off.view(np.int64)).to(dev)
+    L = torch.from_numpy(ln.view(np.int32)).to(dev)
+    cap = max_records(ln)
+    heap_bytes = 80 * len(arena) + (1 << 20)
+    outs = rx.alloc_outputs(len(ln), cap)
+    fouts = rx.alloc_frag_outputs(80 * cap, heap_bytes)
+    iouts = rx.alloc_ingest_outputs(cap, rd.n_proxies)
+    rx.parse_batch_device(A, O, L, len(ln), outs)
+    rx.frag_assemble(A, O, outs, fouts)
+    rx.ingest(A, O, outs, iouts, fouts)
+    rx.sync()
+    _, recs, _, _ = oracle.parse(arena, off, ln, match_table=rd)
+    o_s, o_heap, o_n, o_used = fa.batch_readers(arena, off, recs, rd, life, frag_ref.RS_RECV_NS,
+                                                max_samples=80 * cap, heap_bytes=heap_bytes)
+    ns = int(fouts["n_samples"].item())
+    assert ns == o_n > 0
+    s = fouts["samples"][:ns].cpu().numpy().reshape(-1).view(FRAG_SAMPLE_DTYPE)
+    assert s.tobytes() == o_s.tobytes()
+    o_acc, o_dels, o_ack = ing.batch(arena, off, recs, o_s)
+    na = int(iouts["n_accepted"].item())
+    dels = iouts["accepted"][:na].cpu().numpy().reshape(-1).view(DELIVERY_DTYPE)
+    assert dels.tobytes() == o_dels.tobytes()
+    assert np.array_equal(iouts["ack_base"][:rd.n_proxies].cpu().numpy(), o_ack)
+    late = np.isin(dels["reader_slot"], slots[64:])
+    assert late.sum() > 0 and (dels["reader_slot"] == slots[66]).sum() < (dels["reader_slot"] == slots[65]).sum()
