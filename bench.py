@@ -259,7 +259,8 @@ def roofline(rx, args, arena, off_t, ln_t, n, outs, stream, total_bytes, alg_rea
     ms, kname, extra = time_dominant_kernel(rx, arena, off_t, ln_t, n, outs, stream, args.steps)
     pmc = pmc_profile(args.workload)
     key = {"rtps_parse_spec_kernel": "parse_spec", "rtps_parse_chain_kernel": "parse_chain",
-           "rtps_parse_lds_kernel": "parse_lds", "rtps_parse_item_kernel": "parse_item"}[kname]
+           "rtps_parse_lds_kernel": "parse_lds", "rtps_parse_item_kernel": "parse_item",
+           "rtps_parse_rslab_kernel": "parse_rslab"}[kname]
     k = (pmc or {}).get(key) or {}
     scale = (pmc or {}).get("fetch_scale") or 1.0
     if pmc and pmc.get("datagrams_per_launch") == n and "FETCH_SIZE" in k:

@@ -75,10 +75,8 @@ enum : uint8_t { EV_NONE = 0, EV_SAMPLE = 1, EV_HB = 2, EV_GAP = 3 };
 // counters: window overflow, selected HEARTBEATs, selected deliveries, records of the batch, then
 // the HEARTBEAT / GAP / event / proxy-less sample counts in 64 slot quads (one atomic per block, spread: no hot address)
 // (C_FARC: classify's far-SN candidates, the host's cue for k_far; C_NFAR: far items appended)
-// (C_DONE: classify workgroups finished, for the count signal to the host)
-enum { C_OVF = 0, C_NSEL, C_NDEL, C_NREC, C_FARC, C_NFAR, C_DONE, C_DTOP = C_DONE + 8, C_SPREAD,
-       C_COUNT = C_SPREAD + 4 * 64 };
-// the batch's counts as classify's last workgroup signals them to pinned host memory:
+enum { C_OVF = 0, C_NSEL, C_NDEL, C_NREC, C_FARC, C_NFAR, C_SPREAD, C_COUNT = C_SPREAD + 4 * 64 };
+// the batch's counts as k_signal writes them to pinned host memory:
 // [0] = the batch's tag (written last), HEARTBEAT / GAP / event / proxy-less sample counts,
 // records, far-item candidates
 enum { SIG_TAG = 0, SIG_HB, SIG_GAP, SIG_EV, SIG_FREE, SIG_NREC, SIG_FARC, SIG_WORDS = 8 };
@@ -201,7 +199,7 @@ __global__ __launch_bounds__(IT) void k_fidx(const rtps_frag_sample* frag, const
 __device__ __forceinline__ bool frag_takes(uint64_t fm, bool all, uint32_t pos, const Scratch& x, uint64_t i,
                                            uint16_t slot) {
   if (pos < 64u) return ((fm >> pos) & 1ull) != 0ull;
-  if (all) return true;
+  if (all || !x.frag || !x.n_frag) return all;
   const uint64_t nf = *x.n_frag < x.max_frag ? *x.n_frag : x.max_frag;
   for (uint64_t f = x.fidx[i]; f < nf && x.frag[f].rec_idx == i; ++f)
     if (x.frag[f].status != RTPS_FRAG_SHORT && x.frag[f].reader_slot == slot) return true;
@@ -286,8 +284,6 @@ struct FastOut {
   uint32_t* bk_cnt;  // BUCKET: per (workgroup, proxy) proxied events, workgroup-major: [block * n_proxies + proxy]
   uint32_t* bk_lst;  //         the proxy's first position inside the workgroup's region
   uint32_t sets_lds; // classify: set_first / set_ent staged in LDS behind the hash tables
-  uint64_t* hsig;     // pinned host words (SIG_*) the last workgroup writes, or null
-  uint64_t tag;
 };
 // bytes of the target sets' LDS image (set_first words, then 8-B entries)
 __host__ __device__ inline uint32_t sets_lds_bytes(const ReaderDev& t) { return (t.n_sets + 1u) * 4u + t.n_ent * 8u; }
@@ -344,8 +340,7 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
   __shared__ uint32_t s_part[IT / 64];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const uint64_t n = *n_rec < max ? *n_rec : max;
-  if (blockIdx.x == 0 && tid == 0)  // (write-through: the signalling workgroup reads it)
-    __hip_atomic_store(ctr + C_NREC, (uint64_t)n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (blockIdx.x == 0 && tid == 0) ctr[C_NREC] = n;
   if (FAST && !BUCKET)
     for (uint32_t e = blockIdx.x * IT + tid; e < fo.n_seg; e += gridDim.x * IT) { fo.seg_b[e] = 0u; fo.seg_e[e] = 0u; }
   if (BUCKET)
@@ -599,38 +594,24 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
     atomicAdd(reinterpret_cast<unsigned long long*>(ctr + C_SPREAD + 4u * (blockIdx.x & 63u) + tid),
               (unsigned long long)s_n[tid]);
   if (MARK && nfar) atomicAdd(reinterpret_cast<unsigned long long*>(ctr + C_FARC), (unsigned long long)nfar);
-  if (fo.hsig) {
-    // The last workgroup to finish signals the batch's counts to the host.  The counts are
-    // agent-scope atomics (performed past the per-XCD L2s); each workgroup's are drained
-    // (vmcnt) before its ticket, the last ticket (its returned value) reads them with atomics:
-    // no L2 write-back fence per workgroup (MI355X_MICROARCH.md, inter-workgroup visibility).
-    // (tickets sharded 8 ways, then one top counter: one word takes about 88 returning adds
-    // per microsecond, fewer than a classify grid's workgroups finish)
-    __shared__ uint32_t s_last;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      const uint32_t sh = blockIdx.x & 7u, in_shard = (gridDim.x - sh + 7u) >> 3;
-      const uint32_t shards = gridDim.x < 8u ? gridDim.x : 8u;
-      s_last = atomicAdd(reinterpret_cast<unsigned long long*>(ctr + C_DONE + sh), 1ull) == in_shard - 1u &&
-               atomicAdd(reinterpret_cast<unsigned long long*>(ctr + C_DTOP), 1ull) == shards - 1u;
-    }
-    __syncthreads();
-    if (s_last && tid < 64) {  // one wave: the sums, then the pinned words, the tag last
-      uint64_t v = 0;
-      if (tid < 4) {
-        for (uint32_t k = 0; k < 64; ++k)
-          v += atomicAdd(reinterpret_cast<unsigned long long*>(ctr + C_SPREAD + 4u * k + tid), 0ull);
-      } else if (tid == 4) {
-        v = atomicAdd(reinterpret_cast<unsigned long long*>(ctr + C_NREC), 0ull);
-      } else if (tid == 5) {
-        v = atomicAdd(reinterpret_cast<unsigned long long*>(ctr + C_FARC), 0ull);
-      }
-      if (tid < 6) __hip_atomic_store(fo.hsig + SIG_HB + tid, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (tid == 0) __hip_atomic_store(fo.hsig + SIG_TAG, fo.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+}
+
+// The batch's counts to pinned host memory (one wave, after classify): the sums, then the tag
+// last, written through (system scope) after the sums' stores have completed.  The host
+// spins on the tag instead of a copy and an interrupt-driven stream sync.
+__global__ void k_signal(const uint64_t* ctr, uint64_t* hsig, uint64_t tag) {
+  const uint32_t tid = threadIdx.x;
+  uint64_t v = 0;
+  if (tid < 4) {
+    for (uint32_t k = 0; k < 64; ++k) v += ctr[C_SPREAD + 4u * k + tid];
+  } else if (tid == 4) {
+    v = ctr[C_NREC];
+  } else if (tid == 5) {
+    v = ctr[C_FARC];
   }
+  if (tid < 6) __hip_atomic_store(hsig + SIG_HB + tid, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (tid == 0) __hip_atomic_store(hsig + SIG_TAG, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // 1b: lane per record writes its events at roff[i] (set order = EntityId order of the readers)
@@ -792,6 +773,30 @@ struct FarSrc {
   const rtps_record* recs;
   const uint64_t* dgram_off;
 };
+__device__ __forceinline__ void gap_far_item(uint64_t i, const Scratch& x, const State& s, const FarSrc& fs) {
+  const uint32_t e = x.ent[i];
+  const rtps_record& r = fs.recs[x.erec[i]];
+  const int64_t lim = s.lo[e] + (int64_t)W;
+  if (r.u.gap.list_base + (int64_t)r.u.gap.num_bits > lim)
+    far_push(s.ctr, s.fl,
+             FarItem{PEv{r.sn, r.u.gap.list_base, fs.dgram_off[r.dgram_idx] + r.u.gap.bitmap_off,
+                         EV_GAP | ((r.flags & 1u) ? PM_LE : 0u) | (r.u.gap.num_bits << 8), (uint32_t)i},
+                     lim, e, FI_GAP});
+}
+// a sample's accepting HEARTBEAT threshold at event i (the binary search over the proxy's sorted
+// HEARTBEATs, only when the proxy's final threshold lies above v)
+__device__ __forceinline__ int64_t hb_thr(uint64_t i, int64_t v, int64_t thr, uint32_t sb, uint32_t se,
+                                          const Scratch& x, bool reliable) {
+  if (reliable && se > sb && x.hpre[se - 1u] > v && v >= thr) {
+    uint32_t a = sb, b = se;
+    while (a < b) {  // first sorted position whose event is >= i
+      const uint32_t m = (a + b) >> 1;
+      if (x.sval[m] < (uint32_t)i) a = m + 1u; else b = m;
+    }
+    if (a > sb && x.hpre[a - 1u] > thr) thr = x.hpre[a - 1u];
+  }
+  return thr;
+}
 __device__ __forceinline__ uint8_t decide_one(uint64_t i, uint64_t n, const Scratch& x, const State& s, bool reliable,
                                               uint32_t epoch, const FarSrc& fs, uint32_t& pe, uint64_t& poff,
                                               bool& merge) {
@@ -799,14 +804,7 @@ __device__ __forceinline__ uint8_t decide_one(uint64_t i, uint64_t n, const Scra
   if (i >= n) return 0;
   const uint8_t ev = x.evt[i];
   if (ev == EV_GAP) {  // its coverage past the window is the far replay's
-    const uint32_t e = x.ent[i];
-    const rtps_record& r = fs.recs[x.erec[i]];
-    const int64_t lim = s.lo[e] + (int64_t)W;
-    if (r.u.gap.list_base + (int64_t)r.u.gap.num_bits > lim)
-      far_push(s.ctr, s.fl,
-               FarItem{PEv{r.sn, r.u.gap.list_base, fs.dgram_off[r.dgram_idx] + r.u.gap.bitmap_off,
-                           EV_GAP | ((r.flags & 1u) ? PM_LE : 0u) | (r.u.gap.num_bits << 8), (uint32_t)i},
-                       lim, e, FI_GAP});
+    gap_far_item(i, x, s, fs);
     return 0;
   }
   if (ev != EV_SAMPLE) return 0;
@@ -821,18 +819,7 @@ __device__ __forceinline__ uint8_t decide_one(uint64_t i, uint64_t n, const Scra
     if (v >= lo + (int64_t)W) far_push(s.ctr, s.fl, FarItem{PEv{v, 0, 0, EV_SAMPLE, (uint32_t)i}, lo + (int64_t)W, e, FI_DUP});
     return 1;
   }
-  int64_t thr = s.base[e];
-  const uint32_t sb = s.seg_b[e], se = s.seg_e[e];
-  // accepted HEARTBEATs of this proxy before event i (only needed when the
-  // proxy's final threshold is above v)
-  if (reliable && se > sb && x.hpre[se - 1u] > v && v >= thr) {
-    uint32_t a = sb, b = se;
-    while (a < b) {  // first sorted position whose event is >= i
-      const uint32_t m = (a + b) >> 1;
-      if (x.sval[m] < (uint32_t)i) a = m + 1u; else b = m;
-    }
-    if (a > sb && x.hpre[a - 1u] > thr) thr = x.hpre[a - 1u];
-  }
+  const int64_t thr = hb_thr(i, v, s.base[e], s.seg_b[e], s.seg_e[e], x, reliable);
   if (v < 1 || v < thr) return 0;
   if (v >= lo + (int64_t)W) {  // beyond the window: accepted until the far replay (k_far) decides
     far_push(s.ctr, s.fl, FarItem{PEv{v, 0, 0, EV_SAMPLE, (uint32_t)i}, lo + (int64_t)W, e, FI_SAMPLE});
@@ -906,8 +893,8 @@ __device__ __forceinline__ uint64_t block_sum64(uint64_t v, uint64_t* s_w) {
 // of keys and write each word's positions that carry this batch's epoch into dbits (every
 // word written, zeros too), which state_proxy ORs into the window and clears.  The decisions
 // read `bits` only, so the scan runs beside them; it replaces k_merge's per-sample wave_or.
-constexpr uint32_t FCM_POS = 16384;  // window positions per scanning workgroup
-static_assert(FCM_POS % (IT * 2) == 0 && W % FCM_POS == 0, "whole waves of 64 positions");
+constexpr uint32_t FCM_POS = 8192;  // window positions per scanning workgroup
+static_assert(FCM_POS % (IT * 2) == 0 && W % FCM_POS == 0, "whole wave steps of 128 positions");
 template <int MERGE>
 __global__ __launch_bounds__(IT) void k_decide_t(uint64_t n, uint64_t cap, Scratch x, State s, uint8_t* acc_out,
                                                  bool reliable, uint32_t epoch, uint32_t* tcnt, FarSrc fs,
@@ -916,14 +903,25 @@ __global__ __launch_bounds__(IT) void k_decide_t(uint64_t n, uint64_t cap, Scrat
   // (MERGE 2: the key-scanning workgroups come first, so that they run beside the decisions)
   const uint32_t nfcm = MERGE == 2 ? gridDim.x - ntiles : 0u;
   if (MERGE == 2 && blockIdx.x < nfcm) {
+    // two positions per lane (one 16-B load), 128 per wave step: the even and the odd
+    // positions' ballots interleave into the step's four words (lanes 0..3 store them)
     const uint64_t p0 = (uint64_t)blockIdx.x * FCM_POS;  // a multiple of W / FCM_POS per proxy
-    const uint32_t tag = 0xffffffffu - epoch, lane = threadIdx.x & 63u;
+    const uint32_t tag = 0xffffffffu - epoch, lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    auto spread = [](uint32_t x) {  // bit i -> bit 2i (16 bits)
+      x = (x | (x << 8)) & 0x00ff00ffu;
+      x = (x | (x << 4)) & 0x0f0f0f0fu;
+      x = (x | (x << 2)) & 0x33333333u;
+      return (x | (x << 1)) & 0x55555555u;
+    };
 #pragma unroll 4
-    for (uint32_t r = 0; r < FCM_POS / IT; ++r) {
-      const uint64_t pos = p0 + r * IT + threadIdx.x;
-      const uint64_t m = __ballot((uint32_t)(s.fc[pos] >> 32) == tag);
-      if (lane == 0) s.dbits[pos >> 5] = (uint32_t)m;
-      if (lane == 32) s.dbits[pos >> 5] = (uint32_t)(m >> 32);
+    for (uint32_t r = 0; r < FCM_POS / (IT * 2); ++r) {
+      const uint64_t g = p0 + (uint64_t)(r * (IT / 64) + wave) * 128u;  // the wave's 128 positions
+      const ulonglong2 k = *reinterpret_cast<const ulonglong2*>(s.fc + g + 2u * lane);
+      const uint64_t me = __ballot((uint32_t)(k.x >> 32) == tag), mo = __ballot((uint32_t)(k.y >> 32) == tag);
+      if (lane < 4u) {
+        const uint32_t sh = 16u * lane;
+        s.dbits[(g >> 5) + lane] = spread((uint32_t)(me >> sh) & 0xffffu) | (spread((uint32_t)(mo >> sh) & 0xffffu) << 1);
+      }
     }
     return;
   }
@@ -933,16 +931,99 @@ __global__ __launch_bounds__(IT) void k_decide_t(uint64_t n, uint64_t cap, Scrat
 #pragma unroll
   for (uint32_t q = 0; q < DPT / 4; ++q) w[q] = 0u;
   uint32_t c = 0;
+  // the thread's DPT events in groups of HG, decide_one's rule in phases so that each phase's
+  // loads are in flight together: the event fields (vector loads), the proxies' state, the
+  // window words (HG = 4: 8 would hold 130 VGPRs, 3 waves per SIMD)
+  constexpr uint32_t HG = 4;
 #pragma unroll
-  for (uint32_t j = 0; j < DPT; ++j) {
-    uint32_t e = 0;
-    uint64_t off = 0;
+  for (uint32_t h = 0; h < DPT; h += HG) {
+  const uint64_t g0 = b0 + h;
+  uint32_t evw, ent[HG], meta[HG];
+  int64_t sn[HG];
+  if (g0 + HG <= n) {
+    evw = *reinterpret_cast<const uint32_t*>(x.evt + g0);
+    const uint4 a = *reinterpret_cast<const uint4*>(x.ent + g0);
+    const uint4 b = *reinterpret_cast<const uint4*>(x.emeta + g0);
+    ent[0] = a.x; ent[1] = a.y; ent[2] = a.z; ent[3] = a.w;
+    meta[0] = b.x; meta[1] = b.y; meta[2] = b.z; meta[3] = b.w;
+#pragma unroll
+    for (uint32_t q = 0; q < HG / 2; ++q) {
+      const longlong2 c2 = *reinterpret_cast<const longlong2*>(x.esn + g0 + 2u * q);
+      sn[2 * q] = c2.x; sn[2 * q + 1] = c2.y;
+    }
+  } else {
+    evw = 0u;
+#pragma unroll
+    for (uint32_t j = 0; j < HG; ++j) {
+      const bool in = g0 + j < n;
+      if (in) evw |= (uint32_t)x.evt[g0 + j] << (8u * j);
+      ent[j] = in ? x.ent[g0 + j] : NONE;
+      meta[j] = in ? x.emeta[g0 + j] : 0u;
+      sn[j] = in ? x.esn[g0 + j] : 0;
+    }
+  }
+  int64_t lo[HG], base[HG];
+#pragma unroll
+  for (uint32_t j = 0; j < HG; ++j) {
+    const uint32_t ev = (evw >> (8u * j)) & 0xffu;
+    const uint32_t e = (ev == EV_SAMPLE && ent[j] != NONE) ? ent[j] : 0u;
+    lo[j] = s.lo[e];
+    base[j] = s.base[e];
+  }
+  uint32_t bw[HG];
+  uint64_t fk[HG];
+#pragma unroll
+  for (uint32_t j = 0; j < HG; ++j) {
+    const uint32_t ev = (evw >> (8u * j)) & 0xffu;
+    const bool win = ev == EV_SAMPLE && ent[j] != NONE && sn[j] >= lo[j] && sn[j] < lo[j] + (int64_t)W;
+    const uint64_t off = win ? (uint64_t)(sn[j] - lo[j]) : 0u;
+    const uint32_t e = win ? ent[j] : 0u;
+    bw[j] = s.bits[(uint64_t)e * WW + (off >> 5)];
+    fk[j] = s.fc[(uint64_t)e * W + off];
+  }
+#pragma unroll
+  for (uint32_t jj = 0; jj < HG; ++jj) {
+    const uint32_t j = h + jj;
+    const uint64_t i = b0 + j;
+    const uint32_t ev = (evw >> (8u * jj)) & 0xffu, e = ent[jj];
+    const int64_t v = sn[jj];
+    uint8_t a = 0;
     bool merge = false;
-    const uint8_t a = decide_one(b0 + j, n, x, s, reliable, epoch, fs, e, off, merge);
+    uint64_t off = 0;
+    if (ev == EV_GAP) {
+      gap_far_item(i, x, s, fs);
+    } else if (ev == EV_SAMPLE) {
+      if (e == NONE) {
+        a = 1;  // no proxy: the writer kind is not user-defined (reader.rs:734-739)
+      } else {
+        const bool in_win = v >= lo[jj] && v < lo[jj] + (int64_t)W;
+        off = (uint64_t)(v - lo[jj]);
+        if (meta[jj] & EVF_DUP_OK) {  // the participant reader's duplicates (reader.rs:712-722)
+          a = 1;
+          merge = in_win;
+          if (v >= lo[jj] + (int64_t)W)
+            far_push(s.ctr, s.fl, FarItem{PEv{v, 0, 0, EV_SAMPLE, (uint32_t)i}, lo[jj] + (int64_t)W, e, FI_DUP});
+        } else {
+          const int64_t thr = hb_thr(i, v, base[jj], reliable ? s.seg_b[e] : 0u, reliable ? s.seg_e[e] : 0u, x,
+                                     reliable);
+          if (v >= 1 && v >= thr) {
+            if (v >= lo[jj] + (int64_t)W) {  // beyond the window: accepted until the far replay decides
+              far_push(s.ctr, s.fl, FarItem{PEv{v, 0, 0, EV_SAMPLE, (uint32_t)i}, lo[jj] + (int64_t)W, e, FI_SAMPLE});
+              a = 1;
+            } else {
+              const bool known = (bw[jj] >> (off & 31u)) & 1u;
+              a = (!known && fk[jj] == ekey(epoch, (uint32_t)i)) ? 1 : 0;
+              merge = a != 0;
+            }
+          }
+        }
+      }
+    }
     w[j >> 2] |= (uint32_t)a << (8u * (j & 3u));
     c += a;
     if (MERGE == 1)
       wave_or(s.bits, merge ? s.bits + (uint64_t)e * WW + (off >> 5) : s.bits, 1u << (off & 31u), merge);
+  }
   }
   if (b0 + DPT <= cap) {
 #pragma unroll
@@ -2000,6 +2081,7 @@ static void free_vscratch(IngestState* s) {
   s->x = Scratch{};
   s->x.fidx = keep.fidx; s->x.fmask = keep.fmask; s->x.fall = keep.fall; s->x.rcnt = keep.rcnt; s->x.roff = keep.roff; s->x.rset = keep.rset;
   s->x.rkind = keep.rkind; s->x.rsn = keep.rsn;
+  s->x.frag = keep.frag; s->x.n_frag = keep.n_frag; s->x.max_frag = keep.max_frag;  // (this batch's, set before the events are sized)
   s->tmp = nullptr;
   s->tmp_bytes = 0;
   s->vcap = 0;
@@ -2197,9 +2279,7 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
   // classify workgroups exceed its LDS tables (or path 4: the radix sort, tests)
   const uint64_t nblk = (max + CHR - 1) / CHR;
   const bool bucket = fast && t.n_proxies <= PB_MAX && nblk <= BK_MAX && s->path != 4;
-  // (the paths that wait for the counts: classify signals them to pinned memory, the host spins)
-  FastOut fo{nullptr, nullptr, arena, dgram_off, S.seg_b, S.seg_e, s->ecap, nullptr, nullptr, sets_lds ? 1u : 0u,
-             fast ? nullptr : s->hsig, ++s->sig_tag};
+  FastOut fo{nullptr, nullptr, arena, dgram_off, S.seg_b, S.seg_e, s->ecap, nullptr, nullptr, sets_lds ? 1u : 0u};
   if (fast) {
     if (!grow_pscratch(s, bucket ? nblk * CHR : max, st)) return RTPS_RX_ENOMEM;
     fo.pev = s->pev;
@@ -2243,16 +2323,18 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
     s->hnev_ready = true;
     return hipGetLastError() == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP;
   }
-  // the batch's record / HEARTBEAT / GAP / event counts size the rest: classify's last workgroup
-  // writes them to pinned memory, the host spins on the tag (no copy, no interrupt-driven wait);
-  // a wait past the limit falls back to a stream sync (a failed launch surfaces there)
+  // the batch's record / HEARTBEAT / GAP / event counts size the rest: k_signal writes them to
+  // pinned memory, the host spins on the tag (no copy, no interrupt-driven wait); a wait past
+  // the limit falls back to a stream sync (a failed launch surfaces there)
+  const uint64_t tag = ++s->sig_tag;
+  hipLaunchKernelGGL(k_signal, dim3(1), dim3(64), 0, st, S.ctr, s->hsig, tag);
   if (hipGetLastError() != hipSuccess) return RTPS_RX_EHIP;
   {
     volatile uint64_t* hs = s->hsig;
     const auto t0 = std::chrono::steady_clock::now();
-    for (uint32_t spin = 0; hs[SIG_TAG] != fo.tag; ++spin) {
+    for (uint32_t spin = 0; hs[SIG_TAG] != tag; ++spin) {
       if ((spin & 1023u) == 1023u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
-        if (hipStreamSynchronize(st) != hipSuccess || hs[SIG_TAG] != fo.tag) return RTPS_RX_EHIP;
+        if (hipStreamSynchronize(st) != hipSuccess || hs[SIG_TAG] != tag) return RTPS_RX_EHIP;
         break;
       }
       __builtin_ia32_pause();
