@@ -75,11 +75,12 @@ enum : uint8_t { EV_NONE = 0, EV_SAMPLE = 1, EV_HB = 2, EV_GAP = 3 };
 // counters: window overflow, selected HEARTBEATs, selected deliveries, records of the batch, then
 // the HEARTBEAT / GAP / event / proxy-less sample counts in 64 slot quads (one atomic per block, spread: no hot address)
 // (C_FARC: classify's far-SN candidates, the host's cue for k_far; C_NFAR: far items appended)
-enum { C_OVF = 0, C_NSEL, C_NDEL, C_NREC, C_FARC, C_NFAR, C_SPREAD, C_COUNT = C_SPREAD + 4 * 64 };
+// (C_MODE: k_signal's verdict on an identity batch, read by the kernels queued before the host saw it)
+enum { C_OVF = 0, C_NSEL, C_NDEL, C_NREC, C_FARC, C_NFAR, C_MODE, C_SPREAD, C_COUNT = C_SPREAD + 4 * 64 };
 // the batch's counts as k_signal writes them to pinned host memory:
 // [0] = the batch's tag (written last), HEARTBEAT / GAP / event / proxy-less sample counts,
 // records, far-item candidates
-enum { SIG_TAG = 0, SIG_HB, SIG_GAP, SIG_EV, SIG_FREE, SIG_NREC, SIG_FARC, SIG_WORDS = 8 };
+enum { SIG_TAG = 0, SIG_HB, SIG_GAP, SIG_EV, SIG_FREE, SIG_NREC, SIG_FARC, SIG_MODE, SIG_WORDS = 8 };
 // event metadata: reader slot | flags << 16 (EVF_*)
 constexpr uint32_t EVF_DUP_OK = 1u << 16;  // RTPS_TARGET_DUPLICATES_OK reader
 constexpr uint32_t EVF_FREE = 1u << 17;    // sample without a proxy (writer kind not user-defined)
@@ -599,19 +600,59 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
 // The batch's counts to pinned host memory (one wave, after classify): the sums, then the tag
 // last, written through (system scope) after the sums' stores have completed.  The host
 // spins on the tag instead of a copy and an interrupt-driven stream sync.
-__global__ void k_signal(const uint64_t* ctr, uint64_t* hsig, uint64_t tag) {
-  const uint32_t tid = threadIdx.x;
-  uint64_t v = 0;
-  if (tid < 4) {
-    for (uint32_t k = 0; k < 64; ++k) v += ctr[C_SPREAD + 4u * k + tid];
-  } else if (tid == 4) {
-    v = ctr[C_NREC];
-  } else if (tid == 5) {
-    v = ctr[C_FARC];
+// ident: also the verdict on an identity batch (SIG_MODE): 0 = the host decides, 1 / 2 =
+// the plain global path (no HEARTBEAT that counts, no GAP, no far item, not per proxy), merged by
+// the samples' wave_or / from the first-cover keys; the guarded decide and state launches queued
+// behind this kernel then run it without waiting for the host (the host's rule, on the device).
+struct SigCfg {
+  uint32_t ident, n_proxies, path, reliable;
+};
+// the verdict from the batch's counts (the host's path rule, on the device)
+__device__ __forceinline__ uint64_t plain_mode(uint64_t n_hb, uint64_t n_gap, uint64_t n_ev, uint64_t nev,
+                                               uint64_t farc, const SigCfg& cf) {
+  if (!cf.ident || !nev) return 0;
+  const bool have_hb = cf.reliable && n_hb > 0;
+  const bool per_proxy = cf.n_proxies > 0 && (cf.path == 2 || cf.path == 4 ||
+                                              (cf.path == 0 && cf.n_proxies >= 64 &&
+                                               n_ev <= (uint64_t)cf.n_proxies * 32768u));
+  if (have_hb || n_gap != 0 || farc != 0 || per_proxy) return 0;
+  return (cf.path == 3 || (cf.path != 1 && (uint64_t)cf.n_proxies * W <= 4ull * nev)) ? 2u : 1u;
+}
+// The batch's counts by one wave: lane k loads spread slot k's four counters, a wave reduction
+// sums them (every lane gets the sums)
+struct Counts {
+  uint64_t n_hb, n_gap, n_ev, n_free, nrec, farc;
+};
+__device__ __forceinline__ Counts wave_counts(const uint64_t* ctr, uint32_t lane) {
+  const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(ctr + C_SPREAD + 4u * lane);
+  const ulonglong2 b = *reinterpret_cast<const ulonglong2*>(ctr + C_SPREAD + 4u * lane + 2u);
+  Counts c{a.x, a.y, b.x, b.y, ctr[C_NREC], ctr[C_FARC]};
+#pragma unroll
+  for (uint32_t d = 32; d >= 1; d >>= 1) {
+    c.n_hb += __shfl_xor(c.n_hb, d, 64); c.n_gap += __shfl_xor(c.n_gap, d, 64);
+    c.n_ev += __shfl_xor(c.n_ev, d, 64); c.n_free += __shfl_xor(c.n_free, d, 64);
   }
-  if (tid < 6) __hip_atomic_store(hsig + SIG_HB + tid, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return c;
+}
+// the counts (and the verdict) to pinned host memory, the tag last, written through after the
+// rest completed (one wave: lane k writes word k)
+__device__ __forceinline__ void signal_host(const Counts& c, uint64_t mode, uint64_t* hsig, uint64_t tag,
+                                            uint32_t lane) {
+  const uint64_t v = lane == 0 ? c.n_hb : lane == 1 ? c.n_gap : lane == 2 ? c.n_ev : lane == 3 ? c.n_free
+                   : lane == 4 ? c.nrec : lane == 5 ? c.farc : mode;
+  if (lane < 7) __hip_atomic_store(hsig + SIG_HB + lane, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (tid == 0) __hip_atomic_store(hsig + SIG_TAG, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (lane == 0) __hip_atomic_store(hsig + SIG_TAG, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// one wave: lane k loads spread slot k's four counters, a wave reduction sums them; then the
+// sums, the record / far counts and the verdict go out (C_MODE for the queued kernels, the pinned
+// words for the host, the tag last, written through after the rest completed)
+__global__ void k_signal(uint64_t* ctr, uint64_t* hsig, uint64_t tag, SigCfg cf) {
+  const uint32_t lane = threadIdx.x;
+  const Counts c = wave_counts(ctr, lane);
+  const uint64_t mode = plain_mode(c.n_hb, c.n_gap, c.n_ev, c.nrec, c.farc, cf);
+  if (lane == 0) ctr[C_MODE] = mode;
+  signal_host(c, mode, hsig, tag, lane);
 }
 
 // 1b: lane per record writes its events at roff[i] (set order = EntityId order of the readers)
@@ -895,14 +936,39 @@ __device__ __forceinline__ uint64_t block_sum64(uint64_t v, uint64_t* s_w) {
 // read `bits` only, so the scan runs beside them; it replaces k_merge's per-sample wave_or.
 constexpr uint32_t FCM_POS = 8192;  // window positions per scanning workgroup
 static_assert(FCM_POS % (IT * 2) == 0 && W % FCM_POS == 0, "whole wave steps of 128 positions");
+struct SigOut {
+  uint64_t* hsig;
+  uint64_t tag;
+  SigCfg cf;
+};
 template <int MERGE>
 __global__ __launch_bounds__(IT) void k_decide_t(uint64_t n, uint64_t cap, Scratch x, State s, uint8_t* acc_out,
                                                  bool reliable, uint32_t epoch, uint32_t* tcnt, FarSrc fs,
-                                                 uint32_t ntiles) {
+                                                 uint32_t ntiles, SigOut so) {
   __shared__ uint64_t s_w[IT / 64];
+  __shared__ uint32_t s_mode;
+  // MERGE 3: launched before the host has the counts.  Every workgroup's first wave sums them and
+  // applies the host's path rule (plain_mode); workgroup 0 also hands the counts and the verdict
+  // to the host (and to the state launch, C_MODE).  Not plain: every workgroup returns.
+  int mm = MERGE;
+  if (MERGE == 3) {
+    if (threadIdx.x < 64) {
+      const Counts c = wave_counts(s.ctr, threadIdx.x);
+      const uint64_t mode = plain_mode(c.n_hb, c.n_gap, c.n_ev, c.nrec, c.farc, so.cf);
+      if (threadIdx.x == 0) s_mode = (uint32_t)mode;
+      if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) s.ctr[C_MODE] = mode;
+        signal_host(c, mode, so.hsig, so.tag, threadIdx.x);
+      }
+    }
+    __syncthreads();
+    mm = (int)s_mode;
+    if (mm == 0) return;
+  }
   // (MERGE 2: the key-scanning workgroups come first, so that they run beside the decisions)
-  const uint32_t nfcm = MERGE == 2 ? gridDim.x - ntiles : 0u;
-  if (MERGE == 2 && blockIdx.x < nfcm) {
+  const uint32_t nfcm = (MERGE == 2 || MERGE == 3) ? gridDim.x - ntiles : 0u;
+  if ((MERGE == 2 || MERGE == 3) && blockIdx.x < nfcm) {
+    if (mm != 2) return;
     // two positions per lane (one 16-B load), 128 per wave step: the even and the odd
     // positions' ballots interleave into the step's four words (lanes 0..3 store them)
     const uint64_t p0 = (uint64_t)blockIdx.x * FCM_POS;  // a multiple of W / FCM_POS per proxy
@@ -1021,7 +1087,7 @@ __global__ __launch_bounds__(IT) void k_decide_t(uint64_t n, uint64_t cap, Scrat
     }
     w[j >> 2] |= (uint32_t)a << (8u * (j & 3u));
     c += a;
-    if (MERGE == 1)
+    if (mm == 1)
       wave_or(s.bits, merge ? s.bits + (uint64_t)e * WW + (off >> 5) : s.bits, 1u << (off & 31u), merge);
   }
   }
@@ -1451,12 +1517,17 @@ __global__ __launch_bounds__(IT) void k_state(uint32_t n_entries, Scratch x, Sta
 __global__ __launch_bounds__(IT) void k_dstate(const uint8_t* flag, uint64_t n, const uint32_t* tcnt, uint32_t ntiles,
                                                Scratch x, uint64_t max_out, rtps_delivery* out, uint64_t* n_out,
                                                const uint64_t* ctr, uint64_t* ovf_out, uint32_t n_entries, State s,
-                                               bool reliable, int64_t* ack_out, bool fcm) {
+                                               bool reliable, int64_t* ack_out, bool fcm, bool guarded) {
   __shared__ uint64_t s_w[IT / 64];
   __shared__ uint32_t s_c[IT / 64];
   __shared__ __attribute__((aligned(16))) uint32_t sh[WW];
   __shared__ uint32_t s_first;
   __shared__ int64_t s_nb;
+  if (guarded) {  // queued before the host had the counts: only k_signal's plain batches
+    const uint64_t mode = ctr[C_MODE];
+    if (mode == 0) return;
+    fcm = mode == 2;
+  }
   if (blockIdx.x < ntiles) {
     dwrite_tile(blockIdx.x, flag, n, tcnt, ntiles, x, true, max_out, out, n_out, ctr, ovf_out, nullptr, s_w, s_c);
   } else if (blockIdx.x - ntiles < n_entries) {
@@ -2237,6 +2308,7 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
   if (!ident && s->vcap == 0 && !grow_vscratch(s, 1, st)) return RTPS_RX_ENOMEM;
   const bool reliable = !(flags & RTPS_INGEST_BEST_EFFORT);
   const FarSrc fs{records, dgram_off};
+  const SigCfg cfg{ident ? 1u : 0u, t.n_proxies, s->path, reliable ? 1u : 0u};
   if (++s->epoch == 0xffffffffu) {  // keys would wrap: clear the first-cover table
     if (hipMemsetAsync(s->st.fc, 0xff, (uint64_t)s->ecap * W * 8, st) != hipSuccess) return RTPS_RX_EHIP;
     s->epoch = 1;
@@ -2327,7 +2399,20 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
   // pinned memory, the host spins on the tag (no copy, no interrupt-driven wait); a wait past
   // the limit falls back to a stream sync (a failed launch surfaces there)
   const uint64_t tag = ++s->sig_tag;
-  hipLaunchKernelGGL(k_signal, dim3(1), dim3(64), 0, st, S.ctr, s->hsig, tag);
+  if (ident) {
+    // the plain global path's two launches, queued now: they run at once if the batch's counts
+    // make it plain and return otherwise (the host then launches the batch's path below); the
+    // decide launch signals the counts and its verdict to the host
+    const uint32_t ntiles = (uint32_t)((max + DT - 1) / DT);
+    const uint32_t nfcm = (uint32_t)((uint64_t)t.n_proxies * W / FCM_POS);
+    hipLaunchKernelGGL(k_decide_t<3>, dim3(ntiles + nfcm), dim3(IT), 0, st, max, max, x, S, out->accept, false,
+                       s->epoch, x.sel, fs, ntiles, SigOut{s->hsig, tag, cfg});
+    hipLaunchKernelGGL(k_dstate, dim3(ntiles + t.n_proxies), dim3(IT), 0, st, out->accept, max, x.sel, ntiles, x,
+                       out->max_accepted, out->accepted, out->n_accepted, S.ctr, out->n_window_overflow, t.n_proxies,
+                       S, false, out->ack_base, false, true);
+  } else {
+    hipLaunchKernelGGL(k_signal, dim3(1), dim3(64), 0, st, S.ctr, s->hsig, tag, cfg);
+  }
   if (hipGetLastError() != hipSuccess) return RTPS_RX_EHIP;
   {
     volatile uint64_t* hs = s->hsig;
@@ -2343,6 +2428,7 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
   }
   const uint64_t n_hb = s->hsig[SIG_HB], n_gap = s->hsig[SIG_GAP], n_ev = s->hsig[SIG_EV], n_free = s->hsig[SIG_FREE];
   const uint64_t n_rec = s->hsig[SIG_NREC], farc = s->hsig[SIG_FARC];
+  if (ident && s->hsig[SIG_MODE] != 0) return RTPS_RX_OK;  // the queued plain path runs it
   // events live at [0, nev): record slots in identity batches, the expanded list otherwise
   uint64_t nev = ident ? n_rec : n_ev;
   if (!ident) {
@@ -2429,20 +2515,20 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
     const uint32_t nfcm = fc_merge ? (uint32_t)((uint64_t)t.n_proxies * W / FCM_POS) : 0u;
     if (fc_merge)
       hipLaunchKernelGGL(k_decide_t<2>, dim3(ntiles + nfcm), dim3(IT), 0, st, nev, acc_cap, x, S, acc, have_hb,
-                         s->epoch, x.sel, fs, ntiles);
+                         s->epoch, x.sel, fs, ntiles, SigOut{});
     else if (n_gap == 0)
       hipLaunchKernelGGL(k_decide_t<1>, dim3(ntiles), dim3(IT), 0, st, nev, acc_cap, x, S, acc, have_hb, s->epoch,
-                         x.sel, fs, ntiles);
+                         x.sel, fs, ntiles, SigOut{});
     else
       hipLaunchKernelGGL(k_decide_t<0>, dim3(ntiles), dim3(IT), 0, st, nev, acc_cap, x, S, acc, have_hb, s->epoch,
-                         x.sel, fs, ntiles);
+                         x.sel, fs, ntiles, SigOut{});
     if (farc)  // samples / GAPs past some window: their replay (fixes accept[] and the tile counts)
       hipLaunchKernelGGL(k_far, dim3(1), dim3(KF), 0, st, S, arena, acc, x.sel);
     if (n_gap)
       hipLaunchKernelGGL(k_merge, dim3(gv), dim3(IT), 0, st, records, arena, dgram_off, nev, x, S, true);
     hipLaunchKernelGGL(k_dstate, dim3(ntiles + t.n_proxies), dim3(IT), 0, st, acc, acc_cap, x.sel, ntiles, x,
                        out->max_accepted, out->accepted, out->n_accepted, S.ctr, out->n_window_overflow, t.n_proxies,
-                       S, have_hb, out->ack_base, fc_merge);
+                       S, have_hb, out->ack_base, fc_merge, false);
     return hipGetLastError() == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP;
   }
   if (nev && !per_proxy) {
