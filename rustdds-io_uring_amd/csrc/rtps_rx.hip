@@ -1124,6 +1124,13 @@ __global__ __launch_bounds__(TILE, RTPS_CH_WAVES_PER_SIMD) void rtps_parse_chain
 #define RTPS_IT_CAPW 512u
 #endif
 constexpr uint32_t CAPW = RTPS_IT_CAPW;  // items per wave slab (C3 averages 243 per 64 datagrams)
+// Wide items (48 B): the item also carries the submessage's 32-B window as the walk loaded it
+// (with the tail the record's reader needs), so that the record pass reads it coalesced with
+// the item instead of gathering it from the datagram again.
+#ifndef RTPS_IT_WIDE
+#define RTPS_IT_WIDE 0  // measured: E +49 us, W -11 us on C3
+#endif
+constexpr uint32_t IW = RTPS_IT_WIDE ? 3u : 1u;  // u32x4 per item
 constexpr uint32_t WCNT_OVERFLOW = 0x80000000u;
 #ifndef RTPS_IT_WAVES_PER_SIMD
 #define RTPS_IT_WAVES_PER_SIMD 8
@@ -1155,7 +1162,7 @@ __device__ uint32_t item_walk(const KParams& p, const Src& s, const uint32_t* H,
     if (rem < 4u) return RTPS_DGRAM_SUBMSG_ERR;
     Win W;
     if (o == 20u) head_win(H, W);
-    else load_win_lazy<false>(s, o, W);
+    else load_win_lazy<RTPS_IT_WIDE != 0>(s, o, W);
     const uint32_t kind = W.w[0] & 0xffu, flags = (W.w[0] >> 8) & 0xffu;
     const bool le = (flags & 1u) != 0u;
     const uint32_t eff = eff_len(kind, e16(W.w[0], 1, le), rem);
@@ -1169,11 +1176,16 @@ __device__ uint32_t item_walk(const KParams& p, const Src& s, const uint32_t* H,
     const uint64_t m = __ballot(em);
     if (em) {
       const uint32_t pos = wpos + (uint32_t)__popcll(m & lt);
-      if (pos < CAPW)
-        slab[pos] = u32x4{o | (src_off << 16),
-                          nrec | (lane << 16) | ((st.dst_ok ? 1u : 0u) << 22) | ((st.ts_valid ? 1u : 0u) << 23) |
-                              (kind << 24),
-                          st.ts_sec, st.ts_frac};
+      if (pos < CAPW) {
+        slab[pos * IW] = u32x4{o | (src_off << 16),
+                               nrec | (lane << 16) | ((st.dst_ok ? 1u : 0u) << 22) | ((st.ts_valid ? 1u : 0u) << 23) |
+                                   (kind << 24),
+                               st.ts_sec, st.ts_frac};
+        if (IW == 3u) {
+          slab[pos * IW + 1] = u32x4{W.w[0], W.w[1], W.w[2], W.w[3]};
+          slab[pos * IW + 2] = u32x4{W.w[4], W.w[5], W.w[6], W.w[7]};
+        }
+      }
       nrec++;
     }
     wpos += (uint32_t)__popcll(m);
@@ -1190,7 +1202,7 @@ __global__ __launch_bounds__(TILE, RTPS_IT_WAVES_PER_SIMD) void rtps_parse_item_
   const uint32_t tile = blockIdx.x;
   TileCtx t;
   load_tile(p, tile, t);
-  u32x4* slab = items + (size_t)(tile * WAVES + wave) * CAPW;
+  u32x4* slab = items + (size_t)(tile * WAVES + wave) * CAPW * IW;
   uint32_t cnt = 0, wpos = 0, st = RTPS_DGRAM_OK;
   if (t.valid) {
     if (!t.addressable) st = RTPS_DGRAM_TOO_LONG;
@@ -1377,8 +1389,9 @@ void rtps_parse_emit_kernel(KParams p, uint32_t n_tiles, const u32x4* items, con
   }
   __syncthreads();
   const uint32_t total = s_nit[WAVES];
-  const u32x4* tslab = items + (size_t)tile * WAVES * CAPW;
+  const u32x4* tslab = items + (size_t)tile * WAVES * CAPW * IW;
 #ifdef RTPS_EM_SORT
+  static_assert(!RTPS_IT_WIDE, "the kind-sorted variant takes 16-B items (-DRTPS_IT_WIDE=0)");
   // tuning variant: the tile's items bucketed by kind in LDS first, so that a wave's lanes
   // run the same per-kind reader (the slab order interleaves kinds)
   constexpr uint32_t NCL = 8, RND = WAVES * CAPW / EMT, SLOTS = RND * (EMT / 64);
@@ -1427,7 +1440,8 @@ void rtps_parse_emit_kernel(KParams p, uint32_t n_tiles, const u32x4* items, con
 #else
   for (uint32_t k = tid; k < total; k += EMT) {
     const uint32_t w = (k >= s_nit[1]) + (k >= s_nit[2]) + (k >= s_nit[3]);
-    const u32x4 it = tslab[w * CAPW + (k - s_nit[w])];
+    const size_t ib = (size_t)(w * CAPW + (k - s_nit[w])) * IW;
+    const u32x4 it = tslab[ib];
     const uint32_t jmask = 0xffffu;
     const uint32_t o = it[0] & 0xffffu, src_off = it[0] >> 16;
 #endif
@@ -1437,9 +1451,13 @@ void rtps_parse_emit_kernel(KParams p, uint32_t n_tiles, const u32x4* items, con
     s.base = s_doff[d];
     Win W;
     {
+#if RTPS_IT_WIDE
+      const u32x4 a = tslab[ib + 1], b = tslab[ib + 2];  // the window as the walk loaded it
+#else
       const u32x4 a = ld16(s, o);
       u32x4 b = {0u, 0u, 0u, 0u};
       if (win_needs_tail<true>(kind)) b = ld16(s, o + 16u);
+#endif
       W.w[0] = a[0]; W.w[1] = a[1]; W.w[2] = a[2]; W.w[3] = a[3];
       W.w[4] = b[0]; W.w[5] = b[1]; W.w[6] = b[2]; W.w[7] = b[3];
       W.w[8] = kind == RTPS_DATA_FRAG ? ld4(s, o + 32u) : 0u;
@@ -2540,7 +2558,7 @@ static int parse_launch(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len
       c->rs_tiles = 0;  // (the wave counts and prefixes are shared)
       const uint32_t t = (uint32_t)(((size_t)c->max_datagrams + TILE - 1) / TILE) > tiles
                              ? (uint32_t)(((size_t)c->max_datagrams + TILE - 1) / TILE) : tiles;
-      if (hipMalloc(&c->it_items, (size_t)t * WAVES * CAPW * sizeof(u32x4)) != hipSuccess ||
+      if (hipMalloc(&c->it_items, (size_t)t * WAVES * CAPW * IW * sizeof(u32x4)) != hipSuccess ||
           hipMalloc(&c->it_wcnt, (size_t)t * WAVES * sizeof(uint32_t)) != hipSuccess ||
           hipMalloc(&c->it_prefix, (size_t)t * sizeof(uint64_t)) != hipSuccess)
         return RTPS_RX_ENOMEM;

@@ -20,7 +20,7 @@
 //                    (position < cap and blob end <= bcap: a prefix of the
 //                    destination's items, since both grow with position), else
 //                    to the spill at its exact-layout position; the first item
-//                    that does not fit sets the cut (atomicMin).  The blobs go
+//                    that does not fit sets the cut.  The blobs go
 //                    with their records: small ones copied by their lane, long
 //                    DATA_FRAG payloads by whole waves (16 B per lane).
 // Unpack (owner), with the counts on the host:
@@ -256,24 +256,13 @@ __global__ __launch_bounds__(ST) void shard_scatter(PackArgs a) {
     for (uint32_t v = 0; v < wave; ++v) { pos += wcnt[v][o]; boff += wbyt[v][o]; }
     slot = pos < a.cap && boff + size <= a.bcap;
   }
-  // each destination's first spilled item and byte: the minimum over the wave's spilled
-  // lanes, one atomic per (wave, destination) (a batch that mostly spills would otherwise
-  // serialise on two addresses)
-  for (uint32_t d = 0; d < n; ++d) {
-    const bool sp = o == d && !slot;
-    const uint64_t mm = __ballot(sp);
-    if (mm == 0) continue;
-    uint64_t mp = sp ? pos : ~0ull, mb = sp ? boff : ~0ull;
-#pragma unroll
-    for (uint32_t sft = 1; sft < 64; sft <<= 1) {
-      const uint64_t yp = __shfl_xor(mp, sft, 64), yb = __shfl_xor(mb, sft, 64);
-      mp = yp < mp ? yp : mp;
-      mb = yb < mb ? yb : mb;
-    }
-    if (lane == (uint32_t)__builtin_ctzll(mm)) {
-      atomicMin((unsigned long long*)&a.counts[d].cut, (unsigned long long)mp);
-      atomicMin((unsigned long long*)&a.counts[d].cut_bytes, (unsigned long long)mb);
-    }
+  // each destination's cut: its first item that does not fit (both position and blob end grow
+  // with the position, so the items that fit are a prefix).  That item is the one whose
+  // predecessor fit (position - 1 < cap, its blob ending at this one's start <= bcap): a single
+  // writer per destination, no atomics (the scan set cut = n for a destination that all fits)
+  if (o != NONE && !slot && (pos == 0 || (pos - 1u < a.cap && boff <= a.bcap))) {
+    a.counts[o].cut = pos;
+    a.counts[o].cut_bytes = boff;
   }
   if (o != NONE) {
     shard_item* it = slot ? a.slots + (uint64_t)o * a.cap + pos : a.spill + sbase[o] + pos;
