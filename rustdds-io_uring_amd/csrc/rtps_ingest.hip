@@ -308,6 +308,9 @@ constexpr uint32_t BK_IDX = 4096;  // k_proxy's sampled piece index: proxies of 
 #ifndef RTPS_PB_CHR
 #define RTPS_PB_CHR 1024
 #endif
+#ifndef RTPS_CL_PRELOAD
+#define RTPS_CL_PRELOAD 1
+#endif
 constexpr uint32_t CHR = RTPS_PB_CHR;         // record slots per classify workgroup
 constexpr uint32_t PB_SUB = CHR / (IT / 64);  // slots per wave
 constexpr uint32_t PB_STEPS = PB_SUB / 64;
@@ -365,7 +368,8 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
   uint32_t nh = 0, ng = 0, ne = 0, nf = 0, nfar = 0;
   // record slot i: its events; FAST: *key = the proxy of its proxied event (NONE: none)
   // and *P its packed form, stored at pev[i] unless BUCKET (which places it itself)
-  auto body = [&](uint64_t i, uint32_t& key, PEv& P) {
+  // rq: the record's four 16-B quads (global memory, or registers the caller filled ahead)
+  auto body = [&](uint64_t i, uint32_t& key, PEv& P, const u32x4* rq) {
     uint8_t ev = EV_NONE;
     uint32_t set = NONE;
     int64_t sn = 0;
@@ -376,7 +380,7 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
       // bytes 0..31 of the record (kind @6, prefix||writer_id @8, route @30,
       // payload_kind @31), then 32..47 (sn, gap.list_base) for the candidates:
       // three of the record's four 16-B quads at most
-      const u32x4* q = reinterpret_cast<const u32x4*>(recs + i);
+      const u32x4* q = rq;
       q0 = q[0];
       const u32x4 q1 = q[1];
       const uint32_t kind = (q0[1] >> 16) & 0xffu, route = (q1[3] >> 16) & 0xffu, pk = q1[3] >> 24;
@@ -497,18 +501,34 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
     for (uint64_t i = (uint64_t)blockIdx.x * IT + tid; i < max; i += (uint64_t)gridDim.x * IT) {
       uint32_t key;
       PEv P;
-      body(i, key, P);
+      body(i, key, P, reinterpret_cast<const u32x4*>(recs + i));
     }
   } else {
     // wave w: slots [c0, c0 + PB_SUB) in PB_STEPS steps of 64; the proxied events stay in registers
     const uint64_t c0 = (uint64_t)blockIdx.x * CHR + (uint64_t)wave * PB_SUB;
     uint32_t key[PB_STEPS];
     PEv P[PB_STEPS];
+#if RTPS_CL_PRELOAD
+    // every step's record loaded ahead (whole 64-B records: the same lines), so that the steps'
+    // loads are in flight together instead of one step's dependent chain at a time
+    u32x4 rq[PB_STEPS][4];
+#pragma unroll
+    for (uint32_t j = 0; j < PB_STEPS; ++j) {
+      const uint64_t i = c0 + j * 64u + lane;
+      const u32x4* q = reinterpret_cast<const u32x4*>(recs + i);
+#pragma unroll
+      for (uint32_t k = 0; k < 4; ++k) rq[j][k] = i < n ? q[k] : u32x4{0u, 0u, 0u, 0u};
+    }
+#endif
 #pragma unroll
     for (uint32_t j = 0; j < PB_STEPS; ++j) {
       const uint64_t i = c0 + j * 64u + lane;
       key[j] = NONE;
-      if (i < max) body(i, key[j], P[j]);
+#if RTPS_CL_PRELOAD
+      if (i < max) body(i, key[j], P[j], rq[j]);
+#else
+      if (i < max) body(i, key[j], P[j], reinterpret_cast<const u32x4*>(recs + i));
+#endif
       if (key[j] != NONE) atomicAdd(&s_cnt[wave][key[j]], 1u);
     }
     __syncthreads();
