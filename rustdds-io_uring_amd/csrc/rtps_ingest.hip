@@ -306,10 +306,16 @@ constexpr uint32_t PB_MAX = 1024;  // proxies of the bucketing path (LDS counter
 constexpr uint32_t BK_MAX = 4096;  // classify workgroups of the bucketing path (k_proxy's LDS tables)
 constexpr uint32_t BK_IDX = 4096;  // k_proxy's sampled piece index: proxies of up to 4 x BK_IDX events
 #ifndef RTPS_PB_CHR
-#define RTPS_PB_CHR 1024
+#define RTPS_PB_CHR 2048  // measured on C3: 1024 -> 2048 classify +2 us, k_proxy -8 (half the pieces)
 #endif
 #ifndef RTPS_CL_PRELOAD
-#define RTPS_CL_PRELOAD 1
+#define RTPS_CL_PRELOAD 0  // measured: classify 139 -> 145 us on C3 (VGPRs 77 -> 94)
+#endif
+#ifndef RTPS_CL_GAP_INLINE
+#define RTPS_CL_GAP_INLINE 0  // 1: classify reads short GAP bitmaps inline (a second dependent load)
+#endif
+#ifndef RTPS_CL_FULLREC
+#define RTPS_CL_FULLREC 1  // the whole record in one round trip
 #endif
 constexpr uint32_t CHR = RTPS_PB_CHR;         // record slots per classify workgroup
 constexpr uint32_t PB_SUB = CHR / (IT / 64);  // slots per wave
@@ -332,13 +338,31 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x, uint32_t lane) {
 // (the proxy bucketing above) instead of the radix sort's (key, slot) pairs.
 // MARK (IDENT, not FAST): also the samples' first-cover keys (the marks of the global path,
 // k_marks_d's atomicMin), so that the global path needs no separate marks pass.
+#if defined(RTPS_PROXY_STAMPS) || defined(RTPS_CLS_STAMPS)  // tuning builds: phase timestamps
+__device__ unsigned long long g_proxy_stamps[16384 * 16];
+#endif
+#ifdef RTPS_CLS_STAMPS  // bucketing classify: wave 0's absolute times at its phase ends, per workgroup
+#define CST(k) do { if (BUCKET && threadIdx.x == 0) g_proxy_stamps[blockIdx.x * 16u + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+// inside a record step: wait for everything outstanding, then add the time since the last mark
+// to phase sum k (slots 8.. of the workgroup's 16)
+#define CSS(k) do { if (BUCKET) { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); \
+  const uint64_t t_ = __builtin_amdgcn_s_memrealtime(); css[k] += t_ - css_t; css_t = t_; } } while (0)
+#define CSS_DECL uint64_t css[4] = {0, 0, 0, 0}, css_t = __builtin_amdgcn_s_memrealtime()
+#define CSS_FLUSH() do { if (BUCKET && threadIdx.x == 0) for (uint32_t k_ = 0; k_ < 4; ++k_) g_proxy_stamps[blockIdx.x * 16u + 8u + k_] = css[k_]; } while (0)
+#else
+#define CST(k) do {} while (0)
+#define CSS(k) do {} while (0)
+#define CSS_DECL do {} while (0)
+#define CSS_FLUSH() do {} while (0)
+#endif
 template <bool IDENT, bool FAST, bool BUCKET = false, bool MARK = false>
 __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record* recs, const uint64_t* n_rec,
                                                  uint64_t max, const rtps_frag_sample* frag, uint32_t flags,
                                                  Scratch x, uint64_t* ctr, FastOut fo, uint64_t* ctr_next, State st,
                                                  uint32_t epoch) {
-  extern __shared__ uint32_t s_rt[];
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_rt[];  // (rt_writer_set reads 16-B keys)
   __shared__ uint32_t s_cnt[BUCKET ? IT / 64 : 1][BUCKET ? PB_MAX : 1];  // per (wave, proxy)
+  CST(0);
   if (blockIdx.x == gridDim.x - 1u)  // the next batch's counters start at zero (no memset launch)
     for (uint32_t c = threadIdx.x; c < C_COUNT; c += IT) ctr_next[c] = 0ull;
   __shared__ uint32_t s_part[IT / 64];
@@ -350,22 +374,19 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
   if (BUCKET)
     for (uint32_t e = lane; e < t.n_proxies; e += 64) s_cnt[wave][e] = 0u;
   const bool lds = rt_fits_lds(t);
-  if (lds) rt_stage(t, s_rt);
-  // the target sets behind the hash tables (when the host sized the LDS for them): a record's
-  // set entries then cost two LDS reads instead of two dependent global loads
+  // the tables, and the target sets behind them when the host sized the LDS for them (a
+  // record's set entries then cost two LDS reads instead of two dependent global loads): one
+  // flat copy of the device image
   uint32_t* const s_sf = s_rt + rt_lds_bytes(t.gmask + 1u, t.emask + 1u) / 4u;
   const rtps_target* const s_se = reinterpret_cast<const rtps_target*>(s_sf + t.n_sets + 1u);
-  if (fo.sets_lds) {
-    for (uint32_t i = tid; i <= t.n_sets; i += IT) s_sf[i] = t.set_first[i];
-    const uint32_t* ge = reinterpret_cast<const uint32_t*>(t.set_ent);
-    uint32_t* le = s_sf + t.n_sets + 1u;
-    for (uint32_t i = tid; i < 2u * t.n_ent; i += IT) le[i] = ge[i];
-  }
+  if (lds) rt_copy(s_rt, t.gkeys, fo.sets_lds ? rt_image_words(t) : rt_lds_words(t));
   const uint32_t* const sfirst = fo.sets_lds ? s_sf : t.set_first;
   const rtps_target* const sent = fo.sets_lds ? s_se : t.set_ent;
   if (lds || BUCKET) __syncthreads();
+  CST(1);
   const bool reliable = !(flags & RTPS_INGEST_BEST_EFFORT);
   uint32_t nh = 0, ng = 0, ne = 0, nf = 0, nfar = 0;
+  CSS_DECL;
   // record slot i: its events; FAST: *key = the proxy of its proxied event (NONE: none)
   // and *P its packed form, stored at pev[i] unless BUCKET (which places it itself)
   // rq: the record's four 16-B quads (global memory, or registers the caller filled ahead)
@@ -381,8 +402,14 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
       // payload_kind @31), then 32..47 (sn, gap.list_base) for the candidates:
       // three of the record's four 16-B quads at most
       const u32x4* q = rq;
+      CSS(3);
       q0 = q[0];
       const u32x4 q1 = q[1];
+#if RTPS_CL_FULLREC
+      // the rest of the record in the same round trip (same 64-B line), not after the kind test
+      const u32x4 f2 = q[2], f3 = q[3];
+#endif
+      CSS(0);
       const uint32_t kind = (q0[1] >> 16) & 0xffu, route = (q1[3] >> 16) & 0xffu, pk = q1[3] >> 24;
       const uint32_t f = frag ? x.fidx[i] : NONE;
       // records the receiver passes to the user readers (not a builtin pair: discovery's)
@@ -391,8 +418,13 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
           ev = EV_SAMPLE;
           sn = frag[f].sn;
         } else if (kind == RTPS_DATA || kind == RTPS_HEARTBEAT || kind == RTPS_GAP) {
+#if RTPS_CL_FULLREC
+          q2 = f2;
+          q3 = f3;
+#else
           q2 = q[2];
           if ((FAST && kind != RTPS_DATA) || (MARK && kind == RTPS_GAP)) q3 = q[3];
+#endif
           const int64_t rsn = (int64_t)(((uint64_t)q2[1] << 32) | q2[0]);
           if (kind == RTPS_DATA) {
             // data_to_dds_data must succeed (reader.rs:552-558)
@@ -414,6 +446,7 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
         }
       }
     }
+    CSS(1);
     // the record's events: one per target reader that the event concerns (a completed
     // DataFrag sample: the readers whose assembler completed it)
     uint32_t cnt = 0;
@@ -436,6 +469,7 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
       }
     }
     ne += cnt;
+    CSS(2);
     if (IDENT) {  // at most one event: write it at index i
       const uint8_t evi = cnt ? ev : EV_NONE;
       x.emeta[i] = meta;
@@ -480,7 +514,9 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
             const bool le = (fl & 1u) != 0u;
             P.m |= (le ? PM_LE : 0u) | (nbits << 8);
             P.bw = fo.dgram_off[q0[0]] + (q3[1] & 0xffffu);  // dgram_idx, u.gap.bitmap_off
-            if (nbits <= 64u) {
+            // (RTPS_CL_GAP_INLINE: short bitmaps read here, a dependent load that holds the wave;
+            // measured: classify -15 us, k_proxy +6 on C3 without it)
+            if (RTPS_CL_GAP_INLINE && nbits <= 64u) {
               const uint8_t* bp = fo.arena + P.bw;
               const uint32_t w0 = nbits ? rd32(bp, le) : 0u, w1 = nbits > 32u ? rd32(bp + 4, le) : 0u;
               P.bw = (uint64_t)w0 | ((uint64_t)w1 << 32);
@@ -531,7 +567,11 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
 #endif
       if (key[j] != NONE) atomicAdd(&s_cnt[wave][key[j]], 1u);
     }
+    CSS(3);
+    CSS_FLUSH();
+    CST(2);
     __syncthreads();
+    CST(3);
     // the workgroup's region: proxies in order, each proxy's events in slot order (waves in
     // order); thread t owns proxies [t * PPB, t * PPB + PPB)
     constexpr uint32_t PPB = PB_MAX / IT;
@@ -564,6 +604,7 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
       }
     }
     __syncthreads();
+    CST(4);
     PEv* region = fo.pev + (uint64_t)blockIdx.x * CHR;
 #pragma unroll
     for (uint32_t j = 0; j < PB_STEPS; ++j) {
@@ -598,6 +639,7 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
       pos = (uint32_t)__builtin_amdgcn_ds_permute((int)(sl << 2), (int)pos);
       if (key[j] != NONE) region[pos] = P[j];
     }
+    CST(5);
   }
   __shared__ uint32_t s_n[4];
   if (tid < 4) s_n[tid] = 0;
@@ -615,6 +657,7 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
     atomicAdd(reinterpret_cast<unsigned long long*>(ctr + C_SPREAD + 4u * (blockIdx.x & 63u) + tid),
               (unsigned long long)s_n[tid]);
   if (MARK && nfar) atomicAdd(reinterpret_cast<unsigned long long*>(ctr + C_FARC), (unsigned long long)nfar);
+  CST(6);
 }
 
 // The batch's counts to pinned host memory (one wave, after classify): the sums, then the tag
@@ -1570,7 +1613,6 @@ __global__ __launch_bounds__(IT) void k_dstate(const uint8_t* flag, uint64_t n, 
 // host picks this path only when the mean load per proxy is small.
 #ifdef RTPS_PROXY_STAMPS  // tuning builds: per-phase time sums of k_proxy, per proxy
 constexpr uint32_t PST_N = 8;
-__device__ unsigned long long g_proxy_stamps[16384 * PST_N];
 #define PST_DECL uint64_t pst_t = __builtin_amdgcn_s_memrealtime(), pst_acc[PST_N] = {0, 0, 0, 0, 0, 0, 0, 0}
 #define PST(k) do { const uint64_t t_ = __builtin_amdgcn_s_memrealtime(); pst_acc[k] += t_ - pst_t; pst_t = t_; } while (0)
 #define PST_FLUSH(e) do { if (threadIdx.x == 0) for (uint32_t k_ = 0; k_ < PST_N; ++k_) g_proxy_stamps[(e) * PST_N + k_] = pst_acc[k_]; } while (0)
@@ -2136,8 +2178,8 @@ void rtps_ingest_set_path(IngestState* s, uint32_t path) { s->path = path; }
 
 // tuning builds (RTPS_PROXY_STAMPS): k_proxy's per-proxy phase sums (100 MHz ticks), PST_N per proxy
 int rtps_ingest_proxy_stamps(uint64_t* host, uint64_t n) {
-#ifdef RTPS_PROXY_STAMPS
-  if (n > 16384ull * PST_N) n = 16384ull * PST_N;
+#if defined(RTPS_PROXY_STAMPS) || defined(RTPS_CLS_STAMPS)
+  if (n > 16384ull * 16) n = 16384ull * 16;
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_proxy_stamps), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess
              ? RTPS_RX_OK : RTPS_RX_EHIP;
 #else

@@ -47,8 +47,8 @@ struct ReaderTable {
 
 ReaderTable* rt_new() { return new (std::nothrow) ReaderTable(); }
 
-// Device memory of the tables.  rt_set builds every image into fresh buffers and
-// swaps them in only when all of them are uploaded, so a failed call leaves the
+// Device memory of the tables.  rt_set builds the image into a fresh buffer and
+// swaps it in only when all of it is uploaded, so a failed call leaves the
 // previous table whole (readers and proxies of the last successful call).  The
 // operations are indirect so that a CPU test can run rt_set on host memory with
 // an injected allocation failure (rtps_rx_debug_rt_* below).
@@ -76,8 +76,7 @@ DevMem g_mem = {hip_alloc, hip_release, hip_upload, hip_sync};
 
 void rt_free(ReaderTable* t) {
   if (!t) return;
-  void* p[] = {t->gkeys, t->gset, t->ekeys, t->eset, t->dfirst, t->dent};
-  for (void* q : p) g_mem.release(q);
+  g_mem.release(t->gkeys);  // the one image buffer (gkeys is its base)
   delete t;
 }
 
@@ -164,7 +163,11 @@ int build(const rtps_reader* readers, uint32_t nr, const rtps_proxy* proxies, ui
   }
   first.push_back((uint32_t)ent.size());
   // ---- hash tables ----
-  const uint32_t gcap = pow2_at_least(2ull * wsets.size()), ecap = pow2_at_least(2ull * esets.size());
+  uint32_t gcap = pow2_at_least((uint64_t)RT_SLACK * wsets.size()), ecap = pow2_at_least((uint64_t)RT_SLACK * esets.size());
+  if (rt_lds_bytes(gcap, ecap) > RT_LDS_MAX) {  // the sparse tables would leave LDS: the dense ones
+    gcap = pow2_at_least((uint64_t)RT_SLACK_MIN * wsets.size());
+    ecap = pow2_at_least((uint64_t)RT_SLACK_MIN * esets.size());
+  }
   std::vector<uint32_t> gkeys((size_t)gcap * 4, 0u), gset(gcap, RTPS_NO_TARGET), ekeys(ecap, 0u),
       eset(ecap, RTPS_NO_TARGET);
   for (uint32_t s = 0; s < wsets.size(); ++s) {
@@ -203,24 +206,23 @@ int rt_set(ReaderTable* t, const rtps_reader* readers, uint32_t nr, const rtps_p
   std::vector<rtps_target>& ent = b.ent;
   // ---- upload into new buffers; swap them in only when every step succeeded ----
   if (!g_mem.sync(stream)) return RTPS_RX_EHIP;  // the previous batch may still read the old tables
-  void* nb[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  // one buffer, the arrays back to back (ReaderDev: the LDS image, then the target sets)
+  static_assert(sizeof(rtps_target) == 8 && alignof(rtps_target) <= 4, "target entries at word offsets");
   const void* src[6] = {gkeys.data(), gset.data(), ekeys.data(), eset.data(), first.data(), ent.data()};
   const size_t bytes[6] = {gkeys.size() * 4, gset.size() * 4, ekeys.size() * 4, eset.size() * 4, first.size() * 4,
                            ent.size() * sizeof(rtps_target)};
-  int err = RTPS_RX_OK;
-  for (int k = 0; k < 6 && !err; ++k) {
-    nb[k] = g_mem.alloc(bytes[k]);
-    if (!nb[k]) err = RTPS_RX_ENOMEM;
-    else if (!g_mem.upload(nb[k], src[k], bytes[k])) err = RTPS_RX_EHIP;
-  }
-  if (err) {
-    for (void* q : nb) g_mem.release(q);
-    return err;
-  }
-  void* old[6] = {t->gkeys, t->gset, t->ekeys, t->eset, t->dfirst, t->dent};
-  for (void* q : old) g_mem.release(q);
-  t->gkeys = (uint32_t*)nb[0]; t->gset = (uint32_t*)nb[1]; t->ekeys = (uint32_t*)nb[2]; t->eset = (uint32_t*)nb[3];
-  t->dfirst = (uint32_t*)nb[4]; t->dent = (rtps_target*)nb[5];
+  size_t off[7] = {0};
+  for (int k = 0; k < 6; ++k) off[k + 1] = off[k] + bytes[k];
+  uint8_t* img = static_cast<uint8_t*>(g_mem.alloc(off[6]));
+  if (!img) return RTPS_RX_ENOMEM;
+  for (int k = 0; k < 6; ++k)
+    if (!g_mem.upload(img + off[k], src[k], bytes[k])) {
+      g_mem.release(img);
+      return RTPS_RX_EHIP;
+    }
+  g_mem.release(t->gkeys);  // (the previous image: gkeys is its base)
+  t->gkeys = (uint32_t*)(img + off[0]); t->gset = (uint32_t*)(img + off[1]); t->ekeys = (uint32_t*)(img + off[2]);
+  t->eset = (uint32_t*)(img + off[3]); t->dfirst = (uint32_t*)(img + off[4]); t->dent = (rtps_target*)(img + off[5]);
   t->gcap = gcap;  // the images above are exactly gcap / ecap slots
   t->ecap = ecap;
   t->first.swap(first);

@@ -17,6 +17,8 @@
 
 #include "../../include/rtps_rx.h"
 
+// The six arrays are one device buffer, in this order and with no gaps (the LDS image of
+// rt_stage, then set_first and set_ent): staging copies one flat range of gkeys.
 struct ReaderDev {             // device view (kernel argument by value); gkeys == nullptr: no readers
   const uint32_t* gkeys;       // [gmask + 1] x 4 words: writer GUID keys (prefix || entity id, raw LE words)
   const uint32_t* gset;        // [gmask + 1] writer set of the slot, RTPS_NO_TARGET = empty slot
@@ -44,21 +46,33 @@ __host__ __device__ inline uint32_t rt_hash4(uint32_t e) {
 // LDS image of the two hash tables: gkeys (16 B), gset, ekeys, eset per slot.
 __host__ __device__ constexpr uint32_t rt_lds_bytes(uint32_t gcap, uint32_t ecap) { return gcap * 20u + ecap * 8u; }
 constexpr uint32_t RT_LDS_MAX = 48u * 1024u;  // larger tables are probed in global memory (L2)
+// hash slots per key: 4 (load <= 1/4: short probe runs, a wave waits for its longest) while the
+// tables fit RT_LDS_MAX, else 2
+constexpr uint32_t RT_SLACK = 4u, RT_SLACK_MIN = 2u;
 __host__ __device__ inline bool rt_fits_lds(const ReaderDev& r) {
   return r.gkeys != nullptr && rt_lds_bytes(r.gmask + 1u, r.emask + 1u) <= RT_LDS_MAX;
 }
 
 #ifdef __HIPCC__
-// Stage the tables into dynamic shared memory `lds` (uint32 words).  Caller syncs.
-__device__ inline void rt_stage(const ReaderDev& r, uint32_t* lds) {
-  const uint32_t gcap = r.gmask + 1u, ecap = r.emask + 1u;
-  for (uint32_t i = threadIdx.x; i < gcap * 4u; i += blockDim.x) lds[i] = r.gkeys[i];
-  uint32_t* gs = lds + gcap * 4u;
-  for (uint32_t i = threadIdx.x; i < gcap; i += blockDim.x) gs[i] = r.gset[i];
-  uint32_t* ek = gs + gcap;
-  uint32_t* es = ek + ecap;
-  for (uint32_t i = threadIdx.x; i < ecap; i += blockDim.x) { ek[i] = r.ekeys[i]; es[i] = r.eset[i]; }
+// n words from src (global, 16-B aligned) to dst (LDS, 16-B aligned) by the workgroup: 16-B
+// loads, four in flight per thread before their stores.  Caller syncs.
+__device__ inline void rt_copy(uint32_t* dst, const uint32_t* src, uint32_t n) {
+  const uint32_t n4 = n / 4u, bs = blockDim.x;
+  const uint4* s4 = reinterpret_cast<const uint4*>(src);
+  uint4* d4 = reinterpret_cast<uint4*>(dst);
+  uint32_t k = threadIdx.x;
+  for (; k + 3u * bs < n4; k += 4u * bs) {
+    const uint4 a = s4[k], b = s4[k + bs], c = s4[k + 2u * bs], d = s4[k + 3u * bs];
+    d4[k] = a; d4[k + bs] = b; d4[k + 2u * bs] = c; d4[k + 3u * bs] = d;
+  }
+  for (; k < n4; k += bs) d4[k] = s4[k];
+  for (uint32_t i = n4 * 4u + threadIdx.x; i < n; i += bs) dst[i] = src[i];
 }
+// words of the tables' LDS image; with the target sets (set_first, set_ent) behind them
+__host__ __device__ inline uint32_t rt_lds_words(const ReaderDev& r) { return rt_lds_bytes(r.gmask + 1u, r.emask + 1u) / 4u; }
+__host__ __device__ inline uint32_t rt_image_words(const ReaderDev& r) { return rt_lds_words(r) + r.n_sets + 1u + 2u * r.n_ent; }
+// Stage the tables into dynamic shared memory `lds` (uint32 words, 16-B aligned).  Caller syncs.
+__device__ inline void rt_stage(const ReaderDev& r, uint32_t* lds) { rt_copy(lds, r.gkeys, rt_lds_words(r)); }
 // writer set of the full GUID (a, b, c = prefix words, d = entity id), or RTPS_NO_TARGET
 template <bool LDS>
 __device__ __forceinline__ uint32_t rt_writer_set(const ReaderDev& r, const uint32_t* lds, uint32_t a, uint32_t b,
@@ -67,10 +81,11 @@ __device__ __forceinline__ uint32_t rt_writer_set(const ReaderDev& r, const uint
   const uint32_t* sets = LDS ? lds + (r.gmask + 1u) * 4u : r.gset;
   uint32_t i = rt_hash16(a, b, c, d) & r.gmask;
   for (uint32_t probe = 0; probe <= r.gmask; ++probe) {
+    // the slot's set and key loaded together (one LDS round trip per probe)
     const uint32_t s = sets[i];
+    const uint4 k = *reinterpret_cast<const uint4*>(keys + 4u * i);
     if (s == RTPS_NO_TARGET) return RTPS_NO_TARGET;
-    const uint32_t* k = keys + 4u * i;
-    if (k[0] == a && k[1] == b && k[2] == c && k[3] == d) return s;
+    if (k.x == a && k.y == b && k.z == c && k.w == d) return s;
     i = (i + 1u) & r.gmask;
   }
   return RTPS_NO_TARGET;
@@ -82,9 +97,9 @@ __device__ __forceinline__ uint32_t rt_entity_set(const ReaderDev& r, const uint
   const uint32_t* sets = LDS ? lds + gcap * 5u + r.emask + 1u : r.eset;
   uint32_t i = rt_hash4(d) & r.emask;
   for (uint32_t probe = 0; probe <= r.emask; ++probe) {
-    const uint32_t s = sets[i];
+    const uint32_t s = sets[i], k = keys[i];
     if (s == RTPS_NO_TARGET) return RTPS_NO_TARGET;
-    if (keys[i] == d) return s;
+    if (k == d) return s;
     i = (i + 1u) & r.emask;
   }
   return RTPS_NO_TARGET;

@@ -137,7 +137,7 @@ a, b = table(3, 1), table(40, 2)
 assert rt_set(t, a) == 0
 va = view(t)
 ga = words(va.gset, va.gmask + 1)
-for fail_at in range(6):  # every one of the six table buffers
+for fail_at in range(1):  # the one table image buffer
     L.rtps_rx_debug_rt_host_mode(fail_at)
     assert rt_set(t, b) == -3, fail_at             # RTPS_RX_ENOMEM
     v = view(t)
@@ -158,7 +158,7 @@ print("ok")
 def test_failed_set_readers_keeps_previous_table():
     """a set_readers whose allocation fails part-way must leave the previous
     device tables whole (build into new buffers, swap on success).  Host-memory mode of the
-    table's allocator, failing each of the six buffers in turn (isolated process)."""
+    table's allocator, failing its one image buffer (isolated process)."""
     import os
     import subprocess
     import sys
