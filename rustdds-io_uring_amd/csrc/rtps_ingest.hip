@@ -282,8 +282,8 @@ struct FastOut {
   uint32_t* seg_b;
   uint32_t* seg_e;
   uint32_t n_seg;
-  uint32_t* bk_cnt;  // BUCKET: per (workgroup, proxy) proxied events, workgroup-major: [block * n_proxies + proxy]
-  uint32_t* bk_lst;  //         the proxy's first position inside the workgroup's region
+  uint32_t* bk_cl;   // BUCKET: per (workgroup, proxy), workgroup-major [block * n_proxies + proxy]: the
+                     //   proxy's events in the workgroup's region | their first position there << 16
   uint32_t sets_lds; // classify: set_first / set_ent staged in LDS behind the hash tables
 };
 // bytes of the target sets' LDS image (set_first words, then 8-B entries)
@@ -320,7 +320,8 @@ constexpr uint32_t BK_IDX = 4096;  // k_proxy's sampled piece index: proxies of 
 constexpr uint32_t CHR = RTPS_PB_CHR;         // record slots per classify workgroup
 constexpr uint32_t PB_SUB = CHR / (IT / 64);  // slots per wave
 constexpr uint32_t PB_STEPS = PB_SUB / 64;
-static_assert(PB_SUB % 64 == 0 && PB_MAX <= (1u << 20) && PB_MAX % IT == 0, "bucketing steps and sort words");
+static_assert(PB_SUB % 64 == 0 && PB_MAX <= (1u << 20) && PB_MAX % IT == 0 && CHR < 65536u,
+              "bucketing steps, sort words, packed piece counts");
 
 __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x, uint32_t lane) {
 #pragma unroll
@@ -595,8 +596,7 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
     for (uint32_t r = 0; r < PPB; ++r) {
       const uint32_t e = tid * PPB + r;
       if (e >= np) break;
-      fo.bk_cnt[tb + e] = tot[r];
-      fo.bk_lst[tb + e] = run;
+      fo.bk_cl[tb + e] = tot[r] | run << 16;  // (both <= CHR < 2^16)
       for (uint32_t w = 0; w < IT / 64; ++w) {
         const uint32_t c = s_cnt[w][e];
         s_cnt[w][e] = run;
@@ -1613,9 +1613,10 @@ __global__ __launch_bounds__(IT) void k_dstate(const uint8_t* flag, uint64_t n, 
 // host picks this path only when the mean load per proxy is small.
 #ifdef RTPS_PROXY_STAMPS  // tuning builds: per-phase time sums of k_proxy, per proxy
 constexpr uint32_t PST_N = 8;
-#define PST_DECL uint64_t pst_t = __builtin_amdgcn_s_memrealtime(), pst_acc[PST_N] = {0, 0, 0, 0, 0, 0, 0, 0}
+#define PST_DECL uint64_t pst_t = __builtin_amdgcn_s_memrealtime(), pst_t0 = pst_t, pst_acc[PST_N] = {0, 0, 0, 0, 0, 0, 0, 0}
 #define PST(k) do { const uint64_t t_ = __builtin_amdgcn_s_memrealtime(); pst_acc[k] += t_ - pst_t; pst_t = t_; } while (0)
-#define PST_FLUSH(e) do { if (threadIdx.x == 0) for (uint32_t k_ = 0; k_ < PST_N; ++k_) g_proxy_stamps[(e) * PST_N + k_] = pst_acc[k_]; } while (0)
+#define PST_FLUSH(e) do { if (threadIdx.x == 0) { for (uint32_t k_ = 0; k_ < PST_N; ++k_) g_proxy_stamps[(e) * PST_N + k_] = pst_acc[k_]; \
+  g_proxy_stamps[16384u * 8u + 2u * (e)] = pst_t0; g_proxy_stamps[16384u * 8u + 2u * (e) + 1u] = pst_t; } } while (0)
 #else
 #define PST_DECL do {} while (0)
 #define PST(k) do {} while (0)
@@ -1724,8 +1725,7 @@ __device__ __forceinline__ uint32_t ph_find(const uint32_t* h_key, uint32_t off)
 // the proxy bucketing's tables (k_classify<.., true>): per (classify workgroup, proxy)
 // event counts and first positions in the workgroup's region of pev, nb workgroups
 struct BkIn {
-  const uint32_t* cnt;
-  const uint32_t* lst;
+  const uint32_t* cl;  // FastOut::bk_cl
   uint32_t nb;
 };
 // block-wide EXCLUSIVE sum over the PT threads; *total = the block's sum
@@ -1785,6 +1785,7 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
                 "far replay LDS reuse");
   const uint32_t e = blockIdx.x, tid = threadIdx.x;
   if (e >= n_proxies) return;
+  PST_DECL;  // (setup: the window, the hash and the piece tables)
   if (tid == 0) { s_ngap = 0u; s_nfi = 0u; }
   const int64_t lo = s.lo[e], base = s.base[e];
   uint32_t* gbits = s.bits + (uint64_t)e * WW;
@@ -1800,8 +1801,9 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
 #pragma unroll
     for (uint32_t k = 0; k < K; ++k) {
       const uint32_t b = tid * kp + k;
-      c[k] = (k < kp && b < bk.nb) ? bk.cnt[(uint64_t)b * n_proxies + e] : 0u;
-      l[k] = (k < kp && b < bk.nb) ? bk.lst[(uint64_t)b * n_proxies + e] : 0u;
+      const uint32_t cl = (k < kp && b < bk.nb) ? bk.cl[(uint64_t)b * n_proxies + e] : 0u;
+      c[k] = cl & 0xffffu;
+      l[k] = cl >> 16;
       sum += c[k];
     }
     uint32_t ex = block_sum_excl(sum, s_w32, qe);
@@ -1828,7 +1830,6 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
   }
   int64_t run_cnt = s.hbc[e], run_thr = base;  // max HEARTBEAT count so far; max accepted firstSN (>= base)
   uint64_t n_ovf = 0;
-  PST_DECL;
   __syncthreads();
   PST(0);
   // the chunk at c0's events of this thread (BK: found through the piece tables)
@@ -2135,23 +2136,20 @@ struct IngestState {
   uint64_t last_nev = 0;      // events of the last batch whose counts were read
   uint64_t* hsig = nullptr;    // pinned, coherent: classify's count signal (SIG_*)
   uint64_t sig_tag = 0;
-  uint32_t* bk_cnt = nullptr;  // proxy bucketing: per (classify workgroup, proxy) events and first positions
-  uint32_t* bk_lst = nullptr;
+  uint32_t* bk_cl = nullptr;  // proxy bucketing: per (classify workgroup, proxy) events | first position << 16
   uint64_t bkcap = 0;
 };
 
 static void free_bk(IngestState* s) {
-  if (s->bk_cnt) (void)hipFree(s->bk_cnt);
-  if (s->bk_lst) (void)hipFree(s->bk_lst);
-  s->bk_cnt = nullptr;
-  s->bk_lst = nullptr;
+  if (s->bk_cl) (void)hipFree(s->bk_cl);
+  s->bk_cl = nullptr;
   s->bkcap = 0;
 }
 static bool grow_bk(IngestState* s, uint64_t n, hipStream_t st) {
   if (n <= s->bkcap) return true;
   (void)hipStreamSynchronize(st);
   free_bk(s);
-  if (hipMalloc(&s->bk_cnt, n * 4) != hipSuccess || hipMalloc(&s->bk_lst, n * 4) != hipSuccess) {
+  if (hipMalloc(&s->bk_cl, n * 4) != hipSuccess) {
     free_bk(s);
     return false;
   }
@@ -2413,7 +2411,7 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
   // classify workgroups exceed its LDS tables (or path 4: the radix sort, tests)
   const uint64_t nblk = (max + CHR - 1) / CHR;
   const bool bucket = fast && t.n_proxies <= PB_MAX && nblk <= BK_MAX && s->path != 4;
-  FastOut fo{nullptr, nullptr, arena, dgram_off, S.seg_b, S.seg_e, s->ecap, nullptr, nullptr, sets_lds ? 1u : 0u};
+  FastOut fo{nullptr, nullptr, arena, dgram_off, S.seg_b, S.seg_e, s->ecap, nullptr, sets_lds ? 1u : 0u};
   if (fast) {
     if (!grow_pscratch(s, bucket ? nblk * CHR : max, st)) return RTPS_RX_ENOMEM;
     fo.pev = s->pev;
@@ -2421,8 +2419,7 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
   }
   if (bucket) {
     if (!grow_bk(s, (uint64_t)t.n_proxies * nblk, st)) return RTPS_RX_ENOMEM;
-    fo.bk_cnt = s->bk_cnt;
-    fo.bk_lst = s->bk_lst;
+    fo.bk_cl = s->bk_cl;
     hipLaunchKernelGGL((k_classify<true, true, true>), dim3((uint32_t)nblk), dim3(IT), lds, st, t, records,
                        n_records, max, with_frag ? frag : nullptr, flags, x, S.ctr, fo, ctr_next, S, s->epoch);
   } else if (ident && fast)
@@ -2437,7 +2434,7 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
   s->cpar ^= 1u;  // the next batch uses the set this classify zeroes
   if (bucket) {
     hipLaunchKernelGGL(k_proxy<true>, dim3(t.n_proxies), dim3(PT), 0, st, arena, s->pev, x.hval, t.n_proxies, S,
-                       out->accept, out->ack_base, BkIn{s->bk_cnt, s->bk_lst, (uint32_t)nblk});
+                       out->accept, out->ack_base, BkIn{s->bk_cl, (uint32_t)nblk});
   } else if (fast) {
     uint32_t kb = 1;
     while ((1u << kb) <= t.n_proxies) ++kb;  // keys 0..n_proxies (n_proxies: no proxy, sorts last)

@@ -37,21 +37,26 @@ tbl = np.zeros(len(guids), dtype=MATCH_DTYPE)
 tbl["writer_guid"] = np.frombuffer(guids.tobytes(), dtype=np.uint8).reshape(-1, 16)
 rx.set_match_table(tbl)
 rx.parse_batch_device(arena, off_t, ln_t, n, outs)
-rx.debug_ingest_path(int(os.environ.get("INGEST_PATH", "2")))  # 4: the radix-sort layout
-iouts = rx.alloc_ingest_outputs(outs["max_records"], len(guids))
+rx.debug_ingest_path(int(os.environ.get("INGEST_PATH", "0")))  # 0: the library's choice; 4: the radix-sort layout
+outs["max_records"] = n_rec  # as bench.py sizes the ingest (the proxy bucketing's workgroup bound)
+iouts = rx.alloc_ingest_outputs(n_rec, len(guids))
 for _ in range(3):
     rx.ingest_reset()
     rx.ingest(arena, off_t, outs, iouts)
 rx.sync()
 NS = 8
-buf = np.zeros(len(guids) * NS, dtype=np.uint64)
+buf = np.zeros(16384 * 8 + 2 * len(guids), dtype=np.uint64)  # the sums, then (start, end) per proxy
 fn = lib().rtps_rx_debug_proxy_stamps
 fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
 _check(fn(rx._h, buf.ctypes.data, buf.size))
-st = buf.reshape(-1, NS).astype(np.float64) * 0.01  # 100 MHz ticks -> us
+st = buf[:len(guids) * NS].reshape(-1, NS).astype(np.float64) * 0.01  # 100 MHz ticks -> us
+se = buf[16384 * 8:].reshape(-1, 2).astype(np.float64) * 0.01
+se -= se[:, 0].min()
 names = ["setup", "load chunk", "HB scans", "hash insert", "GAP marks", "decide", "merge", "state"]
 print(f"C3 n={n}: {len(guids)} proxies; per-proxy phase sums, mean / max over proxies (us)")
 for k, nm in enumerate(names):
     print(f"  {nm:12s} {st[:, k].mean():8.1f} {st[:, k].max():8.1f}")
 print(f"  total        {st.sum(1).mean():8.1f} {st.sum(1).max():8.1f}")
+print(f"  workgroup starts: min 0, p50 {np.median(se[:, 0]):.1f}, p90 {np.quantile(se[:, 0], 0.9):.1f}, "
+      f"max {se[:, 0].max():.1f} us; last end {se[:, 1].max():.1f} us")
 rx.close()
