@@ -1306,6 +1306,20 @@ __global__ __launch_bounds__(SCAN_T) void rtps_parse_scan_kernel(KParams p, uint
 #endif
 constexpr uint32_t EMT = RTPS_EM_THREADS;
 static_assert(EMT % TILE == 0, "the prologue threads are the first TILE");
+#if defined(RTPS_LDS_STAMPS) || defined(RTPS_EM_STAMPS)  // tuning builds: per-tile timestamps
+constexpr uint32_t STAMP_TILES = 1u << 16, STAMP_N = 24;
+__device__ uint64_t g_lds_stamps[STAMP_TILES * STAMP_N];
+#endif
+#ifdef RTPS_EM_STAMPS  // W: thread 0's phase ends (0-7; in-item marks wait for their loads), each wave's end (8-23)
+#define EM_STAMP(k, wait) do { if (tid == 0 && tile < STAMP_TILES) { \
+  if (wait) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); \
+  g_lds_stamps[tile * STAMP_N + (k)] = __builtin_amdgcn_s_memrealtime(); } } while (0)
+#define EM_WAVE_END() do { if (lane == 0 && tile < STAMP_TILES) \
+  g_lds_stamps[tile * STAMP_N + 8u + wave] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define EM_STAMP(k, wait) do {} while (0)
+#define EM_WAVE_END() do {} while (0)
+#endif
 __global__ __launch_bounds__(EMT) __attribute__((amdgpu_waves_per_eu(RTPS_EM_WAVES_PER_SIMD)))
 void rtps_parse_emit_kernel(KParams p, uint32_t n_tiles, const u32x4* items, const uint32_t* wcnt,
                             const uint64_t* tprefix) {
@@ -1318,6 +1332,7 @@ void rtps_parse_emit_kernel(KParams p, uint32_t n_tiles, const u32x4* items, con
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const bool pro = tid < TILE;  // a prologue thread: datagram tid of the tile
   const uint32_t tile = blockIdx.x;
+  EM_STAMP(0, false);
   mt_stage(p);  // visible after the __syncthreads below
   Scratch x = scratch_of(p.scratch, n_tiles);
   const uint64_t prefix = tprefix[tile];
@@ -1342,7 +1357,9 @@ void rtps_parse_emit_kernel(KParams p, uint32_t n_tiles, const u32x4* items, con
   }
   if (pro && lane == 63) s_wsum[wave] = incl;
   if (pro && lane == 0) { s_nit[wave] = (wc & WCNT_OVERFLOW) ? 0u : wc; s_lo[wave] = lo; s_hi[wave] = hi; }
+  EM_STAMP(1, false);
   __syncthreads();
+  EM_STAMP(2, false);
   uint32_t wave_off = 0;
   uint64_t tlo = ~0ull, thi = 0;
 #pragma unroll
@@ -1388,6 +1405,7 @@ void rtps_parse_emit_kernel(KParams p, uint32_t n_tiles, const u32x4* items, con
     s_nit[WAVES] = a;
   }
   __syncthreads();
+  EM_STAMP(3, false);
   const uint32_t total = s_nit[WAVES];
   const u32x4* tslab = items + (size_t)tile * WAVES * CAPW * IW;
 #ifdef RTPS_EM_SORT
@@ -1463,6 +1481,7 @@ void rtps_parse_emit_kernel(KParams p, uint32_t n_tiles, const u32x4* items, con
       W.w[8] = kind == RTPS_DATA_FRAG ? ld4(s, o + 32u) : 0u;
       W.w[9] = 0u; W.w[10] = 0u; W.w[11] = 0u;
     }
+    EM_STAMP(4, true);
     Interp st;
     if (src_off == 8u) {
       st.src0 = s_pfx[d * 3 + 0]; st.src1 = s_pfx[d * 3 + 1]; st.src2 = s_pfx[d * 3 + 2];
@@ -1480,16 +1499,20 @@ void rtps_parse_emit_kernel(KParams p, uint32_t n_tiles, const u32x4* items, con
     Rec R;
     rec_clear(R);
     SubOut so;
+    EM_STAMP(5, true);
     sub_body<true>(s, W, kind, flags, le, o + 4u, eff, R, so);  // validated by E's walk
     R.d[0] = tile * TILE + d;
     R.d[1] = o | (kind << 16) | (flags << 24);
+    EM_STAMP(6, true);
     const uint32_t tgt = rec_finish(p, R, so, kind, st);
+    EM_STAMP(7, true);
     const uint64_t r = prefix + rb + j;
     if (r < p.max_records) {
       rec_store(p.records + r, R);
       if (p.target_out) p.target_out[r] = tgt;
     }
   }
+  EM_WAVE_END();
 }
 
 // ---------------------------------------------------------------------------
@@ -1710,10 +1733,9 @@ static_assert(LT >= 1 && LT <= 64, "one wave-0 lane per datagram");
 #ifndef RTPS_LDS_RT  // 1: stage the reader tables in LDS for D too (costs occupancy); 0: probe them in L2
 #define RTPS_LDS_RT 0
 #endif
-// per-phase timestamps of kernel D into a device array (tuning builds only)
+// per-phase timestamps of kernel D into a device array (tuning builds only; the buffer is
+// defined before the record pass, which stamps it under RTPS_EM_STAMPS)
 #ifdef RTPS_LDS_STAMPS
-constexpr uint32_t STAMP_TILES = 1u << 16, STAMP_N = 8;
-__device__ uint64_t g_lds_stamps[STAMP_TILES * STAMP_N];
 #define LDS_STAMP(k) \
   do { if (tid == 0 && tile < STAMP_TILES) g_lds_stamps[tile * STAMP_N + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
@@ -3006,7 +3028,7 @@ int rtps_rx_debug_set_chain_spin_limit(rtps_rx_ctx* c, uint32_t limit) {
    (s_memrealtime, 100 MHz; STAMP_N per tile) of the last launch, in builds with
    RTPS_LDS_STAMPS; RTPS_RX_EINVAL otherwise */
 int rtps_rx_debug_lds_stamps(rtps_rx_ctx* c, uint64_t* host, uint64_t n) {
-#ifdef RTPS_LDS_STAMPS
+#if defined(RTPS_LDS_STAMPS) || defined(RTPS_EM_STAMPS)
   if (!c || !host) return RTPS_RX_EINVAL;
   if (n > (uint64_t)STAMP_TILES * STAMP_N) n = (uint64_t)STAMP_TILES * STAMP_N;
   (void)hipSetDevice(c->device);

@@ -36,7 +36,7 @@ rx.sync()
 which = rx.debug_parse_phases(arena, off_t, ln_t, n, outs, 1)
 rx.sync()
 assert which == 3, f"first kernel {which}, not the LDS tiles"
-NS = 8
+NS = 24  # STAMP_N of the tuning builds
 fn = lib().rtps_rx_debug_lds_stamps
 fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
 tiles = min((n + 31) // 32, 1 << 16)

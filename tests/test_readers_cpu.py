@@ -167,3 +167,52 @@ def test_failed_set_readers_keeps_previous_table():
     r = subprocess.run([sys.executable, "-c", _RT_FAIL_SCRIPT, os.path.join(repo, "rustdds-io_uring_amd"), repo],
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and r.stdout.strip() == "ok", r.stdout + r.stderr
+
+
+_RT_IMAGE_SCRIPT = _RT_FAIL_SCRIPT.split("L.rtps_rx_debug_rt_host_mode(-1)\nt = ")[0] + r'''
+L.rtps_rx_debug_rt_host_mode(-1)
+RT_LDS_MAX = 48 * 1024
+def lds_bytes(gcap, ecap):
+    return gcap * 20 + ecap * 8
+def pow2(n):
+    p = 1
+    while p < n:
+        p <<= 1
+    return p
+def wide_table(n_writers):
+    rd = Readers([(bytes([0, 0, 1, 7]), 1, 0)],
+                 [(bytes([9] * 12) + bytes([0, w >> 8, w & 255, 2]), 0) for w in range(n_writers)])
+    return rd.readers, rd.proxies
+t = L.rtps_rx_debug_rt_new()
+for n_writers in (3, 40, 256, 600, 1500):
+    assert rt_set(t, wide_table(n_writers)) == 0
+    v = view(t)
+    gcap, ecap = v.gmask + 1, v.emask + 1
+    # sparse slots (load <= 1/4) while the tables fit the LDS limit, else the dense ones (<= 1/2)
+    if lds_bytes(pow2(4 * n_writers), pow2(4 * n_writers)) <= RT_LDS_MAX:
+        assert gcap == pow2(4 * n_writers), (n_writers, gcap)
+    else:
+        assert gcap == pow2(2 * n_writers), (n_writers, gcap)
+    # one image in the LDS layout: gkeys, gset, ekeys, eset, set_first, set_ent back to back
+    assert v.gset == v.gkeys + 16 * gcap and v.ekeys == v.gset + 4 * gcap
+    assert v.eset == v.ekeys + 4 * ecap and v.set_first == v.eset + 4 * ecap
+    assert v.set_ent == v.set_first + 4 * (v.n_sets + 1)
+    gs = words(v.gset, gcap)
+    assert sorted(gs[gs != 0xFFFFFFFF].tolist()) == list(range(n_writers))
+L.rtps_rx_debug_rt_free(t)
+print("ok")
+'''
+
+
+def test_reader_table_image_layout():
+    """Round 4: the reader tables are one device image in their LDS layout (staged by one flat
+    copy), with hash slots at load <= 1/4 while they fit RT_LDS_MAX and <= 1/2 past it
+    (host-memory mode of the table's allocator, isolated process)."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    repo = os.path.dirname(here)
+    r = subprocess.run([sys.executable, "-c", _RT_IMAGE_SCRIPT, os.path.join(repo, "rustdds-io_uring_amd"), repo],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stdout + r.stderr
