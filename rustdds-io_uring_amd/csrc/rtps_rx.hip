@@ -1333,15 +1333,20 @@ void rtps_parse_emit_kernel(KParams p, uint32_t n_tiles, const u32x4* items, con
   const bool pro = tid < TILE;  // a prologue thread: datagram tid of the tile
   const uint32_t tile = blockIdx.x;
   EM_STAMP(0, false);
-  mt_stage(p);  // visible after the __syncthreads below
   Scratch x = scratch_of(p.scratch, n_tiles);
   const uint64_t prefix = tprefix[tile];
   const uint32_t wc = pro ? wcnt[tile * WAVES + wave] : 0u;
   const uint32_t i = tile * TILE + tid;
   const bool valid = pro && i < p.n;
-  const uint32_t cnt = valid ? (uint32_t)x.dcount[i] : 0u;
-  const uint64_t off = (valid && cnt) ? p.dgram_off[i] : 0ull;
-  const uint32_t L = (valid && cnt) ? p.dgram_len[i] : 0u;
+  // the datagram's count, offset and length loaded together (offset / length whether or not it
+  // has records), and in flight before the table copy below waits for its own loads
+  const uint32_t cnt0 = valid ? (uint32_t)x.dcount[i] : 0u;
+  const uint64_t off0 = valid ? p.dgram_off[i] : 0ull;
+  const uint32_t L0 = valid ? p.dgram_len[i] : 0u;
+  mt_stage(p);  // visible after the __syncthreads below
+  const uint32_t cnt = cnt0;
+  const uint64_t off = cnt ? off0 : 0ull;
+  const uint32_t L = cnt ? L0 : 0u;
   const uint32_t incl = wave_incl_scan(cnt, lane);
   // descriptor base: the arena when every offset fits 32 bits, else the tile's smallest
   // offset (a tile spanning 4 GiB or more takes the lane walk)
