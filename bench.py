@@ -98,6 +98,10 @@ def pmc_profile(workload):
     return d
 
 
+PMC_KEYS = {"rtps_parse_spec_kernel": "parse_spec", "rtps_parse_chain_kernel": "parse_chain",
+            "rtps_parse_lds_kernel": "parse_lds", "rtps_parse_item_kernel": "parse_item",
+            "rtps_parse_rslab_kernel": "parse_rslab", "rtps_parse_scan_kernel": "parse_scan",
+            "rtps_parse_emit_kernel": "parse_emit", "rtps_parse_emit2_kernel": "parse_emit2"}
 KERNEL_NAMES = {1: "rtps_parse_spec_kernel", 2: "rtps_parse_chain_kernel", 3: "rtps_parse_lds_kernel",
                 4: "rtps_parse_item_kernel", 5: "rtps_parse_rslab_kernel"}
 
@@ -117,17 +121,23 @@ def _time_phases(rx, arena, off_t, ln_t, n, outs, stream, steps, phases):
 
 
 def time_dominant_kernel(rx, arena, off_t, ln_t, n, outs, stream, steps):
-    """Live HIP-event timing of the parse's dominant kernel alone (the first kernel of
-    rtps_rx_parse_batch: rtps_parse_spec_kernel; for mixed traffic the item pass's
-    rtps_parse_item_kernel, or the chained kernels), K back-to-back launches on the parse
-    stream, one event pair.  For the item pass the finishing launches (the tile scan and the
-    record pass rtps_parse_emit_kernel) are timed the same way; the dominant kernel is the
-    slower of the item walk and the record pass."""
+    """Live HIP-event timing of the parse's dominant kernel alone, K back-to-back launches on
+    the parse stream, one event pair.  The first kernel of rtps_rx_parse_batch
+    (rtps_parse_spec_kernel; for mixed traffic the item pass's walk rtps_parse_item_kernel E,
+    or the chained kernels) is timed; for the item pass also the record pass W alone
+    (rtps_parse_emit2_kernel, or rtps_parse_emit_kernel) and the scan + record pass.  The
+    dominant kernel is the slower of E and W: its name and time are returned."""
     ms, which = _time_phases(rx, arena, off_t, ln_t, n, outs, stream, steps, 1)
     kname, extra = KERNEL_NAMES[which], {}
     if which in (4, 5):
         ms2, _ = _time_phases(rx, arena, off_t, ln_t, n, outs, stream, steps, 2)
         extra = {"item_kernel_ms": ms, "scan_plus_emit_ms": ms2}
+        if which == 4:
+            w_ms, _ = _time_phases(rx, arena, off_t, ln_t, n, outs, stream, steps, 2 | 4)
+            wname = "rtps_parse_emit_kernel" if rx.debug_emit() == 1 else "rtps_parse_emit2_kernel"
+            extra.update({"emit_kernel": wname, "emit_kernel_ms": w_ms, "scan_ms": max(0.0, ms2 - w_ms)})
+            if w_ms > ms:
+                kname, ms = wname, w_ms
     for _ in range(2):  # full launches restore the per-launch bookkeeping
         rx.parse_batch_device(arena, off_t, ln_t, n, outs)
     torch.cuda.synchronize()
@@ -249,6 +259,79 @@ def end_to_end(rx, arena, off_t, ln_t, n, outs, n_rec, stream, reps=5):
     return res
 
 
+def full_chain(rx, workload, arena, off_t, ln_t, n, n_rec, n_entries, reps=5):
+    """The receive path from host memory to host memory, as north_star names it (io_uring
+    receive buffers in, parsed samples back to the DDS history cache): the datagrams in pinned
+    host memory -> parse -> history-cache ingest with the topic caches (TopicCache::add_change,
+    reader.rs:693-758 -> make_cache_change :1185-1205 -> dds_cache.rs:210-276) -> CDR decode of
+    the deliveries (compact rows: the samples the cache takes) -> D2H of the deliveries and
+    their rows.  Input two ways: 'zero_copy' (the kernels read the datagram heads and the
+    delivered payloads straight from pinned host memory) and 'copy' (one H2D of the arena
+    first).  Fresh writer proxies and empty topic caches before each run (outside the clock);
+    the host waits for the delivery count, then copies exactly the deliveries and rows.  Wall
+    clock per run, best of `reps`; checked against the same chain on the HBM-resident batch."""
+    from rtps_rx import cdr
+    t = getattr(cdr, CDR_TYPES[workload])
+    dev = arena.device
+    host_arena = torch.empty(arena.numel(), dtype=torch.uint8, pin_memory=True)
+    host_arena.copy_(arena)
+    h_off = torch.empty(n, dtype=torch.int64, pin_memory=True)
+    h_off.copy_(off_t)
+    h_ln = torch.empty(n, dtype=torch.int32, pin_memory=True)
+    h_ln.copy_(ln_t)
+    rx.set_topics([(1, 64)], [(0, 1)])
+    outs = rx.alloc_outputs(n, n_rec)
+    iouts = rx.alloc_ingest_outputs(n_rec, n_entries)
+    max_del = iouts["max_accepted"]
+    rows, rst = rx.alloc_rows(t, max_del)
+    h_na = torch.zeros(1, dtype=torch.int64, pin_memory=True)
+    h_dels = torch.empty((max(max_del, 1), 8), dtype=torch.uint8, pin_memory=True)
+    h_rows = torch.empty((max(max_del, 1), t.row_bytes), dtype=torch.uint8, pin_memory=True)
+    h_rst = torch.empty(max(max_del, 1), dtype=torch.uint8, pin_memory=True)
+    dev_arena = torch.empty_like(arena)
+
+    def chain(src, o, l, copy_in):
+        if copy_in:
+            dev_arena.copy_(host_arena, non_blocking=True)
+            src, o, l = dev_arena, off_t, ln_t
+        rx.parse_batch_device(src, o, l, n, outs)
+        rx.ingest(src, o, outs, iouts, topic_cache=True)
+        rx.cdr_decode_list(t, src, o, outs, iouts["accepted"], 8, iouts["n_accepted"], max_del, rows, rst)
+        h_na.copy_(iouts["n_accepted"], non_blocking=True)
+        torch.cuda.current_stream(dev).synchronize()
+        na = min(int(h_na.item()), max_del)
+        h_dels[:na].copy_(iouts["accepted"][:na], non_blocking=True)
+        h_rows[:na].copy_(rows[:na], non_blocking=True)
+        h_rst[:na].copy_(rst[:na], non_blocking=True)
+        torch.cuda.current_stream(dev).synchronize()
+        return na
+
+    _reset_caches(rx, True)
+    na_ref = chain(arena, off_t, ln_t, False)  # the HBM-resident reference
+    ref = (h_dels[:na_ref].clone(), h_rows[:na_ref].clone(), h_rst[:na_ref].clone())
+    res = {}
+    for name, args in (("zero_copy", (host_arena, h_off, h_ln, False)), ("copy", (None, None, None, True))):
+        times = []
+        for _ in range(reps):
+            _reset_caches(rx, True)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            na = chain(*args)
+            times.append(time.perf_counter() - t0)
+        ok = na == na_ref and torch.equal(h_dels[:na], ref[0]) and torch.equal(h_rows[:na], ref[1]) and \
+            torch.equal(h_rst[:na], ref[2])
+        tm = min(times)
+        res[name] = {"ms": tm * 1e3, "datagrams_per_s": n / tm, "deliveries": na, "deliveries_per_s": na / tm,
+                     "d2h_bytes": na * (8 + t.row_bytes + 1), "parity_ok": bool(ok)}
+    res["copy"]["h2d_bytes"] = int(arena.numel())
+    res["best"] = max(("copy", "zero_copy"), key=lambda k: res[k]["datagrams_per_s"])
+    res["what"] = ("host-memory datagrams -> parse -> ingest + topic caches -> CDR rows of the deliveries -> "
+                   "deliveries and rows in host memory; wall clock incl. the H2D / D2H copies and one host wait "
+                   f"for the delivery count; sample type {CDR_TYPES[workload]}")
+    rx.set_topics([], [])
+    return res
+
+
 def roofline(rx, args, arena, off_t, ln_t, n, outs, stream, total_bytes, alg_reads, alg_writes):
     """SURVEY §8(d) roofline of the dominant parse kernel.  The algorithmic unit is the
     datagram's bytes (Σ lengths) only if every byte streams (FETCH_SIZE >= Σ lengths);
@@ -258,9 +341,7 @@ def roofline(rx, args, arena, off_t, ln_t, n, outs, stream, total_bytes, alg_rea
     8 TB/s.  Writes (the 64-B records) are reported beside it, not in the numerator."""
     ms, kname, extra = time_dominant_kernel(rx, arena, off_t, ln_t, n, outs, stream, args.steps)
     pmc = pmc_profile(args.workload)
-    key = {"rtps_parse_spec_kernel": "parse_spec", "rtps_parse_chain_kernel": "parse_chain",
-           "rtps_parse_lds_kernel": "parse_lds", "rtps_parse_item_kernel": "parse_item",
-           "rtps_parse_rslab_kernel": "parse_rslab"}[kname]
+    key = PMC_KEYS[kname]
     k = (pmc or {}).get(key) or {}
     scale = (pmc or {}).get("fetch_scale") or 1.0
     if pmc and pmc.get("datagrams_per_launch") == n and "FETCH_SIZE" in k:
@@ -283,7 +364,20 @@ def roofline(rx, args, arena, off_t, ln_t, n, outs, stream, total_bytes, alg_rea
     if pmc:
         r["pmc_source"] = pmc["_source"]
     r.update(extra)
-    if kname in ("rtps_parse_chain_kernel", "rtps_parse_item_kernel"):
+    item_pass = "item_kernel_ms" in extra
+    if item_pass:
+        # the whole item pass E + S + W: calibrated reads of the three launches / their time / peak
+        e_ms, sw_ms = extra["item_kernel_ms"], extra["scan_plus_emit_ms"]
+        ks = [(pmc or {}).get(PMC_KEYS[x]) or {} for x in ("rtps_parse_item_kernel", "rtps_parse_scan_kernel",
+                                                            extra.get("emit_kernel", "rtps_parse_emit_kernel"))]
+        if pmc and pmc.get("datagrams_per_launch") == n and all("FETCH_SIZE" in x for x in ks):
+            fetch = sum(x["FETCH_SIZE"] for x in ks) * scale
+            r["item_pass"] = {"ms": e_ms + sw_ms, "read_bytes": fetch,
+                              "write_bytes": sum(x.get("WRITE_SIZE", 0.0) for x in ks),
+                              "frac": fetch / ((e_ms + sw_ms) * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                              "kernels": "rtps_parse_item_kernel + rtps_parse_scan_kernel + " + extra["emit_kernel"]}
+            r["item_pass_frac"] = r["item_pass"]["frac"]
+    if kname == "rtps_parse_chain_kernel" or item_pass:
         torch.cuda.synchronize()
         n_rec = int(outs["n_records"].item())
         c = time_hops_ceilings(arena, off_t, ln_t, n, outs, n_rec, stream, args.steps)
@@ -293,7 +387,7 @@ def roofline(rx, args, arena, off_t, ln_t, n, outs, stream, total_bytes, alg_rea
                                       "parse's positions, no field decode",
                             "one_walk_ms": c[1], "two_walk_ms": c[2]}
             # same-shape one-walk floor / the parse's kernel time (the item pass: all three launches)
-            pm = ms + extra.get("scan_plus_emit_ms", 0.0)
+            pm = extra["item_kernel_ms"] + extra["scan_plus_emit_ms"] if item_pass else ms
             r["attainable_frac"] = c[1] / pm
             r["attainable_frac_two_walk"] = c[2] / pm
     if kname == "rtps_parse_spec_kernel":
@@ -431,26 +525,44 @@ def exchange_prediction(rx, arena, off_t, outs, dev, worlds=(2, 4, 8)):
             "link_gbs": XGMI_LINK_GBS, "item_bytes": 32, **out}
 
 
+def _reset_caches(rx, topic_cache):
+    rx.ingest_reset()
+    if topic_cache:
+        rx.topic_reset()
+
+
+def _time_ingest(rx, arena, off_t, outs, iouts, fa, stream, steps, topic_cache):
+    """Mean HIP-event time of one ingest launch sequence; every step starts from fresh writer
+    proxies (and, with the topic caches, empty caches): the resets are outside the events."""
+    for _ in range(2):
+        _reset_caches(rx, topic_cache)
+        rx.ingest(arena, off_t, outs, iouts, *fa, topic_cache=topic_cache)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    torch.cuda.synchronize()
+    for a, b in ev:
+        _reset_caches(rx, topic_cache)
+        a.record(stream)
+        rx.ingest(arena, off_t, outs, iouts, *fa, topic_cache=topic_cache)
+        b.record(stream)
+    torch.cuda.synchronize()
+    return float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+
 def ingest_leg(rx, arena, off_t, outs, n_rec, recs, n_entries, stream, steps, fouts=None):
     """History-cache ingest (§8f rank 2) of this batch's samples / HEARTBEATs / GAPs,
     timed separately (HIP events on the launch stream).  Every step starts from
     fresh writer proxies (the reset is outside the timed region), so every step
     does the same work: all first copies accepted.  fouts: the batch's reassembled
-    DataFrag samples (C4), ingested at their completing records."""
+    DataFrag samples (C4), ingested at their completing records.  Timed again with the
+    topic caches (RTPS_INGEST_TOPIC_CACHE: TopicCache::add_change of every delivery, the
+    subscribed reader's topic with max_keep 64, emptied before each step): topic_cache_ms."""
     iouts = rx.alloc_ingest_outputs(n_rec, n_entries)
     fa = (fouts,) if fouts is not None else ()
-    for _ in range(2):
-        rx.ingest_reset()
-        rx.ingest(arena, off_t, outs, iouts, *fa)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    rx.set_topics([(1, 64)], [(0, 1)])  # the bench's reader (slot 0) on one topic
+    ms_tc = _time_ingest(rx, arena, off_t, outs, iouts, fa, stream, steps, True)
     torch.cuda.synchronize()
-    for a, b in ev:
-        rx.ingest_reset()
-        a.record(stream)
-        rx.ingest(arena, off_t, outs, iouts, *fa)
-        b.record(stream)
-    torch.cuda.synchronize()
-    ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    cached = int(((iouts["accepted"][:int(iouts["n_accepted"].item())].reshape(-1, 8)[:, 6] & 1) != 0).sum().item())
+    ms = _time_ingest(rx, arena, off_t, outs, iouts, fa, stream, steps, False)
     na = int(iouts["n_accepted"].item())
     k = recs["kind"]
     events = int((((recs["route"] & 0x21) == 0x21) & np.isin(k, (DATA, HEARTBEAT, GAP))).sum())
@@ -460,11 +572,90 @@ def ingest_leg(rx, arena, off_t, outs, n_rec, recs, n_entries, stream, steps, fo
     # delivery, per event 8 B of proxy state read and 4 B of change-set bits touched
     alg = n_rec * (64 + 1) + 8 * na + 12 * events
     return iouts, {"kernel": "rtps_ingest (classify + heartbeat sort/scans + marks + decide + select + merge + state)",
-            "ms": ms, "records": n_rec, "events": events, "accepted": na,
+            "ms": ms, "topic_cache_ms": ms_tc, "topic_cache_extra_ms": ms_tc - ms,
+            "topic_cache_stored": cached,
+            "records": n_rec, "events": events, "accepted": na,
             "samples_per_s": na / (ms * 1e-3), "records_per_s": n_rec / (ms * 1e-3),
             "window_overflow": int(iouts["n_window_overflow"].item()),
             "alg_bytes_per_launch": alg, "achieved_gbs": alg / (ms * 1e-3) / 1e9,
             "frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+
+
+SPDP_READER = bytes([0x00, 0x01, 0x00, 0xC7])  # EntityId::SPDP_BUILTIN_PARTICIPANT_READER (DUPLICATES_OK)
+
+
+def spdp_repeat_batch(n, pattern):
+    """n datagrams of one DATA each (52 B in 64-B slots) from one user writer to the SPDP
+    participant reader, SNs with >= 50 % repeats: 'pairs' = every SN twice in a row (i // 2 + 1),
+    'halves' = the second half repeats the first (i % (n / 2) + 1)."""
+    import struct
+    prefix = bytes([0xB0] * 12)
+    writer = bytes([0, 0, 1, 0x02])
+    body = struct.pack("<HH", 0, 16) + bytes(4) + writer + bytes(8) + b"\x00\x01\x00\x00abcd"
+    dg = b"RTPS\x02\x04\x01\x0f" + prefix + bytes([0x15, 0x05]) + struct.pack("<H", len(body)) + body
+    slot = 64
+    tmpl = np.frombuffer(dg.ljust(slot, b"\0"), dtype=np.uint8)
+    arena = np.tile(tmpl, n)
+    i = np.arange(n, dtype=np.int64)
+    sn = (i // 2 + 1) if pattern == "pairs" else (i % (n // 2) + 1)
+    a = arena.reshape(n, slot)
+    a[:, 36:40] = (sn >> 32).astype("<i4").view(np.uint8).reshape(n, 4)   # SN high (i32), then low (u32)
+    a[:, 40:44] = (sn & 0xFFFFFFFF).astype("<u4").view(np.uint8).reshape(n, 4)
+    off = (i * slot).astype(np.uint64)
+    ln = np.full(n, len(dg), dtype=np.uint32)
+    return arena, off, ln, prefix + writer
+
+
+def spdp_repeats_leg(dev, stream, steps, n=1 << 20):
+    """The topic caches' adversarial case: the SPDP participant reader
+    accepts duplicates (reader.rs:712-722), so every delivery of its topic is a candidate and
+    the repeats of a key stored earlier in the batch are decided in order by one thread per
+    topic (tc_resolve).  1M datagrams, one topic (max_keep 64), >= 50 % repeated SNs; the
+    ingest timed with and without RTPS_INGEST_TOPIC_CACHE (fresh proxies and caches each
+    step), and the CACHED decisions checked against the reference's add_change restated: a
+    change is stored iff its (writer, SN) is not held at that moment."""
+    from rtps_rx.records import Readers
+    out = {}
+    rx = rtps_rx.MessageReceiver(OWN_PREFIX, device=dev.index, max_datagrams=n)
+    rx.set_stream(stream)
+    try:
+        for pattern in ("pairs", "halves"):
+            arena_np, off, ln, guid = spdp_repeat_batch(n, pattern)
+            arena = torch.from_numpy(arena_np).to(dev)
+            off_t = torch.from_numpy(off.view(np.int64)).to(dev)
+            ln_t = torch.from_numpy(ln.view(np.int32)).to(dev)
+            rx.set_readers(Readers([(SPDP_READER, 14, 0)], [(guid, 0)]))
+            rx.set_topics([(9, 64)], [(14, 9)])
+            outs = rx.alloc_outputs(n, n)
+            rx.parse_batch_device(arena, off_t, ln_t, n, outs)
+            iouts = rx.alloc_ingest_outputs(n, 1)
+            ms_tc = _time_ingest(rx, arena, off_t, outs, iouts, (), stream, steps, True)
+            torch.cuda.synchronize()
+            na = int(iouts["n_accepted"].item())
+            flags = iouts["accepted"][:na].reshape(-1, 8)[:, 6].cpu().numpy() & 1
+            ms = _time_ingest(rx, arena, off_t, outs, iouts, (), stream, steps, False)
+            # add_change restated (dds_cache.rs:221-276): GC at SN % 64 == 0 keeps the 64 newest,
+            # then store iff not held (insertion order = receive order)
+            sn = ((np.arange(n) // 2 + 1) if pattern == "pairs" else (np.arange(n) % (n // 2) + 1)).tolist()
+            held, order, exp = set(), [], np.zeros(n, np.uint8)
+            from collections import deque
+            order = deque()
+            for k, x in enumerate(sn):
+                if x % 64 == 0:
+                    while len(order) > 64:
+                        held.discard(order.popleft())
+                if x not in held:
+                    held.add(x)
+                    order.append(x)
+                    exp[k] = 1
+            out[pattern] = {"datagrams": n, "deliveries": na, "repeats": int(n - len(set(sn))),
+                            "stored": int(flags.sum()), "parity_ok": bool(na == n and np.array_equal(flags, exp)),
+                            "ingest_ms": ms, "ingest_topic_cache_ms": ms_tc, "topic_cache_extra_ms": ms_tc - ms}
+    finally:
+        rx.close()
+    return {"what": "SPDP participant reader (DUPLICATES_OK), one topic, max_keep 64: every delivery a candidate, "
+                    ">= 50 % of them repeats of keys stored earlier in the batch (tc_resolve, one thread per topic)",
+            **out}
 
 
 HELLO_PREFIX = bytes([0x01, 0x0f, 0x99, 0x06, 0x78, 0x34, 0x00, 0x00, 0x01, 0x00, 0x00, 0x00])
@@ -1009,6 +1200,11 @@ def measure(args, world, rank, dist, dev, allreduce_sum, allreduce_max):
         result["c1_loopback_4_publishers"] = c1_loopback(dev, stream, n=400_000, publishers=4)
     if world == 1 and not args.no_e2e:
         result["end_to_end"] = end_to_end(rx, arena, off_t, ln_t, n, outs, n_rec, stream)
+        if n_matched_writers:
+            result["end_to_end"]["full_chain"] = full_chain(rx, args.workload, arena, off_t, ln_t, n, n_rec,
+                                                            n_matched_writers)
+    if world == 1 and not args.no_ingest and n_matched_writers and args.workload == "C3" and not c5:
+        result["topic_cache_spdp_repeats"] = spdp_repeats_leg(dev, stream, min(args.steps, 10))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline("C3" if c5 else args.workload, min(n, 1 << 20), match_table=tbl)
     rx.close()

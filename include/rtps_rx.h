@@ -366,9 +366,11 @@ int rtps_rx_exchange(rtps_rx_ctx* ctx, void* comm, void* hip_stream, const void*
  * that state consumes, so that the owner runs rtps_rx_frag_assemble and
  * rtps_rx_ingest as one GPU would on the whole stream:
  *   - items: every writer-kind record that passes (RTPS_ROUTE_PASS: DATA,
- *     DATA_FRAG, HEARTBEAT, HEARTBEAT_FRAG, GAP), owner = fmix32(fnv1a32(prefix ||
- *     writer_id)) % n_ranks (as rtps_rx_bucket_by_writer).  What crosses is a
- *     32-byte rtps_shard_item per record and a "blob": a DATA is its item alone
+ *     DATA_FRAG, HEARTBEAT, HEARTBEAT_FRAG, GAP), owner = the writer's owner in the
+ *     shard's owner table (rtps_rx_shard_set_owners below; default: the context's
+ *     writers dealt evenly), else fmix32(fnv1a32(prefix || writer_id)) % n_ranks.
+ *     What crosses is a 32-byte rtps_shard_item per record and a "blob": a DATA is
+ *     its item alone
  *     (writer GUID, SN, kind, flags, route, payload kind: what the owner's ingest
  *     reads; its payload stays on the source GPU, zero-copy, and `origin` names the
  *     record there); any other kind sends its whole 64-byte record in the blob,
@@ -457,6 +459,38 @@ typedef struct rtps_shard_buffers {
 int rtps_rx_shard_buffers(rtps_shard* s, rtps_shard_buffers* out);
 /* Grow the receive spill to hold `records` records and `bytes` blob bytes. */
 int rtps_rx_shard_reserve_spill(rtps_shard* s, uint64_t records, uint64_t bytes);
+
+/* Writer -> owner assignment of the items.  An owner's step time follows its busiest
+ * owner, and a hash of few writers leaves owners unequal (16 writers over 8 ranks: one
+ * idle, one with 1.5x the mean), so the shard keeps a table of the context's writers
+ * (the writer GUIDs of its proxies) dealt over the ranks; a writer not in it goes by
+ * fmix32(fnv1a32(GUID)) % n_ranks.  Every rank must set the same readers, topics and
+ * arguments: the deal is a function of them alone (not of their order).  The table
+ * follows rtps_rx_set_readers / set_match_table / set_topics (rebuilt at the next pack).
+ *   RTPS_OWNER_BALANCED (the default)  every writer its own group;
+ *   RTPS_OWNER_TOPIC   writers whose target readers share a topic cache (a topic of
+ *     rtps_rx_set_topics, or a reader's own cache) are one group, so one owner holds
+ *     all of a TopicCache's changes: needed for RTPS_INGEST_TOPIC_CACHE on owner
+ *     batches to be exact (the cache's GC spans its writers, dds_cache.rs:367-420);
+ *   RTPS_OWNER_HASH    no table (every writer by the hash).
+ * Groups are dealt by total weight, largest first, each to the least-loaded owner (ties:
+ * the group's smallest GUID, the lowest rank); equal weights deal the sorted GUIDs
+ * round-robin.  guids[n][16] / weights[n] (optional): weights of writers (e.g. their
+ * records in the previous batches); a listed writer the context does not know joins
+ * the table as a group of its own; unlisted writers weigh 1. */
+#define RTPS_OWNER_BALANCED 0u
+#define RTPS_OWNER_HASH 1u
+#define RTPS_OWNER_TOPIC 2u
+int rtps_rx_shard_set_owners(rtps_shard* s, uint32_t mode, const uint8_t* guids, const uint64_t* weights,
+                             uint32_t n);
+/* The owner rank of a writer GUID under the shard's current assignment (host), or a
+ * negative RTPS_RX_* code. */
+int rtps_rx_shard_owner(rtps_shard* s, const uint8_t guid[16]);
+/* The deal itself, on the host (no GPU): writers[n][16], weights[n] (NULL: 1 each),
+ * groups[n] (NULL: every writer its own; else writer w is in group groups[w] < n) ->
+ * owners[n] < n_ranks. */
+int rtps_rx_owner_assign(const uint8_t* writers, const uint64_t* weights, const uint32_t* groups, uint32_t n,
+                         uint32_t n_ranks, uint32_t* owners);
 
 /* ---- batch CDR primitive decode (a18) ------------------------------------
  * Replaces, for fixed-layout sample types, the per-sample decode
@@ -688,8 +722,12 @@ int rtps_rx_ingest(rtps_rx_ctx* ctx, const uint8_t* arena, uint64_t arena_len, c
                    const rtps_record* records, const uint64_t* n_records, uint64_t max_records,
                    const rtps_frag_sample* frag, const uint64_t* n_frag, uint64_t max_frag, uint32_t flags,
                    const rtps_ingest_out* out);
-/* Forget every writer proxy's state (all_ackable_before = 1, empty change set, count 0)
- * and empty every topic cache. */
+/* Forget every writer proxy's state (all_ackable_before = 1, empty change set, count 0),
+ * as re-created RtpsWriterProxy entries start (rtps_writer_proxy.rs:62-90).  The topic
+ * caches keep their changes, as the reference's TopicCache outlives its readers' proxies:
+ * a re-sent (writer GUID, SN) that a fresh proxy accepts is still dropped by add_change's
+ * find_by_sn while the topic holds it (dds_cache.rs:241-276).  rtps_rx_topic_reset empties
+ * the caches. */
 int rtps_rx_ingest_reset(rtps_rx_ctx* ctx);
 
 /* ---- topic caches (TopicCache::add_change, structure/dds_cache.rs:113-420) ----
@@ -723,6 +761,8 @@ int rtps_rx_set_topics(rtps_rx_ctx* ctx, const rtps_topic* topics, uint32_t n_to
 /* DDSCache::garbage_collect: every topic cache trimmed to its max_keep_samples
  * newest changes (asynchronous). */
 int rtps_rx_topic_gc(rtps_rx_ctx* ctx);
+/* Empty every topic cache (a new DDSCache); the writer proxies keep their state. */
+int rtps_rx_topic_reset(rtps_rx_ctx* ctx);
 
 /* ---- UDP batch receive into a datagram arena -----
  * Replaces the receive side of the reference: a UDPListener per locator with

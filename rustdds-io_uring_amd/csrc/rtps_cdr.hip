@@ -350,11 +350,16 @@ void cdr_decode_kernel(CdrProg P, CdrArgs a) {
     if (lane < nv) {
       // the row's record: the row itself, or its list entry (a delivery, a sample index)
       const uint64_t ri = a.list ? *reinterpret_cast<const uint32_t*>(a.list + (r0 + lane) * a.list_stride) : r0 + lane;
-      const rtps_record* rec = a.records + (ri < nrec ? ri : 0);
-      // bytes 0..31 (dgram_idx @0, kind @6, payload_kind @31) and 40..47 (pl_off, pl_len, rep_id)
-      const uint4 h0 = *(const uint4*)rec;
-      const uint4 h1 = *(const uint4*)((const uint8_t*)rec + 16);
-      const uint2 u0 = *(const uint2*)((const uint8_t*)rec + 40);
+      // bytes 0..31 (dgram_idx @0, kind @6, payload_kind @31) and 40..47 (pl_off, pl_len, rep_id); a list
+      // entry past the records loads nothing (nrec may be 0)
+      uint4 h0 = {0u, 0u, 0u, 0u}, h1 = h0;
+      uint2 u0 = {0u, 0u};
+      if (ri < nrec) {
+        const rtps_record* rec = a.records + ri;
+        h0 = *(const uint4*)rec;
+        h1 = *(const uint4*)((const uint8_t*)rec + 16);
+        u0 = *(const uint2*)((const uint8_t*)rec + 40);
+      }
       const uint32_t kind = (h0.y >> 16) & 0xff, pk = h1.w >> 24;
       const uint32_t pl_off = u0.x & 0xffff, pl_len = u0.x >> 16;
       const uint32_t id0 = u0.y & 0xff, id1 = (u0.y >> 8) & 0xff;

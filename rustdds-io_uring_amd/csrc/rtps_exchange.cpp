@@ -97,15 +97,19 @@ int rtps_rx_exchange(rtps_rx_ctx* ctx, void* comm, void* hip_stream, const void*
   ncclComm_t c = (ncclComm_t)comm;
   int world = 0, me = 0;
   if (ncclCommCount(c, &world) != ncclSuccess || ncclCommUserRank(c, &me) != ncclSuccess) return RTPS_RX_EHIP;
-  (void)me;
   if (hipSetDevice(rtps_ctx_device(ctx)) != hipSuccess) return RTPS_RX_EHIP;
   hipStream_t st = hip_stream ? (hipStream_t)hip_stream : rtps_ctx_stream(ctx);
   const size_t bytes = (size_t)cap * item_bytes;
   const uint8_t* s = static_cast<const uint8_t*>(send);
   uint8_t* r = static_cast<uint8_t*>(recv);
+  // this rank's own bucket: a device copy on the same stream, not an RCCL self-send
+  if (hipMemcpyAsync(recv_counts + me, send_counts + me, sizeof(uint64_t), hipMemcpyDeviceToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(r + (size_t)me * bytes, s + (size_t)me * bytes, bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
+    return RTPS_RX_EHIP;
   if (ncclGroupStart() != ncclSuccess) return RTPS_RX_EHIP;
   bool ok = true;
   for (int p = 0; p < world && ok; ++p) {
+    if (p == me) continue;
     ok = ncclSend(send_counts + p, 1, ncclUint64, p, c, st) == ncclSuccess &&
          ncclRecv(recv_counts + p, 1, ncclUint64, p, c, st) == ncclSuccess &&
          send_bytes(s + (size_t)p * bytes, bytes, p, c, st) && recv_bytes(r + (size_t)p * bytes, bytes, p, c, st);
@@ -118,17 +122,26 @@ int rtps_rx_exchange(rtps_rx_ctx* ctx, void* comm, void* hip_stream, const void*
 int rtps_rx_shard_exchange(rtps_shard* s, void* comm, void* hip_stream) {
   if (!s || !comm) return RTPS_RX_EINVAL;
   ncclComm_t c = (ncclComm_t)comm;
-  int world = 0;
-  if (ncclCommCount(c, &world) != ncclSuccess) return RTPS_RX_EHIP;
+  int world = 0, me = 0;
+  if (ncclCommCount(c, &world) != ncclSuccess || ncclCommUserRank(c, &me) != ncclSuccess) return RTPS_RX_EHIP;
   if ((uint32_t)world != s->n_ranks) return RTPS_RX_EINVAL;
   if (hipSetDevice(s->device) != hipSuccess) return RTPS_RX_EHIP;
   hipStream_t st = hip_stream ? (hipStream_t)hip_stream : rtps_ctx_stream(s->ctx);
   if (hipStreamWaitEvent(st, s->packed, 0) != hipSuccess) return RTPS_RX_EHIP;  // the slots are complete
   const size_t rb = (size_t)s->cap * sizeof(shard_item), bb = (size_t)s->bcap;
   const size_t cw = sizeof(rtps_shard_counts) / sizeof(uint64_t);
+  // this rank's own slot: device copies on the same stream, not an RCCL self-send
+  if (hipMemcpyAsync(s->r_counts + me, s->s_counts + me, sizeof(rtps_shard_counts), hipMemcpyDeviceToDevice, st) !=
+          hipSuccess ||
+      hipMemcpyAsync(reinterpret_cast<uint8_t*>(s->r_slots) + me * rb,
+                     reinterpret_cast<const uint8_t*>(s->s_slots) + me * rb, rb, hipMemcpyDeviceToDevice, st) !=
+          hipSuccess ||
+      hipMemcpyAsync(s->r_blob + me * bb, s->s_blob + me * bb, bb, hipMemcpyDeviceToDevice, st) != hipSuccess)
+    return RTPS_RX_EHIP;
   if (ncclGroupStart() != ncclSuccess) return RTPS_RX_EHIP;
   bool ok = true;
   for (int p = 0; p < world && ok; ++p) {
+    if (p == me) continue;
     ok = ncclSend(s->s_counts + p, cw, ncclUint64, p, c, st) == ncclSuccess &&
          ncclRecv(s->r_counts + p, cw, ncclUint64, p, c, st) == ncclSuccess &&
          send_bytes(reinterpret_cast<const uint8_t*>(s->s_slots) + p * rb, rb, p, c, st) &&
@@ -171,6 +184,8 @@ int rtps_rx_shard_finish(rtps_shard* s, void* comm, void* hip_stream) {
     return RTPS_RX_OK;
   }
   if (rtps_rx_shard_reserve_spill(s, need_r, need_b) != RTPS_RX_OK) return abort_comm(c);  // spill not receivable
+  int me = 0;
+  if (ncclCommUserRank(c, &me) != ncclSuccess) return abort_comm(c);
   if (ncclGroupStart() != ncclSuccess) return abort_comm(c);
   bool ok = true;
   uint64_t sb = 0, sbb = 0, rs = 0, rsb = 0;  // send-side exact-layout bases, receive-side spill offsets
@@ -178,10 +193,16 @@ int rtps_rx_shard_finish(rtps_shard* s, void* comm, void* hip_stream) {
     const rtps_shard_counts& q = s->h_send[p];
     const rtps_shard_counts& r = s->h_recv[p];
     const uint64_t sn = q.n - q.cut, sbytes = q.bytes - q.cut_bytes, rn = r.n - r.cut, rbytes = r.bytes - r.cut_bytes;
-    ok = send_bytes(s->s_spill + sb + q.cut, sn * sizeof(shard_item), (int)p, c, st) &&
-         send_bytes(s->s_bspill + sbb + q.cut_bytes, sbytes, (int)p, c, st) &&
-         recv_bytes(s->r_spill + rs, rn * sizeof(shard_item), (int)p, c, st) &&
-         recv_bytes(s->r_bspill + rsb, rbytes, (int)p, c, st);
+    if ((int)p == me)  // this rank's own spill (sn == rn): device copies, not an RCCL self-send
+      ok = (!sn || hipMemcpyAsync(s->r_spill + rs, s->s_spill + sb + q.cut, sn * sizeof(shard_item),
+                                  hipMemcpyDeviceToDevice, st) == hipSuccess) &&
+           (!sbytes || hipMemcpyAsync(s->r_bspill + rsb, s->s_bspill + sbb + q.cut_bytes, sbytes,
+                                      hipMemcpyDeviceToDevice, st) == hipSuccess);
+    else
+      ok = send_bytes(s->s_spill + sb + q.cut, sn * sizeof(shard_item), (int)p, c, st) &&
+           send_bytes(s->s_bspill + sbb + q.cut_bytes, sbytes, (int)p, c, st) &&
+           recv_bytes(s->r_spill + rs, rn * sizeof(shard_item), (int)p, c, st) &&
+           recv_bytes(s->r_bspill + rsb, rbytes, (int)p, c, st);
     sb += q.n;
     sbb += q.bytes;
     rs += rn;
@@ -191,6 +212,21 @@ int rtps_rx_shard_finish(rtps_shard* s, void* comm, void* hip_stream) {
   if (!ok || !ended) return abort_comm(c);
   if (hipEventRecord(s->done, st) != hipSuccess) return abort_comm(c);
   s->finished = true;
+  return RTPS_RX_OK;
+}
+
+/* diagnostic hook (not in the public header; scripts/rccl_size_probe.py): ONE unchunked
+   ncclSend + ncclRecv of `bytes` bytes between this rank and `peer` in one group on
+   hip_stream, to find the message sizes RCCL delivers whole (the reason for XCHUNK). */
+int rtps_rx_debug_rccl_p2p(void* comm, void* hip_stream, const void* send, void* recv, uint64_t bytes, int peer) {
+  if (!comm || !send || !recv) return RTPS_RX_EINVAL;
+  ncclComm_t c = (ncclComm_t)comm;
+  hipStream_t st = (hipStream_t)hip_stream;
+  if (ncclGroupStart() != ncclSuccess) return RTPS_RX_EHIP;
+  const bool ok = ncclSend(send, (size_t)bytes, ncclUint8, peer, c, st) == ncclSuccess &&
+                  ncclRecv(recv, (size_t)bytes, ncclUint8, peer, c, st) == ncclSuccess;
+  const bool ended = ncclGroupEnd() == ncclSuccess;
+  if (!ok || !ended) return abort_comm(c);
   return RTPS_RX_OK;
 }
 

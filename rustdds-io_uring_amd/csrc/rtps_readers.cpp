@@ -18,6 +18,7 @@
 
 namespace {
 typedef std::array<uint8_t, 16> Guid;
+static_assert(sizeof(Guid) == 16, "GUIDs back to back");
 typedef std::array<uint8_t, 4> Eid;
 // EntityId::SPDP_BUILTIN_PARTICIPANT_READER {0x00,0x01,0x00}, 0xc7 (structure/guid.rs)
 const Eid SPDP_PARTICIPANT_READER = {0x00, 0x01, 0x00, 0xc7};
@@ -37,6 +38,7 @@ uint32_t word(const uint8_t* p) {
 struct ReaderTable {
   std::vector<uint32_t> first;     // [n_sets + 1]
   std::vector<rtps_target> ent;
+  std::vector<Guid> wguid;         // [n_writer_sets] the writer GUID of each writer set
   uint32_t n_writer_sets = 0, n_proxies = 0, max_set = 0;
   bool active = false;
   // device images
@@ -84,6 +86,7 @@ namespace {
 struct Built {  // host image of a reader table
   std::vector<uint32_t> first;
   std::vector<rtps_target> ent;
+  std::vector<Guid> wguid;
   std::vector<uint32_t> gkeys, gset, ekeys, eset;
   uint32_t gcap = 0, ecap = 0, n_writer_sets = 0, max_set = 0;
 };
@@ -191,6 +194,7 @@ int build(const rtps_reader* readers, uint32_t nr, const rtps_proxy* proxies, ui
   out.gcap = gcap; out.ecap = ecap;
   out.n_writer_sets = (uint32_t)wsets.size();
   out.max_set = max_set;
+  out.wguid.swap(wsets);
   return RTPS_RX_OK;
 }
 }  // namespace
@@ -227,6 +231,7 @@ int rt_set(ReaderTable* t, const rtps_reader* readers, uint32_t nr, const rtps_p
   t->ecap = ecap;
   t->first.swap(first);
   t->ent.swap(ent);
+  t->wguid.swap(b.wguid);
   t->n_writer_sets = b.n_writer_sets;
   t->n_proxies = np;
   t->max_set = b.max_set;
@@ -278,6 +283,12 @@ ReaderDev rt_dev(const ReaderTable* t) {
   r.max_set = t->max_set;
   r.n_ent = t->first.empty() ? 0u : t->first.back();
   return r;
+}
+
+const uint8_t* rt_writer_guids(const ReaderTable* t, uint32_t* n) {
+  const bool on = t && t->active && !t->wguid.empty();
+  *n = on ? (uint32_t)t->wguid.size() : 0u;
+  return on ? t->wguid[0].data() : nullptr;
 }
 
 void rt_host(const ReaderTable* t, const uint32_t** first, const rtps_target** ent, uint32_t* n_sets) {

@@ -129,3 +129,5 @@ int rt_set(ReaderTable* t, const rtps_reader* readers, uint32_t n_readers, const
 int rt_set_match(ReaderTable* t, const rtps_match* m, uint32_t n, hipStream_t stream);
 ReaderDev rt_dev(const ReaderTable* t);  // gkeys == nullptr when no reader is set
 void rt_host(const ReaderTable* t, const uint32_t** first, const rtps_target** ent, uint32_t* n_sets);
+// the writer GUIDs of the writer sets 0 .. n-1 (16 bytes each, contiguous), nullptr when none
+const uint8_t* rt_writer_guids(const ReaderTable* t, uint32_t* n);

@@ -679,8 +679,8 @@ constexpr uint64_t ARENA_DIRECT = RTPS_ARENA_DIRECT;  // (0: every arena per wav
 // (base = the arena, or for arenas of 4 GiB and more the min offset over the wave:
 // no workgroup barrier) and the 64-byte head
 template <uint32_t TS = TILE>
-__device__ __forceinline__ void load_tile(const KParams& p, uint32_t tile, TileCtx& t, bool enabled = true) {
-  const uint32_t tid = threadIdx.x;
+__device__ __forceinline__ void tile_src(const KParams& p, uint32_t tile, TileCtx& t, bool enabled = true,
+                                         uint32_t tid = threadIdx.x) {
   t.i = tile * TS + tid;
   t.valid = enabled && tid < TS && t.i < p.n;
   const uint64_t off = t.valid ? p.dgram_off[t.i] : ~0ull;
@@ -706,6 +706,12 @@ __device__ __forceinline__ void load_tile(const KParams& p, uint32_t tile, TileC
   const uint64_t rel = t.valid ? off - tb : 0;
   t.addressable = t.valid && off <= p.arena_len && (uint64_t)t.L <= p.arena_len - off && rel + t.L <= avail;
   t.s.base = (uint32_t)rel;
+}
+// tile_src plus the 64-byte head
+template <uint32_t TS = TILE>
+__device__ __forceinline__ void load_tile(const KParams& p, uint32_t tile, TileCtx& t, bool enabled = true,
+                                          uint32_t tid = threadIdx.x) {
+  tile_src<TS>(p, tile, t, enabled, tid);
   u32x4 a = {0u, 0u, 0u, 0u}, b = a, c = a, d = a;
   if (t.addressable) {
     a = ld16(t.s, 0); b = ld16(t.s, 16); c = ld16(t.s, 32);
@@ -1132,6 +1138,7 @@ constexpr uint32_t CAPW = RTPS_IT_CAPW;  // items per wave slab (C3 averages 243
 #endif
 constexpr uint32_t IW = RTPS_IT_WIDE ? 3u : 1u;  // u32x4 per item
 constexpr uint32_t WCNT_OVERFLOW = 0x80000000u;
+constexpr uint32_t DI_NOREC = 0x80000000u;  // dinfo[0]: the datagram has no records
 #ifndef RTPS_IT_WAVES_PER_SIMD
 #define RTPS_IT_WAVES_PER_SIMD 8
 #endif
@@ -1196,7 +1203,7 @@ __device__ uint32_t item_walk(const KParams& p, const Src& s, const uint32_t* H,
 
 __global__ __launch_bounds__(TILE, RTPS_IT_WAVES_PER_SIMD) void rtps_parse_item_kernel(KParams p, uint32_t n_tiles,
                                                                                      uint32_t k_spec, u32x4* items,
-                                                                                     uint32_t* wcnt) {
+                                                                                     uint32_t* wcnt, u32x4* dinfo) {
   __shared__ uint32_t s_wave_sum[WAVES], s_wave_bad[WAVES];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const uint32_t tile = blockIdx.x;
@@ -1209,6 +1216,7 @@ __global__ __launch_bounds__(TILE, RTPS_IT_WAVES_PER_SIMD) void rtps_parse_item_
     else st = item_walk(p, t.s, t.H, t.L, lane, slab, wpos, cnt);
     if (st != RTPS_DGRAM_OK) cnt = 0;
   }
+  const uint32_t incl = dinfo ? wave_incl_scan(cnt, lane) : 0u;
   // the wave's item total: the position of the lane that walked longest
   uint32_t wtot = wpos, wsum = cnt;
 #pragma unroll
@@ -1226,7 +1234,7 @@ __global__ __launch_bounds__(TILE, RTPS_IT_WAVES_PER_SIMD) void rtps_parse_item_
   Scratch x = scratch_of(p.scratch, n_tiles);
   if (t.valid) {
     p.status[t.i] = (uint8_t)st;
-    x.dcount[t.i] = (uint16_t)cnt;
+    if (!dinfo) x.dcount[t.i] = (uint16_t)cnt;
   }
   __syncthreads();
   if (tid == 0) {
@@ -1234,6 +1242,12 @@ __global__ __launch_bounds__(TILE, RTPS_IT_WAVES_PER_SIMD) void rtps_parse_item_
 #pragma unroll
     for (uint32_t w = 0; w < WAVES; ++w) { agg += s_wave_sum[w]; mixed |= s_wave_bad[w]; }
     x.info[tile] = agg | INFO_NONSPEC | (mixed ? INFO_MIXED : 0u);
+  }
+  if (dinfo && t.valid) {  // the record pass's per-datagram prologue, one coalesced 16-B word
+    uint32_t woff = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < WAVES; ++w) woff += w < wave ? s_wave_sum[w] : 0u;
+    dinfo[t.i] = u32x4{(woff + incl - cnt) | (cnt ? 0u : DI_NOREC), t.H[2], t.H[3], t.H[4]};
   }
 }
 
@@ -1518,6 +1532,263 @@ void rtps_parse_emit_kernel(KParams p, uint32_t n_tiles, const u32x4* items, con
     }
   }
   EM_WAVE_END();
+}
+
+// ---------------------------------------------------------------------------
+// W2 rtps_parse_emit2_kernel: wave w of a workgroup takes E's wave slab w of each tile
+// of its grid stride.  The reader tables are staged once per workgroup; after that no
+// wave waits for another (no barrier, no per-tile prologue scan).  The per-datagram
+// prologue is one coalesced 16-B word E wrote (dinfo: the datagram's tile-local first
+// record, its header prefix) plus the (offset, length) arrays: lane l holds datagram l
+// of the slab, and an item takes its datagram's fields with lane permutes.  The
+// descriptor base is E's (the arena, or for large arenas the wave's smallest offset),
+// so every datagram E walked is addressable here.
+// The item of slab position k, its datagram's fields (lane permutes: every lane of the
+// wave calls this) and the record it becomes: R, its target set, its index r (~0: none).
+__device__ __forceinline__ void em2_item(const KParams& p, const Src& s0, const u32x4 it, bool act, const u32x4 di,
+                                         uint32_t doff, uint32_t dlen, uint32_t dg0, uint64_t prefix, Rec& R,
+                                         uint32_t& tgt, uint64_t& r) {
+  const uint32_t d = (it[1] >> 16) & 63u;
+  const uint32_t rb = __shfl(di[0], d, 64);
+  const uint32_t base = __shfl(doff, d, 64), len = __shfl(dlen, d, 64);
+  const uint32_t pf0 = __shfl(di[1], d, 64), pf1 = __shfl(di[2], d, 64), pf2 = __shfl(di[3], d, 64);
+  r = ~0ull;
+  tgt = RTPS_NO_TARGET;
+  if (!act || (rb & DI_NOREC)) return;  // (a datagram dropped after this item)
+  const uint32_t o = it[0] & 0xffffu, src_off = it[0] >> 16;
+  const uint32_t j = it[1] & 0xffffu, kind = it[1] >> 24;
+  Src s = s0;
+  s.base = base;
+  Win W;
+  {
+    const u32x4 a = ld16(s, o);
+    u32x4 bq = {0u, 0u, 0u, 0u};
+    if (win_needs_tail<true>(kind)) bq = ld16(s, o + 16u);
+    W.w[0] = a[0]; W.w[1] = a[1]; W.w[2] = a[2]; W.w[3] = a[3];
+    W.w[4] = bq[0]; W.w[5] = bq[1]; W.w[6] = bq[2]; W.w[7] = bq[3];
+    W.w[8] = kind == RTPS_DATA_FRAG ? ld4(s, o + 32u) : 0u;
+    W.w[9] = 0u; W.w[10] = 0u; W.w[11] = 0u;
+  }
+  Interp st;
+  if (src_off == 8u) {
+    st.src0 = pf0; st.src1 = pf1; st.src2 = pf2;
+  } else {  // an INFO_SRC's prefix is in effect
+    const u32x4 q = ld16(s, src_off);
+    st.src0 = q[0]; st.src1 = q[1]; st.src2 = q[2];
+  }
+  st.dst_ok = ((it[1] >> 22) & 1u) != 0u;
+  st.ts_valid = ((it[1] >> 23) & 1u) != 0u;
+  st.ts_sec = it[2];
+  st.ts_frac = it[3];
+  const uint32_t flags = (W.w[0] >> 8) & 0xffu;
+  const bool le = (flags & 1u) != 0u;
+  const uint32_t eff = eff_len(kind, e16(W.w[0], 1, le), len - o);
+  rec_clear(R);
+  SubOut so;
+  sub_body<true>(s, W, kind, flags, le, o + 4u, eff, R, so);  // validated by E's walk
+  R.d[0] = dg0 + d;
+  R.d[1] = o | (kind << 16) | (flags << 24);
+  tgt = rec_finish(p, R, so, kind, st);
+  r = prefix + rb + j;
+}
+
+// ---------------------------------------------------------------------------
+// W2 rtps_parse_emit2_kernel: wave w of a workgroup takes E's wave slab w of each tile
+// of its grid stride.  The reader tables are staged once per workgroup; after that no
+// wave waits for another (no barrier, no per-tile prologue scan).  The per-datagram
+// prologue is one coalesced 16-B word E wrote (dinfo: the datagram's tile-local first
+// record, its header prefix) plus the (offset, length) arrays: lane l holds datagram l
+// of the slab, and an item takes its datagram's fields with lane permutes.  The
+// descriptor base is E's (the arena, or for large arenas the wave's smallest offset),
+// so every datagram E walked is addressable here.
+// The item of slab position k, its datagram's fields (lane permutes: every lane of the
+// wave calls this) and the record it becomes.
+__device__ __forceinline__ void em2_item(const KParams& p, const Src& s0, const u32x4 it, bool act, const u32x4 di,
+                                         uint32_t doff, uint32_t dlen, uint32_t dg0, uint64_t prefix) {
+  const uint32_t d = (it[1] >> 16) & 63u;
+  const uint32_t rb = __shfl(di[0], d, 64);
+  const uint32_t base = __shfl(doff, d, 64), len = __shfl(dlen, d, 64);
+  const uint32_t pf0 = __shfl(di[1], d, 64), pf1 = __shfl(di[2], d, 64), pf2 = __shfl(di[3], d, 64);
+  if (!act || (rb & DI_NOREC)) return;  // (a datagram dropped after this item)
+  const uint32_t o = it[0] & 0xffffu, src_off = it[0] >> 16;
+  const uint32_t j = it[1] & 0xffffu, kind = it[1] >> 24;
+  Src s = s0;
+  s.base = base;
+  Win W;
+  {
+    const u32x4 a = ld16(s, o);
+    u32x4 bq = {0u, 0u, 0u, 0u};
+    if (win_needs_tail<true>(kind)) bq = ld16(s, o + 16u);
+    W.w[0] = a[0]; W.w[1] = a[1]; W.w[2] = a[2]; W.w[3] = a[3];
+    W.w[4] = bq[0]; W.w[5] = bq[1]; W.w[6] = bq[2]; W.w[7] = bq[3];
+    W.w[8] = kind == RTPS_DATA_FRAG ? ld4(s, o + 32u) : 0u;
+    W.w[9] = 0u; W.w[10] = 0u; W.w[11] = 0u;
+  }
+  Interp st;
+  if (src_off == 8u) {
+    st.src0 = pf0; st.src1 = pf1; st.src2 = pf2;
+  } else {  // an INFO_SRC's prefix is in effect
+    const u32x4 q = ld16(s, src_off);
+    st.src0 = q[0]; st.src1 = q[1]; st.src2 = q[2];
+  }
+  st.dst_ok = ((it[1] >> 22) & 1u) != 0u;
+  st.ts_valid = ((it[1] >> 23) & 1u) != 0u;
+  st.ts_sec = it[2];
+  st.ts_frac = it[3];
+  const uint32_t flags = (W.w[0] >> 8) & 0xffu;
+  const bool le = (flags & 1u) != 0u;
+  const uint32_t eff = eff_len(kind, e16(W.w[0], 1, le), len - o);
+  Rec R;
+  rec_clear(R);
+  SubOut so;
+  sub_body<true>(s, W, kind, flags, le, o + 4u, eff, R, so);  // validated by E's walk
+  R.d[0] = dg0 + d;
+  R.d[1] = o | (kind << 16) | (flags << 24);
+  const uint32_t tgt = rec_finish(p, R, so, kind, st);
+  const uint64_t r = prefix + rb + j;
+  if (r < p.max_records) {
+    rec_store(p.records + r, R);
+    if (p.target_out) p.target_out[r] = tgt;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// W2 rtps_parse_emit2_kernel: wave w of a workgroup takes E's wave slab w of each tile
+// of its grid stride.  The reader tables are staged once per workgroup; after that no
+// wave waits for another (no barrier, no per-tile prologue scan).  The per-datagram
+// prologue is one coalesced 16-B word E wrote (dinfo: the datagram's tile-local first
+// record, its header prefix) plus the (offset, length) arrays: lane l holds datagram l
+// of the slab, and an item takes its datagram's fields with lane permutes.  The
+// descriptor base is E's (the arena, or for large arenas the wave's smallest offset),
+// so every datagram E walked is addressable here.
+// REC_ORDER: the wave first maps its records to their slab positions in LDS (record q of
+// the wave = item k, from the item's datagram and index j), then takes the items in
+// record order: the 64 lanes of a round read neighbouring submessages (a datagram's
+// submessages share lines and DRAM rows) and write 64 consecutive records.  Otherwise the
+// items are taken in slab order (E's walk step major: 64 datagrams' k-th submessages).
+#ifndef RTPS_EM2_WAVES_PER_SIMD
+#define RTPS_EM2_WAVES_PER_SIMD 6  // 80 VGPRs, no spill (the LDS caps the CU at 24 waves anyway)
+#endif
+#ifndef RTPS_EM2_TRANSPOSE
+#define RTPS_EM2_TRANSPOSE 1  // record order: each record store instruction writes 1 KB back to back
+#endif
+#ifndef RTPS_EM2_THREADS
+#define RTPS_EM2_THREADS 512  // two tiles per workgroup (one reader-table copy for 8 waves; 256 / 768: slower)
+#endif
+constexpr uint32_t EM2T = RTPS_EM2_THREADS, EM2_TPB = EM2T / TILE;
+static_assert(EM2T % TILE == 0, "whole tiles per workgroup");
+template <bool REC_ORDER>
+__global__ __launch_bounds__(EM2T, RTPS_EM2_WAVES_PER_SIMD) void rtps_parse_emit2_kernel(
+    KParams p, uint32_t n_tiles, const u32x4* __restrict__ items, const uint32_t* __restrict__ wcnt,
+    const uint64_t* __restrict__ tprefix, const u32x4* __restrict__ dinfo) {
+  static_assert(!RTPS_IT_WIDE, "W2 takes 16-B items");
+  __shared__ uint16_t s_map[REC_ORDER ? (EM2T / 64u) * CAPW : 1];
+#if RTPS_EM2_TRANSPOSE
+  __shared__ u32x4 s_stage[REC_ORDER ? (EM2T / 64u) * 64u : 1];  // 1 KB per wave
+#endif
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+  const uint32_t wave = wv % WAVES, sub = wv / WAVES;  // the wave's slab in its tile, the workgroup's tile
+  uint16_t* map = s_map + (REC_ORDER ? wv * CAPW : 0u);
+  mt_stage(p);
+  __syncthreads();
+  for (uint32_t tile = blockIdx.x * EM2_TPB + sub; tile < n_tiles; tile += gridDim.x * EM2_TPB) {
+    const uint32_t wc = __builtin_amdgcn_readfirstlane(wcnt[tile * WAVES + wave]);
+    const uint64_t prefix = tprefix[tile];
+    TileCtx t;
+    tile_src(p, tile, t, true, wave * 64u + lane);
+    const u32x4 di = t.valid ? dinfo[t.i] : u32x4{DI_NOREC, 0u, 0u, 0u};
+    const uint32_t first = di[0] & ~DI_NOREC;
+    if (t.valid && p.rec_begin) p.rec_begin[t.i] = (uint32_t)(prefix + first);
+    if (wc & WCNT_OVERFLOW) continue;  // walked below
+    const u32x4* slab = items + (size_t)(tile * WAVES + wave) * CAPW;
+    const uint32_t doff = t.s.base, dlen = t.L;
+    const uint32_t dg0 = tile * TILE + wave * 64u;
+    if (!REC_ORDER) {
+      for (uint32_t b = 0; b < wc; b += 64u) {  // (uniform: every lane takes part in the permutes)
+        const uint32_t k = b + lane;
+        const bool act = k < wc;
+        const u32x4 it = act ? slab[k] : u32x4{0u, 0u, 0u, 0u};
+        Rec R;
+        uint32_t tgt;
+        uint64_t r;
+        em2_item(p, t.s, it, act, di, doff, dlen, dg0, prefix, R, tgt, r);
+        if (r < p.max_records) {
+          rec_store(p.records + r, R);
+          if (p.target_out) p.target_out[r] = tgt;
+        }
+      }
+      continue;
+    }
+    // record q of the wave (q = the datagram's first record - the wave's + j) <- slab position k
+    const uint32_t wbase = __builtin_amdgcn_readfirstlane(first);  // lane 0: the wave's first record
+    uint32_t nr = 0;
+    for (uint32_t b = 0; b < wc; b += 64u) {
+      const uint32_t k = b + lane;
+      const uint32_t m1 = k < wc ? slab[k][1] : 0u;
+      const uint32_t rb = __shfl(di[0], (m1 >> 16) & 63u, 64);
+      const bool keep = k < wc && !(rb & DI_NOREC);
+      if (keep) map[rb - wbase + (m1 & 0xffffu)] = (uint16_t)k;
+      nr += (uint32_t)__popcll(__ballot(keep));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (uint32_t b = 0; b < nr; b += 64u) {
+      const uint32_t q = b + lane;
+      const bool act = q < nr;
+      const u32x4 it = act ? slab[map[q]] : u32x4{0u, 0u, 0u, 0u};
+      Rec R;
+      uint32_t tgt;
+      uint64_t r;
+      em2_item(p, t.s, it, act, di, doff, dlen, dg0, prefix, R, tgt, r);
+      // lane l holds record r0 + l: the 64 records are 4 KB back to back
+      const uint64_t r0 = prefix + wbase + b;
+      const uint32_t nact = nr - b < 64u ? nr - b : 64u;
+      if (p.target_out && r < p.max_records) p.target_out[r] = tgt;
+#if RTPS_EM2_TRANSPOSE
+      // through the wave's 1-KB stage, a quarter of the records at a time: lanes 16c .. 16c+15
+      // write their records, then every lane stores 16 B of them, so each store instruction
+      // writes 1 KB of consecutive records
+      u32x4* stg = s_stage + wv * 64u;
+#pragma unroll
+      for (uint32_t c = 0; c < 4u; ++c) {
+        if ((lane >> 4) == c) {
+          u32x4* q4 = stg + (lane & 15u) * 4u;
+          q4[0] = u32x4{R.d[0], R.d[1], R.d[2], R.d[3]};
+          q4[1] = u32x4{R.d[4], R.d[5], R.d[6], R.d[7]};
+          q4[2] = u32x4{R.d[8], R.d[9], R.d[10], R.d[11]};
+          q4[3] = u32x4{R.d[12], R.d[13], R.d[14], R.d[15]};
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const u32x4 v = stg[lane];
+        const uint32_t rl = 16u * c + (lane >> 2);  // the record (of the 64) whose quarter lane l stores
+        if (rl < nact && r0 + rl < p.max_records)
+          reinterpret_cast<u32x4*>(p.records + r0 + rl)[lane & 3u] = v;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // reads before the next quarter's writes
+        __builtin_amdgcn_wave_barrier();
+      }
+#else
+      if (r < p.max_records) rec_store(p.records + r, R);
+#endif
+      (void)r0; (void)nact;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // map reads before the next tile's writes
+    __builtin_amdgcn_wave_barrier();
+  }
+  // slabs whose items did not fit (rare): walk the wave's datagrams, after the item loop so
+  // that its registers do not carry the walk's
+  for (uint32_t tile = blockIdx.x * EM2_TPB + sub; tile < n_tiles; tile += gridDim.x * EM2_TPB) {
+    if (!(wcnt[tile * WAVES + wave] & WCNT_OVERFLOW)) continue;
+    TileCtx th;
+    load_tile(p, tile, th, true, wave * 64u + lane);
+    const uint32_t di0 = th.valid ? dinfo[th.i][0] : DI_NOREC;
+    if (th.valid && !(di0 & DI_NOREC)) {
+      uint32_t n2;
+      walk<true>(p, th.s, th.H, th.L, th.i, tprefix[tile] + di0, n2);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2333,6 +2604,12 @@ struct rtps_rx_ctx {
   u32x4* it_items = nullptr;      // item pass: wave slabs [tiles * WAVES * CAPW]
   uint32_t* it_wcnt = nullptr;    // item pass: items per wave slab [tiles * WAVES]
   uint64_t* it_prefix = nullptr;  // item pass: tile record prefixes [tiles]
+  u32x4* it_dinfo = nullptr;      // item pass: per-datagram prologue of the record pass [tiles * TILE]
+  uint64_t readers_version = 0;   // bumped by set_readers / set_match_table / set_topics (owner tables follow it)
+  uint32_t emit = 5;              // record pass: 1 = W (a workgroup per tile), 2 / 3 = W2 in slab order with
+                                  // a workgroup per tile / persistent (grid = resident workgroups), 4 / 5 = W2
+                                  // in record order, per tile / persistent
+  uint32_t emit_grid = 0, emit_grid_lds = ~0u;  // W2's resident grid and the LDS size it was computed for
   uint32_t it_tiles = 0;          // tiles the item-pass buffers are sized for
   u32x4* rs_recs = nullptr;       // record-slab pass: wave slabs of records [tiles * WAVES * CAPR * 4]
   uint32_t* rs_meta = nullptr;    //   (j | lane << 16) per slab record
@@ -2349,6 +2626,39 @@ struct rtps_rx_ctx {
   void* fx_tmp = nullptr;
   size_t fx_tmp_bytes = 0;
 };
+
+uint64_t rtps_ctx_readers_version(const rtps_rx_ctx* c) { return c->readers_version; }
+
+void rtps_ctx_owner_writers(const rtps_rx_ctx* c, bool by_topic, std::vector<uint8_t>& guids,
+                            std::vector<uint32_t>& group) {
+  uint32_t nw = 0;
+  const uint8_t* g = c->readers ? rt_writer_guids(c->readers, &nw) : nullptr;
+  guids.assign(g, g + 16ull * nw);
+  group.resize(nw);
+  for (uint32_t w = 0; w < nw; ++w) group[w] = w;
+  if (!by_topic || !nw) return;
+  const uint32_t* first = nullptr;
+  const rtps_target* ent = nullptr;
+  uint32_t n_sets = 0;
+  rt_host(c->readers, &first, &ent, &n_sets);
+  auto root = [&](uint32_t x) {
+    while (group[x] != x) x = group[x] = group[group[x]];
+    return x;
+  };
+  std::vector<uint32_t> topic_writer;  // topic cache -> the first writer seen feeding it
+  std::vector<uint32_t> key;           // (parallel) topic cache ids
+  for (uint32_t w = 0; w < nw && w < n_sets; ++w)
+    for (uint32_t k = first[w]; k < first[w + 1]; ++k) {
+      // the reader's topic cache: a configured topic, or its own (no topics set: one per slot)
+      const uint32_t t = c->topics ? rtps_topic_of_slot(c->topics, ent[k].reader_slot) : ent[k].reader_slot;
+      uint32_t j = 0;
+      while (j < key.size() && key[j] != t) ++j;
+      if (j == key.size()) { key.push_back(t); topic_writer.push_back(w); continue; }
+      const uint32_t a = root(w), b = root(topic_writer[j]);
+      if (a != b) group[a > b ? a : b] = a < b ? a : b;  // the smaller index is the root
+    }
+  for (uint32_t w = 0; w < nw; ++w) group[w] = root(w);
+}
 
 static int hip_fail(hipError_t e) { return e == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP; }
 
@@ -2367,6 +2677,8 @@ int rtps_rx_create(const rtps_rx_config* cfg, rtps_rx_ctx** out_ctx) {
   c->stream = c->own_stream;
   if (const char* e = getenv("RTPS_RX_MIXED_PASS"))  // A/B measurements
     c->mixed_pass = (e[0] == '1') ? 1u : (e[0] == '0') ? 0u : (e[0] == '3') ? 3u : 2u;
+  if (const char* e = getenv("RTPS_RX_EMIT"))  // A/B measurements of the record pass
+    c->emit = (e[0] >= '1' && e[0] <= '5') ? (uint32_t)(e[0] - '0') : c->emit;
   {
     int cus = 0, per_cu = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess && cus > 0 &&
@@ -2410,7 +2722,7 @@ int rtps_rx_destroy(rtps_rx_ctx* c) {
   rtps_ingest_state_free(c->ingest);
   rtps_topic_state_free(c->topics);
   {
-    void* it[] = {c->it_items, c->it_wcnt, c->it_prefix, c->rs_recs, c->rs_meta, c->rs_tgt};
+    void* it[] = {c->it_items, c->it_wcnt, c->it_prefix, c->it_dinfo, c->rs_recs, c->rs_meta, c->rs_tgt};
     for (void* q : it) if (q) (void)hipFree(q);
   }
   {
@@ -2447,6 +2759,7 @@ int rtps_rx_set_readers(rtps_rx_ctx* c, const rtps_reader* readers, uint32_t n_r
                         uint32_t n_proxies) {
   if (!c) return RTPS_RX_EINVAL;
   (void)hipSetDevice(c->device);
+  c->readers_version++;
   int rc = readers_table(c);
   if (!rc) rc = rt_set(c->readers, readers, n_readers, proxies, n_proxies, c->stream);
   return rc ? rc : topics_follow(c);
@@ -2455,6 +2768,7 @@ int rtps_rx_set_readers(rtps_rx_ctx* c, const rtps_reader* readers, uint32_t n_r
 int rtps_rx_set_match_table(rtps_rx_ctx* c, const rtps_match* t, uint32_t n) {
   if (!c) return RTPS_RX_EINVAL;
   (void)hipSetDevice(c->device);
+  c->readers_version++;
   int rc = readers_table(c);
   if (!rc) rc = rt_set_match(c->readers, t, n, c->stream);
   return rc ? rc : topics_follow(c);
@@ -2475,6 +2789,7 @@ int rtps_rx_set_topics(rtps_rx_ctx* c, const rtps_topic* topics, uint32_t n_topi
                        uint32_t n_readers) {
   if (!c) return RTPS_RX_EINVAL;
   (void)hipSetDevice(c->device);
+  c->readers_version++;
   int rc = topics_state(c);
   if (rc) return rc;
   const uint32_t* first = nullptr;
@@ -2579,25 +2894,49 @@ static int parse_launch(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len
   if (item) {  // E (phases 1), then S and W (phases 2); no kernel B
     if (tiles > c->it_tiles || !c->it_items) {
       if (hipStreamSynchronize(c->stream) != hipSuccess) return RTPS_RX_EHIP;
-      void* q[] = {c->it_items, c->it_wcnt, c->it_prefix};
+      void* q[] = {c->it_items, c->it_wcnt, c->it_prefix, c->it_dinfo};
       for (void* b : q) if (b) (void)hipFree(b);
-      c->it_items = nullptr; c->it_wcnt = nullptr; c->it_prefix = nullptr; c->it_tiles = 0;
+      c->it_items = nullptr; c->it_wcnt = nullptr; c->it_prefix = nullptr; c->it_dinfo = nullptr; c->it_tiles = 0;
       c->rs_tiles = 0;  // (the wave counts and prefixes are shared)
       const uint32_t t = (uint32_t)(((size_t)c->max_datagrams + TILE - 1) / TILE) > tiles
                              ? (uint32_t)(((size_t)c->max_datagrams + TILE - 1) / TILE) : tiles;
       if (hipMalloc(&c->it_items, (size_t)t * WAVES * CAPW * IW * sizeof(u32x4)) != hipSuccess ||
           hipMalloc(&c->it_wcnt, (size_t)t * WAVES * sizeof(uint32_t)) != hipSuccess ||
-          hipMalloc(&c->it_prefix, (size_t)t * sizeof(uint64_t)) != hipSuccess)
+          hipMalloc(&c->it_prefix, (size_t)t * sizeof(uint64_t)) != hipSuccess ||
+          hipMalloc(&c->it_dinfo, (size_t)t * TILE * sizeof(u32x4)) != hipSuccess)
         return RTPS_RX_ENOMEM;
       c->it_tiles = t;
     }
+    const bool w2 = c->emit != 1u, rec_order = c->emit >= 4u, persist = c->emit == 3u || c->emit == 5u;
+    if (w2 && persist && c->emit_grid_lds != mt_lds) {  // resident W2 workgroups for this LDS size
+      int cus = 0, per_cu = 0;
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess ||
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rtps_parse_emit2_kernel<true>, EM2T, mt_lds) !=
+              hipSuccess)
+        return RTPS_RX_EHIP;
+      c->emit_grid = (uint32_t)(cus > 0 ? cus : 1) * (uint32_t)(per_cu > 0 ? per_cu : 1);
+      c->emit_grid_lds = mt_lds;
+    }
     if (phases & 1u)
       hipLaunchKernelGGL(rtps_parse_item_kernel, dim3(tiles), dim3(TILE), 0, c->stream, p, tiles, k, c->it_items,
-                         c->it_wcnt);
+                         c->it_wcnt, w2 ? c->it_dinfo : nullptr);
     if (phases & 2u) {
-      hipLaunchKernelGGL(rtps_parse_scan_kernel, dim3(1), dim3(SCAN_T), 0, c->stream, p, tiles, parity, c->it_prefix);
-      hipLaunchKernelGGL(rtps_parse_emit_kernel, dim3(tiles), dim3(EMT), mt_lds, c->stream, p, tiles, c->it_items,
-                         c->it_wcnt, c->it_prefix);
+      if (!(phases & 4u))  // (4: the record pass alone, on the previous launch's scan: bench.py's timing)
+        hipLaunchKernelGGL(rtps_parse_scan_kernel, dim3(1), dim3(SCAN_T), 0, c->stream, p, tiles, parity,
+                           c->it_prefix);
+      if (w2) {
+        const uint32_t groups = (tiles + EM2_TPB - 1) / EM2_TPB;
+        const uint32_t g = (persist && c->emit_grid < groups) ? c->emit_grid : groups;
+        if (rec_order)
+          hipLaunchKernelGGL(rtps_parse_emit2_kernel<true>, dim3(g), dim3(EM2T), mt_lds, c->stream, p, tiles,
+                             c->it_items, c->it_wcnt, c->it_prefix, c->it_dinfo);
+        else
+          hipLaunchKernelGGL(rtps_parse_emit2_kernel<false>, dim3(g), dim3(EM2T), mt_lds, c->stream, p, tiles,
+                             c->it_items, c->it_wcnt, c->it_prefix, c->it_dinfo);
+      } else {
+        hipLaunchKernelGGL(rtps_parse_emit_kernel, dim3(tiles), dim3(EMT), mt_lds, c->stream, p, tiles, c->it_items,
+                           c->it_wcnt, c->it_prefix);
+      }
     }
     return hip_fail(hipGetLastError());
   }
@@ -2639,7 +2978,8 @@ int rtps_rx_parse_batch(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len
 /* measurement hook (not part of the public header): launch only the parse's first
    kernel (phases 1) or only the finishing kernels (phases 2: B, or the item pass's S and
    W), so bench.py can time the kernels alone with HIP events.  A full
-   rtps_rx_parse_batch afterwards restores the per-launch bookkeeping (run two).
+   rtps_rx_parse_batch afterwards restores the per-launch bookkeeping (run two).  Phases 2 | 4 on
+   the item pass: the record pass W alone (the scan S of the previous launch stays valid).
    *first_kernel: 1 = spec (A), 2 = chained (C), 3 = chained LDS tiles (D), 4 = item pass (E). */
 int rtps_rx_debug_parse_phases(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len, const uint64_t* dgram_off,
                                const uint32_t* dgram_len, uint32_t n, const rtps_rx_out* out, uint32_t phases,
@@ -3016,6 +3356,13 @@ int rtps_rx_ingest_reset(rtps_rx_ctx* c) {
   (void)hipSetDevice(c->device);
   const int rc = c->ingest ? rtps_ingest_state_reset(c->ingest, c->stream) : RTPS_RX_OK;
   if (rc || !c->topics) return rc;
+  return rtps_topic_proxies_reset(c->topics, c->stream);
+}
+
+int rtps_rx_topic_reset(rtps_rx_ctx* c) {
+  if (!c) return RTPS_RX_EINVAL;
+  if (!c->topics) return RTPS_RX_OK;
+  (void)hipSetDevice(c->device);
   return rtps_topic_reset(c->topics, c->stream);
 }
 
@@ -3053,6 +3400,16 @@ int rtps_rx_debug_set_mixed_pass(rtps_rx_ctx* c, uint32_t pass) {
   if (!c || pass > 3u) return RTPS_RX_EINVAL;
   c->mixed_pass = pass;
   return RTPS_RX_OK;
+}
+
+/* test / measurement hook (not part of the public header): the item pass's record pass,
+   1 = rtps_parse_emit_kernel (a workgroup per tile), 2 = rtps_parse_emit2_kernel with a
+   workgroup per tile, 3 = rtps_parse_emit2_kernel persistent (the default).  Same results.
+   Returns the pass in effect (0 selects nothing new), or RTPS_RX_EINVAL. */
+int rtps_rx_debug_emit(rtps_rx_ctx* c, uint32_t emit) {
+  if (!c || emit > 5u) return RTPS_RX_EINVAL;
+  if (emit) c->emit = emit;
+  return (int)c->emit;
 }
 
 /* test hook (not part of the public header): the last chained launch's epoch, so

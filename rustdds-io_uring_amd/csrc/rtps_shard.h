@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "../../include/rtps_rx.h"
 
 constexpr uint32_t SHARD_MAX_RANKS = 64;
@@ -58,6 +60,16 @@ struct rtps_shard {
   uint64_t* o_n = nullptr;  // device u64
   void* cub_tmp = nullptr;
   size_t cub_bytes = 0;
+  // ---- writer -> owner table (rtps_rx_shard_set_owners) ----
+  uint32_t owner_mode = RTPS_OWNER_BALANCED;
+  std::vector<uint8_t> x_guid;     // the caller's extra writers (16 B each) and their weights
+  std::vector<uint64_t> x_weight;
+  uint64_t owner_version = ~0ull;  // the context's readers version the table follows (~0: build at the next pack)
+  std::vector<uint8_t> t_guid;     // host copy of the table: writer GUIDs and their owners
+  std::vector<uint32_t> t_owner;
+  uint32_t* d_okeys = nullptr;     // device: [ocap * 4] GUID words, open addressing by rt_hash16
+  uint32_t* d_oval = nullptr;      // [ocap] owner, 0xffffffff = empty slot
+  uint32_t ocap = 0;               // 0: no table (every writer by the GUID hash)
 };
 
 // grow-only device buffer (contents are not kept); false on allocation failure

@@ -39,10 +39,13 @@
 #include <hipcub/hipcub.hpp>
 #include <string.h>
 
+#include <algorithm>
 #include <new>
+#include <vector>
 
 #include "../../include/rtps_rx.h"
 #include "rtps_ctx.h"
+#include "rtps_readers.h"
 #include "rtps_shard.h"
 
 namespace {
@@ -80,8 +83,30 @@ __device__ __forceinline__ uint32_t item_bytes(uint32_t kind, const Blob& b) {
   return kind == RTPS_DATA ? 0u : 64u + round16(b.len);
 }
 
+// The writer -> owner table (rtps_rx_shard_set_owners): a writer in it goes to its owner,
+// any other by the GUID hash.
+struct OwnerDev {
+  const uint32_t* keys;  // nullptr: no table
+  const uint32_t* val;
+  uint32_t mask;
+};
+__device__ __forceinline__ uint32_t owner_of_writer(const OwnerDev& t, uint32_t a, uint32_t b, uint32_t c, uint32_t d,
+                                                    uint32_t n_dest) {
+  if (t.keys) {
+    uint32_t i = rt_hash16(a, b, c, d) & t.mask;
+    for (uint32_t probe = 0; probe <= t.mask; ++probe) {
+      const uint32_t v = t.val[i];
+      if (v == NONE) break;
+      const uint4 k = *reinterpret_cast<const uint4*>(t.keys + 4u * i);
+      if (k.x == a && k.y == b && k.z == c && k.w == d) return v;
+      i = (i + 1u) & t.mask;
+    }
+  }
+  return owner_hash(a, b, c, d) % n_dest;
+}
+
 // Destination of a record (NONE: not an item) and its blob
-__device__ __forceinline__ uint32_t item_of(const uint32_t* w, uint32_t n_dest, Blob& b) {
+__device__ __forceinline__ uint32_t item_of(const uint32_t* w, const OwnerDev& ot, uint32_t n_dest, Blob& b) {
   const uint32_t kind = (w[1] >> 16) & 0xffu;
   const uint32_t route = (w[7] >> 16) & 0xffu;
   const bool writer = kind == RTPS_DATA || kind == RTPS_DATA_FRAG || kind == RTPS_HEARTBEAT || kind == RTPS_GAP ||
@@ -89,7 +114,7 @@ __device__ __forceinline__ uint32_t item_of(const uint32_t* w, uint32_t n_dest, 
   b = Blob{0u, 0u};
   if (!writer || !(route & RTPS_ROUTE_PASS)) return NONE;
   b = blob_of(w);
-  return owner_hash(w[2], w[3], w[4], w[5]) % n_dest;
+  return owner_of_writer(ot, w[2], w[3], w[4], w[5], n_dest);
 }
 
 __device__ __forceinline__ void load_record(const rtps_record* r, uint32_t* w) {
@@ -143,8 +168,8 @@ __device__ __forceinline__ uint64_t wave_incl64(uint64_t x, uint32_t lane) {
 }
 
 // 1. per tile t and destination d: hist[2 (t n + d)] = items, [+1] = blob bytes
-__global__ __launch_bounds__(ST) void shard_hist(const rtps_record* recs, const uint64_t* n_rec, uint32_t n_dest,
-                                                 uint32_t* hist) {
+__global__ __launch_bounds__(ST) void shard_hist(const rtps_record* recs, const uint64_t* n_rec, OwnerDev ot,
+                                                 uint32_t n_dest, uint32_t* hist) {
   __shared__ uint32_t h[2 * SHARD_MAX_RANKS];
   if (threadIdx.x < 2 * n_dest) h[threadIdx.x] = 0;
   __syncthreads();
@@ -153,7 +178,7 @@ __global__ __launch_bounds__(ST) void shard_hist(const rtps_record* recs, const 
     uint32_t w[16];
     load_record(recs + i, w);
     Blob b;
-    const uint32_t o = item_of(w, n_dest, b);
+    const uint32_t o = item_of(w, ot, n_dest, b);
     if (o != NONE) {
       atomicAdd(&h[2 * o], 1u);
       const uint32_t ib = item_bytes((w[1] >> 16) & 0xffu, b);
@@ -199,6 +224,7 @@ struct PackArgs {
   const uint64_t* dgram_off;
   const rtps_record* recs;
   const uint64_t* n_rec;
+  OwnerDev ot;
   uint32_t n_dest;
   uint64_t cap, bcap;
   const uint64_t* hscan;
@@ -230,7 +256,7 @@ __global__ __launch_bounds__(ST) void shard_scatter(PackArgs a) {
   Blob b{0u, 0u};
   if (i < *a.n_rec) {
     load_record(a.recs + i, w);
-    o = item_of(w, n, b);
+    o = item_of(w, a.ot, n, b);
   }
   const uint32_t kind = o != NONE ? (w[1] >> 16) & 0xffu : 0u;
   const uint32_t size = o != NONE ? item_bytes(kind, b) : 0u;
@@ -464,7 +490,7 @@ int rtps_rx_shard_destroy(rtps_shard* s) {
   (void)hipDeviceSynchronize();
   void* dev[] = {s->s_slots, s->s_blob, s->s_counts, s->s_spill, s->s_bspill, s->hist, s->hscan, s->r_slots,
                  s->r_blob, s->r_counts, s->r_spill, s->r_bspill, s->o_rec, s->o_off, s->o_origin, s->o_size,
-                 s->o_boff, s->o_arena, s->o_n, s->cub_tmp, s->o_item};
+                 s->o_boff, s->o_arena, s->o_n, s->cub_tmp, s->o_item, s->d_okeys, s->d_oval};
   for (void* p : dev)
     if (p) (void)hipFree(p);
   if (s->h_send) (void)hipHostFree(s->h_send);
@@ -476,11 +502,142 @@ int rtps_rx_shard_destroy(rtps_shard* s) {
   return RTPS_RX_OK;
 }
 
+int rtps_rx_owner_assign(const uint8_t* writers, const uint64_t* weights, const uint32_t* groups, uint32_t n,
+                         uint32_t n_ranks, uint32_t* owners) {
+  if ((n && (!writers || !owners)) || n_ranks < 1) return RTPS_RX_EINVAL;
+  for (uint32_t w = 0; w < n; ++w)
+    if (groups && groups[w] >= n) return RTPS_RX_EINVAL;
+  // groups: total weight, smallest member GUID (the tie-break that makes the deal order-free)
+  std::vector<uint32_t> gid(n), rep;  // writer -> dense group, group -> its smallest-GUID writer
+  std::vector<uint64_t> gw;
+  std::vector<uint32_t> dense(n, NONE);
+  for (uint32_t w = 0; w < n; ++w) {
+    const uint32_t g = groups ? groups[w] : w;
+    if (dense[g] == NONE) { dense[g] = (uint32_t)rep.size(); rep.push_back(w); gw.push_back(0); }
+    const uint32_t k = dense[g];
+    gid[w] = k;
+    gw[k] += weights ? weights[w] : 1u;
+    if (memcmp(writers + 16ull * w, writers + 16ull * rep[k], 16) < 0) rep[k] = w;
+  }
+  std::vector<uint32_t> order(rep.size());
+  for (uint32_t k = 0; k < order.size(); ++k) order[k] = k;
+  std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
+    if (gw[x] != gw[y]) return gw[x] > gw[y];
+    return memcmp(writers + 16ull * rep[x], writers + 16ull * rep[y], 16) < 0;
+  });
+  // largest first, each to the least-loaded owner (ties: the lowest rank)
+  std::vector<uint64_t> load(n_ranks, 0);
+  std::vector<uint32_t> owner_of(rep.size());
+  for (uint32_t k : order) {
+    uint32_t best = 0;
+    for (uint32_t r = 1; r < n_ranks; ++r)
+      if (load[r] < load[best]) best = r;
+    owner_of[k] = best;
+    load[best] += gw[k];
+  }
+  for (uint32_t w = 0; w < n; ++w) owners[w] = owner_of[gid[w]];
+  return RTPS_RX_OK;
+}
+
+// (re)build the owner table from the context's readers (and topics) and the caller's writers
+static int owner_table_build(rtps_shard* s) {
+  s->owner_version = rtps_ctx_readers_version(s->ctx);
+  s->t_guid.clear();
+  s->t_owner.clear();
+  if (s->owner_mode != RTPS_OWNER_HASH) {
+    std::vector<uint8_t> g;
+    std::vector<uint32_t> grp;
+    rtps_ctx_owner_writers(s->ctx, s->owner_mode == RTPS_OWNER_TOPIC, g, grp);
+    std::vector<uint64_t> wt(grp.size(), 1u);
+    for (size_t x = 0; x < s->x_weight.size(); ++x) {  // the caller's writers: weight known ones, add the rest
+      const uint8_t* q = s->x_guid.data() + 16 * x;
+      size_t w = 0;
+      while (w < grp.size() && memcmp(g.data() + 16 * w, q, 16) != 0) ++w;
+      if (w == grp.size()) {
+        g.insert(g.end(), q, q + 16);
+        grp.push_back((uint32_t)w);
+        wt.push_back(0);
+      }
+      wt[w] = s->x_weight[x];
+    }
+    std::vector<uint32_t> own(grp.size());
+    const int rc = rtps_rx_owner_assign(g.data(), wt.data(), grp.data(), (uint32_t)grp.size(), s->n_ranks, own.data());
+    if (rc) return rc;
+    s->t_guid.swap(g);
+    s->t_owner.swap(own);
+  }
+  const uint32_t n = (uint32_t)s->t_owner.size();
+  uint32_t cap = 0;
+  if (n) {
+    cap = 16;
+    while (cap < 4ull * n) cap <<= 1;
+  }
+  std::vector<uint32_t> keys(4ull * cap, 0u), val(cap, NONE);
+  for (uint32_t w = 0; w < n; ++w) {
+    uint32_t k[4];
+    memcpy(k, s->t_guid.data() + 16ull * w, 16);
+    uint32_t i = rt_hash16(k[0], k[1], k[2], k[3]) & (cap - 1);
+    while (val[i] != NONE) i = (i + 1) & (cap - 1);
+    memcpy(&keys[4ull * i], k, 16);
+    val[i] = s->t_owner[w];
+  }
+  hipStream_t st = rtps_ctx_stream(s->ctx);
+  if (hipStreamSynchronize(st) != hipSuccess) return RTPS_RX_EHIP;  // an earlier pack may read the old table
+  if (cap > s->ocap) {
+    (void)hipFree(s->d_okeys);
+    (void)hipFree(s->d_oval);
+    s->d_okeys = nullptr;
+    s->d_oval = nullptr;
+    s->ocap = 0;
+    if (hipMalloc(&s->d_okeys, 16ull * cap) != hipSuccess || hipMalloc(&s->d_oval, 4ull * cap) != hipSuccess)
+      return RTPS_RX_ENOMEM;
+  }
+  s->ocap = cap;
+  if (cap && (hipMemcpy(s->d_okeys, keys.data(), 16ull * cap, hipMemcpyHostToDevice) != hipSuccess ||
+              hipMemcpy(s->d_oval, val.data(), 4ull * cap, hipMemcpyHostToDevice) != hipSuccess))
+    return RTPS_RX_EHIP;
+  return RTPS_RX_OK;
+}
+
+int rtps_rx_shard_set_owners(rtps_shard* s, uint32_t mode, const uint8_t* guids, const uint64_t* weights,
+                             uint32_t n) {
+  if (!s || mode > RTPS_OWNER_TOPIC || (n && (!guids || !weights))) return RTPS_RX_EINVAL;
+  (void)hipSetDevice(s->device);
+  s->owner_mode = mode;
+  s->x_guid.assign(guids, guids + 16ull * n);
+  s->x_weight.assign(weights, weights + n);
+  return owner_table_build(s);
+}
+
+int rtps_rx_shard_owner(rtps_shard* s, const uint8_t guid[16]) {
+  if (!s || !guid) return RTPS_RX_EINVAL;
+  if (s->owner_mode != RTPS_OWNER_HASH && s->owner_version != rtps_ctx_readers_version(s->ctx)) {
+    (void)hipSetDevice(s->device);
+    const int rc = owner_table_build(s);
+    if (rc) return rc;
+  }
+  for (size_t w = 0; w < s->t_owner.size(); ++w)
+    if (memcmp(s->t_guid.data() + 16 * w, guid, 16) == 0) return (int)s->t_owner[w];
+  uint32_t k[4];
+  memcpy(k, guid, 16);
+  uint32_t h = 0x811c9dc5u;  // owner_hash on the host
+  for (int j = 0; j < 4; ++j) h = (h ^ k[j]) * 0x01000193u;
+  h ^= h >> 16; h *= 0x85ebca6bu;
+  h ^= h >> 13; h *= 0xc2b2ae35u;
+  h ^= h >> 16;
+  return (int)(h % s->n_ranks);
+}
+
 int rtps_rx_shard_pack(rtps_shard* s, const uint8_t* arena, uint64_t arena_len, const uint64_t* dgram_off,
                        const rtps_record* records, const uint64_t* n_records, uint64_t max_records) {
   if (!s || !records || !n_records || (max_records && (!arena || !dgram_off))) return RTPS_RX_EINVAL;
   (void)hipSetDevice(s->device);
   hipStream_t st = rtps_ctx_stream(s->ctx);
+  if (s->owner_mode != RTPS_OWNER_HASH && s->owner_version != rtps_ctx_readers_version(s->ctx)) {
+    const int rc = owner_table_build(s);  // the readers changed: the table follows them
+    if (rc) return rc;
+  }
+  const OwnerDev ot{s->ocap ? s->d_okeys : nullptr, s->d_oval, s->ocap ? s->ocap - 1u : 0u};
   const uint32_t n = s->n_ranks;
   const uint64_t tiles = (max_records + ST - 1) / ST;
   if (tiles > 0xffffffffull) return RTPS_RX_ETOOBIG;
@@ -507,9 +664,9 @@ int rtps_rx_shard_pack(rtps_shard* s, const uint8_t* arena, uint64_t arena_len, 
   if (tiles == 0) {
     if (hipMemsetAsync(s->s_counts, 0, n * sizeof(rtps_shard_counts), st) != hipSuccess) return RTPS_RX_EHIP;
   } else {
-    hipLaunchKernelGGL(shard_hist, dim3((uint32_t)tiles), dim3(ST), 0, st, records, n_records, n, s->hist);
+    hipLaunchKernelGGL(shard_hist, dim3((uint32_t)tiles), dim3(ST), 0, st, records, n_records, ot, n, s->hist);
     hipLaunchKernelGGL(shard_scan, dim3(n), dim3(ST), 0, st, s->hist, tiles, n, s->hscan, s->s_counts);
-    PackArgs a{arena, arena_len, dgram_off, records, n_records, n, s->cap, s->bcap, s->hscan, s->s_counts,
+    PackArgs a{arena, arena_len, dgram_off, records, n_records, ot, n, s->cap, s->bcap, s->hscan, s->s_counts,
                s->s_slots, s->s_blob, s->s_spill, s->s_bspill};
     hipLaunchKernelGGL(shard_scatter, dim3((uint32_t)tiles), dim3(ST), 0, st, a);
   }

@@ -20,10 +20,16 @@ int rtps_topic_configure(TopicState* s, const rtps_topic* topics, uint32_t n_top
 // topic checks each delivery against its live changes until those have aged out.
 int rtps_topic_readers_changed(TopicState* s, const uint32_t* set_first, const rtps_target* ent, uint32_t n_sets,
                                hipStream_t st);
-// Every topic cache emptied (rtps_rx_ingest_reset).
+// Every topic cache emptied (rtps_rx_topic_reset).
 int rtps_topic_reset(TopicState* s, hipStream_t st);
+// The writer proxies were reset (rtps_rx_ingest_reset): the caches keep their changes, and
+// fresh proxies may re-accept what a topic still holds, so every topic checks each delivery
+// against its live changes until those have aged out (as after rtps_topic_readers_changed).
+int rtps_topic_proxies_reset(TopicState* s, hipStream_t st);
 // DDSCache::garbage_collect.
 int rtps_topic_gc(TopicState* s, hipStream_t st);
+// The topic cache a reader slot's changes go to (its configured topic, else its own).
+uint32_t rtps_topic_of_slot(const TopicState* s, uint16_t slot);
 // TopicCache::add_change for every delivery of the batch, in order: sets or clears
 // RTPS_DELIVERY_CACHED in del[k].flags (asynchronous).
 int rtps_topic_apply(TopicState* s, hipStream_t st, const rtps_record* recs, const uint64_t* n_records,

@@ -615,6 +615,14 @@ int rtps_topic_reset(TopicState* s, hipStream_t st) {
   return ok ? RTPS_RX_OK : RTPS_RX_EHIP;
 }
 
+int rtps_topic_proxies_reset(TopicState* s, hipStream_t st) {
+  if (!s->I) return RTPS_RX_OK;
+  hipLaunchKernelGGL(tc_until, dim3((s->nt + TT - 1) / TT), dim3(TT), 0, st, s->nt, s->I, s->until);
+  return hipGetLastError() == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP;
+}
+
+uint32_t rtps_topic_of_slot(const TopicState* s, uint16_t slot) { return tid_of(s, slot); }
+
 int rtps_topic_gc(TopicState* s, hipStream_t st) {
   if (!s->I) return RTPS_RX_OK;
   hipLaunchKernelGGL(tc_gc, dim3((s->nt + TT - 1) / TT), dim3(TT), 0, st, s->nt, s->K, s->I, s->E);

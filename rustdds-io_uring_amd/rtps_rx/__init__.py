@@ -77,7 +77,8 @@ EXPORTS = ["rtps_rx_create", "rtps_rx_destroy", "rtps_rx_set_stream", "rtps_rx_s
            "rtps_rx_frag_set_clock", "rtps_rx_frag_gc",
            "rtps_rx_bucket_descriptors", "rtps_rx_ingest", "rtps_rx_ingest_reset", "rtps_udp_open", "rtps_udp_close",
            "rtps_udp_port", "rtps_udp_backend", "rtps_udp_recv_batch", "rtps_udp_release", "rtps_udp_send_batch",
-           "rtps_rx_pump", "rtps_rx_set_topics", "rtps_rx_topic_gc", "rtps_rx_cdr_decode_list"]
+           "rtps_rx_pump", "rtps_rx_set_topics", "rtps_rx_topic_gc", "rtps_rx_cdr_decode_list",
+           "rtps_rx_topic_reset"]
 
 
 def lib():
@@ -339,6 +340,18 @@ class MessageReceiver:
         fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
         _check(fn(self._h, int(pass_)))
 
+    def debug_emit(self, emit=0):
+        """The item pass's record pass (same results): 1 = rtps_parse_emit_kernel, 2 =
+        rtps_parse_emit2_kernel one workgroup per tile, 3 = rtps_parse_emit2_kernel persistent
+        (the default); 0 selects nothing.  Returns the pass in effect."""
+        fn = lib().rtps_rx_debug_emit
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+        fn.restype = ctypes.c_int
+        r = fn(self._h, int(emit))
+        if r < 0:
+            _check(r)
+        return r
+
     def generate(self, workload, arena, off, lens, n, seed=SEED, first_idx=0, n_writers=16):
         """Fill device arena with datagrams [first_idx, first_idx+n) of a synthetic workload."""
         _check(lib().rtps_rx_generate(self._h, workload, seed, first_idx, n_writers, arena.data_ptr(),
@@ -542,7 +555,12 @@ class MessageReceiver:
                                     (INGEST_TOPIC_CACHE if topic_cache else 0), ctypes.byref(o)))
 
     def ingest_reset(self):
+        """Every writer proxy starts afresh; the topic caches keep their changes."""
         _check(lib().rtps_rx_ingest_reset(self._h))
+
+    def topic_reset(self):
+        """Empty every topic cache (the proxies keep their state)."""
+        _check(lib().rtps_rx_topic_reset(self._h))
 
     def ingest_batch(self, arena_np, off_np, len_np, n_proxies, frag=False, best_effort=False, topic_cache=False):
         """Parse (+ reassemble) + ingest host arrays -> (BatchResult, accept u8[m], deliveries

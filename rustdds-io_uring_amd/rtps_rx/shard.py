@@ -49,12 +49,25 @@ def _forget_comm(comm):
             del _COMMS[k]
 
 
-def _check_comm(rc, comm):
-    """_check for the calls that may abort the communicator."""
+def _check_comm(rc, owner):
+    """_check for the calls that may abort the communicator of `owner` (an Exchange or an
+    OwnerShard): on RTPS_RX_EABORTED the library has freed it, so the owner forgets it too and
+    every later exchange call on that object raises instead of passing a freed handle."""
     from . import _check, RTPS_RX_EABORTED
     if rc == RTPS_RX_EABORTED:
-        _forget_comm(comm)
+        _forget_comm(owner.comm)
+        owner.comm = None
+        owner.comm_aborted = True
     _check(rc)
+
+
+def _live_comm(owner):
+    """The owner's communicator, or an error when an earlier call aborted it."""
+    from . import RtpsRxError, RTPS_RX_EABORTED
+    if getattr(owner, "comm_aborted", False):
+        raise RtpsRxError("the RCCL communicator was aborted by an earlier failure; create a new exchange object",
+                          RTPS_RX_EABORTED)
+    return owner.comm
 
 
 def destroy_comms():
@@ -189,10 +202,10 @@ class Exchange:
         L = lib()
         L.rtps_rx_exchange.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p,
                                                                ctypes.c_void_p]
-        _check_comm(L.rtps_rx_exchange(self.rx._h, self.comm, ctypes.c_void_p(self.xstream.cuda_stream),
+        _check_comm(L.rtps_rx_exchange(self.rx._h, _live_comm(self), ctypes.c_void_p(self.xstream.cuda_stream),
                                        self.bucketed.data_ptr(), self.counts.data_ptr(), self.cap,
                                        ITEM_BYTES[self.item], self.received.data_ptr(), self.recv_counts.data_ptr()),
-                    self.comm)
+                    self)
         done = torch.cuda.Event()
         done.record(self.xstream)
         return [_StreamWork(done, self.device)]
@@ -323,12 +336,33 @@ def shard_lib():
         L.rtps_rx_shard_unpack.argtypes = [P, ctypes.POINTER(_OwnerBatch)]
         L.rtps_rx_shard_buffers.argtypes = [P, ctypes.POINTER(_ShardBuffers)]
         L.rtps_rx_shard_reserve_spill.argtypes = [P, U64, U64]
+        L.rtps_rx_shard_set_owners.argtypes = [P, U32, P, P, U32]
+        L.rtps_rx_shard_owner.argtypes = [P, P]
+        L.rtps_rx_owner_assign.argtypes = [P, P, P, U32, U32, P]
         for f in ("rtps_rx_shard_create", "rtps_rx_shard_destroy", "rtps_rx_shard_pack", "rtps_rx_shard_exchange",
                   "rtps_rx_shard_finish", "rtps_rx_shard_unpack", "rtps_rx_shard_buffers",
-                  "rtps_rx_shard_reserve_spill"):
+                  "rtps_rx_shard_reserve_spill", "rtps_rx_shard_set_owners", "rtps_rx_shard_owner",
+                  "rtps_rx_owner_assign"):
             getattr(L, f).restype = ctypes.c_int
         L._shard_bound = True
     return L
+
+
+OWNER_BALANCED, OWNER_HASH, OWNER_TOPIC = 0, 1, 2  # rtps_rx_shard_set_owners modes
+
+
+def owner_assign(writers, n_ranks, weights=None, groups=None):
+    """rtps_rx_owner_assign (host, no GPU): writers = list of 16-byte GUIDs -> owner rank of each.
+    Groups (list of group ids < n, optional) share an owner; weights (optional) per writer."""
+    from . import _check
+    n = len(writers)
+    w = _np.frombuffer(b"".join(bytes(g) for g in writers), dtype=_np.uint8) if n else _np.zeros(16, _np.uint8)
+    wt = None if weights is None else _np.ascontiguousarray(weights, dtype=_np.uint64)
+    gr = None if groups is None else _np.ascontiguousarray(groups, dtype=_np.uint32)
+    out = _np.zeros(max(n, 1), dtype=_np.uint32)
+    _check(shard_lib().rtps_rx_owner_assign(w.ctypes.data, None if wt is None else wt.ctypes.data,
+                                            None if gr is None else gr.ctypes.data, n, n_ranks, out.ctypes.data))
+    return out[:n]
 
 
 def spill_plan(send_counts, recv_counts):
@@ -386,6 +420,25 @@ class OwnerShard:
         _check(shard_lib().rtps_rx_shard_buffers(self._h, ctypes.byref(b)))
         return b
 
+    def set_owners(self, mode=OWNER_BALANCED, weights=None):
+        """rtps_rx_shard_set_owners: the writer -> owner deal (OWNER_BALANCED, OWNER_TOPIC or
+        OWNER_HASH); weights: {16-byte writer GUID: weight} (optional)."""
+        from . import _check
+        weights = weights or {}
+        g = _np.frombuffer(b"".join(bytes(k) for k in weights), dtype=_np.uint8) if weights else None
+        w = _np.array(list(weights.values()), dtype=_np.uint64) if weights else None
+        _check(shard_lib().rtps_rx_shard_set_owners(self._h, mode, None if g is None else g.ctypes.data,
+                                                    None if w is None else w.ctypes.data, len(weights)))
+
+    def owner_of(self, guid):
+        """The owner rank of a 16-byte writer GUID under the current deal."""
+        from . import _check
+        buf = (ctypes.c_uint8 * 16).from_buffer_copy(bytes(guid))
+        r = shard_lib().rtps_rx_shard_owner(self._h, buf)
+        if r < 0:
+            _check(r)
+        return r
+
     def pack(self, arena, off, outs):
         """Source side: this rank's parse output into the slots and the spill (asynchronous)."""
         from . import _check
@@ -403,15 +456,15 @@ class OwnerShard:
         """Round 0 (RCCL: asynchronous on the exchange stream; gloo: the whole protocol)."""
         if self.host_collectives:
             return self._exchange_host()
-        _check_comm(shard_lib().rtps_rx_shard_exchange(self._h, self.comm, ctypes.c_void_p(self.xstream.cuda_stream)),
-                    self.comm)
+        _check_comm(shard_lib().rtps_rx_shard_exchange(self._h, _live_comm(self),
+                                                       ctypes.c_void_p(self.xstream.cuda_stream)), self)
 
     def finish(self):
         """Waits for round 0's counts; moves any spill (RCCL).  No-op after a gloo exchange."""
         if self.host_collectives:
             return
-        _check_comm(shard_lib().rtps_rx_shard_finish(self._h, self.comm, ctypes.c_void_p(self.xstream.cuda_stream)),
-                    self.comm)
+        _check_comm(shard_lib().rtps_rx_shard_finish(self._h, _live_comm(self),
+                                                     ctypes.c_void_p(self.xstream.cuda_stream)), self)
 
     def unpack(self):
         """Owner side -> OwnerBatch (host sync on the received counts)."""

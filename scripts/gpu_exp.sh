@@ -1,0 +1,52 @@
+#!/bin/bash
+# Parametrised GPU steps (round 5): scripts/gpu_exp.sh STEP [STEP ...], each step under its own
+# time limit, stopping at the first failure.  Outputs under gpurun_out/exp/.
+#   parity_mixed   the mixed-pass parity subset of tests/test_gpu_parity.py
+#   c3_emit        C3 bench lines for each record pass (RTPS_RX_EMIT=1/2/3)
+#   kstats_C3      rocprofv3 kernel-trace stats of the C3 bench
+#   gpu_tests      the whole -m gpu suite
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; R=$(pwd); O=$R/gpurun_out/exp; mkdir -p $O; export TMPDIR=/tmp
+PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
+for step in "$@"; do
+  echo "== $step $(date +%T)"
+  case $step in
+    parity_mixed)
+      timeout -k 10 600 $PYT tests/test_gpu_parity.py -k "mixed or chained_launch or lds_tile or soup or edge or reader_sets or full_size or launch_choice or spec_hint or golden or record_passes" > $O/parity_mixed.log 2>&1 \
+        || { tail -30 $O/parity_mixed.log; exit 3; }
+      tail -2 $O/parity_mixed.log ;;
+    c3_emit)
+      for e in ${EMITS:-1 2 3 4 5}; do
+        RTPS_RX_EMIT=$e timeout -k 10 300 python bench.py --workload C3 --steps 20 --warmup 5 --no-c1 --no-e2e --no-cpu-baseline --no-ingest --no-cdr > $O/c3_emit$e.json 2> $O/c3_emit$e.err || { tail -5 $O/c3_emit$e.err; exit 4; }
+        python - $O/c3_emit$e.json $e <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+print("emit", sys.argv[2], "ms_per_step", d["ms_per_step"], {k: v for k, v in d.get("roofline", {}).items() if k in ("kernel", "achieved", "frac")},
+      {k: d.get(k) for k in ("item_kernel_ms", "scan_plus_emit_ms")}, d.get("parse_kernels", ""))
+PY
+      done ;;
+    c3_var)  # the in-tree library, then every tuning variant under rustdds-io_uring_amd/variants/, RTPS_RX_EMIT as set
+      for lib in $R/rustdds-io_uring_amd/librtps_rx.so $R/rustdds-io_uring_amd/variants/librtps_rx_*.so; do
+        v=$(basename $lib .so)
+        RTPS_RX_LIB=$lib timeout -k 10 300 python bench.py --workload C3 --steps 20 --warmup 5 --no-c1 --no-e2e --no-cpu-baseline --no-ingest --no-cdr > $O/c3_$v.json 2> $O/c3_$v.err || { tail -5 $O/c3_$v.err; exit 4; }
+        python - $O/c3_$v.json $v <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); r = d["roofline"]
+print(sys.argv[2], "step", round(d["ms_per_step"] * 1e3, 1), "us", {k: round(r[k] * 1e3, 1) for k in ("item_kernel_ms", "emit_kernel_ms", "scan_ms") if k in r})
+PY
+      done ;;
+    kstats_C3)
+      cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kstats_C3 -o run --output-format csv -- python3 $R/bench.py --workload C3 --steps 20 --warmup 5 --no-cpu-baseline --no-e2e --no-c1 --no-ingest --no-cdr > $O/kstats_C3.log 2>&1 || { tail -5 $O/kstats_C3.log; exit 6; }
+      cd $R; python scripts/prof_table.py $(find $O/kstats_C3 -name "*kernel_stats.csv") ;;
+    shard)
+      timeout -k 10 900 $PYT tests/test_shard_gpu.py > $O/shard.log 2>&1 || { grep -E "FAILED|Error" $O/shard.log | head; tail -30 $O/shard.log; exit 7; }
+      tail -2 $O/shard.log ;;
+    topic)
+      timeout -k 10 900 $PYT tests/test_topic_gpu.py tests/test_cdr_gpu.py > $O/topic.log 2>&1 || { grep -E "FAILED|Error" $O/topic.log | head; tail -30 $O/topic.log; exit 8; }
+      tail -2 $O/topic.log ;;
+    gpu_tests)
+      timeout -k 10 1000 $PYT tests -m gpu > $O/gpu_tests.log 2>&1 || { grep -E "FAILED|Error" $O/gpu_tests.log | head; tail -5 $O/gpu_tests.log; exit 5; }
+      tail -2 $O/gpu_tests.log ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo done

@@ -23,7 +23,7 @@ import torch.distributed as dist
 import oracle
 import rtps_rx
 from rtps_rx.records import DELIVERY_DTYPE, WRITER_KINDS, pack_match_table, max_records
-from rtps_rx.shard import OwnerShard, owner_hash_words, destroy_comms
+from rtps_rx.shard import OwnerShard, destroy_comms
 
 backend = sys.argv[1] if len(sys.argv) > 1 else "gloo"
 c4 = "c4" in sys.argv[2:]
@@ -90,13 +90,23 @@ spilled = int(sum(int(c["n"] - c["cut"]) for c in sh.counts("recv")))
 _, recs, _, _ = oracle.parse(wa, wo, wlen, match_table=tbl, threads=8)
 samples = oracle.FragAssembler().batch_readers(wa, wo, recs, tbl)[0]
 _, odels, oack = oracle.HistoryIngest(tbl).batch(wa, wo, recs, samples)
-mine = np.array([owner_hash_words(r.view(np.uint32)[2:6]) % world == rank for r in recs.view(np.uint8).reshape(-1, 64)])
+# the shard's owner of each writer (its owner table: the default RTPS_OWNER_BALANCED deal)
+own = {}
+
+
+def owner(g):
+    g = bytes(g)
+    if g not in own:
+        own[g] = sh.owner_of(g)
+    return own[g]
+
+
+mine = np.array([owner(r[8:24]) == rank for r in recs.view(np.uint8).reshape(-1, 64)])
 # origin names (source rank, record index in that rank's parse); rank r parsed datagrams [r n, (r+1) n)
 first_rec = np.searchsorted(recs["dgram_idx"], np.arange(world) * n)
 got = [(int(first_rec[int(orank[j])]) + int(osrc[j]), int(d["reader_slot"])) for d in dels for j in [int(d["rec_idx"])]]
 exp = [(int(d["rec_idx"]), int(d["reader_slot"])) for d in odels if mine[int(d["rec_idx"])]]
-owned_proxy = np.array([owner_hash_words(np.frombuffer(bytes(t["writer_guid"]), np.uint32)) % world == rank
-                        for t in tbl])
+owned_proxy = np.array([owner(t["writer_guid"]) == rank for t in tbl])
 ok = got == exp and len(exp) > 0 and np.array_equal(ack[owned_proxy], oack[owned_proxy]) and \
     (ack[~owned_proxy] == 1).all() and (spilled > 0) == (small and world > 0)
 via = "library RCCL rounds" if sh.comm is not None else "torch.distributed " + backend

@@ -22,7 +22,7 @@ KEYS = (("ceil_kernel<1>", "ceil_read_only"), ("ceil_kernel<0>", "ceil_rw"), ("c
         ("ceil_kernel<3>", "ceil_rw_lds"), ("rtps_parse_spec_kernel", "parse_spec"),
         ("rtps_parse_chain_kernel", "parse_chain"), ("rtps_parse_lds_kernel", "parse_lds"),
         ("rtps_parse_fix_kernel", "parse_fix"), ("rtps_parse_item_kernel", "parse_item"),
-        ("rtps_parse_emit_kernel", "parse_emit"), ("rtps_parse_scan_kernel", "parse_scan"),
+        ("rtps_parse_emit_kernel", "parse_emit"), ("rtps_parse_emit2_kernel", "parse_emit2"), ("rtps_parse_scan_kernel", "parse_scan"),
         ("rtps_parse_rslab_kernel", "parse_rslab"), ("rtps_parse_rcopy_kernel", "parse_rcopy"))
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
 grid = collections.defaultdict(list)

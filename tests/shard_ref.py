@@ -79,10 +79,22 @@ def _r16(x):
     return (x + 15) // 16 * 16
 
 
-def shard_items(recs, world):
-    """Owner of every record that is an item (writer kinds with ROUTE_PASS), else -1."""
+def balanced_owner_table(guids, world):
+    """The shard's default owner table (RTPS_OWNER_BALANCED): the writer GUIDs of the context's
+    proxies dealt by rtps_rx_owner_assign -> {16-byte GUID: owner}."""
+    from rtps_rx.shard import owner_assign
+    guids = sorted(set(bytes(g) for g in guids))
+    return dict(zip(guids, (int(x) for x in owner_assign(guids, world))))
+
+
+def shard_items(recs, world, table=None):
+    """Owner of every record that is an item (writer kinds with ROUTE_PASS), else -1: the
+    writer's owner in `table` ({GUID: owner}, the shard's owner table), else the GUID hash."""
     from rtps_rx.records import ROUTE_PASS
     o = owner_np(recs, world)
+    if table:
+        g = recs.view(np.uint8).reshape(-1, 64)[:, 8:24]
+        o = np.array([table.get(bytes(x), int(h)) for x, h in zip(g, o)], dtype=np.int64)
     writer = np.isin(recs["kind"], WRITER_KINDS) & ((recs["route"] & ROUTE_PASS) != 0)
     return np.where(writer, o, -1)
 
@@ -114,9 +126,9 @@ def _item_and_blob(arena, offs, r, i):
     return it, b
 
 
-def shard_pack_np(arena, offs, recs, world, cap, bcap):
+def shard_pack_np(arena, offs, recs, world, cap, bcap, table=None):
     """Per destination d: dict(counts, slot_items, slot_blob (bcap bytes), spill_items, spill_blob)."""
-    o = shard_items(recs, world)
+    o = shard_items(recs, world, table)
     out = []
     for d in range(world):
         idx = np.nonzero(o == d)[0]

@@ -156,3 +156,26 @@ def test_list_decode_parity(rx, wl, t):
         exp_rows = np.zeros((len(lst), typ.row_bytes), np.uint8)
         exp_rows[ok] = o_rows[lst[ok]]
         assert np.array_equal(rows, exp_rows), f"list stride {stride}: rows differ"
+
+
+def test_list_decode_without_records(rx):
+    """list entries when the batch has no decodable records (max_records = 0, or
+    *n_records = 0) are RTPS_CDR_NOT_DATA with zero rows, and the kernel loads no record."""
+    typ = cdr.ShapeType
+    arena, off, ln = _device_gen(rx, 3, 600)
+    dev = torch.device("cuda", 0)
+    a_t = torch.from_numpy(arena).to(dev)
+    off_t = torch.from_numpy(off.view(np.int64)).to(dev)
+    ln_t = torch.from_numpy(ln.view(np.int32)).to(dev)
+    outs = rx.alloc_outputs(len(ln), 4 * len(ln))
+    rx.parse_batch_device(a_t, off_t, ln_t, len(ln), outs)
+    lst = torch.arange(0, 64, dtype=torch.int32, device=dev)
+    n_t = torch.tensor([64], dtype=torch.int64, device=dev)
+    for label, o in (("max_records 0", dict(outs, max_records=0)),
+                     ("n_records 0", dict(outs, n_records=torch.zeros(1, dtype=torch.int64, device=dev)))):
+        rows, rst = rx.alloc_rows(typ, 64)
+        rows.fill_(0x5A)
+        rx.cdr_decode_list(typ, a_t, off_t, o, lst, 4, n_t, 64, rows, rst)
+        torch.cuda.synchronize()
+        assert (rst.cpu().numpy()[:64] == cdr.CDR_NOT_DATA).all(), label
+        assert not rows.cpu().numpy().view(np.uint8).reshape(64, -1)[:64].any(), label

@@ -453,6 +453,33 @@ def test_mixed_pass_malformed_inputs(rx, mp, mname):
         rx.set_spec_hint(1)
 
 
+@pytest.mark.parametrize("emit", [1, 2, 3, 4, 5])
+def test_record_passes_agree(rx, emit):
+    """Every record pass of the item pass (rtps_parse_emit_kernel: a workgroup per tile;
+    rtps_parse_emit2_kernel in slab or record order, a workgroup per tile or persistent),
+    bit-exact on mixed traffic with a reader table, the malformed soup (items of datagrams
+    dropped later in their walk), misaligned packing and a wave whose items overflow its
+    slab (1000 records in one datagram: that wave is walked)."""
+    import ingest_ref as R
+    rx.set_spec_hint(0)
+    rx.debug_set_mixed_pass(2)
+    prev = rx.debug_emit(emit)
+    try:
+        a, o, l = oracle.gen(oracle.WL_C3, 70000, first_idx=99)
+        _parity(rx, a, o, l, f"C3 emit {emit}", table=R.a15_readers())
+        arena, off, ln = _soup(12000, seed=31)
+        _parity(rx, arena, off, ln, f"soup emit {emit}")
+        c3 = [a[int(x):int(x) + int(y)].tobytes() for x, y in zip(o[:600], l[:600])]
+        hdr = b"RTPS\x02\x04\x01\x0f" + bytes(range(12))
+        many = hdr + b"\x09\x03\x00\x00" * 1000
+        A, O, L = oracle.pack(c3[:300] + [many] + c3[300:], align=1)
+        gpu = _parity(rx, A, O, L, f"slab overflow emit {emit}")
+        assert len(gpu.submessages(300)) == 1000
+    finally:
+        rx.debug_emit(prev)
+        rx.set_spec_hint(1)
+
+
 def test_launch_choice_follows_traffic(rx):
     """The speculative / chained choice follows the previous batch's mix (a lagging
     hint): a mixed batch after mixed ones, a one-DATA batch after mixed ones (chained

@@ -23,7 +23,7 @@ import pytest
 
 import oracle
 from rtps_rx.records import RECORD_DTYPE, DELIVERY_DTYPE, pack_match_table, WRITER_KINDS, max_records
-from shard_ref import COUNTS_DTYPE, ITEM_DTYPE, shard_pack_np, shard_unpack_np
+from shard_ref import COUNTS_DTYPE, ITEM_DTYPE, balanced_owner_table, shard_pack_np, shard_unpack_np
 
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
@@ -97,6 +97,45 @@ def test_pack_matches_model(rx, wl, world, small):
         assert (spilled > 0) == small
     finally:
         sh.close()
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_owner_table_modes(rx, world):
+    """the shard's writer -> owner table.  With readers set, the default deal
+    (RTPS_OWNER_BALANCED) is the readers' writer GUIDs dealt by rtps_rx_owner_assign: the device
+    pack equals the model with that table, no owner is idle and max / mean items per owner is
+    <= 1.1 on T's 16 writers; RTPS_OWNER_TOPIC puts every writer of the one reader's topic cache
+    on one owner; RTPS_OWNER_HASH is round 4's hash.  owner_of agrees with the pack."""
+    from rtps_rx.shard import OwnerShard, dev_to_numpy, OWNER_BALANCED, OWNER_HASH, OWNER_TOPIC
+    arena, off, ln = oracle.gen(oracle.WL_T, 8000)
+    _, r0, _, _ = oracle.parse(arena, off, ln)
+    guids = sorted({bytes(x["prefix"]) + bytes(x["writer_id"]) for x in r0})
+    assert len(guids) == 16
+    tbl = pack_match_table([(g, 100) for g in guids])
+    A, O, outs = _device_batch(rx, arena, off, ln, tbl)
+    _, recs, _, _ = oracle.parse(arena, off, ln, match_table=tbl)
+    sh = OwnerShard(rx, world, None, torch.device("cuda", 0), len(recs), 1 << 20)
+    try:
+        for mode in (OWNER_BALANCED, OWNER_TOPIC, OWNER_HASH):
+            sh.set_owners(mode)
+            sh.pack(A, O, outs)
+            rx.sync()
+            table = {OWNER_BALANCED: balanced_owner_table(guids, world), OWNER_TOPIC: {g: 0 for g in guids},
+                     OWNER_HASH: None}[mode]
+            exp = shard_pack_np(arena, off, recs, world, len(recs), 1 << 20, table)
+            counts = dev_to_numpy(sh.buffers().send_counts, 32 * world, COUNTS_DTYPE)
+            assert counts.tobytes() == np.concatenate([e["counts"] for e in exp]).tobytes(), mode
+            n = counts["n"].astype(np.int64)
+            if mode == OWNER_BALANCED:
+                assert n.min() > 0 and n.max() / n.mean() <= 1.1, n
+            if mode == OWNER_TOPIC:
+                assert n[0] == n.sum()
+            for g in guids:
+                want = table[g] if table else sh.owner_of(g)
+                assert sh.owner_of(g) == want
+    finally:
+        sh.close()
+        rx.set_match_table([])
 
 
 @pytest.mark.parametrize("wl", ["C3", "C4"])

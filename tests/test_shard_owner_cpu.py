@@ -11,6 +11,7 @@ of the whole stream gives (reader.rs:563-758, rtps_writer_proxy.rs:202-355),
 including with slots so small that most items travel in the spill."""
 import os
 import socket
+import types
 
 import numpy as np
 import pytest
@@ -21,7 +22,7 @@ import torch.multiprocessing as mp
 import oracle
 from rtps_rx.records import RECORD_DTYPE, DELIVERY_DTYPE, FRAG_SAMPLE_DTYPE, pack_match_table, WRITER_KINDS
 from rtps_rx.shard import spill_plan
-from shard_ref import COUNTS_DTYPE, ITEM_DTYPE, shard_pack_np, shard_unpack_np
+from shard_ref import COUNTS_DTYPE, ITEM_DTYPE, balanced_owner_table, shard_pack_np, shard_unpack_np
 
 C5_STRIDE = 8 << 20  # rank r's chunk starts at generator index r * 8M (BASELINE C5: 64M over 8 GPUs)
 
@@ -88,7 +89,9 @@ def _worker(rank, world, port, wl, n, stride, cap, bcap, tbl, q):
     try:
         arena, off, ln = _chunk(wl, rank, n, stride)
         _, recs, _, _ = oracle.parse(arena, off, ln, match_table=tbl)
-        packed = shard_pack_np(arena, off, recs, world, cap, bcap)
+        # the shard's default owner table (RTPS_OWNER_BALANCED): the table's writers dealt evenly
+        table = balanced_owner_table([bytes(t["writer_guid"]) for t in tbl], world)
+        packed = shard_pack_np(arena, off, recs, world, cap, bcap, table)
         slots, blob, sc, sspill, sbspill = _layout(packed, world, cap, bcap)
         # round 0: counts, slots, blob slots (equal splits)
         rc = np.zeros(world, dtype=COUNTS_DTYPE)
@@ -194,3 +197,84 @@ def test_owner_reassembly_c4(cap, bcap):
     reassembles them from the payload blobs and ingests the completed samples."""
     spilled, items = _run(2, oracle.WL_C4, 3000, 3000, cap=cap, bcap=bcap)
     assert (spilled > 0) == (cap == 64)
+
+
+def test_aborted_communicator_is_forgotten():
+    """after RTPS_RX_EABORTED the library has freed the communicator, so the owning
+    Exchange / OwnerShard drops its handle and every later call raises instead of handing RCCL a
+    freed ncclComm_t."""
+    import rtps_rx
+    from rtps_rx import shard
+    owner = types.SimpleNamespace(comm=object())
+    shard._COMMS[("test", 0)] = owner.comm
+    with pytest.raises(rtps_rx.RtpsRxError):
+        shard._check_comm(rtps_rx.RTPS_RX_EABORTED, owner)
+    assert owner.comm is None and ("test", 0) not in shard._COMMS
+    with pytest.raises(rtps_rx.RtpsRxError):
+        shard._live_comm(owner)
+
+
+def _lpt_mirror(writers, n_ranks, weights=None, groups=None):
+    """Python restatement of rtps_rx_owner_assign: groups by total weight, largest first (ties:
+    the group's smallest GUID), each to the least-loaded owner (ties: the lowest rank)."""
+    n = len(writers)
+    weights = [1] * n if weights is None else list(weights)
+    groups = list(range(n)) if groups is None else list(groups)
+    members = {}
+    for w, g in enumerate(groups):
+        members.setdefault(g, []).append(w)
+    keyed = sorted(members.values(), key=lambda m: (-sum(weights[w] for w in m), min(bytes(writers[w]) for w in m)))
+    load, owner = [0] * n_ranks, [0] * n
+    for m in keyed:
+        best = min(range(n_ranks), key=lambda r: (load[r], r))
+        load[best] += sum(weights[w] for w in m)
+        for w in m:
+            owner[w] = best
+    return owner
+
+
+def test_owner_assign_balances_the_workload_writers():
+    """the writers of T / C3 (16 GUIDs from the generator, weighted by their
+    records in a batch) dealt over 2 / 4 / 8 owners: max / mean records per owner <= 1.1 and
+    no idle owner, where the GUID hash left one of 8 idle and another at 1.5x the mean."""
+    from rtps_rx.shard import owner_assign
+    from rtps_rx.records import DATA, HEARTBEAT, GAP
+    for wl in (oracle.WL_T, oracle.WL_C3):
+        a, o, l = oracle.gen(wl, 20000)
+        _, recs, _, _ = oracle.parse(a, o, l, threads=8)
+        recs = recs[np.isin(recs["kind"], (DATA, HEARTBEAT, GAP))]
+        keys = [bytes(p) + bytes(w) for p, w in zip(recs["prefix"], recs["writer_id"])]
+        writers = sorted(set(keys))
+        assert len(writers) >= 16  # T: 16 writer GUIDs; C3: 16 prefixes x 16 writer ids
+        per = {g: 0 for g in writers}
+        for k in keys:
+            per[k] += 1
+        for n in (2, 4, 8):
+            own = owner_assign(writers, n)
+            assert list(own) == _lpt_mirror(writers, n)
+            load = np.bincount(own, weights=[per[g] for g in writers], minlength=n)
+            assert load.min() > 0 and load.max() / load.mean() <= 1.1, (wl, n, load)
+            # weighted by the records: as good or better
+            wown = owner_assign(writers, n, weights=[per[g] for g in writers])
+            assert list(wown) == _lpt_mirror(writers, n, [per[g] for g in writers])
+            wload = np.bincount(wown, weights=[per[g] for g in writers], minlength=n)
+            assert wload.max() <= load.max()
+
+
+def test_owner_assign_order_free_groups_and_weights():
+    """The deal depends on the writers, weights and groups, not on their order (every rank must
+    get the same table); a group's writers share an owner; uneven weights go largest first."""
+    from rtps_rx.shard import owner_assign
+    rng = np.random.default_rng(3)
+    writers = [bytes(rng.integers(0, 256, 16, dtype=np.uint8)) for _ in range(40)]
+    weights = rng.integers(1, 1000, 40)
+    groups = rng.integers(0, 12, 40)
+    own = owner_assign(writers, 5, weights, groups)
+    assert list(own) == _lpt_mirror(writers, 5, weights, groups)
+    for g in set(groups.tolist()):
+        assert len(set(own[groups == g].tolist())) == 1
+    perm = rng.permutation(40)
+    # the same groups under the permutation (group ids renamed to the permuted positions' own ids)
+    own2 = owner_assign([writers[i] for i in perm], 5, weights[perm], groups[perm])
+    assert [int(x) for x in own2] == [int(own[i]) for i in perm]
+    assert list(owner_assign(writers, 1)) == [0] * 40

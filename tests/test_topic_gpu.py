@@ -150,7 +150,35 @@ def test_a15_topics_across_batches_with_gc(rx, seed):
             tcs.gc()
 
 
-def test_reset_empties_topic_caches(rx):
+def test_ingest_reset_keeps_topic_caches(rx):
+    """rtps_rx_ingest_reset re-creates the writer proxies but not the topic caches,
+    as in the reference (fresh RtpsWriterProxy entries, rtps_writer_proxy.rs:62-90; the
+    TopicCache outlives them): the re-sent SNs pass the fresh proxies and are dropped by
+    add_change's find_by_sn while the topic still holds them (dds_cache.rs:241-276).  The
+    oracle keeps one TopicCaches across a fresh HistoryIngest."""
+    P, wk = R.PREFIXES, R.writer_key
+    rd = Readers([(bytes([0, 0, 1, 7]), 10, 0), (bytes([0, 0, 2, 7]), 11, 0)],
+                 [(P[0] + wk(0), 0), (P[0] + wk(0), 1)])
+    rx.set_readers(rd)
+    rx.set_topics([(1, 64)], [(10, 1), (11, 1)])
+    tcs = oracle.TopicCaches([(1, 64)], [(10, 1), (11, 1)])
+    dg = _data_stream(P[0], wk(0), range(1, 50))
+    for k, want in ((0, 49), (1, 0)):
+        ing = oracle.HistoryIngest(rd)
+        d = _batch(rx, ing, tcs, rd, dg, f"after ingest reset {k}")
+        assert len(d) == 2 * 49 and _cached(d).sum() == want
+        rx.ingest_reset()
+    # past max_keep the topic has let the oldest go: those SNs are stored again
+    dg2 = _data_stream(P[0], wk(0), range(50, 130))
+    _batch(rx, oracle.HistoryIngest(rd), tcs, rd, dg2, "beyond max_keep")
+    rx.ingest_reset()
+    d = _batch(rx, oracle.HistoryIngest(rd), tcs, rd, dg, "old SNs after GC")
+    assert _cached(d).sum() > 0
+
+
+def test_topic_reset_empties_topic_caches(rx):
+    """rtps_rx_topic_reset empties every topic cache (the proxies keep their state): after it, a
+    re-sent stream through reset proxies is stored again in full."""
     P, wk = R.PREFIXES, R.writer_key
     rd = Readers([(bytes([0, 0, 1, 7]), 10, 0), (bytes([0, 0, 2, 7]), 11, 0)],
                  [(P[0] + wk(0), 0), (P[0] + wk(0), 1)])
@@ -159,9 +187,10 @@ def test_reset_empties_topic_caches(rx):
     dg = _data_stream(P[0], wk(0), range(1, 50))
     for k in range(2):
         ing, tcs = oracle.HistoryIngest(rd), oracle.TopicCaches([(1, 64)], [(10, 1), (11, 1)])
-        d = _batch(rx, ing, tcs, rd, dg, f"after reset {k}")
+        d = _batch(rx, ing, tcs, rd, dg, f"after topic reset {k}")
         assert _cached(d).sum() == 49
         rx.ingest_reset()
+        rx.topic_reset()
 
 
 def test_full_size_c3_two_readers_per_topic(rx):
@@ -184,3 +213,22 @@ def test_full_size_c3_two_readers_per_topic(rx):
     o_dels = tcs.apply(recs, o_dels)
     assert dels.tobytes() == o_dels.tobytes()
     assert _cached(dels).sum() < len(dels)
+
+
+@pytest.mark.parametrize("pattern", ["pairs", "halves"])
+def test_spdp_repeats_batch(rx, pattern):
+    """The topic caches' adversarial batch (bench.py topic_cache_spdp_repeats
+    at 1M): the SPDP participant reader accepts duplicates (reader.rs:712-722), so every delivery
+    is a candidate, and >= 50 % of them repeat a key stored earlier in the same batch (the
+    in-order tc_resolve): 'pairs' = every SN twice in a row, 'halves' = the second half repeats
+    the first.  One topic, max_keep 64; bit-exact CACHED flags against the oracle."""
+    P, wk = R.PREFIXES, R.writer_key
+    rd = Readers([(R.SPDP_PARTICIPANT_READER, 14, 0)], [(P[0] + wk(0), 0)])
+    rx.set_readers(rd)
+    topics = [(9, 64)]
+    rx.set_topics(topics, [(14, 9)])
+    ing, tcs = oracle.HistoryIngest(rd), oracle.TopicCaches(topics, [(14, 9)])
+    n = 60000
+    sns = (np.arange(n) // 2 + 1) if pattern == "pairs" else (np.arange(n) % (n // 2) + 1)
+    d = _batch(rx, ing, tcs, rd, _data_stream(P[0], wk(0), sns, per_datagram=1), f"spdp {pattern}")
+    assert len(d) == n and 0 < _cached(d).sum() < n
