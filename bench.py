@@ -525,6 +525,33 @@ def exchange_prediction(rx, arena, off_t, outs, dev, worlds=(2, 4, 8)):
             "link_gbs": XGMI_LINK_GBS, "item_bytes": 32, **out}
 
 
+def time_ingest_ceiling(outs, n_rec, n_sets, stream, steps):
+    """Live timing of the ingest's same-shape floor (csrc/diag/ceiling.hip ceil_ingest_kernel):
+    every 64-B record read, 1 accept byte written; per event (a matched DATA / HEARTBEAT / GAP)
+    its proxy's 8-B state read and a 4-B change-set word OR-ed at its SN's bit; per delivery
+    (a matched DATA) 8 B appended.  None if the diagnostic library is absent."""
+    import ctypes
+    path = os.path.join(REPO, "rustdds-io_uring_amd", "libdiag_ceiling.so")
+    if not os.path.exists(path):
+        return None
+    D = ctypes.CDLL(path)
+    D.diag_ceiling_ingest.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64] + [ctypes.c_void_p] * 5 + \
+        [ctypes.c_uint32, ctypes.c_void_p]
+    dev = outs["records"].device
+    n_sets = max(n_sets, 1)
+    state = torch.zeros(n_sets, dtype=torch.int64, device=dev)
+    bits = torch.zeros(n_sets * (1 << 17) // 32, dtype=torch.int32, device=dev)
+    accept = torch.empty(max(n_rec, 1), dtype=torch.uint8, device=dev)
+    dels = torch.empty(max(n_rec, 1), dtype=torch.int64, device=dev)
+    n_del = torch.zeros(1, dtype=torch.int64, device=dev)
+
+    def run():
+        D.diag_ceiling_ingest(outs["records"].data_ptr(), outs["target"].data_ptr(), n_rec, state.data_ptr(),
+                              bits.data_ptr(), accept.data_ptr(), dels.data_ptr(), n_del.data_ptr(), n_sets,
+                              ctypes.c_void_p(stream.cuda_stream))
+    return _time_launches(run, stream, steps)
+
+
 def _reset_caches(rx, topic_cache):
     rx.ingest_reset()
     if topic_cache:
@@ -571,8 +598,14 @@ def ingest_leg(rx, arena, off_t, outs, n_rec, recs, n_entries, stream, steps, fo
     # algorithmic bytes: every record read once (64 B), 1 accept byte written per record, 8 B per
     # delivery, per event 8 B of proxy state read and 4 B of change-set bits touched
     alg = n_rec * (64 + 1) + 8 * na + 12 * events
+    ceil_ms = time_ingest_ceiling(outs, n_rec, n_entries, stream, steps)
+    ceil = None if ceil_ms is None else {
+        "kernel": "diag ceil_ingest_kernel (csrc/diag/ceiling.hip): each 64-B record read, 1 accept byte; per event "
+                  "8 B of proxy state + a 4-B change-set word at its SN; per delivery 8 B appended",
+        "ms": ceil_ms, "attainable_frac": ceil_ms / ms}
     return iouts, {"kernel": "rtps_ingest (classify + heartbeat sort/scans + marks + decide + select + merge + state)",
             "ms": ms, "topic_cache_ms": ms_tc, "topic_cache_extra_ms": ms_tc - ms,
+            "ceiling": ceil, "attainable_frac": None if ceil is None else ceil["attainable_frac"],
             "topic_cache_stored": cached,
             "records": n_rec, "events": events, "accepted": na,
             "samples_per_s": na / (ms * 1e-3), "records_per_s": n_rec / (ms * 1e-3),

@@ -746,7 +746,11 @@ int rtps_rx_ingest_reset(rtps_rx_ctx* ctx);
  * reference's defaults).  The periodic DDSCache::garbage_collect (the CacheCleaning
  * timer, io_uring/rtps/dp_event_loop.rs:385-389, io_uring/dds/cache.rs:43-51) is
  * rtps_rx_topic_gc.  Set the topics before the readers receive traffic: setting them
- * empties every topic cache. */
+ * empties every topic cache.  A batch whose ingest overflowed its capacities
+ * (*n_window_overflow > 0: samples accepted without the duplicate check) has every delivery
+ * checked against its topic's live changes, so CACHED stays add_change's answer for the
+ * deliveries made.  Owner batches (rtps_rx_shard_*): a topic cache's GC spans all of its
+ * writers, so its changes must all meet on one owner: use RTPS_OWNER_TOPIC there. */
 typedef struct rtps_topic {
   uint32_t topic;             /* caller-defined topic id */
   uint32_t max_keep_samples;  /* >= 1 */

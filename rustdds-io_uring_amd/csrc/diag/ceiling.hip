@@ -307,3 +307,57 @@ extern "C" int diag_ceiling_hops(int walks, const uint8_t* arena, uint64_t arena
   else return -1;
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+
+// ---- the history-cache ingest's floor ----
+// The bytes the ingest must move, at its real scatter pattern, and nothing else: every 64-B
+// record read (one 16-B load per lane of a quad: the record's four quads by four lanes, so a
+// wave reads 16 records back to back), 1 accept byte written per record; per EVENT (a writer
+// record that passes and reaches a proxy: DATA / HEARTBEAT / GAP with MATCHED) the proxy's 8-B
+// state read and 4 B of its change-set bitmap touched at the SN's bit (atomic OR, the
+// window's layout: 2^17 bits per proxy); per DELIVERY (a DATA sample with a proxy) 8 B
+// written, appended in wave order (one atomic per wave).  The proxy is the record's target set
+// (one proxy per writer set when one reader subscribes to every writer, as in bench.py).
+constexpr uint32_t ING_WW = (1u << 17) / 32u;  // change-set words per proxy
+__global__ __launch_bounds__(256) void ceil_ingest_kernel(const u32x4* rec, const uint32_t* target, uint64_t n_rec,
+                                                          const uint64_t* state, uint32_t* bits, uint8_t* accept,
+                                                          uint64_t* dels, unsigned long long* n_del,
+                                                          uint32_t n_sets) {
+  const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint64_t i = t >> 2;  // the record of this lane's quad
+  const uint32_t q = threadIdx.x & 3u, lane = threadIdx.x & 63u;
+  u32x4 v = {0u, 0u, 0u, 0u};
+  if (i < n_rec) v = rec[i * 4 + q];
+  // quad 0 has dgram_idx, sub_off | kind << 16; quad 1 word 3 = aux16 | route << 16 | pk << 24; quad 2 = sn
+  const uint32_t w1 = __shfl(v[1], (lane & ~3u) + 0u, 64), w7 = __shfl(v[3], (lane & ~3u) + 1u, 64);
+  const uint32_t sn = __shfl(v[0], (lane & ~3u) + 2u, 64);
+  const uint32_t kind = (w1 >> 16) & 0xffu, route = (w7 >> 16) & 0xffu;
+  bool event = false, del = false;
+  if (q == 0 && i < n_rec) {
+    accept[i] = 0;
+    const bool matched = (route & 0x01u) && (route & 0x20u);  // PASS and MATCHED
+    event = matched && (kind == 0x15u || kind == 0x07u || kind == 0x08u);
+    del = event && kind == 0x15u;
+  }
+  if (event) {
+    const uint32_t e = target[i] < n_sets ? target[i] : 0u;
+    const uint64_t st = state[e];
+    atomicOr(bits + (uint64_t)e * ING_WW + ((sn + (uint32_t)st) & ((1u << 17) - 1u)) / 32u, 1u << (sn & 31u));
+  }
+  const uint64_t m = __ballot(del);
+  uint64_t base = 0;
+  if (m) {
+    if (lane == (uint32_t)__builtin_ctzll(m)) base = atomicAdd(n_del, (unsigned long long)__popcll(m));
+    base = __shfl(base, (uint32_t)__builtin_ctzll(m), 64);
+    if (del) dels[base + __popcll(m & ((1ull << lane) - 1ull))] = i | ((uint64_t)1 << 32);
+  }
+}
+extern "C" int diag_ceiling_ingest(const void* rec, const uint32_t* target, uint64_t n_rec, const uint64_t* state,
+                                   uint32_t* bits, uint8_t* accept, uint64_t* dels, uint64_t* n_del, uint32_t n_sets,
+                                   void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemsetAsync(n_del, 0, 8, s) != hipSuccess) return -2;
+  const uint64_t threads = 4 * n_rec;
+  hipLaunchKernelGGL(ceil_ingest_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, s,
+                     (const u32x4*)rec, target, n_rec, state, bits, accept, dels, (unsigned long long*)n_del, n_sets);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}

@@ -37,10 +37,17 @@ static_assert(RTPS_RX_EXCHANGE_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "unique id size
 
 // Point-to-point messages are cut into pieces of at most XCHUNK bytes, posted in
 // order inside the same group (NCCL matches a peer's sends and receives in
-// order).  Measured on MI355X with RCCL 2.26: a single 1.2-1.4 GB ncclSend /
-// ncclRecv pair (one rank exchanging with itself at C5's per-rank size) delivered
-// only the first half of the bytes; pieces of this size arrive whole.
+// order).  The cause (round 5, scripts/rccl_size_probe.py, profiles/r5_rccl_size_probe.json:
+// ONE unchunked ncclSend + ncclRecv pair per size, pattern-filled, through
+// rtps_rx_debug_rccl_p2p): this image's RCCL 2.26.6 delivers a single point-to-point
+// message of up to 2^30 bytes whole, and of any larger size (2^30 + 4 B, 1.125, 1.25, 1.5,
+// 2, 2.25 GiB) only its first half: the first wrong byte is at n / 2 every time.  It is
+// RCCL's, not this library's size handling (the probe passes the byte count straight to
+// ncclSend / ncclRecv as size_t).  So no message may exceed 2^30 bytes; 64-MB pieces keep
+// well inside that and let the group's pieces pipeline.  (The probe is a self-send, the only
+// pair a one-GPU box has; the exchanges no longer send to self: the own slot is a device copy.)
 constexpr size_t XCHUNK = size_t(64) << 20;
+static_assert(XCHUNK <= (size_t(1) << 30), "RCCL 2.26 delivers p2p messages of at most 2^30 bytes whole");
 static bool send_bytes(const void* buf, size_t n, int peer, ncclComm_t c, hipStream_t st) {
   const uint8_t* p = static_cast<const uint8_t*>(buf);
   for (size_t o = 0; o < n; o += XCHUNK) {

@@ -38,6 +38,11 @@
 #include <new>
 #include <vector>
 
+// the diagnostic / tuning builds that need the rejected passes (diag/mixed_passes.inc)
+#if (defined(RTPS_ITEM_DIAG) || defined(RTPS_EM_STAMPS) || defined(RTPS_LDS_STAMPS)) && !defined(RTPS_DIAG_PASSES)
+#define RTPS_DIAG_PASSES
+#endif
+
 #include "../../include/rtps_rx.h"
 #include "rtps_gen.h"
 #include "rtps_cdr.h"
@@ -110,25 +115,6 @@ __device__ __forceinline__ uint32_t ld4(const Src& s, uint32_t o) {
   for (uint32_t k = 0; k < 4; ++k)
     if ((uint64_t)a + k < s.avail) r |= ld_u8_raw(s, a + k) << (8u * k);
   return r;
-}
-
-// The same reads from a datagram staged in LDS (rtps_parse_lds_kernel): w = the
-// tile image as words, base = the datagram's 16-B aligned byte offset in it.
-// Unaligned reads combine two aligned words (v_alignbyte).
-struct LSrc {
-  const uint32_t* w;
-  uint32_t base;
-};
-__device__ __forceinline__ uint32_t ld4(const LSrc& s, uint32_t o) {
-  const uint32_t a = s.base + o, i = a >> 2, sh = a & 3u;
-  const uint32_t lo = s.w[i], hi = s.w[i + 1];
-  return __builtin_amdgcn_alignbyte(hi, lo, sh);
-}
-__device__ __forceinline__ u32x4 ld16(const LSrc& s, uint32_t o) {
-  const uint32_t a = s.base + o, i = a >> 2, sh = a & 3u;
-  const uint32_t w0 = s.w[i], w1 = s.w[i + 1], w2 = s.w[i + 2], w3 = s.w[i + 3], w4 = s.w[i + 4];
-  return u32x4{__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
-               __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh)};
 }
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
@@ -930,176 +916,6 @@ __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_fix_kern
   }
 }
 
-// Chained single launch for mixed traffic (C3: every tile non-speculative).
-// One workgroup per tile: count walk, publish the tile's record count, find the
-// tile's exact prefix from the predecessors' published counts, then the
-// writing walk at the exact position while the tile's lines are still in cache.
-// Prefixes are three-level so that a tile needs one poll, not one per 64
-// predecessors: tiles form groups of 64, groups supergroups of 64.  The LAST
-// tile of a group sums its group's earlier counts (which it needs for its own
-// prefix anyway) and publishes the group total; the last tile of the last group
-// of a supergroup likewise the supergroup total.  A tile's prefix = the totals
-// of the earlier supergroups + of the earlier groups of its supergroup + the
-// counts of the earlier tiles of its group, the three polled together.  Every
-// exchanged word is an agent-scope 8-byte {epoch, value} word (no fences, no
-// read-modify-write: a reader polls until the word carries this launch's
-// epoch).  A tile that gives up waiting (a predecessor that never published:
-// only if the dispatcher ran tiles far out of order) stays unwritten and kernel
-// B, launched after it as always, walks it: results never depend on dispatch
-// order or timing.  Nothing is zeroed between launches: words of earlier
-// launches carry older epochs.
-// look-back word = epoch << 32 | value; ready when its epoch is this launch's
-__device__ __forceinline__ uint64_t ch_word(uint32_t epoch, uint64_t value) { return (uint64_t)epoch << 32 | value; }
-#ifndef RTPS_CH_GROUP
-#define RTPS_CH_GROUP 64
-#endif
-#ifndef RTPS_CH_SLEEP
-#define RTPS_CH_SLEEP 32  // s_sleep units (64 clocks) between polls: 2 / 8 / 16 / 32 measured, DESIGN §3.3
-#endif
-constexpr uint32_t CH_GROUP = RTPS_CH_GROUP;  // <= 64: a group's tile words are summed by one wave
-static_assert(RTPS_CH_GROUP >= 1 && RTPS_CH_GROUP <= 64, "a group's words are summed by one wave of 64 lanes");
-// polls before a tile gives up (about 1 ms whatever the sleep between polls)
-constexpr uint32_t CH_SPIN_LIMIT = (1u << 15) / (RTPS_CH_SLEEP > 0 ? RTPS_CH_SLEEP : 1);
-// Look-back words, three levels: [tiles] tile counts | [groups] group totals |
-// [supers] supergroup totals | 2 spare.
-__host__ __device__ constexpr uint32_t chain_groups(uint32_t tiles) { return (tiles + CH_GROUP - 1) / CH_GROUP; }
-__host__ __device__ constexpr uint32_t chain_supers(uint32_t tiles) {
-  return (chain_groups(tiles) + CH_GROUP - 1) / CH_GROUP;
-}
-__host__ __device__ constexpr size_t chain_words(uint32_t tiles) {
-  return (size_t)tiles + chain_groups(tiles) + chain_supers(tiles) + 2;
-}
-__device__ __forceinline__ uint64_t ch_load(const uint64_t* w) {
-  return __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void ch_store(uint64_t* w, uint64_t v) {
-  __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// sum of the value parts of words a[0, na) + b[0, nb) + c[0, nc) (each <= 64, one
-// per lane), polling all three together until every word is ready; false after
-// `limit` polls
-__device__ __forceinline__ bool ch_sum_ready(const uint64_t* a, uint32_t na, const uint64_t* b, uint32_t nb,
-                                             const uint64_t* c, uint32_t nc, uint32_t lane, uint32_t epoch,
-                                             uint32_t limit, uint64_t& sum) {
-  const uint64_t none = ch_word(epoch, 0);
-  for (uint32_t spins = 0;; ++spins) {
-    const uint64_t va = lane < na ? ch_load(a + lane) : none;
-    const uint64_t vb = lane < nb ? ch_load(b + lane) : none;
-    const uint64_t vc = lane < nc ? ch_load(c + lane) : none;
-    const bool ready = (uint32_t)(va >> 32) == epoch && (uint32_t)(vb >> 32) == epoch && (uint32_t)(vc >> 32) == epoch;
-    if (__all(ready)) {
-      uint64_t x = (va & 0xffffffffull) + (vb & 0xffffffffull) + (vc & 0xffffffffull);
-#pragma unroll
-      for (uint32_t d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
-      sum = x;
-      return true;
-    }
-    if (spins >= limit) return false;
-    __builtin_amdgcn_s_sleep(RTPS_CH_SLEEP);
-  }
-}
-// The exact record prefix of `tile` (one wave, all 64 lanes): publish the tile's
-// count (and, as the last tile of its group / supergroup, the group's /
-// supergroup's total), then sum the totals of the earlier supergroups, of the
-// earlier groups of its supergroup and the counts of the earlier tiles of its
-// group.  Every word is an agent-scope {epoch, 32-bit value} word (a supergroup
-// holds at most 64^2 tiles' records: < 2^32 for tiles of 256 datagrams of 16379
-// records, and rec_begin is 32-bit anyway).  false: a poll gave up (the tile is
-// left to B).
-__device__ bool chain_prefix(const KParams& p, uint32_t tile, uint32_t n_tiles, uint64_t agg, uint32_t lane,
-                             uint64_t& excl) {
-  uint64_t* tw = p.chain;
-  const uint32_t ng = chain_groups(n_tiles);
-  uint64_t* gw = tw + n_tiles;
-  uint64_t* sw = gw + ng;
-  const uint32_t g = tile / CH_GROUP, r = tile % CH_GROUP, sg = g / CH_GROUP, rg = g % CH_GROUP;
-  const uint32_t g_size = min(CH_GROUP, n_tiles - g * CH_GROUP), sg_size = min(CH_GROUP, ng - sg * CH_GROUP);
-  const uint32_t ep = p.ch_epoch, lim = p.ch_spin_limit;
-  if (lane == 0) ch_store(tw + tile, ch_word(ep, agg));
-  bool ok = true;
-  uint64_t tiles_sum = 0, groups_sum = 0, part = 0;
-  bool have_tiles = false, have_groups = false;
-  if (r + 1 == g_size) {  // last tile of its group: publish the group total
-    ok = ch_sum_ready(tw + g * CH_GROUP, r, nullptr, 0, nullptr, 0, lane, ep, lim, tiles_sum);
-    have_tiles = true;
-    const uint64_t gtot = tiles_sum + agg;
-    if (ok && lane == 0) ch_store(gw + g, ch_word(ep, gtot));
-    if (ok && rg + 1 == sg_size) {  // ... and of the last group of its supergroup: the supergroup total
-      ok = ch_sum_ready(gw + sg * CH_GROUP, rg, nullptr, 0, nullptr, 0, lane, ep, lim, groups_sum);
-      have_groups = true;
-      if (ok && lane == 0) ch_store(sw + sg, ch_word(ep, groups_sum + gtot));
-    }
-  }
-  // earlier supergroups beyond the first 64 (batches over 64^3 tiles only)
-  excl = 0;
-  uint32_t s0 = 0;
-  for (; ok && s0 + 64 < sg; s0 += 64) {
-    ok = ch_sum_ready(sw + s0, 64, nullptr, 0, nullptr, 0, lane, ep, lim, part);
-    excl += part;
-  }
-  if (ok) {
-    ok = ch_sum_ready(sw + s0, sg - s0, have_groups ? nullptr : gw + sg * CH_GROUP, have_groups ? 0u : rg,
-                      have_tiles ? nullptr : tw + g * CH_GROUP, have_tiles ? 0u : r, lane, ep, lim, part);
-    excl += part + tiles_sum + groups_sum;
-  }
-  return ok;
-}
-
-// 8 waves per SIMD fit the chained kernel in 64 VGPRs without scratch (C3: 411-414 against
-// 427-428 us at 6; the speculative kernel would spill there, so it keeps 6)
-#ifndef RTPS_CH_WAVES_PER_SIMD
-#define RTPS_CH_WAVES_PER_SIMD 8
-#endif
-__global__ __launch_bounds__(TILE, RTPS_CH_WAVES_PER_SIMD) void rtps_parse_chain_kernel(KParams p, uint32_t n_tiles,
-                                                                                      uint32_t k_spec, uint32_t parity) {
-  __shared__ uint32_t s_wave_bad[WAVES];
-  __shared__ uint32_t s_wave_sum[WAVES];
-  __shared__ uint64_t s_excl;
-  __shared__ uint32_t s_ok;
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  const uint32_t tile = blockIdx.x;
-  mt_stage(p);  // visible after the __syncthreads below, before the writing walk
-  TileCtx t;
-  load_tile(p, tile, t);
-  uint32_t cnt;
-  const uint32_t st = count_lane(p, t, cnt);
-  const uint32_t incl = wave_incl_scan(cnt, lane);
-  const uint64_t bad = __ballot(t.valid && cnt != k_spec);
-  if (lane == 63) { s_wave_sum[wave] = incl; s_wave_bad[wave] = bad != 0ull; }
-  __syncthreads();
-  uint32_t wave_off = 0, agg = 0, mixed = 0;
-#pragma unroll
-  for (uint32_t w = 0; w < WAVES; ++w) {
-    const uint32_t v = s_wave_sum[w];
-    if (w < wave) wave_off += v;
-    agg += v;
-    mixed |= s_wave_bad[w];
-  }
-  Scratch x = scratch_of(p.scratch, n_tiles);
-  if (t.valid) {
-    p.status[t.i] = (uint8_t)st;
-    x.dcount[t.i] = (uint16_t)cnt;
-  }
-  if (wave == 0) {
-    uint64_t excl = 0;
-    const bool ok = chain_prefix(p, tile, n_tiles, agg, lane, excl);
-    if (lane == 0) {
-      s_excl = excl;
-      s_ok = ok ? 1u : 0u;
-      x.info[tile] = agg | INFO_NONSPEC | (ok ? INFO_WRITTEN : 0u) | (mixed ? INFO_MIXED : 0u);  // read by B
-      if (tile == 0) x.flag[parity] = 1u;  // B never takes its all-speculative exit
-    }
-  }
-  __syncthreads();
-  if (!s_ok || !t.valid) return;
-  const uint64_t my_first = s_excl + wave_off + (incl - cnt);
-  if (p.rec_begin) p.rec_begin[t.i] = (uint32_t)my_first;
-  if (cnt) {
-    uint32_t n2;
-    walk<true>(p, t.s, t.H, t.L, t.i, my_first, n2);
-  }
-}
-
 // ---------------------------------------------------------------------------
 // E / S / W: the item pass for mixed traffic (the default
 // since round 4).  The chained kernel C spends its time in three places: the
@@ -1312,237 +1128,6 @@ __global__ __launch_bounds__(SCAN_T) void rtps_parse_scan_kernel(KParams p, uint
   }
 }
 
-// W runs EMT threads per tile (the first TILE do the per-datagram prologue), so that most
-// threads take one item: a thread that loops over items waits, before each next item's
-// loads can be used, for the previous item's record stores (vmcnt counts stores too).
-#ifndef RTPS_EM_THREADS
-#define RTPS_EM_THREADS 1024
-#endif
-constexpr uint32_t EMT = RTPS_EM_THREADS;
-static_assert(EMT % TILE == 0, "the prologue threads are the first TILE");
-#if defined(RTPS_LDS_STAMPS) || defined(RTPS_EM_STAMPS)  // tuning builds: per-tile timestamps
-constexpr uint32_t STAMP_TILES = 1u << 16, STAMP_N = 24;
-__device__ uint64_t g_lds_stamps[STAMP_TILES * STAMP_N];
-#endif
-#ifdef RTPS_EM_STAMPS  // W: thread 0's phase ends (0-7; in-item marks wait for their loads), each wave's end (8-23)
-#define EM_STAMP(k, wait) do { if (tid == 0 && tile < STAMP_TILES) { \
-  if (wait) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); \
-  g_lds_stamps[tile * STAMP_N + (k)] = __builtin_amdgcn_s_memrealtime(); } } while (0)
-#define EM_WAVE_END() do { if (lane == 0 && tile < STAMP_TILES) \
-  g_lds_stamps[tile * STAMP_N + 8u + wave] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#else
-#define EM_STAMP(k, wait) do {} while (0)
-#define EM_WAVE_END() do {} while (0)
-#endif
-__global__ __launch_bounds__(EMT) __attribute__((amdgpu_waves_per_eu(RTPS_EM_WAVES_PER_SIMD)))
-void rtps_parse_emit_kernel(KParams p, uint32_t n_tiles, const u32x4* items, const uint32_t* wcnt,
-                            const uint64_t* tprefix) {
-  __shared__ uint32_t s_rbase[TILE];   // tile-local first record of each datagram (NONE: no records)
-  __shared__ uint32_t s_doff[TILE];    // datagram start relative to the workgroup's descriptor base
-  __shared__ uint32_t s_len[TILE];
-  __shared__ uint32_t s_pfx[TILE * 3]; // header GuidPrefix of each datagram
-  __shared__ uint32_t s_wsum[WAVES], s_nit[WAVES + 1];
-  __shared__ uint64_t s_lo[WAVES], s_hi[WAVES];
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  const bool pro = tid < TILE;  // a prologue thread: datagram tid of the tile
-  const uint32_t tile = blockIdx.x;
-  EM_STAMP(0, false);
-  Scratch x = scratch_of(p.scratch, n_tiles);
-  const uint64_t prefix = tprefix[tile];
-  const uint32_t wc = pro ? wcnt[tile * WAVES + wave] : 0u;
-  const uint32_t i = tile * TILE + tid;
-  const bool valid = pro && i < p.n;
-  // the datagram's count, offset and length loaded together (offset / length whether or not it
-  // has records), and in flight before the table copy below waits for its own loads
-  const uint32_t cnt0 = valid ? (uint32_t)x.dcount[i] : 0u;
-  const uint64_t off0 = valid ? p.dgram_off[i] : 0ull;
-  const uint32_t L0 = valid ? p.dgram_len[i] : 0u;
-  mt_stage(p);  // visible after the __syncthreads below
-  const uint32_t cnt = cnt0;
-  const uint64_t off = cnt ? off0 : 0ull;
-  const uint32_t L = cnt ? L0 : 0u;
-  const uint32_t incl = wave_incl_scan(cnt, lane);
-  // descriptor base: the arena when every offset fits 32 bits, else the tile's smallest
-  // offset (a tile spanning 4 GiB or more takes the lane walk)
-  const bool wide = p.arena_len >= ARENA_DIRECT;
-  uint64_t lo = cnt ? off : ~0ull, hi = cnt ? off + L : 0ull;
-  if (wide) {
-#pragma unroll
-    for (uint32_t d = 32; d >= 1; d >>= 1) {
-      const uint64_t a = __shfl_xor(lo, d, 64), b = __shfl_xor(hi, d, 64);
-      lo = a < lo ? a : lo;
-      hi = b > hi ? b : hi;
-    }
-  }
-  if (pro && lane == 63) s_wsum[wave] = incl;
-  if (pro && lane == 0) { s_nit[wave] = (wc & WCNT_OVERFLOW) ? 0u : wc; s_lo[wave] = lo; s_hi[wave] = hi; }
-  EM_STAMP(1, false);
-  __syncthreads();
-  EM_STAMP(2, false);
-  uint32_t wave_off = 0;
-  uint64_t tlo = ~0ull, thi = 0;
-#pragma unroll
-  for (uint32_t w = 0; w < WAVES; ++w) {
-    if (w < wave) wave_off += s_wsum[w];
-    tlo = s_lo[w] < tlo ? s_lo[w] : tlo;
-    thi = s_hi[w] > thi ? s_hi[w] : thi;
-  }
-  const uint64_t tb = (wide && tlo != ~0ull) ? tlo : 0ull;
-  const bool tile_walk = wide && tlo != ~0ull && thi - tlo >= 0xffff0000ull;
-  const bool walk_wave = pro && (tile_walk || (wc & WCNT_OVERFLOW) != 0u);
-  const uint32_t local = wave_off + incl - cnt;
-  if (valid && p.rec_begin) p.rec_begin[i] = (uint32_t)(prefix + local);
-  if (walk_wave) {  // the items did not fit (or cannot be addressed): walk the wave's datagrams
-    s_rbase[tid] = 0xffffffffu;
-    TileCtx t;
-    load_tile(p, tile, t);
-    if (t.valid && cnt) {
-      uint32_t n2;
-      walk<true>(p, t.s, t.H, t.L, t.i, prefix + local, n2);
-    }
-  }
-  const uint64_t avail64 = p.arena_len - tb;
-  const uint32_t avail = avail64 > 0xffffffffull ? 0xffffffffu : (uint32_t)avail64;
-  Src s;
-  s.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p.arena + tb), (short)0, (int)avail, 0x00020000);
-  s.avail = avail;
-  if (pro && !walk_wave) {
-    s_rbase[tid] = cnt ? local : 0xffffffffu;
-    s_doff[tid] = (uint32_t)(off - tb);
-    s_len[tid] = L;
-    if (cnt) {
-      s.base = (uint32_t)(off - tb);
-      const u32x4 h = ld16(s, 8u);
-      s_pfx[tid * 3 + 0] = h[0]; s_pfx[tid * 3 + 1] = h[1]; s_pfx[tid * 3 + 2] = h[2];
-    }
-  }
-  __syncthreads();  // (every s_nit read above happened before this)
-  if (tid == 0) {
-    uint32_t a = 0;
-#pragma unroll
-    for (uint32_t w = 0; w < WAVES; ++w) { const uint32_t v = tile_walk ? 0u : s_nit[w]; s_nit[w] = a; a += v; }
-    s_nit[WAVES] = a;
-  }
-  __syncthreads();
-  EM_STAMP(3, false);
-  const uint32_t total = s_nit[WAVES];
-  const u32x4* tslab = items + (size_t)tile * WAVES * CAPW * IW;
-#ifdef RTPS_EM_SORT
-  static_assert(!RTPS_IT_WIDE, "the kind-sorted variant takes 16-B items (-DRTPS_IT_WIDE=0)");
-  // tuning variant: the tile's items bucketed by kind in LDS first, so that a wave's lanes
-  // run the same per-kind reader (the slab order interleaves kinds)
-  constexpr uint32_t NCL = 8, RND = WAVES * CAPW / EMT, SLOTS = RND * (EMT / 64);
-  __shared__ u32x4 s_it[WAVES * CAPW];
-  __shared__ uint32_t s_cc[NCL][SLOTS];
-  {
-    const uint64_t lt = lane ? (~0ull >> (64u - lane)) : 0ull;
-    u32x4 mine[RND];
-    uint32_t cls[RND], rk[RND];
-#pragma unroll
-    for (uint32_t r = 0; r < RND; ++r) {
-      const uint32_t k = tid + r * EMT;
-      cls[r] = NCL;
-      if (k < total) {
-        const uint32_t w = (k >= s_nit[1]) + (k >= s_nit[2]) + (k >= s_nit[3]);
-        mine[r] = tslab[w * CAPW + (k - s_nit[w])];
-        mine[r][1] |= w << 14;  // (j < 2^14: a datagram holds fewer submessages)
-        const uint32_t kd = mine[r][1] >> 24;
-        cls[r] = kd == RTPS_DATA ? 0u : kd == RTPS_DATA_FRAG ? 1u : kd == RTPS_HEARTBEAT ? 2u : kd == RTPS_GAP ? 3u
-               : kd == RTPS_ACKNACK ? 4u : kd == RTPS_NACK_FRAG ? 5u : kd == RTPS_HEARTBEAT_FRAG ? 6u : 7u;
-      }
-#pragma unroll
-      for (uint32_t c = 0; c < NCL; ++c) {
-        const uint64_t m = __ballot(cls[r] == c);
-        if (cls[r] == c) rk[r] = (uint32_t)__popcll(m & lt);
-        if (lane == 0) s_cc[c][r * (EMT / 64) + wave] = (uint32_t)__popcll(m);
-      }
-    }
-    __syncthreads();
-    if (tid < NCL) {  // class c's slots: exclusive prefix, after every earlier class
-      uint32_t before = 0;
-      for (uint32_t c = 0; c < tid; ++c)
-        for (uint32_t q = 0; q < SLOTS; ++q) before += s_cc[c][q];
-      for (uint32_t q = 0; q < SLOTS; ++q) { const uint32_t v = s_cc[tid][q]; s_cc[tid][q] = before; before += v; }
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t r = 0; r < RND; ++r)
-      if (cls[r] < NCL) s_it[s_cc[cls[r]][r * (EMT / 64) + wave] + rk[r]] = mine[r];
-    __syncthreads();
-  }
-  for (uint32_t k = tid; k < total; k += EMT) {
-    const u32x4 it = s_it[k];
-    const uint32_t w = (it[1] >> 14) & 3u, jmask = 0x3fffu;
-    const uint32_t o = it[0] & 0xffffu, src_off = it[0] >> 16;
-#else
-  for (uint32_t k = tid; k < total; k += EMT) {
-    const uint32_t w = (k >= s_nit[1]) + (k >= s_nit[2]) + (k >= s_nit[3]);
-    const size_t ib = (size_t)(w * CAPW + (k - s_nit[w])) * IW;
-    const u32x4 it = tslab[ib];
-    const uint32_t jmask = 0xffffu;
-    const uint32_t o = it[0] & 0xffffu, src_off = it[0] >> 16;
-#endif
-    const uint32_t j = it[1] & jmask, d = w * 64u + ((it[1] >> 16) & 63u), kind = it[1] >> 24;
-    const uint32_t rb = s_rbase[d];
-    if (rb == 0xffffffffu) continue;  // the datagram was dropped after this item (or has no records)
-    s.base = s_doff[d];
-    Win W;
-    {
-#if RTPS_IT_WIDE
-      const u32x4 a = tslab[ib + 1], b = tslab[ib + 2];  // the window as the walk loaded it
-#else
-      const u32x4 a = ld16(s, o);
-      u32x4 b = {0u, 0u, 0u, 0u};
-      if (win_needs_tail<true>(kind)) b = ld16(s, o + 16u);
-#endif
-      W.w[0] = a[0]; W.w[1] = a[1]; W.w[2] = a[2]; W.w[3] = a[3];
-      W.w[4] = b[0]; W.w[5] = b[1]; W.w[6] = b[2]; W.w[7] = b[3];
-      W.w[8] = kind == RTPS_DATA_FRAG ? ld4(s, o + 32u) : 0u;
-      W.w[9] = 0u; W.w[10] = 0u; W.w[11] = 0u;
-    }
-    EM_STAMP(4, true);
-    Interp st;
-    if (src_off == 8u) {
-      st.src0 = s_pfx[d * 3 + 0]; st.src1 = s_pfx[d * 3 + 1]; st.src2 = s_pfx[d * 3 + 2];
-    } else {
-      const u32x4 q = ld16(s, src_off);
-      st.src0 = q[0]; st.src1 = q[1]; st.src2 = q[2];
-    }
-    st.dst_ok = ((it[1] >> 22) & 1u) != 0u;
-    st.ts_valid = ((it[1] >> 23) & 1u) != 0u;
-    st.ts_sec = it[2];
-    st.ts_frac = it[3];
-    const uint32_t flags = (W.w[0] >> 8) & 0xffu;
-    const bool le = (flags & 1u) != 0u;
-    const uint32_t eff = eff_len(kind, e16(W.w[0], 1, le), s_len[d] - o);
-    Rec R;
-    rec_clear(R);
-    SubOut so;
-    EM_STAMP(5, true);
-    sub_body<true>(s, W, kind, flags, le, o + 4u, eff, R, so);  // validated by E's walk
-    R.d[0] = tile * TILE + d;
-    R.d[1] = o | (kind << 16) | (flags << 24);
-    EM_STAMP(6, true);
-    const uint32_t tgt = rec_finish(p, R, so, kind, st);
-    EM_STAMP(7, true);
-    const uint64_t r = prefix + rb + j;
-    if (r < p.max_records) {
-      rec_store(p.records + r, R);
-      if (p.target_out) p.target_out[r] = tgt;
-    }
-  }
-  EM_WAVE_END();
-}
-
-// ---------------------------------------------------------------------------
-// W2 rtps_parse_emit2_kernel: wave w of a workgroup takes E's wave slab w of each tile
-// of its grid stride.  The reader tables are staged once per workgroup; after that no
-// wave waits for another (no barrier, no per-tile prologue scan).  The per-datagram
-// prologue is one coalesced 16-B word E wrote (dinfo: the datagram's tile-local first
-// record, its header prefix) plus the (offset, length) arrays: lane l holds datagram l
-// of the slab, and an item takes its datagram's fields with lane permutes.  The
-// descriptor base is E's (the arena, or for large arenas the wave's smallest offset),
-// so every datagram E walked is addressable here.
 // The item of slab position k, its datagram's fields (lane permutes: every lane of the
 // wave calls this) and the record it becomes: R, its target set, its index r (~0: none).
 __device__ __forceinline__ void em2_item(const KParams& p, const Src& s0, const u32x4 it, bool act, const u32x4 di,
@@ -1601,94 +1186,34 @@ __device__ __forceinline__ void em2_item(const KParams& p, const Src& s0, const 
 // of the slab, and an item takes its datagram's fields with lane permutes.  The
 // descriptor base is E's (the arena, or for large arenas the wave's smallest offset),
 // so every datagram E walked is addressable here.
-// The item of slab position k, its datagram's fields (lane permutes: every lane of the
-// wave calls this) and the record it becomes.
-__device__ __forceinline__ void em2_item(const KParams& p, const Src& s0, const u32x4 it, bool act, const u32x4 di,
-                                         uint32_t doff, uint32_t dlen, uint32_t dg0, uint64_t prefix) {
-  const uint32_t d = (it[1] >> 16) & 63u;
-  const uint32_t rb = __shfl(di[0], d, 64);
-  const uint32_t base = __shfl(doff, d, 64), len = __shfl(dlen, d, 64);
-  const uint32_t pf0 = __shfl(di[1], d, 64), pf1 = __shfl(di[2], d, 64), pf2 = __shfl(di[3], d, 64);
-  if (!act || (rb & DI_NOREC)) return;  // (a datagram dropped after this item)
-  const uint32_t o = it[0] & 0xffffu, src_off = it[0] >> 16;
-  const uint32_t j = it[1] & 0xffffu, kind = it[1] >> 24;
-  Src s = s0;
-  s.base = base;
-  Win W;
-  {
-    const u32x4 a = ld16(s, o);
-    u32x4 bq = {0u, 0u, 0u, 0u};
-    if (win_needs_tail<true>(kind)) bq = ld16(s, o + 16u);
-    W.w[0] = a[0]; W.w[1] = a[1]; W.w[2] = a[2]; W.w[3] = a[3];
-    W.w[4] = bq[0]; W.w[5] = bq[1]; W.w[6] = bq[2]; W.w[7] = bq[3];
-    W.w[8] = kind == RTPS_DATA_FRAG ? ld4(s, o + 32u) : 0u;
-    W.w[9] = 0u; W.w[10] = 0u; W.w[11] = 0u;
-  }
-  Interp st;
-  if (src_off == 8u) {
-    st.src0 = pf0; st.src1 = pf1; st.src2 = pf2;
-  } else {  // an INFO_SRC's prefix is in effect
-    const u32x4 q = ld16(s, src_off);
-    st.src0 = q[0]; st.src1 = q[1]; st.src2 = q[2];
-  }
-  st.dst_ok = ((it[1] >> 22) & 1u) != 0u;
-  st.ts_valid = ((it[1] >> 23) & 1u) != 0u;
-  st.ts_sec = it[2];
-  st.ts_frac = it[3];
-  const uint32_t flags = (W.w[0] >> 8) & 0xffu;
-  const bool le = (flags & 1u) != 0u;
-  const uint32_t eff = eff_len(kind, e16(W.w[0], 1, le), len - o);
-  Rec R;
-  rec_clear(R);
-  SubOut so;
-  sub_body<true>(s, W, kind, flags, le, o + 4u, eff, R, so);  // validated by E's walk
-  R.d[0] = dg0 + d;
-  R.d[1] = o | (kind << 16) | (flags << 24);
-  const uint32_t tgt = rec_finish(p, R, so, kind, st);
-  const uint64_t r = prefix + rb + j;
-  if (r < p.max_records) {
-    rec_store(p.records + r, R);
-    if (p.target_out) p.target_out[r] = tgt;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// W2 rtps_parse_emit2_kernel: wave w of a workgroup takes E's wave slab w of each tile
-// of its grid stride.  The reader tables are staged once per workgroup; after that no
-// wave waits for another (no barrier, no per-tile prologue scan).  The per-datagram
-// prologue is one coalesced 16-B word E wrote (dinfo: the datagram's tile-local first
-// record, its header prefix) plus the (offset, length) arrays: lane l holds datagram l
-// of the slab, and an item takes its datagram's fields with lane permutes.  The
-// descriptor base is E's (the arena, or for large arenas the wave's smallest offset),
-// so every datagram E walked is addressable here.
-// REC_ORDER: the wave first maps its records to their slab positions in LDS (record q of
-// the wave = item k, from the item's datagram and index j), then takes the items in
-// record order: the 64 lanes of a round read neighbouring submessages (a datagram's
-// submessages share lines and DRAM rows) and write 64 consecutive records.  Otherwise the
-// items are taken in slab order (E's walk step major: 64 datagrams' k-th submessages).
+// Records are taken in RECORD ORDER: the wave first maps its records to their slab positions
+// in LDS (record q of the wave = item k, from the item's datagram and index j), then takes
+// them 64 at a time: the 64 lanes of a round read neighbouring submessages (a datagram's
+// submessages share lines and DRAM rows) and their 64 records are 4 KB back to back, stored
+// through a 1-KB LDS stage so that each store instruction writes 1 KB of consecutive bytes.
+// (Slab order, E's walk-step-major order, measured 254 us against 210 on C3)
 #ifndef RTPS_EM2_WAVES_PER_SIMD
 #define RTPS_EM2_WAVES_PER_SIMD 6  // 80 VGPRs, no spill (the LDS caps the CU at 24 waves anyway)
 #endif
 #ifndef RTPS_EM2_TRANSPOSE
-#define RTPS_EM2_TRANSPOSE 1  // record order: each record store instruction writes 1 KB back to back
+#define RTPS_EM2_TRANSPOSE 1  // 0: per-lane 64-B record stores (measured slower)
 #endif
 #ifndef RTPS_EM2_THREADS
 #define RTPS_EM2_THREADS 512  // two tiles per workgroup (one reader-table copy for 8 waves; 256 / 768: slower)
 #endif
 constexpr uint32_t EM2T = RTPS_EM2_THREADS, EM2_TPB = EM2T / TILE;
 static_assert(EM2T % TILE == 0, "whole tiles per workgroup");
-template <bool REC_ORDER>
 __global__ __launch_bounds__(EM2T, RTPS_EM2_WAVES_PER_SIMD) void rtps_parse_emit2_kernel(
     KParams p, uint32_t n_tiles, const u32x4* __restrict__ items, const uint32_t* __restrict__ wcnt,
     const uint64_t* __restrict__ tprefix, const u32x4* __restrict__ dinfo) {
   static_assert(!RTPS_IT_WIDE, "W2 takes 16-B items");
-  __shared__ uint16_t s_map[REC_ORDER ? (EM2T / 64u) * CAPW : 1];
+  __shared__ uint16_t s_map[(EM2T / 64u) * CAPW];  // the waves' record -> slab position maps
 #if RTPS_EM2_TRANSPOSE
-  __shared__ u32x4 s_stage[REC_ORDER ? (EM2T / 64u) * 64u : 1];  // 1 KB per wave
+  __shared__ u32x4 s_stage[(EM2T / 64u) * 64u];    // 1 KB per wave
 #endif
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
   const uint32_t wave = wv % WAVES, sub = wv / WAVES;  // the wave's slab in its tile, the workgroup's tile
-  uint16_t* map = s_map + (REC_ORDER ? wv * CAPW : 0u);
+  uint16_t* map = s_map + wv * CAPW;
   mt_stage(p);
   __syncthreads();
   for (uint32_t tile = blockIdx.x * EM2_TPB + sub; tile < n_tiles; tile += gridDim.x * EM2_TPB) {
@@ -1703,22 +1228,6 @@ __global__ __launch_bounds__(EM2T, RTPS_EM2_WAVES_PER_SIMD) void rtps_parse_emit
     const u32x4* slab = items + (size_t)(tile * WAVES + wave) * CAPW;
     const uint32_t doff = t.s.base, dlen = t.L;
     const uint32_t dg0 = tile * TILE + wave * 64u;
-    if (!REC_ORDER) {
-      for (uint32_t b = 0; b < wc; b += 64u) {  // (uniform: every lane takes part in the permutes)
-        const uint32_t k = b + lane;
-        const bool act = k < wc;
-        const u32x4 it = act ? slab[k] : u32x4{0u, 0u, 0u, 0u};
-        Rec R;
-        uint32_t tgt;
-        uint64_t r;
-        em2_item(p, t.s, it, act, di, doff, dlen, dg0, prefix, R, tgt, r);
-        if (r < p.max_records) {
-          rec_store(p.records + r, R);
-          if (p.target_out) p.target_out[r] = tgt;
-        }
-      }
-      continue;
-    }
     // record q of the wave (q = the datagram's first record - the wave's + j) <- slab position k
     const uint32_t wbase = __builtin_amdgcn_readfirstlane(first);  // lane 0: the wave's first record
     uint32_t nr = 0;
@@ -1791,549 +1300,9 @@ __global__ __launch_bounds__(EM2T, RTPS_EM2_WAVES_PER_SIMD) void rtps_parse_emit
   }
 }
 
-// ---------------------------------------------------------------------------
-// E' / S / W': the record-slab pass (mixed pass 3).  Like the item pass, but the
-// walk itself builds each record (sub_body<true> + rec_finish, the windows it
-// already holds) and appends the finished 64-B record to its wave's slab with its
-// (record index in its datagram, lane); W' only copies every slab record to tile
-// prefix + datagram's first record + j.  The record pass no longer re-gathers any
-// datagram bytes: its loads are the slab's, coalesced.
-#ifndef RTPS_RS_CAPR
-#define RTPS_RS_CAPR 384u
+#ifdef RTPS_DIAG_PASSES  // the measured, rejected passes for mixed traffic (variant builds)
+#include "diag/mixed_passes.inc"
 #endif
-constexpr uint32_t CAPR = RTPS_RS_CAPR;  // records per wave slab (C3 averages 243 per 64 datagrams)
-
-__device__ uint32_t rslab_walk(const KParams& p, const Src& s, const uint32_t* H, uint32_t L, uint32_t dgram_idx,
-                               uint32_t lane, u32x4* rslab, uint32_t* mslab, uint32_t* tslab, uint32_t& wpos,
-                               uint32_t& nrec) {
-  nrec = 0;
-  if (L > RTPS_MAX_DATAGRAM) return RTPS_DGRAM_TOO_LONG;
-  const uint32_t MAGIC_RTPS = 0x53505452u, MAGIC_RTPX = 0x58505452u;
-  if (L < 20u) {  // message_receiver.rs:238-251
-    if (L >= 16u && H[0] == MAGIC_RTPS && (H[2] >> 8) == 0x534444u && H[3] == 0x474e4950u) return RTPS_DGRAM_PING;
-    return RTPS_DGRAM_SHORT;
-  }
-  if (H[0] != MAGIC_RTPS) return H[0] == MAGIC_RTPX ? RTPS_DGRAM_RTPX : RTPS_DGRAM_BAD_MAGIC;
-  if ((H[1] & 0xffu) > 2u) return RTPS_DGRAM_BAD_HEADER;
-  Interp st{H[2], H[3], H[4], true, false, 0u, 0u};  // handle_parsed_message_2 (:289-295)
-  const uint64_t lt = lane ? (~0ull >> (64u - lane)) : 0ull;
-  uint32_t o = 20;
-  Win Wn;  // the next submessage's window, loaded before this record's stores (as walk<true>)
-  head_win(H, Wn);
-  while (o < L) {
-    const uint32_t rem = L - o;
-    if (rem < 4u) return RTPS_DGRAM_SUBMSG_ERR;
-    Win W = Wn;
-    if (o != 20u && (W.w[0] & 0xffu) == RTPS_DATA_FRAG) W.w[8] = ld4(s, o + 32u);
-    const uint32_t kind = W.w[0] & 0xffu, flags = (W.w[0] >> 8) & 0xffu;
-    const bool le = (flags & 1u) != 0u;
-    const uint32_t eff = eff_len(kind, e16(W.w[0], 1, le), rem);
-    if (4u + eff > rem) return RTPS_DGRAM_SUBMSG_ERR;
-    if (o + 4u + eff < L) load_win_pf(s, o + 4u + eff, Wn);
-    Rec R;
-    rec_clear(R);
-    SubOut so;
-    if (!sub_body<true>(s, W, kind, flags, le, o + 4u, eff, R, so)) return RTPS_DGRAM_SUBMSG_ERR;
-    interp_update(p, st, W, kind, flags, le);
-    const bool em = so.cls != 0u;
-    uint32_t tgt = RTPS_NO_TARGET;
-    if (em) {
-      R.d[0] = dgram_idx;
-      R.d[1] = o | (kind << 16) | (flags << 24);
-      tgt = rec_finish(p, R, so, kind, st);
-    }
-    const uint64_t m = __ballot(em);
-    if (em) {
-      const uint32_t pos = wpos + (uint32_t)__popcll(m & lt);
-      if (pos < CAPR) {
-        rec_store(reinterpret_cast<rtps_record*>(rslab + (size_t)pos * 4u), R);
-        mslab[pos] = nrec | (lane << 16);
-        if (p.target_out) tslab[pos] = tgt;
-      }
-      nrec++;
-    }
-    wpos += (uint32_t)__popcll(m);
-    o += 4u + eff;
-  }
-  return RTPS_DGRAM_OK;
-}
-
-#ifndef RTPS_RS_WAVES_PER_SIMD
-#define RTPS_RS_WAVES_PER_SIMD 6  // (8 spills the record and both windows to scratch)
-#endif
-__global__ __launch_bounds__(TILE, RTPS_RS_WAVES_PER_SIMD) void rtps_parse_rslab_kernel(KParams p, uint32_t n_tiles,
-                                                                                      uint32_t k_spec, u32x4* recs,
-                                                                                      uint32_t* meta, uint32_t* tgts,
-                                                                                      uint32_t* wcnt) {
-  __shared__ uint32_t s_wave_sum[WAVES], s_wave_bad[WAVES];
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  const uint32_t tile = blockIdx.x;
-  mt_stage(p);
-  TileCtx t;
-  load_tile(p, tile, t);
-  __syncthreads();  // the match table's LDS image (rec_finish)
-  const size_t w0 = (size_t)(tile * WAVES + wave) * CAPR;
-  uint32_t cnt = 0, wpos = 0, st = RTPS_DGRAM_OK;
-  if (t.valid) {
-    if (!t.addressable) st = RTPS_DGRAM_TOO_LONG;
-    else st = rslab_walk(p, t.s, t.H, t.L, t.i, lane, recs + w0 * 4u, meta + w0, tgts + w0, wpos, cnt);
-    if (st != RTPS_DGRAM_OK) cnt = 0;
-  }
-  uint32_t wtot = wpos, wsum = cnt;
-#pragma unroll
-  for (uint32_t d = 32; d >= 1; d >>= 1) {
-    const uint32_t y = __shfl_xor(wtot, d, 64);
-    wtot = y > wtot ? y : wtot;
-    wsum += __shfl_xor(wsum, d, 64);
-  }
-  const uint64_t bad = __ballot(t.valid && cnt != k_spec);
-  if (lane == 0) {
-    s_wave_sum[wave] = wsum;
-    s_wave_bad[wave] = bad != 0ull;
-    wcnt[tile * WAVES + wave] = wtot > CAPR ? WCNT_OVERFLOW : wtot;
-  }
-  Scratch x = scratch_of(p.scratch, n_tiles);
-  if (t.valid) {
-    p.status[t.i] = (uint8_t)st;
-    x.dcount[t.i] = (uint16_t)cnt;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    uint32_t agg = 0, mixed = 0;
-#pragma unroll
-    for (uint32_t w = 0; w < WAVES; ++w) { agg += s_wave_sum[w]; mixed |= s_wave_bad[w]; }
-    x.info[tile] = agg | INFO_NONSPEC | (mixed ? INFO_MIXED : 0u);
-  }
-}
-
-// W': the slab records to their places (a wave whose slab overflowed walks its datagrams)
-__global__ __launch_bounds__(EMT) void rtps_parse_rcopy_kernel(KParams p, uint32_t n_tiles, const u32x4* recs,
-                                                               const uint32_t* meta, const uint32_t* tgts,
-                                                               const uint32_t* wcnt, const uint64_t* tprefix) {
-  __shared__ uint32_t s_rbase[TILE];  // tile-local first record of each datagram (NONE: no records)
-  __shared__ uint32_t s_wsum[WAVES], s_nit[WAVES + 1];
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  const bool pro = tid < TILE;
-  const uint32_t tile = blockIdx.x;
-  mt_stage(p);  // (the overflow walk's rec_finish)
-  Scratch x = scratch_of(p.scratch, n_tiles);
-  const uint64_t prefix = tprefix[tile];
-  const uint32_t wc = pro ? wcnt[tile * WAVES + wave] : 0u;
-  const uint32_t i = tile * TILE + tid;
-  const bool valid = pro && i < p.n;
-  const uint32_t cnt = valid ? (uint32_t)x.dcount[i] : 0u;
-  const uint32_t incl = wave_incl_scan(cnt, lane);
-  if (pro && lane == 63) s_wsum[wave] = incl;
-  if (pro && lane == 0) s_nit[wave] = (wc & WCNT_OVERFLOW) ? 0u : wc;
-  __syncthreads();
-  uint32_t wave_off = 0;
-#pragma unroll
-  for (uint32_t w = 0; w < WAVES; ++w)
-    if (w < wave) wave_off += s_wsum[w];
-  const uint32_t local = wave_off + incl - cnt;
-  if (valid && p.rec_begin) p.rec_begin[i] = (uint32_t)(prefix + local);
-  if (pro) s_rbase[tid] = cnt ? local : 0xffffffffu;
-  if (pro && (wc & WCNT_OVERFLOW)) {  // the records did not fit the slab: walk the wave's datagrams
-    s_rbase[tid] = 0xffffffffu;
-    TileCtx t;
-    load_tile(p, tile, t);
-    if (t.valid && cnt) {
-      uint32_t n2;
-      walk<true>(p, t.s, t.H, t.L, t.i, prefix + local, n2);
-    }
-  }
-  __syncthreads();
-  if (tid == 0) {
-    uint32_t a = 0;
-#pragma unroll
-    for (uint32_t w = 0; w < WAVES; ++w) { const uint32_t v = s_nit[w]; s_nit[w] = a; a += v; }
-    s_nit[WAVES] = a;
-  }
-  __syncthreads();
-  const uint32_t total = s_nit[WAVES];
-  const size_t t0 = (size_t)tile * WAVES * CAPR;
-  for (uint32_t k = tid; k < total; k += EMT) {
-    const uint32_t w = (k >= s_nit[1]) + (k >= s_nit[2]) + (k >= s_nit[3]);
-    const size_t e = t0 + (size_t)w * CAPR + (k - s_nit[w]);
-    const uint32_t m = meta[e];
-    const uint32_t rb = s_rbase[w * 64u + (m >> 16)];
-    if (rb == 0xffffffffu) continue;  // the datagram was dropped after this record
-    const uint64_t r = prefix + rb + (m & 0xffffu);
-    if (r < p.max_records) {
-      const u32x4* q = recs + e * 4u;
-      u32x4* d = reinterpret_cast<u32x4*>(p.records + r);
-      const u32x4 a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
-      d[0] = a0; d[1] = a1; d[2] = a2; d[3] = a3;
-      if (p.target_out) p.target_out[r] = tgts[e];
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// D  rtps_parse_lds_kernel: mixed traffic through LDS tiles.
-// A lane walking its datagram's submessage chain in global memory waits on one
-// dependent load per submessage, and the kind-divergent body readers serialise
-// their own loads on top: C3 spends most of its cycles waiting (r1 counters).
-// Here a workgroup takes LT consecutive datagrams and:
-//   1 stages their bytes, packed 16-B aligned, into an LDS image with
-//     coalesced 16-B loads, every load of the tile in flight at once;
-//   2 walks each datagram's submessage headers in LDS (lane per datagram),
-//     twice: counting, then writing one ITEM per materialised submessage
-//     (offset, length, kind, flags, and the interpreter state in effect: the
-//     source prefix, the dest filter, the governing INFO_TS);
-//   3 runs the per-kind body readers over the items (lane per item, the same
-//     sub_body / rec_finish code as the global walk, reading LDS): validity
-//     (any error drops the datagram) and the finished 64-B records;
-//   4 learns the tile's exact record prefix from the chained look-back;
-//   5 writes the records through the LDS image (now free) as contiguous,
-//     coalesced 16-B stores.
-// Tiles whose bytes or items do not fit fall back to the lane walk in global
-// memory (wave 0, one lane per datagram), with the same look-back.  LT = 32
-// datagrams of at most 1500 B (the Ethernet MTU's RTPS payload) always fit the
-// 48 KiB image, so only jumbo datagrams take the fallback.
-// ---------------------------------------------------------------------------
-#ifndef RTPS_LDS_LT
-#define RTPS_LDS_LT 32u
-#endif
-constexpr uint32_t LT = RTPS_LDS_LT;  // datagrams per LDS tile
-static_assert(LT >= 1 && LT <= 64, "one wave-0 lane per datagram");
-#ifndef RTPS_LDS_IMG
-#define RTPS_LDS_IMG (48u * 1024u)
-#endif
-#ifndef RTPS_LDS_ITEMS
-#define RTPS_LDS_ITEMS 512u
-#endif
-#ifndef RTPS_LDS_WG_PER_CU
-#define RTPS_LDS_WG_PER_CU 2
-#endif
-#ifndef RTPS_LDS_RT  // 1: stage the reader tables in LDS for D too (costs occupancy); 0: probe them in L2
-#define RTPS_LDS_RT 0
-#endif
-// per-phase timestamps of kernel D into a device array (tuning builds only; the buffer is
-// defined before the record pass, which stamps it under RTPS_EM_STAMPS)
-#ifdef RTPS_LDS_STAMPS
-#define LDS_STAMP(k) \
-  do { if (tid == 0 && tile < STAMP_TILES) g_lds_stamps[tile * STAMP_N + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#else
-#define LDS_STAMP(k) do {} while (0)
-#endif
-constexpr uint32_t LIMG = RTPS_LDS_IMG;       // image bytes
-constexpr uint32_t LMAXIT = RTPS_LDS_ITEMS;   // items (materialised submessages) per tile
-static_assert(LIMG <= 65536u - 64u, "items hold 16-bit image offsets");
-static_assert(LT % WAVES == 0, "the staging gives every wave LT / WAVES datagrams");
-constexpr uint32_t LDPW = LT / WAVES;  // datagrams staged per wave
-constexpr uint32_t LSTAGE_R = 2;       // 16-B chunks per lane per datagram kept in flight (2 KiB)
-static_assert(LMAXIT * 64u <= LIMG, "the record stage reuses the image");
-static_assert(LMAXIT % TILE == 0, "items in whole rounds");
-constexpr uint32_t LIT_ROUNDS = LMAXIT / TILE;
-constexpr uint32_t IT_NO_TS = 0xffffu;
-
-// item words: [0] image offset of the submessage | eff length << 16
-//             [1] kind | flags << 8 | datagram (tile-local) << 16 | dst_ok << 24
-//             [2] image offset of the source prefix | governing INFO_TS item << 16 (IT_NO_TS: none)
-//             [3] unused
-// One walk over a datagram staged in LDS at image offset `base` (lane per datagram):
-// header checks, the length rules and the interpreter state; WRITE appends the
-// items at it0.  Returns the status (RTPS_DGRAM_*; SUBMSG_ERR only for length /
-// header errors: body errors come from the item pass) and the item count.  As in
-// walk(), a submessage's record carries the interpreter state AFTER the
-// submessage's own transition (INFO_SRC: its prefix; INFO_TS: its time).
-template <bool WRITE>
-__device__ uint32_t lds_walk(const KParams& p, const uint32_t* img, uint32_t base, uint32_t L, uint32_t dlocal,
-                             u32x4* items, uint32_t it0, uint32_t& nit) {
-  nit = 0;
-  const LSrc s{img, base};
-  if (L > RTPS_MAX_DATAGRAM) return RTPS_DGRAM_TOO_LONG;
-  const uint32_t MAGIC_RTPS = 0x53505452u, MAGIC_RTPX = 0x58505452u;
-  const uint32_t h0 = L >= 4u ? ld4(s, 0) : 0u;
-  if (L < 20u) {  // message_receiver.rs:238-251
-    if (L >= 16u && h0 == MAGIC_RTPS && (ld4(s, 8) >> 8) == 0x534444u && ld4(s, 12) == 0x474e4950u)
-      return RTPS_DGRAM_PING;
-    return RTPS_DGRAM_SHORT;
-  }
-  if (h0 != MAGIC_RTPS) return h0 == MAGIC_RTPX ? RTPS_DGRAM_RTPX : RTPS_DGRAM_BAD_MAGIC;
-  if ((ld4(s, 4) & 0xffu) > 2u) return RTPS_DGRAM_BAD_HEADER;
-  // handle_parsed_message_2 (:289-295): src := header prefix, dest := own, ts := None
-  uint32_t src_off = base + 8u, ts_item = IT_NO_TS;
-  bool dst_ok = true;
-  uint32_t o = 20;
-  while (o < L) {
-    const uint32_t rem = L - o;
-    if (rem < 4u) { nit = 0; return RTPS_DGRAM_SUBMSG_ERR; }
-    const uint32_t h = ld4(s, o);
-    const uint32_t kind = h & 0xffu, flags = (h >> 8) & 0xffu;
-    const bool le = (flags & 1u) != 0u;
-    const uint32_t eff = eff_len(kind, e16(h, 1, le), rem);
-    if (4u + eff > rem) { nit = 0; return RTPS_DGRAM_SUBMSG_ERR; }
-    if (emits(kind)) {
-      // interpreter transitions (message_receiver.rs:618-665); a malformed INFO_*
-      // drops the datagram in the item pass, so its state never matters
-      if (kind == RTPS_INFO_TS) {
-        ts_item = (flags & 0x02u) ? IT_NO_TS : it0 + nit;  // Invalidate flag -> None
-      } else if (kind == RTPS_INFO_SRC) {
-        src_off = base + o + 12u;  // header, unused u32, version, vendor, then the prefix
-        ts_item = IT_NO_TS;
-      } else if (kind == RTPS_INFO_DST) {
-        const uint32_t a = ld4(s, o + 4u), b = ld4(s, o + 8u), c = ld4(s, o + 12u);
-        dst_ok = ((a | b | c) == 0u) || (a == p.own0 && b == p.own1 && c == p.own2);
-      }
-      if (WRITE) {
-        u32x4 it;
-        it[0] = (base + o) | (eff << 16);
-        it[1] = kind | (flags << 8) | (dlocal << 16) | ((dst_ok ? 1u : 0u) << 24);
-        it[2] = src_off | (ts_item << 16);
-        it[3] = 0u;
-        items[it0 + nit] = it;
-      }
-      nit++;
-    }
-    o += 4u + eff;
-  }
-  return RTPS_DGRAM_OK;
-}
-
-__global__ __launch_bounds__(TILE, RTPS_LDS_WG_PER_CU) void rtps_parse_lds_kernel(KParams p, uint32_t n_tiles,
-                                                                                   uint32_t k_spec, uint32_t parity) {
-  __shared__ u32x4 s_img[LIMG / 16u + 4u];  // + 64 B: window reads past the last datagram stay inside
-  __shared__ u32x4 s_it[LMAXIT];            // items; after the item pass: the records' target sets
-  __shared__ uint32_t s_doff[LT + 1];       // image offset of each datagram (16-B aligned), total at LT
-  __shared__ uint32_t s_rel[LT];            // datagram offset from the tile's descriptor base
-  __shared__ uint32_t s_ibase[LT + 1];      // first item of each datagram, total at LT
-  __shared__ uint32_t s_rbase[LT];          // first tile-local record of each datagram (NONE: dropped)
-  __shared__ uint32_t s_bad[LT];            // a body reader failed (the datagram is dropped)
-  __shared__ uint32_t s_mode, s_ok, s_agg;  // mode 1: LDS tile, 0: lane-walk fallback
-  __shared__ uint64_t s_excl, s_tb;
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  const uint32_t tile = blockIdx.x;
-  uint32_t* img = reinterpret_cast<uint32_t*>(s_img);
-  Scratch x = scratch_of(p.scratch, n_tiles);
-  // ---- 0 (wave 0, lane = tile-local datagram): lengths, image offsets, descriptor base ----
-  const uint32_t i = tile * LT + lane;
-  uint32_t L = 0;
-  bool valid = false, addressable = false;
-  if (wave == 0) {
-    valid = lane < LT && i < p.n;
-    const uint64_t off = valid ? p.dgram_off[i] : ~0ull;
-    L = valid ? p.dgram_len[i] : 0u;
-    addressable = valid && off <= p.arena_len && (uint64_t)L <= p.arena_len - off;
-    const uint32_t psz = (addressable && L <= RTPS_MAX_DATAGRAM) ? ((L + 15u) & ~15u) : 0u;
-    const uint32_t incl = wave_incl_scan(psz, lane);
-    if (lane < LT) s_doff[lane] = incl - psz;
-    if (lane == 63) s_doff[LT] = incl;
-    uint64_t lo = addressable ? off : ~0ull, hi = addressable ? off + L : 0ull;
-#pragma unroll
-    for (uint32_t d = 32; d >= 1; d >>= 1) {
-      const uint64_t a = __shfl_xor(lo, d, 64), b = __shfl_xor(hi, d, 64);
-      lo = a < lo ? a : lo;
-      hi = b > hi ? b : hi;
-    }
-    const uint64_t tb = lo == ~0ull ? 0ull : lo;
-    if (lane < LT) {
-      s_rel[lane] = addressable ? (uint32_t)(off - tb) : 0u;
-      s_bad[lane] = 0u;
-    }
-    const uint32_t total = __shfl(incl, 63, 64);
-    if (lane == 0) {
-      s_tb = tb;
-      // the LDS path needs the image to fit and the tile's bytes inside one 4 GiB descriptor
-      s_mode = (total <= LIMG && (lo == ~0ull || hi - lo < 0xfffff000ull)) ? 1u : 0u;
-    }
-  }
-  LDS_STAMP(0);
-  mt_stage(p);  // reader tables, for the record pass
-  __syncthreads();
-  LDS_STAMP(1);
-  uint32_t st = RTPS_DGRAM_OK, nit = 0;
-  if (s_mode) {
-    // ---- 1: stage the bytes: wave w copies datagrams w, w + WAVES, ...; its lanes take 16-B
-    // chunks lane, lane + 64 of each (1 KiB per instruction), every load in flight at once ----
-    const uint64_t tb = s_tb;
-    const uint64_t avail64 = p.arena_len - tb;
-    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t*>(p.arena + tb), (short)0,
-        (int)(avail64 > 0xffffffffull ? 0xffffffffu : (uint32_t)avail64), 0x00020000);
-    u32x4 v[LDPW][LSTAGE_R];
-    uint32_t nch[LDPW];
-#pragma unroll
-    for (uint32_t j = 0; j < LDPW; ++j) {
-      const uint32_t d = wave + WAVES * j;
-      nch[j] = (s_doff[d + 1] - s_doff[d]) >> 4;  // 0 for datagrams not staged
-      const uint32_t rel = s_rel[d];
-#pragma unroll
-      for (uint32_t r = 0; r < LSTAGE_R; ++r) {
-        const uint32_t k = r * 64u + lane;
-        v[j][r] = u32x4{0u, 0u, 0u, 0u};
-        if (k < nch[j]) v[j][r] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, rel + 16u * k, 0, 0);
-      }
-    }
-#pragma unroll
-    for (uint32_t j = 0; j < LDPW; ++j) {
-      const uint32_t d = wave + WAVES * j;
-      u32x4* dst = s_img + (s_doff[d] >> 4);
-#pragma unroll
-      for (uint32_t r = 0; r < LSTAGE_R; ++r) {
-        const uint32_t k = r * 64u + lane;
-        if (k < nch[j]) dst[k] = v[j][r];
-      }
-      // datagrams over 2 KiB (rare: jumbo frames): the rest chunk by chunk
-      for (uint32_t k = LSTAGE_R * 64u + lane; k < nch[j]; k += 64u)
-        dst[k] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, s_rel[d] + 16u * k, 0, 0);
-    }
-    __syncthreads();
-    LDS_STAMP(2);
-    // ---- 2a: count walk (wave 0): status from the headers and length rules, items per datagram ----
-    if (wave == 0) {
-      if (valid) st = addressable ? lds_walk<false>(p, img, s_doff[lane], L, lane, s_it, 0, nit)
-                                  : (uint32_t)RTPS_DGRAM_TOO_LONG;
-      const uint32_t incl = wave_incl_scan(nit, lane);
-      if (lane < LT) s_ibase[lane] = incl - nit;
-      if (lane == 63) {
-        s_ibase[LT] = incl;
-        if (incl > LMAXIT) s_mode = 0u;  // too many submessages: the lane walk takes the tile
-      }
-    }
-    __syncthreads();
-  }
-  if (!s_mode) {
-    // ---- fallback: lane walk in global memory (wave 0), the same look-back ----
-    if (wave != 0) return;
-    TileCtx t;
-    load_tile<LT>(p, tile, t);
-    uint32_t cnt;
-    const uint32_t st2 = count_lane(p, t, cnt);
-    const uint32_t incl = wave_incl_scan(cnt, lane);
-    const uint32_t agg = __shfl(incl, 63, 64);
-    const bool mixed = __ballot(t.valid && cnt != k_spec) != 0ull;
-    if (t.valid) {
-      p.status[t.i] = (uint8_t)st2;
-      x.dcount[t.i] = (uint16_t)cnt;
-    }
-    uint64_t excl = 0;
-    const bool ok = chain_prefix(p, tile, n_tiles, agg, lane, excl);
-    if (lane == 0) {
-      x.info[tile] = agg | INFO_NONSPEC | (ok ? INFO_WRITTEN : 0u) | (mixed ? INFO_MIXED : 0u);  // read by B
-      if (tile == 0) x.flag[parity] = 1u;  // B never takes its all-speculative exit
-    }
-    if (!ok || !t.valid) return;
-    const uint64_t my_first = excl + (incl - cnt);
-    if (p.rec_begin) p.rec_begin[t.i] = (uint32_t)my_first;
-    if (cnt) {
-      uint32_t n2;
-      walk<true>(p, t.s, t.H, t.L, t.i, my_first, n2);
-    }
-    return;
-  }
-  LDS_STAMP(3);
-  // ---- 2b: item walk (wave 0) ----
-  if (wave == 0 && valid && st == RTPS_DGRAM_OK) {
-    uint32_t n2;
-    lds_walk<true>(p, img, s_doff[lane], L, lane, s_it, s_ibase[lane], n2);
-  }
-  __syncthreads();
-  LDS_STAMP(4);
-  // ---- 3: item pass: body readers + the records (lane per item) ----
-  const uint32_t nitems = s_ibase[LT];
-  Rec R[LIT_ROUNDS];
-  uint32_t tgt[LIT_ROUNDS], dl[LIT_ROUNDS];
-  const LSrc whole{img, 0u};
-#pragma unroll
-  for (uint32_t r = 0; r < LIT_ROUNDS; ++r) {
-    const uint32_t k = r * TILE + tid;
-    rec_clear(R[r]);
-    tgt[r] = RTPS_NO_TARGET;
-    dl[r] = 0u;
-    if (k < nitems) {
-      const u32x4 it = s_it[k];
-      const uint32_t oabs = it[0] & 0xffffu, eff = it[0] >> 16;
-      const uint32_t kind = it[1] & 0xffu, flags = (it[1] >> 8) & 0xffu, d = (it[1] >> 16) & 0xffu;
-      const uint32_t base = s_doff[d], o = oabs - base;
-      const LSrc ds{img, base};
-      dl[r] = d;
-      const bool le = (flags & 1u) != 0u;
-      Win W;
-      load_win(ds, o, W);
-      SubOut so;
-      if (!sub_body<true>(ds, W, kind, flags, le, o + 4u, eff, R[r], so)) {
-        s_bad[d] = 1u;
-      } else {
-        Interp ist;
-        const uint32_t so_off = it[2] & 0xffffu, ts_it = it[2] >> 16;
-        ist.src0 = ld4(whole, so_off); ist.src1 = ld4(whole, so_off + 4u); ist.src2 = ld4(whole, so_off + 8u);
-        ist.dst_ok = (it[1] >> 24) != 0u;
-        ist.ts_valid = ts_it != IT_NO_TS;
-        ist.ts_sec = 0u; ist.ts_frac = 0u;
-        if (ist.ts_valid) {
-          const u32x4 ti = s_it[ts_it];
-          const uint32_t to = ti[0] & 0xffffu;
-          const bool tle = ((ti[1] >> 8) & 1u) != 0u;
-          ist.ts_sec = e32(ld4(whole, to + 4u), tle);
-          ist.ts_frac = e32(ld4(whole, to + 8u), tle);
-        }
-        R[r].d[0] = tile * LT + d;
-        R[r].d[1] = o | (kind << 16) | (flags << 24);
-        tgt[r] = rec_finish(p, R[r], so, kind, ist);
-      }
-    }
-  }
-  __syncthreads();
-  LDS_STAMP(5);
-  // ---- 4 (wave 0): statuses, counts, the tile prefix (look-back) ----
-  if (wave == 0) {
-    uint32_t st2 = st;
-    if (valid && st2 == RTPS_DGRAM_OK && s_bad[lane]) st2 = RTPS_DGRAM_SUBMSG_ERR;
-    const uint32_t cnt = (valid && st2 == RTPS_DGRAM_OK) ? s_ibase[lane + 1] - s_ibase[lane] : 0u;
-    const uint32_t incl = wave_incl_scan(cnt, lane);
-    const uint32_t agg = __shfl(incl, 63, 64);
-    if (lane < LT) s_rbase[lane] = (valid && st2 == RTPS_DGRAM_OK) ? incl - cnt : 0xffffffffu;
-    const bool mixed = __ballot(valid && cnt != k_spec) != 0ull;
-    if (valid) {
-      p.status[i] = (uint8_t)st2;
-      x.dcount[i] = (uint16_t)cnt;
-    }
-    uint64_t excl = 0;
-    const bool ok = chain_prefix(p, tile, n_tiles, agg, lane, excl);
-    if (ok && valid && p.rec_begin) p.rec_begin[i] = (uint32_t)(excl + incl - cnt);
-    if (lane == 0) {
-      s_excl = excl;
-      s_ok = ok ? 1u : 0u;
-      s_agg = agg;
-      x.info[tile] = agg | INFO_NONSPEC | (ok ? INFO_WRITTEN : 0u) | (mixed ? INFO_MIXED : 0u);  // read by B
-      if (tile == 0) x.flag[parity] = 1u;  // B never takes its all-speculative exit
-    }
-  }
-  __syncthreads();
-  LDS_STAMP(6);
-  if (!s_ok) return;  // B walks the tile
-  // ---- 5: records into the (now free) image at their tile-local positions ----
-  uint32_t* s_tgt = reinterpret_cast<uint32_t*>(s_it);
-#pragma unroll
-  for (uint32_t r = 0; r < LIT_ROUNDS; ++r) {
-    const uint32_t k = r * TILE + tid;
-    if (k < nitems) {
-      const uint32_t rb = s_rbase[dl[r]];
-      if (rb != 0xffffffffu) {
-        const uint32_t pos = rb + (k - s_ibase[dl[r]]);
-        u32x4* q = s_img + pos * 4u;
-        q[0] = u32x4{R[r].d[0], R[r].d[1], R[r].d[2], R[r].d[3]};
-        q[1] = u32x4{R[r].d[4], R[r].d[5], R[r].d[6], R[r].d[7]};
-        q[2] = u32x4{R[r].d[8], R[r].d[9], R[r].d[10], R[r].d[11]};
-        q[3] = u32x4{R[r].d[12], R[r].d[13], R[r].d[14], R[r].d[15]};
-        s_tgt[pos] = tgt[r];
-      }
-    }
-  }
-  __syncthreads();
-  // ---- 6: coalesced copy-out: the tile's records are contiguous at excl ----
-  const uint64_t excl = s_excl;
-  const uint64_t lim = p.max_records > excl ? p.max_records - excl : 0ull;
-  const uint32_t nrec = s_agg < lim ? s_agg : (uint32_t)lim;
-  u32x4* dst = reinterpret_cast<u32x4*>(p.records + excl);
-  for (uint32_t q = tid; q < nrec * 4u; q += TILE) dst[q] = s_img[q];
-  if (p.target_out)
-    for (uint32_t q = tid; q < nrec; q += TILE) p.target_out[excl + q] = s_tgt[q];
-  LDS_STAMP(7);
-}
-
 #ifdef RTPS_ITEM_DIAG  // diagnostic variant builds only (scripts/diag_item_pass.py)
 #include "diag/item_pass_kernel.inc"
 #endif
@@ -2596,24 +1565,29 @@ struct rtps_rx_ctx {
   TopicState* topics = nullptr;   // topic caches (created on first use)
   uint64_t* chain = nullptr;      // look-back words of the chained launch [chain_words(tiles) + 2]
   uint32_t* mixed = nullptr;      // pinned: {mixed tiles, tiles} of the last finished batch (kernel B)
+#ifdef RTPS_DIAG_PASSES
   uint32_t ch_spin_limit = CH_SPIN_LIMIT;
+#else
+  uint32_t ch_spin_limit = 0;
+#endif
   uint32_t ch_epoch = 0;          // last chained launch's epoch (words start zeroed: epoch 0 is never used)
   uint32_t chain_tiles = 0;       // tiles the chain words are sized for
-  uint32_t mixed_pass = 2;        // pass for mixed traffic: 2 = item pass (E/S/W, default), 0 = chained lane walk (C),
-                                  // 1 = chained LDS tiles (D)
+  uint32_t mixed_pass = 2;        // pass for mixed traffic: 2 = the item pass (E / S / W2); diagnostic builds
+                                  // (RTPS_DIAG_PASSES): 0 = chained lane walk (C), 1 = LDS tiles (D), 3 = E' / W'
   u32x4* it_items = nullptr;      // item pass: wave slabs [tiles * WAVES * CAPW]
   uint32_t* it_wcnt = nullptr;    // item pass: items per wave slab [tiles * WAVES]
   uint64_t* it_prefix = nullptr;  // item pass: tile record prefixes [tiles]
   u32x4* it_dinfo = nullptr;      // item pass: per-datagram prologue of the record pass [tiles * TILE]
+  uint64_t* tc_ovf = nullptr;     // device u64: the ingest's window overflows when the caller asks for none
   uint64_t readers_version = 0;   // bumped by set_readers / set_match_table / set_topics (owner tables follow it)
-  uint32_t emit = 5;              // record pass: 1 = W (a workgroup per tile), 2 / 3 = W2 in slab order with
-                                  // a workgroup per tile / persistent (grid = resident workgroups), 4 / 5 = W2
-                                  // in record order, per tile / persistent
+  uint32_t emit = 2;              // record pass: 2 = W2 (rtps_parse_emit2_kernel); 1 = round 4's W (diagnostic builds)
   uint32_t emit_grid = 0, emit_grid_lds = ~0u;  // W2's resident grid and the LDS size it was computed for
   uint32_t it_tiles = 0;          // tiles the item-pass buffers are sized for
-  u32x4* rs_recs = nullptr;       // record-slab pass: wave slabs of records [tiles * WAVES * CAPR * 4]
+  u32x4* rs_recs = nullptr;       // (diagnostic builds) record-slab pass: wave slabs of records
   uint32_t* rs_meta = nullptr;    //   (j | lane << 16) per slab record
   uint32_t* rs_tgt = nullptr;     //   target set per slab record
+  uint32_t* rs_wcnt = nullptr;    //   records per wave slab
+  uint64_t* rs_prefix = nullptr;  //   tile record prefixes
   uint32_t rs_tiles = 0;
   // per-reader DataFrag assembly (frag_x_*): Lifespans by reader slot, the batch's receive time, the expansion
   int64_t* life = nullptr;        // [65536] device, NO_LIFESPAN where none
@@ -2661,6 +1635,9 @@ void rtps_ctx_owner_writers(const rtps_rx_ctx* c, bool by_topic, std::vector<uin
 }
 
 static int hip_fail(hipError_t e) { return e == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP; }
+#ifdef RTPS_DIAG_PASSES
+#include "diag/mixed_passes_host.inc"
+#endif
 
 extern "C" {
 
@@ -2675,10 +1652,12 @@ int rtps_rx_create(const rtps_rx_config* cfg, rtps_rx_ctx** out_ctx) {
   if (hipSetDevice(c->device) != hipSuccess) { delete c; return RTPS_RX_EHIP; }
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) { delete c; return RTPS_RX_EHIP; }
   c->stream = c->own_stream;
+#ifdef RTPS_DIAG_PASSES
   if (const char* e = getenv("RTPS_RX_MIXED_PASS"))  // A/B measurements
     c->mixed_pass = (e[0] == '1') ? 1u : (e[0] == '0') ? 0u : (e[0] == '3') ? 3u : 2u;
   if (const char* e = getenv("RTPS_RX_EMIT"))  // A/B measurements of the record pass
-    c->emit = (e[0] >= '1' && e[0] <= '5') ? (uint32_t)(e[0] - '0') : c->emit;
+    c->emit = (e[0] == '1') ? 1u : 2u;
+#endif
   {
     int cus = 0, per_cu = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess && cus > 0 &&
@@ -2686,15 +1665,19 @@ int rtps_rx_create(const rtps_rx_config* cfg, rtps_rx_ctx** out_ctx) {
         per_cu > 0)
       c->resident_blocks = (uint32_t)cus * (uint32_t)per_cu;
   }
-  // scratch and look-back words sized for the smallest tile (LT datagrams, kernel D)
+#ifdef RTPS_DIAG_PASSES  // scratch and look-back words sized for the smallest tile (LT datagrams, kernel D)
   size_t tiles = ((size_t)cfg->max_datagrams + LT - 1) / LT;
+  const size_t chain_bytes = chain_words((uint32_t)(tiles ? tiles : 1)) * sizeof(uint64_t);
+#else
+  size_t tiles = ((size_t)cfg->max_datagrams + TILE - 1) / TILE;
+  const size_t chain_bytes = 16;
+#endif
   if (tiles == 0) tiles = 1;
   // u32 flag[4] | u32 info[tiles rounded to 4] | u16 dcount[max_datagrams]
   c->scratch_words = 2 + ((tiles + 3) & ~(size_t)3) / 2 + ((size_t)cfg->max_datagrams + 3) / 4 + 2;
   if (hipMalloc(&c->scratch, c->scratch_words * sizeof(uint64_t)) != hipSuccess ||
       hipMemset(c->scratch, 0, c->scratch_words * sizeof(uint64_t)) != hipSuccess ||
-      hipMalloc(&c->chain, chain_words((uint32_t)tiles) * sizeof(uint64_t)) != hipSuccess ||
-      hipMemset(c->chain, 0, chain_words((uint32_t)tiles) * sizeof(uint64_t)) != hipSuccess ||
+      hipMalloc(&c->chain, chain_bytes) != hipSuccess || hipMemset(c->chain, 0, chain_bytes) != hipSuccess ||
       hipHostMalloc(&c->mixed, 2 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
     (void)hipFree(c->scratch);
     (void)hipFree(c->chain);
@@ -2722,7 +1705,8 @@ int rtps_rx_destroy(rtps_rx_ctx* c) {
   rtps_ingest_state_free(c->ingest);
   rtps_topic_state_free(c->topics);
   {
-    void* it[] = {c->it_items, c->it_wcnt, c->it_prefix, c->it_dinfo, c->rs_recs, c->rs_meta, c->rs_tgt};
+    void* it[] = {c->it_items, c->it_wcnt, c->it_prefix, c->it_dinfo, c->rs_recs, c->rs_meta, c->rs_tgt, c->rs_wcnt,
+                  c->rs_prefix, c->tc_ovf};
     for (void* q : it) if (q) (void)hipFree(q);
   }
   {
@@ -2812,8 +1796,10 @@ int rtps_rx_target_table(const rtps_rx_ctx* c, const uint32_t** first, const rtp
   return RTPS_RX_OK;
 }
 
-// phases: 1 = the first kernel (A or C), 2 = the finishing kernel B; *first_kernel (optional):
-// 1 = A (rtps_parse_spec_kernel) or 2 = C (rtps_parse_chain_kernel) was chosen
+// phases: 1 = the first kernel (A, or the item pass's walk E), 2 = the finishing kernels (B, or
+// the item pass's scan S and record pass W2; 2 | 4: W2 alone); *first_kernel (optional): the
+// first kernel chosen, 1 = A (rtps_parse_spec_kernel), 4 = E (rtps_parse_item_kernel); the
+// diagnostic builds' rejected passes (RTPS_DIAG_PASSES): 2 = C, 3 = D, 5 = E'
 static int parse_launch(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len, const uint64_t* dgram_off,
                         const uint32_t* dgram_len, uint32_t n, const rtps_rx_out* out, uint32_t phases,
                         uint32_t* first_kernel) {
@@ -2847,57 +1833,29 @@ static int parse_launch(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len
   p.chain = c->chain;
   p.mixed_out = c->mixed;
   p.ch_spin_limit = c->ch_spin_limit;
-  p.ch_epoch = 0u;  // set below for a chained launch
-  // Launch choice, a performance decision only (both give the same output): a
-  // chained single pass when the spec hint is 0, or when most tiles of the last
-  // finished batch were mixed (B reports that to pinned memory; read without a sync,
-  // so it may lag a batch); else the speculative pass.
+  p.ch_epoch = 0u;  // set below for a chained launch (diagnostic builds)
+  // Launch choice, a performance decision only (both give the same output): the item
+  // pass for mixed traffic when the spec hint is 0, or when most tiles of the last
+  // finished batch were mixed (reported to pinned memory; read without a sync, so it
+  // may lag a batch); else the speculative pass.
   const uint32_t mixed = __atomic_load_n(&c->mixed[0], __ATOMIC_RELAXED);
   const uint32_t seen = __atomic_load_n(&c->mixed[1], __ATOMIC_RELAXED);
-  const bool chain = c->k_spec == 0 || (seen >= 16u && 2u * mixed > seen);
+  const bool mixed_traffic = c->k_spec == 0 || (seen >= 16u && 2u * mixed > seen);
   const uint32_t k = c->k_spec ? c->k_spec : 1u;
-  const bool lds = chain && c->mixed_pass == 1u;
-  const bool item = chain && c->mixed_pass == 2u;
-  const bool rslab = chain && c->mixed_pass == 3u;
-  if (lds) tiles = (n + LT - 1) / LT;  // kernel D: tiles of LT datagrams (B follows the same tiling)
-  if (first_kernel) *first_kernel = rslab ? 5u : item ? 4u : lds ? 3u : chain ? 2u : 1u;
-  if (rslab) {  // E' (phases 1), then S and W' (phases 2); no kernel B
-    const uint32_t t = (uint32_t)(((size_t)c->max_datagrams + TILE - 1) / TILE) > tiles
-                           ? (uint32_t)(((size_t)c->max_datagrams + TILE - 1) / TILE) : tiles;
-    if (tiles > c->it_tiles || tiles > c->rs_tiles) {
-      if (hipStreamSynchronize(c->stream) != hipSuccess) return RTPS_RX_EHIP;
-      void* q[] = {c->it_wcnt, c->it_prefix, c->rs_recs, c->rs_meta, c->rs_tgt};
-      for (void* b : q) if (b) (void)hipFree(b);
-      c->it_wcnt = nullptr; c->it_prefix = nullptr; c->rs_recs = nullptr; c->rs_meta = nullptr; c->rs_tgt = nullptr;
-      c->rs_tiles = 0;
-      if (c->it_items) (void)hipFree(c->it_items);
-      c->it_items = nullptr; c->it_tiles = 0;
-      const size_t slots = (size_t)t * WAVES * CAPR;
-      if (hipMalloc(&c->rs_recs, slots * 4u * sizeof(u32x4)) != hipSuccess ||
-          hipMalloc(&c->rs_meta, slots * sizeof(uint32_t)) != hipSuccess ||
-          hipMalloc(&c->rs_tgt, slots * sizeof(uint32_t)) != hipSuccess ||
-          hipMalloc(&c->it_wcnt, (size_t)t * WAVES * sizeof(uint32_t)) != hipSuccess ||
-          hipMalloc(&c->it_prefix, (size_t)t * sizeof(uint64_t)) != hipSuccess)
-        return RTPS_RX_ENOMEM;
-      c->rs_tiles = t;
-    }
-    if (phases & 1u)
-      hipLaunchKernelGGL(rtps_parse_rslab_kernel, dim3(tiles), dim3(TILE), mt_lds, c->stream, p, tiles, k, c->rs_recs,
-                         c->rs_meta, c->rs_tgt, c->it_wcnt);
-    if (phases & 2u) {
-      hipLaunchKernelGGL(rtps_parse_scan_kernel, dim3(1), dim3(SCAN_T), 0, c->stream, p, tiles, parity, c->it_prefix);
-      hipLaunchKernelGGL(rtps_parse_rcopy_kernel, dim3(tiles), dim3(EMT), mt_lds, c->stream, p, tiles, c->rs_recs,
-                         c->rs_meta, c->rs_tgt, c->it_wcnt, c->it_prefix);
-    }
-    return hip_fail(hipGetLastError());
+  const bool item = mixed_traffic && c->mixed_pass == 2u;
+#ifdef RTPS_DIAG_PASSES
+  if (mixed_traffic && !item) {
+    const int rc = diag_mixed_launch(c, p, tiles, k, parity, mt_lds, phases, first_kernel);
+    return rc;
   }
-  if (item) {  // E (phases 1), then S and W (phases 2); no kernel B
+#endif
+  if (first_kernel) *first_kernel = item ? 4u : 1u;
+  if (item) {  // E (phases 1), then S and W2 (phases 2); no kernel B
     if (tiles > c->it_tiles || !c->it_items) {
       if (hipStreamSynchronize(c->stream) != hipSuccess) return RTPS_RX_EHIP;
       void* q[] = {c->it_items, c->it_wcnt, c->it_prefix, c->it_dinfo};
       for (void* b : q) if (b) (void)hipFree(b);
       c->it_items = nullptr; c->it_wcnt = nullptr; c->it_prefix = nullptr; c->it_dinfo = nullptr; c->it_tiles = 0;
-      c->rs_tiles = 0;  // (the wave counts and prefixes are shared)
       const uint32_t t = (uint32_t)(((size_t)c->max_datagrams + TILE - 1) / TILE) > tiles
                              ? (uint32_t)(((size_t)c->max_datagrams + TILE - 1) / TILE) : tiles;
       if (hipMalloc(&c->it_items, (size_t)t * WAVES * CAPW * IW * sizeof(u32x4)) != hipSuccess ||
@@ -2907,12 +1865,11 @@ static int parse_launch(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len
         return RTPS_RX_ENOMEM;
       c->it_tiles = t;
     }
-    const bool w2 = c->emit != 1u, rec_order = c->emit >= 4u, persist = c->emit == 3u || c->emit == 5u;
-    if (w2 && persist && c->emit_grid_lds != mt_lds) {  // resident W2 workgroups for this LDS size
+    const bool w2 = c->emit == 2u;  // (1: the round-4 record pass W, diagnostic builds)
+    if (w2 && c->emit_grid_lds != mt_lds) {  // resident W2 workgroups for this LDS size
       int cus = 0, per_cu = 0;
       if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess ||
-          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rtps_parse_emit2_kernel<true>, EM2T, mt_lds) !=
-              hipSuccess)
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rtps_parse_emit2_kernel, EM2T, mt_lds) != hipSuccess)
         return RTPS_RX_EHIP;
       c->emit_grid = (uint32_t)(cus > 0 ? cus : 1) * (uint32_t)(per_cu > 0 ? per_cu : 1);
       c->emit_grid_lds = mt_lds;
@@ -2926,46 +1883,25 @@ static int parse_launch(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len
                            c->it_prefix);
       if (w2) {
         const uint32_t groups = (tiles + EM2_TPB - 1) / EM2_TPB;
-        const uint32_t g = (persist && c->emit_grid < groups) ? c->emit_grid : groups;
-        if (rec_order)
-          hipLaunchKernelGGL(rtps_parse_emit2_kernel<true>, dim3(g), dim3(EM2T), mt_lds, c->stream, p, tiles,
-                             c->it_items, c->it_wcnt, c->it_prefix, c->it_dinfo);
-        else
-          hipLaunchKernelGGL(rtps_parse_emit2_kernel<false>, dim3(g), dim3(EM2T), mt_lds, c->stream, p, tiles,
-                             c->it_items, c->it_wcnt, c->it_prefix, c->it_dinfo);
+        const uint32_t g = c->emit_grid < groups ? c->emit_grid : groups;
+        hipLaunchKernelGGL(rtps_parse_emit2_kernel, dim3(g), dim3(EM2T), mt_lds, c->stream, p, tiles, c->it_items,
+                           c->it_wcnt, c->it_prefix, c->it_dinfo);
       } else {
+#ifdef RTPS_DIAG_PASSES
         hipLaunchKernelGGL(rtps_parse_emit_kernel, dim3(tiles), dim3(EMT), mt_lds, c->stream, p, tiles, c->it_items,
                            c->it_wcnt, c->it_prefix);
+#else
+        return RTPS_RX_EINVAL;
+#endif
       }
     }
     return hip_fail(hipGetLastError());
   }
-  if (!(phases & 1u)) {
-  } else if (chain) {  // one chained pass, B only finishes (n_records, stragglers)
-    // the look-back words carry this launch's epoch, so they need no zeroing; only
-    // when the 32-bit epoch wraps are stale words of the same epoch possible
-    if (++c->ch_epoch == 0u) {
-      c->ch_epoch = 1u;
-      if (hipMemsetAsync(c->chain, 0, chain_words(c->chain_tiles) * sizeof(uint64_t), c->stream) != hipSuccess)
-        return RTPS_RX_EHIP;
-    }
-    p.ch_epoch = c->ch_epoch;
-    if (lds) {
-      KParams pd = p;
-      if (!RTPS_LDS_RT) pd.rt_lds = 0u;  // occupancy: the image needs the LDS
-      hipLaunchKernelGGL(rtps_parse_lds_kernel, dim3(tiles), dim3(TILE), pd.rt_lds ? mt_lds : 0u, c->stream, pd,
-                         tiles, k, parity);
-    }
-    else
-      hipLaunchKernelGGL(rtps_parse_chain_kernel, dim3(tiles), dim3(TILE), mt_lds, c->stream, p, tiles, k, parity);
-  } else {
+  if (phases & 1u)
     hipLaunchKernelGGL(rtps_parse_spec_kernel, dim3(tiles), dim3(TILE), mt_lds, c->stream, p, tiles, c->k_spec,
                        parity);
-  }
-  uint32_t grid = tiles < c->resident_blocks ? tiles : c->resident_blocks;
-  if ((phases & 2u) && lds)
-    hipLaunchKernelGGL(rtps_parse_fix_kernel<LT>, dim3(grid), dim3(TILE), mt_lds, c->stream, p, tiles, k, parity);
-  else if (phases & 2u)
+  const uint32_t grid = tiles < c->resident_blocks ? tiles : c->resident_blocks;
+  if (phases & 2u)
     hipLaunchKernelGGL(rtps_parse_fix_kernel<TILE>, dim3(grid), dim3(TILE), mt_lds, c->stream, p, tiles, k, parity);
   return hip_fail(hipGetLastError());
 }
@@ -3305,13 +2241,19 @@ int rtps_rx_ingest(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len, con
     c->ingest = rtps_ingest_state_new(c->device);
     if (!c->ingest) return RTPS_RX_ENOMEM;
   }
+  // with the topic caches, the batch's window-overflow count goes where the topic step reads it
+  rtps_ingest_out o = *out;
+  if ((flags & RTPS_INGEST_TOPIC_CACHE) && !o.n_window_overflow) {
+    if (!c->tc_ovf && hipMalloc(&c->tc_ovf, sizeof(uint64_t)) != hipSuccess) return RTPS_RX_ENOMEM;
+    o.n_window_overflow = c->tc_ovf;
+  }
   int rc = rtps_ingest_batch(c->ingest, c->stream, rd, arena, arena_len, dgram_off, records, n_records, max_records,
-                             frag, n_frag, max_frag, flags & ~RTPS_INGEST_TOPIC_CACHE, out);
+                             frag, n_frag, max_frag, flags & ~RTPS_INGEST_TOPIC_CACHE, &o);
   if (rc || !(flags & RTPS_INGEST_TOPIC_CACHE)) return rc;
   // the topic caches' add_change over the deliveries (rtps_topic.hip)
   rc = topics_state(c);
-  return rc ? rc : rtps_topic_apply(c->topics, c->stream, records, n_records, max_records, out->accepted,
-                                    out->n_accepted, out->max_accepted);
+  return rc ? rc : rtps_topic_apply(c->topics, c->stream, records, n_records, max_records, o.accepted,
+                                    o.n_accepted, o.max_accepted, o.n_window_overflow);
 }
 
 /* test / measurement hook (not part of the public header): the ingest's
@@ -3372,15 +2314,20 @@ uint32_t rtps_rx_record_size(void) { return (uint32_t)sizeof(rtps_record); }
    leaves itself to kernel B; 0 makes most tiles give up, exercising that fallback */
 int rtps_rx_debug_set_chain_spin_limit(rtps_rx_ctx* c, uint32_t limit) {
   if (!c) return RTPS_RX_EINVAL;
+#ifdef RTPS_DIAG_PASSES
   c->ch_spin_limit = limit;
   return RTPS_RX_OK;
+#else
+  (void)limit;
+  return RTPS_RX_EINVAL;  // (no chained pass in the product build)
+#endif
 }
 
-/* tuning hook (not part of the public header): kernel D's per-tile phase stamps
-   (s_memrealtime, 100 MHz; STAMP_N per tile) of the last launch, in builds with
-   RTPS_LDS_STAMPS; RTPS_RX_EINVAL otherwise */
+/* tuning hook (not part of the public header): per-tile phase stamps (s_memrealtime,
+   100 MHz; STAMP_N per tile) of the last launch of kernel D or W, in diagnostic builds
+   with RTPS_LDS_STAMPS / RTPS_EM_STAMPS; RTPS_RX_EINVAL otherwise */
 int rtps_rx_debug_lds_stamps(rtps_rx_ctx* c, uint64_t* host, uint64_t n) {
-#if defined(RTPS_LDS_STAMPS) || defined(RTPS_EM_STAMPS)
+#if defined(RTPS_DIAG_PASSES) && (defined(RTPS_LDS_STAMPS) || defined(RTPS_EM_STAMPS))
   if (!c || !host) return RTPS_RX_EINVAL;
   if (n > (uint64_t)STAMP_TILES * STAMP_N) n = (uint64_t)STAMP_TILES * STAMP_N;
   (void)hipSetDevice(c->device);
@@ -3393,31 +2340,45 @@ int rtps_rx_debug_lds_stamps(rtps_rx_ctx* c, uint64_t* host, uint64_t n) {
 }
 
 /* test / measurement hook (not part of the public header): the pass used for mixed
-   traffic, 2 = the item pass (rtps_parse_item_kernel / scan / emit, the default),
-   0 = the chained lane walk in global memory (rtps_parse_chain_kernel), 1 = chained
-   LDS tiles (rtps_parse_lds_kernel).  Same results. */
+   traffic, 2 = the item pass (rtps_parse_item_kernel / scan / emit2, the product's only
+   one); diagnostic builds (RTPS_DIAG_PASSES) also 0 = the chained lane walk
+   (rtps_parse_chain_kernel), 1 = LDS tiles (rtps_parse_lds_kernel), 3 = the record-slab
+   pass.  Same results.  RTPS_RX_EINVAL for a pass this build does not have. */
 int rtps_rx_debug_set_mixed_pass(rtps_rx_ctx* c, uint32_t pass) {
+#ifdef RTPS_DIAG_PASSES
   if (!c || pass > 3u) return RTPS_RX_EINVAL;
+#else
+  if (!c || pass != 2u) return RTPS_RX_EINVAL;
+#endif
   c->mixed_pass = pass;
   return RTPS_RX_OK;
 }
 
 /* test / measurement hook (not part of the public header): the item pass's record pass,
-   1 = rtps_parse_emit_kernel (a workgroup per tile), 2 = rtps_parse_emit2_kernel with a
-   workgroup per tile, 3 = rtps_parse_emit2_kernel persistent (the default).  Same results.
-   Returns the pass in effect (0 selects nothing new), or RTPS_RX_EINVAL. */
+   2 = rtps_parse_emit2_kernel (the product's); diagnostic builds also 1 = round 4's
+   rtps_parse_emit_kernel.  Same results.  Returns the pass in effect (0 selects nothing
+   new), or RTPS_RX_EINVAL for a pass this build does not have. */
 int rtps_rx_debug_emit(rtps_rx_ctx* c, uint32_t emit) {
-  if (!c || emit > 5u) return RTPS_RX_EINVAL;
+#ifdef RTPS_DIAG_PASSES
+  if (!c || emit > 2u) return RTPS_RX_EINVAL;
+#else
+  if (!c || (emit != 0u && emit != 2u)) return RTPS_RX_EINVAL;
+#endif
   if (emit) c->emit = emit;
   return (int)c->emit;
 }
 
 /* test hook (not part of the public header): the last chained launch's epoch, so
-   that a test can run chained launches across the 32-bit wrap */
+   that a test can run chained launches across the 32-bit wrap (diagnostic builds) */
 int rtps_rx_debug_set_chain_epoch(rtps_rx_ctx* c, uint32_t epoch) {
   if (!c) return RTPS_RX_EINVAL;
+#ifdef RTPS_DIAG_PASSES
   c->ch_epoch = epoch;
   return RTPS_RX_OK;
+#else
+  (void)epoch;
+  return RTPS_RX_EINVAL;
+#endif
 }
 
 #ifdef RTPS_ITEM_DIAG

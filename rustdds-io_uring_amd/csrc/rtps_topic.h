@@ -32,5 +32,9 @@ int rtps_topic_gc(TopicState* s, hipStream_t st);
 uint32_t rtps_topic_of_slot(const TopicState* s, uint16_t slot);
 // TopicCache::add_change for every delivery of the batch, in order: sets or clears
 // RTPS_DELIVERY_CACHED in del[k].flags (asynchronous).
+// ovf (device u64, optional): the batch's ingest window overflows; non-zero = some samples were
+// accepted without the proxies' duplicate check, so no delivery is stored unchecked ("certain"):
+// every one is checked against the topic's live changes.
 int rtps_topic_apply(TopicState* s, hipStream_t st, const rtps_record* recs, const uint64_t* n_records,
-                     uint64_t max_records, rtps_delivery* del, const uint64_t* n_del, uint64_t max_del);
+                     uint64_t max_records, rtps_delivery* del, const uint64_t* n_del, uint64_t max_del,
+                     const uint64_t* ovf = nullptr);

@@ -220,6 +220,7 @@ struct TDev {
   uint32_t *segb, *sege, *frb, *fre;  // [nA]
   uint64_t* ibase;    // [nA] I of the topic at the batch start
   uint64_t* n_full;   // live-index inserts that found no room (0)
+  const uint64_t* ovf;  // the ingest's window overflows of the batch (nullptr: none): all candidates
   uint64_t* n_used;   // claimed live-index slots
 };
 constexpr uint8_t FL_GC = 1, FL_CAND = 2, FL_REP0 = 4, FL_PLIVE = 8, FL_VALID = 16;
@@ -275,7 +276,9 @@ __global__ __launch_bounds__(TT) void tc_mark(TDev d, uint64_t max_del) {
       const bool rep0 = p > 0 && pos_cid(d, p - 1) == c && d.kp[pos_k(d, p - 1)].rec == x.rec;
       const uint32_t t = x.tid;
       const bool user_kind = ((x.g[3] >> 24) & 0xf0u) == 0u;  // EntityKind::is_user_defined (guid.rs:168-170)
-      const bool cand = !d.simple[t] || d.E[t] < d.until[t] || !user_kind;
+      // (a batch whose ingest overflowed its capacities may hold duplicates the proxies did not
+      // see: every delivery is checked then)
+      const bool cand = !d.simple[t] || d.E[t] < d.until[t] || !user_kind || (d.ovf && *d.ovf != 0u);
       if (rep0) {
         f |= FL_REP0;
       } else if (!cand) {
@@ -715,7 +718,8 @@ static int reserve_scratch(TopicState* s, uint64_t n, hipStream_t st) {
 }
 
 int rtps_topic_apply(TopicState* s, hipStream_t st, const rtps_record* recs, const uint64_t* n_records,
-                     uint64_t max_records, rtps_delivery* del, const uint64_t* n_del, uint64_t max_del) {
+                     uint64_t max_records, rtps_delivery* del, const uint64_t* n_del, uint64_t max_del,
+                     const uint64_t* ovf) {
   if (max_del == 0) return RTPS_RX_OK;
   if (max_del > 0x7fffffffull) return RTPS_RX_ETOOBIG;
   if (!s->I) return RTPS_RX_EINVAL;  // no readers known yet
@@ -736,6 +740,7 @@ int rtps_topic_apply(TopicState* s, hipStream_t st, const rtps_record* recs, con
   d.frins = s->frins; d.frlist = s->frlist; d.nfr = s->nfr; d.frcum = s->frcum; d.fridx = s->fridx;
   d.segb = s->segb; d.sege = s->sege; d.frb = s->frb; d.fre = s->fre; d.ibase = s->ibase; d.n_full = s->n_full;
   d.n_used = s->n_used;
+  d.ovf = ovf;
   const uint32_t g = (uint32_t)((max_del + TT - 1) / TT < 8192 ? (max_del + TT - 1) / TT : 8192);
   if (s->nA && hipMemsetAsync(s->segb, 0xff, s->nA * 4ull, st) != hipSuccess) return RTPS_RX_EHIP;
   hipLaunchKernelGGL(tc_gather, dim3(g), dim3(TT), 0, st, d, recs, n_records, max_records, del, n_del, max_del);

@@ -43,6 +43,17 @@ PY
     topic)
       timeout -k 10 900 $PYT tests/test_topic_gpu.py tests/test_cdr_gpu.py > $O/topic.log 2>&1 || { grep -E "FAILED|Error" $O/topic.log | head; tail -30 $O/topic.log; exit 8; }
       tail -2 $O/topic.log ;;
+    rccl_probe)
+      timeout -k 10 300 python -m torch.distributed.run --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 scripts/rccl_size_probe.py > $O/rccl_probe.log 2>&1 || { tail -20 $O/rccl_probe.log; exit 9; }
+      grep rccl_p2p_size_probe $O/rccl_probe.log ;;
+    bench_T|bench_C3|bench_C2|bench_C4)
+      wl=${step#bench_}; extra=""
+      [ $wl = T ] || extra="--no-c1"
+      timeout -k 10 600 python bench.py --workload $wl --steps 20 --warmup 5 $extra > $O/bench_$wl.json 2> $O/bench_$wl.err || { tail -20 $O/bench_$wl.err; exit 10; }
+      python scripts/bench_summary.py $O/bench_$wl.json ;;
+    diag_tests)  # the rejected mixed passes, in their diagnostic build (make variant NAME=passes VDEFS=-DRTPS_DIAG_PASSES)
+      RTPS_RX_LIB=$R/rustdds-io_uring_amd/variants/librtps_rx_passes.so RTPS_RX_DIAG_PASSES=1 timeout -k 10 900 $PYT tests/diag_mixed_passes.py tests/test_gpu_parity.py -k "mixed or record_passes or lds_tile or chained" > $O/diag_tests.log 2>&1 || { grep -E "FAILED|Error" $O/diag_tests.log | head; tail -20 $O/diag_tests.log; exit 11; }
+      tail -2 $O/diag_tests.log ;;
     gpu_tests)
       timeout -k 10 1000 $PYT tests -m gpu > $O/gpu_tests.log 2>&1 || { grep -E "FAILED|Error" $O/gpu_tests.log | head; tail -5 $O/gpu_tests.log; exit 5; }
       tail -2 $O/gpu_tests.log ;;
