@@ -313,10 +313,12 @@ extern "C" int diag_ceiling_hops(int walks, const uint8_t* arena, uint64_t arena
 // record read (one 16-B load per lane of a quad: the record's four quads by four lanes, so a
 // wave reads 16 records back to back), 1 accept byte written per record; per EVENT (a writer
 // record that passes and reaches a proxy: DATA / HEARTBEAT / GAP with MATCHED) the proxy's 8-B
-// state read and 4 B of its change-set bitmap touched at the SN's bit (atomic OR, the
-// window's layout: 2^17 bits per proxy); per DELIVERY (a DATA sample with a proxy) 8 B
-// written, appended in wave order (one atomic per wave).  The proxy is the record's target set
-// (one proxy per writer set when one reader subscribes to every writer, as in bench.py).
+// state read and 4 B of its change-set bitmap written at the SN's word (a plain store: the
+// traffic, not the atomics; the window's layout: 2^17 bits per proxy); per DELIVERY (a DATA
+// sample with a proxy) 8 B written at the record's index (the deliveries' compaction is a
+// scan in the ingest; a counter here would serialise on one address).  The proxy is the
+// record's target set (one proxy per writer set when one reader subscribes to every writer,
+// as in bench.py).
 constexpr uint32_t ING_WW = (1u << 17) / 32u;  // change-set words per proxy
 __global__ __launch_bounds__(256) void ceil_ingest_kernel(const u32x4* rec, const uint32_t* target, uint64_t n_rec,
                                                           const uint64_t* state, uint32_t* bits, uint8_t* accept,
@@ -341,15 +343,10 @@ __global__ __launch_bounds__(256) void ceil_ingest_kernel(const u32x4* rec, cons
   if (event) {
     const uint32_t e = target[i] < n_sets ? target[i] : 0u;
     const uint64_t st = state[e];
-    atomicOr(bits + (uint64_t)e * ING_WW + ((sn + (uint32_t)st) & ((1u << 17) - 1u)) / 32u, 1u << (sn & 31u));
+    bits[(uint64_t)e * ING_WW + ((sn + (uint32_t)st) & ((1u << 17) - 1u)) / 32u] = 1u << (sn & 31u);
   }
-  const uint64_t m = __ballot(del);
-  uint64_t base = 0;
-  if (m) {
-    if (lane == (uint32_t)__builtin_ctzll(m)) base = atomicAdd(n_del, (unsigned long long)__popcll(m));
-    base = __shfl(base, (uint32_t)__builtin_ctzll(m), 64);
-    if (del) dels[base + __popcll(m & ((1ull << lane) - 1ull))] = i | ((uint64_t)1 << 32);
-  }
+  if (del) dels[i] = i | ((uint64_t)1 << 32);
+  (void)n_del;
 }
 extern "C" int diag_ceiling_ingest(const void* rec, const uint32_t* target, uint64_t n_rec, const uint64_t* state,
                                    uint32_t* bits, uint8_t* accept, uint64_t* dels, uint64_t* n_del, uint32_t n_sets,

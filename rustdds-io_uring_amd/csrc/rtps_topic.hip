@@ -77,7 +77,8 @@ struct BEnt {
   uint32_t g[4];
   uint32_t snlo, snhi, tid, _p;
   uint64_t last;   // NO_IDX until the resolver stores a repeat of the key
-  uint64_t _q;
+  uint32_t nrep;   // the key's repeats in this batch (tc_class)
+  uint32_t _q;
 };
 static_assert(sizeof(PEnt) == 48 && sizeof(BEnt) == 64, "entries");
 
@@ -169,6 +170,7 @@ __device__ void b_put(BEnt* B, uint64_t mask, uint32_t epoch, const KeyP& k, uin
       if (atomicCAS(reinterpret_cast<unsigned long long*>(&e.tag), cur, (unsigned long long)tag) == cur) {
         put_key(e, k);
         e.last = NO_IDX;
+        e.nrep = 0;
         atomicExch(&e.minp, p);
         st_rel(&e.ready, epoch);
         done = true;
@@ -221,6 +223,15 @@ struct TDev {
   uint64_t* ibase;    // [nA] I of the topic at the batch start
   uint64_t* n_full;   // live-index inserts that found no room (0)
   const uint64_t* ovf;  // the ingest's window overflows of the batch (nullptr: none): all candidates
+  // repeats decided in parallel (tc_rdec): per repeat j the decision, the exclusive count of the
+  // sure stores before it; the undecided ones (AMB) in order, with their stores' running count
+  uint8_t* rdec;      // [nfr] RD_HOLD / RD_STORE / RD_AMB
+  uint32_t *rst, *rpre;   // [nfr] 1 = sure store; exclusive scan of rst
+  uint8_t* ramb;      // [nfr] 1 = undecided
+  uint32_t* amb;      // [namb] the undecided repeats' j, ascending
+  uint64_t* namb;
+  uint32_t* acum;     // [namb] stored undecided repeats up to amb[a] (inclusive), written in order
+  uint32_t *ab, *ae;  // [nA] the topic's range of amb[]
   uint64_t* n_used;   // claimed live-index slots
 };
 constexpr uint8_t FL_GC = 1, FL_CAND = 2, FL_REP0 = 4, FL_PLIVE = 8, FL_VALID = 16;
@@ -304,10 +315,14 @@ __global__ __launch_bounds__(TT) void tc_class(TDev d, uint64_t max_del) {
     const uint8_t f = d.fl[p];
     if (!(f & FL_CAND)) continue;
     const KeyP x = d.kp[pos_k(d, p)];
-    const BEnt* e = b_find(d.B, d.bmask, d.epoch, x);
+    BEnt* e = b_find(d.B, d.bmask, d.epoch, x);
     const bool rep = (e && e->minp < (uint32_t)p) || (f & FL_PLIVE);
-    if (rep) d.fr[p] = 1;
-    else d.kins[p] = 1;
+    if (rep) {
+      d.fr[p] = 1;
+      if (e) atomicAdd(&e->nrep, 1u);
+    } else {
+      d.kins[p] = 1;
+    }
   }
 }
 
@@ -319,7 +334,83 @@ __device__ __forceinline__ uint32_t lower_bound(const uint32_t* a, uint32_t lo, 
   return lo;
 }
 
-// one thread per topic of the batch: its repeats in order, the GC boundary, the new I / E
+// Repeats.  Whether the topic still holds a repeat's key when it arrives depends on the
+// insertions before it, repeats included, so the reference's add_change is sequential.  Most
+// repeats are decided without that order: with I(q) the insertion count before position q (the
+// sure insertions, kpre, plus the stored repeats before q, Rb(q)), the topic's E at p is
+// max(E0, I(g) - K) for the last GC position g <= p of the segment (I is non-decreasing), and
+// the key is held iff its last insertion L >= E.  For a key with ONE repeat in the batch, L is
+// its first occurrence's insertion I(f) or its live-index entry; Rb(g) - Rb(f) lies in
+// [0, repeats in [f, g)), so the decision is sure when both ends of that range agree:
+//   first occurrence f < g:  held iff (kpre[g] - kpre[f]) + (Rb(g) - Rb(f)) <= K;
+//   f >= g, or no GC yet:    held (I(f) >= I(g) >= I(g) - K, and I(f) >= I0 >= E0);
+//   live entry idx (< I0):   held iff idx >= max(E0, I(g) - K), Rb(g) in [0, repeats before g].
+// The rest (keys with several repeats, ranges that straddle K) go to tc_resolve, one thread per
+// topic, in order: Rb then counts the sure stores (an exclusive scan) plus the undecided ones
+// already stored.  (The SPDP reader with half of a 1M batch repeats: 1.9 s when every repeat
+// was resolved in order, round 4's form.)
+constexpr uint8_t RD_HOLD = 0, RD_STORE = 1, RD_AMB = 2;
+__global__ __launch_bounds__(TT) void tc_rdec(TDev d) {
+  const uint32_t nfr = (uint32_t)*d.nfr;
+  for (uint32_t j = blockIdx.x * TT + threadIdx.x; j < nfr; j += gridDim.x * TT) {
+    const uint32_t p = d.frlist[j];
+    const uint32_t c = pos_cid(d, p);
+    const uint32_t t = d.cid_tid[c];
+    const uint32_t b = d.segb[c];
+    const uint32_t jb = lower_bound(d.frlist, 0, j, b);  // the topic's first repeat
+    const KeyP x = d.kp[pos_k(d, p)];
+    const BEnt* be = b_find(d.B, d.bmask, d.epoch, x);
+    uint8_t dec = RD_AMB;
+    if (be && be->nrep == 1u) {
+      const uint64_t K = d.K[t], E0 = d.E[t], I0 = d.I[t];
+      const uint32_t kb = d.kpre[b];
+      const int64_t g = d.lgc[p];
+      const bool gc = g >= (int64_t)b;  // a GC of this topic at or before p
+      const PEnt* pe = p_find(d.P, d.pmask, x);
+      const uint32_t f = be->minp;
+      const bool has_f = f < p && d.kins[f];
+      // live entry: sure held / sure not held
+      int live = -1;  // -1 none, 0 not held, 1 held, 2 unsure
+      if (pe) {
+        if (!gc) {
+          live = pe->idx >= E0 ? 1 : 0;
+        } else {
+          const uint64_t Ig_lo = I0 + (d.kpre[g] - kb);
+          const uint64_t Ig_hi = Ig_lo + (lower_bound(d.frlist, jb, j, (uint32_t)g) - jb);
+          const uint64_t E_lo = Ig_lo > K && Ig_lo - K > E0 ? Ig_lo - K : E0;
+          const uint64_t E_hi = Ig_hi > K && Ig_hi - K > E0 ? Ig_hi - K : E0;
+          live = pe->idx >= E_hi ? 1 : pe->idx < E_lo ? 0 : 2;
+        }
+      }
+      int first = -1;
+      if (has_f) {
+        if (!gc || f >= (uint32_t)g) {
+          first = 1;
+        } else {
+          const uint64_t A = d.kpre[g] - d.kpre[f];
+          const uint64_t D = lower_bound(d.frlist, jb, j, (uint32_t)g) - lower_bound(d.frlist, jb, j, f);
+          first = A + D <= K ? 1 : A > K ? 0 : 2;
+        }
+      }
+      if (live == 1 || first == 1) dec = RD_HOLD;                     // some last insertion is held
+      else if (live != 2 && first != 2) dec = RD_STORE;                // none is (or there is none)
+    }
+    d.rdec[j] = dec;
+    d.rst[j] = dec == RD_STORE ? 1u : 0u;
+    d.ramb[j] = dec == RD_AMB ? 1u : 0u;
+  }
+}
+
+// stored repeats of the topic before position q (q within the topic's segment; j: the first
+// repeat at or past q is searched in [jb, jcur)): the sure ones plus the undecided ones stored
+__device__ __forceinline__ uint32_t rep_before(const TDev& d, uint32_t q, uint32_t jb, uint32_t jcur, uint32_t ab,
+                                               uint32_t acur) {
+  const uint32_t jq = lower_bound(d.frlist, jb, jcur, q);
+  const uint32_t aq = lower_bound(d.amb, ab, acur, jq);  // undecided repeats before jq
+  return (d.rpre[jq] - d.rpre[jb]) + (aq > ab ? d.acum[aq - 1] : 0u);
+}
+
+// one thread per topic of the batch: its undecided repeats in order, then the new I / E
 __global__ __launch_bounds__(TT) void tc_resolve(TDev d) {
   const uint32_t c = blockIdx.x * TT + threadIdx.x;
   if (c >= d.nA) return;
@@ -327,30 +418,26 @@ __global__ __launch_bounds__(TT) void tc_resolve(TDev d) {
   const uint64_t I0 = d.I[t];
   d.ibase[c] = I0;
   const uint32_t b = d.segb[c], e = d.sege[c];
-  if (b == NONE) { d.frb[c] = d.fre[c] = 0; return; }
-  const uint64_t K = d.K[t];
-  uint64_t E = d.E[t];
-  const uint32_t nfr = (uint32_t)*d.nfr;
+  if (b == NONE) { d.frb[c] = d.fre[c] = 0; d.ab[c] = d.ae[c] = 0; return; }
+  const uint64_t K = d.K[t], E0 = d.E[t];
+  const uint32_t nfr = (uint32_t)*d.nfr, na = (uint32_t)*d.namb;
   const uint32_t jb = lower_bound(d.frlist, 0, nfr, b), je = lower_bound(d.frlist, jb, nfr, e);
+  const uint32_t ab = lower_bound(d.amb, 0, na, jb), ae = lower_bound(d.amb, ab, na, je);
   d.frb[c] = jb;
   d.fre[c] = je;
+  d.ab[c] = ab;
+  d.ae[c] = ae;
   const uint32_t kb = d.kpre[b];
-  uint32_t R = 0;
-  int64_t last_g = -1;
-  // inserted repeats before position q (q <= the current repeat's position)
-  auto ins_before = [&](uint32_t q, uint32_t jcur) -> uint32_t {
-    const uint32_t jq = lower_bound(d.frlist, jb, jcur, q);
-    return jq > jb ? d.frcum[jq - 1] : 0u;
+  uint32_t RA = 0;  // undecided repeats stored so far
+  auto E_at = [&](int64_t g, uint32_t jcur, uint32_t acur) -> uint64_t {  // E after the GCs up to g
+    if (g < (int64_t)b) return E0;
+    const uint64_t Ig = I0 + (d.kpre[g] - kb) + rep_before(d, (uint32_t)g, jb, jcur, ab, acur);
+    return Ig > K && Ig - K > E0 ? Ig - K : E0;
   };
-  auto gc_to = [&](int64_t g, uint32_t jcur) {  // the GC at position g (remove_changes_before(ZERO))
-    if (g < (int64_t)b || g <= last_g) return;
-    const uint64_t Ig = I0 + (d.kpre[g] - kb) + ins_before((uint32_t)g, jcur);
-    if (Ig > K && Ig - K > E) E = Ig - K;
-    last_g = g;
-  };
-  for (uint32_t j = jb; j < je; ++j) {
+  for (uint32_t a = ab; a < ae; ++a) {
+    const uint32_t j = d.amb[a];
     const uint32_t p = d.frlist[j];
-    gc_to(d.lgc[p], j);
+    const uint64_t E = E_at(d.lgc[p], j, a);
     const KeyP x = d.kp[pos_k(d, p)];
     BEnt* be = b_find(d.B, d.bmask, d.epoch, x);
     // the key's last insertion before p: a stored repeat, its first occurrence (stored unless a
@@ -361,24 +448,43 @@ __global__ __launch_bounds__(TT) void tc_resolve(TDev d) {
     if (be) {
       const uint32_t f = be->minp;
       if (f < p && d.kins[f]) {
-        const uint64_t If = I0 + (d.kpre[f] - kb) + ins_before(f, j);
+        const uint64_t If = I0 + (d.kpre[f] - kb) + rep_before(d, f, jb, j, ab, a);
         if (L == NO_IDX || If > L) L = If;
       }
       if (be->last != NO_IDX && (L == NO_IDX || be->last > L)) L = be->last;
     }
-    const uint64_t Ip = I0 + (d.kpre[p] - kb) + R;
     const bool held = L != NO_IDX && L >= E;  // find_by_sn (:241-252, 270-276)
     if (!held) {
+      const uint64_t Ip = I0 + (d.kpre[p] - kb) + (d.rpre[j] - d.rpre[jb]) + RA;
       d.frins[p] = 1;
       d.fridx[p] = Ip;
       if (be) be->last = Ip;
-      ++R;
+      ++RA;
     }
-    d.frcum[j] = R;
+    d.acum[a] = RA;
   }
-  gc_to(d.lgc[e - 1], je);
-  d.I[t] = I0 + (d.kpre[e - 1] + d.kins[e - 1] - kb) + R;
+  const uint64_t E = E_at(d.lgc[e - 1], je, ae);
+  d.I[t] = I0 + (d.kpre[e - 1] + d.kins[e - 1] - kb) + (d.rpre[je] - d.rpre[jb]) + RA;
   d.E[t] = E;
+}
+
+// per repeat: the sure stores' insertion (index: the insertions before it, repeats included)
+// and every repeat's running count of stored repeats in its topic (frcum, for tc_final)
+__global__ __launch_bounds__(TT) void tc_rfill(TDev d) {
+  const uint32_t nfr = (uint32_t)*d.nfr;
+  for (uint32_t j = blockIdx.x * TT + threadIdx.x; j < nfr; j += gridDim.x * TT) {
+    const uint32_t p = d.frlist[j];
+    const uint32_t c = pos_cid(d, p);
+    const uint32_t jb = d.frb[c], ab = d.ab[c], ae = d.ae[c];
+    const uint32_t aq = lower_bound(d.amb, ab, ae, j + 1u);  // undecided repeats up to j
+    const uint32_t before = (d.rpre[j] - d.rpre[jb]) + (aq > ab ? d.acum[aq - 1] : 0u) -
+                            ((aq > ab && d.amb[aq - 1] == j && d.frins[p]) ? 1u : 0u);
+    if (d.rdec[j] == RD_STORE) {
+      d.frins[p] = 1;
+      d.fridx[p] = d.ibase[c] + (d.kpre[p] - d.kpre[d.segb[c]]) + before;
+    }
+    d.frcum[j] = before + (d.frins[p] ? 1u : 0u);
+  }
 }
 
 // per position: the flag on the delivery, survivors into the live index
@@ -462,6 +568,10 @@ struct TopicState {
   uint64_t *fridx = nullptr, *nfr = nullptr, *n_full = nullptr;
   uint32_t *segb = nullptr, *sege = nullptr, *frb = nullptr, *fre = nullptr;
   uint64_t* ibase = nullptr;
+  uint8_t *rdec = nullptr, *ramb = nullptr;                         // [n] parallel repeat decisions
+  uint32_t *rst = nullptr, *rpre = nullptr, *amb = nullptr, *acum = nullptr;  // [n + 1]
+  uint64_t* namb = nullptr;
+  uint32_t *ab = nullptr, *ae = nullptr;  // [nA]
   uint32_t acap = 0;  // [nA] arrays' capacity
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
@@ -478,6 +588,7 @@ static void free_scratch(TopicState* s) {
   dfree(s->kp); dfree(s->skey); dfree(s->skey2); dfree(s->sval); dfree(s->order); dfree(s->kins); dfree(s->kpre);
   dfree(s->gcpos); dfree(s->lgc); dfree(s->fl); dfree(s->fr); dfree(s->frins); dfree(s->frlist); dfree(s->frcum);
   dfree(s->fridx); dfree(s->B); dfree(s->tmp);
+  dfree(s->rdec); dfree(s->ramb); dfree(s->rst); dfree(s->rpre); dfree(s->amb); dfree(s->acum);
   s->cap = 0; s->bcap = 0; s->tmp_bytes = 0;
 }
 
@@ -489,6 +600,7 @@ TopicState* rtps_topic_state_new(int device) {
   s->nt = NSLOT;  // no configured topics: every slot its own
   bool ok = dmalloc((void**)&s->slot_tid, NSLOT * 4) && dmalloc((void**)&s->slot_cid, NSLOT * 4) &&
             dmalloc((void**)&s->nfr, 8) && dmalloc((void**)&s->n_full, 8) && dmalloc((void**)&s->n_used, 8) &&
+            dmalloc((void**)&s->namb, 8) &&
             hipMemset(s->n_full, 0, 8) == hipSuccess && hipMemset(s->n_used, 0, 8) == hipSuccess &&
             hipHostMalloc((void**)&s->h_used, 8, hipHostMallocDefault) == hipSuccess &&
             hipEventCreateWithFlags(&s->used_ev, hipEventDisableTiming) == hipSuccess;
@@ -552,10 +664,11 @@ static int build(TopicState* s, const uint32_t* set_first, const rtps_target* en
   for (uint32_t slot = 0; slot < NSLOT; ++slot) slot_cid[slot] = seen[slot] ? tid_cid[slot_tid[slot]] : s->nA;
   if (s->nA > s->acap || !s->segb) {
     dfree(s->cid_tid); dfree(s->segb); dfree(s->sege); dfree(s->frb); dfree(s->fre); dfree(s->ibase);
+    dfree(s->ab); dfree(s->ae);
     const uint32_t a = s->nA ? s->nA : 1;
     if (!dmalloc((void**)&s->cid_tid, a * 4ull) || !dmalloc((void**)&s->segb, a * 4ull) ||
         !dmalloc((void**)&s->sege, a * 4ull) || !dmalloc((void**)&s->frb, a * 4ull) || !dmalloc((void**)&s->fre, a * 4ull) ||
-        !dmalloc((void**)&s->ibase, a * 8ull))
+        !dmalloc((void**)&s->ibase, a * 8ull) || !dmalloc((void**)&s->ab, a * 4ull) || !dmalloc((void**)&s->ae, a * 4ull))
       return RTPS_RX_ENOMEM;
     s->acap = a;
   }
@@ -698,6 +811,9 @@ static int reserve_scratch(TopicState* s, uint64_t n, hipStream_t st) {
             dmalloc((void**)&s->lgc, n * 4) && dmalloc((void**)&s->fl, n) && dmalloc((void**)&s->fr, n) &&
             dmalloc((void**)&s->frins, n) && dmalloc((void**)&s->frlist, n * 4) && dmalloc((void**)&s->frcum, n * 4) &&
             dmalloc((void**)&s->fridx, n * 8) && dmalloc((void**)&s->B, bcap * sizeof(BEnt)) &&
+            dmalloc((void**)&s->rdec, n) && dmalloc((void**)&s->ramb, n + 1) && dmalloc((void**)&s->rst, (n + 1) * 4) &&
+            dmalloc((void**)&s->rpre, (n + 1) * 4) && dmalloc((void**)&s->amb, (n + 1) * 4) &&
+            dmalloc((void**)&s->acum, (n + 1) * 4) &&
             hipMemsetAsync(s->B, 0, bcap * sizeof(BEnt), st) == hipSuccess;
   size_t b1 = 0, b2 = 0, b3 = 0, b4 = 0;
   ok = ok && rtps_sort_pairs(nullptr, b1, s->skey, s->skey2, s->sval, s->order, (uint32_t)n, 17, st) == hipSuccess;
@@ -706,8 +822,12 @@ static int reserve_scratch(TopicState* s, uint64_t n, hipStream_t st) {
                  hipSuccess;
   ok = ok && hipcub::DeviceSelect::Flagged(nullptr, b4, hipcub::CountingInputIterator<uint32_t>(0), s->fr, s->frlist,
                                            s->nfr, (int64_t)n, st) == hipSuccess;
+  size_t b5 = 0, b6 = 0;
+  ok = ok && hipcub::DeviceScan::ExclusiveSum(nullptr, b5, s->rst, s->rpre, (int64_t)n + 1, st) == hipSuccess;
+  ok = ok && hipcub::DeviceSelect::Flagged(nullptr, b6, hipcub::CountingInputIterator<uint32_t>(0), s->ramb, s->amb,
+                                           s->namb, (int64_t)n, st) == hipSuccess;
   size_t tb = b1;
-  for (size_t b : {b2, b3, b4}) tb = b > tb ? b : tb;
+  for (size_t b : {b2, b3, b4, b5, b6}) tb = b > tb ? b : tb;
   ok = ok && dmalloc(&s->tmp, tb);
   if (!ok) { free_scratch(s); return RTPS_RX_ENOMEM; }
   s->tmp_bytes = tb;
@@ -741,6 +861,8 @@ int rtps_topic_apply(TopicState* s, hipStream_t st, const rtps_record* recs, con
   d.segb = s->segb; d.sege = s->sege; d.frb = s->frb; d.fre = s->fre; d.ibase = s->ibase; d.n_full = s->n_full;
   d.n_used = s->n_used;
   d.ovf = ovf;
+  d.rdec = s->rdec; d.rst = s->rst; d.rpre = s->rpre; d.ramb = s->ramb; d.amb = s->amb; d.namb = s->namb;
+  d.acum = s->acum; d.ab = s->ab; d.ae = s->ae;
   const uint32_t g = (uint32_t)((max_del + TT - 1) / TT < 8192 ? (max_del + TT - 1) / TT : 8192);
   if (s->nA && hipMemsetAsync(s->segb, 0xff, s->nA * 4ull, st) != hipSuccess) return RTPS_RX_EHIP;
   hipLaunchKernelGGL(tc_gather, dim3(g), dim3(TT), 0, st, d, recs, n_records, max_records, del, n_del, max_del);
@@ -765,7 +887,20 @@ int rtps_topic_apply(TopicState* s, hipStream_t st, const rtps_record* recs, con
   if (hipcub::DeviceSelect::Flagged(s->tmp, tb, hipcub::CountingInputIterator<uint32_t>(0), s->fr, s->frlist, s->nfr,
                                     (int64_t)max_del, st) != hipSuccess)
     return RTPS_RX_EHIP;
+  // repeats: the sure ones decided in parallel, the undecided ones per topic in order
+  if (hipMemsetAsync(s->rst, 0, (max_del + 1) * 4, st) != hipSuccess ||
+      hipMemsetAsync(s->ramb, 0, max_del + 1, st) != hipSuccess)
+    return RTPS_RX_EHIP;
+  hipLaunchKernelGGL(tc_rdec, dim3(g), dim3(TT), 0, st, d);
+  tb = s->tmp_bytes;
+  if (hipcub::DeviceScan::ExclusiveSum(s->tmp, tb, s->rst, s->rpre, (int64_t)max_del + 1, st) != hipSuccess)
+    return RTPS_RX_EHIP;
+  tb = s->tmp_bytes;
+  if (hipcub::DeviceSelect::Flagged(s->tmp, tb, hipcub::CountingInputIterator<uint32_t>(0), s->ramb, s->amb, s->namb,
+                                    (int64_t)max_del, st) != hipSuccess)
+    return RTPS_RX_EHIP;
   if (s->nA) hipLaunchKernelGGL(tc_resolve, dim3((s->nA + TT - 1) / TT), dim3(TT), 0, st, d);
+  hipLaunchKernelGGL(tc_rfill, dim3(g), dim3(TT), 0, st, d);
   hipLaunchKernelGGL(tc_final, dim3(g), dim3(TT), 0, st, d, del, max_del);
   s->used_inflight += max_del;
   if (hipMemcpyAsync(s->h_used, s->n_used, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
