@@ -229,12 +229,24 @@ __device__ __forceinline__ void rec_clear(Rec& r) {
 #pragma unroll
   for (int i = 0; i < 16; ++i) r.d[i] = 0u;
 }
+// Record stores: the output is written once and read by the next stage (or the host) well
+// after the L2 has turned over, so the streaming (nontemporal) form when RTPS_NT_RECORDS.
+#ifndef RTPS_NT_RECORDS
+#define RTPS_NT_RECORDS 1  // T kernel 46.6 -> 43.0 us (round 5)
+#endif
+__device__ __forceinline__ void rec_st16(u32x4* p, const u32x4& v) {
+#if RTPS_NT_RECORDS
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
 __device__ __forceinline__ void rec_store(rtps_record* dst, const Rec& r) {
   u32x4* p = reinterpret_cast<u32x4*>(dst);
-  p[0] = u32x4{r.d[0], r.d[1], r.d[2], r.d[3]};
-  p[1] = u32x4{r.d[4], r.d[5], r.d[6], r.d[7]};
-  p[2] = u32x4{r.d[8], r.d[9], r.d[10], r.d[11]};
-  p[3] = u32x4{r.d[12], r.d[13], r.d[14], r.d[15]};
+  rec_st16(p + 0, u32x4{r.d[0], r.d[1], r.d[2], r.d[3]});
+  rec_st16(p + 1, u32x4{r.d[4], r.d[5], r.d[6], r.d[7]});
+  rec_st16(p + 2, u32x4{r.d[8], r.d[9], r.d[10], r.d[11]});
+  rec_st16(p + 3, u32x4{r.d[12], r.d[13], r.d[14], r.d[15]});
 }
 
 // ParameterList::read_from (elements/parameter_list.rs:79-102) over the body
@@ -797,7 +809,7 @@ __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_spec_ker
       const uint64_t lim = p.max_records > tile_first ? p.max_records - tile_first : 0;
       const uint32_t nrec = agg < lim ? agg : (uint32_t)lim;
       u32x4* dst = reinterpret_cast<u32x4*>(p.records + tile_first);
-      for (uint32_t k = tid; k < nrec * 4u; k += TILE) dst[k] = s_stage[k];
+      for (uint32_t k = tid; k < nrec * 4u; k += TILE) rec_st16(dst + k, s_stage[k]);
       if (p.target_out)
         for (uint32_t k = tid; k < nrec; k += TILE) p.target_out[tile_first + k] = s_stage_match[k];
     }
@@ -1000,10 +1012,11 @@ __device__ uint32_t item_walk(const KParams& p, const Src& s, const uint32_t* H,
     if (em) {
       const uint32_t pos = wpos + (uint32_t)__popcll(m & lt);
       if (pos < CAPW) {
-        slab[pos * IW] = u32x4{o | (src_off << 16),
-                               nrec | (lane << 16) | ((st.dst_ok ? 1u : 0u) << 22) | ((st.ts_valid ? 1u : 0u) << 23) |
-                                   (kind << 24),
-                               st.ts_sec, st.ts_frac};
+        const u32x4 iv{o | (src_off << 16),
+                       nrec | (lane << 16) | ((st.dst_ok ? 1u : 0u) << 22) | ((st.ts_valid ? 1u : 0u) << 23) |
+                           (kind << 24),
+                       st.ts_sec, st.ts_frac};
+        slab[pos * IW] = iv;
         if (IW == 3u) {
           slab[pos * IW + 1] = u32x4{W.w[0], W.w[1], W.w[2], W.w[3]};
           slab[pos * IW + 2] = u32x4{W.w[4], W.w[5], W.w[6], W.w[7]};
@@ -1198,6 +1211,9 @@ __device__ __forceinline__ void em2_item(const KParams& p, const Src& s0, const 
 #ifndef RTPS_EM2_TRANSPOSE
 #define RTPS_EM2_TRANSPOSE 1  // 0: per-lane 64-B record stores (measured slower)
 #endif
+#ifndef RTPS_EM2_NT  // W2's record stores streamed: C3 W2 188 -> 177 us (round 5)
+#define RTPS_EM2_NT 1
+#endif
 #ifndef RTPS_EM2_THREADS
 #define RTPS_EM2_THREADS 512  // two tiles per workgroup (one reader-table copy for 8 waves; 256 / 768: slower)
 #endif
@@ -1273,8 +1289,13 @@ __global__ __launch_bounds__(EM2T, RTPS_EM2_WAVES_PER_SIMD) void rtps_parse_emit
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const u32x4 v = stg[lane];
         const uint32_t rl = 16u * c + (lane >> 2);  // the record (of the 64) whose quarter lane l stores
-        if (rl < nact && r0 + rl < p.max_records)
+        if (rl < nact && r0 + rl < p.max_records) {
+#if RTPS_EM2_NT
+          __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p.records + r0 + rl) + (lane & 3u));
+#else
           reinterpret_cast<u32x4*>(p.records + r0 + rl)[lane & 3u] = v;
+#endif
+        }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // reads before the next quarter's writes
         __builtin_amdgcn_wave_barrier();
       }

@@ -25,8 +25,8 @@ print("emit", sys.argv[2], "ms_per_step", d["ms_per_step"], {k: v for k, v in d.
 PY
       done ;;
     c3_var)  # the in-tree library, then every tuning variant under rustdds-io_uring_amd/variants/, RTPS_RX_EMIT as set
-      for lib in $R/rustdds-io_uring_amd/librtps_rx.so $R/rustdds-io_uring_amd/variants/librtps_rx_*.so; do
-        v=$(basename $lib .so)
+      for lib in $R/rustdds-io_uring_amd/librtps_rx.so $R/rustdds-io_uring_amd/variants/librtps_rx_*.so $R/rustdds-io_uring_amd/librtps_rx.so; do
+        v=$(basename $lib .so)  # the in-tree library twice: the first run of a fresh box reads ~15 us slow
         RTPS_RX_LIB=$lib timeout -k 10 300 python bench.py --workload C3 --steps 20 --warmup 5 --no-c1 --no-e2e --no-cpu-baseline --no-ingest --no-cdr > $O/c3_$v.json 2> $O/c3_$v.err || { tail -5 $O/c3_$v.err; exit 4; }
         python - $O/c3_$v.json $v <<'PY'
 import json, sys
@@ -34,9 +34,29 @@ d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); r = d["roofli
 print(sys.argv[2], "step", round(d["ms_per_step"] * 1e3, 1), "us", {k: round(r[k] * 1e3, 1) for k in ("item_kernel_ms", "emit_kernel_ms", "scan_ms") if k in r})
 PY
       done ;;
+    t_var)  # as c3_var on the T workload (spec A+B pass)
+      for lib in $R/rustdds-io_uring_amd/librtps_rx.so $R/rustdds-io_uring_amd/variants/librtps_rx_*.so $R/rustdds-io_uring_amd/librtps_rx.so; do
+        v=$(basename $lib .so)
+        RTPS_RX_LIB=$lib timeout -k 10 300 python bench.py --workload T --steps 20 --warmup 5 --no-c1 --no-e2e --no-cpu-baseline --no-ingest --no-cdr > $O/t_$v.json 2> $O/t_$v.err || { tail -5 $O/t_$v.err; exit 4; }
+        python - $O/t_$v.json $v <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); r = d["roofline"]
+print(sys.argv[2], "step", round(d["ms_per_step"] * 1e3, 1), "us", "frac", round(r["frac"], 3), "kernel_us", round(r.get("kernel_ms", 0) * 1e3, 1))
+PY
+      done ;;
+    pmc)  # FETCH / WRITE passes of T (ceiling + parse) and C3 -> gpurun_out/r${ROUND}_pmc_{T,C3}.json
+      ROUND=${ROUND:-5} timeout -k 10 700 bash scripts/gpu_pmc.sh > $O/pmc.log 2>&1 || { tail -5 $O/pmc.log; exit 12; }
+      cp gpurun_out/r${ROUND:-5}_pmc_T.json gpurun_out/r${ROUND:-5}_pmc_C3.json $O/ ;;
+    bench_C5)
+      timeout -k 10 600 python bench.py --workload C5 --steps 10 --warmup 3 > $O/bench_C5.json 2> $O/bench_C5.err || { tail -20 $O/bench_C5.err; exit 10; }
+      tail -c 600 $O/bench_C5.json ;;
+    kstats_T|kstats_C4)
+      wl=${step#kstats_}
+      cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kstats_$wl -o run --output-format csv -- python3 $R/bench.py --workload $wl --steps 20 --warmup 5 --no-cpu-baseline --no-e2e --no-c1 > $O/kstats_$wl.log 2>&1 || { tail -5 $O/kstats_$wl.log; exit 6; }
+      cd $R; python scripts/prof_table.py $(find $O/kstats_$wl -name "*kernel_stats.csv") | head -30 ;;
     kstats_C3)
-      cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kstats_C3 -o run --output-format csv -- python3 $R/bench.py --workload C3 --steps 20 --warmup 5 --no-cpu-baseline --no-e2e --no-c1 --no-ingest --no-cdr > $O/kstats_C3.log 2>&1 || { tail -5 $O/kstats_C3.log; exit 6; }
-      cd $R; python scripts/prof_table.py $(find $O/kstats_C3 -name "*kernel_stats.csv") ;;
+      cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kstats_C3 -o run --output-format csv -- python3 $R/bench.py --workload C3 --steps 20 --warmup 5 --no-cpu-baseline --no-e2e --no-c1 > $O/kstats_C3.log 2>&1 || { tail -5 $O/kstats_C3.log; exit 6; }
+      cd $R; python scripts/prof_table.py $(find $O/kstats_C3 -name "*kernel_stats.csv") | head -40 ;;
     shard)
       timeout -k 10 900 $PYT tests/test_shard_gpu.py > $O/shard.log 2>&1 || { grep -E "FAILED|Error" $O/shard.log | head; tail -30 $O/shard.log; exit 7; }
       tail -2 $O/shard.log ;;
