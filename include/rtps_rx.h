@@ -687,13 +687,15 @@ int rtps_rx_frag_set_receive_time(rtps_rx_ctx* ctx, uint64_t unix_ns);
  * keep proxies in place (append new ones) or call rtps_rx_ingest_reset after
  * reordering them.
  * The change set is a bitmap over RTPS_INGEST_WINDOW sequence numbers from
- * all_ackable_before plus, per proxy, a sorted set of up to RTPS_INGEST_FAR_CAP
- * covered SNs beyond that window (samples and GAPs further ahead: decided exactly,
- * replayed in event order; all_ackable_before continues through the set).  Only
- * past those capacities (a full far set, more than 8192 far events in a batch) is
- * a sample accepted without the duplicate check; those are counted in
- * *n_window_overflow (the reference's BTreeMap has no bound). */
-#define RTPS_INGEST_FAR_CAP 1024u
+ * all_ackable_before plus, per proxy, a FAR SET: every covered SN beyond that window
+ * (samples and GAPs further ahead), a hash set in device memory that grows with it
+ * (no fixed bound; a batch may add any number of far SNs to any proxy), decided
+ * exactly by first cover (all_ackable_before continues through the set).  The
+ * context keeps room for 4 x (max_records + 1024) + twice the far sets' slots in
+ * use before each batch, growing its pool between batches; only a batch whose GAPs
+ * cover more SNs beyond the window than that finds it full, and then those
+ * proxies' far samples are accepted without the duplicate check and counted in
+ * *n_window_overflow (the reference's BTreeMap inserts such a range SN by SN). */
 #define RTPS_INGEST_WINDOW (1u << 17)
 #define RTPS_INGEST_BEST_EFFORT 0x1u /* flags: treat every reader as BestEffort (HEARTBEATs ignored) */
 #define RTPS_INGEST_TOPIC_CACHE 0x2u /* flags: also run the topic caches' add_change (RTPS_DELIVERY_CACHED) */

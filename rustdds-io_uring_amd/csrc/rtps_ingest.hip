@@ -59,6 +59,7 @@
 #include <atomic>
 #include <chrono>
 #include <new>
+#include <vector>
 
 #include "rtps_ingest.h"
 
@@ -158,9 +159,20 @@ struct State {
   uint32_t* seg_b;  // HEARTBEAT segment of each proxy in sorted order
   uint32_t* seg_e;
   uint64_t* ctr;
-  int64_t* far;      // the far set of proxy e: far[e * FCAP, + far_n[e]), ascending, all >= lo + W
-  uint32_t* far_n;
-  FarItem* fl;       // this batch's far items (global paths), C_NFAR of them
+  // far sets (see "far sequence numbers" below): proxy e's hash table is the pool slots
+  // [far_off[e], + far_cap[e]) of fsn / fkey (far_cap 0: none)
+  uint64_t* far_off;
+  uint32_t* far_cap;
+  uint32_t* far_n;    // occupied slots
+  int64_t* far_min;   // least SN of the set at or above the window's end (INT64_MAX: none)
+  uint64_t* fneed;    // k_far: SNs the batch's items of proxy e cover (then cleared); FNEED_OUT: the pool was out
+  int64_t* fsn;       // pool: SN per slot (FEMPTY: free)
+  uint64_t* fkey;     // pool: the first event that covered the slot's SN, epoch << 32 | event
+  uint64_t* fused;    // pool slots handed out (device counter; may pass fpcap when the pool is out)
+  uint64_t fpcap;     // pool slots
+  FarItem* fl;        // this batch's far items (global paths), C_NFAR of them, at most fl_cap
+  uint64_t fl_cap;
+  uint32_t epoch;     // this batch's (first-cover keys)
 };
 
 // ---- 1 classify ----
@@ -239,35 +251,43 @@ static_assert(sizeof(PEv) == 32, "PEv layout");
 
 // ---- far sequence numbers: the change set beyond the window ----
 // The window [lo, lo + W) holds the change set as bits; the reference's BTreeMap has no
-// bound, so the SNs a proxy has covered at or above lo + W (a writer that jumped ahead,
-// a GAP reaching past the window) are kept per proxy in a sorted array of at most FCAP
-// SNs, the FAR SET.  A batch's events beyond the window, FAR ITEMS (samples past it,
-// DUPLICATES_OK samples there, GAPs whose coverage reaches past it), are decided
-// provisionally by the parallel passes (samples accepted), then replayed per proxy in
-// event order against the far set (k_far on the global paths, the tail of k_proxy on the
-// per-proxy one): a sample already covered is rejected, every SN an item covers joins the
-// set.  The state pass continues all_ackable_before through the set when the window is
-// covered up to its end, re-anchors, and moves the set's SNs the new window spans into
-// its bits.  Inexact only past the capacities (a full far set, more than FL_CAP far items
-// in a batch, more than FPX for one proxy on the per-proxy path): counted in
-// *n_window_overflow, those samples accepted unchecked.
-constexpr uint32_t FCAP = RTPS_INGEST_FAR_CAP;  // far SNs per proxy
-constexpr uint32_t FHS = 2 * FCAP;  // the replay's LDS hash slots
-constexpr uint32_t FL_CAP = 8192;   // far items per batch (global list)
-constexpr uint32_t FPX = 1024;      // far items one k_proxy workgroup replays
+// bound (rtps_writer_proxy.rs:62), so the SNs a proxy has covered at or above lo + W (a
+// writer that jumped ahead, a GAP reaching past the window) are kept per proxy in a FAR
+// SET: an open-addressing hash set of SNs in a device pool (load <= 1/2; grown by rehashing
+// into a larger table), each slot with the first event that covered its SN, epoch-tagged
+// (epoch << 32 | event: the SNs of earlier batches compare smaller).  A batch's events
+// beyond the window, FAR ITEMS (samples past it, DUPLICATES_OK samples there, GAPs whose
+// coverage reaches past it), are decided provisionally (samples accepted), then every SN an
+// item covers is inserted with an atomicMin of the item's key, and a far sample is accepted
+// iff its own key is its SN's minimum: no earlier event of the batch and no earlier batch
+// covered it -- the window's first-cover rule (k_marks_d) over the hash, so no replay in
+// event order is needed.  k_far (global paths: every proxy's items from the batch list) and
+// the chunk loop of k_proxy (per-proxy path: each chunk's items right after they are
+// decided) share it.  The state pass continues all_ackable_before through the set when the
+// window is covered up to its end (far_extend), re-anchors, and sets the bits of the set's
+// SNs the new window spans (far_pull, which also drops what lies below the new window's end
+// once that is most of the table).
+// Capacity: tables come from the pool by a device bump counter; the host keeps the pool's
+// free part at >= 4 x (the batch's record capacity + the live far slots) between batches
+// (far_pool_ensure: grown and compacted there), which holds every table a batch's samples
+// can need.  Only GAPs covering more SNs past the window than that can find the pool out:
+// those samples are accepted unchecked and counted in *n_window_overflow (the reference
+// inserts such ranges one SN at a time too, rtps_writer_proxy.rs:284-291).
+constexpr int64_t FEMPTY = INT64_MIN;   // a free slot (far SNs are >= W > 0)
+constexpr uint32_t FT_MIN = 64;         // smallest table
+constexpr uint64_t FNEED_OUT = ~0ull;   // fneed: the pool could not grow this proxy's table
 enum : uint32_t { FI_SAMPLE = 1, FI_DUP = 2, FI_GAP = 3 };
 struct FarItem {
   PEv p;        // the event as the per-proxy pass packs it (p.k: its accept slot)
   int64_t lim;  // lo + W when it was decided: the SNs at or above it are the far part
   uint32_t e, kind;
 };
-static_assert(sizeof(FarItem) == 48 && FHS == 2048, "FarItem layout, replay hash width");
-// its list position, or NONE: the list is full (the item is lost: its sample stays accepted,
-// its SNs unrecorded)
-__device__ __forceinline__ uint32_t far_push(uint64_t* ctr, FarItem* fl, const FarItem& it) {
-  const unsigned long long pos = atomicAdd(reinterpret_cast<unsigned long long*>(ctr + C_NFAR), 1ull);
-  if (pos >= FL_CAP) return 0xffffffffu;
-  fl[pos] = it;
+static_assert(sizeof(FarItem) == 48, "FarItem layout");
+// its list position, or NONE: the list is full (sized by the host to the batch's events: not reached)
+__device__ __forceinline__ uint32_t far_push(const State& s, const FarItem& it) {
+  const unsigned long long pos = atomicAdd(reinterpret_cast<unsigned long long*>(s.ctr + C_NFAR), 1ull);
+  if (pos >= s.fl_cap) return NONE;
+  s.fl[pos] = it;
   return (uint32_t)pos;
 }
 
@@ -424,7 +444,7 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
           q3 = f3;
 #else
           q2 = q[2];
-          if ((FAST && kind != RTPS_DATA) || (MARK && kind == RTPS_GAP)) q3 = q[3];
+          if ((FAST && kind != RTPS_DATA) || ((MARK || !IDENT) && kind == RTPS_GAP)) q3 = q[3];
 #endif
           const int64_t rsn = (int64_t)(((uint64_t)q2[1] << 32) | q2[0]);
           if (kind == RTPS_DATA) {
@@ -466,6 +486,10 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
           nh += ev == EV_HB;
           ng += ev == EV_GAP;
           nf += en == NONE;
+          if (!IDENT && en != NONE && ev != EV_HB) {  // far-item candidates of expanded batches (see below)
+            const int64_t lim = st.lo[en] + (int64_t)W;
+            if (ev == EV_SAMPLE ? sn >= lim : (int64_t)(((uint64_t)q2[3] << 32) | q2[2]) + (int64_t)q3[0] > lim) ++nfar;
+          }
         }
       }
     }
@@ -656,7 +680,7 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
   if (tid < 4 && s_n[tid])
     atomicAdd(reinterpret_cast<unsigned long long*>(ctr + C_SPREAD + 4u * (blockIdx.x & 63u) + tid),
               (unsigned long long)s_n[tid]);
-  if (MARK && nfar) atomicAdd(reinterpret_cast<unsigned long long*>(ctr + C_FARC), (unsigned long long)nfar);
+  if ((MARK || !IDENT) && nfar) atomicAdd(reinterpret_cast<unsigned long long*>(ctr + C_FARC), (unsigned long long)nfar);
   CST(6);
 }
 
@@ -882,7 +906,7 @@ __device__ __forceinline__ void gap_far_item(uint64_t i, const Scratch& x, const
   const rtps_record& r = fs.recs[x.erec[i]];
   const int64_t lim = s.lo[e] + (int64_t)W;
   if (r.u.gap.list_base + (int64_t)r.u.gap.num_bits > lim)
-    far_push(s.ctr, s.fl,
+    far_push(s,
              FarItem{PEv{r.sn, r.u.gap.list_base, fs.dgram_off[r.dgram_idx] + r.u.gap.bitmap_off,
                          EV_GAP | ((r.flags & 1u) ? PM_LE : 0u) | (r.u.gap.num_bits << 8), (uint32_t)i},
                      lim, e, FI_GAP});
@@ -920,13 +944,13 @@ __device__ __forceinline__ uint8_t decide_one(uint64_t i, uint64_t n, const Scra
   poff = (uint64_t)(v - lo);
   if (meta & EVF_DUP_OK) {  // the participant reader's duplicates (reader.rs:712-722)
     merge = in_win;
-    if (v >= lo + (int64_t)W) far_push(s.ctr, s.fl, FarItem{PEv{v, 0, 0, EV_SAMPLE, (uint32_t)i}, lo + (int64_t)W, e, FI_DUP});
+    if (v >= lo + (int64_t)W) far_push(s, FarItem{PEv{v, 0, 0, EV_SAMPLE, (uint32_t)i}, lo + (int64_t)W, e, FI_DUP});
     return 1;
   }
   const int64_t thr = hb_thr(i, v, s.base[e], s.seg_b[e], s.seg_e[e], x, reliable);
   if (v < 1 || v < thr) return 0;
   if (v >= lo + (int64_t)W) {  // beyond the window: accepted until the far replay (k_far) decides
-    far_push(s.ctr, s.fl, FarItem{PEv{v, 0, 0, EV_SAMPLE, (uint32_t)i}, lo + (int64_t)W, e, FI_SAMPLE});
+    far_push(s, FarItem{PEv{v, 0, 0, EV_SAMPLE, (uint32_t)i}, lo + (int64_t)W, e, FI_SAMPLE});
     return 1;
   }
   const bool known = (s.bits[(uint64_t)e * WW + (poff >> 5)] >> (poff & 31u)) & 1u;
@@ -1131,13 +1155,13 @@ __global__ __launch_bounds__(IT) void k_decide_t(uint64_t n, uint64_t cap, Scrat
           a = 1;
           merge = in_win;
           if (v >= lo[jj] + (int64_t)W)
-            far_push(s.ctr, s.fl, FarItem{PEv{v, 0, 0, EV_SAMPLE, (uint32_t)i}, lo[jj] + (int64_t)W, e, FI_DUP});
+            far_push(s, FarItem{PEv{v, 0, 0, EV_SAMPLE, (uint32_t)i}, lo[jj] + (int64_t)W, e, FI_DUP});
         } else {
           const int64_t thr = hb_thr(i, v, base[jj], reliable ? s.seg_b[e] : 0u, reliable ? s.seg_e[e] : 0u, x,
                                      reliable);
           if (v >= 1 && v >= thr) {
             if (v >= lo[jj] + (int64_t)W) {  // beyond the window: accepted until the far replay decides
-              far_push(s.ctr, s.fl, FarItem{PEv{v, 0, 0, EV_SAMPLE, (uint32_t)i}, lo[jj] + (int64_t)W, e, FI_SAMPLE});
+              far_push(s, FarItem{PEv{v, 0, 0, EV_SAMPLE, (uint32_t)i}, lo[jj] + (int64_t)W, e, FI_SAMPLE});
               a = 1;
             } else {
               const bool known = (bw[jj] >> (off & 31u)) & 1u;
@@ -1234,7 +1258,8 @@ __device__ __forceinline__ void dwrite_tile(uint32_t blk, const uint8_t* flag, u
     if (hev) {  // the batch's events, for the next batch's path choice (pinned host memory, read without a sync)
       uint64_t ne = 0;
       for (uint32_t k = 0; k < 64; ++k) ne += ctr[C_SPREAD + 4 * k + 2];
-      *hev = ne;
+      hev[0] = ne;
+      hev[1] = ctr[C_NFAR];  // (per-proxy path: its far items, sizing the far-set pool's room)
     }
   }
 }
@@ -1255,39 +1280,56 @@ __global__ __launch_bounds__(IT) void k_accept_counts(uint64_t n, uint64_t cap, 
   }
 }
 
-// ---- far replay (see "far sequence numbers" above) ----
-__device__ __forceinline__ uint32_t fh_slot(int64_t v) {
-  return (uint32_t)(((uint64_t)v * 0x9e3779b97f4a7c15ull) >> 53);  // 11 bits: FHS slots
+// ---- far sets (see "far sequence numbers" above) ----
+// Table words are read with device-coherent loads: other workgroups' (k_far, the pool
+// compaction) and other waves' atomics land in the L2, past this CU's L1.
+__device__ __forceinline__ int64_t fld(const int64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ bool fh_has(const int64_t* h, int64_t v) {
-  for (uint32_t j = fh_slot(v);; j = (j + 1u) & (FHS - 1u)) {
-    const int64_t k = h[j];
-    if (k == v) return true;
-    if (k == INT64_MAX) return false;
+__device__ __forceinline__ uint64_t fldk(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t fld32(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t fslot(int64_t v, uint32_t mask) {
+  return (uint32_t)(((uint64_t)v * 0x9e3779b97f4a7c15ull) >> 32) & mask;
+}
+// v into the table (sn, key; mask + 1 slots) with first-cover key k; 1 when it took a free slot
+__device__ uint32_t fset_add(int64_t* sn, uint64_t* key, uint32_t mask, int64_t v, uint64_t k) {
+  for (uint32_t j = fslot(v, mask);; j = (j + 1u) & mask) {
+    int64_t cur = fld(sn + j);
+    if (cur == FEMPTY) {
+      cur = (int64_t)atomicCAS(reinterpret_cast<unsigned long long*>(sn + j), (unsigned long long)FEMPTY,
+                               (unsigned long long)v);
+      if (cur == FEMPTY) {
+        atomicMin(reinterpret_cast<unsigned long long*>(key + j), (unsigned long long)k);
+        return 1u;
+      }
+    }
+    if (cur == v) {
+      atomicMin(reinterpret_cast<unsigned long long*>(key + j), (unsigned long long)k);
+      return 0u;
+    }
   }
 }
-// v into the set (n: its size); false when it is full
-__device__ bool fh_add(int64_t* h, uint32_t& n, int64_t v) {
-  uint32_t j = fh_slot(v);
-  for (;; j = (j + 1u) & (FHS - 1u)) {
-    const int64_t k = h[j];
-    if (k == v) return true;
-    if (k == INT64_MAX) break;
+__device__ uint32_t fset_find(const int64_t* sn, uint32_t mask, int64_t v) {
+  for (uint32_t j = fslot(v, mask);; j = (j + 1u) & mask) {
+    const int64_t cur = fld(sn + j);
+    if (cur == v) return j;
+    if (cur == FEMPTY) return NONE;
   }
-  if (n >= FCAP) return false;
-  h[j] = v;
-  ++n;
-  return true;
 }
 // The SNs >= lim a GAP covers (what gap_cover_w clips at the window's end): the range
-// [gapStart, gapList.base) when not negative, then the listed SNs.  f(sn) false: the set
-// is full; *miss counts what was not recorded.
-template <typename WF, typename F>
-__device__ void gap_far(int64_t start, int64_t base, uint32_t num_bits, WF&& word_of, int64_t lim, F&& f,
-                        uint64_t& miss) {
-  if (start <= base)
-    for (int64_t v = start > lim ? start : lim; v < base; ++v)
-      if (!f(v)) { miss += (uint64_t)(base - v); break; }
+// [gapStart, gapList.base) when not negative, then the listed SNs.  range(a, b) for
+// [a, b) (non-empty), point(v) for each listed one.
+template <typename WF, typename RF, typename PF>
+__device__ void gap_far(int64_t start, int64_t base, uint32_t num_bits, WF&& word_of, int64_t lim, RF&& range,
+                        PF&& point) {
+  if (start <= base) {
+    const int64_t a = start > lim ? start : lim;
+    if (a < base) range(a, base);
+  }
   for (uint32_t w = 0; w * 32u < num_bits; ++w) {
     uint32_t word = word_of(w);
     const uint32_t valid = num_bits - w * 32u;
@@ -1296,162 +1338,281 @@ __device__ void gap_far(int64_t start, int64_t base, uint32_t num_bits, WF&& wor
       const uint32_t b = (uint32_t)__builtin_clz(word);  // MSB first: SN base + 32 w + b
       word &= ~(0x80000000u >> b);
       const int64_t v = base + (int64_t)(w * 32u + b);
-      if (v >= lim && !f(v)) ++miss;
+      if (v >= lim) point(v);
     }
   }
 }
-// one far item, in the proxy's event order: a sample the set (or an earlier item) covers is
-// rejected (acc 0; tcnt: its delivery tile's count); everything covered joins the set
-__device__ uint64_t far_apply(const FarItem& it, int64_t* h, uint32_t& n, const uint8_t* arena, uint8_t* acc,
-                              uint32_t* tcnt) {
-  uint64_t miss = 0;
-  const PEv& P = it.p;
-  if (it.kind == FI_SAMPLE) {
-    if (fh_has(h, P.sn)) {
-      acc[P.k] = 0;
-      if (tcnt) atomicSub(&tcnt[P.k / DT], 1u);
-    } else if (!fh_add(h, n, P.sn)) {
-      ++miss;
-    }
-  } else if (it.kind == FI_DUP) {
-    if (!fh_add(h, n, P.sn)) ++miss;
-  } else {
-    auto f = [&](int64_t v) { return fh_add(h, n, v); };
-    if (P.m & PM_INL)
-      gap_far(P.sn, P.a, P.m >> 8, [&](uint32_t w) { return (uint32_t)(P.bw >> (32u * w)); }, it.lim, f, miss);
-    else
-      gap_far(P.sn, P.a, P.m >> 8, [&](uint32_t w) { return rd32(arena + P.bw + 4u * w, (P.m & PM_LE) != 0u); },
-              it.lim, f, miss);
+// every SN a far item covers: f(v)
+template <typename F>
+__device__ void far_sns(const PEv& P, uint32_t kind, int64_t lim, const uint8_t* arena, F&& f) {
+  if (kind != FI_GAP) {
+    f(P.sn);
+    return;
   }
-  return miss;
+  auto range = [&](int64_t a, int64_t b) { for (int64_t v = a; v < b; ++v) f(v); };
+  if (P.m & PM_INL)
+    gap_far(P.sn, P.a, P.m >> 8, [&](uint32_t w) { return (uint32_t)(P.bw >> (32u * w)); }, lim, range, f);
+  else
+    gap_far(P.sn, P.a, P.m >> 8, [&](uint32_t w) { return rd32(arena + P.bw + 4u * w, (P.m & PM_LE) != 0u); }, lim,
+            range, f);
 }
-// ascending bitonic sort of a power-of-two LDS array by the whole block (nt threads)
-template <typename T>
-__device__ void lds_sort(T* a, uint32_t len, uint32_t nt) {
-  for (uint32_t k = 2; k <= len; k <<= 1)
-    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      for (uint32_t i = threadIdx.x; i < len; i += nt) {
-        const uint32_t l = i ^ j;
-        if (l > i) {
-          const T x = a[i], y = a[l];
-          if (((i & k) == 0) ? (x > y) : (x < y)) { a[i] = y; a[l] = x; }
-        }
+// how many (an upper bound: a GAP's listed SNs inside its own range count twice)
+__device__ uint64_t far_count(const PEv& P, uint32_t kind, int64_t lim, const uint8_t* arena) {
+  if (kind != FI_GAP) return 1;
+  uint64_t c = 0;
+  auto range = [&](int64_t a, int64_t b) { c += (uint64_t)(b - a); };
+  auto point = [&](int64_t) { ++c; };
+  if (P.m & PM_INL)
+    gap_far(P.sn, P.a, P.m >> 8, [&](uint32_t w) { return (uint32_t)(P.bw >> (32u * w)); }, lim, range, point);
+  else
+    gap_far(P.sn, P.a, P.m >> 8, [&](uint32_t w) { return rd32(arena + P.bw + 4u * w, (P.m & PM_LE) != 0u); }, lim,
+            range, point);
+  return c;
+}
+// One proxy's far set as a workgroup works on it (LDS; loaded / stored by thread 0) and the
+// workgroup's scratch for the block-wide operations below.
+struct FTab {
+  uint64_t off;
+  uint32_t cap, n;
+  int64_t min;
+};
+struct FarSh {
+  FTab t;
+  unsigned long long x;  // reductions
+  uint64_t off;
+  uint32_t nc, k;
+};
+__device__ __forceinline__ void ftab_load(const State& s, uint32_t e, FTab& t) {
+  t = FTab{s.far_off[e], s.far_cap[e], s.far_n[e], s.far_min[e]};
+}
+__device__ __forceinline__ void ftab_store(const State& s, uint32_t e, const FTab& t) {
+  s.far_off[e] = t.off;
+  s.far_cap[e] = t.cap;
+  s.far_n[e] = t.n;
+  s.far_min[e] = t.min;
+}
+// t's SNs >= keep_from rehashed (keys kept) into a fresh pool table of nc slots.  Every thread
+// of the block calls it (nt threads), t read by all before; false: the pool is out (t unchanged).
+__device__ bool ftab_rehash(const State& s, FarSh& f, uint64_t nc, int64_t keep_from, uint32_t nt) {
+  const uint32_t tid = threadIdx.x;
+  __syncthreads();  // every thread has read f.t
+  if (tid == 0) {
+    f.nc = 0;
+    if (nc <= (1ull << 31)) {
+      const uint64_t off = atomicAdd(reinterpret_cast<unsigned long long*>(s.fused), (unsigned long long)nc);
+      if (off + nc <= s.fpcap) {
+        f.off = off;
+        f.nc = (uint32_t)nc;
       }
-      __syncthreads();
     }
+    f.k = 0;
+  }
+  __syncthreads();
+  const uint32_t c = f.nc;
+  if (c == 0) return false;
+  int64_t* nsn = s.fsn + f.off;
+  uint64_t* nkey = s.fkey + f.off;
+  for (uint32_t j = tid; j < c; j += nt) {
+    nsn[j] = FEMPTY;
+    nkey[j] = ~0ull;
+  }
+  __threadfence();
+  __syncthreads();
+  uint32_t moved = 0;
+  const int64_t* osn = s.fsn + f.t.off;
+  const uint64_t* okey = s.fkey + f.t.off;
+  for (uint32_t j = tid; j < f.t.cap; j += nt) {
+    const int64_t v = fld(osn + j);
+    if (v != FEMPTY && v >= keep_from) moved += fset_add(nsn, nkey, c - 1u, v, fldk(okey + j));
+  }
+  if (moved) atomicAdd(&f.k, moved);
+  __threadfence();
+  __syncthreads();
+  if (tid == 0) {
+    f.t.off = f.off;
+    f.t.cap = c;
+    f.t.n = f.k;
+  }
+  __syncthreads();
+  return true;
 }
-// Proxy e's far set into the LDS hash h (block-wide), the items' replay by thread 0 (items(k)
-// for k < m, in event order), the set back to global memory ascending.  Returns the misses
-// (thread 0).  Every thread of the block calls it.
-template <typename IF>
-__device__ uint64_t far_replay(uint32_t e, const State& s, int64_t* h, uint32_t m, IF&& items, const uint8_t* arena,
-                               uint8_t* acc, uint32_t* tcnt, uint32_t nt, uint32_t* s_cnt) {
-  int64_t* F = s.far + (uint64_t)e * FCAP;
-  const uint32_t n0 = s.far_n[e];
-  for (uint32_t j = threadIdx.x; j < FHS; j += nt) h[j] = INT64_MAX;
-  __syncthreads();
-  for (uint32_t j = threadIdx.x; j < n0; j += nt) {  // distinct SNs: one CAS each
-    const unsigned long long v = (unsigned long long)F[j];
-    for (uint32_t q = fh_slot(F[j]);; q = (q + 1u) & (FHS - 1u))
-      if (atomicCAS(reinterpret_cast<unsigned long long*>(h + q), (unsigned long long)INT64_MAX, v) ==
-          (unsigned long long)INT64_MAX)
-        break;
-  }
-  __syncthreads();
-  uint64_t miss = 0;
-  if (threadIdx.x == 0) {
-    uint32_t n = n0;
-    for (uint32_t k = 0; k < m; ++k) miss += far_apply(items(k), h, n, arena, acc, tcnt);
-    *s_cnt = n;
-  }
-  __syncthreads();
-  lds_sort(h, FHS, nt);  // the set first (INT64_MAX: free slots last)
-  const uint32_t n1 = *s_cnt;
-  for (uint32_t j = threadIdx.x; j < n1; j += nt) F[j] = h[j];
-  if (threadIdx.x == 0) s.far_n[e] = n1;
-  __threadfence();  // later reads of the set in this kernel (far_extend / far_pull) see it
-  __syncthreads();
-  return miss;
+// t made to take `need` more SNs at load <= 1/2 (a table of >= 4 x (n + need) slots when it
+// must grow).  Every thread calls it with the same need; false: the pool is out.
+__device__ bool ftab_reserve(const State& s, FarSh& f, uint64_t need, uint32_t nt) {
+  const uint64_t want = 2ull * ((uint64_t)f.t.n + need);
+  if (want <= f.t.cap) return true;
+  uint64_t nc = FT_MIN;
+  while (nc < 2ull * want) nc <<= 1;
+  return ftab_rehash(s, f, nc, INT64_MIN + 1, nt);
+}
+// the SNs each thread holds (f_of(j) for j < cnt) into t with key k_of(j); returns this thread's
+// least inserted SN (INT64_MAX: none).  Every thread calls it after ftab_reserve succeeded.
+template <typename F>
+__device__ void ftab_insert(const State& s, FarSh& f, F&& each) {
+  int64_t* sn = s.fsn + f.t.off;
+  uint64_t* key = s.fkey + f.t.off;
+  const uint32_t mask = f.t.cap - 1u;
+  uint32_t claimed = 0;
+  int64_t mn = INT64_MAX;
+  each([&](int64_t v, uint64_t k) {
+    claimed += fset_add(sn, key, mask, v, k);
+    if (v < mn) mn = v;
+  });
+  if (claimed) atomicAdd(&f.t.n, claimed);
+  if (mn != INT64_MAX) atomicMin(reinterpret_cast<unsigned long long*>(&f.t.min), (unsigned long long)mn);
+}
+// is sample key k its SN's first cover in t? (after every insert of the batch is visible)
+__device__ __forceinline__ bool ftab_first(const State& s, const FTab& t, int64_t v, uint64_t k) {
+  const uint32_t j = fset_find(s.fsn + t.off, t.cap - 1u, v);
+  return j != NONE && fldk(s.fkey + t.off + j) == k;
+}
+__device__ __forceinline__ uint64_t fkey_of(uint32_t epoch, uint32_t event) {
+  return ((uint64_t)epoch << 32) | event;
 }
 
-// The global paths' far items (after decide, before the deliveries): sorted by (proxy,
-// event), each proxy's replayed by far_replay.  One workgroup; launched when classify
-// counted candidates (identity batches) or always (expanded batches).
+// The global paths' far items (after decide, before the deliveries): each proxy's table
+// grown for the SNs its items cover, every SN inserted with its item's key, the samples
+// decided (rejected: acc 0; tcnt: its delivery tile's count).  One workgroup; launched when
+// classify counted candidates (identity batches) or always (expanded batches).
 constexpr uint32_t KF = 1024;
-__global__ __launch_bounds__(KF) void k_far(State s, const uint8_t* arena, uint8_t* acc, uint32_t* tcnt) {
-  __shared__ unsigned long long key[FL_CAP];  // proxy << 44 | event << 13 | item
-  __shared__ int64_t h[FHS];
-  __shared__ uint32_t s_cnt, s_end;
-  const uint64_t nf = s.ctr[C_NFAR];
-  const uint32_t m = (uint32_t)(nf < FL_CAP ? nf : FL_CAP);
-  if (m == 0) return;
-  uint32_t len = 1;
-  while (len < m) len <<= 1;
-  for (uint32_t k = threadIdx.x; k < len; k += KF)
-    key[k] = k < m ? ((unsigned long long)s.fl[k].e << 44) | ((unsigned long long)s.fl[k].p.k << 13) | k : ~0ull;
+__global__ __launch_bounds__(KF) void k_far(State s, const uint8_t* arena, uint8_t* acc, uint32_t* tcnt,
+                                            uint32_t n_proxies) {
+  __shared__ FarSh f;
+  __shared__ uint32_t s_list[KF], s_nl;
+  const uint32_t tid = threadIdx.x;
+  const uint64_t nf0 = s.ctr[C_NFAR];
+  const uint64_t nf = nf0 < s.fl_cap ? nf0 : s.fl_cap;
+  if (nf == 0) return;
+  uint64_t miss = tid == 0 ? nf0 - nf : 0;  // (past the list: not reached, the host sizes it)
+  for (uint64_t k = tid; k < nf; k += KF) {
+    const FarItem it = s.fl[k];
+    atomicAdd(reinterpret_cast<unsigned long long*>(s.fneed + it.e),
+              (unsigned long long)far_count(it.p, it.kind, it.lim, arena));
+  }
+  __threadfence();
   __syncthreads();
-  lds_sort(key, len, KF);
-  uint64_t miss = nf - m;  // items past the list: their samples stay accepted, their SNs unrecorded
-  for (uint32_t b = 0; b < m;) {
-    const uint32_t e = (uint32_t)(key[b] >> 44);
-    if (threadIdx.x == 0) {
-      uint32_t end = b + 1;
-      while (end < m && (uint32_t)(key[end] >> 44) == e) ++end;
-      s_end = end;
+  // the tables that must grow, KF proxies at a time, each by the whole workgroup
+  for (uint32_t e0 = 0; e0 < n_proxies; e0 += KF) {
+    if (tid == 0) s_nl = 0;
+    __syncthreads();
+    const uint32_t e = e0 + tid;
+    if (e < n_proxies) {
+      const uint64_t need = fldk(s.fneed + e);
+      if (need && 2ull * ((uint64_t)fld32(s.far_n + e) + need) > fld32(s.far_cap + e)) s_list[atomicAdd(&s_nl, 1u)] = e;
     }
     __syncthreads();
-    const uint32_t end = s_end;
-    miss += far_replay(e, s, h, end - b, [&](uint32_t k) { return s.fl[key[b + k] & 8191u]; }, arena, acc, tcnt, KF,
-                       &s_cnt);
-    b = end;
+    const uint32_t nl = s_nl;
+    for (uint32_t l = 0; l < nl; ++l) {
+      const uint32_t g = s_list[l];
+      if (tid == 0) ftab_load(s, g, f.t);
+      __syncthreads();
+      const bool ok = ftab_reserve(s, f, fldk(s.fneed + g), KF);
+      if (tid == 0) {
+        if (ok) ftab_store(s, g, f.t);
+        else s.fneed[g] = FNEED_OUT;
+      }
+      __threadfence();
+      __syncthreads();
+    }
   }
-  if (threadIdx.x == 0 && miss) atomicAdd(reinterpret_cast<unsigned long long*>(s.ctr + C_OVF), (unsigned long long)miss);
+  // every SN of every item, then the samples
+  for (uint64_t k = tid; k < nf; k += KF) {
+    const FarItem it = s.fl[k];
+    if (fldk(s.fneed + it.e) == FNEED_OUT) continue;
+    const uint64_t toff = fldk(s.far_off + it.e);
+    const uint32_t mask = fld32(s.far_cap + it.e) - 1u;
+    const uint64_t key = fkey_of(s.epoch, it.p.k);
+    uint32_t claimed = 0;
+    int64_t mn = INT64_MAX;
+    far_sns(it.p, it.kind, it.lim, arena, [&](int64_t v) {
+      claimed += fset_add(s.fsn + toff, s.fkey + toff, mask, v, key);
+      if (v < mn) mn = v;
+    });
+    if (claimed) atomicAdd(s.far_n + it.e, claimed);
+    if (mn != INT64_MAX) atomicMin(reinterpret_cast<unsigned long long*>(s.far_min + it.e), (unsigned long long)mn);
+  }
+  __threadfence();
+  __syncthreads();
+  for (uint64_t k = tid; k < nf; k += KF) {
+    const FarItem it = s.fl[k];
+    if (it.kind != FI_SAMPLE) continue;
+    if (fldk(s.fneed + it.e) == FNEED_OUT) {
+      ++miss;  // the pool was out: accepted unchecked
+      continue;
+    }
+    const FTab t{fldk(s.far_off + it.e), fld32(s.far_cap + it.e), 0u, 0};
+    if (!ftab_first(s, t, it.p.sn, fkey_of(s.epoch, it.p.k))) {
+      acc[it.p.k] = 0;
+      if (tcnt) atomicSub(&tcnt[it.p.k / DT], 1u);
+    }
+  }
+  __syncthreads();
+  for (uint64_t k = tid; k < nf; k += KF) s.fneed[s.fl[k].e] = 0;
+  if (miss) atomicAdd(reinterpret_cast<unsigned long long*>(s.ctr + C_OVF), (unsigned long long)miss);
 }
 
 // State, after the window pass found nb (the first uncovered SN >= the threshold inside the
 // window, or >= lo + W: every position covered, or the threshold past the window): nb
-// continues through the far set (thread 0; *s_nb), returned to every thread.
-__device__ int64_t far_extend(uint32_t e, const State& s, int64_t lo, int64_t nb, int64_t* s_nb) {
-  const uint32_t n = s.far_n[e];
-  if (n == 0 || nb < lo + (int64_t)W) return nb;
-  if (threadIdx.x == 0) {
-    const int64_t* F = s.far + (uint64_t)e * FCAP;
-    uint32_t a = 0, b = n;
-    while (a < b) {
-      const uint32_t mid = (a + b) >> 1;
-      if (F[mid] < nb) a = mid + 1u; else b = mid;
+// continues through the far set t, nt SNs looked up at a time.  Every thread; returns to all.
+__device__ int64_t far_extend(const State& s, FarSh& f, int64_t lo, int64_t nb, uint32_t nt) {
+  if (f.t.cap == 0 || nb < lo + (int64_t)W || nb < f.t.min) return nb;
+  const int64_t* sn = s.fsn + f.t.off;
+  const uint32_t mask = f.t.cap - 1u;
+  for (int64_t b = nb;; b += 4 * (int64_t)nt) {  // ends: the set holds at most n SNs
+    __syncthreads();
+    if (threadIdx.x == 0) f.x = ~0ull;
+    __syncthreads();
+    for (uint32_t r = 0; r < 4u; ++r) {
+      const int64_t v = b + (int64_t)(r * nt + threadIdx.x);
+      if (fset_find(sn, mask, v) == NONE) {
+        atomicMin(&f.x, (unsigned long long)v);
+        break;
+      }
     }
-    while (a < n && F[a] == nb) { ++nb; ++a; }
-    *s_nb = nb;
+    __syncthreads();
+    if (f.x != ~0ull) return (int64_t)f.x;
   }
-  __syncthreads();
-  return *s_nb;
 }
-// ...and after the window was re-anchored at nlo (its bits written): the far SNs the new
-// window spans set their bits there, those below it are dropped (below the new ack_base),
-// the rest move to the front of the set.  stage: FCAP int64 of LDS.
-__device__ void far_pull(uint32_t e, const State& s, int64_t nlo, int64_t* stage, uint32_t nt) {
-  const uint32_t n = s.far_n[e];
-  if (n == 0) return;
-  __syncthreads();  // the window's bits are written
-  int64_t* F = s.far + (uint64_t)e * FCAP;
-  uint32_t* bits = s.bits + (uint64_t)e * WW;
+// ...and after the window was re-anchored at nlo (its bits written to `bits`): the far SNs
+// the new window spans set their bits there; t.min becomes the least SN at or above its end.
+// When the SNs at or above it are under a quarter of the table's, they move to a smaller
+// one (the old table is left to the pool's compaction); none: the set is emptied.
+__device__ void far_pull(const State& s, FarSh& f, uint32_t* bits, int64_t nlo, uint32_t nt) {
   const int64_t hi = nlo + (int64_t)W;
-  uint32_t keep = 0;
-  for (uint32_t j = threadIdx.x; j < n; j += nt) {
-    const int64_t v = F[j];
-    stage[j] = v;
-    if (v >= nlo && v < hi) atomicOr(bits + ((uint64_t)(v - nlo) >> 5), 1u << ((uint64_t)(v - nlo) & 31u));
+  if (f.t.cap == 0 || f.t.min >= hi) return;
+  const uint32_t tid = threadIdx.x;
+  __syncthreads();  // the window's bits are written; every thread has read f.t
+  if (tid == 0) {
+    f.x = ~0ull;
+    f.k = 0;
   }
   __syncthreads();
-  uint32_t a = 0, b = n;  // first kept: the first >= hi (ascending)
-  while (a < b) {
-    const uint32_t mid = (a + b) >> 1;
-    if (stage[mid] < hi) a = mid + 1u; else b = mid;
+  const int64_t* sn = s.fsn + f.t.off;
+  uint32_t keep = 0;
+  int64_t mn = INT64_MAX;
+  for (uint32_t j = tid; j < f.t.cap; j += nt) {
+    const int64_t v = fld(sn + j);
+    if (v == FEMPTY || v < nlo) continue;
+    if (v >= hi) {
+      ++keep;
+      if (v < mn) mn = v;
+    } else {
+      atomicOr(bits + ((uint64_t)(v - nlo) >> 5), 1u << ((uint64_t)(v - nlo) & 31u));
+    }
   }
-  keep = n - a;
-  for (uint32_t j = threadIdx.x; j < keep; j += nt) F[j] = stage[a + j];
-  if (threadIdx.x == 0) s.far_n[e] = keep;
+  if (keep) atomicAdd(&f.k, keep);
+  if (mn != INT64_MAX) atomicMin(&f.x, (unsigned long long)mn);
+  __syncthreads();
+  const uint32_t k = f.k;
+  const bool shrink = k != 0 && 4u * k < f.t.n && f.t.cap > FT_MIN;
+  uint64_t nc = FT_MIN;
+  while (nc < 4ull * k) nc <<= 1;
+  if (shrink) (void)ftab_rehash(s, f, nc, hi, nt);  // (the pool out: the table stays as it is)
+  if (tid == 0) {
+    if (k == 0) f.t = FTab{0, 0u, 0u, INT64_MAX};
+    else f.t.min = (int64_t)f.x;
+  }
+  __syncthreads();
 }
 
 // ---- 6 merge ----
@@ -1507,9 +1668,10 @@ __global__ __launch_bounds__(IT) void k_merge(const rtps_record* recs, const uin
 // minimum, and the window re-anchored at the new ack_base from the LDS copy.
 // fcm: the batch's coverage is in dbits (k_decide_t<2>): OR it into the window, clear it
 __device__ __forceinline__ void state_proxy(uint32_t e, const Scratch& x, const State& s, bool reliable,
-                                            int64_t* ack_out, uint32_t* sh, uint32_t& s_first, int64_t* s_nb,
+                                            int64_t* ack_out, uint32_t* sh, uint32_t& s_first, FarSh& f,
                                             bool fcm = false) {
   const uint32_t tid = threadIdx.x;
+  if (tid == 0) ftab_load(s, e, f.t);
   const int64_t lo = s.lo[e];
   int64_t thr = s.base[e];
   int32_t hbc = s.hbc[e];
@@ -1549,15 +1711,16 @@ __device__ __forceinline__ void state_proxy(uint32_t e, const Scratch& x, const 
     __syncthreads();
     nb = lo + (int64_t)(s_first != NONE ? s_first : W);
   }
-  nb = far_extend(e, s, lo, nb, s_nb);
+  nb = far_extend(s, f, lo, nb, IT);
   // re-anchor the window at the new ack_base (bits below it are no longer needed)
   const int64_t nlo = nb & ~(int64_t)31;
   if (nlo != lo) {
     const uint64_t shift = (uint64_t)(nlo - lo) >> 5;
     for (uint32_t w = tid; w < WW; w += IT) bits[w] = (w + shift < WW) ? sh[w + shift] : 0u;
   }
-  far_pull(e, s, nlo, reinterpret_cast<int64_t*>(sh), IT);
+  far_pull(s, f, bits, nlo, IT);
   if (tid == 0) {
+    ftab_store(s, e, f.t);
     s.base[e] = nb;
     s.lo[e] = nlo;
     s.hbc[e] = hbc;
@@ -1569,10 +1732,10 @@ __global__ __launch_bounds__(IT) void k_state(uint32_t n_entries, Scratch x, Sta
                                               uint64_t* ovf_out) {
   __shared__ __attribute__((aligned(16))) uint32_t sh[WW];
   __shared__ uint32_t s_first;
-  __shared__ int64_t s_nb;
+  __shared__ FarSh f;
   const uint32_t e = blockIdx.x;
   if (e >= n_entries) return;
-  state_proxy(e, x, s, reliable, ack_out, sh, s_first, &s_nb);
+  state_proxy(e, x, s, reliable, ack_out, sh, s_first, f);
   if (threadIdx.x == 0 && e == 0 && ovf_out) *ovf_out = s.ctr[C_OVF];
 }
 // Global identity path, last launch: workgroups [0, ntiles) write the deliveries (k_dwrite;
@@ -1585,7 +1748,7 @@ __global__ __launch_bounds__(IT) void k_dstate(const uint8_t* flag, uint64_t n, 
   __shared__ uint32_t s_c[IT / 64];
   __shared__ __attribute__((aligned(16))) uint32_t sh[WW];
   __shared__ uint32_t s_first;
-  __shared__ int64_t s_nb;
+  __shared__ FarSh f;
   if (guarded) {  // queued before the host had the counts: only k_signal's plain batches
     const uint64_t mode = ctr[C_MODE];
     if (mode == 0) return;
@@ -1594,7 +1757,7 @@ __global__ __launch_bounds__(IT) void k_dstate(const uint8_t* flag, uint64_t n, 
   if (blockIdx.x < ntiles) {
     dwrite_tile(blockIdx.x, flag, n, tcnt, ntiles, x, true, max_out, out, n_out, ctr, ovf_out, nullptr, s_w, s_c);
   } else if (blockIdx.x - ntiles < n_entries) {
-    state_proxy(blockIdx.x - ntiles, x, s, reliable, ack_out, sh, s_first, &s_nb, fcm);
+    state_proxy(blockIdx.x - ntiles, x, s, reliable, ack_out, sh, s_first, f, fcm);
   }
 }
 
@@ -1778,15 +1941,16 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
   __shared__ uint32_t s_first;
   __shared__ GapE s_gap[GCAP];  // the chunk's GAPs (the first GCAP), one per thread in the GAP phases
   __shared__ uint32_t s_ngap;
-  __shared__ uint32_t s_nfi, s_fcnt;  // far items pushed by this workgroup; the replay's set size
-  __shared__ uint32_t s_fpos[FPX];     // their list positions (the list is shared by every proxy's workgroup)
-  __shared__ int64_t s_nb;
-  static_assert(PH * 4u >= FHS * 8u && PH * 4u >= FPX * 8u && WW * 4u >= FCAP * 8u && FPX <= FL_CAP,
-                "far replay LDS reuse");
+  __shared__ FarSh fsh;                // the proxy's far set
+  __shared__ unsigned long long s_fp;  // SNs the chunk's far items cover
   const uint32_t e = blockIdx.x, tid = threadIdx.x;
   if (e >= n_proxies) return;
   PST_DECL;  // (setup: the window, the hash and the piece tables)
-  if (tid == 0) { s_ngap = 0u; s_nfi = 0u; }
+  if (tid == 0) {
+    s_ngap = 0u;
+    s_fp = 0ull;
+    ftab_load(s, e, fsh.t);
+  }
   const int64_t lo = s.lo[e], base = s.base[e];
   uint32_t* gbits = s.bits + (uint64_t)e * WW;
   for (uint32_t w = tid; w < WW; w += PT) { sb[w] = gbits[w]; pres[w] = 0u; }
@@ -1972,12 +2136,8 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
     // decide (should_ignore_change: rtps_writer_proxy.rs:202-230, reader.rs:693-758)
     int64_t t_run = thr;
     const int64_t lim = lo + (int64_t)W;
-    auto far = [&](uint32_t j, uint32_t kind) {  // a far item (rare): to the list, replayed at the end
-      const uint32_t pos = far_push(s.ctr, s.fl, FarItem{PEv{v[j], a[j], bwj[j], m[j], kk[j]}, lim, e, kind});
-      const uint32_t c = pos != NONE ? atomicAdd(&s_nfi, 1u) : FPX;
-      if (c < FPX) s_fpos[c] = pos;
-      else ++n_ovf;  // past the list or the replay's capacity: its sample stays accepted
-    };
+    uint32_t fkind = 0;  // far items (rare) of the thread's events: kind << 2 j, into the far set below
+    auto far = [&](uint32_t j, uint32_t kind) { fkind |= kind << (2u * j); };
 #pragma unroll
     for (uint32_t j = 0; j < PPT; ++j) {
       if (f[j] > t_run) t_run = f[j];
@@ -2000,7 +2160,44 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
       }
       acc_out[kk[j]] = acc;
     }
-    __syncthreads();
+    if (__syncthreads_or(fkind != 0u)) {
+      // the chunk's far items: every SN they cover into the far set (the table grown first for
+      // all of them), then their samples decided by first cover (see "far sequence numbers")
+      uint64_t pc = 0;
+#pragma unroll
+      for (uint32_t j = 0; j < PPT; ++j) {
+        const uint32_t kind = (fkind >> (2u * j)) & 3u;
+        if (kind) pc += far_count(PEv{v[j], a[j], bwj[j], m[j], kk[j]}, kind, lim, arena);
+      }
+      if (pc) atomicAdd(&s_fp, (unsigned long long)pc);
+      uint32_t nfi = 0;
+#pragma unroll
+      for (uint32_t j = 0; j < PPT; ++j) nfi += ((fkind >> (2u * j)) & 3u) != 0u;
+      if (nfi) atomicAdd(reinterpret_cast<unsigned long long*>(s.ctr + C_NFAR), (unsigned long long)nfi);
+      __syncthreads();
+      if (ftab_reserve(s, fsh, s_fp, PT)) {
+        ftab_insert(s, fsh, [&](auto&& add) {
+#pragma unroll
+          for (uint32_t j = 0; j < PPT; ++j) {
+            const uint32_t kind = (fkind >> (2u * j)) & 3u;
+            if (kind)
+              far_sns(PEv{v[j], a[j], bwj[j], m[j], kk[j]}, kind, lim, arena,
+                      [&](int64_t sn) { add(sn, fkey_of(s.epoch, kk[j])); });
+          }
+        });
+        __threadfence();
+        __syncthreads();
+#pragma unroll
+        for (uint32_t j = 0; j < PPT; ++j)
+          if (((fkind >> (2u * j)) & 3u) == FI_SAMPLE && !ftab_first(s, fsh.t, v[j], fkey_of(s.epoch, kk[j])))
+            acc_out[kk[j]] = 0;
+      } else {
+#pragma unroll
+        for (uint32_t j = 0; j < PPT; ++j) n_ovf += ((fkind >> (2u * j)) & 3u) == FI_SAMPLE;  // the pool was out: unchecked
+      }
+      __syncthreads();
+      if (tid == 0) s_fp = 0ull;
+    }
     PST(5);
     // merge the chunk's coverage into the window, clear the hash and the presence bits
     auto gap_or = [&](int64_t gv, int64_t ga, uint64_t bw, uint32_t gm) {
@@ -2028,21 +2225,6 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
     __syncthreads();
     PST(6);
   }
-  // the far items (this proxy's, from the batch list) replayed in event order against the far set
-  __syncthreads();
-  if (s_nfi) {
-    __threadfence();  // this workgroup's items in the list are visible to all its threads
-    const uint32_t mi = s_nfi < FPX ? s_nfi : FPX;
-    unsigned long long* fk = reinterpret_cast<unsigned long long*>(h_min);  // FPX keys: event << 13 | item
-    for (uint32_t c = tid; c < mi; c += PT) fk[c] = ((unsigned long long)s.fl[s_fpos[c]].p.k << 13) | s_fpos[c];
-    uint32_t len = 1;
-    while (len < mi) len <<= 1;
-    for (uint32_t k = mi + tid; k < len; k += PT) fk[k] = ~0ull;
-    __syncthreads();
-    lds_sort(fk, len, PT);
-    n_ovf += far_replay(e, s, reinterpret_cast<int64_t*>(h_key), mi,
-                        [&](uint32_t k) { return s.fl[fk[k] & 8191u]; }, arena, acc_out, nullptr, PT, &s_fcnt);
-  }
   if (n_ovf) atomicAdd(reinterpret_cast<unsigned long long*>(s.ctr + C_OVF), (unsigned long long)n_ovf);
   // state (as k_state): ack_base = first sequence number >= threshold outside the change set
   int64_t nb = run_thr;
@@ -2062,12 +2244,13 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
     }
     nb = lo + (int64_t)(s_first != NONE ? s_first : W);
   }
-  nb = far_extend(e, s, lo, nb, &s_nb);
+  nb = far_extend(s, fsh, lo, nb, PT);
   const int64_t nlo = nb & ~(int64_t)31;
   const uint64_t shift = (uint64_t)(nlo - lo) >> 5;
   for (uint32_t w = tid; w < WW; w += PT) gbits[w] = (w + shift < WW) ? sb[w + shift] : 0u;
-  far_pull(e, s, nlo, reinterpret_cast<int64_t*>(pres), PT);
+  far_pull(s, fsh, gbits, nlo, PT);
   if (tid == 0) {
+    ftab_store(s, e, fsh.t);
     s.base[e] = nb;
     s.lo[e] = nlo;
     s.hbc[e] = (int32_t)run_cnt;
@@ -2082,14 +2265,36 @@ __global__ void k_init_state(uint32_t n, State s) {
     s.base[e] = 1;  // RtpsWriterProxy::new: ack_base = SequenceNumber::new(1)
     s.lo[e] = 0;
     s.hbc[e] = 0;
+    s.far_off[e] = 0;
+    s.far_cap[e] = 0;
     s.far_n[e] = 0;
+    s.far_min[e] = INT64_MAX;
+    s.fneed[e] = 0;
   }
+}
+// the far-set pool compacted: proxy e's table [far_off[e], + far_cap[e]) to noff[e] of the new pool
+__global__ void k_far_move(uint32_t n, State s, int64_t* nsn, uint64_t* nkey, const uint64_t* noff) {
+  const uint32_t e = blockIdx.x;
+  if (e >= n || s.far_cap[e] == 0) return;
+  const uint64_t o = s.far_off[e], d = noff[e];
+  for (uint32_t j = threadIdx.x; j < s.far_cap[e]; j += blockDim.x) {
+    nsn[d + j] = s.fsn[o + j];
+    nkey[d + j] = s.fkey[o + j];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) s.far_off[e] = d;
+}
+// the epoch counter wrapped: every far SN held becomes "covered before" (key 0)
+__global__ void k_far_rekey(uint64_t n, int64_t* sn, uint64_t* key) {
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x)
+    key[j] = sn[j] == FEMPTY ? ~0ull : 0ull;
 }
 __global__ void k_finish(const uint64_t* ctr, uint64_t* ovf) { if (ovf) *ovf = ctr[C_OVF]; }
 __global__ void k_hev(const uint64_t* ctr, uint64_t* hev) {
   uint64_t ne = 0;
   for (uint32_t k = 0; k < 64; ++k) ne += ctr[C_SPREAD + 4 * k + 2];
-  *hev = ne;
+  hev[0] = ne;
+  hev[1] = ctr[C_NFAR];
 }
 
 static inline uint64_t hmin(uint64_t a, uint64_t b) { return a < b ? a : b; }
@@ -2134,10 +2339,18 @@ struct IngestState {
   hipEvent_t hnev_ev = nullptr;
   bool hnev_ready = false;
   uint64_t last_nev = 0;      // events of the last batch whose counts were read
+  uint64_t last_far = 0;      // ...and its far items (per-proxy path)
   uint64_t* hsig = nullptr;    // pinned, coherent: classify's count signal (SIG_*)
   uint64_t sig_tag = 0;
   uint32_t* bk_cl = nullptr;  // proxy bucketing: per (classify workgroup, proxy) events | first position << 16
   uint64_t bkcap = 0;
+  // far-set pool (st.fsn / fkey / fused / fpcap; see "far sequence numbers"): the device counter
+  // as last seen -- exact after a sync, else the side stream's copy taken after an earlier batch
+  uint64_t fp_used = 0;
+  uint64_t* hfused = nullptr;  // pinned: that copy
+  hipStream_t fside = nullptr;
+  hipEvent_t fev = nullptr, fcp = nullptr;
+  bool fcp_pending = false;
 };
 
 static void free_bk(IngestState* s) {
@@ -2186,14 +2399,115 @@ int rtps_ingest_proxy_stamps(uint64_t* host, uint64_t n) {
 #endif
 }
 
+// the fields of State that are not per proxy (kept when the per-proxy arrays are rebuilt)
+static void keep_shared(State& m, const State& o) {
+  m.ctr = o.ctr;
+  m.fsn = o.fsn;
+  m.fkey = o.fkey;
+  m.fused = o.fused;
+  m.fpcap = o.fpcap;
+  m.fl = o.fl;
+  m.fl_cap = o.fl_cap;
+  m.epoch = o.epoch;
+}
 static void free_state(IngestState* s) {
   void* p[] = {s->st.base, s->st.lo, s->st.hbc, s->st.bits, s->st.fc, s->st.dbits, s->st.seg_b, s->st.seg_e,
-               s->st.far, s->st.far_n, s->st.fl};
+               s->st.far_off, s->st.far_cap, s->st.far_n, s->st.far_min, s->st.fneed};
   for (void* q : p) if (q) (void)hipFree(q);
-  uint64_t* ctr = s->st.ctr;
-  s->st = State{};
-  s->st.ctr = ctr;
+  State k{};
+  keep_shared(k, s->st);
+  s->st = k;
   s->ecap = 0;
+}
+static void free_far(IngestState* s) {
+  void* p[] = {s->st.fsn, s->st.fkey, s->st.fl};
+  for (void* q : p) if (q) (void)hipFree(q);
+  s->st.fsn = nullptr;
+  s->st.fkey = nullptr;
+  s->st.fpcap = 0;
+  s->st.fl = nullptr;
+  s->st.fl_cap = 0;
+}
+// the batch's far-item list (global paths): one entry per event at most
+static bool grow_fl(IngestState* s, uint64_t n, hipStream_t st) {
+  if (n <= s->st.fl_cap) return true;
+  (void)hipStreamSynchronize(st);
+  if (s->st.fl) (void)hipFree(s->st.fl);
+  s->st.fl = nullptr;
+  s->st.fl_cap = 0;
+  uint64_t c = 1024;
+  while (c < n) c <<= 1;
+  if (hipMalloc(&s->st.fl, c * sizeof(FarItem)) != hipSuccess) {
+    s->st.fl = nullptr;
+    return false;
+  }
+  s->st.fl_cap = c;
+  return true;
+}
+// Before the far items of a batch that can cover up to F far SNs are decided: the far-set pool
+// keeps >= 8 (F + 2^16) + 2 x used slots free -- what the batch's tables can take (a table
+// grows to <= 4 x its SNs, the proxy's old entries included, and a chain of growths in the
+// per-proxy pass sums to <= twice its last table).  When the last seen count says it may
+// not, the stream is synchronised and the count read; still short: the live tables are
+// packed at the front of a larger pool (k_far_move) and the abandoned ones dropped.
+static bool far_pool_ensure(IngestState* s, uint64_t F, hipStream_t st) {
+  if (s->fcp_pending && hipEventQuery(s->fcp) == hipSuccess) {
+    s->fp_used = *s->hfused;
+    s->fcp_pending = false;
+  }
+  auto room = [&](uint64_t used) { return 8 * (F + 65536) + 2 * used; };
+  if (s->st.fpcap && s->fp_used + room(s->fp_used) <= s->st.fpcap) return true;
+  if (hipStreamSynchronize(st) != hipSuccess || hipStreamSynchronize(s->fside) != hipSuccess) return false;
+  s->fcp_pending = false;
+  uint64_t used = 0;
+  if (hipMemcpy(&used, s->st.fused, 8, hipMemcpyDeviceToHost) != hipSuccess) return false;
+  s->fp_used = used;
+  if (s->st.fpcap && used + room(used) <= s->st.fpcap) return true;
+  // compaction: the live tables' new offsets (packed in proxy order)
+  const uint32_t ne = s->ecap;
+  std::vector<uint32_t> cap(ne);
+  std::vector<uint64_t> noff(ne);
+  if (ne && hipMemcpy(cap.data(), s->st.far_cap, ne * 4ull, hipMemcpyDeviceToHost) != hipSuccess) return false;
+  uint64_t live = 0;
+  for (uint32_t e = 0; e < ne; ++e) {
+    noff[e] = live;
+    live += cap[e];
+  }
+  const uint64_t nc = (live + room(live)) * 3 / 2;
+  int64_t* nsn = nullptr;
+  uint64_t* nkey = nullptr;
+  uint64_t* dnoff = nullptr;
+  bool ok = hipMalloc(&nsn, nc * 8) == hipSuccess && hipMalloc(&nkey, nc * 8) == hipSuccess;
+  if (ok && live) {
+    ok = hipMalloc(&dnoff, ne * 8ull) == hipSuccess &&
+         hipMemcpy(dnoff, noff.data(), ne * 8ull, hipMemcpyHostToDevice) == hipSuccess;
+    if (ok) hipLaunchKernelGGL(k_far_move, dim3(ne), dim3(256), 0, st, ne, s->st, nsn, nkey, dnoff);
+    ok = ok && hipStreamSynchronize(st) == hipSuccess;
+  }
+  ok = ok && hipMemcpy(s->st.fused, &live, 8, hipMemcpyHostToDevice) == hipSuccess;
+  if (dnoff) (void)hipFree(dnoff);
+  if (!ok) {
+    if (nsn) (void)hipFree(nsn);
+    if (nkey) (void)hipFree(nkey);
+    return false;
+  }
+  if (s->st.fsn) (void)hipFree(s->st.fsn);
+  if (s->st.fkey) (void)hipFree(s->st.fkey);
+  s->st.fsn = nsn;
+  s->st.fkey = nkey;
+  s->st.fpcap = nc;
+  s->fp_used = live;
+  return true;
+}
+// after the batch: the pool's counter copied to pinned memory on the side stream (no wait on
+// the batch's stream), for the next batch's far_pool_ensure
+static void far_pool_note(IngestState* s, hipStream_t st) {
+  if (s->fcp_pending) return;  // the previous copy is still in flight
+  if (hipEventRecord(s->fev, st) != hipSuccess || hipStreamWaitEvent(s->fside, s->fev, 0) != hipSuccess ||
+      hipMemcpyAsync(s->hfused, s->st.fused, 8, hipMemcpyDeviceToHost, s->fside) != hipSuccess ||
+      hipEventRecord(s->fcp, s->fside) != hipSuccess)
+    return;
+  s->fcp_pending = true;
 }
 static void free_rscratch(IngestState* s) {
   void* p[] = {s->x.fidx, s->x.fmask, s->x.fall, s->x.rcnt, s->x.roff, s->x.rset, s->x.rkind, s->x.rsn};
@@ -2226,13 +2540,14 @@ static bool grow_state(IngestState* s, uint32_t n, hipStream_t st) {
   (void)hipStreamSynchronize(st);
   State o = s->st;
   State m{};
-  m.ctr = o.ctr;
+  keep_shared(m, o);
   bool ok = hipMalloc(&m.base, ncap * 8ull) == hipSuccess && hipMalloc(&m.lo, ncap * 8ull) == hipSuccess &&
             hipMalloc(&m.hbc, ncap * 4ull) == hipSuccess && hipMalloc(&m.bits, (uint64_t)ncap * WW * 4) == hipSuccess &&
             hipMalloc(&m.fc, (uint64_t)ncap * W * 8) == hipSuccess && hipMalloc(&m.seg_b, ncap * 4ull) == hipSuccess &&
             hipMalloc(&m.dbits, (uint64_t)ncap * WW * 4) == hipSuccess &&
-            hipMalloc(&m.seg_e, ncap * 4ull) == hipSuccess && hipMalloc(&m.far, (uint64_t)ncap * FCAP * 8) == hipSuccess &&
-            hipMalloc(&m.far_n, ncap * 4ull) == hipSuccess && hipMalloc(&m.fl, FL_CAP * sizeof(FarItem)) == hipSuccess;
+            hipMalloc(&m.seg_e, ncap * 4ull) == hipSuccess && hipMalloc(&m.far_off, ncap * 8ull) == hipSuccess &&
+            hipMalloc(&m.far_cap, ncap * 4ull) == hipSuccess && hipMalloc(&m.far_n, ncap * 4ull) == hipSuccess &&
+            hipMalloc(&m.far_min, ncap * 8ull) == hipSuccess && hipMalloc(&m.fneed, ncap * 8ull) == hipSuccess;
   ok = ok && hipMemsetAsync(m.bits, 0, (uint64_t)ncap * WW * 4, st) == hipSuccess &&
        hipMemsetAsync(m.dbits, 0, (uint64_t)ncap * WW * 4, st) == hipSuccess &&
        hipMemsetAsync(m.fc, 0xff, (uint64_t)ncap * W * 8, st) == hipSuccess;
@@ -2243,16 +2558,17 @@ static bool grow_state(IngestState* s, uint32_t n, hipStream_t st) {
          hipMemcpyAsync(m.lo, o.lo, e * 8, hipMemcpyDeviceToDevice, st) == hipSuccess &&
          hipMemcpyAsync(m.hbc, o.hbc, e * 4, hipMemcpyDeviceToDevice, st) == hipSuccess &&
          hipMemcpyAsync(m.bits, o.bits, e * WW * 4, hipMemcpyDeviceToDevice, st) == hipSuccess &&
-         hipMemcpyAsync(m.far, o.far, e * FCAP * 8, hipMemcpyDeviceToDevice, st) == hipSuccess &&
-         hipMemcpyAsync(m.far_n, o.far_n, e * 4, hipMemcpyDeviceToDevice, st) == hipSuccess;
+         hipMemcpyAsync(m.far_off, o.far_off, e * 8, hipMemcpyDeviceToDevice, st) == hipSuccess &&
+         hipMemcpyAsync(m.far_cap, o.far_cap, e * 4, hipMemcpyDeviceToDevice, st) == hipSuccess &&
+         hipMemcpyAsync(m.far_n, o.far_n, e * 4, hipMemcpyDeviceToDevice, st) == hipSuccess &&
+         hipMemcpyAsync(m.far_min, o.far_min, e * 8, hipMemcpyDeviceToDevice, st) == hipSuccess;
   }
   ok = ok && hipStreamSynchronize(st) == hipSuccess;
   s->st = m;
   s->ecap = ncap;
   State dead = o;
-  dead.ctr = nullptr;
   void* p[] = {dead.base, dead.lo, dead.hbc, dead.bits, dead.fc, dead.dbits, dead.seg_b, dead.seg_e,
-               dead.far, dead.far_n, dead.fl};
+               dead.far_off, dead.far_cap, dead.far_n, dead.far_min, dead.fneed};
   for (void* q : p) if (q) (void)hipFree(q);
   if (!ok) { free_state(s); return false; }
   return true;
@@ -2314,6 +2630,15 @@ IngestState* rtps_ingest_state_new(int device) {
   if (!s) return nullptr;
   s->device = device;
   if (hipMalloc(&s->ctr_base, 2 * C_COUNT * 8) != hipSuccess) { delete s; return nullptr; }
+  if (hipMalloc(&s->st.fused, 8) != hipSuccess || hipMemset(s->st.fused, 0, 8) != hipSuccess ||
+      hipHostMalloc(&s->hfused, 8, hipHostMallocDefault) != hipSuccess ||
+      hipStreamCreateWithFlags(&s->fside, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&s->fev, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&s->fcp, hipEventDisableTiming) != hipSuccess) {
+    rtps_ingest_state_free(s);
+    return nullptr;
+  }
+  *s->hfused = 0;
   if (hipMemset(s->ctr_base, 0, 2 * C_COUNT * 8) != hipSuccess) {
     (void)hipFree(s->ctr_base);
     delete s;
@@ -2337,6 +2662,12 @@ void rtps_ingest_state_free(IngestState* s) {
   free_vscratch(s);
   free_rscratch(s);
   free_state(s);
+  free_far(s);
+  if (s->st.fused) (void)hipFree(s->st.fused);
+  if (s->hfused) (void)hipHostFree(s->hfused);
+  if (s->fside) (void)hipStreamDestroy(s->fside);
+  if (s->fev) (void)hipEventDestroy(s->fev);
+  if (s->fcp) (void)hipEventDestroy(s->fcp);
   if (s->ctr_base) (void)hipFree(s->ctr_base);
   if (s->hctr) (void)hipHostFree(s->hctr);
   if (s->hctr2) (void)hipHostFree(s->hctr2);
@@ -2350,10 +2681,14 @@ int rtps_ingest_state_reset(IngestState* s, hipStream_t st) {
   bool ok = hipMemsetAsync(s->st.bits, 0, (uint64_t)s->ecap * WW * 4, st) == hipSuccess &&  // fc: epoch-tagged
             hipMemsetAsync(s->st.dbits, 0, (uint64_t)s->ecap * WW * 4, st) == hipSuccess;
   if (ok) hipLaunchKernelGGL(k_init_state, dim3((s->ecap + IT - 1) / IT), dim3(IT), 0, st, s->ecap, s->st);
+  // every far set emptied: the pool's tables are all free again
+  ok = ok && hipStreamSynchronize(s->fside) == hipSuccess && hipMemsetAsync(s->st.fused, 0, 8, st) == hipSuccess;
+  s->fcp_pending = false;
+  s->fp_used = 0;
   return ok && hipGetLastError() == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP;
 }
 
-int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const uint8_t* arena, uint64_t arena_len,
+static int ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const uint8_t* arena, uint64_t arena_len,
                       const uint64_t* dgram_off, const rtps_record* records, const uint64_t* n_records,
                       uint64_t max_records, const rtps_frag_sample* frag, const uint64_t* n_frag, uint64_t max_frag,
                       uint32_t flags, const rtps_ingest_out* out) {
@@ -2369,10 +2704,18 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
   const bool reliable = !(flags & RTPS_INGEST_BEST_EFFORT);
   const FarSrc fs{records, dgram_off};
   const SigCfg cfg{ident ? 1u : 0u, t.n_proxies, s->path, reliable ? 1u : 0u};
-  if (++s->epoch == 0xffffffffu) {  // keys would wrap: clear the first-cover table
+  if (++s->epoch == 0xffffffffu) {  // keys would wrap: clear the first-cover table, age the far sets' keys
     if (hipMemsetAsync(s->st.fc, 0xff, (uint64_t)s->ecap * W * 8, st) != hipSuccess) return RTPS_RX_EHIP;
+    uint64_t used = 0;
+    if (hipStreamSynchronize(st) != hipSuccess || hipMemcpy(&used, s->st.fused, 8, hipMemcpyDeviceToHost) != hipSuccess)
+      return RTPS_RX_EHIP;
+    used = used < s->st.fpcap ? used : s->st.fpcap;
+    if (used)
+      hipLaunchKernelGGL(k_far_rekey, dim3((uint32_t)hmin((used + 255) / 256, 4096)), dim3(256), 0, st, used, s->st.fsn,
+                         s->st.fkey);
     s->epoch = 1;
   }
+  s->st.epoch = s->epoch;
   uint32_t ebits = 1;
   while ((1u << ebits) < t.n_proxies) ++ebits;  // sort key width: proxies < 2^ebits
   const uint32_t gb = (uint32_t)hmin((max + IT - 1) / IT, 8192);
@@ -2402,10 +2745,13 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
   // uses the previous batch's counts (mean events per proxy), read without a sync.
   if (s->hnev_ready && hipEventQuery(s->hnev_ev) == hipSuccess) {
     s->last_nev = s->hctr2[0];
+    s->last_far = s->hctr2[1];
     s->hnev_ready = false;
   }
+  // (after a batch with far items the next takes the signalled path, which sizes the far-set
+  // pool from its own counts; the fast path sizes it from the last one's far items)
   const bool fast = ident && t.n_proxies > 0 &&
-                    (s->path == 2 || s->path == 4 || (s->path == 0 && t.n_proxies >= 64 &&
+                    (s->path == 2 || s->path == 4 || (s->path == 0 && t.n_proxies >= 64 && s->last_far == 0 &&
                                                       s->last_nev <= (uint64_t)t.n_proxies * 32768u));
   // the proxy bucketing (k_classify<.., BUCKET>, k_proxy<true>) unless the proxies or the
   // classify workgroups exceed its LDS tables (or path 4: the radix sort, tests)
@@ -2413,6 +2759,7 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
   const bool bucket = fast && t.n_proxies <= PB_MAX && nblk <= BK_MAX && s->path != 4;
   FastOut fo{nullptr, nullptr, arena, dgram_off, S.seg_b, S.seg_e, s->ecap, nullptr, sets_lds ? 1u : 0u};
   if (fast) {
+    if (!far_pool_ensure(s, 2 * s->last_far, st)) return RTPS_RX_ENOMEM;
     if (!grow_pscratch(s, bucket ? nblk * CHR : max, st)) return RTPS_RX_ENOMEM;
     fo.pev = s->pev;
     fo.acc = out->accept;
@@ -2490,6 +2837,10 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
   if (ident && s->hsig[SIG_MODE] != 0) return RTPS_RX_OK;  // the queued plain path runs it
   // events live at [0, nev): record slots in identity batches, the expanded list otherwise
   uint64_t nev = ident ? n_rec : n_ev;
+  // far items: at most classify's candidates (every path but the fast one counts them); their far SNs
+  // (a GAP's listed ones included) bound the far-set tables this batch can grow
+  const uint64_t nfi = farc;
+  if (nfi && (!grow_fl(s, nfi, st) || !far_pool_ensure(s, nfi + 256 * n_gap, st))) return RTPS_RX_ENOMEM;
   if (!ident) {
     if (n_ev > 0x7fffffffull) return RTPS_RX_ETOOBIG;
     if (!grow_vscratch(s, n_ev ? n_ev : 1, st)) return RTPS_RX_ENOMEM;
@@ -2582,7 +2933,7 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
       hipLaunchKernelGGL(k_decide_t<0>, dim3(ntiles), dim3(IT), 0, st, nev, acc_cap, x, S, acc, have_hb, s->epoch,
                          x.sel, fs, ntiles, SigOut{});
     if (farc)  // samples / GAPs past some window: their replay (fixes accept[] and the tile counts)
-      hipLaunchKernelGGL(k_far, dim3(1), dim3(KF), 0, st, S, arena, acc, x.sel);
+      hipLaunchKernelGGL(k_far, dim3(1), dim3(KF), 0, st, S, arena, acc, x.sel, t.n_proxies);
     if (n_gap)
       hipLaunchKernelGGL(k_merge, dim3(gv), dim3(IT), 0, st, records, arena, dgram_off, nev, x, S, true);
     hipLaunchKernelGGL(k_dstate, dim3(ntiles + t.n_proxies), dim3(IT), 0, st, acc, acc_cap, x.sel, ntiles, x,
@@ -2599,8 +2950,8 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
   if (acc_cap && !per_proxy) {
     hipLaunchKernelGGL(k_decide, dim3((uint32_t)hmin((acc_cap + IT - 1) / IT, 8192)), dim3(IT), 0, st, nev, acc_cap,
                        x, S, acc, have_hb, s->epoch, fs);
-    // the far replay (expanded batches: classify cannot tell their proxies' windows; an empty list returns at once)
-    hipLaunchKernelGGL(k_far, dim3(1), dim3(KF), 0, st, S, arena, acc, (uint32_t*)nullptr);
+    if (farc)  // the far items' first covers (fixes accept[])
+      hipLaunchKernelGGL(k_far, dim3(1), dim3(KF), 0, st, S, arena, acc, (uint32_t*)nullptr, t.n_proxies);
   }
   const bool state_pass = t.n_proxies && !per_proxy;  // k_state copies the overflow count out, else the select does
   deliver(acc, acc_cap, x, ident, out, st, S.ctr, !state_pass);
@@ -2615,4 +2966,14 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
     hipLaunchKernelGGL(k_state, dim3(t.n_proxies), dim3(IT), 0, st, t.n_proxies, x, S, have_hb, out->ack_base,
                        out->n_window_overflow);
   return hipGetLastError() == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP;
+}
+
+int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const uint8_t* arena, uint64_t arena_len,
+                      const uint64_t* dgram_off, const rtps_record* records, const uint64_t* n_records,
+                      uint64_t max_records, const rtps_frag_sample* frag, const uint64_t* n_frag, uint64_t max_frag,
+                      uint32_t flags, const rtps_ingest_out* out) {
+  const int rc = ingest_batch(s, st, t, arena, arena_len, dgram_off, records, n_records, max_records, frag, n_frag,
+                              max_frag, flags, out);
+  if (rc == RTPS_RX_OK) far_pool_note(s, st);
+  return rc;
 }

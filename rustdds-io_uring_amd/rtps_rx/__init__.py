@@ -61,7 +61,6 @@ class _IngestOut(ctypes.Structure):
 INGEST_BEST_EFFORT = 0x1
 INGEST_TOPIC_CACHE = 0x2  # also run the topic caches' add_change (DELIVERY_CACHED on the deliveries)
 INGEST_WINDOW = 1 << 17
-INGEST_FAR_CAP = 1024  # RTPS_INGEST_FAR_CAP: far SNs per proxy beyond the window
 
 
 class _Out(ctypes.Structure):

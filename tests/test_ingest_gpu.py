@@ -209,18 +209,89 @@ def test_far_reader_sets(rx):
         _batch(rx, ing, rd, dgrams[a:b], f"far a15 {a}:{b}")
 
 
-def test_far_set_capacity_counted(rx):
-    """Past FCAP (1024) far SNs of one proxy the set is full: the rest are accepted unchecked
-    and counted in n_window_overflow (the decisions still equal the reference's here)."""
+def _far_datagrams(subs, per=8):
+    """the (prefix 0) submessages in datagrams of `per`, in the given order"""
+    return [R.datagram(R.PREFIXES[0], subs[i:i + per]) for i in range(0, len(subs), per)]
+
+
+def test_far_sets_past_former_caps(rx):
+    """more than 1024 far SNs for one proxy and more than 8192 far events
+    in one batch (round 4's per-proxy FCAP and per-batch FL_CAP), and far GAP ranges of
+    thousands of SNs, batch after batch: bit-exact with the oracle's unbounded change sets
+    (rtps_writer_proxy.rs:62 BTreeMap), n_window_overflow == 0 (_batch); then a GAP fills
+    writer 0's window and all_ackable_before runs through its 6000 far SNs (far_extend), the
+    re-anchored window takes them (far_pull) and re-sent ones are duplicates."""
     import rtps_rx
-    tbl = pack_match_table([(R.PREFIXES[0] + R.writer_key(0), 0)])
+    W = rtps_rx.INGEST_WINDOW
+    w0, w1 = R.writer_key(0), R.writer_key(1)
+    tbl = pack_match_table([(R.PREFIXES[0] + w0, 0), (R.PREFIXES[0] + w1, 1)])
     rx.set_match_table(tbl)
-    w = R.writer_key(0)
-    far = 2 * rtps_rx.INGEST_WINDOW
-    d = [R.datagram(R.PREFIXES[0], [R.data_sub(w, far + 3 * k + j) for j in range(3)]) for k in range(500)]
-    arena, off, ln = oracle.pack(d)
-    _, acc, accepted, ack, ovf, _ = rx.ingest_batch(arena, off, ln, 1)
-    assert len(accepted) == 1500 and ovf == 1500 - 1024 and ack.tolist() == [1]
+    ing = oracle.HistoryIngest(tbl)
+    g = np.random.default_rng(3)
+    # batch 1: writer 0 sends W+1 .. W+3000 four times over in random order (12000 far events,
+    # 3000 far SNs); writer 1 a GAP [2W, 2W + 5000) with a listed bitmap, and samples around it
+    sns = np.repeat(np.arange(W + 1, W + 3001), 4)
+    g.shuffle(sns)
+    subs = [R.data_sub(w0, int(v)) for v in sns]
+    s1 = [R.data_sub(w1, int(v)) for v in g.integers(2 * W - 10, 2 * W + 5100, 3000)]
+    s1.insert(1500, R.gap_sub(w1, 2 * W, 2 * W + 5000, [bool(b) for b in g.random(64) < 0.5]))
+    for k, sub in enumerate(s1):
+        subs.insert(int(g.integers(0, len(subs) + 1)), sub)
+    acc, dels, ack = _batch(rx, ing, tbl, _far_datagrams(subs), "far batch 1")
+    assert len(dels) > 3000 and ack.tolist() == [1, 1]
+    # batch 2: re-sent SNs of batch 1 (duplicates across batches) and W+3001 .. W+6000 twice
+    sns = np.concatenate([g.integers(W + 1, W + 3001, 2000), np.repeat(np.arange(W + 3001, W + 6001), 2)])
+    g.shuffle(sns)
+    subs = [R.data_sub(w0, int(v)) for v in sns] + [R.data_sub(w1, int(v)) for v in range(2 * W - 5, 2 * W + 5)]
+    acc, dels, ack = _batch(rx, ing, tbl, _far_datagrams(subs), "far batch 2")
+    assert len(dels) >= 3000
+    # batch 3: a GAP covering [1, W + 1) for writer 0: ack_base runs through the far set
+    _, _, ack = _batch(rx, ing, tbl, [R.datagram(R.PREFIXES[0], [R.gap_sub(w0, 1, W + 1, [])])], "far gap fills")
+    assert ack.tolist() == [W + 6001, 1]
+    # batch 4: around the new ack_base, and writer 1 past its GAP again
+    subs = [R.data_sub(w0, v) for v in range(W + 5990, W + 6010)] + \
+           [R.data_sub(w1, int(v)) for v in g.integers(2 * W, 2 * W + 5200, 500)]
+    _batch(rx, ing, tbl, _far_datagrams(subs), "far batch 4")
+
+
+def test_far_sets_many_proxies(rx):
+    """Far items spread over 48 proxies (several tables grown in one batch, one workgroup
+    each on the per-proxy path, one k_far pass over all of them on the global one), over
+    three batches; bit-exact, nothing counted."""
+    import rtps_rx
+    W = rtps_rx.INGEST_WINDOW
+    keys = [R.writer_key(k) for k in range(48)]
+    tbl = pack_match_table([(R.PREFIXES[0] + k, i) for i, k in enumerate(keys)])
+    rx.set_match_table(tbl)
+    ing = oracle.HistoryIngest(tbl)
+    g = np.random.default_rng(8)
+    for b in range(3):
+        subs = []
+        for k, w in enumerate(keys):
+            base = (1 + k % 3) * W + 1000 * b
+            subs += [R.data_sub(w, int(v)) for v in g.integers(base, base + 400 + 40 * k, 300)]
+            if k % 5 == 0:
+                subs.append(R.gap_sub(w, base + 100, base + 900, [bool(x) for x in g.random(40) < 0.5]))
+        g.shuffle(subs)
+        _batch(rx, ing, tbl, _far_datagrams(subs, per=5), f"far proxies batch {b}")
+
+
+def test_far_pool_out_counted(rx):
+    """The one capacity left: a GAP covering more SNs past the window than the far-set pool
+    keeps free (here 2^34) cannot be recorded SN by SN; that proxy's far samples of the batch
+    are then accepted without the duplicate check and counted in n_window_overflow, the
+    other proxy's stay exact, and nothing walks the range."""
+    import rtps_rx
+    W = rtps_rx.INGEST_WINDOW
+    w0, w1 = R.writer_key(0), R.writer_key(1)
+    tbl = pack_match_table([(R.PREFIXES[0] + w0, 0), (R.PREFIXES[0] + w1, 1)])
+    rx.set_match_table(tbl)
+    subs = [R.gap_sub(w0, 2 * W, 2 * W + (1 << 34), [])] + [R.data_sub(w0, 3 * W + k % 5) for k in range(10)] + \
+           [R.data_sub(w1, 3 * W + k % 5) for k in range(10)]
+    arena, off, ln = oracle.pack([R.datagram(R.PREFIXES[0], subs)])
+    _, acc, accepted, ack, ovf, _ = rx.ingest_batch(arena, off, ln, 2)
+    w1_dels = int((accepted["rec_idx"] >= 11).sum())
+    assert ovf == 10 and w1_dels == 5 and len(accepted) == 15
 
 
 def test_empty_and_eventless_batches(rx):
