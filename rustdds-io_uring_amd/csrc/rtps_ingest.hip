@@ -80,8 +80,9 @@ enum : uint8_t { EV_NONE = 0, EV_SAMPLE = 1, EV_HB = 2, EV_GAP = 3 };
 enum { C_OVF = 0, C_NSEL, C_NDEL, C_NREC, C_FARC, C_NFAR, C_MODE, C_SPREAD, C_COUNT = C_SPREAD + 4 * 64 };
 // the batch's counts as k_signal writes them to pinned host memory:
 // [0] = the batch's tag (written last), HEARTBEAT / GAP / event / proxy-less sample counts,
-// records, far-item candidates
-enum { SIG_TAG = 0, SIG_HB, SIG_GAP, SIG_EV, SIG_FREE, SIG_NREC, SIG_FARC, SIG_MODE, SIG_WORDS = 8 };
+// records, far-item candidates, the verdict, the far-set pool's slots in use (as the earlier
+// batches left it)
+enum { SIG_TAG = 0, SIG_HB, SIG_GAP, SIG_EV, SIG_FREE, SIG_NREC, SIG_FARC, SIG_MODE, SIG_FUSED, SIG_WORDS = 9 };
 // event metadata: reader slot | flags << 16 (EVF_*)
 constexpr uint32_t EVF_DUP_OK = 1u << 16;  // RTPS_TARGET_DUPLICATES_OK reader
 constexpr uint32_t EVF_FREE = 1u << 17;    // sample without a proxy (writer kind not user-defined)
@@ -165,7 +166,8 @@ struct State {
   uint32_t* far_cap;
   uint32_t* far_n;    // occupied slots
   int64_t* far_min;   // least SN of the set at or above the window's end (INT64_MAX: none)
-  uint64_t* fneed;    // k_far: SNs the batch's items of proxy e cover (then cleared); FNEED_OUT: the pool was out
+  uint64_t* fneed;    // k_far_need: SNs the batch's items of proxy e cover (cleared by k_far_grow)
+  uint32_t* fstat;    // k_far_grow: 1 = the pool could not grow proxy e's table this batch
   int64_t* fsn;       // pool: SN per slot (FEMPTY: free)
   uint64_t* fkey;     // pool: the first event that covered the slot's SN, epoch << 32 | event
   uint64_t* fused;    // pool slots handed out (device counter; may pass fpcap when the pool is out)
@@ -275,7 +277,6 @@ static_assert(sizeof(PEv) == 32, "PEv layout");
 // inserts such ranges one SN at a time too, rtps_writer_proxy.rs:284-291).
 constexpr int64_t FEMPTY = INT64_MIN;   // a free slot (far SNs are >= W > 0)
 constexpr uint32_t FT_MIN = 64;         // smallest table
-constexpr uint64_t FNEED_OUT = ~0ull;   // fneed: the pool could not grow this proxy's table
 enum : uint32_t { FI_SAMPLE = 1, FI_DUP = 2, FI_GAP = 3 };
 struct FarItem {
   PEv p;        // the event as the per-proxy pass packs it (p.k: its accept slot)
@@ -283,9 +284,18 @@ struct FarItem {
   uint32_t e, kind;
 };
 static_assert(sizeof(FarItem) == 48, "FarItem layout");
-// its list position, or NONE: the list is full (sized by the host to the batch's events: not reached)
+// its list position, or NONE: the list is full (sized by the host to the batch's events: not
+// reached).  The lanes of the wave that push at the same call reserve their places with one
+// atomic (the active mask; one counter for the whole batch, so no hot-address queue).
 __device__ __forceinline__ uint32_t far_push(const State& s, const FarItem& it) {
-  const unsigned long long pos = atomicAdd(reinterpret_cast<unsigned long long*>(s.ctr + C_NFAR), 1ull);
+  const uint64_t act = __ballot(1);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t rank = (uint32_t)__popcll(act & ((1ull << lane) - 1ull));
+  unsigned long long b = 0;
+  if (rank == 0) b = atomicAdd(reinterpret_cast<unsigned long long*>(s.ctr + C_NFAR), (unsigned long long)__popcll(act));
+  const uint32_t lo32 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b);
+  const uint32_t hi32 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(b >> 32));
+  const uint64_t pos = (((uint64_t)hi32 << 32) | lo32) + rank;
   if (pos >= s.fl_cap) return NONE;
   s.fl[pos] = it;
   return (uint32_t)pos;
@@ -693,6 +703,7 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
 // behind this kernel then run it without waiting for the host (the host's rule, on the device).
 struct SigCfg {
   uint32_t ident, n_proxies, path, reliable;
+  const uint64_t* fused;  // the far-set pool's counter
 };
 // the verdict from the batch's counts (the host's path rule, on the device)
 __device__ __forceinline__ uint64_t plain_mode(uint64_t n_hb, uint64_t n_gap, uint64_t n_ev, uint64_t nev,
@@ -724,10 +735,10 @@ __device__ __forceinline__ Counts wave_counts(const uint64_t* ctr, uint32_t lane
 // the counts (and the verdict) to pinned host memory, the tag last, written through after the
 // rest completed (one wave: lane k writes word k)
 __device__ __forceinline__ void signal_host(const Counts& c, uint64_t mode, uint64_t* hsig, uint64_t tag,
-                                            uint32_t lane) {
+                                            uint32_t lane, const SigCfg& cf) {
   const uint64_t v = lane == 0 ? c.n_hb : lane == 1 ? c.n_gap : lane == 2 ? c.n_ev : lane == 3 ? c.n_free
-                   : lane == 4 ? c.nrec : lane == 5 ? c.farc : mode;
-  if (lane < 7) __hip_atomic_store(hsig + SIG_HB + lane, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                   : lane == 4 ? c.nrec : lane == 5 ? c.farc : lane == 6 ? mode : cf.fused ? *cf.fused : 0;
+  if (lane < 8) __hip_atomic_store(hsig + SIG_HB + lane, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (lane == 0) __hip_atomic_store(hsig + SIG_TAG, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -739,7 +750,7 @@ __global__ void k_signal(uint64_t* ctr, uint64_t* hsig, uint64_t tag, SigCfg cf)
   const Counts c = wave_counts(ctr, lane);
   const uint64_t mode = plain_mode(c.n_hb, c.n_gap, c.n_ev, c.nrec, c.farc, cf);
   if (lane == 0) ctr[C_MODE] = mode;
-  signal_host(c, mode, hsig, tag, lane);
+  signal_host(c, mode, hsig, tag, lane, cf);
 }
 
 // 1b: lane per record writes its events at roff[i] (set order = EntityId order of the readers)
@@ -1045,7 +1056,7 @@ __global__ __launch_bounds__(IT) void k_decide_t(uint64_t n, uint64_t cap, Scrat
       if (threadIdx.x == 0) s_mode = (uint32_t)mode;
       if (blockIdx.x == 0) {
         if (threadIdx.x == 0) s.ctr[C_MODE] = mode;
-        signal_host(c, mode, so.hsig, so.tag, threadIdx.x);
+        signal_host(c, mode, so.hsig, so.tag, threadIdx.x, so.cf);
       }
     }
     __syncthreads();
@@ -1207,7 +1218,7 @@ __global__ __launch_bounds__(IT) void k_dcount(const uint8_t* flag, uint64_t n, 
 __device__ __forceinline__ void dwrite_tile(uint32_t blk, const uint8_t* flag, uint64_t n, const uint32_t* tcnt,
                                             uint32_t ntiles, const Scratch& x, bool ident, uint64_t max_out,
                                             rtps_delivery* out, uint64_t* n_out, const uint64_t* ctr, uint64_t* ovf_out,
-                                            uint64_t* hev, uint64_t* s_w, uint32_t* s_c) {
+                                            uint64_t* hev, const uint64_t* fused, uint64_t* s_w, uint32_t* s_c) {
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   uint64_t pre = 0;
   for (uint32_t t = tid; t < blk; t += IT) pre += tcnt[t];
@@ -1259,17 +1270,18 @@ __device__ __forceinline__ void dwrite_tile(uint32_t blk, const uint8_t* flag, u
       uint64_t ne = 0;
       for (uint32_t k = 0; k < 64; ++k) ne += ctr[C_SPREAD + 4 * k + 2];
       hev[0] = ne;
-      hev[1] = ctr[C_NFAR];  // (per-proxy path: its far items, sizing the far-set pool's room)
+      hev[1] = ctr[C_NFAR];  // (per-proxy path: its far items and the pool's use, for the far-set room)
+      hev[2] = fused ? *fused : 0;
     }
   }
 }
 __global__ __launch_bounds__(IT) void k_dwrite(const uint8_t* flag, uint64_t n, const uint32_t* tcnt, uint32_t ntiles,
                                                Scratch x, bool ident, uint64_t max_out, rtps_delivery* out,
                                                uint64_t* n_out, const uint64_t* ctr, uint64_t* ovf_out,
-                                               uint64_t* hev) {
+                                               uint64_t* hev, const uint64_t* fused) {
   __shared__ uint64_t s_w[IT / 64];
   __shared__ uint32_t s_c[IT / 64];
-  dwrite_tile(blockIdx.x, flag, n, tcnt, ntiles, x, ident, max_out, out, n_out, ctr, ovf_out, hev, s_w, s_c);
+  dwrite_tile(blockIdx.x, flag, n, tcnt, ntiles, x, ident, max_out, out, n_out, ctr, ovf_out, hev, fused, s_w, s_c);
 }
 __global__ __launch_bounds__(IT) void k_accept_counts(uint64_t n, uint64_t cap, Scratch x, uint8_t* accept) {
   for (uint64_t i = (uint64_t)blockIdx.x * IT + threadIdx.x; i < cap; i += (uint64_t)gridDim.x * IT) {
@@ -1470,99 +1482,129 @@ __device__ __forceinline__ uint64_t fkey_of(uint32_t epoch, uint32_t event) {
   return ((uint64_t)epoch << 32) | event;
 }
 
-// The global paths' far items (after decide, before the deliveries): each proxy's table
-// grown for the SNs its items cover, every SN inserted with its item's key, the samples
-// decided (rejected: acc 0; tcnt: its delivery tile's count).  One workgroup; launched when
-// classify counted candidates (identity batches) or always (expanded batches).
-constexpr uint32_t KF = 1024;
-__global__ __launch_bounds__(KF) void k_far(State s, const uint8_t* arena, uint8_t* acc, uint32_t* tcnt,
-                                            uint32_t n_proxies) {
+// op(base[key], v) for the active lanes of the wave, the lanes sharing a key combined first
+// (red): up to 4 rounds of "the first pending lane's key: every lane on it reduced, one
+// atomic", then one atomic per lane still pending.  Every lane of the wave calls it.
+template <typename T, typename RED, typename OP>
+__device__ __forceinline__ void wave_atomic(uint32_t key, T v, bool active, T ident, RED&& red, OP&& op) {
+  const uint32_t lane = threadIdx.x & 63u;
+  bool todo = active;
+#pragma unroll
+  for (uint32_t r = 0; r < 4u; ++r) {
+    const uint64_t t = __ballot(todo);
+    if (t == 0) return;
+    const uint32_t leader = (uint32_t)__builtin_ctzll(t);
+    const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)key, (int)leader);
+    const bool mine = todo && key == k;
+    T a = mine ? v : ident;  // (the other lanes add the identity: every lane ends with the group's total)
+    for (uint32_t d = 1; d < 64; d <<= 1) a = red(a, (T)__shfl_xor(a, d, 64));
+    if (lane == leader) op(k, a);
+    todo = todo && !mine;
+  }
+  if (todo) op(key, v);
+}
+
+// The global paths' far items (after decide, before the deliveries), in four launches over
+// the batch list (its length on the device, the grid from classify's candidate count):
+//   k_far_need  each item's far SNs summed per proxy (fneed);
+//   k_far_grow  one workgroup per proxy: its table grown for them (fstat: 1 = the pool was out);
+//   k_far_ins   every SN of every item inserted with its key;
+//   k_far_dec   the samples decided (rejected: acc 0; tcnt: its delivery tile's count).
+constexpr uint32_t KF = 256;
+__global__ __launch_bounds__(KF) void k_far_need(State s, const uint8_t* arena) {
+  const uint64_t nf0 = s.ctr[C_NFAR], nf = nf0 < s.fl_cap ? nf0 : s.fl_cap;
+  const uint64_t span = (uint64_t)gridDim.x * KF;
+  for (uint64_t b = (uint64_t)blockIdx.x * KF; b < nf; b += span) {  // (whole waves: wave_atomic)
+    const uint64_t k = b + threadIdx.x;
+    FarItem it{};
+    if (k < nf) it = s.fl[k];
+    const uint64_t c = k < nf ? far_count(it.p, it.kind, it.lim, arena) : 0;
+    wave_atomic<uint64_t>(it.e, c, k < nf, 0ull, [](uint64_t a, uint64_t o) { return a + o; },
+                          [&](uint32_t e, uint64_t a) {
+                            atomicAdd(reinterpret_cast<unsigned long long*>(s.fneed + e), (unsigned long long)a);
+                          });
+  }
+}
+__global__ __launch_bounds__(KF) void k_far_grow(State s, uint32_t n_proxies) {
   __shared__ FarSh f;
-  __shared__ uint32_t s_list[KF], s_nl;
-  const uint32_t tid = threadIdx.x;
-  const uint64_t nf0 = s.ctr[C_NFAR];
-  const uint64_t nf = nf0 < s.fl_cap ? nf0 : s.fl_cap;
-  if (nf == 0) return;
-  uint64_t miss = tid == 0 ? nf0 - nf : 0;  // (past the list: not reached, the host sizes it)
-  for (uint64_t k = tid; k < nf; k += KF) {
-    const FarItem it = s.fl[k];
-    atomicAdd(reinterpret_cast<unsigned long long*>(s.fneed + it.e),
-              (unsigned long long)far_count(it.p, it.kind, it.lim, arena));
+  const uint32_t e = blockIdx.x;
+  if (e >= n_proxies) return;
+  const uint64_t need = s.fneed[e];
+  if (need == 0) {
+    if (threadIdx.x == 0) s.fstat[e] = 0u;
+    return;
   }
-  __threadfence();
+  if (threadIdx.x == 0) ftab_load(s, e, f.t);
   __syncthreads();
-  // the tables that must grow, KF proxies at a time, each by the whole workgroup
-  for (uint32_t e0 = 0; e0 < n_proxies; e0 += KF) {
-    if (tid == 0) s_nl = 0;
-    __syncthreads();
-    const uint32_t e = e0 + tid;
-    if (e < n_proxies) {
-      const uint64_t need = fldk(s.fneed + e);
-      if (need && 2ull * ((uint64_t)fld32(s.far_n + e) + need) > fld32(s.far_cap + e)) s_list[atomicAdd(&s_nl, 1u)] = e;
-    }
-    __syncthreads();
-    const uint32_t nl = s_nl;
-    for (uint32_t l = 0; l < nl; ++l) {
-      const uint32_t g = s_list[l];
-      if (tid == 0) ftab_load(s, g, f.t);
-      __syncthreads();
-      const bool ok = ftab_reserve(s, f, fldk(s.fneed + g), KF);
-      if (tid == 0) {
-        if (ok) ftab_store(s, g, f.t);
-        else s.fneed[g] = FNEED_OUT;
-      }
-      __threadfence();
-      __syncthreads();
-    }
+  const bool ok = ftab_reserve(s, f, need, KF);
+  if (threadIdx.x == 0) {
+    if (ok) ftab_store(s, e, f.t);
+    s.fstat[e] = ok ? 0u : 1u;
+    s.fneed[e] = 0;
   }
-  // every SN of every item, then the samples
-  for (uint64_t k = tid; k < nf; k += KF) {
-    const FarItem it = s.fl[k];
-    if (fldk(s.fneed + it.e) == FNEED_OUT) continue;
-    const uint64_t toff = fldk(s.far_off + it.e);
-    const uint32_t mask = fld32(s.far_cap + it.e) - 1u;
-    const uint64_t key = fkey_of(s.epoch, it.p.k);
+}
+__global__ __launch_bounds__(KF) void k_far_ins(State s, const uint8_t* arena) {
+  const uint64_t nf0 = s.ctr[C_NFAR], nf = nf0 < s.fl_cap ? nf0 : s.fl_cap;
+  const uint64_t span = (uint64_t)gridDim.x * KF;
+  for (uint64_t b = (uint64_t)blockIdx.x * KF; b < nf; b += span) {
+    const uint64_t k = b + threadIdx.x;
+    FarItem it{};
+    bool act = k < nf;
+    if (act) {
+      it = s.fl[k];
+      act = s.fstat[it.e] == 0u;
+    }
     uint32_t claimed = 0;
     int64_t mn = INT64_MAX;
-    far_sns(it.p, it.kind, it.lim, arena, [&](int64_t v) {
-      claimed += fset_add(s.fsn + toff, s.fkey + toff, mask, v, key);
-      if (v < mn) mn = v;
-    });
-    if (claimed) atomicAdd(s.far_n + it.e, claimed);
-    if (mn != INT64_MAX) atomicMin(reinterpret_cast<unsigned long long*>(s.far_min + it.e), (unsigned long long)mn);
+    if (act) {
+      const uint64_t toff = s.far_off[it.e];
+      const uint32_t mask = s.far_cap[it.e] - 1u;
+      const uint64_t key = fkey_of(s.epoch, it.p.k);
+      far_sns(it.p, it.kind, it.lim, arena, [&](int64_t v) {
+        claimed += fset_add(s.fsn + toff, s.fkey + toff, mask, v, key);
+        if (v < mn) mn = v;
+      });
+    }
+    wave_atomic<uint32_t>(it.e, claimed, act && claimed, 0u, [](uint32_t a, uint32_t o) { return a + o; },
+                          [&](uint32_t e, uint32_t a) { atomicAdd(s.far_n + e, a); });
+    wave_atomic<uint64_t>(it.e, (uint64_t)mn, act && mn != INT64_MAX, ~0ull,
+                          [](uint64_t a, uint64_t o) { return a < o ? a : o; },
+                          [&](uint32_t e, uint64_t a) {
+                            atomicMin(reinterpret_cast<unsigned long long*>(s.far_min + e), (unsigned long long)a);
+                          });
   }
-  __threadfence();
-  __syncthreads();
-  for (uint64_t k = tid; k < nf; k += KF) {
+}
+__global__ __launch_bounds__(KF) void k_far_dec(State s, uint8_t* acc, uint32_t* tcnt) {
+  const uint64_t nf0 = s.ctr[C_NFAR], nf = nf0 < s.fl_cap ? nf0 : s.fl_cap;
+  uint64_t miss = (blockIdx.x == 0 && threadIdx.x == 0) ? nf0 - nf : 0;  // (past the list: not reached)
+  for (uint64_t k = (uint64_t)blockIdx.x * KF + threadIdx.x; k < nf; k += (uint64_t)gridDim.x * KF) {
     const FarItem it = s.fl[k];
     if (it.kind != FI_SAMPLE) continue;
-    if (fldk(s.fneed + it.e) == FNEED_OUT) {
+    if (s.fstat[it.e] != 0u) {
       ++miss;  // the pool was out: accepted unchecked
       continue;
     }
-    const FTab t{fldk(s.far_off + it.e), fld32(s.far_cap + it.e), 0u, 0};
+    const FTab t{s.far_off[it.e], s.far_cap[it.e], 0u, 0};
     if (!ftab_first(s, t, it.p.sn, fkey_of(s.epoch, it.p.k))) {
       acc[it.p.k] = 0;
       if (tcnt) atomicSub(&tcnt[it.p.k / DT], 1u);
     }
   }
-  __syncthreads();
-  for (uint64_t k = tid; k < nf; k += KF) s.fneed[s.fl[k].e] = 0;
   if (miss) atomicAdd(reinterpret_cast<unsigned long long*>(s.ctr + C_OVF), (unsigned long long)miss);
 }
 
 // State, after the window pass found nb (the first uncovered SN >= the threshold inside the
 // window, or >= lo + W: every position covered, or the threshold past the window): nb
-// continues through the far set t, nt SNs looked up at a time.  Every thread; returns to all.
+// continues through the far set t, 8 nt SNs looked up at a time.  Every thread; returns to all.
 __device__ int64_t far_extend(const State& s, FarSh& f, int64_t lo, int64_t nb, uint32_t nt) {
   if (f.t.cap == 0 || nb < lo + (int64_t)W || nb < f.t.min) return nb;
   const int64_t* sn = s.fsn + f.t.off;
   const uint32_t mask = f.t.cap - 1u;
-  for (int64_t b = nb;; b += 4 * (int64_t)nt) {  // ends: the set holds at most n SNs
+  for (int64_t b = nb;; b += 8 * (int64_t)nt) {  // ends: the set holds at most n SNs
     __syncthreads();
     if (threadIdx.x == 0) f.x = ~0ull;
     __syncthreads();
-    for (uint32_t r = 0; r < 4u; ++r) {
+    for (uint32_t r = 0; r < 8u; ++r) {
       const int64_t v = b + (int64_t)(r * nt + threadIdx.x);
       if (fset_find(sn, mask, v) == NONE) {
         atomicMin(&f.x, (unsigned long long)v);
@@ -1755,7 +1797,8 @@ __global__ __launch_bounds__(IT) void k_dstate(const uint8_t* flag, uint64_t n, 
     fcm = mode == 2;
   }
   if (blockIdx.x < ntiles) {
-    dwrite_tile(blockIdx.x, flag, n, tcnt, ntiles, x, true, max_out, out, n_out, ctr, ovf_out, nullptr, s_w, s_c);
+    dwrite_tile(blockIdx.x, flag, n, tcnt, ntiles, x, true, max_out, out, n_out, ctr, ovf_out, nullptr, nullptr, s_w,
+                s_c);
   } else if (blockIdx.x - ntiles < n_entries) {
     state_proxy(blockIdx.x - ntiles, x, s, reliable, ack_out, sh, s_first, f, fcm);
   }
@@ -1943,12 +1986,14 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
   __shared__ uint32_t s_ngap;
   __shared__ FarSh fsh;                // the proxy's far set
   __shared__ unsigned long long s_fp;  // SNs the chunk's far items cover
+  __shared__ uint32_t s_anyfar;        // some thread holds a far item of the chunk
   const uint32_t e = blockIdx.x, tid = threadIdx.x;
   if (e >= n_proxies) return;
   PST_DECL;  // (setup: the window, the hash and the piece tables)
   if (tid == 0) {
     s_ngap = 0u;
     s_fp = 0ull;
+    s_anyfar = 0u;
     ftab_load(s, e, fsh.t);
   }
   const int64_t lo = s.lo[e], base = s.base[e];
@@ -2160,7 +2205,9 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
       }
       acc_out[kk[j]] = acc;
     }
-    if (__syncthreads_or(fkind != 0u)) {
+    if (__ballot(fkind != 0u) && (tid & 63u) == 0u) s_anyfar = 1u;  // (rare: one LDS store per wave)
+    __syncthreads();
+    if (s_anyfar) {
       // the chunk's far items: every SN they cover into the far set (the table grown first for
       // all of them), then their samples decided by first cover (see "far sequence numbers")
       uint64_t pc = 0;
@@ -2196,7 +2243,10 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
         for (uint32_t j = 0; j < PPT; ++j) n_ovf += ((fkind >> (2u * j)) & 3u) == FI_SAMPLE;  // the pool was out: unchecked
       }
       __syncthreads();
-      if (tid == 0) s_fp = 0ull;
+      if (tid == 0) {
+        s_fp = 0ull;
+        s_anyfar = 0u;
+      }
     }
     PST(5);
     // merge the chunk's coverage into the window, clear the hash and the presence bits
@@ -2270,6 +2320,7 @@ __global__ void k_init_state(uint32_t n, State s) {
     s.far_n[e] = 0;
     s.far_min[e] = INT64_MAX;
     s.fneed[e] = 0;
+    s.fstat[e] = 0;
   }
 }
 // the far-set pool compacted: proxy e's table [far_off[e], + far_cap[e]) to noff[e] of the new pool
@@ -2290,30 +2341,42 @@ __global__ void k_far_rekey(uint64_t n, int64_t* sn, uint64_t* key) {
     key[j] = sn[j] == FEMPTY ? ~0ull : 0ull;
 }
 __global__ void k_finish(const uint64_t* ctr, uint64_t* ovf) { if (ovf) *ovf = ctr[C_OVF]; }
-__global__ void k_hev(const uint64_t* ctr, uint64_t* hev) {
+__global__ void k_hev(const uint64_t* ctr, uint64_t* hev, const uint64_t* fused) {
   uint64_t ne = 0;
   for (uint32_t k = 0; k < 64; ++k) ne += ctr[C_SPREAD + 4 * k + 2];
   hev[0] = ne;
   hev[1] = ctr[C_NFAR];
+  hev[2] = *fused;
 }
 
 static inline uint64_t hmin(uint64_t a, uint64_t b) { return a < b ? a : b; }
+
+// the global paths' far items (at most farc of them, see k_far_need)
+static void far_launch(const State& S, const uint8_t* arena, uint8_t* acc, uint32_t* tcnt, uint32_t n_proxies,
+                       uint64_t farc, hipStream_t st) {
+  const uint32_t g = (uint32_t)hmin((farc + KF - 1) / KF, 2048);
+  hipLaunchKernelGGL(k_far_need, dim3(g), dim3(KF), 0, st, S, arena);
+  hipLaunchKernelGGL(k_far_grow, dim3(n_proxies), dim3(KF), 0, st, S, n_proxies);
+  hipLaunchKernelGGL(k_far_ins, dim3(g), dim3(KF), 0, st, S, arena);
+  hipLaunchKernelGGL(k_far_dec, dim3(g), dim3(KF), 0, st, S, acc, tcnt);
+}
 
 // accepted flags[0, n) -> deliveries (k_dcount + k_dwrite; x.sel holds the tile counts)
 // ovf: also copy the batch's window-overflow count out (the paths whose last kernel this is)
 // hev: also write the batch's event count there (pinned host memory)
 static void deliver(const uint8_t* flag, uint64_t n, const Scratch& x, bool ident, const rtps_ingest_out* out,
-                    hipStream_t st, const uint64_t* ctr = nullptr, bool ovf = false, uint64_t* hev = nullptr) {
+                    hipStream_t st, const uint64_t* ctr = nullptr, bool ovf = false, uint64_t* hev = nullptr,
+                    const uint64_t* fused = nullptr) {
   const uint32_t ntiles = (uint32_t)((n + DT - 1) / DT);
   if (ntiles == 0) {
     (void)hipMemsetAsync(out->n_accepted, 0, sizeof(uint64_t), st);
     if (ovf && out->n_window_overflow) hipLaunchKernelGGL(k_finish, dim3(1), dim3(1), 0, st, ctr, out->n_window_overflow);
-    if (hev) hipLaunchKernelGGL(k_hev, dim3(1), dim3(1), 0, st, ctr, hev);
+    if (hev) hipLaunchKernelGGL(k_hev, dim3(1), dim3(1), 0, st, ctr, hev, fused);
     return;
   }
   hipLaunchKernelGGL(k_dcount, dim3(ntiles), dim3(IT), 0, st, flag, n, x.sel);
   hipLaunchKernelGGL(k_dwrite, dim3(ntiles), dim3(IT), 0, st, flag, n, x.sel, ntiles, x, ident, out->max_accepted,
-                     out->accepted, out->n_accepted, ctr, ovf ? out->n_window_overflow : nullptr, hev);
+                     out->accepted, out->n_accepted, ctr, ovf ? out->n_window_overflow : nullptr, hev, fused);
 }
 
 }  // namespace
@@ -2345,12 +2408,9 @@ struct IngestState {
   uint32_t* bk_cl = nullptr;  // proxy bucketing: per (classify workgroup, proxy) events | first position << 16
   uint64_t bkcap = 0;
   // far-set pool (st.fsn / fkey / fused / fpcap; see "far sequence numbers"): the device counter
-  // as last seen -- exact after a sync, else the side stream's copy taken after an earlier batch
+  // as last seen -- exact after a sync or from the count signal (every earlier batch done), else
+  // from the last per-proxy batch's pinned words (hctr2[2])
   uint64_t fp_used = 0;
-  uint64_t* hfused = nullptr;  // pinned: that copy
-  hipStream_t fside = nullptr;
-  hipEvent_t fev = nullptr, fcp = nullptr;
-  bool fcp_pending = false;
 };
 
 static void free_bk(IngestState* s) {
@@ -2412,7 +2472,7 @@ static void keep_shared(State& m, const State& o) {
 }
 static void free_state(IngestState* s) {
   void* p[] = {s->st.base, s->st.lo, s->st.hbc, s->st.bits, s->st.fc, s->st.dbits, s->st.seg_b, s->st.seg_e,
-               s->st.far_off, s->st.far_cap, s->st.far_n, s->st.far_min, s->st.fneed};
+               s->st.far_off, s->st.far_cap, s->st.far_n, s->st.far_min, s->st.fneed, s->st.fstat};
   for (void* q : p) if (q) (void)hipFree(q);
   State k{};
   keep_shared(k, s->st);
@@ -2451,14 +2511,9 @@ static bool grow_fl(IngestState* s, uint64_t n, hipStream_t st) {
 // not, the stream is synchronised and the count read; still short: the live tables are
 // packed at the front of a larger pool (k_far_move) and the abandoned ones dropped.
 static bool far_pool_ensure(IngestState* s, uint64_t F, hipStream_t st) {
-  if (s->fcp_pending && hipEventQuery(s->fcp) == hipSuccess) {
-    s->fp_used = *s->hfused;
-    s->fcp_pending = false;
-  }
   auto room = [&](uint64_t used) { return 8 * (F + 65536) + 2 * used; };
   if (s->st.fpcap && s->fp_used + room(s->fp_used) <= s->st.fpcap) return true;
-  if (hipStreamSynchronize(st) != hipSuccess || hipStreamSynchronize(s->fside) != hipSuccess) return false;
-  s->fcp_pending = false;
+  if (hipStreamSynchronize(st) != hipSuccess) return false;
   uint64_t used = 0;
   if (hipMemcpy(&used, s->st.fused, 8, hipMemcpyDeviceToHost) != hipSuccess) return false;
   s->fp_used = used;
@@ -2499,16 +2554,6 @@ static bool far_pool_ensure(IngestState* s, uint64_t F, hipStream_t st) {
   s->fp_used = live;
   return true;
 }
-// after the batch: the pool's counter copied to pinned memory on the side stream (no wait on
-// the batch's stream), for the next batch's far_pool_ensure
-static void far_pool_note(IngestState* s, hipStream_t st) {
-  if (s->fcp_pending) return;  // the previous copy is still in flight
-  if (hipEventRecord(s->fev, st) != hipSuccess || hipStreamWaitEvent(s->fside, s->fev, 0) != hipSuccess ||
-      hipMemcpyAsync(s->hfused, s->st.fused, 8, hipMemcpyDeviceToHost, s->fside) != hipSuccess ||
-      hipEventRecord(s->fcp, s->fside) != hipSuccess)
-    return;
-  s->fcp_pending = true;
-}
 static void free_rscratch(IngestState* s) {
   void* p[] = {s->x.fidx, s->x.fmask, s->x.fall, s->x.rcnt, s->x.roff, s->x.rset, s->x.rkind, s->x.rsn};
   for (void* q : p) if (q) (void)hipFree(q);
@@ -2547,7 +2592,8 @@ static bool grow_state(IngestState* s, uint32_t n, hipStream_t st) {
             hipMalloc(&m.dbits, (uint64_t)ncap * WW * 4) == hipSuccess &&
             hipMalloc(&m.seg_e, ncap * 4ull) == hipSuccess && hipMalloc(&m.far_off, ncap * 8ull) == hipSuccess &&
             hipMalloc(&m.far_cap, ncap * 4ull) == hipSuccess && hipMalloc(&m.far_n, ncap * 4ull) == hipSuccess &&
-            hipMalloc(&m.far_min, ncap * 8ull) == hipSuccess && hipMalloc(&m.fneed, ncap * 8ull) == hipSuccess;
+            hipMalloc(&m.far_min, ncap * 8ull) == hipSuccess && hipMalloc(&m.fneed, ncap * 8ull) == hipSuccess &&
+            hipMalloc(&m.fstat, ncap * 4ull) == hipSuccess;
   ok = ok && hipMemsetAsync(m.bits, 0, (uint64_t)ncap * WW * 4, st) == hipSuccess &&
        hipMemsetAsync(m.dbits, 0, (uint64_t)ncap * WW * 4, st) == hipSuccess &&
        hipMemsetAsync(m.fc, 0xff, (uint64_t)ncap * W * 8, st) == hipSuccess;
@@ -2568,7 +2614,7 @@ static bool grow_state(IngestState* s, uint32_t n, hipStream_t st) {
   s->ecap = ncap;
   State dead = o;
   void* p[] = {dead.base, dead.lo, dead.hbc, dead.bits, dead.fc, dead.dbits, dead.seg_b, dead.seg_e,
-               dead.far_off, dead.far_cap, dead.far_n, dead.far_min, dead.fneed};
+               dead.far_off, dead.far_cap, dead.far_n, dead.far_min, dead.fneed, dead.fstat};
   for (void* q : p) if (q) (void)hipFree(q);
   if (!ok) { free_state(s); return false; }
   return true;
@@ -2630,15 +2676,10 @@ IngestState* rtps_ingest_state_new(int device) {
   if (!s) return nullptr;
   s->device = device;
   if (hipMalloc(&s->ctr_base, 2 * C_COUNT * 8) != hipSuccess) { delete s; return nullptr; }
-  if (hipMalloc(&s->st.fused, 8) != hipSuccess || hipMemset(s->st.fused, 0, 8) != hipSuccess ||
-      hipHostMalloc(&s->hfused, 8, hipHostMallocDefault) != hipSuccess ||
-      hipStreamCreateWithFlags(&s->fside, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&s->fev, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&s->fcp, hipEventDisableTiming) != hipSuccess) {
+  if (hipMalloc(&s->st.fused, 8) != hipSuccess || hipMemset(s->st.fused, 0, 8) != hipSuccess) {
     rtps_ingest_state_free(s);
     return nullptr;
   }
-  *s->hfused = 0;
   if (hipMemset(s->ctr_base, 0, 2 * C_COUNT * 8) != hipSuccess) {
     (void)hipFree(s->ctr_base);
     delete s;
@@ -2664,10 +2705,6 @@ void rtps_ingest_state_free(IngestState* s) {
   free_state(s);
   free_far(s);
   if (s->st.fused) (void)hipFree(s->st.fused);
-  if (s->hfused) (void)hipHostFree(s->hfused);
-  if (s->fside) (void)hipStreamDestroy(s->fside);
-  if (s->fev) (void)hipEventDestroy(s->fev);
-  if (s->fcp) (void)hipEventDestroy(s->fcp);
   if (s->ctr_base) (void)hipFree(s->ctr_base);
   if (s->hctr) (void)hipHostFree(s->hctr);
   if (s->hctr2) (void)hipHostFree(s->hctr2);
@@ -2682,8 +2719,7 @@ int rtps_ingest_state_reset(IngestState* s, hipStream_t st) {
             hipMemsetAsync(s->st.dbits, 0, (uint64_t)s->ecap * WW * 4, st) == hipSuccess;
   if (ok) hipLaunchKernelGGL(k_init_state, dim3((s->ecap + IT - 1) / IT), dim3(IT), 0, st, s->ecap, s->st);
   // every far set emptied: the pool's tables are all free again
-  ok = ok && hipStreamSynchronize(s->fside) == hipSuccess && hipMemsetAsync(s->st.fused, 0, 8, st) == hipSuccess;
-  s->fcp_pending = false;
+  ok = ok && hipMemsetAsync(s->st.fused, 0, 8, st) == hipSuccess;
   s->fp_used = 0;
   return ok && hipGetLastError() == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP;
 }
@@ -2703,7 +2739,7 @@ static int ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, cons
   if (!ident && s->vcap == 0 && !grow_vscratch(s, 1, st)) return RTPS_RX_ENOMEM;
   const bool reliable = !(flags & RTPS_INGEST_BEST_EFFORT);
   const FarSrc fs{records, dgram_off};
-  const SigCfg cfg{ident ? 1u : 0u, t.n_proxies, s->path, reliable ? 1u : 0u};
+  const SigCfg cfg{ident ? 1u : 0u, t.n_proxies, s->path, reliable ? 1u : 0u, s->st.fused};
   if (++s->epoch == 0xffffffffu) {  // keys would wrap: clear the first-cover table, age the far sets' keys
     if (hipMemsetAsync(s->st.fc, 0xff, (uint64_t)s->ecap * W * 8, st) != hipSuccess) return RTPS_RX_EHIP;
     uint64_t used = 0;
@@ -2746,6 +2782,7 @@ static int ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, cons
   if (s->hnev_ready && hipEventQuery(s->hnev_ev) == hipSuccess) {
     s->last_nev = s->hctr2[0];
     s->last_far = s->hctr2[1];
+    s->fp_used = s->fp_used > s->hctr2[2] ? s->fp_used : s->hctr2[2];  // (a compaction since lowered it: exact then)
     s->hnev_ready = false;
   }
   // (after a batch with far items the next takes the signalled path, which sizes the far-set
@@ -2796,7 +2833,7 @@ static int ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, cons
   if (fast) {
     // the select also writes this batch's event count for the next batch's choice (pinned, read
     // without a sync once the event has passed)
-    deliver(out->accept, max, x, true, out, st, S.ctr, true, s->hctr2);
+    deliver(out->accept, max, x, true, out, st, S.ctr, true, s->hctr2, S.fused);
     if (hipEventRecord(s->hnev_ev, st) != hipSuccess) return RTPS_RX_EHIP;
     s->hnev_ready = true;
     return hipGetLastError() == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP;
@@ -2834,6 +2871,7 @@ static int ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, cons
   }
   const uint64_t n_hb = s->hsig[SIG_HB], n_gap = s->hsig[SIG_GAP], n_ev = s->hsig[SIG_EV], n_free = s->hsig[SIG_FREE];
   const uint64_t n_rec = s->hsig[SIG_NREC], farc = s->hsig[SIG_FARC];
+  s->fp_used = s->hsig[SIG_FUSED];  // (exact: every earlier batch has finished)
   if (ident && s->hsig[SIG_MODE] != 0) return RTPS_RX_OK;  // the queued plain path runs it
   // events live at [0, nev): record slots in identity batches, the expanded list otherwise
   uint64_t nev = ident ? n_rec : n_ev;
@@ -2932,8 +2970,8 @@ static int ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, cons
     else
       hipLaunchKernelGGL(k_decide_t<0>, dim3(ntiles), dim3(IT), 0, st, nev, acc_cap, x, S, acc, have_hb, s->epoch,
                          x.sel, fs, ntiles, SigOut{});
-    if (farc)  // samples / GAPs past some window: their replay (fixes accept[] and the tile counts)
-      hipLaunchKernelGGL(k_far, dim3(1), dim3(KF), 0, st, S, arena, acc, x.sel, t.n_proxies);
+    if (farc)  // samples / GAPs past some window: their first covers (fixes accept[] and the tile counts)
+      far_launch(S, arena, acc, x.sel, t.n_proxies, farc, st);
     if (n_gap)
       hipLaunchKernelGGL(k_merge, dim3(gv), dim3(IT), 0, st, records, arena, dgram_off, nev, x, S, true);
     hipLaunchKernelGGL(k_dstate, dim3(ntiles + t.n_proxies), dim3(IT), 0, st, acc, acc_cap, x.sel, ntiles, x,
@@ -2951,7 +2989,7 @@ static int ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, cons
     hipLaunchKernelGGL(k_decide, dim3((uint32_t)hmin((acc_cap + IT - 1) / IT, 8192)), dim3(IT), 0, st, nev, acc_cap,
                        x, S, acc, have_hb, s->epoch, fs);
     if (farc)  // the far items' first covers (fixes accept[])
-      hipLaunchKernelGGL(k_far, dim3(1), dim3(KF), 0, st, S, arena, acc, (uint32_t*)nullptr, t.n_proxies);
+      far_launch(S, arena, acc, nullptr, t.n_proxies, farc, st);
   }
   const bool state_pass = t.n_proxies && !per_proxy;  // k_state copies the overflow count out, else the select does
   deliver(acc, acc_cap, x, ident, out, st, S.ctr, !state_pass);
@@ -2972,8 +3010,6 @@ int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const 
                       const uint64_t* dgram_off, const rtps_record* records, const uint64_t* n_records,
                       uint64_t max_records, const rtps_frag_sample* frag, const uint64_t* n_frag, uint64_t max_frag,
                       uint32_t flags, const rtps_ingest_out* out) {
-  const int rc = ingest_batch(s, st, t, arena, arena_len, dgram_off, records, n_records, max_records, frag, n_frag,
-                              max_frag, flags, out);
-  if (rc == RTPS_RX_OK) far_pool_note(s, st);
-  return rc;
+  return ingest_batch(s, st, t, arena, arena_len, dgram_off, records, n_records, max_records, frag, n_frag, max_frag,
+                      flags, out);
 }
