@@ -275,7 +275,9 @@ static_assert(sizeof(PEv) == 32, "PEv layout");
 // can need.  Only GAPs covering more SNs past the window than that can find the pool out:
 // those samples are accepted unchecked and counted in *n_window_overflow (the reference
 // inserts such ranges one SN at a time too, rtps_writer_proxy.rs:284-291).
-constexpr int64_t FEMPTY = INT64_MIN;   // a free slot (far SNs are >= W > 0)
+// a free slot: all ones (far SNs are >= W > 0), like its key ~0, so that a byte fill clears the
+// pool; the slots at and above the pool's counter are always free (fresh tables need no clearing)
+constexpr int64_t FEMPTY = -1;
 constexpr uint32_t FT_MIN = 64;         // smallest table
 enum : uint32_t { FI_SAMPLE = 1, FI_DUP = 2, FI_GAP = 3 };
 struct FarItem {
@@ -1422,14 +1424,8 @@ __device__ bool ftab_rehash(const State& s, FarSh& f, uint64_t nc, int64_t keep_
   __syncthreads();
   const uint32_t c = f.nc;
   if (c == 0) return false;
-  int64_t* nsn = s.fsn + f.off;
+  int64_t* nsn = s.fsn + f.off;  // (free: taken from above the counter)
   uint64_t* nkey = s.fkey + f.off;
-  for (uint32_t j = tid; j < c; j += nt) {
-    nsn[j] = FEMPTY;
-    nkey[j] = ~0ull;
-  }
-  __threadfence();
-  __syncthreads();
   uint32_t moved = 0;
   const int64_t* osn = s.fsn + f.t.off;
   const uint64_t* okey = s.fkey + f.t.off;
@@ -1455,7 +1451,7 @@ __device__ bool ftab_reserve(const State& s, FarSh& f, uint64_t need, uint32_t n
   if (want <= f.t.cap) return true;
   uint64_t nc = FT_MIN;
   while (nc < 2ull * want) nc <<= 1;
-  return ftab_rehash(s, f, nc, INT64_MIN + 1, nt);
+  return ftab_rehash(s, f, nc, 0, nt);
 }
 // the SNs each thread holds (f_of(j) for j < cnt) into t with key k_of(j); returns this thread's
 // least inserted SN (INT64_MAX: none).  Every thread calls it after ftab_reserve succeeded.
@@ -1525,7 +1521,8 @@ __global__ __launch_bounds__(KF) void k_far_need(State s, const uint8_t* arena) 
                           });
   }
 }
-__global__ __launch_bounds__(KF) void k_far_grow(State s, uint32_t n_proxies) {
+constexpr uint32_t KG = 1024;  // k_far_grow: a new table's slots initialised and the old one rehashed by 16 waves
+__global__ __launch_bounds__(KG) void k_far_grow(State s, uint32_t n_proxies) {
   __shared__ FarSh f;
   const uint32_t e = blockIdx.x;
   if (e >= n_proxies) return;
@@ -1536,7 +1533,7 @@ __global__ __launch_bounds__(KF) void k_far_grow(State s, uint32_t n_proxies) {
   }
   if (threadIdx.x == 0) ftab_load(s, e, f.t);
   __syncthreads();
-  const bool ok = ftab_reserve(s, f, need, KF);
+  const bool ok = ftab_reserve(s, f, need, KG);
   if (threadIdx.x == 0) {
     if (ok) ftab_store(s, e, f.t);
     s.fstat[e] = ok ? 0u : 1u;
@@ -1604,9 +1601,15 @@ __device__ int64_t far_extend(const State& s, FarSh& f, int64_t lo, int64_t nb, 
     __syncthreads();
     if (threadIdx.x == 0) f.x = ~0ull;
     __syncthreads();
+    // the 8 SNs' first probes issued together (independent loads), then each resolved
+    int64_t cur[8];
+#pragma unroll
+    for (uint32_t r = 0; r < 8u; ++r) cur[r] = fld(sn + fslot(b + (int64_t)(r * nt + threadIdx.x), mask));
+#pragma unroll
     for (uint32_t r = 0; r < 8u; ++r) {
       const int64_t v = b + (int64_t)(r * nt + threadIdx.x);
-      if (fset_find(sn, mask, v) == NONE) {
+      const bool miss = cur[r] == FEMPTY || (cur[r] != v && fset_find(sn, mask, v) == NONE);
+      if (miss) {
         atomicMin(&f.x, (unsigned long long)v);
         break;
       }
@@ -1629,18 +1632,24 @@ __device__ void far_pull(const State& s, FarSh& f, uint32_t* bits, int64_t nlo, 
     f.k = 0;
   }
   __syncthreads();
+  __threadfence();  // (the table's inserts of this kernel, by other waves, are seen by the plain loads below)
   const int64_t* sn = s.fsn + f.t.off;
   uint32_t keep = 0;
   int64_t mn = INT64_MAX;
-  for (uint32_t j = tid; j < f.t.cap; j += nt) {
-    const int64_t v = fld(sn + j);
-    if (v == FEMPTY || v < nlo) continue;
+  auto one = [&](int64_t v) {
+    if (v == FEMPTY || v < nlo) return;
     if (v >= hi) {
       ++keep;
       if (v < mn) mn = v;
     } else {
       atomicOr(bits + ((uint64_t)(v - nlo) >> 5), 1u << ((uint64_t)(v - nlo) & 31u));
     }
+  };
+  const longlong2* sn2 = reinterpret_cast<const longlong2*>(sn);  // (tables: >= 64 slots, 16-B aligned)
+  for (uint32_t j = tid; j < f.t.cap / 2u; j += nt) {
+    const longlong2 p = sn2[j];
+    one(p.x);
+    one(p.y);
   }
   if (keep) atomicAdd(&f.k, keep);
   if (mn != INT64_MAX) atomicMin(&f.x, (unsigned long long)mn);
@@ -2356,7 +2365,7 @@ static void far_launch(const State& S, const uint8_t* arena, uint8_t* acc, uint3
                        uint64_t farc, hipStream_t st) {
   const uint32_t g = (uint32_t)hmin((farc + KF - 1) / KF, 2048);
   hipLaunchKernelGGL(k_far_need, dim3(g), dim3(KF), 0, st, S, arena);
-  hipLaunchKernelGGL(k_far_grow, dim3(n_proxies), dim3(KF), 0, st, S, n_proxies);
+  hipLaunchKernelGGL(k_far_grow, dim3(n_proxies), dim3(KG), 0, st, S, n_proxies);
   hipLaunchKernelGGL(k_far_ins, dim3(g), dim3(KF), 0, st, S, arena);
   hipLaunchKernelGGL(k_far_dec, dim3(g), dim3(KF), 0, st, S, acc, tcnt);
 }
@@ -2532,7 +2541,8 @@ static bool far_pool_ensure(IngestState* s, uint64_t F, hipStream_t st) {
   int64_t* nsn = nullptr;
   uint64_t* nkey = nullptr;
   uint64_t* dnoff = nullptr;
-  bool ok = hipMalloc(&nsn, nc * 8) == hipSuccess && hipMalloc(&nkey, nc * 8) == hipSuccess;
+  bool ok = hipMalloc(&nsn, nc * 8) == hipSuccess && hipMalloc(&nkey, nc * 8) == hipSuccess &&
+            hipMemsetAsync(nsn, 0xff, nc * 8, st) == hipSuccess && hipMemsetAsync(nkey, 0xff, nc * 8, st) == hipSuccess;
   if (ok && live) {
     ok = hipMalloc(&dnoff, ne * 8ull) == hipSuccess &&
          hipMemcpy(dnoff, noff.data(), ne * 8ull, hipMemcpyHostToDevice) == hipSuccess;
@@ -2720,6 +2730,9 @@ int rtps_ingest_state_reset(IngestState* s, hipStream_t st) {
   if (ok) hipLaunchKernelGGL(k_init_state, dim3((s->ecap + IT - 1) / IT), dim3(IT), 0, st, s->ecap, s->st);
   // every far set emptied: the pool's tables are all free again
   ok = ok && hipMemsetAsync(s->st.fused, 0, 8, st) == hipSuccess;
+  if (s->st.fpcap)  // the whole pool free again (all ones)
+    ok = ok && hipMemsetAsync(s->st.fsn, 0xff, s->st.fpcap * 8, st) == hipSuccess &&
+         hipMemsetAsync(s->st.fkey, 0xff, s->st.fpcap * 8, st) == hipSuccess;
   s->fp_used = 0;
   return ok && hipGetLastError() == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP;
 }
