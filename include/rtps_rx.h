@@ -690,11 +690,13 @@ int rtps_rx_frag_set_receive_time(rtps_rx_ctx* ctx, uint64_t unix_ns);
  * all_ackable_before plus, per proxy, a FAR SET: every covered SN beyond that window
  * (samples and GAPs further ahead), a hash set in device memory that grows with it
  * (no fixed bound; a batch may add any number of far SNs to any proxy), decided
- * exactly by first cover (all_ackable_before continues through the set).  The
- * context keeps room for 4 x (max_records + 1024) + twice the far sets' slots in
- * use before each batch, growing its pool between batches; only a batch whose GAPs
- * cover more SNs beyond the window than that finds it full, and then those
- * proxies' far samples are accepted without the duplicate check and counted in
+ * exactly by first cover (all_ackable_before continues through the set).  Before
+ * a batch's far samples are decided the context makes room in its pool for
+ * 8 x (the batch's far candidates + 256 per GAP + 2^16) + twice the far-set slots
+ * in use, growing the pool between batches (on the per-proxy path without a count
+ * read-back: from the previous batch's far items); only a batch whose GAPs cover
+ * more SNs beyond the window than that finds it full, and then those proxies' far
+ * samples are accepted without the duplicate check and counted in
  * *n_window_overflow (the reference's BTreeMap inserts such a range SN by SN). */
 #define RTPS_INGEST_WINDOW (1u << 17)
 #define RTPS_INGEST_BEST_EFFORT 0x1u /* flags: treat every reader as BestEffort (HEARTBEATs ignored) */
