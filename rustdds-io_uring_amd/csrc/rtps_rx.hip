@@ -320,21 +320,26 @@ struct SubOut {
 // reference reader rejects; WRITE additionally fills the kind-specific record
 // words R.d[8..13] (and R.d[2..4] / R.d[10..11] for INFO_DST / INFO_SRC /
 // INFO_REPLY).  Returns false on a read error (the datagram is dropped).
-template <bool WRITE, class S>
+// TRUSTED: the submessage is known valid (its datagram's count walk passed): the checks are skipped.
+#ifndef RTPS_TRUSTED_WRITE
+#define RTPS_TRUSTED_WRITE 1
+#endif
+#define SB_CHECK(c) do { if (!TRUSTED && (c)) return false; } while (0)
+template <bool WRITE, bool TRUSTED = false, class S>
 __device__ __forceinline__ bool sub_body(const S& s, const Win& W, uint32_t kind, uint32_t flags, bool le,
                                          uint32_t body, uint32_t blen, Rec& R, SubOut& so) {
   so.cls = 0; so.route = 0; so.pk = 0; so.aux16 = blen; so.rid = 0; so.wid = 0;
   switch (kind) {
     case RTPS_DATA: {  // Data::deserialize_data (data.rs:57-144)
-      if (blen < 20u) return false;
+      SB_CHECK(blen < 20u);
       uint32_t otq = e16(W.w[1], 1, le);
-      if (otq < 16u) return false;
+      SB_CHECK(otq < 16u);
       uint32_t pos = 20u;
-      if (otq > 16u) { pos = 4u + otq; if (pos > blen) return false; }
+      if (otq > 16u) { pos = 4u + otq; SB_CHECK(pos > blen); }
       uint32_t fl = flags & 0x1fu;
       bool q = (fl & 0x02u) != 0u, dk = (fl & 0x0cu) != 0u;
       uint32_t qstart = pos, kh = 0, si = 0, rsi = 0, si_flags = SI_ABSENT;
-      if (q && !param_list(s, body, blen, le, pos, kh, si, rsi, si_flags)) return false;
+      { const bool plok = !q || param_list(s, body, blen, le, pos, kh, si, rsi, si_flags); SB_CHECK(!plok); }
       so.cls = 1;
       if (WRITE) {
         so.rid = W.w[2]; so.wid = W.w[3];
@@ -365,22 +370,22 @@ __device__ __forceinline__ bool sub_body(const S& s, const Win& W, uint32_t kind
       return true;
     }
     case RTPS_DATA_FRAG: {  // DataFrag::deserialize (data_frag.rs:121-257)
-      if (blen < 32u) return false;
+      SB_CHECK(blen < 32u);
       uint32_t otq = e16(W.w[1], 1, le);
-      if (otq < 28u) return false;
+      SB_CHECK(otq < 28u);
       uint32_t pos = 32u;
-      if (otq > 28u) { pos = 4u + otq; if (pos > blen) return false; }
+      if (otq > 28u) { pos = 4u + otq; SB_CHECK(pos > blen); }
       bool q = (flags & 0x02u) != 0u;
       uint32_t qstart = pos, kh = 0, si = 0, rsi = 0, si_flags = SI_ABSENT;
-      if (q && !param_list(s, body, blen, le, pos, kh, si, rsi, si_flags)) return false;
+      { const bool plok = !q || param_list(s, body, blen, le, pos, kh, si, rsi, si_flags); SB_CHECK(!plok); }
       int64_t sn = sn_of(W.w[4], W.w[5], le);
-      if (sn < 1) return false;
+      SB_CHECK(sn < 1);
       uint32_t frag_start = e32(W.w[6], le);
       uint32_t frags_in_sub = e16(W.w[7], 0, le), frag_size = e16(W.w[7], 1, le);
       uint32_t data_size = e32(W.w[8], le);
-      if (frag_size < 1u || frag_size > data_size) return false;
+      SB_CHECK(frag_size < 1u || frag_size > data_size);
       uint32_t total = data_size / frag_size + ((data_size % frag_size) ? 1u : 0u);
-      if (frag_start < 1u || frag_start > total) return false;
+      SB_CHECK(frag_start < 1u || frag_start > total);
       so.cls = 1;
       if (WRITE) {
         so.rid = W.w[2]; so.wid = W.w[3];
@@ -397,7 +402,7 @@ __device__ __forceinline__ bool sub_body(const S& s, const Win& W, uint32_t kind
       return true;
     }
     case RTPS_HEARTBEAT: {  // Heartbeat (heartbeat.rs:21-49): 28 bytes
-      if (blen < 28u) return false;
+      SB_CHECK(blen < 28u);
       so.cls = 1;
       if (WRITE) {
         so.rid = W.w[1]; so.wid = W.w[2];
@@ -409,7 +414,7 @@ __device__ __forceinline__ bool sub_body(const S& s, const Win& W, uint32_t kind
       return true;
     }
     case RTPS_HEARTBEAT_FRAG: {  // HeartbeatFrag (heartbeat_frag.rs:16-37): 24 bytes
-      if (blen < 24u) return false;
+      SB_CHECK(blen < 24u);
       so.cls = 1;
       if (WRITE) {
         so.rid = W.w[1]; so.wid = W.w[2];
@@ -421,11 +426,11 @@ __device__ __forceinline__ bool sub_body(const S& s, const Win& W, uint32_t kind
       return true;
     }
     case RTPS_GAP: {  // Gap (gap.rs:23-46): rid wid gapStart SNSet
-      if (blen < 28u) return false;
+      SB_CHECK(blen < 28u);
       uint32_t nb = e32(W.w[7], le);
-      if (nb > 256u) return false;
+      SB_CHECK(nb > 256u);
       uint32_t words = (nb + 31u) >> 5;
-      if (28u + 4u * words > blen) return false;
+      SB_CHECK(28u + 4u * words > blen);
       so.cls = 1;
       if (WRITE) {
         so.rid = W.w[1]; so.wid = W.w[2];
@@ -438,11 +443,11 @@ __device__ __forceinline__ bool sub_body(const S& s, const Win& W, uint32_t kind
       return true;
     }
     case RTPS_ACKNACK: {  // AckNack (ack_nack.rs:27-50): rid wid SNSet count
-      if (blen < 20u) return false;
+      SB_CHECK(blen < 20u);
       uint32_t nb = e32(W.w[5], le);
-      if (nb > 256u) return false;
+      SB_CHECK(nb > 256u);
       uint32_t words = (nb + 31u) >> 5;
-      if (24u + 4u * words > blen) return false;
+      SB_CHECK(24u + 4u * words > blen);
       so.cls = 2;
       if (WRITE) {
         so.rid = W.w[1]; so.wid = W.w[2];
@@ -455,11 +460,11 @@ __device__ __forceinline__ bool sub_body(const S& s, const Win& W, uint32_t kind
       return true;
     }
     case RTPS_NACK_FRAG: {  // NackFrag (nack_frag.rs:31-53): rid wid sn FNSet count
-      if (blen < 24u) return false;
+      SB_CHECK(blen < 24u);
       uint32_t nb = e32(W.w[6], le);
-      if (nb > 256u) return false;
+      SB_CHECK(nb > 256u);
       uint32_t words = (nb + 31u) >> 5;
-      if (28u + 4u * words > blen) return false;
+      SB_CHECK(28u + 4u * words > blen);
       so.cls = 2;
       if (WRITE) {
         so.rid = W.w[1]; so.wid = W.w[2];
@@ -473,32 +478,32 @@ __device__ __forceinline__ bool sub_body(const S& s, const Win& W, uint32_t kind
       return true;
     }
     case RTPS_INFO_TS:  // rtps/submessage.rs:211-225 (Invalidate flag: no body read)
-      if (!(flags & 0x02u) && blen < 8u) return false;
+      SB_CHECK(!(flags & 0x02u) && blen < 8u);
       so.cls = 3;
       return true;
     case RTPS_INFO_SRC:  // InfoSource (info_source.rs:22-36)
-      if (blen < 20u) return false;
+      SB_CHECK(blen < 20u);
       so.cls = 3;
       if (WRITE) R.d[10] = W.w[2];
       return true;
     case RTPS_INFO_DST:  // InfoDestination (info_destination.rs:20-25)
-      if (blen < 12u) return false;
+      SB_CHECK(blen < 12u);
       so.cls = 3;
       if (WRITE) { R.d[2] = W.w[1]; R.d[3] = W.w[2]; R.d[4] = W.w[3]; }
       return true;
     case RTPS_INFO_REPLY: {  // InfoReply (info_reply.rs:9-21): Vec<Locator> + Option<Vec<Locator>>
-      if (blen < 4u) return false;
+      SB_CHECK(blen < 4u);
       uint32_t n1 = e32(W.w[1], le), n2 = 0xffffffffu;
       uint64_t pos = 4u + 24ull * n1;
-      if (pos > blen) return false;
-      if (pos + 1u > blen) return false;
+      SB_CHECK(pos > blen);
+      SB_CHECK(pos + 1u > blen);
       uint32_t tag = ld4(s, body + (uint32_t)pos) & 0xffu;
       pos += 1u;
       if (tag != 0u) {
-        if (pos + 4u > blen) return false;
+        SB_CHECK(pos + 4u > blen);
         n2 = e32(ld4(s, body + (uint32_t)pos), le);
         pos += 4u;
-        if (pos + 24ull * n2 > blen) return false;
+        SB_CHECK(pos + 24ull * n2 > blen);
       }
       so.cls = 3;
       if (WRITE) { R.d[10] = n1; R.d[11] = n2; }
@@ -605,7 +610,8 @@ __device__ uint32_t walk(const KParams& p, const Src& s, const uint32_t* H, uint
     Rec R;
     if (WRITE) rec_clear(R);
     SubOut so;
-    if (!sub_body<WRITE>(s, W, kind, flags, le, o + 4u, eff, R, so)) return RTPS_DGRAM_SUBMSG_ERR;
+    if (!sub_body<WRITE, WRITE && RTPS_TRUSTED_WRITE != 0>(s, W, kind, flags, le, o + 4u, eff, R, so))
+      return RTPS_DGRAM_SUBMSG_ERR;  // (WRITE: the datagram passed its count walk)
     interp_update(p, st, W, kind, flags, le);
     if (so.cls != 0u) {
       if (WRITE) {
@@ -1183,7 +1189,7 @@ __device__ __forceinline__ void em2_item(const KParams& p, const Src& s0, const 
   const uint32_t eff = eff_len(kind, e16(W.w[0], 1, le), len - o);
   rec_clear(R);
   SubOut so;
-  sub_body<true>(s, W, kind, flags, le, o + 4u, eff, R, so);  // validated by E's walk
+  sub_body<true, RTPS_TRUSTED_WRITE != 0>(s, W, kind, flags, le, o + 4u, eff, R, so);  // validated by E's walk
   R.d[0] = dg0 + d;
   R.d[1] = o | (kind << 16) | (flags << 24);
   tgt = rec_finish(p, R, so, kind, st);
