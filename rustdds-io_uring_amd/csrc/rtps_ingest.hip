@@ -1370,18 +1370,23 @@ __device__ void far_sns(const PEv& P, uint32_t kind, int64_t lim, const uint8_t*
     gap_far(P.sn, P.a, P.m >> 8, [&](uint32_t w) { return rd32(arena + P.bw + 4u * w, (P.m & PM_LE) != 0u); }, lim,
             range, f);
 }
-// how many (an upper bound: a GAP's listed SNs inside its own range count twice)
+// how many (an upper bound: a GAP's listed SNs inside its own range count twice), at most
+// FAR_COUNT_MAX: no table can hold more (ftab_reserve), and sums of counts cannot wrap
+constexpr uint64_t FAR_COUNT_MAX = 1ull << 32;  // (x 2^31 items per batch: no u64 sum wraps)
 __device__ uint64_t far_count(const PEv& P, uint32_t kind, int64_t lim, const uint8_t* arena) {
   if (kind != FI_GAP) return 1;
   uint64_t c = 0;
-  auto range = [&](int64_t a, int64_t b) { c += (uint64_t)(b - a); };
+  auto range = [&](int64_t a, int64_t b) {
+    const uint64_t r = (uint64_t)b - (uint64_t)a;
+    c += r < FAR_COUNT_MAX ? r : FAR_COUNT_MAX;
+  };
   auto point = [&](int64_t) { ++c; };
   if (P.m & PM_INL)
     gap_far(P.sn, P.a, P.m >> 8, [&](uint32_t w) { return (uint32_t)(P.bw >> (32u * w)); }, lim, range, point);
   else
     gap_far(P.sn, P.a, P.m >> 8, [&](uint32_t w) { return rd32(arena + P.bw + 4u * w, (P.m & PM_LE) != 0u); }, lim,
             range, point);
-  return c;
+  return c < FAR_COUNT_MAX ? c : FAR_COUNT_MAX;
 }
 // One proxy's far set as a workgroup works on it (LDS; loaded / stored by thread 0) and the
 // workgroup's scratch for the block-wide operations below.
@@ -1447,6 +1452,7 @@ __device__ bool ftab_rehash(const State& s, FarSh& f, uint64_t nc, int64_t keep_
 // t made to take `need` more SNs at load <= 1/2 (a table of >= 4 x (n + need) slots when it
 // must grow).  Every thread calls it with the same need; false: the pool is out.
 __device__ bool ftab_reserve(const State& s, FarSh& f, uint64_t need, uint32_t nt) {
+  if (need > (1ull << 31)) return false;  // (no table that large: the pool is out for it)
   const uint64_t want = 2ull * ((uint64_t)f.t.n + need);
   if (want <= f.t.cap) return true;
   uint64_t nc = FT_MIN;
