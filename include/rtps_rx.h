@@ -694,8 +694,10 @@ int rtps_rx_frag_set_receive_time(rtps_rx_ctx* ctx, uint64_t unix_ns);
  * a batch's far samples are decided the context makes room in its pool for
  * 8 x (the batch's far candidates + 256 per GAP + 2^16) + twice the far-set slots
  * in use, growing the pool between batches (on the per-proxy path without a count
- * read-back: from the previous batch's far items); only a batch whose GAPs cover
- * more SNs beyond the window than that finds it full, and then those proxies' far
+ * read-back: from the previous batch's far items).  A GAP whose range starts at or
+ * below all_ackable_before only moves it (a threshold, as the reference's
+ * irrelevant_changes_range does), whatever its length.  Only a batch whose other
+ * GAPs cover more SNs beyond the window than that room finds it full, and then those proxies' far
  * samples are accepted without the duplicate check and counted in
  * *n_window_overflow (the reference's BTreeMap inserts such a range SN by SN). */
 #define RTPS_INGEST_WINDOW (1u << 17)

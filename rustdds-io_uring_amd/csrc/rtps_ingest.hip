@@ -77,12 +77,15 @@ enum : uint8_t { EV_NONE = 0, EV_SAMPLE = 1, EV_HB = 2, EV_GAP = 3 };
 // the HEARTBEAT / GAP / event / proxy-less sample counts in 64 slot quads (one atomic per block, spread: no hot address)
 // (C_FARC: classify's far-SN candidates, the host's cue for k_far; C_NFAR: far items appended)
 // (C_MODE: k_signal's verdict on an identity batch, read by the kernels queued before the host saw it)
-enum { C_OVF = 0, C_NSEL, C_NDEL, C_NREC, C_FARC, C_NFAR, C_MODE, C_SPREAD, C_COUNT = C_SPREAD + 4 * 64 };
+// (C_TGAP: GAPs whose range starts at or below their proxy's all_ackable_before and reaches past its
+//  window: irrelevant_changes_range then only moves all_ackable_before, a threshold the per-proxy
+//  path applies as such; the host sends such batches there)
+enum { C_OVF = 0, C_NSEL, C_NDEL, C_NREC, C_FARC, C_NFAR, C_MODE, C_TGAP, C_SPREAD, C_COUNT = C_SPREAD + 4 * 64 };
 // the batch's counts as k_signal writes them to pinned host memory:
 // [0] = the batch's tag (written last), HEARTBEAT / GAP / event / proxy-less sample counts,
 // records, far-item candidates, the verdict, the far-set pool's slots in use (as the earlier
-// batches left it)
-enum { SIG_TAG = 0, SIG_HB, SIG_GAP, SIG_EV, SIG_FREE, SIG_NREC, SIG_FARC, SIG_MODE, SIG_FUSED, SIG_WORDS = 9 };
+// batches left it), threshold GAPs (C_TGAP)
+enum { SIG_TAG = 0, SIG_HB, SIG_GAP, SIG_EV, SIG_FREE, SIG_NREC, SIG_FARC, SIG_MODE, SIG_FUSED, SIG_TGAP, SIG_WORDS = 10 };
 // event metadata: reader slot | flags << 16 (EVF_*)
 constexpr uint32_t EVF_DUP_OK = 1u << 16;  // RTPS_TARGET_DUPLICATES_OK reader
 constexpr uint32_t EVF_FREE = 1u << 17;    // sample without a proxy (writer kind not user-defined)
@@ -418,7 +421,7 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
   if (lds || BUCKET) __syncthreads();
   CST(1);
   const bool reliable = !(flags & RTPS_INGEST_BEST_EFFORT);
-  uint32_t nh = 0, ng = 0, ne = 0, nf = 0, nfar = 0;
+  uint32_t nh = 0, ng = 0, ne = 0, nf = 0, nfar = 0, ntg = 0;
   CSS_DECL;
   // record slot i: its events; FAST: *key = the proxy of its proxied event (NONE: none)
   // and *P its packed form, stored at pev[i] unless BUCKET (which places it itself)
@@ -500,7 +503,10 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
           nf += en == NONE;
           if (!IDENT && en != NONE && ev != EV_HB) {  // far-item candidates of expanded batches (see below)
             const int64_t lim = st.lo[en] + (int64_t)W;
-            if (ev == EV_SAMPLE ? sn >= lim : (int64_t)(((uint64_t)q2[3] << 32) | q2[2]) + (int64_t)q3[0] > lim) ++nfar;
+            if (ev == EV_SAMPLE ? sn >= lim : (int64_t)(((uint64_t)q2[3] << 32) | q2[2]) + (int64_t)q3[0] > lim) {
+              ++nfar;
+              if (ev == EV_GAP && sn <= st.base[en]) ++ntg;
+            }
           }
         }
       }
@@ -524,7 +530,10 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
             ++nfar;  // a far-item candidate: the host launches k_far
         } else if (MARK && evi == EV_GAP) {
           const int64_t list_base = (int64_t)(((uint64_t)q2[3] << 32) | q2[2]);
-          if (list_base + (int64_t)q3[0] > st.lo[ent] + (int64_t)W) ++nfar;  // coverage past the window
+          if (list_base + (int64_t)q3[0] > st.lo[ent] + (int64_t)W) {  // coverage past the window
+            ++nfar;
+            if (sn <= st.base[ent]) ++ntg;
+          }
         }
       }
       if (!FAST) {
@@ -693,6 +702,7 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
     atomicAdd(reinterpret_cast<unsigned long long*>(ctr + C_SPREAD + 4u * (blockIdx.x & 63u) + tid),
               (unsigned long long)s_n[tid]);
   if ((MARK || !IDENT) && nfar) atomicAdd(reinterpret_cast<unsigned long long*>(ctr + C_FARC), (unsigned long long)nfar);
+  if ((MARK || !IDENT) && ntg) atomicAdd(reinterpret_cast<unsigned long long*>(ctr + C_TGAP), (unsigned long long)ntg);
   CST(6);
 }
 
@@ -721,12 +731,12 @@ __device__ __forceinline__ uint64_t plain_mode(uint64_t n_hb, uint64_t n_gap, ui
 // The batch's counts by one wave: lane k loads spread slot k's four counters, a wave reduction
 // sums them (every lane gets the sums)
 struct Counts {
-  uint64_t n_hb, n_gap, n_ev, n_free, nrec, farc;
+  uint64_t n_hb, n_gap, n_ev, n_free, nrec, farc, tgap;
 };
 __device__ __forceinline__ Counts wave_counts(const uint64_t* ctr, uint32_t lane) {
   const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(ctr + C_SPREAD + 4u * lane);
   const ulonglong2 b = *reinterpret_cast<const ulonglong2*>(ctr + C_SPREAD + 4u * lane + 2u);
-  Counts c{a.x, a.y, b.x, b.y, ctr[C_NREC], ctr[C_FARC]};
+  Counts c{a.x, a.y, b.x, b.y, ctr[C_NREC], ctr[C_FARC], ctr[C_TGAP]};
 #pragma unroll
   for (uint32_t d = 32; d >= 1; d >>= 1) {
     c.n_hb += __shfl_xor(c.n_hb, d, 64); c.n_gap += __shfl_xor(c.n_gap, d, 64);
@@ -739,8 +749,9 @@ __device__ __forceinline__ Counts wave_counts(const uint64_t* ctr, uint32_t lane
 __device__ __forceinline__ void signal_host(const Counts& c, uint64_t mode, uint64_t* hsig, uint64_t tag,
                                             uint32_t lane, const SigCfg& cf) {
   const uint64_t v = lane == 0 ? c.n_hb : lane == 1 ? c.n_gap : lane == 2 ? c.n_ev : lane == 3 ? c.n_free
-                   : lane == 4 ? c.nrec : lane == 5 ? c.farc : lane == 6 ? mode : cf.fused ? *cf.fused : 0;
-  if (lane < 8) __hip_atomic_store(hsig + SIG_HB + lane, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                   : lane == 4 ? c.nrec : lane == 5 ? c.farc : lane == 6 ? mode : lane == 7 ? (cf.fused ? *cf.fused : 0)
+                   : c.tgap;
+  if (lane < 9) __hip_atomic_store(hsig + SIG_HB + lane, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (lane == 0) __hip_atomic_store(hsig + SIG_TAG, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -2116,6 +2127,10 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
       const bool hb = (m[j] & 3u) == EV_HB;
       f[j] = (hb && a[j] > c_ex) ? v[j] : INT64_MIN;
       if (hb && a[j] > c_ex) c_ex = a[j];
+      // a GAP whose range starts at or below all_ackable_before (the batch's: it only grows)
+      // moves it to gapList.base (irrelevant_changes_range, rtps_writer_proxy.rs:241-292): a
+      // threshold like an accepted HEARTBEAT's, with no SN to record past the window
+      if ((m[j] & 3u) == EV_GAP && v[j] <= base && v[j] <= a[j] && a[j] > f[j]) f[j] = a[j];
       if (f[j] > fmax) fmax = f[j];
     }
     int64_t thr_total;
@@ -2198,6 +2213,8 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
     const int64_t lim = lo + (int64_t)W;
     uint32_t fkind = 0;  // far items (rare) of the thread's events: kind << 2 j, into the far set below
     auto far = [&](uint32_t j, uint32_t kind) { fkind |= kind << (2u * j); };
+    // a far item's first SN: a threshold GAP's range is the threshold's (above), only its list is recorded
+    auto fsn0 = [&](uint32_t kind, int64_t gv, int64_t ga) { return (kind == FI_GAP && gv <= base) ? ga + 1 : gv; };
 #pragma unroll
     for (uint32_t j = 0; j < PPT; ++j) {
       if (f[j] > t_run) t_run = f[j];
@@ -2229,7 +2246,7 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
 #pragma unroll
       for (uint32_t j = 0; j < PPT; ++j) {
         const uint32_t kind = (fkind >> (2u * j)) & 3u;
-        if (kind) pc += far_count(PEv{v[j], a[j], bwj[j], m[j], kk[j]}, kind, lim, arena);
+        if (kind) pc += far_count(PEv{fsn0(kind, v[j], a[j]), a[j], bwj[j], m[j], kk[j]}, kind, lim, arena);
       }
       if (pc) atomicAdd(&s_fp, (unsigned long long)pc);
       uint32_t nfi = 0;
@@ -2243,7 +2260,7 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
           for (uint32_t j = 0; j < PPT; ++j) {
             const uint32_t kind = (fkind >> (2u * j)) & 3u;
             if (kind)
-              far_sns(PEv{v[j], a[j], bwj[j], m[j], kk[j]}, kind, lim, arena,
+              far_sns(PEv{fsn0(kind, v[j], a[j]), a[j], bwj[j], m[j], kk[j]}, kind, lim, arena,
                       [&](int64_t sn) { add(sn, fkey_of(s.epoch, kk[j])); });
           }
         });
@@ -2910,8 +2927,11 @@ static int ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, cons
   const uint32_t gv = (uint32_t)hmin((nev + IT - 1) / IT, 8192) ? (uint32_t)hmin((nev + IT - 1) / IT, 8192) : 1u;
   // per-proxy workgroups when the events spread over many proxies (mean load bounded:
   // one workgroup replays a proxy's events in order); global marks / merge otherwise
+  // (threshold GAPs past a window: the per-proxy path applies them as thresholds, whatever the path)
+  const uint64_t tgap = s->hsig[SIG_TGAP];
   const bool per_proxy = t.n_proxies > 0 && nev > 0 &&
-                         (s->path == 2 || s->path == 4 || (s->path == 0 && t.n_proxies >= 64 && n_ev <= (uint64_t)t.n_proxies * 32768u));
+                         (tgap != 0 || s->path == 2 || s->path == 4 ||
+                          (s->path == 0 && t.n_proxies >= 64 && n_ev <= (uint64_t)t.n_proxies * 32768u));
   uint8_t* acc = ident ? out->accept : x.eacc;
   const uint64_t acc_cap = ident ? max : nev;
   if (per_proxy) {

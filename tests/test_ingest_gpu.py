@@ -276,6 +276,34 @@ def test_far_sets_many_proxies(rx):
         _batch(rx, ing, tbl, _far_datagrams(subs, per=5), f"far proxies batch {b}")
 
 
+def test_late_joiner_gap_threshold(rx):
+    """A reader that joins late: the writer's GAP [1, 10^6) starts at or below the proxy's
+    all_ackable_before, so irrelevant_changes_range only moves it to 10^6
+    (rtps_writer_proxy.rs:241-292) -- a threshold, with nothing to record SN by SN past the
+    window (the per-proxy path takes such batches whatever the path).  Samples before the GAP in
+    event order are accepted, those after it below 10^6 rejected; bit-exact with the oracle,
+    nothing counted (_batch), across batches, next to a writer with ordinary far traffic."""
+    import rtps_rx
+    W = rtps_rx.INGEST_WINDOW
+    w0, w1 = R.writer_key(0), R.writer_key(1)
+    tbl = pack_match_table([(R.PREFIXES[0] + w0, 0), (R.PREFIXES[0] + w1, 1)])
+    rx.set_match_table(tbl)
+    ing = oracle.HistoryIngest(tbl)
+    top = 1_000_000
+    subs = [R.data_sub(w0, top - 7), R.data_sub(w0, 5),
+            R.gap_sub(w0, 1, top, [True, False, True]),
+            R.data_sub(w0, top - 7), R.data_sub(w0, top - 1), R.data_sub(w0, top + 1), R.data_sub(w0, top + 2),
+            R.data_sub(w0, top), R.data_sub(w1, 3 * W), R.data_sub(w1, 3 * W), R.data_sub(w1, 1)]
+    _, dels, ack = _batch(rx, ing, tbl, [R.datagram(R.PREFIXES[0], subs[i:i + 3]) for i in range(0, len(subs), 3)],
+                          "late joiner")
+    assert ack.tolist()[0] == top + 3
+    # the next batch: below the new all_ackable_before, a second threshold GAP, fresh SNs
+    subs = [R.data_sub(w0, top - 3), R.gap_sub(w0, 2, top + 2 * W, []), R.data_sub(w0, top + 2 * W - 1),
+            R.data_sub(w0, top + 2 * W), R.data_sub(w1, 3 * W), R.data_sub(w1, 2)]
+    _, dels, ack = _batch(rx, ing, tbl, [R.datagram(R.PREFIXES[0], subs)], "late joiner 2")
+    assert ack.tolist()[0] == top + 2 * W + 1
+
+
 def test_far_pool_out_counted(rx):
     """The one capacity left: a GAP covering more SNs past the window than the far-set pool
     keeps free (here 2^34) cannot be recorded SN by SN; that proxy's far samples of the batch
