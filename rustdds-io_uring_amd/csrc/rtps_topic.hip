@@ -233,6 +233,7 @@ struct TDev {
   uint32_t* acum;     // [namb] stored undecided repeats up to amb[a] (inclusive), written in order
   uint32_t *ab, *ae;  // [nA] the topic's range of amb[]
   uint64_t* n_used;   // claimed live-index slots
+  uint64_t* h_used;   // pinned: n_used as the earlier batches left it (tc_gather)
 };
 constexpr uint8_t FL_GC = 1, FL_CAND = 2, FL_REP0 = 4, FL_PLIVE = 8, FL_VALID = 16;
 
@@ -245,6 +246,11 @@ __global__ __launch_bounds__(TT) void tc_gather(TDev d, const rtps_record* recs,
                                                 uint64_t max_del) {
   const uint64_t nrec = *n_records < max_records ? *n_records : max_records;
   const uint64_t nd = *n_del < max_del ? *n_del : max_del;
+  // the topics' segment starts: none until tc_mark finds one
+  for (uint32_t c = blockIdx.x * TT + threadIdx.x; c < d.nA; c += gridDim.x * TT) d.segb[c] = NONE;
+  // the live index's use as the earlier batches left it, to pinned host memory for reserve_live
+  // (read once this batch's event has passed: no copy on the stream)
+  if (blockIdx.x == 0 && threadIdx.x == 0) __hip_atomic_store(d.h_used, *d.n_used, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   for (uint64_t k = (uint64_t)blockIdx.x * TT + threadIdx.x; k < max_del; k += (uint64_t)gridDim.x * TT) {
     KeyP x{};
     x.rec = NONE;
@@ -306,6 +312,12 @@ __global__ __launch_bounds__(TT) void tc_mark(TDev d, uint64_t max_del) {
     d.gcpos[p] = gcp;
     d.fr[p] = 0;
     d.frins[p] = 0;
+    d.rst[p] = 0;   // (tc_rdec's outputs for the repeats j < nfr <= p; the scans read all of them)
+    d.ramb[p] = 0;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    d.rst[max_del] = 0;
+    d.ramb[max_del] = 0;
   }
 }
 
@@ -551,7 +563,8 @@ struct TopicState {
   PEnt* P = nullptr;
   uint64_t pcap = 0;
   uint64_t* n_used = nullptr;       // device: claimed live-index slots
-  uint64_t* h_used = nullptr;       // pinned copy, written after each batch
+  uint64_t* h_used = nullptr;       // pinned (mapped): n_used before each batch (its tc_gather)
+  uint64_t last_del = 0;            // max_del of the latest batch
   hipEvent_t used_ev = nullptr;     // that copy of the last batch
   bool used_pending = false;
   uint64_t used_known = 0;          // claimed slots when the last observed copy was made
@@ -602,7 +615,7 @@ TopicState* rtps_topic_state_new(int device) {
             dmalloc((void**)&s->nfr, 8) && dmalloc((void**)&s->n_full, 8) && dmalloc((void**)&s->n_used, 8) &&
             dmalloc((void**)&s->namb, 8) &&
             hipMemset(s->n_full, 0, 8) == hipSuccess && hipMemset(s->n_used, 0, 8) == hipSuccess &&
-            hipHostMalloc((void**)&s->h_used, 8, hipHostMallocDefault) == hipSuccess &&
+            hipHostMalloc((void**)&s->h_used, 8, hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess &&
             hipEventCreateWithFlags(&s->used_ev, hipEventDisableTiming) == hipSuccess;
   if (!ok) { rtps_topic_state_free(s); return nullptr; }
   return s;
@@ -782,8 +795,8 @@ static int rebuild_live(TopicState* s, uint64_t ncap, hipStream_t st) {
 }
 static int reserve_live(TopicState* s, uint64_t max_del, hipStream_t st) {
   if (s->used_pending && hipEventQuery(s->used_ev) == hipSuccess) {  // every batch so far is done
-    s->used_known = *s->h_used;
-    s->used_inflight = 0;
+    s->used_known = *s->h_used;       // (before the latest batch: its tc_gather wrote it)
+    s->used_inflight = s->last_del;   // what the latest batch may have claimed
     s->used_pending = false;
   }
   if (s->P && 2 * (s->used_known + s->used_inflight + max_del) <= s->pcap) return RTPS_RX_OK;
@@ -860,11 +873,11 @@ int rtps_topic_apply(TopicState* s, hipStream_t st, const rtps_record* recs, con
   d.frins = s->frins; d.frlist = s->frlist; d.nfr = s->nfr; d.frcum = s->frcum; d.fridx = s->fridx;
   d.segb = s->segb; d.sege = s->sege; d.frb = s->frb; d.fre = s->fre; d.ibase = s->ibase; d.n_full = s->n_full;
   d.n_used = s->n_used;
+  d.h_used = s->h_used;
   d.ovf = ovf;
   d.rdec = s->rdec; d.rst = s->rst; d.rpre = s->rpre; d.ramb = s->ramb; d.amb = s->amb; d.namb = s->namb;
   d.acum = s->acum; d.ab = s->ab; d.ae = s->ae;
   const uint32_t g = (uint32_t)((max_del + TT - 1) / TT < 8192 ? (max_del + TT - 1) / TT : 8192);
-  if (s->nA && hipMemsetAsync(s->segb, 0xff, s->nA * 4ull, st) != hipSuccess) return RTPS_RX_EHIP;
   hipLaunchKernelGGL(tc_gather, dim3(g), dim3(TT), 0, st, d, recs, n_records, max_records, del, n_del, max_del);
   if (d.order) {
     uint32_t bits = 1;
@@ -888,9 +901,6 @@ int rtps_topic_apply(TopicState* s, hipStream_t st, const rtps_record* recs, con
                                     (int64_t)max_del, st) != hipSuccess)
     return RTPS_RX_EHIP;
   // repeats: the sure ones decided in parallel, the undecided ones per topic in order
-  if (hipMemsetAsync(s->rst, 0, (max_del + 1) * 4, st) != hipSuccess ||
-      hipMemsetAsync(s->ramb, 0, max_del + 1, st) != hipSuccess)
-    return RTPS_RX_EHIP;
   hipLaunchKernelGGL(tc_rdec, dim3(g), dim3(TT), 0, st, d);
   tb = s->tmp_bytes;
   if (hipcub::DeviceScan::ExclusiveSum(s->tmp, tb, s->rst, s->rpre, (int64_t)max_del + 1, st) != hipSuccess)
@@ -903,9 +913,8 @@ int rtps_topic_apply(TopicState* s, hipStream_t st, const rtps_record* recs, con
   hipLaunchKernelGGL(tc_rfill, dim3(g), dim3(TT), 0, st, d);
   hipLaunchKernelGGL(tc_final, dim3(g), dim3(TT), 0, st, d, del, max_del);
   s->used_inflight += max_del;
-  if (hipMemcpyAsync(s->h_used, s->n_used, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
-      hipEventRecord(s->used_ev, st) != hipSuccess)
-    return RTPS_RX_EHIP;
+  s->last_del = max_del;
+  if (hipEventRecord(s->used_ev, st) != hipSuccess) return RTPS_RX_EHIP;
   s->used_pending = true;
   return hipGetLastError() == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP;
 }

@@ -5,6 +5,7 @@
 #   c3_emit        C3 bench lines for each record pass (RTPS_RX_EMIT=1/2/3)
 #   kstats_C3      rocprofv3 kernel-trace stats of the C3 bench
 #   gpu_tests      the whole -m gpu suite
+shopt -s nullglob  # (no variants: the loops run the in-tree library only)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; R=$(pwd); O=$R/gpurun_out/exp; mkdir -p $O; export TMPDIR=/tmp
 PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
 for step in "$@"; do
@@ -44,6 +45,17 @@ d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); r = d["roofli
 print(sys.argv[2], "step", round(d["ms_per_step"] * 1e3, 1), "us", "frac", round(r["frac"], 3), "kernel_us", round(r.get("kernel_ms", 0) * 1e3, 1))
 PY
       done ;;
+    ing_var)  # C3 and T parse + ingest for the in-tree library and every variant (RTPS_RX_LIB)
+      for wl in C3 T; do
+      for lib in $R/rustdds-io_uring_amd/librtps_rx.so $R/rustdds-io_uring_amd/variants/librtps_rx_*.so $R/rustdds-io_uring_amd/librtps_rx.so; do
+        v=$(basename $lib .so)
+        RTPS_RX_LIB=$lib timeout -k 10 300 python bench.py --workload $wl --steps 20 --warmup 5 --no-c1 --no-e2e --no-cpu-baseline --no-cdr > $O/ing_${wl}_$v.json 2> $O/ing_${wl}_$v.err || { tail -5 $O/ing_${wl}_$v.err; exit 4; }
+        python - $O/ing_${wl}_$v.json $v $wl <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); g = d["ingest"]
+print(sys.argv[3], sys.argv[2], "step", round(d["ms_per_step"] * 1e3, 1), "us ingest", round(g["ms"] * 1e3, 1), "tc", round(g["topic_cache_ms"] * 1e3, 1))
+PY
+      done; done ;;
     pmc)  # FETCH / WRITE passes of T (ceiling + parse) and C3 -> gpurun_out/r${ROUND}_pmc_{T,C3}.json
       ROUND=${ROUND:-5} timeout -k 10 700 bash scripts/gpu_pmc.sh > $O/pmc.log 2>&1 || { tail -5 $O/pmc.log; exit 12; }
       cp gpurun_out/r${ROUND:-5}_pmc_T.json gpurun_out/r${ROUND:-5}_pmc_C3.json $O/ ;;
