@@ -1040,7 +1040,8 @@ __global__ __launch_bounds__(TILE, RTPS_IT_WAVES_PER_SIMD) void rtps_parse_item_
                                                                                      uint32_t k_spec, u32x4* items,
                                                                                      uint32_t* wcnt, u32x4* dinfo) {
   __shared__ uint32_t s_wave_sum[WAVES], s_wave_bad[WAVES];
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // (uniform: the slab base in SGPRs)
   const uint32_t tile = blockIdx.x;
   TileCtx t;
   load_tile(p, tile, t);
@@ -1233,7 +1234,7 @@ __global__ __launch_bounds__(EM2T, RTPS_EM2_WAVES_PER_SIMD) void rtps_parse_emit
 #if RTPS_EM2_TRANSPOSE
   __shared__ u32x4 s_stage[(EM2T / 64u) * 64u];    // 1 KB per wave
 #endif
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t wave = wv % WAVES, sub = wv / WAVES;  // the wave's slab in its tile, the workgroup's tile
   uint16_t* map = s_map + wv * CAPW;
   mt_stage(p);
