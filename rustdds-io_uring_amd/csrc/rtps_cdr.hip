@@ -332,7 +332,8 @@ extern __shared__ uint8_t cdr_lds[];
 template <bool WIDE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CDR_WAVES_PER_EU)))
 void cdr_decode_kernel(CdrProg P, CdrArgs a) {
-  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, wpb = blockDim.x >> 6;
+  const uint32_t lane = threadIdx.x & 63u, wpb = blockDim.x >> 6;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (uniform: LDS bases in SGPRs)
   uint8_t* T = cdr_lds + wave * P.lds_per_wave;
   uint32_t* meta = (uint32_t*)T;             // [64] status | le << 8
   uint64_t* vbase = (uint64_t*)(T + 256);    // [64] arena offset of the value

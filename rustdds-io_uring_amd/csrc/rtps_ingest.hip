@@ -402,7 +402,7 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
   if (blockIdx.x == gridDim.x - 1u)  // the next batch's counters start at zero (no memset launch)
     for (uint32_t c = threadIdx.x; c < C_COUNT; c += IT) ctr_next[c] = 0ull;
   __shared__ uint32_t s_part[IT / 64];
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint64_t n = *n_rec < max ? *n_rec : max;
   if (blockIdx.x == 0 && tid == 0) ctr[C_NREC] = n;
   if (FAST && !BUCKET)
@@ -1232,7 +1232,7 @@ __device__ __forceinline__ void dwrite_tile(uint32_t blk, const uint8_t* flag, u
                                             uint32_t ntiles, const Scratch& x, bool ident, uint64_t max_out,
                                             rtps_delivery* out, uint64_t* n_out, const uint64_t* ctr, uint64_t* ovf_out,
                                             uint64_t* hev, const uint64_t* fused, uint64_t* s_w, uint32_t* s_c) {
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   uint64_t pre = 0;
   for (uint32_t t = tid; t < blk; t += IT) pre += tcnt[t];
   pre = block_sum64(pre, s_w);

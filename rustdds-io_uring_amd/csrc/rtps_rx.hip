@@ -770,7 +770,7 @@ __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_spec_ker
   __shared__ uint32_t s_wave_sum[WAVES], s_wave_bad[WAVES];
   __shared__ u32x4 s_stage[STAGE_RECS * 4];
   __shared__ uint32_t s_stage_match[STAGE_RECS];
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t tile = blockIdx.x;
   mt_stage(p);  // visible after the __syncthreads below, before the writing walk
   TileCtx t;
@@ -863,7 +863,7 @@ __global__ __launch_bounds__(TILE, RTPS_WAVES_PER_SIMD) void rtps_parse_fix_kern
   __shared__ uint32_t s_wave_sum[WAVES];
   __shared__ uint64_t s_rsum[WAVES];
   __shared__ uint32_t s_rmin[WAVES];
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   Scratch x = scratch_of(p.scratch, n_tiles);
   if (blockIdx.x == 0 && tid == 0) x.flag[parity ^ 1u] = 0u;  // for the next launch
   if (__builtin_amdgcn_readfirstlane(x.flag[parity]) == 0u) {
