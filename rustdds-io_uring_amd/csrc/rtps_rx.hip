@@ -588,18 +588,18 @@ __device__ uint32_t walk(const KParams& p, const Src& s, const uint32_t* H, uint
   // WRITE: the window of the next submessage is loaded before this record's
   // stores are issued.  vmcnt counts stores too, so a load issued after them
   // would make the next iteration wait for their write acknowledgements.
-  Win Wn;
+  // The count walk takes its first window from the head before the loop, so
+  // the head's registers are dead in it.
+  Win Wn, W;
   if (WRITE) head_win(H, Wn);
+  else head_win(H, W);
   while (o < L) {
     uint32_t rem = L - o;
     if (rem < 4u) return RTPS_DGRAM_SUBMSG_ERR;  // SubmessageHeader needs 4 bytes
-    Win W;
     if (WRITE) {
       W = Wn;
       if (o != 20u && (W.w[0] & 0xffu) == RTPS_DATA_FRAG) W.w[8] = ld4(s, o + 32u);
-    } else if (o == 20u) {
-      head_win(H, W);
-    } else {
+    } else if (o != 20u) {
       load_win_lazy<WRITE>(s, o, W);
     }
     uint32_t kind = W.w[0] & 0xffu, flags = (W.w[0] >> 8) & 0xffu;
@@ -998,12 +998,13 @@ __device__ uint32_t item_walk(const KParams& p, const Src& s, const uint32_t* H,
   uint32_t src_off = 8u;
   const uint64_t lt = lane ? (~0ull >> (64u - lane)) : 0ull;
   uint32_t o = 20;
+  // the first window comes from the head, before the loop: the head's registers are dead in it
+  Win W;
+  head_win(H, W);
   while (o < L) {
     const uint32_t rem = L - o;
     if (rem < 4u) return RTPS_DGRAM_SUBMSG_ERR;
-    Win W;
-    if (o == 20u) head_win(H, W);
-    else load_win_lazy<RTPS_IT_WIDE != 0>(s, o, W);
+    if (o != 20u) load_win_lazy<RTPS_IT_WIDE != 0>(s, o, W);
     const uint32_t kind = W.w[0] & 0xffu, flags = (W.w[0] >> 8) & 0xffu;
     const bool le = (flags & 1u) != 0u;
     const uint32_t eff = eff_len(kind, e16(W.w[0], 1, le), rem);
