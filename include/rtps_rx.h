@@ -492,38 +492,52 @@ int rtps_rx_shard_owner(rtps_shard* s, const uint8_t guid[16]);
 int rtps_rx_owner_assign(const uint8_t* writers, const uint64_t* weights, const uint32_t* groups, uint32_t n,
                          uint32_t n_ranks, uint32_t* owners);
 
-/* ---- batch CDR primitive decode (a18) ------------------------------------
- * Replaces, for fixed-layout sample types, the per-sample decode
+/* ---- batch CDR decode (a18) ----------------------------------------------
+ * Replaces the per-sample decode
  *   SimpleDataReader::deserialize_with -> DA::from_bytes_with(&payload.value, rep_id, ..)
  *       io_uring/dds/with_key/simpledatareader.rs:137-160, dds/adapters.rs:128-139
  *   -> deserialize_from_cdr_with_decoder_and_rep_id   serialization/cdr_adapters.rs:246-275
  *   -> cdr_encoding::CdrDeserializer (external crate cdr-encoding 0.10)
- * The type is a flat "program" of ops (a struct's fields in order; nested
- * structs flatten because classic CDR aligns each primitive to its own size
- * relative to the first byte after the 4-byte encapsulation header).  Every
- * DATA record with payload_kind == RTPS_PK_DATA is decoded into a row of
- * row_bytes at rows + record_index * row_bytes (host byte order). */
+ * The type is a "program" of ops (a struct's fields in order; nested structs
+ * flatten because classic CDR aligns each primitive to its own size relative
+ * to the first byte after the 4-byte encapsulation header).  Sequences and
+ * arrays of non-primitive elements (strings, structs, sequences) are a
+ * SEQ_BEGIN / ARRAY_BEGIN op, the element's ops, and an END op.  Every DATA
+ * record with payload_kind == RTPS_PK_DATA is decoded into a row of row_bytes
+ * at rows + record_index * row_bytes (host byte order). */
 enum rtps_cdr_op_kind {
-  RTPS_CDR_PRIM = 1,   /* size 1/2/4/8 (ints, f32, f64, unit enum = u32)                          */
-  RTPS_CDR_BOOL = 2,   /* 1 byte, must be 0 or 1                                                   */
-  RTPS_CDR_STRING = 3, /* u32 length incl. NUL + bytes, UTF-8 checked; count = max chars (no NUL) */
-  RTPS_CDR_SEQ = 4,    /* u32 n + n primitives of `size`; count = max elements                     */
-  RTPS_CDR_ARRAY = 5   /* count primitives of `size`, no length                                    */
+  RTPS_CDR_PRIM = 1,        /* size 1/2/4/8 (ints, f32, f64, unit enum = u32)                          */
+  RTPS_CDR_BOOL = 2,        /* 1 byte, must be 0 or 1                                                   */
+  RTPS_CDR_STRING = 3,      /* u32 length incl. NUL + bytes, UTF-8 checked; count = max chars (no NUL) */
+  RTPS_CDR_SEQ = 4,         /* u32 n + n primitives of `size`; count = max elements                     */
+  RTPS_CDR_ARRAY = 5,       /* count primitives of `size`, no length                                    */
+  RTPS_CDR_SEQ_BEGIN = 6,   /* u32 n + n elements = the ops up to the matching END; count = max elements */
+  RTPS_CDR_ARRAY_BEGIN = 7, /* count elements = the ops up to the matching END, no length               */
+  RTPS_CDR_END = 8          /* closes the innermost open SEQ_BEGIN / ARRAY_BEGIN (size, count, out_off 0) */
 };
 /* Row layout: each op owns a slot that starts at out_off (4-aligned) and spans
- * a multiple of 4 bytes; slots must not overlap and must lie inside the row:
+ * a multiple of 4 bytes; sibling slots must not overlap and must lie inside
+ * their container (the row, or one element):
  *   PRIM  align4(size)           value (host order), zero-extended
  *   BOOL  4                      byte 0 = 0/1, rest 0
  *   STRING 4 + align4(count)     u32 chars, then the chars, zero tail (no NUL)
  *   SEQ   4 + align4(size*count) u32 n, then n elements, zero tail
  *   ARRAY align4(size*count)     count elements
- * Bytes not covered by a slot are zero.  A row whose decode fails is all zero. */
+ *   SEQ_BEGIN   4 + count*stride u32 n, then element i at +4 + i*stride (i < n)
+ *   ARRAY_BEGIN count*stride     element i at i*stride
+ * The ops between a BEGIN and its END lay out ONE element: their out_off are
+ * relative to the element's start and their slots lie inside [0, stride).
+ * Bytes not covered by a slot (elements >= n included) are zero.  A row whose
+ * decode fails is all zero.  Nesting depth <= RTPS_CDR_MAX_DEPTH.
+ * A sequence longer than its slot (n > count) is RTPS_CDR_TOO_LONG once its
+ * elements have been read (so a malformed element reports the reference's own
+ * error); elements that occupy no wire bytes cannot fail and report it at once. */
 typedef struct rtps_cdr_op {
   uint8_t kind;      /* rtps_cdr_op_kind */
   uint8_t size;      /* primitive size for PRIM / SEQ / ARRAY */
-  uint16_t _r;
-  uint32_t count;    /* STRING: max chars; SEQ: max elements; ARRAY: elements */
-  uint32_t out_off;  /* byte offset of the slot in the output row (multiple of 4) */
+  uint16_t stride;   /* SEQ_BEGIN / ARRAY_BEGIN: row bytes per element (multiple of 4, >= 4); else 0 */
+  uint32_t count;    /* STRING: max chars; SEQ / SEQ_BEGIN: max elements; ARRAY / ARRAY_BEGIN: elements */
+  uint32_t out_off;  /* byte offset of the slot in the row / element (multiple of 4) */
 } rtps_cdr_op;
 enum rtps_cdr_status {
   RTPS_CDR_OK = 0,
@@ -534,6 +548,7 @@ enum rtps_cdr_status {
   RTPS_CDR_BAD_UTF8 = 5,        /* string bytes are not UTF-8                               */
   RTPS_CDR_TOO_LONG = 6         /* string/sequence longer than the row slot (not a reference error) */
 };
+#define RTPS_CDR_MAX_DEPTH 4u
 #define RTPS_CDR_MAX_OPS 64u
 /* prog: host array of n_ops ops (copied at the call).  arena / dgram_off: the
  * batch given to rtps_rx_parse_batch; records / n_records: its outputs.

@@ -837,12 +837,51 @@ static void cdr_store(uint8_t* row, uint32_t off, uint64_t x, uint32_t size) {
   for (uint32_t k = 0; k < size; ++k) row[off + k] = (uint8_t)(x >> (8 * k)); /* host = little-endian */
 }
 
+/* Composite elements (RTPS_CDR_SEQ_BEGIN / ARRAY_BEGIN ... END): serde's Vec<T> /
+ * [T; N] through cdr-encoding's deserialize_seq / deserialize_tuple: a u32 count
+ * (aligned to 4; arrays have none), then each element's fields in order, with no
+ * alignment of the element's own.  cdr_match: the END that closes the BEGIN at k. */
+static uint32_t cdr_match(const rtps_cdr_op* prog, uint32_t n_ops, uint32_t k) {
+  uint32_t depth = 0;
+  for (uint32_t j = k; j < n_ops; ++j) {
+    if (prog[j].kind == RTPS_CDR_SEQ_BEGIN || prog[j].kind == RTPS_CDR_ARRAY_BEGIN) depth++;
+    else if (prog[j].kind == RTPS_CDR_END && --depth == 0) return j;
+  }
+  return n_ops;
+}
+/* the fewest wire bytes ops [a, b) can consume (0: they read nothing, so they cannot fail) */
+static uint64_t cdr_min_wire(const rtps_cdr_op* prog, uint32_t n_ops, uint32_t a, uint32_t b) {
+  uint64_t m = 0;
+  for (uint32_t k = a; k < b; ++k) {
+    const rtps_cdr_op* op = &prog[k];
+    switch (op->kind) {
+      case RTPS_CDR_PRIM: m += op->size; break;
+      case RTPS_CDR_BOOL: m += 1; break;
+      case RTPS_CDR_ARRAY: m += (uint64_t)op->size * op->count; break;
+      case RTPS_CDR_STRING: case RTPS_CDR_SEQ: case RTPS_CDR_SEQ_BEGIN: m += 4; break;
+      case RTPS_CDR_ARRAY_BEGIN: {
+        uint32_t j = cdr_match(prog, n_ops, k);
+        m += (uint64_t)op->count * cdr_min_wire(prog, n_ops, k + 1, j);
+        break;
+      }
+      default: break;
+    }
+    if (op->kind == RTPS_CDR_SEQ_BEGIN || op->kind == RTPS_CDR_ARRAY_BEGIN) k = cdr_match(prog, n_ops, k);
+  }
+  return m;
+}
+typedef struct cdr_frame { uint32_t begin, n, i, elem0, base; int write; } cdr_frame;
+
 static uint8_t cdr_decode_one(const rtps_cdr_op* prog, uint32_t n_ops, const uint8_t* value, uint32_t len, int le,
                               uint8_t* row) {
   cdr_cur c = {value, len, 0, le};
+  cdr_frame fr[RTPS_CDR_MAX_DEPTH];
+  uint32_t depth = 0, base = 0; /* base: row offset of the current element (0: the row) */
+  int write = 1;                /* 0 inside elements past a sequence's slot (n > count) */
   for (uint32_t k = 0; k < n_ops; ++k) {
     const rtps_cdr_op* op = &prog[k];
     uint32_t size = op->size;
+    uint8_t* dst = row + base; /* elements past the slot are read (and validated), not stored */
     switch (op->kind) {
       case RTPS_CDR_PRIM:
       case RTPS_CDR_ARRAY: {
@@ -851,7 +890,8 @@ static uint8_t cdr_decode_one(const rtps_cdr_op* prog, uint32_t n_ops, const uin
         uint32_t pad = cdr_pad(c.pos, size);
         if ((uint64_t)c.pos + pad + (uint64_t)cnt * size > c.len) return RTPS_CDR_EOF;
         c.pos += pad;
-        for (uint32_t e = 0; e < cnt; ++e) cdr_store(row, op->out_off + e * size, cdr_get(&c, c.pos + e * size, size), size);
+        if (write)
+          for (uint32_t e = 0; e < cnt; ++e) cdr_store(dst, op->out_off + e * size, cdr_get(&c, c.pos + e * size, size), size);
         c.pos += cnt * size;
         break;
       }
@@ -859,7 +899,7 @@ static uint8_t cdr_decode_one(const rtps_cdr_op* prog, uint32_t n_ops, const uin
         if (c.pos + 1 > c.len) return RTPS_CDR_EOF;
         uint8_t b = c.v[c.pos];
         if (b > 1) return RTPS_CDR_BAD_BOOL;
-        row[op->out_off] = b;
+        if (write) dst[op->out_off] = b;
         c.pos += 1;
         break;
       }
@@ -873,8 +913,10 @@ static uint8_t cdr_decode_one(const rtps_cdr_op* prog, uint32_t n_ops, const uin
         uint32_t m = l ? l - 1 : 0;
         if (!utf8_ok(c.v + c.pos, m)) return RTPS_CDR_BAD_UTF8;
         if (m > op->count) return RTPS_CDR_TOO_LONG;
-        cdr_store(row, op->out_off, m, 4);
-        memcpy(row + op->out_off + 4, c.v + c.pos, m);
+        if (write) {
+          cdr_store(dst, op->out_off, m, 4);
+          memcpy(dst + op->out_off + 4, c.v + c.pos, m);
+        }
         c.pos += l;
         break;
       }
@@ -889,11 +931,47 @@ static uint8_t cdr_decode_one(const rtps_cdr_op* prog, uint32_t n_ops, const uin
           if ((uint64_t)c.pos + pe + (uint64_t)n * size > c.len) return RTPS_CDR_EOF;
           if (n > op->count) return RTPS_CDR_TOO_LONG;
           c.pos += pe;
-          for (uint32_t e = 0; e < n; ++e)
-            cdr_store(row, op->out_off + 4 + e * size, cdr_get(&c, c.pos + e * size, size), size);
+          for (uint32_t e = 0; write && e < n; ++e)
+            cdr_store(dst, op->out_off + 4 + e * size, cdr_get(&c, c.pos + e * size, size), size);
           c.pos += n * size;
         }
-        cdr_store(row, op->out_off, n, 4);
+        if (write) cdr_store(dst, op->out_off, n, 4);
+        break;
+      }
+      case RTPS_CDR_SEQ_BEGIN:
+      case RTPS_CDR_ARRAY_BEGIN: {
+        const int seq = op->kind == RTPS_CDR_SEQ_BEGIN;
+        uint32_t n = op->count;
+        if (seq) {
+          uint32_t pad = cdr_pad(c.pos, 4);
+          if ((uint64_t)c.pos + pad + 4 > c.len) return RTPS_CDR_EOF;
+          c.pos += pad;
+          n = (uint32_t)cdr_get(&c, c.pos, 4);
+          c.pos += 4;
+          if (write) cdr_store(dst, op->out_off, n, 4);
+        }
+        const uint32_t j = cdr_match(prog, n_ops, k);
+        if (n == 0) { k = j; break; }
+        if (n > op->count && cdr_min_wire(prog, n_ops, k + 1, j) == 0) return RTPS_CDR_TOO_LONG;
+        cdr_frame f = {k, n, 0, base + op->out_off + (seq ? 4u : 0u), base, write};
+        fr[depth++] = f;
+        base = f.elem0;
+        write = write && op->count > 0;
+        break;
+      }
+      case RTPS_CDR_END: {
+        cdr_frame* f = &fr[depth - 1];
+        const rtps_cdr_op* b = &prog[f->begin];
+        if (++f->i < f->n) {
+          base = f->elem0 + f->i * b->stride;
+          write = f->write && f->i < b->count;
+          k = f->begin; /* the loop's ++k enters the element's first op */
+        } else {
+          depth--;
+          base = f->base;
+          write = f->write;
+          if (f->n > b->count) return RTPS_CDR_TOO_LONG;
+        }
         break;
       }
       default:

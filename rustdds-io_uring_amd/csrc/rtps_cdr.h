@@ -55,6 +55,22 @@ struct CdrArgs {
   uint64_t max_list;
 };
 
+// Composite programs (SEQ_BEGIN / ARRAY_BEGIN ... END, include/rtps_rx.h): one lane
+// decodes one row, following the program with a stack of open elements.
+struct CdrNest {  // kernel argument
+  rtps_cdr_op ops[RTPS_CDR_MAX_OPS];
+  uint8_t match[RTPS_CDR_MAX_OPS];    // BEGIN k -> its END; END -> its BEGIN
+  uint8_t zero_el[RTPS_CDR_MAX_OPS];  // BEGIN k: the element reads no wire bytes (it cannot fail)
+  uint32_t n_ops;
+  uint32_t row_bytes;
+};
+// true if the program has composite ops
+bool rtps_cdr_is_composite(const rtps_cdr_op* prog, uint32_t n_ops);
+// Validates a composite program (op kinds and sizes, slots inside their container and
+// not overlapping, BEGIN/END matched, depth <= RTPS_CDR_MAX_DEPTH) and fills N.
+bool rtps_cdr_build_nested(const rtps_cdr_op* prog, uint32_t n_ops, uint32_t row_bytes, CdrNest& N);
+int rtps_cdr_launch_nested(hipStream_t s, const CdrNest& N, const CdrArgs& a, uint32_t max_blocks);
+
 // Builds the slot list from validated ops (host).  Returns false if slots overlap
 // or leave the row.
 bool rtps_cdr_build_slots(CdrProg& P);

@@ -15,6 +15,7 @@
 // the value bytes a decoded row consumes + row_bytes + 1 status byte written.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
 
 #include "../../include/rtps_rx.h"
 #include "rtps_cdr.h"
@@ -467,7 +468,253 @@ void cdr_decode_kernel(CdrProg P, CdrArgs a) {
   }
 }
 
+// ---- composite programs ----------------------------------------------------
+// Lane-serial decode of one row with the restated cdr-encoding rules of
+// cdr_validate, plus elements: SEQ_BEGIN reads a u32 count (aligned to 4),
+// ARRAY_BEGIN has none; each element is the ops up to the matching END, with
+// no alignment of its own (serde's Vec<T> / [T; N] through deserialize_seq /
+// deserialize_tuple).  Elements past the slot (n > count) are read and
+// validated but not stored; the sequence is then TOO_LONG (at once when its
+// element reads no bytes, as it cannot fail).  The lane zeroed its row first
+// (its own stores: program order), and zeroes it again when the decode fails.
+__device__ __forceinline__ void copy_bytes(uint8_t* d, const uint8_t* s, uint32_t m) {
+  uint32_t i = 0;
+  for (; i + 4 <= m; i += 4) *(uint32_t*)(d + i) = *(const u32u*)(s + i);  // d is 4-aligned
+  for (; i < m; ++i) d[i] = s[i];
+}
+__device__ uint8_t nest_decode(const rtps_cdr_op* ops, const uint8_t* match, const uint8_t* zero_el, uint32_t n_ops,
+                               const uint8_t* v, uint32_t len, bool le, uint8_t* row) {
+  struct Frame { uint32_t begin, n, i, elem0, base; bool write; };
+  Frame fr[RTPS_CDR_MAX_DEPTH];
+  uint32_t depth = 0, base = 0, pos = 0;
+  bool write = true;
+  for (uint32_t k = 0; k < n_ops; ++k) {
+    const rtps_cdr_op op = ops[k];
+    const uint32_t size = op.size;
+    uint8_t* d = row + base + op.out_off;
+    switch (op.kind) {
+      case RTPS_CDR_PRIM:
+      case RTPS_CDR_ARRAY: {
+        const uint32_t cnt = op.kind == RTPS_CDR_PRIM ? 1u : op.count;
+        if (cnt == 0) break;
+        const uint32_t pad = pad_to(pos, size);
+        if ((uint64_t)pos + pad + (uint64_t)cnt * size > len) return RTPS_CDR_EOF;
+        pos += pad;
+        if (write)
+          for (uint32_t e = 0; e < cnt; ++e) store_prim(d + e * size, load_prim(v + pos + e * size, size, le), size);
+        pos += cnt * size;
+        break;
+      }
+      case RTPS_CDR_BOOL:
+        if (pos + 1 > len) return RTPS_CDR_EOF;
+        if (v[pos] > 1) return RTPS_CDR_BAD_BOOL;
+        if (write) d[0] = v[pos];
+        pos += 1;
+        break;
+      case RTPS_CDR_STRING: {
+        pos += pad_to(pos, 4);
+        if ((uint64_t)pos + 4 > len) return RTPS_CDR_EOF;
+        const uint32_t l = (uint32_t)load_prim(v + pos, 4, le);
+        pos += 4;
+        if ((uint64_t)pos + l > len) return RTPS_CDR_EOF;
+        const uint32_t m = l ? l - 1 : 0;
+        if (!utf8_ok(v + pos, m)) return RTPS_CDR_BAD_UTF8;
+        if (m > op.count) return RTPS_CDR_TOO_LONG;
+        if (write) {
+          *(uint32_t*)d = m;
+          copy_bytes(d + 4, v + pos, m);
+        }
+        pos += l;
+        break;
+      }
+      case RTPS_CDR_SEQ: {
+        pos += pad_to(pos, 4);
+        if ((uint64_t)pos + 4 > len) return RTPS_CDR_EOF;
+        const uint32_t n = (uint32_t)load_prim(v + pos, 4, le);
+        pos += 4;
+        if (n) {
+          const uint32_t pe = pad_to(pos, size);
+          if ((uint64_t)pos + pe + (uint64_t)n * size > len) return RTPS_CDR_EOF;
+          if (n > op.count) return RTPS_CDR_TOO_LONG;
+          pos += pe;
+          if (write)
+            for (uint32_t e = 0; e < n; ++e) store_prim(d + 4 + e * size, load_prim(v + pos + e * size, size, le), size);
+          pos += n * size;
+        }
+        if (write) *(uint32_t*)d = n;
+        break;
+      }
+      case RTPS_CDR_SEQ_BEGIN:
+      case RTPS_CDR_ARRAY_BEGIN: {
+        const bool seq = op.kind == RTPS_CDR_SEQ_BEGIN;
+        uint32_t n = op.count;
+        if (seq) {
+          pos += pad_to(pos, 4);
+          if ((uint64_t)pos + 4 > len) return RTPS_CDR_EOF;
+          n = (uint32_t)load_prim(v + pos, 4, le);
+          pos += 4;
+          if (write) *(uint32_t*)d = n;
+        }
+        if (n == 0) { k = match[k]; break; }
+        if (n > op.count && zero_el[k]) return RTPS_CDR_TOO_LONG;
+        fr[depth] = Frame{k, n, 0u, base + op.out_off + (seq ? 4u : 0u), base, write};
+        base = fr[depth].elem0;
+        write = write && op.count > 0;
+        depth++;
+        break;
+      }
+      case RTPS_CDR_END: {
+        Frame& f = fr[depth - 1];
+        const rtps_cdr_op b = ops[f.begin];
+        if (++f.i < f.n) {
+          base = f.elem0 + f.i * b.stride;
+          write = f.write && f.i < b.count;
+          k = f.begin;  // ++k: the element's first op
+        } else {
+          depth--;
+          base = f.base;
+          write = f.write;
+          if (f.n > b.count) return RTPS_CDR_TOO_LONG;
+        }
+        break;
+      }
+      default:
+        return RTPS_CDR_TOO_LONG;
+    }
+  }
+  return RTPS_CDR_OK;
+}
+
+__device__ __forceinline__ void zero_row(uint8_t* r, uint32_t bytes) {
+  uint32_t b = 0;
+  for (; b + 16 <= bytes; b += 16) st16u(r + b, make_uint4(0, 0, 0, 0));
+  for (; b < bytes; b += 4) *(uint32_t*)(r + b) = 0u;
+}
+
+__global__ __launch_bounds__(256) void cdr_nested_kernel(CdrNest N, CdrArgs a) {
+  __shared__ rtps_cdr_op s_ops[RTPS_CDR_MAX_OPS];
+  __shared__ uint8_t s_match[RTPS_CDR_MAX_OPS], s_zero[RTPS_CDR_MAX_OPS];
+  if (threadIdx.x < N.n_ops) {
+    s_ops[threadIdx.x] = N.ops[threadIdx.x];
+    s_match[threadIdx.x] = N.match[threadIdx.x];
+    s_zero[threadIdx.x] = N.zero_el[threadIdx.x];
+  }
+  __syncthreads();
+  const uint64_t n = a.list ? min(*a.n_list, a.max_list) : min(*a.n_records, a.max_records);
+  const uint64_t nrec = min(*a.n_records, a.max_records);
+  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t ri = a.list ? *reinterpret_cast<const uint32_t*>(a.list + r * a.list_stride) : r;
+    uint8_t* row = a.rows + r * N.row_bytes;
+    zero_row(row, N.row_bytes);
+    uint32_t st;
+    if (ri >= nrec) {
+      st = RTPS_CDR_NOT_DATA;
+    } else {
+      const uint8_t* rec = (const uint8_t*)(a.records + ri);
+      const uint4 h0 = *(const uint4*)rec, h1 = *(const uint4*)(rec + 16);
+      const uint2 u0 = *(const uint2*)(rec + 40);
+      const uint32_t kind = (h0.y >> 16) & 0xff, pk = h1.w >> 24;
+      const uint32_t pl_off = u0.x & 0xffff, pl_len = u0.x >> 16;
+      const uint32_t id0 = u0.y & 0xff, id1 = (u0.y >> 8) & 0xff;
+      if (kind != RTPS_DATA || pk != RTPS_PK_DATA || pl_len < 4) {
+        st = RTPS_CDR_NOT_DATA;
+      } else if (id0 != 0 || (id1 != 0 && id1 != 1 && id1 != 3)) {
+        st = RTPS_CDR_BAD_ENCODING;
+      } else {
+        const uint64_t vb = a.dgram_off[h0.x] + pl_off + 4;
+        const uint32_t len = pl_len - 4;
+        st = (vb + len > a.arena_len) ? (uint32_t)RTPS_CDR_NOT_DATA
+                                      : nest_decode(s_ops, s_match, s_zero, N.n_ops, a.arena + vb, len, id1 != 0, row);
+        if (st != RTPS_CDR_OK) zero_row(row, N.row_bytes);
+      }
+    }
+    a.row_status[r] = (uint8_t)st;
+  }
+}
+
 }  // namespace
+
+bool rtps_cdr_is_composite(const rtps_cdr_op* prog, uint32_t n_ops) {
+  for (uint32_t k = 0; k < n_ops; ++k)
+    if (prog[k].kind == RTPS_CDR_SEQ_BEGIN || prog[k].kind == RTPS_CDR_ARRAY_BEGIN || prog[k].kind == RTPS_CDR_END)
+      return true;
+  return false;
+}
+
+bool rtps_cdr_build_nested(const rtps_cdr_op* prog, uint32_t n_ops, uint32_t row_bytes, CdrNest& N) {
+  if (n_ops > RTPS_CDR_MAX_OPS) return false;
+  memset(&N, 0, sizeof(N));
+  // open containers: the row, then one per open BEGIN (its element)
+  struct Box { uint32_t begin, limit; uint64_t min_wire; };
+  Box box[RTPS_CDR_MAX_DEPTH + 1];
+  uint32_t iv_lo[RTPS_CDR_MAX_OPS], iv_hi[RTPS_CDR_MAX_OPS];
+  uint32_t n_iv = 0, depth = 0;
+  box[0] = Box{0u, row_bytes, 0u};
+  auto close_box = [&](uint32_t from) -> bool {  // sibling slots of the box: no overlap
+    for (uint32_t i = from; i < n_iv; ++i)
+      for (uint32_t j = i + 1; j < n_iv; ++j)
+        if (iv_lo[i] < iv_hi[j] && iv_lo[j] < iv_hi[i]) return false;
+    return true;
+  };
+  uint32_t box_first[RTPS_CDR_MAX_DEPTH + 1] = {0};
+  for (uint32_t k = 0; k < n_ops; ++k) {
+    const rtps_cdr_op& op = prog[k];
+    const uint64_t sz = op.size, cnt = op.count;
+    const bool pow2 = sz == 1 || sz == 2 || sz == 4 || sz == 8;
+    uint64_t slot = 0, wire = 0;
+    switch (op.kind) {
+      case RTPS_CDR_PRIM: if (!pow2) return false; slot = (sz + 3) / 4 * 4; wire = sz; break;
+      case RTPS_CDR_BOOL: slot = 4; wire = 1; break;
+      case RTPS_CDR_STRING: slot = 4 + (cnt + 3) / 4 * 4; wire = 4; break;
+      case RTPS_CDR_SEQ: if (!pow2) return false; slot = 4 + (sz * cnt + 3) / 4 * 4; wire = 4; break;
+      case RTPS_CDR_ARRAY: if (!pow2) return false; slot = (sz * cnt + 3) / 4 * 4; wire = sz * cnt; break;
+      case RTPS_CDR_SEQ_BEGIN:
+      case RTPS_CDR_ARRAY_BEGIN:
+        if (op.stride < 4 || (op.stride & 3u) || depth >= RTPS_CDR_MAX_DEPTH) return false;
+        slot = (op.kind == RTPS_CDR_SEQ_BEGIN ? 4u : 0u) + cnt * op.stride;
+        break;
+      case RTPS_CDR_END: {
+        if (depth == 0) return false;
+        Box& b = box[depth];
+        if (!close_box(box_first[depth])) return false;
+        n_iv = box_first[depth];
+        const rtps_cdr_op& bo = prog[b.begin];
+        N.match[b.begin] = (uint8_t)k;
+        N.match[k] = (uint8_t)b.begin;
+        N.zero_el[b.begin] = b.min_wire == 0;
+        depth--;
+        box[depth].min_wire += bo.kind == RTPS_CDR_SEQ_BEGIN ? 4u : b.min_wire * bo.count;
+        N.ops[k] = op;
+        continue;
+      }
+      default: return false;
+    }
+    if ((op.out_off & 3u) || (uint64_t)op.out_off + slot > box[depth].limit) return false;
+    iv_lo[n_iv] = op.out_off;
+    iv_hi[n_iv] = (uint32_t)(op.out_off + slot);
+    n_iv++;
+    box[depth].min_wire += wire;
+    N.ops[k] = op;
+    if (op.kind == RTPS_CDR_SEQ_BEGIN || op.kind == RTPS_CDR_ARRAY_BEGIN) {
+      depth++;
+      box[depth] = Box{k, op.stride, 0u};
+      box_first[depth] = n_iv;
+    }
+  }
+  if (depth != 0 || !close_box(0)) return false;
+  N.n_ops = n_ops;
+  N.row_bytes = row_bytes;
+  return true;
+}
+
+int rtps_cdr_launch_nested(hipStream_t s, const CdrNest& N, const CdrArgs& a, uint32_t max_blocks) {
+  const uint64_t rows = a.list ? a.max_list : a.max_records;
+  uint64_t blocks = (rows + 255) / 256;
+  if (blocks > max_blocks) blocks = max_blocks;
+  if (blocks == 0) return 0;
+  hipLaunchKernelGGL(cdr_nested_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, N, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 static uint32_t slot_dwords(const rtps_cdr_op& op) {
   const uint64_t sz = op.size;

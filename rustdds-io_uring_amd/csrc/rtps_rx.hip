@@ -2084,19 +2084,39 @@ static int cdr_prog(const rtps_cdr_op* prog, uint32_t n_ops, uint32_t row_bytes,
   return rtps_cdr_build_slots(P) ? RTPS_RX_OK : RTPS_RX_EINVAL;
 }
 
+// Validates the program and launches the decode: the slot-parallel kernel for flat
+// programs, the lane-per-row one for composite programs (SEQ_BEGIN / ARRAY_BEGIN).
+static int cdr_run(rtps_rx_ctx* c, const rtps_cdr_op* prog, uint32_t n_ops, uint32_t row_bytes, const CdrArgs& a) {
+  (void)hipSetDevice(c->device);
+  if (rtps_cdr_is_composite(prog, n_ops)) {
+    CdrNest N;
+    if (!rtps_cdr_build_nested(prog, n_ops, row_bytes, N)) return RTPS_RX_EINVAL;
+    return rtps_cdr_launch_nested(c->stream, N, a, c->resident_blocks) == 0 ? RTPS_RX_OK : RTPS_RX_EHIP;
+  }
+  CdrProg P;
+  const int rc = cdr_prog(prog, n_ops, row_bytes, P);
+  if (rc) return rc;
+  return rtps_cdr_launch(c->stream, P, a, c->resident_blocks) == 0 ? RTPS_RX_OK : RTPS_RX_EHIP;
+}
+static bool cdr_prog_ok(const rtps_cdr_op* prog, uint32_t n_ops, uint32_t row_bytes) {
+  if (!prog || n_ops > RTPS_CDR_MAX_OPS || row_bytes == 0 || (row_bytes & 3u) || row_bytes > (1u << 20)) return false;
+  if (rtps_cdr_is_composite(prog, n_ops)) {
+    CdrNest N;
+    return rtps_cdr_build_nested(prog, n_ops, row_bytes, N);
+  }
+  CdrProg P;
+  return cdr_prog(prog, n_ops, row_bytes, P) == RTPS_RX_OK;
+}
+
 int rtps_rx_cdr_decode(rtps_rx_ctx* c, const rtps_cdr_op* prog, uint32_t n_ops, uint32_t row_bytes,
                        const uint8_t* arena, uint64_t arena_len, const uint64_t* dgram_off,
                        const rtps_record* records, const uint64_t* n_records, uint64_t max_records,
                        uint8_t* rows, uint8_t* row_status) {
-  if (!c) return RTPS_RX_EINVAL;
-  CdrProg P;
-  const int rc = cdr_prog(prog, n_ops, row_bytes, P);
-  if (rc) return rc;
+  if (!c || !cdr_prog_ok(prog, n_ops, row_bytes)) return RTPS_RX_EINVAL;
   if (!records || !n_records || (max_records && (!arena || !dgram_off || !rows || !row_status))) return RTPS_RX_EINVAL;
   if (max_records == 0) return RTPS_RX_OK;
-  (void)hipSetDevice(c->device);
   CdrArgs a{arena, arena_len, dgram_off, records, n_records, max_records, rows, row_status, nullptr, 0, nullptr, 0};
-  return rtps_cdr_launch(c->stream, P, a, c->resident_blocks) == 0 ? RTPS_RX_OK : RTPS_RX_EHIP;
+  return cdr_run(c, prog, n_ops, row_bytes, a);
 }
 
 int rtps_rx_cdr_decode_list(rtps_rx_ctx* c, const rtps_cdr_op* prog, uint32_t n_ops, uint32_t row_bytes,
@@ -2104,17 +2124,13 @@ int rtps_rx_cdr_decode_list(rtps_rx_ctx* c, const rtps_cdr_op* prog, uint32_t n_
                             const rtps_record* records, const uint64_t* n_records, uint64_t max_records,
                             const void* list, uint32_t list_stride, const uint64_t* n_list, uint64_t max_list,
                             uint8_t* rows, uint8_t* row_status) {
-  if (!c) return RTPS_RX_EINVAL;
-  CdrProg P;
-  const int rc = cdr_prog(prog, n_ops, row_bytes, P);
-  if (rc) return rc;
+  if (!c || !cdr_prog_ok(prog, n_ops, row_bytes)) return RTPS_RX_EINVAL;
   if (!records || !n_records || !n_list || list_stride < 4 || (list_stride & 3u)) return RTPS_RX_EINVAL;
   if (max_list && (!list || !arena || !dgram_off || !rows || !row_status)) return RTPS_RX_EINVAL;
   if (max_list == 0) return RTPS_RX_OK;
-  (void)hipSetDevice(c->device);
   CdrArgs a{arena, arena_len, dgram_off, records, n_records, max_records, rows, row_status,
             static_cast<const uint8_t*>(list), list_stride, n_list, max_list};
-  return rtps_cdr_launch(c->stream, P, a, c->resident_blocks) == 0 ? RTPS_RX_OK : RTPS_RX_EHIP;
+  return cdr_run(c, prog, n_ops, row_bytes, a);
 }
 
 /* DataFrag reassembly (rtps_frag.hip) */

@@ -10,20 +10,28 @@ a parsed batch, plus the numpy dtype of the fixed-layout output row.
 
     ShapeType = CdrType([("color", String(128)), ("x", "i32"), ("y", "i32"), ("shapesize", "i32")])
 
-Field specs: a primitive name (PRIMS), "bool", String(cap), Seq(prim, cap),
-Array(prim, n) or a nested CdrType (flattened: classic CDR aligns each
+Field specs: a primitive name (PRIMS), "bool", String(cap), Seq(elem, cap),
+Array(elem, n) or a nested CdrType (flattened: classic CDR aligns each
 primitive to its own size from the start of the value, so nesting adds no
-padding of its own).
+padding of its own).  A Seq / Array element is a primitive name (one SEQ /
+ARRAY op) or any other spec -- String, Seq, Array, CdrType -- which becomes a
+SEQ_BEGIN / ARRAY_BEGIN op, the element's own program and an END op (serde's
+Vec<T> / [T; N] of strings, structs or sequences):
+
+    Polygon = CdrType([("name", String(16)), ("pts", Seq(CdrType([("x", "f32"), ("y", "f32")]), 8)),
+                       ("tags", Seq(String(12), 4))])
 """
 import numpy as np
 
 OP_PRIM, OP_BOOL, OP_STRING, OP_SEQ, OP_ARRAY = 1, 2, 3, 4, 5
+OP_SEQ_BEGIN, OP_ARRAY_BEGIN, OP_END = 6, 7, 8
 CDR_OK, CDR_NOT_DATA, CDR_BAD_ENCODING, CDR_EOF, CDR_BAD_BOOL, CDR_BAD_UTF8, CDR_TOO_LONG = range(7)
 CDR_STATUS_NAMES = {0: "OK", 1: "NOT_DATA", 2: "BAD_ENCODING", 3: "EOF", 4: "BAD_BOOL", 5: "BAD_UTF8",
                     6: "TOO_LONG"}
 MAX_OPS = 64
+MAX_DEPTH = 4  # RTPS_CDR_MAX_DEPTH
 
-OP_DTYPE = np.dtype([("kind", "u1"), ("size", "u1"), ("_r", "<u2"), ("count", "<u4"), ("out_off", "<u4")])
+OP_DTYPE = np.dtype([("kind", "u1"), ("size", "u1"), ("stride", "<u2"), ("count", "<u4"), ("out_off", "<u4")])
 assert OP_DTYPE.itemsize == 12
 
 # serde primitive -> numpy type.  (Rust `char` is a 4-byte code point in
@@ -37,16 +45,28 @@ class String:
         self.cap = int(cap)
 
 
-class Seq:
-    def __init__(self, prim, cap):
-        assert prim in PRIMS
-        self.prim, self.cap = prim, int(cap)
+class _Composite:
+    """Seq / Array: element `elem` (a primitive name or any other field spec)."""
+
+    def __init__(self, elem, count):
+        self.elem = elem
+        self.prim = elem if isinstance(elem, str) and elem in PRIMS else None
+        if self.prim is None:
+            # a bare element spec is wrapped in a one-field struct "v" (unwrapped by to_python)
+            self.wrapped = not isinstance(elem, CdrType)
+            self.elem_type = CdrType([("v", elem)]) if self.wrapped else elem
 
 
-class Array:
-    def __init__(self, prim, n):
-        assert prim in PRIMS
-        self.prim, self.n = prim, int(n)
+class Seq(_Composite):
+    def __init__(self, elem, cap):
+        super().__init__(elem, cap)
+        self.cap = int(cap)
+
+
+class Array(_Composite):
+    def __init__(self, elem, n):
+        super().__init__(elem, n)
+        self.n = int(n)
 
 
 def _align(x, a):
@@ -60,6 +80,7 @@ class CdrType:
         self.fields = list(fields)
         ops, names, formats, offsets = [], [], [], []
         self._layout = []  # (name, kind, spec) in program order, for encoders/decoders
+        self.depth = 0     # SEQ_BEGIN / ARRAY_BEGIN nesting
         pos = 0
 
         def add(name, spec):
@@ -77,6 +98,24 @@ class CdrType:
             elif isinstance(spec, String):
                 kind, size, count, slot = OP_STRING, 1, spec.cap, 4 + _align(spec.cap, 4)
                 fmt = np.dtype([("len", "<u4")] + ([("data", f"S{_align(spec.cap, 4)}")] if spec.cap else []))
+            elif isinstance(spec, (Seq, Array)) and spec.prim is None:
+                et = spec.elem_type
+                seq = isinstance(spec, Seq)
+                count = spec.cap if seq else spec.n
+                if et.row_bytes > 0xFFFF or et.depth + 1 > MAX_DEPTH:
+                    raise ValueError(f"{name}: element too large or nested too deep")
+                hdr = 4 if seq else 0
+                fmt = np.dtype(([("n", "<u4")] if seq else []) + [("data", et.row_dtype, (count,))])
+                ops.append((OP_SEQ_BEGIN if seq else OP_ARRAY_BEGIN, 0, et.row_bytes, count, pos))
+                ops.extend(tuple(o) for o in et.ops.tolist())
+                ops.append((OP_END, 0, 0, 0, 0))
+                self.depth = max(self.depth, et.depth + 1)
+                names.append(name)
+                formats.append(fmt)
+                offsets.append(pos)
+                self._layout.append((name, OP_SEQ_BEGIN if seq else OP_ARRAY_BEGIN, spec))
+                pos += hdr + count * et.row_bytes
+                return
             elif isinstance(spec, Seq):
                 dt = np.dtype(PRIMS[spec.prim])
                 kind, size, count, slot = OP_SEQ, dt.itemsize, spec.cap, 4 + _align(dt.itemsize * spec.cap, 4)
@@ -120,6 +159,10 @@ class CdrType:
                 out[name] = v.tobytes()[4:4 + int(v["len"])].decode()
             elif kind == OP_SEQ:
                 out[name] = v["data"][: int(v["n"])].tolist() if spec.cap else []
+            elif kind in (OP_SEQ_BEGIN, OP_ARRAY_BEGIN):
+                et = spec.elem_type
+                els = v["data"][: int(v["n"])] if kind == OP_SEQ_BEGIN else v["data"]
+                out[name] = [et.to_python(e)["v"] if spec.wrapped else et.to_python(e) for e in els]
             elif kind == OP_ARRAY:
                 out[name] = v.tolist()
             elif kind == OP_BOOL:

@@ -30,9 +30,14 @@ def _pad(buf, a):
 
 
 def serialize(t, values, le=True):
-    """values: {flat field name: value} for CdrType t -> CDR value bytes (no encapsulation header)."""
-    e = "<" if le else ">"
+    """values: {flat field name: value} for CdrType t -> CDR value bytes (no encapsulation header).
+    A composite Seq / Array value is a list of element values (dicts for struct elements)."""
     buf = bytearray()
+    _ser(t, values, "<" if le else ">", buf)
+    return bytes(buf)
+
+
+def _ser(t, values, e, buf):
     for name, kind, spec in t._layout:
         v = values[name]
         if kind == cdr.OP_PRIM:
@@ -57,7 +62,12 @@ def serialize(t, values, le=True):
             if spec.n:
                 _pad(buf, struct.calcsize(f))
                 buf += struct.pack(e + f * spec.n, *v)
-    return bytes(buf)
+        elif kind in (cdr.OP_SEQ_BEGIN, cdr.OP_ARRAY_BEGIN):
+            if kind == cdr.OP_SEQ_BEGIN:  # serde serialize_seq: u32 length, then the elements
+                _pad(buf, 4)
+                buf += struct.pack(e + "I", len(v))
+            for x in v:
+                _ser(spec.elem_type, {"v": x} if spec.wrapped else x, e, buf)
 
 
 def payload(t, values, le=True, rep=None):
@@ -76,86 +86,164 @@ def _utf8_ok(b):
     return True
 
 
+def min_wire(t):
+    """The fewest value bytes t can consume (0: it reads nothing, so it cannot fail)."""
+    m = 0
+    for _, kind, spec in t._layout:
+        if kind == cdr.OP_PRIM:
+            m += struct.calcsize(_FMT[spec])
+        elif kind == cdr.OP_BOOL:
+            m += 1
+        elif kind in (cdr.OP_STRING, cdr.OP_SEQ, cdr.OP_SEQ_BEGIN):
+            m += 4
+        elif kind == cdr.OP_ARRAY:
+            m += spec.n * struct.calcsize(_FMT[spec.prim])
+        elif kind == cdr.OP_ARRAY_BEGIN:
+            m += spec.n * min_wire(spec.elem_type)
+    return m
+
+
+class _Fail(Exception):
+    def __init__(self, st):
+        self.st = st
+
+
 def decode(t, value, le):
     """(status, {name: value}, expected row bytes) for value bytes (after the 4-byte header).
-    The row is built from raw (byte-swapped) element bytes, so floats compare bit-exactly."""
-    e = "<" if le else ">"
-    pos = 0
-    out = {}
+    The row is built from raw (byte-swapped) element bytes, so floats compare bit-exactly.
+    Composite sequences: the elements are read recursively; elements past the slot
+    (n > cap) are read but not stored, and the sequence is TOO_LONG after them (at once
+    when an element reads no bytes at all, as it cannot fail)."""
     row = bytearray(t.row_bytes)
+    cur = [0]
+    try:
+        out = _dec(t, bytes(value), "<" if le else ">", le, cur, row, 0, True)
+    except _Fail as f:
+        return f.st, None, bytes(t.row_bytes)
+    return cdr.CDR_OK, out, bytes(row)
+
+
+def _dec(t, value, e, le, cur, row, base, write):
     n = len(value)
+    out = {}
 
     def put(off, raw, sz):  # raw element bytes in wire order -> host (LE) order in the row
+        if not write:
+            return
         for k in range(0, len(raw), sz):
             el = raw[k:k + sz]
-            row[off + k:off + k + sz] = el if le else el[::-1]
+            row[base + off + k:base + off + k + sz] = el if le else el[::-1]
 
-    err = lambda st: (st, None, bytes(t.row_bytes))  # noqa: E731
-    for (name, kind, spec), op in zip(t._layout, t.ops):
-        o = int(op["out_off"])
+    def put_raw(off, raw):
+        if write:
+            row[base + off:base + off + len(raw)] = raw
+
+    def u32():
+        cur[0] += (-cur[0]) % 4
+        if cur[0] + 4 > n:
+            raise _Fail(cdr.CDR_EOF)
+        x = struct.unpack_from(e + "I", value, cur[0])[0]
+        cur[0] += 4
+        return x
+
+    off = 0
+    for name, kind, spec in t._layout:
+        o = off
         if kind in (cdr.OP_PRIM, cdr.OP_ARRAY):
             prim = spec if kind == cdr.OP_PRIM else spec.prim
             f = _FMT[prim]
             sz = struct.calcsize(f)
             cnt = 1 if kind == cdr.OP_PRIM else spec.n
+            off += _slot(kind, spec)
             if cnt == 0:
                 out[name] = []
                 continue
+            pos = cur[0]
             pad = (-pos) % sz
             if pos + pad + cnt * sz > n:
-                return err(cdr.CDR_EOF)
+                raise _Fail(cdr.CDR_EOF)
             pos += pad
             vals = list(struct.unpack_from(e + f * cnt, value, pos))
-            put(o, bytes(value[pos:pos + cnt * sz]), sz)
+            put(o, value[pos:pos + cnt * sz], sz)
             out[name] = vals[0] if kind == cdr.OP_PRIM else vals
-            pos += cnt * sz
+            cur[0] = pos + cnt * sz
         elif kind == cdr.OP_BOOL:
-            if pos + 1 > n:
-                return err(cdr.CDR_EOF)
-            if value[pos] > 1:
-                return err(cdr.CDR_BAD_BOOL)
-            out[name] = value[pos] == 1
-            row[o] = value[pos]
-            pos += 1
+            off += 4
+            if cur[0] + 1 > n:
+                raise _Fail(cdr.CDR_EOF)
+            if value[cur[0]] > 1:
+                raise _Fail(cdr.CDR_BAD_BOOL)
+            out[name] = value[cur[0]] == 1
+            put_raw(o, value[cur[0]:cur[0] + 1])
+            cur[0] += 1
         elif kind == cdr.OP_STRING:
-            pos += (-pos) % 4
-            if pos + 4 > n:
-                return err(cdr.CDR_EOF)
-            ln = struct.unpack_from(e + "I", value, pos)[0]
-            pos += 4
-            if pos + ln > n:
-                return err(cdr.CDR_EOF)
-            sb = bytes(value[pos:pos + max(ln - 1, 0)])
+            off += _slot(kind, spec)
+            ln = u32()
+            if cur[0] + ln > n:
+                raise _Fail(cdr.CDR_EOF)
+            sb = value[cur[0]:cur[0] + max(ln - 1, 0)]
             if not _utf8_ok(sb):
-                return err(cdr.CDR_BAD_UTF8)
+                raise _Fail(cdr.CDR_BAD_UTF8)
             if len(sb) > spec.cap:
-                return err(cdr.CDR_TOO_LONG)
+                raise _Fail(cdr.CDR_TOO_LONG)
             out[name] = sb.decode()
-            row[o:o + 4] = struct.pack("<I", len(sb))
-            row[o + 4:o + 4 + len(sb)] = sb
-            pos += ln
+            put_raw(o, struct.pack("<I", len(sb)) + sb)
+            cur[0] += ln
         elif kind == cdr.OP_SEQ:
+            off += _slot(kind, spec)
             f = _FMT[spec.prim]
             sz = struct.calcsize(f)
-            pos += (-pos) % 4
-            if pos + 4 > n:
-                return err(cdr.CDR_EOF)
-            cnt = struct.unpack_from(e + "I", value, pos)[0]
-            pos += 4
+            cnt = u32()
             vals = []
             if cnt:
-                pad = (-pos) % sz
-                if pos + pad + cnt * sz > n:
-                    return err(cdr.CDR_EOF)
+                pad = (-cur[0]) % sz
+                if cur[0] + pad + cnt * sz > n:
+                    raise _Fail(cdr.CDR_EOF)
                 if cnt > spec.cap:
-                    return err(cdr.CDR_TOO_LONG)
-                pos += pad
-                vals = list(struct.unpack_from(e + f * cnt, value, pos))
-                put(o + 4, bytes(value[pos:pos + cnt * sz]), sz)
-                pos += cnt * sz
-            row[o:o + 4] = struct.pack("<I", cnt)
+                    raise _Fail(cdr.CDR_TOO_LONG)
+                cur[0] += pad
+                vals = list(struct.unpack_from(e + f * cnt, value, cur[0]))
+                put(o + 4, value[cur[0]:cur[0] + cnt * sz], sz)
+                cur[0] += cnt * sz
+            put_raw(o, struct.pack("<I", cnt))
             out[name] = vals
-    return cdr.CDR_OK, out, bytes(row)
+        elif kind in (cdr.OP_SEQ_BEGIN, cdr.OP_ARRAY_BEGIN):
+            off += _slot(kind, spec)
+            et = spec.elem_type
+            seq = kind == cdr.OP_SEQ_BEGIN
+            cap = spec.cap if seq else spec.n
+            cnt = u32() if seq else cap
+            if seq:
+                put_raw(o, struct.pack("<I", cnt))
+            if cnt > cap and min_wire(et) == 0:
+                raise _Fail(cdr.CDR_TOO_LONG)
+            els = []
+            for i in range(cnt):
+                x = _dec(et, value, e, le, cur, row, base + o + (4 if seq else 0) + i * et.row_bytes,
+                         write and i < cap)
+                els.append(x["v"] if spec.wrapped else x)
+            if cnt > cap:
+                raise _Fail(cdr.CDR_TOO_LONG)
+            out[name] = els
+    return out
+
+
+def _slot(kind, spec):
+    """Row bytes of one field's slot (include/rtps_rx.h row layout)."""
+    a4 = lambda x: (x + 3) // 4 * 4  # noqa: E731
+    if kind == cdr.OP_PRIM:
+        return a4(struct.calcsize(_FMT[spec]))
+    if kind == cdr.OP_BOOL:
+        return 4
+    if kind == cdr.OP_STRING:
+        return 4 + a4(spec.cap)
+    if kind == cdr.OP_SEQ:
+        return 4 + a4(struct.calcsize(_FMT[spec.prim]) * spec.cap)
+    if kind == cdr.OP_ARRAY:
+        return a4(struct.calcsize(_FMT[spec.prim]) * spec.n)
+    if kind == cdr.OP_SEQ_BEGIN:
+        return 4 + spec.cap * spec.elem_type.row_bytes
+    return spec.n * spec.elem_type.row_bytes
 
 
 def expected_rows(t, arena, offs, recs):
@@ -213,7 +301,15 @@ def random_values(t, rng, str_alphabet=("a", "Z", "0", " ", "é", "ß", "€", "
             vals[name] = [_rand_prim(spec.prim, rng) for _ in range(int(rng.integers(0, spec.cap + 1)))]
         elif kind == cdr.OP_ARRAY:
             vals[name] = [_rand_prim(spec.prim, rng) for _ in range(spec.n)]
+        elif kind in (cdr.OP_SEQ_BEGIN, cdr.OP_ARRAY_BEGIN):
+            cnt = int(rng.integers(0, spec.cap + 1)) if kind == cdr.OP_SEQ_BEGIN else spec.n
+            vals[name] = [_rand_elem(spec, rng, str_alphabet) for _ in range(cnt)]
     return vals
+
+
+def _rand_elem(spec, rng, str_alphabet):
+    x = random_values(spec.elem_type, rng, str_alphabet)
+    return x["v"] if spec.wrapped else x
 
 
 def _rand_prim(p, rng):
@@ -255,6 +351,10 @@ def corpus(t, n, seed, prefix=bytes(range(1, 13)), le_only=False, clean=False):
         elif mode == 6 and cdr.OP_SEQ in has:     # more elements than the slot
             name, _, spec = next(x for x in t._layout if x[1] == cdr.OP_SEQ)
             vals[name] = [0] * (spec.cap + 1)
+        elif mode == 6 and cdr.OP_SEQ_BEGIN in has:
+            seqs = [x for x in t._layout if x[1] == cdr.OP_SEQ_BEGIN]
+            name, _, spec = seqs[int(rng.integers(0, len(seqs)))]
+            vals[name] = [_rand_elem(spec, rng, ("a", "é")) for _ in range(spec.cap + 1 + int(rng.integers(0, 3)))]
         elif mode == 7:
             rep = [REP_PL_CDR_BE, b"\x00\x06", b"\x01\x00", b"\x00\x0a"][int(rng.integers(0, 4))]
         elif mode == 8:
@@ -299,3 +399,13 @@ MIXED = cdr.CdrType([("id", "u8"), ("temp", "f64"), ("flag", "bool"), ("name", c
 # little-endian chunks copy it as one block (a "segment"), others field by field
 SEGS = cdr.CdrType([("a", "u64"), ("b", "f64"), ("c", cdr.Array("i32", 5)), ("d", "u32"), ("s", cdr.String(8)),
                     ("e", "u64"), ("f", cdr.Array("u16", 3))])
+
+
+# Composite elements: a polygon (sequence of structs, sequence of strings) and
+# deeper nesting (sequences of sequences, an array of structs holding a
+# sequence, strings three levels down)
+POLYGON = cdr.CdrType([("name", cdr.String(16)), ("pts", cdr.Seq(cdr.CdrType([("x", "f32"), ("y", "f32")]), 8)),
+                       ("tags", cdr.Seq(cdr.String(12), 4)), ("k", "u8")])
+NESTED = cdr.CdrType([("a", "u8"), ("m", cdr.Seq(cdr.Seq("u16", 3), 4)),
+                      ("grid", cdr.Array(cdr.CdrType([("id", "u8"), ("v", cdr.Seq("f64", 2)), ("ok", "bool")]), 3)),
+                      ("deep", cdr.Seq(cdr.Seq(cdr.Array(cdr.String(5), 2), 2), 2)), ("z", "i64")])

@@ -179,3 +179,78 @@ def test_list_decode_without_records(rx):
         torch.cuda.synchronize()
         assert (rst.cpu().numpy()[:64] == cdr.CDR_NOT_DATA).all(), label
         assert not rows.cpu().numpy().view(np.uint8).reshape(64, -1)[:64].any(), label
+
+
+@pytest.mark.parametrize("name", ["polygon", "nested"])
+def test_composite_list_parity(rx, name):
+    """Composite programs (lane-per-row kernel) in list mode: every DATA sample, then a
+    shuffled list with non-sample and out-of-range entries, against the oracle."""
+    t = TYPES[name]
+    dgrams = cdr_ref.corpus(t, 4000, seed=31)
+    arena, off, ln = oracle.pack(dgrams, align=1)
+    st, recs, _, _ = oracle.parse(arena, off, ln, threads=8)
+    o_rows, o_status = oracle.cdr_decode(t, arena, off, recs)
+    dev = torch.device("cuda", 0)
+    a_t = torch.from_numpy(arena).to(dev)
+    off_t = torch.from_numpy(off.view(np.int64)).to(dev)
+    ln_t = torch.from_numpy(ln.view(np.int32)).to(dev)
+    outs = rx.alloc_outputs(len(ln), max(len(recs), 1))
+    rx.parse_batch_device(a_t, off_t, ln_t, len(ln), outs)
+    rng = np.random.default_rng(3)
+    lst = np.concatenate([np.arange(len(recs)), [len(recs), 0xFFFFFFFF]]).astype(np.uint32)
+    rng.shuffle(lst)
+    l_t = torch.from_numpy(lst.view(np.int32)).to(dev)
+    n_t = torch.tensor([len(lst)], dtype=torch.int64, device=dev)
+    rows, rst = rx.alloc_rows(t, len(lst))
+    rx.cdr_decode_list(t, a_t, off_t, outs, l_t, 4, n_t, len(lst), rows, rst)
+    torch.cuda.synchronize()
+    rows = rows.cpu().numpy().view(np.uint8).reshape(-1, t.row_bytes)[:len(lst)]
+    rst = rst.cpu().numpy()[:len(lst)]
+    ok = lst < len(recs)
+    exp_st = np.full(len(lst), cdr.CDR_NOT_DATA, np.uint8)
+    exp_st[ok] = o_status[lst[ok]]
+    assert np.array_equal(rst, exp_st)
+    exp_rows = np.zeros((len(lst), t.row_bytes), np.uint8)
+    exp_rows[ok] = o_rows[lst[ok]]
+    assert np.array_equal(rows, exp_rows)
+    assert (o_status == cdr.CDR_OK).sum() > 500
+
+
+def test_bad_composite_program_rejected(rx):
+    """Host validation of composite programs: unmatched BEGIN / END, a stride that is not a
+    multiple of 4, an element slot past its stride, overlapping slots, depth > 4."""
+    import rtps_rx
+    dev = torch.device("cuda", 0)
+    outs = rx.alloc_outputs(1, 4)
+    arena = torch.zeros(64, dtype=torch.uint8, device=dev)
+    off = torch.zeros(1, dtype=torch.int64, device=dev)
+    good = cdr_ref.POLYGON
+    rows, st = rx.alloc_rows(good, 4)
+    rx.cdr_decode(good, arena, off, outs, rows, st)  # accepted as built
+    b = [int(k) for k in good.ops["kind"]].index(cdr.OP_SEQ_BEGIN)
+    e = [int(k) for k in good.ops["kind"]].index(cdr.OP_END)
+
+    def bad(edit):
+        t = cdr_ref.POLYGON
+        saved = t.ops
+        t.ops = t.ops.copy()
+        try:
+            edit(t.ops)
+            with pytest.raises(rtps_rx.RtpsRxError):
+                rx.cdr_decode(t, arena, off, outs, rows, st)
+        finally:
+            t.ops = saved
+    bad(lambda o: o.__setitem__(e, (cdr.OP_PRIM, 4, 0, 1, 0)))                       # BEGIN never closed
+    bad(lambda o: o.__setitem__(b, (cdr.OP_PRIM, 4, 0, 1, int(o[b]["out_off"]))))    # stray END
+    bad(lambda o: o["stride"].__setitem__(b, 6))                                       # stride % 4
+    bad(lambda o: o["out_off"].__setitem__(b + 2, 8))                                  # y past the 8-B element
+    bad(lambda o: o["out_off"].__setitem__(b + 2, 0))                                  # y over x
+    bad(lambda o: o["count"].__setitem__(b, 1 << 20))                                  # slot past the row
+    deep = cdr.CdrType([("d", cdr.Seq(cdr.Seq(cdr.Seq(cdr.Seq(cdr.String(1), 1), 1), 1), 1))])
+    r2, s2 = rx.alloc_rows(deep, 4)
+    rx.cdr_decode(deep, arena, off, outs, r2, s2)  # depth 4 accepted
+    ops = deep.ops.copy()
+    wrap = np.array([(cdr.OP_ARRAY_BEGIN, 0, deep.row_bytes, 1, 0)], dtype=cdr.OP_DTYPE)  # fits, but depth 5
+    deep.ops = np.concatenate([wrap, ops, ops[-1:]])
+    with pytest.raises(rtps_rx.RtpsRxError):
+        rx.cdr_decode(deep, arena, off, outs, r2, s2)

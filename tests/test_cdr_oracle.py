@@ -20,6 +20,9 @@ TYPES = {
                          ("v", cdr.Seq("i32", 0))]),
     "empty": cdr.CdrType([]),
     "segs": cdr_ref.SEGS,
+    # composite elements (SEQ_BEGIN / ARRAY_BEGIN ... END): parity unpinned (no reference vector)
+    "polygon": cdr_ref.POLYGON,
+    "nested": cdr_ref.NESTED,
 }
 
 
@@ -60,8 +63,9 @@ def test_oracle_matches_python_restatement(name):
 
 
 @pytest.mark.parametrize("le", [True, False])
-def test_round_trip(le):
-    t = cdr_ref.MIXED
+@pytest.mark.parametrize("name", ["mixed", "polygon", "nested"])
+def test_round_trip(le, name):
+    t = TYPES[name]
     rng = np.random.default_rng(7 + le)
     vals = [cdr_ref.random_values(t, rng) for _ in range(64)]
     dgrams = [cdr_ref.data_datagram(cdr_ref.payload(t, v, le), sn=i + 1) for i, v in enumerate(vals)]
@@ -75,8 +79,20 @@ def test_round_trip(le):
             want = v[k]
             if isinstance(want, float):
                 assert struct.pack("<d", got[k]) == struct.pack("<d", want) or got[k] == want, k
+            elif name != "mixed":  # composite values: float32 elements round-trip through f32
+                assert _approx(got[k], want), (k, got[k], want)
             else:
                 assert got[k] == (list(want) if isinstance(want, list) else want), (k, got[k], want)
+
+
+def _approx(a, b):
+    if isinstance(b, dict):
+        return a.keys() == b.keys() and all(_approx(a[k], b[k]) for k in b)
+    if isinstance(b, (list, tuple)):
+        return len(a) == len(b) and all(_approx(x, y) for x, y in zip(a, b))
+    if isinstance(b, float):
+        return float(np.float32(b)) == a or a == b
+    return a == b
 
 
 def _one(t, value, rep=cdr_ref.REP_CDR_LE):
@@ -124,3 +140,52 @@ def test_type_layout():
     assert cdr.ShapeType.row_bytes == 144
     with pytest.raises(ValueError):
         cdr.CdrType([(f"f{i}", "u8") for i in range(cdr.MAX_OPS + 1)])
+
+
+def test_composite_rules():
+    """Sequences / arrays of strings and structs (serde Vec<T> / [T; N] through cdr-encoding):
+    a u32 count aligned to 4, elements with no alignment of their own, each primitive
+    aligned to its size from the value start; TOO_LONG only after the elements validate."""
+    Tg = cdr.CdrType([("t", cdr.Seq(cdr.String(4), 2))])
+    s3 = lambda a, b, c: struct.pack("<I", 3) + b"".join(  # noqa: E731
+        struct.pack("<I", len(x) + 1) + x + b"\x00" + bytes((-(len(x) + 1)) % 4) for x in (a, b, c))
+    st, row = _one(Tg, struct.pack("<I", 2) + struct.pack("<I", 3) + b"ab\x00\x00" + struct.pack("<I", 1) + b"\x00")
+    assert st == cdr.CDR_OK and Tg.to_python(Tg.rows(row)[0]) == {"t": ["ab", ""]}
+    assert _one(Tg, s3(b"a", b"b", b"c"))[0] == cdr.CDR_TOO_LONG           # n = 3 > 2, all valid
+    assert _one(Tg, s3(b"a", b"b", b"\xff"))[0] == cdr.CDR_BAD_UTF8        # the element's own error first
+    assert _one(Tg, s3(b"a", b"b", b"c")[:-4])[0] == cdr.CDR_EOF
+    assert _one(Tg, s3(b"a", b"abcde", b"c"))[0] == cdr.CDR_TOO_LONG       # a string past its slot
+    # struct elements: u8 then f64 aligned to 8 from the value start
+    E = cdr.CdrType([("e", cdr.Seq(cdr.CdrType([("a", "u8"), ("b", "f64")]), 3)), ("z", "u16")])
+    v = struct.pack("<IB3xdB7xdH", 2, 7, 1.5, 9, -2.0, 5)
+    st, row = _one(E, v)
+    assert st == cdr.CDR_OK
+    assert E.to_python(E.rows(row)[0]) == {"e": [{"a": 7, "b": 1.5}, {"a": 9, "b": -2.0}], "z": 5}
+    # empty sequence of 8-aligned elements: no padding consumed
+    assert E.to_python(E.rows(_one(E, struct.pack("<IH", 0, 3))[1])[0]) == {"e": [], "z": 3}
+    # elements that read no bytes cannot fail: n > count is TOO_LONG at once (no 2^32 loop)
+    Z = cdr.CdrType([("q", cdr.Seq(cdr.Array("u32", 0), 3)), ("x", "u8")])
+    assert _one(Z, struct.pack("<IB", 0xFFFFFFFF, 1))[0] == cdr.CDR_TOO_LONG
+    st, row = _one(Z, struct.pack("<IB", 2, 1))
+    assert st == cdr.CDR_OK and Z.to_python(Z.rows(row)[0]) == {"q": [[], []], "x": 1}
+    # a huge count of non-empty elements ends at EOF after the bytes run out
+    assert _one(E, struct.pack("<I", 0xFFFFFFFF) + bytes(64))[0] == cdr.CDR_EOF
+    # arrays of structs: no count; nested sequences
+    A = cdr.CdrType([("p", cdr.Array(cdr.CdrType([("x", "i16"), ("ok", "bool")]), 2)),
+                     ("m", cdr.Seq(cdr.Seq("u16", 2), 2))])
+    v = struct.pack("<hBxhB", -3, 1, 4, 0) + bytes(1) + struct.pack("<IIHHIH", 2, 2, 10, 11, 1, 12)
+    st, row = _one(A, v)
+    assert st == cdr.CDR_OK, st
+    assert A.to_python(A.rows(row)[0]) == {"p": [{"x": -3, "ok": True}, {"x": 4, "ok": False}], "m": [[10, 11], [12]]}
+    assert _one(A, struct.pack("<hBxhB", -3, 2, 4, 0))[0] == cdr.CDR_BAD_BOOL
+
+
+def test_composite_layout():
+    t = cdr_ref.POLYGON
+    kinds = [int(k) for k in t.ops["kind"]]
+    assert kinds.count(cdr.OP_SEQ_BEGIN) == 2 and kinds.count(cdr.OP_END) == 2
+    b = kinds.index(cdr.OP_SEQ_BEGIN)
+    assert int(t.ops[b]["stride"]) == 8 and int(t.ops[b]["count"]) == 8
+    assert t.row_dtype.itemsize == t.row_bytes == t.row_dtype["pts"].itemsize + 20 + 4 + 4 * 16 + 4
+    with pytest.raises(ValueError):  # depth > RTPS_CDR_MAX_DEPTH
+        cdr.CdrType([("d", cdr.Seq(cdr.Seq(cdr.Seq(cdr.Seq(cdr.Seq(cdr.String(1), 1), 1), 1), 1), 1))])
