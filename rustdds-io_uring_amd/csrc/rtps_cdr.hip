@@ -482,10 +482,10 @@ __device__ __forceinline__ void copy_bytes(uint8_t* d, const uint8_t* s, uint32_
   for (; i + 4 <= m; i += 4) *(uint32_t*)(d + i) = *(const u32u*)(s + i);  // d is 4-aligned
   for (; i < m; ++i) d[i] = s[i];
 }
+// Open elements live in LDS, one 16-B frame per (depth, lane):
+// {n, i, elem0, base | begin << 24 | write << 31} (base, elem0 < 2^20: row offsets).
 __device__ uint8_t nest_decode(const rtps_cdr_op* ops, const uint8_t* match, const uint8_t* zero_el, uint32_t n_ops,
-                               const uint8_t* v, uint32_t len, bool le, uint8_t* row) {
-  struct Frame { uint32_t begin, n, i, elem0, base; bool write; };
-  Frame fr[RTPS_CDR_MAX_DEPTH];
+                               const uint8_t* v, uint32_t len, bool le, uint8_t* row, uint4* fr) {
   uint32_t depth = 0, base = 0, pos = 0;
   bool write = true;
   for (uint32_t k = 0; k < n_ops; ++k) {
@@ -557,24 +557,28 @@ __device__ uint8_t nest_decode(const rtps_cdr_op* ops, const uint8_t* match, con
         }
         if (n == 0) { k = match[k]; break; }
         if (n > op.count && zero_el[k]) return RTPS_CDR_TOO_LONG;
-        fr[depth] = Frame{k, n, 0u, base + op.out_off + (seq ? 4u : 0u), base, write};
-        base = fr[depth].elem0;
+        const uint32_t elem0 = base + op.out_off + (seq ? 4u : 0u);
+        fr[depth * 64u] = make_uint4(n, 0u, elem0, base | (k << 24) | (write ? 0x80000000u : 0u));
+        base = elem0;
         write = write && op.count > 0;
         depth++;
         break;
       }
       case RTPS_CDR_END: {
-        Frame& f = fr[depth - 1];
-        const rtps_cdr_op b = ops[f.begin];
-        if (++f.i < f.n) {
-          base = f.elem0 + f.i * b.stride;
-          write = f.write && f.i < b.count;
-          k = f.begin;  // ++k: the element's first op
+        uint4 f = fr[(depth - 1) * 64u];
+        const uint32_t begin = (f.w >> 24) & 63u;
+        const bool fw = (f.w >> 31) != 0;
+        const rtps_cdr_op b = ops[begin];
+        if (++f.y < f.x) {
+          fr[(depth - 1) * 64u].y = f.y;
+          base = f.z + f.y * b.stride;
+          write = fw && f.y < b.count;
+          k = begin;  // ++k: the element's first op
         } else {
           depth--;
-          base = f.base;
-          write = f.write;
-          if (f.n > b.count) return RTPS_CDR_TOO_LONG;
+          base = f.w & 0xfffffu;
+          write = fw;
+          if (f.x > b.count) return RTPS_CDR_TOO_LONG;
         }
         break;
       }
@@ -591,44 +595,89 @@ __device__ __forceinline__ void zero_row(uint8_t* r, uint32_t bytes) {
   for (; b < bytes; b += 4) *(uint32_t*)(r + b) = 0u;
 }
 
-__global__ __launch_bounds__(256) void cdr_nested_kernel(CdrNest N, CdrArgs a) {
+// One wave per chunk of 64 rows: lane = row.  The chunk's values (up to NEST_VCAP
+// bytes each) are staged in LDS by the whole wave (16-B loads, all in flight
+// together), so the lane-serial walk reads LDS, not HBM; longer values are read in
+// place.
+#ifndef CDR_NEST_VCAP
+#define CDR_NEST_VCAP 128  // LDS 49 KB per block: 3 blocks (12 waves) per CU
+#endif
+constexpr uint32_t NEST_WAVES = 4, NEST_VCAP = CDR_NEST_VCAP, NEST_VQ = NEST_VCAP / 16;
+__global__ __launch_bounds__(64 * NEST_WAVES) void cdr_nested_kernel(CdrNest N, CdrArgs a) {
   __shared__ rtps_cdr_op s_ops[RTPS_CDR_MAX_OPS];
   __shared__ uint8_t s_match[RTPS_CDR_MAX_OPS], s_zero[RTPS_CDR_MAX_OPS];
+  __shared__ uint4 s_val[NEST_WAVES][64][NEST_VQ];
+  __shared__ uint4 s_fr[NEST_WAVES][RTPS_CDR_MAX_DEPTH * 64];
+  __shared__ uint64_t s_vb[NEST_WAVES][64];
+  __shared__ uint32_t s_len[NEST_WAVES][64];
   if (threadIdx.x < N.n_ops) {
     s_ops[threadIdx.x] = N.ops[threadIdx.x];
     s_match[threadIdx.x] = N.match[threadIdx.x];
     s_zero[threadIdx.x] = N.zero_el[threadIdx.x];
   }
   __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t n = a.list ? min(*a.n_list, a.max_list) : min(*a.n_records, a.max_records);
   const uint64_t nrec = min(*a.n_records, a.max_records);
-  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t ri = a.list ? *reinterpret_cast<const uint32_t*>(a.list + r * a.list_stride) : r;
-    uint8_t* row = a.rows + r * N.row_bytes;
-    zero_row(row, N.row_bytes);
-    uint32_t st;
-    if (ri >= nrec) {
-      st = RTPS_CDR_NOT_DATA;
-    } else {
-      const uint8_t* rec = (const uint8_t*)(a.records + ri);
-      const uint4 h0 = *(const uint4*)rec, h1 = *(const uint4*)(rec + 16);
-      const uint2 u0 = *(const uint2*)(rec + 40);
-      const uint32_t kind = (h0.y >> 16) & 0xff, pk = h1.w >> 24;
-      const uint32_t pl_off = u0.x & 0xffff, pl_len = u0.x >> 16;
-      const uint32_t id0 = u0.y & 0xff, id1 = (u0.y >> 8) & 0xff;
-      if (kind != RTPS_DATA || pk != RTPS_PK_DATA || pl_len < 4) {
-        st = RTPS_CDR_NOT_DATA;
-      } else if (id0 != 0 || (id1 != 0 && id1 != 1 && id1 != 3)) {
-        st = RTPS_CDR_BAD_ENCODING;
-      } else {
-        const uint64_t vb = a.dgram_off[h0.x] + pl_off + 4;
-        const uint32_t len = pl_len - 4;
-        st = (vb + len > a.arena_len) ? (uint32_t)RTPS_CDR_NOT_DATA
-                                      : nest_decode(s_ops, s_match, s_zero, N.n_ops, a.arena + vb, len, id1 != 0, row);
-        if (st != RTPS_CDR_OK) zero_row(row, N.row_bytes);
+  const uint64_t chunks = (n + 63) / 64;
+  for (uint64_t c = (uint64_t)blockIdx.x * NEST_WAVES + wave; c < chunks; c += (uint64_t)gridDim.x * NEST_WAVES) {
+    const uint64_t r = c * 64 + lane;
+    uint32_t st = RTPS_CDR_NOT_DATA, len = 0;
+    uint64_t vb = 0;
+    bool le = true;
+    if (r < n) {
+      const uint64_t ri = a.list ? *reinterpret_cast<const uint32_t*>(a.list + r * a.list_stride) : r;
+      if (ri < nrec) {
+        const uint8_t* rec = (const uint8_t*)(a.records + ri);
+        const uint4 h0 = *(const uint4*)rec, h1 = *(const uint4*)(rec + 16);
+        const uint2 u0 = *(const uint2*)(rec + 40);
+        const uint32_t kind = (h0.y >> 16) & 0xff, pk = h1.w >> 24;
+        const uint32_t pl_off = u0.x & 0xffff, pl_len = u0.x >> 16;
+        const uint32_t id0 = u0.y & 0xff, id1 = (u0.y >> 8) & 0xff;
+        if (kind != RTPS_DATA || pk != RTPS_PK_DATA || pl_len < 4) {
+          st = RTPS_CDR_NOT_DATA;
+        } else if (id0 != 0 || (id1 != 0 && id1 != 1 && id1 != 3)) {
+          st = RTPS_CDR_BAD_ENCODING;
+        } else {
+          vb = a.dgram_off[h0.x] + pl_off + 4;
+          len = pl_len - 4;
+          le = id1 != 0;
+          st = vb + len > a.arena_len ? (uint32_t)RTPS_CDR_NOT_DATA : 0xffu;  // 0xff: decode
+        }
       }
     }
-    a.row_status[r] = (uint8_t)st;
+    s_vb[wave][lane] = vb;
+    s_len[wave][lane] = (st == 0xffu && len <= NEST_VCAP) ? len : 0u;
+    wave_sync();
+#pragma unroll 8
+    for (uint32_t k = 0; k < NEST_VQ; ++k) {  // unit u: row u / NEST_VQ, quad u % NEST_VQ
+      const uint32_t u = k * 64u + lane, rw = u / NEST_VQ, q = u % NEST_VQ;
+      const uint32_t L = s_len[wave][rw];
+      if (16u * q < L) {
+        const uint64_t abs = s_vb[wave][rw] + 16u * q;
+        uint4 x;
+        if (abs + 16 <= a.arena_len) {
+          x = ld16u(a.arena + abs);
+        } else {  // the arena's last bytes
+          uint32_t w[4] = {0u, 0u, 0u, 0u};
+          for (uint32_t b = 0; b < 16 && abs + b < a.arena_len; ++b) w[b >> 2] |= (uint32_t)a.arena[abs + b] << (8 * (b & 3));
+          x = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+        s_val[wave][rw][q] = x;
+      }
+    }
+    wave_sync();
+    if (r < n) {
+      uint8_t* row = a.rows + r * N.row_bytes;
+      zero_row(row, N.row_bytes);
+      if (st == 0xffu) {
+        const uint8_t* v = len <= NEST_VCAP ? (const uint8_t*)&s_val[wave][lane][0] : a.arena + vb;
+        st = nest_decode(s_ops, s_match, s_zero, N.n_ops, v, len, le, row, &s_fr[wave][lane]);
+        if (st != RTPS_CDR_OK) zero_row(row, N.row_bytes);
+      }
+      a.row_status[r] = (uint8_t)st;
+    }
+    wave_sync();  // s_val / s_len are reused by the wave's next chunk
   }
 }
 
@@ -709,10 +758,10 @@ bool rtps_cdr_build_nested(const rtps_cdr_op* prog, uint32_t n_ops, uint32_t row
 
 int rtps_cdr_launch_nested(hipStream_t s, const CdrNest& N, const CdrArgs& a, uint32_t max_blocks) {
   const uint64_t rows = a.list ? a.max_list : a.max_records;
-  uint64_t blocks = (rows + 255) / 256;
+  uint64_t blocks = (rows + 64 * NEST_WAVES - 1) / (64 * NEST_WAVES);
   if (blocks > max_blocks) blocks = max_blocks;
   if (blocks == 0) return 0;
-  hipLaunchKernelGGL(cdr_nested_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, N, a);
+  hipLaunchKernelGGL(cdr_nested_kernel, dim3((uint32_t)blocks), dim3(64 * NEST_WAVES), 0, s, N, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
