@@ -5,11 +5,14 @@
 //   -> CDRDeserializerAdapter (REPR_IDS)     serialization/cdr_adapters.rs:96-100
 //   -> deserialize_from_cdr_with_decoder_and_rep_id   cdr_adapters.rs:246-275
 //   -> cdr_encoding::CdrDeserializer         (external crate cdr-encoding 0.10)
-// The sample type is a flat program of ops (rtps_cdr_op), wave-uniform (a
-// kernel argument).  A wave takes 64 records: each lane validates one record
-// and leaves its per-op data offsets in LDS; then the whole wave writes the 64
-// rows slot by slot, one 4-byte word per lane, so row stores are coalesced and
-// every row byte is written once (failed rows as zeros).
+// The sample type is a program of ops (rtps_cdr_op), wave-uniform (a kernel
+// argument).  Flat programs (cdr_decode_kernel): a wave takes 64 records, each
+// lane validates one record and leaves its per-op data offsets in LDS, then the
+// whole wave writes the 64 rows slot by slot, one 4-byte word per lane, so row
+// stores are coalesced and every row byte is written once (failed rows as
+// zeros).  Composite programs (SEQ_BEGIN / ARRAY_BEGIN ... END, whose element
+// offsets differ per record: cdr_nested_kernel): lane = row, the values staged in
+// LDS by the wave, the open elements as LDS frames.
 //
 // Roofline: HBM-bound.  Algorithmic bytes per record = 40 B of the record +
 // the value bytes a decoded row consumes + row_bytes + 1 status byte written.
@@ -47,7 +50,10 @@ __device__ __forceinline__ void store_prim(uint8_t* d, uint64_t x, uint32_t size
   }
 }
 
-// std::str::from_utf8 acceptance over m bytes.
+// std::str::from_utf8 acceptance over m bytes.  A multi-byte character is
+// checked with selects (its lead's class and the allowed range of its first
+// continuation byte), not a branch per lead class: lanes that validate different
+// characters then run the same instructions.
 __device__ bool utf8_ok(const uint8_t* s, uint32_t m) {
   uint32_t i = 0;
   while (i < m) {
@@ -56,20 +62,17 @@ __device__ bool utf8_ok(const uint8_t* s, uint32_t m) {
       uint32_t w = *(const u32u*)(s + i);
       if ((w & 0x80808080u) == 0) { i += 4; continue; }
     }
-    uint32_t c = s[i];
+    const uint32_t c = s[i];
     if (c < 0x80) { i++; continue; }
-    uint32_t need, lo = 0x80, hi = 0xBF;
-    if (c >= 0xC2 && c <= 0xDF) need = 1;
-    else if (c >= 0xE0 && c <= 0xEF) { need = 2; lo = (c == 0xE0) ? 0xA0 : 0x80; hi = (c == 0xED) ? 0x9F : 0xBF; }
-    else if (c >= 0xF0 && c <= 0xF4) { need = 3; lo = (c == 0xF0) ? 0x90 : 0x80; hi = (c == 0xF4) ? 0x8F : 0xBF; }
-    else return false;
-    if (i + need >= m) return false;
-    uint32_t b1 = s[i + 1];
-    if (b1 < lo || b1 > hi) return false;
-    for (uint32_t k = 2; k <= need; ++k) {
-      uint32_t b = s[i + k];
-      if (b < 0x80 || b > 0xBF) return false;
-    }
+    // C2..DF: 1 continuation, E0..EF: 2, F0..F4: 3; E0 / ED / F0 / F4 narrow the first one
+    const uint32_t need = c >= 0xF0 ? 3u : (c >= 0xE0 ? 2u : 1u);
+    const uint32_t lo = c == 0xE0 ? 0xA0u : (c == 0xF0 ? 0x90u : 0x80u);
+    const uint32_t hi = c == 0xED ? 0x9Fu : (c == 0xF4 ? 0x8Fu : 0xBFu);
+    if (c < 0xC2 || c > 0xF4 || i + need >= m) return false;
+    const uint32_t b1 = s[i + 1];
+    const uint32_t b2 = s[i + (need >= 2 ? 2u : 1u)], b3 = s[i + need];  // (re-read b1 / b2 when shorter)
+    const bool cont = ((b2 & 0xC0u) == 0x80u) & ((b3 & 0xC0u) == 0x80u);
+    if (b1 < lo || b1 > hi || !cont) return false;
     i += need + 1;
   }
   return true;

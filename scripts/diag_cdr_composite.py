@@ -2,6 +2,7 @@
 clean little-endian samples of tests/cdr_ref.py's POLYGON and NESTED types, 8 copies
 of 65,536 distinct datagrams, parsed once on the GPU, then rtps_rx_cdr_decode timed
 with HIP events on the receiver's stream.  Checks a sample of rows against the oracle.
+--ascii: strings of ASCII characters only.
 Algorithmic bytes per decoded row: 40 B of the record + the value bytes + row_bytes
 + 1 status byte."""
 import os
@@ -18,6 +19,8 @@ import oracle  # noqa: E402
 import rtps_rx  # noqa: E402
 
 dev = torch.device("cuda", 0)
+if "--ascii" in sys.argv:  # ASCII-only strings (the default alphabet has 2-4-byte UTF-8 characters)
+    cdr_ref.random_values.__defaults__ = (("a", "Z", "0", " ", "q"),)
 for name, t in (("polygon", cdr_ref.POLYGON), ("nested", cdr_ref.NESTED)):
     base = cdr_ref.corpus(t, 65536, seed=11, le_only=True, clean=True)
     dgrams = base * 8
