@@ -669,10 +669,20 @@ __global__ __launch_bounds__(64 * NEST_WAVES) void cdr_nested_kernel(CdrNest N, 
         s_val[wave][rw][q] = x;
       }
     }
+    {  // the chunk's rows zeroed by the whole wave (16 B per lane, consecutive), complete before any
+       // lane stores into them (vmcnt(0): the stores are acknowledged)
+      const uint64_t r0 = c * 64, nv = n - r0 < 64 ? n - r0 : 64;
+      uint8_t* rowc = a.rows + r0 * N.row_bytes;
+      const uint64_t bytes = nv * N.row_bytes;
+      for (uint64_t b = 16u * lane; b < bytes; b += 1024u) {
+        if (b + 16 <= bytes) st16u(rowc + b, make_uint4(0, 0, 0, 0));
+        else for (uint64_t t2 = b; t2 < bytes; t2 += 4) *(uint32_t*)(rowc + t2) = 0u;
+      }
+      __builtin_amdgcn_s_waitcnt(0);  // (vector counters only: no scalar stores are issued)
+    }
     wave_sync();
     if (r < n) {
       uint8_t* row = a.rows + r * N.row_bytes;
-      zero_row(row, N.row_bytes);
       if (st == 0xffu) {
         const uint8_t* v = len <= NEST_VCAP ? (const uint8_t*)&s_val[wave][lane][0] : a.arena + vb;
         st = nest_decode(s_ops, s_match, s_zero, N.n_ops, v, len, le, row, &s_fr[wave][lane]);
