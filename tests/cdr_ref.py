@@ -409,3 +409,35 @@ POLYGON = cdr.CdrType([("name", cdr.String(16)), ("pts", cdr.Seq(cdr.CdrType([("
 NESTED = cdr.CdrType([("a", "u8"), ("m", cdr.Seq(cdr.Seq("u16", 3), 4)),
                       ("grid", cdr.Array(cdr.CdrType([("id", "u8"), ("v", cdr.Seq("f64", 2)), ("ok", "bool")]), 3)),
                       ("deep", cdr.Seq(cdr.Seq(cdr.Array(cdr.String(5), 2), 2), 2)), ("z", "i64")])
+
+
+def random_type(rng, depth=0, budget=None):
+    """A random sample type of primitives, bools, strings, sequences, arrays and nested
+    structs, with composite sequences / arrays up to 4 levels deep (at most MAX_OPS ops)."""
+    budget = budget if budget is not None else [cdr.MAX_OPS - 4]
+    prims = list(cdr.PRIMS)
+    fields = []
+    for k in range(int(rng.integers(2, 6))):
+        if budget[0] <= 2:
+            break
+        r = rng.random()
+        if r < 0.25:
+            spec = prims[int(rng.integers(0, len(prims)))]
+        elif r < 0.30:
+            spec = "bool"
+        elif r < 0.40:
+            spec = cdr.String(int(rng.integers(0, 13)))
+        elif r < 0.48:
+            spec = cdr.Seq(prims[int(rng.integers(0, len(prims)))], int(rng.integers(0, 5)))
+        elif r < 0.53:
+            spec = cdr.Array(prims[int(rng.integers(0, len(prims)))], int(rng.integers(0, 4)))
+        elif depth < cdr.MAX_DEPTH and budget[0] > 6:
+            budget[0] -= 2  # BEGIN + END
+            elem = random_type(rng, depth + 1, budget) if rng.random() < 0.6 else cdr.String(int(rng.integers(0, 9)))
+            spec = (cdr.Seq(elem, int(rng.integers(0, 4))) if rng.random() < 0.6
+                    else cdr.Array(elem, int(rng.integers(1, 3))))
+        else:
+            spec = prims[int(rng.integers(0, len(prims)))]
+        budget[0] -= 1
+        fields.append((f"f{depth}_{k}", spec))
+    return cdr.CdrType(fields)

@@ -254,3 +254,13 @@ def test_bad_composite_program_rejected(rx):
     deep.ops = np.concatenate([wrap, ops, ops[-1:]])
     with pytest.raises(rtps_rx.RtpsRxError):
         rx.cdr_decode(deep, arena, off, outs, r2, s2)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_composite_types_gpu(rx, seed):
+    """The GPU against the oracle on random types (test_cdr_oracle.test_random_composite_types)."""
+    rng = np.random.default_rng(1000 + seed)
+    t = cdr_ref.random_type(rng)
+    dgrams = cdr_ref.corpus(t, 1500, seed=seed)
+    arena, off, ln = oracle.pack(dgrams, align=1)
+    _check(rx, t, arena, off, ln, f"random-{seed}")
