@@ -210,6 +210,24 @@ __global__ __launch_bounds__(IT) void k_fidx(const rtps_frag_sample* frag, const
   }
 }
 
+// k_fidx's tables cleared for the batch's record slots in one launch (three memsets before):
+// four slots per thread, 16-B / 32-B / 4-B stores (the arrays are hipMalloc-aligned)
+__global__ __launch_bounds__(IT) void k_fclear(uint64_t max, uint32_t* fidx, uint64_t* fmask, uint8_t* fall) {
+  const uint64_t n4 = max / 4u;
+  for (uint64_t q = (uint64_t)blockIdx.x * IT + threadIdx.x; q < n4; q += (uint64_t)gridDim.x * IT) {
+    reinterpret_cast<uint4*>(fidx)[q] = make_uint4(NONE, NONE, NONE, NONE);
+    reinterpret_cast<ulonglong2*>(fmask)[2u * q] = make_ulonglong2(0ull, 0ull);
+    reinterpret_cast<ulonglong2*>(fmask)[2u * q + 1u] = make_ulonglong2(0ull, 0ull);
+    reinterpret_cast<uint32_t*>(fall)[q] = 0u;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (max & 3u)) {
+    const uint64_t i = 4u * n4 + threadIdx.x;
+    fidx[i] = NONE;
+    fmask[i] = 0ull;
+    fall[i] = 0u;
+  }
+}
+
 // Does entry `pos` (reader `slot`) of record i's target set take its completed DataFrag
 // sample?  fm: the entries whose assembler completed it (bits 0..63), all: a writer-keyed
 // sample (every entry); a record without one: fm = ~0, all.  Entries past 64 look for
@@ -2801,13 +2819,12 @@ static int ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, cons
   x.frag = frag;
   x.n_frag = n_frag;
   x.max_frag = max_frag;
-  if (with_frag) ok = ok && hipMemsetAsync(x.fidx, 0xff, max * 4, st) == hipSuccess &&
-                     hipMemsetAsync(x.fmask, 0, max * 8, st) == hipSuccess &&
-                     hipMemsetAsync(x.fall, 0, max, st) == hipSuccess;
-  if (!ok) return RTPS_RX_EHIP;
-  if (with_frag)
+  if (with_frag) {
+    hipLaunchKernelGGL(k_fclear, dim3((uint32_t)hmin((max / 4u + IT - 1) / IT + 1u, 4096)), dim3(IT), 0, st, max,
+                       x.fidx, x.fmask, x.fall);
     hipLaunchKernelGGL(k_fidx, dim3((uint32_t)hmin((max_frag + IT - 1) / IT, 4096)), dim3(IT), 0, st, frag, n_frag,
                        max_frag, max, x.fidx, x.fmask, x.fall, t, records);
+  }
   uint32_t lds = rt_fits_lds(t) ? rt_lds_bytes(t.gmask + 1u, t.emask + 1u) : 0u;
   // the target sets join the hash tables in LDS when both fit the tables' own limit
   const bool sets_lds = lds && lds + sets_lds_bytes(t) <= RT_LDS_MAX;
