@@ -951,8 +951,10 @@ static uint8_t cdr_decode_one(const rtps_cdr_op* prog, uint32_t n_ops, const uin
           if (write) cdr_store(dst, op->out_off, n, 4);
         }
         const uint32_t j = cdr_match(prog, n_ops, k);
-        if (n == 0) { k = j; break; }
-        if (n > op->count && cdr_min_wire(prog, n_ops, k + 1, j) == 0) return RTPS_CDR_TOO_LONG;
+        const int zero_wire = cdr_min_wire(prog, n_ops, k + 1, j) == 0;
+        if (n > op->count && zero_wire) return RTPS_CDR_TOO_LONG;
+        /* elements that read no bytes cannot fail and store nothing (zero-count arrays only) */
+        if (n == 0 || zero_wire) { k = j; break; }
         cdr_frame f = {k, n, 0, base + op->out_off + (seq ? 4u : 0u), base, write};
         fr[depth++] = f;
         base = f.elem0;

@@ -558,12 +558,15 @@ __device__ uint8_t nest_decode(const rtps_cdr_op* ops, const uint8_t* match, con
           pos += 4;
           if (write) *(uint32_t*)d = n;
         }
-        if (n == 0) { k = match[k]; break; }
         if (n > op.count && zero_el[k]) return RTPS_CDR_TOO_LONG;
-        const uint32_t elem0 = base + op.out_off + (seq ? 4u : 0u);
+        // elements that read no wire bytes also write nothing (zero-count arrays only): skipped,
+        // so a crafted count cannot make the walk loop without consuming bytes
+        if (n == 0 || zero_el[k]) { k = match[k]; break; }
+        // base < 2^20 always (a row offset; 0 while nothing is stored), so it packs beside k
+        const uint32_t elem0 = write ? base + op.out_off + (seq ? 4u : 0u) : 0u;
         fr[depth * 64u] = make_uint4(n, 0u, elem0, base | (k << 24) | (write ? 0x80000000u : 0u));
-        base = elem0;
         write = write && op.count > 0;
+        base = write ? elem0 : 0u;
         depth++;
         break;
       }
@@ -574,8 +577,8 @@ __device__ uint8_t nest_decode(const rtps_cdr_op* ops, const uint8_t* match, con
         const rtps_cdr_op b = ops[begin];
         if (++f.y < f.x) {
           fr[(depth - 1) * 64u].y = f.y;
-          base = f.z + f.y * b.stride;
           write = fw && f.y < b.count;
+          base = write ? f.z + f.y * b.stride : 0u;  // (elements past the slot store nothing)
           k = begin;  // ++k: the element's first op
         } else {
           depth--;

@@ -441,3 +441,21 @@ def random_type(rng, depth=0, budget=None):
         budget[0] -= 1
         fields.append((f"f{depth}_{k}", spec))
     return cdr.CdrType(fields)
+
+
+# A crafted type for the walk's bounds: elements of 64,004 row bytes holding an array of
+# 16,000 zero-width structs, one byte on the wire each.  A 40,000-element sequence of them
+# (slot: one element) walks 39,999 elements past its slot; the zero-width arrays read and
+# store nothing and are skipped, so the walk stays O(bytes).
+WIDE_EL = cdr.CdrType([("b", "bool"), ("z", cdr.Array(cdr.CdrType([("q", cdr.Array("u32", 0))]), 16000))])
+WIDE = cdr.CdrType([("s", cdr.Seq(WIDE_EL, 1)), ("t", "u8")])
+
+
+def wide_payloads():
+    """(label, value bytes, expected status) for WIDE."""
+    import struct as st
+    return [("ok", st.pack("<I", 1) + b"\x01" + b"\x07", cdr.CDR_OK),
+            ("too_long", st.pack("<I", 40000) + b"\x01" * 40000 + b"\x07", cdr.CDR_TOO_LONG),
+            ("bad_bool", st.pack("<I", 40000) + b"\x01" * 39000 + b"\x02" + b"\x00" * 999 + b"\x07",
+             cdr.CDR_BAD_BOOL),
+            ("eof", st.pack("<I", 40000) + b"\x01" * 30000, cdr.CDR_EOF)]

@@ -264,3 +264,16 @@ def test_random_composite_types_gpu(rx, seed):
     dgrams = cdr_ref.corpus(t, 1500, seed=seed)
     arena, off, ln = oracle.pack(dgrams, align=1)
     _check(rx, t, arena, off, ln, f"random-{seed}")
+
+
+def test_wide_elements_gpu(rx):
+    """cdr_ref.WIDE on the GPU: statuses and rows equal the oracle's, in bounded time."""
+    t = cdr_ref.WIDE
+    dgrams, want = [], []
+    for i, (label, value, st) in enumerate(cdr_ref.wide_payloads()):
+        pad = (-len(value)) % 4
+        dgrams.append(cdr_ref.data_datagram(cdr_ref.REP_CDR_LE + bytes([0, pad]) + value + bytes(pad), sn=i + 1))
+        want.append(st)
+    arena, off, ln = oracle.pack(dgrams * 16, align=1)
+    _, status = _check(rx, t, arena, off, ln, "wide")
+    assert list(status[:4]) == want

@@ -203,3 +203,13 @@ def test_random_composite_types(seed):
     assert np.array_equal(status, exp_status), f"seed {seed}: statuses differ"
     assert np.array_equal(rows, exp_rows), f"seed {seed}: rows differ"
     assert (status == cdr.CDR_OK).any()
+
+
+def test_wide_elements_past_the_slot():
+    """cdr_ref.WIDE: 40,000 one-byte elements of a 64,004-byte element row walked past a
+    one-element slot (the oracle; the GPU in test_cdr_gpu.py::test_wide_elements_gpu)."""
+    for label, value, want in cdr_ref.wide_payloads():
+        st, row = _one(cdr_ref.WIDE, value)
+        assert st == want, label
+        if want == cdr.CDR_OK:
+            assert cdr_ref.WIDE.to_python(cdr_ref.WIDE.rows(row)[0])["t"] == 7
