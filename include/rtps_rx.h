@@ -464,15 +464,28 @@ int rtps_rx_shard_reserve_spill(rtps_shard* s, uint64_t records, uint64_t bytes)
  * owner, and a hash of few writers leaves owners unequal (16 writers over 8 ranks: one
  * idle, one with 1.5x the mean), so the shard keeps a table of the context's writers
  * (the writer GUIDs of its proxies) dealt over the ranks; a writer not in it goes by
- * fmix32(fnv1a32(GUID)) % n_ranks.  Every rank must set the same readers, topics and
- * arguments: the deal is a function of them alone (not of their order).  The table
- * follows rtps_rx_set_readers / set_match_table / set_topics (rebuilt at the next pack).
- *   RTPS_OWNER_BALANCED (the default)  every writer its own group;
- *   RTPS_OWNER_TOPIC   writers whose target readers share a topic cache (a topic of
+ * fmix32(fnv1a32(GUID)) % n_ranks.  Every rank must make the same calls (readers, topics,
+ * set_owners, packs) in the same order: the deal is a function of them alone (not of the
+ * order inside a table).
+ *   RTPS_OWNER_BALANCED  every writer its own group (the default while no topic is set);
+ *   RTPS_OWNER_TOPIC     writers whose target readers share a topic cache (a topic of
  *     rtps_rx_set_topics, or a reader's own cache) are one group, so one owner holds
- *     all of a TopicCache's changes: needed for RTPS_INGEST_TOPIC_CACHE on owner
- *     batches to be exact (the cache's GC spans its writers, dds_cache.rs:367-420);
- *   RTPS_OWNER_HASH    no table (every writer by the hash).
+ *     all of a TopicCache's changes, as RTPS_INGEST_TOPIC_CACHE on owner batches needs (the
+ *     cache's GC spans its writers, dds_cache.rs:367-420).  The group also holds an ENTITY
+ *     KEY per entity id that a reader contains (0xff x 12 || entity id): a writer without a
+ *     proxy that reaches the topic by entity id (rt_classify's entity sets) goes to that
+ *     group's owner.  The default once rtps_rx_set_topics has configured a topic, unless
+ *     set_owners chose a mode;
+ *   RTPS_OWNER_HASH      no table (every writer by the hash).
+ * rtps_rx_ingest refuses RTPS_INGEST_TOPIC_CACHE (RTPS_RX_EINVAL) on a context with a
+ * shard of >= 2 ranks in another mode: its topic caches would diverge.
+ * The table is STICKY: when the readers or topics change, the next pack (re)builds it,
+ * and every writer the previous table held keeps its owner (its writer proxy, far set,
+ * DataFrag assemblies and topic-cache changes live there); new writers are dealt onto the
+ * ranks' loads.  Only a topic group that comes to join writers of different owners moves
+ * the smaller part to the owner holding most of its weight: those writers' state stays
+ * behind on the old owner (as after rtps_rx_ingest_reset there).  set_owners deals afresh
+ * (an explicit rebalance with the same state caveat for every writer that moves).
  * Groups are dealt by total weight, largest first, each to the least-loaded owner (ties:
  * the group's smallest GUID, the lowest rank); equal weights deal the sorted GUIDs
  * round-robin.  guids[n][16] / weights[n] (optional): weights of writers (e.g. their
@@ -483,7 +496,8 @@ int rtps_rx_shard_reserve_spill(rtps_shard* s, uint64_t records, uint64_t bytes)
 #define RTPS_OWNER_TOPIC 2u
 int rtps_rx_shard_set_owners(rtps_shard* s, uint32_t mode, const uint8_t* guids, const uint64_t* weights,
                              uint32_t n);
-/* The owner rank of a writer GUID under the shard's current assignment (host), or a
+/* The owner rank of a writer GUID under the shard's current assignment (host; a table the
+ * next pack would rebuild is answered from that rebuild, without committing it), or a
  * negative RTPS_RX_* code. */
 int rtps_rx_shard_owner(rtps_shard* s, const uint8_t guid[16]);
 /* The deal itself, on the host (no GPU): writers[n][16], weights[n] (NULL: 1 each),
@@ -491,6 +505,12 @@ int rtps_rx_shard_owner(rtps_shard* s, const uint8_t guid[16]);
  * owners[n] < n_ranks. */
 int rtps_rx_owner_assign(const uint8_t* writers, const uint64_t* weights, const uint32_t* groups, uint32_t n,
                          uint32_t n_ranks, uint32_t* owners);
+/* The sticky deal: prev[n] (NULL: none) = each writer's owner in the previous table, or -1
+ * for a new one.  A group with owned members goes to the rank holding most of their weight
+ * (each owned member counts weight + 1; ties: the lowest rank), and the other groups are
+ * dealt as above onto the loads those leave. */
+int rtps_rx_owner_assign_sticky(const uint8_t* writers, const uint64_t* weights, const uint32_t* groups, uint32_t n,
+                                uint32_t n_ranks, const int32_t* prev, uint32_t* owners);
 
 /* ---- batch CDR decode (a18) ----------------------------------------------
  * Replaces the per-sample decode
@@ -771,7 +791,8 @@ int rtps_rx_ingest_reset(rtps_rx_ctx* ctx);
  * (*n_window_overflow > 0: samples accepted without the duplicate check) has every delivery
  * checked against its topic's live changes, so CACHED stays add_change's answer for the
  * deliveries made.  Owner batches (rtps_rx_shard_*): a topic cache's GC spans all of its
- * writers, so its changes must all meet on one owner: use RTPS_OWNER_TOPIC there. */
+ * writers, so its changes must all meet on one owner: RTPS_OWNER_TOPIC (the shard's default
+ * once topics are set; the ingest refuses the topic caches under another mode). */
 typedef struct rtps_topic {
   uint32_t topic;             /* caller-defined topic id */
   uint32_t max_keep_samples;  /* >= 1 */

@@ -298,6 +298,15 @@ static_assert(sizeof(PEv) == 32, "PEv layout");
 // inserts such ranges one SN at a time too, rtps_writer_proxy.rs:284-291).
 // a free slot: all ones (far SNs are >= W > 0), like its key ~0, so that a byte fill clears the
 // pool; the slots at and above the pool's counter are always free (fresh tables need no clearing)
+// A GAP whose range reaches more than FAR_BIG sequence numbers past its proxy's window would
+// fill the far set SN by SN.  It is a threshold instead (irrelevant_changes_range's jump,
+// rtps_writer_proxy.rs:241-292) whenever its gapStart is at or below all_ackable_before when it
+// arrives, which this batch's earlier events may have moved: classify sends every such GAP to
+// the per-proxy path (C_TGAP), whose k_proxy decides it against the running value.
+constexpr int64_t FAR_BIG = 256;
+__host__ __device__ __forceinline__ bool gap_far_big(int64_t start, int64_t list_base, int64_t lim) {
+  return start <= list_base && list_base - (start > lim ? start : lim) > FAR_BIG;
+}
 constexpr int64_t FEMPTY = -1;
 constexpr uint32_t FT_MIN = 64;         // smallest table
 enum : uint32_t { FI_SAMPLE = 1, FI_DUP = 2, FI_GAP = 3 };
@@ -523,7 +532,8 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
             const int64_t lim = st.lo[en] + (int64_t)W;
             if (ev == EV_SAMPLE ? sn >= lim : (int64_t)(((uint64_t)q2[3] << 32) | q2[2]) + (int64_t)q3[0] > lim) {
               ++nfar;
-              if (ev == EV_GAP && sn <= st.base[en]) ++ntg;
+              if (ev == EV_GAP && (sn <= st.base[en] || gap_far_big(sn, (int64_t)(((uint64_t)q2[3] << 32) | q2[2]), lim)))
+                ++ntg;
             }
           }
         }
@@ -550,7 +560,7 @@ __global__ __launch_bounds__(IT) void k_classify(ReaderDev t, const rtps_record*
           const int64_t list_base = (int64_t)(((uint64_t)q2[3] << 32) | q2[2]);
           if (list_base + (int64_t)q3[0] > st.lo[ent] + (int64_t)W) {  // coverage past the window
             ++nfar;
-            if (sn <= st.base[ent]) ++ntg;
+            if (sn <= st.base[ent] || gap_far_big(sn, list_base, st.lo[ent] + (int64_t)W)) ++ntg;
           }
         }
       }
@@ -2025,7 +2035,7 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
   __shared__ uint32_t s_pre[BK ? BK_MAX + 1 : 1];  // BK: the proxy's events before workgroup b's piece
   __shared__ uint32_t s_base[BK ? BK_MAX : 1];     // BK: pev index of the proxy's event q in piece b = s_base[b] + q
   __shared__ uint32_t s_idx[BK ? BK_IDX : 1];      // BK: the piece holding event 4m (when the proxy has <= 4 BK_IDX)
-  __shared__ uint32_t s_first;
+  __shared__ uint32_t s_first, s_split;
   __shared__ GapE s_gap[GCAP];  // the chunk's GAPs (the first GCAP), one per thread in the GAP phases
   __shared__ uint32_t s_ngap;
   __shared__ FarSh fsh;                // the proxy's far set
@@ -2082,7 +2092,27 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
     qe = s.seg_e[e];
   }
   int64_t run_cnt = s.hbc[e], run_thr = base;  // max HEARTBEAT count so far; max accepted firstSN (>= base)
+  int64_t abc = base;  // a lower bound of all_ackable_before at the chunk's start (exact where a far GAP asked)
   uint64_t n_ovf = 0;
+  // the first sequence number >= from that the window leaves uncovered (lo + W: none; from < lo + W)
+  auto first_open = [&](int64_t from) -> int64_t {
+    const uint32_t off0 = (uint32_t)(from - lo);
+    if (tid == 0) s_first = NONE;
+    __syncthreads();
+    for (uint32_t w0 = (off0 >> 5); w0 < WW; w0 += PT) {  // rounds of PT words, stop at the first hit
+      const uint32_t w = w0 + tid;
+      uint32_t word = w < WW ? sb[w] : 0xffffffffu;
+      if (w == (off0 >> 5)) word |= (1u << (off0 & 31u)) - 1u;
+      const uint64_t open = __ballot(word != 0xffffffffu);  // lowest lane first: one LDS atomic per wave
+      if (open && (tid & 63u) == (uint32_t)__builtin_ctzll(open))
+        atomicMin(&s_first, w * 32u + (uint32_t)__builtin_ctz(~word));
+      __syncthreads();
+      if (s_first != NONE) break;
+    }
+    const int64_t r = lo + (int64_t)(s_first != NONE ? s_first : W);
+    __syncthreads();  // (s_first read by every thread before it is reused)
+    return r;
+  };
   __syncthreads();
   PST(0);
   // the chunk at c0's events of this thread (BK: found through the piece tables)
@@ -2117,7 +2147,7 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
   // this chunk is decided (its barriers are LDS-only: plain loads survive them)
   PEv nx[PPT];
   if (qb < qe) load_chunk(qb, nx);
-  for (uint32_t q0 = qb; q0 < qe; q0 += PCH) {
+  for (uint32_t q0 = qb, q1; q0 < qe; q0 = q1) {
     uint32_t m[PPT], slot[PPT], kk[PPT];
     int64_t v[PPT], a[PPT];
     uint64_t bwj[PPT];
@@ -2129,9 +2159,41 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
       a[j] = nx[j].a;
       bwj[j] = nx[j].bw;
       kk[j] = nx[j].k;
-      if ((m[j] & 3u) == EV_HB && a[j] > cmax) cmax = a[j];
     }
+    q1 = q0 + PCH < qe ? q0 + PCH : qe;
     if (q0 + PCH < qe) load_chunk(q0 + PCH, nx);
+    // A GAP reaching far past the window (gap_far_big) that the chunk-start bound abc does not
+    // show at or below all_ackable_before may still be (the chunk's earlier events can move it):
+    // abc is made exact for the window, and the chunk ends before the first such GAP after its
+    // start, so that the next chunk starts at that GAP with the exact running value
+    {
+      const int64_t lim0 = lo + (int64_t)W;
+      bool big = false;
+#pragma unroll
+      for (uint32_t j = 0; j < PPT; ++j) big |= (m[j] & 3u) == EV_GAP && v[j] > abc && gap_far_big(v[j], a[j], lim0);
+      if (__syncthreads_or(big)) {
+        const int64_t from = run_thr > abc ? run_thr : abc;
+        abc = from < lim0 ? first_open(from) : from;
+        if (tid == 0) s_split = NONE;
+        __syncthreads();
+#pragma unroll
+        for (uint32_t j = 0; j < PPT; ++j) {
+          const uint32_t q = q0 + tid * PPT + j;
+          if (q > q0 && (m[j] & 3u) == EV_GAP && v[j] > abc && gap_far_big(v[j], a[j], lim0)) atomicMin(&s_split, q);
+        }
+        __syncthreads();
+        if (s_split != NONE) {
+          q1 = s_split;
+#pragma unroll
+          for (uint32_t j = 0; j < PPT; ++j)
+            if (q0 + tid * PPT + j >= q1) m[j] = EV_NONE;  // (the next chunk, which starts at q1, takes them)
+        }
+        __syncthreads();  // (s_split read by every thread)
+      }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < PPT; ++j)
+      if ((m[j] & 3u) == EV_HB && a[j] > cmax) cmax = a[j];
     // HEARTBEATs: accepted iff count > every earlier count and the state's (reader.rs:902-905);
     // an accepted one covers [0, firstSN) (irrelevant_changes_up_to)
     PST(1);
@@ -2145,10 +2207,10 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
       const bool hb = (m[j] & 3u) == EV_HB;
       f[j] = (hb && a[j] > c_ex) ? v[j] : INT64_MIN;
       if (hb && a[j] > c_ex) c_ex = a[j];
-      // a GAP whose range starts at or below all_ackable_before (the batch's: it only grows)
-      // moves it to gapList.base (irrelevant_changes_range, rtps_writer_proxy.rs:241-292): a
+      // a GAP whose range starts at or below all_ackable_before (abc bounds it from below: it only
+      // grows) moves it to gapList.base (irrelevant_changes_range, rtps_writer_proxy.rs:241-292): a
       // threshold like an accepted HEARTBEAT's, with no SN to record past the window
-      if ((m[j] & 3u) == EV_GAP && v[j] <= base && v[j] <= a[j] && a[j] > f[j]) f[j] = a[j];
+      if ((m[j] & 3u) == EV_GAP && v[j] <= abc && v[j] <= a[j] && a[j] > f[j]) f[j] = a[j];
       if (f[j] > fmax) fmax = f[j];
     }
     int64_t thr_total;
@@ -2232,7 +2294,7 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
     uint32_t fkind = 0;  // far items (rare) of the thread's events: kind << 2 j, into the far set below
     auto far = [&](uint32_t j, uint32_t kind) { fkind |= kind << (2u * j); };
     // a far item's first SN: a threshold GAP's range is the threshold's (above), only its list is recorded
-    auto fsn0 = [&](uint32_t kind, int64_t gv, int64_t ga) { return (kind == FI_GAP && gv <= base) ? ga + 1 : gv; };
+    auto fsn0 = [&](uint32_t kind, int64_t gv, int64_t ga) { return (kind == FI_GAP && gv <= abc) ? ga + 1 : gv; };
 #pragma unroll
     for (uint32_t j = 0; j < PPT; ++j) {
       if (f[j] > t_run) t_run = f[j];
@@ -2324,26 +2386,11 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
     }
     __syncthreads();
     PST(6);
+    if (q1 < q0 + PCH && q1 < qe) load_chunk(q1, nx);  // the chunk ended at a far GAP: the next starts there
   }
   if (n_ovf) atomicAdd(reinterpret_cast<unsigned long long*>(s.ctr + C_OVF), (unsigned long long)n_ovf);
   // state (as k_state): ack_base = first sequence number >= threshold outside the change set
-  int64_t nb = run_thr;
-  if (run_thr < lo + (int64_t)W) {
-    const uint32_t off0 = (uint32_t)(run_thr - lo);
-    if (tid == 0) s_first = NONE;
-    __syncthreads();
-    for (uint32_t w0 = (off0 >> 5); w0 < WW; w0 += PT) {  // rounds of PT words, stop at the first hit
-      const uint32_t w = w0 + tid;
-      uint32_t word = w < WW ? sb[w] : 0xffffffffu;
-      if (w == (off0 >> 5)) word |= (1u << (off0 & 31u)) - 1u;
-      const uint64_t open = __ballot(word != 0xffffffffu);  // lowest lane first: one LDS atomic per wave
-      if (open && (tid & 63u) == (uint32_t)__builtin_ctzll(open))
-        atomicMin(&s_first, w * 32u + (uint32_t)__builtin_ctz(~word));
-      __syncthreads();
-      if (s_first != NONE) break;
-    }
-    nb = lo + (int64_t)(s_first != NONE ? s_first : W);
-  }
+  int64_t nb = run_thr < lo + (int64_t)W ? first_open(run_thr) : run_thr;
   nb = far_extend(s, fsh, lo, nb, PT);
   const int64_t nlo = nb & ~(int64_t)31;
   const uint64_t shift = (uint64_t)(nlo - lo) >> 5;

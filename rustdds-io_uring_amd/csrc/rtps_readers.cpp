@@ -39,6 +39,7 @@ struct ReaderTable {
   std::vector<uint32_t> first;     // [n_sets + 1]
   std::vector<rtps_target> ent;
   std::vector<Guid> wguid;         // [n_writer_sets] the writer GUID of each writer set
+  std::vector<Eid> eids;           // [n_sets - n_writer_sets] the writer entity id of each entity set
   uint32_t n_writer_sets = 0, n_proxies = 0, max_set = 0;
   bool active = false;
   // device images
@@ -87,6 +88,7 @@ struct Built {  // host image of a reader table
   std::vector<uint32_t> first;
   std::vector<rtps_target> ent;
   std::vector<Guid> wguid;
+  std::vector<Eid> eids;
   std::vector<uint32_t> gkeys, gset, ekeys, eset;
   uint32_t gcap = 0, ecap = 0, n_writer_sets = 0, max_set = 0;
 };
@@ -195,6 +197,7 @@ int build(const rtps_reader* readers, uint32_t nr, const rtps_proxy* proxies, ui
   out.n_writer_sets = (uint32_t)wsets.size();
   out.max_set = max_set;
   out.wguid.swap(wsets);
+  out.eids.swap(esets);
   return RTPS_RX_OK;
 }
 }  // namespace
@@ -232,6 +235,7 @@ int rt_set(ReaderTable* t, const rtps_reader* readers, uint32_t nr, const rtps_p
   t->first.swap(first);
   t->ent.swap(ent);
   t->wguid.swap(b.wguid);
+  t->eids.swap(b.eids);
   t->n_writer_sets = b.n_writer_sets;
   t->n_proxies = np;
   t->max_set = b.max_set;
@@ -289,6 +293,12 @@ const uint8_t* rt_writer_guids(const ReaderTable* t, uint32_t* n) {
   const bool on = t && t->active && !t->wguid.empty();
   *n = on ? (uint32_t)t->wguid.size() : 0u;
   return on ? t->wguid[0].data() : nullptr;
+}
+
+const uint8_t* rt_entity_ids(const ReaderTable* t, uint32_t* n) {
+  const bool on = t && t->active && !t->eids.empty();
+  *n = on ? (uint32_t)t->eids.size() : 0u;
+  return on ? t->eids[0].data() : nullptr;
 }
 
 void rt_host(const ReaderTable* t, const uint32_t** first, const rtps_target** ent, uint32_t* n_sets) {

@@ -131,3 +131,5 @@ ReaderDev rt_dev(const ReaderTable* t);  // gkeys == nullptr when no reader is s
 void rt_host(const ReaderTable* t, const uint32_t** first, const rtps_target** ent, uint32_t* n_sets);
 // the writer GUIDs of the writer sets 0 .. n-1 (16 bytes each, contiguous), nullptr when none
 const uint8_t* rt_writer_guids(const ReaderTable* t, uint32_t* n);
+// the writer entity ids of the entity sets n_writer_sets .. n_sets - 1 (4 bytes each), nullptr when none
+const uint8_t* rt_entity_ids(const ReaderTable* t, uint32_t* n);

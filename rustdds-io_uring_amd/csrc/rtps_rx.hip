@@ -34,6 +34,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
 #include <new>
 #include <vector>
@@ -1628,18 +1629,25 @@ struct rtps_rx_ctx {
   uint64_t fx_cap = 0, fx_xcap = 0;
   void* fx_tmp = nullptr;
   size_t fx_tmp_bytes = 0;
+  std::vector<rtps_shard*> shards;  // owner-side exchanges created on this context (rtps_ctx_shard_attach)
 };
 
 uint64_t rtps_ctx_readers_version(const rtps_rx_ctx* c) { return c->readers_version; }
 
-void rtps_ctx_owner_writers(const rtps_rx_ctx* c, bool by_topic, std::vector<uint8_t>& guids,
-                            std::vector<uint32_t>& group) {
-  uint32_t nw = 0;
+void rtps_ctx_owner_keys(const rtps_rx_ctx* c, bool by_topic, std::vector<uint8_t>& keys,
+                         std::vector<uint32_t>& group) {
+  uint32_t nw = 0, ne = 0;
   const uint8_t* g = c->readers ? rt_writer_guids(c->readers, &nw) : nullptr;
-  guids.assign(g, g + 16ull * nw);
-  group.resize(nw);
-  for (uint32_t w = 0; w < nw; ++w) group[w] = w;
-  if (!by_topic || !nw) return;
+  const uint8_t* e = (by_topic && c->readers) ? rt_entity_ids(c->readers, &ne) : nullptr;
+  keys.assign(g, g + 16ull * nw);
+  for (uint32_t k = 0; k < ne; ++k) {  // entity keys: OWNER_EKEY_PREFIX x 12, then the entity id
+    keys.insert(keys.end(), 12, OWNER_EKEY_PREFIX);
+    keys.insert(keys.end(), e + 4ull * k, e + 4ull * k + 4);
+  }
+  const uint32_t nk = nw + ne;
+  group.resize(nk);
+  for (uint32_t w = 0; w < nk; ++w) group[w] = w;
+  if (!by_topic || !nk) return;
   const uint32_t* first = nullptr;
   const rtps_target* ent = nullptr;
   uint32_t n_sets = 0;
@@ -1648,19 +1656,34 @@ void rtps_ctx_owner_writers(const rtps_rx_ctx* c, bool by_topic, std::vector<uin
     while (group[x] != x) x = group[x] = group[group[x]];
     return x;
   };
-  std::vector<uint32_t> topic_writer;  // topic cache -> the first writer seen feeding it
-  std::vector<uint32_t> key;           // (parallel) topic cache ids
-  for (uint32_t w = 0; w < nw && w < n_sets; ++w)
+  std::vector<uint32_t> topic_key;  // topic cache -> the first key seen feeding it
+  std::vector<uint32_t> topic;      // (parallel) topic cache ids
+  // key w is target set w: writer sets first, then entity sets (rtps_readers.cpp)
+  for (uint32_t w = 0; w < nk && w < n_sets; ++w)
     for (uint32_t k = first[w]; k < first[w + 1]; ++k) {
       // the reader's topic cache: a configured topic, or its own (no topics set: one per slot)
       const uint32_t t = c->topics ? rtps_topic_of_slot(c->topics, ent[k].reader_slot) : ent[k].reader_slot;
       uint32_t j = 0;
-      while (j < key.size() && key[j] != t) ++j;
-      if (j == key.size()) { key.push_back(t); topic_writer.push_back(w); continue; }
-      const uint32_t a = root(w), b = root(topic_writer[j]);
+      while (j < topic.size() && topic[j] != t) ++j;
+      if (j == topic.size()) { topic.push_back(t); topic_key.push_back(w); continue; }
+      const uint32_t a = root(w), b = root(topic_key[j]);
       if (a != b) group[a > b ? a : b] = a < b ? a : b;  // the smaller index is the root
     }
-  for (uint32_t w = 0; w < nw; ++w) group[w] = root(w);
+  for (uint32_t w = 0; w < nk; ++w) group[w] = root(w);
+}
+
+bool rtps_ctx_topics_configured(const rtps_rx_ctx* c) { return c->topics && rtps_topic_n_configured(c->topics) > 0; }
+
+void rtps_ctx_shard_attach(rtps_rx_ctx* c, rtps_shard* s, bool attach) {
+  auto& v = c->shards;
+  v.erase(std::remove(v.begin(), v.end(), s), v.end());
+  if (attach) v.push_back(s);
+}
+
+bool rtps_ctx_topic_split(const rtps_rx_ctx* c) {
+  for (const rtps_shard* s : c->shards)
+    if (rtps_shard_splits_topics(s)) return true;
+  return false;
 }
 
 static int hip_fail(hipError_t e) { return e == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP; }
@@ -2281,6 +2304,9 @@ int rtps_rx_ingest(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len, con
   if (max_records && (!arena || !dgram_off)) return RTPS_RX_EINVAL;
   if (flags & ~(RTPS_INGEST_BEST_EFFORT | RTPS_INGEST_TOPIC_CACHE)) return RTPS_RX_EINVAL;
   if (frag && (!n_frag || !max_frag)) return RTPS_RX_EINVAL;
+  // a topic cache's GC spans all of its writers (dds_cache.rs:210-276, 367-420): on owner batches
+  // they must all meet on one owner, which only RTPS_OWNER_TOPIC guarantees
+  if ((flags & RTPS_INGEST_TOPIC_CACHE) && rtps_ctx_topic_split(c)) return RTPS_RX_EINVAL;
   (void)hipSetDevice(c->device);
   if (!c->ingest) {
     c->ingest = rtps_ingest_state_new(c->device);

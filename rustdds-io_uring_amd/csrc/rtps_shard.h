@@ -62,11 +62,14 @@ struct rtps_shard {
   size_t cub_bytes = 0;
   // ---- writer -> owner table (rtps_rx_shard_set_owners) ----
   uint32_t owner_mode = RTPS_OWNER_BALANCED;
+  bool mode_explicit = false;      // rtps_rx_shard_set_owners chose the mode (else: TOPIC once topics are set)
   std::vector<uint8_t> x_guid;     // the caller's extra writers (16 B each) and their weights
   std::vector<uint64_t> x_weight;
   uint64_t owner_version = ~0ull;  // the context's readers version the table follows (~0: build at the next pack)
-  std::vector<uint8_t> t_guid;     // host copy of the table: writer GUIDs and their owners
+  uint32_t t_mode = ~0u;           // the mode the table was dealt in (~0u: none yet)
+  std::vector<uint8_t> t_guid;     // host copy of the table: keys (writer GUIDs, entity keys) and their owners
   std::vector<uint32_t> t_owner;
+  bool t_ent = false;              // the table has entity keys (RTPS_OWNER_TOPIC)
   uint32_t* d_okeys = nullptr;     // device: [ocap * 4] GUID words, open addressing by rt_hash16
   uint32_t* d_oval = nullptr;      // [ocap] owner, 0xffffffff = empty slot
   uint32_t ocap = 0;               // 0: no table (every writer by the GUID hash)

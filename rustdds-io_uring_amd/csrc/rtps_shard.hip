@@ -85,22 +85,33 @@ __device__ __forceinline__ uint32_t item_bytes(uint32_t kind, const Blob& b) {
 
 // The writer -> owner table (rtps_rx_shard_set_owners): a writer in it goes to its owner,
 // any other by the GUID hash.
+// RTPS_OWNER_TOPIC adds entity keys (OWNER_EKEY_PREFIX x 12 || entity id): a writer without a
+// proxy whose entity id some reader contains (its records reach that reader's topic cache,
+// rt_classify's entity sets) goes to the owner of that entity set's group.
 struct OwnerDev {
   const uint32_t* keys;  // nullptr: no table
   const uint32_t* val;
   uint32_t mask;
+  uint32_t ent;          // the table has entity keys
 };
+constexpr uint32_t EKEY_WORD = 0x01010101u * OWNER_EKEY_PREFIX;
+__device__ __forceinline__ uint32_t owner_probe(const OwnerDev& t, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  uint32_t i = rt_hash16(a, b, c, d) & t.mask;
+  for (uint32_t probe = 0; probe <= t.mask; ++probe) {
+    const uint32_t v = t.val[i];
+    if (v == NONE) break;
+    const uint4 k = *reinterpret_cast<const uint4*>(t.keys + 4u * i);
+    if (k.x == a && k.y == b && k.z == c && k.w == d) return v;
+    i = (i + 1u) & t.mask;
+  }
+  return NONE;
+}
 __device__ __forceinline__ uint32_t owner_of_writer(const OwnerDev& t, uint32_t a, uint32_t b, uint32_t c, uint32_t d,
                                                     uint32_t n_dest) {
   if (t.keys) {
-    uint32_t i = rt_hash16(a, b, c, d) & t.mask;
-    for (uint32_t probe = 0; probe <= t.mask; ++probe) {
-      const uint32_t v = t.val[i];
-      if (v == NONE) break;
-      const uint4 k = *reinterpret_cast<const uint4*>(t.keys + 4u * i);
-      if (k.x == a && k.y == b && k.z == c && k.w == d) return v;
-      i = (i + 1u) & t.mask;
-    }
+    uint32_t v = owner_probe(t, a, b, c, d);
+    if (v == NONE && t.ent) v = owner_probe(t, EKEY_WORD, EKEY_WORD, EKEY_WORD, d);
+    if (v != NONE) return v;
   }
   return owner_hash(a, b, c, d) % n_dest;
 }
@@ -480,12 +491,14 @@ int rtps_rx_shard_create(rtps_rx_ctx* ctx, uint32_t n_ranks, uint64_t cap, uint6
     rtps_rx_shard_destroy(s);
     return RTPS_RX_ENOMEM;
   }
+  rtps_ctx_shard_attach(ctx, s, true);
   *out = s;
   return RTPS_RX_OK;
 }
 
 int rtps_rx_shard_destroy(rtps_shard* s) {
   if (!s) return RTPS_RX_EINVAL;
+  rtps_ctx_shard_attach(s->ctx, s, false);
   (void)hipSetDevice(s->device);
   (void)hipDeviceSynchronize();
   void* dev[] = {s->s_slots, s->s_blob, s->s_counts, s->s_spill, s->s_bspill, s->hist, s->hscan, s->r_slots,
@@ -502,11 +515,11 @@ int rtps_rx_shard_destroy(rtps_shard* s) {
   return RTPS_RX_OK;
 }
 
-int rtps_rx_owner_assign(const uint8_t* writers, const uint64_t* weights, const uint32_t* groups, uint32_t n,
-                         uint32_t n_ranks, uint32_t* owners) {
+int rtps_rx_owner_assign_sticky(const uint8_t* writers, const uint64_t* weights, const uint32_t* groups, uint32_t n,
+                                uint32_t n_ranks, const int32_t* prev, uint32_t* owners) {
   if ((n && (!writers || !owners)) || n_ranks < 1) return RTPS_RX_EINVAL;
   for (uint32_t w = 0; w < n; ++w)
-    if (groups && groups[w] >= n) return RTPS_RX_EINVAL;
+    if ((groups && groups[w] >= n) || (prev && prev[w] >= (int32_t)n_ranks)) return RTPS_RX_EINVAL;
   // groups: total weight, smallest member GUID (the tie-break that makes the deal order-free)
   std::vector<uint32_t> gid(n), rep;  // writer -> dense group, group -> its smallest-GUID writer
   std::vector<uint64_t> gw;
@@ -519,15 +532,33 @@ int rtps_rx_owner_assign(const uint8_t* writers, const uint64_t* weights, const 
     gw[k] += weights ? weights[w] : 1u;
     if (memcmp(writers + 16ull * w, writers + 16ull * rep[k], 16) < 0) rep[k] = w;
   }
-  std::vector<uint32_t> order(rep.size());
-  for (uint32_t k = 0; k < order.size(); ++k) order[k] = k;
+  std::vector<uint64_t> load(n_ranks, 0);
+  std::vector<uint32_t> owner_of(rep.size(), NONE);
+  if (prev) {  // sticky: a group with owned members stays where most of its weight is (ties: lowest rank)
+    std::vector<uint64_t> held((size_t)rep.size() * n_ranks, 0);
+    std::vector<uint8_t> any(rep.size(), 0);
+    for (uint32_t w = 0; w < n; ++w)
+      if (prev[w] >= 0) {
+        held[(size_t)gid[w] * n_ranks + (uint32_t)prev[w]] += (weights ? weights[w] : 1u) + 1u;
+        any[gid[w]] = 1;
+      }
+    for (uint32_t k = 0; k < rep.size(); ++k) {
+      if (!any[k]) continue;
+      uint32_t best = 0;
+      for (uint32_t r = 1; r < n_ranks; ++r)
+        if (held[(size_t)k * n_ranks + r] > held[(size_t)k * n_ranks + best]) best = r;
+      owner_of[k] = best;
+      load[best] += gw[k];
+    }
+  }
+  std::vector<uint32_t> order;
+  for (uint32_t k = 0; k < rep.size(); ++k)
+    if (owner_of[k] == NONE) order.push_back(k);
   std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
     if (gw[x] != gw[y]) return gw[x] > gw[y];
     return memcmp(writers + 16ull * rep[x], writers + 16ull * rep[y], 16) < 0;
   });
-  // largest first, each to the least-loaded owner (ties: the lowest rank)
-  std::vector<uint64_t> load(n_ranks, 0);
-  std::vector<uint32_t> owner_of(rep.size());
+  // the new groups: largest first, each to the least-loaded owner (ties: the lowest rank)
   for (uint32_t k : order) {
     uint32_t best = 0;
     for (uint32_t r = 1; r < n_ranks; ++r)
@@ -539,33 +570,74 @@ int rtps_rx_owner_assign(const uint8_t* writers, const uint64_t* weights, const 
   return RTPS_RX_OK;
 }
 
-// (re)build the owner table from the context's readers (and topics) and the caller's writers
-static int owner_table_build(rtps_shard* s) {
-  s->owner_version = rtps_ctx_readers_version(s->ctx);
-  s->t_guid.clear();
-  s->t_owner.clear();
-  if (s->owner_mode != RTPS_OWNER_HASH) {
-    std::vector<uint8_t> g;
-    std::vector<uint32_t> grp;
-    rtps_ctx_owner_writers(s->ctx, s->owner_mode == RTPS_OWNER_TOPIC, g, grp);
-    std::vector<uint64_t> wt(grp.size(), 1u);
-    for (size_t x = 0; x < s->x_weight.size(); ++x) {  // the caller's writers: weight known ones, add the rest
-      const uint8_t* q = s->x_guid.data() + 16 * x;
-      size_t w = 0;
-      while (w < grp.size() && memcmp(g.data() + 16 * w, q, 16) != 0) ++w;
-      if (w == grp.size()) {
-        g.insert(g.end(), q, q + 16);
-        grp.push_back((uint32_t)w);
-        wt.push_back(0);
-      }
-      wt[w] = s->x_weight[x];
+int rtps_rx_owner_assign(const uint8_t* writers, const uint64_t* weights, const uint32_t* groups, uint32_t n,
+                         uint32_t n_ranks, uint32_t* owners) {
+  return rtps_rx_owner_assign_sticky(writers, weights, groups, n, n_ranks, nullptr, owners);
+}
+
+}  // extern "C"
+
+// the mode the table follows: the caller's, else RTPS_OWNER_TOPIC once the context has topics
+// (the topic caches' GC needs every writer of a topic on one owner), else RTPS_OWNER_BALANCED
+static uint32_t effective_mode(const rtps_shard* s) {
+  if (s->mode_explicit) return s->owner_mode;
+  return rtps_ctx_topics_configured(s->ctx) ? RTPS_OWNER_TOPIC : RTPS_OWNER_BALANCED;
+}
+static bool owner_stale(const rtps_shard* s) {
+  const uint32_t m = effective_mode(s);
+  return m != s->t_mode || (m != RTPS_OWNER_HASH && s->owner_version != rtps_ctx_readers_version(s->ctx));
+}
+bool rtps_shard_splits_topics(const rtps_shard* s) { return s->n_ranks > 1 && effective_mode(s) != RTPS_OWNER_TOPIC; }
+
+// The owner table for the context's current readers (and topics) and the caller's writers.
+// Sticky: a key the previous table (same mode) held keeps its owner, so that its writer
+// proxy, far set, DataFrag assemblies and topic-cache changes stay where they are; new keys
+// are dealt onto the ranks' loads.  Only a group that joins keys of different owners (a topic
+// linking them, RTPS_OWNER_TOPIC) moves some, to where most of its weight already is.
+static int owner_table_compute(const rtps_shard* s, bool fresh, std::vector<uint8_t>& g, std::vector<uint32_t>& own,
+                               bool& ent) {
+  const uint32_t mode = effective_mode(s);
+  g.clear();
+  own.clear();
+  ent = false;
+  if (mode == RTPS_OWNER_HASH) return RTPS_RX_OK;
+  std::vector<uint32_t> grp;
+  rtps_ctx_owner_keys(s->ctx, mode == RTPS_OWNER_TOPIC, g, grp);
+  ent = mode == RTPS_OWNER_TOPIC;
+  std::vector<uint64_t> wt(grp.size(), 1u);
+  for (size_t x = 0; x < s->x_weight.size(); ++x) {  // the caller's writers: weight known ones, add the rest
+    const uint8_t* q = s->x_guid.data() + 16 * x;
+    size_t w = 0;
+    while (w < grp.size() && memcmp(g.data() + 16 * w, q, 16) != 0) ++w;
+    if (w == grp.size()) {
+      g.insert(g.end(), q, q + 16);
+      grp.push_back((uint32_t)w);
+      wt.push_back(0);
     }
-    std::vector<uint32_t> own(grp.size());
-    const int rc = rtps_rx_owner_assign(g.data(), wt.data(), grp.data(), (uint32_t)grp.size(), s->n_ranks, own.data());
-    if (rc) return rc;
-    s->t_guid.swap(g);
-    s->t_owner.swap(own);
+    wt[w] = s->x_weight[x];
   }
+  std::vector<int32_t> prev(grp.size(), -1);
+  if (!fresh && mode == s->t_mode)
+    for (size_t w = 0; w < grp.size(); ++w)
+      for (size_t k = 0; k < s->t_owner.size(); ++k)
+        if (memcmp(g.data() + 16 * w, s->t_guid.data() + 16 * k, 16) == 0) { prev[w] = (int32_t)s->t_owner[k]; break; }
+  own.resize(grp.size());
+  return rtps_rx_owner_assign_sticky(g.data(), wt.data(), grp.data(), (uint32_t)grp.size(), s->n_ranks, prev.data(),
+                                     own.data());
+}
+
+// (re)build the owner table and upload it
+static int owner_table_build(rtps_shard* s, bool fresh) {
+  std::vector<uint8_t> g;
+  std::vector<uint32_t> own;
+  bool ent = false;
+  const int rc = owner_table_compute(s, fresh, g, own, ent);
+  if (rc) return rc;
+  s->owner_version = rtps_ctx_readers_version(s->ctx);
+  s->t_mode = effective_mode(s);
+  s->t_guid.swap(g);
+  s->t_owner.swap(own);
+  s->t_ent = ent;
   const uint32_t n = (uint32_t)s->t_owner.size();
   uint32_t cap = 0;
   if (n) {
@@ -599,25 +671,41 @@ static int owner_table_build(rtps_shard* s) {
   return RTPS_RX_OK;
 }
 
+extern "C" {
+
 int rtps_rx_shard_set_owners(rtps_shard* s, uint32_t mode, const uint8_t* guids, const uint64_t* weights,
                              uint32_t n) {
   if (!s || mode > RTPS_OWNER_TOPIC || (n && (!guids || !weights))) return RTPS_RX_EINVAL;
   (void)hipSetDevice(s->device);
   s->owner_mode = mode;
+  s->mode_explicit = true;
   s->x_guid.assign(guids, guids + 16ull * n);
   s->x_weight.assign(weights, weights + n);
-  return owner_table_build(s);
+  return owner_table_build(s, true);  // an explicit deal starts afresh (documented: moved writers' state stays behind)
 }
 
 int rtps_rx_shard_owner(rtps_shard* s, const uint8_t guid[16]) {
   if (!s || !guid) return RTPS_RX_EINVAL;
-  if (s->owner_mode != RTPS_OWNER_HASH && s->owner_version != rtps_ctx_readers_version(s->ctx)) {
-    (void)hipSetDevice(s->device);
-    const int rc = owner_table_build(s);
+  // a stale table is answered from the table the next pack will build, without committing it,
+  // so that a query never changes the deal's history (every rank must build the same tables)
+  std::vector<uint8_t> tg;
+  std::vector<uint32_t> to;
+  bool ent = s->t_ent;
+  const std::vector<uint8_t>* g = &s->t_guid;
+  const std::vector<uint32_t>* o = &s->t_owner;
+  if (owner_stale(s)) {
+    const int rc = owner_table_compute(s, false, tg, to, ent);
     if (rc) return rc;
+    g = &tg;
+    o = &to;
   }
-  for (size_t w = 0; w < s->t_owner.size(); ++w)
-    if (memcmp(s->t_guid.data() + 16 * w, guid, 16) == 0) return (int)s->t_owner[w];
+  for (int pass = 0; pass < (ent ? 2 : 1); ++pass) {
+    uint8_t key[16];
+    memcpy(key, guid, 16);
+    if (pass) memset(key, OWNER_EKEY_PREFIX, 12);
+    for (size_t w = 0; w < o->size(); ++w)
+      if (memcmp(g->data() + 16 * w, key, 16) == 0) return (int)(*o)[w];
+  }
   uint32_t k[4];
   memcpy(k, guid, 16);
   uint32_t h = 0x811c9dc5u;  // owner_hash on the host
@@ -633,11 +721,11 @@ int rtps_rx_shard_pack(rtps_shard* s, const uint8_t* arena, uint64_t arena_len, 
   if (!s || !records || !n_records || (max_records && (!arena || !dgram_off))) return RTPS_RX_EINVAL;
   (void)hipSetDevice(s->device);
   hipStream_t st = rtps_ctx_stream(s->ctx);
-  if (s->owner_mode != RTPS_OWNER_HASH && s->owner_version != rtps_ctx_readers_version(s->ctx)) {
-    const int rc = owner_table_build(s);  // the readers changed: the table follows them
+  if (owner_stale(s)) {
+    const int rc = owner_table_build(s, false);  // the readers (or topics) changed: the table follows them
     if (rc) return rc;
   }
-  const OwnerDev ot{s->ocap ? s->d_okeys : nullptr, s->d_oval, s->ocap ? s->ocap - 1u : 0u};
+  const OwnerDev ot{s->ocap ? s->d_okeys : nullptr, s->d_oval, s->ocap ? s->ocap - 1u : 0u, s->t_ent ? 1u : 0u};
   const uint32_t n = s->n_ranks;
   const uint64_t tiles = (max_records + ST - 1) / ST;
   if (tiles > 0xffffffffull) return RTPS_RX_ETOOBIG;

@@ -28,6 +28,8 @@ int rtps_topic_reset(TopicState* s, hipStream_t st);
 int rtps_topic_proxies_reset(TopicState* s, hipStream_t st);
 // DDSCache::garbage_collect.
 int rtps_topic_gc(TopicState* s, hipStream_t st);
+// Topics rtps_rx_set_topics configured (0: every reader slot its own cache).
+uint32_t rtps_topic_n_configured(const TopicState* s);
 // The topic cache a reader slot's changes go to (its configured topic, else its own).
 uint32_t rtps_topic_of_slot(const TopicState* s, uint16_t slot);
 // TopicCache::add_change for every delivery of the batch, in order: sets or clears

@@ -751,6 +751,7 @@ int rtps_topic_proxies_reset(TopicState* s, hipStream_t st) {
 }
 
 uint32_t rtps_topic_of_slot(const TopicState* s, uint16_t slot) { return tid_of(s, slot); }
+uint32_t rtps_topic_n_configured(const TopicState* s) { return s->n_cfg; }
 
 int rtps_topic_gc(TopicState* s, hipStream_t st) {
   if (!s->I) return RTPS_RX_OK;

@@ -339,10 +339,11 @@ def shard_lib():
         L.rtps_rx_shard_set_owners.argtypes = [P, U32, P, P, U32]
         L.rtps_rx_shard_owner.argtypes = [P, P]
         L.rtps_rx_owner_assign.argtypes = [P, P, P, U32, U32, P]
+        L.rtps_rx_owner_assign_sticky.argtypes = [P, P, P, U32, U32, P, P]
         for f in ("rtps_rx_shard_create", "rtps_rx_shard_destroy", "rtps_rx_shard_pack", "rtps_rx_shard_exchange",
                   "rtps_rx_shard_finish", "rtps_rx_shard_unpack", "rtps_rx_shard_buffers",
                   "rtps_rx_shard_reserve_spill", "rtps_rx_shard_set_owners", "rtps_rx_shard_owner",
-                  "rtps_rx_owner_assign"):
+                  "rtps_rx_owner_assign", "rtps_rx_owner_assign_sticky"):
             getattr(L, f).restype = ctypes.c_int
         L._shard_bound = True
     return L
@@ -351,17 +352,23 @@ def shard_lib():
 OWNER_BALANCED, OWNER_HASH, OWNER_TOPIC = 0, 1, 2  # rtps_rx_shard_set_owners modes
 
 
-def owner_assign(writers, n_ranks, weights=None, groups=None):
+def owner_assign(writers, n_ranks, weights=None, groups=None, prev=None):
     """rtps_rx_owner_assign (host, no GPU): writers = list of 16-byte GUIDs -> owner rank of each.
-    Groups (list of group ids < n, optional) share an owner; weights (optional) per writer."""
+    Groups (list of group ids < n, optional) share an owner; weights (optional) per writer;
+    prev (optional, rtps_rx_owner_assign_sticky): each writer's previous owner, -1 = new."""
     from . import _check
     n = len(writers)
     w = _np.frombuffer(b"".join(bytes(g) for g in writers), dtype=_np.uint8) if n else _np.zeros(16, _np.uint8)
     wt = None if weights is None else _np.ascontiguousarray(weights, dtype=_np.uint64)
     gr = None if groups is None else _np.ascontiguousarray(groups, dtype=_np.uint32)
     out = _np.zeros(max(n, 1), dtype=_np.uint32)
-    _check(shard_lib().rtps_rx_owner_assign(w.ctypes.data, None if wt is None else wt.ctypes.data,
-                                            None if gr is None else gr.ctypes.data, n, n_ranks, out.ctypes.data))
+    args = (w.ctypes.data, None if wt is None else wt.ctypes.data, None if gr is None else gr.ctypes.data, n, n_ranks)
+    if prev is None:
+        _check(shard_lib().rtps_rx_owner_assign(*args, out.ctypes.data))
+    else:
+        pv = _np.ascontiguousarray(prev, dtype=_np.int32)
+        assert len(pv) == n
+        _check(shard_lib().rtps_rx_owner_assign_sticky(*args, pv.ctypes.data if n else None, out.ctypes.data))
     return out[:n]
 
 

@@ -87,14 +87,73 @@ def balanced_owner_table(guids, world):
     return dict(zip(guids, (int(x) for x in owner_assign(guids, world))))
 
 
+EKEY = b"\xff" * 12  # an entity key's prefix (RTPS_OWNER_TOPIC: writers without a proxy, by entity id)
+
+
+def topic_owner_keys(readers, topic_readers=()):
+    """Python restatement of rtps_ctx_owner_keys(by_topic) over a Readers table: the keys (writer
+    GUIDs of the writer sets in first-appearance order, then EKEY || entity id per entity set)
+    and each key's group (the smallest key index of its group): keys whose target readers share
+    a topic cache (topic_readers [(slot, topic)], else the reader's own) are one group."""
+    from rtps_rx.records import as_readers, READER_STATELESS
+    rd = as_readers(readers)
+    flags = [int(r["flags"]) for r in rd.readers]
+    slot = [int(r["reader_slot"]) for r in rd.readers]
+    contains = [set() for _ in rd.readers]
+    wsets = []
+    for p in rd.proxies:
+        r, g = int(p["reader"]), bytes(p["writer_guid"])
+        if flags[r] & READER_STATELESS:
+            continue
+        contains[r].add(g[12:])
+        if g not in wsets:
+            wsets.append(g)
+    esets = []
+    for g in wsets:
+        if g[12:] not in esets:
+            esets.append(g[12:])
+    keys = wsets + [EKEY + e for e in esets]
+    topic_of = dict(topic_readers)
+    group = list(range(len(keys)))
+
+    def root(x):
+        while group[x] != x:
+            x = group[x]
+        return x
+    first_key = {}
+    for w, k in enumerate(keys):
+        for r in range(len(slot)):
+            if flags[r] & READER_STATELESS or k[12:] not in contains[r]:
+                continue
+            t = topic_of.get(slot[r], ("own", slot[r]))
+            if t not in first_key:
+                first_key[t] = w
+                continue
+            a, b = root(w), root(first_key[t])
+            if a != b:
+                group[max(a, b)] = min(a, b)
+    return keys, [root(w) for w in range(len(keys))]
+
+
+def topic_owner_table(readers, topic_readers, world, prev=None):
+    """The shard's RTPS_OWNER_TOPIC table: {16-byte key: owner} (prev: {key: owner} of the
+    previous table, the sticky deal)."""
+    from rtps_rx.shard import owner_assign
+    keys, groups = topic_owner_keys(readers, topic_readers)
+    pv = None if prev is None else [prev.get(k, -1) for k in keys]
+    return dict(zip(keys, (int(x) for x in owner_assign(keys, world, groups=groups, prev=pv))))
+
+
 def shard_items(recs, world, table=None):
     """Owner of every record that is an item (writer kinds with ROUTE_PASS), else -1: the
-    writer's owner in `table` ({GUID: owner}, the shard's owner table), else the GUID hash."""
+    writer's owner in `table` ({GUID: owner}, the shard's owner table), else (entity keys in
+    the table) its entity id's owner, else the GUID hash."""
     from rtps_rx.records import ROUTE_PASS
     o = owner_np(recs, world)
     if table:
         g = recs.view(np.uint8).reshape(-1, 64)[:, 8:24]
-        o = np.array([table.get(bytes(x), int(h)) for x, h in zip(g, o)], dtype=np.int64)
+        o = np.array([table.get(bytes(x), table.get(EKEY + bytes(x)[12:], int(h))) for x, h in zip(g, o)],
+                     dtype=np.int64)
     writer = np.isin(recs["kind"], WRITER_KINDS) & ((recs["route"] & ROUTE_PASS) != 0)
     return np.where(writer, o, -1)
 

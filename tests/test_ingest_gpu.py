@@ -304,6 +304,40 @@ def test_late_joiner_gap_threshold(rx):
     assert ack.tolist()[0] == top + 2 * W + 1
 
 
+@pytest.mark.parametrize("case", ["samples", "samples_hb", "hb_only", "small_gap", "two_chunks"])
+def test_gap_threshold_moved_in_batch(rx, case):
+    """a GAP whose range starts above all_ackable_before as it was at the
+    batch's start, but at or below it when the GAP arrives (the batch's own DATA, HEARTBEAT or
+    GAPs moved it), is irrelevant_changes_range's jump (rtps_writer_proxy.rs:241-292), not a
+    range to insert SN by SN: DATA 1..5 then GAP [6, 10^6) in one batch; with a HEARTBEAT
+    firstSN 100 before a GAP [50, 10^6); a small GAP closing the hole; 3000 samples so that the
+    GAP sits in the per-proxy kernel's second chunk.  Bit-exact with the oracle and nothing
+    counted in n_window_overflow (_batch), samples after the GAP decided against it."""
+    top = 1_000_000
+    w0, w1 = R.writer_key(0), R.writer_key(1)
+    tbl = pack_match_table([(R.PREFIXES[0] + w0, 0), (R.PREFIXES[0] + w1, 1)])
+    rx.set_match_table(tbl)
+    ing = oracle.HistoryIngest(tbl)
+    D = lambda sn: R.data_sub(w0, sn)
+    if case == "samples":
+        subs = [D(k) for k in range(1, 6)] + [R.gap_sub(w0, 6, top, [True, False, True])]
+    elif case == "samples_hb":
+        subs = [D(k) for k in range(1, 6)] + [R.hb_sub(w0, 100, 120, 1), R.gap_sub(w0, 50, top, [])]
+    elif case == "hb_only":
+        subs = [R.hb_sub(w0, 100, 120, 1), D(99), R.gap_sub(w0, 6, top, [])]
+    elif case == "small_gap":
+        subs = [D(1), D(2), D(3), R.gap_sub(w0, 4, 8, []), R.gap_sub(w0, 8, top, [False, True])]
+    else:
+        subs = [D(k) for k in range(1, 3001)] + [R.gap_sub(w0, 3001, top, [])]
+    subs += [D(7), D(60), D(top - 1), D(top), D(top + 1), D(top + 1), R.data_sub(w1, 4), D(top + 3)]
+    dg = [R.datagram(R.PREFIXES[0], subs[i:i + 3]) for i in range(0, len(subs), 3)]
+    acc, dels, ack = _batch(rx, ing, tbl, dg, case)
+    assert ack.tolist()[0] == (top + 4 if case == "samples" else top + 2)  # (the oracle's: the jump happened)
+    # a second batch: the new all_ackable_before holds (below it rejected, above accepted once)
+    dg = [R.datagram(R.PREFIXES[0], [D(top - 5), D(top + 2), D(top + 2), D(top + 4)])]
+    _batch(rx, ing, tbl, dg, case + " next")
+
+
 def test_far_pool_out_counted(rx):
     """The one capacity left: a GAP covering more SNs past the window than the far-set pool
     keeps free (here 2^34) cannot be recorded SN by SN; that proxy's far samples of the batch

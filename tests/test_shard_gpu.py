@@ -138,6 +138,101 @@ def test_owner_table_modes(rx, world):
         rx.set_match_table([])
 
 
+def test_owner_table_sticky_device(rx):
+    """the default table follows the readers STICKILY.  A writer whose GUID
+    sorts before every other joins the readers; the next pack keeps every earlier writer's
+    owner (owner_of answers the pending table the same way before the pack commits it), the
+    newcomer goes to the least-loaded rank, and the device pack equals the model with that table."""
+    from rtps_rx.shard import OwnerShard, dev_to_numpy
+    arena, off, ln = oracle.gen(oracle.WL_T, 8000)
+    _, r0, _, _ = oracle.parse(arena, off, ln)
+    guids = sorted({bytes(x["prefix"]) + bytes(x["writer_id"]) for x in r0})
+    world = 4
+    A, O, outs = _device_batch(rx, arena, off, ln, pack_match_table([(g, 100) for g in guids]))
+    sh = OwnerShard(rx, world, None, torch.device("cuda", 0), len(r0) + 16, 1 << 20)
+    try:
+        sh.pack(A, O, outs)
+        rx.sync()
+        before = {g: sh.owner_of(g) for g in guids}
+        assert before == balanced_owner_table(guids, world)
+        first = b"\x00" * 12 + bytes([0, 0, 1, 2])
+        tbl = pack_match_table([(first, 100)] + [(g, 100) for g in guids])
+        rx.set_match_table(tbl)
+        assert {g: sh.owner_of(g) for g in guids} == before  # pending table, not committed
+        sh.pack(A, O, outs)
+        rx.sync()
+        assert {g: sh.owner_of(g) for g in guids} == before
+        load = np.bincount(list(before.values()), minlength=world)
+        assert sh.owner_of(first) == int(np.argmin(load))
+        table = dict(before)
+        table[first] = sh.owner_of(first)
+        _, recs, _, _ = oracle.parse(arena, off, ln, match_table=tbl)
+        exp = shard_pack_np(arena, off, recs, world, len(r0) + 16, 1 << 20, table)
+        counts = dev_to_numpy(sh.buffers().send_counts, 32 * world, COUNTS_DTYPE)
+        assert counts.tobytes() == np.concatenate([e["counts"] for e in exp]).tobytes()
+    finally:
+        sh.close()
+        rx.set_match_table([])
+
+
+def test_owner_topic_default_and_refusal(rx):
+    """once topics are set, the shard's default deal is RTPS_OWNER_TOPIC: its
+    table (writer GUIDs and entity keys) equals tests/shard_ref.topic_owner_table, a writer
+    without a proxy follows its entity id's group, and the device pack equals the model.  Under
+    an explicit RTPS_OWNER_BALANCED deal over 2 ranks the ingest refuses the topic caches
+    (RTPS_RX_EINVAL); a one-rank shard and RTPS_OWNER_TOPIC take them."""
+    import rtps_rx
+    from rtps_rx.shard import OwnerShard, dev_to_numpy, OWNER_BALANCED, OWNER_TOPIC
+    from shard_ref import topic_owner_table, EKEY
+    from test_shard_owner_cpu import _topic_setup
+    import ingest_ref as R
+    tbl, topics, dgrams = _topic_setup()
+    arena, off, ln = oracle.pack(dgrams[:2000], align=16)
+    rx.set_readers(tbl)
+    rx.set_topics(*topics)
+    dev = torch.device("cuda", 0)
+    A = torch.from_numpy(arena).to(dev)
+    O = torch.from_numpy(off.view(np.int64)).to(dev)
+    L = torch.from_numpy(ln.view(np.int32)).to(dev)
+    outs = rx.alloc_outputs(len(ln), max_records(ln))
+    rx.parse_batch_device(A, O, L, len(ln), outs)
+    rx.sync()
+    _, recs, _, _ = oracle.parse(arena, off, ln, match_table=tbl)
+    sh = OwnerShard(rx, 2, None, dev, len(recs), 1 << 20)
+    one = None
+    try:
+        table = topic_owner_table(tbl, topics[1], 2)
+        for k, v in table.items():
+            if not k.startswith(EKEY):
+                assert sh.owner_of(k) == v, k
+        stray = R.PREFIXES[2] + R.BUILTIN_KIND_KEY  # no proxy: by its entity id's group
+        assert sh.owner_of(stray) == table[EKEY + R.BUILTIN_KIND_KEY]
+        sh.pack(A, O, outs)
+        rx.sync()
+        exp = shard_pack_np(arena, off, recs, 2, len(recs), 1 << 20, table)
+        counts = dev_to_numpy(sh.buffers().send_counts, 64, COUNTS_DTYPE)
+        assert counts.tobytes() == np.concatenate([e["counts"] for e in exp]).tobytes()
+        rx.ingest_batch(arena, off, ln, tbl.n_proxies, topic_cache=True)  # TOPIC (the default): accepted
+        sh.set_owners(OWNER_BALANCED)
+        with pytest.raises(rtps_rx.RtpsRxError):
+            rx.ingest_batch(arena, off, ln, tbl.n_proxies, topic_cache=True)
+        rx.ingest_batch(arena, off, ln, tbl.n_proxies)  # without the topic caches: fine
+        sh.set_owners(OWNER_TOPIC)
+        rx.ingest_batch(arena, off, ln, tbl.n_proxies, topic_cache=True)
+        sh.close()
+        one = OwnerShard(rx, 1, None, dev, len(recs), 1 << 20)
+        one.set_owners(OWNER_BALANCED)
+        rx.ingest_batch(arena, off, ln, tbl.n_proxies, topic_cache=True)  # one rank splits nothing
+    finally:
+        sh.close()
+        if one is not None:
+            one.close()
+        rx.set_topics([], [])
+        rx.ingest_reset()
+        rx.topic_reset()
+        rx.set_match_table([])
+
+
 @pytest.mark.parametrize("wl", ["C3", "C4"])
 @pytest.mark.parametrize("small", [False, True])
 def test_unpack_matches_model(rx, wl, small):

@@ -22,7 +22,8 @@ import torch.multiprocessing as mp
 import oracle
 from rtps_rx.records import RECORD_DTYPE, DELIVERY_DTYPE, FRAG_SAMPLE_DTYPE, pack_match_table, WRITER_KINDS
 from rtps_rx.shard import spill_plan
-from shard_ref import COUNTS_DTYPE, ITEM_DTYPE, balanced_owner_table, shard_pack_np, shard_unpack_np
+from shard_ref import COUNTS_DTYPE, ITEM_DTYPE, balanced_owner_table, shard_pack_np, shard_unpack_np, \
+    topic_owner_table
 
 C5_STRIDE = 8 << 20  # rank r's chunk starts at generator index r * 8M (BASELINE C5: 64M over 8 GPUs)
 
@@ -34,6 +35,8 @@ def _free_port():
 
 
 def _chunk(wl, rank, n, stride):
+    if isinstance(wl, list):  # a datagram list: rank r's chunk is datagrams [r n, (r + 1) n)
+        return oracle.pack(wl[rank * n:(rank + 1) * n], align=16)
     return oracle.gen(wl, n, first_idx=rank * stride)
 
 
@@ -83,14 +86,14 @@ def _a2a(send, recv, ss=None, rs=None):
     dist.all_to_all_single(out, torch.from_numpy(np.ascontiguousarray(send)), rs, ss)
 
 
-def _worker(rank, world, port, wl, n, stride, cap, bcap, tbl, q):
+def _worker(rank, world, port, wl, n, stride, cap, bcap, tbl, q, topics=None, table=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         arena, off, ln = _chunk(wl, rank, n, stride)
         _, recs, _, _ = oracle.parse(arena, off, ln, match_table=tbl)
-        # the shard's default owner table (RTPS_OWNER_BALANCED): the table's writers dealt evenly
-        table = balanced_owner_table([bytes(t["writer_guid"]) for t in tbl], world)
+        if table is None:  # the shard's default owner table (RTPS_OWNER_BALANCED): the table's writers dealt evenly
+            table = balanced_owner_table([bytes(t["writer_guid"]) for t in tbl], world)
         packed = shard_pack_np(arena, off, recs, world, cap, bcap, table)
         slots, blob, sc, sspill, sbspill = _layout(packed, world, cap, bcap)
         # round 0: counts, slots, blob slots (equal splits)
@@ -124,18 +127,23 @@ def _worker(rank, world, port, wl, n, stride, cap, bcap, tbl, q):
         samples = fa.batch_readers(oarena, ooff, orecs, tbl)[0]
         ing = oracle.HistoryIngest(tbl)
         acc, dels, ack = ing.batch(oarena, ooff, orecs, samples)
+        if topics is not None:  # the owner's topic caches over its deliveries (TopicCache::add_change)
+            dels = oracle.TopicCaches(*topics).apply(orecs, dels)
         q.put((rank, dels.tobytes(), ack.tobytes(), orank.tobytes(), osrc.tobytes(),
                samples.tobytes(), int(sum(p["recv_rec"][1] for p in plan)), len(orecs)))
     finally:
         dist.destroy_process_group()
 
 
-def _run(world, wl, n, stride, cap, bcap):
-    tbl = _table(wl, world, n, stride)
+def _run(world, wl, n, stride, cap, bcap, tbl=None, topics=None, table=None, check_flags=True):
+    """-> (items that crossed in the spill, items): every owner's deliveries, ack_base and (with
+    topics = (topics, topic_readers)) DELIVERY_CACHED flags against one oracle over the stream;
+    with check_flags=False, the number of (record, reader) pairs whose flags differ instead."""
+    tbl = _table(wl, world, n, stride) if tbl is None else tbl
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, wl, n, stride, cap, bcap, tbl, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, wl, n, stride, cap, bcap, tbl, q, topics, table))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -151,6 +159,8 @@ def _run(world, wl, n, stride, cap, bcap):
     _, recs, _, rb = oracle.parse(a, o, l, match_table=tbl)
     samples = oracle.FragAssembler().batch_readers(a, o, recs, tbl)[0]
     _, dels, ack = oracle.HistoryIngest(tbl).batch(a, o, recs, samples)
+    if topics is not None:
+        dels = oracle.TopicCaches(*topics).apply(recs, dels)
     # origin = (source rank, record index in that rank's parse); rank r parsed datagrams [r n, (r+1) n)
     first_rec = np.searchsorted(recs["dgram_idx"], np.arange(world) * n)
     got, spilled, items = [], 0, 0
@@ -163,16 +173,19 @@ def _run(world, wl, n, stride, cap, bcap):
         items += ni
         for x in d:
             j = int(x["rec_idx"])
-            got.append((int(first_rec[int(orank[j])]) + int(osrc[j]), int(x["reader_slot"])))
+            got.append((int(first_rec[int(orank[j])]) + int(osrc[j]), int(x["reader_slot"]), int(x["flags"])))
         k = np.frombuffer(k, np.int64)
         moved = k != 1
         assert not (moved & (owner_ack != 1)).any(), "two owners advanced one proxy"
         owner_ack[moved] = k[moved]
     got.sort(key=lambda t: t[0])  # stable: set order inside a record
-    exp = [(int(x["rec_idx"]), int(x["reader_slot"])) for x in dels]
-    assert got == exp, (len(got), len(exp))
+    exp = [(int(x["rec_idx"]), int(x["reader_slot"]), int(x["flags"])) for x in dels]
+    assert [g[:2] for g in got] == [e[:2] for e in exp], (len(got), len(exp))
     assert np.array_equal(owner_ack, ack)
     assert len(exp) > 0
+    if not check_flags:
+        return sum(g[2] != e[2] for g, e in zip(got, exp))
+    assert got == exp, [(g, e) for g, e in zip(got, exp) if g != e][:5]
     return spilled, items
 
 
@@ -278,3 +291,91 @@ def test_owner_assign_order_free_groups_and_weights():
     own2 = owner_assign([writers[i] for i in perm], 5, weights[perm], groups[perm])
     assert [int(x) for x in own2] == [int(own[i]) for i in perm]
     assert list(owner_assign(writers, 1)) == [0] * 40
+
+
+def _topic_setup():
+    """Readers on three topic caches that a writer split would break (structure/dds_cache.rs:210-276,
+    367-420): topic 1 (two reliable readers, max_keep 4) fed by four writers; topic 2, the SPDP
+    participant reader (accepts duplicates, reader.rs:712-722, max_keep 3) on two writers; topic 3
+    (max_keep 3) on a user writer and a builtin-kind entity whose writers without a proxy are
+    accepted by entity id (reader.rs:734-739): their records reach topic 3 through an entity set."""
+    import ingest_ref as R
+    from rtps_rx.records import Readers
+    P, wk, B = R.PREFIXES, R.writer_key, R.BUILTIN_KIND_KEY
+    readers = [(bytes([0, 0, 1, 7]), 10, 0), (bytes([0, 0, 2, 7]), 11, 0), (R.SPDP_PARTICIPANT_READER, 14, 0),
+               (bytes([0, 0, 3, 7]), 12, 0)]
+    proxies = [(P[0] + wk(0), 0), (P[1] + wk(0), 0), (P[2] + wk(1), 0), (P[3] + wk(2), 1),
+               (P[0] + wk(3), 2), (P[2] + wk(3), 2),
+               (P[1] + wk(4), 3), (P[0] + B, 3)]
+    topics = ([(1, 4), (2, 3), (3, 3)], [(10, 1), (11, 1), (14, 2), (12, 3)])
+    # every writer key from every prefix: proxied writers, and the same entity ids without a proxy
+    dgrams = R.stream(4000, 17, sn_hi=200, n_prefix=4, keys=[wk(k) for k in range(5)] + [B])
+    return Readers(readers, proxies), topics, dgrams
+
+
+def test_owner_topic_caches_two_ranks():
+    """VERDICT r5 missing 2: topic caches on owner batches.  Each topic is fed by writers from
+    both source ranks; with the RTPS_OWNER_TOPIC table (writer GUIDs and entity keys grouped by
+    topic, tests/shard_ref.topic_owner_table) every owner's DELIVERY_CACHED flags equal one
+    oracle run (proxies + TopicCache::add_change) over the whole stream.  The balanced deal of
+    the same writers splits the topics, and its flags differ: the test can see a wrong table."""
+    tbl, topics, dgrams = _topic_setup()
+    table = topic_owner_table(tbl, topics[1], 2)
+    assert len(set(table.values())) == 2  # the three topic groups use both owners
+    _run(2, dgrams, 2000, 0, cap=20000, bcap=1 << 20, tbl=tbl, topics=topics, table=table)
+    writers = sorted({bytes(p["writer_guid"]) for p in tbl.proxies})
+    split = _run(2, dgrams, 2000, 0, cap=20000, bcap=1 << 20, tbl=tbl, topics=topics,
+                 table=balanced_owner_table(writers, 2), check_flags=False)
+    assert split > 0
+    # without the entity keys the builtin-kind writers without a proxy go by the hash and split topic 3
+    from shard_ref import EKEY
+    no_ent = {k: v for k, v in table.items() if not k.startswith(EKEY)}
+    assert _run(2, dgrams, 2000, 0, cap=20000, bcap=1 << 20, tbl=tbl, topics=topics, table=no_ent,
+                check_flags=False) > 0
+
+
+def test_topic_owner_table_groups():
+    """The topic table's keys and groups: every writer set and entity set of a topic on one owner."""
+    from shard_ref import topic_owner_keys, EKEY
+    tbl, topics, _ = _topic_setup()
+    keys, groups = topic_owner_keys(tbl, topics[1])
+    assert sum(k.startswith(EKEY) for k in keys) == 6  # entity ids wk0..wk4 and the builtin kind
+    assert len(set(groups)) == 3
+    table = topic_owner_table(tbl, topics[1], 3)
+    assert sorted(set(table.values())) == [0, 1, 2]
+
+
+def test_owner_assign_sticky():
+    """a writer that sorts first joins the table; every writer the previous
+    table held keeps its owner (its proxy state lives there), and the newcomer goes to the
+    least-loaded rank.  Without prev the deal moves most of them."""
+    from rtps_rx.shard import owner_assign
+    rng = np.random.default_rng(11)
+    writers = sorted(bytes(rng.integers(1, 256, 16, dtype=np.uint8)) for _ in range(16))
+    for world in (2, 4, 8):
+        own = [int(x) for x in owner_assign(writers, world)]
+        new = [b"\x00" * 16] + writers
+        fresh = [int(x) for x in owner_assign(new, world)]
+        assert sum(a != b for a, b in zip(fresh[1:], own)) >= len(own) // 2  # the hazard ADVICE names
+        sticky = [int(x) for x in owner_assign(new, world, prev=[-1] + own)]
+        assert sticky[1:] == own
+        load = np.bincount(own, minlength=world)
+        assert sticky[0] == int(np.argmin(load))
+        assert list(owner_assign(new, world, prev=[-1] * len(new))) == fresh  # nothing owned: the plain deal
+
+
+def test_owner_assign_sticky_groups():
+    """Sticky groups: a group whose members are owned stays on the rank holding most of their
+    weight (each owned member counts weight + 1; ties: the lowest rank); only the minority moves."""
+    from rtps_rx.shard import owner_assign
+    w = [bytes([k]) * 16 for k in range(1, 7)]
+    # writers 0, 1 on rank 1, writer 2 on rank 0; a topic now joins 0, 1, 2; 3 new; 4, 5 kept
+    prev = [1, 1, 0, -1, 0, 1]
+    groups = [0, 0, 0, 3, 4, 5]
+    out = [int(x) for x in owner_assign(w, 2, groups=groups, prev=prev)]
+    assert out[:3] == [1, 1, 1] and out[4] == 0 and out[5] == 1
+    # loads after the kept groups: rank 0 = 1 (writer 4), rank 1 = 4: the new writer goes to 0
+    assert out[3] == 0
+    # weights decide the majority
+    out = [int(x) for x in owner_assign(w, 2, weights=[1, 1, 9, 1, 1, 1], groups=groups, prev=prev)]
+    assert out[:3] == [0, 0, 0]
