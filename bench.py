@@ -332,6 +332,227 @@ def full_chain(rx, workload, arena, off_t, ln_t, n, n_rec, n_entries, reps=5):
     return res
 
 
+def pcie_probe(h2d_bytes, d2h_bytes, dev, reps=3, chunk=128 << 20):
+    """Pinned-memory PCIe rates of this box: h2d_bytes host -> device alone, d2h_bytes device ->
+    host alone, and both at once (full duplex: the H2D chunks on one stream, the D2H chunks on
+    another, issued interleaved as a receive pipeline issues them): the bound of a host-to-host
+    chain that moves those bytes.  Copies of `chunk` bytes; best of `reps` wall-clock runs."""
+    hs = torch.empty(h2d_bytes, dtype=torch.uint8, pin_memory=True)
+    hd = torch.empty(d2h_bytes, dtype=torch.uint8, pin_memory=True)
+    ds = torch.empty(h2d_bytes, dtype=torch.uint8, device=dev)
+    dd = torch.empty(d2h_bytes, dtype=torch.uint8, device=dev)
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+
+    def run(h2d, d2h):
+        best = float("inf")
+        for _ in range(reps):
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for c in range(0, max(h2d_bytes, d2h_bytes), chunk):
+                if h2d and c < h2d_bytes:
+                    with torch.cuda.stream(s1):
+                        ds[c:c + chunk].copy_(hs[c:c + chunk], non_blocking=True)
+                if d2h and c < d2h_bytes:
+                    with torch.cuda.stream(s2):
+                        hd[c:c + chunk].copy_(dd[c:c + chunk], non_blocking=True)
+            s1.synchronize()
+            s2.synchronize()
+            best = min(best, time.perf_counter() - t0)
+        return best
+    t_h, t_d, t_b = run(True, False), run(False, True), run(True, True)
+    # the duplex rate: 1 GiB each way in interleaved chunks (short transfers do not overlap on this
+    # box's copy engines, so the rate is taken where they do)
+    sym = 1 << 30
+    hb, db = h2d_bytes, d2h_bytes
+    hs = torch.empty(sym, dtype=torch.uint8, pin_memory=True)
+    hd = torch.empty(sym, dtype=torch.uint8, pin_memory=True)
+    ds = torch.empty(sym, dtype=torch.uint8, device=dev)
+    dd = torch.empty(sym, dtype=torch.uint8, device=dev)
+    h2d_bytes = d2h_bytes = sym
+    t_s = run(True, True)
+    h2d_bytes, d2h_bytes = hb, db
+    duplex = 2 * sym / t_s / 1e9
+    bound = max(t_h, t_d, (hb + db) / (duplex * 1e9))
+    return {"h2d_gbs": hb / t_h / 1e9, "d2h_gbs": db / t_d / 1e9, "h2d_ms": t_h * 1e3,
+            "d2h_ms": t_d * 1e3, "both_ms": t_b * 1e3, "duplex_gbs": duplex, "duplex_probe_bytes_each_way": sym,
+            "serial_ms": (t_h + t_d) * 1e3, "h2d_bytes": hb, "d2h_bytes": db, "chunk_bytes": chunk,
+            "bound_ms": bound * 1e3,
+            "bound": "max(H2D alone, D2H alone, both volumes at the measured duplex rate)"}
+
+
+def full_chain_pipelined(rx, workload, arena, off_t, ln_t, n, n_entries, batch=1 << 17, slots=3, reps=3,
+                         rows_to_host=False):
+    """VERDICT r5 item 4: the host-to-host chain as a receive loop runs it (Domain::handle_event
+    per CQE, io_uring/rtps/dp_event_loop.rs:164-211, batched): the 1M-datagram stream in pinned
+    host memory cut into batches of `batch` datagrams; batch k+1's H2D (arena piece + offsets +
+    lengths) on a copy stream, batch k's parse -> ingest + topic caches -> CDR decode of the
+    deliveries on the compute stream, batch k-1's D2H of exactly its deliveries and rows on a
+    third stream, ordered by events (the host waits only for a finished batch's delivery count,
+    which it needs to size that batch's D2H).  The writer proxies and topic caches carry across
+    the batches (one stream, as the reference's reader sees it).  Every batch is checked against
+    the same chain run batch by batch on the HBM-resident stream (parity_ok).
+    rows_to_host: the CDR decode writes each batch's rows and row statuses straight into the
+    batch's pinned host buffers (the device -> host direction carried by the kernel's own PCIe
+    writes, beside the copy engine's host -> device traffic); only the deliveries are copied."""
+    from rtps_rx import cdr
+    t = getattr(cdr, CDR_TYPES[workload])
+    dev = arena.device
+    comp = torch.cuda.current_stream(dev)
+    off = off_t.cpu().numpy().astype(np.int64)
+    ln = ln_t.cpu().numpy().astype(np.int64)
+    nb = (n + batch - 1) // batch
+    cuts = [(k * batch, min(n, (k + 1) * batch)) for k in range(nb)]
+    spans = [(int(off[a]), int(off[b - 1] + ln[b - 1])) for a, b in cuts]
+    host_arena = torch.empty(arena.numel(), dtype=torch.uint8, pin_memory=True)
+    host_arena.copy_(arena)
+    h_off = [torch.from_numpy(off[a:b] - off[a]).pin_memory() for a, b in cuts]
+    h_ln = [torch.from_numpy(ln[a:b].astype(np.int32)).pin_memory() for a, b in cuts]
+    piece = max(e - a for a, e in spans)
+    rx.set_topics([(1, 64)], [(0, 1)])
+    # per-slot device buffers, sized from a probe parse of every batch (records per batch)
+    n_rec_b = []
+    probe = rx.alloc_outputs(batch, 1)
+    for (a, b), (s0, s1) in zip(cuts, spans):
+        o = (off_t[a:b] - int(off[a])).contiguous()
+        rx.parse_batch_device(arena[s0:s1], o, ln_t[a:b].contiguous(), b - a, probe)
+        torch.cuda.synchronize(dev)
+        n_rec_b.append(int(probe["n_records"].item()))
+    del probe
+    mrec = max(n_rec_b)
+    S = [{"arena": torch.empty(piece, dtype=torch.uint8, device=dev),
+          "off": torch.empty(batch, dtype=torch.int64, device=dev),
+          "ln": torch.empty(batch, dtype=torch.int32, device=dev),
+          "outs": rx.alloc_outputs(batch, mrec),
+          "iouts": rx.alloc_ingest_outputs(mrec, n_entries)} for _ in range(slots)]
+    max_del = S[0]["iouts"]["max_accepted"]
+    for x in S:
+        x["rows"], x["rst"] = rx.alloc_rows(t, max_del)
+    h_na = [torch.zeros(1, dtype=torch.int64, pin_memory=True) for _ in range(nb)]
+    h_dels = [torch.empty((max(n_rec_b[k], 1), 8), dtype=torch.uint8, pin_memory=True) for k in range(nb)]
+    h_rows = [torch.empty((max(n_rec_b[k], 1), t.row_bytes), dtype=torch.uint8, pin_memory=True) for k in range(nb)]
+    h_rst = [torch.empty(max(n_rec_b[k], 1), dtype=torch.uint8, pin_memory=True) for k in range(nb)]
+    h2d, d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+
+    def compute(k, x, src, o, l, to_host=False):
+        m = cuts[k][1] - cuts[k][0]
+        rx.parse_batch_device(src, o, l, m, x["outs"])
+        rx.ingest(src, o, x["outs"], x["iouts"], topic_cache=True)
+        rows, rst, cap = (h_rows[k], h_rst[k], h_rst[k].shape[0]) if to_host else (x["rows"], x["rst"], max_del)
+        rx.cdr_decode_list(t, src, o, x["outs"], x["iouts"]["accepted"], 8, x["iouts"]["n_accepted"], cap, rows, rst)
+        h_na[k].copy_(x["iouts"]["n_accepted"], non_blocking=True)
+
+    def copy_out(k, x, stream, to_host=False):
+        na = min(int(h_na[k].item()), max_del, h_dels[k].shape[0])
+        with torch.cuda.stream(stream):
+            h_dels[k][:na].copy_(x["iouts"]["accepted"][:na], non_blocking=True)
+            if not to_host:
+                h_rows[k][:na].copy_(x["rows"][:na], non_blocking=True)
+                h_rst[k][:na].copy_(x["rst"][:na], non_blocking=True)
+        return na
+
+    # the reference: batch by batch on the HBM-resident stream, synchronised
+    _reset_caches(rx, True)
+    ref = []
+    for k, ((a, b), (s0, s1)) in enumerate(zip(cuts, spans)):
+        x = S[0]
+        compute(k, x, arena[s0:s1], (off_t[a:b] - int(off[a])).contiguous(), ln_t[a:b].contiguous())
+        torch.cuda.synchronize(dev)
+        na = copy_out(k, x, comp)
+        torch.cuda.synchronize(dev)
+        ref.append((na, h_dels[k][:na].clone(), h_rows[k][:na].clone(), h_rst[k][:na].clone()))
+
+    def pipelined():
+        ev_h2d = [torch.cuda.Event() for _ in range(nb)]
+        ev_comp = [torch.cuda.Event() for _ in range(nb)]
+        ev_d2h = [torch.cuda.Event() for _ in range(nb)]
+        t1 = torch.cuda.Event(enable_timing=True)
+        nas = [0] * nb
+
+        def load(k):
+            x = S[k % slots]
+            (a, b), (s0, s1) = cuts[k], spans[k]
+            with torch.cuda.stream(h2d):
+                if k >= slots:
+                    h2d.wait_event(ev_comp[k - slots])  # the slot's last compute has read its inputs
+                x["arena"][:s1 - s0].copy_(host_arena[s0:s1], non_blocking=True)
+                x["off"][:b - a].copy_(h_off[k], non_blocking=True)
+                x["ln"][:b - a].copy_(h_ln[k], non_blocking=True)
+                ev_h2d[k].record(h2d)
+
+        def drain(k):
+            ev_comp[k].synchronize()  # (host: this batch's delivery count is in h_na[k])
+            x = S[k % slots]
+            d2h.wait_event(ev_comp[k])
+            nas[k] = copy_out(k, x, d2h, rows_to_host)
+            ev_d2h[k].record(d2h)
+
+        load(0)
+        t0 = torch.cuda.Event(enable_timing=True)
+        t0.record(h2d)  # batch 0 is in: the steady window starts
+        for k in range(nb):
+            if k + 1 < nb:
+                load(k + 1)
+            x = S[k % slots]
+            (a, b), (s0, s1) = cuts[k], spans[k]
+            comp.wait_event(ev_h2d[k])
+            if k >= slots:
+                comp.wait_event(ev_d2h[k - slots])  # the slot's outputs have left for the host
+            compute(k, x, x["arena"][:s1 - s0], x["off"][:b - a], x["ln"][:b - a], rows_to_host)
+            ev_comp[k].record(comp)
+            if k >= 1:
+                drain(k - 1)
+                if k == nb - 1:
+                    t1.record(d2h)  # batch nb-2 is out: the steady window ends
+        drain(nb - 1)
+        d2h.synchronize()
+        if nb > 1:
+            steady.append(t0.elapsed_time(t1) * 1e-3)
+        return nas
+
+    times = []
+    steady = []  # seconds from batch 0's arrival to batch nb-2's departure: nb-1 batches each way
+    ok = True
+    nas = []
+    for _ in range(reps):
+        _reset_caches(rx, True)
+        for k in range(nb):  # (the reference's copies stay in ref; every output is rewritten)
+            h_rows[k].zero_()
+            h_rst[k].fill_(0xff)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        nas = pipelined()
+        times.append(time.perf_counter() - t0)
+        for k in range(nb):
+            na = nas[k]
+            r = ref[k]
+            ok = ok and na == r[0] and torch.equal(h_dels[k][:na], r[1]) and torch.equal(h_rows[k][:na], r[2]) and \
+                torch.equal(h_rst[k][:na], r[3])
+    tm = min(times)
+    dels = int(sum(nas))
+    h2d_bytes = int(sum(e - a for a, e in spans)) + 12 * n
+    d2h_bytes = dels * (8 + t.row_bytes + 1) + 8 * nb
+    probe = pcie_probe(h2d_bytes, max(d2h_bytes, 1), dev)
+    rx.set_topics([], [])
+    bound_ms = probe["bound_ms"]
+    return {"what": f"{nb} batches of {batch} datagrams streamed host -> device -> host: batch k+1's H2D, batch "
+                    "k's parse + ingest + topic caches + CDR rows, batch k-1's D2H on three streams ordered by "
+                    "events; proxies and topic caches carry across batches; wall clock, best of "
+                    f"{reps}; sample type {CDR_TYPES[workload]}" + (
+                        "; rows written by the decode kernel straight into pinned host memory" if rows_to_host else
+                        "; deliveries, rows and statuses copied by the copy engine"),
+            "rows_to_host": rows_to_host,
+            "batches": nb, "batch_datagrams": batch, "slots": slots, "ms": tm * 1e3, "datagrams_per_s": n / tm,
+            "steady_state_datagrams_per_s": (n - (cuts[0][1] - cuts[0][0])) / min(steady) if nb > 1 else None,
+            "steady_state": "batches 1..nb-1 in and 0..nb-2 out, from batch 0's arrival to batch nb-2's departure "
+                            "(HIP events on the copy streams): the pipeline without its fill and drain",
+            "deliveries": dels, "deliveries_per_s": dels / tm, "h2d_bytes": h2d_bytes, "d2h_bytes": d2h_bytes,
+            "parity_ok": bool(ok), "pcie": probe,
+            "pcie_bound_ms": bound_ms, "pcie_bound_datagrams_per_s": n / (bound_ms * 1e-3),
+            "frac_of_pcie_bound": bound_ms / (tm * 1e3),
+            "steady_frac_of_pcie_bound": ((n - (cuts[0][1] - cuts[0][0])) / min(steady)) /
+                                         (n / (bound_ms * 1e-3)) if nb > 1 else None}
+
+
 def roofline(rx, args, arena, off_t, ln_t, n, outs, stream, total_bytes, alg_reads, alg_writes):
     """SURVEY §8(d) roofline of the dominant parse kernel.  The algorithmic unit is the
     datagram's bytes (Σ lengths) only if every byte streams (FETCH_SIZE >= Σ lengths);
@@ -590,6 +811,7 @@ def ingest_leg(rx, arena, off_t, outs, n_rec, recs, n_entries, stream, steps, fo
     torch.cuda.synchronize()
     cached = int(((iouts["accepted"][:int(iouts["n_accepted"].item())].reshape(-1, 8)[:, 6] & 1) != 0).sum().item())
     ms = _time_ingest(rx, arena, off_t, outs, iouts, fa, stream, steps, False)
+    rx.set_topics([], [])  # (no topic configured: the owner tables of the legs below deal writers, not topics)
     na = int(iouts["n_accepted"].item())
     k = recs["kind"]
     events = int((((recs["route"] & 0x21) == 0x21) & np.isin(k, (DATA, HEARTBEAT, GAP))).sum())
@@ -1236,6 +1458,14 @@ def measure(args, world, rank, dist, dev, allreduce_sum, allreduce_max):
         if n_matched_writers:
             result["end_to_end"]["full_chain"] = full_chain(rx, args.workload, arena, off_t, ln_t, n, n_rec,
                                                             n_matched_writers)
+            fc = result["end_to_end"]["full_chain"]
+            fc["pipelined"] = full_chain_pipelined(rx, args.workload, arena, off_t, ln_t, n, n_matched_writers)
+            fc["pipelined_64k"] = full_chain_pipelined(rx, args.workload, arena, off_t, ln_t, n, n_matched_writers,
+                                                       batch=1 << 16)
+            fc["pipelined_32k"] = full_chain_pipelined(rx, args.workload, arena, off_t, ln_t, n, n_matched_writers,
+                                                       batch=1 << 15)
+            fc["pipelined_best"] = max(("pipelined", "pipelined_64k", "pipelined_32k"),
+                                       key=lambda k: fc[k]["datagrams_per_s"] if fc[k]["parity_ok"] else 0)
     if world == 1 and not args.no_ingest and n_matched_writers and args.workload == "C3" and not c5:
         result["topic_cache_spdp_repeats"] = spdp_repeats_leg(dev, stream, min(args.steps, 10))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
