@@ -80,7 +80,9 @@ enum : uint8_t { EV_NONE = 0, EV_SAMPLE = 1, EV_HB = 2, EV_GAP = 3 };
 // (C_TGAP: GAPs whose range starts at or below their proxy's all_ackable_before and reaches past its
 //  window: irrelevant_changes_range then only moves all_ackable_before, a threshold the per-proxy
 //  path applies as such; the host sends such batches there)
-enum { C_OVF = 0, C_NSEL, C_NDEL, C_NREC, C_FARC, C_NFAR, C_MODE, C_TGAP, C_SPREAD, C_COUNT = C_SPREAD + 4 * 64 };
+enum { C_OVF = 0, C_NSEL, C_NDEL, C_NREC, C_FARC, C_NFAR, C_MODE, C_TGAP, C_FDEF, C_PAD, C_SPREAD,
+       C_COUNT = C_SPREAD + 4 * 64 };
+static_assert(C_SPREAD % 2 == 0, "the spread counters are loaded as 16-B pairs");
 // the batch's counts as k_signal writes them to pinned host memory:
 // [0] = the batch's tag (written last), HEARTBEAT / GAP / event / proxy-less sample counts,
 // records, far-item candidates, the verdict, the far-set pool's slots in use (as the earlier
@@ -178,6 +180,13 @@ struct State {
   FarItem* fl;        // this batch's far items (global paths), C_NFAR of them, at most fl_cap
   uint64_t fl_cap;
   uint32_t epoch;     // this batch's (first-cover keys)
+  // far sets of more than FT_BIG slots: the state pass leaves their far_extend / far_pull to the
+  // grid-wide k_fx_* launches (fdefer: the host launches them after this batch's state pass)
+  uint32_t fdefer;
+  uint32_t* fdl;      // the deferred proxies (C_FDEF of them)
+  int64_t* fext;      // per proxy: all_ackable_before through the far set (k_fx_ext's minimum)
+  uint32_t* fkeep;    // per proxy: the far SNs left past the new window (k_fx_pull; 0 between batches)
+  int64_t* fkmin;     // per proxy: their least (INT64_MAX between batches)
 };
 
 // ---- 1 classify ----
@@ -1711,6 +1720,143 @@ __device__ void far_pull(const State& s, FarSh& f, uint32_t* bits, int64_t nlo, 
   __syncthreads();
 }
 
+// ---- far sets past FT_BIG slots: far_extend / far_pull by the whole grid ----
+// far_extend probes the set one SN after another from all_ackable_before, and far_pull scans the
+// whole table: one workgroup does that for a large set in milliseconds (one writer a million SNs
+// ahead of its window: the SPDP reader's repeats).  With S.fdefer the state pass leaves such a
+// proxy at its window's answer (base = nb, the window unshifted in dbits, its table stored) and
+// lists it; four launches then finish it with every workgroup:
+//   k_fx_ext    the first SN >= nb the set lacks: the candidates [nb, nb + n] in chunks, one
+//               probe per thread, an atomicMin; chunks past the minimum found are skipped;
+//   k_fx_shift  the window re-anchored at the new all_ackable_before (from dbits);
+//   k_fx_pull   the table's SNs the new window spans set their bits, the rest past it counted;
+//   k_fx_fin    base / lo / the far set's min (emptied when nothing lies past the window).
+constexpr uint32_t FT_BIG = 1u << 14;
+// does the state pass need the far set (far_extend, far_pull) after finding nb in the window?
+__device__ __forceinline__ bool far_touch(const FTab& t, int64_t lo, int64_t nb) {
+  if (t.cap == 0) return false;
+  if (nb >= lo + (int64_t)W && nb >= t.min) return true;  // extend
+  return t.min < (nb & ~(int64_t)31) + (int64_t)W;      // pull
+}
+// the deferral (every thread of the state workgroup): the window `win` (LDS, unshifted) to
+// dbits, the table and the window's answer stored, the proxy listed
+__device__ void far_defer(const State& s, uint32_t e, const FTab& t, const uint32_t* win, int64_t nb, int32_t hbc,
+                          uint32_t nt) {
+  uint32_t* db = s.dbits + (uint64_t)e * WW;
+  for (uint32_t w = threadIdx.x; w < WW; w += nt) db[w] = win[w];
+  if (threadIdx.x == 0) {
+    ftab_store(s, e, t);
+    s.base[e] = nb;
+    s.hbc[e] = hbc;
+    s.fext[e] = nb + (int64_t)t.n;  // (at most n SNs of the set lie at or above nb)
+    const uint64_t i = atomicAdd(reinterpret_cast<unsigned long long*>(s.ctr + C_FDEF), 1ull);
+    s.fdl[i] = e;
+  }
+}
+constexpr uint32_t FX = 256, FX_PER = 16;  // threads, SNs per thread per k_fx_ext chunk
+__global__ __launch_bounds__(FX) void k_fx_ext(State s) {
+  const uint32_t nd = (uint32_t)s.ctr[C_FDEF];
+  for (uint32_t i = 0; i < nd; ++i) {
+    const uint32_t e = s.fdl[i];
+    const int64_t lo = s.lo[e], nb = s.base[e], mn = s.far_min[e];
+    const uint32_t cap = s.far_cap[e];
+    if (cap == 0 || nb < lo + (int64_t)W || nb < mn) continue;  // no extension (far_extend's test)
+    const int64_t* sn = s.fsn + s.far_off[e];
+    const uint32_t mask = cap - 1u;
+    const uint64_t span = (uint64_t)s.far_n[e] + 1u, chunk = (uint64_t)FX * FX_PER;
+    for (uint64_t c = blockIdx.x; c * chunk < span; c += gridDim.x) {
+      const int64_t c0 = nb + (int64_t)(c * chunk);
+      if (__hip_atomic_load(&s.fext[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < c0) break;  // (uniform)
+      int64_t cur[FX_PER];
+#pragma unroll
+      for (uint32_t r = 0; r < FX_PER; ++r) cur[r] = fld(sn + fslot(c0 + (int64_t)(r * FX + threadIdx.x), mask));
+#pragma unroll
+      for (uint32_t r = 0; r < FX_PER; ++r) {
+        const int64_t v = c0 + (int64_t)(r * FX + threadIdx.x);
+        if (cur[r] == FEMPTY || (cur[r] != v && fset_find(sn, mask, v) == NONE)) {
+          atomicMin(reinterpret_cast<long long*>(&s.fext[e]), (long long)v);
+          break;
+        }
+      }
+    }
+  }
+}
+// the window re-anchored at the new all_ackable_before: bits from dbits (the state pass's window
+// at lo), dbits' words read only (k_fx_pull clears them)
+__global__ __launch_bounds__(FX) void k_fx_shift(State s) {
+  const uint32_t nd = (uint32_t)s.ctr[C_FDEF];
+  for (uint64_t k = (uint64_t)blockIdx.x * FX + threadIdx.x; k < (uint64_t)nd * WW; k += (uint64_t)gridDim.x * FX) {
+    const uint32_t e = s.fdl[k / WW], w = (uint32_t)(k % WW);
+    const int64_t lo = s.lo[e], nb = s.base[e], mn = s.far_min[e];
+    const int64_t fnb = (s.far_cap[e] && nb >= lo + (int64_t)W && nb >= mn) ? s.fext[e] : nb;
+    const uint64_t shift = (uint64_t)((fnb & ~(int64_t)31) - lo) >> 5;
+    s.bits[(uint64_t)e * WW + w] = (w + shift < WW) ? s.dbits[(uint64_t)e * WW + w + shift] : 0u;
+  }
+}
+__global__ __launch_bounds__(FX) void k_fx_pull(State s) {
+  __shared__ uint32_t s_keep;
+  __shared__ unsigned long long s_min;
+  const uint32_t nd = (uint32_t)s.ctr[C_FDEF];
+  for (uint64_t k = (uint64_t)blockIdx.x * FX + threadIdx.x; k < (uint64_t)nd * WW; k += (uint64_t)gridDim.x * FX)
+    s.dbits[(uint64_t)s.fdl[k / WW] * WW + k % WW] = 0u;  // (k_fx_shift has read them)
+  for (uint32_t i = 0; i < nd; ++i) {
+    const uint32_t e = s.fdl[i];
+    const int64_t lo = s.lo[e], nb = s.base[e], mn = s.far_min[e];
+    const uint32_t cap = s.far_cap[e];
+    const int64_t fnb = (cap && nb >= lo + (int64_t)W && nb >= mn) ? s.fext[e] : nb;
+    const int64_t nlo = fnb & ~(int64_t)31, hi = nlo + (int64_t)W;
+    if (cap == 0 || mn >= hi) continue;  // (far_pull's test)
+    if (threadIdx.x == 0) { s_keep = 0; s_min = ~0ull; }
+    __syncthreads();
+    const int64_t* sn = s.fsn + s.far_off[e];
+    uint32_t* bits = s.bits + (uint64_t)e * WW;
+    uint32_t keep = 0;
+    int64_t kmin = INT64_MAX;
+    for (uint64_t j = (uint64_t)blockIdx.x * FX + threadIdx.x; j < cap; j += (uint64_t)gridDim.x * FX) {
+      const int64_t v = fld(sn + j);
+      if (v == FEMPTY || v < nlo) continue;
+      if (v >= hi) {
+        ++keep;
+        if (v < kmin) kmin = v;
+      } else {
+        atomicOr(bits + ((uint64_t)(v - nlo) >> 5), 1u << ((uint64_t)(v - nlo) & 31u));
+      }
+    }
+    if (keep) atomicAdd(&s_keep, keep);
+    if (kmin != INT64_MAX) atomicMin(&s_min, (unsigned long long)kmin);
+    __syncthreads();
+    if (threadIdx.x == 0 && s_keep) {
+      atomicAdd(&s.fkeep[e], s_keep);
+      atomicMin(reinterpret_cast<long long*>(&s.fkmin[e]), (long long)s_min);
+    }
+    __syncthreads();
+  }
+}
+__global__ __launch_bounds__(FX) void k_fx_fin(State s, int64_t* ack_out) {
+  const uint32_t nd = (uint32_t)s.ctr[C_FDEF];
+  for (uint32_t i = threadIdx.x; i < nd; i += FX) {
+    const uint32_t e = s.fdl[i];
+    const int64_t lo = s.lo[e], nb = s.base[e], mn = s.far_min[e];
+    const uint32_t cap = s.far_cap[e];
+    const int64_t fnb = (cap && nb >= lo + (int64_t)W && nb >= mn) ? s.fext[e] : nb;
+    const int64_t nlo = fnb & ~(int64_t)31, hi = nlo + (int64_t)W;
+    if (cap && mn < hi) {  // far_pull ran: the set's least SN past the window, or the set emptied
+      if (s.fkeep[e] == 0) {
+        s.far_off[e] = 0; s.far_cap[e] = 0; s.far_n[e] = 0; s.far_min[e] = INT64_MAX;
+      } else {
+        s.far_min[e] = s.fkmin[e];
+      }
+    }
+    s.fkeep[e] = 0;
+    s.fkmin[e] = INT64_MAX;
+    s.base[e] = fnb;
+    s.lo[e] = nlo;
+    if (ack_out) ack_out[e] = fnb;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) s.ctr[C_FDEF] = 0;  // (a later state pass of this batch's counters may list again)
+}
+
 // ---- 6 merge ----
 // Batches without GAPs whose proxies' windows are few against their events (T:
 // 16 proxies x 2^17 positions for 1M samples): the batch's sample coverage is
@@ -1806,6 +1952,10 @@ __device__ __forceinline__ void state_proxy(uint32_t e, const Scratch& x, const 
     }
     __syncthreads();
     nb = lo + (int64_t)(s_first != NONE ? s_first : W);
+  }
+  if (s.fdefer && f.t.cap > FT_BIG && far_touch(f.t, lo, nb)) {  // (uniform: f is shared)
+    far_defer(s, e, f.t, sh, nb, hbc, IT);  // the k_fx_* launches finish it
+    return;
   }
   nb = far_extend(s, f, lo, nb, IT);
   // re-anchor the window at the new ack_base (bits below it are no longer needed)
@@ -2391,6 +2541,11 @@ __global__ __launch_bounds__(PT) void k_proxy(const uint8_t* arena, const PEv* p
   if (n_ovf) atomicAdd(reinterpret_cast<unsigned long long*>(s.ctr + C_OVF), (unsigned long long)n_ovf);
   // state (as k_state): ack_base = first sequence number >= threshold outside the change set
   int64_t nb = run_thr < lo + (int64_t)W ? first_open(run_thr) : run_thr;
+  __syncthreads();  // (fsh.t final for every thread)
+  if (s.fdefer && fsh.t.cap > FT_BIG && far_touch(fsh.t, lo, nb)) {
+    far_defer(s, e, fsh.t, sb, nb, (int32_t)run_cnt, PT);  // the k_fx_* launches finish it
+    return;
+  }
   nb = far_extend(s, fsh, lo, nb, PT);
   const int64_t nlo = nb & ~(int64_t)31;
   const uint64_t shift = (uint64_t)(nlo - lo) >> 5;
@@ -2418,6 +2573,8 @@ __global__ void k_init_state(uint32_t n, State s) {
     s.far_min[e] = INT64_MAX;
     s.fneed[e] = 0;
     s.fstat[e] = 0;
+    s.fkeep[e] = 0;
+    s.fkmin[e] = INT64_MAX;
   }
 }
 // the far-set pool compacted: proxy e's table [far_off[e], + far_cap[e]) to noff[e] of the new pool
@@ -2500,6 +2657,7 @@ struct IngestState {
   bool hnev_ready = false;
   uint64_t last_nev = 0;      // events of the last batch whose counts were read
   uint64_t last_far = 0;      // ...and its far items (per-proxy path)
+  uint64_t last_farc = 0;     // the last signalled batch's far candidates (its tables may have grown)
   uint64_t* hsig = nullptr;    // pinned, coherent: classify's count signal (SIG_*)
   uint64_t sig_tag = 0;
   uint32_t* bk_cl = nullptr;  // proxy bucketing: per (classify workgroup, proxy) events | first position << 16
@@ -2569,7 +2727,8 @@ static void keep_shared(State& m, const State& o) {
 }
 static void free_state(IngestState* s) {
   void* p[] = {s->st.base, s->st.lo, s->st.hbc, s->st.bits, s->st.fc, s->st.dbits, s->st.seg_b, s->st.seg_e,
-               s->st.far_off, s->st.far_cap, s->st.far_n, s->st.far_min, s->st.fneed, s->st.fstat};
+               s->st.far_off, s->st.far_cap, s->st.far_n, s->st.far_min, s->st.fneed, s->st.fstat,
+               s->st.fdl, s->st.fext, s->st.fkeep, s->st.fkmin};
   for (void* q : p) if (q) (void)hipFree(q);
   State k{};
   keep_shared(k, s->st);
@@ -2691,7 +2850,9 @@ static bool grow_state(IngestState* s, uint32_t n, hipStream_t st) {
             hipMalloc(&m.seg_e, ncap * 4ull) == hipSuccess && hipMalloc(&m.far_off, ncap * 8ull) == hipSuccess &&
             hipMalloc(&m.far_cap, ncap * 4ull) == hipSuccess && hipMalloc(&m.far_n, ncap * 4ull) == hipSuccess &&
             hipMalloc(&m.far_min, ncap * 8ull) == hipSuccess && hipMalloc(&m.fneed, ncap * 8ull) == hipSuccess &&
-            hipMalloc(&m.fstat, ncap * 4ull) == hipSuccess;
+            hipMalloc(&m.fstat, ncap * 4ull) == hipSuccess && hipMalloc(&m.fdl, ncap * 4ull) == hipSuccess &&
+            hipMalloc(&m.fext, ncap * 8ull) == hipSuccess && hipMalloc(&m.fkeep, ncap * 4ull) == hipSuccess &&
+            hipMalloc(&m.fkmin, ncap * 8ull) == hipSuccess;
   ok = ok && hipMemsetAsync(m.bits, 0, (uint64_t)ncap * WW * 4, st) == hipSuccess &&
        hipMemsetAsync(m.dbits, 0, (uint64_t)ncap * WW * 4, st) == hipSuccess &&
        hipMemsetAsync(m.fc, 0xff, (uint64_t)ncap * W * 8, st) == hipSuccess;
@@ -2712,7 +2873,8 @@ static bool grow_state(IngestState* s, uint32_t n, hipStream_t st) {
   s->ecap = ncap;
   State dead = o;
   void* p[] = {dead.base, dead.lo, dead.hbc, dead.bits, dead.fc, dead.dbits, dead.seg_b, dead.seg_e,
-               dead.far_off, dead.far_cap, dead.far_n, dead.far_min, dead.fneed, dead.fstat};
+               dead.far_off, dead.far_cap, dead.far_n, dead.far_min, dead.fneed, dead.fstat,
+               dead.fdl, dead.fext, dead.fkeep, dead.fkmin};
   for (void* q : p) if (q) (void)hipFree(q);
   if (!ok) { free_state(s); return false; }
   return true;
@@ -2825,6 +2987,16 @@ int rtps_ingest_state_reset(IngestState* s, hipStream_t st) {
   return ok && hipGetLastError() == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP;
 }
 
+// the k_fx_* launches that finish the far sets a state pass deferred (S.fdefer: that pass may
+// have listed some; none listed: each returns at once)
+static void far_finish(const State& S, int64_t* ack_out, hipStream_t st) {
+  if (!S.fdefer) return;
+  hipLaunchKernelGGL(k_fx_ext, dim3(1024), dim3(FX), 0, st, S);
+  hipLaunchKernelGGL(k_fx_shift, dim3(512), dim3(FX), 0, st, S);
+  hipLaunchKernelGGL(k_fx_pull, dim3(1024), dim3(FX), 0, st, S);
+  hipLaunchKernelGGL(k_fx_fin, dim3(1), dim3(FX), 0, st, S, ack_out);
+}
+
 static int ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const uint8_t* arena, uint64_t arena_len,
                       const uint64_t* dgram_off, const rtps_record* records, const uint64_t* n_records,
                       uint64_t max_records, const rtps_frag_sample* frag, const uint64_t* n_frag, uint64_t max_frag,
@@ -2916,9 +3088,13 @@ static int ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, cons
     hipLaunchKernelGGL((k_classify<false, false>), dim3(gb), dim3(IT), lds, st, t, records, n_records, max,
                        with_frag ? frag : nullptr, flags, x, S.ctr, fo, ctr_next, S, s->epoch);
   s->cpar ^= 1u;  // the next batch uses the set this classify zeroes
+  // a far set past FT_BIG slots exists only where the pool holds that many, or grows in a batch
+  // with far items (the signalled path's farc; the fast path is not taken after one)
+  S.fdefer = s->fp_used > FT_BIG ? 1u : 0u;
   if (bucket) {
     hipLaunchKernelGGL(k_proxy<true>, dim3(t.n_proxies), dim3(PT), 0, st, arena, s->pev, x.hval, t.n_proxies, S,
                        out->accept, out->ack_base, BkIn{s->bk_cl, (uint32_t)nblk});
+    far_finish(S, out->ack_base, st);
   } else if (fast) {
     uint32_t kb = 1;
     while ((1u << kb) <= t.n_proxies) ++kb;  // keys 0..n_proxies (n_proxies: no proxy, sorts last)
@@ -2929,6 +3105,7 @@ static int ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, cons
     hipLaunchKernelGGL(k_pseg, dim3(gm), dim3(IT), 0, st, max, t.n_proxies, x, S);
     hipLaunchKernelGGL(k_proxy<false>, dim3(t.n_proxies), dim3(PT), 0, st, arena, s->pev, x.hval, t.n_proxies, S,
                        out->accept, out->ack_base, BkIn{});
+    far_finish(S, out->ack_base, st);
   }
   if (fast) {
     // the select also writes this batch's event count for the next batch's choice (pinned, read
@@ -2950,9 +3127,11 @@ static int ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, cons
     const uint32_t nfcm = (uint32_t)((uint64_t)t.n_proxies * W / FCM_POS);
     hipLaunchKernelGGL(k_decide_t<3>, dim3(ntiles + nfcm), dim3(IT), 0, st, max, max, x, S, out->accept, false,
                        s->epoch, x.sel, fs, ntiles, SigOut{s->hsig, tag, cfg});
+    S.fdefer = (s->fp_used > FT_BIG || s->last_farc) ? 1u : 0u;  // (the pool as the last batch left it)
     hipLaunchKernelGGL(k_dstate, dim3(ntiles + t.n_proxies), dim3(IT), 0, st, out->accept, max, x.sel, ntiles, x,
                        out->max_accepted, out->accepted, out->n_accepted, S.ctr, out->n_window_overflow, t.n_proxies,
                        S, false, out->ack_base, false, true);
+    far_finish(S, out->ack_base, st);
   } else {
     hipLaunchKernelGGL(k_signal, dim3(1), dim3(64), 0, st, S.ctr, s->hsig, tag, cfg);
   }
@@ -2979,6 +3158,8 @@ static int ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, cons
   // (a GAP's listed ones included) bound the far-set tables this batch can grow
   const uint64_t nfi = farc;
   if (nfi && (!grow_fl(s, nfi, st) || !far_pool_ensure(s, nfi + 256 * n_gap, st))) return RTPS_RX_ENOMEM;
+  s->last_farc = farc;
+  S.fdefer = (farc || s->fp_used > FT_BIG) ? 1u : 0u;  // (this batch's state pass may defer large far sets)
   if (!ident) {
     if (n_ev > 0x7fffffffull) return RTPS_RX_ETOOBIG;
     if (!grow_vscratch(s, n_ev ? n_ev : 1, st)) return RTPS_RX_ENOMEM;
@@ -3025,6 +3206,7 @@ static int ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, cons
                        acc_cap, x, acc);
     hipLaunchKernelGGL(k_proxy<false>, dim3(t.n_proxies), dim3(PT), 0, st, arena, s->pev, x.hval, t.n_proxies, S,
                        acc, out->ack_base, BkIn{});
+    far_finish(S, out->ack_base, st);
   }
   const bool have_hb = reliable && n_hb > 0 && !per_proxy;
   if (have_hb) {  // stable compaction of the HEARTBEAT events, sort by proxy, scans by key
@@ -3080,6 +3262,7 @@ static int ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, cons
     hipLaunchKernelGGL(k_dstate, dim3(ntiles + t.n_proxies), dim3(IT), 0, st, acc, acc_cap, x.sel, ntiles, x,
                        out->max_accepted, out->accepted, out->n_accepted, S.ctr, out->n_window_overflow, t.n_proxies,
                        S, have_hb, out->ack_base, fc_merge, false);
+    far_finish(S, out->ack_base, st);
     return hipGetLastError() == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP;
   }
   if (nev && !per_proxy) {
@@ -3103,9 +3286,11 @@ static int ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, cons
                        t.n_proxies, S, s->epoch);
   else if (nev && !per_proxy)
     hipLaunchKernelGGL(k_merge, dim3(gv), dim3(IT), 0, st, records, arena, dgram_off, nev, x, S, n_gap > 0);
-  if (state_pass)
+  if (state_pass) {
     hipLaunchKernelGGL(k_state, dim3(t.n_proxies), dim3(IT), 0, st, t.n_proxies, x, S, have_hb, out->ack_base,
                        out->n_window_overflow);
+    far_finish(S, out->ack_base, st);
+  }
   return hipGetLastError() == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP;
 }
 

@@ -338,6 +338,36 @@ def test_gap_threshold_moved_in_batch(rx, case):
     _batch(rx, ing, tbl, dg, case + " next")
 
 
+def test_big_far_set_grid_pass(rx):
+    """far sets past FT_BIG slots are finished by the grid-wide k_fx_* pass.
+    One writer sends 150,000 SNs past its window first (a far table of 2^20 slots), then SNs
+    1..100 (all_ackable_before 101: the re-anchored window pulls the far SNs it now spans, the set
+    is not extended), then the rest of the window (all_ackable_before runs through all 150,000
+    far SNs), then re-sends of far SNs (rejected) and fresh ones; a second writer beside it stays
+    small.  Bit-exact with the oracle on every ingest path, nothing counted."""
+    import rtps_rx
+    W = rtps_rx.INGEST_WINDOW
+    w0, w1 = R.writer_key(0), R.writer_key(1)
+    tbl = pack_match_table([(R.PREFIXES[0] + w0, 0), (R.PREFIXES[0] + w1, 1)])
+    rx.set_match_table(tbl)
+    ing = oracle.HistoryIngest(tbl)
+    rng = np.random.default_rng(21)
+    far = W + 10 + rng.permutation(150_000)
+
+    def dgrams(sns, w=w0, per=4):
+        return [R.datagram(R.PREFIXES[0], [R.data_sub(w, int(x)) for x in sns[i:i + per]])
+                for i in range(0, len(sns), per)]
+    _, _, ack = _batch(rx, ing, tbl, dgrams(far) + dgrams(np.arange(1, 30), w1), "far first")
+    assert ack.tolist() == [1, 30]
+    _, _, ack = _batch(rx, ing, tbl, dgrams(np.arange(1, 101)), "pull only")
+    assert ack.tolist()[0] == 101
+    rest = np.concatenate([np.arange(101, W + 10), far[:5], [W + 150_010 + 3, W + 150_010]])
+    _, dels, ack = _batch(rx, ing, tbl, dgrams(rest), "extension")
+    assert ack.tolist()[0] == W + 150_010 + 1
+    _, dels, ack = _batch(rx, ing, tbl, dgrams(np.concatenate([far[-7:], [W + 150_012, W + 150_010 + 3]])), "after")
+    assert len(dels) == 1 and ack.tolist()[0] == W + 150_011
+
+
 def test_far_pool_out_counted(rx):
     """The one capacity left: a GAP covering more SNs past the window than the far-set pool
     keeps free (here 2^34) cannot be recorded SN by SN; that proxy's far samples of the batch
