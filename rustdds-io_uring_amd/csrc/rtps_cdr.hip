@@ -708,6 +708,9 @@ bool rtps_cdr_is_composite(const rtps_cdr_op* prog, uint32_t n_ops) {
 
 bool rtps_cdr_build_nested(const rtps_cdr_op* prog, uint32_t n_ops, uint32_t row_bytes, CdrNest& N) {
   if (n_ops > RTPS_CDR_MAX_OPS) return false;
+  // the composite walk packs a slot's row offset into 20 bits beside its op index
+  // (the LDS frame word restored with `f.w & 0xfffff`): wider rows cannot be framed
+  if (row_bytes > (1u << 20)) return false;
   memset(&N, 0, sizeof(N));
   // open containers: the row, then one per open BEGIN (its element)
   struct Box { uint32_t begin, limit; uint64_t min_wire; };

@@ -1228,6 +1228,40 @@ __device__ __forceinline__ void em2_item(const KParams& p, const Src& s0, const 
 #endif
 constexpr uint32_t EM2T = RTPS_EM2_THREADS, EM2_TPB = EM2T / TILE;
 static_assert(EM2T % TILE == 0, "whole tiles per workgroup");
+// Tile order of W2's grid stride.  0: ascending.  1: descending, so that the first tiles W2
+// takes are the last E walked (their lines and items are the likeliest still in the Infinity
+// Cache).  2: descending inside each XCD: workgroup b (XCD b % 8, as the dispatcher deals
+// workgroups round robin) takes only tiles t = b (mod 8), the ones E's workgroup t walked on
+// the same XCD, so E's items and dinfo words can still be in that XCD's L2.
+#ifndef RTPS_EM2_ORDER
+#define RTPS_EM2_ORDER 2  // C3 step 316 -> 307 us, W2 168 -> 165.4 (1: 309.5 us; scripts/gpu_variant_ab.sh)
+#endif
+constexpr uint32_t XCDS = 8;
+struct Em2Seq {  // the tiles one wave of a W2 workgroup takes, in order
+  uint32_t x, step, mx, n_tiles;  // ORDER 2: its XCD, stride, tiles of that XCD
+  uint32_t m;                     // position in the sequence
+};
+__device__ __forceinline__ Em2Seq em2_seq(uint32_t n_tiles, uint32_t sub) {
+  Em2Seq q;
+  q.n_tiles = n_tiles;
+  if (RTPS_EM2_ORDER == 2 && gridDim.x % XCDS == 0) {
+    q.x = blockIdx.x % XCDS;
+    q.step = (gridDim.x / XCDS) * EM2_TPB;
+    q.m = (blockIdx.x / XCDS) * EM2_TPB + sub;
+    q.mx = n_tiles > q.x ? (n_tiles - q.x + XCDS - 1) / XCDS : 0u;
+  } else {
+    q.x = ~0u;
+    q.step = gridDim.x * EM2_TPB;
+    q.m = blockIdx.x * EM2_TPB + sub;
+    q.mx = n_tiles;
+  }
+  return q;
+}
+__device__ __forceinline__ bool em2_more(const Em2Seq& q) { return q.m < q.mx; }
+__device__ __forceinline__ uint32_t em2_tile(const Em2Seq& q) {
+  if (q.x != ~0u) return q.x + XCDS * (q.mx - 1u - q.m);
+  return RTPS_EM2_ORDER ? q.n_tiles - 1u - q.m : q.m;
+}
 __global__ __launch_bounds__(EM2T, RTPS_EM2_WAVES_PER_SIMD) void rtps_parse_emit2_kernel(
     KParams p, uint32_t n_tiles, const u32x4* __restrict__ items, const uint32_t* __restrict__ wcnt,
     const uint64_t* __restrict__ tprefix, const u32x4* __restrict__ dinfo) {
@@ -1241,7 +1275,8 @@ __global__ __launch_bounds__(EM2T, RTPS_EM2_WAVES_PER_SIMD) void rtps_parse_emit
   uint16_t* map = s_map + wv * CAPW;
   mt_stage(p);
   __syncthreads();
-  for (uint32_t tile = blockIdx.x * EM2_TPB + sub; tile < n_tiles; tile += gridDim.x * EM2_TPB) {
+  for (Em2Seq sq = em2_seq(n_tiles, sub); em2_more(sq); sq.m += sq.step) {
+    const uint32_t tile = em2_tile(sq);
     const uint32_t wc = __builtin_amdgcn_readfirstlane(wcnt[tile * WAVES + wave]);
     const uint64_t prefix = tprefix[tile];
     TileCtx t;
@@ -1318,7 +1353,8 @@ __global__ __launch_bounds__(EM2T, RTPS_EM2_WAVES_PER_SIMD) void rtps_parse_emit
   }
   // slabs whose items did not fit (rare): walk the wave's datagrams, after the item loop so
   // that its registers do not carry the walk's
-  for (uint32_t tile = blockIdx.x * EM2_TPB + sub; tile < n_tiles; tile += gridDim.x * EM2_TPB) {
+  for (Em2Seq sq = em2_seq(n_tiles, sub); em2_more(sq); sq.m += sq.step) {
+    const uint32_t tile = em2_tile(sq);
     if (!(wcnt[tile * WAVES + wave] & WCNT_OVERFLOW)) continue;
     TileCtx th;
     load_tile(p, tile, th, true, wave * 64u + lane);

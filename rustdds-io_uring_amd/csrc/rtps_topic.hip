@@ -208,133 +208,337 @@ struct TDev {
   BEnt* B;
   uint64_t bmask;
   uint32_t epoch, nA;
-  // batch scratch (positions p in topic order)
-  KeyP* kp;           // [max] by delivery
-  uint32_t *skey, *skey2, *sval, *order;  // sort: compact topic, delivery index
+  // the batch: a delivery's change is read from its record when needed (no per-delivery key copy)
+  const rtps_record* recs;
+  const uint64_t* n_records;
+  uint64_t max_records;
+  rtps_delivery* del;
+  const uint64_t* n_del;
+  uint64_t max_del;
+  // batch scratch (positions p in topic order; only p < the batch's delivery count is read)
+  uint32_t *skey, *skey2, *sval, *order;  // sort: compact topic, delivery index (order == nullptr: no sort)
   uint8_t* fl;        // FL_* per position
-  uint32_t *kins, *kpre;
-  int32_t *gcpos, *lgc;
-  uint8_t *fr, *frins;
+  uint32_t* kpre;     // [max + 1] stored (FL_INS) positions before p
+  int32_t* lgc;       // last GC position <= p (-1: none)
+  uint8_t* frins;     // a repeat (FL_REP) position's change stored (written for repeats only)
   uint32_t* frlist;   // repeat positions, ascending
   uint64_t* nfr;
   uint32_t* frcum;    // inserted repeats of the topic up to frlist[j] (inclusive)
   uint64_t* fridx;    // [max] insertion index of an inserted repeat
-  uint32_t *segb, *sege, *frb, *fre;  // [nA]
+  uint32_t *segb, *sege;  // [nA] this batch's topic segments (one of two parity buffers)
+  uint32_t *segb_next, *sege_next;  // the other buffer: cleared here for the next batch
+  uint32_t *frb, *fre;  // [nA]
   uint64_t* ibase;    // [nA] I of the topic at the batch start
   uint64_t* n_full;   // live-index inserts that found no room (0)
   const uint64_t* ovf;  // the ingest's window overflows of the batch (nullptr: none): all candidates
-  // repeats decided in parallel (tc_rdec): per repeat j the decision, the exclusive count of the
+  // repeats decided in parallel (tc_rscan): per repeat j the decision, the exclusive count of the
   // sure stores before it; the undecided ones (AMB) in order, with their stores' running count
   uint8_t* rdec;      // [nfr] RD_HOLD / RD_STORE / RD_AMB
-  uint32_t *rst, *rpre;   // [nfr] 1 = sure store; exclusive scan of rst
-  uint8_t* ramb;      // [nfr] 1 = undecided
+  uint32_t* rpre;     // [nfr + 1] sure stores before repeat j
   uint32_t* amb;      // [namb] the undecided repeats' j, ascending
   uint64_t* namb;
   uint32_t* acum;     // [namb] stored undecided repeats up to amb[a] (inclusive), written in order
   uint32_t *ab, *ae;  // [nA] the topic's range of amb[]
   uint64_t* n_used;   // claimed live-index slots
-  uint64_t* h_used;   // pinned: n_used as the earlier batches left it (tc_gather)
+  uint64_t* h_used;   // pinned: n_used as the earlier batches left it (the batch's first kernel)
+  // the single-pass scans (tc_cscan over positions, tc_rscan over repeats): tile tickets and
+  // decoupled look-back words, cleared by the batch's first kernel
+  uint32_t* ticket;         // [2]
+  unsigned long long* lb;   // [4 * ntl]: tc_cscan's count words, its GC words, tc_rscan's count words
+  uint32_t ntl;
 };
-constexpr uint8_t FL_GC = 1, FL_CAND = 2, FL_REP0 = 4, FL_PLIVE = 8, FL_VALID = 16;
+constexpr uint8_t FL_GC = 1, FL_CAND = 2, FL_REP0 = 4, FL_PLIVE = 8, FL_VALID = 16, FL_INS = 32, FL_REP = 64;
 
-__device__ __forceinline__ uint32_t pos_cid(const TDev& d, uint64_t p) { return d.order ? d.skey2[p] : d.skey[p]; }
 __device__ __forceinline__ uint32_t pos_k(const TDev& d, uint64_t p) { return d.order ? d.order[p] : (uint32_t)p; }
+__device__ __forceinline__ uint32_t pos_cid(const TDev& d, uint64_t p) {
+  return d.order ? d.skey2[p] : d.slot_cid[d.del[p].reader_slot];
+}
+__device__ __forceinline__ uint64_t n_deliveries(const TDev& d) { return *d.n_del < d.max_del ? *d.n_del : d.max_del; }
+__device__ __forceinline__ bool ins_at(const TDev& d, uint64_t p) { return (d.fl[p] & FL_INS) != 0; }
+// delivery dl's change (writer GUID, SN, topic); rec = NONE when its record is outside the batch
+__device__ __forceinline__ KeyP key_of(const TDev& d, const rtps_delivery& dl) {
+  KeyP x{};
+  x.rec = NONE;
+  const uint64_t nrec = *d.n_records < d.max_records ? *d.n_records : d.max_records;
+  if (dl.rec_idx < nrec) {
+    const uint4* q = reinterpret_cast<const uint4*>(d.recs + dl.rec_idx);
+    const uint4 a = q[0], b = q[1], c = q[2];
+    x.g[0] = a.z; x.g[1] = a.w; x.g[2] = b.x; x.g[3] = b.y;  // prefix @8, writer_id @20
+    x.snlo = c.x; x.snhi = c.y;                              // sn @32
+    x.tid = d.slot_tid[dl.reader_slot];
+    x.rec = dl.rec_idx;
+  }
+  return x;
+}
 
-// deliveries -> their changes (writer GUID, SN, topic) and the sort pairs
-__global__ __launch_bounds__(TT) void tc_gather(TDev d, const rtps_record* recs, const uint64_t* n_records,
-                                                uint64_t max_records, const rtps_delivery* del, const uint64_t* n_del,
-                                                uint64_t max_del) {
-  const uint64_t nrec = *n_records < max_records ? *n_records : max_records;
-  const uint64_t nd = *n_del < max_del ? *n_del : max_del;
-  // the topics' segment starts: none until tc_mark finds one
-  for (uint32_t c = blockIdx.x * TT + threadIdx.x; c < d.nA; c += gridDim.x * TT) d.segb[c] = NONE;
-  // the live index's use as the earlier batches left it, to pinned host memory for reserve_live
-  // (read once this batch's event has passed: no copy on the stream)
-  if (blockIdx.x == 0 && threadIdx.x == 0) __hip_atomic_store(d.h_used, *d.n_used, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  for (uint64_t k = (uint64_t)blockIdx.x * TT + threadIdx.x; k < max_del; k += (uint64_t)gridDim.x * TT) {
-    KeyP x{};
-    x.rec = NONE;
-    uint32_t cid = d.nA;
-    if (k < nd) {
-      const rtps_delivery dl = del[k];
-      cid = d.slot_cid[dl.reader_slot];
-      if (dl.rec_idx < nrec) {
-        const uint4* q = reinterpret_cast<const uint4*>(recs + dl.rec_idx);
-        const uint4 a = q[0], b = q[1], c = q[2];
-        x.g[0] = a.z; x.g[1] = a.w; x.g[2] = b.x; x.g[3] = b.y;  // prefix @8, writer_id @20
-        x.snlo = c.x; x.snhi = c.y;                              // sn @32
-        x.tid = d.slot_tid[dl.reader_slot];
-        x.rec = dl.rec_idx;
-      }
+// The batch's first kernel also clears what the later ones count on: the other parity's topic
+// segments (the next batch's), the scans' tickets and look-back words, and it publishes the live
+// index's use as the earlier batches left it (pinned host memory, for reserve_live: read once
+// this batch's event has passed, no copy on the stream).
+__device__ __forceinline__ void batch_prologue(const TDev& d) {
+  const uint32_t t0 = blockIdx.x * TT + threadIdx.x, st = gridDim.x * TT;
+  for (uint32_t c = t0; c < d.nA; c += st) { d.segb_next[c] = NONE; d.sege_next[c] = 0u; }
+  for (uint32_t k = t0; k < 3u * d.ntl; k += st) d.lb[k] = 0ull;
+  if (t0 < 2u) d.ticket[t0] = 0u;
+  if (t0 == 0) {
+    __hip_atomic_store(d.h_used, *d.n_used, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    *d.nfr = 0ull;  // (tc_cscan sets it when the batch has deliveries)
+    d.kpre[0] = 0u;
+  }
+}
+
+// One position's flags (the change x of delivery dl, prev: the delivery before it in topic order,
+// same topic): GC, certain (stored unchecked: FL_INS), the same record as the previous position,
+// or a candidate (looked up in the live index, claimed in the batch map).
+__device__ __forceinline__ uint8_t mark_one(const TDev& d, uint64_t p, const KeyP& x, bool same_rec_before) {
+  if (x.rec == NONE) return 0;
+  uint8_t f = FL_VALID;
+  if ((x.snlo & 63u) == 0u) f |= FL_GC;  // (sn as usize) % 64 == 0 (:230-233)
+  // the same record delivered earlier to this topic (another reader of it): the change it stored
+  // (or found) is held now: max_keep >= 1 keeps the newest
+  if (same_rec_before) return f | FL_REP0;
+  const uint32_t t = x.tid;
+  const bool user_kind = ((x.g[3] >> 24) & 0xf0u) == 0u;  // EntityKind::is_user_defined (guid.rs:168-170)
+  // (a batch whose ingest overflowed its capacities may hold duplicates the proxies did not
+  // see: every delivery is checked then)
+  const bool cand = !d.simple[t] || d.E[t] < d.until[t] || !user_kind || (d.ovf && *d.ovf != 0u);
+  if (!cand) return f | FL_INS;
+  f |= FL_CAND;
+  const PEnt* e = p_find(d.P, d.pmask, x);
+  if (e && e->idx >= d.E[t]) f |= FL_PLIVE;
+  b_put(d.B, d.bmask, d.epoch, x, (uint32_t)p);
+  return f;
+}
+
+// No sort (at most one topic receives): position = delivery.  The changes are read from the
+// records, the positions marked, the topic's segment bounds found (atomics on the boundary
+// positions only), in one launch.
+__global__ __launch_bounds__(TT) void tc_gm(TDev d) {
+  batch_prologue(d);
+  const uint64_t nd = n_deliveries(d);
+  for (uint64_t p = (uint64_t)blockIdx.x * TT + threadIdx.x; p < nd; p += (uint64_t)gridDim.x * TT) {
+    const rtps_delivery dl = d.del[p];
+    const uint32_t c = d.slot_cid[dl.reader_slot];
+    uint8_t f = 0;
+    if (c < d.nA) {
+      const rtps_delivery pv = p > 0 ? d.del[p - 1] : rtps_delivery{NONE, 0, 0};
+      const bool pv_same = p > 0 && d.slot_cid[pv.reader_slot] == c;
+      if (!pv_same) atomicMin(&d.segb[c], (uint32_t)p);
+      if (p + 1 == nd || d.slot_cid[d.del[p + 1].reader_slot] != c) atomicMax(&d.sege[c], (uint32_t)p + 1u);
+      f = mark_one(d, p, key_of(d, dl), pv_same && pv.rec_idx == dl.rec_idx);
     }
-    d.kp[k] = x;
-    d.skey[k] = cid;
+    d.fl[p] = f;
+  }
+}
+
+// Sort mode: deliveries -> the sort pairs (compact topic, delivery index)
+__global__ __launch_bounds__(TT) void tc_gather(TDev d) {
+  batch_prologue(d);
+  const uint64_t nd = n_deliveries(d);
+  for (uint64_t k = (uint64_t)blockIdx.x * TT + threadIdx.x; k < d.max_del; k += (uint64_t)gridDim.x * TT) {
+    d.skey[k] = k < nd ? d.slot_cid[d.del[k].reader_slot] : d.nA;
     d.sval[k] = (uint32_t)k;
   }
 }
-
-// per position: GC, segment bounds, certain / same-record / candidate, the batch map
-__global__ __launch_bounds__(TT) void tc_mark(TDev d, uint64_t max_del) {
-  for (uint64_t p = (uint64_t)blockIdx.x * TT + threadIdx.x; p < max_del; p += (uint64_t)gridDim.x * TT) {
-    const uint32_t c = pos_cid(d, p);
-    const KeyP x = d.kp[pos_k(d, p)];
+// Sort mode: per position in topic order, the flags and the segment bounds
+__global__ __launch_bounds__(TT) void tc_mark(TDev d) {
+  const uint64_t nd = n_deliveries(d);
+  for (uint64_t p = (uint64_t)blockIdx.x * TT + threadIdx.x; p < nd; p += (uint64_t)gridDim.x * TT) {
+    const uint32_t c = d.skey2[p];
     uint8_t f = 0;
-    uint32_t kins = 0;
-    int32_t gcp = -1;
     if (c < d.nA) {
-      if (p == 0 || pos_cid(d, p - 1) != c) d.segb[c] = (uint32_t)p;
-      if (p + 1 == max_del || pos_cid(d, p + 1) != c) d.sege[c] = (uint32_t)p + 1u;
-    }
-    if (c < d.nA && x.rec != NONE) {
-      f = FL_VALID;
-      if ((x.snlo & 63u) == 0u) { f |= FL_GC; gcp = (int32_t)p; }  // (sn as usize) % 64 == 0 (:230-233)
-      // the same record delivered earlier to this topic (another reader of it): the change
-      // it stored (or found) is held now: max_keep >= 1 keeps the newest
-      const bool rep0 = p > 0 && pos_cid(d, p - 1) == c && d.kp[pos_k(d, p - 1)].rec == x.rec;
-      const uint32_t t = x.tid;
-      const bool user_kind = ((x.g[3] >> 24) & 0xf0u) == 0u;  // EntityKind::is_user_defined (guid.rs:168-170)
-      // (a batch whose ingest overflowed its capacities may hold duplicates the proxies did not
-      // see: every delivery is checked then)
-      const bool cand = !d.simple[t] || d.E[t] < d.until[t] || !user_kind || (d.ovf && *d.ovf != 0u);
-      if (rep0) {
-        f |= FL_REP0;
-      } else if (!cand) {
-        kins = 1;
-      } else {
-        f |= FL_CAND;
-        const PEnt* e = p_find(d.P, d.pmask, x);
-        if (e && e->idx >= d.E[t]) f |= FL_PLIVE;
-        b_put(d.B, d.bmask, d.epoch, x, (uint32_t)p);
-      }
+      const bool pv_same = p > 0 && d.skey2[p - 1] == c;
+      if (!pv_same) d.segb[c] = (uint32_t)p;
+      if (p + 1 == nd || d.skey2[p + 1] != c) d.sege[c] = (uint32_t)p + 1u;
+      const rtps_delivery dl = d.del[d.order[p]];
+      f = mark_one(d, p, key_of(d, dl), pv_same && d.del[d.order[p - 1]].rec_idx == dl.rec_idx);
     }
     d.fl[p] = f;
-    d.kins[p] = kins;
-    d.gcpos[p] = gcp;
-    d.fr[p] = 0;
-    d.frins[p] = 0;
-    d.rst[p] = 0;   // (tc_rdec's outputs for the repeats j < nfr <= p; the scans read all of them)
-    d.ramb[p] = 0;
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    d.rst[max_del] = 0;
-    d.ramb[max_del] = 0;
   }
 }
 
-// candidates: first occurrence not held live -> stored; else a repeat (resolved in order)
-__global__ __launch_bounds__(TT) void tc_class(TDev d, uint64_t max_del) {
-  for (uint64_t p = (uint64_t)blockIdx.x * TT + threadIdx.x; p < max_del; p += (uint64_t)gridDim.x * TT) {
-    const uint8_t f = d.fl[p];
-    if (!(f & FL_CAND)) continue;
-    const KeyP x = d.kp[pos_k(d, p)];
-    BEnt* e = b_find(d.B, d.bmask, d.epoch, x);
-    const bool rep = (e && e->minp < (uint32_t)p) || (f & FL_PLIVE);
-    if (rep) {
-      d.fr[p] = 1;
-      if (e) atomicAdd(&e->nrep, 1u);
-    } else {
-      d.kins[p] = 1;
+// ---- single-pass scans with decoupled look-back ----
+// A workgroup takes the next tile by ticket (so every earlier tile has started), publishes its
+// aggregate, adds its predecessors' (walking back until an inclusive prefix), publishes its
+// inclusive prefix.  A word: flag (1 aggregate, 2 inclusive) << 62 | value.
+constexpr uint32_t CPT = 8, TS = TT * CPT;  // positions per thread / per tile
+constexpr unsigned long long LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_VAL = (1ull << 62) - 1ull;
+constexpr unsigned long long M31 = (1ull << 31) - 1ull;
+// The words are self-contained (no data rides on them), so relaxed agent-scope atomics suffice:
+// no acquire / release fences (each would write back or invalidate the caches).
+__device__ __forceinline__ unsigned long long lb_get(unsigned long long* w) {
+  return __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lb_put(unsigned long long* w, unsigned long long v) {
+  __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Wave 0: the exclusive prefix of `tile` from its predecessors' words, 64 of them per step (lane l
+// reads tile - 1 - l): the step waits until every word up to the newest inclusive one is
+// published, then reduces them.  MAX: a running maximum, else the sum of two 31-bit halves
+// (counts of at most 2^31 - 1 positions: no carry between them).
+template <bool MAX>
+__device__ unsigned long long lb_prefix(unsigned long long* words, uint32_t tile, uint32_t lane) {
+  unsigned long long acc = 0;
+  for (int64_t hi = (int64_t)tile - 1; hi >= 0; hi -= 64) {
+    const int64_t t = hi - (int64_t)lane;
+    unsigned long long v;
+    uint32_t fi;
+    for (;;) {
+      v = t >= 0 ? lb_get(words + t) : LB_INC;  // (before tile 0: an inclusive zero)
+      const uint64_t inc = __ballot((v >> 62) == 2ull), wait = __ballot((v >> 62) == 0ull);
+      fi = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;
+      const uint64_t upto = fi >= 63u ? ~0ull : ((2ull << fi) - 1ull);
+      if (!(wait & upto)) break;
+      __builtin_amdgcn_s_sleep(1);
     }
+    unsigned long long x = lane <= fi ? (v & LB_VAL) : 0ull;
+#pragma unroll
+    for (uint32_t d = 32; d >= 1; d >>= 1) {
+      const unsigned long long y = __shfl_xor(x, d, 64);
+      x = MAX ? (y > x ? y : x) : x + y;
+    }
+    acc = MAX ? (x > acc ? x : acc) : acc + x;
+    if (fi < 64u) break;
+  }
+  return acc;
+}
+// block-wide exclusive scan of (a, b) sums and an inclusive max of m; totals to every thread
+__device__ __forceinline__ void block_scan3(uint32_t& a, uint32_t& b, int32_t& m, uint32_t& ta, uint32_t& tb,
+                                            int32_t& tm) {
+  __shared__ uint32_t s_a[TT / 64], s_b[TT / 64];
+  __shared__ int32_t s_m[TT / 64];
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  uint32_t ia = a, ib = b;
+  int32_t im = m;
+#pragma unroll
+  for (uint32_t k = 1; k < 64; k <<= 1) {
+    const uint32_t ya = (uint32_t)__shfl_up((int)ia, k, 64), yb = (uint32_t)__shfl_up((int)ib, k, 64);
+    const int32_t ym = __shfl_up(im, k, 64);
+    if (lane >= k) { ia += ya; ib += yb; im = ym > im ? ym : im; }
+  }
+  if (lane == 63u) { s_a[wave] = ia; s_b[wave] = ib; s_m[wave] = im; }
+  __syncthreads();
+  uint32_t pa = 0, pb = 0;
+  int32_t pm = -1;
+  ta = 0; tb = 0; tm = -1;
+#pragma unroll
+  for (uint32_t w = 0; w < TT / 64; ++w) {
+    if (w < wave) { pa += s_a[w]; pb += s_b[w]; pm = s_m[w] > pm ? s_m[w] : pm; }
+    ta += s_a[w]; tb += s_b[w]; tm = s_m[w] > tm ? s_m[w] : tm;
+  }
+  a = pa + ia - a;  // exclusive
+  b = pb + ib - b;
+  m = pm > im ? pm : im;  // inclusive
+  __syncthreads();  // (the shared words are reused by the caller's next scan)
+}
+
+// candidates: first occurrence not held live -> stored; else a repeat (resolved below).  Then the
+// scans every later pass reads: kpre (stored positions before p), lgc (last GC position <= p), the
+// repeat list (frlist, nfr).  One launch, no host count.
+__global__ __launch_bounds__(TT) void tc_cscan(TDev d) {
+  __shared__ uint32_t s_tile;
+  __shared__ unsigned long long s_pre[2];
+  if (threadIdx.x == 0) s_tile = atomicAdd(&d.ticket[0], 1u);
+  __syncthreads();
+  const uint32_t tile = s_tile;
+  const uint64_t nd = n_deliveries(d);
+  const uint64_t base = (uint64_t)tile * TS;
+  if (base >= nd) return;  // (no later tile looks back at it)
+  const uint64_t p0 = base + (uint64_t)threadIdx.x * CPT;
+  uint8_t fv[CPT];
+  {
+    const uint2 w = p0 + CPT <= nd ? *reinterpret_cast<const uint2*>(d.fl + p0) : uint2{0u, 0u};
+#pragma unroll
+    for (uint32_t i = 0; i < CPT; ++i)
+      fv[i] = p0 + CPT <= nd ? (uint8_t)((i < 4 ? w.x >> (8 * i) : w.y >> (8 * (i - 4))) & 0xffu)
+                             : (p0 + i < nd ? d.fl[p0 + i] : (uint8_t)0);
+  }
+  uint32_t ins = 0, rep = 0;
+  int32_t gc = -1;
+#pragma unroll
+  for (uint32_t i = 0; i < CPT; ++i) {
+    const uint64_t p = p0 + i;
+    uint8_t f = fv[i];
+    if (f & FL_CAND) {
+      const KeyP x = key_of(d, d.del[pos_k(d, p)]);
+      BEnt* e = b_find(d.B, d.bmask, d.epoch, x);
+      if ((e && e->minp < (uint32_t)p) || (f & FL_PLIVE)) {
+        f |= FL_REP;
+        if (e) atomicAdd(&e->nrep, 1u);
+      } else {
+        f |= FL_INS;
+      }
+      d.fl[p] = f;
+      fv[i] = f;
+    }
+    ins += (f & FL_INS) ? 1u : 0u;
+    rep += (f & FL_REP) ? 1u : 0u;
+    if (f & FL_GC) gc = (int32_t)p;
+  }
+  uint32_t ta, tb;
+  int32_t tm;
+  uint32_t ea = ins, eb = rep;
+  int32_t im = gc;
+  block_scan3(ea, eb, im, ta, tb, tm);
+  unsigned long long* const lw = d.lb;
+  unsigned long long* const lg = d.lb + d.ntl;
+  if (threadIdx.x < 64u) {
+    const uint32_t lane = threadIdx.x;
+    const unsigned long long agg = (unsigned long long)ta | ((unsigned long long)tb << 31);
+    const unsigned long long gm = (unsigned long long)(tm + 1);
+    if (tile == 0) {
+      if (lane == 0) { lb_put(lw, LB_INC | agg); lb_put(lg, LB_INC | gm); s_pre[0] = 0; s_pre[1] = 0; }
+    } else {
+      if (lane == 0) { lb_put(lw + tile, LB_AGG | agg); lb_put(lg + tile, LB_AGG | gm); }
+      const unsigned long long ex = lb_prefix<false>(lw, tile, lane), exm = lb_prefix<true>(lg, tile, lane);
+      if (lane == 0) {
+        lb_put(lw + tile, LB_INC | (ex + agg));
+        lb_put(lg + tile, LB_INC | (exm > gm ? exm : gm));
+        s_pre[0] = ex;
+        s_pre[1] = exm;
+      }
+    }
+  }
+  __syncthreads();
+  uint32_t ki = (uint32_t)(s_pre[0] & M31) + ea, kr = (uint32_t)(s_pre[0] >> 31) + eb;
+  // the last GC position before this thread's first: the earlier tiles' (look-back), then the
+  // earlier threads' (the block scan's inclusive value of the previous thread)
+  const int32_t before = (int32_t)s_pre[1] - 1;
+  int32_t cur;
+  {
+    __shared__ int32_t s_last[TT / 64];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const int32_t prev_incl = __shfl_up(im, 1, 64);
+    if (lane == 63u) s_last[wave] = im;
+    __syncthreads();
+    const int32_t blk_ex = lane ? prev_incl : (wave ? s_last[wave - 1] : -1);
+    cur = blk_ex > before ? blk_ex : before;
+  }
+  uint32_t kv[CPT];
+  int32_t gv[CPT];
+#pragma unroll
+  for (uint32_t i = 0; i < CPT; ++i) {
+    const uint64_t p = p0 + i;
+    const uint8_t f = fv[i];
+    kv[i] = ki;
+    if (f & FL_GC) cur = (int32_t)p;
+    gv[i] = cur;
+    if (p < nd && (f & FL_REP)) d.frlist[kr++] = (uint32_t)p;
+    ki += (f & FL_INS) ? 1u : 0u;
+  }
+  if (p0 + CPT <= nd) {
+    reinterpret_cast<uint4*>(d.kpre + p0)[0] = uint4{kv[0], kv[1], kv[2], kv[3]};
+    reinterpret_cast<uint4*>(d.kpre + p0)[1] = uint4{kv[4], kv[5], kv[6], kv[7]};
+    reinterpret_cast<int4*>(d.lgc + p0)[0] = int4{gv[0], gv[1], gv[2], gv[3]};
+    reinterpret_cast<int4*>(d.lgc + p0)[1] = int4{gv[4], gv[5], gv[6], gv[7]};
+  } else {
+#pragma unroll
+    for (uint32_t i = 0; i < CPT; ++i)
+      if (p0 + i < nd) { d.kpre[p0 + i] = kv[i]; d.lgc[p0 + i] = gv[i]; }
+  }
+  if (p0 < nd && nd <= p0 + CPT) {  // the thread holding the last position: the totals
+    d.kpre[nd] = ki;
+    *d.nfr = kr;
   }
 }
 
@@ -362,54 +566,111 @@ __device__ __forceinline__ uint32_t lower_bound(const uint32_t* a, uint32_t lo, 
 // already stored.  (The SPDP reader with half of a 1M batch repeats: 1.9 s when every repeat
 // was resolved in order, round 4's form.)
 constexpr uint8_t RD_HOLD = 0, RD_STORE = 1, RD_AMB = 2;
-__global__ __launch_bounds__(TT) void tc_rdec(TDev d) {
-  const uint32_t nfr = (uint32_t)*d.nfr;
-  for (uint32_t j = blockIdx.x * TT + threadIdx.x; j < nfr; j += gridDim.x * TT) {
-    const uint32_t p = d.frlist[j];
-    const uint32_t c = pos_cid(d, p);
-    const uint32_t t = d.cid_tid[c];
-    const uint32_t b = d.segb[c];
-    const uint32_t jb = lower_bound(d.frlist, 0, j, b);  // the topic's first repeat
-    const KeyP x = d.kp[pos_k(d, p)];
-    const BEnt* be = b_find(d.B, d.bmask, d.epoch, x);
-    uint8_t dec = RD_AMB;
-    if (be && be->nrep == 1u) {
-      const uint64_t K = d.K[t], E0 = d.E[t], I0 = d.I[t];
-      const uint32_t kb = d.kpre[b];
-      const int64_t g = d.lgc[p];
-      const bool gc = g >= (int64_t)b;  // a GC of this topic at or before p
-      const PEnt* pe = p_find(d.P, d.pmask, x);
-      const uint32_t f = be->minp;
-      const bool has_f = f < p && d.kins[f];
-      // live entry: sure held / sure not held
-      int live = -1;  // -1 none, 0 not held, 1 held, 2 unsure
-      if (pe) {
-        if (!gc) {
-          live = pe->idx >= E0 ? 1 : 0;
-        } else {
-          const uint64_t Ig_lo = I0 + (d.kpre[g] - kb);
-          const uint64_t Ig_hi = Ig_lo + (lower_bound(d.frlist, jb, j, (uint32_t)g) - jb);
-          const uint64_t E_lo = Ig_lo > K && Ig_lo - K > E0 ? Ig_lo - K : E0;
-          const uint64_t E_hi = Ig_hi > K && Ig_hi - K > E0 ? Ig_hi - K : E0;
-          live = pe->idx >= E_hi ? 1 : pe->idx < E_lo ? 0 : 2;
-        }
+__device__ __forceinline__ uint8_t rdec_one(const TDev& d, uint32_t j) {
+  const uint32_t p = d.frlist[j];
+  const uint32_t c = pos_cid(d, p);
+  const uint32_t t = d.cid_tid[c];
+  const uint32_t b = d.segb[c];
+  const uint32_t jb = lower_bound(d.frlist, 0, j, b);  // the topic's first repeat
+  const KeyP x = key_of(d, d.del[pos_k(d, p)]);
+  const BEnt* be = b_find(d.B, d.bmask, d.epoch, x);
+  uint8_t dec = RD_AMB;
+  if (be && be->nrep == 1u) {
+    const uint64_t K = d.K[t], E0 = d.E[t], I0 = d.I[t];
+    const uint32_t kb = d.kpre[b];
+    const int64_t g = d.lgc[p];
+    const bool gc = g >= (int64_t)b;  // a GC of this topic at or before p
+    const PEnt* pe = p_find(d.P, d.pmask, x);
+    const uint32_t f = be->minp;
+    const bool has_f = f < p && ins_at(d, f);
+    // live entry: sure held / sure not held
+    int live = -1;  // -1 none, 0 not held, 1 held, 2 unsure
+    if (pe) {
+      if (!gc) {
+        live = pe->idx >= E0 ? 1 : 0;
+      } else {
+        const uint64_t Ig_lo = I0 + (d.kpre[g] - kb);
+        const uint64_t Ig_hi = Ig_lo + (lower_bound(d.frlist, jb, j, (uint32_t)g) - jb);
+        const uint64_t E_lo = Ig_lo > K && Ig_lo - K > E0 ? Ig_lo - K : E0;
+        const uint64_t E_hi = Ig_hi > K && Ig_hi - K > E0 ? Ig_hi - K : E0;
+        live = pe->idx >= E_hi ? 1 : pe->idx < E_lo ? 0 : 2;
       }
-      int first = -1;
-      if (has_f) {
-        if (!gc || f >= (uint32_t)g) {
-          first = 1;
-        } else {
-          const uint64_t A = d.kpre[g] - d.kpre[f];
-          const uint64_t D = lower_bound(d.frlist, jb, j, (uint32_t)g) - lower_bound(d.frlist, jb, j, f);
-          first = A + D <= K ? 1 : A > K ? 0 : 2;
-        }
-      }
-      if (live == 1 || first == 1) dec = RD_HOLD;                     // some last insertion is held
-      else if (live != 2 && first != 2) dec = RD_STORE;                // none is (or there is none)
     }
-    d.rdec[j] = dec;
-    d.rst[j] = dec == RD_STORE ? 1u : 0u;
-    d.ramb[j] = dec == RD_AMB ? 1u : 0u;
+    int first = -1;
+    if (has_f) {
+      if (!gc || f >= (uint32_t)g) {
+        first = 1;
+      } else {
+        const uint64_t A = d.kpre[g] - d.kpre[f];
+        const uint64_t D = lower_bound(d.frlist, jb, j, (uint32_t)g) - lower_bound(d.frlist, jb, j, f);
+        first = A + D <= K ? 1 : A > K ? 0 : 2;
+      }
+    }
+    if (live == 1 || first == 1) dec = RD_HOLD;                     // some last insertion is held
+    else if (live != 2 && first != 2) dec = RD_STORE;                // none is (or there is none)
+  }
+  return dec;
+}
+// per repeat the decision, then the scans: rpre (sure stores before j), the undecided list (amb,
+// namb).  Single pass like tc_cscan; a batch without repeats costs one workgroup's ticket.
+__global__ __launch_bounds__(TT) void tc_rscan(TDev d) {
+  __shared__ uint32_t s_tile;
+  __shared__ unsigned long long s_pre;
+  if (threadIdx.x == 0) s_tile = atomicAdd(&d.ticket[1], 1u);
+  __syncthreads();
+  const uint32_t tile = s_tile;
+  const uint32_t nfr = (uint32_t)*d.nfr;
+  if (nfr == 0u) {
+    if (tile == 0 && threadIdx.x == 0) { d.rpre[0] = 0u; *d.namb = 0ull; }
+    return;
+  }
+  const uint64_t base = (uint64_t)tile * TS;
+  if (base >= nfr) return;
+  const uint64_t j0 = base + (uint64_t)threadIdx.x * CPT;
+  uint8_t dv[CPT];
+  uint32_t ns = 0, na = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < CPT; ++i) {
+    const uint64_t j = j0 + i;
+    uint8_t dec = RD_HOLD;
+    if (j < nfr) {
+      dec = rdec_one(d, (uint32_t)j);
+      d.rdec[j] = dec;
+      d.frins[d.frlist[j]] = 0;  // (set below for the stored ones: tc_resolve, tc_rfill)
+    }
+    dv[i] = j < nfr ? dec : (uint8_t)0xff;
+    ns += dec == RD_STORE && j < nfr;
+    na += dec == RD_AMB && j < nfr;
+  }
+  uint32_t ta, tb;
+  int32_t tm, im = -1;
+  uint32_t es = ns, ea = na;
+  block_scan3(es, ea, im, ta, tb, tm);
+  unsigned long long* const lw = d.lb + 2u * d.ntl;
+  if (threadIdx.x < 64u) {
+    const uint32_t lane = threadIdx.x;
+    const unsigned long long agg = (unsigned long long)ta | ((unsigned long long)tb << 31);
+    if (tile == 0) {
+      if (lane == 0) { lb_put(lw, LB_INC | agg); s_pre = 0; }
+    } else {
+      if (lane == 0) lb_put(lw + tile, LB_AGG | agg);
+      const unsigned long long ex = lb_prefix<false>(lw, tile, lane);
+      if (lane == 0) { lb_put(lw + tile, LB_INC | (ex + agg)); s_pre = ex; }
+    }
+  }
+  __syncthreads();
+  uint32_t rs = (uint32_t)(s_pre & M31) + es, ra = (uint32_t)(s_pre >> 31) + ea;
+#pragma unroll
+  for (uint32_t i = 0; i < CPT; ++i) {
+    const uint64_t j = j0 + i;
+    if (j >= nfr) break;
+    d.rpre[j] = rs;
+    if (dv[i] == RD_STORE) ++rs;
+    if (dv[i] == RD_AMB) d.amb[ra++] = (uint32_t)j;
+  }
+  if (j0 < nfr && nfr <= j0 + CPT) {  // the thread holding the last repeat: the totals
+    d.rpre[nfr] = rs;
+    *d.namb = ra;
   }
 }
 
@@ -432,7 +693,7 @@ __global__ __launch_bounds__(TT) void tc_resolve(TDev d) {
   const uint32_t b = d.segb[c], e = d.sege[c];
   if (b == NONE) { d.frb[c] = d.fre[c] = 0; d.ab[c] = d.ae[c] = 0; return; }
   const uint64_t K = d.K[t], E0 = d.E[t];
-  const uint32_t nfr = (uint32_t)*d.nfr, na = (uint32_t)*d.namb;
+  const uint32_t nfr = (uint32_t)*d.nfr, na = nfr ? (uint32_t)*d.namb : 0u;
   const uint32_t jb = lower_bound(d.frlist, 0, nfr, b), je = lower_bound(d.frlist, jb, nfr, e);
   const uint32_t ab = lower_bound(d.amb, 0, na, jb), ae = lower_bound(d.amb, ab, na, je);
   d.frb[c] = jb;
@@ -443,14 +704,14 @@ __global__ __launch_bounds__(TT) void tc_resolve(TDev d) {
   uint32_t RA = 0;  // undecided repeats stored so far
   auto E_at = [&](int64_t g, uint32_t jcur, uint32_t acur) -> uint64_t {  // E after the GCs up to g
     if (g < (int64_t)b) return E0;
-    const uint64_t Ig = I0 + (d.kpre[g] - kb) + rep_before(d, (uint32_t)g, jb, jcur, ab, acur);
+    const uint64_t Ig = I0 + (d.kpre[g] - kb) + (nfr ? rep_before(d, (uint32_t)g, jb, jcur, ab, acur) : 0u);
     return Ig > K && Ig - K > E0 ? Ig - K : E0;
   };
   for (uint32_t a = ab; a < ae; ++a) {
     const uint32_t j = d.amb[a];
     const uint32_t p = d.frlist[j];
     const uint64_t E = E_at(d.lgc[p], j, a);
-    const KeyP x = d.kp[pos_k(d, p)];
+    const KeyP x = key_of(d, d.del[pos_k(d, p)]);
     BEnt* be = b_find(d.B, d.bmask, d.epoch, x);
     // the key's last insertion before p: a stored repeat, its first occurrence (stored unless a
     // repeat itself), or the live index
@@ -459,7 +720,7 @@ __global__ __launch_bounds__(TT) void tc_resolve(TDev d) {
     if (pe) L = pe->idx;
     if (be) {
       const uint32_t f = be->minp;
-      if (f < p && d.kins[f]) {
+      if (f < p && ins_at(d, f)) {
         const uint64_t If = I0 + (d.kpre[f] - kb) + rep_before(d, f, jb, j, ab, a);
         if (L == NO_IDX || If > L) L = If;
       }
@@ -476,7 +737,7 @@ __global__ __launch_bounds__(TT) void tc_resolve(TDev d) {
     d.acum[a] = RA;
   }
   const uint64_t E = E_at(d.lgc[e - 1], je, ae);
-  d.I[t] = I0 + (d.kpre[e - 1] + d.kins[e - 1] - kb) + (d.rpre[je] - d.rpre[jb]) + RA;
+  d.I[t] = I0 + (d.kpre[e] - kb) + (nfr ? d.rpre[je] - d.rpre[jb] : 0u) + RA;
   d.E[t] = E;
 }
 
@@ -499,31 +760,36 @@ __global__ __launch_bounds__(TT) void tc_rfill(TDev d) {
   }
 }
 
-// per position: the flag on the delivery, survivors into the live index
-__global__ __launch_bounds__(TT) void tc_final(TDev d, rtps_delivery* del, uint64_t max_del) {
-  for (uint64_t p = (uint64_t)blockIdx.x * TT + threadIdx.x; p < max_del; p += (uint64_t)gridDim.x * TT) {
+// per position: the flag on the delivery (its whole 8-B entry rewritten: full-line stores),
+// survivors into the live index
+__global__ __launch_bounds__(TT) void tc_final(TDev d) {
+  const uint64_t nd = n_deliveries(d);
+  const uint32_t nfr = (uint32_t)*d.nfr;
+  for (uint64_t p = (uint64_t)blockIdx.x * TT + threadIdx.x; p < nd; p += (uint64_t)gridDim.x * TT) {
     const uint8_t f = d.fl[p];
     if (!(f & FL_VALID)) continue;
     const uint32_t k = pos_k(d, p);
-    const uint32_t c = pos_cid(d, p);
-    const bool ins = d.kins[p] || d.frins[p];
-    rtps_delivery* dl = del + k;
-    dl->flags = (uint16_t)((dl->flags & ~RTPS_DELIVERY_CACHED) | (ins ? RTPS_DELIVERY_CACHED : 0u));
+    rtps_delivery dl = d.del[k];
+    const uint32_t c = d.order ? d.skey2[p] : d.slot_cid[dl.reader_slot];
+    const bool rp = (f & FL_REP) != 0;
+    const bool ins = (f & FL_INS) || (rp && d.frins[p]);
+    dl.flags = (uint16_t)((dl.flags & ~RTPS_DELIVERY_CACHED) | (ins ? RTPS_DELIVERY_CACHED : 0u));
+    d.del[k] = dl;
     if (!ins) continue;
-    const KeyP x = d.kp[k];
     uint64_t idx;
-    if (d.fr[p]) {
+    if (rp) {
       idx = d.fridx[p];
     } else {
       const uint32_t jb = d.frb[c], je = d.fre[c];
       uint32_t r = 0;
-      if (je > jb) {
+      if (nfr && je > jb) {
         const uint32_t jq = lower_bound(d.frlist, jb, je, (uint32_t)p);
         r = jq > jb ? d.frcum[jq - 1] : 0u;
       }
       idx = d.ibase[c] + (d.kpre[p] - d.kpre[d.segb[c]]) + r;
     }
-    if (idx >= d.E[x.tid] && !p_put(d.P, d.pmask, x, idx, d.n_used))
+    const uint32_t t = d.cid_tid[c];
+    if (idx >= d.E[t] && !p_put(d.P, d.pmask, key_of(d, dl), idx, d.n_used))
       atomicAdd(reinterpret_cast<unsigned long long*>(d.n_full), 1ull);
   }
 }
@@ -573,16 +839,18 @@ struct TopicState {
   uint64_t bcap = 0;
   uint32_t epoch = 0;
   uint64_t cap = 0;  // batch scratch capacity (deliveries)
-  KeyP* kp = nullptr;
-  uint32_t *skey = nullptr, *skey2 = nullptr, *sval = nullptr, *order = nullptr, *kins = nullptr, *kpre = nullptr;
-  int32_t *gcpos = nullptr, *lgc = nullptr;
-  uint8_t *fl = nullptr, *fr = nullptr, *frins = nullptr;
+  uint32_t *skey = nullptr, *skey2 = nullptr, *sval = nullptr, *order = nullptr, *kpre = nullptr;
+  int32_t* lgc = nullptr;
+  uint8_t *fl = nullptr, *frins = nullptr;
+  uint32_t* ticket = nullptr;          // the single-pass scans' tile tickets [2]
+  unsigned long long* lb = nullptr;    // their look-back words [3 * ntl]
+  uint32_t ntl = 0;
   uint32_t *frlist = nullptr, *frcum = nullptr;
   uint64_t *fridx = nullptr, *nfr = nullptr, *n_full = nullptr;
-  uint32_t *segb = nullptr, *sege = nullptr, *frb = nullptr, *fre = nullptr;
+  uint32_t *segb = nullptr, *sege = nullptr, *frb = nullptr, *fre = nullptr;  // segb / sege: [2 * acap], by batch parity
   uint64_t* ibase = nullptr;
   uint8_t *rdec = nullptr, *ramb = nullptr;                         // [n] parallel repeat decisions
-  uint32_t *rst = nullptr, *rpre = nullptr, *amb = nullptr, *acum = nullptr;  // [n + 1]
+  uint32_t *rpre = nullptr, *amb = nullptr, *acum = nullptr;  // [n + 1]
   uint64_t* namb = nullptr;
   uint32_t *ab = nullptr, *ae = nullptr;  // [nA]
   uint32_t acap = 0;  // [nA] arrays' capacity
@@ -598,11 +866,11 @@ static void dfree(T*& p) {
 }
 
 static void free_scratch(TopicState* s) {
-  dfree(s->kp); dfree(s->skey); dfree(s->skey2); dfree(s->sval); dfree(s->order); dfree(s->kins); dfree(s->kpre);
-  dfree(s->gcpos); dfree(s->lgc); dfree(s->fl); dfree(s->fr); dfree(s->frins); dfree(s->frlist); dfree(s->frcum);
-  dfree(s->fridx); dfree(s->B); dfree(s->tmp);
-  dfree(s->rdec); dfree(s->ramb); dfree(s->rst); dfree(s->rpre); dfree(s->amb); dfree(s->acum);
-  s->cap = 0; s->bcap = 0; s->tmp_bytes = 0;
+  dfree(s->skey); dfree(s->skey2); dfree(s->sval); dfree(s->order); dfree(s->kpre);
+  dfree(s->lgc); dfree(s->fl); dfree(s->frins); dfree(s->frlist); dfree(s->frcum);
+  dfree(s->fridx); dfree(s->B); dfree(s->tmp); dfree(s->lb);
+  dfree(s->rdec); dfree(s->rpre); dfree(s->amb); dfree(s->acum);
+  s->cap = 0; s->bcap = 0; s->tmp_bytes = 0; s->ntl = 0;
 }
 
 TopicState* rtps_topic_state_new(int device) {
@@ -613,6 +881,7 @@ TopicState* rtps_topic_state_new(int device) {
   s->nt = NSLOT;  // no configured topics: every slot its own
   bool ok = dmalloc((void**)&s->slot_tid, NSLOT * 4) && dmalloc((void**)&s->slot_cid, NSLOT * 4) &&
             dmalloc((void**)&s->nfr, 8) && dmalloc((void**)&s->n_full, 8) && dmalloc((void**)&s->n_used, 8) &&
+            dmalloc((void**)&s->ticket, 8) &&
             dmalloc((void**)&s->namb, 8) &&
             hipMemset(s->n_full, 0, 8) == hipSuccess && hipMemset(s->n_used, 0, 8) == hipSuccess &&
             hipHostMalloc((void**)&s->h_used, 8, hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess &&
@@ -626,7 +895,7 @@ void rtps_topic_state_free(TopicState* s) {
   free_scratch(s);
   dfree(s->slot_tid); dfree(s->slot_cid); dfree(s->cid_tid); dfree(s->K); dfree(s->simple); dfree(s->I);
   dfree(s->E); dfree(s->until); dfree(s->P); dfree(s->nfr); dfree(s->n_full); dfree(s->segb); dfree(s->sege);
-  dfree(s->frb); dfree(s->fre); dfree(s->ibase); dfree(s->n_used);
+  dfree(s->frb); dfree(s->fre); dfree(s->ibase); dfree(s->n_used); dfree(s->ticket);
   if (s->h_used) (void)hipHostFree(s->h_used);
   if (s->used_ev) (void)hipEventDestroy(s->used_ev);
   delete s;
@@ -679,12 +948,16 @@ static int build(TopicState* s, const uint32_t* set_first, const rtps_target* en
     dfree(s->cid_tid); dfree(s->segb); dfree(s->sege); dfree(s->frb); dfree(s->fre); dfree(s->ibase);
     dfree(s->ab); dfree(s->ae);
     const uint32_t a = s->nA ? s->nA : 1;
-    if (!dmalloc((void**)&s->cid_tid, a * 4ull) || !dmalloc((void**)&s->segb, a * 4ull) ||
-        !dmalloc((void**)&s->sege, a * 4ull) || !dmalloc((void**)&s->frb, a * 4ull) || !dmalloc((void**)&s->fre, a * 4ull) ||
+    if (!dmalloc((void**)&s->cid_tid, a * 4ull) || !dmalloc((void**)&s->segb, 2 * a * 4ull) ||
+        !dmalloc((void**)&s->sege, 2 * a * 4ull) || !dmalloc((void**)&s->frb, a * 4ull) || !dmalloc((void**)&s->fre, a * 4ull) ||
         !dmalloc((void**)&s->ibase, a * 8ull) || !dmalloc((void**)&s->ab, a * 4ull) || !dmalloc((void**)&s->ae, a * 4ull))
       return RTPS_RX_ENOMEM;
     s->acap = a;
   }
+  // both parity buffers of the topic segments start empty (each batch clears the next one's)
+  if (hipMemsetAsync(s->segb, 0xff, 2 * s->acap * 4ull, st) != hipSuccess ||
+      hipMemsetAsync(s->sege, 0, 2 * s->acap * 4ull, st) != hipSuccess)
+    return RTPS_RX_EHIP;
   if (hipMemcpyAsync(s->K, K.data(), nt * 4ull, hipMemcpyHostToDevice, st) != hipSuccess ||
       hipMemcpyAsync(s->simple, simple.data(), nt, hipMemcpyHostToDevice, st) != hipSuccess ||
       hipMemcpyAsync(s->slot_tid, slot_tid.data(), NSLOT * 4ull, hipMemcpyHostToDevice, st) != hipSuccess ||
@@ -819,38 +1092,33 @@ static int reserve_scratch(TopicState* s, uint64_t n, hipStream_t st) {
   if (hipStreamSynchronize(st) != hipSuccess) return RTPS_RX_EHIP;
   free_scratch(s);
   const uint64_t bcap = pow2_at_least(2 * n + 64);
-  bool ok = dmalloc((void**)&s->kp, n * sizeof(KeyP)) && dmalloc((void**)&s->skey, n * 4) &&
-            dmalloc((void**)&s->skey2, n * 4) && dmalloc((void**)&s->sval, n * 4) && dmalloc((void**)&s->order, n * 4) &&
-            dmalloc((void**)&s->kins, n * 4) && dmalloc((void**)&s->kpre, n * 4) && dmalloc((void**)&s->gcpos, n * 4) &&
-            dmalloc((void**)&s->lgc, n * 4) && dmalloc((void**)&s->fl, n) && dmalloc((void**)&s->fr, n) &&
-            dmalloc((void**)&s->frins, n) && dmalloc((void**)&s->frlist, n * 4) && dmalloc((void**)&s->frcum, n * 4) &&
+  const uint32_t ntl = (uint32_t)((n + TS - 1) / TS);
+  bool ok = dmalloc((void**)&s->skey, n * 4) && dmalloc((void**)&s->skey2, n * 4) && dmalloc((void**)&s->sval, n * 4) &&
+            dmalloc((void**)&s->order, n * 4) && dmalloc((void**)&s->kpre, (n + 1) * 4) &&
+            dmalloc((void**)&s->lgc, n * 4) && dmalloc((void**)&s->fl, n + 8) && dmalloc((void**)&s->frins, n) &&
+            dmalloc((void**)&s->frlist, n * 4) && dmalloc((void**)&s->frcum, n * 4) &&
             dmalloc((void**)&s->fridx, n * 8) && dmalloc((void**)&s->B, bcap * sizeof(BEnt)) &&
-            dmalloc((void**)&s->rdec, n) && dmalloc((void**)&s->ramb, n + 1) && dmalloc((void**)&s->rst, (n + 1) * 4) &&
-            dmalloc((void**)&s->rpre, (n + 1) * 4) && dmalloc((void**)&s->amb, (n + 1) * 4) &&
-            dmalloc((void**)&s->acum, (n + 1) * 4) &&
+            dmalloc((void**)&s->rdec, n) && dmalloc((void**)&s->rpre, (n + 1) * 4) &&
+            dmalloc((void**)&s->amb, (n + 1) * 4) && dmalloc((void**)&s->acum, (n + 1) * 4) &&
+            dmalloc((void**)&s->lb, 3ull * ntl * 8) &&
             hipMemsetAsync(s->B, 0, bcap * sizeof(BEnt), st) == hipSuccess;
-  size_t b1 = 0, b2 = 0, b3 = 0, b4 = 0;
-  ok = ok && rtps_sort_pairs(nullptr, b1, s->skey, s->skey2, s->sval, s->order, (uint32_t)n, 17, st) == hipSuccess;
-  ok = ok && hipcub::DeviceScan::ExclusiveSum(nullptr, b2, s->kins, s->kpre, (int64_t)n, st) == hipSuccess;
-  ok = ok && hipcub::DeviceScan::InclusiveScan(nullptr, b3, s->gcpos, s->lgc, hipcub::Max(), (int64_t)n, st) ==
-                 hipSuccess;
-  ok = ok && hipcub::DeviceSelect::Flagged(nullptr, b4, hipcub::CountingInputIterator<uint32_t>(0), s->fr, s->frlist,
-                                           s->nfr, (int64_t)n, st) == hipSuccess;
-  size_t b5 = 0, b6 = 0;
-  ok = ok && hipcub::DeviceScan::ExclusiveSum(nullptr, b5, s->rst, s->rpre, (int64_t)n + 1, st) == hipSuccess;
-  ok = ok && hipcub::DeviceSelect::Flagged(nullptr, b6, hipcub::CountingInputIterator<uint32_t>(0), s->ramb, s->amb,
-                                           s->namb, (int64_t)n, st) == hipSuccess;
-  size_t tb = b1;
-  for (size_t b : {b2, b3, b4, b5, b6}) tb = b > tb ? b : tb;
+  size_t tb = 0;  // the sort's temporary storage (more than one topic receives)
+  ok = ok && rtps_sort_pairs(nullptr, tb, s->skey, s->skey2, s->sval, s->order, (uint32_t)n, 17, st) == hipSuccess;
   ok = ok && dmalloc(&s->tmp, tb);
   if (!ok) { free_scratch(s); return RTPS_RX_ENOMEM; }
   s->tmp_bytes = tb;
   s->cap = n;
   s->bcap = bcap;
+  s->ntl = ntl;
   s->epoch = 0;
   return RTPS_RX_OK;
 }
 
+// A batch in six launches when at most one topic receives (no sort): tc_gm (changes + marks),
+// tc_cscan (candidates + the position scans), tc_rscan (repeats' decisions + their scans),
+// tc_resolve (per topic), tc_rfill, tc_final.  Every launch reads the delivery count on the
+// device, so a batch sized by its capacity costs only its deliveries; a batch without
+// candidates leaves tc_rscan / tc_rfill one ticket / an empty loop.
 int rtps_topic_apply(TopicState* s, hipStream_t st, const rtps_record* recs, const uint64_t* n_records,
                      uint64_t max_records, rtps_delivery* del, const uint64_t* n_del, uint64_t max_del,
                      const uint64_t* ovf) {
@@ -861,58 +1129,52 @@ int rtps_topic_apply(TopicState* s, hipStream_t st, const rtps_record* recs, con
   if (rc) return rc;
   rc = reserve_live(s, max_del, st);
   if (rc) return rc;
-  if (++s->epoch == 0u) {  // batch-map tags would repeat: clear it
-    if (hipMemsetAsync(s->B, 0, s->bcap * sizeof(BEnt), st) != hipSuccess) return RTPS_RX_EHIP;
+  if (++s->epoch == 0u) {  // batch-map tags would repeat: clear it (and restart the segment parity)
+    if (hipMemsetAsync(s->B, 0, s->bcap * sizeof(BEnt), st) != hipSuccess ||
+        hipMemsetAsync(s->segb, 0xff, 2 * s->acap * 4ull, st) != hipSuccess ||
+        hipMemsetAsync(s->sege, 0, 2 * s->acap * 4ull, st) != hipSuccess)
+      return RTPS_RX_EHIP;
     s->epoch = 1;
   }
   TDev d{};
   d.slot_tid = s->slot_tid; d.slot_cid = s->slot_cid; d.cid_tid = s->cid_tid; d.simple = s->simple; d.K = s->K;
   d.I = s->I; d.E = s->E; d.until = s->until; d.P = s->P; d.pmask = s->pcap - 1; d.B = s->B; d.bmask = s->bcap - 1;
   d.epoch = s->epoch; d.nA = s->nA;
-  d.kp = s->kp; d.skey = s->skey; d.skey2 = s->skey2; d.sval = s->sval; d.order = s->nA > 1 ? s->order : nullptr;
-  d.fl = s->fl; d.kins = s->kins; d.kpre = s->kpre; d.gcpos = s->gcpos; d.lgc = s->lgc; d.fr = s->fr;
-  d.frins = s->frins; d.frlist = s->frlist; d.nfr = s->nfr; d.frcum = s->frcum; d.fridx = s->fridx;
-  d.segb = s->segb; d.sege = s->sege; d.frb = s->frb; d.fre = s->fre; d.ibase = s->ibase; d.n_full = s->n_full;
+  d.recs = recs; d.n_records = n_records; d.max_records = max_records; d.del = del; d.n_del = n_del; d.max_del = max_del;
+  d.skey = s->skey; d.skey2 = s->skey2; d.sval = s->sval; d.order = s->nA > 1 ? s->order : nullptr;
+  d.fl = s->fl; d.kpre = s->kpre; d.lgc = s->lgc; d.frins = s->frins;
+  d.frlist = s->frlist; d.nfr = s->nfr; d.frcum = s->frcum; d.fridx = s->fridx;
+  const uint32_t par = s->epoch & 1u;
+  d.segb = s->segb + par * s->acap; d.sege = s->sege + par * s->acap;
+  d.segb_next = s->segb + (par ^ 1u) * s->acap; d.sege_next = s->sege + (par ^ 1u) * s->acap;
+  d.frb = s->frb; d.fre = s->fre; d.ibase = s->ibase; d.n_full = s->n_full;
   d.n_used = s->n_used;
   d.h_used = s->h_used;
   d.ovf = ovf;
-  d.rdec = s->rdec; d.rst = s->rst; d.rpre = s->rpre; d.ramb = s->ramb; d.amb = s->amb; d.namb = s->namb;
+  d.rdec = s->rdec; d.rpre = s->rpre; d.amb = s->amb; d.namb = s->namb;
   d.acum = s->acum; d.ab = s->ab; d.ae = s->ae;
+  d.ticket = s->ticket; d.lb = s->lb;
+  const uint32_t ntl = (uint32_t)((max_del + TS - 1) / TS);
+  d.ntl = s->ntl;
   const uint32_t g = (uint32_t)((max_del + TT - 1) / TT < 8192 ? (max_del + TT - 1) / TT : 8192);
-  hipLaunchKernelGGL(tc_gather, dim3(g), dim3(TT), 0, st, d, recs, n_records, max_records, del, n_del, max_del);
   if (d.order) {
+    hipLaunchKernelGGL(tc_gather, dim3(g), dim3(TT), 0, st, d);
     uint32_t bits = 1;
     while ((1u << bits) <= s->nA) ++bits;  // keys 0..nA (nA: no topic, sorts last)
     size_t tb = s->tmp_bytes;
     if (rtps_sort_pairs(s->tmp, tb, s->skey, s->skey2, s->sval, s->order, (uint32_t)max_del, (int)bits, st) !=
         hipSuccess)
       return RTPS_RX_EHIP;
+    hipLaunchKernelGGL(tc_mark, dim3(g), dim3(TT), 0, st, d);
+  } else {
+    hipLaunchKernelGGL(tc_gm, dim3(g), dim3(TT), 0, st, d);
   }
-  hipLaunchKernelGGL(tc_mark, dim3(g), dim3(TT), 0, st, d, max_del);
-  hipLaunchKernelGGL(tc_class, dim3(g), dim3(TT), 0, st, d, max_del);
-  size_t tb = s->tmp_bytes;
-  if (hipcub::DeviceScan::ExclusiveSum(s->tmp, tb, s->kins, s->kpre, (int64_t)max_del, st) != hipSuccess)
-    return RTPS_RX_EHIP;
-  tb = s->tmp_bytes;
-  if (hipcub::DeviceScan::InclusiveScan(s->tmp, tb, s->gcpos, s->lgc, hipcub::Max(), (int64_t)max_del, st) !=
-      hipSuccess)
-    return RTPS_RX_EHIP;
-  tb = s->tmp_bytes;
-  if (hipcub::DeviceSelect::Flagged(s->tmp, tb, hipcub::CountingInputIterator<uint32_t>(0), s->fr, s->frlist, s->nfr,
-                                    (int64_t)max_del, st) != hipSuccess)
-    return RTPS_RX_EHIP;
+  hipLaunchKernelGGL(tc_cscan, dim3(ntl), dim3(TT), 0, st, d);
   // repeats: the sure ones decided in parallel, the undecided ones per topic in order
-  hipLaunchKernelGGL(tc_rdec, dim3(g), dim3(TT), 0, st, d);
-  tb = s->tmp_bytes;
-  if (hipcub::DeviceScan::ExclusiveSum(s->tmp, tb, s->rst, s->rpre, (int64_t)max_del + 1, st) != hipSuccess)
-    return RTPS_RX_EHIP;
-  tb = s->tmp_bytes;
-  if (hipcub::DeviceSelect::Flagged(s->tmp, tb, hipcub::CountingInputIterator<uint32_t>(0), s->ramb, s->amb, s->namb,
-                                    (int64_t)max_del, st) != hipSuccess)
-    return RTPS_RX_EHIP;
+  hipLaunchKernelGGL(tc_rscan, dim3(ntl), dim3(TT), 0, st, d);
   if (s->nA) hipLaunchKernelGGL(tc_resolve, dim3((s->nA + TT - 1) / TT), dim3(TT), 0, st, d);
   hipLaunchKernelGGL(tc_rfill, dim3(g), dim3(TT), 0, st, d);
-  hipLaunchKernelGGL(tc_final, dim3(g), dim3(TT), 0, st, d, del, max_del);
+  hipLaunchKernelGGL(tc_final, dim3(g), dim3(TT), 0, st, d);
   s->used_inflight += max_del;
   s->last_del = max_del;
   if (hipEventRecord(s->used_ev, st) != hipSuccess) return RTPS_RX_EHIP;

@@ -1,0 +1,43 @@
+#!/bin/bash
+# Round-6 iteration steps on the box: gpu_r6_iter.sh STEP [STEP ...], each under its own limit,
+# stopping at the first failure.  Logs under gpurun_out/r6/.
+#   topic      topic-cache + ingest GPU tests
+#   wab        W2 variant A/B (scripts/gpu_variant_ab.sh, C3)
+#   ing        T and C3 bench lines with the ingest + topic-cache legs (no CPU baseline / C1 / e2e)
+#   spdp       C3 bench line's SPDP repeats leg only numbers (part of ing)
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; R=$(pwd); O=$R/gpurun_out/r6; mkdir -p $O; export TMPDIR=/tmp
+PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
+for step in "$@"; do
+  echo "== $step $(date +%T)"
+  case $step in
+    topic)
+      timeout -k 10 900 $PYT tests/test_topic_gpu.py tests/test_ingest_gpu.py tests/test_shard_gpu.py -m gpu > $O/topic.log 2>&1 \
+        || { grep -E "FAILED|Error|error" $O/topic.log | head -20; tail -30 $O/topic.log; exit 3; }
+      tail -2 $O/topic.log ;;
+    wab)
+      WLS=C3 timeout -k 10 900 bash scripts/gpu_variant_ab.sh > $O/wab.log 2>&1 || { tail -20 $O/wab.log; exit 4; }
+      cat $O/wab.log ;;
+    ing)
+      for wl in T C3; do
+        timeout -k 10 300 python bench.py --workload $wl --steps 20 --warmup 5 --no-c1 --no-e2e --no-cpu-baseline --no-cdr > $O/ing_$wl.json 2> $O/ing_$wl.err || { tail -20 $O/ing_$wl.err; exit 5; }
+        python3 - $O/ing_$wl.json $wl <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); g = d["ingest"]
+print(sys.argv[2], "step %.1f us" % (d["ms_per_step"] * 1e3), "ingest %.1f us" % (g["ms"] * 1e3),
+      "tc_extra %.1f us" % (g["topic_cache_extra_ms"] * 1e3), "stored", g.get("topic_cache_stored"))
+s = d.get("topic_cache_spdp_repeats")
+if s:
+    for k in ("pairs", "halves"):
+        v = s[k]; print("  spdp", k, "parity", v["parity_ok"], "ingest %.1f us" % (v["ingest_ms"] * 1e3), "tc_extra %.1f us" % (v["topic_cache_extra_ms"] * 1e3))
+PY
+      done ;;
+    kt_T|kt_C3|kt_C4)  # rocprofv3 kernel stats of one bench line (no CPU baseline / C1 / e2e)
+      wl=${step#kt_}
+      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt_$wl -o run --output-format csv \
+        -- python3 $R/bench.py --workload $wl --steps 20 --warmup 5 --no-cpu-baseline --no-e2e --no-c1 ${KT_ARGS} > $O/kt_$wl.json 2> $O/kt_$wl.err) \
+        || { tail -5 $O/kt_$wl.err; exit 6; }
+      f=$(find $O/kt_$wl -name "*kernel_stats.csv" | head -1); cp "$f" $O/kt_${wl}_kernel_stats.csv; rm -rf $O/kt_$wl
+      python3 scripts/prof_table.py $O/kt_${wl}_kernel_stats.csv | head -45 ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
