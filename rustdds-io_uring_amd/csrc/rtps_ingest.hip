@@ -3000,8 +3000,9 @@ static void far_finish(const State& S, int64_t* ack_out, hipStream_t st) {
 static int ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const uint8_t* arena, uint64_t arena_len,
                       const uint64_t* dgram_off, const rtps_record* records, const uint64_t* n_records,
                       uint64_t max_records, const rtps_frag_sample* frag, const uint64_t* n_frag, uint64_t max_frag,
-                      uint32_t flags, const rtps_ingest_out* out) {
+                      uint32_t flags, const rtps_ingest_out* out, const IngestTail* tail, bool& tail_queued) {
   (void)arena_len;
+  tail_queued = false;
   if (t.n_proxies > ECAP_MAX) return RTPS_RX_ETOOBIG;
   if (max_records > 0x7fffffffull) return RTPS_RX_ETOOBIG;
   if (!grow_state(s, t.n_proxies ? t.n_proxies : 1, st)) return RTPS_RX_ENOMEM;
@@ -3132,6 +3133,10 @@ static int ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, cons
                        out->max_accepted, out->accepted, out->n_accepted, S.ctr, out->n_window_overflow, t.n_proxies,
                        S, false, out->ack_base, false, true);
     far_finish(S, out->ack_base, st);
+    if (tail) {  // behind the plain path, gated by its verdict (C_MODE, written by k_decide_t<3>)
+      const int rc = tail->run(tail->ctx, S.ctr + C_MODE);
+      if (rc) return rc;
+    }
   } else {
     hipLaunchKernelGGL(k_signal, dim3(1), dim3(64), 0, st, S.ctr, s->hsig, tag, cfg);
   }
@@ -3151,7 +3156,10 @@ static int ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, cons
   const uint64_t n_hb = s->hsig[SIG_HB], n_gap = s->hsig[SIG_GAP], n_ev = s->hsig[SIG_EV], n_free = s->hsig[SIG_FREE];
   const uint64_t n_rec = s->hsig[SIG_NREC], farc = s->hsig[SIG_FARC];
   s->fp_used = s->hsig[SIG_FUSED];  // (exact: every earlier batch has finished)
-  if (ident && s->hsig[SIG_MODE] != 0) return RTPS_RX_OK;  // the queued plain path runs it
+  if (ident && s->hsig[SIG_MODE] != 0) {  // the queued plain path runs it (and the gated tail)
+    tail_queued = true;
+    return RTPS_RX_OK;
+  }
   // events live at [0, nev): record slots in identity batches, the expanded list otherwise
   uint64_t nev = ident ? n_rec : n_ev;
   // far items: at most classify's candidates (every path but the fast one counts them); their far SNs
@@ -3297,7 +3305,10 @@ static int ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, cons
 int rtps_ingest_batch(IngestState* s, hipStream_t st, const ReaderDev& t, const uint8_t* arena, uint64_t arena_len,
                       const uint64_t* dgram_off, const rtps_record* records, const uint64_t* n_records,
                       uint64_t max_records, const rtps_frag_sample* frag, const uint64_t* n_frag, uint64_t max_frag,
-                      uint32_t flags, const rtps_ingest_out* out) {
-  return ingest_batch(s, st, t, arena, arena_len, dgram_off, records, n_records, max_records, frag, n_frag, max_frag,
-                      flags, out);
+                      uint32_t flags, const rtps_ingest_out* out, const IngestTail* tail) {
+  bool queued = false;
+  const int rc = ingest_batch(s, st, t, arena, arena_len, dgram_off, records, n_records, max_records, frag, n_frag,
+                              max_frag, flags, out, tail, queued);
+  if (rc || !tail || queued) return rc;
+  return tail->run(tail->ctx, nullptr);
 }

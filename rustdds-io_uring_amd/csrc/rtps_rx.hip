@@ -2354,13 +2354,29 @@ int rtps_rx_ingest(rtps_rx_ctx* c, const uint8_t* arena, uint64_t arena_len, con
     if (!c->tc_ovf && hipMalloc(&c->tc_ovf, sizeof(uint64_t)) != hipSuccess) return RTPS_RX_ENOMEM;
     o.n_window_overflow = c->tc_ovf;
   }
-  int rc = rtps_ingest_batch(c->ingest, c->stream, rd, arena, arena_len, dgram_off, records, n_records, max_records,
-                             frag, n_frag, max_frag, flags & ~RTPS_INGEST_TOPIC_CACHE, &o);
-  if (rc || !(flags & RTPS_INGEST_TOPIC_CACHE)) return rc;
-  // the topic caches' add_change over the deliveries (rtps_topic.hip)
-  rc = topics_state(c);
-  return rc ? rc : rtps_topic_apply(c->topics, c->stream, records, n_records, max_records, o.accepted,
-                                    o.n_accepted, o.max_accepted, o.n_window_overflow);
+  if (!(flags & RTPS_INGEST_TOPIC_CACHE))
+    return rtps_ingest_batch(c->ingest, c->stream, rd, arena, arena_len, dgram_off, records, n_records, max_records,
+                             frag, n_frag, max_frag, flags, &o);
+  // the topic caches' add_change over the deliveries (rtps_topic.hip), queued by the ingest
+  // behind its deliveries (gated by its verdict where it queues its plain path ahead)
+  int rc = topics_state(c);
+  if (rc) return rc;
+  struct TopicTail {
+    rtps_rx_ctx* c;
+    const rtps_record* records;
+    const uint64_t* n_records;
+    uint64_t max_records;
+    const rtps_ingest_out* o;
+  } tt{c, records, n_records, max_records, &o};
+  const IngestTail tail{[](void* p, const uint64_t* gate) -> int {
+                          const TopicTail& a = *static_cast<const TopicTail*>(p);
+                          return rtps_topic_apply(a.c->topics, a.c->stream, a.records, a.n_records, a.max_records,
+                                                  a.o->accepted, a.o->n_accepted, a.o->max_accepted,
+                                                  a.o->n_window_overflow, gate);
+                        },
+                        &tt};
+  return rtps_ingest_batch(c->ingest, c->stream, rd, arena, arena_len, dgram_off, records, n_records, max_records,
+                           frag, n_frag, max_frag, flags & ~RTPS_INGEST_TOPIC_CACHE, &o, &tail);
 }
 
 /* test / measurement hook (not part of the public header): the ingest's

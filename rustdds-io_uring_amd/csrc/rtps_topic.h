@@ -37,6 +37,8 @@ uint32_t rtps_topic_of_slot(const TopicState* s, uint16_t slot);
 // ovf (device u64, optional): the batch's ingest window overflows; non-zero = some samples were
 // accepted without the proxies' duplicate check, so no delivery is stored unchecked ("certain"):
 // every one is checked against the topic's live changes.
+// gate (device u64, optional): the batch's kernels do nothing unless *gate != 0 when they run
+// (queued ahead of the host's knowledge of whether the ingest path they follow runs).
 int rtps_topic_apply(TopicState* s, hipStream_t st, const rtps_record* recs, const uint64_t* n_records,
                      uint64_t max_records, rtps_delivery* del, const uint64_t* n_del, uint64_t max_del,
-                     const uint64_t* ovf = nullptr);
+                     const uint64_t* ovf = nullptr, const uint64_t* gate = nullptr);

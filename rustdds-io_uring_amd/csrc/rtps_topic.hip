@@ -37,6 +37,7 @@
 // reference's sequential add_change.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <stdlib.h>
 #include <string.h>
 
 #include <new>
@@ -223,14 +224,16 @@ struct TDev {
   uint8_t* frins;     // a repeat (FL_REP) position's change stored (written for repeats only)
   uint32_t* frlist;   // repeat positions, ascending
   uint64_t* nfr;
-  uint32_t* frcum;    // inserted repeats of the topic up to frlist[j] (inclusive)
   uint64_t* fridx;    // [max] insertion index of an inserted repeat
   uint32_t *segb, *sege;  // [nA] this batch's topic segments (one of two parity buffers)
   uint32_t *segb_next, *sege_next;  // the other buffer: cleared here for the next batch
   uint32_t *frb, *fre;  // [nA]
-  uint64_t* ibase;    // [nA] I of the topic at the batch start
+  uint64_t* ibase;    // [3 * nA] the resolve's per-topic values for tc_final: I at the batch start minus
+                      // the stored positions before its segment (mod 2^64), the topic's new E, the first
+                      // position whose change stays live
   uint64_t* n_full;   // live-index inserts that found no room (0)
   const uint64_t* ovf;  // the ingest's window overflows of the batch (nullptr: none): all candidates
+  const uint64_t* gate; // (optional) the batch's kernels do nothing unless *gate != 0 (the prologue runs)
   // repeats decided in parallel (tc_rscan): per repeat j the decision, the exclusive count of the
   // sure stores before it; the undecided ones (AMB) in order, with their stores' running count
   uint8_t* rdec;      // [nfr] RD_HOLD / RD_STORE / RD_AMB
@@ -243,7 +246,7 @@ struct TDev {
   uint64_t* h_used;   // pinned: n_used as the earlier batches left it (the batch's first kernel)
   // the single-pass scans (tc_cscan over positions, tc_rscan over repeats): tile tickets and
   // decoupled look-back words, cleared by the batch's first kernel
-  uint32_t* ticket;         // [2]
+  uint32_t* ticket;         // [4]: tc_cscan's, tc_rscan's tickets, tc_rscan's finished workgroups
   unsigned long long* lb;   // [4 * ntl]: tc_cscan's count words, its GC words, tc_rscan's count words
   uint32_t ntl;
 };
@@ -254,9 +257,10 @@ __device__ __forceinline__ uint32_t pos_cid(const TDev& d, uint64_t p) {
   return d.order ? d.skey2[p] : d.slot_cid[d.del[p].reader_slot];
 }
 __device__ __forceinline__ uint64_t n_deliveries(const TDev& d) { return *d.n_del < d.max_del ? *d.n_del : d.max_del; }
+__device__ __forceinline__ bool gated_off(const TDev& d) { return d.gate && *d.gate == 0ull; }
 __device__ __forceinline__ bool ins_at(const TDev& d, uint64_t p) { return (d.fl[p] & FL_INS) != 0; }
 // delivery dl's change (writer GUID, SN, topic); rec = NONE when its record is outside the batch
-__device__ __forceinline__ KeyP key_of(const TDev& d, const rtps_delivery& dl) {
+__device__ __forceinline__ KeyP key_of(const TDev& d, const rtps_delivery& dl, uint32_t tid = NONE) {
   KeyP x{};
   x.rec = NONE;
   const uint64_t nrec = *d.n_records < d.max_records ? *d.n_records : d.max_records;
@@ -265,7 +269,7 @@ __device__ __forceinline__ KeyP key_of(const TDev& d, const rtps_delivery& dl) {
     const uint4 a = q[0], b = q[1], c = q[2];
     x.g[0] = a.z; x.g[1] = a.w; x.g[2] = b.x; x.g[3] = b.y;  // prefix @8, writer_id @20
     x.snlo = c.x; x.snhi = c.y;                              // sn @32
-    x.tid = d.slot_tid[dl.reader_slot];
+    x.tid = tid != NONE ? tid : d.slot_tid[dl.reader_slot];
     x.rec = dl.rec_idx;
   }
   return x;
@@ -279,9 +283,9 @@ __device__ __forceinline__ void batch_prologue(const TDev& d) {
   const uint32_t t0 = blockIdx.x * TT + threadIdx.x, st = gridDim.x * TT;
   for (uint32_t c = t0; c < d.nA; c += st) { d.segb_next[c] = NONE; d.sege_next[c] = 0u; }
   for (uint32_t k = t0; k < 3u * d.ntl; k += st) d.lb[k] = 0ull;
-  if (t0 < 2u) d.ticket[t0] = 0u;
+  if (t0 < 4u) d.ticket[t0] = 0u;
   if (t0 == 0) {
-    __hip_atomic_store(d.h_used, *d.n_used, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (d.h_used) __hip_atomic_store(d.h_used, *d.n_used, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     *d.nfr = 0ull;  // (tc_cscan sets it when the batch has deliveries)
     d.kpre[0] = 0u;
   }
@@ -290,50 +294,104 @@ __device__ __forceinline__ void batch_prologue(const TDev& d) {
 // One position's flags (the change x of delivery dl, prev: the delivery before it in topic order,
 // same topic): GC, certain (stored unchecked: FL_INS), the same record as the previous position,
 // or a candidate (looked up in the live index, claimed in the batch map).
-__device__ __forceinline__ uint8_t mark_one(const TDev& d, uint64_t p, const KeyP& x, bool same_rec_before) {
+struct TopicFacts {  // what the marks read of a topic (loaded once per run of positions of one topic)
+  uint32_t t;
+  bool sure;      // its single non-DUPLICATES_OK reader's proxy saw everything it holds (no overflow)
+  uint64_t E;
+};
+__device__ __forceinline__ TopicFacts facts_of(const TDev& d, uint32_t t) {
+  TopicFacts z;
+  z.t = t;
+  z.E = d.E[t];
+  // (a batch whose ingest overflowed its capacities may hold duplicates the proxies did not
+  // see: every delivery is checked then)
+  z.sure = d.simple[t] && z.E >= d.until[t] && !(d.ovf && *d.ovf != 0u);
+  return z;
+}
+__device__ __forceinline__ uint8_t mark_one(const TDev& d, uint64_t p, const KeyP& x, bool same_rec_before,
+                                            TopicFacts& tf) {
   if (x.rec == NONE) return 0;
   uint8_t f = FL_VALID;
   if ((x.snlo & 63u) == 0u) f |= FL_GC;  // (sn as usize) % 64 == 0 (:230-233)
   // the same record delivered earlier to this topic (another reader of it): the change it stored
   // (or found) is held now: max_keep >= 1 keeps the newest
   if (same_rec_before) return f | FL_REP0;
-  const uint32_t t = x.tid;
+  if (tf.t != x.tid) tf = facts_of(d, x.tid);
   const bool user_kind = ((x.g[3] >> 24) & 0xf0u) == 0u;  // EntityKind::is_user_defined (guid.rs:168-170)
-  // (a batch whose ingest overflowed its capacities may hold duplicates the proxies did not
-  // see: every delivery is checked then)
-  const bool cand = !d.simple[t] || d.E[t] < d.until[t] || !user_kind || (d.ovf && *d.ovf != 0u);
-  if (!cand) return f | FL_INS;
+  if (tf.sure && user_kind) return f | FL_INS;
   f |= FL_CAND;
   const PEnt* e = p_find(d.P, d.pmask, x);
-  if (e && e->idx >= d.E[t]) f |= FL_PLIVE;
+  if (e && e->idx >= tf.E) f |= FL_PLIVE;
   b_put(d.B, d.bmask, d.epoch, x, (uint32_t)p);
   return f;
 }
 
 // No sort (at most one topic receives): position = delivery.  The changes are read from the
 // records, the positions marked, the topic's segment bounds found (atomics on the boundary
-// positions only), in one launch.
-__global__ __launch_bounds__(TT) void tc_gm(TDev d) {
-  batch_prologue(d);
-  const uint64_t nd = n_deliveries(d);
-  for (uint64_t p = (uint64_t)blockIdx.x * TT + threadIdx.x; p < nd; p += (uint64_t)gridDim.x * TT) {
-    const rtps_delivery dl = d.del[p];
-    const uint32_t c = d.slot_cid[dl.reader_slot];
-    uint8_t f = 0;
-    if (c < d.nA) {
-      const rtps_delivery pv = p > 0 ? d.del[p - 1] : rtps_delivery{NONE, 0, 0};
-      const bool pv_same = p > 0 && d.slot_cid[pv.reader_slot] == c;
-      if (!pv_same) atomicMin(&d.segb[c], (uint32_t)p);
-      if (p + 1 == nd || d.slot_cid[d.del[p + 1].reader_slot] != c) atomicMax(&d.sege[c], (uint32_t)p + 1u);
-      f = mark_one(d, p, key_of(d, dl), pv_same && pv.rec_idx == dl.rec_idx);
+// positions only), in one launch.  GV positions per thread (their loads in flight together).
+constexpr uint32_t GV = 4;
+__device__ __forceinline__ void load_dels(const rtps_delivery* del, uint64_t p0, uint64_t nd, rtps_delivery* dv) {
+  if (p0 + GV <= nd) {  // (hipMalloc-aligned, p0 a multiple of 4: two 16-B loads)
+    const uint4 a = reinterpret_cast<const uint4*>(del + p0)[0], b = reinterpret_cast<const uint4*>(del + p0)[1];
+    const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (uint32_t i = 0; i < GV; ++i) {
+      dv[i].rec_idx = w[2 * i];
+      dv[i].reader_slot = (uint16_t)(w[2 * i + 1] & 0xffffu);
+      dv[i].flags = (uint16_t)(w[2 * i + 1] >> 16);
     }
-    d.fl[p] = f;
+  } else {
+#pragma unroll
+    for (uint32_t i = 0; i < GV; ++i) dv[i] = p0 + i < nd ? del[p0 + i] : rtps_delivery{NONE, 0, 0};
+  }
+}
+__global__ __launch_bounds__(TT) void tc_gm(TDev d) {
+  batch_prologue(d);  // (gated off too: the next batch's segment buffer is cleared here)
+  if (gated_off(d)) return;
+  const uint64_t nd = n_deliveries(d);
+  if (d.nA == 0 || nd == 0) return;
+  // every valid position is the one topic's: its facts loaded once, beside the first deliveries
+  const uint32_t t0 = d.cid_tid[0];
+  TopicFacts tf0 = facts_of(d, t0);
+  for (uint64_t p0 = ((uint64_t)blockIdx.x * TT + threadIdx.x) * GV; p0 < nd; p0 += (uint64_t)gridDim.x * TT * GV) {
+    rtps_delivery dv[GV];
+    load_dels(d.del, p0, nd, dv);
+    const rtps_delivery pv0 = p0 > 0 ? d.del[p0 - 1] : rtps_delivery{NONE, 0, 0};
+    const uint32_t cprev = p0 > 0 ? d.slot_cid[pv0.reader_slot] : NONE;
+    const uint32_t cnext = p0 + GV < nd ? d.slot_cid[d.del[p0 + GV].reader_slot] : NONE;
+    uint32_t cid[GV];
+    KeyP x[GV];
+#pragma unroll
+    for (uint32_t i = 0; i < GV; ++i) {
+      cid[i] = p0 + i < nd ? d.slot_cid[dv[i].reader_slot] : NONE;
+      x[i] = cid[i] < d.nA ? key_of(d, dv[i], t0) : KeyP{{0, 0, 0, 0}, 0, 0, 0, NONE};
+    }
+    uint32_t fw = 0;
+    TopicFacts tf = tf0;
+#pragma unroll
+    for (uint32_t i = 0; i < GV; ++i) {
+      const uint64_t p = p0 + i;
+      const uint32_t c = cid[i];
+      if (c >= d.nA) continue;
+      const uint32_t cp = i ? cid[i - 1] : cprev, cn = i + 1 < GV ? cid[i + 1] : cnext;
+      const uint32_t rp = i ? dv[i - 1].rec_idx : pv0.rec_idx;
+      if (cp != c) atomicMin(&d.segb[c], (uint32_t)p);
+      if (p + 1 == nd || cn != c) atomicMax(&d.sege[c], (uint32_t)p + 1u);
+      fw |= (uint32_t)mark_one(d, p, x[i], cp == c && rp == dv[i].rec_idx, tf) << (8 * i);
+    }
+    if (p0 + GV <= nd) *reinterpret_cast<uint32_t*>(d.fl + p0) = fw;
+    else
+      for (uint32_t i = 0; p0 + i < nd; ++i) d.fl[p0 + i] = (uint8_t)(fw >> (8 * i));
   }
 }
 
+// (RTPS_TC_PROBE measurement kernels)
+__global__ void tc_nop_big(TDev d) { if (threadIdx.x == 0 && blockIdx.x == 0 && d.gate == (const uint64_t*)1) d.fl[0] = 0; }
+__global__ void tc_nop_small(uint8_t* p) { if (threadIdx.x == 0 && blockIdx.x == 0 && p == (uint8_t*)1) *p = 0; }
 // Sort mode: deliveries -> the sort pairs (compact topic, delivery index)
 __global__ __launch_bounds__(TT) void tc_gather(TDev d) {
   batch_prologue(d);
+  if (gated_off(d)) return;
   const uint64_t nd = n_deliveries(d);
   for (uint64_t k = (uint64_t)blockIdx.x * TT + threadIdx.x; k < d.max_del; k += (uint64_t)gridDim.x * TT) {
     d.skey[k] = k < nd ? d.slot_cid[d.del[k].reader_slot] : d.nA;
@@ -342,6 +400,7 @@ __global__ __launch_bounds__(TT) void tc_gather(TDev d) {
 }
 // Sort mode: per position in topic order, the flags and the segment bounds
 __global__ __launch_bounds__(TT) void tc_mark(TDev d) {
+  if (gated_off(d)) return;
   const uint64_t nd = n_deliveries(d);
   for (uint64_t p = (uint64_t)blockIdx.x * TT + threadIdx.x; p < nd; p += (uint64_t)gridDim.x * TT) {
     const uint32_t c = d.skey2[p];
@@ -351,17 +410,21 @@ __global__ __launch_bounds__(TT) void tc_mark(TDev d) {
       if (!pv_same) d.segb[c] = (uint32_t)p;
       if (p + 1 == nd || d.skey2[p + 1] != c) d.sege[c] = (uint32_t)p + 1u;
       const rtps_delivery dl = d.del[d.order[p]];
-      f = mark_one(d, p, key_of(d, dl), pv_same && d.del[d.order[p - 1]].rec_idx == dl.rec_idx);
+      TopicFacts tf{NONE, false, 0};
+      f = mark_one(d, p, key_of(d, dl), pv_same && d.del[d.order[p - 1]].rec_idx == dl.rec_idx, tf);
     }
     d.fl[p] = f;
   }
 }
 
 // ---- single-pass scans with decoupled look-back ----
-// A workgroup takes the next tile by ticket (so every earlier tile has started), publishes its
-// aggregate, adds its predecessors' (walking back until an inclusive prefix), publishes its
-// inclusive prefix.  A word: flag (1 aggregate, 2 inclusive) << 62 | value.
-constexpr uint32_t CPT = 8, TS = TT * CPT;  // positions per thread / per tile
+// Workgroup t takes tile t (workgroups are dispatched in index order, so every earlier tile has
+// started), publishes its aggregate, adds its predecessors' (walking back until an inclusive
+// prefix), publishes its inclusive prefix.  A word: flag (1 aggregate, 2 inclusive) << 62 | value.
+#ifndef RTPS_TC_CPT
+#define RTPS_TC_CPT 8
+#endif
+constexpr uint32_t CPT = RTPS_TC_CPT, TS = TT * CPT;  // positions per thread / per tile
 constexpr unsigned long long LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_VAL = (1ull << 62) - 1ull;
 constexpr unsigned long long M31 = (1ull << 31) - 1ull;
 // The words are self-contained (no data rides on them), so relaxed agent-scope atomics suffice:
@@ -436,11 +499,9 @@ __device__ __forceinline__ void block_scan3(uint32_t& a, uint32_t& b, int32_t& m
 // scans every later pass reads: kpre (stored positions before p), lgc (last GC position <= p), the
 // repeat list (frlist, nfr).  One launch, no host count.
 __global__ __launch_bounds__(TT) void tc_cscan(TDev d) {
-  __shared__ uint32_t s_tile;
   __shared__ unsigned long long s_pre[2];
-  if (threadIdx.x == 0) s_tile = atomicAdd(&d.ticket[0], 1u);
-  __syncthreads();
-  const uint32_t tile = s_tile;
+  const uint32_t tile = blockIdx.x;
+  if (gated_off(d)) return;
   const uint64_t nd = n_deliveries(d);
   const uint64_t base = (uint64_t)tile * TS;
   if (base >= nd) return;  // (no later tile looks back at it)
@@ -475,6 +536,11 @@ __global__ __launch_bounds__(TT) void tc_cscan(TDev d) {
     rep += (f & FL_REP) ? 1u : 0u;
     if (f & FL_GC) gc = (int32_t)p;
   }
+  // a stored position's delivery is flagged now (the ingest writes every delivery's flags as 0):
+  // tc_final then visits only the repeats and the changes that stay live
+#pragma unroll
+  for (uint32_t i = 0; i < CPT; ++i)
+    if (fv[i] & FL_INS) d.del[pos_k(d, p0 + i)].flags = (uint16_t)RTPS_DELIVERY_CACHED;
   uint32_t ta, tb;
   int32_t tm;
   uint32_t ea = ins, eb = rep;
@@ -611,69 +677,6 @@ __device__ __forceinline__ uint8_t rdec_one(const TDev& d, uint32_t j) {
   }
   return dec;
 }
-// per repeat the decision, then the scans: rpre (sure stores before j), the undecided list (amb,
-// namb).  Single pass like tc_cscan; a batch without repeats costs one workgroup's ticket.
-__global__ __launch_bounds__(TT) void tc_rscan(TDev d) {
-  __shared__ uint32_t s_tile;
-  __shared__ unsigned long long s_pre;
-  if (threadIdx.x == 0) s_tile = atomicAdd(&d.ticket[1], 1u);
-  __syncthreads();
-  const uint32_t tile = s_tile;
-  const uint32_t nfr = (uint32_t)*d.nfr;
-  if (nfr == 0u) {
-    if (tile == 0 && threadIdx.x == 0) { d.rpre[0] = 0u; *d.namb = 0ull; }
-    return;
-  }
-  const uint64_t base = (uint64_t)tile * TS;
-  if (base >= nfr) return;
-  const uint64_t j0 = base + (uint64_t)threadIdx.x * CPT;
-  uint8_t dv[CPT];
-  uint32_t ns = 0, na = 0;
-#pragma unroll
-  for (uint32_t i = 0; i < CPT; ++i) {
-    const uint64_t j = j0 + i;
-    uint8_t dec = RD_HOLD;
-    if (j < nfr) {
-      dec = rdec_one(d, (uint32_t)j);
-      d.rdec[j] = dec;
-      d.frins[d.frlist[j]] = 0;  // (set below for the stored ones: tc_resolve, tc_rfill)
-    }
-    dv[i] = j < nfr ? dec : (uint8_t)0xff;
-    ns += dec == RD_STORE && j < nfr;
-    na += dec == RD_AMB && j < nfr;
-  }
-  uint32_t ta, tb;
-  int32_t tm, im = -1;
-  uint32_t es = ns, ea = na;
-  block_scan3(es, ea, im, ta, tb, tm);
-  unsigned long long* const lw = d.lb + 2u * d.ntl;
-  if (threadIdx.x < 64u) {
-    const uint32_t lane = threadIdx.x;
-    const unsigned long long agg = (unsigned long long)ta | ((unsigned long long)tb << 31);
-    if (tile == 0) {
-      if (lane == 0) { lb_put(lw, LB_INC | agg); s_pre = 0; }
-    } else {
-      if (lane == 0) lb_put(lw + tile, LB_AGG | agg);
-      const unsigned long long ex = lb_prefix<false>(lw, tile, lane);
-      if (lane == 0) { lb_put(lw + tile, LB_INC | (ex + agg)); s_pre = ex; }
-    }
-  }
-  __syncthreads();
-  uint32_t rs = (uint32_t)(s_pre & M31) + es, ra = (uint32_t)(s_pre >> 31) + ea;
-#pragma unroll
-  for (uint32_t i = 0; i < CPT; ++i) {
-    const uint64_t j = j0 + i;
-    if (j >= nfr) break;
-    d.rpre[j] = rs;
-    if (dv[i] == RD_STORE) ++rs;
-    if (dv[i] == RD_AMB) d.amb[ra++] = (uint32_t)j;
-  }
-  if (j0 < nfr && nfr <= j0 + CPT) {  // the thread holding the last repeat: the totals
-    d.rpre[nfr] = rs;
-    *d.namb = ra;
-  }
-}
-
 // stored repeats of the topic before position q (q within the topic's segment; j: the first
 // repeat at or past q is searched in [jb, jcur)): the sure ones plus the undecided ones stored
 __device__ __forceinline__ uint32_t rep_before(const TDev& d, uint32_t q, uint32_t jb, uint32_t jcur, uint32_t ab,
@@ -684,14 +687,12 @@ __device__ __forceinline__ uint32_t rep_before(const TDev& d, uint32_t q, uint32
 }
 
 // one thread per topic of the batch: its undecided repeats in order, then the new I / E
-__global__ __launch_bounds__(TT) void tc_resolve(TDev d) {
-  const uint32_t c = blockIdx.x * TT + threadIdx.x;
-  if (c >= d.nA) return;
+__device__ void resolve_topic(const TDev& d, uint32_t c) {
   const uint32_t t = d.cid_tid[c];
   const uint64_t I0 = d.I[t];
-  d.ibase[c] = I0;
   const uint32_t b = d.segb[c], e = d.sege[c];
   if (b == NONE) { d.frb[c] = d.fre[c] = 0; d.ab[c] = d.ae[c] = 0; return; }
+  d.ibase[c] = I0 - d.kpre[b];
   const uint64_t K = d.K[t], E0 = d.E[t];
   const uint32_t nfr = (uint32_t)*d.nfr, na = nfr ? (uint32_t)*d.namb : 0u;
   const uint32_t jb = lower_bound(d.frlist, 0, nfr, b), je = lower_bound(d.frlist, jb, nfr, e);
@@ -739,57 +740,140 @@ __global__ __launch_bounds__(TT) void tc_resolve(TDev d) {
   const uint64_t E = E_at(d.lgc[e - 1], je, ae);
   d.I[t] = I0 + (d.kpre[e] - kb) + (nfr ? d.rpre[je] - d.rpre[jb] : 0u) + RA;
   d.E[t] = E;
+  d.ibase[d.nA + c] = E;
+  // the first position whose change (if stored) stays live: the insertion count before p,
+  // I0 + stored positions + stored repeats before p, is non-decreasing in p
+  uint32_t lo = b, hi = e;
+  while (lo < hi) {
+    const uint32_t m = (lo + hi) >> 1;
+    const uint64_t Im = I0 + (d.kpre[m] - kb) + (nfr ? rep_before(d, m, jb, je, ab, ae) : 0u);
+    if (Im >= E) hi = m; else lo = m + 1;
+  }
+  d.ibase[2u * d.nA + c] = lo;
 }
 
-// per repeat: the sure stores' insertion (index: the insertions before it, repeats included)
-// and every repeat's running count of stored repeats in its topic (frcum, for tc_final)
-__global__ __launch_bounds__(TT) void tc_rfill(TDev d) {
+// per repeat the decision, then the scans: rpre (sure stores before j), the undecided list (amb,
+// namb).  Single pass like tc_cscan; a batch without repeats costs one workgroup's ticket.
+__device__ void rscan_tile(const TDev& d, uint32_t tile, uint32_t nfr);
+// ... and the workgroup that finishes last resolves every topic (tc_resolve's pass: the topics'
+// undecided repeats in order, their new I / E), so that a batch's repeats take one launch.
+__global__ __launch_bounds__(TT) void tc_rscan(TDev d) {
+  __shared__ uint32_t s_last;
+  const uint32_t tile = blockIdx.x;
+  if (gated_off(d)) return;
   const uint32_t nfr = (uint32_t)*d.nfr;
-  for (uint32_t j = blockIdx.x * TT + threadIdx.x; j < nfr; j += gridDim.x * TT) {
-    const uint32_t p = d.frlist[j];
-    const uint32_t c = pos_cid(d, p);
-    const uint32_t jb = d.frb[c], ab = d.ab[c], ae = d.ae[c];
-    const uint32_t aq = lower_bound(d.amb, ab, ae, j + 1u);  // undecided repeats up to j
-    const uint32_t before = (d.rpre[j] - d.rpre[jb]) + (aq > ab ? d.acum[aq - 1] : 0u) -
-                            ((aq > ab && d.amb[aq - 1] == j && d.frins[p]) ? 1u : 0u);
-    if (d.rdec[j] == RD_STORE) {
-      d.frins[p] = 1;
-      d.fridx[p] = d.ibase[c] + (d.kpre[p] - d.kpre[d.segb[c]]) + before;
+  const uint32_t n_work = nfr ? (uint32_t)((nfr + TS - 1) / TS) : 1u;  // workgroups with a tile
+  if (tile >= n_work) return;
+  if (nfr == 0u) {
+    if (threadIdx.x == 0) { d.rpre[0] = 0u; *d.namb = 0ull; }
+  } else {
+    rscan_tile(d, tile, nfr);
+  }
+  __syncthreads();
+  if (n_work > 1u) {  // the last of the working workgroups to finish resolves (release / acquire)
+    if (threadIdx.x == 0)
+      s_last = __hip_atomic_fetch_add(&d.ticket[2], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) == n_work - 1u;
+    __syncthreads();
+    if (!s_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  for (uint32_t c = threadIdx.x; c < d.nA; c += TT) resolve_topic(d, c);
+}
+__device__ void rscan_tile(const TDev& d, uint32_t tile, uint32_t nfr) {
+  __shared__ unsigned long long s_pre;
+  const uint64_t base = (uint64_t)tile * TS;
+  const uint64_t j0 = base + (uint64_t)threadIdx.x * CPT;
+  uint8_t dv[CPT];
+  uint32_t ns = 0, na = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < CPT; ++i) {
+    const uint64_t j = j0 + i;
+    uint8_t dec = RD_HOLD;
+    if (j < nfr) {
+      dec = rdec_one(d, (uint32_t)j);
+      d.rdec[j] = dec;
+      d.frins[d.frlist[j]] = 0;  // (the resolve sets it for the undecided repeats it stores)
     }
-    d.frcum[j] = before + (d.frins[p] ? 1u : 0u);
+    dv[i] = j < nfr ? dec : (uint8_t)0xff;
+    ns += dec == RD_STORE && j < nfr;
+    na += dec == RD_AMB && j < nfr;
+  }
+  uint32_t ta, tb;
+  int32_t tm, im = -1;
+  uint32_t es = ns, ea = na;
+  block_scan3(es, ea, im, ta, tb, tm);
+  unsigned long long* const lw = d.lb + 2u * d.ntl;
+  if (threadIdx.x < 64u) {
+    const uint32_t lane = threadIdx.x;
+    const unsigned long long agg = (unsigned long long)ta | ((unsigned long long)tb << 31);
+    if (tile == 0) {
+      if (lane == 0) { lb_put(lw, LB_INC | agg); s_pre = 0; }
+    } else {
+      if (lane == 0) lb_put(lw + tile, LB_AGG | agg);
+      const unsigned long long ex = lb_prefix<false>(lw, tile, lane);
+      if (lane == 0) { lb_put(lw + tile, LB_INC | (ex + agg)); s_pre = ex; }
+    }
+  }
+  __syncthreads();
+  uint32_t rs = (uint32_t)(s_pre & M31) + es, ra = (uint32_t)(s_pre >> 31) + ea;
+#pragma unroll
+  for (uint32_t i = 0; i < CPT; ++i) {
+    const uint64_t j = j0 + i;
+    if (j >= nfr) break;
+    d.rpre[j] = rs;
+    if (dv[i] == RD_STORE) ++rs;
+    if (dv[i] == RD_AMB) d.amb[ra++] = (uint32_t)j;
+  }
+  if (j0 < nfr && nfr <= j0 + CPT) {  // the thread holding the last repeat: the totals
+    d.rpre[nfr] = rs;
+    *d.namb = ra;
   }
 }
 
+
 // per position: the flag on the delivery (its whole 8-B entry rewritten: full-line stores),
-// survivors into the live index
+// survivors into the live index.  A change's insertion index: the topic's count at the batch
+// start + the stored positions before it + the stored repeats before it (rep_before); an
+// undecided repeat's comes from the resolve.
+// The changes that stay live go into the live index; the stored repeats get their flag.
+// Workgroups [0, nA): topic c's positions from its first live one (the resolve's binary search)
+// to its segment's end, the stored ones inserted; workgroups [nA, grid): the repeats.
 __global__ __launch_bounds__(TT) void tc_final(TDev d) {
+  if (gated_off(d)) return;
   const uint64_t nd = n_deliveries(d);
+  if (nd == 0) return;
   const uint32_t nfr = (uint32_t)*d.nfr;
-  for (uint64_t p = (uint64_t)blockIdx.x * TT + threadIdx.x; p < nd; p += (uint64_t)gridDim.x * TT) {
-    const uint8_t f = d.fl[p];
-    if (!(f & FL_VALID)) continue;
-    const uint32_t k = pos_k(d, p);
-    rtps_delivery dl = d.del[k];
-    const uint32_t c = d.order ? d.skey2[p] : d.slot_cid[dl.reader_slot];
-    const bool rp = (f & FL_REP) != 0;
-    const bool ins = (f & FL_INS) || (rp && d.frins[p]);
-    dl.flags = (uint16_t)((dl.flags & ~RTPS_DELIVERY_CACHED) | (ins ? RTPS_DELIVERY_CACHED : 0u));
-    d.del[k] = dl;
-    if (!ins) continue;
+  if (blockIdx.x < d.nA) {
+    const uint32_t c = blockIdx.x;
+    const uint32_t b = d.segb[c], e = d.sege[c];
+    if (b == NONE) return;
+    const uint64_t base = d.ibase[c], E = d.ibase[d.nA + c];
+    const uint32_t first = (uint32_t)d.ibase[2u * d.nA + c];
+    const uint32_t jb = nfr ? d.frb[c] : 0u, je = nfr ? d.fre[c] : 0u;
+    const uint32_t ab = nfr ? d.ab[c] : 0u, ae = nfr ? d.ae[c] : 0u;
+    for (uint32_t p = first + threadIdx.x; p < e; p += TT) {
+      if (!(d.fl[p] & FL_INS)) continue;  // (stored repeats: below)
+      const uint64_t idx = base + d.kpre[p] + (je > jb ? rep_before(d, p, jb, je, ab, ae) : 0u);
+      if (idx >= E && !p_put(d.P, d.pmask, key_of(d, d.del[pos_k(d, p)]), idx, d.n_used))
+        atomicAdd(reinterpret_cast<unsigned long long*>(d.n_full), 1ull);
+    }
+    return;
+  }
+  for (uint32_t j = (blockIdx.x - d.nA) * TT + threadIdx.x; j < nfr; j += (gridDim.x - d.nA) * TT) {
+    const uint32_t p = d.frlist[j];
+    const uint8_t dec = d.rdec[j];
+    const uint32_t c = pos_cid(d, p);
     uint64_t idx;
-    if (rp) {
+    if (dec == RD_STORE) {
+      idx = d.ibase[c] + d.kpre[p] + rep_before(d, p, d.frb[c], d.fre[c], d.ab[c], d.ae[c]);
+    } else if (dec == RD_AMB && d.frins[p]) {
       idx = d.fridx[p];
     } else {
-      const uint32_t jb = d.frb[c], je = d.fre[c];
-      uint32_t r = 0;
-      if (nfr && je > jb) {
-        const uint32_t jq = lower_bound(d.frlist, jb, je, (uint32_t)p);
-        r = jq > jb ? d.frcum[jq - 1] : 0u;
-      }
-      idx = d.ibase[c] + (d.kpre[p] - d.kpre[d.segb[c]]) + r;
+      continue;  // held: not stored
     }
-    const uint32_t t = d.cid_tid[c];
-    if (idx >= d.E[t] && !p_put(d.P, d.pmask, key_of(d, dl), idx, d.n_used))
+    rtps_delivery* dl = d.del + pos_k(d, p);
+    dl->flags = (uint16_t)RTPS_DELIVERY_CACHED;
+    if (idx >= d.ibase[d.nA + c] && !p_put(d.P, d.pmask, key_of(d, *dl), idx, d.n_used))
       atomicAdd(reinterpret_cast<unsigned long long*>(d.n_full), 1ull);
   }
 }
@@ -842,11 +926,12 @@ struct TopicState {
   uint32_t *skey = nullptr, *skey2 = nullptr, *sval = nullptr, *order = nullptr, *kpre = nullptr;
   int32_t* lgc = nullptr;
   uint8_t *fl = nullptr, *frins = nullptr;
-  uint32_t* ticket = nullptr;          // the single-pass scans' tile tickets [2]
+  uint32_t* ticket = nullptr;          // the single-pass scans' tile tickets [4]
   unsigned long long* lb = nullptr;    // their look-back words [3 * ntl]
   uint32_t ntl = 0;
-  uint32_t *frlist = nullptr, *frcum = nullptr;
+  uint32_t* frlist = nullptr;
   uint64_t *fridx = nullptr, *nfr = nullptr, *n_full = nullptr;
+  uint64_t* n_full_zero = nullptr;  // a device zero word (RTPS_TC_PROBE=2)
   uint32_t *segb = nullptr, *sege = nullptr, *frb = nullptr, *fre = nullptr;  // segb / sege: [2 * acap], by batch parity
   uint64_t* ibase = nullptr;
   uint8_t *rdec = nullptr, *ramb = nullptr;                         // [n] parallel repeat decisions
@@ -867,7 +952,7 @@ static void dfree(T*& p) {
 
 static void free_scratch(TopicState* s) {
   dfree(s->skey); dfree(s->skey2); dfree(s->sval); dfree(s->order); dfree(s->kpre);
-  dfree(s->lgc); dfree(s->fl); dfree(s->frins); dfree(s->frlist); dfree(s->frcum);
+  dfree(s->lgc); dfree(s->fl); dfree(s->frins); dfree(s->frlist);
   dfree(s->fridx); dfree(s->B); dfree(s->tmp); dfree(s->lb);
   dfree(s->rdec); dfree(s->rpre); dfree(s->amb); dfree(s->acum);
   s->cap = 0; s->bcap = 0; s->tmp_bytes = 0; s->ntl = 0;
@@ -881,7 +966,8 @@ TopicState* rtps_topic_state_new(int device) {
   s->nt = NSLOT;  // no configured topics: every slot its own
   bool ok = dmalloc((void**)&s->slot_tid, NSLOT * 4) && dmalloc((void**)&s->slot_cid, NSLOT * 4) &&
             dmalloc((void**)&s->nfr, 8) && dmalloc((void**)&s->n_full, 8) && dmalloc((void**)&s->n_used, 8) &&
-            dmalloc((void**)&s->ticket, 8) &&
+            dmalloc((void**)&s->ticket, 16) && dmalloc((void**)&s->n_full_zero, 8) &&
+            hipMemset(s->n_full_zero, 0, 8) == hipSuccess &&
             dmalloc((void**)&s->namb, 8) &&
             hipMemset(s->n_full, 0, 8) == hipSuccess && hipMemset(s->n_used, 0, 8) == hipSuccess &&
             hipHostMalloc((void**)&s->h_used, 8, hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess &&
@@ -895,7 +981,7 @@ void rtps_topic_state_free(TopicState* s) {
   free_scratch(s);
   dfree(s->slot_tid); dfree(s->slot_cid); dfree(s->cid_tid); dfree(s->K); dfree(s->simple); dfree(s->I);
   dfree(s->E); dfree(s->until); dfree(s->P); dfree(s->nfr); dfree(s->n_full); dfree(s->segb); dfree(s->sege);
-  dfree(s->frb); dfree(s->fre); dfree(s->ibase); dfree(s->n_used); dfree(s->ticket);
+  dfree(s->frb); dfree(s->fre); dfree(s->ibase); dfree(s->n_used); dfree(s->ticket); dfree(s->n_full_zero);
   if (s->h_used) (void)hipHostFree(s->h_used);
   if (s->used_ev) (void)hipEventDestroy(s->used_ev);
   delete s;
@@ -950,7 +1036,7 @@ static int build(TopicState* s, const uint32_t* set_first, const rtps_target* en
     const uint32_t a = s->nA ? s->nA : 1;
     if (!dmalloc((void**)&s->cid_tid, a * 4ull) || !dmalloc((void**)&s->segb, 2 * a * 4ull) ||
         !dmalloc((void**)&s->sege, 2 * a * 4ull) || !dmalloc((void**)&s->frb, a * 4ull) || !dmalloc((void**)&s->fre, a * 4ull) ||
-        !dmalloc((void**)&s->ibase, a * 8ull) || !dmalloc((void**)&s->ab, a * 4ull) || !dmalloc((void**)&s->ae, a * 4ull))
+        !dmalloc((void**)&s->ibase, 3 * a * 8ull) || !dmalloc((void**)&s->ab, a * 4ull) || !dmalloc((void**)&s->ae, a * 4ull))
       return RTPS_RX_ENOMEM;
     s->acap = a;
   }
@@ -1096,7 +1182,7 @@ static int reserve_scratch(TopicState* s, uint64_t n, hipStream_t st) {
   bool ok = dmalloc((void**)&s->skey, n * 4) && dmalloc((void**)&s->skey2, n * 4) && dmalloc((void**)&s->sval, n * 4) &&
             dmalloc((void**)&s->order, n * 4) && dmalloc((void**)&s->kpre, (n + 1) * 4) &&
             dmalloc((void**)&s->lgc, n * 4) && dmalloc((void**)&s->fl, n + 8) && dmalloc((void**)&s->frins, n) &&
-            dmalloc((void**)&s->frlist, n * 4) && dmalloc((void**)&s->frcum, n * 4) &&
+            dmalloc((void**)&s->frlist, n * 4) &&
             dmalloc((void**)&s->fridx, n * 8) && dmalloc((void**)&s->B, bcap * sizeof(BEnt)) &&
             dmalloc((void**)&s->rdec, n) && dmalloc((void**)&s->rpre, (n + 1) * 4) &&
             dmalloc((void**)&s->amb, (n + 1) * 4) && dmalloc((void**)&s->acum, (n + 1) * 4) &&
@@ -1114,17 +1200,21 @@ static int reserve_scratch(TopicState* s, uint64_t n, hipStream_t st) {
   return RTPS_RX_OK;
 }
 
-// A batch in six launches when at most one topic receives (no sort): tc_gm (changes + marks),
-// tc_cscan (candidates + the position scans), tc_rscan (repeats' decisions + their scans),
-// tc_resolve (per topic), tc_rfill, tc_final.  Every launch reads the delivery count on the
-// device, so a batch sized by its capacity costs only its deliveries; a batch without
-// candidates leaves tc_rscan / tc_rfill one ticket / an empty loop.
+// A batch in four launches when at most one topic receives (no sort): tc_gm (changes + marks),
+// tc_cscan (candidates + the position scans), tc_rscan (repeats' decisions + their scans, then
+// the per-topic resolve), tc_final.  Every launch reads the delivery count on the device, so a
+// batch sized by its capacity costs only its deliveries.
 int rtps_topic_apply(TopicState* s, hipStream_t st, const rtps_record* recs, const uint64_t* n_records,
                      uint64_t max_records, rtps_delivery* del, const uint64_t* n_del, uint64_t max_del,
-                     const uint64_t* ovf) {
+                     const uint64_t* ovf, const uint64_t* gate) {
   if (max_del == 0) return RTPS_RX_OK;
   if (max_del > 0x7fffffffull) return RTPS_RX_ETOOBIG;
   if (!s->I) return RTPS_RX_EINVAL;  // no readers known yet
+  // measurement knob (tuning only): RTPS_TC_PROBE=1 queues nothing, =2 queues the launches with
+  // every kernel gated off (a zero word), so that the launches' own cost can be timed
+  static const int probe = [] { const char* e = getenv("RTPS_TC_PROBE"); return e ? atoi(e) : 0; }();
+  if (probe & 1) return RTPS_RX_OK;
+  if (probe & 2) gate = s->n_full_zero;
   int rc = reserve_scratch(s, max_del, st);
   if (rc) return rc;
   rc = reserve_live(s, max_del, st);
@@ -1143,20 +1233,23 @@ int rtps_topic_apply(TopicState* s, hipStream_t st, const rtps_record* recs, con
   d.recs = recs; d.n_records = n_records; d.max_records = max_records; d.del = del; d.n_del = n_del; d.max_del = max_del;
   d.skey = s->skey; d.skey2 = s->skey2; d.sval = s->sval; d.order = s->nA > 1 ? s->order : nullptr;
   d.fl = s->fl; d.kpre = s->kpre; d.lgc = s->lgc; d.frins = s->frins;
-  d.frlist = s->frlist; d.nfr = s->nfr; d.frcum = s->frcum; d.fridx = s->fridx;
+  d.frlist = s->frlist; d.nfr = s->nfr; d.fridx = s->fridx;
   const uint32_t par = s->epoch & 1u;
   d.segb = s->segb + par * s->acap; d.sege = s->sege + par * s->acap;
   d.segb_next = s->segb + (par ^ 1u) * s->acap; d.sege_next = s->sege + (par ^ 1u) * s->acap;
   d.frb = s->frb; d.fre = s->fre; d.ibase = s->ibase; d.n_full = s->n_full;
   d.n_used = s->n_used;
-  d.h_used = s->h_used;
+  d.h_used = (probe & 8) ? nullptr : s->h_used;
   d.ovf = ovf;
+  d.gate = gate;
   d.rdec = s->rdec; d.rpre = s->rpre; d.amb = s->amb; d.namb = s->namb;
   d.acum = s->acum; d.ab = s->ab; d.ae = s->ae;
   d.ticket = s->ticket; d.lb = s->lb;
   const uint32_t ntl = (uint32_t)((max_del + TS - 1) / TS);
   d.ntl = s->ntl;
   const uint32_t g = (uint32_t)((max_del + TT - 1) / TT < 8192 ? (max_del + TT - 1) / TT : 8192);
+  if (probe & 32) { hipLaunchKernelGGL(tc_nop_big, dim3(1024), dim3(TT), 0, st, d); return RTPS_RX_OK; }
+  if (probe & 64) { hipLaunchKernelGGL(tc_nop_small, dim3(1024), dim3(TT), 0, st, s->fl); return RTPS_RX_OK; }
   if (d.order) {
     hipLaunchKernelGGL(tc_gather, dim3(g), dim3(TT), 0, st, d);
     uint32_t bits = 1;
@@ -1167,17 +1260,22 @@ int rtps_topic_apply(TopicState* s, hipStream_t st, const rtps_record* recs, con
       return RTPS_RX_EHIP;
     hipLaunchKernelGGL(tc_mark, dim3(g), dim3(TT), 0, st, d);
   } else {
-    hipLaunchKernelGGL(tc_gm, dim3(g), dim3(TT), 0, st, d);
+    const uint64_t gq = (max_del + TT * GV - 1) / (TT * GV);
+    hipLaunchKernelGGL(tc_gm, dim3((uint32_t)(gq < 8192 ? gq : 8192)), dim3(TT), 0, st, d);
   }
+  if (probe & 16) return RTPS_RX_OK;
   hipLaunchKernelGGL(tc_cscan, dim3(ntl), dim3(TT), 0, st, d);
   // repeats: the sure ones decided in parallel, the undecided ones per topic in order
   hipLaunchKernelGGL(tc_rscan, dim3(ntl), dim3(TT), 0, st, d);
-  if (s->nA) hipLaunchKernelGGL(tc_resolve, dim3((s->nA + TT - 1) / TT), dim3(TT), 0, st, d);
-  hipLaunchKernelGGL(tc_rfill, dim3(g), dim3(TT), 0, st, d);
-  hipLaunchKernelGGL(tc_final, dim3(g), dim3(TT), 0, st, d);
+  {  // a workgroup per topic (its live tail), then the repeats' workgroups
+    const uint64_t gr = (max_del + TT - 1) / TT;
+    hipLaunchKernelGGL(tc_final, dim3(s->nA + (uint32_t)(gr < 1024 ? gr : 1024)), dim3(TT), 0, st, d);
+  }
   s->used_inflight += max_del;
   s->last_del = max_del;
-  if (hipEventRecord(s->used_ev, st) != hipSuccess) return RTPS_RX_EHIP;
-  s->used_pending = true;
+  if (!(probe & 4)) {
+    if (hipEventRecord(s->used_ev, st) != hipSuccess) return RTPS_RX_EHIP;
+    s->used_pending = true;
+  }
   return hipGetLastError() == hipSuccess ? RTPS_RX_OK : RTPS_RX_EHIP;
 }

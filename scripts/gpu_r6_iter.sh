@@ -38,6 +38,18 @@ PY
         || { tail -5 $O/kt_$wl.err; exit 6; }
       f=$(find $O/kt_$wl -name "*kernel_stats.csv" | head -1); cp "$f" $O/kt_${wl}_kernel_stats.csv; rm -rf $O/kt_$wl
       python3 scripts/prof_table.py $O/kt_${wl}_kernel_stats.csv | head -45 ;;
+    tl_T|tl_C3)  # rocprofv3 kernel trace (per dispatch) of one bench line, for gap analysis
+      wl=${step#tl_}
+      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d $O/tl_$wl -o run --output-format csv \
+        -- python3 $R/bench.py --workload $wl --steps 6 --warmup 2 --no-cpu-baseline --no-e2e --no-c1 --no-cdr --no-frag > $O/tl_$wl.json 2> $O/tl_$wl.err) \
+        || { tail -5 $O/tl_$wl.err; exit 7; }
+      f=$(find $O/tl_$wl -name "*kernel_trace.csv" | head -1); cp "$f" $O/tl_${wl}_kernel_trace.csv; rm -rf $O/tl_$wl
+      wc -l $O/tl_${wl}_kernel_trace.csv ;;
+    probe)  # T ingest legs with the topic step queued normally / not at all / gated off (RTPS_TC_PROBE)
+      for pr in ${PROBES:-0 1 2}; do
+        RTPS_TC_PROBE=$pr timeout -k 10 300 python bench.py --workload T --steps 20 --warmup 5 --no-c1 --no-e2e --no-cpu-baseline --no-cdr > $O/probe_$pr.json 2> $O/probe_$pr.err || { tail -20 $O/probe_$pr.err; exit 8; }
+        python3 -c "import json; d=json.loads(open('$O/probe_$pr.json').read().strip().splitlines()[-1]); g=d['ingest']; print('probe $pr ingest %.1f us tc_extra %.1f us' % (g['ms']*1e3, g['topic_cache_extra_ms']*1e3))"
+      done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
