@@ -1089,6 +1089,39 @@ struct SigOut {
   uint64_t tag;
   SigCfg cf;
 };
+// The workgroup's far samples (per thread: bit j of fpm = event b0 + j, fpd: DUPLICATES_OK) into
+// the far list: a block scan of the counts, one atomic on the list counter, then each thread
+// writes its items (their fields re-read: the event's sn and proxy, the proxy's window).
+// Every thread calls it.
+__device__ void far_push_block(const State& s, const Scratch& x, uint64_t b0, uint32_t fpm, uint32_t fpd) {
+  __shared__ uint32_t s_fw[IT / 64];
+  __shared__ unsigned long long s_fbase;
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t cnt = (uint32_t)__builtin_popcount(fpm);
+  const uint32_t incl = wave_incl_sum(cnt, lane);
+  if (lane == 63u) s_fw[wave] = incl;
+  __syncthreads();
+  uint32_t off = incl - cnt, tot = 0;
+#pragma unroll
+  for (uint32_t v = 0; v < IT / 64; ++v) {
+    off += v < wave ? s_fw[v] : 0u;
+    tot += s_fw[v];
+  }
+  if (tot == 0) return;  // (uniform)
+  if (threadIdx.x == 0) s_fbase = atomicAdd(reinterpret_cast<unsigned long long*>(s.ctr + C_NFAR), (unsigned long long)tot);
+  __syncthreads();
+  uint64_t pos = s_fbase + off;
+  while (fpm) {
+    const uint32_t j = (uint32_t)__builtin_ctz(fpm);
+    fpm &= fpm - 1u;
+    const uint64_t i = b0 + j;
+    const uint32_t e = x.ent[i];
+    const int64_t v = x.esn[i], lim = s.lo[e] + (int64_t)W;
+    if (pos < s.fl_cap)
+      s.fl[pos] = FarItem{PEv{v, 0, 0, EV_SAMPLE, (uint32_t)i}, lim, e, ((fpd >> j) & 1u) ? (uint32_t)FI_DUP : (uint32_t)FI_SAMPLE};
+    ++pos;
+  }
+}
 template <int MERGE>
 __global__ __launch_bounds__(IT) void k_decide_t(uint64_t n, uint64_t cap, Scratch x, State s, uint8_t* acc_out,
                                                  bool reliable, uint32_t epoch, uint32_t* tcnt, FarSrc fs,
@@ -1145,6 +1178,10 @@ __global__ __launch_bounds__(IT) void k_decide_t(uint64_t n, uint64_t cap, Scrat
 #pragma unroll
   for (uint32_t q = 0; q < DPT / 4; ++q) w[q] = 0u;
   uint32_t c = 0;
+  // far samples: bit j of fpm = event b0 + j goes to the far list, fpd: as a DUPLICATES_OK one;
+  // the workgroup reserves their places with ONE atomic at the end (far_push's per-wave atomic
+  // on the list counter serialises at the memory side when most samples are far: SPDP)
+  uint32_t fpm = 0, fpd = 0;
   // the thread's DPT events in groups of HG, decide_one's rule in phases so that each phase's
   // loads are in flight together: the event fields (vector loads), the proxies' state, the
   // window words (HG = 4: 8 would hold 130 VGPRs, 3 waves per SIMD)
@@ -1215,14 +1252,13 @@ __global__ __launch_bounds__(IT) void k_decide_t(uint64_t n, uint64_t cap, Scrat
         if (meta[jj] & EVF_DUP_OK) {  // the participant reader's duplicates (reader.rs:712-722)
           a = 1;
           merge = in_win;
-          if (v >= lo[jj] + (int64_t)W)
-            far_push(s, FarItem{PEv{v, 0, 0, EV_SAMPLE, (uint32_t)i}, lo[jj] + (int64_t)W, e, FI_DUP});
+          if (v >= lo[jj] + (int64_t)W) { fpm |= 1u << j; fpd |= 1u << j; }
         } else {
           const int64_t thr = hb_thr(i, v, base[jj], reliable ? s.seg_b[e] : 0u, reliable ? s.seg_e[e] : 0u, x,
                                      reliable);
           if (v >= 1 && v >= thr) {
             if (v >= lo[jj] + (int64_t)W) {  // beyond the window: accepted until the far replay decides
-              far_push(s, FarItem{PEv{v, 0, 0, EV_SAMPLE, (uint32_t)i}, lo[jj] + (int64_t)W, e, FI_SAMPLE});
+              fpm |= 1u << j;
               a = 1;
             } else {
               const bool known = (bw[jj] >> (off & 31u)) & 1u;
@@ -1250,6 +1286,7 @@ __global__ __launch_bounds__(IT) void k_decide_t(uint64_t n, uint64_t cap, Scrat
   }
   const uint64_t t = block_sum64(c, s_w);
   if (threadIdx.x == 0) tcnt[blk] = (uint32_t)t;
+  far_push_block(s, x, b0, fpm, fpd);
 }
 
 __global__ __launch_bounds__(IT) void k_dcount(const uint8_t* flag, uint64_t n, uint32_t* tcnt) {
@@ -1561,9 +1598,20 @@ __device__ __forceinline__ void wave_atomic(uint32_t key, T v, bool active, T id
 //   k_far_ins   every SN of every item inserted with its key;
 //   k_far_dec   the samples decided (rejected: acc 0; tcnt: its delivery tile's count).
 constexpr uint32_t KF = 256;
+// The proxy of a workgroup's first item (its "hot" proxy: one proxy's backlog fills the list,
+// SPDP) is reduced in LDS and added to global memory once per workgroup; the rest per wave.
+__device__ __forceinline__ uint32_t far_hot(const State& s, uint64_t nf) {
+  __shared__ uint32_t s_hk;
+  if (threadIdx.x == 0) s_hk = (uint64_t)blockIdx.x * KF < nf ? s.fl[(uint64_t)blockIdx.x * KF].e : NONE;
+  __syncthreads();
+  return s_hk;
+}
 __global__ __launch_bounds__(KF) void k_far_need(State s, const uint8_t* arena) {
+  __shared__ unsigned long long s_need;
   const uint64_t nf0 = s.ctr[C_NFAR], nf = nf0 < s.fl_cap ? nf0 : s.fl_cap;
   const uint64_t span = (uint64_t)gridDim.x * KF;
+  if (threadIdx.x == 0) s_need = 0;
+  const uint32_t hk = far_hot(s, nf);
   for (uint64_t b = (uint64_t)blockIdx.x * KF; b < nf; b += span) {  // (whole waves: wave_atomic)
     const uint64_t k = b + threadIdx.x;
     FarItem it{};
@@ -1571,9 +1619,12 @@ __global__ __launch_bounds__(KF) void k_far_need(State s, const uint8_t* arena) 
     const uint64_t c = k < nf ? far_count(it.p, it.kind, it.lim, arena) : 0;
     wave_atomic<uint64_t>(it.e, c, k < nf, 0ull, [](uint64_t a, uint64_t o) { return a + o; },
                           [&](uint32_t e, uint64_t a) {
-                            atomicAdd(reinterpret_cast<unsigned long long*>(s.fneed + e), (unsigned long long)a);
+                            if (e == hk) atomicAdd(&s_need, (unsigned long long)a);
+                            else atomicAdd(reinterpret_cast<unsigned long long*>(s.fneed + e), (unsigned long long)a);
                           });
   }
+  __syncthreads();
+  if (threadIdx.x == 0 && s_need) atomicAdd(reinterpret_cast<unsigned long long*>(s.fneed + hk), s_need);
 }
 constexpr uint32_t KG = 1024;  // k_far_grow: a new table's slots initialised and the old one rehashed by 16 waves
 __global__ __launch_bounds__(KG) void k_far_grow(State s, uint32_t n_proxies) {
@@ -1595,8 +1646,12 @@ __global__ __launch_bounds__(KG) void k_far_grow(State s, uint32_t n_proxies) {
   }
 }
 __global__ __launch_bounds__(KF) void k_far_ins(State s, const uint8_t* arena) {
+  __shared__ uint32_t s_n;
+  __shared__ unsigned long long s_min;
   const uint64_t nf0 = s.ctr[C_NFAR], nf = nf0 < s.fl_cap ? nf0 : s.fl_cap;
   const uint64_t span = (uint64_t)gridDim.x * KF;
+  if (threadIdx.x == 0) { s_n = 0; s_min = ~0ull; }
+  const uint32_t hk = far_hot(s, nf);
   for (uint64_t b = (uint64_t)blockIdx.x * KF; b < nf; b += span) {
     const uint64_t k = b + threadIdx.x;
     FarItem it{};
@@ -1617,12 +1672,21 @@ __global__ __launch_bounds__(KF) void k_far_ins(State s, const uint8_t* arena) {
       });
     }
     wave_atomic<uint32_t>(it.e, claimed, act && claimed, 0u, [](uint32_t a, uint32_t o) { return a + o; },
-                          [&](uint32_t e, uint32_t a) { atomicAdd(s.far_n + e, a); });
+                          [&](uint32_t e, uint32_t a) {
+                            if (e == hk) atomicAdd(&s_n, a);
+                            else atomicAdd(s.far_n + e, a);
+                          });
     wave_atomic<uint64_t>(it.e, (uint64_t)mn, act && mn != INT64_MAX, ~0ull,
                           [](uint64_t a, uint64_t o) { return a < o ? a : o; },
                           [&](uint32_t e, uint64_t a) {
-                            atomicMin(reinterpret_cast<unsigned long long*>(s.far_min + e), (unsigned long long)a);
+                            if (e == hk) atomicMin(&s_min, (unsigned long long)a);
+                            else atomicMin(reinterpret_cast<unsigned long long*>(s.far_min + e), (unsigned long long)a);
                           });
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && hk != NONE) {
+    if (s_n) atomicAdd(s.far_n + hk, s_n);
+    if (s_min != ~0ull) atomicMin(reinterpret_cast<unsigned long long*>(s.far_min + hk), s_min);
   }
 }
 __global__ __launch_bounds__(KF) void k_far_dec(State s, uint8_t* acc, uint32_t* tcnt) {

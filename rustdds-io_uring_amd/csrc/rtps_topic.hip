@@ -40,6 +40,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <chrono>
 #include <new>
 #include <vector>
 
@@ -1210,9 +1211,18 @@ int rtps_topic_apply(TopicState* s, hipStream_t st, const rtps_record* recs, con
   if (max_del == 0) return RTPS_RX_OK;
   if (max_del > 0x7fffffffull) return RTPS_RX_ETOOBIG;
   if (!s->I) return RTPS_RX_EINVAL;  // no readers known yet
-  // measurement knob (tuning only): RTPS_TC_PROBE=1 queues nothing, =2 queues the launches with
-  // every kernel gated off (a zero word), so that the launches' own cost can be timed
+  // measurement knob (tuning only; scripts/gpu_r6_iter.sh probe), bits: 1 queue nothing, 2 every
+  // kernel gated off (a zero word), 4 no event record, 8 no pinned n_used store, 16 the first
+  // kernel only, 32 / 64 an empty 1024-workgroup kernel with the TDev / an 8-B argument instead,
+  // 128 a 20-us host spin instead, 256 / 512 one / three empty one-wave kernels instead.
+  // Measured on T: the first kernel queued behind the ingest costs ~15 us of
+  // device time whatever it is (one empty wave: +17 us, three: +23 us, a 20-us host delay: 0).
   static const int probe = [] { const char* e = getenv("RTPS_TC_PROBE"); return e ? atoi(e) : 0; }();
+  if (probe & 128) {  // host time only: a 20-us spin, nothing queued
+    const auto t0 = std::chrono::steady_clock::now();
+    while (std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(20)) {}
+    return RTPS_RX_OK;
+  }
   if (probe & 1) return RTPS_RX_OK;
   if (probe & 2) gate = s->n_full_zero;
   int rc = reserve_scratch(s, max_del, st);
@@ -1250,6 +1260,13 @@ int rtps_topic_apply(TopicState* s, hipStream_t st, const rtps_record* recs, con
   const uint32_t g = (uint32_t)((max_del + TT - 1) / TT < 8192 ? (max_del + TT - 1) / TT : 8192);
   if (probe & 32) { hipLaunchKernelGGL(tc_nop_big, dim3(1024), dim3(TT), 0, st, d); return RTPS_RX_OK; }
   if (probe & 64) { hipLaunchKernelGGL(tc_nop_small, dim3(1024), dim3(TT), 0, st, s->fl); return RTPS_RX_OK; }
+  if (probe & 256) { hipLaunchKernelGGL(tc_nop_small, dim3(1), dim3(64), 0, st, s->fl); return RTPS_RX_OK; }
+  if (probe & 512) {
+    hipLaunchKernelGGL(tc_nop_small, dim3(1), dim3(64), 0, st, s->fl);
+    hipLaunchKernelGGL(tc_nop_small, dim3(1), dim3(64), 0, st, s->fl);
+    hipLaunchKernelGGL(tc_nop_small, dim3(1), dim3(64), 0, st, s->fl);
+    return RTPS_RX_OK;
+  }
   if (d.order) {
     hipLaunchKernelGGL(tc_gather, dim3(g), dim3(TT), 0, st, d);
     uint32_t bits = 1;
