@@ -722,10 +722,10 @@ XGMI_LINK_GBS = 153.0  # one xGMI link, one direction (8-GPU node: one link per 
 def exchange_prediction(rx, arena, off_t, outs, dev, worlds=(2, 4, 8)):
     """What the owner-side exchange of THIS batch would move at N ranks (weak scaling: every
     rank parses a batch like this one): the library's pack with n_ranks = N, its per-destination
-    counts (32-B items + blob bytes), the bytes each rank sends to its peers per step and the
+    counts (16-B items + blob bytes), the bytes each rank sends to its peers per step and the
     xGMI time they take at the link rate (every peer on its own link, all in parallel: the
     largest per-peer volume bounds the round)."""
-    from rtps_rx.shard import OwnerShard
+    from rtps_rx.shard import OwnerShard, ITEM_BYTES_OWNER
     out = {}
     for w in worlds:
         sh = OwnerShard(rx, w, None, dev, 1, 0)
@@ -736,14 +736,14 @@ def exchange_prediction(rx, arena, off_t, outs, dev, worlds=(2, 4, 8)):
             sh.close()
         n, b = c["n"].astype(np.int64), c["bytes"].astype(np.int64)
         # rank 0's view: destination 0 stays local; the others cross a link each
-        peer = 32 * n[1:] + b[1:] + 32
+        peer = ITEM_BYTES_OWNER * n[1:] + b[1:] + 32  # items, blobs, the 32-B counts
         out[str(w)] = {"items_per_dest": [int(v) for v in n], "blob_bytes_per_dest": [int(v) for v in b],
                        "bytes_sent_per_rank_per_step": int(peer.sum()),
                        "max_bytes_per_peer": int(peer.max()),
                        "predicted_xgmi_ms": float(peer.max()) / (XGMI_LINK_GBS * 1e9) * 1e3}
     return {"what": "owner-side exchange volume of this batch at N ranks (rank 0's sends; library pack with "
                     "n_ranks = N on this GPU), predicted round time at one xGMI link per peer",
-            "link_gbs": XGMI_LINK_GBS, "item_bytes": 32, **out}
+            "link_gbs": XGMI_LINK_GBS, "item_bytes": ITEM_BYTES_OWNER, **out}
 
 
 def time_ingest_ceiling(outs, n_rec, n_sets, stream, steps):
@@ -1239,7 +1239,7 @@ def measure(args, world, rank, dist, dev, allreduce_sum, allreduce_max):
         # writer's owner with its GAP bitmap / DATA_FRAG payload bytes.  Slots sized from a
         # first pack of this batch (largest (source, owner) pair over all ranks); anything
         # that does not fit would cross in the exact spill round, never be dropped.
-        from rtps_rx.shard import OwnerShard
+        from rtps_rx.shard import OwnerShard, ITEM_BYTES_OWNER
         probe_sh = OwnerShard(rx, world, dist, dev, 1, 0)
         rx.parse_batch_device(arena, off_t, ln_t, n, outs)
         probe_sh.pack(arena, off_t, outs)
@@ -1417,12 +1417,13 @@ def measure(args, world, rank, dist, dev, allreduce_sum, allreduce_max):
         result["config"]["exchange"] = {
             "mode": "owner-side exchange: fixed slots (equal-split RCCL group, pipelined with the next parse) "
                     "+ exact spill round when a slot overflows",
-            "item": "32-B rtps_shard_item per writer submessage that passes (a DATA: GUID, SN, kind, flags, "
-                    "route, payload kind; any other kind: its 64-B record + GAP bitmap / DATA_FRAG payload bytes "
-                    "in the blob), owner = writer-GUID hash % world; unpacked on the owner as one batch",
+            "item": "16-B rtps_shard_item per writer submessage that passes (a DATA of a listed writer: its "
+                    "writer-list index, SN, kind, flags, route, payload kind; another DATA adds its GUID and SN "
+                    "(32-B blob); any other kind: its 64-B record + GAP bitmap / DATA_FRAG payload bytes in the "
+                    "blob), owner = the shard's owner table; unpacked on the owner as one batch",
             "slot_items": slot[0], "slot_blob_bytes": slot[1],
-            "bytes_sent_per_rank_per_step": (world - 1) * (slot[0] * 32 + slot[1] + 32),
-            "predicted_xgmi_ms": (slot[0] * 32 + slot[1] + 32) / (XGMI_LINK_GBS * 1e9) * 1e3,
+            "bytes_sent_per_rank_per_step": (world - 1) * (slot[0] * ITEM_BYTES_OWNER + slot[1] + 32),
+            "predicted_xgmi_ms": (slot[0] * ITEM_BYTES_OWNER + slot[1] + 32) / (XGMI_LINK_GBS * 1e9) * 1e3,
             "spilled_records_rank0": int((rcv["n"] - rcv["cut"]).sum()), "overflow": False}
     elif world > 1:
         got, split = exch[(args.warmup + args.steps - 1) & 1].gather_received()

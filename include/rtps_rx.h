@@ -369,13 +369,16 @@ int rtps_rx_exchange(rtps_rx_ctx* ctx, void* comm, void* hip_stream, const void*
  *     DATA_FRAG, HEARTBEAT, HEARTBEAT_FRAG, GAP), owner = the writer's owner in the
  *     shard's owner table (rtps_rx_shard_set_owners below; default: the context's
  *     writers dealt evenly), else fmix32(fnv1a32(prefix || writer_id)) % n_ranks.
- *     What crosses is a 32-byte rtps_shard_item per record and a "blob": a DATA is
- *     its item alone
- *     (writer GUID, SN, kind, flags, route, payload kind: what the owner's ingest
- *     reads; its payload stays on the source GPU, zero-copy, and `origin` names the
- *     record there); any other kind sends its whole 64-byte record in the blob,
- *     followed by the arena bytes the owner's consumers read (a GAP's bitmap words,
- *     a DATA_FRAG's payload), 16-byte aligned;
+ *     What crosses is a 16-byte rtps_shard_item per record and a "blob".  A DATA
+ *     of a writer in the shard's writer list (the owner table's writer GUIDs in
+ *     ascending byte order; every rank builds the same table) whose SN's high word
+ *     is 0..255 is its item alone ("compact": the writer's list index, the SN,
+ *     kind, flags, route, payload kind: what the owner's ingest reads; its payload
+ *     stays on the source GPU, zero-copy, and `origin` names the record there); any
+ *     other DATA sends its writer GUID and SN in a 32-byte blob; any other kind
+ *     sends its whole 64-byte record in the blob, followed by the arena bytes the
+ *     owner's consumers read (a GAP's bitmap words, a DATA_FRAG's payload), 16-byte
+ *     aligned;
  *   - order: rank r parses the r-th contiguous chunk of the stream, so the
  *     records an owner receives, concatenated in source-rank order, are its
  *     writers' records in stream order;
@@ -389,14 +392,17 @@ int rtps_rx_exchange(rtps_rx_ctx* ctx, void* comm, void* hip_stream, const void*
  * for rtps_rx_frag_assemble / rtps_rx_ingest on the same context.
  * New: the reference has one process and no exchange. */
 typedef struct rtps_shard rtps_shard;
-typedef struct rtps_shard_item {  /* one exchanged writer record (32 bytes) */
-  uint32_t w[4];       /* DATA: the writer GUID (prefix || writer_id, as in the record); else w[0] = the
-                          item's blob bytes (64 + its consumers' bytes, rounded to 16), w[1..3] = 0 */
-  int64_t sn;          /* DATA: writer SN; else 0 */
-  uint8_t kind, flags, route, payload_kind;
+typedef struct rtps_shard_item {  /* one exchanged writer record (16 bytes) */
+  uint32_t w0;         /* compact DATA: 1 | the writer's list index << 4 (< 2^20) | the SN's high word << 24;
+                          else the item's blob bytes (a multiple of 16: the low nibble tells them apart):
+                          32 for a DATA (its writer GUID, SN, 8 zero bytes), else 64 + its consumers'
+                          bytes rounded to 16 (its record, dgram_idx = src_rec, then those bytes) */
   uint32_t src_rec;    /* the record's index in the source rank's parse output */
+  uint32_t sn_lo;      /* compact DATA: the SN's low word; else 0 */
+  uint8_t kind, flags, route, payload_kind;
 } rtps_shard_item;
-RTPS_RX_STATIC_ASSERT(sizeof(rtps_shard_item) == 32, "rtps_shard_item must be 32 bytes");
+RTPS_RX_STATIC_ASSERT(sizeof(rtps_shard_item) == 16, "rtps_shard_item must be 16 bytes");
+#define RTPS_SHARD_COMPACT 0x1u  /* rtps_shard_item.w0 & 0xf: a compact DATA */
 typedef struct rtps_shard_counts {  /* one (source, destination) pair */
   uint64_t n;          /* items */
   uint64_t bytes;      /* blob bytes (multiple of 16) */

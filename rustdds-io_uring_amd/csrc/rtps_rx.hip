@@ -2147,7 +2147,9 @@ static int cdr_prog(const rtps_cdr_op* prog, uint32_t n_ops, uint32_t row_bytes,
 // programs, the lane-per-row one for composite programs (SEQ_BEGIN / ARRAY_BEGIN).
 static int cdr_run(rtps_rx_ctx* c, const rtps_cdr_op* prog, uint32_t n_ops, uint32_t row_bytes, const CdrArgs& a) {
   (void)hipSetDevice(c->device);
-  if (rtps_cdr_is_composite(prog, n_ops)) {
+  // tuning knob: RTPS_CDR_NESTED=1 runs flat programs through the lane-per-row kernel too
+  static const bool force_nested = [] { const char* e = getenv("RTPS_CDR_NESTED"); return e && e[0] == '1'; }();
+  if (rtps_cdr_is_composite(prog, n_ops) || force_nested) {
     CdrNest N;
     if (!rtps_cdr_build_nested(prog, n_ops, row_bytes, N)) return RTPS_RX_EINVAL;
     return rtps_cdr_launch_nested(c->stream, N, a, c->resident_blocks) == 0 ? RTPS_RX_OK : RTPS_RX_EHIP;

@@ -10,10 +10,12 @@
 #include "../../include/rtps_rx.h"
 
 constexpr uint32_t SHARD_MAX_RANKS = 64;
-// what crosses xGMI per writer record: rtps_shard_item (include/rtps_rx.h); a DATA is the item
-// alone, any other kind the item + its 64-B record + the bytes its consumers read, in the blob
+// what crosses xGMI per writer record: rtps_shard_item (include/rtps_rx.h); a compact DATA is the
+// item alone, any other kind the item + a blob (a DATA's GUID and SN; else its 64-B record + the
+// bytes its consumers read)
 typedef rtps_shard_item shard_item;
-static_assert(sizeof(shard_item) == 32, "32-B exchange items");
+static_assert(sizeof(shard_item) == 16, "16-B exchange items");
+constexpr uint32_t SHARD_WLIST_MAX = 1u << 20;  // writers a compact item can name
 
 struct rtps_shard {
   rtps_rx_ctx* ctx = nullptr;
@@ -71,8 +73,10 @@ struct rtps_shard {
   std::vector<uint32_t> t_owner;
   bool t_ent = false;              // the table has entity keys (RTPS_OWNER_TOPIC)
   uint32_t* d_okeys = nullptr;     // device: [ocap * 4] GUID words, open addressing by rt_hash16
-  uint32_t* d_oval = nullptr;      // [ocap] owner, 0xffffffff = empty slot
+  uint32_t* d_oval = nullptr;      // [ocap] owner | (writer-list index + 1) << 8 (0: an entity key), ~0 = empty
   uint32_t ocap = 0;               // 0: no table (every writer by the GUID hash)
+  uint32_t* d_wlist = nullptr;     // [n_wlist * 4] the table's writer GUIDs, ascending bytes (compact items)
+  uint32_t n_wlist = 0, wlist_cap = 0;
 };
 
 // grow-only device buffer (contents are not kept); false on allocation failure

@@ -8,10 +8,11 @@
 // submessage of that writer is seen, in order.  With the stream split over N
 // GPUs by datagram, that place is the writer's owner GPU.
 //
-// What crosses per writer record is a 32-B item (rtps_shard_item): a DATA's item holds
-// everything the owner's ingest reads of it (writer GUID, SN, kind, flags, route,
-// payload kind), so a DATA costs 32 B instead of its 64-B record; any other kind
-// sends its 64-B record in its blob, ahead of the bytes its consumers read.
+// What crosses per writer record is a 16-B item (rtps_shard_item): a DATA of a writer in the
+// owner table's writer list holds everything the owner's ingest reads of it (the writer's list
+// index, SN, kind, flags, route, payload kind: "compact"), so it costs 16 B instead of its 64-B
+// record; another DATA adds a 32-B blob (GUID, SN); any other kind sends its 64-B record in its
+// blob, ahead of the bytes its consumers read.
 // Pack (source rank), three launches over the parse output:
 //   1. shard_hist    per 256-record tile and destination: items and blob bytes;
 //   2. shard_scan    per destination, exclusive scans of both over the tiles
@@ -78,9 +79,10 @@ __device__ __forceinline__ Blob blob_of(const uint32_t* w) {  // w: the record's
   return Blob{0u, 0u};
 }
 __device__ __forceinline__ uint32_t round16(uint32_t x) { return (x + 15u) & ~15u; }
-// blob bytes of an item: none for a DATA, else its record + its consumers' bytes
-__device__ __forceinline__ uint32_t item_bytes(uint32_t kind, const Blob& b) {
-  return kind == RTPS_DATA ? 0u : 64u + round16(b.len);
+// blob bytes of an item: none for a compact DATA, 32 for another DATA (GUID, SN), else its record +
+// its consumers' bytes
+__device__ __forceinline__ uint32_t item_bytes(uint32_t kind, bool compact, const Blob& b) {
+  return kind == RTPS_DATA ? (compact ? 0u : 32u) : 64u + round16(b.len);
 }
 
 // The writer -> owner table (rtps_rx_shard_set_owners): a writer in it goes to its owner,
@@ -90,7 +92,7 @@ __device__ __forceinline__ uint32_t item_bytes(uint32_t kind, const Blob& b) {
 // rt_classify's entity sets) goes to the owner of that entity set's group.
 struct OwnerDev {
   const uint32_t* keys;  // nullptr: no table
-  const uint32_t* val;
+  const uint32_t* val;   // owner | (writer-list index + 1) << 8
   uint32_t mask;
   uint32_t ent;          // the table has entity keys
 };
@@ -106,26 +108,38 @@ __device__ __forceinline__ uint32_t owner_probe(const OwnerDev& t, uint32_t a, u
   }
   return NONE;
 }
+// a writer's owner and its writer-list index (NONE: not in the list)
 __device__ __forceinline__ uint32_t owner_of_writer(const OwnerDev& t, uint32_t a, uint32_t b, uint32_t c, uint32_t d,
-                                                    uint32_t n_dest) {
+                                                    uint32_t n_dest, uint32_t& widx) {
+  widx = NONE;
   if (t.keys) {
     uint32_t v = owner_probe(t, a, b, c, d);
-    if (v == NONE && t.ent) v = owner_probe(t, EKEY_WORD, EKEY_WORD, EKEY_WORD, d);
-    if (v != NONE) return v;
+    if (v != NONE) {
+      if (v >> 8) widx = (v >> 8) - 1u;
+      return v & 0xffu;
+    }
+    if (t.ent) v = owner_probe(t, EKEY_WORD, EKEY_WORD, EKEY_WORD, d);
+    if (v != NONE) return v & 0xffu;
   }
   return owner_hash(a, b, c, d) % n_dest;
 }
 
-// Destination of a record (NONE: not an item) and its blob
-__device__ __forceinline__ uint32_t item_of(const uint32_t* w, const OwnerDev& ot, uint32_t n_dest, Blob& b) {
+// Destination of a record (NONE: not an item), its blob, and whether it crosses as a compact item
+// (a DATA of a listed writer whose SN's high word is 0..255)
+__device__ __forceinline__ uint32_t item_of(const uint32_t* w, const OwnerDev& ot, uint32_t n_dest, Blob& b,
+                                            bool& compact, uint32_t& widx) {
   const uint32_t kind = (w[1] >> 16) & 0xffu;
   const uint32_t route = (w[7] >> 16) & 0xffu;
   const bool writer = kind == RTPS_DATA || kind == RTPS_DATA_FRAG || kind == RTPS_HEARTBEAT || kind == RTPS_GAP ||
                       kind == RTPS_HEARTBEAT_FRAG;
   b = Blob{0u, 0u};
+  compact = false;
+  widx = NONE;
   if (!writer || !(route & RTPS_ROUTE_PASS)) return NONE;
   b = blob_of(w);
-  return owner_of_writer(ot, w[2], w[3], w[4], w[5], n_dest);
+  const uint32_t o = owner_of_writer(ot, w[2], w[3], w[4], w[5], n_dest, widx);
+  compact = kind == RTPS_DATA && widx < SHARD_WLIST_MAX && w[9] <= 0xffu;  // (w[9]: the SN's high word)
+  return o;
 }
 
 __device__ __forceinline__ void load_record(const rtps_record* r, uint32_t* w) {
@@ -189,10 +203,12 @@ __global__ __launch_bounds__(ST) void shard_hist(const rtps_record* recs, const 
     uint32_t w[16];
     load_record(recs + i, w);
     Blob b;
-    const uint32_t o = item_of(w, ot, n_dest, b);
+    bool compact;
+    uint32_t widx;
+    const uint32_t o = item_of(w, ot, n_dest, b, compact, widx);
     if (o != NONE) {
       atomicAdd(&h[2 * o], 1u);
-      const uint32_t ib = item_bytes((w[1] >> 16) & 0xffu, b);
+      const uint32_t ib = item_bytes((w[1] >> 16) & 0xffu, compact, b);
       if (ib) atomicAdd(&h[2 * o + 1], ib);
     }
   }
@@ -263,14 +279,15 @@ __global__ __launch_bounds__(ST) void shard_scatter(PackArgs a) {
   }
   const uint64_t i = (uint64_t)blockIdx.x * ST + tid;
   uint32_t w[16];
-  uint32_t o = NONE;
+  uint32_t o = NONE, widx = NONE;
+  bool compact = false;
   Blob b{0u, 0u};
   if (i < *a.n_rec) {
     load_record(a.recs + i, w);
-    o = item_of(w, a.ot, n, b);
+    o = item_of(w, a.ot, n, b, compact, widx);
   }
   const uint32_t kind = o != NONE ? (w[1] >> 16) & 0xffu : 0u;
-  const uint32_t size = o != NONE ? item_bytes(kind, b) : 0u;
+  const uint32_t size = o != NONE ? item_bytes(kind, compact, b) : 0u;
   uint32_t rank = 0, bex = 0;
   const uint64_t lt = lane ? (~0ull >> (64u - lane)) : 0ull;
   for (uint32_t d = 0; d < n; ++d) {
@@ -306,12 +323,15 @@ __global__ __launch_bounds__(ST) void shard_scatter(PackArgs a) {
     uint8_t* bd = slot ? a.blob + (uint64_t)o * a.bcap + boff : a.bspill + bsbase[o] + boff;
     const uint32_t tail = kind | (w[1] & 0xff000000u) >> 16 | (w[7] & 0xffff0000u);  // kind, flags, route, pk
     uint4* q = reinterpret_cast<uint4*>(it);
-    if (kind == RTPS_DATA) {
-      q[0] = make_uint4(w[2], w[3], w[4], w[5]);  // writer GUID
-      q[1] = make_uint4(w[8], w[9], tail, (uint32_t)i);
+    if (compact) {
+      *q = make_uint4(RTPS_SHARD_COMPACT | widx << 4 | w[9] << 24, (uint32_t)i, w[8], tail);
+    } else if (kind == RTPS_DATA) {  // its GUID and SN in a 32-B blob
+      *q = make_uint4(size, (uint32_t)i, 0u, tail);
+      uint4* bq = reinterpret_cast<uint4*>(bd);
+      bq[0] = make_uint4(w[2], w[3], w[4], w[5]);
+      bq[1] = make_uint4(w[8], w[9], 0u, 0u);
     } else {
-      q[0] = make_uint4(size, 0u, 0u, 0u);
-      q[1] = make_uint4(0u, 0u, tail, (uint32_t)i);
+      *q = make_uint4(size, (uint32_t)i, 0u, tail);
       const uint32_t didx = w[0];
       w[0] = (uint32_t)i;  // the record's copy names its source record
       store_record(reinterpret_cast<rtps_record*>(bd), w);
@@ -412,27 +432,33 @@ __global__ __launch_bounds__(ST) void shard_fix(FixArgs a) {
   if (j >= a.n) return;
   uint32_t s = 0;
   while (s + 1 < a.n_src && a.first[s + 1] <= j) ++s;
-  const uint4* q = reinterpret_cast<const uint4*>(a.item + j);
-  const uint4 q0 = q[0], q1 = q[1];
-  a.origin[j] = ((uint64_t)s << 32) | q1.w;                 // src_rec
-  a.size[j] = (q1.z & 0xffu) == RTPS_DATA ? 0u : q0.x;  // the blob bytes (record + consumers' bytes)
+  const uint4 q = *reinterpret_cast<const uint4*>(a.item + j);
+  a.origin[j] = ((uint64_t)s << 32) | q.y;                        // src_rec
+  a.size[j] = (q.x & 0xfu) == RTPS_SHARD_COMPACT ? 0u : q.x;  // the blob bytes (none for a compact DATA)
 }
 // the owner's records: a DATA's from its item, the others' from the copy in their blob
 __global__ __launch_bounds__(ST) void shard_expand(const shard_item* item, const uint8_t* arena, const uint64_t* boff,
-                                                   rtps_record* rec, uint64_t* off, uint64_t n) {
+                                                   const uint32_t* wlist, rtps_record* rec, uint64_t* off, uint64_t n) {
   const uint64_t j = (uint64_t)blockIdx.x * ST + threadIdx.x;
   if (j >= n) return;
-  const uint4* q = reinterpret_cast<const uint4*>(item + j);
-  const uint4 q0 = q[0], q1 = q[1];
-  const uint32_t kind = q1.z & 0xffu;
+  const uint4 q = *reinterpret_cast<const uint4*>(item + j);
+  const uint32_t kind = q.w & 0xffu;
   uint32_t w[16];
   if (kind == RTPS_DATA) {
     for (int k = 0; k < 16; ++k) w[k] = 0u;
-    w[1] = (kind << 16) | ((q1.z >> 8) & 0xffu) << 24;  // sub_off 0, kind, flags
-    w[2] = q0.x; w[3] = q0.y; w[4] = q0.z; w[5] = q0.w;  // writer GUID
-    w[7] = q1.z & 0xffff0000u;                           // route, payload_kind
-    w[8] = q1.x; w[9] = q1.y;                            // sn
-    off[j] = RTPS_SHARD_LEAD;                            // (no bytes in the owner arena)
+    w[1] = (kind << 16) | ((q.w >> 8) & 0xffu) << 24;  // sub_off 0, kind, flags
+    w[7] = q.w & 0xffff0000u;                          // route, payload_kind
+    if ((q.x & 0xfu) == RTPS_SHARD_COMPACT) {          // the writer from the list
+      const uint4 g = *reinterpret_cast<const uint4*>(wlist + 4u * ((q.x >> 4) & (SHARD_WLIST_MAX - 1u)));
+      w[2] = g.x; w[3] = g.y; w[4] = g.z; w[5] = g.w;
+      w[8] = q.z; w[9] = q.x >> 24;                    // sn
+    } else {                                           // from its blob
+      const uint4* bq = reinterpret_cast<const uint4*>(arena + RTPS_SHARD_LEAD + boff[j]);
+      const uint4 g = bq[0], sn = bq[1];
+      w[2] = g.x; w[3] = g.y; w[4] = g.z; w[5] = g.w;
+      w[8] = sn.x; w[9] = sn.y;
+    }
+    off[j] = RTPS_SHARD_LEAD;                          // (no payload bytes in the owner arena)
   } else {
     load_record(reinterpret_cast<const rtps_record*>(arena + RTPS_SHARD_LEAD + boff[j]), w);
     off[j] = RTPS_SHARD_LEAD + boff[j] + 64u - blob_of(w).rel;
@@ -503,7 +529,7 @@ int rtps_rx_shard_destroy(rtps_shard* s) {
   (void)hipDeviceSynchronize();
   void* dev[] = {s->s_slots, s->s_blob, s->s_counts, s->s_spill, s->s_bspill, s->hist, s->hscan, s->r_slots,
                  s->r_blob, s->r_counts, s->r_spill, s->r_bspill, s->o_rec, s->o_off, s->o_origin, s->o_size,
-                 s->o_boff, s->o_arena, s->o_n, s->cub_tmp, s->o_item, s->d_okeys, s->d_oval};
+                 s->o_boff, s->o_arena, s->o_n, s->cub_tmp, s->o_item, s->d_okeys, s->d_oval, s->d_wlist};
   for (void* p : dev)
     if (p) (void)hipFree(p);
   if (s->h_send) (void)hipHostFree(s->h_send);
@@ -644,6 +670,23 @@ static int owner_table_build(rtps_shard* s, bool fresh) {
     cap = 16;
     while (cap < 4ull * n) cap <<= 1;
   }
+  // the writer list (compact DATA items name their writer by its index): the table's writer GUIDs
+  // (not the entity keys) in ascending byte order, the same on every rank that builds this table
+  std::vector<uint32_t> wl;
+  for (uint32_t w = 0; w < n; ++w) {
+    const uint8_t* g = s->t_guid.data() + 16ull * w;
+    bool ekey = true;
+    for (int b = 0; b < 12; ++b) ekey = ekey && g[b] == OWNER_EKEY_PREFIX;
+    if (!ekey) wl.push_back(w);
+  }
+  std::sort(wl.begin(), wl.end(), [&](uint32_t x, uint32_t y) {
+    return memcmp(s->t_guid.data() + 16ull * x, s->t_guid.data() + 16ull * y, 16) < 0;
+  });
+  std::vector<uint32_t> widx(n, NONE), wlist(4ull * wl.size());
+  for (size_t r = 0; r < wl.size(); ++r) {
+    widx[wl[r]] = (uint32_t)r;
+    memcpy(&wlist[4 * r], s->t_guid.data() + 16ull * wl[r], 16);
+  }
   std::vector<uint32_t> keys(4ull * cap, 0u), val(cap, NONE);
   for (uint32_t w = 0; w < n; ++w) {
     uint32_t k[4];
@@ -651,7 +694,8 @@ static int owner_table_build(rtps_shard* s, bool fresh) {
     uint32_t i = rt_hash16(k[0], k[1], k[2], k[3]) & (cap - 1);
     while (val[i] != NONE) i = (i + 1) & (cap - 1);
     memcpy(&keys[4ull * i], k, 16);
-    val[i] = s->t_owner[w];
+    // owner | (list index + 1) << 8; writers past the compact items' reach keep 0 (never compact)
+    val[i] = s->t_owner[w] | (widx[w] < SHARD_WLIST_MAX ? (widx[w] + 1u) << 8 : 0u);
   }
   hipStream_t st = rtps_ctx_stream(s->ctx);
   if (hipStreamSynchronize(st) != hipSuccess) return RTPS_RX_EHIP;  // an earlier pack may read the old table
@@ -668,6 +712,16 @@ static int owner_table_build(rtps_shard* s, bool fresh) {
   if (cap && (hipMemcpy(s->d_okeys, keys.data(), 16ull * cap, hipMemcpyHostToDevice) != hipSuccess ||
               hipMemcpy(s->d_oval, val.data(), 4ull * cap, hipMemcpyHostToDevice) != hipSuccess))
     return RTPS_RX_EHIP;
+  const uint32_t nw = (uint32_t)wl.size();
+  if (nw > s->wlist_cap) {
+    (void)hipFree(s->d_wlist);
+    s->d_wlist = nullptr;
+    s->wlist_cap = 0;
+    if (hipMalloc(&s->d_wlist, 16ull * nw) != hipSuccess) return RTPS_RX_ENOMEM;
+    s->wlist_cap = nw;
+  }
+  s->n_wlist = nw;
+  if (nw && hipMemcpy(s->d_wlist, wlist.data(), 16ull * nw, hipMemcpyHostToDevice) != hipSuccess) return RTPS_RX_EHIP;
   return RTPS_RX_OK;
 }
 
@@ -866,8 +920,8 @@ int rtps_rx_shard_unpack(rtps_shard* s, rtps_owner_batch* out) {
     }
     if (hipcub::DeviceScan::ExclusiveSum(s->cub_tmp, tb, s->o_size, s->o_boff, (int64_t)total, st) != hipSuccess)
       return RTPS_RX_EHIP;
-    hipLaunchKernelGGL(shard_expand, dim3(g), dim3(ST), 0, st, s->o_item, s->o_arena, s->o_boff, s->o_rec, s->o_off,
-                       total);
+    hipLaunchKernelGGL(shard_expand, dim3(g), dim3(ST), 0, st, s->o_item, s->o_arena, s->o_boff, s->d_wlist, s->o_rec,
+                       s->o_off, total);
   }
   hipLaunchKernelGGL(shard_set_n, dim3(1), dim3(1), 0, st, s->o_n, total);
   if (hipGetLastError() != hipSuccess) return RTPS_RX_EHIP;

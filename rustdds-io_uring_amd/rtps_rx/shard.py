@@ -100,7 +100,7 @@ def rccl_comm(rx, dist, device):
         _COMMS[key] = comm
     return _COMMS[key]
 ITEM_BYTES = {"records": 64, "descriptors": 16}
-ITEM_BYTES_OWNER = 32  # rtps_shard_item: what the owner-side exchange moves per writer record
+ITEM_BYTES_OWNER = 16  # rtps_shard_item: what the owner-side exchange moves per writer record
 
 
 def owner_hash_words(words):

@@ -50,6 +50,24 @@ PY
         RTPS_TC_PROBE=$pr timeout -k 10 300 python bench.py --workload T --steps 20 --warmup 5 --no-c1 --no-e2e --no-cpu-baseline --no-cdr > $O/probe_$pr.json 2> $O/probe_$pr.err || { tail -20 $O/probe_$pr.err; exit 8; }
         python3 -c "import json; d=json.loads(open('$O/probe_$pr.json').read().strip().splitlines()[-1]); g=d['ingest']; print('probe $pr ingest %.1f us tc_extra %.1f us' % (g['ms']*1e3, g['topic_cache_extra_ms']*1e3))"
       done ;;
+    cdr)  # C3 CDR decode legs (list / per record), flat kernel vs RTPS_CDR_NESTED=1 (+ CDR_ENV)
+      for nest in 0 1; do
+        RTPS_CDR_NESTED=$nest timeout -k 10 300 python bench.py --workload C3 --steps 20 --warmup 5 --no-c1 --no-e2e --no-cpu-baseline --no-frag > $O/cdr_$nest.json 2> $O/cdr_$nest.err || { tail -20 $O/cdr_$nest.err; exit 9; }
+        python3 -c "import json; d=json.loads(open('$O/cdr_$nest.json').read().strip().splitlines()[-1]); c=d['cdr_decode']; print('nested $nest list %.1f us (%d rows, ok %d) per-record %.1f us' % (c['kernel_ms']*1e3, c['rows'], c['rows_ok'], c['per_record_layout']['kernel_ms']*1e3))"
+      done ;;
+    cdr_var)  # C3 CDR legs for the product library and each variant (twice, interleaved)
+      for round in 1 2; do
+      for lib in $R/rustdds-io_uring_amd/librtps_rx.so $R/rustdds-io_uring_amd/variants/librtps_rx_*.so; do
+        v=$(basename $lib .so)
+        RTPS_RX_LIB=$lib timeout -k 10 300 python bench.py --workload C3 --steps 20 --warmup 5 --no-c1 --no-e2e --no-cpu-baseline --no-frag > $O/cdrv_$v.json 2> $O/cdrv_$v.err || { tail -20 $O/cdrv_$v.err; exit 9; }
+        python3 -c "import json; d=json.loads(open('$O/cdrv_$v.json').read().strip().splitlines()[-1]); c=d['cdr_decode']; print('$v list %.1f us per-record %.1f us' % (c['kernel_ms']*1e3, c['per_record_layout']['kernel_ms']*1e3))"
+      done; done ;;
+    shard)  # owner-side exchange GPU tests
+      timeout -k 10 900 $PYT tests/test_shard_gpu.py -m gpu > $O/shard.log 2>&1 || { grep -E "FAILED|Error|error" $O/shard.log | head -20; tail -30 $O/shard.log; exit 10; }
+      tail -2 $O/shard.log ;;
+    xpred)  # C3 line's exchange prediction (N = 2/4/8) and step
+      timeout -k 10 300 python bench.py --workload C3 --steps 20 --warmup 5 --no-c1 --no-e2e --no-cpu-baseline --no-cdr > $O/xpred.json 2> $O/xpred.err || { tail -20 $O/xpred.err; exit 11; }
+      python3 -c "import json; d=json.loads(open('$O/xpred.json').read().strip().splitlines()[-1]); x=d['exchange_prediction']; print('C3 step %.1f us' % (d['ms_per_step']*1e3), {k: (round(v['predicted_xgmi_ms'], 3), v['max_bytes_per_peer']) for k, v in x.items() if isinstance(v, dict)})" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

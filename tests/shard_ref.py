@@ -158,22 +158,41 @@ def shard_items(recs, world, table=None):
     return np.where(writer, o, -1)
 
 
-ITEM_DTYPE = np.dtype([("w", "<u4", (4,)), ("sn", "<i8"), ("kind", "u1"), ("flags", "u1"), ("route", "u1"),
-                       ("payload_kind", "u1"), ("src_rec", "<u4")])
-assert ITEM_DTYPE.itemsize == 32
+ITEM_DTYPE = np.dtype([("w0", "<u4"), ("src_rec", "<u4"), ("sn_lo", "<u4"), ("kind", "u1"), ("flags", "u1"),
+                       ("route", "u1"), ("payload_kind", "u1")])
+assert ITEM_DTYPE.itemsize == 16
+COMPACT = 0x1  # w0 & 0xf of a compact DATA (RTPS_SHARD_COMPACT)
+WLIST_MAX = 1 << 20
 
 
-def _item_and_blob(arena, offs, r, i):
-    """(rtps_shard_item, blob bytes) of record r (index i of the source's parse output): a DATA is
-    its item alone; any other kind sends its record (dgram_idx := i) and its consumers' bytes."""
+def writer_list(table):
+    """The shard's writer list: the owner table's writer GUIDs (not its entity keys), ascending bytes."""
+    return sorted(k for k in (table or {}) if not k.startswith(EKEY))
+
+
+def _item_and_blob(arena, offs, r, i, windex):
+    """(rtps_shard_item, blob bytes) of record r (index i of the source's parse output): a DATA of a
+    listed writer (windex: GUID -> list index) whose SN's high word is 0..255 is its item alone
+    (compact); another DATA sends its GUID and SN (32 B); any other kind its record (dgram_idx := i)
+    and its consumers' bytes."""
     from rtps_rx.records import DATA
     it = np.zeros(1, dtype=ITEM_DTYPE)[0]
     it["kind"], it["flags"], it["route"], it["payload_kind"] = r["kind"], r["flags"], r["route"], r["payload_kind"]
     it["src_rec"] = i
     if int(r["kind"]) == DATA:
-        it["w"] = np.frombuffer(bytes(r["prefix"]) + bytes(r["writer_id"]), dtype="<u4")
-        it["sn"] = r["sn"]
-        return it, np.zeros(0, np.uint8)
+        g = bytes(r["prefix"]) + bytes(r["writer_id"])
+        sn = int(r["sn"])
+        hi, lo = (sn >> 32) & 0xFFFFFFFF, sn & 0xFFFFFFFF
+        k = windex.get(g)
+        if k is not None and k < WLIST_MAX and hi <= 0xFF:
+            it["w0"] = COMPACT | (k << 4) | (hi << 24)
+            it["sn_lo"] = lo
+            return it, np.zeros(0, np.uint8)
+        b = np.zeros(32, dtype=np.uint8)
+        b[:16] = np.frombuffer(g, np.uint8)
+        b[16:24] = np.frombuffer(np.int64(sn).tobytes(), np.uint8)
+        it["w0"] = 32
+        return it, b
     rel, ln = _blob(r)
     rc = r.copy()
     rc["dgram_idx"] = i
@@ -181,17 +200,18 @@ def _item_and_blob(arena, offs, r, i):
     b[:64] = np.frombuffer(rc.tobytes(), dtype=np.uint8)
     src = int(offs[int(r["dgram_idx"])]) + rel
     b[64:64 + ln] = arena[src:src + ln]
-    it["w"][0] = len(b)
+    it["w0"] = len(b)
     return it, b
 
 
 def shard_pack_np(arena, offs, recs, world, cap, bcap, table=None):
     """Per destination d: dict(counts, slot_items, slot_blob (bcap bytes), spill_items, spill_blob)."""
     o = shard_items(recs, world, table)
+    windex = {g: k for k, g in enumerate(writer_list(table))}
     out = []
     for d in range(world):
         idx = np.nonzero(o == d)[0]
-        pairs = [_item_and_blob(arena, offs, recs[i], int(i)) for i in idx]
+        pairs = [_item_and_blob(arena, offs, recs[i], int(i), windex) for i in idx]
         items = np.array([p[0] for p in pairs], dtype=ITEM_DTYPE) if pairs else np.zeros(0, ITEM_DTYPE)
         blobs = [p[1] for p in pairs]
         sizes = np.array([len(b) for b in blobs], dtype=np.int64)
@@ -208,10 +228,12 @@ def shard_pack_np(arena, offs, recs, world, cap, bcap, table=None):
     return out
 
 
-def shard_unpack_np(received):
-    """received: per source s (rank order) the dict shard_pack_np made for this owner.
+def shard_unpack_np(received, table=None):
+    """received: per source s (rank order) the dict shard_pack_np made for this owner (table: the
+    owner table the packs used, whose writer list compact items name).
     -> (records with dgram_idx = i, dgram_off u64, arena u8, origin (rank u32, source record u32))."""
     from rtps_rx.records import RECORD_DTYPE, DATA
+    wl = writer_list(table)
     rank, src = [], []
     items = [np.concatenate([x["slot_items"], x["spill_items"]]) for x in received]
     for s, it in enumerate(items):
@@ -224,19 +246,25 @@ def shard_unpack_np(received):
     off = np.zeros(len(out), dtype=np.uint64)
     pos = LEAD
     for i, it in enumerate(allit):
+        w0 = int(it["w0"])
         if int(it["kind"]) == DATA:
-            g = it["w"].astype("<u4").tobytes()
             out[i]["kind"], out[i]["flags"] = it["kind"], it["flags"]
+            out[i]["route"], out[i]["payload_kind"] = it["route"], it["payload_kind"]
+            if w0 & 0xF == COMPACT:
+                g = wl[(w0 >> 4) & (WLIST_MAX - 1)]
+                out[i]["sn"] = ((w0 >> 24) << 32) | int(it["sn_lo"])
+            else:
+                g = blobs[pos:pos + 16].tobytes()
+                out[i]["sn"] = np.frombuffer(blobs[pos + 16:pos + 24].tobytes(), "<i8")[0]
+                pos += w0
             out[i]["prefix"] = np.frombuffer(g[:12], np.uint8)
             out[i]["writer_id"] = np.frombuffer(g[12:], np.uint8)
-            out[i]["route"], out[i]["payload_kind"] = it["route"], it["payload_kind"]
-            out[i]["sn"] = it["sn"]
             off[i] = LEAD
         else:
             out[i] = np.frombuffer(blobs[pos:pos + 64].tobytes(), dtype=RECORD_DTYPE)[0]
             rel, _ = _blob(out[i])
             off[i] = pos + 64 - rel
-            pos += int(it["w"][0])
+            pos += w0
         out[i]["dgram_idx"] = i
     assert pos == len(blobs)
     return out, off, blobs, (np.concatenate(rank) if rank else np.zeros(0, np.uint32),

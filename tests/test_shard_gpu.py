@@ -75,11 +75,11 @@ def test_pack_matches_model(rx, wl, world, small):
         exp = shard_pack_np(arena, off, recs, world, cap, bcap)
         b = sh.buffers()
         counts = dev_to_numpy(b.send_counts, 32 * world, COUNTS_DTYPE)
-        slots = dev_to_numpy(b.send_slots, 32 * world * cap, ITEM_DTYPE)
+        slots = dev_to_numpy(b.send_slots, ITEM_DTYPE.itemsize * world * cap, ITEM_DTYPE)
         blob = dev_to_numpy(b.send_blob, world * bcap)
         tot_n = int(counts["n"].sum())
         tot_b = int(counts["bytes"].sum())
-        spill = dev_to_numpy(b.send_spill, 32 * tot_n, ITEM_DTYPE)
+        spill = dev_to_numpy(b.send_spill, ITEM_DTYPE.itemsize * tot_n, ITEM_DTYPE)
         bspill = dev_to_numpy(b.send_blob_spill, tot_b)
         sb = sbb = 0
         spilled = 0
@@ -259,10 +259,10 @@ def test_unpack_matches_model(rx, wl, small):
         dev_copy(b.recv_counts, rc.ctypes.data, rc.nbytes)
         rs = rbs = 0
         for s, x in enumerate(received):
-            dev_copy(b.recv_slots + s * cap * 32, x["slot_items"].ctypes.data, x["slot_items"].nbytes)
+            dev_copy(b.recv_slots + s * cap * ITEM_DTYPE.itemsize, x["slot_items"].ctypes.data, x["slot_items"].nbytes)
             dev_copy(b.recv_blob + s * bcap, x["slot_blob"].ctypes.data, x["slot_blob"].nbytes)
             sr = np.ascontiguousarray(x["spill_items"])
-            dev_copy((b.recv_spill or 0) + rs * 32, sr.ctypes.data, sr.nbytes)
+            dev_copy((b.recv_spill or 0) + rs * ITEM_DTYPE.itemsize, sr.ctypes.data, sr.nbytes)
             dev_copy((b.recv_blob_spill or 0) + rbs, x["spill_blob"].ctypes.data, x["spill_blob"].nbytes)
             rs += len(sr)
             rbs += len(x["spill_blob"])

@@ -106,9 +106,10 @@ def _worker(rank, world, port, wl, n, stride, cap, bcap, tbl, q, topics=None, ta
         # round 1: the exact spill, from the counts alone
         plan = spill_plan(sc, rc)
         sr = sspill.view(np.uint8)
-        sends = [sr[p["send_rec"][0] * 32:(p["send_rec"][0] + p["send_rec"][1]) * 32] for p in plan]
-        rspill = np.zeros(sum(p["recv_rec"][1] for p in plan) * 32, np.uint8)
-        _a2a(np.concatenate(sends), rspill, [len(x) for x in sends], [p["recv_rec"][1] * 32 for p in plan])
+        ib = ITEM_DTYPE.itemsize
+        sends = [sr[p["send_rec"][0] * ib:(p["send_rec"][0] + p["send_rec"][1]) * ib] for p in plan]
+        rspill = np.zeros(sum(p["recv_rec"][1] for p in plan) * ib, np.uint8)
+        _a2a(np.concatenate(sends), rspill, [len(x) for x in sends], [p["recv_rec"][1] * ib for p in plan])
         sends = [sbspill[p["send_bytes"][0]:p["send_bytes"][0] + p["send_bytes"][1]] for p in plan]
         rbspill = np.zeros(sum(p["recv_bytes"][1] for p in plan), np.uint8)
         _a2a(np.concatenate(sends), rbspill, [len(x) for x in sends], [p["recv_bytes"][1] for p in plan])
@@ -122,7 +123,7 @@ def _worker(rank, world, port, wl, n, stride, cap, bcap, tbl, q, topics=None, ta
                              "spill_items": rspill[rs:rs + nn - cut], "spill_blob": rbspill[rbs:rbs + nb - cb]})
             rs += nn - cut
             rbs += nb - cb
-        orecs, ooff, oarena, (orank, osrc) = shard_unpack_np(received)
+        orecs, ooff, oarena, (orank, osrc) = shard_unpack_np(received, table)
         fa = oracle.FragAssembler()
         samples = fa.batch_readers(oarena, ooff, orecs, tbl)[0]
         ing = oracle.HistoryIngest(tbl)
