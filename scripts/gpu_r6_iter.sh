@@ -56,12 +56,13 @@ PY
         python3 -c "import json; d=json.loads(open('$O/cdr_$nest.json').read().strip().splitlines()[-1]); c=d['cdr_decode']; print('nested $nest list %.1f us (%d rows, ok %d) per-record %.1f us' % (c['kernel_ms']*1e3, c['rows'], c['rows_ok'], c['per_record_layout']['kernel_ms']*1e3))"
       done ;;
     cdr_var)  # C3 CDR legs for the product library and each variant (twice, interleaved)
+      for wl in ${WLS:-C3}; do
       for round in 1 2; do
       for lib in $R/rustdds-io_uring_amd/librtps_rx.so $R/rustdds-io_uring_amd/variants/librtps_rx_*.so; do
         v=$(basename $lib .so)
-        RTPS_RX_LIB=$lib timeout -k 10 300 python bench.py --workload C3 --steps 20 --warmup 5 --no-c1 --no-e2e --no-cpu-baseline --no-frag > $O/cdrv_$v.json 2> $O/cdrv_$v.err || { tail -20 $O/cdrv_$v.err; exit 9; }
-        python3 -c "import json; d=json.loads(open('$O/cdrv_$v.json').read().strip().splitlines()[-1]); c=d['cdr_decode']; print('$v list %.1f us per-record %.1f us' % (c['kernel_ms']*1e3, c['per_record_layout']['kernel_ms']*1e3))"
-      done; done ;;
+        RTPS_RX_LIB=$lib timeout -k 10 300 python bench.py --workload $wl --steps 20 --warmup 5 --no-c1 --no-e2e --no-cpu-baseline --no-frag > $O/cdrv_$v.json 2> $O/cdrv_$v.err || { tail -20 $O/cdrv_$v.err; exit 9; }
+        python3 -c "import json; d=json.loads(open('$O/cdrv_$v.json').read().strip().splitlines()[-1]); c=d['cdr_decode']; p=c.get('per_record_layout') or {}; print('$wl $v list %.1f us per-record %.1f us' % (c['kernel_ms']*1e3, (p.get('kernel_ms') or 0)*1e3))"
+      done; done; done ;;
     shard)  # owner-side exchange GPU tests
       timeout -k 10 900 $PYT tests/test_shard_gpu.py -m gpu > $O/shard.log 2>&1 || { grep -E "FAILED|Error|error" $O/shard.log | head -20; tail -30 $O/shard.log; exit 10; }
       tail -2 $O/shard.log ;;
