@@ -18,6 +18,7 @@
 // the value bytes a decoded row consumes + row_bytes + 1 status byte written.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "../../include/rtps_rx.h"
@@ -49,6 +50,15 @@ __device__ __forceinline__ void store_prim(uint8_t* d, uint64_t x, uint32_t size
     default: *(u64u*)d = x; break;
   }
 }
+
+// 16-byte loads / stores at any byte alignment (gfx950 runs them as single
+// unaligned dwordx4 accesses)
+__device__ __forceinline__ uint4 ld16u(const uint8_t* p) {
+  uint4 v;
+  __builtin_memcpy(&v, p, 16);
+  return v;
+}
+__device__ __forceinline__ void st16u(uint8_t* p, uint4 v) { __builtin_memcpy(p, &v, 16); }
 
 // std::str::from_utf8 acceptance over m bytes.  A multi-byte character is
 // checked with selects (its lead's class and the allowed range of its first
@@ -82,8 +92,15 @@ __device__ bool utf8_ok(const uint8_t* s, uint32_t m) {
 // record each op's data start (pos) and run-time length (string chars /
 // sequence elements) in the wave's LDS table.  Reads only lengths, bools and
 // string bytes.
-__device__ uint8_t cdr_validate(const CdrProg& P, const uint8_t* v, uint32_t len, bool le, uint32_t* posT,
-                                uint32_t* lenT, uint32_t lane) {
+// the bytes [b, b + 4) of a word that lie below m, as a mask
+__device__ __forceinline__ uint32_t byte_mask(uint32_t m, uint32_t b) {
+  const uint32_t n = m > b ? m - b : 0u;
+  return n >= 4u ? 0xffffffffu : (1u << (8u * n)) - 1u;
+}
+
+// avail: the arena bytes readable from v (at least len)
+__device__ uint8_t cdr_validate(const CdrProg& P, const uint8_t* v, uint32_t len, uint64_t avail, bool le,
+                                uint32_t* posT, uint32_t* lenT, uint32_t lane) {
   uint32_t pos = 0;
   for (uint32_t k = 0; k < P.n_ops; ++k) {
     const rtps_cdr_op op = P.ops[k];
@@ -108,11 +125,18 @@ __device__ uint8_t cdr_validate(const CdrProg& P, const uint8_t* v, uint32_t len
       case RTPS_CDR_STRING: {
         pos += pad_to(pos, 4);
         if ((uint64_t)pos + 4 > len) return RTPS_CDR_EOF;
-        const uint32_t l = (uint32_t)load_prim(v + pos, 4, le);
+        // the length and the first 12 characters in one 16-B load when the arena has the bytes:
+        // a short ASCII string is then checked without the byte loop's dependent loads
+        const bool q16 = (uint64_t)pos + 16 <= avail;
+        const uint4 h = ld16u(v + (q16 ? pos : 0u));
+        const uint32_t l = q16 ? (le ? h.x : __builtin_bswap32(h.x)) : (uint32_t)load_prim(v + pos, 4, le);
         pos += 4;
         if ((uint64_t)pos + l > len) return RTPS_CDR_EOF;
         const uint32_t m = l ? l - 1 : 0;
-        if (!utf8_ok(v + pos, m)) return RTPS_CDR_BAD_UTF8;
+        const bool ascii12 = q16 && m <= 12u &&
+                             (((h.y & byte_mask(m, 0)) | (h.z & byte_mask(m, 4)) | (h.w & byte_mask(m, 8))) &
+                              0x80808080u) == 0u;
+        if (!ascii12 && !utf8_ok(v + pos, m)) return RTPS_CDR_BAD_UTF8;
         if (m > op.count) return RTPS_CDR_TOO_LONG;
         dpos = pos;
         dlen = m;
@@ -153,6 +177,9 @@ __device__ uint8_t cdr_validate(const CdrProg& P, const uint8_t* v, uint32_t len
 #ifndef CDR_GRID_MULT
 #define CDR_GRID_MULT 1  // grid cap = resident blocks x this
 #endif
+#ifndef CDR_PROBE
+#define CDR_PROBE 0  // diagnosis builds only: 1 phase A only, 2 no wide slots, 3 no narrow slots, 4 loads of phase A only
+#endif
 #ifndef CDR_WAVES_PER_EU
 #define CDR_WAVES_PER_EU 6  // 80 VGPRs: C2 162 -> 135 us, C3 211 -> 200 us, T unchanged (scripts/gpu_cdr_ab.sh)
 #endif
@@ -160,14 +187,6 @@ constexpr uint32_t CDR_UNROLL = CDR_UNROLL_N;
 constexpr uint32_t CDR_WIDE_DWORDS = 8;   // slots at least this long take the 16-B-per-lane path
 constexpr uint32_t CDR_RUN = CDR_RUN_N;   // record groups per round of the wide path
 
-// 16-byte loads / stores at any byte alignment (gfx950 runs them as single
-// unaligned dwordx4 accesses)
-__device__ __forceinline__ uint4 ld16u(const uint8_t* p) {
-  uint4 v;
-  __builtin_memcpy(&v, p, 16);
-  return v;
-}
-__device__ __forceinline__ void st16u(uint8_t* p, uint4 v) { __builtin_memcpy(p, &v, 16); }
 
 // Host-order fix of one loaded word (mask the bytes at or past nb, swap big-endian elements)
 __device__ __forceinline__ uint32_t fix_word(uint32_t x, uint32_t bb, uint32_t nb, uint32_t size, bool le) {
@@ -321,6 +340,101 @@ __device__ __forceinline__ void seg_copy(const CdrProg& P, const CdrSlot& S, con
   }
 }
 
+#ifndef CDR_OQ
+#define CDR_OQ 2  // output quads per lane per round of the output-stationary path (3: 36-B spill at 80 VGPRs)
+#endif
+
+// Output-stationary phase B (programs with a string or a sequence, rows up to CDR_OSTAT_ROW
+// bytes): the chunk's rows are contiguous (nv * row_bytes bytes), so lane = 16-B output quad
+// and every row store is a whole coalesced quad; each word finds its slot in the block's word
+// table wt[row_bytes / 4] = {kind | size << 8 | op << 16, k | static bytes << 16} (k = word of
+// the slot; segments are overlays and are not in it).  The narrow slot-by-slot walk stores one
+// word per row per instruction (64 rows, 64 lines) and waits for each slot's loads in turn:
+// C3's 3 one-word slots cost 86 of its 284 us, 56 of them the scattered stores (diagnosis builds).
+// Word ctl: bits 0-2 bytes kept (0: the word is zero), 3-4 bytes clamped at the arena end,
+// 5-6 swap (1: 16-bit halves, 2: 32-bit), bit 7 immediate (val is the word).
+__device__ __forceinline__ void ostat_word(const CdrArgs& a, const uint2* wt, uint32_t r, uint32_t w, bool in,
+                                           const uint32_t* meta, const uint64_t* vbase, const uint32_t* posT,
+                                           const uint32_t* lenT, uint32_t& val, uint32_t& ctl) {
+  const uint2 d = wt[in ? w : 0u];
+  const uint32_t kind = d.x & 0xffu, size = (d.x >> 8) & 0xffu, op = d.x >> 16;
+  const uint32_t k = d.y & 0xffffu;
+  const uint32_t m = meta[r];
+  const bool le = (m >> 8) != 0, ok = in && (m & 0xffu) == RTPS_CDR_OK && kind != CDR_SLOT_ZERO;
+  const bool hdr = kind == RTPS_CDR_STRING || kind == RTPS_CDR_SEQ;
+  const uint32_t ln = hdr ? lenT[op * 64u + r] : 0u;
+  const uint32_t nb = kind == RTPS_CDR_STRING ? ln : (kind == RTPS_CDR_SEQ ? ln * size : d.y >> 16);
+  const uint32_t bb = 4u * (k - (hdr ? 1u : 0u));
+  const bool data = ok && !(hdr && k == 0u) && bb < nb;
+  uint64_t abs = vbase[r] + posT[op * 64u + r] + ((!le && size == 8u) ? (bb ^ 4u) : bb);
+  abs = data ? abs : 0ull;
+  const uint32_t over = (abs + 4 > a.arena_len) ? (uint32_t)(abs + 4 - a.arena_len) : 0u;
+  const uint32_t rem = nb - bb;
+  const uint32_t keep = data ? (rem >= 4u ? 4u : rem) : 0u;
+  const uint32_t sw = le ? 0u : (size == 2u ? 1u : (size >= 4u ? 2u : 0u));
+  const bool imm = ok && hdr && k == 0u;
+  ctl = keep | (over << 3) | (sw << 5) | (imm ? 0x80u : 0u);
+  // words without data read a record word instead (in bounds, cached)
+  const uint8_t* pa = data ? a.arena + (abs - over) : (const uint8_t*)a.records;
+  val = imm ? ln : *(const u32u*)pa;
+}
+__device__ __forceinline__ uint32_t ostat_fix(uint32_t x, uint32_t ctl) {
+  if (ctl & 0x80u) return x;
+  const uint32_t keep = ctl & 7u;
+  if (keep == 0u) return 0u;
+  x >>= 8u * ((ctl >> 3) & 3u);
+  if (keep < 4u) x &= (1u << (8u * keep)) - 1u;
+  const uint32_t sw = (ctl >> 5) & 3u;
+  if (sw == 1u) x = ((x & 0xff00ff00u) >> 8) | ((x & 0x00ff00ffu) << 8);
+  else if (sw == 2u) x = __builtin_bswap32(x);
+  return x;
+}
+__device__ __forceinline__ void ostat_rows(const CdrArgs& a, const uint2* wt, uint32_t rdw, uint32_t nv,
+                                           uint32_t lane, const uint32_t* meta, const uint64_t* vbase,
+                                           const uint32_t* posT, const uint32_t* lenT, uint8_t* rowc) {
+  const uint32_t nwords = nv * rdw, nquads = (nwords + 3u) >> 2;
+  const float inv = 1.0f / (float)rdw;
+  for (uint32_t q0 = 0; q0 < nquads; q0 += 64u * CDR_OQ) {
+    uint32_t val[4 * CDR_OQ], ctl[CDR_OQ];  // ctl: a byte per word
+#pragma unroll
+    for (uint32_t u = 0; u < CDR_OQ; ++u) {
+      const uint32_t wd = 4u * (q0 + u * 64u + lane);
+      uint32_t r = (uint32_t)((float)wd * inv);
+      r = (r * rdw > wd) ? r - 1u : r;
+      r = ((r + 1u) * rdw <= wd) ? r + 1u : r;
+      uint32_t w = wd - r * rdw;
+      ctl[u] = 0u;
+#pragma unroll
+      for (uint32_t t = 0; t < 4u; ++t) {
+        const bool in = wd + t < nwords;
+        uint32_t c;
+        ostat_word(a, wt, in ? r : 0u, w, in, meta, vbase, posT, lenT, val[4 * u + t], c);
+        ctl[u] |= c << (8u * t);
+        if (++w == rdw) { w = 0u; ++r; }
+      }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < CDR_OQ; ++u) {
+      const uint32_t q = q0 + u * 64u + lane;
+      if (q >= nquads) break;
+      uint4 o;
+      o.x = ostat_fix(val[4 * u], ctl[u] & 0xffu);
+      o.y = ostat_fix(val[4 * u + 1], (ctl[u] >> 8) & 0xffu);
+      o.z = ostat_fix(val[4 * u + 2], (ctl[u] >> 16) & 0xffu);
+      o.w = ostat_fix(val[4 * u + 3], ctl[u] >> 24);
+      uint8_t* d = rowc + 16u * q;
+      if (4u * q + 4u <= nwords) {
+        st16u(d, o);
+      } else {
+        const uint32_t nw = nwords - 4u * q;
+        *(uint32_t*)d = o.x;
+        if (nw > 1) *(uint32_t*)(d + 4) = o.y;
+        if (nw > 2) *(uint32_t*)(d + 8) = o.z;
+      }
+    }
+  }
+}
+
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -333,12 +447,25 @@ extern __shared__ uint8_t cdr_lds[];
 // naming a record).  Phase A: lane = row (validation, LDS table).  Phase B: the wave writes the chunk's rows slot by slot, one 4-byte
 // word per lane and item (item = record x word of the slot), so consecutive
 // lanes store consecutive words and every row byte is written exactly once.
-template <bool WIDE>
+template <bool WIDE, bool OSTAT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CDR_WAVES_PER_EU)))
 void cdr_decode_kernel(CdrProg P, CdrArgs a) {
   const uint32_t lane = threadIdx.x & 63u, wpb = blockDim.x >> 6;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (uniform: LDS bases in SGPRs)
   uint8_t* T = cdr_lds + wave * P.lds_per_wave;
+  uint2* wt = (uint2*)(cdr_lds + wpb * P.lds_per_wave);  // OSTAT: the block's word table
+  const uint32_t rdw = P.row_bytes >> 2;
+  if (OSTAT) {
+    for (uint32_t si = 0; si < P.n_slots; ++si) {
+      const CdrSlot S = P.slots[si];
+      if (S.kind == CDR_SLOT_SEG) continue;  // an overlay: its member slots cover its words
+      const uint32_t info = S.kind | ((uint32_t)S.size << 8) | ((uint32_t)S.op << 16);
+      const uint32_t nbs = S.count * S.size;
+      for (uint32_t t = threadIdx.x; t < S.dwords; t += blockDim.x)
+        wt[(S.out_off >> 2) + t] = make_uint2(info, t | (nbs << 16));
+    }
+    __syncthreads();
+  }
   uint32_t* meta = (uint32_t*)T;             // [64] status | le << 8
   uint64_t* vbase = (uint64_t*)(T + 256);    // [64] arena offset of the value
   uint32_t* posT = (uint32_t*)(T + 768);     // [n_ops][64]
@@ -377,7 +504,8 @@ void cdr_decode_kernel(CdrProg P, CdrArgs a) {
         const uint32_t len = pl_len - 4;
         le = id1 != 0;
         st = (vb + len > a.arena_len) ? (uint32_t)RTPS_CDR_NOT_DATA  // cannot happen for parse outputs
-                                      : cdr_validate(P, a.arena + vb, len, le, posT, lenT, lane);
+             : CDR_PROBE == 4 ? (a.arena[vb] == 0xee ? 0u : 1u)
+                                      : cdr_validate(P, a.arena + vb, len, a.arena_len - vb, le, posT, lenT, lane);
       }
       a.row_status[r0 + lane] = (uint8_t)st;
     }
@@ -389,6 +517,7 @@ void cdr_decode_kernel(CdrProg P, CdrArgs a) {
     const bool all_fail = __all(lane >= nv || st != RTPS_CDR_OK);
     wave_sync();
     // ---- phase B ----
+    if (CDR_PROBE == 1 || CDR_PROBE == 4) { wave_sync(); continue; }
     uint8_t* rowc = a.rows + r0 * P.row_bytes;
     if (all_fail) {  // every row of the chunk is zero: one contiguous fill
       const uint32_t bytes = nv * P.row_bytes;
@@ -396,6 +525,11 @@ void cdr_decode_kernel(CdrProg P, CdrArgs a) {
         if (b + 16 <= bytes) st16u(rowc + b, make_uint4(0, 0, 0, 0));
         else for (uint32_t t = b; t < bytes; t += 4) *(uint32_t*)(rowc + t) = 0u;
       }
+      wave_sync();
+      continue;
+    }
+    if (OSTAT) {
+      ostat_rows(a, wt, rdw, nv, lane, meta, vbase, posT, lenT, rowc);
       wave_sync();
       continue;
     }
@@ -408,9 +542,11 @@ void cdr_decode_kernel(CdrProg P, CdrArgs a) {
         continue;
       }
       if (S.dwords >= CDR_WIDE_DWORDS) {
+        if (CDR_PROBE == 2) continue;
         wide_slot(P, S, a, hdr, nv, lane, meta, vbase, posT, lenT, rowc);
         continue;
       }
+      if (CDR_PROBE == 3) continue;
       const uint32_t total = nv * S.dwords;
       const bool swap8 = S.size == 8;
       const float inv_dwords = 1.0f / (float)S.dwords;
@@ -451,7 +587,7 @@ void cdr_decode_kernel(CdrProg P, CdrArgs a) {
           flags[u] = (ok && k < hdr ? 1u : 0u) | (le ? 2u : 0u);
           // lanes without data read a record word instead (always in bounds, cached)
           const uint8_t* pa = data ? a.arena + (abs - over) : (const uint8_t*)a.records;
-          val[u] = ok && k < hdr ? ln : *(const u32u*)pa;
+          val[u] = ok && k < hdr ? ln : (CDR_PROBE == 6 ? (uint32_t)(uintptr_t)pa : *(const u32u*)pa);
         }
 #pragma unroll
         for (uint32_t u = 0; u < CDR_UNROLL; ++u) {
@@ -463,7 +599,8 @@ void cdr_decode_kernel(CdrProg P, CdrArgs a) {
               else if (S.size >= 4) x = __builtin_bswap32(x);
             }
           }
-          if (dst[u] != ~0u) *(uint32_t*)(rowc + dst[u]) = x;
+          if (CDR_PROBE == 5) { if (dst[u] != ~0u) *(uint32_t*)(rowc + 4u * lane + 256u * ((u + si) % 9u)) = x; }
+          else if (dst[u] != ~0u) *(uint32_t*)(rowc + dst[u]) = x;
         }
       }
     }
@@ -870,6 +1007,21 @@ bool rtps_cdr_build_slots(CdrProg& P) {
   return true;
 }
 
+// The output-stationary phase B: flat programs whose field offsets turn dynamic (a string or a
+// sequence: no segment covers the fields behind it) with rows up to CDR_OSTAT_ROW bytes (the word
+// table is 2 B per row byte of LDS).  RTPS_CDR_OSTAT=0 / 1 overrides (diagnosis).
+#ifndef CDR_OSTAT_ROW
+#define CDR_OSTAT_ROW 1024u
+#endif
+static bool rtps_cdr_ostat(const CdrProg& P) {
+  static const int force = [] { const char* e = getenv("RTPS_CDR_OSTAT"); return e ? (e[0] == '1' ? 1 : 0) : -1; }();
+  if (force >= 0) return force == 1 && P.row_bytes <= 8192u;
+  if (P.row_bytes > CDR_OSTAT_ROW) return false;
+  for (uint32_t k = 0; k < P.n_ops; ++k)
+    if (P.ops[k].kind == RTPS_CDR_STRING || P.ops[k].kind == RTPS_CDR_SEQ) return true;
+  return false;
+}
+
 // Host launcher, called by rtps_rx_cdr_decode / _list (rtps_rx.hip) after validation.
 int rtps_cdr_launch(hipStream_t s, const CdrProg& P, const CdrArgs& a, uint32_t max_blocks) {
   uint32_t wpb = 65536u / P.lds_per_wave;
@@ -881,10 +1033,15 @@ int rtps_cdr_launch(hipStream_t s, const CdrProg& P, const CdrArgs& a, uint32_t 
   bool wide = false;  // a segment of more than 32 quads: one record per pass (seg_copy<true>)
   for (uint32_t i = 0; i < P.n_slots; ++i)
     wide = wide || (P.slots[i].kind == CDR_SLOT_SEG && (P.slots[i].dwords + 3u) / 4u > 32u);
-  if (wide)
-    hipLaunchKernelGGL(cdr_decode_kernel<true>, dim3((uint32_t)blocks), dim3(64 * wpb), wpb * P.lds_per_wave, s, P, a);
-  else
-    hipLaunchKernelGGL(cdr_decode_kernel<false>, dim3((uint32_t)blocks), dim3(64 * wpb), wpb * P.lds_per_wave, s, P,
-                       a);
+  if (rtps_cdr_ostat(P)) {
+    hipLaunchKernelGGL((cdr_decode_kernel<false, true>), dim3((uint32_t)blocks), dim3(64 * wpb),
+                       wpb * P.lds_per_wave + 2u * P.row_bytes, s, P, a);
+  } else if (wide) {
+    hipLaunchKernelGGL((cdr_decode_kernel<true, false>), dim3((uint32_t)blocks), dim3(64 * wpb), wpb * P.lds_per_wave,
+                       s, P, a);
+  } else {
+    hipLaunchKernelGGL((cdr_decode_kernel<false, false>), dim3((uint32_t)blocks), dim3(64 * wpb),
+                       wpb * P.lds_per_wave, s, P, a);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
