@@ -340,8 +340,15 @@ __device__ __forceinline__ void seg_copy(const CdrProg& P, const CdrSlot& S, con
   }
 }
 
+#ifndef CDR_OST_MASKED
+#define CDR_OST_MASKED 1  // words without data skip their load (exec-masked): C3 list 190 -> 186 us
+#endif
 #ifndef CDR_OQ
-#define CDR_OQ 2  // output quads per lane per round of the output-stationary path (3: 36-B spill at 80 VGPRs)
+#define CDR_OQ 1  // output quads per lane per round of the output-stationary path: one at 8 waves / SIMD
+                  // (63 VGPRs) 183.5 us on C3, two at 6 waves 186, three at 5 waves 208, four at 4 285
+#endif
+#ifndef CDR_OST_WAVES_PER_EU
+#define CDR_OST_WAVES_PER_EU 8
 #endif
 
 // Output-stationary phase B (programs with a string or a sequence, rows up to CDR_OSTAT_ROW
@@ -374,9 +381,13 @@ __device__ __forceinline__ void ostat_word(const CdrArgs& a, const uint2* wt, ui
   const uint32_t sw = le ? 0u : (size == 2u ? 1u : (size >= 4u ? 2u : 0u));
   const bool imm = ok && hdr && k == 0u;
   ctl = keep | (over << 3) | (sw << 5) | (imm ? 0x80u : 0u);
+#if CDR_OST_MASKED
+  val = imm ? ln : (data ? *(const u32u*)(a.arena + (abs - over)) : 0u);
+#else
   // words without data read a record word instead (in bounds, cached)
   const uint8_t* pa = data ? a.arena + (abs - over) : (const uint8_t*)a.records;
   val = imm ? ln : *(const u32u*)pa;
+#endif
 }
 __device__ __forceinline__ uint32_t ostat_fix(uint32_t x, uint32_t ctl) {
   if (ctl & 0x80u) return x;
@@ -448,7 +459,7 @@ extern __shared__ uint8_t cdr_lds[];
 // word per lane and item (item = record x word of the slot), so consecutive
 // lanes store consecutive words and every row byte is written exactly once.
 template <bool WIDE, bool OSTAT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CDR_WAVES_PER_EU)))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OSTAT ? CDR_OST_WAVES_PER_EU : CDR_WAVES_PER_EU)))
 void cdr_decode_kernel(CdrProg P, CdrArgs a) {
   const uint32_t lane = threadIdx.x & 63u, wpb = blockDim.x >> 6;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (uniform: LDS bases in SGPRs)
