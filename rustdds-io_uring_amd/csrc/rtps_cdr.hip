@@ -1033,26 +1033,56 @@ static bool rtps_cdr_ostat(const CdrProg& P) {
   return false;
 }
 
+// Grid cap: the kernel's own residency (its VGPRs and LDS) on every CU, cached per thread for the
+// last (kernel, block, LDS) asked.  The context's resident_blocks is the parse kernel's; under it
+// the 8-wave output-stationary kernel ran with a part of the chip idle (C3 list 183.6 -> 179.4 us,
+// per-record 416 -> 387 us).  CDR_OCC_CAP=0: the old cap (diagnosis builds).
+#ifndef CDR_OCC_CAP
+#define CDR_OCC_CAP 1
+#endif
+static uint64_t cdr_grid_cap(const void* fn, uint32_t threads, size_t lds, uint32_t max_blocks) {
+  if (!CDR_OCC_CAP) return (uint64_t)max_blocks * CDR_GRID_MULT;
+  thread_local const void* c_fn = nullptr;
+  thread_local uint32_t c_threads = 0;
+  thread_local size_t c_lds = 0;
+  thread_local int c_dev = -1;
+  thread_local uint64_t c_cap = 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return max_blocks;
+  if (fn != c_fn || threads != c_threads || lds != c_lds || dev != c_dev) {
+    int cus = 0, per = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0 ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, (int)threads, lds) != hipSuccess || per <= 0)
+      return max_blocks;
+    c_fn = fn; c_threads = threads; c_lds = lds; c_dev = dev;
+    c_cap = (uint64_t)cus * (uint64_t)per * CDR_GRID_MULT;
+  }
+  return c_cap;
+}
+
 // Host launcher, called by rtps_rx_cdr_decode / _list (rtps_rx.hip) after validation.
 int rtps_cdr_launch(hipStream_t s, const CdrProg& P, const CdrArgs& a, uint32_t max_blocks) {
   uint32_t wpb = 65536u / P.lds_per_wave;
   wpb = wpb < 1 ? 1 : (wpb > 4 ? 4 : wpb);
   const uint64_t chunks = ((a.list ? a.max_list : a.max_records) + 63) / 64;
   uint64_t blocks = (chunks + wpb - 1) / wpb;
-  if (blocks > (uint64_t)max_blocks * CDR_GRID_MULT) blocks = (uint64_t)max_blocks * CDR_GRID_MULT;
-  if (blocks == 0) return 0;
   bool wide = false;  // a segment of more than 32 quads: one record per pass (seg_copy<true>)
   for (uint32_t i = 0; i < P.n_slots; ++i)
     wide = wide || (P.slots[i].kind == CDR_SLOT_SEG && (P.slots[i].dwords + 3u) / 4u > 32u);
-  if (rtps_cdr_ostat(P)) {
-    hipLaunchKernelGGL((cdr_decode_kernel<false, true>), dim3((uint32_t)blocks), dim3(64 * wpb),
-                       wpb * P.lds_per_wave + 2u * P.row_bytes, s, P, a);
+  const bool ost = rtps_cdr_ostat(P);
+  const void* fn = ost ? (const void*)cdr_decode_kernel<false, true>
+                 : wide ? (const void*)cdr_decode_kernel<true, false> : (const void*)cdr_decode_kernel<false, false>;
+  const size_t lds = wpb * P.lds_per_wave + (ost ? 2u * P.row_bytes : 0u);
+  // the slot-walk kernels keep the context's cap: C2 at its own residency took 148 -> 172 us (T unchanged)
+  const uint64_t cap = ost ? cdr_grid_cap(fn, 64 * wpb, lds, max_blocks) : (uint64_t)max_blocks * CDR_GRID_MULT;
+  if (blocks > cap) blocks = cap;
+  if (blocks == 0) return 0;
+  if (ost) {
+    hipLaunchKernelGGL((cdr_decode_kernel<false, true>), dim3((uint32_t)blocks), dim3(64 * wpb), lds, s, P, a);
   } else if (wide) {
-    hipLaunchKernelGGL((cdr_decode_kernel<true, false>), dim3((uint32_t)blocks), dim3(64 * wpb), wpb * P.lds_per_wave,
-                       s, P, a);
+    hipLaunchKernelGGL((cdr_decode_kernel<true, false>), dim3((uint32_t)blocks), dim3(64 * wpb), lds, s, P, a);
   } else {
-    hipLaunchKernelGGL((cdr_decode_kernel<false, false>), dim3((uint32_t)blocks), dim3(64 * wpb),
-                       wpb * P.lds_per_wave, s, P, a);
+    hipLaunchKernelGGL((cdr_decode_kernel<false, false>), dim3((uint32_t)blocks), dim3(64 * wpb), lds, s, P, a);
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
