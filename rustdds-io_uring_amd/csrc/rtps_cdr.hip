@@ -227,7 +227,7 @@ __device__ __forceinline__ void wide_slot(const CdrProg& P, const CdrSlot& S, co
         const uint32_t rr = r + u * rpi + lr;
         const uint32_t rec = min(rr, nv - 1);
         const uint32_t m = meta[rec];
-        const bool okrec = (m & 0xffu) == RTPS_CDR_OK, le = (m >> 8) != 0;
+        const bool okrec = (m & 0xffu) == RTPS_CDR_OK, le = ((m >> 8) & 1u) != 0;
         const bool ok = rr < nv && okrec && S.kind != CDR_SLOT_ZERO;
         const uint32_t ln = hdr ? lenT[S.op * 64u + rec] : 0u;
         const uint32_t nb = S.kind == CDR_SLOT_SEG ? 4u * S.dwords
@@ -245,7 +245,7 @@ __device__ __forceinline__ void wide_slot(const CdrProg& P, const CdrSlot& S, co
         if (rr >= nv) break;
         if (!own[u]) continue;
         const uint32_t m = meta[rr];
-        const bool le = (m >> 8) != 0;
+        const bool le = ((m >> 8) & 1u) != 0;
         const uint32_t nb = nbv[u];
         uint8_t* rowp = rowc + (uint64_t)rr * P.row_bytes + S.out_off;
         if (hdr && q == 0) *(uint32_t*)rowp = nb ? lenT[S.op * 64u + rr] : 0u;  // nb == 0 <=> length 0 or failed row
@@ -340,6 +340,10 @@ __device__ __forceinline__ void seg_copy(const CdrProg& P, const CdrSlot& S, con
   }
 }
 
+#ifndef CDR_OST_STAGE
+#define CDR_OST_STAGE 0  // output-stationary: the first 32 B of every value staged in LDS by phase A
+#endif
+constexpr uint32_t CDR_STAGE_BYTES = 32;  // per row; + 16 B of pad per wave (the funnel's second word)
 #ifndef CDR_OST_MASKED
 #define CDR_OST_MASKED 1  // words without data skip their load (exec-masked): C3 list 190 -> 186 us
 #endif
@@ -362,19 +366,22 @@ __device__ __forceinline__ void seg_copy(const CdrProg& P, const CdrSlot& S, con
 // 5-6 swap (1: 16-bit halves, 2: 32-bit), bit 7 immediate (val is the word).
 __device__ __forceinline__ void ostat_word(const CdrArgs& a, const uint2* wt, uint32_t r, uint32_t w, bool in,
                                            const uint32_t* meta, const uint64_t* vbase, const uint32_t* posT,
-                                           const uint32_t* lenT, uint32_t& val, uint32_t& ctl) {
+                                           const uint32_t* lenT, const uint32_t* stg, uint32_t& val, uint32_t& ctl) {
   const uint2 d = wt[in ? w : 0u];
   const uint32_t kind = d.x & 0xffu, size = (d.x >> 8) & 0xffu, op = d.x >> 16;
   const uint32_t k = d.y & 0xffffu;
   const uint32_t m = meta[r];
-  const bool le = (m >> 8) != 0, ok = in && (m & 0xffu) == RTPS_CDR_OK && kind != CDR_SLOT_ZERO;
+  const bool le = ((m >> 8) & 1u) != 0, ok = in && (m & 0xffu) == RTPS_CDR_OK && kind != CDR_SLOT_ZERO;
   const bool hdr = kind == RTPS_CDR_STRING || kind == RTPS_CDR_SEQ;
   const uint32_t ln = hdr ? lenT[op * 64u + r] : 0u;
   const uint32_t nb = kind == RTPS_CDR_STRING ? ln : (kind == RTPS_CDR_SEQ ? ln * size : d.y >> 16);
   const uint32_t bb = 4u * (k - (hdr ? 1u : 0u));
   const bool data = ok && !(hdr && k == 0u) && bb < nb;
-  uint64_t abs = vbase[r] + posT[op * 64u + r] + ((!le && size == 8u) ? (bb ^ 4u) : bb);
+  const uint32_t off = posT[op * 64u + r] + ((!le && size == 8u) ? (bb ^ 4u) : bb);  // in the value
+  uint64_t abs = vbase[r] + off;
   abs = data ? abs : 0ull;
+  // a word inside the row's staged window (meta bits 16-23: its length) is read from LDS
+  const bool staged = CDR_OST_STAGE && data && off + 4u <= ((m >> 16) & 0xffu);
   const uint32_t over = (abs + 4 > a.arena_len) ? (uint32_t)(abs + 4 - a.arena_len) : 0u;
   const uint32_t rem = nb - bb;
   const uint32_t keep = data ? (rem >= 4u ? 4u : rem) : 0u;
@@ -382,7 +389,12 @@ __device__ __forceinline__ void ostat_word(const CdrArgs& a, const uint2* wt, ui
   const bool imm = ok && hdr && k == 0u;
   ctl = keep | (over << 3) | (sw << 5) | (imm ? 0x80u : 0u);
 #if CDR_OST_MASKED
-  val = imm ? ln : (data ? *(const u32u*)(a.arena + (abs - over)) : 0u);
+  if (CDR_OST_STAGE && staged) {
+    const uint32_t i = r * (CDR_STAGE_BYTES / 4u) + (off >> 2);
+    val = __builtin_amdgcn_alignbyte(stg[i + 1], stg[i], off & 3u);
+  } else {
+    val = imm ? ln : (data ? *(const u32u*)(a.arena + (abs - over)) : 0u);
+  }
 #else
   // words without data read a record word instead (in bounds, cached)
   const uint8_t* pa = data ? a.arena + (abs - over) : (const uint8_t*)a.records;
@@ -402,7 +414,8 @@ __device__ __forceinline__ uint32_t ostat_fix(uint32_t x, uint32_t ctl) {
 }
 __device__ __forceinline__ void ostat_rows(const CdrArgs& a, const uint2* wt, uint32_t rdw, uint32_t nv,
                                            uint32_t lane, const uint32_t* meta, const uint64_t* vbase,
-                                           const uint32_t* posT, const uint32_t* lenT, uint8_t* rowc) {
+                                           const uint32_t* posT, const uint32_t* lenT, const uint32_t* stg,
+                                           uint8_t* rowc) {
   const uint32_t nwords = nv * rdw, nquads = (nwords + 3u) >> 2;
   const float inv = 1.0f / (float)rdw;
   for (uint32_t q0 = 0; q0 < nquads; q0 += 64u * CDR_OQ) {
@@ -419,7 +432,7 @@ __device__ __forceinline__ void ostat_rows(const CdrArgs& a, const uint2* wt, ui
       for (uint32_t t = 0; t < 4u; ++t) {
         const bool in = wd + t < nwords;
         uint32_t c;
-        ostat_word(a, wt, in ? r : 0u, w, in, meta, vbase, posT, lenT, val[4 * u + t], c);
+        ostat_word(a, wt, in ? r : 0u, w, in, meta, vbase, posT, lenT, stg, val[4 * u + t], c);
         ctl[u] |= c << (8u * t);
         if (++w == rdw) { w = 0u; ++r; }
       }
@@ -481,6 +494,7 @@ void cdr_decode_kernel(CdrProg P, CdrArgs a) {
   uint64_t* vbase = (uint64_t*)(T + 256);    // [64] arena offset of the value
   uint32_t* posT = (uint32_t*)(T + 768);     // [n_ops][64]
   uint32_t* lenT = posT + P.n_ops * 64u;     // [n_ops][64]
+  uint32_t* stg = lenT + P.n_ops * 64u;      // OSTAT: [64][CDR_STAGE_BYTES / 4] + pad, the staged values
   const uint64_t n = a.list ? min(*a.n_list, a.max_list) : min(*a.n_records, a.max_records);
   const uint64_t nrec = min(*a.n_records, a.max_records);
   const uint64_t chunks = (n + 63) / 64;
@@ -488,7 +502,7 @@ void cdr_decode_kernel(CdrProg P, CdrArgs a) {
     const uint64_t r0 = c * 64;
     const uint32_t nv = (uint32_t)min<uint64_t>(64, n - r0);
     // ---- phase A ----
-    uint32_t st = 0xff, le = 1;
+    uint32_t st = 0xff, le = 1, wl = 0;
     uint64_t vb = 0;
     if (lane < nv) {
       // the row's record: the row itself, or its list entry (a delivery, a sample index)
@@ -514,13 +528,20 @@ void cdr_decode_kernel(CdrProg P, CdrArgs a) {
         vb = a.dgram_off[h0.x] + pl_off + 4;
         const uint32_t len = pl_len - 4;
         le = id1 != 0;
+        if (OSTAT && CDR_OST_STAGE) {  // the value's first 32 B, in flight beside the validation's loads
+          const bool sw = vb + CDR_STAGE_BYTES <= a.arena_len;
+          const uint4 s0 = ld16u(a.arena + (sw ? vb : 0ull)), s1 = ld16u(a.arena + (sw ? vb + 16u : 0ull));
+          *(uint4*)(stg + lane * (CDR_STAGE_BYTES / 4u)) = s0;
+          *(uint4*)(stg + lane * (CDR_STAGE_BYTES / 4u) + 4u) = s1;
+          wl = sw ? min(len, CDR_STAGE_BYTES) : 0u;
+        }
         st = (vb + len > a.arena_len) ? (uint32_t)RTPS_CDR_NOT_DATA  // cannot happen for parse outputs
              : CDR_PROBE == 4 ? (a.arena[vb] == 0xee ? 0u : 1u)
                                       : cdr_validate(P, a.arena + vb, len, a.arena_len - vb, le, posT, lenT, lane);
       }
       a.row_status[r0 + lane] = (uint8_t)st;
     }
-    meta[lane] = st | (le << 8);
+    meta[lane] = st | (le << 8) | (wl << 16);
     vbase[lane] = vb;
     // every record of the chunk decoded little-endian: segments are plain copies
     // and their member slots have nothing to write
@@ -540,7 +561,7 @@ void cdr_decode_kernel(CdrProg P, CdrArgs a) {
       continue;
     }
     if (OSTAT) {
-      ostat_rows(a, wt, rdw, nv, lane, meta, vbase, posT, lenT, rowc);
+      ostat_rows(a, wt, rdw, nv, lane, meta, vbase, posT, lenT, stg, rowc);
       wave_sync();
       continue;
     }
@@ -575,7 +596,7 @@ void cdr_decode_kernel(CdrProg P, CdrArgs a) {
           rec = in ? rec : 0u;
           const uint32_t k = item - rec * S.dwords;
           const uint32_t m = meta[rec];
-          const bool le = (m >> 8) != 0;
+          const bool le = ((m >> 8) & 1u) != 0;
           const bool okrec = (m & 0xffu) == RTPS_CDR_OK;
           const bool mine = S.kind == CDR_SLOT_SEG ? (okrec && le) : (S.flags & CDR_IN_SEG) ? !(okrec && le) : true;
           dst[u] = (in && mine) ? rec * P.row_bytes + S.out_off + 4u * k : ~0u;
@@ -943,6 +964,8 @@ static uint32_t slot_dwords(const rtps_cdr_op& op) {
   }
 }
 
+static bool rtps_cdr_ostat(const CdrProg& P);
+
 bool rtps_cdr_build_slots(CdrProg& P) {
   // op slots sorted by out_off (insertion sort: n_ops <= 64)
   uint32_t order[RTPS_CDR_MAX_OPS];
@@ -1014,7 +1037,8 @@ bool rtps_cdr_build_slots(CdrProg& P) {
   close_run();
   if (full) return false;
   P.n_slots = ns;
-  P.lds_per_wave = 768u + 512u * P.n_ops;
+  // output-stationary programs stage 32 B of every value per wave (+ the funnel's pad)
+  P.lds_per_wave = 768u + 512u * P.n_ops + (CDR_OST_STAGE && rtps_cdr_ostat(P) ? 64u * CDR_STAGE_BYTES + 16u : 0u);
   return true;
 }
 
@@ -1073,6 +1097,7 @@ int rtps_cdr_launch(hipStream_t s, const CdrProg& P, const CdrArgs& a, uint32_t 
   const void* fn = ost ? (const void*)cdr_decode_kernel<false, true>
                  : wide ? (const void*)cdr_decode_kernel<true, false> : (const void*)cdr_decode_kernel<false, false>;
   const size_t lds = wpb * P.lds_per_wave + (ost ? 2u * P.row_bytes : 0u);
+  // (the staged values live in each wave's table: lds_per_wave counts them for output-stationary programs)
   // the slot-walk kernels keep the context's cap: C2 at its own residency took 148 -> 172 us (T unchanged)
   const uint64_t cap = ost ? cdr_grid_cap(fn, 64 * wpb, lds, max_blocks) : (uint64_t)max_blocks * CDR_GRID_MULT;
   if (blocks > cap) blocks = cap;
