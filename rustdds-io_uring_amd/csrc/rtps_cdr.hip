@@ -1086,8 +1086,12 @@ static uint64_t cdr_grid_cap(const void* fn, uint32_t threads, size_t lds, uint3
 
 // Host launcher, called by rtps_rx_cdr_decode / _list (rtps_rx.hip) after validation.
 int rtps_cdr_launch(hipStream_t s, const CdrProg& P, const CdrArgs& a, uint32_t max_blocks) {
+#ifndef CDR_OST_WPB
+#define CDR_OST_WPB 1  // one wave per block for the output-stationary kernel: C3 list 180.5 -> 177.7 us (2: 179.3)
+#endif
   uint32_t wpb = 65536u / P.lds_per_wave;
-  wpb = wpb < 1 ? 1 : (wpb > 4 ? 4 : wpb);
+  const uint32_t wmax = rtps_cdr_ostat(P) ? CDR_OST_WPB : 4u;
+  wpb = wpb < 1 ? 1 : (wpb > wmax ? wmax : wpb);
   const uint64_t chunks = ((a.list ? a.max_list : a.max_records) + 63) / 64;
   uint64_t blocks = (chunks + wpb - 1) / wpb;
   bool wide = false;  // a segment of more than 32 quads: one record per pass (seg_copy<true>)
