@@ -7,6 +7,7 @@
 #   spdp       C3 bench line's SPDP repeats leg only numbers (part of ing)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; R=$(pwd); O=$R/gpurun_out/r6; mkdir -p $O; export TMPDIR=/tmp
 PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
+shopt -s nullglob  # (no variants: the variant loops run the in-tree library only)
 for step in "$@"; do
   echo "== $step $(date +%T)"
   case $step in
